@@ -1,0 +1,305 @@
+/*
+ * gpuscore.h — C-ABI of libgpuscore, the MI355X-native batched Filter/Score engine
+ * for koord-scheduler's LoadAwareScheduling / NodeResourcesFit (LeastAllocated) hot path.
+ *
+ * This header is the drop-in boundary. A cgo package (pkg/scheduler/gpuscore, see
+ * INTEGRATION.md) binds exactly these entry points; a ctypes mirror lives in
+ * koordinator_amd/abi.py. Only fixed-width POD structs and plain pointers cross the
+ * boundary: the caller owns every host buffer, the library owns every device buffer,
+ * and no pointer is retained across calls.
+ *
+ * Each entry point names the reference interface it replaces (paths relative to
+ * hormes/koordinator; "[upstream]" = k8s.io/kubernetes@v1.24.15, pinned at go.mod:57,276).
+ *
+ * Quantity convention (reference: pkg/scheduler/plugins/loadaware/helper.go:146-151
+ * getResourceValue): GS_RES_CPU is carried in milli-CPU (Quantity.MilliValue()), every
+ * other resource slot in units (Quantity.Value()). Inputs must be integral in that unit.
+ *
+ * Return convention: 0 = OK, <0 = error (GS_E*); gs_last_error(ctx) has the message.
+ */
+#ifndef GPUSCORE_H
+#define GPUSCORE_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GS_ABI_VERSION 1u
+
+/* ---- resource slots (corev1.ResourceName restricted to the hot-path set) ---- */
+enum gs_resource {
+  GS_RES_CPU = 0,          /* "cpu"                          (milli) */
+  GS_RES_MEMORY = 1,       /* "memory"                       (bytes) */
+  GS_RES_EPHEMERAL = 2,    /* "ephemeral-storage"            (bytes) */
+  GS_RES_BATCH_CPU = 3,    /* "kubernetes.io/batch-cpu"      (units, apis/extension/resource.go:26) */
+  GS_RES_BATCH_MEMORY = 4, /* "kubernetes.io/batch-memory" */
+  GS_RES_MID_CPU = 5,      /* "kubernetes.io/mid-cpu" */
+  GS_RES_MID_MEMORY = 6,   /* "kubernetes.io/mid-memory" */
+  GS_RES_RESERVED = 7,
+  GS_NUM_RES = 8
+};
+/* Scalar (extended) resources in the sense of [upstream] schedutil.IsScalarResourceName. */
+#define GS_SCALAR_RES_MASK 0x78u
+
+/* extension.PriorityClass after GetPodPriorityClassWithDefault (apis/extension/priority_utils.go:26-33) */
+enum gs_priority_class {
+  GS_PRIO_NONE = 0, GS_PRIO_PROD = 1, GS_PRIO_MID = 2, GS_PRIO_BATCH = 3, GS_PRIO_FREE = 4
+};
+
+/* extension.AggregationType (apis/extension/... AggregationType: avg,p50,p90,p95,p99) */
+enum gs_aggregation_type {
+  GS_AGG_NONE = -1, GS_AGG_AVG = 0, GS_AGG_P50 = 1, GS_AGG_P90 = 2, GS_AGG_P95 = 3, GS_AGG_P99 = 4,
+  GS_NUM_AGG_TYPES = 5
+};
+#define GS_MAX_AGG_USAGES 4
+
+/* gs_usage.mask bits: which keys the ResourceList holds */
+#define GS_USAGE_CPU 0x1u
+#define GS_USAGE_MEMORY 0x2u
+#define GS_USAGE_OTHER 0x80u /* some key outside {cpu,memory}: only len(ResourceList) > 0 observes it */
+
+/* ---- pod (decoded by the caller from corev1.Pod) ---- */
+#define GS_POD_DAEMONSET 0x1u  /* loadaware/helper.go:189-196 isDaemonSetPod */
+#define GS_POD_TERMINATED 0x2u /* pkg/util IsPodTerminated: podAssignCache.assign skips it */
+
+typedef struct gs_pod {
+  uint64_t uid;                    /* types.UID (hashed): podAssignCache key */
+  uint64_t name_key;               /* hash of "namespace/name": PodMetricInfo match key (helper.go:142-144) */
+  int64_t requests[GS_NUM_RES];    /* [upstream] resourceapi.PodRequestsAndLimits requests (== Fit computePodResourceRequest) */
+  int64_t limits[GS_NUM_RES];      /* same, limits */
+  int64_t nonzero_requests[2];     /* [upstream] Σ_containers schedutil.GetNonzeroRequests (max init, +overhead): cpu milli, memory */
+  uint32_t request_mask;           /* bit r: requests holds key r (Fit: len(podRequest.ScalarResources) > 0) */
+  int32_t priority_class;          /* gs_priority_class */
+  uint32_t flags;                  /* GS_POD_* */
+  uint32_t pad0;
+} gs_pod;
+
+/* ---- node snapshot row (NodeInfo + node object annotations, decoded by the caller) ---- */
+#define GS_NODE_CUSTOM_THRESHOLDS 0x1u  /* annotation scheduling.koordinator.sh/usage-thresholds present and parsed */
+#define GS_NODE_CUSTOM_AGGREGATED 0x2u  /* ... and its aggregatedUsage is non-nil */
+
+typedef struct gs_node {
+  int64_t allocatable[GS_NUM_RES];   /* NodeInfo.Allocatable (node.Status.Allocatable after transformers) */
+  int64_t requested[GS_NUM_RES];     /* NodeInfo.Requested */
+  int64_t nonzero_requested[2];      /* NodeInfo.NonZeroRequested cpu milli, memory */
+  int64_t allowed_pod_number;        /* NodeInfo.Allocatable.AllowedPodNumber */
+  int64_t pod_count;                 /* len(NodeInfo.Pods) */
+  int64_t raw_allocatable[2];        /* annotation node.koordinator.sh/raw-allocatable: cpu milli, memory */
+  uint32_t raw_allocatable_mask;     /* GS_USAGE_* keys present in raw-allocatable (0: absent or unparsable) */
+  uint32_t custom_flags;             /* GS_NODE_CUSTOM_* (apis/extension/load_aware.go:51-62) */
+  int64_t custom_usage_thresholds[2];      /* CustomUsageThresholds.UsageThresholds cpu, memory */
+  int64_t custom_prod_usage_thresholds[2]; /* .ProdUsageThresholds */
+  int64_t custom_agg_usage_thresholds[2];  /* .AggregatedUsage.UsageThresholds */
+  uint32_t custom_usage_mask;        /* GS_USAGE_* keys present in each map */
+  uint32_t custom_prod_usage_mask;
+  uint32_t custom_agg_usage_mask;
+  int32_t custom_agg_type;           /* .AggregatedUsage.UsageAggregationType (GS_AGG_NONE = "") */
+  int64_t custom_agg_duration_ns;    /* .AggregatedUsage.UsageAggregatedDuration (0 = nil/0) */
+} gs_node;
+
+/* ---- NodeMetric (apis/slo/v1alpha1/nodemetric_types.go:38-137), decoded ---- */
+typedef struct gs_usage {
+  int64_t cpu_milli;
+  int64_t memory;
+  uint32_t mask; /* GS_USAGE_* */
+  uint32_t pad0;
+} gs_usage;
+
+typedef struct gs_agg_usage {
+  int64_t duration_ns;                 /* AggregatedUsage.Duration */
+  uint32_t type_mask;                  /* bit t: Usage[t] present */
+  uint32_t pad0;
+  gs_usage usage[GS_NUM_AGG_TYPES];
+} gs_agg_usage;
+
+typedef struct gs_node_metric {
+  int32_t exists;                      /* nodeMetricLister.Get(node) found it */
+  int32_t has_update_time;             /* Status.UpdateTime != nil */
+  int64_t update_time_ns;              /* unix ns */
+  int32_t has_report_interval;         /* Spec.CollectPolicy.ReportIntervalSeconds != nil */
+  int32_t has_node_metric;             /* Status.NodeMetric != nil */
+  int64_t report_interval_s;
+  gs_usage node_usage;                 /* Status.NodeMetric.NodeUsage */
+  int32_t n_aggregated;                /* len(AggregatedNodeUsages) <= GS_MAX_AGG_USAGES */
+  uint32_t pad0;
+  gs_agg_usage aggregated[GS_MAX_AGG_USAGES];
+} gs_node_metric;
+
+/* Status.PodsMetric entry, pre-joined with the pod lister (helper.go:153-170) */
+typedef struct gs_pod_metric {
+  uint64_t name_key;                   /* namespace/name key, same hash as gs_pod.name_key */
+  int32_t in_lister;                   /* podLister.Pods(ns).Get(name) succeeded */
+  int32_t priority_class;              /* GetPodPriorityClassWithDefault(listed pod) */
+  gs_usage usage;                      /* PodUsage */
+} gs_pod_metric;
+
+/* ---- plugin args (pkg/scheduler/apis/config/types.go:30-76; v1beta2 defaults in gs_loadaware_args_default) ---- */
+typedef struct gs_loadaware_args {
+  int32_t filter_expired_node_metrics;         /* FilterExpiredNodeMetrics (*bool; default true) */
+  int32_t has_node_metric_expiration;          /* NodeMetricExpirationSeconds != nil */
+  int64_t node_metric_expiration_seconds;      /* default 180 */
+  int64_t resource_weights[2];                 /* ResourceWeights cpu, memory */
+  int64_t usage_thresholds[2];                 /* UsageThresholds */
+  int64_t prod_usage_thresholds[2];            /* ProdUsageThresholds */
+  int64_t estimated_scaling_factors[2];        /* EstimatedScalingFactors */
+  uint32_t resource_weights_mask;              /* GS_USAGE_* keys present in each map */
+  uint32_t usage_thresholds_mask;
+  uint32_t prod_usage_thresholds_mask;
+  uint32_t estimated_scaling_factors_mask;
+  int32_t score_according_prod_usage;          /* ScoreAccordingProdUsage */
+  int32_t has_aggregated;                      /* Aggregated != nil */
+  int64_t agg_usage_thresholds[2];             /* Aggregated.UsageThresholds */
+  uint32_t agg_usage_thresholds_mask;
+  int32_t agg_usage_type;                      /* Aggregated.UsageAggregationType (GS_AGG_NONE = "") */
+  int64_t agg_usage_duration_ns;               /* Aggregated.UsageAggregatedDuration */
+  int32_t agg_score_type;                      /* Aggregated.ScoreAggregationType */
+  int32_t pad0;
+  int64_t agg_score_duration_ns;               /* Aggregated.ScoreAggregatedDuration */
+} gs_loadaware_args;
+
+/* [upstream] NodeResourcesFitArgs.ScoringStrategy (LeastAllocated only on this path) */
+typedef struct gs_fit_args {
+  int64_t resource_weights[GS_NUM_RES];        /* ScoringStrategy.Resources weights per slot (0 = not listed) */
+} gs_fit_args;
+
+/* plugin ids / enabled-plugin bits */
+enum gs_plugin { GS_PLUGIN_FIT = 0, GS_PLUGIN_LOADAWARE = 1, GS_NUM_PLUGINS = 2 };
+#define GS_ENABLE_FIT_FILTER 0x1u
+#define GS_ENABLE_FIT_SCORE 0x2u
+#define GS_ENABLE_LA_FILTER 0x4u
+#define GS_ENABLE_LA_SCORE 0x8u
+
+typedef struct gs_config {
+  uint32_t abi_version;                /* GS_ABI_VERSION */
+  int32_t device;                      /* HIP device ordinal */
+  uint32_t num_nodes;                  /* node table size (global, all ranks) */
+  uint32_t enabled;                    /* GS_ENABLE_* */
+  int64_t plugin_weights[GS_NUM_PLUGINS]; /* profile score weights (framework multiplies, runtime/framework.go) */
+  gs_loadaware_args loadaware;
+  gs_fit_args fit;
+  uint64_t seed;                       /* tie-break stream seed (selectHost) */
+  uint32_t batch_size;                 /* pods per device pass (0 = default 128) */
+  uint32_t cand_cap;                   /* candidate-list capacity per pod and shard (0 = default 256) */
+} gs_config;
+
+/* ---- outputs ---- */
+/* per (pod,node) filter codes (bits; 0 = feasible) */
+#define GS_FAIL_FIT_PODS 0x01u      /* "Too many pods" */
+#define GS_FAIL_FIT_CPU 0x02u       /* "Insufficient cpu" */
+#define GS_FAIL_FIT_MEMORY 0x04u
+#define GS_FAIL_FIT_EPHEMERAL 0x08u
+#define GS_FAIL_FIT_SCALAR 0x10u
+#define GS_FAIL_LOADAWARE 0x20u     /* "node(s) ... usage exceed threshold" (load_aware.go:45-46) */
+
+typedef struct gs_placement {
+  int32_t node;                        /* selected node index, -1 = unschedulable (no feasible node) */
+  uint32_t feasible;                   /* number of feasible nodes */
+  int64_t score;                       /* total weighted score of the selected node */
+  uint32_t ties;                       /* nodes sharing the max score (selectHost reservoir size) */
+  uint32_t flags;                      /* GS_PLACED_* diagnostics */
+} gs_placement;
+#define GS_PLACED_SLOWPATH 0x1u        /* resolved by the exact full-row path (no valid candidate list) */
+
+/* ---- errors ---- */
+#define GS_OK 0
+#define GS_EINVAL -1
+#define GS_EDEVICE -2
+#define GS_ENOMEM -3
+#define GS_EUNSUPPORTED -4
+#define GS_ECOMM -5
+#define GS_ESTATE -6
+
+/* ---------------------------------------------------------------------------------------- */
+
+typedef struct gs_ctx gs_ctx; /* one per scheduler profile and GPU (rank) */
+
+/* Multi-GPU exchange: all-gather of `bytes` from every rank, rank-major into recv (host memory).
+ * Used when the caller supplies its own transport (tests); production uses native RCCL. */
+typedef int (*gs_allgather_fn)(void* user, const void* send, void* recv, size_t bytes);
+
+typedef struct gs_stats {
+  uint64_t batches;          /* device passes (eval + candidate + commit) */
+  uint64_t pods;             /* pods placed or found unschedulable by gs_schedule */
+  uint64_t cuts;             /* batches cut short because a candidate list was exhausted */
+  uint64_t slowpath_pods;    /* pods resolved by the exact full-row path */
+  uint64_t eval_launches;    /* launches of the fused filter+score kernel */
+  uint64_t eval_pairs;       /* pod x node pairs evaluated by it (this rank's shard) */
+  double eval_ms;            /* summed device time of the fused filter+score kernel (HIP events) */
+  double cand_ms;            /* summed device time of candidate extraction */
+  double commit_ms;          /* summed device time of the sequential commit kernel */
+  double exchange_ms;        /* host wall time in the all-gather (multi-GPU) */
+  uint64_t node_row_bytes;   /* bytes one pod x node evaluation reads from the node mirror */
+  uint32_t shard_begin, shard_end; /* this rank's node range */
+} gs_stats;
+
+/* v1beta2.SetDefaults_LoadAwareSchedulingArgs (pkg/scheduler/apis/config/v1beta2/defaults.go:76-99) */
+void gs_loadaware_args_default(gs_loadaware_args* a);
+/* v1beta2 NodeResourcesFitArgs default scoring strategy: LeastAllocated cpu=1, memory=1 */
+void gs_fit_args_default(gs_fit_args* a);
+/* validation.ValidateLoadAwareSchedulingArgs (pkg/scheduler/apis/config/validation/validation_pluginargs.go:31-84) */
+int gs_loadaware_args_validate(const gs_loadaware_args* a, char* msg, size_t msg_len);
+
+/* Plugin construction for one profile: loadaware.New (pkg/scheduler/plugins/loadaware/load_aware.go:76-110)
+ * and [upstream] noderesources.NewFit, registered through frameworkext.PluginFactoryProxy
+ * (pkg/scheduler/frameworkext/framework_extender_factory.go:209-221). Allocates the HBM mirror. */
+int gs_create(const gs_config* cfg, gs_ctx** out);
+int gs_destroy(gs_ctx* ctx);
+const char* gs_last_error(gs_ctx* ctx);
+const char* gs_version(void);
+
+/* Injected clock: replaces time.Now in loadaware/helper.go:36-41 (isNodeMetricExpired) and
+ * loadaware/pod_assign_cache.go:30-32,65 (assign timestamps). */
+int gs_set_now(gs_ctx* ctx, int64_t now_unix_ns);
+
+/* Node snapshot rows: [upstream] internal/cache Cache.UpdateSnapshot -> NodeInfo (Allocatable, Requested,
+ * NonZeroRequested, Pods) plus the node annotations read by EstimateNode
+ * (loadaware/estimator/default_estimator.go:110-129) and generateUsageThresholdsFilterProfile (loadaware/helper.go:102-140).
+ * Only the given rows are recomputed and copied to HBM. */
+int gs_nodes_upsert(gs_ctx* ctx, const uint32_t* idx, const gs_node* nodes, uint32_t n);
+
+/* NodeMetric informer events (lister reads at loadaware/load_aware.go:133,278). pod_metrics holds the
+ * PodsMetric of metric i at [pm_offsets[i], pm_offsets[i+1]). */
+int gs_node_metrics_upsert(gs_ctx* ctx, const uint32_t* idx, const gs_node_metric* metrics, uint32_t n,
+                           const gs_pod_metric* pod_metrics, const uint32_t* pm_offsets);
+
+/* podAssignCache.assign / unAssign (loadaware/pod_assign_cache.go:53-80), i.e. LoadAware Reserve/Unreserve
+ * (load_aware.go:260-267) and the pod informer handlers (pod_assign_cache.go:82-117). Does not touch NodeInfo. */
+int gs_pods_assign(gs_ctx* ctx, const uint32_t* node_idx, const gs_pod* pods, const int64_t* timestamps_ns,
+                   uint32_t n);
+int gs_pods_unassign(gs_ctx* ctx, const uint32_t* node_idx, const gs_pod* pods, uint32_t n);
+
+/* Filter + Score of every pod against every node of the current snapshot, no selection, no state change:
+ * [upstream] RunFilterPlugins (Fit.Filter fit.go, LoadAware.Filter load_aware.go:123-171) and
+ * RunScorePlugins (Fit.Score least_allocated.go, LoadAware.Score load_aware.go:269-335) with profile weights.
+ * scores[p*N+n]  = weighted total, or -1 when the node is infeasible (may be NULL)
+ * codes[p*N+n]   = GS_FAIL_* bits of every failing filter (may be NULL)
+ * plugin_scores[(p*N+n)*GS_NUM_PLUGINS + k] = unweighted score of plugin k, for every node (may be NULL) */
+int gs_evaluate(gs_ctx* ctx, const gs_pod* pods, uint32_t npods, int16_t* scores, uint16_t* codes,
+                int16_t* plugin_scores);
+
+/* Sequential scheduling of npods pods, in order: for each pod the [upstream] scheduleOne cycle
+ * findNodesThatFitPod (percentageOfNodesToScore = 100) -> prioritizeNodes -> selectHost ->
+ * assume (NodeInfo.AddPod) -> Reserve (LoadAware podAssignCache.assign, timestamp = now).
+ * seq[i] keys pod i's tie-break stream. Multi-GPU: every rank passes the same pods and gets the same out[]. */
+int gs_schedule(gs_ctx* ctx, const gs_pod* pods, uint32_t npods, const uint64_t* seq, gs_placement* out);
+
+/* Multi-GPU: nodes are sharded in contiguous ranges [r*ceil(N/R), (r+1)*ceil(N/R)); every rank keeps the full
+ * mirror (replicated deltas) and evaluates only its shard. Native RCCL over xGMI: */
+int gs_comm_unique_id(uint8_t out[128]);
+int gs_comm_init_rccl(gs_ctx* ctx, const uint8_t id[128], int nranks, int rank);
+/* Caller-supplied transport (host buffers): */
+int gs_comm_init_callback(gs_ctx* ctx, int nranks, int rank, gs_allgather_fn fn, void* user);
+
+int gs_get_stats(gs_ctx* ctx, gs_stats* out);
+int gs_reset_stats(gs_ctx* ctx);
+/* Blocks until all device work of ctx has completed. */
+int gs_synchronize(gs_ctx* ctx);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* GPUSCORE_H */

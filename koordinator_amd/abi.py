@@ -1,0 +1,198 @@
+"""ctypes mirror of include/gpuscore.h (the drop-in C-ABI of libgpuscore).
+
+Struct layouts here must match the header byte for byte; tests/test_abi.py checks the sizes
+against the compiled library (gs_abi_sizes) and that every declared symbol is exported.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+GS_ABI_VERSION = 1
+GS_NUM_RES = 8
+GS_RES_CPU, GS_RES_MEMORY, GS_RES_EPHEMERAL = 0, 1, 2
+GS_RES_BATCH_CPU, GS_RES_BATCH_MEMORY, GS_RES_MID_CPU, GS_RES_MID_MEMORY = 3, 4, 5, 6
+GS_SCALAR_RES_MASK = 0x78
+
+GS_PRIO_NONE, GS_PRIO_PROD, GS_PRIO_MID, GS_PRIO_BATCH, GS_PRIO_FREE = 0, 1, 2, 3, 4
+GS_AGG_NONE, GS_AGG_AVG, GS_AGG_P50, GS_AGG_P90, GS_AGG_P95, GS_AGG_P99 = -1, 0, 1, 2, 3, 4
+GS_NUM_AGG_TYPES = 5
+GS_MAX_AGG_USAGES = 4
+GS_USAGE_CPU, GS_USAGE_MEMORY, GS_USAGE_OTHER = 0x1, 0x2, 0x80
+GS_POD_DAEMONSET, GS_POD_TERMINATED = 0x1, 0x2
+GS_NODE_CUSTOM_THRESHOLDS, GS_NODE_CUSTOM_AGGREGATED = 0x1, 0x2
+
+GS_PLUGIN_FIT, GS_PLUGIN_LOADAWARE, GS_NUM_PLUGINS = 0, 1, 2
+GS_ENABLE_FIT_FILTER, GS_ENABLE_FIT_SCORE = 0x1, 0x2
+GS_ENABLE_LA_FILTER, GS_ENABLE_LA_SCORE = 0x4, 0x8
+GS_ENABLE_ALL = 0xF
+
+GS_FAIL_FIT_PODS, GS_FAIL_FIT_CPU, GS_FAIL_FIT_MEMORY = 0x01, 0x02, 0x04
+GS_FAIL_FIT_EPHEMERAL, GS_FAIL_FIT_SCALAR, GS_FAIL_LOADAWARE = 0x08, 0x10, 0x20
+GS_PLACED_SLOWPATH = 0x1
+
+GS_OK, GS_EINVAL, GS_EDEVICE, GS_ENOMEM, GS_EUNSUPPORTED, GS_ECOMM, GS_ESTATE = 0, -1, -2, -3, -4, -5, -6
+
+i64, u64, i32, u32 = C.c_int64, C.c_uint64, C.c_int32, C.c_uint32
+
+
+class GsPod(C.Structure):
+    _fields_ = [
+        ("uid", u64), ("name_key", u64),
+        ("requests", i64 * GS_NUM_RES), ("limits", i64 * GS_NUM_RES),
+        ("nonzero_requests", i64 * 2),
+        ("request_mask", u32), ("priority_class", i32), ("flags", u32), ("pad0", u32),
+    ]
+
+
+class GsNode(C.Structure):
+    _fields_ = [
+        ("allocatable", i64 * GS_NUM_RES), ("requested", i64 * GS_NUM_RES),
+        ("nonzero_requested", i64 * 2),
+        ("allowed_pod_number", i64), ("pod_count", i64),
+        ("raw_allocatable", i64 * 2),
+        ("raw_allocatable_mask", u32), ("custom_flags", u32),
+        ("custom_usage_thresholds", i64 * 2), ("custom_prod_usage_thresholds", i64 * 2),
+        ("custom_agg_usage_thresholds", i64 * 2),
+        ("custom_usage_mask", u32), ("custom_prod_usage_mask", u32), ("custom_agg_usage_mask", u32),
+        ("custom_agg_type", i32), ("custom_agg_duration_ns", i64),
+    ]
+
+
+class GsUsage(C.Structure):
+    _fields_ = [("cpu_milli", i64), ("memory", i64), ("mask", u32), ("pad0", u32)]
+
+
+class GsAggUsage(C.Structure):
+    _fields_ = [("duration_ns", i64), ("type_mask", u32), ("pad0", u32), ("usage", GsUsage * GS_NUM_AGG_TYPES)]
+
+
+class GsNodeMetric(C.Structure):
+    _fields_ = [
+        ("exists", i32), ("has_update_time", i32), ("update_time_ns", i64),
+        ("has_report_interval", i32), ("has_node_metric", i32), ("report_interval_s", i64),
+        ("node_usage", GsUsage), ("n_aggregated", i32), ("pad0", u32),
+        ("aggregated", GsAggUsage * GS_MAX_AGG_USAGES),
+    ]
+
+
+class GsPodMetric(C.Structure):
+    _fields_ = [("name_key", u64), ("in_lister", i32), ("priority_class", i32), ("usage", GsUsage)]
+
+
+class GsLoadAwareArgs(C.Structure):
+    _fields_ = [
+        ("filter_expired_node_metrics", i32), ("has_node_metric_expiration", i32),
+        ("node_metric_expiration_seconds", i64),
+        ("resource_weights", i64 * 2), ("usage_thresholds", i64 * 2),
+        ("prod_usage_thresholds", i64 * 2), ("estimated_scaling_factors", i64 * 2),
+        ("resource_weights_mask", u32), ("usage_thresholds_mask", u32),
+        ("prod_usage_thresholds_mask", u32), ("estimated_scaling_factors_mask", u32),
+        ("score_according_prod_usage", i32), ("has_aggregated", i32),
+        ("agg_usage_thresholds", i64 * 2), ("agg_usage_thresholds_mask", u32),
+        ("agg_usage_type", i32), ("agg_usage_duration_ns", i64),
+        ("agg_score_type", i32), ("pad0", i32), ("agg_score_duration_ns", i64),
+    ]
+
+
+class GsFitArgs(C.Structure):
+    _fields_ = [("resource_weights", i64 * GS_NUM_RES)]
+
+
+class GsConfig(C.Structure):
+    _fields_ = [
+        ("abi_version", u32), ("device", i32), ("num_nodes", u32), ("enabled", u32),
+        ("plugin_weights", i64 * GS_NUM_PLUGINS),
+        ("loadaware", GsLoadAwareArgs), ("fit", GsFitArgs),
+        ("seed", u64), ("batch_size", u32), ("cand_cap", u32),
+    ]
+
+
+class GsPlacement(C.Structure):
+    _fields_ = [("node", i32), ("feasible", u32), ("score", i64), ("ties", u32), ("flags", u32)]
+
+
+class GsStats(C.Structure):
+    _fields_ = [
+        ("batches", u64), ("pods", u64), ("cuts", u64), ("slowpath_pods", u64),
+        ("eval_launches", u64), ("eval_pairs", u64),
+        ("eval_ms", C.c_double), ("cand_ms", C.c_double), ("commit_ms", C.c_double), ("exchange_ms", C.c_double),
+        ("node_row_bytes", u64), ("shard_begin", u32), ("shard_end", u32),
+    ]
+
+
+ALLGATHER_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t)
+
+# numpy dtypes with the exact C layout (for bulk construction of node/pod arrays)
+POD_DTYPE = np.dtype(GsPod)
+NODE_DTYPE = np.dtype(GsNode)
+METRIC_DTYPE = np.dtype(GsNodeMetric)
+POD_METRIC_DTYPE = np.dtype(GsPodMetric)
+PLACEMENT_DTYPE = np.dtype(GsPlacement)
+
+STRUCT_SIZES = {
+    "gs_pod": C.sizeof(GsPod), "gs_node": C.sizeof(GsNode), "gs_node_metric": C.sizeof(GsNodeMetric),
+    "gs_pod_metric": C.sizeof(GsPodMetric), "gs_config": C.sizeof(GsConfig),
+    "gs_placement": C.sizeof(GsPlacement), "gs_stats": C.sizeof(GsStats),
+    "gs_loadaware_args": C.sizeof(GsLoadAwareArgs),
+}
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(PKG_DIR, "libgpuscore.so")
+
+# every symbol include/gpuscore.h declares: name -> (restype, argtypes)
+P = C.c_void_p
+SIGNATURES = {
+    "gs_loadaware_args_default": (None, [C.POINTER(GsLoadAwareArgs)]),
+    "gs_fit_args_default": (None, [C.POINTER(GsFitArgs)]),
+    "gs_loadaware_args_validate": (C.c_int, [C.POINTER(GsLoadAwareArgs), C.c_char_p, C.c_size_t]),
+    "gs_create": (C.c_int, [C.POINTER(GsConfig), C.POINTER(P)]),
+    "gs_destroy": (C.c_int, [P]),
+    "gs_last_error": (C.c_char_p, [P]),
+    "gs_version": (C.c_char_p, []),
+    "gs_set_now": (C.c_int, [P, i64]),
+    "gs_nodes_upsert": (C.c_int, [P, P, P, u32]),
+    "gs_node_metrics_upsert": (C.c_int, [P, P, P, u32, P, P]),
+    "gs_pods_assign": (C.c_int, [P, P, P, P, u32]),
+    "gs_pods_unassign": (C.c_int, [P, P, P, u32]),
+    "gs_evaluate": (C.c_int, [P, P, u32, P, P, P]),
+    "gs_schedule": (C.c_int, [P, P, u32, P, P]),
+    "gs_comm_unique_id": (C.c_int, [P]),
+    "gs_comm_init_rccl": (C.c_int, [P, P, C.c_int, C.c_int]),
+    "gs_comm_init_callback": (C.c_int, [P, C.c_int, C.c_int, ALLGATHER_FN, P]),
+    "gs_get_stats": (C.c_int, [P, C.POINTER(GsStats)]),
+    "gs_reset_stats": (C.c_int, [P]),
+    "gs_synchronize": (C.c_int, [P]),
+}
+
+
+def header_symbols(header_path: str | None = None) -> list[str]:
+    """Function names declared in include/gpuscore.h (parsed, not hard-coded)."""
+    import re
+    if header_path is None:
+        header_path = os.path.join(os.path.dirname(PKG_DIR), "include", "gpuscore.h")
+    text = open(header_path).read()
+    return sorted(set(re.findall(r"^\s*(?:[A-Za-z_][\w\s\*]*?)\b(gs_\w+)\s*\(", text, re.M)))
+
+
+def load(path: str = LIB_PATH) -> C.CDLL:
+    """Load libgpuscore and declare signatures. Raises if the HIP extension is missing."""
+    if not os.path.exists(path):
+        raise RuntimeError(f"libgpuscore not built: {path} missing (run __graft_entry__.build())")
+    lib = C.CDLL(path)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    lib.gs_abi_sizes.restype = None
+    lib.gs_abi_sizes.argtypes = [C.POINTER(u64), u32]
+    return lib
+
+
+def ptr(a) -> int | None:
+    """Address of a numpy array's data (None for None)."""
+    if a is None:
+        return None
+    return a.ctypes.data

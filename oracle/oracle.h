@@ -1,0 +1,54 @@
+/*
+ * oracle.h — CPU restatement of the koord-scheduler Filter/Score hot path.
+ *
+ * TEST INFRASTRUCTURE ONLY. Nothing in koordinator_amd/ may include, link or call this.
+ * It is used by tests/ (as the parity checker), by __graft_entry__.smoke() (as the checker)
+ * and by bench.py's cpu_baseline leg (kind "port": the reference Go path cannot be built
+ * here — no Go toolchain, no module cache).
+ *
+ * Every function follows a reference file:line, cited in oracle.cpp. It consumes the same
+ * decoded POD structs as the product C-ABI (include/gpuscore.h) but re-derives everything
+ * per call with reference-shaped data structures (per-node assign cache, per-call metric maps),
+ * sharing no code with the product.
+ */
+#ifndef GS_ORACLE_H
+#define GS_ORACLE_H
+
+#include "../include/gpuscore.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct or_cluster or_cluster;
+
+or_cluster* or_create(const gs_config* cfg);
+void or_destroy(or_cluster* c);
+int or_set_now(or_cluster* c, int64_t now_ns);
+int or_nodes_upsert(or_cluster* c, const uint32_t* idx, const gs_node* nodes, uint32_t n);
+int or_node_metrics_upsert(or_cluster* c, const uint32_t* idx, const gs_node_metric* m, uint32_t n,
+                           const gs_pod_metric* pm, const uint32_t* pm_offsets);
+int or_pods_assign(or_cluster* c, const uint32_t* node_idx, const gs_pod* pods, const int64_t* ts, uint32_t n);
+int or_pods_unassign(or_cluster* c, const uint32_t* node_idx, const gs_pod* pods, uint32_t n);
+
+/* plugin-level restatements */
+int or_estimate_pod(const gs_loadaware_args* a, const gs_pod* pod, int64_t out[2], uint32_t* out_mask);
+int or_estimate_node(const gs_node* node, int64_t out[2]);
+int or_loadaware_filter(or_cluster* c, const gs_pod* pod, uint32_t node, int32_t* fail);
+int or_loadaware_score(or_cluster* c, const gs_pod* pod, uint32_t node, int64_t* score);
+int or_fit_filter(or_cluster* c, const gs_pod* pod, uint32_t node, uint32_t* fail_bits);
+int or_fit_score(or_cluster* c, const gs_pod* pod, uint32_t node, int64_t* score);
+
+/* framework-level restatements (same output layout as gs_evaluate / gs_schedule) */
+int or_evaluate(or_cluster* c, const gs_pod* pods, uint32_t npods, int16_t* scores, uint16_t* codes,
+                int16_t* plugin_scores);
+/* nthreads <= 1: serial; otherwise a worker pool emulating parallelize.Until (pkg/util/parallelize/parallelism.go:29-49) */
+int or_schedule(or_cluster* c, const gs_pod* pods, uint32_t npods, const uint64_t* seq, gs_placement* out,
+                int nthreads);
+/* the selectHost tie-break stream: Intn(cnt) of pod stream `seq` (see oracle.cpp TieBreakRand) */
+int32_t or_tiebreak_intn(uint64_t seed, uint64_t seq, int64_t cnt);
+
+#ifdef __cplusplus
+}
+#endif
+#endif
