@@ -298,6 +298,13 @@ int gs_reset_stats(gs_ctx* ctx);
 /* Blocks until all device work of ctx has completed. */
 int gs_synchronize(gs_ctx* ctx);
 
+/* Diagnostics: re-derives every node row on the host and compares it with the HBM mirror; returns the
+ * number of mismatching rows (0 = the device-side Assume/Reserve replay matches the host mirror). */
+int gs_debug_mirror_check(gs_ctx* ctx);
+/* sizeof() of the ABI structs as compiled into the library, in this order: gs_pod, gs_node,
+ * gs_node_metric, gs_pod_metric, gs_config, gs_placement, gs_stats, gs_loadaware_args. */
+void gs_abi_sizes(uint64_t* out, uint32_t n);
+
 #ifdef __cplusplus
 }
 #endif

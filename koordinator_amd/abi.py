@@ -165,6 +165,8 @@ SIGNATURES = {
     "gs_get_stats": (C.c_int, [P, C.POINTER(GsStats)]),
     "gs_reset_stats": (C.c_int, [P]),
     "gs_synchronize": (C.c_int, [P]),
+    "gs_debug_mirror_check": (C.c_int, [P]),
+    "gs_abi_sizes": (None, [C.POINTER(u64), u32]),
 }
 
 
@@ -186,8 +188,6 @@ def load(path: str = LIB_PATH) -> C.CDLL:
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
-    lib.gs_abi_sizes.restype = None
-    lib.gs_abi_sizes.argtypes = [C.POINTER(u64), u32]
     return lib
 
 

@@ -1,0 +1,1080 @@
+// gs_engine.cpp — libgpuscore host side: the C-ABI of include/gpuscore.h over the HIP kernels.
+//
+// Owns the host mirror of the scheduler state the hot path reads (NodeInfo rows, NodeMetrics, the
+// LoadAware podAssignCache) and its HBM structure-of-arrays image. Per-node derived columns (LoadAware
+// usage verdicts, estimated usage, free capacities) are recomputed on the host only for rows an event
+// touched and scattered to HBM; pod placements made by gs_schedule are applied on the device by the
+// commit kernel and replayed on the host mirror, so no row crosses PCIe for them.
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/gpuscore.h"
+#include "gs_kernels.h"
+
+using namespace gs;
+
+namespace {
+
+constexpr int64_t kDefaultMilliCPURequest = 250;              // loadaware/estimator/default_estimator.go:36
+constexpr int64_t kDefaultMemoryRequest = 200LL * 1024 * 1024; // loadaware/estimator/default_estimator.go:38
+constexpr int64_t kDefaultReportIntervalNs = 60LL * 1000000000LL;
+constexpr int64_t kZeroTime = INT64_MIN;
+constexpr int64_t kMaxExact = 1LL << 53;                      // value bound for the exact int64 score paths
+
+struct Assigned {
+  int64_t ts;
+  gs_pod pod;
+};
+
+struct HostNode {
+  gs_node node{};
+  bool valid = false;
+  gs_node_metric metric{};
+  std::vector<gs_pod_metric> pms;
+  std::unordered_map<uint64_t, Assigned> assigned;   // podAssignCache.podInfoItems[node]
+};
+
+struct Vec2 {
+  int64_t v[2] = {0, 0};
+  uint32_t mask = 0;
+  bool has(int r) const { return mask & (1u << r); }
+  int64_t get(int r) const { return has(r) ? v[r] : 0; }
+  void add(int r, int64_t x) { v[r] = get(r) + x; mask |= 1u << r; }
+};
+
+Vec2 usage_of(const gs_usage& u) {
+  Vec2 o;
+  if (u.mask & GS_USAGE_CPU) { o.v[0] = u.cpu_milli; o.mask |= 1; }
+  if (u.mask & GS_USAGE_MEMORY) { o.v[1] = u.memory; o.mask |= 2; }
+  if (u.mask & GS_USAGE_OTHER) o.mask |= GS_USAGE_OTHER;
+  return o;
+}
+
+}  // namespace
+
+struct gs_ctx {
+  gs_config cfg{};
+  std::string err;
+  uint32_t N = 0, npad = 0;
+  hipStream_t st = nullptr;
+  // device mirror
+  int64_t* d_i64 = nullptr;
+  int32_t* d_i32 = nullptr;
+  MirrorView mv{};
+  // batch buffers
+  int B = MAX_BATCH;
+  PodVec* d_pods = nullptr;
+  uint64_t* d_seq = nullptr;
+  int16_t* d_S = nullptr;
+  uint32_t ld = 0;
+  uint8_t* d_xchg_send = nullptr;   // local lists + headers (contiguous, all-gathered)
+  uint8_t* d_xchg_recv = nullptr;   // R blocks
+  size_t xchg_bytes = 0;
+  PlacementDev* d_out = nullptr;
+  int32_t* d_committed = nullptr;
+  RowStat* d_rowstat = nullptr;
+  int32_t* d_sel = nullptr;
+  uint32_t* d_stage_idx = nullptr;
+  int64_t* d_stage_rows = nullptr;
+  uint32_t stage_cap = 0;
+  // pinned host buffers
+  PodVec* h_pods = nullptr;
+  uint64_t* h_seq = nullptr;
+  PlacementDev* h_out = nullptr;
+  int32_t* h_committed = nullptr;
+  uint32_t* h_stage_idx = nullptr;
+  int64_t* h_stage_rows = nullptr;
+  uint8_t* h_xchg_send = nullptr;
+  uint8_t* h_xchg_recv = nullptr;
+  hipEvent_t ev[8] = {};
+  // host mirror
+  std::vector<HostNode> nodes;
+  std::vector<uint8_t> row_dirty;
+  std::vector<uint32_t> dirty_list;
+  std::unordered_map<uint64_t, uint32_t> uid_node;
+  std::unordered_map<uint64_t, int> metric_names;
+  int64_t now = 0;
+  bool prep_stale = true;
+  Profile pf{};
+  int max_score = 0;
+  // sharding
+  int nranks = 1, rank = 0;
+  uint32_t n0 = 0, n1 = 0;
+  ncclComm_t comm = nullptr;
+  gs_allgather_fn cb = nullptr;
+  void* cb_user = nullptr;
+  gs_stats stats{};
+};
+
+namespace {
+
+int fail(gs_ctx* c, int code, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  if (c) c->err = buf;
+  return code;
+}
+
+#define HIP_TRY(c, expr)                                                                    \
+  do {                                                                                      \
+    hipError_t _e = (expr);                                                                 \
+    if (_e != hipSuccess) return fail((c), GS_EDEVICE, "%s: %s", #expr, hipGetErrorString(_e)); \
+  } while (0)
+
+// ---- DefaultEstimator (loadaware/estimator/default_estimator.go:57-108) ------------------------
+int translate(int32_t prio, int r) {   // extension.TranslateResourceNameByPriorityClass
+  if (prio == GS_PRIO_PROD || prio == GS_PRIO_NONE) return r;
+  if (prio == GS_PRIO_BATCH) return r == 0 ? GS_RES_BATCH_CPU : GS_RES_BATCH_MEMORY;
+  if (prio == GS_PRIO_MID) return r == 0 ? GS_RES_MID_CPU : GS_RES_MID_MEMORY;
+  return -1;
+}
+
+int64_t estimate_resource(const gs_pod& p, int real, int64_t sf) {
+  int64_t lim = real >= 0 ? p.limits[real] : 0, req = real >= 0 ? p.requests[real] : 0;
+  int64_t q = req;
+  if (lim > req) { sf = 100; q = lim; }
+  if (q == 0) {
+    if (real == GS_RES_CPU || real == GS_RES_BATCH_CPU) return kDefaultMilliCPURequest;
+    if (real == GS_RES_MEMORY || real == GS_RES_BATCH_MEMORY) return kDefaultMemoryRequest;
+    return 0;
+  }
+  int64_t e = (int64_t)std::round((double)q * (double)sf / 100);
+  if (lim > 0 && e > lim) e = lim;
+  return e;
+}
+
+Vec2 estimate_pod(const gs_loadaware_args& a, const gs_pod& p) {
+  Vec2 o;
+  for (int r = 0; r < 2; ++r) {
+    if (!(a.resource_weights_mask & (1u << r))) continue;
+    int64_t sf = (a.estimated_scaling_factors_mask & (1u << r)) ? a.estimated_scaling_factors[r] : 0;
+    o.add(r, estimate_resource(p, translate(p.priority_class, r), sf));
+  }
+  return o;
+}
+
+int64_t estimate_node(const gs_node& n, int r) {   // EstimateNode (default_estimator.go:110-129)
+  return (n.raw_allocatable_mask & (1u << r)) ? n.raw_allocatable[r] : n.allocatable[r];
+}
+
+// ---- LoadAware node-side derivations (loadaware/load_aware.go, helper.go) -----------------------
+bool target_agg(const gs_node_metric& m, int64_t dur, int32_t type, Vec2* out) {   // helper.go:58-90
+  if (!m.has_node_metric || m.n_aggregated <= 0 || type < 0 || type >= GS_NUM_AGG_TYPES) return false;
+  int n = std::min(m.n_aggregated, GS_MAX_AGG_USAGES);
+  if (dur == 0) {
+    int64_t maxd = 0;
+    int mi = 0;
+    for (int i = 0; i < n; ++i)
+      if (m.aggregated[i].duration_ns > maxd) { maxd = m.aggregated[i].duration_ns; mi = i; }
+    if (m.aggregated[mi].type_mask & (1u << type)) {
+      Vec2 u = usage_of(m.aggregated[mi].usage[type]);
+      if (u.mask) { *out = u; return true; }
+    }
+    return false;
+  }
+  for (int i = 0; i < n; ++i) {
+    if (m.aggregated[i].duration_ns != dur || !(m.aggregated[i].type_mask & (1u << type))) continue;
+    Vec2 u = usage_of(m.aggregated[i].usage[type]);
+    if (u.mask) { *out = u; return true; }
+  }
+  return false;
+}
+
+struct Thr {
+  int64_t v[2] = {0, 0};
+  uint32_t mask = 0;
+};
+
+bool usage_exceeds(const Thr& th, const Vec2& used, const gs_node& n) {
+  for (int r = 0; r < 2; ++r) {
+    if (!(th.mask & (1u << r)) || th.v[r] == 0) continue;
+    int64_t total = estimate_node(n, r);
+    if (total == 0) continue;
+    int64_t u = used.get(r);
+    double mu = (double)(r == 0 ? u : u * 1000), mt = (double)(r == 0 ? total : total * 1000);
+    int64_t pct = (int64_t)std::round(mu / mt * 100);   // load_aware.go:214,248
+    if (pct >= th.v[r]) return true;
+  }
+  return false;
+}
+
+struct LaDerived {
+  uint32_t sflags = 0;
+  int64_t used_np[2] = {0, 0};
+  int64_t used_p[2] = {0, 0};
+};
+
+LaDerived derive_loadaware(const gs_loadaware_args& a, const HostNode& hn) {
+  LaDerived d;
+  const gs_node& n = hn.node;
+  const gs_node_metric& m = hn.metric;
+  if (!m.exists) return d;
+  d.sflags |= SF_METRIC;
+  if (m.has_update_time) d.sflags |= SF_UPDATE_TIME;
+  // ---- Filter profile (helper.go:102-140)
+  Thr usage{{a.usage_thresholds[0], a.usage_thresholds[1]}, a.usage_thresholds_mask};
+  Thr prod{{a.prod_usage_thresholds[0], a.prod_usage_thresholds[1]}, a.prod_usage_thresholds_mask};
+  bool has_agg = false;
+  Thr agg;
+  int32_t agg_type = GS_AGG_NONE;
+  int64_t agg_dur = 0;
+  if (n.custom_flags & GS_NODE_CUSTOM_THRESHOLDS) {
+    if (n.custom_usage_mask) usage = Thr{{n.custom_usage_thresholds[0], n.custom_usage_thresholds[1]}, n.custom_usage_mask};
+    if (n.custom_prod_usage_mask)
+      prod = Thr{{n.custom_prod_usage_thresholds[0], n.custom_prod_usage_thresholds[1]}, n.custom_prod_usage_mask};
+    if ((n.custom_flags & GS_NODE_CUSTOM_AGGREGATED) && n.custom_agg_usage_mask && n.custom_agg_type != GS_AGG_NONE) {
+      has_agg = true;
+      agg = Thr{{n.custom_agg_usage_thresholds[0], n.custom_agg_usage_thresholds[1]}, n.custom_agg_usage_mask};
+      agg_type = n.custom_agg_type;
+      agg_dur = n.custom_agg_duration_ns;
+    }
+  }
+  if (!has_agg && a.has_aggregated && a.agg_usage_thresholds_mask && a.agg_usage_type != GS_AGG_NONE) {
+    has_agg = true;
+    agg = Thr{{a.agg_usage_thresholds[0], a.agg_usage_thresholds[1]}, a.agg_usage_thresholds_mask};
+    agg_type = a.agg_usage_type;
+    agg_dur = a.agg_usage_duration_ns;
+  }
+  // non-prod verdict: filterNodeUsage (load_aware.go:173-224)
+  const Thr& th = has_agg ? agg : usage;
+  if (th.mask && m.has_node_metric) {
+    Vec2 u;
+    bool have = has_agg ? target_agg(m, agg_dur, agg_type, &u) : (u = usage_of(m.node_usage), true);
+    if (have && usage_exceeds(th, u, n)) d.sflags |= SF_FAIL_NP;
+  }
+  // prod verdict: filterProdUsage (load_aware.go:226-254)
+  if (prod.mask) {
+    d.sflags |= SF_PROD_THR;
+    if (!hn.pms.empty()) {
+      std::unordered_map<uint64_t, Vec2> pm;
+      for (const auto& e : hn.pms)
+        if (e.in_lister && e.priority_class == GS_PRIO_PROD) pm[e.name_key] = usage_of(e.usage);
+      Vec2 sum;
+      for (const auto& kv : pm)
+        for (int r = 0; r < 2; ++r)
+          if (kv.second.has(r)) sum.add(r, kv.second.v[r]);
+      if (usage_exceeds(prod, sum, n)) d.sflags |= SF_FAIL_P;
+    }
+  }
+  // ---- Score-side usage (load_aware.go:291-327, 337-376), for both prodPod modes
+  int64_t update = m.has_update_time ? m.update_time_ns : kZeroTime;
+  int64_t interval = m.has_report_interval ? m.report_interval_s * 1000000000LL : kDefaultReportIntervalNs;
+  bool score_agg = a.has_aggregated && a.agg_score_type != GS_AGG_NONE;
+  Vec2 score_usage;
+  bool have_score_usage = false;
+  if (score_agg) have_score_usage = target_agg(m, a.agg_score_duration_ns, a.agg_score_type, &score_usage);
+  bool agg_missing = score_agg && !have_score_usage;
+  for (int mode = 0; mode < 2; ++mode) {
+    bool prod_mode = mode == 1;
+    std::unordered_map<uint64_t, Vec2> pm;
+    for (const auto& e : hn.pms) {
+      if (!e.in_lister) continue;
+      if (prod_mode && e.priority_class != GS_PRIO_PROD) continue;
+      pm[e.name_key] = usage_of(e.usage);
+    }
+    Vec2 used;
+    std::unordered_map<uint64_t, bool> estimated;
+    for (const auto& kv : hn.assigned) {
+      const Assigned& as = kv.second;
+      if (prod_mode && as.pod.priority_class != GS_PRIO_PROD) continue;
+      auto it = pm.find(as.pod.name_key);
+      Vec2 pu;
+      if (it != pm.end()) pu = it->second;
+      bool est_it = pu.mask == 0 || as.ts > update || (as.ts < update && update - as.ts < interval) || agg_missing;
+      if (!est_it) continue;
+      Vec2 e = estimate_pod(a, as.pod);
+      for (int r = 0; r < 2; ++r) {
+        if (!e.has(r)) continue;
+        int64_t v = e.v[r];
+        if (pu.has(r) && pu.v[r] > v) v = pu.v[r];
+        used.add(r, v);
+      }
+      estimated[as.pod.name_key] = true;
+    }
+    Vec2 actual, est_actual;
+    for (const auto& kv : pm) {
+      Vec2& dst = estimated.count(kv.first) ? est_actual : actual;
+      for (int r = 0; r < 2; ++r)
+        if (kv.second.has(r)) dst.add(r, kv.second.v[r]);
+    }
+    if (prod_mode) {
+      for (int r = 0; r < 2; ++r) used.add(r, actual.get(r));
+    } else if (m.has_node_metric) {
+      Vec2 nu;
+      bool have = score_agg ? have_score_usage : true;
+      if (score_agg) nu = score_usage;
+      else nu = usage_of(m.node_usage);
+      if (have) {
+        for (int r = 0; r < 2; ++r) {
+          if (!nu.has(r)) continue;
+          int64_t q = nu.v[r], e = est_actual.get(r);
+          if (e != 0 && q >= e) q -= e;
+          used.add(r, q);
+        }
+      }
+    }
+    int64_t* dst = prod_mode ? d.used_p : d.used_np;
+    dst[0] = used.get(0);
+    dst[1] = used.get(1);
+  }
+  return d;
+}
+
+void derive_row(const gs_ctx* c, const HostNode& hn, int64_t* row) {
+  const gs_node& n = hn.node;
+  for (int s = 0; s < 7; ++s) {
+    row[C_FREE_CPU + s] = n.allocatable[s] - n.requested[s];
+    row[C_ALLOC_CPU + s] = n.allocatable[s];
+  }
+  row[C_NZFREE_CPU] = n.allocatable[0] - n.nonzero_requested[0];
+  row[C_NZFREE_MEM] = n.allocatable[1] - n.nonzero_requested[1];
+  LaDerived d = derive_loadaware(c->cfg.loadaware, hn);
+  for (int r = 0; r < 2; ++r) {
+    int64_t cap = estimate_node(n, r);
+    row[C_LA_CAP_CPU + r] = cap;
+    row[C_LA_FREE_CPU + r] = cap - d.used_np[r];
+    row[C_LA_PFREE_CPU + r] = cap - d.used_p[r];
+  }
+  row[C_UPDATE_TIME] = hn.metric.has_update_time ? hn.metric.update_time_ns : 0;
+  int64_t fp = n.allowed_pod_number - n.pod_count;
+  fp = std::max<int64_t>(INT32_MIN, std::min<int64_t>(INT32_MAX, fp));
+  row[NUM_I64_COLS + C_FREE_PODS] = fp;
+  row[NUM_I64_COLS + C_SFLAGS] = (int64_t)(d.sflags | (hn.valid ? SF_VALID : 0));
+  row[NUM_I64_COLS + C_DFLAGS] = 0;
+}
+
+bool in_range(int64_t v) { return v > -kMaxExact && v < kMaxExact; }
+
+int validate_node(gs_ctx* c, const gs_node& n) {
+  for (int s = 0; s < GS_NUM_RES; ++s)
+    if (!in_range(n.allocatable[s]) || !in_range(n.requested[s]) || n.allocatable[s] < 0)
+      return fail(c, GS_EUNSUPPORTED, "node resource slot %d outside the exact range [0, 2^53)", s);
+  if (!in_range(n.nonzero_requested[0]) || !in_range(n.nonzero_requested[1]) || !in_range(n.raw_allocatable[0]) ||
+      !in_range(n.raw_allocatable[1]) || n.raw_allocatable[0] < 0 || n.raw_allocatable[1] < 0)
+    return fail(c, GS_EUNSUPPORTED, "node quantity outside the exact range [0, 2^53)");
+  if (n.allocatable[GS_RES_RESERVED] || n.requested[GS_RES_RESERVED])
+    return fail(c, GS_EINVAL, "resource slot 7 is reserved");
+  return GS_OK;
+}
+
+PodVec prep_pod(const gs_ctx* c, const gs_pod& p) {
+  PodVec v{};
+  for (int s = 0; s < 7; ++s) v.req[s] = p.requests[s];
+  v.nz[0] = p.nonzero_requests[0];
+  v.nz[1] = p.nonzero_requests[1];
+  Vec2 e = estimate_pod(c->cfg.loadaware, p);
+  v.est[0] = e.get(0);
+  v.est[1] = e.get(1);
+  uint32_t f = 0;
+  if (p.flags & GS_POD_DAEMONSET) f |= PF_DAEMONSET;
+  if (p.priority_class == GS_PRIO_PROD) {
+    f |= PF_PROD;
+    if (c->cfg.loadaware.score_according_prod_usage) f |= PF_PROD_SCORE;
+  }
+  uint32_t scalar = p.request_mask & GS_SCALAR_RES_MASK;
+  if (p.requests[0] == 0 && p.requests[1] == 0 && p.requests[2] == 0 && scalar == 0) f |= PF_ALL_ZERO;
+  v.flags = f;
+  v.scalar_mask = scalar;
+  return v;
+}
+
+int validate_pod(gs_ctx* c, const gs_pod& p) {
+  for (int s = 0; s < GS_NUM_RES; ++s)
+    if (!in_range(p.requests[s]) || p.requests[s] < 0 || !in_range(p.limits[s]) || p.limits[s] < 0)
+      return fail(c, GS_EUNSUPPORTED, "pod resource slot %d outside the exact range [0, 2^53)", s);
+  if (p.requests[GS_RES_RESERVED] || (p.request_mask & 0x80u)) return fail(c, GS_EINVAL, "resource slot 7 is reserved");
+  return GS_OK;
+}
+
+void mark_dirty(gs_ctx* c, uint32_t i) {
+  if (!c->row_dirty[i]) {
+    c->row_dirty[i] = 1;
+    c->dirty_list.push_back(i);
+  }
+}
+
+int flush_rows(gs_ctx* c) {
+  if (c->dirty_list.empty()) return GS_OK;
+  size_t done = 0;
+  while (done < c->dirty_list.size()) {
+    uint32_t n = (uint32_t)std::min<size_t>(c->stage_cap, c->dirty_list.size() - done);
+    // staging buffers are reused: the previous scatter must have consumed them
+    HIP_TRY(c, hipStreamSynchronize(c->st));
+    for (uint32_t j = 0; j < n; ++j) {
+      uint32_t i = c->dirty_list[done + j];
+      c->h_stage_idx[j] = i;
+      derive_row(c, c->nodes[i], c->h_stage_rows + (size_t)j * ROW_WORDS);
+      c->row_dirty[i] = 0;
+    }
+    HIP_TRY(c, hipMemcpyAsync(c->d_stage_idx, c->h_stage_idx, n * 4, hipMemcpyHostToDevice, c->st));
+    HIP_TRY(c, hipMemcpyAsync(c->d_stage_rows, c->h_stage_rows, (size_t)n * ROW_WORDS * 8, hipMemcpyHostToDevice, c->st));
+    HIP_TRY(c, launch_scatter_rows(c->mv, c->d_stage_idx, c->d_stage_rows, n, c->st));
+    done += n;
+  }
+  c->dirty_list.clear();
+  c->prep_stale = true;
+  return GS_OK;
+}
+
+int node_prep(gs_ctx* c) {
+  const gs_loadaware_args& a = c->cfg.loadaware;
+  int64_t exp_ns = a.has_node_metric_expiration ? a.node_metric_expiration_seconds * 1000000000LL : 0;
+  HIP_TRY(c, launch_node_prep(c->mv, 0, c->N, c->now, a.filter_expired_node_metrics, a.has_node_metric_expiration,
+                              exp_ns, c->st));
+  c->prep_stale = false;
+  return GS_OK;
+}
+
+int ready(gs_ctx* c) {
+  for (uint32_t i = 0; i < c->N; ++i)
+    if (!c->nodes[i].valid) return fail(c, GS_ESTATE, "node %u was never upserted", i);
+  return GS_OK;
+}
+
+int exchange(gs_ctx* c, const void* d_send, void* d_recv, size_t bytes) {
+  auto t0 = std::chrono::steady_clock::now();
+  if (c->comm) {
+    ncclResult_t r = ncclAllGather(d_send, d_recv, bytes, ncclUint8, c->comm, c->st);
+    if (r != ncclSuccess) return fail(c, GS_ECOMM, "ncclAllGather: %s", ncclGetErrorString(r));
+  } else if (c->cb) {
+    if (bytes > c->xchg_bytes) return fail(c, GS_EINVAL, "exchange payload too large");
+    HIP_TRY(c, hipMemcpyAsync(c->h_xchg_send, d_send, bytes, hipMemcpyDeviceToHost, c->st));
+    HIP_TRY(c, hipStreamSynchronize(c->st));
+    if (c->cb(c->cb_user, c->h_xchg_send, c->h_xchg_recv, bytes) != 0) return fail(c, GS_ECOMM, "allgather callback failed");
+    HIP_TRY(c, hipMemcpyAsync(d_recv, c->h_xchg_recv, bytes * c->nranks, hipMemcpyHostToDevice, c->st));
+  } else {
+    return fail(c, GS_ESTATE, "multi-rank context without a communicator");
+  }
+  c->stats.exchange_ms +=
+      std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  return GS_OK;
+}
+
+bool special_pod(const gs_ctx* c, const gs_pod& p) {
+  // Placements whose LoadAware effect is not "+EstimatePod" on the chosen row: the pod UID already sits
+  // in an assign cache, a PodMetric with the pod's name exists, or the pod is terminated (assign skips it).
+  if (p.flags & GS_POD_TERMINATED) return true;
+  if (c->uid_node.count(p.uid)) return true;
+  if (c->metric_names.count(p.name_key)) return true;
+  return false;
+}
+
+void apply_placement(gs_ctx* c, const gs_pod& p, int32_t node, bool special) {
+  if (node < 0) return;
+  HostNode& hn = c->nodes[node];
+  for (int s = 0; s < GS_NUM_RES; ++s) hn.node.requested[s] += p.requests[s];
+  hn.node.nonzero_requested[0] += p.nonzero_requests[0];
+  hn.node.nonzero_requested[1] += p.nonzero_requests[1];
+  hn.node.pod_count += 1;
+  if (!(p.flags & GS_POD_TERMINATED)) {
+    hn.assigned[p.uid] = Assigned{c->now, p};
+    c->uid_node[p.uid] = (uint32_t)node;
+  }
+  if (special) mark_dirty(c, (uint32_t)node);
+}
+
+void index_metric_names(gs_ctx* c, const HostNode& hn, int delta) {
+  for (const auto& e : hn.pms) {
+    auto it = c->metric_names.find(e.name_key);
+    if (delta > 0) {
+      c->metric_names[e.name_key] += 1;
+    } else if (it != c->metric_names.end()) {
+      if (--it->second <= 0) c->metric_names.erase(it);
+    }
+  }
+}
+
+int compute_profile(gs_ctx* c) {
+  const gs_config& cfg = c->cfg;
+  Profile& pf = c->pf;
+  pf = Profile{};
+  pf.enabled = cfg.enabled & 0xFu;
+  pf.w_fit = (int32_t)cfg.plugin_weights[GS_PLUGIN_FIT];
+  pf.w_la = (int32_t)cfg.plugin_weights[GS_PLUGIN_LOADAWARE];
+  for (int r = 0; r < 2; ++r) {
+    if (cfg.loadaware.resource_weights_mask & (1u << r)) pf.la_w[r] = (int32_t)cfg.loadaware.resource_weights[r];
+    pf.la_wsum += pf.la_w[r];
+  }
+  for (int s = 0; s < 7; ++s) {
+    int64_t w = cfg.fit.resource_weights[s];
+    if (w < 0 || w > 100) return fail(c, GS_EINVAL, "NodeResourcesFit weight of slot %d not in (0, 100]", s);
+    pf.fit_w[s] = (int32_t)w;
+    if (s >= 2 && w) pf.fit_scalar_w_mask |= 1u << s;
+  }
+  if (cfg.fit.resource_weights[7]) return fail(c, GS_EINVAL, "resource slot 7 is reserved");
+  if ((pf.enabled & GS_ENABLE_LA_SCORE) && pf.la_wsum == 0)
+    return fail(c, GS_EINVAL, "LoadAwareScheduling scoring needs at least one resource weight");
+  int64_t ms = 0;
+  if (pf.enabled & GS_ENABLE_FIT_SCORE) ms += 100 * cfg.plugin_weights[GS_PLUGIN_FIT];
+  if (pf.enabled & GS_ENABLE_LA_SCORE) ms += 100 * cfg.plugin_weights[GS_PLUGIN_LOADAWARE];
+  if (cfg.plugin_weights[0] < 0 || cfg.plugin_weights[1] < 0 || ms > 8191)
+    return fail(c, GS_EUNSUPPORTED, "profile score weights must keep the max total score <= 8191 (got %lld)",
+                (long long)ms);
+  c->max_score = (int)ms;
+  return GS_OK;
+}
+
+void set_shard(gs_ctx* c) {
+  uint32_t per = (c->N + c->nranks - 1) / c->nranks;
+  c->n0 = std::min(c->N, per * (uint32_t)c->rank);
+  c->n1 = std::min(c->N, c->n0 + per);
+  c->stats.shard_begin = c->n0;
+  c->stats.shard_end = c->n1;
+}
+
+// one rank's exchange block: [B x CAND_CAP list keys | B headers], padded so that rank blocks stay
+// addressable as whole pod lists (stride in units of CAND_CAP keys)
+size_t xchg_block_bytes(int B) {
+  size_t raw = (size_t)B * CAND_CAP * 8 + (size_t)B * sizeof(CandHdr);
+  size_t unit = (size_t)CAND_CAP * 8;
+  return (raw + unit - 1) / unit * unit;
+}
+
+int alloc_exchange(gs_ctx* c) {
+  c->xchg_bytes = xchg_block_bytes(c->B);
+  if (c->d_xchg_recv) { (void)hipFree(c->d_xchg_recv); c->d_xchg_recv = nullptr; }
+  if (c->h_xchg_recv) { (void)hipHostFree(c->h_xchg_recv); c->h_xchg_recv = nullptr; }
+  HIP_TRY(c, hipMalloc(&c->d_xchg_recv, c->xchg_bytes * c->nranks + 64));
+  HIP_TRY(c, hipHostMalloc(&c->h_xchg_recv, c->xchg_bytes * c->nranks + 64, hipHostMallocDefault));
+  return GS_OK;
+}
+
+double ev_ms(hipEvent_t a, hipEvent_t b) {
+  float ms = 0;
+  if (hipEventElapsedTime(&ms, a, b) != hipSuccess) return 0;
+  return ms;
+}
+
+// One device pass over pods [0, b) of the staged batch. Returns number of pods committed (>= 1).
+int run_batch(gs_ctx* c, const gs_pod* pods, int b, int* committed_out) {
+  const size_t lists_bytes = (size_t)c->B * CAND_CAP * 8;
+  uint64_t* d_lists = reinterpret_cast<uint64_t*>(c->d_xchg_send);
+  CandHdr* d_hdrs = reinterpret_cast<CandHdr*>(c->d_xchg_send + lists_bytes);
+  int prod_cols = 0;
+  for (int i = 0; i < b; ++i) prod_cols |= (c->h_pods[i].flags & PF_PROD_SCORE) ? 1 : 0;
+  uint32_t len = c->n1 - c->n0;
+  HIP_TRY(c, hipEventRecord(c->ev[0], c->st));
+  HIP_TRY(c, launch_eval(c->mv, c->d_pods, b, c->pf, c->n0, c->n1, c->d_S, c->ld, prod_cols, c->st));
+  HIP_TRY(c, hipEventRecord(c->ev[1], c->st));
+  HIP_TRY(c, launch_cand(c->d_S, c->ld, len, c->n0, b, c->max_score, d_lists, d_hdrs, c->st));
+  HIP_TRY(c, hipEventRecord(c->ev[2], c->st));
+  const uint64_t* all_lists = d_lists;
+  const CandHdr* all_hdrs = d_hdrs;
+  size_t list_stride = (size_t)c->B, hdr_stride = (size_t)c->B;
+  if (c->nranks > 1) {
+    int rc = exchange(c, c->d_xchg_send, c->d_xchg_recv, c->xchg_bytes);
+    if (rc) return rc;
+    // recv = R blocks of [lists | hdrs]; view them with strides in units of one rank block
+    all_lists = reinterpret_cast<const uint64_t*>(c->d_xchg_recv);
+    all_hdrs = reinterpret_cast<const CandHdr*>(c->d_xchg_recv + lists_bytes);
+    list_stride = c->xchg_bytes / (CAND_CAP * 8);              // pods-per-rank-block in list units
+    hdr_stride = c->xchg_bytes / sizeof(CandHdr);
+  }
+  CommitArgs a{};
+  a.m = c->mv;
+  a.pods = c->d_pods;
+  a.seq = c->d_seq;
+  a.npods = b;
+  a.nranks = c->nranks;
+  a.lists = all_lists;
+  a.hdrs = all_hdrs;
+  a.list_stride = list_stride;
+  a.hdr_stride = hdr_stride;
+  a.pf = c->pf;
+  a.seed = c->cfg.seed;
+  a.forced_node = -1;
+  a.out = c->d_out;
+  a.committed = c->d_committed;
+  HIP_TRY(c, hipEventRecord(c->ev[3], c->st));
+  HIP_TRY(c, launch_commit(a, c->st));
+  HIP_TRY(c, hipEventRecord(c->ev[4], c->st));
+  HIP_TRY(c, hipMemcpyAsync(c->h_committed, c->d_committed, 4, hipMemcpyDeviceToHost, c->st));
+  HIP_TRY(c, hipStreamSynchronize(c->st));
+  c->stats.eval_ms += ev_ms(c->ev[0], c->ev[1]);
+  c->stats.cand_ms += ev_ms(c->ev[1], c->ev[2]);
+  c->stats.commit_ms += ev_ms(c->ev[3], c->ev[4]);
+  c->stats.eval_launches += 1;
+  c->stats.eval_pairs += (uint64_t)b * len;
+  c->stats.batches += 1;
+  int committed = *c->h_committed;
+  if (committed == 0) {
+    // exact full-row path for pod 0: (max, ties, feasible) of every shard's row, global selection
+    c->stats.slowpath_pods += 1;
+    HIP_TRY(c, launch_row_stats(c->d_S, len, c->d_rowstat, c->st));
+    std::vector<RowStat> rs(c->nranks);
+    if (c->nranks > 1) {
+      int rc = exchange(c, c->d_rowstat, c->d_rowstat + 1, sizeof(RowStat));
+      if (rc) return rc;
+      HIP_TRY(c, hipMemcpyAsync(rs.data(), c->d_rowstat + 1, sizeof(RowStat) * c->nranks, hipMemcpyDeviceToHost, c->st));
+    } else {
+      HIP_TRY(c, hipMemcpyAsync(rs.data(), c->d_rowstat, sizeof(RowStat), hipMemcpyDeviceToHost, c->st));
+    }
+    HIP_TRY(c, hipStreamSynchronize(c->st));
+    int M = -1;
+    int64_t T = 0, F = 0;
+    for (const auto& r : rs) {
+      F += r.feasible;
+      if (r.max_score > M) { M = r.max_score; T = r.ties; }
+      else if (r.max_score == M && M >= 0) T += r.ties;
+    }
+    if (M < 0) {
+      c->h_out[0] = PlacementDev{-1, (uint32_t)F, 0, 0, GS_PLACED_SLOWPATH};
+      *committed_out = 1;
+      return GS_OK;
+    }
+    int64_t jstar = host_tiebreak_position(c->cfg.seed, c->h_seq[0], T);
+    int owner = -1;
+    int64_t before = 0;
+    for (int r = 0; r < c->nranks; ++r) {
+      if (rs[r].max_score != M) continue;
+      if (jstar <= before + rs[r].ties) { owner = r; break; }
+      before += rs[r].ties;
+    }
+    int32_t winner = -1;
+    if (owner == c->rank) {
+      HIP_TRY(c, launch_row_select(c->d_S, len, M, jstar - before, c->n0, c->d_sel, c->st));
+    } else {
+      HIP_TRY(c, hipMemsetAsync(c->d_sel, 0xff, 4, c->st));
+    }
+    if (c->nranks > 1) {
+      int rc = exchange(c, c->d_sel, c->d_sel + 1, 4);
+      if (rc) return rc;
+      std::vector<int32_t> w(c->nranks);
+      HIP_TRY(c, hipMemcpyAsync(w.data(), c->d_sel + 1, 4 * c->nranks, hipMemcpyDeviceToHost, c->st));
+      HIP_TRY(c, hipStreamSynchronize(c->st));
+      winner = w[owner];
+    } else {
+      HIP_TRY(c, hipMemcpyAsync(&winner, c->d_sel, 4, hipMemcpyDeviceToHost, c->st));
+      HIP_TRY(c, hipStreamSynchronize(c->st));
+    }
+    if (winner < 0) return fail(c, GS_ESTATE, "exact path could not locate tie %lld", (long long)jstar);
+    a.forced_node = winner;
+    a.forced_score = M;
+    a.forced_ties = T;
+    a.forced_feasible = (int32_t)F;
+    HIP_TRY(c, hipEventRecord(c->ev[3], c->st));
+    HIP_TRY(c, launch_commit(a, c->st));
+    HIP_TRY(c, hipEventRecord(c->ev[4], c->st));
+    HIP_TRY(c, hipMemcpyAsync(c->h_committed, c->d_committed, 4, hipMemcpyDeviceToHost, c->st));
+    HIP_TRY(c, hipStreamSynchronize(c->st));
+    c->stats.commit_ms += ev_ms(c->ev[3], c->ev[4]);
+    committed = *c->h_committed;
+    if (committed < 1) return fail(c, GS_ESTATE, "forced commit made no progress");
+  }
+  if (committed < b) c->stats.cuts += 1;
+  HIP_TRY(c, hipMemcpyAsync(c->h_out, c->d_out, sizeof(PlacementDev) * committed, hipMemcpyDeviceToHost, c->st));
+  HIP_TRY(c, hipStreamSynchronize(c->st));
+  if (c->stats.slowpath_pods && committed >= 1 && a.forced_node >= 0) c->h_out[0].flags |= GS_PLACED_SLOWPATH;
+  *committed_out = committed;
+  (void)pods;
+  return GS_OK;
+}
+
+}  // namespace
+
+// ================================================================================================
+extern "C" {
+
+const char* gs_version(void) { return "libgpuscore 0.1 (gfx950, ABI 1)"; }
+
+void gs_abi_sizes(uint64_t* out, uint32_t n) {
+  const uint64_t s[] = {sizeof(gs_pod), sizeof(gs_node), sizeof(gs_node_metric), sizeof(gs_pod_metric),
+                        sizeof(gs_config), sizeof(gs_placement), sizeof(gs_stats), sizeof(gs_loadaware_args)};
+  for (uint32_t i = 0; i < n && i < sizeof(s) / sizeof(s[0]); ++i) out[i] = s[i];
+}
+
+void gs_loadaware_args_default(gs_loadaware_args* a) {
+  if (!a) return;
+  std::memset(a, 0, sizeof(*a));
+  a->filter_expired_node_metrics = 1;
+  a->has_node_metric_expiration = 1;
+  a->node_metric_expiration_seconds = 180;
+  a->resource_weights[0] = a->resource_weights[1] = 1;
+  a->resource_weights_mask = GS_USAGE_CPU | GS_USAGE_MEMORY;
+  a->usage_thresholds[0] = 65;
+  a->usage_thresholds[1] = 95;
+  a->usage_thresholds_mask = GS_USAGE_CPU | GS_USAGE_MEMORY;
+  a->estimated_scaling_factors[0] = 85;
+  a->estimated_scaling_factors[1] = 70;
+  a->estimated_scaling_factors_mask = GS_USAGE_CPU | GS_USAGE_MEMORY;
+  a->agg_usage_type = GS_AGG_NONE;
+  a->agg_score_type = GS_AGG_NONE;
+}
+
+void gs_fit_args_default(gs_fit_args* a) {
+  if (!a) return;
+  std::memset(a, 0, sizeof(*a));
+  a->resource_weights[GS_RES_CPU] = 1;
+  a->resource_weights[GS_RES_MEMORY] = 1;
+}
+
+int gs_loadaware_args_validate(const gs_loadaware_args* a, char* msg, size_t len) {
+  auto bad = [&](const char* s) {
+    if (msg && len) snprintf(msg, len, "%s", s);
+    return GS_EINVAL;
+  };
+  if (!a) return bad("nil args");
+  if (a->has_node_metric_expiration && a->node_metric_expiration_seconds <= 0)
+    return bad("nodeMetricExpiredSeconds should be a positive value");
+  for (int r = 0; r < 2; ++r) {
+    if (a->resource_weights_mask & (1u << r)) {
+      if (a->resource_weights[r] <= 0) return bad("resource Weight should be a positive value");
+      if (a->resource_weights[r] > 100) return bad("resource Weight should be less than 100");
+    }
+    if (a->usage_thresholds_mask & (1u << r)) {
+      if (a->usage_thresholds[r] < 0) return bad("resource Threshold should be a positive value");
+      if (a->usage_thresholds[r] > 100) return bad("resource Threshold should be less than 100");
+    }
+    if (a->estimated_scaling_factors_mask & (1u << r)) {
+      if (a->estimated_scaling_factors[r] <= 0) return bad("estimated resource Threshold should be a positive value");
+      if (a->estimated_scaling_factors[r] > 100) return bad("estimated  resource Threshold should be less than 100");
+    }
+    if ((a->resource_weights_mask & (1u << r)) && !(a->estimated_scaling_factors_mask & (1u << r)))
+      return bad("estimatedScalingFactors: Not found");
+  }
+  if ((a->resource_weights_mask | a->usage_thresholds_mask | a->prod_usage_thresholds_mask |
+       a->estimated_scaling_factors_mask | a->agg_usage_thresholds_mask) & GS_USAGE_OTHER)
+    return bad("resources other than cpu/memory are not supported on this path");
+  if (msg && len) msg[0] = 0;
+  return GS_OK;
+}
+
+int gs_create(const gs_config* cfg, gs_ctx** out) {
+  if (!cfg || !out) return GS_EINVAL;
+  *out = nullptr;
+  if (cfg->abi_version != GS_ABI_VERSION) return GS_EINVAL;
+  gs_ctx* c = new gs_ctx();
+  c->cfg = *cfg;
+  char msg[256];
+  if (gs_loadaware_args_validate(&cfg->loadaware, msg, sizeof msg) != GS_OK) {
+    fprintf(stderr, "gpuscore: invalid LoadAwareSchedulingArgs: %s\n", msg);
+    delete c;
+    return GS_EINVAL;
+  }
+  if (cfg->num_nodes == 0) { delete c; return GS_EINVAL; }
+  if (compute_profile(c) != GS_OK) {
+    fprintf(stderr, "gpuscore: %s\n", c->err.c_str());
+    delete c;
+    return GS_EINVAL;
+  }
+  c->B = cfg->batch_size ? (int)cfg->batch_size : MAX_BATCH;
+  if (c->B < 1 || c->B > MAX_BATCH || (cfg->cand_cap && cfg->cand_cap != (uint32_t)CAND_CAP)) {
+    fprintf(stderr, "gpuscore: batch_size must be in [1,%d] and cand_cap %d\n", MAX_BATCH, CAND_CAP);
+    delete c;
+    return GS_EUNSUPPORTED;
+  }
+  c->N = cfg->num_nodes;
+  c->npad = (c->N + 1023) & ~1023u;
+  c->nodes.resize(c->N);
+  c->row_dirty.assign(c->N, 0);
+  set_shard(c);
+  auto bail = [&](const char* what, hipError_t e) {
+    fprintf(stderr, "gpuscore: %s: %s\n", what, hipGetErrorString(e));
+    gs_destroy(c);
+    return GS_EDEVICE;
+  };
+  hipError_t e;
+  if ((e = hipSetDevice(cfg->device)) != hipSuccess) return bail("hipSetDevice", e);
+  if ((e = set_kernel_attributes()) != hipSuccess) return bail("hipFuncSetAttribute", e);
+  if ((e = hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking)) != hipSuccess) return bail("hipStreamCreate", e);
+  for (auto& ev : c->ev)
+    if ((e = hipEventCreate(&ev)) != hipSuccess) return bail("hipEventCreate", e);
+  size_t np = c->npad;
+  if ((e = hipMalloc(&c->d_i64, np * NUM_I64_COLS * 8)) != hipSuccess) return bail("hipMalloc mirror", e);
+  if ((e = hipMalloc(&c->d_i32, np * NUM_I32_COLS * 4)) != hipSuccess) return bail("hipMalloc mirror", e);
+  (void)hipMemset(c->d_i64, 0, np * NUM_I64_COLS * 8);
+  (void)hipMemset(c->d_i32, 0, np * NUM_I32_COLS * 4);
+  for (int k = 0; k < NUM_I64_COLS; ++k) c->mv.i64[k] = c->d_i64 + (size_t)k * np;
+  for (int k = 0; k < NUM_I32_COLS; ++k) c->mv.i32[k] = c->d_i32 + (size_t)k * np;
+  c->ld = c->npad;
+  if ((e = hipMalloc(&c->d_pods, sizeof(PodVec) * c->B)) != hipSuccess) return bail("hipMalloc", e);
+  if ((e = hipMalloc(&c->d_seq, 8 * c->B)) != hipSuccess) return bail("hipMalloc", e);
+  if ((e = hipMalloc(&c->d_S, (size_t)c->B * c->ld * 2)) != hipSuccess) return bail("hipMalloc S", e);
+  size_t xb = xchg_block_bytes(c->B);
+  if ((e = hipMalloc(&c->d_xchg_send, xb)) != hipSuccess) return bail("hipMalloc", e);
+  c->xchg_bytes = xb;
+  if ((e = hipMalloc(&c->d_out, sizeof(PlacementDev) * c->B)) != hipSuccess) return bail("hipMalloc", e);
+  if ((e = hipMalloc(&c->d_committed, 4)) != hipSuccess) return bail("hipMalloc", e);
+  if ((e = hipMalloc(&c->d_rowstat, sizeof(RowStat) * (1 + MAX_RANKS))) != hipSuccess) return bail("hipMalloc", e);
+  if ((e = hipMalloc(&c->d_sel, 4 * (1 + MAX_RANKS))) != hipSuccess) return bail("hipMalloc", e);
+  c->stage_cap = std::min<uint32_t>(c->N, 65536);
+  if ((e = hipMalloc(&c->d_stage_idx, 4 * c->stage_cap)) != hipSuccess) return bail("hipMalloc", e);
+  if ((e = hipMalloc(&c->d_stage_rows, (size_t)8 * ROW_WORDS * c->stage_cap)) != hipSuccess) return bail("hipMalloc", e);
+  if ((e = hipHostMalloc(&c->h_stage_idx, 4 * c->stage_cap, hipHostMallocDefault)) != hipSuccess) return bail("hipHostMalloc", e);
+  if ((e = hipHostMalloc(&c->h_stage_rows, (size_t)8 * ROW_WORDS * c->stage_cap, hipHostMallocDefault)) != hipSuccess)
+    return bail("hipHostMalloc", e);
+  if ((e = hipHostMalloc(&c->h_pods, sizeof(PodVec) * c->B, hipHostMallocDefault)) != hipSuccess) return bail("hipHostMalloc", e);
+  if ((e = hipHostMalloc(&c->h_seq, 8 * c->B, hipHostMallocDefault)) != hipSuccess) return bail("hipHostMalloc", e);
+  if ((e = hipHostMalloc(&c->h_out, sizeof(PlacementDev) * c->B, hipHostMallocDefault)) != hipSuccess) return bail("hipHostMalloc", e);
+  if ((e = hipHostMalloc(&c->h_committed, 4, hipHostMallocDefault)) != hipSuccess) return bail("hipHostMalloc", e);
+  if ((e = hipHostMalloc(&c->h_xchg_send, xb, hipHostMallocDefault)) != hipSuccess) return bail("hipHostMalloc", e);
+  (void)hipMemset(c->d_S, 0xff, (size_t)c->B * c->ld * 2);
+  if ((e = hipDeviceSynchronize()) != hipSuccess) return bail("hipDeviceSynchronize", e);
+  c->stats.node_row_bytes = 3 * 8 + 4 + 2 * 8 + 2 * 8 + 2 * 8 + 2 * 8 + 4;   // 96 B
+  *out = c;
+  return GS_OK;
+}
+
+int gs_destroy(gs_ctx* c) {
+  if (!c) return GS_EINVAL;
+  if (c->comm) ncclCommDestroy(c->comm);
+  if (c->st) (void)hipStreamSynchronize(c->st);
+  void* dev[] = {c->d_i64, c->d_i32, c->d_pods, c->d_seq, c->d_S, c->d_xchg_send, c->d_xchg_recv, c->d_out,
+                 c->d_committed, c->d_rowstat, c->d_sel, c->d_stage_idx, c->d_stage_rows};
+  for (void* p : dev)
+    if (p) (void)hipFree(p);
+  void* host[] = {c->h_pods, c->h_seq, c->h_out, c->h_committed, c->h_stage_idx, c->h_stage_rows, c->h_xchg_send,
+                  c->h_xchg_recv};
+  for (void* p : host)
+    if (p) (void)hipHostFree(p);
+  for (auto& ev : c->ev)
+    if (ev) (void)hipEventDestroy(ev);
+  if (c->st) (void)hipStreamDestroy(c->st);
+  delete c;
+  return GS_OK;
+}
+
+const char* gs_last_error(gs_ctx* c) { return c ? c->err.c_str() : "nil context"; }
+
+int gs_set_now(gs_ctx* c, int64_t now) {
+  if (!c) return GS_EINVAL;
+  if (now != c->now) c->prep_stale = true;
+  c->now = now;
+  return GS_OK;
+}
+
+int gs_nodes_upsert(gs_ctx* c, const uint32_t* idx, const gs_node* nodes, uint32_t n) {
+  if (!c || (!nodes && n)) return GS_EINVAL;
+  for (uint32_t j = 0; j < n; ++j) {
+    uint32_t i = idx ? idx[j] : j;
+    if (i >= c->N) return fail(c, GS_EINVAL, "node index %u >= %u", i, c->N);
+    int rc = validate_node(c, nodes[j]);
+    if (rc) return rc;
+    c->nodes[i].node = nodes[j];
+    c->nodes[i].valid = true;
+    mark_dirty(c, i);
+  }
+  return flush_rows(c);
+}
+
+int gs_node_metrics_upsert(gs_ctx* c, const uint32_t* idx, const gs_node_metric* m, uint32_t n,
+                           const gs_pod_metric* pm, const uint32_t* off) {
+  if (!c || (!m && n)) return GS_EINVAL;
+  for (uint32_t j = 0; j < n; ++j) {
+    uint32_t i = idx ? idx[j] : j;
+    if (i >= c->N) return fail(c, GS_EINVAL, "node index %u >= %u", i, c->N);
+    if (m[j].n_aggregated < 0 || m[j].n_aggregated > GS_MAX_AGG_USAGES)
+      return fail(c, GS_EINVAL, "n_aggregated %d outside [0,%d]", m[j].n_aggregated, GS_MAX_AGG_USAGES);
+    HostNode& hn = c->nodes[i];
+    index_metric_names(c, hn, -1);
+    hn.metric = m[j];
+    hn.pms.clear();
+    if (pm && off) hn.pms.assign(pm + off[j], pm + off[j + 1]);
+    index_metric_names(c, hn, +1);
+    mark_dirty(c, i);
+  }
+  return flush_rows(c);
+}
+
+int gs_pods_assign(gs_ctx* c, const uint32_t* node_idx, const gs_pod* pods, const int64_t* ts, uint32_t n) {
+  if (!c || (n && (!node_idx || !pods))) return GS_EINVAL;
+  for (uint32_t j = 0; j < n; ++j) {
+    uint32_t i = node_idx[j];
+    if (i >= c->N) return fail(c, GS_EINVAL, "node index %u >= %u", i, c->N);
+    if (pods[j].flags & GS_POD_TERMINATED) continue;       // pod_assign_cache.go:54
+    c->nodes[i].assigned[pods[j].uid] = Assigned{ts ? ts[j] : c->now, pods[j]};
+    c->uid_node[pods[j].uid] = i;
+    mark_dirty(c, i);
+  }
+  return flush_rows(c);
+}
+
+int gs_pods_unassign(gs_ctx* c, const uint32_t* node_idx, const gs_pod* pods, uint32_t n) {
+  if (!c || (n && (!node_idx || !pods))) return GS_EINVAL;
+  for (uint32_t j = 0; j < n; ++j) {
+    uint32_t i = node_idx[j];
+    if (i >= c->N) return fail(c, GS_EINVAL, "node index %u >= %u", i, c->N);
+    c->nodes[i].assigned.erase(pods[j].uid);
+    auto it = c->uid_node.find(pods[j].uid);
+    if (it != c->uid_node.end() && it->second == i) c->uid_node.erase(it);
+    mark_dirty(c, i);
+  }
+  return flush_rows(c);
+}
+
+int gs_evaluate(gs_ctx* c, const gs_pod* pods, uint32_t npods, int16_t* scores, uint16_t* codes,
+                int16_t* plugin_scores) {
+  if (!c || (npods && !pods)) return GS_EINVAL;
+  int rc = ready(c);
+  if (rc) return rc;
+  if ((rc = flush_rows(c))) return rc;
+  if ((rc = node_prep(c))) return rc;
+  const uint32_t N = c->N;
+  const int chunk = c->B;
+  int16_t *d_sc = nullptr, *d_pl = nullptr;
+  uint16_t* d_cd = nullptr;
+  HIP_TRY(c, hipMalloc(&d_sc, (size_t)chunk * N * 2));
+  HIP_TRY(c, hipMalloc(&d_cd, (size_t)chunk * N * 2));
+  HIP_TRY(c, hipMalloc(&d_pl, (size_t)chunk * N * 4));
+  for (uint32_t p0 = 0; p0 < npods; p0 += chunk) {
+    int b = (int)std::min<uint32_t>(chunk, npods - p0);
+    int prod_cols = 0;
+    for (int i = 0; i < b; ++i) {
+      if ((rc = validate_pod(c, pods[p0 + i]))) break;
+      c->h_pods[i] = prep_pod(c, pods[p0 + i]);
+      prod_cols |= (c->h_pods[i].flags & PF_PROD_SCORE) ? 1 : 0;
+    }
+    if (rc) break;
+    HIP_TRY(c, hipMemcpyAsync(c->d_pods, c->h_pods, sizeof(PodVec) * b, hipMemcpyHostToDevice, c->st));
+    HIP_TRY(c, launch_eval_full(c->mv, c->d_pods, b, c->pf, N, d_sc, d_cd, d_pl, prod_cols, c->st));
+    if (scores) HIP_TRY(c, hipMemcpyAsync(scores + (size_t)p0 * N, d_sc, (size_t)b * N * 2, hipMemcpyDeviceToHost, c->st));
+    if (codes) HIP_TRY(c, hipMemcpyAsync(codes + (size_t)p0 * N, d_cd, (size_t)b * N * 2, hipMemcpyDeviceToHost, c->st));
+    if (plugin_scores)
+      HIP_TRY(c, hipMemcpyAsync(plugin_scores + (size_t)p0 * N * 2, d_pl, (size_t)b * N * 4, hipMemcpyDeviceToHost, c->st));
+    HIP_TRY(c, hipStreamSynchronize(c->st));
+  }
+  (void)hipFree(d_sc);
+  (void)hipFree(d_cd);
+  (void)hipFree(d_pl);
+  return rc;
+}
+
+int gs_schedule(gs_ctx* c, const gs_pod* pods, uint32_t npods, const uint64_t* seq, gs_placement* out) {
+  if (!c || (npods && (!pods || !out))) return GS_EINVAL;
+  int rc = ready(c);
+  if (rc) return rc;
+  for (uint32_t i = 0; i < npods; ++i)
+    if ((rc = validate_pod(c, pods[i]))) return rc;
+  uint32_t i = 0;
+  while (i < npods) {
+    if ((rc = flush_rows(c))) return rc;
+    if (c->prep_stale && (rc = node_prep(c))) return rc;
+    // batch [i, i+b): a special pod always runs alone (its row is re-derived on the host afterwards)
+    int b = (int)std::min<uint32_t>(c->B, npods - i);
+    bool special_first = special_pod(c, pods[i]);
+    if (special_first) {
+      b = 1;
+    } else {
+      for (int j = 1; j < b; ++j)
+        if (special_pod(c, pods[i + j])) { b = j; break; }
+    }
+    for (int j = 0; j < b; ++j) {
+      c->h_pods[j] = prep_pod(c, pods[i + j]);
+      c->h_seq[j] = seq ? seq[i + j] : (uint64_t)(i + j);
+    }
+    HIP_TRY(c, hipMemcpyAsync(c->d_pods, c->h_pods, sizeof(PodVec) * b, hipMemcpyHostToDevice, c->st));
+    HIP_TRY(c, hipMemcpyAsync(c->d_seq, c->h_seq, 8 * b, hipMemcpyHostToDevice, c->st));
+    int committed = 0;
+    if ((rc = run_batch(c, pods + i, b, &committed))) return rc;
+    for (int j = 0; j < committed; ++j) {
+      const PlacementDev& pd = c->h_out[j];
+      gs_placement& o = out[i + j];
+      o.node = pd.node;
+      o.feasible = pd.feasible;
+      o.score = pd.node >= 0 ? pd.score : 0;
+      o.ties = pd.node >= 0 ? pd.ties : 0;
+      o.flags = pd.flags;
+      apply_placement(c, pods[i + j], pd.node, special_first);
+    }
+    c->stats.pods += committed;
+    i += committed;
+  }
+  return flush_rows(c);
+}
+
+int gs_comm_unique_id(uint8_t out[128]) {
+  if (!out) return GS_EINVAL;
+  ncclUniqueId id;
+  if (ncclGetUniqueId(&id) != ncclSuccess) return GS_ECOMM;
+  static_assert(sizeof(ncclUniqueId) == 128, "ncclUniqueId size");
+  std::memcpy(out, &id, 128);
+  return GS_OK;
+}
+
+int gs_comm_init_rccl(gs_ctx* c, const uint8_t id[128], int nranks, int rank) {
+  if (!c || !id || nranks < 1 || nranks > MAX_RANKS || rank < 0 || rank >= nranks) return GS_EINVAL;
+  if (nranks > 1) {
+    ncclUniqueId uid;
+    std::memcpy(&uid, id, 128);
+    HIP_TRY(c, hipSetDevice(c->cfg.device));
+    ncclResult_t r = ncclCommInitRank(&c->comm, nranks, uid, rank);
+    if (r != ncclSuccess) return fail(c, GS_ECOMM, "ncclCommInitRank: %s", ncclGetErrorString(r));
+  }
+  c->nranks = nranks;
+  c->rank = rank;
+  set_shard(c);
+  return alloc_exchange(c);
+}
+
+int gs_comm_init_callback(gs_ctx* c, int nranks, int rank, gs_allgather_fn fn, void* user) {
+  if (!c || !fn || nranks < 1 || nranks > MAX_RANKS || rank < 0 || rank >= nranks) return GS_EINVAL;
+  c->cb = fn;
+  c->cb_user = user;
+  c->nranks = nranks;
+  c->rank = rank;
+  set_shard(c);
+  return alloc_exchange(c);
+}
+
+int gs_get_stats(gs_ctx* c, gs_stats* out) {
+  if (!c || !out) return GS_EINVAL;
+  *out = c->stats;
+  return GS_OK;
+}
+
+int gs_reset_stats(gs_ctx* c) {
+  if (!c) return GS_EINVAL;
+  uint64_t rb = c->stats.node_row_bytes;
+  c->stats = gs_stats{};
+  c->stats.node_row_bytes = rb;
+  c->stats.shard_begin = c->n0;
+  c->stats.shard_end = c->n1;
+  return GS_OK;
+}
+
+int gs_synchronize(gs_ctx* c) {
+  if (!c) return GS_EINVAL;
+  HIP_TRY(c, hipStreamSynchronize(c->st));
+  return GS_OK;
+}
+
+// Compares every HBM mirror row against a fresh host derivation; returns the number of mismatching rows.
+int gs_debug_mirror_check(gs_ctx* c) {
+  if (!c) return GS_EINVAL;
+  int rc = flush_rows(c);
+  if (rc) return rc;
+  std::vector<int64_t> d64((size_t)c->npad * NUM_I64_COLS);
+  std::vector<int32_t> d32((size_t)c->npad * NUM_I32_COLS);
+  HIP_TRY(c, hipStreamSynchronize(c->st));
+  HIP_TRY(c, hipMemcpy(d64.data(), c->d_i64, d64.size() * 8, hipMemcpyDeviceToHost));
+  HIP_TRY(c, hipMemcpy(d32.data(), c->d_i32, d32.size() * 4, hipMemcpyDeviceToHost));
+  int bad = 0;
+  std::vector<int64_t> row(ROW_WORDS);
+  for (uint32_t i = 0; i < c->N; ++i) {
+    derive_row(c, c->nodes[i], row.data());
+    bool ok = true;
+    for (int k = 0; k < NUM_I64_COLS; ++k) ok &= d64[(size_t)k * c->npad + i] == row[k];
+    ok &= d32[(size_t)C_FREE_PODS * c->npad + i] == (int32_t)row[NUM_I64_COLS + C_FREE_PODS];
+    ok &= d32[(size_t)C_SFLAGS * c->npad + i] == (int32_t)row[NUM_I64_COLS + C_SFLAGS];
+    if (!ok) {
+      if (bad < 4) fprintf(stderr, "gpuscore: mirror row %u differs from its host derivation\n", i);
+      ++bad;
+    }
+  }
+  return bad;
+}
+
+}  // extern "C"

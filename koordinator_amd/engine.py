@@ -1,0 +1,157 @@
+"""Python host mirror of the plugin interface over libgpuscore's C-ABI.
+
+`Engine` is one scheduler profile (NodeResourcesFit + LoadAwareScheduling) on one GPU. Its methods map
+1:1 onto the C-ABI, which in turn replaces the reference plugin entry points:
+
+  Engine(cfg)            loadaware.New / noderesources.NewFit        (load_aware.go:76-110)
+  set_now                time.Now injection                           (helper.go:36-41, pod_assign_cache.go:30)
+  upsert_nodes           scheduler cache snapshot (NodeInfo)          ([upstream] Cache.UpdateSnapshot)
+  upsert_metrics         NodeMetric informer                          (load_aware.go:95,133,278)
+  assign / unassign      podAssignCache.assign / unAssign             (pod_assign_cache.go:53-80)
+  evaluate               RunFilterPlugins + RunScorePlugins per node  (load_aware.go:123-171,269-335)
+  schedule               scheduleOne loop incl. selectHost + Reserve  ([upstream] schedule_one.go)
+
+The product path has no CPU fallback: if libgpuscore or a GPU is missing, construction fails.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from . import abi
+
+_lib = None
+
+
+def lib() -> C.CDLL:
+    global _lib
+    if _lib is None:
+        _lib = abi.load()
+    return _lib
+
+
+class GpuScoreError(RuntimeError):
+    pass
+
+
+class Engine:
+    def __init__(self, cfg: abi.GsConfig):
+        self.cfg = cfg
+        self.n = cfg.num_nodes
+        h = C.c_void_p()
+        rc = lib().gs_create(C.byref(cfg), C.byref(h))
+        if rc != 0:
+            raise GpuScoreError(f"gs_create failed: {rc}")
+        self._h = h
+        self._cb = None
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().gs_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _chk(self, rc: int, what: str):
+        if rc != 0:
+            msg = lib().gs_last_error(self._h)
+            raise GpuScoreError(f"{what}: rc={rc}: {msg.decode() if msg else ''}")
+
+    def set_now(self, now_ns: int):
+        self._chk(lib().gs_set_now(self._h, int(now_ns)), "gs_set_now")
+
+    def upsert_nodes(self, nodes, idx=None):
+        nodes = np.ascontiguousarray(nodes, dtype=abi.NODE_DTYPE)
+        if idx is not None:
+            idx = np.ascontiguousarray(idx, dtype=np.uint32)
+        self._chk(lib().gs_nodes_upsert(self._h, abi.ptr(idx), abi.ptr(nodes), len(nodes)), "gs_nodes_upsert")
+
+    def upsert_metrics(self, metrics, pod_metrics=None, offsets=None, idx=None):
+        metrics = np.ascontiguousarray(metrics, dtype=abi.METRIC_DTYPE)
+        if idx is not None:
+            idx = np.ascontiguousarray(idx, dtype=np.uint32)
+        if pod_metrics is not None:
+            pod_metrics = np.ascontiguousarray(pod_metrics, dtype=abi.POD_METRIC_DTYPE)
+            offsets = np.ascontiguousarray(offsets, dtype=np.uint32)
+        self._chk(lib().gs_node_metrics_upsert(self._h, abi.ptr(idx), abi.ptr(metrics), len(metrics),
+                                               abi.ptr(pod_metrics), abi.ptr(offsets)), "gs_node_metrics_upsert")
+
+    def assign(self, node_idx, pods, ts):
+        node_idx = np.ascontiguousarray(node_idx, dtype=np.uint32)
+        pods = np.ascontiguousarray(pods, dtype=abi.POD_DTYPE)
+        ts = np.ascontiguousarray(ts, dtype=np.int64)
+        self._chk(lib().gs_pods_assign(self._h, abi.ptr(node_idx), abi.ptr(pods), abi.ptr(ts), len(pods)),
+                  "gs_pods_assign")
+
+    def unassign(self, node_idx, pods):
+        node_idx = np.ascontiguousarray(node_idx, dtype=np.uint32)
+        pods = np.ascontiguousarray(pods, dtype=abi.POD_DTYPE)
+        self._chk(lib().gs_pods_unassign(self._h, abi.ptr(node_idx), abi.ptr(pods), len(pods)), "gs_pods_unassign")
+
+    def evaluate(self, pods):
+        pods = np.ascontiguousarray(pods, dtype=abi.POD_DTYPE)
+        P, N = len(pods), self.n
+        scores = np.empty((P, N), np.int16)
+        codes = np.empty((P, N), np.uint16)
+        plugin = np.empty((P, N, abi.GS_NUM_PLUGINS), np.int16)
+        self._chk(lib().gs_evaluate(self._h, abi.ptr(pods), P, abi.ptr(scores), abi.ptr(codes), abi.ptr(plugin)),
+                  "gs_evaluate")
+        return scores, codes, plugin
+
+    def schedule(self, pods, seq=None):
+        pods = np.ascontiguousarray(pods, dtype=abi.POD_DTYPE)
+        if seq is None:
+            seq = np.arange(len(pods), dtype=np.uint64)
+        seq = np.ascontiguousarray(seq, dtype=np.uint64)
+        out = np.zeros(len(pods), abi.PLACEMENT_DTYPE)
+        self._chk(lib().gs_schedule(self._h, abi.ptr(pods), len(pods), abi.ptr(seq), abi.ptr(out)), "gs_schedule")
+        return out
+
+    # ---- multi-GPU
+    def comm_init_rccl(self, uid: bytes, nranks: int, rank: int):
+        buf = (C.c_uint8 * 128).from_buffer_copy(uid)
+        self._chk(lib().gs_comm_init_rccl(self._h, buf, nranks, rank), "gs_comm_init_rccl")
+
+    def comm_init_callback(self, nranks: int, rank: int, allgather):
+        """allgather(send: bytes) -> list[bytes] of every rank's payload (rank order)."""
+        def _cb(user, send, recv, nbytes):
+            try:
+                data = C.string_at(send, nbytes)
+                parts = allgather(data)
+                blob = b"".join(parts)
+                C.memmove(recv, blob, len(blob))
+                return 0
+            except Exception:
+                return -1
+        self._cb = abi.ALLGATHER_FN(_cb)
+        self._chk(lib().gs_comm_init_callback(self._h, nranks, rank, self._cb, None), "gs_comm_init_callback")
+
+    def stats(self) -> dict:
+        s = abi.GsStats()
+        self._chk(lib().gs_get_stats(self._h, C.byref(s)), "gs_get_stats")
+        return {k: getattr(s, k) for k, _ in abi.GsStats._fields_}
+
+    def reset_stats(self):
+        self._chk(lib().gs_reset_stats(self._h), "gs_reset_stats")
+
+    def synchronize(self):
+        self._chk(lib().gs_synchronize(self._h), "gs_synchronize")
+
+    def mirror_check(self) -> int:
+        rc = lib().gs_debug_mirror_check(self._h)
+        if rc < 0:
+            self._chk(rc, "gs_debug_mirror_check")
+        return rc
+
+
+def unique_id() -> bytes:
+    buf = (C.c_uint8 * 128)()
+    rc = lib().gs_comm_unique_id(buf)
+    if rc != 0:
+        raise GpuScoreError(f"gs_comm_unique_id failed: {rc}")
+    return bytes(buf)

@@ -1,0 +1,210 @@
+"""Deterministic synthetic clusters for the BASELINE.json configurations.
+
+Counter-based splitmix64 streams (seed 0x6b6f6f7264 + config id): every value is a pure function of
+(seed, stream, index), so every rank of a multi-GPU run builds the identical cluster without
+communication, and the CPU oracle sees exactly the bytes the GPU sees. All quantities are integral
+milli-CPU / bytes, so resource.Quantity rounding is inert.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import numpy as np
+
+from . import abi
+
+BASE_SEED = 0x6B6F6F7264
+NOW_NS = 1_700_000_000 * 10**9
+GiB = 1 << 30
+MiB = 1 << 20
+SEC = 10**9
+
+CONFIGS = {
+    # id: (nodes, pods, description)  — BASELINE.json "configs"
+    0: (1_000, 1_000, "C1: 1k nodes x 1k pods, LoadAware + NodeResourcesFit LeastAllocated (CPU bench analogue)"),
+    1: (5_000, 10_000, "C2: 5k nodes x 10k pods, synthetic NodeMetric usage, batched pod queue, 1 GPU"),
+    2: (50_000, 50_000, "C3: 50k nodes x 50k pods, 1 GPU"),
+    3: (100_000, 50_000, "C4: 100k nodes node-sharded across GPUs"),
+}
+
+_M1, _M2, _GOLD = np.uint64(0xBF58476D1CE4E5B9), np.uint64(0x94D049BB133111EB), np.uint64(0x9E3779B97F4A7C15)
+
+
+def mix64(x: np.ndarray) -> np.ndarray:
+    with np.errstate(over="ignore"):
+        z = x + _GOLD
+        z = (z ^ (z >> np.uint64(30))) * _M1
+        z = (z ^ (z >> np.uint64(27))) * _M2
+        return z ^ (z >> np.uint64(31))
+
+
+class Stream:
+    def __init__(self, seed: int):
+        self.seed = np.uint64(seed & 0xFFFFFFFFFFFFFFFF)
+
+    def u64(self, stream: int, n: int) -> np.ndarray:
+        key = mix64(np.array([self.seed ^ np.uint64(stream)], np.uint64))[0]
+        with np.errstate(over="ignore"):
+            return mix64(np.arange(n, dtype=np.uint64) + key * np.uint64(0x100000001B3))
+
+    def randint(self, stream: int, n: int, lo, hi) -> np.ndarray:
+        """Uniform integers in [lo, hi] (inclusive; lo/hi scalars or arrays)."""
+        lo = np.asarray(lo, np.int64)
+        hi = np.asarray(hi, np.int64)
+        span = (hi - lo + 1).astype(np.uint64)
+        return lo + (self.u64(stream, n) % span).astype(np.int64)
+
+    def uniform(self, stream: int, n: int) -> np.ndarray:
+        return (self.u64(stream, n) >> np.uint64(11)).astype(np.float64) * (1.0 / (1 << 53))
+
+
+@dataclass
+class Cluster:
+    now_ns: int
+    nodes: np.ndarray        # NODE_DTYPE[N]
+    metrics: np.ndarray      # METRIC_DTYPE[N]
+    pod_metrics: np.ndarray  # POD_METRIC_DTYPE[M]
+    pm_offsets: np.ndarray   # uint32[N+1]
+    assigned_node: np.ndarray
+    assigned_pods: np.ndarray
+    assigned_ts: np.ndarray
+    pods: np.ndarray         # POD_DTYPE[P] pending, in scheduling order
+
+    @property
+    def num_nodes(self) -> int:
+        return len(self.nodes)
+
+
+def make_pods(s: Stream, n: int, base_stream: int, name_base: int) -> np.ndarray:
+    pods = np.zeros(n, abi.POD_DTYPE)
+    kind = s.randint(base_stream + 0, n, 0, 99)           # 70% limit=req, 20% limit=2req, 10% no requests
+    no_req = kind >= 90
+    cpu = s.randint(base_stream + 1, n, 1, 80) * 100       # [100m, 8] step 100m
+    mem = s.randint(base_stream + 2, n, 128, 16 * 1024) * MiB
+    cpu = np.where(no_req, 0, cpu)
+    mem = np.where(no_req, 0, mem)
+    lim_mul = np.where(kind < 70, 1, np.where(kind < 90, 2, 0))
+    prio_prod = s.randint(base_stream + 3, n, 0, 99) < 40   # 40% Prod priority (9000-9999), 60% none
+    req = np.zeros((n, abi.GS_NUM_RES), np.int64)
+    lim = np.zeros((n, abi.GS_NUM_RES), np.int64)
+    req[:, 0], req[:, 1] = cpu, mem
+    lim[:, 0], lim[:, 1] = cpu * lim_mul, mem * lim_mul
+    pods["requests"] = req
+    pods["limits"] = lim
+    nz = np.zeros((n, 2), np.int64)
+    nz[:, 0] = np.where(no_req, 100, cpu)                   # schedutil DefaultMilliCPURequest
+    nz[:, 1] = np.where(no_req, 200 * MiB, mem)             # schedutil DefaultMemoryRequest
+    pods["nonzero_requests"] = nz
+    pods["request_mask"] = np.where(no_req, 0, (1 << abi.GS_RES_CPU) | (1 << abi.GS_RES_MEMORY)).astype(np.uint32)
+    # GetPodPriorityClassWithDefault: priority 9000-9999 -> Prod; otherwise the QoS default
+    # (Guaranteed -> LSR, Burstable -> LS: Prod; BestEffort -> BE: Batch).
+    pods["priority_class"] = np.where(prio_prod | ~no_req, abi.GS_PRIO_PROD, abi.GS_PRIO_BATCH)
+    pods["uid"] = s.u64(base_stream + 4, n)
+    pods["name_key"] = mix64(np.arange(name_base, name_base + n, dtype=np.uint64))
+    return pods
+
+
+def make_cluster(num_nodes: int, num_pods: int, config_id: int = 1, seed: int | None = None) -> Cluster:
+    s = Stream((BASE_SEED + config_id) if seed is None else seed)
+    N = num_nodes
+    now = NOW_NS
+    cores = np.array([32, 48, 64, 96, 128], np.int64)[s.randint(1, N, 0, 4)]
+    mem_g = np.array([128, 256, 384, 512, 1024], np.int64)[s.randint(2, N, 0, 4)]
+    nodes = np.zeros(N, abi.NODE_DTYPE)
+    alloc = np.zeros((N, abi.GS_NUM_RES), np.int64)
+    alloc[:, 0] = cores * 1000
+    alloc[:, 1] = mem_g * GiB
+    alloc[:, 2] = 500 * GiB
+    nodes["allocatable"] = alloc
+    reqd = np.zeros((N, abi.GS_NUM_RES), np.int64)
+    reqd[:, 0] = s.randint(3, N, 0, alloc[:, 0] // 100 * 70 // 100) * 100     # U[0,70%] in 100m steps
+    reqd[:, 1] = s.randint(4, N, 0, alloc[:, 1] // MiB * 70 // 100) * MiB      # U[0,70%] in 1MiB steps
+    reqd[:, 2] = s.randint(5, N, 0, 50) * GiB
+    nodes["requested"] = reqd
+    pod_count = s.randint(6, N, 0, 60)
+    zero_req = s.randint(7, N, 0, pod_count // 10)                           # ~5% zero-request pods
+    nz = np.zeros((N, 2), np.int64)
+    nz[:, 0] = reqd[:, 0] + zero_req * 100
+    nz[:, 1] = reqd[:, 1] + zero_req * 200 * MiB
+    nodes["nonzero_requested"] = nz
+    nodes["allowed_pod_number"] = 110
+    nodes["pod_count"] = pod_count
+    # 5% of nodes carry node.koordinator.sh/raw-allocatable (EstimateNode override)
+    raw = s.randint(8, N, 0, 99) < 5
+    rawv = np.zeros((N, 2), np.int64)
+    rawv[:, 0] = np.where(raw, alloc[:, 0] * 9 // 10 // 1000 * 1000, 0)
+    rawv[:, 1] = np.where(raw, alloc[:, 1] * 9 // 10, 0)
+    nodes["raw_allocatable"] = rawv
+    nodes["raw_allocatable_mask"] = np.where(raw, abi.GS_USAGE_CPU | abi.GS_USAGE_MEMORY, 0).astype(np.uint32)
+    # 3% custom usage thresholds, 1% custom prod thresholds (scheduling.koordinator.sh/usage-thresholds)
+    cu = s.randint(9, N, 0, 99)
+    custom = cu < 4
+    nodes["custom_flags"] = np.where(custom, abi.GS_NODE_CUSTOM_THRESHOLDS, 0).astype(np.uint32)
+    ut = np.zeros((N, 2), np.int64)
+    ut[:, 0], ut[:, 1] = 70, 90
+    nodes["custom_usage_thresholds"] = ut
+    nodes["custom_usage_mask"] = np.where(cu < 3, abi.GS_USAGE_CPU | abi.GS_USAGE_MEMORY, 0).astype(np.uint32)
+    pt = np.zeros((N, 2), np.int64)
+    pt[:, 0] = 60
+    nodes["custom_prod_usage_thresholds"] = pt
+    nodes["custom_prod_usage_mask"] = np.where(cu == 3, abi.GS_USAGE_CPU, 0).astype(np.uint32)
+    nodes["custom_agg_type"] = abi.GS_AGG_NONE
+
+    # NodeMetric: 2% missing, 1% expired (now - 300s), else now - U[0,120]s (+ ns jitter)
+    metrics = np.zeros(N, abi.METRIC_DTYPE)
+    mk = s.randint(10, N, 0, 99)
+    exists = mk >= 2
+    expired = mk == 2
+    upd = now - s.randint(11, N, 0, 120) * SEC - s.randint(12, N, 1, 999_999)
+    upd = np.where(expired, now - 300 * SEC, upd)
+    metrics["exists"] = exists
+    metrics["has_update_time"] = exists
+    metrics["update_time_ns"] = np.where(exists, upd, 0)
+    metrics["has_report_interval"] = exists
+    metrics["report_interval_s"] = 60
+    metrics["has_node_metric"] = exists
+    metrics["node_usage"]["cpu_milli"] = s.randint(13, N, 0, alloc[:, 0] * 80 // 100)
+    metrics["node_usage"]["memory"] = s.randint(14, N, 0, alloc[:, 1] * 95 // 100)
+    metrics["node_usage"]["mask"] = np.where(exists, abi.GS_USAGE_CPU | abi.GS_USAGE_MEMORY, 0)
+
+    # podAssignCache: 0-3 pods per node, timestamps straddling updateTime (>= 1s from every boundary)
+    na = s.randint(15, N, 0, 3)
+    A = int(na.sum())
+    a_node = np.repeat(np.arange(N, dtype=np.uint32), na)
+    a_pods = make_pods(s, A, 100, 10_000_000)
+    a_pods["uid"] = s.u64(120, A)
+    off_kind = s.randint(16, A, 0, 2)
+    off = np.where(off_kind == 0, -s.randint(17, A, 61, 300),         # old: metric may cover it
+                   np.where(off_kind == 1, -s.randint(18, A, 1, 59),   # within the report interval
+                            s.randint(19, A, 1, 30)))                  # after the last update
+    base = np.where(exists[a_node], upd[a_node], now - 100 * SEC)
+    a_ts = base + off * SEC + s.randint(20, A, 0, 999) * 1000
+    a_ts = np.minimum(a_ts, now)
+    # PodsMetric: 70% of assigned pods on nodes with metrics report usage (in the pod lister)
+    has_pm = (s.randint(21, A, 0, 99) < 70) & exists[a_node]
+    pm_node = a_node[has_pm]
+    pm = np.zeros(int(has_pm.sum()), abi.POD_METRIC_DTYPE)
+    pm["name_key"] = a_pods["name_key"][has_pm]
+    pm["in_lister"] = 1
+    pm["priority_class"] = a_pods["priority_class"][has_pm]
+    rq = a_pods["requests"][has_pm]
+    pm["usage"]["cpu_milli"] = s.randint(22, len(pm), 0, np.maximum(rq[:, 0], 100))
+    pm["usage"]["memory"] = s.randint(23, len(pm), 0, np.maximum(rq[:, 1], 128 * MiB))
+    pm["usage"]["mask"] = abi.GS_USAGE_CPU | abi.GS_USAGE_MEMORY
+    order = np.argsort(pm_node, kind="stable")
+    pm = pm[order]
+    counts = np.bincount(pm_node, minlength=N)
+    offsets = np.zeros(N + 1, np.uint32)
+    offsets[1:] = np.cumsum(counts)
+
+    pods = make_pods(s, num_pods, 200, 20_000_000)
+    return Cluster(now, nodes, metrics, pm, offsets, a_node, a_pods, a_ts.astype(np.int64), pods)
+
+
+def load_into(engine, c: Cluster) -> None:
+    """Push a cluster into an Engine / Oracle (same calls a scheduler's informers would make)."""
+    engine.set_now(c.now_ns)
+    engine.upsert_nodes(c.nodes)
+    engine.upsert_metrics(c.metrics, c.pod_metrics, c.pm_offsets)
+    if len(c.assigned_pods):
+        engine.assign(c.assigned_node, c.assigned_pods, c.assigned_ts)

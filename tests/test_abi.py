@@ -1,0 +1,92 @@
+"""C-ABI boundary checks that need no GPU: exports, struct layout, args defaulting/validation,
+and that the product path refuses to run (loudly) without a device."""
+import ctypes as C
+import os
+
+import numpy as np
+import pytest
+
+from koordinator_amd import abi, build, config, objects
+
+torch_cuda = None
+try:
+    import torch
+    torch_cuda = torch.cuda.is_available()
+except Exception:
+    torch_cuda = False
+
+
+@pytest.fixture(scope="module")
+def lib():
+    build.build()
+    return abi.load()
+
+
+def test_exports_every_header_symbol(lib):
+    syms = abi.header_symbols()
+    assert len(syms) >= 20
+    for s in syms:
+        assert hasattr(lib, s), f"{s} declared in include/gpuscore.h but not exported"
+    assert set(syms) == set(abi.SIGNATURES), "abi.SIGNATURES out of sync with the header"
+
+
+def test_struct_sizes_match_library(lib):
+    arr = (C.c_uint64 * 8)()
+    lib.gs_abi_sizes(arr, 8)
+    names = ["gs_pod", "gs_node", "gs_node_metric", "gs_pod_metric", "gs_config", "gs_placement", "gs_stats",
+             "gs_loadaware_args"]
+    for name, size in zip(names, arr):
+        assert abi.STRUCT_SIZES[name] == size, name
+
+
+def test_loadaware_defaults_match_v1beta2(lib):
+    a = abi.GsLoadAwareArgs()
+    lib.gs_loadaware_args_default(C.byref(a))
+    b = config.loadaware_args()
+    assert bytes(a) == bytes(b)
+    assert a.node_metric_expiration_seconds == 180 and a.filter_expired_node_metrics == 1
+    assert list(a.usage_thresholds) == [65, 95] and list(a.estimated_scaling_factors) == [85, 70]
+
+
+@pytest.mark.parametrize("kw,msg", [
+    ({"nodeMetricExpirationSeconds": -1}, b"nodeMetricExpiredSeconds should be a positive value"),
+    ({"resourceWeights": {"cpu": 0}}, b"resource Weight should be a positive value"),
+    ({"resourceWeights": {"cpu": 101}}, b"resource Weight should be less than 100"),
+    ({"usageThresholds": {"cpu": 101}}, b"resource Threshold should be less than 100"),
+    ({"estimatedScalingFactors": {"cpu": 0}}, b"estimated resource Threshold should be a positive value"),
+])
+def test_loadaware_validation(lib, kw, msg):
+    a = config.loadaware_args(**kw)
+    buf = C.create_string_buffer(256)
+    assert lib.gs_loadaware_args_validate(C.byref(a), buf, 256) == abi.GS_EINVAL
+    assert buf.value == msg
+
+
+def test_validation_accepts_defaults(lib):
+    a = config.loadaware_args()
+    assert lib.gs_loadaware_args_validate(C.byref(a), None, 0) == 0
+
+
+def test_unsupported_resource_rejected():
+    with pytest.raises(ValueError):
+        config.loadaware_args(resourceWeights={"nvidia.com/gpu": 1})
+
+
+@pytest.mark.skipif(bool(torch_cuda), reason="GPU present: the no-GPU failure path is not reachable")
+def test_no_gpu_fails_loudly():
+    from koordinator_amd import engine
+    cfg = config.make_config(16)
+    with pytest.raises(engine.GpuScoreError):
+        engine.Engine(cfg)
+
+
+def test_pod_decoding_quantities():
+    p = objects.make_pod({"containers": [{"requests": {"cpu": "1500m", "memory": "1Gi"},
+                                          "limits": {"cpu": "2", "memory": "1Gi"}}]})
+    assert list(p["requests"][:2]) == [1500, 1 << 30]
+    assert list(p["limits"][:2]) == [2000, 1 << 30]
+    assert list(p["nonzero_requests"]) == [1500, 1 << 30]
+    assert p["priority_class"] == abi.GS_PRIO_PROD     # Burstable -> LS -> Prod
+    be = objects.make_pod({"containers": [{}]})
+    assert be["priority_class"] == abi.GS_PRIO_BATCH   # BestEffort -> BE -> Batch
+    assert list(be["nonzero_requests"]) == [100, 200 << 20]

@@ -1,0 +1,198 @@
+"""Parity of the HIP path (through the C-ABI) with the CPU oracle. Needs an MI355X: -m gpu.
+
+Bit-exact is the bar everywhere: feasibility codes, per-plugin int64 scores, weighted totals, and the
+selected node / max score / tie count of every sequentially scheduled pod.
+"""
+import threading
+
+import numpy as np
+import pytest
+
+from koordinator_amd import abi, config, objects, synth
+from oracle import oracle as orc
+from tests import golden_util as gu
+
+pytestmark = pytest.mark.gpu
+
+
+def engine_cls():
+    from koordinator_amd.engine import Engine
+    return Engine
+
+
+def pair(cluster, **cfg_kw):
+    cfg = config.make_config(cluster.num_nodes, **cfg_kw)
+    e = engine_cls()(cfg)
+    o = orc.Oracle(cfg)
+    synth.load_into(e, cluster)
+    synth.load_into(o, cluster)
+    return e, o
+
+
+G = gu.load()
+
+
+@pytest.mark.parametrize("case", G["filter_expired"] + G["filter_usage"], ids=lambda c: c["name"])
+def test_golden_loadaware_filter(case):
+    eng, pod = gu.build(case, engine_cls())
+    _, codes, _ = eng.evaluate(np.array([pod], abi.POD_DTYPE))
+    assert bool(codes[0, 0] & abi.GS_FAIL_LOADAWARE) == case["want_fail"], case["src"]
+
+
+@pytest.mark.parametrize("case", G["score"], ids=lambda c: c["name"])
+def test_golden_loadaware_score(case):
+    eng, pod = gu.build(case, engine_cls())
+    _, _, plugin = eng.evaluate(np.array([pod], abi.POD_DTYPE))
+    assert plugin[0, 0, abi.GS_PLUGIN_LOADAWARE] == case["want"], case["src"]
+
+
+@pytest.mark.parametrize("cid,nodes,pods", [(0, 1000, 300), (1, 5000, 64)])
+def test_evaluate_matches_oracle(cid, nodes, pods):
+    c = synth.make_cluster(nodes, pods, cid)
+    e, o = pair(c)
+    gs, gc, gp = e.evaluate(c.pods)
+    os_, oc, op = o.evaluate(c.pods)
+    assert np.array_equal(gc, oc), "filter codes differ"
+    assert np.array_equal(gp, op), "per-plugin scores differ"
+    assert np.array_equal(gs, os_), "weighted totals differ"
+    # the synthetic cluster exercises every verdict
+    assert (gc == 0).any() and (gc & abi.GS_FAIL_LOADAWARE).any() and (gc & abi.GS_FAIL_FIT_CPU).any()
+
+
+def _check_schedule(e, o, pods, seq=None):
+    got = e.schedule(pods, seq)
+    want = o.schedule(pods, seq)
+    for f in ("node", "score", "ties", "feasible"):
+        bad = np.nonzero(got[f] != want[f])[0]
+        assert len(bad) == 0, f"{f} differs first at pod {bad[0]}: gpu {got[bad[0]]} oracle {want[bad[0]]}"
+    assert e.mirror_check() == 0
+    return got
+
+
+@pytest.mark.parametrize("batch", [1, 7, 128])
+def test_schedule_c1_matches_oracle(batch):
+    c = synth.make_cluster(1000, 1000, 0)
+    e, o = pair(c, batch_size=batch)
+    got = _check_schedule(e, o, c.pods)
+    assert (got["node"] >= 0).all()
+
+
+def test_schedule_c2_slice_matches_oracle():
+    c = synth.make_cluster(5000, 1500, 1)
+    e, o = pair(c)
+    _check_schedule(e, o, c.pods)
+    st = e.stats()
+    assert st["pods"] == 1500 and st["batches"] >= 12
+
+
+def test_schedule_in_chunks_and_custom_seq():
+    c = synth.make_cluster(2000, 600, 7)
+    e, o = pair(c)
+    seq = np.arange(10_000, 10_600, dtype=np.uint64)
+    for lo in range(0, 600, 150):
+        _check_schedule(e, o, c.pods[lo:lo + 150], seq[lo:lo + 150])
+
+
+def test_homogeneous_cluster_massive_ties():
+    """Identical empty nodes: every node ties, candidate lists overflow -> exact full-row path."""
+    c = synth.make_cluster(3000, 200, 3)
+    c.nodes["requested"] = 0
+    c.nodes["nonzero_requested"] = 0
+    c.nodes["allocatable"][:, 0] = 64000
+    c.nodes["allocatable"][:, 1] = 256 << 30
+    c.nodes["raw_allocatable_mask"] = 0
+    c.nodes["custom_flags"] = 0
+    c.metrics["exists"] = 0
+    c.assigned_pods = c.assigned_pods[:0]
+    c.assigned_node = c.assigned_node[:0]
+    c.assigned_ts = c.assigned_ts[:0]
+    c.pod_metrics = c.pod_metrics[:0]
+    c.pm_offsets[:] = 0
+    e, o = pair(c)
+    got = _check_schedule(e, o, c.pods)
+    assert got["ties"].max() > 1000
+    assert e.stats()["slowpath_pods"] > 0
+
+
+def test_unschedulable_and_special_pods():
+    c = synth.make_cluster(800, 100, 11)
+    pods = c.pods.copy()
+    pods["requests"][::10, 0] = 10**9         # never fits: FitError, nothing assumed
+    pods["request_mask"][::10] |= 1
+    pods["flags"][5] |= abi.GS_POD_DAEMONSET
+    pods["flags"][6] |= abi.GS_POD_TERMINATED
+    pods["uid"][7] = c.assigned_pods["uid"][0]      # UID already in an assign cache
+    pods["name_key"][8] = c.pod_metrics["name_key"][0]  # a PodMetric carries its name
+    e, o = pair(c)
+    got = _check_schedule(e, o, pods)
+    assert (got["node"][::10] == -1).all()
+
+
+def test_score_according_prod_usage_and_weights():
+    c = synth.make_cluster(1500, 400, 5)
+    la = config.loadaware_args(scoreAccordingProdUsage=True, resourceWeights={"cpu": 3, "memory": 1},
+                               prodUsageThresholds={"cpu": 55})
+    fit = config.fit_args({"cpu": 2, "memory": 1, "ephemeral-storage": 1})
+    e, o = pair(c, la=la, fit=fit, weights=(2, 3))
+    _check_schedule(e, o, c.pods)
+
+
+def test_metric_and_node_updates_between_batches():
+    c = synth.make_cluster(1200, 600, 9)
+    e, o = pair(c)
+    _check_schedule(e, o, c.pods[:200])
+    # informer events: new metrics for some nodes, a node resize, pods unassigned, clock moves
+    idx = np.arange(0, 1200, 7, dtype=np.uint32)
+    m = c.metrics[idx].copy()
+    m["node_usage"]["cpu_milli"] //= 2
+    m["update_time_ns"] = c.now_ns + 30 * synth.SEC
+    for x in (e, o):
+        x.set_now(c.now_ns + 200 * synth.SEC)
+        x.upsert_metrics(m, idx=idx)
+        n = c.nodes[:50].copy()
+        n["allocatable"][:, 0] += 8000
+        x.upsert_nodes(n, idx=np.arange(50, dtype=np.uint32))
+        x.unassign(c.assigned_node[:40], c.assigned_pods[:40])
+    _check_schedule(e, o, c.pods[200:])
+
+
+def test_two_ranks_on_one_gpu_callback_transport():
+    """The sharded path (2 ranks, host all-gather) on one GPU: same placements as one rank / the oracle."""
+    c = synth.make_cluster(3001, 500, 13)
+    cfg = config.make_config(c.num_nodes)
+    E = engine_cls()
+    engines = [E(cfg), E(cfg)]
+    for x in engines:
+        synth.load_into(x, c)
+    barrier = threading.Barrier(2)
+    slots = [None, None]
+
+    def make_ag(r):
+        def ag(data):
+            slots[r] = data
+            barrier.wait()
+            out = list(slots)
+            barrier.wait()
+            return out
+        return ag
+
+    for r, x in enumerate(engines):
+        x.comm_init_callback(2, r, make_ag(r))
+    res = [None, None]
+
+    def run(r):
+        res[r] = engines[r].schedule(c.pods)
+
+    th = [threading.Thread(target=run, args=(r,)) for r in range(2)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=300)
+    o = orc.Oracle(cfg)
+    synth.load_into(o, c)
+    want = o.schedule(c.pods)
+    for r in range(2):
+        assert res[r] is not None
+        for f in ("node", "score", "ties", "feasible"):
+            assert np.array_equal(res[r][f], want[f]), (r, f)
+    assert engines[0].stats()["shard_end"] == engines[1].stats()["shard_begin"]
