@@ -221,9 +221,10 @@ LaDerived derive_loadaware(const gs_loadaware_args& a, const HostNode& hn) {
   LaDerived d;
   const gs_node& n = hn.node;
   const gs_node_metric& m = hn.metric;
-  if (!m.exists) return d;
-  d.sflags |= SF_METRIC;
-  if (m.has_update_time) d.sflags |= SF_UPDATE_TIME;
+  // Score-side usage is derived even without a NodeMetric (Score then returns 0 anyway): the value is
+  // what the row must hold once a metric appears, and what device-side Reserve deltas accumulate into.
+  if (m.exists) d.sflags |= SF_METRIC;
+  if (m.exists && m.has_update_time) d.sflags |= SF_UPDATE_TIME;
   // ---- Filter profile (helper.go:102-140)
   Thr usage{{a.usage_thresholds[0], a.usage_thresholds[1]}, a.usage_thresholds_mask};
   Thr prod{{a.prod_usage_thresholds[0], a.prod_usage_thresholds[1]}, a.prod_usage_thresholds_mask};
@@ -250,7 +251,7 @@ LaDerived derive_loadaware(const gs_loadaware_args& a, const HostNode& hn) {
   }
   // non-prod verdict: filterNodeUsage (load_aware.go:173-224)
   const Thr& th = has_agg ? agg : usage;
-  if (th.mask && m.has_node_metric) {
+  if (m.exists && th.mask && m.has_node_metric) {
     Vec2 u;
     bool have = has_agg ? target_agg(m, agg_dur, agg_type, &u) : (u = usage_of(m.node_usage), true);
     if (have && usage_exceeds(th, u, n)) d.sflags |= SF_FAIL_NP;
@@ -258,7 +259,7 @@ LaDerived derive_loadaware(const gs_loadaware_args& a, const HostNode& hn) {
   // prod verdict: filterProdUsage (load_aware.go:226-254)
   if (prod.mask) {
     d.sflags |= SF_PROD_THR;
-    if (!hn.pms.empty()) {
+    if (m.exists && !hn.pms.empty()) {
       std::unordered_map<uint64_t, Vec2> pm;
       for (const auto& e : hn.pms)
         if (e.in_lister && e.priority_class == GS_PRIO_PROD) pm[e.name_key] = usage_of(e.usage);

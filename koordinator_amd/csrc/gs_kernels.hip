@@ -853,10 +853,11 @@ hipError_t launch_scatter_rows(const MirrorView& m, const uint32_t* idx, const i
 
 hipError_t set_kernel_attributes() {
   hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(commit_kernel),
-                                     hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+                                     hipFuncAttributeMaxDynamicSharedMemorySize,
+                                     (int)commit_smem_bytes(MAX_BATCH, MAX_RANKS));
   if (e != hipSuccess) return e;
   return hipFuncSetAttribute(reinterpret_cast<const void*>(cand_kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
-                             64 * 1024);
+                             (int)cand_smem_bytes(8191));
 }
 
 }  // namespace gs

@@ -49,6 +49,9 @@ def test_golden_loadaware_score(case):
 @pytest.mark.parametrize("cid,nodes,pods", [(0, 1000, 300), (1, 5000, 64)])
 def test_evaluate_matches_oracle(cid, nodes, pods):
     c = synth.make_cluster(nodes, pods, cid)
+    c.pods["requests"][::5, 0] = 40_000          # 40-core pods: exercise Fit "Insufficient cpu"
+    c.pods["requests"][1::7, 2] = 480 << 30      # and "Insufficient ephemeral-storage"
+    c.pods["request_mask"][:] |= 0x7
     e, o = pair(c)
     gs, gc, gp = e.evaluate(c.pods)
     os_, oc, op = o.evaluate(c.pods)
@@ -56,7 +59,9 @@ def test_evaluate_matches_oracle(cid, nodes, pods):
     assert np.array_equal(gp, op), "per-plugin scores differ"
     assert np.array_equal(gs, os_), "weighted totals differ"
     # the synthetic cluster exercises every verdict
-    assert (gc == 0).any() and (gc & abi.GS_FAIL_LOADAWARE).any() and (gc & abi.GS_FAIL_FIT_CPU).any()
+    for bit in (abi.GS_FAIL_LOADAWARE, abi.GS_FAIL_FIT_CPU, abi.GS_FAIL_FIT_EPHEMERAL):
+        assert (gc & bit).any(), bit
+    assert (gc == 0).any()
 
 
 def _check_schedule(e, o, pods, seq=None):
