@@ -151,7 +151,7 @@ def main() -> None:
                             "sequential scheduleOne with NodeResourcesFit(LeastAllocated)+LoadAwareScheduling "
                             "filter+score, selectHost, assume+Reserve; NodeNUMAResource not yet on the path",
                 "nodes": n_nodes, "pods_per_step": P, "batch": args.batch, "parallelism": f"node-shard x{world}",
-                "cand_cap": 256,
+                "level_list_cap": 2048,
             },
             "roofline": {
                 "bound": "hbm",

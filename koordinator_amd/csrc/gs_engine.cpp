@@ -13,6 +13,7 @@
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <unordered_map>
@@ -114,6 +115,7 @@ struct gs_ctx {
   gs_allgather_fn cb = nullptr;
   void* cb_user = nullptr;
   gs_stats stats{};
+  uint64_t* d_stamps = nullptr;   // GS_COMMIT_STAMPS=1: commit-kernel phase cycle sums
 };
 
 namespace {
@@ -521,9 +523,9 @@ int compute_profile(gs_ctx* c) {
   int64_t ms = 0;
   if (pf.enabled & GS_ENABLE_FIT_SCORE) ms += 100 * cfg.plugin_weights[GS_PLUGIN_FIT];
   if (pf.enabled & GS_ENABLE_LA_SCORE) ms += 100 * cfg.plugin_weights[GS_PLUGIN_LOADAWARE];
-  if (cfg.plugin_weights[0] < 0 || cfg.plugin_weights[1] < 0 || ms > 8191)
-    return fail(c, GS_EUNSUPPORTED, "profile score weights must keep the max total score <= 8191 (got %lld)",
-                (long long)ms);
+  if (cfg.plugin_weights[0] < 0 || cfg.plugin_weights[1] < 0 || ms > MAX_SCORE_LIMIT)
+    return fail(c, GS_EUNSUPPORTED, "profile score weights must keep the max total score <= %d (got %lld)",
+                MAX_SCORE_LIMIT, (long long)ms);
   c->max_score = (int)ms;
   return GS_OK;
 }
@@ -536,12 +538,11 @@ void set_shard(gs_ctx* c) {
   c->stats.shard_end = c->n1;
 }
 
-// one rank's exchange block: [B x CAND_CAP list keys | B headers], padded so that rank blocks stay
-// addressable as whole pod lists (stride in units of CAND_CAP keys)
+// one rank's exchange block: [B x LCAP listed node ids | B LevelHdr], padded to 256 B
+size_t lists_bytes(int B) { return (size_t)B * LCAP * 4; }
 size_t xchg_block_bytes(int B) {
-  size_t raw = (size_t)B * CAND_CAP * 8 + (size_t)B * sizeof(CandHdr);
-  size_t unit = (size_t)CAND_CAP * 8;
-  return (raw + unit - 1) / unit * unit;
+  size_t raw = lists_bytes(B) + (size_t)B * sizeof(LevelHdr);
+  return (raw + 255) / 256 * 256;
 }
 
 int alloc_exchange(gs_ctx* c) {
@@ -561,9 +562,8 @@ double ev_ms(hipEvent_t a, hipEvent_t b) {
 
 // One device pass over pods [0, b) of the staged batch. Returns number of pods committed (>= 1).
 int run_batch(gs_ctx* c, const gs_pod* pods, int b, int* committed_out) {
-  const size_t lists_bytes = (size_t)c->B * CAND_CAP * 8;
-  uint64_t* d_lists = reinterpret_cast<uint64_t*>(c->d_xchg_send);
-  CandHdr* d_hdrs = reinterpret_cast<CandHdr*>(c->d_xchg_send + lists_bytes);
+  uint32_t* d_lists = reinterpret_cast<uint32_t*>(c->d_xchg_send);
+  LevelHdr* d_hdrs = reinterpret_cast<LevelHdr*>(c->d_xchg_send + lists_bytes(c->B));
   int prod_cols = 0;
   for (int i = 0; i < b; ++i) prod_cols |= (c->h_pods[i].flags & PF_PROD_SCORE) ? 1 : 0;
   uint32_t len = c->n1 - c->n0;
@@ -572,17 +572,11 @@ int run_batch(gs_ctx* c, const gs_pod* pods, int b, int* committed_out) {
   HIP_TRY(c, hipEventRecord(c->ev[1], c->st));
   HIP_TRY(c, launch_cand(c->d_S, c->ld, len, c->n0, b, c->max_score, d_lists, d_hdrs, c->st));
   HIP_TRY(c, hipEventRecord(c->ev[2], c->st));
-  const uint64_t* all_lists = d_lists;
-  const CandHdr* all_hdrs = d_hdrs;
-  size_t list_stride = (size_t)c->B, hdr_stride = (size_t)c->B;
+  const uint8_t* xbase = c->d_xchg_send;
   if (c->nranks > 1) {
     int rc = exchange(c, c->d_xchg_send, c->d_xchg_recv, c->xchg_bytes);
     if (rc) return rc;
-    // recv = R blocks of [lists | hdrs]; view them with strides in units of one rank block
-    all_lists = reinterpret_cast<const uint64_t*>(c->d_xchg_recv);
-    all_hdrs = reinterpret_cast<const CandHdr*>(c->d_xchg_recv + lists_bytes);
-    list_stride = c->xchg_bytes / (CAND_CAP * 8);              // pods-per-rank-block in list units
-    hdr_stride = c->xchg_bytes / sizeof(CandHdr);
+    xbase = c->d_xchg_recv;
   }
   CommitArgs a{};
   a.m = c->mv;
@@ -590,15 +584,16 @@ int run_batch(gs_ctx* c, const gs_pod* pods, int b, int* committed_out) {
   a.seq = c->d_seq;
   a.npods = b;
   a.nranks = c->nranks;
-  a.lists = all_lists;
-  a.hdrs = all_hdrs;
-  a.list_stride = list_stride;
-  a.hdr_stride = hdr_stride;
+  a.shard_size = (c->N + c->nranks - 1) / c->nranks;
+  a.xbase = xbase;
+  a.xblock = c->xchg_bytes;
+  a.bmax = c->B;
   a.pf = c->pf;
   a.seed = c->cfg.seed;
   a.forced_node = -1;
   a.out = c->d_out;
   a.committed = c->d_committed;
+  a.stamps = c->d_stamps;
   HIP_TRY(c, hipEventRecord(c->ev[3], c->st));
   HIP_TRY(c, launch_commit(a, c->st));
   HIP_TRY(c, hipEventRecord(c->ev[4], c->st));
@@ -772,8 +767,8 @@ int gs_create(const gs_config* cfg, gs_ctx** out) {
     return GS_EINVAL;
   }
   c->B = cfg->batch_size ? (int)cfg->batch_size : MAX_BATCH;
-  if (c->B < 1 || c->B > MAX_BATCH || (cfg->cand_cap && cfg->cand_cap != (uint32_t)CAND_CAP)) {
-    fprintf(stderr, "gpuscore: batch_size must be in [1,%d] and cand_cap %d\n", MAX_BATCH, CAND_CAP);
+  if (c->B < 1 || c->B > MAX_BATCH || (cfg->cand_cap && cfg->cand_cap != (uint32_t)LCAP)) {
+    fprintf(stderr, "gpuscore: batch_size must be in [1,%d] and cand_cap %d\n", MAX_BATCH, LCAP);
     delete c;
     return GS_EUNSUPPORTED;
   }
@@ -798,8 +793,9 @@ int gs_create(const gs_config* cfg, gs_ctx** out) {
   if ((e = hipMalloc(&c->d_i32, np * NUM_I32_COLS * 4)) != hipSuccess) return bail("hipMalloc mirror", e);
   (void)hipMemset(c->d_i64, 0, np * NUM_I64_COLS * 8);
   (void)hipMemset(c->d_i32, 0, np * NUM_I32_COLS * 4);
-  for (int k = 0; k < NUM_I64_COLS; ++k) c->mv.i64[k] = c->d_i64 + (size_t)k * np;
-  for (int k = 0; k < NUM_I32_COLS; ++k) c->mv.i32[k] = c->d_i32 + (size_t)k * np;
+  c->mv.i64 = c->d_i64;
+  c->mv.i32 = c->d_i32;
+  c->mv.npad = (uint32_t)np;
   c->ld = c->npad;
   if ((e = hipMalloc(&c->d_pods, sizeof(PodVec) * c->B)) != hipSuccess) return bail("hipMalloc", e);
   if ((e = hipMalloc(&c->d_seq, 8 * c->B)) != hipSuccess) return bail("hipMalloc", e);
@@ -823,6 +819,10 @@ int gs_create(const gs_config* cfg, gs_ctx** out) {
   if ((e = hipHostMalloc(&c->h_committed, 4, hipHostMallocDefault)) != hipSuccess) return bail("hipHostMalloc", e);
   if ((e = hipHostMalloc(&c->h_xchg_send, xb, hipHostMallocDefault)) != hipSuccess) return bail("hipHostMalloc", e);
   (void)hipMemset(c->d_S, 0xff, (size_t)c->B * c->ld * 2);
+  if (getenv("GS_COMMIT_STAMPS") && getenv("GS_COMMIT_STAMPS")[0] == '1') {
+    if ((e = hipMalloc(&c->d_stamps, 8 * 8)) != hipSuccess) return bail("hipMalloc", e);
+    (void)hipMemset(c->d_stamps, 0, 64);
+  }
   if ((e = hipDeviceSynchronize()) != hipSuccess) return bail("hipDeviceSynchronize", e);
   c->stats.node_row_bytes = 3 * 8 + 4 + 2 * 8 + 2 * 8 + 2 * 8 + 2 * 8 + 4;   // 96 B
   *out = c;
@@ -831,6 +831,17 @@ int gs_create(const gs_config* cfg, gs_ctx** out) {
 
 int gs_destroy(gs_ctx* c) {
   if (!c) return GS_EINVAL;
+  if (c->d_stamps) {
+    uint64_t st[8] = {};
+    if (hipMemcpy(st, c->d_stamps, 64, hipMemcpyDeviceToHost) == hipSuccess) {
+      uint64_t tot = 0;
+      for (uint64_t v : st) tot += v;
+      fprintf(stderr, "gpuscore commit phases (s_memtime ticks, %% of %llu):", (unsigned long long)tot);
+      for (int i = 0; i < 8; ++i) fprintf(stderr, " p%d=%.1f%%", i, tot ? 100.0 * st[i] / tot : 0.0);
+      fprintf(stderr, "\n");
+    }
+    (void)hipFree(c->d_stamps);
+  }
   if (c->comm) ncclCommDestroy(c->comm);
   if (c->st) (void)hipStreamSynchronize(c->st);
   void* dev[] = {c->d_i64, c->d_i32, c->d_pods, c->d_seq, c->d_S, c->d_xchg_send, c->d_xchg_recv, c->d_out,

@@ -8,17 +8,42 @@
 
 namespace gs {
 
-constexpr int CAND_CAP = 256;                                   // candidate-list capacity per (pod, shard)
-constexpr int MAX_BATCH = 128;                                  // pods per device pass (commit LDS budget)
+constexpr int MAX_BATCH = 128;       // pods per device pass (commit-kernel LDS budget)
 constexpr int MAX_RANKS = 8;
-constexpr int ROW_WORDS = NUM_I64_COLS + NUM_I32_COLS;          // staging row: i64 columns, then i32 columns widened
+constexpr int MAXLEV = 8;            // score levels listed per (pod, shard)
+constexpr int LCAP = 2048;           // listed nodes per (pod, shard)
+constexpr int PODS_PER_BLOCK = 16;   // eval kernel: pods per workgroup (grid.y = ceil(B / 16))
+constexpr int MAX_SCORE_LIMIT = 2047; // cand kernel keeps one histogram per wave in LDS
+constexpr int ROW_WORDS = NUM_I64_COLS + NUM_I32_COLS;  // staging row: i64 columns, then i32 widened
 
+// The HBM mirror: column c of the int64 table starts at i64 + c*npad.
 struct MirrorView {
-  int64_t* i64[NUM_I64_COLS];
-  int32_t* i32[NUM_I32_COLS];
+  int64_t* i64;
+  int32_t* i32;
+  uint32_t npad;
+#ifdef __HIPCC__
+  __host__ __device__
+#endif
+  int64_t* c64(int c) const { return i64 + (size_t)c * npad; }
+#ifdef __HIPCC__
+  __host__ __device__
+#endif
+  int32_t* c32(int c) const { return i32 + (size_t)c * npad; }
 };
 
-struct PlacementDev {   // layout == gs_placement minus flags
+// Per (pod, shard) candidate summary: the top score levels of the shard's row, each with its full
+// node list (node index order). Every feasible node of the shard with a score above `next` is listed.
+struct LevelHdr {
+  int32_t nlev;              // listed levels
+  int32_t feasible;          // feasible nodes of the shard for this pod
+  int32_t next;              // highest score of a feasible node that is NOT listed (-1: none)
+  int32_t total;             // listed nodes
+  int32_t score[MAXLEV];     // descending
+  int32_t count[MAXLEV];     // nodes per level; level j starts at sum(count[0..j))
+};
+static_assert(sizeof(LevelHdr) == 80, "LevelHdr layout");
+
+struct PlacementDev {   // layout == gs_placement
   int32_t node;
   uint32_t feasible;
   int64_t score;
@@ -32,10 +57,10 @@ struct CommitArgs {
   const uint64_t* seq;
   int npods;
   int nranks;
-  const uint64_t* lists;     // [rank][pod][CAND_CAP]
-  const CandHdr* hdrs;       // [rank][pod]
-  size_t list_stride;        // pods per rank block in `lists`
-  size_t hdr_stride;
+  uint32_t shard_size;       // ceil(N / nranks): shard of node i = i / shard_size
+  const uint8_t* xbase;      // rank r block at xbase + r*xblock: [npods_max x LCAP u32 lists | LevelHdr x npods_max]
+  size_t xblock;
+  int bmax;                  // pods per block layout (lists/hdrs are laid out for bmax pods)
   Profile pf;
   uint64_t seed;
   int32_t forced_node;       // >= 0: pod 0 was resolved by the exact full-row path
@@ -44,6 +69,7 @@ struct CommitArgs {
   int32_t forced_feasible;
   PlacementDev* out;
   int32_t* committed;
+  uint64_t* stamps;          // diagnostics: per-phase s_memtime cycle sums (nullptr: normal build)
 };
 
 hipError_t set_kernel_attributes();
@@ -54,9 +80,8 @@ hipError_t launch_eval(const MirrorView& m, const PodVec* pods, int npods, const
 hipError_t launch_eval_full(const MirrorView& m, const PodVec* pods, int npods, const Profile& pf, uint32_t N,
                             int16_t* scores, uint16_t* codes, int16_t* plugin, int prod_cols, hipStream_t st);
 hipError_t launch_cand(const int16_t* S, uint32_t ld, uint32_t len, uint32_t n0, int npods, int max_score,
-                       uint64_t* lists, CandHdr* hdrs, hipStream_t st);
-size_t cand_smem_bytes(int max_score);
-size_t commit_smem_bytes(int B, int nranks);
+                       uint32_t* lists, LevelHdr* hdrs, hipStream_t st);
+size_t commit_smem_bytes(int B);
 hipError_t launch_commit(const CommitArgs& a, hipStream_t st);
 hipError_t launch_row_stats(const int16_t* S, uint32_t len, RowStat* out, hipStream_t st);
 hipError_t launch_row_select(const int16_t* S, uint32_t len, int score, int64_t target, uint32_t n0, int32_t* out,

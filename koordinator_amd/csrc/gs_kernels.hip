@@ -1,18 +1,19 @@
 // gs_kernels.hip — CDNA4 (gfx950) kernels of the batched Filter/Score engine.
 //
 //   node_prep_kernel   per batch, O(N): LoadAware expiry against `now` -> dynamic filter/score flags
-//   eval_kernel        the hot kernel: B pods x shard nodes, fused Fit filter + LoadAware filter +
-//                      Fit LeastAllocated score + LoadAware score + weighted sum -> int16 score rows
-//   cand_kernel        per pod: histogram -> threshold -> compaction -> bitonic sort -> candidate list
-//   commit_kernel      one wave: sequential selectHost + assume/Reserve deltas over the batch, with
-//                      exact re-scoring of the nodes earlier pods of the batch landed on
-//   row_stats_kernel / row_select_kernel   exact full-row path (massive ties)
+//   eval_kernel        the hot kernel: (node tile x pod group) workgroups, fused Fit filter + LoadAware
+//                      filter + Fit LeastAllocated score + LoadAware score + weighted sum -> int16 rows
+//   cand_kernel        per pod: per-wave histograms -> top score levels -> order-preserving compaction of
+//                      every node of those levels (node index order) -> LevelHdr + level lists
+//   commit_kernel      one workgroup: the batch's pods in order — selectHost over (listed levels of every
+//                      shard, minus/plus the rows earlier pods of the batch landed on, re-scored exactly),
+//                      then assume/Reserve deltas; cuts the batch if a pod's levels are exhausted
+//   row_stats_kernel / row_select_kernel   exact full-row path (a level too large to list)
 //   scatter_rows_kernel   host -> HBM delta rows (AoS staging -> SoA columns)
 //
-// Integer semantics follow Go: int64 two's complement, truncating division. The three float64 spots
-// of the reference (LoadAware filter %, estimator scaling, amplification) are host-side per node /
-// per pod (PreFilter / mirror update); the per-pair work here is pure int64 with an exact
-// reciprocal-estimate-plus-correction division (quotients are in [0,100]).
+// Integer semantics follow Go: int64 two's complement, truncating division. The float64 spots of the
+// reference (LoadAware filter %, estimator scaling) are host-side per node / per pod; per-pair work here is
+// int64 with an exact reciprocal-estimate-plus-correction division (quotients lie in [0,100]).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -21,7 +22,7 @@
 namespace gs {
 
 // ------------------------------------------------------------------------------------------------
-// exact floor((x*100)/cap) for 0 <= x <= cap, cap > 0, x*100 < 2^63
+// exact floor((x*100)/cap) for 0 <= x <= cap, 0 < cap < 2^53
 __device__ __forceinline__ float u64_to_f32(uint64_t v) {
   return (float)(uint32_t)(v >> 32) * 4294967296.0f + (float)(uint32_t)v;
 }
@@ -54,9 +55,10 @@ __device__ __forceinline__ int32_t small_div(int32_t a, int32_t b) {
   return q;
 }
 
-// node row as held in registers by the filter+score kernel
+// A node row: everything one Filter+Score evaluation reads (scalar-resource columns stay in HBM and are
+// read only for pods that request / profiles that weigh scalar resources).
 struct Row {
-  int64_t free[3];      // cpu, mem, eph
+  int64_t free[7];      // Allocatable - Requested per slot (slots 3..6 only in the commit's LDS copy)
   int64_t alloc[2];     // cpu, mem
   int64_t nzfree[2];
   int64_t la_cap[2];
@@ -65,28 +67,37 @@ struct Row {
   int32_t free_pods;
   uint32_t dflags;
   uint32_t node;        // global index
+  uint32_t pad;
 };
+constexpr int ROW_I64 = 17;   // int64 words of Row, in the column order of kRowCol
+
+__constant__ int kRowCol[ROW_I64] = {C_FREE_CPU,     C_FREE_MEM,    C_FREE_EPH,   C_FREE_BCPU,  C_FREE_BMEM,
+                                     C_FREE_MCPU,    C_FREE_MMEM,   C_ALLOC_CPU,  C_ALLOC_MEM,  C_NZFREE_CPU,
+                                     C_NZFREE_MEM,   C_LA_CAP_CPU,  C_LA_CAP_MEM, C_LA_FREE_CPU, C_LA_FREE_MEM,
+                                     C_LA_PFREE_CPU, C_LA_PFREE_MEM};
+// Row words an assume/Reserve changes (written back by the commit kernel)
+__device__ __forceinline__ bool row_word_mutable(int j) { return j < 7 || j == 9 || j == 10 || j >= 13; }
 
 __device__ __forceinline__ void load_row(const MirrorView& m, uint32_t i, bool prod_cols, Row& r) {
-  r.free[0] = m.i64[C_FREE_CPU][i];
-  r.free[1] = m.i64[C_FREE_MEM][i];
-  r.free[2] = m.i64[C_FREE_EPH][i];
-  r.alloc[0] = m.i64[C_ALLOC_CPU][i];
-  r.alloc[1] = m.i64[C_ALLOC_MEM][i];
-  r.nzfree[0] = m.i64[C_NZFREE_CPU][i];
-  r.nzfree[1] = m.i64[C_NZFREE_MEM][i];
-  r.la_cap[0] = m.i64[C_LA_CAP_CPU][i];
-  r.la_cap[1] = m.i64[C_LA_CAP_MEM][i];
-  r.la_free[0] = m.i64[C_LA_FREE_CPU][i];
-  r.la_free[1] = m.i64[C_LA_FREE_MEM][i];
+  r.free[0] = m.c64(C_FREE_CPU)[i];
+  r.free[1] = m.c64(C_FREE_MEM)[i];
+  r.free[2] = m.c64(C_FREE_EPH)[i];
+  r.alloc[0] = m.c64(C_ALLOC_CPU)[i];
+  r.alloc[1] = m.c64(C_ALLOC_MEM)[i];
+  r.nzfree[0] = m.c64(C_NZFREE_CPU)[i];
+  r.nzfree[1] = m.c64(C_NZFREE_MEM)[i];
+  r.la_cap[0] = m.c64(C_LA_CAP_CPU)[i];
+  r.la_cap[1] = m.c64(C_LA_CAP_MEM)[i];
+  r.la_free[0] = m.c64(C_LA_FREE_CPU)[i];
+  r.la_free[1] = m.c64(C_LA_FREE_MEM)[i];
   if (prod_cols) {
-    r.la_pfree[0] = m.i64[C_LA_PFREE_CPU][i];
-    r.la_pfree[1] = m.i64[C_LA_PFREE_MEM][i];
+    r.la_pfree[0] = m.c64(C_LA_PFREE_CPU)[i];
+    r.la_pfree[1] = m.c64(C_LA_PFREE_MEM)[i];
   } else {
     r.la_pfree[0] = r.la_pfree[1] = 0;
   }
-  r.free_pods = m.i32[C_FREE_PODS][i];
-  r.dflags = (uint32_t)m.i32[C_DFLAGS][i];
+  r.free_pods = m.c32(C_FREE_PODS)[i];
+  r.dflags = (uint32_t)m.c32(C_DFLAGS)[i];
   r.node = i;
 }
 
@@ -96,7 +107,8 @@ struct PairOut {
 };
 
 // Filter (Fit + LoadAware) and Score (Fit LeastAllocated + LoadAware) of one pod on one node.
-template <bool FULL>
+// LDS_SCALARS: scalar free columns come from r.free[3..6] (the commit's LDS copy) instead of HBM.
+template <bool FULL, bool LDS_SCALARS>
 __device__ __forceinline__ PairOut eval_pair(const Row& r, const PodVec& p, const Profile& pf, const MirrorView& m) {
   PairOut o{0u, 0, 0};
   // ---- [upstream] noderesources Fit.Filter -> fitsRequest
@@ -107,8 +119,11 @@ __device__ __forceinline__ PairOut eval_pair(const Row& r, const PodVec& p, cons
       if (p.req[1] > r.free[1]) o.code |= 0x04u;
       if (p.req[2] > r.free[2]) o.code |= 0x08u;
       if (p.scalar_mask) {
-        for (int s = 3; s < 7; ++s)
-          if ((p.scalar_mask & (1u << s)) && p.req[s] > m.i64[C_FREE_EPH + s - 2][r.node]) o.code |= 0x10u;
+        for (int s = 3; s < 7; ++s) {
+          if (!(p.scalar_mask & (1u << s))) continue;
+          int64_t fr = LDS_SCALARS ? r.free[s] : m.c64(C_FREE_CPU + s)[r.node];
+          if (p.req[s] > fr) o.code |= 0x10u;
+        }
       }
     }
   }
@@ -134,9 +149,10 @@ __device__ __forceinline__ PairOut eval_pair(const Row& r, const PodVec& p, cons
         if (!(pf.fit_scalar_w_mask & (1u << s))) continue;
         int64_t preq = p.req[s];
         if (s >= 3 && preq == 0) continue;                              // un-requested scalar: bypass
-        int64_t cap = m.i64[C_ALLOC_CPU + s][r.node];
+        int64_t cap = m.c64(C_ALLOC_CPU + s)[r.node];
         if (cap == 0) continue;
-        ns += least_requested(m.i64[C_FREE_CPU + s][r.node], preq, cap) * pf.fit_w[s];
+        int64_t fr = (LDS_SCALARS || s == 2) ? r.free[s] : m.c64(C_FREE_CPU + s)[r.node];
+        ns += least_requested(fr, preq, cap) * pf.fit_w[s];
         ws += pf.fit_w[s];
       }
     }
@@ -159,14 +175,14 @@ __device__ __forceinline__ int32_t total_score(const PairOut& o, const Profile& 
 }
 
 // ------------------------------------------------------------------------------------------------
-// node-prep: LoadAware expiry (helper.go:36-41) evaluated at `now` for every node of the shard.
+// node-prep: LoadAware expiry (helper.go:36-41) evaluated at `now` for every node.
 __global__ void __launch_bounds__(256) node_prep_kernel(MirrorView m, uint32_t n0, uint32_t n1, int64_t now,
                                                         int32_t filter_expired, int32_t has_exp, int64_t exp_ns) {
   uint32_t i = n0 + blockIdx.x * 256 + threadIdx.x;
   if (i >= n1) return;
-  uint32_t sf = (uint32_t)m.i32[C_SFLAGS][i];
+  uint32_t sf = (uint32_t)m.c32(C_SFLAGS)[i];
   bool exists = sf & SF_METRIC;
-  bool expired = !exists || !(sf & SF_UPDATE_TIME) || (exp_ns > 0 && now - m.i64[C_UPDATE_TIME][i] >= exp_ns);
+  bool expired = !exists || !(sf & SF_UPDATE_TIME) || (exp_ns > 0 && now - m.c64(C_UPDATE_TIME)[i] >= exp_ns);
   bool skip_filter = !exists || (filter_expired && has_exp && expired);
   uint32_t df = 0;
   if (!skip_filter) {
@@ -174,38 +190,26 @@ __global__ void __launch_bounds__(256) node_prep_kernel(MirrorView m, uint32_t n
     if ((sf & SF_PROD_THR) ? (sf & SF_FAIL_P) : (sf & SF_FAIL_NP)) df |= DF_LA_FAIL_P;
   }
   if (!exists || (has_exp && expired)) df |= DF_LA_ZERO;
-  m.i32[C_DFLAGS][i] = (int32_t)df;
+  m.c32(C_DFLAGS)[i] = (int32_t)df;
 }
 
 // ------------------------------------------------------------------------------------------------
-// The hot kernel. Block = 256 threads x NPT nodes; every thread keeps its NPT node rows in registers
-// and sweeps all B pods (pod vectors are wave-uniform: scalar loads), writing one int16 score per
-// (pod,node): coalesced NPT*2-byte stores per lane, one contiguous row segment per pod.
-constexpr int NPT = 2;
-
+// The hot kernel. Workgroup = 256 consecutive nodes of the shard x PODS_PER_BLOCK pods. Each thread keeps
+// its node row in registers and sweeps the group's pods (wave-uniform pod vectors: scalar loads), writing
+// one int16 score per (pod, node): one coalesced 512-B row segment per pod per workgroup.
 __global__ void __launch_bounds__(256) eval_kernel(MirrorView m, const PodVec* __restrict__ pods, int npods,
                                                    Profile pf, uint32_t n0, uint32_t n1, int16_t* __restrict__ S,
                                                    uint32_t ld, int prod_cols) {
-  uint32_t local = (blockIdx.x * 256 + threadIdx.x) * NPT;
-  uint32_t len = n1 - n0;
-  Row row[NPT];
-  bool ok[NPT];
-#pragma unroll
-  for (int j = 0; j < NPT; ++j) {
-    ok[j] = local + j < len;
-    load_row(m, ok[j] ? n0 + local + j : n0, prod_cols, row[j]);
-  }
-  if (local >= ld) return;
-  for (int k = 0; k < npods; ++k) {
-    const PodVec& p = pods[k];
-    int16_t out[NPT];
-#pragma unroll
-    for (int j = 0; j < NPT; ++j) {
-      PairOut o = eval_pair<false>(row[j], p, pf, m);
-      out[j] = ok[j] ? (int16_t)total_score(o, pf) : (int16_t)-1;
-    }
-    uint32_t packed = (uint32_t)(uint16_t)out[0] | ((uint32_t)(uint16_t)out[1] << 16);
-    *reinterpret_cast<uint32_t*>(S + (size_t)k * ld + local) = packed;
+  const uint32_t local = blockIdx.x * 256 + threadIdx.x;
+  const uint32_t len = n1 - n0;
+  const bool ok = local < len;
+  Row row;
+  load_row(m, ok ? n0 + local : n0, prod_cols, row);
+  const int k0 = blockIdx.y * PODS_PER_BLOCK;
+  const int k1 = min(npods, k0 + PODS_PER_BLOCK);
+  for (int k = k0; k < k1; ++k) {
+    PairOut o = eval_pair<false, false>(row, pods[k], pf, m);
+    S[(size_t)k * ld + local] = ok ? (int16_t)total_score(o, pf) : (int16_t)-1;
   }
 }
 
@@ -218,7 +222,7 @@ __global__ void __launch_bounds__(256) eval_full_kernel(MirrorView m, const PodV
   Row r;
   load_row(m, i, prod_cols, r);
   for (int k = 0; k < npods; ++k) {
-    PairOut o = eval_pair<true>(r, pods[k], pf, m);
+    PairOut o = eval_pair<true, false>(r, pods[k], pf, m);
     size_t off = (size_t)k * N + i;
     if (scores) scores[off] = (int16_t)total_score(o, pf);
     if (codes) codes[off] = (uint16_t)o.code;
@@ -230,120 +234,137 @@ __global__ void __launch_bounds__(256) eval_full_kernel(MirrorView m, const PodV
 }
 
 // ------------------------------------------------------------------------------------------------
-// Candidate extraction: one block per pod row of the shard.
+// Candidate levels: one workgroup (4 waves) per pod row of the shard; wave w owns a contiguous quarter of
+// the row so that per-wave histograms give every wave its output offset within each level.
 constexpr int CAND_THREADS = 256;
 
 __global__ void __launch_bounds__(CAND_THREADS) cand_kernel(const int16_t* __restrict__ S, uint32_t ld, uint32_t len,
-                                                            uint32_t n0, int max_score, uint64_t* __restrict__ lists,
-                                                            CandHdr* __restrict__ hdrs) {
+                                                            uint32_t n0, int max_score, uint32_t* __restrict__ lists,
+                                                            LevelHdr* __restrict__ hdrs) {
   extern __shared__ __align__(16) uint32_t smem[];
   const int nbins = max_score + 1;
-  uint32_t* hist = smem;                                             // nbins
-  uint64_t* keys = reinterpret_cast<uint64_t*>(smem + ((nbins + 3) & ~3));  // CAND_CAP
-  __shared__ uint32_t seg[CAND_THREADS];
-  __shared__ int32_t s_theta, s_count, s_feasible;
+  uint32_t* whist = smem;                                        // [4][nbins]
+  uint32_t* comb = smem + 4 * nbins;                             // [nbins]
+  int8_t* slot_of = reinterpret_cast<int8_t*>(comb + nbins);     // [nbins]
+  __shared__ uint32_t segsum[CAND_THREADS];
+  __shared__ uint32_t s_total;
+  __shared__ LevelHdr s_hdr;
+  __shared__ uint32_t s_woff[4][MAXLEV];
   const int k = blockIdx.x;
-  const int t = threadIdx.x;
+  const int t = threadIdx.x, wave = t >> 6, lane = t & 63;
   const int16_t* row = S + (size_t)k * ld;
-  for (int b = t; b < nbins; b += CAND_THREADS) hist[b] = 0;
+  for (int b = t; b < 4 * nbins; b += CAND_THREADS) whist[b] = 0;
+  if (t == 0) s_total = 0;
   __syncthreads();
-  // pass 1: histogram of feasible scores (16-B loads: 8 scores per lane)
-  uint32_t nvec = len / 8;
-  for (uint32_t v = t; v < nvec; v += CAND_THREADS) {
-    int4 q = reinterpret_cast<const int4*>(row)[v];
+  // 16-B loads: 8 scores per lane, 512 per wave step. Rows are padded with -1 up to ld (a multiple of
+  // 1024), so the row is read as lenv = round_up(len, 512) entries.
+  const uint32_t lenv = (len + 511) & ~511u;
+  const uint32_t seg = (lenv / 512 + 3) / 4 * 512;
+  const uint32_t wb = min(lenv, wave * seg), we = min(lenv, wb + seg);
+  const int4* row4 = reinterpret_cast<const int4*>(row);
+  // pass 1: per-wave histograms of feasible scores
+  for (uint32_t i = wb + lane * 8; i < we; i += 512) {
+    int4 q = row4[i / 8];
     const int16_t* e = reinterpret_cast<const int16_t*>(&q);
 #pragma unroll
-    for (int j = 0; j < 8; ++j)
-      if (e[j] >= 0) atomicAdd(&hist[e[j]], 1u);
+    for (int x = 0; x < 8; ++x)
+      if (e[x] >= 0) atomicAdd(&whist[wave * nbins + e[x]], 1u);
   }
-  for (uint32_t i = nvec * 8 + t; i < len; i += CAND_THREADS)
-    if (row[i] >= 0) atomicAdd(&hist[row[i]], 1u);
   __syncthreads();
-  // threshold: smallest level theta with count(score >= theta) <= CAND_CAP
-  int per = (nbins + CAND_THREADS - 1) / CAND_THREADS;
+  const int per = (nbins + CAND_THREADS - 1) / CAND_THREADS;
   {
     uint32_t s = 0;
-    for (int b = t * per; b < min(nbins, (t + 1) * per); ++b) s += hist[b];
-    seg[t] = s;
+    for (int b = t * per; b < min(nbins, (t + 1) * per); ++b) {
+      uint32_t h = whist[b] + whist[nbins + b] + whist[2 * nbins + b] + whist[3 * nbins + b];
+      comb[b] = h;
+      slot_of[b] = -1;
+      s += h;
+    }
+    segsum[t] = s;
+    if (s) atomicAdd(&s_total, s);
   }
   __syncthreads();
   if (t == 0) {
-    uint32_t total = 0;
-    for (int i = 0; i < CAND_THREADS; ++i) total += seg[i];
+    // levels from the top until the pod's position in the batch is covered: pod k can find at most k of
+    // the listed nodes dirtied by earlier pods, so k+1 listed nodes always leave a clean one.
+    const uint32_t target = (uint32_t)k + 1;
+    LevelHdr h;
+    h.nlev = 0;
+    h.feasible = (int32_t)s_total;
+    h.next = -1;
     uint32_t cum = 0;
-    int theta = 0;
-    if (total <= (uint32_t)CAND_CAP) {
-      cum = total;                                 // every feasible node fits: complete list
-    } else {
-      theta = nbins;
-      bool stop = false;
-      for (int i = CAND_THREADS - 1; i >= 0 && !stop; --i) {
-        if (cum + seg[i] <= (uint32_t)CAND_CAP) {  // whole segment fits
-          cum += seg[i];
-          if (i * per < theta) theta = i * per;
-          continue;
+    bool stop = false;
+    for (int sg = CAND_THREADS - 1; sg >= 0 && !stop; --sg) {
+      if (!segsum[sg]) continue;
+      for (int b = min(nbins, (sg + 1) * per) - 1; b >= sg * per; --b) {
+        uint32_t c = comb[b];
+        if (!c) continue;
+        if (h.nlev == MAXLEV || cum + c > (uint32_t)LCAP || cum >= target) {
+          h.next = b;
+          stop = true;
+          break;
         }
-        for (int b = min(nbins, (i + 1) * per) - 1; b >= i * per; --b) {
-          if (cum + hist[b] > (uint32_t)CAND_CAP) break;
-          cum += hist[b];
-          theta = b;
-        }
-        stop = true;
+        h.score[h.nlev] = b;
+        h.count[h.nlev] = (int32_t)c;
+        slot_of[b] = (int8_t)h.nlev;
+        ++h.nlev;
+        cum += c;
       }
     }
-    s_theta = theta;
-    s_count = 0;
-    s_feasible = (int32_t)total;
+    for (int j = h.nlev; j < MAXLEV; ++j) { h.score[j] = -1; h.count[j] = 0; }
+    h.total = (int32_t)cum;
+    s_hdr = h;
   }
   __syncthreads();
-  const int theta = s_theta;
-  // pass 2: compaction of score >= theta
-  for (uint32_t v = t; v < nvec; v += CAND_THREADS) {
-    int4 q = reinterpret_cast<const int4*>(row)[v];
-    const int16_t* e = reinterpret_cast<const int16_t*>(&q);
+  const int nlev = s_hdr.nlev;
+  if (t < 4 * MAXLEV) {
+    int w = t / MAXLEV, j = t % MAXLEV;
+    uint32_t off = 0;
+    if (j < nlev) {
+      for (int jj = 0; jj < j; ++jj) off += s_hdr.count[jj];
+      for (int ww = 0; ww < w; ++ww) off += whist[ww * nbins + s_hdr.score[j]];
+    }
+    s_woff[w][j] = off;
+  }
+  __syncthreads();
+  // pass 2: order-preserving compaction of the listed levels (node order = (lane, element) order)
+  uint32_t* out = lists + (size_t)k * LCAP;
+  if (nlev > 0) {
+    uint32_t run[MAXLEV];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      if (e[j] >= 0 && e[j] >= theta) {
-        int pos = atomicAdd(&s_count, 1);
-        keys[pos] = cand_key(e[j], n0 + v * 8 + j);
+    for (int j = 0; j < MAXLEV; ++j) run[j] = s_woff[wave][j];
+    for (uint32_t base = wb; base < we; base += 512) {
+      int4 q = row4[(base + lane * 8) / 8];
+      const int16_t* e = reinterpret_cast<const int16_t*>(&q);
+      int slot[8];
+      bool any = false;
+#pragma unroll
+      for (int x = 0; x < 8; ++x) {
+        slot[x] = e[x] >= 0 ? slot_of[e[x]] : -1;
+        any |= slot[x] >= 0;
       }
-    }
-  }
-  for (uint32_t i = nvec * 8 + t; i < len; i += CAND_THREADS) {
-    int16_t e = row[i];
-    if (e >= 0 && e >= theta) {
-      int pos = atomicAdd(&s_count, 1);
-      keys[pos] = cand_key(e, n0 + i);
-    }
-  }
-  __syncthreads();
-  const int cnt = s_count;
-  for (int i = cnt + t; i < CAND_CAP; i += CAND_THREADS) keys[i] = 0;
-  __syncthreads();
-  // bitonic sort, descending
-  for (int size = 2; size <= CAND_CAP; size <<= 1) {
-    for (int stride = size >> 1; stride > 0; stride >>= 1) {
-      for (int i = t; i < CAND_CAP; i += CAND_THREADS) {
-        int jx = i ^ stride;
-        if (jx > i) {
-          bool desc = ((i & size) == 0);
-          uint64_t a = keys[i], b = keys[jx];
-          if (desc ? (a < b) : (a > b)) { keys[i] = b; keys[jx] = a; }
+      if (!__ballot(any)) continue;
+#pragma unroll
+      for (int j = 0; j < MAXLEV; ++j) {
+        if (j >= nlev) break;
+        int c = 0;
+#pragma unroll
+        for (int x = 0; x < 8; ++x) c += slot[x] == j;
+        if (!__ballot(c > 0)) continue;
+        int incl = c;
+        for (int o = 1; o < 64; o <<= 1) {
+          int v = __shfl_up(incl, o);
+          if (lane >= o) incl += v;
         }
+        int pos = run[j] + incl - c;
+#pragma unroll
+        for (int x = 0; x < 8; ++x)
+          if (slot[x] == j) out[pos++] = n0 + base + lane * 8 + x;
+        run[j] += __shfl(incl, 63);
       }
-      __syncthreads();
     }
   }
-  uint64_t* out = lists + (size_t)k * CAND_CAP;
-  for (int i = t; i < cnt; i += CAND_THREADS) out[i] = keys[i];
-  if (t == 0) {
-    CandHdr h;
-    h.count = cnt;
-    h.theta = theta;
-    h.complete = (cnt == s_feasible) ? 1 : 0;
-    h.feasible = s_feasible;
-    hdrs[k] = h;
-  }
+  if (t == 0) hdrs[k] = s_hdr;
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -374,103 +395,39 @@ __host__ __device__ inline int64_t tiebreak_position(uint64_t seed, uint64_t seq
 int64_t host_tiebreak_position(uint64_t seed, uint64_t seq, int64_t T) { return tiebreak_position(seed, seq, T); }
 
 // ------------------------------------------------------------------------------------------------
-// Sequential commit (one wave). For pod k of the batch: effective scores = candidate lists (snapshot
-// at batch start) for clean nodes + exact re-scores (dsc) for nodes earlier pods landed on. Valid while
-// the max effective score is >= every incomplete list's threshold; otherwise the batch is cut at k.
-constexpr int HASH = 512;
+// Sequential commit: ONE wave walks the batch's pods in order (no workgroup barriers: LDS traffic of a
+// single wave is in order, so phases only need compiler scheduling fences, and global prefetches of the
+// next pod's headers stay in flight while the current pod is resolved).
+//
+// For pod k the effective score of a node is its batch-start score (S, summarized per shard by the listed
+// levels) unless an earlier pod of the batch landed on it ("dirty"): dirty rows live in LDS and their
+// scores for every later pod are re-evaluated exactly (dso = batch-start score, dsc = current score).
+// The max M is valid when it exceeds every shard's highest unlisted score (`next`); otherwise the batch
+// is cut at k. Ties at M are ordered by node index across shards (shards are contiguous ranges).
+constexpr int HASH = 1024;
+constexpr int WIN = 2 * MAX_BATCH + 8;
+#define WAVE_FENCE() __builtin_amdgcn_wave_barrier()
 
-struct __align__(16) DRow {
-  int64_t free[7];
-  int64_t alloc[2];
-  int64_t nzfree[2];
-  int64_t la_cap[2];
-  int64_t la_free[2];
-  int64_t la_pfree[2];
-  int32_t free_pods;
-  uint32_t dflags;
-  uint32_t node;
-  uint32_t pad;
-};
-
-__device__ __forceinline__ void drow_load(const MirrorView& m, uint32_t i, DRow& d) {
-  for (int s = 0; s < 7; ++s) d.free[s] = m.i64[C_FREE_CPU + s][i];
-  d.alloc[0] = m.i64[C_ALLOC_CPU][i];
-  d.alloc[1] = m.i64[C_ALLOC_MEM][i];
-  d.nzfree[0] = m.i64[C_NZFREE_CPU][i];
-  d.nzfree[1] = m.i64[C_NZFREE_MEM][i];
-  d.la_cap[0] = m.i64[C_LA_CAP_CPU][i];
-  d.la_cap[1] = m.i64[C_LA_CAP_MEM][i];
-  d.la_free[0] = m.i64[C_LA_FREE_CPU][i];
-  d.la_free[1] = m.i64[C_LA_FREE_MEM][i];
-  d.la_pfree[0] = m.i64[C_LA_PFREE_CPU][i];
-  d.la_pfree[1] = m.i64[C_LA_PFREE_MEM][i];
-  d.free_pods = m.i32[C_FREE_PODS][i];
-  d.dflags = (uint32_t)m.i32[C_DFLAGS][i];
-  d.node = i;
+__device__ __forceinline__ int32_t row_score(const Row& d, const PodVec& p, const Profile& pf, const MirrorView& m) {
+  return total_score(eval_pair<false, true>(d, p, pf, m), pf);
 }
 
-__device__ __forceinline__ void drow_to_row(const DRow& d, Row& r) {
-  r.free[0] = d.free[0]; r.free[1] = d.free[1]; r.free[2] = d.free[2];
-  r.alloc[0] = d.alloc[0]; r.alloc[1] = d.alloc[1];
-  r.nzfree[0] = d.nzfree[0]; r.nzfree[1] = d.nzfree[1];
-  r.la_cap[0] = d.la_cap[0]; r.la_cap[1] = d.la_cap[1];
-  r.la_free[0] = d.la_free[0]; r.la_free[1] = d.la_free[1];
-  r.la_pfree[0] = d.la_pfree[0]; r.la_pfree[1] = d.la_pfree[1];
-  r.free_pods = d.free_pods; r.dflags = d.dflags; r.node = d.node;
-}
-
-// eval_pair reads scalar free columns from the mirror for scalar-requesting pods: in the commit those
-// must come from the LDS row, so the commit uses this wrapper with a mirror view onto a 1-row table.
-__device__ __forceinline__ int32_t drow_score(const DRow& d, const PodVec& p, const Profile& pf, const MirrorView& m) {
-  Row r;
-  drow_to_row(d, r);
-  PairOut o;
-  if (p.scalar_mask || pf.fit_scalar_w_mask) {
-    // slow generic path: evaluate against the LDS copy for scalar columns
-    o = PairOut{0u, 0, 0};
-    if (pf.enabled & 0x1u) {
-      if (d.free_pods < 1) o.code |= 0x01u;
-      if (!(p.flags & PF_ALL_ZERO)) {
-        for (int s = 0; s < 7; ++s) {
-          bool chk = s < 3 || (p.scalar_mask & (1u << s));
-          if (chk && p.req[s] > d.free[s]) o.code |= (s < 3) ? (0x02u << s) : 0x10u;
-        }
-      }
-    }
-    if ((pf.enabled & 0x4u) && !(p.flags & PF_DAEMONSET)) {
-      uint32_t bit = (p.flags & PF_PROD) ? DF_LA_FAIL_P : DF_LA_FAIL_NP;
-      if (d.dflags & bit) o.code |= 0x20u;
-    }
-    if (o.code) return -1;
-    if (pf.enabled & 0x2u) {
-      int32_t ns = 0, ws = 0;
-      for (int s = 0; s < 7; ++s) {
-        if (!pf.fit_w[s]) continue;
-        int64_t preq, cap, fr;
-        if (s < 2) { preq = p.nz[s]; cap = d.alloc[s]; fr = d.nzfree[s]; }
-        else {
-          preq = p.req[s];
-          if (s >= 3 && preq == 0) continue;
-          cap = m.i64[C_ALLOC_CPU + s][d.node];
-          fr = d.free[s];
-        }
-        if (cap == 0) continue;
-        ns += least_requested(fr, preq, cap) * pf.fit_w[s];
-        ws += pf.fit_w[s];
-      }
-      o.fit = ws ? small_div(ns, ws) : 0;
-    }
-    if ((pf.enabled & 0x8u) && !(d.dflags & DF_LA_ZERO)) {
-      bool prod = p.flags & PF_PROD_SCORE;
-      int32_t ns = 0;
-      if (pf.la_w[0]) ns += least_requested(prod ? d.la_pfree[0] : d.la_free[0], p.est[0], d.la_cap[0]) * pf.la_w[0];
-      if (pf.la_w[1]) ns += least_requested(prod ? d.la_pfree[1] : d.la_free[1], p.est[1], d.la_cap[1]) * pf.la_w[1];
-      o.la = small_div(ns, pf.la_wsum);
-    }
-    return total_score(o, pf);
+__device__ __forceinline__ int hash_find(const int32_t* hkey, const int32_t* hval, uint32_t node) {
+  uint32_t h = (node * 2654435761u) & (HASH - 1);
+  for (int probe = 0; probe < HASH; ++probe) {
+    int kk = hkey[h];
+    if (kk == (int)node) return hval[h];
+    if (kk < 0) return -1;
+    h = (h + 1) & (HASH - 1);
   }
-  o = eval_pair<false>(r, p, pf, m);
-  return total_score(o, pf);
+  return -1;
+}
+
+__device__ __forceinline__ const LevelHdr* hdr_ptr(const CommitArgs& a, int r, int k) {
+  return reinterpret_cast<const LevelHdr*>(a.xbase + (size_t)r * a.xblock + (size_t)a.bmax * LCAP * 4) + k;
+}
+__device__ __forceinline__ const uint32_t* list_ptr(const CommitArgs& a, int r, int k) {
+  return reinterpret_cast<const uint32_t*>(a.xbase + (size_t)r * a.xblock) + (size_t)k * LCAP;
 }
 
 __device__ __forceinline__ int wave_max(int v) {
@@ -481,198 +438,290 @@ __device__ __forceinline__ int wave_sum(int v) {
   for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
   return v;
 }
-__device__ __forceinline__ int key_score(uint64_t key) { return (int)(uint32_t)(key >> 32); }
-__device__ __forceinline__ uint32_t key_node(uint64_t key) { return ~(uint32_t)key; }
 
-__global__ void __launch_bounds__(64) commit_kernel(CommitArgs a) {
+// sort n (<= 128) distinct node ids in place, tmp as scratch (one wave)
+__device__ __forceinline__ void wave_rank_sort(uint32_t* v, int n, uint32_t* tmp, int lane) {
+  for (int i = lane; i < n; i += 64) {
+    uint32_t x = v[i];
+    int r = 0;
+    for (int u = 0; u < n; ++u) r += v[u] < x;
+    tmp[r] = x;
+  }
+  WAVE_FENCE();
+  for (int i = lane; i < n; i += 64) v[i] = tmp[i];
+  WAVE_FENCE();
+}
+
+// ST: diagnostic build with s_memtime phase stamps (accumulated per phase, written to a.stamps)
+template <bool ST>
+__global__ void __launch_bounds__(256) commit_kernel(CommitArgs a) {
+  uint64_t st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  uint64_t st_last = ST ? __builtin_amdgcn_s_memtime() : 0;
+#define STAMP(i)                                    \
+  do {                                              \
+    if (ST) {                                       \
+      uint64_t t_ = __builtin_amdgcn_s_memtime();   \
+      st_acc[i] += t_ - st_last;                    \
+      st_last = t_;                                 \
+    }                                               \
+  } while (0)
   extern __shared__ __align__(16) unsigned char cm[];
   const int B = a.npods;
-  const int lane = threadIdx.x;
-  // LDS carve
-  PodVec* pods = reinterpret_cast<PodVec*>(cm);                         // B
-  DRow* drows = reinterpret_cast<DRow*>(pods + B);                      // B (dirty slots)
-  int16_t* dsc = reinterpret_cast<int16_t*>(drows + B);                 // B x B  [pod][slot]
-  uint8_t* dof = reinterpret_cast<uint8_t*>(dsc + B * B);               // B x B  old feasibility
-  int32_t* hkey = reinterpret_cast<int32_t*>(dof + ((B * B + 15) & ~15));  // HASH
-  int32_t* hval = hkey + HASH;                                          // HASH
-  uint32_t* ties = reinterpret_cast<uint32_t*>(hval + HASH);            // CAND_CAP * R + B
-  const int tie_cap = CAND_CAP * a.nranks + B;
-  uint32_t* dties = ties + tie_cap;                                     // B
-  __shared__ int s_nd;
+  const int R = a.nranks;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const uint64_t lt_mask = (1ull << lane) - 1ull;
+  PodVec* pods = reinterpret_cast<PodVec*>(cm);                              // B
+  Row* drows = reinterpret_cast<Row*>(pods + B);                             // B dirty slots
+  int16_t* dsc = reinterpret_cast<int16_t*>(drows + B);                      // [pod][slot] current score
+  int16_t* dso = dsc + B * B;                                                // [pod][slot] batch-start score
+  int32_t* hkey = reinterpret_cast<int32_t*>(
+      (reinterpret_cast<uintptr_t>(dso + B * B) + 15) & ~(uintptr_t)15);     // HASH
+  int32_t* hval = hkey + HASH;                                               // HASH
 
-  for (int i = lane; i < B; i += 64) pods[i] = a.pods[i];
-  for (int i = lane; i < HASH; i += 64) { hkey[i] = -1; hval[i] = -1; }
-  if (lane == 0) s_nd = 0;
-  __syncthreads();
+  __shared__ int32_t sh_score[MAX_RANKS * MAXLEV], sh_count[MAX_RANKS * MAXLEV], sh_dec[MAX_RANKS * MAXLEV];
+  __shared__ uint32_t dnew[MAX_BATCH], tmp[MAX_BATCH];
+  __shared__ uint32_t win[WIN];
+  __shared__ int32_t pre_old[WIN + 1];
+  __shared__ Row orow;                                  // batch-start copy of a freshly dirtied row
+  __shared__ int s_action, s_slot, s_fresh, s_M, s_F;  // wave-0 decision for pod k (0 commit, 1 skip, 2 cut)
+  __shared__ uint32_t s_winner;
+  __shared__ int64_t s_T;
+  __shared__ PlacementDev res[MAX_BATCH];              // placements, written to HBM once at the end
+
+  for (int i = tid; i < B; i += 256) pods[i] = a.pods[i];
+  for (int i = tid; i < HASH; i += 256) { hkey[i] = -1; hval[i] = -1; }
   const MirrorView& m = a.m;
+  const int nhl = R * MAXLEV;                    // header lanes: lane = r*MAXLEV + j
+  // LevelHdrs and seq of HCH pods at a time are staged in LDS (one HBM round trip per chunk)
+  constexpr int HCH = 16;
+  __shared__ int32_t hs_score[HCH][MAX_RANKS * MAXLEV], hs_count[HCH][MAX_RANKS * MAXLEV];
+  __shared__ int32_t hs_nlev[HCH][MAX_RANKS], hs_feas[HCH][MAX_RANKS], hs_next[HCH][MAX_RANKS];
+  __shared__ uint64_t hs_seq[HCH];
+  int nd = 0;
   int committed = B;
-
-  auto lookup = [&](uint32_t node) -> int {
-    uint32_t h = (node * 2654435761u) & (HASH - 1);
-    for (int probe = 0; probe < HASH; ++probe) {
-      int kk = hkey[h];
-      if (kk == (int)node) return hval[h];
-      if (kk < 0) return -1;
-      h = (h + 1) & (HASH - 1);
-    }
-    return -1;
-  };
+  __syncthreads();
 
   for (int k = 0; k < B; ++k) {
-    const int nd = s_nd;
-    const PodVec& pk = pods[k];
-    // ---- dirty nodes: exact current scores for pod k
-    int Md = -1;
-    for (int s = lane; s < nd; s += 64) Md = max(Md, (int)dsc[k * B + s]);
+   if (k % HCH == 0) {
+     for (int e = tid; e < HCH * nhl; e += 256) {
+       int kk = e / nhl, l = e % nhl;
+       if (k + kk < B) {
+         const LevelHdr* h = hdr_ptr(a, l / MAXLEV, k + kk);
+         hs_score[kk][l] = h->score[l % MAXLEV];
+         hs_count[kk][l] = h->count[l % MAXLEV];
+       }
+     }
+     for (int e = tid; e < HCH * R; e += 256) {
+       int kk = e / R, r = e % R;
+       if (k + kk < B) {
+         const LevelHdr* h = hdr_ptr(a, r, k + kk);
+         hs_nlev[kk][r] = h->nlev;
+         hs_feas[kk][r] = h->feasible;
+         hs_next[kk][r] = h->next;
+       }
+     }
+     for (int e = tid; e < HCH; e += 256)
+       if (k + e < B) hs_seq[e] = a.seq[k + e];
+     __syncthreads();
+   }
+   if (wave == 0) do {   // ===================== wave 0: selectHost for pod k =====================
+    const int kc = k % HCH;
+    const int r_l = lane / MAXLEV, j_l = lane % MAXLEV;
+    int hs = lane < nhl ? hs_score[kc][lane] : -1, hc = lane < nhl ? hs_count[kc][lane] : 0;
+    const int feas_l = lane < R ? hs_feas[kc][lane] : 0, next_l = lane < R ? hs_next[kc][lane] : -1;
+    const uint64_t seqk = hs_seq[kc];
+    const bool lvl = lane < nhl && j_l < hs_nlev[kc][r_l < MAX_RANKS ? r_l : 0];
+    if (!lvl) { hs = -1; hc = 0; }
+    if (lane < nhl) { sh_score[lane] = hs; sh_count[lane] = hc; sh_dec[lane] = 0; }
+    WAVE_FENCE();
+    STAMP(0);
+    const bool forced = (k == 0 && a.forced_node >= 0);
+    // ---- dirty rows: batch-start / current scores of pod k, listed-level decrements
+    int Md = -1, Fd = 0;
+    for (int s = lane; s < nd; s += 64) {
+      int sc = dsc[k * B + s], so = dso[k * B + s];
+      Md = max(Md, sc);
+      Fd += (sc >= 0 ? 1 : 0) - (so >= 0 ? 1 : 0);
+      if (so >= 0) {
+        int base = (int)(drows[s].node / a.shard_size) * MAXLEV;
+        for (int j = 0; j < MAXLEV; ++j)
+          if (sh_score[base + j] == so) { atomicAdd(&sh_dec[base + j], 1); break; }
+      }
+    }
     Md = wave_max(Md);
-    // ---- clean heads of every shard's list
-    int Mnd = -1;
-    int first_r[8];
-    bool valid = true;
-    for (int r = 0; r < a.nranks; ++r) {
-      const CandHdr h = a.hdrs[(size_t)r * a.hdr_stride + k];
-      const uint64_t* L = a.lists + ((size_t)r * a.list_stride + (size_t)k) * CAND_CAP;
-      int first = h.count;
-      for (int c = 0; c < h.count; c += 64) {
-        int i = c + lane;
-        bool clean = false;
-        if (i < h.count) clean = lookup(key_node(L[i])) < 0;
-        uint64_t bal = __ballot(clean);
-        if (bal) { first = c + __ffsll((long long)bal) - 1; break; }
-      }
-      first_r[r] = first;
-      if (first < h.count) Mnd = max(Mnd, key_score(L[first]));
-    }
-    int M = max(Mnd, Md);
-    if (a.forced_node >= 0 && k == 0) {
-      // pod 0 resolved by the exact full-row path
-    } else {
-      for (int r = 0; r < a.nranks; ++r) {
-        const CandHdr h = a.hdrs[(size_t)r * a.hdr_stride + k];
-        if (!h.complete && M < h.theta) valid = false;
-      }
-      if (!valid) { committed = k; break; }
-    }
-    // feasible count: snapshot count, corrected for re-scored nodes
-    int F = 0;
-    for (int r = 0; r < a.nranks; ++r) F += a.hdrs[(size_t)r * a.hdr_stride + k].feasible;
-    {
-      int d = 0;
-      for (int s = lane; s < nd; s += 64) d += (dsc[k * B + s] >= 0 ? 1 : 0) - (int)dof[k * B + s];
-      F += wave_sum(d);
-    }
-    int64_t T = 0;
-    uint32_t winner = 0xffffffffu;
-    if (a.forced_node >= 0 && k == 0) {
-      winner = (uint32_t)a.forced_node;
+    Fd = wave_sum(Fd);
+    WAVE_FENCE();
+    STAMP(1);
+    const int clean = lvl ? hc - sh_dec[lane] : 0;
+    int M = max(wave_max(clean > 0 ? hs : -1), Md);
+    int F = Fd + wave_sum(lane < R ? feas_l : 0);
+    if (forced) {
       M = a.forced_score;
-      T = a.forced_ties;
       F = a.forced_feasible;
-    } else if (M >= 0) {
-      // ---- clean ties at level M, shard order == node order
-      int nt = 0;
-      for (int r = 0; r < a.nranks; ++r) {
-        const CandHdr h = a.hdrs[(size_t)r * a.hdr_stride + k];
-        const uint64_t* L = a.lists + ((size_t)r * a.list_stride + (size_t)k) * CAND_CAP;
-        int first = first_r[r];
-        if (first >= h.count || key_score(L[first]) != M) continue;
-        for (int c = first; c < h.count; c += 64) {
-          int i = c + lane;
-          bool in = false, clean = false;
-          uint32_t node = 0;
-          if (i < h.count) {
-            uint64_t key = L[i];
-            in = key_score(key) == M;
-            node = key_node(key);
-            clean = in && lookup(node) < 0;
-          }
-          uint64_t bal = __ballot(clean);
-          int pos = __popcll(bal & ((1ull << lane) - 1ull));
-          if (clean && nt + pos < tie_cap) ties[nt + pos] = node;
-          nt += __popcll(bal);
-          uint64_t inb = __ballot(in);
-          uint64_t valid_lanes = __ballot(i < h.count);
-          if (inb != valid_lanes) break;
-        }
-      }
-      // ---- dirty ties
-      int ndt = 0;
+    } else if (__ballot(lane < R && M <= next_l)) {
+      if (lane == 0) s_action = 2;   // a shard may hold unlisted nodes at M: cut, the host re-evaluates from k
+      break;
+    }
+    if (M < 0) {       // FitError: no feasible node anywhere, nothing assumed
+      if (lane == 0) { res[k] = PlacementDev{-1, (uint32_t)F, 0, 0, 0}; s_action = 1; }
+      break;
+    }
+    uint32_t winner = 0xffffffffu;
+    int64_t T = 0;
+    STAMP(2);
+    if (forced) {
+      winner = (uint32_t)a.forced_node;
+      T = a.forced_ties;
+    } else {
+      // ---- tie set at M: clean listed nodes + dirty rows now at M ("dnew") - dirty rows listed at M ("old")
+      const int cm_lane = (lvl && hs == M) ? clean : 0;
+      int ndn = 0;
       for (int s0 = 0; s0 < nd; s0 += 64) {
         int s = s0 + lane;
-        bool in = s < nd && dsc[k * B + s] == M;
-        uint64_t bal = __ballot(in);
-        int pos = __popcll(bal & ((1ull << lane) - 1ull));
-        if (in) dties[ndt + pos] = drows[s].node;
-        ndt += __popcll(bal);
+        bool isn = s < nd && dsc[k * B + s] == M;
+        uint64_t bn = __ballot(isn);
+        if (isn) dnew[ndn + __popcll(bn & lt_mask)] = drows[s].node;
+        ndn += __popcll(bn);
       }
-      __syncthreads();
-      T = nt + ndt;
-      int64_t jstar = tiebreak_position(a.seed, a.seq[k], T);   // uniform across lanes
-      // ---- j*-th in node order of (clean ties, sorted) U (dirty ties, unsorted)
-      // clean tie i: position = i + 1 + #dirty ties with smaller node
-      for (int i0 = 0; i0 < nt; i0 += 64) {
-        int i = i0 + lane;
-        bool hit = false;
-        uint32_t node = 0;
-        if (i < nt) {
-          node = ties[i];
-          int less = 0;
-          for (int d = 0; d < ndt; ++d) less += dties[d] < node;
-          hit = (int64_t)(i + 1 + less) == jstar;
+      WAVE_FENCE();
+      T = (int64_t)wave_sum(cm_lane) + ndn;
+      int64_t jp = tiebreak_position(a.seed, seqk, T);
+      if (ndn > 1) wave_rank_sort(dnew, ndn, tmp, lane);
+      STAMP(3);
+      // per shard: clean ties + dirty ties (lane r < R), owning shard r* by prefix
+      int here = 0;
+      {
+        int c = 0;
+        for (int j = 0; j < MAXLEV; ++j) c += __shfl(cm_lane, (lane < R ? lane : 0) * MAXLEV + j);
+        if (lane < R) {
+          uint32_t sb = (uint32_t)lane * a.shard_size, se = sb + a.shard_size;
+          int dn = 0;
+          for (int u = 0; u < ndn; ++u) dn += dnew[u] >= sb && dnew[u] < se;
+          here = c + dn;
         }
-        uint64_t bal = __ballot(hit);
-        if (bal) { winner = __shfl(node, __ffsll((long long)bal) - 1); break; }
       }
-      if (winner == 0xffffffffu) {
-        // dirty tie d: position = #clean ties with smaller node + #dirty ties with smaller node + 1
-        for (int d0 = 0; d0 < ndt; d0 += 64) {
-          int d = d0 + lane;
-          bool hit = false;
-          uint32_t node = 0;
-          if (d < ndt) {
-            node = dties[d];
-            int lo = 0, hi = nt;                      // lower_bound in the sorted clean ties
-            while (lo < hi) { int mid = (lo + hi) >> 1; if (ties[mid] < node) lo = mid + 1; else hi = mid; }
-            int less = lo;
-            for (int e = 0; e < ndt; ++e) less += dties[e] < node;
-            hit = (int64_t)(less + 1) == jstar;
+      int incl = here;
+      for (int off = 1; off < 64; off <<= 1) {
+        int v = __shfl_up(incl, off);
+        if (lane >= off) incl += v;
+      }
+      uint64_t hit = __ballot(lane < R && incl >= jp);
+      const int rstar = hit ? (__ffsll((long long)hit) - 1) : (R - 1);
+      jp -= __shfl(incl - here, rstar);
+      // level-M segment of r*'s list
+      int off = 0, len = 0;
+      for (int j = 0; j < MAXLEV; ++j) {
+        int sc = sh_score[rstar * MAXLEV + j];
+        if (sc < 0) break;
+        if (sc == M) { len = sh_count[rstar * MAXLEV + j]; break; }
+        off += sh_count[rstar * MAXLEV + j];
+      }
+      const uint32_t sb = (uint32_t)rstar * a.shard_size, se = sb + a.shard_size;
+      int nn_lo = 0;
+      while (nn_lo < ndn && dnew[nn_lo] < sb) ++nn_lo;
+      int nn_hi = nn_lo;
+      while (nn_hi < ndn && dnew[nn_hi] < se) ++nn_hi;
+      // dirty rows of r* listed at M (batch-start score M)
+      int ndo_r = 0;
+      for (int s = lane; s < nd; s += 64) {
+        uint32_t node = drows[s].node;
+        ndo_r += (dso[k * B + s] == M && node >= sb && node < se) ? 1 : 0;
+      }
+      ndo_r = wave_sum(ndo_r);
+      const int lo = (int)max<int64_t>(0, jp - 2 - (nn_hi - nn_lo));
+      const int hi = (int)min<int64_t>(len - 1, jp - 1 + ndo_r);
+      const int W = hi - lo + 1;
+      // ---- the jp-th node of (listed level-M nodes of r* - old) U dnew, node order, over window L[lo..hi]
+      const uint32_t* L = list_ptr(a, rstar, k) + off;
+      uint32_t cand = 0xffffffffu;
+      if (len > 0) {
+        for (int i = lane; i < W; i += 64) win[i] = L[lo + i];
+        WAVE_FENCE();
+        STAMP(4);
+        // old rows before the window, then a running count over the window (membership via the hash)
+        int base_old = 0;
+        for (int s = lane; s < nd; s += 64) {
+          uint32_t node = drows[s].node;
+          base_old += (dso[k * B + s] == M && node >= sb && node < win[0]) ? 1 : 0;
+        }
+        base_old = wave_sum(base_old);
+        int running = base_old;
+        for (int i0 = 0; i0 < W; i0 += 64) {
+          int i = i0 + lane;
+          uint32_t x = i < W ? win[i] : 0xffffffffu;
+          bool isold = false;
+          if (i < W) {
+            int sl = hash_find(hkey, hval, x);
+            isold = sl >= 0 && dso[k * B + sl] == M;
           }
-          uint64_t bal = __ballot(hit);
-          if (bal) { winner = __shfl(node, __ffsll((long long)bal) - 1); break; }
+          uint64_t bo = __ballot(isold);
+          int older = running + __popcll(bo & lt_mask);
+          if (i < W) {
+            pre_old[i] = older;
+            int newer = 0;
+            for (int u = nn_lo; u < nn_hi; ++u) newer += dnew[u] < x;
+            if (!isold && (int64_t)(lo + i - older + newer + 1) == jp) cand = x;
+          }
+          running += __popcll(bo);
         }
+        if (lane == 0) pre_old[W] = running;
+        WAVE_FENCE();
       }
-      __syncthreads();
+      for (int u0 = nn_lo + lane; u0 < nn_hi; u0 += 64) {
+        uint32_t n = dnew[u0];
+        int64_t ltn = -1;   // #listed level-M nodes < n, when it can decide position jp
+        int older = 0;
+        if (len == 0) {
+          ltn = 0;
+        } else {
+          int p = 0, q = W;      // lower_bound(win, n)
+          while (p < q) { int mid = (p + q) >> 1; if (win[mid] < n) p = mid + 1; else q = mid; }
+          if (p == 0) ltn = (lo == 0) ? 0 : -1;
+          else if (p == W) ltn = (hi == len - 1) ? len : -1;
+          else ltn = lo + p;
+          older = pre_old[p];
+        }
+        if (ltn >= 0 && ltn - older + (u0 - nn_lo) + 1 == jp) cand = n;
+      }
+      uint64_t got = __ballot(cand != 0xffffffffu);
+      if (!got) { if (lane == 0) s_action = 2; break; }   // unreachable for a valid max: cut, exact re-run
+      winner = __shfl(cand, __ffsll((long long)got) - 1);
     }
-    PlacementDev out;
-    out.node = (M >= 0) ? (int32_t)winner : -1;
-    out.score = M;
-    out.ties = (uint32_t)T;
-    out.feasible = (uint32_t)F;
-    if (M < 0) {
-      if (lane == 0) a.out[k] = out;
-      continue;
-    }
-    // ---- assume + Reserve on the winner: update its row (LDS copy), re-score later pods on it
-    int slot = lookup(winner);
-    bool fresh = slot < 0;
+    STAMP(5);
+    // ---- slot of the winner in the dirty set (batch-start row fetched from HBM when fresh)
+    int slot = hash_find(hkey, hval, winner);
+    const bool fresh = slot < 0;
     if (fresh) {
       slot = nd;
       if (lane == 0) {
-        drow_load(m, winner, drows[slot]);
         uint32_t h = (winner * 2654435761u) & (HASH - 1);
         while (hkey[h] >= 0) h = (h + 1) & (HASH - 1);
-        hkey[h] = (int)winner;
+        hkey[h] = (int32_t)winner;
         hval[h] = slot;
-        s_nd = nd + 1;
       }
-      __syncthreads();
-      // old (batch-start) feasibility of the winner for every later pod
-      for (int q = k + 1 + lane; q < B; q += 64)
-        dof[q * B + slot] = drow_score(drows[slot], pods[q], a.pf, m) >= 0 ? 1 : 0;
-      __syncthreads();
+      ++nd;
+      int64_t* dw = reinterpret_cast<int64_t*>(&orow);
+      if (lane < ROW_I64) dw[lane] = m.c64(kRowCol[lane])[winner];
+      if (lane == ROW_I64) orow.free_pods = m.c32(C_FREE_PODS)[winner];
+      if (lane == ROW_I64 + 1) orow.dflags = (uint32_t)m.c32(C_DFLAGS)[winner];
+      if (lane == ROW_I64 + 2) { orow.node = winner; orow.pad = 0; }
     }
     if (lane == 0) {
-      DRow& d = drows[slot];
+      s_action = 0; s_slot = slot; s_fresh = fresh; s_winner = winner; s_M = M; s_F = F; s_T = T;
+    }
+    STAMP(6);
+   } while (0);
+    __syncthreads();
+    // ===================== all waves: assume + Reserve, re-score later pods =====================
+    const int action = s_action;
+    if (action == 2) { committed = k; break; }
+    if (action == 1) continue;
+    const int slot = s_slot;
+    const bool fresh = s_fresh;
+    Row& d = drows[slot];
+    if (tid == 0) {
+      if (fresh) d = orow;
+      const PodVec& pk = pods[k];
       for (int s = 0; s < 7; ++s) d.free[s] -= pk.req[s];
       d.nzfree[0] -= pk.nz[0];
       d.nzfree[1] -= pk.nz[1];
@@ -683,28 +732,40 @@ __global__ void __launch_bounds__(64) commit_kernel(CommitArgs a) {
         d.la_pfree[0] -= pk.est[0];
         d.la_pfree[1] -= pk.est[1];
       }
-      a.out[k] = out;
+      const bool forced = (k == 0 && a.forced_node >= 0);
+      res[k] = PlacementDev{(int32_t)s_winner, (uint32_t)s_F, (int64_t)s_M, (uint32_t)s_T, forced ? 1u : 0u};
     }
     __syncthreads();
-    for (int q = k + 1 + lane; q < B; q += 64) dsc[q * B + slot] = (int16_t)drow_score(drows[slot], pods[q], a.pf, m);
+    // batch-start scores (fresh rows) on threads 0..127, current scores on threads 128..255
+    if (tid < 128) {
+      int q = k + 1 + tid;
+      if (fresh && q < B) dso[q * B + slot] = (int16_t)row_score(orow, pods[q], a.pf, m);
+    } else {
+      int q = k + 1 + (tid - 128);
+      if (q < B) dsc[q * B + slot] = (int16_t)row_score(d, pods[q], a.pf, m);
+    }
     __syncthreads();
+    if (tid == 0) STAMP(7);
   }
-  // write back dirty rows
+  // write back dirty rows (slots are dense: count them from the hash)
+  __shared__ int s_nd;
+  if (tid == 0) {
+    int n = 0;
+    for (int i = 0; i < HASH; ++i) n += hkey[i] >= 0;
+    s_nd = n;
+  }
   __syncthreads();
-  const int nd = s_nd;
-  for (int s = lane; s < nd; s += 64) {
-    const DRow& d = drows[s];
-    uint32_t i = d.node;
-    for (int c = 0; c < 7; ++c) m.i64[C_FREE_CPU + c][i] = d.free[c];
-    m.i64[C_NZFREE_CPU][i] = d.nzfree[0];
-    m.i64[C_NZFREE_MEM][i] = d.nzfree[1];
-    m.i64[C_LA_FREE_CPU][i] = d.la_free[0];
-    m.i64[C_LA_FREE_MEM][i] = d.la_free[1];
-    m.i64[C_LA_PFREE_CPU][i] = d.la_pfree[0];
-    m.i64[C_LA_PFREE_MEM][i] = d.la_pfree[1];
-    m.i32[C_FREE_PODS][i] = d.free_pods;
+  nd = s_nd;
+  for (int e = tid; e < nd * ROW_I64; e += 256) {
+    int s = e / ROW_I64, j = e % ROW_I64;
+    if (row_word_mutable(j)) m.c64(kRowCol[j])[drows[s].node] = reinterpret_cast<const int64_t*>(&drows[s])[j];
   }
-  if (lane == 0) *a.committed = committed;
+  for (int s = tid; s < nd; s += 256) m.c32(C_FREE_PODS)[drows[s].node] = drows[s].free_pods;
+  for (int i = tid; i < committed; i += 256) a.out[i] = res[i];
+  if (tid == 0) *a.committed = committed;
+  if (ST && tid == 0)
+    for (int i = 0; i < 8; ++i) a.stamps[i] += st_acc[i];
+#undef STAMP
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -720,7 +781,6 @@ __global__ void __launch_bounds__(1024) row_stats_kernel(const int16_t* __restri
     if (v > mx) { mx = v; cnt = 1; }
     else if (v == mx && v >= 0) ++cnt;
   }
-  // wave reduce (max, count at max, feasible)
   for (int off = 32; off > 0; off >>= 1) {
     int om = __shfl_xor(mx, off), oc = __shfl_xor(cnt, off), of = __shfl_xor(feas, off);
     if (om > mx) { mx = om; cnt = oc; } else if (om == mx) cnt += oc;
@@ -777,8 +837,8 @@ __global__ void __launch_bounds__(256) scatter_rows_kernel(MirrorView m, const u
   if (r >= nrows) return;
   uint32_t i = idx[r];
   const int64_t* src = rows + (size_t)r * ROW_WORDS;
-  for (int c = 0; c < NUM_I64_COLS; ++c) m.i64[c][i] = src[c];
-  for (int c = 0; c < NUM_I32_COLS; ++c) m.i32[c][i] = (int32_t)src[NUM_I64_COLS + c];
+  for (int c = 0; c < NUM_I64_COLS; ++c) m.c64(c)[i] = src[c];
+  for (int c = 0; c < NUM_I32_COLS; ++c) m.c32(c)[i] = (int32_t)src[NUM_I64_COLS + c];
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -794,9 +854,10 @@ hipError_t launch_node_prep(const MirrorView& m, uint32_t n0, uint32_t n1, int64
 hipError_t launch_eval(const MirrorView& m, const PodVec* pods, int npods, const Profile& pf, uint32_t n0, uint32_t n1,
                        int16_t* S, uint32_t ld, int prod_cols, hipStream_t st) {
   uint32_t len = n1 - n0;
-  uint32_t grid = (len + 256 * NPT - 1) / (256 * NPT);
-  if (grid == 0) return hipSuccess;
-  hipLaunchKernelGGL(eval_kernel, dim3(grid), dim3(256), 0, st, m, pods, npods, pf, n0, n1, S, ld, prod_cols);
+  uint32_t gx = (len + 255) / 256;
+  uint32_t gy = (npods + PODS_PER_BLOCK - 1) / PODS_PER_BLOCK;
+  if (gx == 0 || gy == 0) return hipSuccess;
+  hipLaunchKernelGGL(eval_kernel, dim3(gx, gy), dim3(256), 0, st, m, pods, npods, pf, n0, n1, S, ld, prod_cols);
   return hipGetLastError();
 }
 
@@ -808,28 +869,30 @@ hipError_t launch_eval_full(const MirrorView& m, const PodVec* pods, int npods, 
   return hipGetLastError();
 }
 
-size_t cand_smem_bytes(int max_score) {
-  return (size_t)(((max_score + 1) + 3) & ~3) * 4 + (size_t)CAND_CAP * 8;
+static size_t cand_smem_bytes(int max_score) {
+  size_t nb = (size_t)max_score + 1;
+  return nb * 4 * 4 + nb * 4 + ((nb + 15) & ~(size_t)15);
 }
 
 hipError_t launch_cand(const int16_t* S, uint32_t ld, uint32_t len, uint32_t n0, int npods, int max_score,
-                       uint64_t* lists, CandHdr* hdrs, hipStream_t st) {
-  size_t smem = cand_smem_bytes(max_score);
-  hipLaunchKernelGGL(cand_kernel, dim3(npods), dim3(CAND_THREADS), smem, st, S, ld, len, n0, max_score, lists, hdrs);
+                       uint32_t* lists, LevelHdr* hdrs, hipStream_t st) {
+  hipLaunchKernelGGL(cand_kernel, dim3(npods), dim3(CAND_THREADS), cand_smem_bytes(max_score), st, S, ld, len, n0,
+                     max_score, lists, hdrs);
   return hipGetLastError();
 }
 
-size_t commit_smem_bytes(int B, int nranks) {
-  size_t b = (size_t)B * sizeof(PodVec) + (size_t)B * sizeof(DRow) + (size_t)B * B * 2;
-  b += (size_t)((B * B + 15) & ~15);
-  b += (size_t)HASH * 8;
-  b += (size_t)(CAND_CAP * nranks + B) * 4 + (size_t)B * 4;
-  return (b + 15) & ~(size_t)15;
+size_t commit_smem_bytes(int B) {
+  size_t b = (size_t)B * sizeof(PodVec) + (size_t)B * sizeof(Row) + (size_t)B * B * 2 * 2;
+  b = (b + 15) & ~(size_t)15;
+  b += (size_t)HASH * 8 + 16;
+  return b;
 }
 
 hipError_t launch_commit(const CommitArgs& a, hipStream_t st) {
-  size_t smem = commit_smem_bytes(a.npods, a.nranks);
-  hipLaunchKernelGGL(commit_kernel, dim3(1), dim3(64), smem, st, a);
+  if (a.stamps)
+    hipLaunchKernelGGL(commit_kernel<true>, dim3(1), dim3(256), commit_smem_bytes(a.npods), st, a);
+  else
+    hipLaunchKernelGGL(commit_kernel<false>, dim3(1), dim3(256), commit_smem_bytes(a.npods), st, a);
   return hipGetLastError();
 }
 
@@ -852,12 +915,14 @@ hipError_t launch_scatter_rows(const MirrorView& m, const uint32_t* idx, const i
 }
 
 hipError_t set_kernel_attributes() {
-  hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(commit_kernel),
-                                     hipFuncAttributeMaxDynamicSharedMemorySize,
-                                     (int)commit_smem_bytes(MAX_BATCH, MAX_RANKS));
+  hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(commit_kernel<false>),
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)commit_smem_bytes(MAX_BATCH));
+  if (e != hipSuccess) return e;
+  e = hipFuncSetAttribute(reinterpret_cast<const void*>(commit_kernel<true>),
+                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)commit_smem_bytes(MAX_BATCH));
   if (e != hipSuccess) return e;
   return hipFuncSetAttribute(reinterpret_cast<const void*>(cand_kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
-                             (int)cand_smem_bytes(8191));
+                             (int)cand_smem_bytes(MAX_SCORE_LIMIT));
 }
 
 }  // namespace gs

@@ -88,23 +88,6 @@ struct Profile {
   uint32_t fit_scalar_w_mask; // slots 2..6 with non-zero weight
 };
 
-// candidate list entry key: (score << 32) | ~node — descending key order = score desc, node asc
-static inline
-#ifdef __HIPCC__
-__host__ __device__
-#endif
-uint64_t cand_key(int32_t score, uint32_t node) {
-  return ((uint64_t)(uint32_t)score << 32) | (uint64_t)(~node);
-}
-
-// per (pod, shard) candidate list header
-struct CandHdr {
-  int32_t count;      // entries written (sorted by key desc)
-  int32_t theta;      // every node with score >= theta is listed
-  int32_t complete;   // every feasible node is listed (theta == 0)
-  int32_t feasible;   // feasible nodes of the shard for this pod
-};
-
 // per (pod, shard) full-row summary for the exact slow path
 struct RowStat {
   int32_t max_score;  // -1 if nothing feasible
