@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define GS_ABI_VERSION 1u
+#define GS_ABI_VERSION 2u
 
 /* ---- resource slots (corev1.ResourceName restricted to the hot-path set) ---- */
 enum gs_resource {
@@ -61,6 +61,32 @@ enum gs_aggregation_type {
 #define GS_USAGE_MEMORY 0x2u
 #define GS_USAGE_OTHER 0x80u /* some key outside {cpu,memory}: only len(ResourceList) > 0 observes it */
 
+/* ---- NodeNUMAResource vocabulary (apis/extension/numa_aware.go, pkg/scheduler/apis/config/types.go:103-150) ---- */
+#define GS_MAX_NUMA 4            /* NUMA nodes (NodeResourceTopology zones) per node on the device path */
+#define GS_MAX_CPUS 256          /* logical CPUs per node: CPUDetails ids 0..255 */
+#define GS_CPU_WORDS 4           /* uint64 words of a cpuset.CPUSet over GS_MAX_CPUS */
+
+enum gs_qos_class { GS_QOS_NONE = 0, GS_QOS_LSE = 1, GS_QOS_LSR = 2, GS_QOS_LS = 3, GS_QOS_BE = 4, GS_QOS_SYSTEM = 5 };
+enum gs_cpu_bind_policy {          /* schedulingconfig.CPUBindPolicy; UNSET = "" */
+  GS_CPU_BIND_UNSET = 0, GS_CPU_BIND_DEFAULT = 1, GS_CPU_BIND_FULL_PCPUS = 2, GS_CPU_BIND_SPREAD_BY_PCPUS = 3,
+  GS_CPU_BIND_CONSTRAINED_BURST = 4
+};
+enum gs_cpu_exclusive_policy {     /* schedulingconfig.CPUExclusivePolicy; NONE = "" or "None" */
+  GS_CPU_EXCLUSIVE_NONE = 0, GS_CPU_EXCLUSIVE_PCPU_LEVEL = 1, GS_CPU_EXCLUSIVE_NUMA_NODE_LEVEL = 2
+};
+enum gs_node_cpu_bind_policy {     /* extension.NodeCPUBindPolicy after GetNodeCPUBindPolicy (numa_aware.go:314-325) */
+  GS_NODE_CPU_BIND_NONE = 0, GS_NODE_CPU_BIND_FULL_PCPUS_ONLY = 1, GS_NODE_CPU_BIND_SPREAD_BY_PCPUS = 2
+};
+enum gs_numa_topology_policy {     /* extension.NUMATopologyPolicy; NONE = "" */
+  GS_NUMA_POLICY_NONE = 0, GS_NUMA_POLICY_BEST_EFFORT = 1, GS_NUMA_POLICY_RESTRICTED = 2,
+  GS_NUMA_POLICY_SINGLE_NUMA_NODE = 3
+};
+enum gs_numa_allocate_strategy {   /* extension.NUMAAllocateStrategy; UNSET = no node label (args default) */
+  GS_NUMA_ALLOC_UNSET = 0, GS_NUMA_ALLOC_MOST_ALLOCATED = 1, GS_NUMA_ALLOC_LEAST_ALLOCATED = 2,
+  GS_NUMA_ALLOC_DISTRIBUTE_EVENLY = 3
+};
+enum gs_scoring_type { GS_SCORING_LEAST_ALLOCATED = 0, GS_SCORING_MOST_ALLOCATED = 1 };
+
 /* ---- pod (decoded by the caller from corev1.Pod) ---- */
 #define GS_POD_DAEMONSET 0x1u  /* loadaware/helper.go:189-196 isDaemonSetPod */
 #define GS_POD_TERMINATED 0x2u /* pkg/util IsPodTerminated: podAssignCache.assign skips it */
@@ -74,7 +100,12 @@ typedef struct gs_pod {
   uint32_t request_mask;           /* bit r: requests holds key r (Fit: len(podRequest.ScalarResources) > 0) */
   int32_t priority_class;          /* gs_priority_class */
   uint32_t flags;                  /* GS_POD_* */
-  uint32_t pad0;
+  int32_t qos_class;               /* gs_qos_class: extension.GetPodQoSClassRaw (label koordinator.sh/qosClass) */
+  /* annotation scheduling.koordinator.sh/resource-spec (apis/extension/numa_aware.go:190-245), decoded */
+  int32_t required_cpu_bind_policy;       /* gs_cpu_bind_policy: ResourceSpec.RequiredCPUBindPolicy */
+  int32_t preferred_cpu_bind_policy;      /* ResourceSpec.PreferredCPUBindPolicy */
+  int32_t preferred_cpu_exclusive_policy; /* gs_cpu_exclusive_policy: ResourceSpec.PreferredCPUExclusivePolicy */
+  int32_t pad0;
 } gs_pod;
 
 /* ---- node snapshot row (NodeInfo + node object annotations, decoded by the caller) ---- */
@@ -99,6 +130,48 @@ typedef struct gs_node {
   int32_t custom_agg_type;           /* .AggregatedUsage.UsageAggregationType (GS_AGG_NONE = "") */
   int64_t custom_agg_duration_ns;    /* .AggregatedUsage.UsageAggregatedDuration (0 = nil/0) */
 } gs_node;
+
+/* ---- NodeNUMAResource topology (TopologyOptions, nodenumaresource/topology_options.go:40-50), decoded ---- */
+/* CPUTopology (cpu_topology.go:25-31) as reported in the NRT annotation: one entry per logical CPU. Many nodes
+ * share one hardware shape, so topologies are registered once (gs_topology_register) and referenced by id. */
+typedef struct gs_cpu_topology {
+  int32_t num_cpus;                  /* CPUDetails holds cpu ids 0..num_cpus-1 (<= GS_MAX_CPUS) */
+  int32_t pad0;
+  int32_t core_id[GS_MAX_CPUS];      /* CPUInfo.CoreID (socket<<16 | core, CPUTopologyBuilder.AddCPUInfo) */
+  uint8_t socket_id[GS_MAX_CPUS];    /* CPUInfo.SocketID */
+  uint8_t node_id[GS_MAX_CPUS];      /* CPUInfo.NodeID (NUMA node) */
+} gs_cpu_topology;
+
+typedef struct gs_numa_zone {        /* NUMANodeResource (topology_options.go:52-55) */
+  int32_t node_id;                   /* NUMA node id (< 64, bitmask.BitMask) */
+  uint32_t mask;                     /* GS_USAGE_CPU | GS_USAGE_MEMORY: keys present in Resources */
+  int64_t cpu_milli;
+  int64_t memory;
+} gs_numa_zone;
+
+typedef struct gs_node_numa {
+  int32_t has_options;               /* TopologyOptionsManager holds options for the node (an NRT was seen) */
+  int32_t topology;                  /* gs_topology_register id; -1 = empty CPUTopology (IsValid() false) */
+  int32_t max_ref_count;             /* TopologyOptions.MaxRefCount */
+  int32_t node_cpu_bind_policy;      /* gs_node_cpu_bind_policy: GetNodeCPUBindPolicy(labels, options.Policy) */
+  int32_t numa_topology_policy;      /* gs_numa_topology_policy: getNUMATopologyPolicy (nodenumaresource/util.go:52-58) */
+  int32_t numa_allocate_strategy;    /* gs_numa_allocate_strategy: label node.koordinator.sh/numa-allocate-strategy */
+  double cpu_amplification_ratio;    /* options.AmplificationRatios[cpu] after amplifyNUMANodeResources (<= 1: none) */
+  double node_cpu_amplification_ratio; /* GetNodeResourceAmplificationRatio(node.Annotations, cpu); -1 = unset */
+  int32_t node_amplification_invalid;  /* that annotation fails to parse (filterAmplifiedCPUs error) */
+  int32_t num_zones;                 /* len(NUMANodeResources) <= GS_MAX_NUMA */
+  gs_numa_zone zones[GS_MAX_NUMA];   /* NUMANodeResources after amplifyNUMANodeResources, sorted by node id */
+  uint64_t reserved_cpus[GS_CPU_WORDS]; /* TopologyOptions.ReservedCPUs */
+} gs_node_numa;
+
+/* PodAllocation (nodenumaresource/node_allocation.go:40-47): what resourceManager.Update records. */
+typedef struct gs_pod_allocation {
+  uint64_t uid;
+  uint64_t cpuset[GS_CPU_WORDS];     /* CPUSet */
+  int32_t cpu_exclusive_policy;      /* gs_cpu_exclusive_policy */
+  int32_t num_numa;                  /* len(NUMANodeResources) <= GS_MAX_NUMA */
+  gs_numa_zone numa[GS_MAX_NUMA];    /* NUMANodeResources (node id + allocated cpu/memory) */
+} gs_pod_allocation;
 
 /* ---- NodeMetric (apis/slo/v1alpha1/nodemetric_types.go:38-137), decoded ---- */
 typedef struct gs_usage {
@@ -165,12 +238,23 @@ typedef struct gs_fit_args {
   int64_t resource_weights[GS_NUM_RES];        /* ScoringStrategy.Resources weights per slot (0 = not listed) */
 } gs_fit_args;
 
+/* NodeNUMAResourceArgs (pkg/scheduler/apis/config/types.go:103-114; v1beta2 defaults defaults.go:101-136) */
+typedef struct gs_numa_args {
+  int32_t default_cpu_bind_policy;             /* DefaultCPUBindPolicy (default FullPCPUs) */
+  int32_t scoring_type;                        /* ScoringStrategy.Type (gs_scoring_type) */
+  int32_t numa_scoring_type;                   /* NUMAScoringStrategy.Type; its Resources are NOT used (scoring.go:37-52) */
+  int32_t pad0;
+  int64_t resource_weights[GS_NUM_RES];        /* ScoringStrategy.Resources weights per slot (0 = not listed) */
+} gs_numa_args;
+
 /* plugin ids / enabled-plugin bits */
-enum gs_plugin { GS_PLUGIN_FIT = 0, GS_PLUGIN_LOADAWARE = 1, GS_NUM_PLUGINS = 2 };
+enum gs_plugin { GS_PLUGIN_FIT = 0, GS_PLUGIN_LOADAWARE = 1, GS_PLUGIN_NUMA = 2, GS_NUM_PLUGINS = 3 };
 #define GS_ENABLE_FIT_FILTER 0x1u
 #define GS_ENABLE_FIT_SCORE 0x2u
 #define GS_ENABLE_LA_FILTER 0x4u
 #define GS_ENABLE_LA_SCORE 0x8u
+#define GS_ENABLE_NUMA_FILTER 0x10u
+#define GS_ENABLE_NUMA_SCORE 0x20u
 
 typedef struct gs_config {
   uint32_t abi_version;                /* GS_ABI_VERSION */
@@ -180,6 +264,7 @@ typedef struct gs_config {
   int64_t plugin_weights[GS_NUM_PLUGINS]; /* profile score weights (framework multiplies, runtime/framework.go) */
   gs_loadaware_args loadaware;
   gs_fit_args fit;
+  gs_numa_args numa;
   uint64_t seed;                       /* tie-break stream seed (selectHost) */
   uint32_t batch_size;                 /* pods per device pass (0 = default 128) */
   uint32_t cand_cap;                   /* candidate-list capacity per pod and shard (0 = default 256) */
@@ -193,6 +278,23 @@ typedef struct gs_config {
 #define GS_FAIL_FIT_EPHEMERAL 0x08u
 #define GS_FAIL_FIT_SCALAR 0x10u
 #define GS_FAIL_LOADAWARE 0x20u     /* "node(s) ... usage exceed threshold" (load_aware.go:45-46) */
+/* NodeNUMAResource: the first failing check of the plugin, as a 4-bit reason at GS_FAIL_NUMA_SHIFT */
+#define GS_FAIL_NUMA_SHIFT 6
+#define GS_FAIL_NUMA_MASK 0x3C0u
+enum gs_numa_reason {
+  GS_NUMA_OK = 0,
+  GS_NUMA_INVALID_REQUESTED_CPUS = 1,   /* ErrInvalidRequestedCPUs (PreFilter or requestCPUBind, util.go:105-122) */
+  GS_NUMA_INVALID_AMP_RATIO = 2,        /* ErrInvalidCPUAmplificationRatio (plugin.go:345-347) */
+  GS_NUMA_AVAILABLE_CPUS_ERROR = 3,     /* GetAvailableCPUs error in filterAmplifiedCPUs (plugin.go:357-360) */
+  GS_NUMA_INSUFFICIENT_AMP_CPU = 4,     /* ErrInsufficientAmplifiedCPU (plugin.go:368-370) */
+  GS_NUMA_INVALID_TOPOLOGY = 5,         /* ErrInvalidCPUTopology (plugin.go:301-303) */
+  GS_NUMA_BIND_POLICY_CONFLICT = 6,     /* ErrCPUBindPolicyConflict (plugin.go:311-313) */
+  GS_NUMA_SMT_ALIGNMENT = 7,            /* ErrSMTAlignmentError (plugin.go:315-319) */
+  GS_NUMA_ALLOCATE_FAILED = 8,          /* resourceManager.Allocate error in Filter (plugin.go:321-330) */
+  GS_NUMA_MISSING_NUMA_RESOURCES = 9,   /* "node(s) missing NUMA resources" (topology_hint.go:34-36) */
+  GS_NUMA_AFFINITY_ERROR = 10,          /* "node(s) NUMA Topology affinity error" (topologymanager/manager.go:67-69) */
+  GS_NUMA_ADMIT_ALLOCATE_FAILED = 11    /* provider Allocate error after admit (topology_hint.go:89-95) */
+};
 
 typedef struct gs_placement {
   int32_t node;                        /* selected node index, -1 = unschedulable (no feasible node) */
@@ -202,6 +304,9 @@ typedef struct gs_placement {
   uint32_t flags;                      /* GS_PLACED_* diagnostics */
 } gs_placement;
 #define GS_PLACED_SLOWPATH 0x1u        /* resolved by the exact full-row path (no valid candidate list) */
+#define GS_PLACED_NUMA 0x2u            /* NodeNUMAResource Reserve allocated NUMA resources along an affinity hint */
+#define GS_PLACED_CPUSET 0x4u          /* NodeNUMAResource Reserve allocated a cpuset (gs_numa_allocation_get) */
+#define GS_PLACED_AFFINITY_SHIFT 8     /* bits 8..11: the affinity hint as a mask over gs_node_numa.zones slots */
 
 /* ---- errors ---- */
 #define GS_OK 0
@@ -286,6 +391,21 @@ int gs_evaluate(gs_ctx* ctx, const gs_pod* pods, uint32_t npods, int16_t* scores
  * seq[i] keys pod i's tie-break stream. Multi-GPU: every rank passes the same pods and gets the same out[]. */
 int gs_schedule(gs_ctx* ctx, const gs_pod* pods, uint32_t npods, const uint64_t* seq, gs_placement* out);
 
+/* ---- NodeNUMAResource state ---- */
+/* Register a CPUTopology; returns its id in *id (identical topologies may share one id). */
+int gs_topology_register(gs_ctx* ctx, const gs_cpu_topology* topo, int32_t* id);
+/* NodeResourceTopology informer (nodenumaresource/topology_eventhandler.go) + node labels/annotations read by the
+ * plugin: TopologyOptionsManager.UpdateTopologyOptions (topology_options.go:76-86) for the given nodes. */
+int gs_nodes_numa_upsert(gs_ctx* ctx, const uint32_t* idx, const gs_node_numa* numa, uint32_t n);
+/* resourceManager.Update / Release (resource_manager.go:362-381): pod allocations restored from pods' resource-status
+ * annotations (pod_eventhandler.go) or released on delete. Reserve of gs_schedule records its own. */
+int gs_numa_allocations_update(gs_ctx* ctx, const uint32_t* node_idx, const gs_pod_allocation* allocs, uint32_t n);
+int gs_numa_allocations_release(gs_ctx* ctx, const uint32_t* node_idx, const uint64_t* uids, uint32_t n);
+/* The recorded PodAllocation of a pod on a node (PreBind's resource-status, plugin.go:438-478). 1 = found, 0 = none. */
+int gs_numa_allocation_get(gs_ctx* ctx, uint32_t node, uint64_t uid, gs_pod_allocation* out);
+/* v1beta2.SetDefaults_NodeNUMAResourceArgs (defaults.go:101-136) */
+void gs_numa_args_default(gs_numa_args* a);
+
 /* Multi-GPU: nodes are sharded in contiguous ranges [r*ceil(N/R), (r+1)*ceil(N/R)); every rank keeps the full
  * mirror (replicated deltas) and evaluates only its shard. Native RCCL over xGMI: */
 int gs_comm_unique_id(uint8_t out[128]);
@@ -302,7 +422,8 @@ int gs_synchronize(gs_ctx* ctx);
  * number of mismatching rows (0 = the device-side Assume/Reserve replay matches the host mirror). */
 int gs_debug_mirror_check(gs_ctx* ctx);
 /* sizeof() of the ABI structs as compiled into the library, in this order: gs_pod, gs_node,
- * gs_node_metric, gs_pod_metric, gs_config, gs_placement, gs_stats, gs_loadaware_args. */
+ * gs_node_metric, gs_pod_metric, gs_config, gs_placement, gs_stats, gs_loadaware_args, gs_cpu_topology,
+ * gs_node_numa, gs_pod_allocation, gs_numa_args. */
 void gs_abi_sizes(uint64_t* out, uint32_t n);
 
 #ifdef __cplusplus

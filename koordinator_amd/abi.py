@@ -10,7 +10,7 @@ import os
 
 import numpy as np
 
-GS_ABI_VERSION = 1
+GS_ABI_VERSION = 2
 GS_NUM_RES = 8
 GS_RES_CPU, GS_RES_MEMORY, GS_RES_EPHEMERAL = 0, 1, 2
 GS_RES_BATCH_CPU, GS_RES_BATCH_MEMORY, GS_RES_MID_CPU, GS_RES_MID_MEMORY = 3, 4, 5, 6
@@ -24,10 +24,27 @@ GS_USAGE_CPU, GS_USAGE_MEMORY, GS_USAGE_OTHER = 0x1, 0x2, 0x80
 GS_POD_DAEMONSET, GS_POD_TERMINATED = 0x1, 0x2
 GS_NODE_CUSTOM_THRESHOLDS, GS_NODE_CUSTOM_AGGREGATED = 0x1, 0x2
 
-GS_PLUGIN_FIT, GS_PLUGIN_LOADAWARE, GS_NUM_PLUGINS = 0, 1, 2
+GS_PLUGIN_FIT, GS_PLUGIN_LOADAWARE, GS_PLUGIN_NUMA, GS_NUM_PLUGINS = 0, 1, 2, 3
 GS_ENABLE_FIT_FILTER, GS_ENABLE_FIT_SCORE = 0x1, 0x2
 GS_ENABLE_LA_FILTER, GS_ENABLE_LA_SCORE = 0x4, 0x8
-GS_ENABLE_ALL = 0xF
+GS_ENABLE_NUMA_FILTER, GS_ENABLE_NUMA_SCORE = 0x10, 0x20
+GS_ENABLE_LA_FIT = 0xF
+GS_ENABLE_ALL = 0x3F
+
+# NodeNUMAResource vocabulary
+GS_MAX_NUMA, GS_MAX_CPUS, GS_CPU_WORDS = 4, 256, 4
+GS_QOS_NONE, GS_QOS_LSE, GS_QOS_LSR, GS_QOS_LS, GS_QOS_BE, GS_QOS_SYSTEM = 0, 1, 2, 3, 4, 5
+CPU_BIND = {"": 0, "Default": 1, "FullPCPUs": 2, "SpreadByPCPUs": 3, "ConstrainedBurst": 4}
+CPU_EXCLUSIVE = {"": 0, "None": 0, "PCPULevel": 1, "NUMANodeLevel": 2}
+NODE_CPU_BIND = {"": 0, "None": 0, "FullPCPUsOnly": 1, "SpreadByPCPUs": 2}
+NUMA_POLICY = {"": 0, "BestEffort": 1, "Restricted": 2, "SingleNUMANode": 3}
+NUMA_ALLOC = {"": 0, "MostAllocated": 1, "LeastAllocated": 2, "DistributeEvenly": 3}
+GS_SCORING_LEAST_ALLOCATED, GS_SCORING_MOST_ALLOCATED = 0, 1
+GS_FAIL_NUMA_SHIFT, GS_FAIL_NUMA_MASK = 6, 0x3C0
+NUMA_REASONS = ["OK", "InvalidRequestedCPUs", "InvalidAmplificationRatio", "AvailableCPUsError",
+                "InsufficientAmplifiedCPU", "InvalidCPUTopology", "CPUBindPolicyConflict", "SMTAlignment",
+                "AllocateFailed", "MissingNUMAResources", "NUMATopologyAffinity", "AdmitAllocateFailed"]
+GS_PLACED_NUMA, GS_PLACED_CPUSET, GS_PLACED_AFFINITY_SHIFT = 0x2, 0x4, 8
 
 GS_FAIL_FIT_PODS, GS_FAIL_FIT_CPU, GS_FAIL_FIT_MEMORY = 0x01, 0x02, 0x04
 GS_FAIL_FIT_EPHEMERAL, GS_FAIL_FIT_SCALAR, GS_FAIL_LOADAWARE = 0x08, 0x10, 0x20
@@ -43,7 +60,9 @@ class GsPod(C.Structure):
         ("uid", u64), ("name_key", u64),
         ("requests", i64 * GS_NUM_RES), ("limits", i64 * GS_NUM_RES),
         ("nonzero_requests", i64 * 2),
-        ("request_mask", u32), ("priority_class", i32), ("flags", u32), ("pad0", u32),
+        ("request_mask", u32), ("priority_class", i32), ("flags", u32),
+        ("qos_class", i32), ("required_cpu_bind_policy", i32), ("preferred_cpu_bind_policy", i32),
+        ("preferred_cpu_exclusive_policy", i32), ("pad0", i32),
     ]
 
 
@@ -59,6 +78,35 @@ class GsNode(C.Structure):
         ("custom_usage_mask", u32), ("custom_prod_usage_mask", u32), ("custom_agg_usage_mask", u32),
         ("custom_agg_type", i32), ("custom_agg_duration_ns", i64),
     ]
+
+
+class GsCpuTopology(C.Structure):
+    _fields_ = [("num_cpus", i32), ("pad0", i32), ("core_id", i32 * GS_MAX_CPUS),
+                ("socket_id", C.c_uint8 * GS_MAX_CPUS), ("node_id", C.c_uint8 * GS_MAX_CPUS)]
+
+
+class GsNumaZone(C.Structure):
+    _fields_ = [("node_id", i32), ("mask", u32), ("cpu_milli", i64), ("memory", i64)]
+
+
+class GsNodeNuma(C.Structure):
+    _fields_ = [
+        ("has_options", i32), ("topology", i32), ("max_ref_count", i32), ("node_cpu_bind_policy", i32),
+        ("numa_topology_policy", i32), ("numa_allocate_strategy", i32),
+        ("cpu_amplification_ratio", C.c_double), ("node_cpu_amplification_ratio", C.c_double),
+        ("node_amplification_invalid", i32), ("num_zones", i32), ("zones", GsNumaZone * GS_MAX_NUMA),
+        ("reserved_cpus", u64 * GS_CPU_WORDS),
+    ]
+
+
+class GsPodAllocation(C.Structure):
+    _fields_ = [("uid", u64), ("cpuset", u64 * GS_CPU_WORDS), ("cpu_exclusive_policy", i32), ("num_numa", i32),
+                ("numa", GsNumaZone * GS_MAX_NUMA)]
+
+
+class GsNumaArgs(C.Structure):
+    _fields_ = [("default_cpu_bind_policy", i32), ("scoring_type", i32), ("numa_scoring_type", i32), ("pad0", i32),
+                ("resource_weights", i64 * GS_NUM_RES)]
 
 
 class GsUsage(C.Structure):
@@ -105,7 +153,7 @@ class GsConfig(C.Structure):
     _fields_ = [
         ("abi_version", u32), ("device", i32), ("num_nodes", u32), ("enabled", u32),
         ("plugin_weights", i64 * GS_NUM_PLUGINS),
-        ("loadaware", GsLoadAwareArgs), ("fit", GsFitArgs),
+        ("loadaware", GsLoadAwareArgs), ("fit", GsFitArgs), ("numa", GsNumaArgs),
         ("seed", u64), ("batch_size", u32), ("cand_cap", u32),
     ]
 
@@ -131,12 +179,17 @@ NODE_DTYPE = np.dtype(GsNode)
 METRIC_DTYPE = np.dtype(GsNodeMetric)
 POD_METRIC_DTYPE = np.dtype(GsPodMetric)
 PLACEMENT_DTYPE = np.dtype(GsPlacement)
+TOPOLOGY_DTYPE = np.dtype(GsCpuTopology)
+NODE_NUMA_DTYPE = np.dtype(GsNodeNuma)
+POD_ALLOCATION_DTYPE = np.dtype(GsPodAllocation)
 
 STRUCT_SIZES = {
     "gs_pod": C.sizeof(GsPod), "gs_node": C.sizeof(GsNode), "gs_node_metric": C.sizeof(GsNodeMetric),
     "gs_pod_metric": C.sizeof(GsPodMetric), "gs_config": C.sizeof(GsConfig),
     "gs_placement": C.sizeof(GsPlacement), "gs_stats": C.sizeof(GsStats),
-    "gs_loadaware_args": C.sizeof(GsLoadAwareArgs),
+    "gs_loadaware_args": C.sizeof(GsLoadAwareArgs), "gs_cpu_topology": C.sizeof(GsCpuTopology),
+    "gs_node_numa": C.sizeof(GsNodeNuma), "gs_pod_allocation": C.sizeof(GsPodAllocation),
+    "gs_numa_args": C.sizeof(GsNumaArgs),
 }
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
@@ -167,6 +220,12 @@ SIGNATURES = {
     "gs_synchronize": (C.c_int, [P]),
     "gs_debug_mirror_check": (C.c_int, [P]),
     "gs_abi_sizes": (None, [C.POINTER(u64), u32]),
+    "gs_topology_register": (C.c_int, [P, C.POINTER(GsCpuTopology), C.POINTER(i32)]),
+    "gs_nodes_numa_upsert": (C.c_int, [P, P, P, u32]),
+    "gs_numa_allocations_update": (C.c_int, [P, P, P, u32]),
+    "gs_numa_allocations_release": (C.c_int, [P, P, P, u32]),
+    "gs_numa_allocation_get": (C.c_int, [P, u32, u64, C.POINTER(GsPodAllocation)]),
+    "gs_numa_args_default": (None, [C.POINTER(GsNumaArgs)]),
 }
 
 

@@ -64,10 +64,27 @@ def fit_args(resources: dict | None = None) -> abi.GsFitArgs:
     return f
 
 
+def numa_args(defaultCPUBindPolicy: str | None = None, scoringStrategy: dict | None = None,
+              numaScoringStrategy: dict | None = None) -> abi.GsNumaArgs:
+    """v1beta2.NodeNUMAResourceArgs (None = unset) -> defaulted internal args (defaults.go:101-136).
+    scoringStrategy = {"type": "LeastAllocated"|"MostAllocated", "resources": {"cpu": 1, "memory": 1}}."""
+    from .objects import RESOURCE_SLOTS
+    a = abi.GsNumaArgs()
+    a.default_cpu_bind_policy = abi.CPU_BIND["FullPCPUs" if defaultCPUBindPolicy is None else defaultCPUBindPolicy]
+    ss = scoringStrategy or {"type": "LeastAllocated", "resources": {"cpu": 1, "memory": 1}}
+    a.scoring_type = abi.GS_SCORING_MOST_ALLOCATED if ss.get("type") == "MostAllocated" else abi.GS_SCORING_LEAST_ALLOCATED
+    for k, w in ss.get("resources", {}).items():
+        a.resource_weights[RESOURCE_SLOTS[k]] = int(w)
+    ns = numaScoringStrategy or {"type": "LeastAllocated"}
+    a.numa_scoring_type = abi.GS_SCORING_MOST_ALLOCATED if ns.get("type") == "MostAllocated" \
+        else abi.GS_SCORING_LEAST_ALLOCATED
+    return a
+
+
 def make_config(num_nodes: int, la: abi.GsLoadAwareArgs | None = None, fit: abi.GsFitArgs | None = None,
-                enabled: int = abi.GS_ENABLE_ALL, weights=(1, 1), seed: int = 0x6B6F6F7264, device: int = 0,
-                batch_size: int = 0, cand_cap: int = 0) -> abi.GsConfig:
-    """One scheduler profile: NodeResourcesFit + LoadAwareScheduling with their score weights."""
+                enabled: int = abi.GS_ENABLE_LA_FIT, weights=(1, 1, 1), seed: int = 0x6B6F6F7264, device: int = 0,
+                batch_size: int = 0, cand_cap: int = 0, numa: abi.GsNumaArgs | None = None) -> abi.GsConfig:
+    """One scheduler profile: NodeResourcesFit + LoadAwareScheduling (+ NodeNUMAResource) with score weights."""
     cfg = abi.GsConfig()
     cfg.abi_version = abi.GS_ABI_VERSION
     cfg.device = device
@@ -75,8 +92,10 @@ def make_config(num_nodes: int, la: abi.GsLoadAwareArgs | None = None, fit: abi.
     cfg.enabled = enabled
     cfg.plugin_weights[abi.GS_PLUGIN_FIT] = weights[0]
     cfg.plugin_weights[abi.GS_PLUGIN_LOADAWARE] = weights[1]
+    cfg.plugin_weights[abi.GS_PLUGIN_NUMA] = weights[2] if len(weights) > 2 else 1
     cfg.loadaware = la if la is not None else loadaware_args()
     cfg.fit = fit if fit is not None else fit_args()
+    cfg.numa = numa if numa is not None else numa_args()
     cfg.seed = seed
     cfg.batch_size = batch_size
     cfg.cand_cap = cand_cap

@@ -21,6 +21,7 @@
 
 #include "../../include/gpuscore.h"
 #include "gs_kernels.h"
+#include "gs_numa_host.h"
 
 using namespace gs;
 
@@ -116,6 +117,12 @@ struct gs_ctx {
   void* cb_user = nullptr;
   gs_stats stats{};
   uint64_t* d_stamps = nullptr;   // GS_COMMIT_STAMPS=1: commit-kernel phase cycle sums
+  // NodeNUMAResource: per-node TopologyOptions + NodeAllocation mirror, registered CPU topologies
+  std::vector<NumaNode> numa;
+  std::vector<std::shared_ptr<TopoClass>> topos;
+  std::shared_ptr<TopoClass> empty_topo = std::make_shared<TopoClass>();
+  std::unordered_map<uint64_t, uint32_t> numa_uid_node;   // pods holding a NodeAllocation record
+  bool numa_on = false;
 };
 
 namespace {
@@ -359,6 +366,10 @@ void derive_row(const gs_ctx* c, const HostNode& hn, int64_t* row) {
   row[NUM_I64_COLS + C_DFLAGS] = 0;
 }
 
+void derive_row_numa(const gs_ctx* c, uint32_t i, int64_t* row) {
+  numa_derive(c->numa[i], row, row + NUM_I64_COLS);
+}
+
 bool in_range(int64_t v) { return v > -kMaxExact && v < kMaxExact; }
 
 int validate_node(gs_ctx* c, const gs_node& n) {
@@ -391,6 +402,30 @@ PodVec prep_pod(const gs_ctx* c, const gs_pod& p) {
   if (p.requests[0] == 0 && p.requests[1] == 0 && p.requests[2] == 0 && scalar == 0) f |= PF_ALL_ZERO;
   v.flags = f;
   v.scalar_mask = scalar;
+  // NodeNUMAResource PreFilter (nodenumaresource/plugin.go:219-269)
+  uint32_t keys = p.request_mask & 0x7Fu;
+  v.req_keys = keys;
+  bool zero = true;
+  for (int s = 0; s < 7; ++s)
+    if ((keys >> s & 1) && p.requests[s] != 0) zero = false;
+  uint32_t pn = 0;
+  int64_t cpu = (keys & 1u) ? p.requests[GS_RES_CPU] : 0;
+  v.num_cpus = (int32_t)(cpu / 1000);
+  if (zero) {
+    pn |= PN_SKIP;
+  } else if ((p.qos_class == GS_QOS_LSE || p.qos_class == GS_QOS_LSR) && p.priority_class == GS_PRIO_PROD) {
+    const int def = c->cfg.numa.default_cpu_bind_policy;
+    int bind = p.preferred_cpu_bind_policy;
+    if (bind == GS_CPU_BIND_UNSET || bind == GS_CPU_BIND_DEFAULT) bind = def;
+    int required = p.required_cpu_bind_policy;
+    if (required == GS_CPU_BIND_DEFAULT) required = def;
+    if (required != GS_CPU_BIND_UNSET) bind = required;
+    if (bind == GS_CPU_BIND_FULL_PCPUS || bind == GS_CPU_BIND_SPREAD_BY_PCPUS) {
+      if (cpu % 1000 != 0) pn |= PN_PREFAIL;
+      else if (cpu > 0) pn |= PN_BIND | ((uint32_t)required << PN_REQ_SHIFT) | ((uint32_t)bind << PN_PREF_SHIFT);
+    }
+  }
+  v.numa = pn;
   return v;
 }
 
@@ -399,6 +434,15 @@ int validate_pod(gs_ctx* c, const gs_pod& p) {
     if (!in_range(p.requests[s]) || p.requests[s] < 0 || !in_range(p.limits[s]) || p.limits[s] < 0)
       return fail(c, GS_EUNSUPPORTED, "pod resource slot %d outside the exact range [0, 2^53)", s);
   if (p.requests[GS_RES_RESERVED] || (p.request_mask & 0x80u)) return fail(c, GS_EINVAL, "resource slot 7 is reserved");
+  if (c->numa_on) {
+    for (int s = 2; s < 7; ++s)
+      if ((p.request_mask >> s & 1) && p.requests[s] == 0)
+        return fail(c, GS_EUNSUPPORTED, "NodeNUMAResource: a zero-valued request key other than cpu/memory (slot %d) "
+                    "is not supported on the device path", s);
+    if (p.required_cpu_bind_policy < 0 || p.required_cpu_bind_policy > 4 || p.preferred_cpu_bind_policy < 0 ||
+        p.preferred_cpu_bind_policy > 4 || p.preferred_cpu_exclusive_policy < 0 || p.preferred_cpu_exclusive_policy > 2)
+      return fail(c, GS_EINVAL, "pod cpu bind / exclusive policy out of range");
+  }
   return GS_OK;
 }
 
@@ -420,6 +464,7 @@ int flush_rows(gs_ctx* c) {
       uint32_t i = c->dirty_list[done + j];
       c->h_stage_idx[j] = i;
       derive_row(c, c->nodes[i], c->h_stage_rows + (size_t)j * ROW_WORDS);
+      derive_row_numa(c, i, c->h_stage_rows + (size_t)j * ROW_WORDS);
       c->row_dirty[i] = 0;
     }
     HIP_TRY(c, hipMemcpyAsync(c->d_stage_idx, c->h_stage_idx, n * 4, hipMemcpyHostToDevice, c->st));
@@ -472,7 +517,52 @@ bool special_pod(const gs_ctx* c, const gs_pod& p) {
   if (p.flags & GS_POD_TERMINATED) return true;
   if (c->uid_node.count(p.uid)) return true;
   if (c->metric_names.count(p.name_key)) return true;
+  if (c->numa_on && c->numa_uid_node.count(p.uid)) return true;   // Update() would release its old allocation
   return false;
+}
+
+// NodeNUMAResource Reserve (nodenumaresource/plugin.go:375-422) replayed on the host mirror: NUMA resources
+// along the device-chosen affinity (already applied to HBM by the commit kernel), and for cpuset pods the
+// cpuset selection itself (resourceManager.Allocate -> allocateCPUSet -> takeCPUs).
+int numa_reserve(gs_ctx* c, const gs_pod& p, const PodVec& v, const PlacementDev& pd) {
+  if (!c->numa_on || pd.node < 0) return GS_OK;
+  if (v.numa & (PN_SKIP | PN_PREFAIL)) return GS_OK;
+  NumaNode& nn = c->numa[pd.node];
+  const bool rb = pd.flags & GS_PLACED_CPUSET;
+  if (!rb && nn.cfg.numa_topology_policy == GS_NUMA_POLICY_NONE) return GS_OK;
+  PodAllocRec rec;
+  rec.uid = p.uid;
+  rec.excl = (v.numa & PN_BIND) ? p.preferred_cpu_exclusive_policy : GS_CPU_EXCLUSIVE_NONE;
+  for (int z = 0; z < GS_MAX_NUMA; ++z) {
+    if (!(pd.zkeys >> z & 1) && !(pd.zkeys >> (4 + z) & 1)) continue;
+    gs_numa_zone a{};
+    a.node_id = nn.cfg.zones[z].node_id;
+    if (pd.zkeys >> z & 1) { a.mask |= GS_USAGE_CPU; a.cpu_milli = pd.zcpu[z]; }
+    if (pd.zkeys >> (4 + z) & 1) { a.mask |= GS_USAGE_MEMORY; a.memory = pd.zmem[z]; }
+    rec.numa.push_back(a);
+  }
+  if (rb) {
+    // getCPUBindPolicy (util.go:85-103) and GetNUMAAllocateStrategy (util.go:35-41)
+    int req = (v.numa >> PN_REQ_SHIFT) & 7, pref = (v.numa >> PN_PREF_SHIFT) & 7;
+    int bind = pref;
+    bool required = false;
+    if (req != GS_CPU_BIND_UNSET) { bind = req; required = true; }
+    else if (nn.cfg.node_cpu_bind_policy == GS_NODE_CPU_BIND_SPREAD_BY_PCPUS) { bind = GS_CPU_BIND_SPREAD_BY_PCPUS; required = true; }
+    else if (nn.cfg.node_cpu_bind_policy == GS_NODE_CPU_BIND_FULL_PCPUS_ONLY) { bind = GS_CPU_BIND_FULL_PCPUS; required = true; }
+    int strategy = nn.cfg.numa_allocate_strategy;
+    if (strategy == GS_NUMA_ALLOC_UNSET)
+      strategy = c->cfg.numa.numa_scoring_type == GS_SCORING_MOST_ALLOCATED ? GS_NUMA_ALLOC_MOST_ALLOCATED
+                                                                          : GS_NUMA_ALLOC_LEAST_ALLOCATED;
+    if (!numa_allocate_cpuset(nn, v.num_cpus, bind, required, rec.excl, strategy, rec.numa, &rec.cpus))
+      return fail(c, GS_ESTATE, "NodeNUMAResource Reserve: cpuset allocation failed on node %d after a feasible Filter",
+                  pd.node);
+  }
+  if (!nn.topo_valid()) return GS_OK;   // resourceManager.Update skips nodes without a valid CPU topology
+  numa_release(nn, rec.uid);
+  numa_add(nn, rec);
+  c->numa_uid_node[rec.uid] = (uint32_t)pd.node;
+  if (rb) mark_dirty(c, (uint32_t)pd.node);
+  return GS_OK;
 }
 
 void apply_placement(gs_ctx* c, const gs_pod& p, int32_t node, bool special) {
@@ -504,7 +594,21 @@ int compute_profile(gs_ctx* c) {
   const gs_config& cfg = c->cfg;
   Profile& pf = c->pf;
   pf = Profile{};
-  pf.enabled = cfg.enabled & 0xFu;
+  pf.enabled = cfg.enabled & 0x3Fu;
+  c->numa_on = (pf.enabled & (GS_ENABLE_NUMA_FILTER | GS_ENABLE_NUMA_SCORE)) != 0;
+  pf.w_numa = (int32_t)cfg.plugin_weights[GS_PLUGIN_NUMA];
+  for (int s = 0; s < 7; ++s) {
+    int64_t w = cfg.numa.resource_weights[s];
+    if (w < 0 || w > 100) return fail(c, GS_EINVAL, "NodeNUMAResource weight of slot %d not in [0, 100]", s);
+    pf.numa_w[s] = (int32_t)w;
+  }
+  pf.numa_most = cfg.numa.scoring_type == GS_SCORING_MOST_ALLOCATED;
+  pf.numa_hint_most = cfg.numa.numa_scoring_type == GS_SCORING_MOST_ALLOCATED;
+  {
+    int d = cfg.numa.default_cpu_bind_policy;   // validation.ValidateNodeNUMAResourceArgs (validation_pluginargs.go:156-172)
+    if (d != GS_CPU_BIND_UNSET && d != GS_CPU_BIND_FULL_PCPUS && d != GS_CPU_BIND_SPREAD_BY_PCPUS)
+      return fail(c, GS_EINVAL, "defaultCPUBindPolicy must specified CPU bind policy FullPCPUs or SpreadByPCPUs");
+  }
   pf.w_fit = (int32_t)cfg.plugin_weights[GS_PLUGIN_FIT];
   pf.w_la = (int32_t)cfg.plugin_weights[GS_PLUGIN_LOADAWARE];
   for (int r = 0; r < 2; ++r) {
@@ -523,7 +627,8 @@ int compute_profile(gs_ctx* c) {
   int64_t ms = 0;
   if (pf.enabled & GS_ENABLE_FIT_SCORE) ms += 100 * cfg.plugin_weights[GS_PLUGIN_FIT];
   if (pf.enabled & GS_ENABLE_LA_SCORE) ms += 100 * cfg.plugin_weights[GS_PLUGIN_LOADAWARE];
-  if (cfg.plugin_weights[0] < 0 || cfg.plugin_weights[1] < 0 || ms > MAX_SCORE_LIMIT)
+  if (pf.enabled & GS_ENABLE_NUMA_SCORE) ms += 100 * cfg.plugin_weights[GS_PLUGIN_NUMA];
+  if (cfg.plugin_weights[0] < 0 || cfg.plugin_weights[1] < 0 || cfg.plugin_weights[2] < 0 || ms > MAX_SCORE_LIMIT)
     return fail(c, GS_EUNSUPPORTED, "profile score weights must keep the max total score <= %d (got %lld)",
                 MAX_SCORE_LIMIT, (long long)ms);
   c->max_score = (int)ms;
@@ -627,7 +732,7 @@ int run_batch(gs_ctx* c, const gs_pod* pods, int b, int* committed_out) {
       else if (r.max_score == M && M >= 0) T += r.ties;
     }
     if (M < 0) {
-      c->h_out[0] = PlacementDev{-1, (uint32_t)F, 0, 0, GS_PLACED_SLOWPATH};
+      c->h_out[0] = PlacementDev{-1, (uint32_t)F, 0, 0, GS_PLACED_SLOWPATH, 0, 0, {0, 0, 0, 0}, {0, 0, 0, 0}};
       *committed_out = 1;
       return GS_OK;
     }
@@ -688,7 +793,8 @@ const char* gs_version(void) { return "libgpuscore 0.1 (gfx950, ABI 1)"; }
 
 void gs_abi_sizes(uint64_t* out, uint32_t n) {
   const uint64_t s[] = {sizeof(gs_pod), sizeof(gs_node), sizeof(gs_node_metric), sizeof(gs_pod_metric),
-                        sizeof(gs_config), sizeof(gs_placement), sizeof(gs_stats), sizeof(gs_loadaware_args)};
+                        sizeof(gs_config), sizeof(gs_placement), sizeof(gs_stats), sizeof(gs_loadaware_args),
+                        sizeof(gs_cpu_topology), sizeof(gs_node_numa), sizeof(gs_pod_allocation), sizeof(gs_numa_args)};
   for (uint32_t i = 0; i < n && i < sizeof(s) / sizeof(s[0]); ++i) out[i] = s[i];
 }
 
@@ -775,6 +881,7 @@ int gs_create(const gs_config* cfg, gs_ctx** out) {
   c->N = cfg->num_nodes;
   c->npad = (c->N + 1023) & ~1023u;
   c->nodes.resize(c->N);
+  c->numa.resize(c->N);
   c->row_dirty.assign(c->N, 0);
   set_shard(c);
   auto bail = [&](const char* what, hipError_t e) {
@@ -940,7 +1047,7 @@ int gs_evaluate(gs_ctx* c, const gs_pod* pods, uint32_t npods, int16_t* scores, 
   uint16_t* d_cd = nullptr;
   HIP_TRY(c, hipMalloc(&d_sc, (size_t)chunk * N * 2));
   HIP_TRY(c, hipMalloc(&d_cd, (size_t)chunk * N * 2));
-  HIP_TRY(c, hipMalloc(&d_pl, (size_t)chunk * N * 4));
+  HIP_TRY(c, hipMalloc(&d_pl, (size_t)chunk * N * 2 * GS_NUM_PLUGINS));
   for (uint32_t p0 = 0; p0 < npods; p0 += chunk) {
     int b = (int)std::min<uint32_t>(chunk, npods - p0);
     int prod_cols = 0;
@@ -955,7 +1062,8 @@ int gs_evaluate(gs_ctx* c, const gs_pod* pods, uint32_t npods, int16_t* scores, 
     if (scores) HIP_TRY(c, hipMemcpyAsync(scores + (size_t)p0 * N, d_sc, (size_t)b * N * 2, hipMemcpyDeviceToHost, c->st));
     if (codes) HIP_TRY(c, hipMemcpyAsync(codes + (size_t)p0 * N, d_cd, (size_t)b * N * 2, hipMemcpyDeviceToHost, c->st));
     if (plugin_scores)
-      HIP_TRY(c, hipMemcpyAsync(plugin_scores + (size_t)p0 * N * 2, d_pl, (size_t)b * N * 4, hipMemcpyDeviceToHost, c->st));
+      HIP_TRY(c, hipMemcpyAsync(plugin_scores + (size_t)p0 * N * GS_NUM_PLUGINS, d_pl, (size_t)b * N * 2 * GS_NUM_PLUGINS,
+                                hipMemcpyDeviceToHost, c->st));
     HIP_TRY(c, hipStreamSynchronize(c->st));
   }
   (void)hipFree(d_sc);
@@ -999,12 +1107,108 @@ int gs_schedule(gs_ctx* c, const gs_pod* pods, uint32_t npods, const uint64_t* s
       o.score = pd.node >= 0 ? pd.score : 0;
       o.ties = pd.node >= 0 ? pd.ties : 0;
       o.flags = pd.flags;
+      if ((rc = numa_reserve(c, pods[i + j], c->h_pods[j], pd))) return rc;
       apply_placement(c, pods[i + j], pd.node, special_first);
     }
     c->stats.pods += committed;
     i += committed;
   }
   return flush_rows(c);
+}
+
+void gs_numa_args_default(gs_numa_args* a) {
+  if (!a) return;
+  std::memset(a, 0, sizeof(*a));
+  a->default_cpu_bind_policy = GS_CPU_BIND_FULL_PCPUS;   // defaults.go:50,103-106
+  a->scoring_type = GS_SCORING_LEAST_ALLOCATED;
+  a->numa_scoring_type = GS_SCORING_LEAST_ALLOCATED;
+  a->resource_weights[GS_RES_CPU] = 1;
+  a->resource_weights[GS_RES_MEMORY] = 1;
+}
+
+int gs_topology_register(gs_ctx* c, const gs_cpu_topology* t, int32_t* id) {
+  if (!c || !t || !id) return GS_EINVAL;
+  const char* err = nullptr;
+  auto topo = make_topo(*t, &err);
+  if (!topo) return fail(c, GS_EUNSUPPORTED, "gs_topology_register: %s", err ? err : "invalid topology");
+  c->topos.push_back(topo);
+  *id = (int32_t)c->topos.size() - 1;
+  return GS_OK;
+}
+
+int gs_nodes_numa_upsert(gs_ctx* c, const uint32_t* idx, const gs_node_numa* nn, uint32_t n) {
+  if (!c || (!nn && n)) return GS_EINVAL;
+  for (uint32_t j = 0; j < n; ++j) {
+    uint32_t i = idx ? idx[j] : j;
+    if (i >= c->N) return fail(c, GS_EINVAL, "node index %u >= %u", i, c->N);
+    const gs_node_numa& x = nn[j];
+    if (x.num_zones < 0 || x.num_zones > GS_MAX_NUMA)
+      return fail(c, GS_EUNSUPPORTED, "node %u: %d NUMA zones (device path supports <= %d)", i, x.num_zones, GS_MAX_NUMA);
+    for (int z = 0; z < x.num_zones; ++z) {
+      if (x.zones[z].node_id < 0 || x.zones[z].node_id >= 64 || (z && x.zones[z].node_id <= x.zones[z - 1].node_id))
+        return fail(c, GS_EINVAL, "node %u: NUMA zones must be sorted by distinct node id in [0,64)", i);
+      if (x.zones[z].cpu_milli < 0 || x.zones[z].memory < 0 || x.zones[z].cpu_milli >= kMaxExact || x.zones[z].memory >= kMaxExact)
+        return fail(c, GS_EUNSUPPORTED, "node %u: NUMA zone quantity outside [0, 2^53)", i);
+    }
+    if (x.numa_topology_policy < 0 || x.numa_topology_policy > 3 || x.node_cpu_bind_policy < 0 ||
+        x.node_cpu_bind_policy > 2 || x.numa_allocate_strategy < 0 || x.numa_allocate_strategy > 3)
+      return fail(c, GS_EINVAL, "node %u: policy enum out of range", i);
+    if (x.has_options && x.topology >= (int32_t)c->topos.size())
+      return fail(c, GS_EINVAL, "node %u: topology id %d not registered", i, x.topology);
+    NumaNode& st = c->numa[i];
+    st.cfg = x;
+    st.topo = !x.has_options ? nullptr : (x.topology >= 0 ? c->topos[x.topology] : c->empty_topo);
+    mark_dirty(c, i);
+  }
+  return flush_rows(c);
+}
+
+int gs_numa_allocations_update(gs_ctx* c, const uint32_t* node_idx, const gs_pod_allocation* a, uint32_t n) {
+  if (!c || (n && (!node_idx || !a))) return GS_EINVAL;
+  for (uint32_t j = 0; j < n; ++j) {
+    uint32_t i = node_idx[j];
+    if (i >= c->N) return fail(c, GS_EINVAL, "node index %u >= %u", i, c->N);
+    NumaNode& st = c->numa[i];
+    if (!st.topo_valid()) continue;   // resourceManager.Update (resource_manager.go:362-373)
+    PodAllocRec rec;
+    rec.uid = a[j].uid;
+    for (int w = 0; w < GS_CPU_WORDS; ++w) rec.cpus.w[w] = a[j].cpuset[w];
+    rec.excl = a[j].cpu_exclusive_policy;
+    if (a[j].num_numa < 0 || a[j].num_numa > GS_MAX_NUMA) return fail(c, GS_EINVAL, "num_numa out of range");
+    for (int z = 0; z < a[j].num_numa; ++z) rec.numa.push_back(a[j].numa[z]);
+    numa_release(st, rec.uid);
+    numa_add(st, rec);
+    c->numa_uid_node[rec.uid] = i;
+    mark_dirty(c, i);
+  }
+  return flush_rows(c);
+}
+
+int gs_numa_allocations_release(gs_ctx* c, const uint32_t* node_idx, const uint64_t* uids, uint32_t n) {
+  if (!c || (n && (!node_idx || !uids))) return GS_EINVAL;
+  for (uint32_t j = 0; j < n; ++j) {
+    uint32_t i = node_idx[j];
+    if (i >= c->N) return fail(c, GS_EINVAL, "node index %u >= %u", i, c->N);
+    numa_release(c->numa[i], uids[j]);
+    auto it = c->numa_uid_node.find(uids[j]);
+    if (it != c->numa_uid_node.end() && it->second == i) c->numa_uid_node.erase(it);
+    mark_dirty(c, i);
+  }
+  return flush_rows(c);
+}
+
+int gs_numa_allocation_get(gs_ctx* c, uint32_t node, uint64_t uid, gs_pod_allocation* out) {
+  if (!c || !out || node >= c->N) return GS_EINVAL;
+  const NumaNode& st = c->numa[node];
+  auto it = st.pods.find(uid);
+  if (it == st.pods.end()) return 0;
+  std::memset(out, 0, sizeof(*out));
+  out->uid = uid;
+  for (int w = 0; w < GS_CPU_WORDS; ++w) out->cpuset[w] = it->second.cpus.w[w];
+  out->cpu_exclusive_policy = it->second.excl;
+  out->num_numa = (int32_t)std::min<size_t>(it->second.numa.size(), GS_MAX_NUMA);
+  for (int z = 0; z < out->num_numa; ++z) out->numa[z] = it->second.numa[z];
+  return 1;
 }
 
 int gs_comm_unique_id(uint8_t out[128]) {
@@ -1078,9 +1282,10 @@ int gs_debug_mirror_check(gs_ctx* c) {
   for (uint32_t i = 0; i < c->N; ++i) {
     derive_row(c, c->nodes[i], row.data());
     bool ok = true;
+    derive_row_numa(c, i, row.data());
     for (int k = 0; k < NUM_I64_COLS; ++k) ok &= d64[(size_t)k * c->npad + i] == row[k];
-    ok &= d32[(size_t)C_FREE_PODS * c->npad + i] == (int32_t)row[NUM_I64_COLS + C_FREE_PODS];
-    ok &= d32[(size_t)C_SFLAGS * c->npad + i] == (int32_t)row[NUM_I64_COLS + C_SFLAGS];
+    for (int k = 0; k < NUM_I32_COLS; ++k)
+      if (k != C_DFLAGS) ok &= d32[(size_t)k * c->npad + i] == (int32_t)row[NUM_I64_COLS + k];
     if (!ok) {
       if (bad < 4) fprintf(stderr, "gpuscore: mirror row %u differs from its host derivation\n", i);
       ++bad;

@@ -43,12 +43,15 @@ struct LevelHdr {
 };
 static_assert(sizeof(LevelHdr) == 80, "LevelHdr layout");
 
-struct PlacementDev {   // layout == gs_placement
+struct PlacementDev {   // gs_placement + the NodeNUMAResource Reserve the device applied / the host must apply
   int32_t node;
   uint32_t feasible;
   int64_t score;
   uint32_t ties;
-  uint32_t flags;
+  uint32_t flags;        // GS_PLACED_* (GS_PLACED_CPUSET: the host selects the cpuset and cuts the batch here)
+  uint32_t zkeys;        // NUMA allocation by hint: bit z = zone z cpu allocated, bit 4+z = memory
+  uint32_t pad;
+  int64_t zcpu[4], zmem[4];
 };
 
 struct CommitArgs {

@@ -18,6 +18,7 @@
 #include <stdint.h>
 
 #include "gs_kernels.h"
+#include "gs_numa_dev.h"
 
 namespace gs {
 
@@ -68,8 +69,13 @@ struct Row {
   uint32_t dflags;
   uint32_t node;        // global index
   uint32_t pad;
+  NumaRow nr;           // NodeNUMAResource columns (loaded when the profile enables the plugin)
 };
 constexpr int ROW_I64 = 17;   // int64 words of Row, in the column order of kRowCol
+constexpr int NUMA_I64 = 18;  // NumaRow int64 words: C_ZCAP_CPU0 .. C_NAMP (contiguous columns)
+constexpr int NUMA_I32 = 12;  // NumaRow int32 words: C_NFLAGS .. C_ZADJ0+3 (contiguous columns)
+static_assert(C_NAMP - C_ZCAP_CPU0 + 1 == NUMA_I64, "NUMA i64 columns contiguous");
+static_assert(C_ZADJ0 + 3 - C_NFLAGS + 1 == NUMA_I32, "NUMA i32 columns contiguous");
 
 __constant__ int kRowCol[ROW_I64] = {C_FREE_CPU,     C_FREE_MEM,    C_FREE_EPH,   C_FREE_BCPU,  C_FREE_BMEM,
                                      C_FREE_MCPU,    C_FREE_MMEM,   C_ALLOC_CPU,  C_ALLOC_MEM,  C_NZFREE_CPU,
@@ -78,7 +84,8 @@ __constant__ int kRowCol[ROW_I64] = {C_FREE_CPU,     C_FREE_MEM,    C_FREE_EPH, 
 // Row words an assume/Reserve changes (written back by the commit kernel)
 __device__ __forceinline__ bool row_word_mutable(int j) { return j < 7 || j == 9 || j == 10 || j >= 13; }
 
-__device__ __forceinline__ void load_row(const MirrorView& m, uint32_t i, bool prod_cols, Row& r) {
+__device__ __forceinline__ void load_row(const MirrorView& m, uint32_t i, bool prod_cols, bool numa, Row& r) {
+  if (numa) load_numa_row(m, i, r.nr);
   r.free[0] = m.c64(C_FREE_CPU)[i];
   r.free[1] = m.c64(C_FREE_MEM)[i];
   r.free[2] = m.c64(C_FREE_EPH)[i];
@@ -103,14 +110,28 @@ __device__ __forceinline__ void load_row(const MirrorView& m, uint32_t i, bool p
 
 struct PairOut {
   uint32_t code;
-  int32_t fit, la;
+  int32_t fit, la, numa;
+};
+
+// NodeInfo slot views for numa_eval: Allocatable and Allocatable - Requested per resource slot
+struct SlotsHbm {
+  const Row& r;
+  const MirrorView& m;
+  __device__ int64_t alloc(int s) const { return s < 2 ? r.alloc[s] : m.c64(C_ALLOC_CPU + s)[r.node]; }
+  __device__ int64_t free(int s) const { return s < 3 ? r.free[s] : m.c64(C_FREE_CPU + s)[r.node]; }
+};
+struct SlotsLds {
+  const Row& r;
+  const MirrorView& m;
+  __device__ int64_t alloc(int s) const { return s < 2 ? r.alloc[s] : m.c64(C_ALLOC_CPU + s)[r.node]; }
+  __device__ int64_t free(int s) const { return r.free[s]; }
 };
 
 // Filter (Fit + LoadAware) and Score (Fit LeastAllocated + LoadAware) of one pod on one node.
 // LDS_SCALARS: scalar free columns come from r.free[3..6] (the commit's LDS copy) instead of HBM.
 template <bool FULL, bool LDS_SCALARS>
 __device__ __forceinline__ PairOut eval_pair(const Row& r, const PodVec& p, const Profile& pf, const MirrorView& m) {
-  PairOut o{0u, 0, 0};
+  PairOut o{0u, 0, 0, 0};
   // ---- [upstream] noderesources Fit.Filter -> fitsRequest
   if (pf.enabled & 0x1u) {
     if (r.free_pods < 1) o.code |= 0x01u;                               // len(Pods)+1 > AllowedPodNumber
@@ -133,6 +154,15 @@ __device__ __forceinline__ PairOut eval_pair(const Row& r, const PodVec& p, cons
     if (r.dflags & bit) o.code |= 0x20u;
   }
   if (!FULL && o.code) return o;
+  // ---- NodeNUMAResource Filter (+ Admit) and Score (gs_numa_dev.h)
+  if (pf.enabled & 0x30u) {
+    NumaOut no;
+    if (LDS_SCALARS) no = numa_eval(r.nr, p, pf, SlotsLds{r, m}, pf.enabled & 0x10u, pf.enabled & 0x20u);
+    else no = numa_eval(r.nr, p, pf, SlotsHbm{r, m}, pf.enabled & 0x10u, pf.enabled & 0x20u);
+    o.code |= no.reason << GS_FAIL_NUMA_SHIFT;
+    if (!FULL && o.code) return o;
+    o.numa = no.reason ? 0 : no.score;
+  }
   // ---- Fit.Score, LeastAllocated over NonZeroRequested ([upstream] resource_allocation.go)
   if (pf.enabled & 0x2u) {
     int32_t ns = 0, ws = 0;
@@ -171,7 +201,7 @@ __device__ __forceinline__ PairOut eval_pair(const Row& r, const PodVec& p, cons
 
 __device__ __forceinline__ int32_t total_score(const PairOut& o, const Profile& pf) {
   if (o.code) return -1;
-  return o.fit * pf.w_fit + o.la * pf.w_la;
+  return o.fit * pf.w_fit + o.la * pf.w_la + o.numa * pf.w_numa;
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -197,6 +227,7 @@ __global__ void __launch_bounds__(256) node_prep_kernel(MirrorView m, uint32_t n
 // The hot kernel. Workgroup = 256 consecutive nodes of the shard x PODS_PER_BLOCK pods. Each thread keeps
 // its node row in registers and sweeps the group's pods (wave-uniform pod vectors: scalar loads), writing
 // one int16 score per (pod, node): one coalesced 512-B row segment per pod per workgroup.
+template <bool NUMA>
 __global__ void __launch_bounds__(256) eval_kernel(MirrorView m, const PodVec* __restrict__ pods, int npods,
                                                    Profile pf, uint32_t n0, uint32_t n1, int16_t* __restrict__ S,
                                                    uint32_t ld, int prod_cols) {
@@ -204,7 +235,8 @@ __global__ void __launch_bounds__(256) eval_kernel(MirrorView m, const PodVec* _
   const uint32_t len = n1 - n0;
   const bool ok = local < len;
   Row row;
-  load_row(m, ok ? n0 + local : n0, prod_cols, row);
+  load_row(m, ok ? n0 + local : n0, prod_cols, NUMA, row);
+  if (!NUMA) pf.enabled &= ~0x30u;
   const int k0 = blockIdx.y * PODS_PER_BLOCK;
   const int k1 = min(npods, k0 + PODS_PER_BLOCK);
   for (int k = k0; k < k1; ++k) {
@@ -220,15 +252,16 @@ __global__ void __launch_bounds__(256) eval_full_kernel(MirrorView m, const PodV
   uint32_t i = blockIdx.x * 256 + threadIdx.x;
   if (i >= N) return;
   Row r;
-  load_row(m, i, prod_cols, r);
+  load_row(m, i, prod_cols, (pf.enabled & 0x30u) != 0, r);
   for (int k = 0; k < npods; ++k) {
     PairOut o = eval_pair<true, false>(r, pods[k], pf, m);
     size_t off = (size_t)k * N + i;
     if (scores) scores[off] = (int16_t)total_score(o, pf);
     if (codes) codes[off] = (uint16_t)o.code;
     if (plugin) {
-      plugin[off * 2 + 0] = (int16_t)o.fit;
-      plugin[off * 2 + 1] = (int16_t)o.la;
+      plugin[off * 3 + 0] = (int16_t)o.fit;
+      plugin[off * 3 + 1] = (int16_t)o.la;
+      plugin[off * 3 + 2] = (int16_t)o.numa;
     }
   }
 }
@@ -486,7 +519,8 @@ __global__ void __launch_bounds__(256) commit_kernel(CommitArgs a) {
   __shared__ int s_action, s_slot, s_fresh, s_M, s_F;  // wave-0 decision for pod k (0 commit, 1 skip, 2 cut)
   __shared__ uint32_t s_winner;
   __shared__ int64_t s_T;
-  __shared__ PlacementDev res[MAX_BATCH];              // placements, written to HBM once at the end
+  __shared__ int s_cut;                                // the pod just committed needs host-side Reserve
+  const bool numa_on = (a.pf.enabled & 0x30u) != 0;
 
   for (int i = tid; i < B; i += 256) pods[i] = a.pods[i];
   for (int i = tid; i < HASH; i += 256) { hkey[i] = -1; hval[i] = -1; }
@@ -563,7 +597,10 @@ __global__ void __launch_bounds__(256) commit_kernel(CommitArgs a) {
       break;
     }
     if (M < 0) {       // FitError: no feasible node anywhere, nothing assumed
-      if (lane == 0) { res[k] = PlacementDev{-1, (uint32_t)F, 0, 0, 0}; s_action = 1; }
+      if (lane == 0) {
+        a.out[k] = PlacementDev{-1, (uint32_t)F, 0, 0, 0, 0, 0, {0, 0, 0, 0}, {0, 0, 0, 0}};
+        s_action = 1;
+      }
       break;
     }
     uint32_t winner = 0xffffffffu;
@@ -705,6 +742,12 @@ __global__ void __launch_bounds__(256) commit_kernel(CommitArgs a) {
       if (lane == ROW_I64) orow.free_pods = m.c32(C_FREE_PODS)[winner];
       if (lane == ROW_I64 + 1) orow.dflags = (uint32_t)m.c32(C_DFLAGS)[winner];
       if (lane == ROW_I64 + 2) { orow.node = winner; orow.pad = 0; }
+      if (numa_on) {
+        int64_t* nw = reinterpret_cast<int64_t*>(&orow.nr);
+        if (lane >= 32 && lane < 32 + NUMA_I64) nw[lane - 32] = m.c64(C_ZCAP_CPU0 + (lane - 32))[winner];
+        int32_t* iw = reinterpret_cast<int32_t*>(&orow.nr.nflags);
+        if (lane >= 50 && lane < 50 + NUMA_I32) iw[lane - 50] = m.c32(C_NFLAGS + (lane - 50))[winner];
+      }
     }
     if (lane == 0) {
       s_action = 0; s_slot = slot; s_fresh = fresh; s_winner = winner; s_M = M; s_F = F; s_T = T;
@@ -722,6 +765,37 @@ __global__ void __launch_bounds__(256) commit_kernel(CommitArgs a) {
     if (tid == 0) {
       if (fresh) d = orow;
       const PodVec& pk = pods[k];
+      const bool forced = (k == 0 && a.forced_node >= 0);
+      PlacementDev pl{(int32_t)s_winner, (uint32_t)s_F, (int64_t)s_M, (uint32_t)s_T, forced ? 1u : 0u, 0, 0,
+                      {0, 0, 0, 0}, {0, 0, 0, 0}};
+      s_cut = 0;
+      if (numa_on && !(pk.numa & (PN_SKIP | PN_PREFAIL))) {
+        // NodeNUMAResource Reserve (plugin.go:375-422) on the pre-assume row: the Filter-time affinity and the
+        // NUMA split of Allocate; a cpuset pod ends the batch (its CPUs are chosen on the host)
+        NumaOut no = numa_eval(d.nr, pk, a.pf, SlotsLds{d, m}, a.pf.enabled & 0x10u, false);
+        const uint32_t nf = d.nr.nflags;
+        const bool rb = no.flags & GS_PLACED_CPUSET;
+        if (no.reason) pl.flags |= 0x80000000u;   // cannot happen for a feasible winner: the host fails loudly
+        if (rb || ((nf >> NF_POLICY_SHIFT) & 3u)) {
+          pl.flags |= no.flags;
+          pl.zkeys = no.zkeys;
+#pragma unroll
+          for (int z = 0; z < 4; ++z) { pl.zcpu[z] = no.zcpu[z]; pl.zmem[z] = no.zmem[z]; }
+          if (nf & NF_TOPO_VALID) {   // resourceManager.Update -> NodeAllocation.addPodAllocation
+#pragma unroll
+            for (int z = 0; z < 4; ++z) {
+              const bool zc = no.zkeys >> z & 1u, zm = no.zkeys >> (4 + z) & 1u;
+              if (!zc && !zm) continue;
+              d.nr.zraw_cpu[z] += no.zcpu[z];
+              d.nr.zraw_mem[z] += no.zmem[z];
+              d.nr.nflags2 |= (1u << (NF2_ENTRY_SHIFT + z)) | (zc ? 1u << (NF2_ACPU_SHIFT + z) : 0u) |
+                              (zm ? 1u << (NF2_AMEM_SHIFT + z) : 0u);
+            }
+          }
+          if (rb) s_cut = 1;
+        }
+      }
+      a.out[k] = pl;
       for (int s = 0; s < 7; ++s) d.free[s] -= pk.req[s];
       d.nzfree[0] -= pk.nz[0];
       d.nzfree[1] -= pk.nz[1];
@@ -732,10 +806,9 @@ __global__ void __launch_bounds__(256) commit_kernel(CommitArgs a) {
         d.la_pfree[0] -= pk.est[0];
         d.la_pfree[1] -= pk.est[1];
       }
-      const bool forced = (k == 0 && a.forced_node >= 0);
-      res[k] = PlacementDev{(int32_t)s_winner, (uint32_t)s_F, (int64_t)s_M, (uint32_t)s_T, forced ? 1u : 0u};
     }
     __syncthreads();
+    if (s_cut) { committed = k + 1; break; }
     // batch-start scores (fresh rows) on threads 0..127, current scores on threads 128..255
     if (tid < 128) {
       int q = k + 1 + tid;
@@ -761,7 +834,12 @@ __global__ void __launch_bounds__(256) commit_kernel(CommitArgs a) {
     if (row_word_mutable(j)) m.c64(kRowCol[j])[drows[s].node] = reinterpret_cast<const int64_t*>(&drows[s])[j];
   }
   for (int s = tid; s < nd; s += 256) m.c32(C_FREE_PODS)[drows[s].node] = drows[s].free_pods;
-  for (int i = tid; i < committed; i += 256) a.out[i] = res[i];
+  if (numa_on)
+    for (int e = tid; e < nd * 9; e += 256) {
+      int sl = e / 9, j = e % 9;
+      if (j < 8) m.c64(C_ZRAW_CPU0 + j)[drows[sl].node] = (&drows[sl].nr.zraw_cpu[0])[j];
+      else m.c32(C_NFLAGS2)[drows[sl].node] = (int32_t)drows[sl].nr.nflags2;
+    }
   if (tid == 0) *a.committed = committed;
   if (ST && tid == 0)
     for (int i = 0; i < 8; ++i) a.stamps[i] += st_acc[i];
@@ -857,7 +935,10 @@ hipError_t launch_eval(const MirrorView& m, const PodVec* pods, int npods, const
   uint32_t gx = (len + 255) / 256;
   uint32_t gy = (npods + PODS_PER_BLOCK - 1) / PODS_PER_BLOCK;
   if (gx == 0 || gy == 0) return hipSuccess;
-  hipLaunchKernelGGL(eval_kernel, dim3(gx, gy), dim3(256), 0, st, m, pods, npods, pf, n0, n1, S, ld, prod_cols);
+  if (pf.enabled & 0x30u)
+    hipLaunchKernelGGL(eval_kernel<true>, dim3(gx, gy), dim3(256), 0, st, m, pods, npods, pf, n0, n1, S, ld, prod_cols);
+  else
+    hipLaunchKernelGGL(eval_kernel<false>, dim3(gx, gy), dim3(256), 0, st, m, pods, npods, pf, n0, n1, S, ld, prod_cols);
   return hipGetLastError();
 }
 

@@ -34,6 +34,13 @@ enum I64Col : int {
   C_LA_PFREE_CPU,      // EstimateNode - la_used_prod (ScoreAccordingProdUsage for Prod pods)
   C_LA_PFREE_MEM,
   C_UPDATE_TIME,       // NodeMetric Status.UpdateTime (unix ns)
+  // NodeNUMAResource (zone z = gs_node_numa.zones[z], sorted by NUMA node id)
+  C_ZCAP_CPU0,         // NUMANodeResources[z] cpu (milli) / memory: the zone's allocatable
+  C_ZCAP_MEM0 = C_ZCAP_CPU0 + 4,
+  C_ZRAW_CPU0 = C_ZCAP_MEM0 + 4,   // NodeAllocation.allocatedResources[z] (raw sums of pod NUMA allocations)
+  C_ZRAW_MEM0 = C_ZRAW_CPU0 + 4,
+  C_AMP = C_ZRAW_MEM0 + 4,         // options.AmplificationRatios[cpu] (f64 bits)
+  C_NAMP,                          // node annotation cpu amplification ratio (f64 bits; -1 unset)
   NUM_I64_COLS
 };
 
@@ -42,7 +49,33 @@ enum I32Col : int {
   C_FREE_PODS = 0,     // AllowedPodNumber - len(Pods)
   C_SFLAGS,            // static LoadAware flags (host-derived, time independent)
   C_DFLAGS,            // dynamic flags (node-prep kernel, depend on `now`)
-  NUM_I32_COLS
+  C_NFLAGS,            // NodeNUMAResource static flags (NF_*), host-derived
+  C_NFLAGS2,           // zone allocation entries / keys (NF2_*), changed by device-side Reserve
+  C_ALLOC_CPUS,        // |NodeAllocation.allocatedCPUs| (0 when CPUTopology == nil)
+  C_TFREE,             // available CPUs of the node: raw | full-core CPUs << 9 | cores with a free CPU << 18
+  C_ZFREE0,            // same, restricted to zone z
+  C_ZADJ0 = C_ZFREE0 + 4,          // Amplify(c_z*1000) - c_z*1000, c_z = allocated CPUs in zone z (amp > 1)
+  NUM_I32_COLS = C_ZADJ0 + 4
+};
+
+// C_NFLAGS bits
+enum : uint32_t {
+  NF_HAS_OPTIONS = 1u << 0,   // TopologyOptions exist
+  NF_TOPO = 1u << 1,          // CPUTopology != nil
+  NF_TOPO_VALID = 1u << 2,    // CPUTopology.IsValid()
+  NF_AMP_INVALID = 1u << 3,   // node amplification annotation unparsable
+  NF_POLICY_SHIFT = 4,        // 2 bits: gs_numa_topology_policy
+  NF_BIND_SHIFT = 6,          // 2 bits: gs_node_cpu_bind_policy
+  NF_ZONES_SHIFT = 8,         // 3 bits: number of zones
+  NF_ZCPU_SHIFT = 12,         // 4 bits: zone z lists cpu
+  NF_ZMEM_SHIFT = 16,         // 4 bits: zone z lists memory
+  NF_CPC_SHIFT = 20,          // 8 bits: CPUsPerCore
+};
+// C_NFLAGS2 bits
+enum : uint32_t {
+  NF2_ENTRY_SHIFT = 0,        // 4 bits: allocatedResources has an entry for zone z
+  NF2_ACPU_SHIFT = 4,         // 4 bits: that entry lists cpu
+  NF2_AMEM_SHIFT = 8,         // 4 bits: that entry lists memory
 };
 
 // C_SFLAGS bits
@@ -68,7 +101,11 @@ struct PodVec {
   int64_t est[2];        // DefaultEstimator.EstimatePod cpu/memory (LoadAware)
   uint32_t flags;        // PF_*
   uint32_t scalar_mask;  // scalar request keys (slots 3..6)
-  uint64_t pad[3];
+  uint32_t numa;         // NodeNUMAResource PreFilter state (PN_*)
+  int32_t num_cpus;      // preFilterState.numCPUsNeeded
+  uint32_t req_keys;     // request keys (slots 0..6)
+  uint32_t pad0;
+  uint64_t pad[1];
 };
 enum : uint32_t {
   PF_DAEMONSET = 1u << 0,
@@ -76,6 +113,14 @@ enum : uint32_t {
   PF_PROD_SCORE = 1u << 2,    // Prod && ScoreAccordingProdUsage
   PF_ALL_ZERO = 1u << 3,      // cpu == mem == eph == 0 && no scalar keys (Fit filter short cut)
   PF_LA_W_CPU = 1u << 4,      // (unused on device; args carry the weights)
+};
+// PodVec.numa: preFilterState (nodenumaresource/plugin.go:172-181)
+enum : uint32_t {
+  PN_SKIP = 1u << 0,          // requests are zero
+  PN_BIND = 1u << 1,          // requestCPUBind
+  PN_PREFAIL = 1u << 2,       // PreFilter returned ErrInvalidRequestedCPUs
+  PN_REQ_SHIFT = 4,           // 3 bits: requiredCPUBindPolicy (gs_cpu_bind_policy)
+  PN_PREF_SHIFT = 8,          // 3 bits: preferredCPUBindPolicy
 };
 
 // kernel-uniform profile constants
@@ -86,6 +131,10 @@ struct Profile {
   int32_t la_wsum;            // Σ LoadAware weights (divisor, load_aware.go:385)
   int32_t fit_w[7];           // Fit LeastAllocated weights per slot
   uint32_t fit_scalar_w_mask; // slots 2..6 with non-zero weight
+  int32_t w_numa;             // NodeNUMAResource plugin weight
+  int32_t numa_w[7];          // NodeNUMAResource ScoringStrategy.Resources weights per slot
+  int32_t numa_most;          // ScoringStrategy.Type == MostAllocated
+  int32_t numa_hint_most;     // NUMAScoringStrategy.Type == MostAllocated (hint scores)
 };
 
 // per (pod, shard) full-row summary for the exact slow path

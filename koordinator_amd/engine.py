@@ -112,6 +112,38 @@ class Engine:
         self._chk(lib().gs_schedule(self._h, abi.ptr(pods), len(pods), abi.ptr(seq), abi.ptr(out)), "gs_schedule")
         return out
 
+    # ---- NodeNUMAResource state
+    def register_topology(self, topo) -> int:
+        t = abi.GsCpuTopology.from_buffer_copy(np.ascontiguousarray(np.atleast_1d(topo), abi.TOPOLOGY_DTYPE).tobytes())
+        out = C.c_int32()
+        self._chk(lib().gs_topology_register(self._h, C.byref(t), C.byref(out)), "gs_topology_register")
+        return out.value
+
+    def upsert_numa(self, numa, idx=None):
+        numa = np.ascontiguousarray(numa, dtype=abi.NODE_NUMA_DTYPE)
+        if idx is not None:
+            idx = np.ascontiguousarray(idx, dtype=np.uint32)
+        self._chk(lib().gs_nodes_numa_upsert(self._h, abi.ptr(idx), abi.ptr(numa), len(numa)), "gs_nodes_numa_upsert")
+
+    def update_allocations(self, node_idx, allocs):
+        node_idx = np.ascontiguousarray(node_idx, dtype=np.uint32)
+        allocs = np.ascontiguousarray(allocs, dtype=abi.POD_ALLOCATION_DTYPE)
+        self._chk(lib().gs_numa_allocations_update(self._h, abi.ptr(node_idx), abi.ptr(allocs), len(allocs)),
+                  "gs_numa_allocations_update")
+
+    def release_allocations(self, node_idx, uids):
+        node_idx = np.ascontiguousarray(node_idx, dtype=np.uint32)
+        uids = np.ascontiguousarray(uids, dtype=np.uint64)
+        self._chk(lib().gs_numa_allocations_release(self._h, abi.ptr(node_idx), abi.ptr(uids), len(uids)),
+                  "gs_numa_allocations_release")
+
+    def allocation(self, node: int, uid: int):
+        out = abi.GsPodAllocation()
+        rc = lib().gs_numa_allocation_get(self._h, node, uid, C.byref(out))
+        if rc < 0:
+            self._chk(rc, "gs_numa_allocation_get")
+        return np.frombuffer(bytes(out), abi.POD_ALLOCATION_DTYPE)[0] if rc == 1 else None
+
     # ---- multi-GPU
     def comm_init_rccl(self, uid: bytes, nranks: int, rank: int):
         buf = (C.c_uint8 * 128).from_buffer_copy(uid)

@@ -69,6 +69,7 @@ class Cluster:
     assigned_pods: np.ndarray
     assigned_ts: np.ndarray
     pods: np.ndarray         # POD_DTYPE[P] pending, in scheduling order
+    numa: dict | None = None # NodeNUMAResource state: topologies, node_numa, allocations (make_numa)
 
     @property
     def num_nodes(self) -> int:
@@ -201,6 +202,91 @@ def make_cluster(num_nodes: int, num_pods: int, config_id: int = 1, seed: int | 
     return Cluster(now, nodes, metrics, pm, offsets, a_node, a_pods, a_ts.astype(np.int64), pods)
 
 
+def make_numa(c: Cluster, seed: int | None = None, numa_policy_pct: int = 30, cpuset_pod_pct: int = 20) -> Cluster:
+    """Adds the C3 NodeNUMAResource state to a cluster, in place:
+    2 sockets, k in {2, 4} NUMA nodes, SMT2 (logical CPUs = allocatable cores, <= 128); NRT zones split cpu and
+    memory evenly; `numa_policy_pct`% of nodes labelled numa-topology-policy in {SingleNUMANode, Restricted,
+    BestEffort}; 3% node cpu-bind-policy FullPCPUsOnly, 2% SpreadByPCPUs; 4% cpu amplification 1.5; existing
+    cpuset pods on 25% of nodes and NUMA allocations on labelled nodes; `cpuset_pod_pct`% of pending pods LSR/LSE
+    Prod with integer CPUs (some with a required bind policy)."""
+    from . import numa as nm
+    s = Stream((BASE_SEED + 77) if seed is None else seed)
+    N = c.num_nodes
+    cores = c.nodes["allocatable"][:, 0] // 1000
+    k = np.where(s.randint(300, N, 0, 1) == 0, 2, 4)
+    # topology classes by (cores, k)
+    classes, tid_of = {}, np.zeros(N, np.int32)
+    for i in range(N):
+        key = (int(cores[i]), int(k[i]))
+        if key not in classes:
+            classes[key] = len(classes)
+        tid_of[i] = classes[key]
+    topos = []
+    for (nc, kk), _ in sorted(classes.items(), key=lambda kv: kv[1]):
+        per_socket = kk // 2
+        cores_per_numa = nc // 2 // kk
+        cpus = []
+        for sk in range(2):
+            for nn in range(per_socket):
+                for co in range(cores_per_numa):
+                    for _t in range(2):
+                        cpus.append((sk, sk * per_socket + nn, nn * cores_per_numa + co))
+        topos.append(nm.topology(cpus))
+    pol = s.randint(301, N, 0, 99)
+    policy = np.where(pol < numa_policy_pct // 3, "SingleNUMANode",
+                      np.where(pol < 2 * numa_policy_pct // 3, "Restricted",
+                               np.where(pol < numa_policy_pct, "BestEffort", "")))
+    bindk = s.randint(302, N, 0, 99)
+    amp = s.randint(303, N, 0, 99) < 4
+    recs = np.zeros(N, abi.NODE_NUMA_DTYPE)
+    mem = c.nodes["allocatable"][:, 1]
+    for i in range(N):
+        kk = int(k[i])
+        ratio = 1.5 if amp[i] else 0.0
+        zc = int(cores[i]) * 1000 // kk
+        if amp[i]:
+            zc = int(np.ceil(zc * 1.5))
+        zones = [(z, zc, int(mem[i]) // kk) for z in range(kk)]
+        recs[i] = nm.node_numa(int(tid_of[i]), zones, numa_policy=str(policy[i]),
+                               node_cpu_bind="FullPCPUsOnly" if bindk[i] < 3 else ("SpreadByPCPUs" if bindk[i] < 5 else ""),
+                               cpu_ratio=ratio, node_cpu_ratio=1.5 if amp[i] else -1.0)
+    if amp.any():   # amplified allocatable (NodeResource controller), as makeNode does in plugin_test.go:114-120
+        c.nodes["allocatable"][amp, 0] = np.ceil(c.nodes["allocatable"][amp, 0] * 1.5).astype(np.int64)
+    # existing allocations: a cpuset pod (2-8 CPUs from CPU 0 up, full cores) on 25% of nodes; NUMA resources on
+    # labelled nodes (zone 0)
+    allocs, a_nodes = [], []
+    has_cs = s.randint(304, N, 0, 99) < 25
+    ncs = s.randint(305, N, 1, 4) * 2
+    for i in np.nonzero(has_cs | (policy != ""))[0]:
+        cpus = list(range(int(ncs[i]))) if has_cs[i] else []
+        numa_res = [(0, int(ncs[i]) * 1000, 4 << 30)] if policy[i] != "" else []
+        allocs.append(nm.pod_allocation(int(0x5EED0000 + i), cpus, numa_res))
+        a_nodes.append(int(i))
+    c.numa = {"topologies": topos, "node_numa": recs,
+              "alloc_nodes": np.array(a_nodes, np.uint32),
+              "allocs": np.array(allocs, abi.POD_ALLOCATION_DTYPE) if allocs else np.zeros(0, abi.POD_ALLOCATION_DTYPE)}
+    # pending pods: cpuset_pod_pct% LSR/LSE Prod with integer cpus
+    P = len(c.pods)
+    cs = s.randint(306, P, 0, 99) < cpuset_pod_pct
+    cpus = s.randint(307, P, 1, 8) * 1000
+    c.pods["requests"][cs, 0] = cpus[cs]
+    c.pods["nonzero_requests"][cs, 0] = cpus[cs]
+    c.pods["limits"][cs, 0] = cpus[cs]
+    c.pods["requests"][cs, 1] = np.maximum(c.pods["requests"][cs, 1], 256 << 20)
+    c.pods["nonzero_requests"][cs, 1] = c.pods["requests"][cs, 1]
+    c.pods["limits"][cs, 1] = c.pods["requests"][cs, 1]
+    c.pods["request_mask"][cs] = (1 << abi.GS_RES_CPU) | (1 << abi.GS_RES_MEMORY)
+    c.pods["priority_class"][cs] = abi.GS_PRIO_PROD
+    c.pods["qos_class"] = np.where(cs, np.where(s.randint(308, P, 0, 1) == 0, abi.GS_QOS_LSR, abi.GS_QOS_LSE),
+                                   abi.GS_QOS_LS)
+    req = s.randint(309, P, 0, 99)
+    c.pods["required_cpu_bind_policy"] = np.where(cs & (req < 10), abi.CPU_BIND["FullPCPUs"],
+                                                  np.where(cs & (req < 15), abi.CPU_BIND["SpreadByPCPUs"], 0))
+    c.pods["preferred_cpu_bind_policy"] = np.where(cs & (req >= 15) & (req < 30), abi.CPU_BIND["SpreadByPCPUs"], 0)
+    c.pods["preferred_cpu_exclusive_policy"] = np.where(cs & (req >= 90), abi.CPU_EXCLUSIVE["PCPULevel"], 0)
+    return c
+
+
 def load_into(engine, c: Cluster) -> None:
     """Push a cluster into an Engine / Oracle (same calls a scheduler's informers would make)."""
     engine.set_now(c.now_ns)
@@ -208,3 +294,10 @@ def load_into(engine, c: Cluster) -> None:
     engine.upsert_metrics(c.metrics, c.pod_metrics, c.pm_offsets)
     if len(c.assigned_pods):
         engine.assign(c.assigned_node, c.assigned_pods, c.assigned_ts)
+    if c.numa is not None:
+        ids = [engine.register_topology(t) for t in c.numa["topologies"]]
+        recs = c.numa["node_numa"].copy()
+        recs["topology"] = np.array(ids, np.int32)[recs["topology"]]
+        engine.upsert_numa(recs)
+        if len(c.numa["allocs"]):
+            engine.update_allocations(c.numa["alloc_nodes"], c.numa["allocs"])

@@ -3,6 +3,7 @@
 // k8s.io/kubernetes@v1.24.15 code (go.mod:57,276), not vendored in /root/reference, restated
 // from its published source — parity for those parts is unpinned by in-repo tests.
 #include "oracle.h"
+#include "numa.h"
 
 #include <atomic>
 #include <cmath>
@@ -110,6 +111,11 @@ struct or_cluster {
   gs_config cfg;
   int64_t now = 0;
   std::vector<NodeState> nodes;
+  // NodeNUMAResource (oracle/numa.cpp)
+  orn::NumaArgs numa_args;
+  std::vector<std::shared_ptr<orn::CPUTopology>> topologies;
+  std::vector<orn::NodeNUMA> numa;
+  bool reverse_hint_order = false;
 };
 
 namespace {
@@ -473,16 +479,33 @@ int64_t fit_score(const gs_fit_args& f, const gs_pod& pod, const gs_node& n) {
 
 struct PairResult {
   uint16_t code;
-  int64_t fit, la;
+  int64_t fit, la, numa;
 };
 
-PairResult eval_pair(const or_cluster& c, const gs_pod& pod, const NodeState& s) {
-  PairResult res{0, 0, 0};
+orn::NodeView node_view(const gs_node& n) {
+  return orn::NodeView{n.allocatable[GS_RES_CPU], n.allocatable[GS_RES_MEMORY], n.requested[GS_RES_CPU],
+                       n.requested[GS_RES_MEMORY], n.allocatable, n.requested};
+}
+
+// NodeNUMAResource Filter of one (pod, node) pair: reason bits + the affinity Admit stored for Score/Reserve
+uint16_t numa_filter(const or_cluster& c, const orn::PreState& st, uint32_t i, orn::Hint* aff) {
+  bool has = false;
+  int reason = orn::filter(c.numa_args, st, c.numa[i], node_view(c.nodes[i].node), aff, &has, c.reverse_hint_order);
+  if (!has) *aff = orn::Hint{};
+  return (uint16_t)(reason << GS_FAIL_NUMA_SHIFT);
+}
+
+PairResult eval_pair(const or_cluster& c, const gs_pod& pod, const orn::PreState& st, uint32_t i) {
+  const NodeState& s = c.nodes[i];
+  PairResult res{0, 0, 0, 0};
   uint32_t en = c.cfg.enabled;
   if (en & GS_ENABLE_FIT_FILTER) res.code |= (uint16_t)fit_filter(pod, s.node);
   if ((en & GS_ENABLE_LA_FILTER) && loadaware_filter(c, pod, s)) res.code |= GS_FAIL_LOADAWARE;
+  orn::Hint aff;
+  if (en & GS_ENABLE_NUMA_FILTER) res.code |= numa_filter(c, st, i, &aff);
   if (en & GS_ENABLE_FIT_SCORE) res.fit = fit_score(c.cfg.fit, pod, s.node);
   if (en & GS_ENABLE_LA_SCORE) res.la = loadaware_score(c, pod, s);
+  if (en & GS_ENABLE_NUMA_SCORE) res.numa = orn::score(c.numa_args, st, c.numa[i], node_view(s.node), aff);
   return res;
 }
 
@@ -490,7 +513,46 @@ int64_t weighted_total(const or_cluster& c, const PairResult& r) {
   int64_t t = 0;
   if (c.cfg.enabled & GS_ENABLE_FIT_SCORE) t += r.fit * c.cfg.plugin_weights[GS_PLUGIN_FIT];
   if (c.cfg.enabled & GS_ENABLE_LA_SCORE) t += r.la * c.cfg.plugin_weights[GS_PLUGIN_LOADAWARE];
+  if (c.cfg.enabled & GS_ENABLE_NUMA_SCORE) t += r.numa * c.cfg.plugin_weights[GS_PLUGIN_NUMA];
   return t;
+}
+
+orn::NumaArgs numa_args_of(const gs_numa_args& a) {
+  orn::NumaArgs o;
+  o.default_bind = a.default_cpu_bind_policy;
+  o.scoring = a.scoring_type;
+  o.numa_scoring = a.numa_scoring_type;
+  for (int r = 0; r < GS_NUM_RES; ++r) o.weights[r] = a.resource_weights[r];
+  return o;
+}
+
+orn::PodAllocation pod_allocation_of(const gs_pod_allocation& a) {
+  orn::PodAllocation p;
+  p.uid = a.uid;
+  for (int c = 0; c < GS_MAX_CPUS; ++c)
+    if (a.cpuset[c >> 6] >> (c & 63) & 1) p.cpus.insert(c);
+  p.excl = a.cpu_exclusive_policy;
+  for (int j = 0; j < a.num_numa && j < GS_MAX_NUMA; ++j) {
+    orn::NUMANodeResource nr;
+    nr.node = a.numa[j].node_id;
+    if (a.numa[j].mask & GS_USAGE_CPU) nr.res.set(GS_RES_CPU, a.numa[j].cpu_milli);
+    if (a.numa[j].mask & GS_USAGE_MEMORY) nr.res.set(GS_RES_MEMORY, a.numa[j].memory);
+    p.numa.push_back(nr);
+  }
+  return p;
+}
+
+void export_allocation(const orn::PodAllocation& p, gs_pod_allocation* out) {
+  std::memset(out, 0, sizeof(*out));
+  out->uid = p.uid;
+  for (int c : p.cpus) out->cpuset[c >> 6] |= 1ull << (c & 63);
+  out->cpu_exclusive_policy = p.excl;
+  out->num_numa = (int32_t)std::min<size_t>(p.numa.size(), GS_MAX_NUMA);
+  for (int j = 0; j < out->num_numa; ++j) {
+    out->numa[j].node_id = p.numa[j].node;
+    if (p.numa[j].res.has(GS_RES_CPU)) { out->numa[j].mask |= GS_USAGE_CPU; out->numa[j].cpu_milli = p.numa[j].res.v[GS_RES_CPU]; }
+    if (p.numa[j].res.has(GS_RES_MEMORY)) { out->numa[j].mask |= GS_USAGE_MEMORY; out->numa[j].memory = p.numa[j].res.v[GS_RES_MEMORY]; }
+  }
 }
 
 // ---- parallelize.Until emulation (pkg/util/parallelize/parallelism.go:29-49) ------------------
@@ -557,8 +619,9 @@ or_cluster* or_create(const gs_config* cfg) {
   if (!cfg) return nullptr;
   or_cluster* c = new or_cluster();
   c->cfg = *cfg;
-  if (c->cfg.plugin_weights[0] == 0 && c->cfg.plugin_weights[1] == 0) c->cfg.plugin_weights[0] = c->cfg.plugin_weights[1] = 1;
   c->nodes.resize(cfg->num_nodes);
+  c->numa.resize(cfg->num_nodes);
+  c->numa_args = numa_args_of(cfg->numa);
   return c;
 }
 
@@ -663,19 +726,125 @@ int or_evaluate(or_cluster* c, const gs_pod* pods, uint32_t npods, int16_t* scor
   if (!c) return GS_EINVAL;
   size_t N = c->nodes.size();
   for (uint32_t p = 0; p < npods; ++p) {
+    orn::PreState st = orn::prefilter(c->numa_args, pods[p]);
     for (size_t n = 0; n < N; ++n) {
       if (!c->nodes[n].has_node) return GS_ESTATE;
-      PairResult r = eval_pair(*c, pods[p], c->nodes[n]);
+      PairResult r = eval_pair(*c, pods[p], st, (uint32_t)n);
       size_t o = (size_t)p * N + n;
       if (codes) codes[o] = r.code;
       if (scores) scores[o] = r.code ? (int16_t)-1 : (int16_t)weighted_total(*c, r);
       if (plugin_scores) {
         plugin_scores[o * GS_NUM_PLUGINS + GS_PLUGIN_FIT] = (int16_t)r.fit;
         plugin_scores[o * GS_NUM_PLUGINS + GS_PLUGIN_LOADAWARE] = (int16_t)r.la;
+        plugin_scores[o * GS_NUM_PLUGINS + GS_PLUGIN_NUMA] = (int16_t)r.numa;
       }
     }
   }
   return GS_OK;
+}
+
+int or_topology_register(or_cluster* c, const gs_cpu_topology* t, int32_t* id) {
+  if (!c || !t || !id || t->num_cpus < 0 || t->num_cpus > GS_MAX_CPUS) return GS_EINVAL;
+  auto topo = orn::build_topology(*t);
+  if (topo->num_sockets > 12) return GS_EUNSUPPORTED;
+  c->topologies.push_back(topo);
+  *id = (int32_t)c->topologies.size() - 1;
+  return GS_OK;
+}
+
+// TopologyOptionsManager.UpdateTopologyOptions (topology_options.go:76-86) with the node labels resolved
+int or_nodes_numa_upsert(or_cluster* c, const uint32_t* idx, const gs_node_numa* nn, uint32_t n) {
+  if (!c) return GS_EINVAL;
+  for (uint32_t j = 0; j < n; ++j) {
+    uint32_t k = idx ? idx[j] : j;
+    if (k >= c->numa.size()) return GS_EINVAL;
+    const gs_node_numa& x = nn[j];
+    orn::TopologyOptions o;
+    o.present = x.has_options != 0;
+    if (o.present) {
+      if (x.topology >= 0) {
+        if (x.topology >= (int)c->topologies.size()) return GS_EINVAL;
+        o.topo = c->topologies[x.topology];
+      } else {
+        o.topo = std::make_shared<orn::CPUTopology>();   // reported but empty: non-nil, invalid
+      }
+      for (int cpu = 0; cpu < GS_MAX_CPUS; ++cpu)
+        if (x.reserved_cpus[cpu >> 6] >> (cpu & 63) & 1) o.reserved.insert(cpu);
+      o.max_ref = x.max_ref_count ? x.max_ref_count : 1;
+      for (int z = 0; z < x.num_zones && z < GS_MAX_NUMA; ++z) {
+        orn::NUMANodeResource nr;
+        nr.node = x.zones[z].node_id;
+        if (x.zones[z].mask & GS_USAGE_CPU) nr.res.set(GS_RES_CPU, x.zones[z].cpu_milli);
+        if (x.zones[z].mask & GS_USAGE_MEMORY) nr.res.set(GS_RES_MEMORY, x.zones[z].memory);
+        o.numa.push_back(nr);
+      }
+    }
+    o.amp_ratio = x.cpu_amplification_ratio;   // effective ratio after amplifyNUMANodeResources (util.go:62-83)
+    o.node_cpu_bind = x.node_cpu_bind_policy;
+    o.numa_policy = x.numa_topology_policy;
+    o.numa_alloc_strategy = x.numa_allocate_strategy;
+    o.node_amp_ratio = x.node_cpu_amplification_ratio;
+    o.node_amp_invalid = x.node_amplification_invalid != 0;
+    c->numa[k].opts = o;
+  }
+  return GS_OK;
+}
+
+int or_numa_allocations_update(or_cluster* c, const uint32_t* node_idx, const gs_pod_allocation* a, uint32_t n) {
+  if (!c) return GS_EINVAL;
+  for (uint32_t j = 0; j < n; ++j) {
+    if (node_idx[j] >= c->numa.size()) return GS_EINVAL;
+    orn::NodeNUMA& nn = c->numa[node_idx[j]];
+    if (!(nn.opts.topo && nn.opts.topo->valid())) continue;   // resourceManager.Update skips
+    nn.alloc.update(pod_allocation_of(a[j]), nn.opts.topo.get());
+  }
+  return GS_OK;
+}
+
+int or_numa_allocations_release(or_cluster* c, const uint32_t* node_idx, const uint64_t* uids, uint32_t n) {
+  if (!c) return GS_EINVAL;
+  for (uint32_t j = 0; j < n; ++j) {
+    if (node_idx[j] >= c->numa.size()) return GS_EINVAL;
+    c->numa[node_idx[j]].alloc.release(uids[j]);
+  }
+  return GS_OK;
+}
+
+int or_numa_allocation_get(or_cluster* c, uint32_t node, uint64_t uid, gs_pod_allocation* out) {
+  if (!c || node >= c->numa.size() || !out) return GS_EINVAL;
+  auto it = c->numa[node].alloc.pods.find(uid);
+  if (it == c->numa[node].alloc.pods.end()) return 0;
+  export_allocation(it->second, out);
+  return 1;
+}
+
+int or_set_hint_order(or_cluster* c, int reverse) {
+  if (!c) return GS_EINVAL;
+  c->reverse_hint_order = reverse != 0;
+  return GS_OK;
+}
+
+int or_take_cpus_test(int sockets, int nodes_per_socket, int cores_per_node, int cpus_per_core, int max_ref,
+                      const uint64_t* available, const int32_t* alloc_ref, const int32_t* alloc_excl, int needed,
+                      int bind, int excl, int strategy, uint64_t* result) {
+  auto topo = orn::build_test_topology(sockets, nodes_per_socket, cores_per_node, cpus_per_core);
+  orn::CPUSet avail;
+  orn::CPUDetails details;
+  for (auto& kv : topo->details) {
+    int cpu = kv.first;
+    if (available[cpu >> 6] >> (cpu & 63) & 1) avail.insert(cpu);
+    if (alloc_ref && alloc_ref[cpu] >= 0) {
+      orn::CPUInfo info = kv.second;
+      info.ref = alloc_ref[cpu];
+      info.excl = alloc_excl ? alloc_excl[cpu] : 0;
+      details[cpu] = info;
+    }
+  }
+  orn::CPUSet out;
+  bool ok = orn::take_cpus(*topo, max_ref, avail, details, needed, bind, excl, strategy, &out);
+  for (int w = 0; w < GS_CPU_WORDS; ++w) result[w] = 0;
+  for (int cpu : out) result[cpu >> 6] |= 1ull << (cpu & 63);
+  return ok ? 0 : -1;
 }
 
 int32_t or_tiebreak_intn(uint64_t seed, uint64_t seq, int64_t cnt) {
@@ -692,12 +861,14 @@ int or_schedule(or_cluster* c, const gs_pod* pods, uint32_t npods, const uint64_
     if (!c->nodes[n].has_node) return GS_ESTATE;
   std::vector<uint8_t> feasible(N);
   std::vector<int64_t> score(N);
+  std::vector<orn::Hint> affinity(N);   // topologymanager Store of the cycle (store.go:55-66)
   std::vector<int> feasible_list;
   feasible_list.reserve(N);
   std::unique_ptr<Pool> pool;
   if (nthreads > 1) pool.reset(new Pool(nthreads));
   for (uint32_t p = 0; p < npods; ++p) {
     const gs_pod& pod = pods[p];
+    const orn::PreState st = orn::prefilter(c->numa_args, pod);
     // findNodesThatPassFilters: percentageOfNodesToScore = 100, so every node is checked and
     // nextStartNodeIndex = (start + N) % N stays put: feasible order = node index order.
     auto check = [&](int n) {
@@ -705,6 +876,8 @@ int or_schedule(or_cluster* c, const gs_pod* pods, uint32_t npods, const uint64_
       uint16_t code = 0;
       if (c->cfg.enabled & GS_ENABLE_FIT_FILTER) code |= (uint16_t)fit_filter(pod, s.node);
       if ((c->cfg.enabled & GS_ENABLE_LA_FILTER) && loadaware_filter(*c, pod, s)) code |= GS_FAIL_LOADAWARE;
+      affinity[n] = orn::Hint{};
+      if (!code && (c->cfg.enabled & GS_ENABLE_NUMA_FILTER)) code |= numa_filter(*c, st, (uint32_t)n, &affinity[n]);
       feasible[n] = code == 0;
     };
     if (pool) pool->until(N, check);
@@ -722,9 +895,11 @@ int or_schedule(or_cluster* c, const gs_pod* pods, uint32_t npods, const uint64_
     // prioritizeNodes: RunScorePlugins over the feasible list, weight and sum.
     auto score_one = [&](int i) {
       int n = feasible_list[i];
-      PairResult r{0, 0, 0};
+      PairResult r{0, 0, 0, 0};
       if (c->cfg.enabled & GS_ENABLE_FIT_SCORE) r.fit = fit_score(c->cfg.fit, pod, c->nodes[n].node);
       if (c->cfg.enabled & GS_ENABLE_LA_SCORE) r.la = loadaware_score(*c, pod, c->nodes[n]);
+      if (c->cfg.enabled & GS_ENABLE_NUMA_SCORE)
+        r.numa = orn::score(c->numa_args, st, c->numa[n], node_view(c->nodes[n].node), affinity[n]);
       score[n] = weighted_total(*c, r);
     };
     int F = (int)feasible_list.size();
@@ -745,6 +920,19 @@ int or_schedule(or_cluster* c, const gs_pod* pods, uint32_t npods, const uint64_
       }
     }
     o.node = selected; o.score = max_score; o.ties = (uint32_t)cnt;
+    // Reserve: NodeNUMAResource (plugin.go:375-422) on the pre-assume NodeInfo
+    if (c->cfg.enabled & (GS_ENABLE_NUMA_FILTER | GS_ENABLE_NUMA_SCORE)) {
+      orn::PodAllocation pa;
+      if (orn::reserve(c->numa_args, st, c->numa[selected], pod, affinity[selected], &pa) != 0) return GS_ESTATE;
+      if (!pa.numa.empty()) {
+        o.flags |= GS_PLACED_NUMA;
+        const auto& zones = c->numa[selected].opts.numa;
+        for (const auto& nr : pa.numa)
+          for (size_t z = 0; z < zones.size(); ++z)
+            if (zones[z].node == nr.node) o.flags |= 1u << (GS_PLACED_AFFINITY_SHIFT + z);
+      }
+      if (!pa.cpus.empty()) o.flags |= GS_PLACED_CPUSET;
+    }
     // assume: NodeInfo.AddPod ([upstream] framework/types.go calculateResource)
     gs_node& nd = c->nodes[selected].node;
     for (int r = 0; r < GS_NUM_RES; ++r) nd.requested[r] += pod.requests[r];

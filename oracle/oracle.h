@@ -45,6 +45,19 @@ int or_evaluate(or_cluster* c, const gs_pod* pods, uint32_t npods, int16_t* scor
 /* nthreads <= 1: serial; otherwise a worker pool emulating parallelize.Until (pkg/util/parallelize/parallelism.go:29-49) */
 int or_schedule(or_cluster* c, const gs_pod* pods, uint32_t npods, const uint64_t* seq, gs_placement* out,
                 int nthreads);
+/* NodeNUMAResource state (mirrors gs_topology_register / gs_nodes_numa_upsert / gs_numa_allocations_*) */
+int or_topology_register(or_cluster* c, const gs_cpu_topology* t, int32_t* id);
+int or_nodes_numa_upsert(or_cluster* c, const uint32_t* idx, const gs_node_numa* nn, uint32_t n);
+int or_numa_allocations_update(or_cluster* c, const uint32_t* node_idx, const gs_pod_allocation* a, uint32_t n);
+int or_numa_allocations_release(or_cluster* c, const uint32_t* node_idx, const uint64_t* uids, uint32_t n);
+int or_numa_allocation_get(or_cluster* c, uint32_t node, uint64_t uid, gs_pod_allocation* out);
+/* 1: iterate hint resources in reverse name order (exposes Go map-order dependence, policy.go:108) */
+int or_set_hint_order(or_cluster* c, int reverse);
+/* takeCPUs on a buildCPUTopologyForTest topology (cpu_accumulator_test.go:30-57), for the golden vectors.
+ * available: cpuset words; alloc_ref[cpu] >= 0 puts the cpu in allocatedCPUs with that RefCount and alloc_excl[cpu]. */
+int or_take_cpus_test(int sockets, int nodes_per_socket, int cores_per_node, int cpus_per_core, int max_ref,
+                      const uint64_t* available, const int32_t* alloc_ref, const int32_t* alloc_excl, int needed,
+                      int bind, int excl, int strategy, uint64_t* result);
 /* the selectHost tie-break stream: Intn(cnt) of pod stream `seq` (see oracle.cpp TieBreakRand) */
 int32_t or_tiebreak_intn(uint64_t seed, uint64_t seq, int64_t cnt);
 

@@ -43,6 +43,13 @@ def _load() -> C.CDLL:
         "or_evaluate": (C.c_int, [P, P, C.c_uint32, P, P, P]),
         "or_schedule": (C.c_int, [P, P, C.c_uint32, P, P, C.c_int]),
         "or_tiebreak_intn": (C.c_int32, [C.c_uint64, C.c_uint64, C.c_int64]),
+        "or_topology_register": (C.c_int, [P, P, P]),
+        "or_nodes_numa_upsert": (C.c_int, [P, P, P, C.c_uint32]),
+        "or_numa_allocations_update": (C.c_int, [P, P, P, C.c_uint32]),
+        "or_numa_allocations_release": (C.c_int, [P, P, P, C.c_uint32]),
+        "or_numa_allocation_get": (C.c_int, [P, C.c_uint32, C.c_uint64, P]),
+        "or_set_hint_order": (C.c_int, [P, C.c_int]),
+        "or_take_cpus_test": (C.c_int, [C.c_int] * 5 + [P, P, P] + [C.c_int] * 4 + [P]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -149,6 +156,39 @@ class Oracle:
              "evaluate")
         return scores, codes, plugin
 
+    # NodeNUMAResource state
+    def register_topology(self, topo) -> int:
+        t = np.ascontiguousarray(np.atleast_1d(topo), dtype=abi.TOPOLOGY_DTYPE)
+        out = C.c_int32()
+        _chk(lib().or_topology_register(self._h, abi.ptr(t), C.addressof(out)), "topology_register")
+        return out.value
+
+    def upsert_numa(self, numa, idx=None):
+        numa = np.ascontiguousarray(numa, dtype=abi.NODE_NUMA_DTYPE)
+        if idx is not None:
+            idx = np.ascontiguousarray(idx, dtype=np.uint32)
+        _chk(lib().or_nodes_numa_upsert(self._h, abi.ptr(idx), abi.ptr(numa), len(numa)), "nodes_numa_upsert")
+
+    def update_allocations(self, node_idx, allocs):
+        node_idx = np.ascontiguousarray(node_idx, dtype=np.uint32)
+        allocs = np.ascontiguousarray(allocs, dtype=abi.POD_ALLOCATION_DTYPE)
+        _chk(lib().or_numa_allocations_update(self._h, abi.ptr(node_idx), abi.ptr(allocs), len(allocs)), "alloc_update")
+
+    def release_allocations(self, node_idx, uids):
+        node_idx = np.ascontiguousarray(node_idx, dtype=np.uint32)
+        uids = np.ascontiguousarray(uids, dtype=np.uint64)
+        _chk(lib().or_numa_allocations_release(self._h, abi.ptr(node_idx), abi.ptr(uids), len(uids)), "alloc_release")
+
+    def allocation(self, node: int, uid: int):
+        out = np.zeros(1, abi.POD_ALLOCATION_DTYPE)
+        rc = lib().or_numa_allocation_get(self._h, node, uid, abi.ptr(out))
+        if rc < 0:
+            _chk(rc, "allocation_get")
+        return out[0] if rc == 1 else None
+
+    def set_hint_order(self, reverse: bool):
+        _chk(lib().or_set_hint_order(self._h, int(reverse)), "set_hint_order")
+
     def schedule(self, pods, seq=None, nthreads: int = 1):
         pods = np.ascontiguousarray(pods, dtype=abi.POD_DTYPE)
         if seq is None:
@@ -177,3 +217,17 @@ def estimate_node(node) -> tuple[int, int]:
 
 def tiebreak_intn(seed: int, seq: int, cnt: int) -> int:
     return lib().or_tiebreak_intn(seed, seq, cnt)
+
+
+def take_cpus_test(topology, max_ref, available, alloc_ref, alloc_excl, needed, bind, excl, strategy):
+    """takeCPUs on buildCPUTopologyForTest(*topology); returns (ok, sorted cpu list)."""
+    words = np.zeros(4, np.uint64)
+    for c in available:
+        words[c >> 6] |= np.uint64(1) << np.uint64(c & 63)
+    ref = np.ascontiguousarray(alloc_ref, dtype=np.int32)
+    ex = np.ascontiguousarray(alloc_excl, dtype=np.int32)
+    out = np.zeros(4, np.uint64)
+    rc = lib().or_take_cpus_test(*[int(x) for x in topology], int(max_ref), abi.ptr(words), abi.ptr(ref), abi.ptr(ex),
+                                 int(needed), int(bind), int(excl), int(strategy), abi.ptr(out))
+    cpus = [c for c in range(256) if (int(out[c >> 6]) >> (c & 63)) & 1]
+    return rc == 0, cpus

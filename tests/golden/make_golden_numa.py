@@ -1,0 +1,223 @@
+"""Transcribes the reference's own NodeNUMAResource test vectors into tests/golden/numa_takecpus.json.
+
+Data only (inputs and expected outputs typed in from the Go tests); no reference code is copied or run.
+Source: pkg/scheduler/plugins/nodenumaresource/cpu_accumulator_test.go
+  TestTakeFullPCPUs                          :59-173   (FullPCPUs, NUMAMostAllocated)
+  TestTakeFullPCPUsWithNUMALeastAllocated    :175-289  (FullPCPUs, NUMALeastAllocated)
+  TestCPUSpreadByPCPUs                       :291-299  (freeCPUs + spreadCPUs order)
+  TestTakeSpreadByPCPUs                      :301-361  (SpreadByPCPUs, NUMAMostAllocated)
+  TestTakeSpreadByPCPUsWithNUMALeastAllocated:373-433
+  TestTakeCPUsWithExclusivePolicy            :435-558
+  TestTakeCPUsWithMaxRefCount                :560-599  (sequence, maxRefCount 2)
+  TestTakeCPUsSortByRefCount                 :601-648  (sequence, maxRefCount 2)
+  TestTakePreferredCPUs                      :724-744  (first call only: plain takeCPUs)
+
+Topologies are buildCPUTopologyForTest(sockets, nodesPerSocket, coresPerNode, cpusPerCore) (:30-57).
+Run: python tests/golden/make_golden_numa.py
+"""
+import json
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def parse(s):
+    """cpuset.MustParse / NewCPUSet -> sorted list"""
+    if isinstance(s, list):
+        return sorted(s)
+    out = []
+    for part in s.split(","):
+        part = part.strip()
+        if not part:
+            continue
+        if "-" in part:
+            a, b = part.split("-")
+            out.extend(range(int(a), int(b) + 1))
+        else:
+            out.append(int(part))
+    return sorted(out)
+
+
+def case(src, name, topo, need, want, allocated=(), bind="FullPCPUs", excl="None", strategy="MostAllocated",
+         max_ref=1, alloc_excl=None, error=False):
+    return {"src": src, "name": name, "topology": list(topo), "max_ref": max_ref, "allocated": parse(list(allocated)
+            if not isinstance(allocated, str) else allocated), "alloc_excl": alloc_excl or "None", "needed": need,
+            "bind": bind, "excl": excl, "strategy": strategy, "want": parse(want), "want_error": error}
+
+
+T = "cpu_accumulator_test.go"
+cases = []
+# TestTakeFullPCPUs (Most) / ...WithNUMALeastAllocated
+full_most = [
+    ("allocate on non-NUMA node", (1, 1, 4, 2), [], 2, [0, 1]),
+    ("with allocated cpus", (1, 1, 4, 2), [0, 1], 2, [2, 3]),
+    ("allocate whole socket", (2, 1, 4, 2), [], 8, "0-7"),
+    ("allocate across socket", (2, 1, 4, 2), [], 12, "0-11"),
+    ("allocate whole socket with partially-allocated socket", (2, 1, 4, 2), [0, 1], 8, "8-15"),
+    ("allocate in the smallest idle socket", (2, 2, 4, 2), "0-5,16-23", 6, "24-29"),
+    ("allocate the most of CPUs on the same socket", (2, 2, 4, 2), "0-5,16-23", 12, "6-15,24-25"),
+    ("allocate from first socket", (2, 2, 4, 2), "0-3,8-11", 4, "4-7"),
+    ("allocate with less spread cpus", (2, 2, 2, 2), [0, 2, 4, 8, 12], 4, [10, 11, 14, 15]),
+    ("allocate with the most spread cpus", (2, 2, 2, 2), [0, 2, 4, 8, 10, 12], 6, [5, 6, 7, 13, 14, 15]),
+    ("allocate with the most spread cpus on the smallest idle cpus socket", (2, 2, 2, 2), [0, 2, 4, 8, 9, 10, 12], 6,
+     [6, 7, 11, 13, 14, 15]),
+]
+for n, topo, al, need, want in full_most:
+    cases.append(case(f"{T}:59-173 TestTakeFullPCPUs", n, topo, need, want, al))
+full_least = [
+    ("allocate on non-NUMA node", (1, 1, 4, 2), [], 2, [0, 1]),
+    ("with allocated cpus", (1, 1, 4, 2), [0, 1], 2, [2, 3]),
+    ("allocate whole socket", (2, 1, 4, 2), [], 8, "0-7"),
+    ("allocate across socket", (2, 1, 4, 2), [], 12, "0-11"),
+    ("allocate whole socket with partially-allocated socket", (2, 1, 4, 2), [0, 1], 8, "8-15"),
+    ("allocate in the most idle socket", (2, 2, 4, 2), "0-5,16-23", 6, "8-13"),
+    ("allocate the most of CPUs on the same socket", (2, 2, 4, 2), "0-5,16-23", 12, "6-15,24-25"),
+    ("allocate from second socket", (2, 2, 4, 2), "0-3,8-11", 4, "16-19"),
+    ("allocate with less spread cpus", (2, 2, 2, 2), [0, 2, 4, 8, 12], 4, [10, 11, 14, 15]),
+    ("allocate with the less spread cpus 2", (2, 2, 2, 2), [0, 2, 4, 8, 10, 12], 6, [6, 7, 14, 15, 1, 3]),
+    ("allocate with the most spread cpus on the most idle cpus socket 3", (2, 2, 4, 2), [0, 2, 4, 8, 9, 10, 12], 6,
+     [16, 17, 18, 19, 20, 21]),
+]
+for n, topo, al, need, want in full_least:
+    cases.append(case(f"{T}:175-289 TestTakeFullPCPUsWithNUMALeastAllocated", n, topo, need, want, al,
+                      strategy="LeastAllocated"))
+spread_most = [
+    ("allocate on non-NUMA node", (1, 1, 4, 2), [], 4, [0, 2, 4, 6]),
+    ("allocate satisfied the partially-allocated socket", (2, 1, 4, 2), [0, 2], 4, [1, 3, 4, 6]),
+    ("allocate cpus on full-free socket", (2, 1, 4, 2), [0, 1, 2, 3], 4, [8, 10, 12, 14]),
+    ("allocate most of CPUs in the same socket and overlapped-cores", (2, 1, 4, 2), [0, 2], 6, "1,3-7"),
+]
+for n, topo, al, need, want in spread_most:
+    cases.append(case(f"{T}:301-361 TestTakeSpreadByPCPUs", n, topo, need, want, al, bind="SpreadByPCPUs"))
+spread_least = [
+    ("allocate on non-NUMA node", (1, 1, 4, 2), [], 4, [0, 2, 4, 6]),
+    ("allocate satisfied the partially-allocated socket", (2, 1, 4, 2), [0, 2], 4, [8, 10, 12, 14]),
+    ("allocate cpus on full-free socket", (2, 1, 4, 2), [0, 1, 2, 3], 4, [8, 10, 12, 14]),
+    ("allocate most of CPUs in the same socket and overlapped-cores", (2, 1, 4, 2), [0, 2], 6,
+     [8, 10, 12, 14, 9, 11]),
+]
+for n, topo, al, need, want in spread_least:
+    cases.append(case(f"{T}:373-433 TestTakeSpreadByPCPUsWithNUMALeastAllocated", n, topo, need, want, al,
+                      bind="SpreadByPCPUs", strategy="LeastAllocated"))
+# TestTakeCPUsWithExclusivePolicy: allocated CPUs carry allocatedExclusivePolicy (default PCPULevel);
+# exclusivePolicy defaults to PCPULevel, bindPolicy to SpreadByPCPUs
+excl_cases = [
+    ("allocate cpus on full-free socket with PCPULevel", (2, 1, 4, 2), [0, 2], None, None, None, 4, [8, 10, 12, 14]),
+    ("allocate overlapped cpus with PCPULevel", (2, 1, 4, 2), [], None, None, None, 10, [0, 1, 2, 3, 4, 6, 8, 10, 12, 14]),
+    ("allocate cpus on large-size partially-allocated socket with PCPULevel", (2, 1, 8, 2), [0, 2], None, None, None, 4,
+     [4, 6, 8, 10]),
+    ("allocate cpus with none exclusive policy", (2, 1, 8, 2), [0, 2], None, "None", None, 4, [1, 3, 4, 6]),
+    ("allocate cpus on full-free socket with NUMANodeLevel", (2, 1, 4, 2), [0, 2], "NUMANodeLevel", "NUMANodeLevel",
+     None, 4, [8, 10, 12, 14]),
+    ("allocate cpus on partially-allocated socket without NUMANodeLevel", (2, 1, 4, 2), [0, 2], "NUMANodeLevel", "None",
+     None, 4, [1, 3, 4, 6]),
+    ("allocate cpus on full-free socket with NUMANodeLevel with PCPUs", (2, 1, 4, 2), [0, 2], "NUMANodeLevel",
+     "NUMANodeLevel", "FullPCPUs", 4, [8, 9, 10, 11]),
+    ("allocate cpus on partially-allocated socket without NUMANodeLevel with PCPUs", (2, 1, 4, 2), [0, 2],
+     "NUMANodeLevel", "None", "FullPCPUs", 4, [4, 5, 6, 7]),
+]
+for n, topo, al, aexcl, excl, bind, need, want in excl_cases:
+    # an unset exclusivePolicy ("") is defaulted to PCPULevel; CPUExclusivePolicyNone is the string "None"
+    e = "PCPULevel" if excl is None else excl
+    cases.append(case(f"{T}:435-558 TestTakeCPUsWithExclusivePolicy", n, topo, need, want, al,
+                      bind=bind or "SpreadByPCPUs", excl=e, alloc_excl=aexcl or "PCPULevel"))
+cases.append(case(f"{T}:724-744 TestTakePreferredCPUs", "takeCPUs spread 2", (2, 1, 16, 2), 2, [0, 2],
+                  bind="SpreadByPCPUs"))
+
+# sequences (maxRefCount 2): each step takes CPUs then addCPUs(..., PCPULevel)
+sequences = [
+    {"src": f"{T}:560-599 TestTakeCPUsWithMaxRefCount", "topology": [1, 1, 4, 2], "max_ref": 2,
+     "steps": [{"needed": 4, "bind": "FullPCPUs", "want": parse("0-3")},
+               {"needed": 5, "bind": "FullPCPUs", "want": parse("0,4-7")},
+               {"needed": 4, "bind": "FullPCPUs", "want": parse("2-5")}]},
+    {"src": f"{T}:601-648 TestTakeCPUsSortByRefCount", "topology": [1, 1, 16, 2], "max_ref": 2,
+     "steps": [{"needed": 16, "bind": "SpreadByPCPUs", "want": parse("0,2,4,6,8,10,12,14,16,18,20,22,24,26,28,30")},
+               {"needed": 16, "bind": "FullPCPUs", "want": parse("0-15")},
+               {"needed": 16, "bind": "SpreadByPCPUs", "want": parse("1,3,5,7,9,11,13,15,17,19,21,23,25,27,29,31")},
+               {"needed": 16, "bind": "FullPCPUs", "want": parse("16-31")}],
+     "final_available": []},
+]
+
+out = {"takecpus": cases, "sequences": sequences,
+       "spread_order": {"src": f"{T}:291-299 TestCPUSpreadByPCPUs", "topology": [2, 2, 4, 2], "needed": 8,
+                        "want": [0, 2, 4, 6, 8, 10, 12, 14, 16, 18, 20, 22, 24, 26, 28, 30,
+                                 1, 3, 5, 7, 9, 11, 13, 15, 17, 19, 21, 23, 25, 27, 29, 31]}}
+with open(os.path.join(HERE, "numa_takecpus.json"), "w") as f:
+    json.dump(out, f, indent=1)
+print(f"wrote {len(cases)} takeCPUs cases, {len(sequences)} sequences")
+
+# ---- plugin-level vectors: scoring_test.go --------------------------------------------------------
+S = "scoring_test.go"
+GI = 1 << 30
+
+
+def numa_node(cpu, mem_gi, policy, count):
+    """TestNUMANodeScore node: Capacity(cpu, memory) + numa-topology-policy label; options per scoring_test.go:255-272"""
+    cpu_milli, mem = cpu * 1000, mem_gi * GI
+    cores = cpu_milli // 1000 // 2 // count
+    return {"cpu_milli": cpu_milli, "memory": mem, "numa_policy": policy, "topology": [count, 1, cores, 2],
+            "zones": [[i, cpu_milli // count, mem // count] for i in range(count)]}
+
+
+def existing(node, uid, cpu, mem_gi, cpuset_pod):
+    """resourceManager.Update of an existing pod (scoring_test.go:274-293): cpuset 0..cpu-1 when LSR+Prod,
+    NUMANodeResources [{Node 0, container requests}]"""
+    return {"node": node, "uid": uid, "cpus": list(range(cpu)) if cpuset_pod else [],
+            "numa": [[0, cpu * 1000, mem_gi * GI]]}
+
+
+most = {"scoring": "MostAllocated", "weights": {"cpu": 1, "memory": 1}}
+score_cases = [
+    {"src": f"{S}:47-330 TestNUMANodeScore", "name": "single numa nodes score", "args": most,
+     "nodes": [numa_node(104, 256, "SingleNUMANode", 2), numa_node(64, 128, "SingleNUMANode", 1)],
+     "allocations": [], "pod": {"cpu": 21000, "memory": 40 * GI}, "filter": True, "want": [35, 31]},
+    {"src": f"{S}:47-330 TestNUMANodeScore", "name": "restricted numa nodes score", "args": most,
+     "nodes": [numa_node(104, 256, "Restricted", 2), numa_node(64, 128, "Restricted", 1)],
+     "allocations": [], "pod": {"cpu": 50000, "memory": 40 * GI}, "filter": True, "want": [63, 54]},
+    {"src": f"{S}:47-330 TestNUMANodeScore", "name": "single numa nodes score with same capacity but different requested",
+     "args": most, "nodes": [numa_node(104, 256, "SingleNUMANode", 2)] * 3,
+     "allocations": [existing(0, 0, 4, 8, False), existing(1, 0, 8, 32, False), existing(2, 0, 32, 40, False)],
+     "pod": {"cpu": 4000, "memory": 40 * GI}, "filter": True, "want": [19, 19, 19]},
+    {"src": f"{S}:47-330 TestNUMANodeScore",
+     "name": "single numa nodes score with same capacity but different requested and LSR", "args": most,
+     "nodes": [numa_node(104, 256, "SingleNUMANode", 2)] * 3,
+     "allocations": [existing(0, 0, 4, 8, False), existing(0, 123, 4, 8, True),
+                     existing(1, 0, 8, 32, False), existing(1, 123, 8, 32, True),
+                     existing(2, 0, 16, 40, False), existing(2, 123, 16, 40, True)],
+     "pod": {"cpu": 4000, "memory": 40 * GI, "qos": "LSR", "prod": True}, "filter": True, "want": [23, 27, 34]},
+]
+
+
+def plain_node(topo, labels=None):
+    """TestPlugin_Score node (scoring_test.go:478-496): allocatable cpu = |CPUs|, memory 512Gi; options hold only
+    the CPUTopology (MaxRefCount defaulted to 1 by UpdateTopologyOptions)"""
+    s, n, c, p = topo
+    d = {"cpu_milli": s * n * c * p * 1000, "memory": 512 * GI, "numa_policy": "", "topology": list(topo),
+         "zones": []}
+    d.update(labels or {})
+    return d
+
+
+cpu_most = {"scoring": "MostAllocated", "weights": {"cpu": 1}}
+plugin_score = [
+    ("score with full empty node FullPCPUs", (2, 1, 4, 2), "FullPCPUs", 4, {}, 25),
+    ("score with satisfied node FullPCPUs", (2, 1, 4, 2), "FullPCPUs", 8, {}, 50),
+    ("score with full empty node SpreadByPCPUs", (2, 1, 4, 2), "SpreadByPCPUs", 4, {}, 25),
+    ("score with exceed socket FullPCPUs", (2, 1, 4, 2), "FullPCPUs", 16, {}, 100),
+    ("score with satisfied socket FullPCPUs", (2, 2, 4, 2), "FullPCPUs", 16, {}, 50),
+    ("score with full empty socket SpreadByPCPUs", (2, 1, 4, 2), "SpreadByPCPUs", 4, {}, 25),
+    ("score with Node NUMA Allocate Strategy", (2, 1, 4, 2), "SpreadByPCPUs", 2,
+     {"numa_allocate_strategy": "LeastAllocated"}, 12),
+    ("score with Node CPU Bind Policy", (2, 1, 4, 2), "SpreadByPCPUs", 8, {"node_cpu_bind": "FullPCPUsOnly"}, 50),
+]
+for name, topo, pref, n, labels, want in plugin_score:
+    # the Go test injects preFilterState{requestCPUBind, preferredCPUBindPolicy, numCPUsNeeded, requests{cpu}};
+    # an LSR Prod pod with that preferred policy and cpu request makes PreFilter produce the same state
+    score_cases.append({"src": f"{S}:332-554 TestPlugin_Score", "name": name, "args": cpu_most,
+                        "nodes": [plain_node(topo, labels)], "allocations": [],
+                        "pod": {"cpu": n * 1000, "qos": "LSR", "prod": True, "preferred": pref},
+                        "filter": False, "want": [want]})
+
+with open(os.path.join(HERE, "numa_score.json"), "w") as f:
+    json.dump({"cases": score_cases}, f, indent=1)
+print(f"wrote {len(score_cases)} NodeNUMAResource score cases")
