@@ -1,9 +1,10 @@
 """Benchmark of the koord-scheduler Filter/Score hot path on MI355X (BASELINE.json metric).
 
 A step = one pass of the hot path over one batch of synthetic pending pods: the scheduleOne loop
-(Fit + LoadAware Filter over every node, Fit LeastAllocated + LoadAware Score, selectHost, assume +
-Reserve) for `--pods-per-step` pods, sequentially, against the 50k-node synthetic cluster (weak
-scaling: 50k nodes per GPU, node-sharded, RCCL all-gather of per-shard candidate lists per batch).
+(NodeResourcesFit + LoadAwareScheduling + NodeNUMAResource Filter over every node, their Scores, selectHost,
+assume + Reserve incl. NUMA allocation and cpuset selection) for `--pods-per-step` pods, sequentially, against
+the 50k-node synthetic C3 cluster (weak scaling: 50k nodes per GPU, node-sharded, RCCL all-gather of per-shard
+candidate lists per batch). `--profile la-fit` drops NodeNUMAResource (the C2 plugin set).
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
@@ -50,6 +51,7 @@ def main() -> None:
     ap.add_argument("--batch", type=int, default=128)
     ap.add_argument("--cpu-sample-pods", type=int, default=400)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--profile", choices=["c3", "la-fit"], default="c3")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -73,20 +75,28 @@ def main() -> None:
     n_nodes = args.nodes_per_gpu * world
     total_pods = (args.warmup + args.steps) * args.pods_per_step
     cluster = synth.make_cluster(n_nodes, total_pods, config_id=2)
-    cfg = config.make_config(n_nodes, device=local_rank, batch_size=args.batch)
+    numa = args.profile == "c3"
+    if numa:
+        synth.make_numa(cluster)
+    from koordinator_amd import abi
+    cfg = config.make_config(n_nodes, device=local_rank, batch_size=args.batch,
+                             enabled=abi.GS_ENABLE_ALL if numa else abi.GS_ENABLE_LA_FIT)
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         threads = min(os.cpu_count() or 1, int(os.environ.get("OMP_NUM_THREADS", "16")), 16)
         r16 = cpu_baseline(cluster, cfg, args.cpu_sample_pods, threads)
         r1 = cpu_baseline(cluster, cfg, max(20, args.cpu_sample_pods // 8), 1)
+        nall = len(os.sched_getaffinity(0)) or 1
+        rall = cpu_baseline(cluster, cfg, args.cpu_sample_pods, nall) if nall > threads else r16
         cpu = {"value": r16["evals_per_s"], "unit": "evals/s", "cores": threads, "kind": "port",
                "sample": f"first {args.cpu_sample_pods} pods of the same {n_nodes}-node cluster, sequential "
                          f"scheduleOne with Filter/Score fanned out over {threads} threads "
                          f"(parallelize.Until emulation, parallelism={threads}); CPU restatement of the "
                          f"reference Go path (oracle/), not the Go binary",
                "pods_per_s": r16["pods_per_s"], "seconds": r16["seconds"],
-               "single_thread_evals_per_s": r1["evals_per_s"]}
+               "single_thread_evals_per_s": r1["evals_per_s"],
+               "all_cores": {"threads": nall, "evals_per_s": rall["evals_per_s"], "pods_per_s": rall["pods_per_s"]}}
 
     eng = Engine(cfg)
     if world > 1:
@@ -147,9 +157,13 @@ def main() -> None:
             "data": "synthetic",
             "pods_per_s": pods_timed / dt,
             "config": {
-                "workload": f"C3-profile-LA+Fit: {n_nodes} nodes ({args.nodes_per_gpu}/GPU) x {P} pods/step, "
-                            "sequential scheduleOne with NodeResourcesFit(LeastAllocated)+LoadAwareScheduling "
-                            "filter+score, selectHost, assume+Reserve; NodeNUMAResource not yet on the path",
+                "workload": (f"C3: {n_nodes} nodes ({args.nodes_per_gpu}/GPU) x {P} pods/step, sequential scheduleOne "
+                             "with NodeResourcesFit(LeastAllocated) + LoadAwareScheduling + NodeNUMAResource filter+"
+                             "score (30% NUMA-policy nodes, 20% LSE/LSR cpuset pods), selectHost, assume+Reserve"
+                             if numa else
+                             f"C2 plugin set at C3 scale: {n_nodes} nodes ({args.nodes_per_gpu}/GPU) x {P} pods/step, "
+                             "NodeResourcesFit(LeastAllocated)+LoadAwareScheduling filter+score, selectHost, "
+                             "assume+Reserve"),
                 "nodes": n_nodes, "pods_per_step": P, "batch": args.batch, "parallelism": f"node-shard x{world}",
                 "level_list_cap": 2048,
             },
@@ -164,8 +178,8 @@ def main() -> None:
                 "bytes_per_eval": st["node_row_bytes"],
                 "avg_launch_us": avg_launch_ms * 1e3,
                 "pairs_per_launch": pairs_per_launch,
-                "note": "algorithmic bytes = 96 B node row per pod x node eval (un-batched convention); "
-                        "the kernel reads each row once per batch of up to 128 pods, so frac > 1 means reuse",
+                "note": f"algorithmic bytes = {st['node_row_bytes']} B node row per pod x node eval (un-batched "
+                        "convention); the kernel reads each row once per group of 16 pods, so frac > 1 means reuse",
             },
             "breakdown_ms": {"eval": st["eval_ms"], "cand": st["cand_ms"], "commit": st["commit_ms"],
                              "exchange": st["exchange_ms"], "batches": st["batches"], "cuts": st["cuts"],

@@ -381,7 +381,8 @@ int gs_pods_unassign(gs_ctx* ctx, const uint32_t* node_idx, const gs_pod* pods, 
  * RunScorePlugins (Fit.Score least_allocated.go, LoadAware.Score load_aware.go:269-335) with profile weights.
  * scores[p*N+n]  = weighted total, or -1 when the node is infeasible (may be NULL)
  * codes[p*N+n]   = GS_FAIL_* bits of every failing filter (may be NULL)
- * plugin_scores[(p*N+n)*GS_NUM_PLUGINS + k] = unweighted score of plugin k, for every node (may be NULL) */
+ * plugin_scores[(p*N+n)*GS_NUM_PLUGINS + k] = unweighted score of plugin k, for every node (may be NULL);
+ *   NodeNUMAResource's entry is 0 where its own Filter fails (the reference never scores such a node) */
 int gs_evaluate(gs_ctx* ctx, const gs_pod* pods, uint32_t npods, int16_t* scores, uint16_t* codes,
                 int16_t* plugin_scores);
 

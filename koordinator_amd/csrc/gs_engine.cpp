@@ -931,7 +931,8 @@ int gs_create(const gs_config* cfg, gs_ctx** out) {
     (void)hipMemset(c->d_stamps, 0, 64);
   }
   if ((e = hipDeviceSynchronize()) != hipSuccess) return bail("hipDeviceSynchronize", e);
-  c->stats.node_row_bytes = 3 * 8 + 4 + 2 * 8 + 2 * 8 + 2 * 8 + 2 * 8 + 4;   // 96 B
+  // 96 B (LoadAware + Fit row), + 192 B NodeNUMAResource columns when enabled
+  c->stats.node_row_bytes = 3 * 8 + 4 + 2 * 8 + 2 * 8 + 2 * 8 + 2 * 8 + 4 + (c->numa_on ? 18 * 8 + 12 * 4 : 0);
   *out = c;
   return GS_OK;
 }
@@ -1253,7 +1254,7 @@ int gs_get_stats(gs_ctx* c, gs_stats* out) {
 
 int gs_reset_stats(gs_ctx* c) {
   if (!c) return GS_EINVAL;
-  uint64_t rb = c->stats.node_row_bytes;
+  uint64_t rb = c->stats.node_row_bytes;   // keep
   c->stats = gs_stats{};
   c->stats.node_row_bytes = rb;
   c->stats.shard_begin = c->n0;

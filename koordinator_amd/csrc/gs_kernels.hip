@@ -159,7 +159,7 @@ __device__ __forceinline__ PairOut eval_pair(const Row& r, const PodVec& p, cons
     NumaOut no;
     if (LDS_SCALARS) no = numa_eval(r.nr, p, pf, SlotsLds{r, m}, pf.enabled & 0x10u, pf.enabled & 0x20u);
     else no = numa_eval(r.nr, p, pf, SlotsHbm{r, m}, pf.enabled & 0x10u, pf.enabled & 0x20u);
-    o.code |= no.reason << GS_FAIL_NUMA_SHIFT;
+    if (pf.enabled & 0x10u) o.code |= no.reason << GS_FAIL_NUMA_SHIFT;
     if (!FULL && o.code) return o;
     o.numa = no.reason ? 0 : no.score;
   }

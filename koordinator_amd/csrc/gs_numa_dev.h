@@ -399,6 +399,8 @@ __device__ __forceinline__ NumaOut numa_eval(const NumaRow& r, const PodVec& p, 
   }
   if (!fail && rb) {   // allocateCPUSet (resource_manager.go:273-360), counted
     if (cnt_sel(r.tfree, bind, reqflag) < p.num_cpus) fail = true;
+    // satisfiedRequiredCPUBindPolicy: FullPCPUs over full cores is met iff the count is a multiple of CPUsPerCore
+    if (!fail && !o.zkeys && reqflag && bind == BIND_FULL && cpc && p.num_cpus % cpc) fail = true;
     if (!fail && o.zkeys) {
       int sum = 0;
 #pragma unroll

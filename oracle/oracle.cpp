@@ -505,7 +505,9 @@ PairResult eval_pair(const or_cluster& c, const gs_pod& pod, const orn::PreState
   if (en & GS_ENABLE_NUMA_FILTER) res.code |= numa_filter(c, st, i, &aff);
   if (en & GS_ENABLE_FIT_SCORE) res.fit = fit_score(c.cfg.fit, pod, s.node);
   if (en & GS_ENABLE_LA_SCORE) res.la = loadaware_score(c, pod, s);
-  if (en & GS_ENABLE_NUMA_SCORE) res.numa = orn::score(c.numa_args, st, c.numa[i], node_view(s.node), aff);
+  // gs_evaluate reports NodeNUMAResource's score as 0 where its own Filter fails (such nodes are never scored)
+  if ((en & GS_ENABLE_NUMA_SCORE) && !(res.code & GS_FAIL_NUMA_MASK))
+    res.numa = orn::score(c.numa_args, st, c.numa[i], node_view(s.node), aff);
   return res;
 }
 
