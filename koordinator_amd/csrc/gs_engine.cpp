@@ -123,6 +123,10 @@ struct gs_ctx {
   std::shared_ptr<TopoClass> empty_topo = std::make_shared<TopoClass>();
   std::unordered_map<uint64_t, uint32_t> numa_uid_node;   // pods holding a NodeAllocation record
   bool numa_on = false;
+  // the shard's nodes with a NUMA topology policy (eval_numa_kernel's work list), rebuilt when policies change
+  uint32_t* d_numa_idx = nullptr;
+  uint32_t numa_n = 0;
+  bool numa_idx_stale = true;
 };
 
 namespace {
@@ -673,7 +677,20 @@ int run_batch(gs_ctx* c, const gs_pod* pods, int b, int* committed_out) {
   for (int i = 0; i < b; ++i) prod_cols |= (c->h_pods[i].flags & PF_PROD_SCORE) ? 1 : 0;
   uint32_t len = c->n1 - c->n0;
   HIP_TRY(c, hipEventRecord(c->ev[0], c->st));
-  HIP_TRY(c, launch_eval(c->mv, c->d_pods, b, c->pf, c->n0, c->n1, c->d_S, c->ld, prod_cols, c->st));
+  if (c->numa_on && c->numa_idx_stale) {
+    std::vector<uint32_t> idx;
+    for (uint32_t n = c->n0; n < c->n1; ++n)
+      if (c->numa[n].cfg.numa_topology_policy != GS_NUMA_POLICY_NONE) idx.push_back(n);
+    if (c->d_numa_idx) { HIP_TRY(c, hipStreamSynchronize(c->st)); (void)hipFree(c->d_numa_idx); c->d_numa_idx = nullptr; }
+    c->numa_n = (uint32_t)idx.size();
+    if (c->numa_n) {
+      HIP_TRY(c, hipMalloc(&c->d_numa_idx, 4 * idx.size()));
+      HIP_TRY(c, hipMemcpy(c->d_numa_idx, idx.data(), 4 * idx.size(), hipMemcpyHostToDevice));
+    }
+    c->numa_idx_stale = false;
+  }
+  HIP_TRY(c, launch_eval(c->mv, c->d_pods, b, c->pf, c->n0, c->n1, c->d_S, c->ld, prod_cols, c->d_numa_idx, c->numa_n,
+                         c->st));
   HIP_TRY(c, hipEventRecord(c->ev[1], c->st));
   HIP_TRY(c, launch_cand(c->d_S, c->ld, len, c->n0, b, c->max_score, d_lists, d_hdrs, c->st));
   HIP_TRY(c, hipEventRecord(c->ev[2], c->st));
@@ -953,7 +970,7 @@ int gs_destroy(gs_ctx* c) {
   if (c->comm) ncclCommDestroy(c->comm);
   if (c->st) (void)hipStreamSynchronize(c->st);
   void* dev[] = {c->d_i64, c->d_i32, c->d_pods, c->d_seq, c->d_S, c->d_xchg_send, c->d_xchg_recv, c->d_out,
-                 c->d_committed, c->d_rowstat, c->d_sel, c->d_stage_idx, c->d_stage_rows};
+                 c->d_committed, c->d_rowstat, c->d_sel, c->d_stage_idx, c->d_stage_rows, c->d_numa_idx};
   for (void* p : dev)
     if (p) (void)hipFree(p);
   void* host[] = {c->h_pods, c->h_seq, c->h_out, c->h_committed, c->h_stage_idx, c->h_stage_rows, c->h_xchg_send,
@@ -1095,6 +1112,8 @@ int gs_schedule(gs_ctx* c, const gs_pod* pods, uint32_t npods, const uint64_t* s
     for (int j = 0; j < b; ++j) {
       c->h_pods[j] = prep_pod(c, pods[i + j]);
       c->h_seq[j] = seq ? seq[i + j] : (uint64_t)(i + j);
+      // a cpuset pod's Reserve (takeCPUs) runs on the host: the batch ends with it
+      if (c->numa_on && (c->h_pods[j].numa & PN_BIND)) { b = j + 1; break; }
     }
     HIP_TRY(c, hipMemcpyAsync(c->d_pods, c->h_pods, sizeof(PodVec) * b, hipMemcpyHostToDevice, c->st));
     HIP_TRY(c, hipMemcpyAsync(c->d_seq, c->h_seq, 8 * b, hipMemcpyHostToDevice, c->st));
@@ -1157,6 +1176,7 @@ int gs_nodes_numa_upsert(gs_ctx* c, const uint32_t* idx, const gs_node_numa* nn,
     if (x.has_options && x.topology >= (int32_t)c->topos.size())
       return fail(c, GS_EINVAL, "node %u: topology id %d not registered", i, x.topology);
     NumaNode& st = c->numa[i];
+    if (st.cfg.numa_topology_policy != x.numa_topology_policy) c->numa_idx_stale = true;
     st.cfg = x;
     st.topo = !x.has_options ? nullptr : (x.topology >= 0 ? c->topos[x.topology] : c->empty_topo);
     mark_dirty(c, i);
@@ -1233,6 +1253,7 @@ int gs_comm_init_rccl(gs_ctx* c, const uint8_t id[128], int nranks, int rank) {
   c->nranks = nranks;
   c->rank = rank;
   set_shard(c);
+  c->numa_idx_stale = true;
   return alloc_exchange(c);
 }
 
@@ -1243,6 +1264,7 @@ int gs_comm_init_callback(gs_ctx* c, int nranks, int rank, gs_allgather_fn fn, v
   c->nranks = nranks;
   c->rank = rank;
   set_shard(c);
+  c->numa_idx_stale = true;
   return alloc_exchange(c);
 }
 

@@ -78,8 +78,10 @@ struct CommitArgs {
 hipError_t set_kernel_attributes();
 hipError_t launch_node_prep(const MirrorView& m, uint32_t n0, uint32_t n1, int64_t now, int32_t filter_expired,
                             int32_t has_exp, int64_t exp_ns, hipStream_t st);
+// NodeNUMAResource profiles: numa_idx lists the shard's nodes with a NUMA topology policy (ascending)
 hipError_t launch_eval(const MirrorView& m, const PodVec* pods, int npods, const Profile& pf, uint32_t n0, uint32_t n1,
-                       int16_t* S, uint32_t ld, int prod_cols, hipStream_t st);
+                       int16_t* S, uint32_t ld, int prod_cols, const uint32_t* numa_idx, uint32_t numa_n,
+                       hipStream_t st);
 hipError_t launch_eval_full(const MirrorView& m, const PodVec* pods, int npods, const Profile& pf, uint32_t N,
                             int16_t* scores, uint16_t* codes, int16_t* plugin, int prod_cols, hipStream_t st);
 hipError_t launch_cand(const int16_t* S, uint32_t ld, uint32_t len, uint32_t n0, int npods, int max_score,

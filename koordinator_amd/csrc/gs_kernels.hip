@@ -129,7 +129,9 @@ struct SlotsLds {
 
 // Filter (Fit + LoadAware) and Score (Fit LeastAllocated + LoadAware) of one pod on one node.
 // LDS_SCALARS: scalar free columns come from r.free[3..6] (the commit's LDS copy) instead of HBM.
-template <bool FULL, bool LDS_SCALARS>
+// NUMA_POLICY_NODES = false: NodeNUMAResource's topology-policy path is compiled out (eval_kernel routes those
+// nodes to eval_numa_kernel)
+template <bool FULL, bool LDS_SCALARS, bool NUMA_POLICY_NODES = true>
 __device__ __forceinline__ PairOut eval_pair(const Row& r, const PodVec& p, const Profile& pf, const MirrorView& m) {
   PairOut o{0u, 0, 0, 0};
   // ---- [upstream] noderesources Fit.Filter -> fitsRequest
@@ -157,8 +159,8 @@ __device__ __forceinline__ PairOut eval_pair(const Row& r, const PodVec& p, cons
   // ---- NodeNUMAResource Filter (+ Admit) and Score (gs_numa_dev.h)
   if (pf.enabled & 0x30u) {
     NumaOut no;
-    if (LDS_SCALARS) no = numa_eval(r.nr, p, pf, SlotsLds{r, m}, pf.enabled & 0x10u, pf.enabled & 0x20u);
-    else no = numa_eval(r.nr, p, pf, SlotsHbm{r, m}, pf.enabled & 0x10u, pf.enabled & 0x20u);
+    if (LDS_SCALARS) no = numa_eval<NUMA_POLICY_NODES>(r.nr, p, pf, SlotsLds{r, m}, pf.enabled & 0x10u, pf.enabled & 0x20u);
+    else no = numa_eval<NUMA_POLICY_NODES>(r.nr, p, pf, SlotsHbm{r, m}, pf.enabled & 0x10u, pf.enabled & 0x20u);
     if (pf.enabled & 0x10u) o.code |= no.reason << GS_FAIL_NUMA_SHIFT;
     if (!FULL && o.code) return o;
     o.numa = no.reason ? 0 : no.score;
@@ -237,11 +239,32 @@ __global__ void __launch_bounds__(256) eval_kernel(MirrorView m, const PodVec* _
   Row row;
   load_row(m, ok ? n0 + local : n0, prod_cols, NUMA, row);
   if (!NUMA) pf.enabled &= ~0x30u;
+  // nodes with a NUMA topology policy are evaluated by eval_numa_kernel (compacted, divergence-free)
+  if (NUMA && ok && ((row.nr.nflags >> NF_POLICY_SHIFT) & 3u)) return;
   const int k0 = blockIdx.y * PODS_PER_BLOCK;
   const int k1 = min(npods, k0 + PODS_PER_BLOCK);
   for (int k = k0; k < k1; ++k) {
-    PairOut o = eval_pair<false, false>(row, pods[k], pf, m);
+    PairOut o = eval_pair<false, false, false>(row, pods[k], pf, m);
     S[(size_t)k * ld + local] = ok ? (int16_t)total_score(o, pf) : (int16_t)-1;
+  }
+}
+
+// The NUMA-topology-policy nodes of the shard (host-maintained ascending index list): hints over zone subsets,
+// the topology-manager merge, Allocate by hint. Same (node x 16 pods) tiling as eval_kernel over the list.
+__global__ void __launch_bounds__(256) eval_numa_kernel(MirrorView m, const PodVec* __restrict__ pods, int npods,
+                                                        Profile pf, const uint32_t* __restrict__ idx, uint32_t nidx,
+                                                        uint32_t n0, int16_t* __restrict__ S, uint32_t ld,
+                                                        int prod_cols) {
+  const uint32_t t = blockIdx.x * 256 + threadIdx.x;
+  if (t >= nidx) return;
+  const uint32_t node = idx[t];
+  Row row;
+  load_row(m, node, prod_cols, true, row);
+  const int k0 = blockIdx.y * PODS_PER_BLOCK;
+  const int k1 = min(npods, k0 + PODS_PER_BLOCK);
+  for (int k = k0; k < k1; ++k) {
+    PairOut o = eval_pair<false, false, true>(row, pods[k], pf, m);
+    S[(size_t)k * ld + (node - n0)] = (int16_t)total_score(o, pf);
   }
 }
 
@@ -930,15 +953,20 @@ hipError_t launch_node_prep(const MirrorView& m, uint32_t n0, uint32_t n1, int64
 }
 
 hipError_t launch_eval(const MirrorView& m, const PodVec* pods, int npods, const Profile& pf, uint32_t n0, uint32_t n1,
-                       int16_t* S, uint32_t ld, int prod_cols, hipStream_t st) {
+                       int16_t* S, uint32_t ld, int prod_cols, const uint32_t* numa_idx, uint32_t numa_n,
+                       hipStream_t st) {
   uint32_t len = n1 - n0;
   uint32_t gx = (len + 255) / 256;
   uint32_t gy = (npods + PODS_PER_BLOCK - 1) / PODS_PER_BLOCK;
   if (gx == 0 || gy == 0) return hipSuccess;
-  if (pf.enabled & 0x30u)
+  if (pf.enabled & 0x30u) {
     hipLaunchKernelGGL(eval_kernel<true>, dim3(gx, gy), dim3(256), 0, st, m, pods, npods, pf, n0, n1, S, ld, prod_cols);
-  else
+    if (numa_n)
+      hipLaunchKernelGGL(eval_numa_kernel, dim3((numa_n + 255) / 256, gy), dim3(256), 0, st, m, pods, npods, pf,
+                         numa_idx, numa_n, n0, S, ld, prod_cols);
+  } else {
     hipLaunchKernelGGL(eval_kernel<false>, dim3(gx, gy), dim3(256), 0, st, m, pods, npods, pf, n0, n1, S, ld, prod_cols);
+  }
   return hipGetLastError();
 }
 

@@ -101,18 +101,9 @@ __device__ __forceinline__ int32_t sdiv(int32_t a, int32_t b) {
   return q;
 }
 
-// IterateBitMasks order over zone slots (bitmask.go:206-222) for 1..4 zones
-__constant__ uint8_t kMaskOrder[4][15] = {
-    {1},
-    {1, 2, 3},
-    {1, 2, 4, 3, 5, 6, 7},
-    {1, 2, 4, 8, 3, 5, 9, 6, 10, 12, 7, 11, 13, 14, 15}};
-
-struct HintL {
-  uint8_t mask[15];
-  int16_t score[15];
-  int n;
-};
+// IterateBitMasks order over zone slots (bitmask.go:206-222) for 1..4 zones, 4 bits per position:
+//   1 zone: 1 | 2 zones: 1 2 3 | 3 zones: 1 2 4 3 5 6 7 | 4 zones: 1 2 4 8 3 5 9 6 10 12 7 11 13 14 15
+__constant__ uint64_t kMaskOrderPacked[4] = {0x1ull, 0x321ull, 0x7653421ull, 0xFEDB7CA69538421ull};
 
 __device__ __forceinline__ bool narrower(uint32_t a, uint32_t b) {   // bitmask.IsNarrowerThan
   int ca = __popc(a), cb = __popc(b);
@@ -123,7 +114,9 @@ __device__ __forceinline__ bool narrower(uint32_t a, uint32_t b) {   // bitmask.
 // do_score: Score with that affinity (none when the filter is off, as in the reference without a Filter call);
 // want_alloc: fill the Reserve allocation.
 // `alloc[s]`/`free[s]` give NodeInfo.Allocatable / Allocatable-Requested for slots 0..2 and the scalars.
-template <class Slots>
+// POLICY_NODES = false compiles only the path of nodes without a NUMA topology policy (the caller routes
+// policy nodes to a kernel of their own); such a call on a policy node returns with reason 0 and no score.
+template <bool POLICY_NODES = true, class Slots>
 __device__ __forceinline__ NumaOut numa_eval(const NumaRow& r, const PodVec& p, const Profile& pf, const Slots& sl,
                                              bool do_filter, bool do_score) {
   NumaOut o{};
@@ -212,6 +205,7 @@ __device__ __forceinline__ NumaOut numa_eval(const NumaRow& r, const PodVec& p, 
   }
 
   // ---- NUMA-policy node
+  if (!POLICY_NODES) return o;
   const int nz = (nf >> NF_ZONES_SHIFT) & 7;
   if (do_filter && nz == 0) { o.reason = GS_NUMA_MISSING_NUMA_RESOURCES; return o; }
   const uint32_t nf2 = r.nflags2;
@@ -254,14 +248,17 @@ __device__ __forceinline__ NumaOut numa_eval(const NumaRow& r, const PodVec& p, 
         }
       }
     }
-    HintL lc, lm;
-    lc.n = lm.n = 0;
+    // hint lists as bitmaps over IterateBitMasks positions (bit mi = the mi-th mask of the order), hint scores
+    // (<= 100) packed 7 bits per position: no dynamically indexed arrays, nothing spills to scratch
+    const uint64_t order = kMaskOrderPacked[nz - 1];
+    uint32_t lc = 0, lm = 0;
+    uint64_t sc_lo = 0, sc_hi = 0;
     int min_c = nz, min_m = nz;
     bool tot_c_any = false, tot_m_any = false;
     if (!nil_hints) {
       const int nmasks = (1 << nz) - 1;
       for (int mi = 0; mi < nmasks; ++mi) {
-        const uint32_t mk = kMaskOrder[nz - 1][mi];
+        const uint32_t mk = (uint32_t)(order >> (4 * mi)) & 15u;
         int64_t tc = 0, tm = 0, fc = 0, fm = 0;
         bool kc = false, km = false;
 #pragma unroll
@@ -285,66 +282,62 @@ __device__ __forceinline__ NumaOut numa_eval(const NumaRow& r, const PodVec& p, 
           ns += (pf.numa_hint_most ? mr_score(rq, al) : lr_score(rq, al)) * w;
           ws += w;
         }
-        const int16_t hs = (int16_t)(ws ? sdiv(ns, ws) : 0);
+        const uint64_t hs = (uint64_t)(ws ? sdiv(ns, ws) : 0);
+        if (mi < 9) sc_lo |= hs << (7 * mi);
+        else sc_hi |= hs << (7 * (mi - 9));
         const int cnt = __popc(mk);
         // generateHints: memory group first, then cpu (resource_manager.go:464-476, 499-532)
         if (has_mem) {
           if (km) tot_m_any = true;
           if (tm >= mem) {
             if (cnt < min_m) min_m = cnt;
-            if (fm >= mem) { lm.mask[lm.n] = (uint8_t)mk; lm.score[lm.n] = hs; ++lm.n; }
+            if (fm >= mem) lm |= 1u << mi;
           }
         }
         if (has_cpu) {
           if (kc) tot_c_any = true;
           if (tc >= pcpu) {
             if (cnt < min_c) min_c = cnt;
-            if (fc >= pcpu) { lc.mask[lc.n] = (uint8_t)mk; lc.score[lc.n] = hs; ++lc.n; }
+            if (fc >= pcpu) lc |= 1u << mi;
           }
         }
       }
     }
-    // filterProvidersHints (policy.go:98-126): lists in resource-name order cpu, memory
-    // list kinds: 0 absent, 1 hints, 2 empty-list marker {nil, false}
-    const int kc_kind = nil_hints ? 0 : (lc.n ? 1 : ((has_cpu && tot_c_any) ? 2 : 0));
-    const int km_kind = nil_hints ? 0 : (lm.n ? 1 : ((has_mem && tot_m_any) ? 2 : 0));
+    auto mask_at = [&](int mi) -> uint32_t { return (uint32_t)(order >> (4 * mi)) & 15u; };
+    auto score_at = [&](int mi) -> int32_t {
+      return (int32_t)((mi < 9 ? sc_lo >> (7 * mi) : sc_hi >> (7 * (mi - 9))) & 127u);
+    };
+    // filterProvidersHints (policy.go:98-126): lists in resource-name order cpu, memory.
+    // kind: 0 absent, 1 hints, 2 the empty-list marker {nil, false}
+    const int kc_kind = nil_hints ? 0 : (lc ? 1 : ((has_cpu && tot_c_any) ? 2 : 0));
+    const int km_kind = nil_hints ? 0 : (lm ? 1 : ((has_mem && tot_m_any) ? 2 : 0));
     const bool single = policy == GS_NUMA_POLICY_SINGLE_NUMA_NODE;
-    // list entry i of list L: (has_mask, mask, preferred, score); a "none" list is the preferred any-numa hint
-    const bool no_lists = kc_kind == 0 && km_kind == 0;
-    auto entry = [&](int kind, const HintL& L, int minsz, int i, bool& has, uint32_t& mk, bool& pref, int32_t& sc) {
-      if (kind == 1) { has = true; mk = L.mask[i]; pref = __popc(mk) == minsz; sc = L.score[i]; }
-      else if (kind == 2) { has = false; mk = 0; pref = false; sc = 0; }
-      else { has = false; mk = 0; pref = true; sc = 0; }
-    };
-    auto keep = [&](bool has, uint32_t mk, bool pref) {   // filterSingleNumaHints (policy_single_numa_node.go:36-52)
-      if (!single) return true;
-      return pref && (!has || __popc(mk) == 1);
-    };
-    // mergeFilteredHints (policy.go:128-186)
+    const bool no_lists = kc_kind == 0 && km_kind == 0;   // empty map: one preferred any-numa hint
+    // a list as a sequence of entries: kind 1 = its set bits, kind 2 / absent = a single pseudo entry (bit 31)
+    const uint32_t seq0 = kc_kind == 1 ? lc : 0x80000000u;
+    const uint32_t seq1 = km_kind == 1 ? lm : 0x80000000u;
+    const bool use0 = no_lists || kc_kind != 0, use1 = !no_lists && km_kind != 0;
+    // mergeFilteredHints (policy.go:128-186) with filterSingleNumaHints for SingleNUMANode
     bool b_has = true, b_pref = false;
     uint32_t b_mask = full_mask;
     int32_t b_score = 0;
-    const int n0 = no_lists ? 1 : (kc_kind == 1 ? lc.n : (kc_kind == 2 ? 1 : 1));
-    const int n1 = no_lists ? 1 : (km_kind == 1 ? lm.n : (km_kind == 2 ? 1 : 1));
-    for (int i = 0; i < n0; ++i) {
-      bool h0, p0;
-      uint32_t m0;
-      int32_t s0;
-      if (no_lists) { h0 = false; m0 = 0; p0 = true; s0 = 0; }
-      else if (kc_kind) entry(kc_kind, lc, min_c, i, h0, m0, p0, s0);
-      else { h0 = false; m0 = 0; p0 = true; s0 = 0; }   // absent list: identity element of the AND
-      const bool use0 = no_lists || kc_kind != 0;
-      if (use0 && !keep(h0, m0, p0)) continue;
-      for (int j = 0; j < n1; ++j) {
-        bool h1, p1;
-        uint32_t m1;
-        int32_t s1;
-        const bool use1 = !no_lists && km_kind != 0;
+    for (uint32_t r0 = seq0; r0; r0 &= r0 - 1) {
+      const int i0 = __ffs(r0) - 1;
+      bool h0 = false, p0 = true;
+      uint32_t m0 = 0;
+      int32_t s0 = 0;
+      if (kc_kind == 1) { h0 = true; m0 = mask_at(i0); p0 = __popc(m0) == min_c; s0 = score_at(i0); }
+      else if (kc_kind == 2) { p0 = false; }
+      if (use0 && single && !(p0 && (!h0 || __popc(m0) == 1))) continue;
+      for (uint32_t r1 = seq1; r1; r1 &= r1 - 1) {
+        const int i1 = __ffs(r1) - 1;
+        bool h1 = false, p1 = true;
+        uint32_t m1 = 0;
+        int32_t s1 = 0;
         if (use1) {
-          entry(km_kind, lm, min_m, j, h1, m1, p1, s1);
-          if (!keep(h1, m1, p1)) continue;
-        } else {
-          h1 = false; m1 = 0; p1 = true; s1 = 0;
+          if (km_kind == 1) { h1 = true; m1 = mask_at(i1); p1 = __popc(m1) == min_m; s1 = score_at(i1); }
+          else { p1 = false; }
+          if (single && !(p1 && (!h1 || __popc(m1) == 1))) continue;
         }
         uint32_t mg = full_mask;
         bool pg = true;
