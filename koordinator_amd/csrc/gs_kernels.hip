@@ -255,17 +255,16 @@ __global__ void __launch_bounds__(256) eval_numa_kernel(MirrorView m, const PodV
                                                         Profile pf, const uint32_t* __restrict__ idx, uint32_t nidx,
                                                         uint32_t n0, int16_t* __restrict__ S, uint32_t ld,
                                                         int prod_cols) {
+  // one (node, pod) pair per thread: the per-pair work is long and batches ending at cpuset pods are short,
+  // so parallelism over pods matters more than row reuse (rows are L2/MALL resident)
   const uint32_t t = blockIdx.x * 256 + threadIdx.x;
-  if (t >= nidx) return;
+  const int k = blockIdx.y;
+  if (t >= nidx || k >= npods) return;
   const uint32_t node = idx[t];
   Row row;
   load_row(m, node, prod_cols, true, row);
-  const int k0 = blockIdx.y * PODS_PER_BLOCK;
-  const int k1 = min(npods, k0 + PODS_PER_BLOCK);
-  for (int k = k0; k < k1; ++k) {
-    PairOut o = eval_pair<false, false, true>(row, pods[k], pf, m);
-    S[(size_t)k * ld + (node - n0)] = (int16_t)total_score(o, pf);
-  }
+  PairOut o = eval_pair<false, false, true>(row, pods[k], pf, m);
+  S[(size_t)k * ld + (node - n0)] = (int16_t)total_score(o, pf);
 }
 
 // Diagnostic variant (gs_evaluate): every plugin's verdict and score for every pair.
@@ -290,32 +289,33 @@ __global__ void __launch_bounds__(256) eval_full_kernel(MirrorView m, const PodV
 }
 
 // ------------------------------------------------------------------------------------------------
-// Candidate levels: one workgroup (4 waves) per pod row of the shard; wave w owns a contiguous quarter of
-// the row so that per-wave histograms give every wave its output offset within each level.
-constexpr int CAND_THREADS = 256;
-
-__global__ void __launch_bounds__(CAND_THREADS) cand_kernel(const int16_t* __restrict__ S, uint32_t ld, uint32_t len,
-                                                            uint32_t n0, int max_score, uint32_t* __restrict__ lists,
-                                                            LevelHdr* __restrict__ hdrs) {
+// Candidate levels: one workgroup (W waves) per pod row of the shard; wave w owns a contiguous W-th of the
+// row so that per-wave histograms give every wave its output offset within each level. W = 16 for profiles
+// with small score ranges (more bandwidth per row when batches are short), else 4.
+template <int W>
+__global__ void __launch_bounds__(64 * W) cand_kernel(const int16_t* __restrict__ S, uint32_t ld, uint32_t len,
+                                                      uint32_t n0, int max_score, uint32_t* __restrict__ lists,
+                                                      LevelHdr* __restrict__ hdrs) {
+  constexpr int CAND_THREADS = 64 * W;
   extern __shared__ __align__(16) uint32_t smem[];
   const int nbins = max_score + 1;
-  uint32_t* whist = smem;                                        // [4][nbins]
-  uint32_t* comb = smem + 4 * nbins;                             // [nbins]
+  uint32_t* whist = smem;                                        // [W][nbins]
+  uint32_t* comb = smem + W * nbins;                             // [nbins]
   int8_t* slot_of = reinterpret_cast<int8_t*>(comb + nbins);     // [nbins]
   __shared__ uint32_t segsum[CAND_THREADS];
   __shared__ uint32_t s_total;
   __shared__ LevelHdr s_hdr;
-  __shared__ uint32_t s_woff[4][MAXLEV];
+  __shared__ uint32_t s_woff[W][MAXLEV];
   const int k = blockIdx.x;
   const int t = threadIdx.x, wave = t >> 6, lane = t & 63;
   const int16_t* row = S + (size_t)k * ld;
-  for (int b = t; b < 4 * nbins; b += CAND_THREADS) whist[b] = 0;
+  for (int b = t; b < W * nbins; b += CAND_THREADS) whist[b] = 0;
   if (t == 0) s_total = 0;
   __syncthreads();
   // 16-B loads: 8 scores per lane, 512 per wave step. Rows are padded with -1 up to ld (a multiple of
   // 1024), so the row is read as lenv = round_up(len, 512) entries.
   const uint32_t lenv = (len + 511) & ~511u;
-  const uint32_t seg = (lenv / 512 + 3) / 4 * 512;
+  const uint32_t seg = (lenv / 512 + W - 1) / W * 512;
   const uint32_t wb = min(lenv, wave * seg), we = min(lenv, wb + seg);
   const int4* row4 = reinterpret_cast<const int4*>(row);
   // pass 1: per-wave histograms of feasible scores
@@ -331,7 +331,9 @@ __global__ void __launch_bounds__(CAND_THREADS) cand_kernel(const int16_t* __res
   {
     uint32_t s = 0;
     for (int b = t * per; b < min(nbins, (t + 1) * per); ++b) {
-      uint32_t h = whist[b] + whist[nbins + b] + whist[2 * nbins + b] + whist[3 * nbins + b];
+      uint32_t h = 0;
+#pragma unroll
+      for (int w = 0; w < W; ++w) h += whist[w * nbins + b];
       comb[b] = h;
       slot_of[b] = -1;
       s += h;
@@ -373,7 +375,7 @@ __global__ void __launch_bounds__(CAND_THREADS) cand_kernel(const int16_t* __res
   }
   __syncthreads();
   const int nlev = s_hdr.nlev;
-  if (t < 4 * MAXLEV) {
+  if (t < W * MAXLEV) {
     int w = t / MAXLEV, j = t % MAXLEV;
     uint32_t off = 0;
     if (j < nlev) {
@@ -962,7 +964,7 @@ hipError_t launch_eval(const MirrorView& m, const PodVec* pods, int npods, const
   if (pf.enabled & 0x30u) {
     hipLaunchKernelGGL(eval_kernel<true>, dim3(gx, gy), dim3(256), 0, st, m, pods, npods, pf, n0, n1, S, ld, prod_cols);
     if (numa_n)
-      hipLaunchKernelGGL(eval_numa_kernel, dim3((numa_n + 255) / 256, gy), dim3(256), 0, st, m, pods, npods, pf,
+      hipLaunchKernelGGL(eval_numa_kernel, dim3((numa_n + 255) / 256, npods), dim3(256), 0, st, m, pods, npods, pf,
                          numa_idx, numa_n, n0, S, ld, prod_cols);
   } else {
     hipLaunchKernelGGL(eval_kernel<false>, dim3(gx, gy), dim3(256), 0, st, m, pods, npods, pf, n0, n1, S, ld, prod_cols);
@@ -978,15 +980,20 @@ hipError_t launch_eval_full(const MirrorView& m, const PodVec* pods, int npods, 
   return hipGetLastError();
 }
 
-static size_t cand_smem_bytes(int max_score) {
+static size_t cand_smem_bytes(int max_score, int waves) {
   size_t nb = (size_t)max_score + 1;
-  return nb * 4 * 4 + nb * 4 + ((nb + 15) & ~(size_t)15);
+  return nb * 4 * waves + nb * 4 + ((nb + 15) & ~(size_t)15);
 }
+static bool cand_wide(int max_score) { return cand_smem_bytes(max_score, 16) <= 48 * 1024; }
 
 hipError_t launch_cand(const int16_t* S, uint32_t ld, uint32_t len, uint32_t n0, int npods, int max_score,
                        uint32_t* lists, LevelHdr* hdrs, hipStream_t st) {
-  hipLaunchKernelGGL(cand_kernel, dim3(npods), dim3(CAND_THREADS), cand_smem_bytes(max_score), st, S, ld, len, n0,
-                     max_score, lists, hdrs);
+  if (cand_wide(max_score))
+    hipLaunchKernelGGL(cand_kernel<16>, dim3(npods), dim3(1024), cand_smem_bytes(max_score, 16), st, S, ld, len, n0,
+                       max_score, lists, hdrs);
+  else
+    hipLaunchKernelGGL(cand_kernel<4>, dim3(npods), dim3(256), cand_smem_bytes(max_score, 4), st, S, ld, len, n0,
+                       max_score, lists, hdrs);
   return hipGetLastError();
 }
 
@@ -1030,8 +1037,11 @@ hipError_t set_kernel_attributes() {
   e = hipFuncSetAttribute(reinterpret_cast<const void*>(commit_kernel<true>),
                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)commit_smem_bytes(MAX_BATCH));
   if (e != hipSuccess) return e;
-  return hipFuncSetAttribute(reinterpret_cast<const void*>(cand_kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
-                             (int)cand_smem_bytes(MAX_SCORE_LIMIT));
+  e = hipFuncSetAttribute(reinterpret_cast<const void*>(cand_kernel<16>), hipFuncAttributeMaxDynamicSharedMemorySize,
+                          48 * 1024);
+  if (e != hipSuccess) return e;
+  return hipFuncSetAttribute(reinterpret_cast<const void*>(cand_kernel<4>), hipFuncAttributeMaxDynamicSharedMemorySize,
+                             (int)cand_smem_bytes(MAX_SCORE_LIMIT, 4));
 }
 
 }  // namespace gs
