@@ -984,7 +984,9 @@ static size_t cand_smem_bytes(int max_score, int waves) {
   size_t nb = (size_t)max_score + 1;
   return nb * 4 * waves + nb * 4 + ((nb + 15) & ~(size_t)15);
 }
-static bool cand_wide(int max_score) { return cand_smem_bytes(max_score, 16) <= 48 * 1024; }
+// The 16-wave variant measured slower on MI355X (its serial level scan walks 4x more segments): kept for
+// experiments, not selected.
+static bool cand_wide(int max_score) { return false && cand_smem_bytes(max_score, 16) <= 48 * 1024; }
 
 hipError_t launch_cand(const int16_t* S, uint32_t ld, uint32_t len, uint32_t n0, int npods, int max_score,
                        uint32_t* lists, LevelHdr* hdrs, hipStream_t st) {

@@ -321,7 +321,28 @@ __device__ __forceinline__ NumaOut numa_eval(const NumaRow& r, const PodVec& p, 
     bool b_has = true, b_pref = false;
     uint32_t b_mask = full_mask;
     int32_t b_score = 0;
-    for (uint32_t r0 = seq0; r0; r0 &= r0 - 1) {
+    // Fast path (exact): when every present list has single-zone preferred hints (min size 1), a preferred
+    // merged hint is only produced by equal single-bit masks, so the preferred, narrowest candidates are the
+    // single zones z present in every list, visited in ascending z; mergeFilteredHints then keeps the first
+    // one of maximal score. (The 1-bit masks occupy order positions 0..nz-1.)
+    const uint32_t ones = (1u << nz) - 1u;
+    uint32_t both = 0xFu;
+    bool fast = !no_lists && (kc_kind == 1 || kc_kind == 0) && (km_kind == 1 || km_kind == 0);
+    if (fast && kc_kind == 1) { fast = min_c == 1; both &= lc & ones; }
+    if (fast && km_kind == 1) { fast = min_m == 1; both &= lm & ones; }
+    fast = fast && both != 0;
+    if (fast) {
+      int best_z = 0, best_s = -1;
+      for (uint32_t rr = both; rr; rr &= rr - 1) {
+        const int z = __ffs(rr) - 1;
+        const int sz = score_at(z);
+        if (sz > best_s) { best_s = sz; best_z = z; }
+      }
+      b_mask = 1u << best_z;
+      b_pref = true;
+      b_score = best_s;
+    }
+    for (uint32_t r0 = fast ? 0u : seq0; r0; r0 &= r0 - 1) {
       const int i0 = __ffs(r0) - 1;
       bool h0 = false, p0 = true;
       uint32_t m0 = 0;
