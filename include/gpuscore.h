@@ -422,6 +422,9 @@ int gs_synchronize(gs_ctx* ctx);
 /* Diagnostics: re-derives every node row on the host and compares it with the HBM mirror; returns the
  * number of mismatching rows (0 = the device-side Assume/Reserve replay matches the host mirror). */
 int gs_debug_mirror_check(gs_ctx* ctx);
+/* Diagnostics: on != 0 makes gs_schedule re-run the host takeCPUs (cpu_accumulator.go:87-232) for every cpuset
+ * the commit kernel selected and fail with GS_ESTATE on any difference. */
+int gs_debug_verify_cpuset(gs_ctx* ctx, int on);
 /* sizeof() of the ABI structs as compiled into the library, in this order: gs_pod, gs_node,
  * gs_node_metric, gs_pod_metric, gs_config, gs_placement, gs_stats, gs_loadaware_args, gs_cpu_topology,
  * gs_node_numa, gs_pod_allocation, gs_numa_args. */

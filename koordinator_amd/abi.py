@@ -219,6 +219,7 @@ SIGNATURES = {
     "gs_reset_stats": (C.c_int, [P]),
     "gs_synchronize": (C.c_int, [P]),
     "gs_debug_mirror_check": (C.c_int, [P]),
+    "gs_debug_verify_cpuset": (C.c_int, [P, C.c_int]),
     "gs_abi_sizes": (None, [C.POINTER(u64), u32]),
     "gs_topology_register": (C.c_int, [P, C.POINTER(GsCpuTopology), C.POINTER(i32)]),
     "gs_nodes_numa_upsert": (C.c_int, [P, P, P, u32]),

@@ -127,6 +127,10 @@ struct gs_ctx {
   uint32_t* d_numa_idx = nullptr;
   uint32_t numa_n = 0;
   bool numa_idx_stale = true;
+  // registered topologies in bit-plane form (the commit kernel's cpuset Reserve), and the host re-check of
+  // every device-chosen cpuset (GS_VERIFY_CPUSET=1)
+  TopoDev* d_topos = nullptr;
+  bool verify_cpuset = false;
 };
 
 namespace {
@@ -371,7 +375,7 @@ void derive_row(const gs_ctx* c, const HostNode& hn, int64_t* row) {
 }
 
 void derive_row_numa(const gs_ctx* c, uint32_t i, int64_t* row) {
-  numa_derive(c->numa[i], row, row + NUM_I64_COLS);
+  numa_derive(c->numa[i], c->cfg.numa.numa_scoring_type == GS_SCORING_MOST_ALLOCATED, row, row + NUM_I64_COLS);
 }
 
 bool in_range(int64_t v) { return v > -kMaxExact && v < kMaxExact; }
@@ -426,7 +430,9 @@ PodVec prep_pod(const gs_ctx* c, const gs_pod& p) {
     if (required != GS_CPU_BIND_UNSET) bind = required;
     if (bind == GS_CPU_BIND_FULL_PCPUS || bind == GS_CPU_BIND_SPREAD_BY_PCPUS) {
       if (cpu % 1000 != 0) pn |= PN_PREFAIL;
-      else if (cpu > 0) pn |= PN_BIND | ((uint32_t)required << PN_REQ_SHIFT) | ((uint32_t)bind << PN_PREF_SHIFT);
+      else if (cpu > 0)
+        pn |= PN_BIND | ((uint32_t)required << PN_REQ_SHIFT) | ((uint32_t)bind << PN_PREF_SHIFT) |
+              ((uint32_t)p.preferred_cpu_exclusive_policy << PN_EXCL_SHIFT);
     }
   }
   v.numa = pn;
@@ -545,7 +551,11 @@ int numa_reserve(gs_ctx* c, const gs_pod& p, const PodVec& v, const PlacementDev
     if (pd.zkeys >> (4 + z) & 1) { a.mask |= GS_USAGE_MEMORY; a.memory = pd.zmem[z]; }
     rec.numa.push_back(a);
   }
-  if (rb) {
+  if (pd.flags & PL_RESERVE_FAILED)
+    return fail(c, GS_ESTATE, "NodeNUMAResource Reserve failed on the device for node %d after a feasible Filter",
+                pd.node);
+  const bool on_device = pd.flags & PL_DEVICE_CPUSET;   // the commit kernel chose the cpuset and updated the row
+  if (rb && (!on_device || c->verify_cpuset)) {
     // getCPUBindPolicy (util.go:85-103) and GetNUMAAllocateStrategy (util.go:35-41)
     int req = (v.numa >> PN_REQ_SHIFT) & 7, pref = (v.numa >> PN_PREF_SHIFT) & 7;
     int bind = pref;
@@ -560,12 +570,17 @@ int numa_reserve(gs_ctx* c, const gs_pod& p, const PodVec& v, const PlacementDev
     if (!numa_allocate_cpuset(nn, v.num_cpus, bind, required, rec.excl, strategy, rec.numa, &rec.cpus))
       return fail(c, GS_ESTATE, "NodeNUMAResource Reserve: cpuset allocation failed on node %d after a feasible Filter",
                   pd.node);
+    if (on_device && std::memcmp(rec.cpus.w, pd.cpuset, sizeof(pd.cpuset)) != 0)
+      return fail(c, GS_ESTATE, "NodeNUMAResource Reserve: device cpuset differs from the host takeCPUs on node %d",
+                  pd.node);
   }
+  if (on_device)
+    for (int w = 0; w < GS_CPU_WORDS; ++w) rec.cpus.w[w] = pd.cpuset[w];
   if (!nn.topo_valid()) return GS_OK;   // resourceManager.Update skips nodes without a valid CPU topology
   numa_release(nn, rec.uid);
   numa_add(nn, rec);
   c->numa_uid_node[rec.uid] = (uint32_t)pd.node;
-  if (rb) mark_dirty(c, (uint32_t)pd.node);
+  if (rb && !on_device) mark_dirty(c, (uint32_t)pd.node);
   return GS_OK;
 }
 
@@ -716,6 +731,7 @@ int run_batch(gs_ctx* c, const gs_pod* pods, int b, int* committed_out) {
   a.out = c->d_out;
   a.committed = c->d_committed;
   a.stamps = c->d_stamps;
+  a.topos = c->d_topos;
   HIP_TRY(c, hipEventRecord(c->ev[3], c->st));
   HIP_TRY(c, launch_commit(a, c->st));
   HIP_TRY(c, hipEventRecord(c->ev[4], c->st));
@@ -970,7 +986,8 @@ int gs_destroy(gs_ctx* c) {
   if (c->comm) ncclCommDestroy(c->comm);
   if (c->st) (void)hipStreamSynchronize(c->st);
   void* dev[] = {c->d_i64, c->d_i32, c->d_pods, c->d_seq, c->d_S, c->d_xchg_send, c->d_xchg_recv, c->d_out,
-                 c->d_committed, c->d_rowstat, c->d_sel, c->d_stage_idx, c->d_stage_rows, c->d_numa_idx};
+                 c->d_committed, c->d_rowstat, c->d_sel, c->d_stage_idx, c->d_stage_rows, c->d_numa_idx,
+                 c->d_topos};
   for (void* p : dev)
     if (p) (void)hipFree(p);
   void* host[] = {c->h_pods, c->h_seq, c->h_out, c->h_committed, c->h_stage_idx, c->h_stage_rows, c->h_xchg_send,
@@ -1109,11 +1126,10 @@ int gs_schedule(gs_ctx* c, const gs_pod* pods, uint32_t npods, const uint64_t* s
       for (int j = 1; j < b; ++j)
         if (special_pod(c, pods[i + j])) { b = j; break; }
     }
+    // (a cpuset pod whose node is outside the device cpuset scope ends the batch inside the commit kernel)
     for (int j = 0; j < b; ++j) {
       c->h_pods[j] = prep_pod(c, pods[i + j]);
       c->h_seq[j] = seq ? seq[i + j] : (uint64_t)(i + j);
-      // a cpuset pod's Reserve (takeCPUs) runs on the host: the batch ends with it
-      if (c->numa_on && (c->h_pods[j].numa & PN_BIND)) { b = j + 1; break; }
     }
     HIP_TRY(c, hipMemcpyAsync(c->d_pods, c->h_pods, sizeof(PodVec) * b, hipMemcpyHostToDevice, c->st));
     HIP_TRY(c, hipMemcpyAsync(c->d_seq, c->h_seq, 8 * b, hipMemcpyHostToDevice, c->st));
@@ -1126,7 +1142,7 @@ int gs_schedule(gs_ctx* c, const gs_pod* pods, uint32_t npods, const uint64_t* s
       o.feasible = pd.feasible;
       o.score = pd.node >= 0 ? pd.score : 0;
       o.ties = pd.node >= 0 ? pd.ties : 0;
-      o.flags = pd.flags;
+      o.flags = pd.flags & ~PL_INTERNAL_FLAGS;
       if ((rc = numa_reserve(c, pods[i + j], c->h_pods[j], pd))) return rc;
       apply_placement(c, pods[i + j], pd.node, special_first);
     }
@@ -1153,6 +1169,13 @@ int gs_topology_register(gs_ctx* c, const gs_cpu_topology* t, int32_t* id) {
   if (!topo) return fail(c, GS_EUNSUPPORTED, "gs_topology_register: %s", err ? err : "invalid topology");
   c->topos.push_back(topo);
   *id = (int32_t)c->topos.size() - 1;
+  // device copy of every registered topology's TopoDev (index = topology id)
+  std::vector<TopoDev> all(c->topos.size());
+  for (size_t i = 0; i < all.size(); ++i) all[i] = c->topos[i]->dev;
+  HIP_TRY(c, hipStreamSynchronize(c->st));
+  if (c->d_topos) { (void)hipFree(c->d_topos); c->d_topos = nullptr; }
+  HIP_TRY(c, hipMalloc(&c->d_topos, sizeof(TopoDev) * all.size()));
+  HIP_TRY(c, hipMemcpy(c->d_topos, all.data(), sizeof(TopoDev) * all.size(), hipMemcpyHostToDevice));
   return GS_OK;
 }
 
@@ -1287,6 +1310,12 @@ int gs_reset_stats(gs_ctx* c) {
 int gs_synchronize(gs_ctx* c) {
   if (!c) return GS_EINVAL;
   HIP_TRY(c, hipStreamSynchronize(c->st));
+  return GS_OK;
+}
+
+int gs_debug_verify_cpuset(gs_ctx* c, int on) {
+  if (!c) return GS_EINVAL;
+  c->verify_cpuset = on != 0;
   return GS_OK;
 }
 

@@ -4,6 +4,7 @@
 #include <stddef.h>
 #include <stdint.h>
 
+#include "gs_cpuset_dev.h"
 #include "gs_layout.h"
 
 namespace gs {
@@ -48,10 +49,16 @@ struct PlacementDev {   // gs_placement + the NodeNUMAResource Reserve the devic
   uint32_t feasible;
   int64_t score;
   uint32_t ties;
-  uint32_t flags;        // GS_PLACED_* (GS_PLACED_CPUSET: the host selects the cpuset and cuts the batch here)
+  uint32_t flags;        // GS_PLACED_* | PL_* below
   uint32_t zkeys;        // NUMA allocation by hint: bit z = zone z cpu allocated, bit 4+z = memory
   uint32_t pad;
   int64_t zcpu[4], zmem[4];
+  uint64_t cpuset[4];    // with PL_DEVICE_CPUSET: the CPUs the commit kernel allocated
+};
+enum : uint32_t {
+  PL_DEVICE_CPUSET = 0x40000000u,   // cpuset chosen and applied on the device (else: host takeCPUs, batch cut)
+  PL_RESERVE_FAILED = 0x80000000u,  // Reserve failed after a feasible Filter: the host fails loudly
+  PL_INTERNAL_FLAGS = PL_DEVICE_CPUSET | PL_RESERVE_FAILED,
 };
 
 struct CommitArgs {
@@ -73,6 +80,7 @@ struct CommitArgs {
   PlacementDev* out;
   int32_t* committed;
   uint64_t* stamps;          // diagnostics: per-phase s_memtime cycle sums (nullptr: normal build)
+  const TopoDev* topos;      // registered topologies, bit-plane form (cpuset Reserve on the device)
 };
 
 hipError_t set_kernel_attributes();

@@ -17,6 +17,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "gs_cpuset_dev.h"
 #include "gs_kernels.h"
 #include "gs_numa_dev.h"
 
@@ -510,6 +511,46 @@ __device__ __forceinline__ void wave_rank_sort(uint32_t* v, int n, uint32_t* tmp
   WAVE_FENCE();
 }
 
+// Device-side cpuset Reserve of one pod on its winner row (one thread): allocateCPUSet with the NUMA split of
+// Allocate (resource_manager.go:273-360, gs_cpuset_dev.h), then NodeAllocation.addPodAllocation
+// (node_allocation.go:82-110) on the CPU state and the row's available-CPU summaries, as numa_derive
+// (gs_numa_host.cpp) would recompute them. false: allocateCPUSet errors (the host fails loudly).
+__device__ __noinline__ bool cpuset_reserve(const TopoDev& t, CpuStateDev& cs, const PodVec& p, uint32_t nf,
+                                            const NumaOut& no, NumaRow& nr, uint64_t* cpuset) {
+  // getCPUBindPolicy (util.go:85-103)
+  const uint32_t pn = p.numa;
+  const int st_req = (pn >> PN_REQ_SHIFT) & 7, nb = (nf >> NF_BIND_SHIFT) & 3;
+  int bind = (pn >> PN_PREF_SHIFT) & 7;
+  bool required = false;
+  if (st_req != BIND_UNSET) { bind = st_req; required = true; }
+  else if (nb == GS_NODE_CPU_BIND_SPREAD_BY_PCPUS) { bind = BIND_SPREAD; required = true; }
+  else if (nb == GS_NODE_CPU_BIND_FULL_PCPUS_ONLY) { bind = BIND_FULL; required = true; }
+  const int ep = (pn & PN_BIND) ? (int)((pn >> PN_EXCL_SHIFT) & 3u) : GS_CPU_EXCLUSIVE_NONE;
+  uint64_t R[TD_POS];
+  if (!td_allocate_cpuset(t, cs, p.num_cpus, bind, required, ep, no.zkeys, no.zcpu, R)) return false;
+  const uint64_t cores = td_any(R);
+  for (int j = 0; j < TD_POS; ++j) cs.un[j] |= R[j];
+  if (ep == GS_CPU_EXCLUSIVE_PCPU_LEVEL) cs.xc |= cores;
+  else if (ep == GS_CPU_EXCLUSIVE_NUMA_NODE_LEVEL)
+    for (uint64_t b = cores; b; b &= b - 1) cs.meta |= 1u << t.core_node[td_ctz(b)];
+  nr.alloc_cpus += td_cnt(R, ~0ull);
+  nr.tfree = (uint32_t)td_counts(t, cs, ~0ull);
+  const int nz = (nf >> NF_ZONES_SHIFT) & 7;
+  for (int z = 0; z < 4; ++z) {
+    const int n = td_zone_node(cs, z);
+    if (z >= nz || n >= t.nnodes) continue;   // a zone the topology lacks keeps its zero summaries
+    const uint64_t zc = ((cs.zal >> (16 * z)) & 0xFFFFull) + (uint64_t)td_cnt(R, t.node_cores[n]);
+    cs.zal = (cs.zal & ~(0xFFFFull << (16 * z))) | (zc << (16 * z));
+    nr.zfree[z] = (uint32_t)td_counts(t, cs, t.node_cores[n]);
+    if (nr.amp > 1.0) {
+      const int64_t c = (int64_t)zc * 1000;
+      nr.zadj[z] = (int32_t)(amplify_d(c, nr.amp) - c);
+    }
+  }
+  td_to_cpus(t, R, cpuset);
+  return true;
+}
+
 // ST: diagnostic build with s_memtime phase stamps (accumulated per phase, written to a.stamps)
 template <bool ST>
 __global__ void __launch_bounds__(256) commit_kernel(CommitArgs a) {
@@ -535,6 +576,7 @@ __global__ void __launch_bounds__(256) commit_kernel(CommitArgs a) {
   int32_t* hkey = reinterpret_cast<int32_t*>(
       (reinterpret_cast<uintptr_t>(dso + B * B) + 15) & ~(uintptr_t)15);     // HASH
   int32_t* hval = hkey + HASH;                                               // HASH
+  CpuStateDev* cst = reinterpret_cast<CpuStateDev*>(hval + HASH);            // B dirty slots: CPU state
 
   __shared__ int32_t sh_score[MAX_RANKS * MAXLEV], sh_count[MAX_RANKS * MAXLEV], sh_dec[MAX_RANKS * MAXLEV];
   __shared__ uint32_t dnew[MAX_BATCH], tmp[MAX_BATCH];
@@ -545,8 +587,11 @@ __global__ void __launch_bounds__(256) commit_kernel(CommitArgs a) {
   __shared__ uint32_t s_winner;
   __shared__ int64_t s_T;
   __shared__ int s_cut;                                // the pod just committed needs host-side Reserve
+  __shared__ TopoDev s_topo;                           // topology of the last cpuset Reserve (bit-plane form)
+  __shared__ int s_topo_id;
   const bool numa_on = (a.pf.enabled & 0x30u) != 0;
 
+  if (tid == 0) s_topo_id = -1;
   for (int i = tid; i < B; i += 256) pods[i] = a.pods[i];
   for (int i = tid; i < HASH; i += 256) { hkey[i] = -1; hval[i] = -1; }
   const MirrorView& m = a.m;
@@ -772,6 +817,11 @@ __global__ void __launch_bounds__(256) commit_kernel(CommitArgs a) {
         if (lane >= 32 && lane < 32 + NUMA_I64) nw[lane - 32] = m.c64(C_ZCAP_CPU0 + (lane - 32))[winner];
         int32_t* iw = reinterpret_cast<int32_t*>(&orow.nr.nflags);
         if (lane >= 50 && lane < 50 + NUMA_I32) iw[lane - 50] = m.c32(C_NFLAGS + (lane - 50))[winner];
+        // CPU state for a device-side cpuset Reserve (lives in its slot directly)
+        uint64_t* cw = reinterpret_cast<uint64_t*>(&cst[slot]);
+        if (lane >= 20 && lane < 26) cw[lane - 20] = (uint64_t)m.c64(C_CPU_UN0 + (lane - 20))[winner];
+        if (lane == 26) cst[slot].meta = (uint32_t)m.c32(C_CPU_META)[winner];
+        if (lane == 27) cst[slot].topo = m.c32(C_TOPO_DEV)[winner];
       }
     }
     if (lane == 0) {
@@ -787,6 +837,19 @@ __global__ void __launch_bounds__(256) commit_kernel(CommitArgs a) {
     const int slot = s_slot;
     const bool fresh = s_fresh;
     Row& d = drows[slot];
+    if (numa_on) {   // stage the winner's topology in LDS for a device-side cpuset Reserve (block-uniform test)
+      const PodVec& pq = pods[k];
+      const int tp = cst[slot].topo;
+      const uint32_t nfl = fresh ? orow.nr.nflags : d.nr.nflags;
+      if (tp >= 0 && tp != s_topo_id && !(pq.numa & (PN_SKIP | PN_PREFAIL)) &&
+          ((pq.numa & PN_BIND) || ((nfl >> NF_BIND_SHIFT) & 3u))) {
+        const uint64_t* src = reinterpret_cast<const uint64_t*>(a.topos + tp);
+        uint64_t* dst = reinterpret_cast<uint64_t*>(&s_topo);
+        for (int i = tid; i < (int)(sizeof(TopoDev) / 8); i += 256) dst[i] = src[i];
+        __syncthreads();
+        if (tid == 0) s_topo_id = tp;
+      }
+    }
     if (tid == 0) {
       if (fresh) d = orow;
       const PodVec& pk = pods[k];
@@ -796,11 +859,12 @@ __global__ void __launch_bounds__(256) commit_kernel(CommitArgs a) {
       s_cut = 0;
       if (numa_on && !(pk.numa & (PN_SKIP | PN_PREFAIL))) {
         // NodeNUMAResource Reserve (plugin.go:375-422) on the pre-assume row: the Filter-time affinity and the
-        // NUMA split of Allocate; a cpuset pod ends the batch (its CPUs are chosen on the host)
+        // NUMA split of Allocate; a cpuset pod's CPUs are selected here (gs_cpuset_dev.h) when the node's
+        // topology is in the device scope, else the batch ends with it and the host selects them
         NumaOut no = numa_eval(d.nr, pk, a.pf, SlotsLds{d, m}, a.pf.enabled & 0x10u, false);
         const uint32_t nf = d.nr.nflags;
         const bool rb = no.flags & GS_PLACED_CPUSET;
-        if (no.reason) pl.flags |= 0x80000000u;   // cannot happen for a feasible winner: the host fails loudly
+        if (no.reason) pl.flags |= PL_RESERVE_FAILED;   // cannot happen for a feasible winner
         if (rb || ((nf >> NF_POLICY_SHIFT) & 3u)) {
           pl.flags |= no.flags;
           pl.zkeys = no.zkeys;
@@ -817,7 +881,15 @@ __global__ void __launch_bounds__(256) commit_kernel(CommitArgs a) {
                               (zm ? 1u << (NF2_AMEM_SHIFT + z) : 0u);
             }
           }
-          if (rb) s_cut = 1;
+          if (rb) {
+            CpuStateDev& cs = cst[slot];
+            if (cs.topo >= 0 && cs.topo == s_topo_id) {
+              if (cpuset_reserve(s_topo, cs, pk, nf, no, d.nr, pl.cpuset)) pl.flags |= PL_DEVICE_CPUSET;
+              else pl.flags |= PL_RESERVE_FAILED;
+            } else {
+              s_cut = 1;
+            }
+          }
         }
       }
       a.out[k] = pl;
@@ -859,11 +931,17 @@ __global__ void __launch_bounds__(256) commit_kernel(CommitArgs a) {
     if (row_word_mutable(j)) m.c64(kRowCol[j])[drows[s].node] = reinterpret_cast<const int64_t*>(&drows[s])[j];
   }
   for (int s = tid; s < nd; s += 256) m.c32(C_FREE_PODS)[drows[s].node] = drows[s].free_pods;
+  // NUMA words Reserve changes: ZRAW (8 i64), NFLAGS2 .. ZADJ3 (11 i32), CPU state (6 i64 + meta)
+  constexpr int NW = 8 + 11 + 6 + 1;
+  static_assert(C_ZADJ0 + 3 - C_NFLAGS2 + 1 == 11, "NUMA i32 write-back columns contiguous");
   if (numa_on)
-    for (int e = tid; e < nd * 9; e += 256) {
-      int sl = e / 9, j = e % 9;
-      if (j < 8) m.c64(C_ZRAW_CPU0 + j)[drows[sl].node] = (&drows[sl].nr.zraw_cpu[0])[j];
-      else m.c32(C_NFLAGS2)[drows[sl].node] = (int32_t)drows[sl].nr.nflags2;
+    for (int e = tid; e < nd * NW; e += 256) {
+      const int sl = e / NW, j = e % NW;
+      const uint32_t node = drows[sl].node;
+      if (j < 8) m.c64(C_ZRAW_CPU0 + j)[node] = (&drows[sl].nr.zraw_cpu[0])[j];
+      else if (j < 19) m.c32(C_NFLAGS2 + (j - 8))[node] = reinterpret_cast<const int32_t*>(&drows[sl].nr.nflags2)[j - 8];
+      else if (j < 25) m.c64(C_CPU_UN0 + (j - 19))[node] = reinterpret_cast<const int64_t*>(&cst[sl])[j - 19];
+      else m.c32(C_CPU_META)[node] = (int32_t)cst[sl].meta;
     }
   if (tid == 0) *a.committed = committed;
   if (ST && tid == 0)
@@ -1003,6 +1081,7 @@ size_t commit_smem_bytes(int B) {
   size_t b = (size_t)B * sizeof(PodVec) + (size_t)B * sizeof(Row) + (size_t)B * B * 2 * 2;
   b = (b + 15) & ~(size_t)15;
   b += (size_t)HASH * 8 + 16;
+  b += (size_t)B * sizeof(CpuStateDev);
   return b;
 }
 

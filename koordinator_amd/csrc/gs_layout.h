@@ -41,6 +41,10 @@ enum I64Col : int {
   C_ZRAW_MEM0 = C_ZRAW_CPU0 + 4,
   C_AMP = C_ZRAW_MEM0 + 4,         // options.AmplificationRatios[cpu] (f64 bits)
   C_NAMP,                          // node annotation cpu amplification ratio (f64 bits; -1 unset)
+  // device-side cpuset Reserve state (gs_cpuset_dev.h CpuStateDev; read by the commit kernel only)
+  C_CPU_UN0,                       // 4 planes: CPUs not available (allocated or reserved) per core rank
+  C_CPU_XC = C_CPU_UN0 + 4,        // cores holding a PCPULevel-exclusive allocated CPU
+  C_CPU_ZAL,                       // allocated CPUs per zone slot (4 x 16 bits)
   NUM_I64_COLS
 };
 
@@ -55,7 +59,9 @@ enum I32Col : int {
   C_TFREE,             // available CPUs of the node: raw | full-core CPUs << 9 | cores with a free CPU << 18
   C_ZFREE0,            // same, restricted to zone z
   C_ZADJ0 = C_ZFREE0 + 4,          // Amplify(c_z*1000) - c_z*1000, c_z = allocated CPUs in zone z (amp > 1)
-  NUM_I32_COLS = C_ZADJ0 + 4
+  C_CPU_META = C_ZADJ0 + 4,        // CpuStateDev.meta (CM_*)
+  C_TOPO_DEV,                      // TopoDev index of the node's topology; -1: cpuset Reserve on the host
+  NUM_I32_COLS
 };
 
 // C_NFLAGS bits
@@ -121,6 +127,7 @@ enum : uint32_t {
   PN_PREFAIL = 1u << 2,       // PreFilter returned ErrInvalidRequestedCPUs
   PN_REQ_SHIFT = 4,           // 3 bits: requiredCPUBindPolicy (gs_cpu_bind_policy)
   PN_PREF_SHIFT = 8,          // 3 bits: preferredCPUBindPolicy
+  PN_EXCL_SHIFT = 12,         // 2 bits: preferredCPUExclusivePolicy (with PN_BIND)
 };
 
 // kernel-uniform profile constants

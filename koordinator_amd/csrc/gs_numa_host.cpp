@@ -4,6 +4,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdio>
 #include <cstring>
 #include <set>
 
@@ -327,7 +328,117 @@ bool take_preferred(const TopoClass& t, int max_ref, const CpuMask& available, c
   return take_cpus(t, max_ref, available, ref, ex, needed, bind, excl, strategy, out);
 }
 
+// TopoDev (gs_cpuset_dev.h) of a topology; leaves ok = 0 outside the device scope
+void make_topo_dev(const TopoClass& t, TopoDev* d) {
+  std::memset(d, 0, sizeof(*d));
+  if (!t.valid || t.num_cpus <= 0) return;
+  std::vector<int> cores, nodes, socks;
+  for (int c = 0; c < t.num_cpus; ++c) {
+    cores.push_back(t.core[c]);
+    nodes.push_back(t.node[c]);
+    socks.push_back(t.socket[c]);
+  }
+  auto uniq = [](std::vector<int>& v) {
+    std::sort(v.begin(), v.end());
+    v.erase(std::unique(v.begin(), v.end()), v.end());
+  };
+  uniq(cores);
+  uniq(nodes);
+  uniq(socks);
+  if ((int)cores.size() > TD_CORES || (int)nodes.size() > TD_NODES || (int)socks.size() > TD_SOCKETS) return;
+  if (t.cpc < 1 || t.cpc > TD_POS || (int)nodes.size() != t.num_nodes) return;   // a NUMA node id in two sockets
+  auto idx = [](const std::vector<int>& v, int x) { return (int)(std::lower_bound(v.begin(), v.end(), x) - v.begin()); };
+  int core_sock[TD_CORES], core_node[TD_CORES], node_sock[TD_NODES], npos[TD_CORES] = {0};
+  std::fill(core_sock, core_sock + TD_CORES, -1);
+  std::fill(core_node, core_node + TD_CORES, -1);
+  std::fill(node_sock, node_sock + TD_NODES, -1);
+  std::memset(d->core_cpu, 0xff, sizeof(d->core_cpu));
+  std::memset(d->cpu_core, 0xff, sizeof(d->cpu_core));
+  std::memset(d->cpu_pos, 0xff, sizeof(d->cpu_pos));
+  for (int c = 0; c < t.num_cpus; ++c) {   // ascending CPU id: position j = rank of the CPU inside its core
+    const int k = idx(cores, t.core[c]), n = idx(nodes, t.node[c]), s = idx(socks, t.socket[c]);
+    if ((core_sock[k] >= 0 && core_sock[k] != s) || (core_node[k] >= 0 && core_node[k] != n) ||
+        (node_sock[n] >= 0 && node_sock[n] != s))
+      { std::memset(d, 0, sizeof(*d)); return; }
+    core_sock[k] = s;
+    core_node[k] = n;
+    node_sock[n] = s;
+    const int j = npos[k]++;
+    if (j >= TD_POS) { std::memset(d, 0, sizeof(*d)); return; }
+    const uint64_t b = 1ull << k;
+    d->core_cpu[k][j] = (uint8_t)c;
+    d->cpu_core[c] = (uint8_t)k;
+    d->cpu_pos[c] = (uint8_t)j;
+    d->pos_cores[j] |= b;
+    d->node_cores[n] |= b;
+    d->sock_cores[s] |= b;
+    d->core_node[k] = (uint8_t)n;
+  }
+  for (int n = 0; n < (int)nodes.size(); ++n) d->node_sock[n] = (uint8_t)node_sock[n];
+  d->num_cpus = t.num_cpus;
+  d->ncores = (int)cores.size();
+  d->nnodes = (int)nodes.size();
+  d->nsockets = (int)socks.size();
+  d->cpc = t.cpc;
+  d->cpn = t.cpn;
+  d->cps = t.cps;
+  d->ok = 1;
+}
+
+// node index (TopoDev order) of a NUMA node id, TD_NODES if the topology has no such node
+int dev_node_index(const TopoClass& t, int node_id) {
+  for (int c = 0; c < t.num_cpus; ++c)
+    if (t.node[c] == node_id) return t.dev.core_node[t.dev.cpu_core[c]];
+  return TD_NODES;
+}
+
 }  // namespace
+
+void numa_cpu_state(const NumaNode& n, bool default_most, CpuStateDev* cs) {
+  std::memset(cs, 0, sizeof(*cs));
+  cs->topo = -1;
+  const TopoClass* t = n.topo.get();
+  if (!t || !t->dev.ok) return;
+  const TopoDev& d = t->dev;
+  const int mr = n.max_ref();
+  for (int c = 0; c < t->num_cpus; ++c) {   // getAvailableCPUs (node_allocation.go:142-162)
+    const bool taken = n.ref[c] > 0 && n.ref[c] >= mr;
+    const bool reserved = (n.cfg.reserved_cpus[c >> 6] >> (c & 63)) & 1;
+    if (taken || reserved) cs->un[d.cpu_pos[c]] |= 1ull << d.cpu_core[c];
+  }
+  // exclusiveInCores / exclusiveInNUMANodes of newCPUAccumulator (cpu_accumulator.go:256-264): the CoreID /
+  // NodeID of every allocated CPU (zero values for CPUs outside the topology)
+  uint32_t xn = 0;
+  for (int c = 0; c < GS_MAX_CPUS; ++c) {
+    if (n.ref[c] == 0) continue;
+    const int core = c < t->num_cpus ? t->core[c] : 0, node = c < t->num_cpus ? t->node[c] : 0;
+    if (n.excl[c] == GS_CPU_EXCLUSIVE_PCPU_LEVEL) {
+      for (int c2 = 0; c2 < t->num_cpus; ++c2)
+        if (t->core[c2] == core) { cs->xc |= 1ull << d.cpu_core[c2]; break; }
+    } else if (n.excl[c] == GS_CPU_EXCLUSIVE_NUMA_NODE_LEVEL) {
+      const int ni = dev_node_index(*t, node);
+      if (ni < TD_NODES) xn |= 1u << ni;
+    }
+  }
+  const int nz = n.cfg.has_options ? n.cfg.num_zones : 0;
+  uint32_t zidx = 0;
+  for (int z = 0; z < GS_MAX_NUMA; ++z) {
+    int ni = TD_NODES;
+    if (z < nz) {
+      const int id = n.cfg.zones[z].node_id;
+      ni = dev_node_index(*t, id);
+      uint64_t cnt = 0;
+      for (int c = 0; c < t->num_cpus; ++c)
+        if (n.ref[c] > 0 && t->node[c] == id) ++cnt;
+      cs->zal |= cnt << (16 * z);
+    }
+    zidx |= (uint32_t)(ni < TD_NODES ? ni : 15) << (4 * z);
+  }
+  int strategy = n.cfg.numa_allocate_strategy;
+  if (strategy == GS_NUMA_ALLOC_UNSET) strategy = default_most ? GS_NUMA_ALLOC_MOST_ALLOCATED : GS_NUMA_ALLOC_LEAST_ALLOCATED;
+  cs->meta = xn | (zidx << CM_ZIDX_SHIFT) | (strategy == GS_NUMA_ALLOC_MOST_ALLOCATED ? CM_MOST : 0u);
+  cs->topo = mr <= 1 ? n.cfg.topology : -1;
+}
 
 bool take_cpus(const TopoClass& t, int max_ref, const CpuMask& available, const uint16_t* ref, const uint8_t* ex,
                int needed, int bind, int excl, int strategy, CpuMask* out) {
@@ -409,6 +520,7 @@ std::shared_ptr<TopoClass> make_topo(const gs_cpu_topology& in, const char** err
   t->cpn = t->num_nodes ? t->num_cpus / t->num_nodes : 0;
   t->cps = t->num_sockets ? t->num_cpus / t->num_sockets : 0;
   if (t->cpc > 255) { *err = "CPUsPerCore > 255"; return nullptr; }
+  make_topo_dev(*t, &t->dev);
   return t;
 }
 
@@ -456,7 +568,14 @@ CpuMask numa_available(const NumaNode& n) {
   return m;
 }
 
-void numa_derive(const NumaNode& n, int64_t* i64, int64_t* i32) {
+void numa_derive(const NumaNode& n, bool default_most, int64_t* i64, int64_t* i32) {
+  CpuStateDev cs;
+  numa_cpu_state(n, default_most, &cs);
+  for (int j = 0; j < TD_POS; ++j) i64[C_CPU_UN0 + j] = (int64_t)cs.un[j];
+  i64[C_CPU_XC] = (int64_t)cs.xc;
+  i64[C_CPU_ZAL] = (int64_t)cs.zal;
+  i32[C_CPU_META] = (int32_t)cs.meta;
+  i32[C_TOPO_DEV] = cs.topo;
   const gs_node_numa& g = n.cfg;
   const TopoClass* t = n.topo.get();
   uint32_t f = 0;
@@ -550,3 +669,143 @@ bool numa_allocate_cpuset(const NumaNode& n, int num_cpus, int bind, bool requir
 }
 
 }  // namespace gs
+
+// Self-test of the bit-plane cpuset selection (gs_cpuset_dev.h, the code the commit kernel runs) against the
+// host restatement on random compact topologies (core-major and sibling-interleaved CPU numbering, SMT 1/2/4,
+// 1-2 sockets x 1-4 NUMA nodes), random allocations / exclusivity / reservations and random requests
+// (bind and exclusive policies, strategies, NUMA splits). Returns the number of mismatches; `msg` describes
+// the first one. Test hook, not part of include/gpuscore.h.
+extern "C" int gsx_cpuset_selftest(uint64_t seed, int iters, char* msg, size_t len) {
+  using namespace gs;
+  uint64_t s = seed;
+  auto rnd = [&](int n) {
+    s += 0x9E3779B97F4A7C15ull;
+    uint64_t z = s;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    z ^= z >> 31;
+    return (int)(z % (uint64_t)n);
+  };
+  int bad = 0;
+  if (msg && len) msg[0] = 0;
+  auto report = [&](int it, const char* what) {
+    if (!bad && msg && len) snprintf(msg, len, "iteration %d: %s", it, what);
+    ++bad;
+  };
+  static const int kCpc[] = {1, 2, 2, 4};
+  for (int it = 0; it < iters; ++it) {
+    const int sockets = 1 + rnd(2), nps = 1 + rnd(4), cores_pn = 1 + rnd(6), cpc = kCpc[rnd(4)];
+    const bool interleave = rnd(2);
+    const int ncores = sockets * nps * cores_pn;
+    gs_cpu_topology in;
+    std::memset(&in, 0, sizeof(in));
+    in.num_cpus = ncores * cpc;
+    for (int sk = 0; sk < sockets; ++sk)
+      for (int nn = 0; nn < nps; ++nn)
+        for (int co = 0; co < cores_pn; ++co)
+          for (int th = 0; th < cpc; ++th) {
+            const int gcore = (sk * nps + nn) * cores_pn + co;
+            const int cpu = interleave ? th * ncores + gcore : gcore * cpc + th;
+            in.core_id[cpu] = (sk << 16) | (nn * cores_pn + co);
+            in.socket_id[cpu] = sk;
+            in.node_id[cpu] = 2 * (sk * nps + nn);   // sparse ids
+          }
+    const char* err = nullptr;
+    auto t = make_topo(in, &err);
+    if (!t || !t->dev.ok) { report(it, "topology outside the device scope"); continue; }
+    NumaNode n;
+    n.cfg.has_options = 1;
+    n.cfg.max_ref_count = 1;
+    n.cfg.topology = 0;
+    n.topo = t;
+    const int nnodes = sockets * nps, nz = nnodes < GS_MAX_NUMA ? nnodes : GS_MAX_NUMA;
+    n.cfg.num_zones = nz;
+    for (int z = 0; z < nz; ++z) {
+      n.cfg.zones[z].node_id = 2 * z + (rnd(8) == 0 ? 1 : 0);   // now and then a zone the topology lacks
+      n.cfg.zones[z].mask = GS_USAGE_CPU | GS_USAGE_MEMORY;
+    }
+    const int density = 1 + rnd(4);
+    for (int c = 0; c < in.num_cpus; ++c) {
+      if (rnd(density + 1) == 0) {
+        n.ref[c] = 1;
+        const int e = rnd(6);
+        n.excl[c] = (uint8_t)(e == 0 ? GS_CPU_EXCLUSIVE_PCPU_LEVEL : e == 1 ? GS_CPU_EXCLUSIVE_NUMA_NODE_LEVEL
+                                                                    : GS_CPU_EXCLUSIVE_NONE);
+      }
+      if (rnd(24) == 0) n.cfg.reserved_cpus[c >> 6] |= 1ull << (c & 63);
+    }
+    n.cfg.numa_allocate_strategy = rnd(3);
+    const bool dmost = rnd(2);
+    int strategy = n.cfg.numa_allocate_strategy;
+    if (strategy == GS_NUMA_ALLOC_UNSET) strategy = dmost ? GS_NUMA_ALLOC_MOST_ALLOCATED : GS_NUMA_ALLOC_LEAST_ALLOCATED;
+    CpuStateDev cs;
+    numa_cpu_state(n, dmost, &cs);
+    if (cs.topo != 0) { report(it, "cpu state not device-eligible"); continue; }
+    const CpuMask avail = numa_available(n);
+    const int na = avail.count();
+    const int needed = 1 + rnd(std::max(1, std::min(na + 2, 24)));
+    const int bind = rnd(4), ep = rnd(3);
+    // takeCPUs over the whole available set
+    CpuMask h;
+    const bool hok = take_cpus(*t, 1, avail, n.ref, n.excl, needed, bind, ep, strategy, &h);
+    uint64_t P[TD_POS], R[TD_POS], w[4];
+    td_available(t->dev, cs, P);
+    const bool dok = td_take_cpus(t->dev, P, cs.xc, cs.meta & CM_XN_MASK, needed, bind, ep,
+                                  strategy == GS_NUMA_ALLOC_MOST_ALLOCATED, R);
+    td_to_cpus(t->dev, R, w);
+    if (hok != dok || (hok && std::memcmp(w, h.w, sizeof(w)) != 0)) {
+      char b[256];
+      snprintf(b, sizeof b, "takeCPUs differs (host ok=%d dev ok=%d, need %d bind %d excl %d strategy %d, cpc %d, "
+               "interleave %d)", hok, dok, needed, bind, ep, strategy, cpc, interleave);
+      report(it, b);
+      continue;
+    }
+    // allocateCPUSet with an optional NUMA split
+    const bool required = rnd(2);
+    std::vector<gs_numa_zone> split;
+    uint32_t zkeys = 0;
+    int64_t zcpu[4] = {0, 0, 0, 0};
+    if (rnd(2)) {
+      for (int z = 0; z < nz; ++z) {
+        const int k = rnd(4);
+        if (k == 0) continue;
+        gs_numa_zone a{};
+        a.node_id = n.cfg.zones[z].node_id;
+        if (k != 2) { a.mask |= GS_USAGE_CPU; a.cpu_milli = 1000LL * rnd(needed + 1); zkeys |= 1u << z; zcpu[z] = a.cpu_milli; }
+        if (k != 1) { a.mask |= GS_USAGE_MEMORY; a.memory = 1 << 20; zkeys |= 1u << (4 + z); }
+        split.push_back(a);
+      }
+    }
+    CpuMask h2;
+    const bool hok2 = numa_allocate_cpuset(n, needed, bind, required, ep, strategy, split, &h2);
+    const bool dok2 = td_allocate_cpuset(t->dev, cs, needed, bind, required, ep, zkeys, zcpu, R);
+    td_to_cpus(t->dev, R, w);
+    if (hok2 != dok2 || (hok2 && std::memcmp(w, h2.w, sizeof(w)) != 0)) {
+      char b[256];
+      snprintf(b, sizeof b, "allocateCPUSet differs (host ok=%d dev ok=%d, need %d bind %d required %d excl %d, "
+               "%zu zones)", hok2, dok2, needed, bind, required, ep, split.size());
+      report(it, b);
+      continue;
+    }
+    // post-Reserve counts (the columns the commit kernel recomputes)
+    if (hok2) {
+      PodAllocRec rec;
+      rec.uid = 1;
+      rec.cpus = h2;
+      rec.excl = ep;
+      NumaNode n2 = n;
+      numa_add(n2, rec);
+      CpuStateDev cs2 = cs, want;
+      for (int j = 0; j < TD_POS; ++j) cs2.un[j] |= R[j];
+      numa_cpu_state(n2, dmost, &want);
+      int64_t i64[NUM_I64_COLS] = {0}, i32[NUM_I32_COLS] = {0};
+      numa_derive(n2, dmost, i64, i32);
+      if (td_counts(t->dev, cs2, ~0ull) != (int32_t)i32[C_TFREE] ||
+          std::memcmp(cs2.un, want.un, sizeof(want.un)) != 0) {
+        report(it, "post-Reserve availability counts differ");
+        continue;
+      }
+    }
+  }
+  return bad;
+}

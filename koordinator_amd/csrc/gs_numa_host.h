@@ -11,6 +11,7 @@
 #include <vector>
 
 #include "../../include/gpuscore.h"
+#include "gs_cpuset_dev.h"
 
 namespace gs {
 
@@ -31,6 +32,7 @@ struct TopoClass {
   int cpc = 0, cpn = 0, cps = 0;    // CPUsPerCore / CPUsPerNode / CPUsPerSocket
   int32_t core[GS_MAX_CPUS] = {0};
   uint8_t socket[GS_MAX_CPUS] = {0}, node[GS_MAX_CPUS] = {0};
+  TopoDev dev{};                    // bit-plane form for the device-side cpuset Reserve (dev.ok = 0: host only)
 };
 
 struct ZoneAlloc {                  // NodeAllocation.allocatedResources[numa node] (node_allocation.go:37)
@@ -59,8 +61,11 @@ struct NumaNode {
 std::shared_ptr<TopoClass> make_topo(const gs_cpu_topology& t, const char** err);
 void numa_add(NumaNode& n, const PodAllocRec& a);      // addPodAllocation (node_allocation.go:82-110)
 void numa_release(NumaNode& n, uint64_t uid);          // release (node_allocation.go:112-140)
-// Derived columns: i64 = the row's int64 words, i32 = its int32 words (gs_layout.h order)
-void numa_derive(const NumaNode& n, int64_t* i64, int64_t* i32_widened);
+// Derived columns: i64 = the row's int64 words, i32 = its int32 words (gs_layout.h order). default_most:
+// NUMAScoringStrategy MostAllocated (the NUMAAllocateStrategy of nodes that do not set one).
+void numa_derive(const NumaNode& n, bool default_most, int64_t* i64, int64_t* i32_widened);
+// CpuStateDev of a node (topo = -1 unless its topology has a TopoDev and maxRefCount <= 1)
+void numa_cpu_state(const NumaNode& n, bool default_most, CpuStateDev* cs);
 // Available CPUs (getAvailableCPUs, node_allocation.go:142-162, preferred = {})
 CpuMask numa_available(const NumaNode& n);
 // allocateCPUSet (resource_manager.go:273-360) given the NUMA split Allocate produced on the device.

@@ -180,6 +180,10 @@ class Engine:
             self._chk(rc, "gs_debug_mirror_check")
         return rc
 
+    def verify_cpusets(self, on: bool = True):
+        """Re-run the host takeCPUs for every cpuset the commit kernel selects (schedule fails on a difference)."""
+        self._chk(lib().gs_debug_verify_cpuset(self._h, int(on)), "gs_debug_verify_cpuset")
+
 
 def unique_id() -> bytes:
     buf = (C.c_uint8 * 128)()

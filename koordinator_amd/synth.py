@@ -202,13 +202,17 @@ def make_cluster(num_nodes: int, num_pods: int, config_id: int = 1, seed: int | 
     return Cluster(now, nodes, metrics, pm, offsets, a_node, a_pods, a_ts.astype(np.int64), pods)
 
 
-def make_numa(c: Cluster, seed: int | None = None, numa_policy_pct: int = 30, cpuset_pod_pct: int = 20) -> Cluster:
+def make_numa(c: Cluster, seed: int | None = None, numa_policy_pct: int = 30, cpuset_pod_pct: int = 20,
+              mixed: bool = False) -> Cluster:
     """Adds the C3 NodeNUMAResource state to a cluster, in place:
     2 sockets, k in {2, 4} NUMA nodes, SMT2 (logical CPUs = allocatable cores, <= 128); NRT zones split cpu and
     memory evenly; `numa_policy_pct`% of nodes labelled numa-topology-policy in {SingleNUMANode, Restricted,
     BestEffort}; 3% node cpu-bind-policy FullPCPUsOnly, 2% SpreadByPCPUs; 4% cpu amplification 1.5; existing
     cpuset pods on 25% of nodes and NUMA allocations on labelled nodes; `cpuset_pod_pct`% of pending pods LSR/LSE
-    Prod with integer CPUs (some with a required bind policy)."""
+    Prod with integer CPUs (some with a required bind policy).
+    mixed: also sibling-interleaved CPU numbering (cpu = thread * cores + core), SMT-4 and SMT-1 classes (128
+    SMT-1 cores exceed the device cpuset scope), maxRefCount 2 on 3% of nodes, PCPU- and NUMANode-level
+    exclusive existing allocations and pods."""
     from . import numa as nm
     s = Stream((BASE_SEED + 77) if seed is None else seed)
     N = c.num_nodes
@@ -222,15 +226,23 @@ def make_numa(c: Cluster, seed: int | None = None, numa_policy_pct: int = 30, cp
             classes[key] = len(classes)
         tid_of[i] = classes[key]
     topos = []
-    for (nc, kk), _ in sorted(classes.items(), key=lambda kv: kv[1]):
+    for ci, ((nc, kk), _) in enumerate(sorted(classes.items(), key=lambda kv: kv[1])):
         per_socket = kk // 2
-        cores_per_numa = nc // 2 // kk
-        cpus = []
+        smt, interleave = 2, False
+        if mixed:
+            smt = 4 if ci % 5 == 2 else (1 if ci % 7 == 3 else 2)
+            interleave = ci % 3 == 1
+        cores_per_numa = nc // smt // kk
+        ncores = 2 * per_socket * cores_per_numa
+        cpus = [None] * (ncores * smt)
+        g = 0
         for sk in range(2):
             for nn in range(per_socket):
                 for co in range(cores_per_numa):
-                    for _t in range(2):
-                        cpus.append((sk, sk * per_socket + nn, nn * cores_per_numa + co))
+                    for t in range(smt):
+                        cpu = t * ncores + g if interleave else g * smt + t
+                        cpus[cpu] = (sk, sk * per_socket + nn, nn * cores_per_numa + co)
+                    g += 1
         topos.append(nm.topology(cpus))
     pol = s.randint(301, N, 0, 99)
     policy = np.where(pol < numa_policy_pct // 3, "SingleNUMANode",
@@ -249,7 +261,8 @@ def make_numa(c: Cluster, seed: int | None = None, numa_policy_pct: int = 30, cp
         zones = [(z, zc, int(mem[i]) // kk) for z in range(kk)]
         recs[i] = nm.node_numa(int(tid_of[i]), zones, numa_policy=str(policy[i]),
                                node_cpu_bind="FullPCPUsOnly" if bindk[i] < 3 else ("SpreadByPCPUs" if bindk[i] < 5 else ""),
-                               cpu_ratio=ratio, node_cpu_ratio=1.5 if amp[i] else -1.0)
+                               cpu_ratio=ratio, node_cpu_ratio=1.5 if amp[i] else -1.0,
+                               max_ref_count=2 if (mixed and bindk[i] >= 97) else 1)
     if amp.any():   # amplified allocatable (NodeResource controller), as makeNode does in plugin_test.go:114-120
         c.nodes["allocatable"][amp, 0] = np.ceil(c.nodes["allocatable"][amp, 0] * 1.5).astype(np.int64)
     # existing allocations: a cpuset pod (2-8 CPUs from CPU 0 up, full cores) on 25% of nodes; NUMA resources on
@@ -260,7 +273,8 @@ def make_numa(c: Cluster, seed: int | None = None, numa_policy_pct: int = 30, cp
     for i in np.nonzero(has_cs | (policy != ""))[0]:
         cpus = list(range(int(ncs[i]))) if has_cs[i] else []
         numa_res = [(0, int(ncs[i]) * 1000, 4 << 30)] if policy[i] != "" else []
-        allocs.append(nm.pod_allocation(int(0x5EED0000 + i), cpus, numa_res))
+        excl = ("PCPULevel", "NUMANodeLevel", "")[i % 3] if (mixed and cpus) else ""
+        allocs.append(nm.pod_allocation(int(0x5EED0000 + i), cpus, numa_res, exclusive=excl))
         a_nodes.append(int(i))
     c.numa = {"topologies": topos, "node_numa": recs,
               "alloc_nodes": np.array(a_nodes, np.uint32),
@@ -284,6 +298,10 @@ def make_numa(c: Cluster, seed: int | None = None, numa_policy_pct: int = 30, cp
                                                   np.where(cs & (req < 15), abi.CPU_BIND["SpreadByPCPUs"], 0))
     c.pods["preferred_cpu_bind_policy"] = np.where(cs & (req >= 15) & (req < 30), abi.CPU_BIND["SpreadByPCPUs"], 0)
     c.pods["preferred_cpu_exclusive_policy"] = np.where(cs & (req >= 90), abi.CPU_EXCLUSIVE["PCPULevel"], 0)
+    if mixed:
+        c.pods["preferred_cpu_exclusive_policy"] = np.where(cs & (req >= 80) & (req < 90),
+                                                            abi.CPU_EXCLUSIVE["NUMANodeLevel"],
+                                                            c.pods["preferred_cpu_exclusive_policy"])
     return c
 
 

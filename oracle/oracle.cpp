@@ -926,12 +926,14 @@ int or_schedule(or_cluster* c, const gs_pod* pods, uint32_t npods, const uint64_
     if (c->cfg.enabled & (GS_ENABLE_NUMA_FILTER | GS_ENABLE_NUMA_SCORE)) {
       orn::PodAllocation pa;
       if (orn::reserve(c->numa_args, st, c->numa[selected], pod, affinity[selected], &pa) != 0) return GS_ESTATE;
-      if (!pa.numa.empty()) {
-        o.flags |= GS_PLACED_NUMA;
+      if (!pa.numa.empty()) o.flags |= GS_PLACED_NUMA;
+      // the Filter-time affinity hint (topologymanager store) as a mask over the node's zone slots
+      const orn::Hint& h = affinity[selected];
+      if (h.has_mask) {
         const auto& zones = c->numa[selected].opts.numa;
-        for (const auto& nr : pa.numa)
-          for (size_t z = 0; z < zones.size(); ++z)
-            if (zones[z].node == nr.node) o.flags |= 1u << (GS_PLACED_AFFINITY_SHIFT + z);
+        for (size_t z = 0; z < zones.size() && z < 4; ++z)
+          if (zones[z].node >= 0 && zones[z].node < 64 && ((h.mask >> zones[z].node) & 1))
+            o.flags |= 1u << (GS_PLACED_AFFINITY_SHIFT + z);
       }
       if (!pa.cpus.empty()) o.flags |= GS_PLACED_CPUSET;
     }

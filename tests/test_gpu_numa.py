@@ -30,6 +30,7 @@ def test_numa_score_golden_gpu(case):
 def numa_pair(c, **kw):
     cfg = config.make_config(c.num_nodes, enabled=abi.GS_ENABLE_ALL, **kw)
     e = engine_cls()(cfg)
+    e.verify_cpusets(True)   # every device-chosen cpuset is re-checked against the host takeCPUs
     o = orc.Oracle(cfg)
     synth.load_into(e, c)
     synth.load_into(o, c)
@@ -103,6 +104,18 @@ def test_numa_schedule_dense_policies_and_cpusets():
     synth.make_numa(c, numa_policy_pct=90, cpuset_pod_pct=60)
     e, o = numa_pair(c)
     _check_schedule(e, o, c, [150, 1, 249])
+
+
+@pytest.mark.parametrize("batch", [16, 128])
+def test_numa_schedule_mixed_topologies(batch):
+    """Sibling-interleaved CPU numbering, SMT 4, 128-core SMT-1 nodes (outside the device cpuset scope: host
+    takeCPUs and a batch cut), maxRefCount 2 nodes (host path too), PCPU- and NUMANode-level exclusivity."""
+    c = synth.make_cluster(1500, 300, 7)
+    synth.make_numa(c, numa_policy_pct=40, cpuset_pod_pct=60, mixed=True)
+    e, o = numa_pair(c, batch_size=batch)
+    _check_schedule(e, o, c, [200, 100])
+    st = e.stats()
+    assert st["cuts"] > 0, "the host cpuset path was not exercised"
 
 
 def test_numa_schedule_after_release():
