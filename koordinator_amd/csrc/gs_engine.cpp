@@ -130,6 +130,7 @@ struct gs_ctx {
   // registered topologies in bit-plane form (the commit kernel's cpuset Reserve), and the host re-check of
   // every device-chosen cpuset (GS_VERIFY_CPUSET=1)
   TopoDev* d_topos = nullptr;
+  uint8_t* d_aff = nullptr;       // [pod][ld] Filter-time NUMA affinity of policy nodes (eval -> commit Reserve)
   bool verify_cpuset = false;
 };
 
@@ -705,7 +706,7 @@ int run_batch(gs_ctx* c, const gs_pod* pods, int b, int* committed_out) {
     c->numa_idx_stale = false;
   }
   HIP_TRY(c, launch_eval(c->mv, c->d_pods, b, c->pf, c->n0, c->n1, c->d_S, c->ld, prod_cols, c->d_numa_idx, c->numa_n,
-                         c->st));
+                         c->d_aff, c->st));
   HIP_TRY(c, hipEventRecord(c->ev[1], c->st));
   HIP_TRY(c, launch_cand(c->d_S, c->ld, len, c->n0, b, c->max_score, d_lists, d_hdrs, c->st));
   HIP_TRY(c, hipEventRecord(c->ev[2], c->st));
@@ -732,6 +733,10 @@ int run_batch(gs_ctx* c, const gs_pod* pods, int b, int* committed_out) {
   a.committed = c->d_committed;
   a.stamps = c->d_stamps;
   a.topos = c->d_topos;
+  a.aff = c->d_aff;
+  a.ld = c->ld;
+  a.own0 = c->n0;
+  a.own1 = c->n1;
   HIP_TRY(c, hipEventRecord(c->ev[3], c->st));
   HIP_TRY(c, launch_commit(a, c->st));
   HIP_TRY(c, hipEventRecord(c->ev[4], c->st));
@@ -940,6 +945,7 @@ int gs_create(const gs_config* cfg, gs_ctx** out) {
   if ((e = hipMalloc(&c->d_pods, sizeof(PodVec) * c->B)) != hipSuccess) return bail("hipMalloc", e);
   if ((e = hipMalloc(&c->d_seq, 8 * c->B)) != hipSuccess) return bail("hipMalloc", e);
   if ((e = hipMalloc(&c->d_S, (size_t)c->B * c->ld * 2)) != hipSuccess) return bail("hipMalloc S", e);
+  if ((e = hipMalloc(&c->d_aff, (size_t)c->B * c->ld)) != hipSuccess) return bail("hipMalloc aff", e);
   size_t xb = xchg_block_bytes(c->B);
   if ((e = hipMalloc(&c->d_xchg_send, xb)) != hipSuccess) return bail("hipMalloc", e);
   c->xchg_bytes = xb;
@@ -960,8 +966,8 @@ int gs_create(const gs_config* cfg, gs_ctx** out) {
   if ((e = hipHostMalloc(&c->h_xchg_send, xb, hipHostMallocDefault)) != hipSuccess) return bail("hipHostMalloc", e);
   (void)hipMemset(c->d_S, 0xff, (size_t)c->B * c->ld * 2);
   if (getenv("GS_COMMIT_STAMPS") && getenv("GS_COMMIT_STAMPS")[0] == '1') {
-    if ((e = hipMalloc(&c->d_stamps, 8 * 8)) != hipSuccess) return bail("hipMalloc", e);
-    (void)hipMemset(c->d_stamps, 0, 64);
+    if ((e = hipMalloc(&c->d_stamps, 8 * 12)) != hipSuccess) return bail("hipMalloc", e);
+    (void)hipMemset(c->d_stamps, 0, 96);
   }
   if ((e = hipDeviceSynchronize()) != hipSuccess) return bail("hipDeviceSynchronize", e);
   // 96 B (LoadAware + Fit row), + 192 B NodeNUMAResource columns when enabled
@@ -973,12 +979,12 @@ int gs_create(const gs_config* cfg, gs_ctx** out) {
 int gs_destroy(gs_ctx* c) {
   if (!c) return GS_EINVAL;
   if (c->d_stamps) {
-    uint64_t st[8] = {};
-    if (hipMemcpy(st, c->d_stamps, 64, hipMemcpyDeviceToHost) == hipSuccess) {
+    uint64_t st[12] = {};
+    if (hipMemcpy(st, c->d_stamps, 96, hipMemcpyDeviceToHost) == hipSuccess) {
       uint64_t tot = 0;
       for (uint64_t v : st) tot += v;
       fprintf(stderr, "gpuscore commit phases (s_memtime ticks, %% of %llu):", (unsigned long long)tot);
-      for (int i = 0; i < 8; ++i) fprintf(stderr, " p%d=%.1f%%", i, tot ? 100.0 * st[i] / tot : 0.0);
+      for (int i = 0; i < 12; ++i) fprintf(stderr, " p%d=%.1f%%", i, tot ? 100.0 * st[i] / tot : 0.0);
       fprintf(stderr, "\n");
     }
     (void)hipFree(c->d_stamps);
@@ -987,7 +993,7 @@ int gs_destroy(gs_ctx* c) {
   if (c->st) (void)hipStreamSynchronize(c->st);
   void* dev[] = {c->d_i64, c->d_i32, c->d_pods, c->d_seq, c->d_S, c->d_xchg_send, c->d_xchg_recv, c->d_out,
                  c->d_committed, c->d_rowstat, c->d_sel, c->d_stage_idx, c->d_stage_rows, c->d_numa_idx,
-                 c->d_topos};
+                 c->d_topos, c->d_aff};
   for (void* p : dev)
     if (p) (void)hipFree(p);
   void* host[] = {c->h_pods, c->h_seq, c->h_out, c->h_committed, c->h_stage_idx, c->h_stage_rows, c->h_xchg_send,

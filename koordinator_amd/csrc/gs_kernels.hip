@@ -112,6 +112,7 @@ __device__ __forceinline__ void load_row(const MirrorView& m, uint32_t i, bool p
 struct PairOut {
   uint32_t code;
   int32_t fit, la, numa;
+  uint32_t aff;         // NodeNUMAResource Filter-time affinity (NumaOut.aff)
 };
 
 // NodeInfo slot views for numa_eval: Allocatable and Allocatable - Requested per resource slot
@@ -134,7 +135,7 @@ struct SlotsLds {
 // nodes to eval_numa_kernel)
 template <bool FULL, bool LDS_SCALARS, bool NUMA_POLICY_NODES = true>
 __device__ __forceinline__ PairOut eval_pair(const Row& r, const PodVec& p, const Profile& pf, const MirrorView& m) {
-  PairOut o{0u, 0, 0, 0};
+  PairOut o{0u, 0, 0, 0, 0u};
   // ---- [upstream] noderesources Fit.Filter -> fitsRequest
   if (pf.enabled & 0x1u) {
     if (r.free_pods < 1) o.code |= 0x01u;                               // len(Pods)+1 > AllowedPodNumber
@@ -165,6 +166,7 @@ __device__ __forceinline__ PairOut eval_pair(const Row& r, const PodVec& p, cons
     if (pf.enabled & 0x10u) o.code |= no.reason << GS_FAIL_NUMA_SHIFT;
     if (!FULL && o.code) return o;
     o.numa = no.reason ? 0 : no.score;
+    o.aff = no.aff;
   }
   // ---- Fit.Score, LeastAllocated over NonZeroRequested ([upstream] resource_allocation.go)
   if (pf.enabled & 0x2u) {
@@ -255,7 +257,7 @@ __global__ void __launch_bounds__(256) eval_kernel(MirrorView m, const PodVec* _
 __global__ void __launch_bounds__(256) eval_numa_kernel(MirrorView m, const PodVec* __restrict__ pods, int npods,
                                                         Profile pf, const uint32_t* __restrict__ idx, uint32_t nidx,
                                                         uint32_t n0, int16_t* __restrict__ S, uint32_t ld,
-                                                        int prod_cols) {
+                                                        int prod_cols, uint8_t* __restrict__ aff) {
   // one (node, pod) pair per thread: the per-pair work is long and batches ending at cpuset pods are short,
   // so parallelism over pods matters more than row reuse (rows are L2/MALL resident)
   const uint32_t t = blockIdx.x * 256 + threadIdx.x;
@@ -266,6 +268,7 @@ __global__ void __launch_bounds__(256) eval_numa_kernel(MirrorView m, const PodV
   load_row(m, node, prod_cols, true, row);
   PairOut o = eval_pair<false, false, true>(row, pods[k], pf, m);
   S[(size_t)k * ld + (node - n0)] = (int16_t)total_score(o, pf);
+  aff[(size_t)k * ld + (node - n0)] = (uint8_t)(o.code ? 0u : o.aff);   // read by the commit's Reserve
 }
 
 // Diagnostic variant (gs_evaluate): every plugin's verdict and score for every pair.
@@ -554,7 +557,7 @@ __device__ __noinline__ bool cpuset_reserve(const TopoDev& t, CpuStateDev& cs, c
 // ST: diagnostic build with s_memtime phase stamps (accumulated per phase, written to a.stamps)
 template <bool ST>
 __global__ void __launch_bounds__(256) commit_kernel(CommitArgs a) {
-  uint64_t st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  uint64_t st_acc[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
   uint64_t st_last = ST ? __builtin_amdgcn_s_memtime() : 0;
 #define STAMP(i)                                    \
   do {                                              \
@@ -589,6 +592,7 @@ __global__ void __launch_bounds__(256) commit_kernel(CommitArgs a) {
   __shared__ int s_cut;                                // the pod just committed needs host-side Reserve
   __shared__ TopoDev s_topo;                           // topology of the last cpuset Reserve (bit-plane form)
   __shared__ int s_topo_id;
+  __shared__ int s_aff;                                // known affinity of pod k on its winner row (-1: recompute)
   const bool numa_on = (a.pf.enabled & 0x30u) != 0;
 
   if (tid == 0) s_topo_id = -1;
@@ -822,10 +826,15 @@ __global__ void __launch_bounds__(256) commit_kernel(CommitArgs a) {
         if (lane >= 20 && lane < 26) cw[lane - 20] = (uint64_t)m.c64(C_CPU_UN0 + (lane - 20))[winner];
         if (lane == 26) cst[slot].meta = (uint32_t)m.c32(C_CPU_META)[winner];
         if (lane == 27) cst[slot].topo = m.c32(C_TOPO_DEV)[winner];
+        if (lane == 28) {   // the batch-start Filter's affinity for this pair (own shard, NUMA-policy nodes)
+          const bool own = a.aff && winner >= a.own0 && winner < a.own1;
+          s_aff = own ? (int)a.aff[(size_t)k * a.ld + (winner - a.own0)] : -1;
+        }
       }
     }
     if (lane == 0) {
       s_action = 0; s_slot = slot; s_fresh = fresh; s_winner = winner; s_M = M; s_F = F; s_T = T;
+      if (!fresh || !numa_on) s_aff = -1;   // a dirty row changed since the batch-start Filter
     }
     STAMP(6);
    } while (0);
@@ -850,6 +859,7 @@ __global__ void __launch_bounds__(256) commit_kernel(CommitArgs a) {
         if (tid == 0) s_topo_id = tp;
       }
     }
+    if (tid == 0) STAMP(9);
     if (tid == 0) {
       if (fresh) d = orow;
       const PodVec& pk = pods[k];
@@ -857,12 +867,15 @@ __global__ void __launch_bounds__(256) commit_kernel(CommitArgs a) {
       PlacementDev pl{(int32_t)s_winner, (uint32_t)s_F, (int64_t)s_M, (uint32_t)s_T, forced ? 1u : 0u, 0, 0,
                       {0, 0, 0, 0}, {0, 0, 0, 0}};
       s_cut = 0;
-      if (numa_on && !(pk.numa & (PN_SKIP | PN_PREFAIL))) {
+      const uint32_t nf = d.nr.nflags;
+      // Reserve returns at once unless requestCPUBind (util.go:105-122) or the node has a NUMA policy
+      const bool maybe_rb = (pk.numa & PN_BIND) || (((nf >> NF_BIND_SHIFT) & 3u) && (pk.req_keys & 1u) && pk.req[0]);
+      if (numa_on && !(pk.numa & (PN_SKIP | PN_PREFAIL)) && (maybe_rb || ((nf >> NF_POLICY_SHIFT) & 3u))) {
         // NodeNUMAResource Reserve (plugin.go:375-422) on the pre-assume row: the Filter-time affinity and the
         // NUMA split of Allocate; a cpuset pod's CPUs are selected here (gs_cpuset_dev.h) when the node's
         // topology is in the device scope, else the batch ends with it and the host selects them
-        NumaOut no = numa_eval(d.nr, pk, a.pf, SlotsLds{d, m}, a.pf.enabled & 0x10u, false);
-        const uint32_t nf = d.nr.nflags;
+        NumaOut no = numa_eval(d.nr, pk, a.pf, SlotsLds{d, m}, a.pf.enabled & 0x10u, false, s_aff);
+        STAMP(10);
         const bool rb = no.flags & GS_PLACED_CPUSET;
         if (no.reason) pl.flags |= PL_RESERVE_FAILED;   // cannot happen for a feasible winner
         if (rb || ((nf >> NF_POLICY_SHIFT) & 3u)) {
@@ -886,6 +899,7 @@ __global__ void __launch_bounds__(256) commit_kernel(CommitArgs a) {
             if (cs.topo >= 0 && cs.topo == s_topo_id) {
               if (cpuset_reserve(s_topo, cs, pk, nf, no, d.nr, pl.cpuset)) pl.flags |= PL_DEVICE_CPUSET;
               else pl.flags |= PL_RESERVE_FAILED;
+              STAMP(11);
             } else {
               s_cut = 1;
             }
@@ -906,16 +920,17 @@ __global__ void __launch_bounds__(256) commit_kernel(CommitArgs a) {
     }
     __syncthreads();
     if (s_cut) { committed = k + 1; break; }
+    if (tid == 0) STAMP(7);
     // batch-start scores (fresh rows) on threads 0..127, current scores on threads 128..255
     if (tid < 128) {
-      int q = k + 1 + tid;
+      const int q = k + 1 + tid;
       if (fresh && q < B) dso[q * B + slot] = (int16_t)row_score(orow, pods[q], a.pf, m);
     } else {
-      int q = k + 1 + (tid - 128);
+      const int q = k + 1 + (tid - 128);
       if (q < B) dsc[q * B + slot] = (int16_t)row_score(d, pods[q], a.pf, m);
     }
     __syncthreads();
-    if (tid == 0) STAMP(7);
+    if (tid == 0) STAMP(8);
   }
   // write back dirty rows (slots are dense: count them from the hash)
   __shared__ int s_nd;
@@ -945,7 +960,7 @@ __global__ void __launch_bounds__(256) commit_kernel(CommitArgs a) {
     }
   if (tid == 0) *a.committed = committed;
   if (ST && tid == 0)
-    for (int i = 0; i < 8; ++i) a.stamps[i] += st_acc[i];
+    for (int i = 0; i < 12; ++i) a.stamps[i] += st_acc[i];
 #undef STAMP
 }
 
@@ -1034,7 +1049,7 @@ hipError_t launch_node_prep(const MirrorView& m, uint32_t n0, uint32_t n1, int64
 
 hipError_t launch_eval(const MirrorView& m, const PodVec* pods, int npods, const Profile& pf, uint32_t n0, uint32_t n1,
                        int16_t* S, uint32_t ld, int prod_cols, const uint32_t* numa_idx, uint32_t numa_n,
-                       hipStream_t st) {
+                       uint8_t* aff, hipStream_t st) {
   uint32_t len = n1 - n0;
   uint32_t gx = (len + 255) / 256;
   uint32_t gy = (npods + PODS_PER_BLOCK - 1) / PODS_PER_BLOCK;
@@ -1043,7 +1058,7 @@ hipError_t launch_eval(const MirrorView& m, const PodVec* pods, int npods, const
     hipLaunchKernelGGL(eval_kernel<true>, dim3(gx, gy), dim3(256), 0, st, m, pods, npods, pf, n0, n1, S, ld, prod_cols);
     if (numa_n)
       hipLaunchKernelGGL(eval_numa_kernel, dim3((numa_n + 255) / 256, npods), dim3(256), 0, st, m, pods, npods, pf,
-                         numa_idx, numa_n, n0, S, ld, prod_cols);
+                         numa_idx, numa_n, n0, S, ld, prod_cols, aff);
   } else {
     hipLaunchKernelGGL(eval_kernel<false>, dim3(gx, gy), dim3(256), 0, st, m, pods, npods, pf, n0, n1, S, ld, prod_cols);
   }

@@ -37,6 +37,8 @@ struct NumaOut {
   uint32_t flags;          // GS_PLACED_NUMA / GS_PLACED_CPUSET / affinity bits, for Reserve
   uint32_t zkeys;          // allocation by hint: bit z cpu, bit 4+z memory
   int64_t zcpu[4], zmem[4];
+  uint32_t aff;            // the Filter-time affinity: 0x10 | zone-slot mask, 0 = none (NUMA-policy nodes)
+  uint32_t pad;
 };
 
 __device__ __forceinline__ void load_numa_row(const MirrorView& m, uint32_t i, NumaRow& r) {
@@ -116,9 +118,11 @@ __device__ __forceinline__ bool narrower(uint32_t a, uint32_t b) {   // bitmask.
 // `alloc[s]`/`free[s]` give NodeInfo.Allocatable / Allocatable-Requested for slots 0..2 and the scalars.
 // POLICY_NODES = false compiles only the path of nodes without a NUMA topology policy (the caller routes
 // policy nodes to a kernel of their own); such a call on a policy node returns with reason 0 and no score.
+// known_aff >= 0: the affinity this pair's Filter produced on the same row state (NumaOut.aff; Reserve of a
+// row untouched since the batch-start evaluation): hint generation and merge are skipped.
 template <bool POLICY_NODES = true, class Slots>
 __device__ __forceinline__ NumaOut numa_eval(const NumaRow& r, const PodVec& p, const Profile& pf, const Slots& sl,
-                                             bool do_filter, bool do_score) {
+                                             bool do_filter, bool do_score, int known_aff = -1) {
   NumaOut o{};
   const uint32_t pn = p.numa;
   if (pn & PN_PREFAIL) { o.reason = GS_NUMA_INVALID_REQUESTED_CPUS; return o; }
@@ -229,7 +233,10 @@ __device__ __forceinline__ NumaOut numa_eval(const NumaRow& r, const PodVec& p, 
   const uint32_t full_mask = (1u << nz) - 1u;
   bool aff_has = false;
   uint32_t aff = 0;
-  if (do_filter) {
+  if (do_filter && known_aff >= 0) {
+    aff_has = known_aff & 0x10;
+    aff = (uint32_t)known_aff & 15u;
+  } else if (do_filter) {
     // GetPodTopologyHints (topology_hint.go:41-67) -> GetTopologyHints (resource_manager.go:122-138)
     bool nil_hints = false;
     int64_t hv_cpu[4];
@@ -255,6 +262,33 @@ __device__ __forceinline__ NumaOut numa_eval(const NumaRow& r, const PodVec& p, 
     uint64_t sc_lo = 0, sc_hi = 0;
     int min_c = nz, min_m = nz;
     bool tot_c_any = false, tot_m_any = false;
+    // numaScorer.score(requested = total - available (non-negative), total, pod) of the hint over mask mk
+    // (resource_manager.go:454-457); evaluated only for the hints the merge below can compare
+    auto mask_score = [&](uint32_t mk) -> uint64_t {
+      int64_t tc = 0, tm = 0, fc = 0, fm = 0;
+      bool kc = false, km = false;
+#pragma unroll
+      for (int z = 0; z < 4; ++z) {
+        if (!(mk >> z & 1u)) continue;
+        if (nf >> (NF_ZCPU_SHIFT + z) & 1u) { tc += r.zcap_cpu[z]; kc = true; }
+        if (nf >> (NF_ZMEM_SHIFT + z) & 1u) { tm += r.zcap_mem[z]; km = true; }
+        fc += hv_cpu[z];
+        fm += av_mem[z];
+      }
+      int32_t ns = 0, ws = 0;
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        int32_t w = pf.numa_w[s];
+        if (!w) continue;
+        const int64_t al = s == 0 ? (kc ? tc : 0) : (km ? tm : 0);
+        if (al == 0) continue;
+        const int64_t used = s == 0 ? (kc ? (tc - fc > 0 ? tc - fc : 0) : 0) : (km ? (tm - fm > 0 ? tm - fm : 0) : 0);
+        const int64_t rq = used + (s == 0 ? pcpu : mem);
+        ns += (pf.numa_hint_most ? mr_score(rq, al) : lr_score(rq, al)) * w;
+        ws += w;
+      }
+      return (uint64_t)(ws ? sdiv(ns, ws) : 0);
+    };
     if (!nil_hints) {
       const int nmasks = (1 << nz) - 1;
       for (int mi = 0; mi < nmasks; ++mi) {
@@ -269,22 +303,6 @@ __device__ __forceinline__ NumaOut numa_eval(const NumaRow& r, const PodVec& p, 
           fc += hv_cpu[z];
           fm += av_mem[z];
         }
-        // numaScorer.score(requested = total - available (non-negative), total, pod) (resource_manager.go:454-457)
-        int32_t ns = 0, ws = 0;
-#pragma unroll
-        for (int s = 0; s < 2; ++s) {
-          int32_t w = pf.numa_w[s];
-          if (!w) continue;
-          const int64_t al = s == 0 ? (kc ? tc : 0) : (km ? tm : 0);
-          if (al == 0) continue;
-          const int64_t used = s == 0 ? (kc ? (tc - fc > 0 ? tc - fc : 0) : 0) : (km ? (tm - fm > 0 ? tm - fm : 0) : 0);
-          const int64_t rq = used + (s == 0 ? pcpu : mem);
-          ns += (pf.numa_hint_most ? mr_score(rq, al) : lr_score(rq, al)) * w;
-          ws += w;
-        }
-        const uint64_t hs = (uint64_t)(ws ? sdiv(ns, ws) : 0);
-        if (mi < 9) sc_lo |= hs << (7 * mi);
-        else sc_hi |= hs << (7 * (mi - 9));
         const int cnt = __popc(mk);
         // generateHints: memory group first, then cpu (resource_manager.go:464-476, 499-532)
         if (has_mem) {
@@ -335,12 +353,19 @@ __device__ __forceinline__ NumaOut numa_eval(const NumaRow& r, const PodVec& p, 
       int best_z = 0, best_s = -1;
       for (uint32_t rr = both; rr; rr &= rr - 1) {
         const int z = __ffs(rr) - 1;
-        const int sz = score_at(z);
+        const int sz = (int)mask_score(1u << z);
         if (sz > best_s) { best_s = sz; best_z = z; }
       }
       b_mask = 1u << best_z;
       b_pref = true;
       b_score = best_s;
+    } else if (!nil_hints) {   // the general merge compares the scores of every listed hint
+      for (uint32_t rr = lc | lm; rr; rr &= rr - 1) {
+        const int mi = __ffs(rr) - 1;
+        const uint64_t hs = mask_score(mask_at(mi));
+        if (mi < 9) sc_lo |= hs << (7 * mi);
+        else sc_hi |= hs << (7 * (mi - 9));
+      }
     }
     for (uint32_t r0 = fast ? 0u : seq0; r0; r0 &= r0 - 1) {
       const int i0 = __ffs(r0) - 1;
@@ -435,7 +460,7 @@ __device__ __forceinline__ NumaOut numa_eval(const NumaRow& r, const PodVec& p, 
     return o;
   }
   if (o.zkeys) o.flags |= GS_PLACED_NUMA;
-  if (aff_has) o.flags |= aff << GS_PLACED_AFFINITY_SHIFT;
+  if (aff_has) { o.flags |= aff << GS_PLACED_AFFINITY_SHIFT; o.aff = 0x10u | aff; }
   if (do_score) {   // calculateAllocatableAndRequested (scoring.go:118-164)
     if (o.zkeys) {
       int64_t ac = 0, am = 0, rqc = 0, rqm = 0;
