@@ -467,6 +467,8 @@ int64_t host_tiebreak_position(uint64_t seed, uint64_t seq, int64_t T) { return 
 // The max M is valid when it exceeds every shard's highest unlisted score (`next`); otherwise the batch
 // is cut at k. Ties at M are ordered by node index across shards (shards are contiguous ranges).
 constexpr int HASH = 1024;
+constexpr int POD_STRIDE = 136;   // LDS bytes per pod vector in the commit kernel (sizeof(PodVec) + 8)
+static_assert(POD_STRIDE >= (int)sizeof(PodVec) && POD_STRIDE % 8 == 0, "pod stride");
 constexpr int WIN = 2 * MAX_BATCH + 8;
 #define WAVE_FENCE() __builtin_amdgcn_wave_barrier()
 
@@ -557,7 +559,7 @@ __device__ __noinline__ bool cpuset_reserve(const TopoDev& t, CpuStateDev& cs, c
 // ST: diagnostic build with s_memtime phase stamps (accumulated per phase, written to a.stamps)
 template <bool ST>
 __global__ void __launch_bounds__(256) commit_kernel(CommitArgs a) {
-  uint64_t st_acc[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+  uint64_t st_acc[14] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
   uint64_t st_last = ST ? __builtin_amdgcn_s_memtime() : 0;
 #define STAMP(i)                                    \
   do {                                              \
@@ -572,8 +574,10 @@ __global__ void __launch_bounds__(256) commit_kernel(CommitArgs a) {
   const int R = a.nranks;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const uint64_t lt_mask = (1ull << lane) - 1ull;
-  PodVec* pods = reinterpret_cast<PodVec*>(cm);                              // B
-  Row* drows = reinterpret_cast<Row*>(pods + B);                             // B dirty slots
+  // pod vectors at a 136-B stride: the re-scoring threads read different pods, and a 128-B stride would put
+  // every lane of a wave on the same two LDS banks
+  auto pods = [&](int i) -> PodVec& { return *reinterpret_cast<PodVec*>(cm + (size_t)i * POD_STRIDE); };
+  Row* drows = reinterpret_cast<Row*>(cm + (size_t)B * POD_STRIDE);          // B dirty slots
   int16_t* dsc = reinterpret_cast<int16_t*>(drows + B);                      // [pod][slot] current score
   int16_t* dso = dsc + B * B;                                                // [pod][slot] batch-start score
   int32_t* hkey = reinterpret_cast<int32_t*>(
@@ -596,7 +600,8 @@ __global__ void __launch_bounds__(256) commit_kernel(CommitArgs a) {
   const bool numa_on = (a.pf.enabled & 0x30u) != 0;
 
   if (tid == 0) s_topo_id = -1;
-  for (int i = tid; i < B; i += 256) pods[i] = a.pods[i];
+  const int my_col = lane < ROW_I64 ? kRowCol[lane] : 0;   // fresh-row fetch column of this lane (loop invariant)
+  for (int i = tid; i < B; i += 256) pods(i) = a.pods[i];
   for (int i = tid; i < HASH; i += 256) { hkey[i] = -1; hval[i] = -1; }
   const MirrorView& m = a.m;
   const int nhl = R * MAXLEV;                    // header lanes: lane = r*MAXLEV + j
@@ -812,7 +817,7 @@ __global__ void __launch_bounds__(256) commit_kernel(CommitArgs a) {
       }
       ++nd;
       int64_t* dw = reinterpret_cast<int64_t*>(&orow);
-      if (lane < ROW_I64) dw[lane] = m.c64(kRowCol[lane])[winner];
+      if (lane < ROW_I64) dw[lane] = m.c64(my_col)[winner];
       if (lane == ROW_I64) orow.free_pods = m.c32(C_FREE_PODS)[winner];
       if (lane == ROW_I64 + 1) orow.dflags = (uint32_t)m.c32(C_DFLAGS)[winner];
       if (lane == ROW_I64 + 2) { orow.node = winner; orow.pad = 0; }
@@ -847,7 +852,7 @@ __global__ void __launch_bounds__(256) commit_kernel(CommitArgs a) {
     const bool fresh = s_fresh;
     Row& d = drows[slot];
     if (numa_on) {   // stage the winner's topology in LDS for a device-side cpuset Reserve (block-uniform test)
-      const PodVec& pq = pods[k];
+      const PodVec& pq = pods(k);
       const int tp = cst[slot].topo;
       const uint32_t nfl = fresh ? orow.nr.nflags : d.nr.nflags;
       if (tp >= 0 && tp != s_topo_id && !(pq.numa & (PN_SKIP | PN_PREFAIL)) &&
@@ -859,10 +864,9 @@ __global__ void __launch_bounds__(256) commit_kernel(CommitArgs a) {
         if (tid == 0) s_topo_id = tp;
       }
     }
-    if (tid == 0) STAMP(9);
     if (tid == 0) {
       if (fresh) d = orow;
-      const PodVec& pk = pods[k];
+      const PodVec& pk = pods(k);
       const bool forced = (k == 0 && a.forced_node >= 0);
       PlacementDev pl{(int32_t)s_winner, (uint32_t)s_F, (int64_t)s_M, (uint32_t)s_T, forced ? 1u : 0u, 0, 0,
                       {0, 0, 0, 0}, {0, 0, 0, 0}};
@@ -921,16 +925,26 @@ __global__ void __launch_bounds__(256) commit_kernel(CommitArgs a) {
     __syncthreads();
     if (s_cut) { committed = k + 1; break; }
     if (tid == 0) STAMP(7);
-    // batch-start scores (fresh rows) on threads 0..127, current scores on threads 128..255
-    if (tid < 128) {
-      const int q = k + 1 + tid;
-      if (fresh && q < B) dso[q * B + slot] = (int16_t)row_score(orow, pods[q], a.pf, m);
-    } else {
-      const int q = k + 1 + (tid - 128);
-      if (q < B) dsc[q * B + slot] = (int16_t)row_score(d, pods[q], a.pf, m);
+    // batch-start scores (fresh rows) on threads 0..127, current scores on threads 128..255; one call site,
+    // so the long pair evaluation exists once in the instruction cache
+    {
+      const bool start = tid < 128;
+      const int q = k + 1 + (tid & 127);
+      const uint64_t t0_ = ST ? __builtin_amdgcn_s_memtime() : 0;
+      if (q < B && (fresh || !start)) {
+        const Row rr = start ? orow : d;   // registers: the evaluation re-reads row words many times
+        (start ? dso : dsc)[q * B + slot] = (int16_t)row_score(rr, pods(q), a.pf, m);
+      }
+      if (ST && tid == 128 && ((d.nr.nflags >> NF_POLICY_SHIFT) & 3u)) {
+        st_acc[12] += 1;
+        st_acc[13] += __builtin_amdgcn_s_memtime() - t0_;
+      }
     }
     __syncthreads();
-    if (tid == 0) STAMP(8);
+    if (tid == 0) {   // rescoring time, split by the winner row's NUMA policy (p8: policy node, p9: none)
+      if ((d.nr.nflags >> NF_POLICY_SHIFT) & 3u) STAMP(8);
+      else STAMP(9);
+    }
   }
   // write back dirty rows (slots are dense: count them from the hash)
   __shared__ int s_nd;
@@ -961,6 +975,7 @@ __global__ void __launch_bounds__(256) commit_kernel(CommitArgs a) {
   if (tid == 0) *a.committed = committed;
   if (ST && tid == 0)
     for (int i = 0; i < 12; ++i) a.stamps[i] += st_acc[i];
+  if (ST && tid == 128) { a.stamps[12] += st_acc[12]; a.stamps[13] += st_acc[13]; }
 #undef STAMP
 }
 
@@ -1093,7 +1108,7 @@ hipError_t launch_cand(const int16_t* S, uint32_t ld, uint32_t len, uint32_t n0,
 }
 
 size_t commit_smem_bytes(int B) {
-  size_t b = (size_t)B * sizeof(PodVec) + (size_t)B * sizeof(Row) + (size_t)B * B * 2 * 2;
+  size_t b = (size_t)B * POD_STRIDE + (size_t)B * sizeof(Row) + (size_t)B * B * 2 * 2;
   b = (b + 15) & ~(size_t)15;
   b += (size_t)HASH * 8 + 16;
   b += (size_t)B * sizeof(CpuStateDev);

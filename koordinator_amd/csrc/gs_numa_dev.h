@@ -96,6 +96,11 @@ __device__ __forceinline__ int32_t mr_score(int64_t req, int64_t cap) {
   if (req > cap) req = cap;
   return numa_pct(req, cap);
 }
+// either scorer with one division site (numa_eval inlines its scorers several times)
+__device__ __forceinline__ int32_t req_score(bool most, int64_t req, int64_t cap) {
+  if (cap == 0 || (!most && req > cap)) return 0;
+  return numa_pct(most ? (req > cap ? cap : req) : cap - req, cap);
+}
 __device__ __forceinline__ int32_t sdiv(int32_t a, int32_t b) {
   int32_t q = (int32_t)((float)a * __builtin_amdgcn_rcpf((float)b));
   if (q * b > a) --q;
@@ -190,20 +195,17 @@ __device__ __forceinline__ NumaOut numa_eval(const NumaRow& r, const PodVec& p, 
       int64_t al = sl.alloc(s);
       if (al == 0) continue;
       int64_t rq = (s == 0 ? rq_cpu : al - sl.free(s)) + preq;
-      ns += (pf.numa_most ? mr_score(rq, al) : lr_score(rq, al)) * w;
+      ns += req_score(pf.numa_most, rq, al) * w;
       ws += w;
     }
     return ws ? sdiv(ns, ws) : 0;
   };
 
   if (policy == GS_NUMA_POLICY_NONE) {
-    if (do_score) {   // scoreWithAmplifiedCPUs (scoring.go:99-116)
-      if (cpu == 0 || amp <= 1.0) {
-        o.score = node_score(req_cpu);
-      } else if (!(topo && !valid)) {
-        int64_t am = (int64_t)r.alloc_cpus * 1000;
-        o.score = node_score(req_cpu - am + amplify_d(am, amp));
-      }
+    const bool plain = cpu == 0 || amp <= 1.0;
+    if (do_score && (plain || !(topo && !valid))) {   // scoreWithAmplifiedCPUs (scoring.go:99-116)
+      const int64_t am = (int64_t)r.alloc_cpus * 1000;
+      o.score = node_score(plain ? req_cpu : req_cpu - am + amplify_d(am, amp));
     }
     return o;
   }
@@ -284,7 +286,7 @@ __device__ __forceinline__ NumaOut numa_eval(const NumaRow& r, const PodVec& p, 
         if (al == 0) continue;
         const int64_t used = s == 0 ? (kc ? (tc - fc > 0 ? tc - fc : 0) : 0) : (km ? (tm - fm > 0 ? tm - fm : 0) : 0);
         const int64_t rq = used + (s == 0 ? pcpu : mem);
-        ns += (pf.numa_hint_most ? mr_score(rq, al) : lr_score(rq, al)) * w;
+        ns += req_score(pf.numa_hint_most, rq, al) * w;
         ws += w;
       }
       return (uint64_t)(ws ? sdiv(ns, ws) : 0);
@@ -349,57 +351,86 @@ __device__ __forceinline__ NumaOut numa_eval(const NumaRow& r, const PodVec& p, 
     if (fast && kc_kind == 1) { fast = min_c == 1; both &= lc & ones; }
     if (fast && km_kind == 1) { fast = min_m == 1; both &= lm & ones; }
     fast = fast && both != 0;
-    if (fast) {
-      int best_z = 0, best_s = -1;
-      for (uint32_t rr = both; rr; rr &= rr - 1) {
-        const int z = __ffs(rr) - 1;
-        const int sz = (int)mask_score(1u << z);
-        if (sz > best_s) { best_s = sz; best_z = z; }
-      }
-      b_mask = 1u << best_z;
-      b_pref = true;
-      b_score = best_s;
-    } else if (!nil_hints) {   // the general merge compares the scores of every listed hint
-      for (uint32_t rr = lc | lm; rr; rr &= rr - 1) {
+    // Preferred-first merge (exact): the first preferred merged hint is always taken and a non-preferred one
+    // never replaces a preferred best, so the permutation scan's result equals the scan over the pairs of
+    // preferred entries alone whenever one of them merges to a non-empty mask (pass 0, at most 6 x 6 pairs);
+    // only otherwise does the full scan run (pass 1). Both visit pairs in policy.go's order.
+    uint32_t pre0 = 0, pre1 = 0;
+    if (!fast && !nil_hints) {
+      for (uint32_t rr = lc; rr; rr &= rr - 1) {
         const int mi = __ffs(rr) - 1;
-        const uint64_t hs = mask_score(mask_at(mi));
-        if (mi < 9) sc_lo |= hs << (7 * mi);
-        else sc_hi |= hs << (7 * (mi - 9));
+        if (__popc(mask_at(mi)) == min_c) pre0 |= 1u << mi;
+      }
+      for (uint32_t rr = lm; rr; rr &= rr - 1) {
+        const int mi = __ffs(rr) - 1;
+        if (__popc(mask_at(mi)) == min_m) pre1 |= 1u << mi;
       }
     }
-    for (uint32_t r0 = fast ? 0u : seq0; r0; r0 &= r0 - 1) {
-      const int i0 = __ffs(r0) - 1;
-      bool h0 = false, p0 = true;
-      uint32_t m0 = 0;
-      int32_t s0 = 0;
-      if (kc_kind == 1) { h0 = true; m0 = mask_at(i0); p0 = __popc(m0) == min_c; s0 = score_at(i0); }
-      else if (kc_kind == 2) { p0 = false; }
-      if (use0 && single && !(p0 && (!h0 || __popc(m0) == 1))) continue;
-      for (uint32_t r1 = seq1; r1; r1 &= r1 - 1) {
-        const int i1 = __ffs(r1) - 1;
-        bool h1 = false, p1 = true;
-        uint32_t m1 = 0;
-        int32_t s1 = 0;
-        if (use1) {
-          if (km_kind == 1) { h1 = true; m1 = mask_at(i1); p1 = __popc(m1) == min_m; s1 = score_at(i1); }
-          else { p1 = false; }
-          if (single && !(p1 && (!h1 || __popc(m1) == 1))) continue;
+    for (int pass = 0; pass < 2; ++pass) {
+      if (pass == 1) {
+        if (fast || b_pref) break;
+        b_mask = full_mask;
+        b_pref = false;
+        b_score = 0;
+      }
+      // scores of the hints this pass compares (single-zone candidates, preferred entries, then the rest)
+      if (!nil_hints) {
+        const uint32_t need = pass == 1 ? (lc | lm) & ~(pre0 | pre1) : (fast ? both : (pre0 | pre1));
+        for (uint32_t rr = need; rr; rr &= rr - 1) {
+          const int mi = __ffs(rr) - 1;
+          const uint64_t hs = mask_score(mask_at(mi));
+          if (mi < 9) sc_lo |= hs << (7 * mi);
+          else sc_hi |= hs << (7 * (mi - 9));
         }
-        uint32_t mg = full_mask;
-        bool pg = true;
-        if (use0) { mg &= h0 ? m0 : full_mask; pg = pg && p0; }
-        if (use1) { mg &= h1 ? m1 : full_mask; pg = pg && p1; }
-        if (mg == 0) continue;
-        int32_t sg = 0;
-        if (use0 && h0 && m0 == mg && s0 > sg) sg = s0;
-        if (use1 && h1 && m1 == mg && s1 > sg) sg = s1;
-        if (pg && !b_pref) { b_mask = mg; b_pref = pg; b_score = sg; continue; }
-        if (!pg && b_pref) continue;
-        if (!narrower(mg, b_mask)) {
-          if (__popc(mg) == __popc(b_mask) && sg > b_score) { b_mask = mg; b_pref = pg; b_score = sg; }
-          continue;
+      }
+      if (fast) {
+        int best_z = 0, best_s = -1;
+        for (uint32_t rr = both; rr; rr &= rr - 1) {
+          const int z = __ffs(rr) - 1;
+          const int sz = score_at(z);
+          if (sz > best_s) { best_s = sz; best_z = z; }
         }
-        b_mask = mg; b_pref = pg; b_score = sg;
+        b_mask = 1u << best_z;
+        b_pref = true;
+        b_score = best_s;
+        continue;
+      }
+      const uint32_t set0 = kc_kind == 1 ? (pass == 0 ? pre0 : lc) : 0x80000000u;
+      const uint32_t set1 = km_kind == 1 ? (pass == 0 ? pre1 : lm) : 0x80000000u;
+      for (uint32_t r0 = set0; r0; r0 &= r0 - 1) {
+        const int i0 = __ffs(r0) - 1;
+        bool h0 = false, p0 = true;
+        uint32_t m0 = 0;
+        int32_t s0 = 0;
+        if (kc_kind == 1) { h0 = true; m0 = mask_at(i0); p0 = __popc(m0) == min_c; s0 = score_at(i0); }
+        else if (kc_kind == 2) { p0 = false; }
+        if (use0 && single && !(p0 && (!h0 || __popc(m0) == 1))) continue;
+        for (uint32_t r1 = set1; r1; r1 &= r1 - 1) {
+          const int i1 = __ffs(r1) - 1;
+          bool h1 = false, p1 = true;
+          uint32_t m1 = 0;
+          int32_t s1 = 0;
+          if (use1) {
+            if (km_kind == 1) { h1 = true; m1 = mask_at(i1); p1 = __popc(m1) == min_m; s1 = score_at(i1); }
+            else { p1 = false; }
+            if (single && !(p1 && (!h1 || __popc(m1) == 1))) continue;
+          }
+          uint32_t mg = full_mask;
+          bool pg = true;
+          if (use0) { mg &= h0 ? m0 : full_mask; pg = pg && p0; }
+          if (use1) { mg &= h1 ? m1 : full_mask; pg = pg && p1; }
+          if (mg == 0) continue;
+          int32_t sg = 0;
+          if (use0 && h0 && m0 == mg && s0 > sg) sg = s0;
+          if (use1 && h1 && m1 == mg && s1 > sg) sg = s1;
+          if (pg && !b_pref) { b_mask = mg; b_pref = pg; b_score = sg; continue; }
+          if (!pg && b_pref) continue;
+          if (!narrower(mg, b_mask)) {
+            if (__popc(mg) == __popc(b_mask) && sg > b_score) { b_mask = mg; b_pref = pg; b_score = sg; }
+            continue;
+          }
+          b_mask = mg; b_pref = pg; b_score = sg;
+        }
       }
     }
     bool admit = true;
@@ -483,7 +514,7 @@ __device__ __forceinline__ NumaOut numa_eval(const NumaRow& r, const PodVec& p, 
         const int64_t al = s == 0 ? ac : am;
         if (al == 0) continue;
         const int64_t rq = (s == 0 ? rqc : rqm) + (s == 0 ? pcpu : mem);
-        ns += (pf.numa_most ? mr_score(rq, al) : lr_score(rq, al)) * w;
+        ns += req_score(pf.numa_most, rq, al) * w;
         ws += w;
       }
       o.score = ws ? sdiv(ns, ws) : 0;
