@@ -966,8 +966,8 @@ int gs_create(const gs_config* cfg, gs_ctx** out) {
   if ((e = hipHostMalloc(&c->h_xchg_send, xb, hipHostMallocDefault)) != hipSuccess) return bail("hipHostMalloc", e);
   (void)hipMemset(c->d_S, 0xff, (size_t)c->B * c->ld * 2);
   if (getenv("GS_COMMIT_STAMPS") && getenv("GS_COMMIT_STAMPS")[0] == '1') {
-    if ((e = hipMalloc(&c->d_stamps, 8 * 14)) != hipSuccess) return bail("hipMalloc", e);
-    (void)hipMemset(c->d_stamps, 0, 112);
+    if ((e = hipMalloc(&c->d_stamps, 8 * 20)) != hipSuccess) return bail("hipMalloc", e);
+    (void)hipMemset(c->d_stamps, 0, 160);
   }
   if ((e = hipDeviceSynchronize()) != hipSuccess) return bail("hipDeviceSynchronize", e);
   // 96 B (LoadAware + Fit row), + 192 B NodeNUMAResource columns when enabled
@@ -979,14 +979,18 @@ int gs_create(const gs_config* cfg, gs_ctx** out) {
 int gs_destroy(gs_ctx* c) {
   if (!c) return GS_EINVAL;
   if (c->d_stamps) {
-    uint64_t st[14] = {};
-    if (hipMemcpy(st, c->d_stamps, 112, hipMemcpyDeviceToHost) == hipSuccess) {
+    uint64_t st[20] = {};
+    if (hipMemcpy(st, c->d_stamps, 160, hipMemcpyDeviceToHost) == hipSuccess) {
       uint64_t tot = 0;
       for (int i = 0; i < 12; ++i) tot += st[i];
       fprintf(stderr, "gpuscore commit phases (s_memtime ticks, %% of %llu):", (unsigned long long)tot);
       for (int i = 0; i < 12; ++i) fprintf(stderr, " p%d=%.1f%%", i, tot ? 100.0 * st[i] / tot : 0.0);
       fprintf(stderr, " | policy-row rescoring: %llu pods, %.0f ticks per pair (thread 128)\n",
               (unsigned long long)st[12], st[12] ? (double)st[13] / st[12] : 0.0);
+      fprintf(stderr, "  numa_eval segments per pair: prelim %.0f hints %.0f merge %.0f alloc %.0f cpuset %.0f score %.0f\n",
+              st[12] ? (double)st[14] / st[12] : 0.0, st[12] ? (double)st[15] / st[12] : 0.0,
+              st[12] ? (double)st[16] / st[12] : 0.0, st[12] ? (double)st[17] / st[12] : 0.0,
+              st[12] ? (double)st[18] / st[12] : 0.0, st[12] ? (double)st[19] / st[12] : 0.0);
     }
     (void)hipFree(c->d_stamps);
   }

@@ -127,7 +127,18 @@ __device__ __forceinline__ bool narrower(uint32_t a, uint32_t b) {   // bitmask.
 // row untouched since the batch-start evaluation): hint generation and merge are skipped.
 template <bool POLICY_NODES = true, class Slots>
 __device__ __forceinline__ NumaOut numa_eval(const NumaRow& r, const PodVec& p, const Profile& pf, const Slots& sl,
-                                             bool do_filter, bool do_score, int known_aff = -1) {
+                                             bool do_filter, bool do_score, int known_aff = -1,
+                                             uint64_t* prof = nullptr) {
+  // prof (diagnostics): s_memtime cycles per segment accumulated into prof[0..5]
+  uint64_t t_np = prof ? __builtin_amdgcn_s_memtime() : 0;
+#define NP(i)                                          \
+  do {                                                 \
+    if (prof) {                                        \
+      const uint64_t t_ = __builtin_amdgcn_s_memtime(); \
+      prof[i] += t_ - t_np;                            \
+      t_np = t_;                                       \
+    }                                                  \
+  } while (0)
   NumaOut o{};
   const uint32_t pn = p.numa;
   if (pn & PN_PREFAIL) { o.reason = GS_NUMA_INVALID_REQUESTED_CPUS; return o; }
@@ -211,6 +222,7 @@ __device__ __forceinline__ NumaOut numa_eval(const NumaRow& r, const PodVec& p, 
   }
 
   // ---- NUMA-policy node
+  NP(0);
   if (!POLICY_NODES) return o;
   const int nz = (nf >> NF_ZONES_SHIFT) & 7;
   if (do_filter && nz == 0) { o.reason = GS_NUMA_MISSING_NUMA_RESOURCES; return o; }
@@ -294,6 +306,18 @@ __device__ __forceinline__ NumaOut numa_eval(const NumaRow& r, const PodVec& p, 
     if (!nil_hints) {
       const int nmasks = (1 << nz) - 1;
       for (int mi = 0; mi < nmasks; ++mi) {
+        if (mi == nz) {
+          // all single-zone masks seen (order positions 0..nz-1): if they already settle the fast merge below
+          // (preferred single-zone hints in every list, a zone common to all), larger masks cannot change
+          // the kinds, minima or candidates it uses, and their hints are never compared
+          const int kc1 = lc ? 1 : ((has_cpu && tot_c_any) ? 2 : 0);
+          const int km1 = lm ? 1 : ((has_mem && tot_m_any) ? 2 : 0);
+          uint32_t bp = (1u << nz) - 1u;
+          if (kc1 == 1) bp &= lc;
+          if (km1 == 1) bp &= lm;
+          if ((kc1 | km1) != 0 && kc1 != 2 && km1 != 2 && (kc1 != 1 || min_c == 1) && (km1 != 1 || min_m == 1) && bp)
+            break;
+        }
         const uint32_t mk = (uint32_t)(order >> (4 * mi)) & 15u;
         int64_t tc = 0, tm = 0, fc = 0, fm = 0;
         bool kc = false, km = false;
@@ -323,6 +347,7 @@ __device__ __forceinline__ NumaOut numa_eval(const NumaRow& r, const PodVec& p, 
         }
       }
     }
+    NP(1);
     auto mask_at = [&](int mi) -> uint32_t { return (uint32_t)(order >> (4 * mi)) & 15u; };
     auto score_at = [&](int mi) -> int32_t {
       return (int32_t)((mi < 9 ? sc_lo >> (7 * mi) : sc_hi >> (7 * (mi - 9))) & 127u);
@@ -433,6 +458,7 @@ __device__ __forceinline__ NumaOut numa_eval(const NumaRow& r, const PodVec& p, 
         }
       }
     }
+    NP(2);
     bool admit = true;
     if (single) {
       if (b_mask == full_mask) b_has = false;   // policy_single_numa_node.go:70-73
@@ -467,6 +493,7 @@ __device__ __forceinline__ NumaOut numa_eval(const NumaRow& r, const PodVec& p, 
     }
     if ((ic && rc != 0) || (im && rm != 0)) fail = true;
   }
+  NP(3);
   if (!fail && rb) {   // allocateCPUSet (resource_manager.go:273-360), counted
     if (cnt_sel(r.tfree, bind, reqflag) < p.num_cpus) fail = true;
     // satisfiedRequiredCPUBindPolicy: FullPCPUs over full cores is met iff the count is a multiple of CPUsPerCore
@@ -492,6 +519,7 @@ __device__ __forceinline__ NumaOut numa_eval(const NumaRow& r, const PodVec& p, 
   }
   if (o.zkeys) o.flags |= GS_PLACED_NUMA;
   if (aff_has) { o.flags |= aff << GS_PLACED_AFFINITY_SHIFT; o.aff = 0x10u | aff; }
+  NP(4);
   if (do_score) {   // calculateAllocatableAndRequested (scoring.go:118-164)
     if (o.zkeys) {
       int64_t ac = 0, am = 0, rqc = 0, rqm = 0;
@@ -522,6 +550,8 @@ __device__ __forceinline__ NumaOut numa_eval(const NumaRow& r, const PodVec& p, 
       o.score = node_score(rb ? amplify_d((int64_t)r.alloc_cpus * 1000, amp) : req_cpu);
     }
   }
+  NP(5);
+#undef NP
   return o;
 }
 
