@@ -221,3 +221,157 @@ for name, topo, pref, n, labels, want in plugin_score:
 with open(os.path.join(HERE, "numa_score.json"), "w") as f:
     json.dump({"cases": score_cases}, f, indent=1)
 print(f"wrote {len(score_cases)} NodeNUMAResource score cases")
+
+# ---- plugin-level Filter / affinity / Reserve vectors: plugin_test.go -----------------------------------------
+P = "plugin_test.go"
+
+
+def filter_node(labels=None):
+    """TestPlugin_Filter node (plugin_test.go:827-876): allocatable cpu 96, memory 512Gi; options = CPUTopology
+    (2,1,4,2) + one NUMANodeResource per NUMA node {cpu: CPUsPerNode, memory: 32Gi}"""
+    d = {"cpu_milli": 96000, "memory": 512 * GI, "numa_policy": "", "topology": [2, 1, 4, 2],
+         "zones": [[0, 8000, 32 * GI], [1, 8000, 32 * GI]]}
+    d.update(labels or {})
+    return d
+
+
+# (name, lines, node labels, pod, want reason); the Go test writes preFilterState directly: requestCPUBind
+# true <=> an LSR Prod pod with the listed policies, false <=> an LS pod with the same cpu request
+LSR = {"qos": "LSR", "prod": True}
+filter_cases = [
+    ("failed to verify Node FullPCPUsOnly with SMTAlignmentError", "592-605", {"node_cpu_bind": "FullPCPUsOnly"},
+     {"cpu": 5000, **LSR, "preferred": "FullPCPUs"}, "SMT_ALIGNMENT"),
+    ("LS Pod failed to verify Node FullPCPUsOnly with SMTAlignmentError", "606-621", {"node_cpu_bind": "FullPCPUsOnly"},
+     {"cpu": 5000}, "SMT_ALIGNMENT"),
+    ("LS Pod failed to verify Node FullPCPUsOnly with non-integer request", "622-637", {"node_cpu_bind": "FullPCPUsOnly"},
+     {"cpu": 5200}, "INVALID_REQUESTED_CPUS"),
+    ("verify Node FullPCPUsOnly", "638-651", {"node_cpu_bind": "FullPCPUsOnly"},
+     {"cpu": 4000, **LSR, "preferred": "FullPCPUs"}, None),
+    ("failed to verify required FullPCPUs SMTAlignmentError", "652-662", {},
+     {"cpu": 5000, **LSR, "required": "FullPCPUs"}, "SMT_ALIGNMENT"),
+    ("verify required FullPCPUs", "663-673", {}, {"cpu": 4000, **LSR, "required": "FullPCPUs"}, None),
+    ("verify FullPCPUsOnly with preferred SpreadByPCPUs", "674-687", {"node_cpu_bind": "FullPCPUsOnly"},
+     {"cpu": 4000, **LSR, "preferred": "SpreadByPCPUs"}, None),
+    ("failed to verify FullPCPUsOnly with required SpreadByPCPUs", "688-701", {"node_cpu_bind": "SpreadByPCPUs"},
+     {"cpu": 4000, **LSR, "required": "FullPCPUs"}, "BIND_POLICY_CONFLICT"),
+    ("verify FullPCPUsOnly with required FullPCPUs", "702-715", {"node_cpu_bind": "FullPCPUsOnly"},
+     {"cpu": 4000, **LSR, "required": "FullPCPUs"}, None),
+    # the kubelet static policy with full-pcpus-only decodes to the node CPU bind policy FullPCPUsOnly
+    ("verify Kubelet FullPCPUsOnly with SMTAlignmentError", "716-732", {"node_cpu_bind": "FullPCPUsOnly"},
+     {"cpu": 5000, **LSR, "preferred": "FullPCPUs"}, "SMT_ALIGNMENT"),
+    ("verify Kubelet FullPCPUsOnly with required SpreadByPCPUs", "733-749", {"node_cpu_bind": "FullPCPUsOnly"},
+     {"cpu": 4000, **LSR, "required": "SpreadByPCPUs"}, "BIND_POLICY_CONFLICT"),
+    ("verify Kubelet FullPCPUsOnly with required FullPCPUs", "750-766", {"node_cpu_bind": "FullPCPUsOnly"},
+     {"cpu": 4000, **LSR, "required": "FullPCPUs"}, None),
+    ("verify required FullPCPUs with none NUMA topology policy", "767-777", {},
+     {"cpu": 4000, **LSR, "required": "FullPCPUs", "preferred": "FullPCPUs"}, None),
+    ("verify FullPCPUs with NUMA Topology Policy", "778-791", {"numa_policy": "SingleNUMANode"},
+     {"cpu": 4000, **LSR, "required": "FullPCPUs", "preferred": "FullPCPUs"}, None),
+    ("verify FullPCPUs with NUMA Topology Policy and amplification ratio", "792-808",
+     {"numa_policy": "SingleNUMANode", "node_cpu_ratio": 1.5},
+     {"cpu": 4000, **LSR, "required": "FullPCPUs", "preferred": "FullPCPUs"}, None),
+    ("verify FullPCPUs with None NUMA Topology Policy and amplification ratio", "809-825", {"node_cpu_ratio": 1.5},
+     {"cpu": 4000, **LSR, "required": "FullPCPUs", "preferred": "FullPCPUs"}, None),
+]
+default_args = {"scoring": "LeastAllocated", "weights": {"cpu": 1, "memory": 1}}
+plugin_cases = []
+for name, lines, labels, pod, want in filter_cases:
+    plugin_cases.append({"kind": "filter", "src": f"{P}:{lines} TestPlugin_Filter", "name": name, "args": default_args,
+                         "nodes": [filter_node(labels)], "allocations": [], "pod": pod, "filter": True,
+                         "want_reason": want})
+
+
+def amp_node(ratio, nrt, requested_cpu):
+    """TestFilterWithAmplifiedCPUs node (plugin_test.go:969-996): makeNode(cpu = NumCPUs of (2,1,8,2) = 32,
+    memory 40Gi, ratio) amplifies allocatable cpu; with NRT the options hold the CPUTopology and per NUMA node
+    {cpu: Amplify(CPUsPerNode, ratio), memory 20Gi}; without NRT there are no topology options"""
+    amp = lambda x: x if ratio <= 1 else int(-(-x * ratio // 1))   # noqa: E731  (ceil; integral here)
+    d = {"cpu_milli": amp(32000), "memory": 40 * GI, "numa_policy": "", "node_cpu_ratio": ratio,
+         "requested_cpu": requested_cpu}
+    if nrt:
+        d.update({"topology": [2, 1, 8, 2], "zones": [[0, amp(16) * 1000, 20 * GI], [1, amp(16) * 1000, 20 * GI]]})
+    else:
+        d.update({"topology": None, "zones": [], "has_options": False})
+    return d
+
+
+# (name, lines, pod cpu (None: no requests), pod is cpuset, existing cpu, existing is cpuset, nrt, ratio, want)
+amp_cases = [
+    ("no resources requested always fits", "911-917", None, False, 4, False, False, 2.0, None),
+    ("no filtering without node cpu amplification", "918-924", 32, False, 32, False, False, 1.0, None),
+    ("cpu fits on no NRT node", "925-931", 32, False, 32, False, False, 2.0, None),
+    ("insufficient cpu", "932-939", 32, False, 64, False, False, 2.0, "INSUFFICIENT_AMP_CPU"),
+    ("insufficient cpu with cpuset pod on node", "940-948", 32, False, 32, True, True, 2.0, "INSUFFICIENT_AMP_CPU"),
+    ("insufficient cpu when scheduling cpuset pod", "949-957", 32, True, 32, False, True, 2.0, "INSUFFICIENT_AMP_CPU"),
+    ("insufficient cpu when scheduling cpuset pod with cpuset pod on node", "958-966", 32, True, 32, True, True, 2.0,
+     "INSUFFICIENT_AMP_CPU"),
+]
+for name, lines, pcpu, pcs, ecpu, ecs, nrt, ratio, want in amp_cases:
+    # makePod / makePodOnNode (plugin_test.go:122-139): Prod priority; cpuset pods carry the LSR label and, once on
+    # the node, a resource-status cpuset 0..n-1 that the pod event handler records (only with a valid topology)
+    pod = {"prod": True}
+    if pcpu is not None:
+        pod["cpu"] = pcpu * 1000
+    if pcs:
+        pod["qos"] = "LSR"
+    allocs = [{"node": 0, "uid": 0x1E, "cpus": list(range(ecpu)), "numa": []}] if (ecs and nrt) else []
+    plugin_cases.append({"kind": "filter", "src": f"{P}:{lines} TestFilterWithAmplifiedCPUs", "name": name,
+                         "args": default_args, "nodes": [amp_node(ratio, nrt, ecpu * 1000)], "allocations": allocs,
+                         "pod": pod, "filter": True, "want_reason": want})
+
+
+def affinity_node(policy, count):
+    n = numa_node(104, 256, policy, count)   # TestFilterWithNUMANodeScoring (plugin_test.go:1819-1840)
+    return n
+
+
+least = {"type": "LeastAllocated", "resources": {"cpu": 1, "memory": 1}}
+mostS = {"type": "MostAllocated", "resources": {"cpu": 1, "memory": 1}}
+affinity_cases = [
+    ("single numa nodes and select most allocated", "1685-1706", "SingleNUMANode", 2, {0: (4, 8), 1: (40, 8)}, mostS, [1]),
+    ("single numa nodes and select least allocated", "1707-1728", "SingleNUMANode", 2, {0: (4, 8), 1: (40, 8)}, least, [0]),
+    ("single numa nodes and only one node can be used", "1729-1750", "SingleNUMANode", 2, {0: (4, 8), 1: (52, 8)}, least,
+     [0]),
+    ("restricted numa nodes and select most allocated and preferred", "1751-1778", "Restricted", 4,
+     {0: (24, 8), 1: (23, 8), 2: (4, 8), 3: (8, 8)}, mostS, [3]),
+    ("restricted numa nodes and select least allocated and preferred", "1779-1806", "Restricted", 4,
+     {0: (24, 8), 1: (23, 8), 2: (4, 8), 3: (8, 8)}, least, [2]),
+]
+for name, lines, policy, count, existing_pods, nss, want in affinity_cases:
+    allocs = [{"node": 0, "uid": 0x100 + z, "cpus": [], "numa": [[z, c * 1000, m * GI]]}
+              for z, (c, m) in existing_pods.items()]
+    plugin_cases.append({"kind": "affinity", "src": f"{P}:{lines} TestFilterWithNUMANodeScoring", "name": name,
+                         "args": {**default_args, "numa_scoring": nss}, "nodes": [affinity_node(policy, count)],
+                         "allocations": allocs, "pod": {"cpu": 4000, "memory": 40 * GI}, "filter": True,
+                         "want_affinity": want})
+
+
+def reserve_node(topo, labels=None):
+    """TestPlugin_Reserve node (plugin_test.go:1152-1191): allocatable cpu 96, memory 512Gi; options hold only the
+    CPUTopology (no NUMANodeResources); allocated CPUs added with CPUExclusivePolicyNone"""
+    d = {"cpu_milli": 96000, "memory": 512 * GI, "numa_policy": "", "topology": list(topo), "zones": []}
+    d.update(labels or {})
+    return d
+
+
+FULL = {"cpu": 4000, **LSR, "preferred": "FullPCPUs"}
+reserve_cases = [
+    ("succeed with valid cpu topology", "1048-1059", reserve_node((2, 1, 4, 2)), [], FULL, [0, 1, 2, 3]),
+    ("allocated by node cpu bind policy", "1060-1076", reserve_node((2, 1, 4, 2), {"node_cpu_bind": "SpreadByPCPUs"}),
+     [], {"cpu": 4000}, [0, 2, 4, 6]),
+    ("BE Pod reserves with node cpu bind policy", "1077-1093",
+     reserve_node((2, 1, 4, 2), {"node_cpu_bind": "SpreadByPCPUs"}), [], {"batch_cpu": 4000}, []),
+    ("succeed with valid cpu topology and node numa least allocate strategy", "1104-1119",
+     reserve_node((2, 1, 8, 2), {"numa_allocate_strategy": "LeastAllocated"}), [0, 1, 2, 3], FULL, [16, 17, 18, 19]),
+    ("succeed with valid cpu topology and node numa most allocate strategy", "1120-1135",
+     reserve_node((2, 1, 8, 2), {"numa_allocate_strategy": "MostAllocated"}), [0, 1, 2, 3], FULL, [4, 5, 6, 7]),
+]
+for name, lines, node, allocated, pod, want in reserve_cases:
+    allocs = [{"node": 0, "uid": 0x77, "cpus": allocated, "numa": []}] if allocated else []
+    plugin_cases.append({"kind": "reserve", "src": f"{P}:{lines} TestPlugin_Reserve", "name": name,
+                         "args": default_args, "nodes": [node], "allocations": allocs, "pod": pod, "filter": True,
+                         "want_cpuset": want})
+
+with open(os.path.join(HERE, "numa_plugin.json"), "w") as f:
+    json.dump({"cases": plugin_cases}, f, indent=1)
+print(f"wrote {len(plugin_cases)} NodeNUMAResource plugin cases (Filter, affinity, Reserve)")

@@ -9,15 +9,16 @@ from koordinator_amd import abi, config, numa
 HERE = os.path.dirname(os.path.abspath(__file__))
 
 
-def load():
-    return json.load(open(os.path.join(HERE, "golden", "numa_score.json")))
+def load(name="numa_score.json"):
+    return json.load(open(os.path.join(HERE, "golden", name)))
 
 
 def build(case, cls, device=0):
     nodes_spec = case["nodes"]
     N = len(nodes_spec)
     a = case["args"]
-    nargs = config.numa_args(scoringStrategy={"type": a["scoring"], "resources": a["weights"]})
+    extra = {"numaScoringStrategy": a["numa_scoring"]} if "numa_scoring" in a else {}
+    nargs = config.numa_args(scoringStrategy={"type": a["scoring"], "resources": a["weights"]}, **extra)
     enabled = abi.GS_ENABLE_NUMA_SCORE | (abi.GS_ENABLE_NUMA_FILTER if case["filter"] else 0)
     cfg = config.make_config(N, enabled=enabled, numa=nargs, device=device)
     e = cls(cfg)
@@ -26,6 +27,7 @@ def build(case, cls, device=0):
         nodes[i]["allocatable"][abi.GS_RES_CPU] = n["cpu_milli"]
         nodes[i]["allocatable"][abi.GS_RES_MEMORY] = n["memory"]
         nodes[i]["allowed_pod_number"] = 110
+        nodes[i]["requested"][abi.GS_RES_CPU] = n.get("requested_cpu", 0)
     e.set_now(0)
     e.upsert_nodes(nodes)
     metrics = np.zeros(N, abi.METRIC_DTYPE)
@@ -35,7 +37,9 @@ def build(case, cls, device=0):
         tid = e.register_topology(numa.test_topology(*n["topology"])) if n["topology"] else None
         recs.append(numa.node_numa(tid, zones=[tuple(z) for z in n["zones"]], numa_policy=n["numa_policy"],
                                    node_cpu_bind=n.get("node_cpu_bind", ""),
-                                   numa_allocate_strategy=n.get("numa_allocate_strategy", "")))
+                                   numa_allocate_strategy=n.get("numa_allocate_strategy", ""),
+                                   node_cpu_ratio=n.get("node_cpu_ratio", -1.0),
+                                   has_options=n.get("has_options", True)))
     e.upsert_numa(np.array(recs, abi.NODE_NUMA_DTYPE))
     if case["allocations"]:
         allocs = [numa.pod_allocation(x["uid"], x["cpus"], [tuple(z) for z in x["numa"]]) for x in case["allocations"]]
@@ -47,6 +51,9 @@ def build(case, cls, device=0):
         pod["requests"][abi.GS_RES_CPU] = p["cpu"]
         pod["nonzero_requests"][0] = p["cpu"]
         mask |= 1 << abi.GS_RES_CPU
+    if "batch_cpu" in p:
+        pod["requests"][abi.GS_RES_BATCH_CPU] = p["batch_cpu"]
+        mask |= 1 << abi.GS_RES_BATCH_CPU
     if "memory" in p:
         pod["requests"][abi.GS_RES_MEMORY] = p["memory"]
         pod["nonzero_requests"][1] = p["memory"]

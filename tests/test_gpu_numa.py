@@ -129,3 +129,56 @@ def test_numa_schedule_after_release():
     e.release_allocations(nodes, uids)
     o.release_allocations(nodes, uids)
     _check_schedule(e, o, c.__class__(**{**c.__dict__, "pods": c.pods[100:]}), [100])
+
+
+def test_numa_two_ranks_on_one_gpu_callback_transport():
+    """Node-sharded NodeNUMAResource path (2 ranks, host all-gather) on one GPU: every rank replays the same Reserve
+    (NUMA splits and device-chosen cpusets; a rank reuses the batch-start affinity only for its own shard) and both
+    match the oracle."""
+    import threading
+    c = synth.make_cluster(1201, 200, 17)
+    synth.make_numa(c, numa_policy_pct=50, cpuset_pod_pct=50, mixed=True)
+    cfg = config.make_config(c.num_nodes, enabled=abi.GS_ENABLE_ALL)
+    E = engine_cls()
+    engines = [E(cfg), E(cfg)]
+    for x in engines:
+        synth.load_into(x, c)
+        x.verify_cpusets(True)
+    barrier = threading.Barrier(2)
+    slots = [None, None]
+
+    def make_ag(r):
+        def ag(data):
+            slots[r] = data
+            barrier.wait()
+            out = list(slots)
+            barrier.wait()
+            return out
+        return ag
+
+    for r, x in enumerate(engines):
+        x.comm_init_callback(2, r, make_ag(r))
+    res = [None, None]
+
+    def run(r):
+        res[r] = engines[r].schedule(c.pods, np.arange(len(c.pods), dtype=np.uint64))
+
+    th = [threading.Thread(target=run, args=(r,)) for r in range(2)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=300)
+    o = orc.Oracle(cfg)
+    synth.load_into(o, c)
+    want = o.schedule(c.pods, np.arange(len(c.pods), dtype=np.uint64))
+    mask = abi.GS_PLACED_NUMA | abi.GS_PLACED_CPUSET | (0xF << abi.GS_PLACED_AFFINITY_SHIFT)
+    for r in range(2):
+        assert res[r] is not None, f"rank {r} did not finish"
+        for f in ("node", "score", "ties", "feasible"):
+            bad = np.nonzero(res[r][f] != want[f])[0]
+            assert not len(bad), f"rank {r}: {f} differs at pod {bad[0]}"
+        assert np.array_equal(res[r]["flags"] & mask, want["flags"] & mask), f"rank {r}: Reserve flags differ"
+        for j in np.nonzero(want["flags"] & abi.GS_PLACED_CPUSET)[0]:
+            node, uid = int(want["node"][j]), int(c.pods["uid"][j])
+            assert engines[r].allocation(node, uid).tobytes() == o.allocation(node, uid).tobytes(), (r, j)
+        assert engines[r].mirror_check() == 0
