@@ -737,6 +737,7 @@ int run_batch(gs_ctx* c, const gs_pod* pods, int b, int* committed_out) {
   a.ld = c->ld;
   a.own0 = c->n0;
   a.own1 = c->n1;
+  a.S = c->nranks == 1 ? c->d_S : nullptr;
   HIP_TRY(c, hipEventRecord(c->ev[3], c->st));
   HIP_TRY(c, launch_commit(a, c->st));
   HIP_TRY(c, hipEventRecord(c->ev[4], c->st));
@@ -751,7 +752,6 @@ int run_batch(gs_ctx* c, const gs_pod* pods, int b, int* committed_out) {
   int committed = *c->h_committed;
   if (committed == 0) {
     // exact full-row path for pod 0: (max, ties, feasible) of every shard's row, global selection
-    c->stats.slowpath_pods += 1;
     HIP_TRY(c, launch_row_stats(c->d_S, len, c->d_rowstat, c->st));
     std::vector<RowStat> rs(c->nranks);
     if (c->nranks > 1) {
@@ -816,7 +816,6 @@ int run_batch(gs_ctx* c, const gs_pod* pods, int b, int* committed_out) {
   if (committed < b) c->stats.cuts += 1;
   HIP_TRY(c, hipMemcpyAsync(c->h_out, c->d_out, sizeof(PlacementDev) * committed, hipMemcpyDeviceToHost, c->st));
   HIP_TRY(c, hipStreamSynchronize(c->st));
-  if (c->stats.slowpath_pods && committed >= 1 && a.forced_node >= 0) c->h_out[0].flags |= GS_PLACED_SLOWPATH;
   *committed_out = committed;
   (void)pods;
   return GS_OK;
@@ -1154,6 +1153,7 @@ int gs_schedule(gs_ctx* c, const gs_pod* pods, uint32_t npods, const uint64_t* s
       o.score = pd.node >= 0 ? pd.score : 0;
       o.ties = pd.node >= 0 ? pd.ties : 0;
       o.flags = pd.flags & ~PL_INTERNAL_FLAGS;
+      if (pd.flags & GS_PLACED_SLOWPATH) c->stats.slowpath_pods += 1;   // resolved from its whole score row
       if ((rc = numa_reserve(c, pods[i + j], c->h_pods[j], pd))) return rc;
       apply_placement(c, pods[i + j], pd.node, special_first);
     }

@@ -84,6 +84,7 @@ struct CommitArgs {
   const uint8_t* aff;        // [pod][ld] Filter-time affinity of NUMA-policy nodes of the own shard (eval_numa_kernel)
   uint32_t ld;
   uint32_t own0, own1;       // this rank's shard [own0, own1)
+  const int16_t* S;          // batch-start score rows (one shard only: in-kernel full-row resolution; else nullptr)
 };
 
 hipError_t set_kernel_attributes();

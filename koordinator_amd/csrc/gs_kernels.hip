@@ -590,7 +590,12 @@ __global__ void __launch_bounds__(256) commit_kernel(CommitArgs a) {
   __shared__ uint32_t win[WIN];
   __shared__ int32_t pre_old[WIN + 1];
   __shared__ Row orow;                                  // batch-start copy of a freshly dirtied row
-  __shared__ int s_action, s_slot, s_fresh, s_M, s_F;  // wave-0 decision for pod k (0 commit, 1 skip, 2 cut)
+  __shared__ int s_action, s_slot, s_fresh, s_M, s_F;  // wave-0 decision for pod k (0 commit, 1 skip, 2 cut,
+                                                       // 3 resolve from the full row)
+  // a pod resolved from its whole score row (host slow path for pod 0, or in-kernel on one shard): its selectHost
+  __shared__ int s_fk, s_fnode, s_fscore, s_ffeas, s_Md, s_Fd, s_ndc;
+  __shared__ int64_t s_fties;
+  __shared__ int s_red[8];
   __shared__ uint32_t s_winner;
   __shared__ int64_t s_T;
   __shared__ int s_cut;                                // the pod just committed needs host-side Reserve
@@ -599,7 +604,14 @@ __global__ void __launch_bounds__(256) commit_kernel(CommitArgs a) {
   __shared__ int s_aff;                                // known affinity of pod k on its winner row (-1: recompute)
   const bool numa_on = (a.pf.enabled & 0x30u) != 0;
 
-  if (tid == 0) s_topo_id = -1;
+  if (tid == 0) {
+    s_topo_id = -1;
+    s_fk = a.forced_node >= 0 ? 0 : -1;
+    s_fnode = a.forced_node;
+    s_fscore = a.forced_score;
+    s_ffeas = a.forced_feasible;
+    s_fties = a.forced_ties;
+  }
   const int my_col = lane < ROW_I64 ? kRowCol[lane] : 0;   // fresh-row fetch column of this lane (loop invariant)
   for (int i = tid; i < B; i += 256) pods(i) = a.pods[i];
   for (int i = tid; i < HASH; i += 256) { hkey[i] = -1; hval[i] = -1; }
@@ -637,6 +649,7 @@ __global__ void __launch_bounds__(256) commit_kernel(CommitArgs a) {
        if (k + e < B) hs_seq[e] = a.seq[k + e];
      __syncthreads();
    }
+   for (;;) {   // one pass; a second, forced one after an in-kernel full-row resolution
    if (wave == 0) do {   // ===================== wave 0: selectHost for pod k =====================
     const int kc = k % HCH;
     const int r_l = lane / MAXLEV, j_l = lane % MAXLEV;
@@ -648,7 +661,7 @@ __global__ void __launch_bounds__(256) commit_kernel(CommitArgs a) {
     if (lane < nhl) { sh_score[lane] = hs; sh_count[lane] = hc; sh_dec[lane] = 0; }
     WAVE_FENCE();
     STAMP(0);
-    const bool forced = (k == 0 && a.forced_node >= 0);
+    const bool forced = k == s_fk;
     // ---- dirty rows: batch-start / current scores of pod k, listed-level decrements
     int Md = -1, Fd = 0;
     for (int s = lane; s < nd; s += 64) {
@@ -669,10 +682,17 @@ __global__ void __launch_bounds__(256) commit_kernel(CommitArgs a) {
     int M = max(wave_max(clean > 0 ? hs : -1), Md);
     int F = Fd + wave_sum(lane < R ? feas_l : 0);
     if (forced) {
-      M = a.forced_score;
-      F = a.forced_feasible;
+      M = s_fscore;
+      F = s_ffeas;
     } else if (__ballot(lane < R && M <= next_l)) {
-      if (lane == 0) s_action = 2;   // a shard may hold unlisted nodes at M: cut, the host re-evaluates from k
+      // a shard may hold unlisted nodes at M: one shard resolves pod k from its whole row right here; with
+      // several shards the batch is cut and the host resolves it (row_stats / row_select / exchange)
+      if (lane == 0) {
+        s_action = (R == 1 && a.S) ? 3 : 2;
+        s_Md = Md;
+        s_Fd = Fd;
+        s_ndc = nd;   // the dirty-slot count lives in wave 0's registers only
+      }
       break;
     }
     if (M < 0) {       // FitError: no feasible node anywhere, nothing assumed
@@ -686,8 +706,9 @@ __global__ void __launch_bounds__(256) commit_kernel(CommitArgs a) {
     int64_t T = 0;
     STAMP(2);
     if (forced) {
-      winner = (uint32_t)a.forced_node;
-      T = a.forced_ties;
+      if (s_fnode < 0) { if (lane == 0) s_action = 2; break; }   // unreachable for a valid max: cut, host re-run
+      winner = (uint32_t)s_fnode;
+      T = s_fties;
     } else {
       // ---- tie set at M: clean listed nodes + dirty rows now at M ("dnew") - dirty rows listed at M ("old")
       const int cm_lane = (lvl && hs == M) ? clean : 0;
@@ -844,6 +865,61 @@ __global__ void __launch_bounds__(256) commit_kernel(CommitArgs a) {
     STAMP(6);
    } while (0);
     __syncthreads();
+    if (s_action != 3) break;
+    // ---- exact full-row resolution of pod k on the single shard: batch-start scores S[k][*] for clean nodes,
+    // current scores for dirty rows; max, ties and feasible count, then the j*-th tie in node order
+    {
+      const int16_t* row = a.S + (size_t)k * a.ld;
+      const uint32_t len = a.own1 - a.own0, chunk = (len + 255) / 256;
+      const uint32_t i0 = min(len, (uint32_t)tid * chunk), i1 = min(len, i0 + chunk);
+      int lmax = -1, lfeas = 0;
+      for (uint32_t i = i0; i < i1; ++i) {
+        const int x = row[i];
+        lfeas += x >= 0 ? 1 : 0;
+        if (x > lmax && hash_find(hkey, hval, a.own0 + i) < 0) lmax = x;
+      }
+      lmax = wave_max(lmax);
+      lfeas = wave_sum(lfeas);
+      if (lane == 0) { s_red[wave] = lmax; s_red[4 + wave] = lfeas; }
+      __syncthreads();
+      const int M = max(max(max(s_red[0], s_red[1]), max(s_red[2], s_red[3])), s_Md);
+      const int F = s_red[4] + s_red[5] + s_red[6] + s_red[7] + s_Fd;
+      __syncthreads();
+      int cnt = 0;
+      if (M >= 0) {
+        for (uint32_t i = i0; i < i1; ++i)
+          if (row[i] == M && hash_find(hkey, hval, a.own0 + i) < 0) ++cnt;
+        for (int s = 0; s < s_ndc; ++s) {
+          const uint32_t n = drows[s].node;
+          if (n >= a.own0 + i0 && n < a.own0 + i1 && dsc[k * B + s] == M) ++cnt;
+        }
+      }
+      int incl = cnt;
+      for (int off = 1; off < 64; off <<= 1) {
+        const int v = __shfl_up(incl, off);
+        if (lane >= off) incl += v;
+      }
+      if (lane == 63) s_red[wave] = incl;
+      __syncthreads();
+      int base = 0;
+      for (int w = 0; w < wave; ++w) base += s_red[w];
+      const int64_t T = (int64_t)s_red[0] + s_red[1] + s_red[2] + s_red[3];
+      const int64_t jp = T > 0 ? tiebreak_position(a.seed, hs_seq[k % HCH], T) : 0;
+      const int64_t excl = base + incl - cnt;
+      if (tid == 0) s_fnode = -1;
+      __syncthreads();
+      if (T > 0 && jp > excl && jp <= excl + cnt) {   // this thread's chunk holds the jp-th tie
+        int64_t need = jp - excl;
+        for (uint32_t i = i0; i < i1; ++i) {
+          const int sl = hash_find(hkey, hval, a.own0 + i);
+          const bool tie = sl >= 0 ? dsc[k * B + sl] == M : row[i] == M;
+          if (tie && --need == 0) { s_fnode = (int)(a.own0 + i); break; }
+        }
+      }
+      if (tid == 0) { s_fk = k; s_fscore = M; s_fties = T; s_ffeas = F; }
+      __syncthreads();
+    }
+   }
     // ===================== all waves: assume + Reserve, re-score later pods =====================
     const int action = s_action;
     if (action == 2) { committed = k; break; }
@@ -867,7 +943,7 @@ __global__ void __launch_bounds__(256) commit_kernel(CommitArgs a) {
     if (tid == 0) {
       if (fresh) d = orow;
       const PodVec& pk = pods(k);
-      const bool forced = (k == 0 && a.forced_node >= 0);
+      const bool forced = k == s_fk;
       PlacementDev pl{(int32_t)s_winner, (uint32_t)s_F, (int64_t)s_M, (uint32_t)s_T, forced ? 1u : 0u, 0, 0,
                       {0, 0, 0, 0}, {0, 0, 0, 0}};
       s_cut = 0;

@@ -3,7 +3,7 @@
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-ok() { local rc=$1; [ "$rc" -eq 0 ] || [ "$rc" -eq 1 ]; }
+ok() { [ "$1" -eq 0 ]; }
 if [ "${SKIP_TESTS:-0}" != 1 ]; then
   timeout -k 10 600 python -u -m pytest tests -m gpu -v --timeout 120 --timeout-method thread \
       > gpurun_out/pytest_gpu.log 2>&1

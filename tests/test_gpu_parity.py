@@ -98,9 +98,8 @@ def test_schedule_in_chunks_and_custom_seq():
         _check_schedule(e, o, c.pods[lo:lo + 150], seq[lo:lo + 150])
 
 
-def test_homogeneous_cluster_massive_ties():
-    """Identical empty nodes: every node ties, candidate lists overflow -> exact full-row path."""
-    c = synth.make_cluster(3000, 200, 3)
+def homogeneous_cluster(nodes, pods, seed):
+    c = synth.make_cluster(nodes, pods, seed)
     c.nodes["requested"] = 0
     c.nodes["nonzero_requested"] = 0
     c.nodes["allocatable"][:, 0] = 64000
@@ -113,10 +112,31 @@ def test_homogeneous_cluster_massive_ties():
     c.assigned_ts = c.assigned_ts[:0]
     c.pod_metrics = c.pod_metrics[:0]
     c.pm_offsets[:] = 0
+    return c
+
+
+def test_homogeneous_cluster_massive_ties():
+    """Identical empty nodes: every node ties, candidate lists overflow -> exact full-row path (in the commit
+    kernel on a single shard)."""
+    c = homogeneous_cluster(3000, 200, 3)
     e, o = pair(c)
     got = _check_schedule(e, o, c.pods)
     assert got["ties"].max() > 1000
     assert e.stats()["slowpath_pods"] > 0
+
+
+def test_homogeneous_cluster_two_ranks_host_slow_path():
+    """The same on 2 shards: the batch is cut and the host resolves the pod (row_stats / row_select / exchange)."""
+    c = homogeneous_cluster(6001, 120, 4)   # 3000 nodes per shard: a top level beyond the list capacity (2048)
+    cfg = config.make_config(c.num_nodes)
+    res, engines = run_two_ranks(c, cfg)
+    o = orc.Oracle(cfg)
+    synth.load_into(o, c)
+    want = o.schedule(c.pods)
+    for r in range(2):
+        for f in ("node", "score", "ties", "feasible"):
+            assert np.array_equal(res[r][f], want[f]), (r, f)
+        assert engines[r].stats()["slowpath_pods"] > 0
 
 
 def test_unschedulable_and_special_pods():
@@ -161,10 +181,7 @@ def test_metric_and_node_updates_between_batches():
     _check_schedule(e, o, c.pods[200:])
 
 
-def test_two_ranks_on_one_gpu_callback_transport():
-    """The sharded path (2 ranks, host all-gather) on one GPU: same placements as one rank / the oracle."""
-    c = synth.make_cluster(3001, 500, 13)
-    cfg = config.make_config(c.num_nodes)
+def run_two_ranks(c, cfg):
     E = engine_cls()
     engines = [E(cfg), E(cfg)]
     for x in engines:
@@ -193,11 +210,19 @@ def test_two_ranks_on_one_gpu_callback_transport():
         t.start()
     for t in th:
         t.join(timeout=300)
+    assert res[0] is not None and res[1] is not None
+    return res, engines
+
+
+def test_two_ranks_on_one_gpu_callback_transport():
+    """The sharded path (2 ranks, host all-gather) on one GPU: same placements as one rank / the oracle."""
+    c = synth.make_cluster(3001, 500, 13)
+    cfg = config.make_config(c.num_nodes)
+    res, engines = run_two_ranks(c, cfg)
     o = orc.Oracle(cfg)
     synth.load_into(o, c)
     want = o.schedule(c.pods)
     for r in range(2):
-        assert res[r] is not None
         for f in ("node", "score", "ties", "feasible"):
             assert np.array_equal(res[r][f], want[f]), (r, f)
     assert engines[0].stats()["shard_end"] == engines[1].stats()["shard_begin"]
