@@ -16,6 +16,7 @@
 // int64 with an exact reciprocal-estimate-plus-correction division (quotients lie in [0,100]).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "gs_cpuset_dev.h"
 #include "gs_kernels.h"
@@ -253,22 +254,26 @@ __global__ void __launch_bounds__(256) eval_kernel(MirrorView m, const PodVec* _
 }
 
 // The NUMA-topology-policy nodes of the shard (host-maintained ascending index list): hints over zone subsets,
-// the topology-manager merge, Allocate by hint. Same (node x 16 pods) tiling as eval_kernel over the list.
+// the topology-manager merge, Allocate by hint. A thread keeps one node row in registers and evaluates PPT
+// consecutive pods of the batch: the row (gathered through the index list, ~30% of the shard's lines) is read
+// once per PPT pods instead of once per pair, while a full batch still puts ~nidx*B/PPT threads in flight.
+template <int PPT>
 __global__ void __launch_bounds__(256) eval_numa_kernel(MirrorView m, const PodVec* __restrict__ pods, int npods,
                                                         Profile pf, const uint32_t* __restrict__ idx, uint32_t nidx,
                                                         uint32_t n0, int16_t* __restrict__ S, uint32_t ld,
                                                         int prod_cols, uint8_t* __restrict__ aff) {
-  // one (node, pod) pair per thread: the per-pair work is long and batches ending at cpuset pods are short,
-  // so parallelism over pods matters more than row reuse (rows are L2/MALL resident)
   const uint32_t t = blockIdx.x * 256 + threadIdx.x;
-  const int k = blockIdx.y;
-  if (t >= nidx || k >= npods) return;
+  const int k0 = blockIdx.y * PPT;
+  if (t >= nidx || k0 >= npods) return;
+  const int k1 = min(npods, k0 + PPT);
   const uint32_t node = idx[t];
   Row row;
   load_row(m, node, prod_cols, true, row);
-  PairOut o = eval_pair<false, false, true>(row, pods[k], pf, m);
-  S[(size_t)k * ld + (node - n0)] = (int16_t)total_score(o, pf);
-  aff[(size_t)k * ld + (node - n0)] = (uint8_t)(o.code ? 0u : o.aff);   // read by the commit's Reserve
+  for (int k = k0; k < k1; ++k) {
+    PairOut o = eval_pair<false, false, true>(row, pods[k], pf, m);
+    S[(size_t)k * ld + (node - n0)] = (int16_t)total_score(o, pf);
+    aff[(size_t)k * ld + (node - n0)] = (uint8_t)(o.code ? 0u : o.aff);   // read by the commit's Reserve
+  }
 }
 
 // Diagnostic variant (gs_evaluate): every plugin's verdict and score for every pair.
@@ -466,6 +471,7 @@ int64_t host_tiebreak_position(uint64_t seed, uint64_t seq, int64_t T) { return 
 // scores for every later pod are re-evaluated exactly (dso = batch-start score, dsc = current score).
 // The max M is valid when it exceeds every shard's highest unlisted score (`next`); otherwise the batch
 // is cut at k. Ties at M are ordered by node index across shards (shards are contiguous ranges).
+constexpr int NUMA_PPT = 2;   // pods per thread in eval_numa_kernel (full batches)
 constexpr int HASH = 1024;
 constexpr int POD_STRIDE = 136;   // LDS bytes per pod vector in the commit kernel (sizeof(PodVec) + 8)
 static_assert(POD_STRIDE >= (int)sizeof(PodVec) && POD_STRIDE % 8 == 0, "pod stride");
@@ -520,8 +526,12 @@ __device__ __forceinline__ void wave_rank_sort(uint32_t* v, int n, uint32_t* tmp
 // Allocate (resource_manager.go:273-360, gs_cpuset_dev.h), then NodeAllocation.addPodAllocation
 // (node_allocation.go:82-110) on the CPU state and the row's available-CPU summaries, as numa_derive
 // (gs_numa_host.cpp) would recompute them. false: allocateCPUSet errors (the host fails loudly).
+// Arguments live in LDS or registers (zone split by value, cpuset into an LDS array): nothing of the caller's
+// frame has its address taken, so the commit kernel keeps its Reserve state out of scratch.
 __device__ __noinline__ bool cpuset_reserve(const TopoDev& t, CpuStateDev& cs, const PodVec& p, uint32_t nf,
-                                            const NumaOut& no, NumaRow& nr, uint64_t* cpuset) {
+                                            uint32_t zkeys, int64_t zc0, int64_t zc1, int64_t zc2, int64_t zc3,
+                                            NumaRow& nr, uint64_t* cpuset) {
+  const int64_t zcpu[4] = {zc0, zc1, zc2, zc3};
   // getCPUBindPolicy (util.go:85-103)
   const uint32_t pn = p.numa;
   const int st_req = (pn >> PN_REQ_SHIFT) & 7, nb = (nf >> NF_BIND_SHIFT) & 3;
@@ -532,7 +542,7 @@ __device__ __noinline__ bool cpuset_reserve(const TopoDev& t, CpuStateDev& cs, c
   else if (nb == GS_NODE_CPU_BIND_FULL_PCPUS_ONLY) { bind = BIND_FULL; required = true; }
   const int ep = (pn & PN_BIND) ? (int)((pn >> PN_EXCL_SHIFT) & 3u) : GS_CPU_EXCLUSIVE_NONE;
   uint64_t R[TD_POS];
-  if (!td_allocate_cpuset(t, cs, p.num_cpus, bind, required, ep, no.zkeys, no.zcpu, R)) return false;
+  if (!td_allocate_cpuset(t, cs, p.num_cpus, bind, required, ep, zkeys, zcpu, R)) return false;
   const uint64_t cores = td_any(R);
   for (int j = 0; j < TD_POS; ++j) cs.un[j] |= R[j];
   if (ep == GS_CPU_EXCLUSIVE_PCPU_LEVEL) cs.xc |= cores;
@@ -602,6 +612,7 @@ __global__ void __launch_bounds__(256) commit_kernel(CommitArgs a) {
   __shared__ TopoDev s_topo;                           // topology of the last cpuset Reserve (bit-plane form)
   __shared__ int s_topo_id;
   __shared__ int s_aff;                                // known affinity of pod k on its winner row (-1: recompute)
+  __shared__ uint64_t s_cpuset[4];                     // CPUs of a device-side cpuset Reserve
   const bool numa_on = (a.pf.enabled & 0x30u) != 0;
 
   if (tid == 0) {
@@ -612,7 +623,25 @@ __global__ void __launch_bounds__(256) commit_kernel(CommitArgs a) {
     s_ffeas = a.forced_feasible;
     s_fties = a.forced_ties;
   }
-  const int my_col = lane < ROW_I64 ? kRowCol[lane] : 0;   // fresh-row fetch column of this lane (loop invariant)
+  // fresh-row fetch map of this wave-0 lane (loop invariant): kind 0 none, 1 i64 column, 2 i32 column, 3 the
+  // Filter-time affinity byte, 4 the node index; destination region 0 orow, 1 the slot's CPU state, 2 s_aff
+  int f_kind = 0, f_region = 0, f_off = 0, f_size = 8;
+  const void* f_src = nullptr;
+  if (lane < ROW_I64) { f_kind = 1; f_src = a.m.c64(kRowCol[lane]); f_off = lane * 8; }
+  else if (lane == ROW_I64) { f_kind = 2; f_src = a.m.c32(C_FREE_PODS); f_off = offsetof(Row, free_pods); f_size = 4; }
+  else if (lane == ROW_I64 + 1) { f_kind = 2; f_src = a.m.c32(C_DFLAGS); f_off = offsetof(Row, dflags); f_size = 4; }
+  else if (lane == ROW_I64 + 2) { f_kind = 4; f_off = offsetof(Row, node); }
+  else if (numa_on) {
+    if (lane >= 20 && lane < 26) { f_kind = 1; f_src = a.m.c64(C_CPU_UN0 + (lane - 20)); f_region = 1; f_off = (lane - 20) * 8; }
+    else if (lane == 26) { f_kind = 2; f_src = a.m.c32(C_CPU_META); f_region = 1; f_off = offsetof(CpuStateDev, meta); f_size = 4; }
+    else if (lane == 27) { f_kind = 2; f_src = a.m.c32(C_TOPO_DEV); f_region = 1; f_off = offsetof(CpuStateDev, topo); f_size = 4; }
+    else if (lane == 28) { f_kind = 3; f_src = a.aff; f_region = 2; f_size = 4; }
+    else if (lane >= 32 && lane < 32 + NUMA_I64) {
+      f_kind = 1; f_src = a.m.c64(C_ZCAP_CPU0 + (lane - 32)); f_off = offsetof(Row, nr) + (lane - 32) * 8;
+    } else if (lane >= 50 && lane < 50 + NUMA_I32) {
+      f_kind = 2; f_src = a.m.c32(C_NFLAGS + (lane - 50)); f_off = offsetof(Row, nr.nflags) + (lane - 50) * 4; f_size = 4;
+    }
+  }
   for (int i = tid; i < B; i += 256) pods(i) = a.pods[i];
   for (int i = tid; i < HASH; i += 256) { hkey[i] = -1; hval[i] = -1; }
   const MirrorView& m = a.m;
@@ -837,25 +866,20 @@ __global__ void __launch_bounds__(256) commit_kernel(CommitArgs a) {
         hval[h] = slot;
       }
       ++nd;
-      int64_t* dw = reinterpret_cast<int64_t*>(&orow);
-      if (lane < ROW_I64) dw[lane] = m.c64(my_col)[winner];
-      if (lane == ROW_I64) orow.free_pods = m.c32(C_FREE_PODS)[winner];
-      if (lane == ROW_I64 + 1) orow.dflags = (uint32_t)m.c32(C_DFLAGS)[winner];
-      if (lane == ROW_I64 + 2) { orow.node = winner; orow.pad = 0; }
-      if (numa_on) {
-        int64_t* nw = reinterpret_cast<int64_t*>(&orow.nr);
-        if (lane >= 32 && lane < 32 + NUMA_I64) nw[lane - 32] = m.c64(C_ZCAP_CPU0 + (lane - 32))[winner];
-        int32_t* iw = reinterpret_cast<int32_t*>(&orow.nr.nflags);
-        if (lane >= 50 && lane < 50 + NUMA_I32) iw[lane - 50] = m.c32(C_NFLAGS + (lane - 50))[winner];
-        // CPU state for a device-side cpuset Reserve (lives in its slot directly)
-        uint64_t* cw = reinterpret_cast<uint64_t*>(&cst[slot]);
-        if (lane >= 20 && lane < 26) cw[lane - 20] = (uint64_t)m.c64(C_CPU_UN0 + (lane - 20))[winner];
-        if (lane == 26) cst[slot].meta = (uint32_t)m.c32(C_CPU_META)[winner];
-        if (lane == 27) cst[slot].topo = m.c32(C_TOPO_DEV)[winner];
-        if (lane == 28) {   // the batch-start Filter's affinity for this pair (own shard, NUMA-policy nodes)
-          const bool own = a.aff && winner >= a.own0 && winner < a.own1;
-          s_aff = own ? (int)a.aff[(size_t)k * a.ld + (winner - a.own0)] : -1;
-        }
+      // one load per lane, all issued before a single wait (the per-lane source/destination map is built once)
+      int64_t v = 0;
+      if (f_kind == 1) v = reinterpret_cast<const int64_t*>(f_src)[winner];
+      else if (f_kind == 2) v = reinterpret_cast<const int32_t*>(f_src)[winner];
+      else if (f_kind == 3) {   // the batch-start Filter's affinity for this pair (own shard, NUMA-policy nodes)
+        const bool own = f_src && winner >= a.own0 && winner < a.own1;
+        v = own ? (int64_t)reinterpret_cast<const uint8_t*>(f_src)[(size_t)k * a.ld + (winner - a.own0)] : -1;
+      } else if (f_kind == 4) v = (int64_t)winner;   // Row.node, Row.pad = 0
+      if (f_kind) {
+        unsigned char* dst = f_region == 0 ? reinterpret_cast<unsigned char*>(&orow)
+                           : f_region == 1 ? reinterpret_cast<unsigned char*>(&cst[slot])
+                                           : reinterpret_cast<unsigned char*>(&s_aff);
+        if (f_size == 8) *reinterpret_cast<int64_t*>(dst + f_off) = v;
+        else *reinterpret_cast<int32_t*>(dst + f_off) = (int32_t)v;
       }
     }
     if (lane == 0) {
@@ -977,8 +1001,14 @@ __global__ void __launch_bounds__(256) commit_kernel(CommitArgs a) {
           if (rb) {
             CpuStateDev& cs = cst[slot];
             if (cs.topo >= 0 && cs.topo == s_topo_id) {
-              if (cpuset_reserve(s_topo, cs, pk, nf, no, d.nr, pl.cpuset)) pl.flags |= PL_DEVICE_CPUSET;
-              else pl.flags |= PL_RESERVE_FAILED;
+              if (cpuset_reserve(s_topo, cs, pk, nf, no.zkeys, no.zcpu[0], no.zcpu[1], no.zcpu[2], no.zcpu[3],
+                                 d.nr, s_cpuset)) {
+                pl.flags |= PL_DEVICE_CPUSET;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) pl.cpuset[j] = s_cpuset[j];
+              } else {
+                pl.flags |= PL_RESERVE_FAILED;
+              }
               STAMP(11);
             } else {
               s_cut = 1;
@@ -1147,9 +1177,24 @@ hipError_t launch_eval(const MirrorView& m, const PodVec* pods, int npods, const
   if (gx == 0 || gy == 0) return hipSuccess;
   if (pf.enabled & 0x30u) {
     hipLaunchKernelGGL(eval_kernel<true>, dim3(gx, gy), dim3(256), 0, st, m, pods, npods, pf, n0, n1, S, ld, prod_cols);
-    if (numa_n)
-      hipLaunchKernelGGL(eval_numa_kernel, dim3((numa_n + 255) / 256, npods), dim3(256), 0, st, m, pods, npods, pf,
-                         numa_idx, numa_n, n0, S, ld, prod_cols, aff);
+    // short batches: one pair per thread keeps the grid wide
+    static const int ppt_env = getenv("GS_NUMA_PPT") ? atoi(getenv("GS_NUMA_PPT")) : NUMA_PPT;
+    const int ppt = npods >= 32 ? ppt_env : 1;
+    const dim3 g((numa_n + 255) / 256, (npods + ppt - 1) / ppt);
+    if (numa_n == 0) {
+    } else if (ppt == 2) {
+      hipLaunchKernelGGL(eval_numa_kernel<2>, g, dim3(256), 0, st, m, pods, npods, pf, numa_idx, numa_n, n0, S, ld,
+                         prod_cols, aff);
+    } else if (ppt == 4) {
+      hipLaunchKernelGGL(eval_numa_kernel<4>, g, dim3(256), 0, st, m, pods, npods, pf, numa_idx, numa_n, n0, S, ld,
+                         prod_cols, aff);
+    } else if (ppt == 8) {
+      hipLaunchKernelGGL(eval_numa_kernel<8>, g, dim3(256), 0, st, m, pods, npods, pf, numa_idx, numa_n, n0, S, ld,
+                         prod_cols, aff);
+    } else {
+      hipLaunchKernelGGL(eval_numa_kernel<1>, dim3((numa_n + 255) / 256, npods), dim3(256), 0, st, m, pods, npods,
+                         pf, numa_idx, numa_n, n0, S, ld, prod_cols, aff);
+    }
   } else {
     hipLaunchKernelGGL(eval_kernel<false>, dim3(gx, gy), dim3(256), 0, st, m, pods, npods, pf, n0, n1, S, ld, prod_cols);
   }

@@ -855,8 +855,21 @@ int32_t or_tiebreak_intn(uint64_t seed, uint64_t seq, int64_t cnt) {
 }
 
 // [upstream] scheduleOne for each pod: findNodesThatFitPod -> prioritizeNodes -> selectHost -> assume + Reserve.
+int or_schedule_replay(or_cluster* c, const gs_pod* pods, uint32_t npods, const uint64_t* seq,
+                       const int32_t* given, gs_placement* out, int nthreads);
+
 int or_schedule(or_cluster* c, const gs_pod* pods, uint32_t npods, const uint64_t* seq, gs_placement* out,
                 int nthreads) {
+  return or_schedule_replay(c, pods, npods, seq, nullptr, out, nthreads);
+}
+
+// Replay (test infrastructure for full-size parity): a pod with given[p] >= 0 is not scheduled but placed on
+// that node — its Filter runs on that node alone (the topologymanager affinity Reserve consumes; a node that
+// fails Filter is an error), then Reserve + assume exactly as for a scheduled pod; only node and flags are
+// reported for it. given[p] == -2 replays a FitError (nothing assumed); pods with given[p] == -1 run the full
+// scheduleOne below on the replayed state.
+int or_schedule_replay(or_cluster* c, const gs_pod* pods, uint32_t npods, const uint64_t* seq,
+                       const int32_t* given, gs_placement* out, int nthreads) {
   if (!c || !out) return GS_EINVAL;
   int N = (int)c->nodes.size();
   for (int n = 0; n < N; ++n)
@@ -871,6 +884,25 @@ int or_schedule(or_cluster* c, const gs_pod* pods, uint32_t npods, const uint64_
   for (uint32_t p = 0; p < npods; ++p) {
     const gs_pod& pod = pods[p];
     const orn::PreState st = orn::prefilter(c->numa_args, pod);
+    gs_placement& o = out[p];
+    int selected = -1;
+    if (given && given[p] == -2) {   // replayed FitError: nothing assumed
+      o.feasible = 0; o.flags = 0; o.node = -1; o.score = 0; o.ties = 0;
+      continue;
+    }
+    if (given && given[p] >= 0) {
+      if (given[p] >= N) return GS_EINVAL;
+      selected = given[p];
+      const NodeState& s = c->nodes[selected];
+      uint16_t code = 0;
+      if (c->cfg.enabled & GS_ENABLE_FIT_FILTER) code |= (uint16_t)fit_filter(pod, s.node);
+      if ((c->cfg.enabled & GS_ENABLE_LA_FILTER) && loadaware_filter(*c, pod, s)) code |= GS_FAIL_LOADAWARE;
+      affinity[selected] = orn::Hint{};
+      if (!code && (c->cfg.enabled & GS_ENABLE_NUMA_FILTER))
+        code |= numa_filter(*c, st, (uint32_t)selected, &affinity[selected]);
+      if (code) return GS_ESTATE;
+      o.feasible = 0; o.flags = 0; o.node = selected; o.score = 0; o.ties = 0;
+    } else {
     // findNodesThatPassFilters: percentageOfNodesToScore = 100, so every node is checked and
     // nextStartNodeIndex = (start + N) % N stays put: feasible order = node index order.
     auto check = [&](int n) {
@@ -887,7 +919,6 @@ int or_schedule(or_cluster* c, const gs_pod* pods, uint32_t npods, const uint64_
     feasible_list.clear();
     for (int n = 0; n < N; ++n)
       if (feasible[n]) feasible_list.push_back(n);
-    gs_placement& o = out[p];
     o.feasible = (uint32_t)feasible_list.size();
     o.flags = 0;
     if (feasible_list.empty()) {   // FitError: nothing is assumed
@@ -909,7 +940,7 @@ int or_schedule(or_cluster* c, const gs_pod* pods, uint32_t npods, const uint64_
     else for (int i = 0; i < F; ++i) score_one(i);
     // selectHost ([upstream] schedule_one.go)
     TieBreakRand rnd(c->cfg.seed, seq ? seq[p] : p);
-    int selected = feasible_list[0];
+    selected = feasible_list[0];
     int64_t max_score = score[selected];
     int64_t cnt = 1;
     for (int i = 1; i < F; ++i) {
@@ -922,6 +953,7 @@ int or_schedule(or_cluster* c, const gs_pod* pods, uint32_t npods, const uint64_
       }
     }
     o.node = selected; o.score = max_score; o.ties = (uint32_t)cnt;
+    }
     // Reserve: NodeNUMAResource (plugin.go:375-422) on the pre-assume NodeInfo
     if (c->cfg.enabled & (GS_ENABLE_NUMA_FILTER | GS_ENABLE_NUMA_SCORE)) {
       orn::PodAllocation pa;

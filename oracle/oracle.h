@@ -45,6 +45,10 @@ int or_evaluate(or_cluster* c, const gs_pod* pods, uint32_t npods, int16_t* scor
 /* nthreads <= 1: serial; otherwise a worker pool emulating parallelize.Until (pkg/util/parallelize/parallelism.go:29-49) */
 int or_schedule(or_cluster* c, const gs_pod* pods, uint32_t npods, const uint64_t* seq, gs_placement* out,
                 int nthreads);
+/* replay: pods with given[p] >= 0 are placed on that node (Filter on it alone for the affinity, Reserve,
+   assume); the others run scheduleOne on the replayed state */
+int or_schedule_replay(or_cluster* c, const gs_pod* pods, uint32_t npods, const uint64_t* seq,
+                       const int32_t* given, gs_placement* out, int nthreads);
 /* NodeNUMAResource state (mirrors gs_topology_register / gs_nodes_numa_upsert / gs_numa_allocations_*) */
 int or_topology_register(or_cluster* c, const gs_cpu_topology* t, int32_t* id);
 int or_nodes_numa_upsert(or_cluster* c, const uint32_t* idx, const gs_node_numa* nn, uint32_t n);

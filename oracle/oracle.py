@@ -42,6 +42,7 @@ def _load() -> C.CDLL:
         "or_fit_score": (C.c_int, [P, P, C.c_uint32, P]),
         "or_evaluate": (C.c_int, [P, P, C.c_uint32, P, P, P]),
         "or_schedule": (C.c_int, [P, P, C.c_uint32, P, P, C.c_int]),
+        "or_schedule_replay": (C.c_int, [P, P, C.c_uint32, P, P, P, C.c_int]),
         "or_tiebreak_intn": (C.c_int32, [C.c_uint64, C.c_uint64, C.c_int64]),
         "or_topology_register": (C.c_int, [P, P, P]),
         "or_nodes_numa_upsert": (C.c_int, [P, P, P, C.c_uint32]),
@@ -197,6 +198,20 @@ class Oracle:
         out = np.zeros(len(pods), abi.PLACEMENT_DTYPE)
         _chk(lib().or_schedule(self._h, abi.ptr(pods), len(pods), abi.ptr(seq), abi.ptr(out), int(nthreads)),
              "schedule")
+        return out
+
+    def schedule_replay(self, pods, given, seq=None, nthreads: int = 1):
+        """Pods with given[i] >= 0 are placed on that node (Filter there for the affinity, Reserve, assume);
+        given[i] == -2 replays a FitError (nothing assumed); given[i] == -1 runs scheduleOne on the replayed state."""
+        pods = np.ascontiguousarray(pods, dtype=abi.POD_DTYPE)
+        if seq is None:
+            seq = np.arange(len(pods), dtype=np.uint64)
+        seq = np.ascontiguousarray(seq, dtype=np.uint64)
+        given = np.ascontiguousarray(given, dtype=np.int32)
+        assert len(given) == len(pods) and len(seq) == len(pods)
+        out = np.zeros(len(pods), abi.PLACEMENT_DTYPE)
+        _chk(lib().or_schedule_replay(self._h, abi.ptr(pods), len(pods), abi.ptr(seq), abi.ptr(given),
+                                      abi.ptr(out), int(nthreads)), "schedule_replay")
         return out
 
 
