@@ -41,6 +41,21 @@ def cpu_baseline(cluster, cfg, sample_pods: int, threads: int) -> dict:
     return {"evals_per_s": sample_pods * cluster.num_nodes / dt, "pods_per_s": sample_pods / dt, "seconds": dt}
 
 
+PMC_FILE = os.path.join(ROOT, "profiles", "pmc_latest.json")
+
+
+def pmc_traffic() -> tuple[float | None, str | None]:
+    """HBM bytes per eval pass from the committed rocprofv3 PMC summary (scripts/gpu_profile.sh ->
+    scripts/pmc_summary.py): counters cannot be read from inside this process, so the figure is the one measured
+    by the separate --pmc passes over this same bench command."""
+    try:
+        with open(PMC_FILE) as f:
+            d = json.load(f)
+        return float(d["eval_pass"]["hbm_bytes_per_launch"]), os.path.relpath(PMC_FILE, ROOT)
+    except (OSError, KeyError, ValueError):
+        return None, None
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -140,6 +155,7 @@ def main() -> None:
     pairs_per_launch = st["eval_pairs"] / launches
     bytes_per_launch = pairs_per_launch * st["node_row_bytes"]
     achieved = bytes_per_launch / (avg_launch_ms * 1e-3) / 1e9 if avg_launch_ms > 0 else 0.0
+    traffic, traffic_src = pmc_traffic() if numa else (None, None)
 
     if rank == 0:
         line = {
@@ -173,13 +189,17 @@ def main() -> None:
                 "peak": HBM_PEAK_GBPS,
                 "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBPS,
-                "traffic": None,
-                "kernel": "eval_kernel",
+                "traffic": traffic,
+                "traffic_unit": "bytes per eval pass (2 x FETCH_SIZE + WRITE_SIZE, gfx950 correction)",
+                "traffic_source": traffic_src,
+                "kernel": "eval pass = eval_kernel + eval_numa_kernel (one launch each per batch)",
                 "bytes_per_eval": st["node_row_bytes"],
                 "avg_launch_us": avg_launch_ms * 1e3,
                 "pairs_per_launch": pairs_per_launch,
                 "note": f"algorithmic bytes = {st['node_row_bytes']} B node row per pod x node eval (un-batched "
-                        "convention); the kernel reads each row once per group of 16 pods, so frac > 1 means reuse",
+                        "convention); eval_kernel reads each row once per group of 16 pods (eval_numa_kernel: "
+                        "once per 2 pods), so frac > 1 would mean reuse; avg_launch_us is the HIP-event time of the "
+                        "pass on the library stream",
             },
             "breakdown_ms": {"eval": st["eval_ms"], "cand": st["cand_ms"], "commit": st["commit_ms"],
                              "exchange": st["exchange_ms"], "batches": st["batches"], "cuts": st["cuts"],

@@ -21,3 +21,4 @@ for ctr in FETCH_SIZE WRITE_SIZE; do
   [ $rc -eq 0 ] || exit $rc
 done
 find gpurun_out/prof gpurun_out/pmc_* -name "*.csv" | head -20
+python scripts/pmc_summary.py gpurun_out/pmc_fetch gpurun_out/pmc_write gpurun_out/pmc_latest.json

@@ -45,3 +45,16 @@ def test_replay_rejects_infeasible_node():
     p["requests"][0, 0] = 10 ** 9          # cannot fit anywhere
     with pytest.raises(Exception):
         a.schedule_replay(p, np.array([0], np.int32))
+
+
+def test_hint_provider_order_sensitivity():
+    """policy.go:108 merges the providers' hints in Go map order; the restatement fixes (cpu, memory).
+    Reported, not asserted: how many decisions the reverse order changes on a NUMA-dense synthetic cluster."""
+    c = synth.make_cluster(400, 300, 23)
+    synth.make_numa(c, numa_policy_pct=90, cpuset_pod_pct=40)
+    a, b = _pair(c, True)
+    b.set_hint_order(True)
+    x, y = a.schedule(c.pods), b.schedule(c.pods)
+    diff = int((x["node"] != y["node"]).sum() + (x["score"] != y["score"]).sum())
+    print(f"hint-order sensitivity: {diff} of {len(c.pods)} decisions differ under the reverse provider order")
+    assert (x["node"] >= 0).sum() > 0
