@@ -17,6 +17,7 @@
 #include <cstring>
 #include <string>
 #include <unordered_map>
+#include <unordered_set>
 #include <vector>
 
 #include "../../include/gpuscore.h"
@@ -99,6 +100,20 @@ struct gs_ctx {
   uint8_t* h_xchg_send = nullptr;
   uint8_t* h_xchg_recv = nullptr;
   hipEvent_t ev[8] = {};
+  // double-buffered per-batch buffers (slot 0 = the fields above when bound): the next batch is enqueued
+  // speculatively before the current one is read back (gs_schedule)
+  struct Slot {
+    PodVec* d_pods = nullptr;
+    uint64_t* d_seq = nullptr;
+    PlacementDev* d_out = nullptr;
+    int32_t* d_committed = nullptr;
+    PodVec* h_pods = nullptr;
+    uint64_t* h_seq = nullptr;
+    PlacementDev* h_out = nullptr;
+    int32_t* h_committed = nullptr;
+    hipEvent_t ev[6] = {};
+  } slot[2];
+  int cur_slot = 0;
   // host mirror
   std::vector<HostNode> nodes;
   std::vector<uint8_t> row_dirty;
@@ -685,8 +700,46 @@ double ev_ms(hipEvent_t a, hipEvent_t b) {
   return ms;
 }
 
-// One device pass over pods [0, b) of the staged batch. Returns number of pods committed (>= 1).
-int run_batch(gs_ctx* c, const gs_pod* pods, int b, int* committed_out) {
+void bind_slot(gs_ctx* c, int s) {
+  const gs_ctx::Slot& x = c->slot[s];
+  c->d_pods = x.d_pods; c->d_seq = x.d_seq; c->d_out = x.d_out; c->d_committed = x.d_committed;
+  c->h_pods = x.h_pods; c->h_seq = x.h_seq; c->h_out = x.h_out; c->h_committed = x.h_committed;
+  for (int i = 0; i < 6; ++i) c->ev[i] = x.ev[i];
+  c->cur_slot = s;
+}
+
+constexpr int GS_REDO = 1;   // internal: re-run the batch (its score rows were overwritten by a speculative pass)
+
+CommitArgs commit_args(gs_ctx* c, int b) {
+  CommitArgs a{};
+  a.m = c->mv;
+  a.pods = c->d_pods;
+  a.seq = c->d_seq;
+  a.npods = b;
+  a.nranks = c->nranks;
+  a.shard_size = (c->N + c->nranks - 1) / c->nranks;
+  a.xbase = c->nranks > 1 ? c->d_xchg_recv : c->d_xchg_send;
+  a.xblock = c->xchg_bytes;
+  a.bmax = c->B;
+  a.pf = c->pf;
+  a.seed = c->cfg.seed;
+  a.forced_node = -1;
+  a.out = c->d_out;
+  a.committed = c->d_committed;
+  a.stamps = c->d_stamps;
+  a.topos = c->d_topos;
+  a.aff = c->d_aff;
+  a.ld = c->ld;
+  a.own0 = c->n0;
+  a.own1 = c->n1;
+  a.S = c->nranks == 1 ? c->d_S : nullptr;
+  return a;
+}
+
+// Enqueue one device pass over pods [0, b) of the bound slot's staged batch, and its read-back; no host wait.
+// prev != nullptr: a speculative pass behind the batch that wrote `prev` on the same stream — its commit kernel
+// does nothing unless that batch committed every pod and needs no host-side Reserve (prev[1] == 1).
+int launch_batch(gs_ctx* c, int b, const int32_t* prev) {
   uint32_t* d_lists = reinterpret_cast<uint32_t*>(c->d_xchg_send);
   LevelHdr* d_hdrs = reinterpret_cast<LevelHdr*>(c->d_xchg_send + lists_bytes(c->B));
   int prod_cols = 0;
@@ -710,47 +763,37 @@ int run_batch(gs_ctx* c, const gs_pod* pods, int b, int* committed_out) {
   HIP_TRY(c, hipEventRecord(c->ev[1], c->st));
   HIP_TRY(c, launch_cand(c->d_S, c->ld, len, c->n0, b, c->max_score, d_lists, d_hdrs, c->st));
   HIP_TRY(c, hipEventRecord(c->ev[2], c->st));
-  const uint8_t* xbase = c->d_xchg_send;
   if (c->nranks > 1) {
     int rc = exchange(c, c->d_xchg_send, c->d_xchg_recv, c->xchg_bytes);
     if (rc) return rc;
-    xbase = c->d_xchg_recv;
   }
-  CommitArgs a{};
-  a.m = c->mv;
-  a.pods = c->d_pods;
-  a.seq = c->d_seq;
-  a.npods = b;
-  a.nranks = c->nranks;
-  a.shard_size = (c->N + c->nranks - 1) / c->nranks;
-  a.xbase = xbase;
-  a.xblock = c->xchg_bytes;
-  a.bmax = c->B;
-  a.pf = c->pf;
-  a.seed = c->cfg.seed;
-  a.forced_node = -1;
-  a.out = c->d_out;
-  a.committed = c->d_committed;
-  a.stamps = c->d_stamps;
-  a.topos = c->d_topos;
-  a.aff = c->d_aff;
-  a.ld = c->ld;
-  a.own0 = c->n0;
-  a.own1 = c->n1;
-  a.S = c->nranks == 1 ? c->d_S : nullptr;
+  CommitArgs a = commit_args(c, b);
+  a.prev = prev;
   HIP_TRY(c, hipEventRecord(c->ev[3], c->st));
   HIP_TRY(c, launch_commit(a, c->st));
   HIP_TRY(c, hipEventRecord(c->ev[4], c->st));
-  HIP_TRY(c, hipMemcpyAsync(c->h_committed, c->d_committed, 4, hipMemcpyDeviceToHost, c->st));
-  HIP_TRY(c, hipStreamSynchronize(c->st));
+  HIP_TRY(c, hipMemcpyAsync(c->h_committed, c->d_committed, 8, hipMemcpyDeviceToHost, c->st));
+  HIP_TRY(c, hipMemcpyAsync(c->h_out, c->d_out, sizeof(PlacementDev) * b, hipMemcpyDeviceToHost, c->st));
+  HIP_TRY(c, hipEventRecord(c->ev[5], c->st));
+  return GS_OK;
+}
+
+// Wait for the bound slot's batch; when it committed nothing, resolve its pod 0 by the exact full-row path
+// (several shards). clobbered: a speculative pass has overwritten the score rows and lists since -> GS_REDO.
+int finish_batch(gs_ctx* c, int b, bool clobbered, int* committed_out) {
+  uint32_t len = c->n1 - c->n0;
+  HIP_TRY(c, hipEventSynchronize(c->ev[5]));
   c->stats.eval_ms += ev_ms(c->ev[0], c->ev[1]);
   c->stats.cand_ms += ev_ms(c->ev[1], c->ev[2]);
   c->stats.commit_ms += ev_ms(c->ev[3], c->ev[4]);
   c->stats.eval_launches += 1;
   c->stats.eval_pairs += (uint64_t)b * len;
   c->stats.batches += 1;
-  int committed = *c->h_committed;
+  int committed = c->h_committed[0];
+  if (committed < 0) return fail(c, GS_ESTATE, "commit pass of a batch was voided unexpectedly");
+  if (committed == 0 && clobbered) return GS_REDO;
   if (committed == 0) {
+    CommitArgs a = commit_args(c, b);
     // exact full-row path for pod 0: (max, ties, feasible) of every shard's row, global selection
     HIP_TRY(c, launch_row_stats(c->d_S, len, c->d_rowstat, c->st));
     std::vector<RowStat> rs(c->nranks);
@@ -807,17 +850,16 @@ int run_batch(gs_ctx* c, const gs_pod* pods, int b, int* committed_out) {
     HIP_TRY(c, hipEventRecord(c->ev[3], c->st));
     HIP_TRY(c, launch_commit(a, c->st));
     HIP_TRY(c, hipEventRecord(c->ev[4], c->st));
-    HIP_TRY(c, hipMemcpyAsync(c->h_committed, c->d_committed, 4, hipMemcpyDeviceToHost, c->st));
+    HIP_TRY(c, hipMemcpyAsync(c->h_committed, c->d_committed, 8, hipMemcpyDeviceToHost, c->st));
     HIP_TRY(c, hipStreamSynchronize(c->st));
     c->stats.commit_ms += ev_ms(c->ev[3], c->ev[4]);
-    committed = *c->h_committed;
+    committed = c->h_committed[0];
     if (committed < 1) return fail(c, GS_ESTATE, "forced commit made no progress");
+    HIP_TRY(c, hipMemcpyAsync(c->h_out, c->d_out, sizeof(PlacementDev) * committed, hipMemcpyDeviceToHost, c->st));
+    HIP_TRY(c, hipStreamSynchronize(c->st));
   }
   if (committed < b) c->stats.cuts += 1;
-  HIP_TRY(c, hipMemcpyAsync(c->h_out, c->d_out, sizeof(PlacementDev) * committed, hipMemcpyDeviceToHost, c->st));
-  HIP_TRY(c, hipStreamSynchronize(c->st));
   *committed_out = committed;
-  (void)pods;
   return GS_OK;
 }
 
@@ -949,7 +991,7 @@ int gs_create(const gs_config* cfg, gs_ctx** out) {
   if ((e = hipMalloc(&c->d_xchg_send, xb)) != hipSuccess) return bail("hipMalloc", e);
   c->xchg_bytes = xb;
   if ((e = hipMalloc(&c->d_out, sizeof(PlacementDev) * c->B)) != hipSuccess) return bail("hipMalloc", e);
-  if ((e = hipMalloc(&c->d_committed, 4)) != hipSuccess) return bail("hipMalloc", e);
+  if ((e = hipMalloc(&c->d_committed, 8)) != hipSuccess) return bail("hipMalloc", e);
   if ((e = hipMalloc(&c->d_rowstat, sizeof(RowStat) * (1 + MAX_RANKS))) != hipSuccess) return bail("hipMalloc", e);
   if ((e = hipMalloc(&c->d_sel, 4 * (1 + MAX_RANKS))) != hipSuccess) return bail("hipMalloc", e);
   c->stage_cap = std::min<uint32_t>(c->N, 65536);
@@ -961,9 +1003,26 @@ int gs_create(const gs_config* cfg, gs_ctx** out) {
   if ((e = hipHostMalloc(&c->h_pods, sizeof(PodVec) * c->B, hipHostMallocDefault)) != hipSuccess) return bail("hipHostMalloc", e);
   if ((e = hipHostMalloc(&c->h_seq, 8 * c->B, hipHostMallocDefault)) != hipSuccess) return bail("hipHostMalloc", e);
   if ((e = hipHostMalloc(&c->h_out, sizeof(PlacementDev) * c->B, hipHostMallocDefault)) != hipSuccess) return bail("hipHostMalloc", e);
-  if ((e = hipHostMalloc(&c->h_committed, 4, hipHostMallocDefault)) != hipSuccess) return bail("hipHostMalloc", e);
+  if ((e = hipHostMalloc(&c->h_committed, 8, hipHostMallocDefault)) != hipSuccess) return bail("hipHostMalloc", e);
   if ((e = hipHostMalloc(&c->h_xchg_send, xb, hipHostMallocDefault)) != hipSuccess) return bail("hipHostMalloc", e);
   (void)hipMemset(c->d_S, 0xff, (size_t)c->B * c->ld * 2);
+  {
+    gs_ctx::Slot& s0 = c->slot[0];
+    s0.d_pods = c->d_pods; s0.d_seq = c->d_seq; s0.d_out = c->d_out; s0.d_committed = c->d_committed;
+    s0.h_pods = c->h_pods; s0.h_seq = c->h_seq; s0.h_out = c->h_out; s0.h_committed = c->h_committed;
+    for (int i = 0; i < 6; ++i) s0.ev[i] = c->ev[i];
+    gs_ctx::Slot& s1 = c->slot[1];
+    if ((e = hipMalloc(&s1.d_pods, sizeof(PodVec) * c->B)) != hipSuccess) return bail("hipMalloc", e);
+    if ((e = hipMalloc(&s1.d_seq, 8 * c->B)) != hipSuccess) return bail("hipMalloc", e);
+    if ((e = hipMalloc(&s1.d_out, sizeof(PlacementDev) * c->B)) != hipSuccess) return bail("hipMalloc", e);
+    if ((e = hipMalloc(&s1.d_committed, 8)) != hipSuccess) return bail("hipMalloc", e);
+    if ((e = hipHostMalloc(&s1.h_pods, sizeof(PodVec) * c->B, hipHostMallocDefault)) != hipSuccess) return bail("hipHostMalloc", e);
+    if ((e = hipHostMalloc(&s1.h_seq, 8 * c->B, hipHostMallocDefault)) != hipSuccess) return bail("hipHostMalloc", e);
+    if ((e = hipHostMalloc(&s1.h_out, sizeof(PlacementDev) * c->B, hipHostMallocDefault)) != hipSuccess) return bail("hipHostMalloc", e);
+    if ((e = hipHostMalloc(&s1.h_committed, 8, hipHostMallocDefault)) != hipSuccess) return bail("hipHostMalloc", e);
+    for (auto& ev : s1.ev)
+      if ((e = hipEventCreate(&ev)) != hipSuccess) return bail("hipEventCreate", e);
+  }
   if (getenv("GS_COMMIT_STAMPS") && getenv("GS_COMMIT_STAMPS")[0] == '1') {
     if ((e = hipMalloc(&c->d_stamps, 8 * 20)) != hipSuccess) return bail("hipMalloc", e);
     (void)hipMemset(c->d_stamps, 0, 160);
@@ -995,6 +1054,18 @@ int gs_destroy(gs_ctx* c) {
   }
   if (c->comm) ncclCommDestroy(c->comm);
   if (c->st) (void)hipStreamSynchronize(c->st);
+  if (c->slot[0].d_pods) bind_slot(c, 0);
+  {
+    gs_ctx::Slot& s1 = c->slot[1];
+    void* d1[] = {s1.d_pods, s1.d_seq, s1.d_out, s1.d_committed};
+    for (void* p : d1)
+      if (p) (void)hipFree(p);
+    void* h1[] = {s1.h_pods, s1.h_seq, s1.h_out, s1.h_committed};
+    for (void* p : h1)
+      if (p) (void)hipHostFree(p);
+    for (auto& ev : s1.ev)
+      if (ev) (void)hipEventDestroy(ev);
+  }
   void* dev[] = {c->d_i64, c->d_i32, c->d_pods, c->d_seq, c->d_S, c->d_xchg_send, c->d_xchg_recv, c->d_out,
                  c->d_committed, c->d_rowstat, c->d_sel, c->d_stage_idx, c->d_stage_rows, c->d_numa_idx,
                  c->d_topos, c->d_aff};
@@ -1117,48 +1188,122 @@ int gs_evaluate(gs_ctx* c, const gs_pod* pods, uint32_t npods, int16_t* scores, 
   return rc;
 }
 
+namespace {
+// batch [i, i+b): a special pod always runs alone (its row is re-derived on the host afterwards)
+int batch_len(const gs_ctx* c, const gs_pod* pods, uint32_t i, uint32_t npods, bool* special_first) {
+  int b = (int)std::min<uint32_t>(c->B, npods - i);
+  *special_first = special_pod(c, pods[i]);
+  if (*special_first) return 1;
+  for (int j = 1; j < b; ++j)
+    if (special_pod(c, pods[i + j])) return j;
+  return b;
+}
+
+// PreFilter of pods [i, i+b) into the bound slot, and their upload
+int stage_batch(gs_ctx* c, const gs_pod* pods, const uint64_t* seq, uint32_t i, int b) {
+  for (int j = 0; j < b; ++j) {
+    c->h_pods[j] = prep_pod(c, pods[i + j]);
+    c->h_seq[j] = seq ? seq[i + j] : (uint64_t)(i + j);
+  }
+  HIP_TRY(c, hipMemcpyAsync(c->d_pods, c->h_pods, sizeof(PodVec) * b, hipMemcpyHostToDevice, c->st));
+  HIP_TRY(c, hipMemcpyAsync(c->d_seq, c->h_seq, 8 * b, hipMemcpyHostToDevice, c->st));
+  return GS_OK;
+}
+
+bool uid_overlap(const gs_pod* a, int na, const gs_pod* b, int nb) {
+  std::unordered_set<uint64_t> u;
+  u.reserve(2 * na);
+  for (int i = 0; i < na; ++i) u.insert(a[i].uid);
+  for (int i = 0; i < nb; ++i)
+    if (u.count(b[i].uid)) return true;
+  return false;
+}
+}  // namespace
+
 int gs_schedule(gs_ctx* c, const gs_pod* pods, uint32_t npods, const uint64_t* seq, gs_placement* out) {
   if (!c || (npods && (!pods || !out))) return GS_EINVAL;
   int rc = ready(c);
   if (rc) return rc;
   for (uint32_t i = 0; i < npods; ++i)
     if ((rc = validate_pod(c, pods[i]))) return rc;
+  // Pipelining: while batch [i, i+b) runs, the next batch is staged and enqueued behind it on the stream
+  // (other slot). Its commit kernel checks on the device that the batch before committed all its pods with no
+  // host-side Reserve pending, else it is a no-op; the host only keeps it when the same holds on its side.
+  // Every rank takes the same decisions (replicated host state), so speculative exchanges pair up; with the
+  // host-callback transport the speculative pass's exchange waits for the current batch (no overlap, same result).
+  static const bool no_spec = getenv("GS_NO_PIPELINE") && getenv("GS_NO_PIPELINE")[0] == '1';
+  const bool can_spec = !no_spec;
   uint32_t i = 0;
+  bool inflight = false, cur_special = false, spec_ok = true;
+  int cur_b = 0;
+  auto drain = [&]() { (void)hipStreamSynchronize(c->st); };
   while (i < npods) {
-    if ((rc = flush_rows(c))) return rc;
-    if (c->prep_stale && (rc = node_prep(c))) return rc;
-    // batch [i, i+b): a special pod always runs alone (its row is re-derived on the host afterwards)
-    int b = (int)std::min<uint32_t>(c->B, npods - i);
-    bool special_first = special_pod(c, pods[i]);
-    if (special_first) {
-      b = 1;
-    } else {
-      for (int j = 1; j < b; ++j)
-        if (special_pod(c, pods[i + j])) { b = j; break; }
+    if (!inflight) {
+      if ((rc = flush_rows(c))) return rc;
+      if (c->prep_stale && (rc = node_prep(c))) return rc;
+      cur_b = batch_len(c, pods, i, npods, &cur_special);
+      // (a cpuset pod whose node is outside the device cpuset scope ends the batch inside the commit kernel)
+      if ((rc = stage_batch(c, pods, seq, i, cur_b))) return rc;
+      if ((rc = launch_batch(c, cur_b, nullptr))) return rc;
     }
-    // (a cpuset pod whose node is outside the device cpuset scope ends the batch inside the commit kernel)
-    for (int j = 0; j < b; ++j) {
-      c->h_pods[j] = prep_pod(c, pods[i + j]);
-      c->h_seq[j] = seq ? seq[i + j] : (uint64_t)(i + j);
+    bool spec = false;
+    int nb = 0;
+    const uint32_t j = i + cur_b;
+    if (can_spec && spec_ok && !cur_special && j < npods && c->dirty_list.empty() && !c->prep_stale) {
+      bool sf = false;
+      nb = batch_len(c, pods, j, npods, &sf);
+      if (!sf && !uid_overlap(pods + i, cur_b, pods + j, nb)) {
+        const int32_t* prev = c->d_committed;
+        const int here = c->cur_slot;
+        bind_slot(c, 1 - here);
+        rc = stage_batch(c, pods, seq, j, nb);
+        if (!rc) rc = launch_batch(c, nb, prev);
+        bind_slot(c, here);
+        if (rc) { drain(); return rc; }
+        spec = true;
+      }
     }
-    HIP_TRY(c, hipMemcpyAsync(c->d_pods, c->h_pods, sizeof(PodVec) * b, hipMemcpyHostToDevice, c->st));
-    HIP_TRY(c, hipMemcpyAsync(c->d_seq, c->h_seq, 8 * b, hipMemcpyHostToDevice, c->st));
+    spec_ok = true;
     int committed = 0;
-    if ((rc = run_batch(c, pods + i, b, &committed))) return rc;
-    for (int j = 0; j < committed; ++j) {
-      const PlacementDev& pd = c->h_out[j];
-      gs_placement& o = out[i + j];
+    rc = finish_batch(c, cur_b, spec, &committed);
+    if (rc == GS_REDO) {   // pod 0 needs the full-row path, the speculative pass (void) overwrote its rows: re-run
+      drain();
+      if ((rc = launch_batch(c, cur_b, nullptr))) return rc;
+      inflight = true;
+      spec_ok = false;
+      continue;
+    }
+    if (rc) { if (spec) drain(); return rc; }
+    const bool host_work = c->h_committed[1] != 1;   // the device-side continuation flag the speculative pass read
+    for (int k = 0; k < committed; ++k) {
+      const PlacementDev& pd = c->h_out[k];
+      gs_placement& o = out[i + k];
       o.node = pd.node;
       o.feasible = pd.feasible;
       o.score = pd.node >= 0 ? pd.score : 0;
       o.ties = pd.node >= 0 ? pd.ties : 0;
       o.flags = pd.flags & ~PL_INTERNAL_FLAGS;
       if (pd.flags & GS_PLACED_SLOWPATH) c->stats.slowpath_pods += 1;   // resolved from its whole score row
-      if ((rc = numa_reserve(c, pods[i + j], c->h_pods[j], pd))) return rc;
-      apply_placement(c, pods[i + j], pd.node, special_first);
+      if ((rc = numa_reserve(c, pods[i + k], c->h_pods[k], pd))) { if (spec) drain(); return rc; }
+      apply_placement(c, pods[i + k], pd.node, cur_special);
     }
     c->stats.pods += committed;
     i += committed;
+    inflight = false;
+    if (spec) {
+      if (!host_work && committed == cur_b) {
+        if (!c->dirty_list.empty() || c->prep_stale) {
+          drain();
+          return fail(c, GS_ESTATE, "speculative batch ran while host rows were pending");
+        }
+        bind_slot(c, 1 - c->cur_slot);
+        cur_b = nb;
+        cur_special = false;
+        inflight = true;
+      } else {
+        drain();   // its commit kernel was a no-op
+      }
+    }
   }
   return flush_rows(c);
 }

@@ -85,6 +85,7 @@ struct CommitArgs {
   uint32_t ld;
   uint32_t own0, own1;       // this rank's shard [own0, own1)
   const int16_t* S;          // batch-start score rows (one shard only: in-kernel full-row resolution; else nullptr)
+  const int32_t* prev;       // speculative pass: the previous batch's committed[2]; run only if prev[1] == 1
 };
 
 hipError_t set_kernel_attributes();

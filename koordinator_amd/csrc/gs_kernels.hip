@@ -614,6 +614,12 @@ __global__ void __launch_bounds__(256) commit_kernel(CommitArgs a) {
   __shared__ int s_aff;                                // known affinity of pod k on its winner row (-1: recompute)
   __shared__ uint64_t s_cpuset[4];                     // CPUs of a device-side cpuset Reserve
   const bool numa_on = (a.pf.enabled & 0x30u) != 0;
+  // speculative pass queued behind another batch: only if that one committed every pod with nothing left for
+  // the host (committed[1] == 1); otherwise a no-op (committed = -1) the host discards
+  if (a.prev && a.prev[1] != 1) {
+    if (tid == 0) { a.committed[0] = -1; a.committed[1] = 0; }
+    return;
+  }
 
   if (tid == 0) {
     s_topo_id = -1;
@@ -653,6 +659,7 @@ __global__ void __launch_bounds__(256) commit_kernel(CommitArgs a) {
   __shared__ uint64_t hs_seq[HCH];
   int nd = 0;
   int committed = B;
+  bool host_cut = false;   // the batch ended at a pod whose cpuset Reserve the host performs
   __syncthreads();
 
   for (int k = 0; k < B; ++k) {
@@ -1029,7 +1036,7 @@ __global__ void __launch_bounds__(256) commit_kernel(CommitArgs a) {
       }
     }
     __syncthreads();
-    if (s_cut) { committed = k + 1; break; }
+    if (s_cut) { committed = k + 1; host_cut = true; break; }
     if (tid == 0) STAMP(7);
     // batch-start scores (fresh rows) on threads 0..127, current scores on threads 128..255; one call site,
     // so the long pair evaluation exists once in the instruction cache
@@ -1078,7 +1085,10 @@ __global__ void __launch_bounds__(256) commit_kernel(CommitArgs a) {
       else if (j < 25) m.c64(C_CPU_UN0 + (j - 19))[node] = reinterpret_cast<const int64_t*>(&cst[sl])[j - 19];
       else m.c32(C_CPU_META)[node] = (int32_t)cst[sl].meta;
     }
-  if (tid == 0) *a.committed = committed;
+  if (tid == 0) {
+    a.committed[0] = committed;
+    a.committed[1] = (committed == B && !host_cut) ? 1 : 0;
+  }
   if (ST && tid == 0)
     for (int i = 0; i < 12; ++i) a.stamps[i] += st_acc[i];
   if (ST && tid == 128) { a.stamps[12] += st_acc[12]; a.stamps[13] += st_acc[13]; }
