@@ -70,6 +70,8 @@ struct gs_ctx {
   std::string err;
   uint32_t N = 0, npad = 0;
   hipStream_t st = nullptr;
+  hipStream_t st2 = nullptr;                // side stream: eval_kernel beside eval_numa_kernel
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   // device mirror
   int64_t* d_i64 = nullptr;
   int32_t* d_i32 = nullptr;
@@ -759,7 +761,7 @@ int launch_batch(gs_ctx* c, int b, const int32_t* prev) {
     c->numa_idx_stale = false;
   }
   HIP_TRY(c, launch_eval(c->mv, c->d_pods, b, c->pf, c->n0, c->n1, c->d_S, c->ld, prod_cols, c->d_numa_idx, c->numa_n,
-                         c->d_aff, c->st));
+                         c->d_aff, c->st, c->st2, c->ev_fork, c->ev_join));
   HIP_TRY(c, hipEventRecord(c->ev[1], c->st));
   HIP_TRY(c, launch_cand(c->d_S, c->ld, len, c->n0, b, c->max_score, d_lists, d_hdrs, c->st));
   HIP_TRY(c, hipEventRecord(c->ev[2], c->st));
@@ -972,6 +974,9 @@ int gs_create(const gs_config* cfg, gs_ctx** out) {
   if ((e = hipSetDevice(cfg->device)) != hipSuccess) return bail("hipSetDevice", e);
   if ((e = set_kernel_attributes()) != hipSuccess) return bail("hipFuncSetAttribute", e);
   if ((e = hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking)) != hipSuccess) return bail("hipStreamCreate", e);
+  if ((e = hipStreamCreateWithFlags(&c->st2, hipStreamNonBlocking)) != hipSuccess) return bail("hipStreamCreate", e);
+  if ((e = hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming)) != hipSuccess) return bail("hipEventCreate", e);
+  if ((e = hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming)) != hipSuccess) return bail("hipEventCreate", e);
   for (auto& ev : c->ev)
     if ((e = hipEventCreate(&ev)) != hipSuccess) return bail("hipEventCreate", e);
   size_t np = c->npad;
@@ -1077,6 +1082,10 @@ int gs_destroy(gs_ctx* c) {
     if (p) (void)hipHostFree(p);
   for (auto& ev : c->ev)
     if (ev) (void)hipEventDestroy(ev);
+  if (c->st2) (void)hipStreamSynchronize(c->st2);
+  if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
+  if (c->ev_join) (void)hipEventDestroy(c->ev_join);
+  if (c->st2) (void)hipStreamDestroy(c->st2);
   if (c->st) (void)hipStreamDestroy(c->st);
   delete c;
   return GS_OK;

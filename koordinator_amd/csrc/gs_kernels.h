@@ -94,7 +94,8 @@ hipError_t launch_node_prep(const MirrorView& m, uint32_t n0, uint32_t n1, int64
 // NodeNUMAResource profiles: numa_idx lists the shard's nodes with a NUMA topology policy (ascending)
 hipError_t launch_eval(const MirrorView& m, const PodVec* pods, int npods, const Profile& pf, uint32_t n0, uint32_t n1,
                        int16_t* S, uint32_t ld, int prod_cols, const uint32_t* numa_idx, uint32_t numa_n,
-                       uint8_t* aff, hipStream_t st);
+                       uint8_t* aff, hipStream_t st, hipStream_t st2 = nullptr, hipEvent_t fork = nullptr,
+                       hipEvent_t join = nullptr);
 hipError_t launch_eval_full(const MirrorView& m, const PodVec* pods, int npods, const Profile& pf, uint32_t N,
                             int16_t* scores, uint16_t* codes, int16_t* plugin, int prod_cols, hipStream_t st);
 hipError_t launch_cand(const int16_t* S, uint32_t ld, uint32_t len, uint32_t n0, int npods, int max_score,

@@ -135,7 +135,8 @@ struct SlotsLds {
 // NUMA_POLICY_NODES = false: NodeNUMAResource's topology-policy path is compiled out (eval_kernel routes those
 // nodes to eval_numa_kernel)
 template <bool FULL, bool LDS_SCALARS, bool NUMA_POLICY_NODES = true>
-__device__ __forceinline__ PairOut eval_pair(const Row& r, const PodVec& p, const Profile& pf, const MirrorView& m) {
+__device__ __forceinline__ PairOut eval_pair(const Row& r, const PodVec& p, const Profile& pf, const MirrorView& m,
+                                             uint64_t* prof = nullptr) {
   PairOut o{0u, 0, 0, 0, 0u};
   // ---- [upstream] noderesources Fit.Filter -> fitsRequest
   if (pf.enabled & 0x1u) {
@@ -162,7 +163,8 @@ __device__ __forceinline__ PairOut eval_pair(const Row& r, const PodVec& p, cons
   // ---- NodeNUMAResource Filter (+ Admit) and Score (gs_numa_dev.h)
   if (pf.enabled & 0x30u) {
     NumaOut no;
-    if (LDS_SCALARS) no = numa_eval<NUMA_POLICY_NODES>(r.nr, p, pf, SlotsLds{r, m}, pf.enabled & 0x10u, pf.enabled & 0x20u);
+    if (LDS_SCALARS) no = numa_eval<NUMA_POLICY_NODES>(r.nr, p, pf, SlotsLds{r, m}, pf.enabled & 0x10u, pf.enabled & 0x20u,
+                                                       -1, prof);
     else no = numa_eval<NUMA_POLICY_NODES>(r.nr, p, pf, SlotsHbm{r, m}, pf.enabled & 0x10u, pf.enabled & 0x20u);
     if (pf.enabled & 0x10u) o.code |= no.reason << GS_FAIL_NUMA_SHIFT;
     if (!FULL && o.code) return o;
@@ -478,8 +480,9 @@ static_assert(POD_STRIDE >= (int)sizeof(PodVec) && POD_STRIDE % 8 == 0, "pod str
 constexpr int WIN = 2 * MAX_BATCH + 8;
 #define WAVE_FENCE() __builtin_amdgcn_wave_barrier()
 
-__device__ __forceinline__ int32_t row_score(const Row& d, const PodVec& p, const Profile& pf, const MirrorView& m) {
-  return total_score(eval_pair<false, true>(d, p, pf, m), pf);
+__device__ __forceinline__ int32_t row_score(const Row& d, const PodVec& p, const Profile& pf, const MirrorView& m,
+                                             uint64_t* prof = nullptr) {
+  return total_score(eval_pair<false, true>(d, p, pf, m, prof), pf);
 }
 
 __device__ __forceinline__ int hash_find(const int32_t* hkey, const int32_t* hval, uint32_t node) {
@@ -570,6 +573,7 @@ __device__ __noinline__ bool cpuset_reserve(const TopoDev& t, CpuStateDev& cs, c
 template <bool ST>
 __global__ void __launch_bounds__(256) commit_kernel(CommitArgs a) {
   uint64_t st_acc[14] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+  uint64_t np_acc[6] = {0, 0, 0, 0, 0, 0};   // numa_eval segments of thread 128's policy-row rescoring (ST)
   uint64_t st_last = ST ? __builtin_amdgcn_s_memtime() : 0;
 #define STAMP(i)                                    \
   do {                                              \
@@ -1046,7 +1050,8 @@ __global__ void __launch_bounds__(256) commit_kernel(CommitArgs a) {
       const uint64_t t0_ = ST ? __builtin_amdgcn_s_memtime() : 0;
       if (q < B && (fresh || !start)) {
         const Row rr = start ? orow : d;   // registers: the evaluation re-reads row words many times
-        (start ? dso : dsc)[q * B + slot] = (int16_t)row_score(rr, pods(q), a.pf, m);
+        uint64_t* np = (ST && tid == 128 && ((d.nr.nflags >> NF_POLICY_SHIFT) & 3u)) ? np_acc : nullptr;
+        (start ? dso : dsc)[q * B + slot] = (int16_t)row_score(rr, pods(q), a.pf, m, np);
       }
       if (ST && tid == 128 && ((d.nr.nflags >> NF_POLICY_SHIFT) & 3u)) {
         st_acc[12] += 1;
@@ -1091,7 +1096,11 @@ __global__ void __launch_bounds__(256) commit_kernel(CommitArgs a) {
   }
   if (ST && tid == 0)
     for (int i = 0; i < 12; ++i) a.stamps[i] += st_acc[i];
-  if (ST && tid == 128) { a.stamps[12] += st_acc[12]; a.stamps[13] += st_acc[13]; }
+  if (ST && tid == 128) {
+    a.stamps[12] += st_acc[12];
+    a.stamps[13] += st_acc[13];
+    for (int i = 0; i < 6; ++i) a.stamps[14 + i] += np_acc[i];
+  }
 #undef STAMP
 }
 
@@ -1180,13 +1189,21 @@ hipError_t launch_node_prep(const MirrorView& m, uint32_t n0, uint32_t n1, int64
 
 hipError_t launch_eval(const MirrorView& m, const PodVec* pods, int npods, const Profile& pf, uint32_t n0, uint32_t n1,
                        int16_t* S, uint32_t ld, int prod_cols, const uint32_t* numa_idx, uint32_t numa_n,
-                       uint8_t* aff, hipStream_t st) {
+                       uint8_t* aff, hipStream_t st, hipStream_t st2, hipEvent_t fork, hipEvent_t join) {
   uint32_t len = n1 - n0;
   uint32_t gx = (len + 255) / 256;
   uint32_t gy = (npods + PODS_PER_BLOCK - 1) / PODS_PER_BLOCK;
   if (gx == 0 || gy == 0) return hipSuccess;
   if (pf.enabled & 0x30u) {
-    hipLaunchKernelGGL(eval_kernel<true>, dim3(gx, gy), dim3(256), 0, st, m, pods, npods, pf, n0, n1, S, ld, prod_cols);
+    // eval_kernel (nodes without a NUMA policy) and eval_numa_kernel write disjoint score entries: with a side
+    // stream they run concurrently, eval_kernel's blocks filling the CUs eval_numa_kernel's low-occupancy waves
+    // (and its tail) leave idle
+    const bool side = st2 && fork && join && numa_n;
+    hipError_t e;
+    if (side) {
+      if ((e = hipEventRecord(fork, st)) != hipSuccess) return e;
+      if ((e = hipStreamWaitEvent(st2, fork, 0)) != hipSuccess) return e;
+    }
     // short batches: one pair per thread keeps the grid wide
     static const int ppt_env = getenv("GS_NUMA_PPT") ? atoi(getenv("GS_NUMA_PPT")) : NUMA_PPT;
     const int ppt = npods >= 32 ? ppt_env : 1;
@@ -1204,6 +1221,14 @@ hipError_t launch_eval(const MirrorView& m, const PodVec* pods, int npods, const
     } else {
       hipLaunchKernelGGL(eval_numa_kernel<1>, dim3((numa_n + 255) / 256, npods), dim3(256), 0, st, m, pods, npods,
                          pf, numa_idx, numa_n, n0, S, ld, prod_cols, aff);
+    }
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    hipLaunchKernelGGL(eval_kernel<true>, dim3(gx, gy), dim3(256), 0, side ? st2 : st, m, pods, npods, pf, n0, n1, S,
+                       ld, prod_cols);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    if (side) {
+      if ((e = hipEventRecord(join, st2)) != hipSuccess) return e;
+      if ((e = hipStreamWaitEvent(st, join, 0)) != hipSuccess) return e;
     }
   } else {
     hipLaunchKernelGGL(eval_kernel<false>, dim3(gx, gy), dim3(256), 0, st, m, pods, npods, pf, n0, n1, S, ld, prod_cols);
