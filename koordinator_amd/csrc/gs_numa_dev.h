@@ -391,8 +391,10 @@ __device__ __forceinline__ NumaOut numa_eval(const NumaRow& r, const PodVec& p, 
         if (__popc(mask_at(mi)) == min_m) pre1 |= 1u << mi;
       }
     }
+    bool b_pref_after0 = false;   // diagnostics: pass 0 settled the merge
     for (int pass = 0; pass < 2; ++pass) {
       if (pass == 1) {
+        b_pref_after0 = b_pref;
         if (fast || b_pref) break;
         b_mask = full_mask;
         b_pref = false;
@@ -459,6 +461,11 @@ __device__ __forceinline__ NumaOut numa_eval(const NumaRow& r, const PodVec& p, 
       }
     }
     NP(2);
+    if (prof) {   // merge path counters: [6] fast, [7] preferred pass only, [8] full pass, [9] a wave lane ran a full pass
+      const bool full = !fast && !nil_hints && !b_pref_after0;
+      prof[fast ? 6 : (full ? 8 : 7)] += 1;
+      if (__ballot(full)) prof[9] += 1;
+    }
     bool admit = true;
     if (single) {
       if (b_mask == full_mask) b_has = false;   // policy_single_numa_node.go:70-73
