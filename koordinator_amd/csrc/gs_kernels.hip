@@ -573,7 +573,7 @@ __device__ __noinline__ bool cpuset_reserve(const TopoDev& t, CpuStateDev& cs, c
 template <bool ST>
 __global__ void __launch_bounds__(256) commit_kernel(CommitArgs a) {
   uint64_t st_acc[14] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-  uint64_t np_acc[6] = {0, 0, 0, 0, 0, 0};   // numa_eval segments of thread 128's policy-row rescoring (ST)
+  uint64_t np_acc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};   // numa_eval segments of thread 128's policy-row rescoring (ST)
   uint64_t st_last = ST ? __builtin_amdgcn_s_memtime() : 0;
 #define STAMP(i)                                    \
   do {                                              \
@@ -1099,7 +1099,7 @@ __global__ void __launch_bounds__(256) commit_kernel(CommitArgs a) {
   if (ST && tid == 128) {
     a.stamps[12] += st_acc[12];
     a.stamps[13] += st_acc[13];
-    for (int i = 0; i < 6; ++i) a.stamps[14 + i] += np_acc[i];
+    for (int i = 0; i < 10; ++i) a.stamps[14 + i] += np_acc[i];
   }
 #undef STAMP
 }
