@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define GS_ABI_VERSION 2u
+#define GS_ABI_VERSION 3u
 
 /* ---- resource slots (corev1.ResourceName restricted to the hot-path set) ---- */
 enum gs_resource {
@@ -268,6 +268,14 @@ typedef struct gs_config {
   uint64_t seed;                       /* tie-break stream seed (selectHost) */
   uint32_t batch_size;                 /* pods per device pass (0 = default 128) */
   uint32_t cand_cap;                   /* candidate-list capacity per pod and shard (0 = default 256) */
+  /* [upstream] findNodesThatPassFilters node sampling (schedule_one.go numFeasibleNodesToFind,
+   * KubeSchedulerConfiguration.PercentageOfNodesToScore). sample_nodes = 0: every node is checked (the parity
+   * harness's percentageOfNodesToScore = 100; nextStartNodeIndex never moves). sample_nodes = 1: the scheduler
+   * keeps nextStartNodeIndex and checks nodes in rotation order from it until numFeasibleNodesToFind(N) feasible
+   * nodes are found (parallelism-1 order; percentage_of_nodes_to_score 0 = the adaptive default
+   * 50 - N/125 %, at least 5 % and 100 nodes). Single GPU only (GS_EUNSUPPORTED with several ranks). */
+  int32_t sample_nodes;
+  int32_t percentage_of_nodes_to_score;
 } gs_config;
 
 /* ---- outputs ---- */
@@ -338,10 +346,15 @@ typedef struct gs_stats {
   double exchange_ms;        /* host wall time in the all-gather (multi-GPU) */
   uint64_t node_row_bytes;   /* bytes one pod x node evaluation reads from the node mirror */
   uint32_t shard_begin, shard_end; /* this rank's node range */
+  uint32_t next_start_node_index;  /* [upstream] Scheduler.nextStartNodeIndex after the last scheduled pod */
+  uint32_t pad0;
 } gs_stats;
 
 /* v1beta2.SetDefaults_LoadAwareSchedulingArgs (pkg/scheduler/apis/config/v1beta2/defaults.go:76-99) */
 void gs_loadaware_args_default(gs_loadaware_args* a);
+/* [upstream] Scheduler.numFeasibleNodesToFind (schedule_one.go, minFeasibleNodesToFind = 100,
+ * minFeasibleNodesPercentageToFind = 5) for N nodes and PercentageOfNodesToScore pct. */
+uint32_t gs_num_feasible_nodes_to_find(uint32_t num_all_nodes, int32_t pct);
 /* v1beta2 NodeResourcesFitArgs default scoring strategy: LeastAllocated cpu=1, memory=1 */
 void gs_fit_args_default(gs_fit_args* a);
 /* validation.ValidateLoadAwareSchedulingArgs (pkg/scheduler/apis/config/validation/validation_pluginargs.go:31-84) */

@@ -10,7 +10,7 @@ import os
 
 import numpy as np
 
-GS_ABI_VERSION = 2
+GS_ABI_VERSION = 3
 GS_NUM_RES = 8
 GS_RES_CPU, GS_RES_MEMORY, GS_RES_EPHEMERAL = 0, 1, 2
 GS_RES_BATCH_CPU, GS_RES_BATCH_MEMORY, GS_RES_MID_CPU, GS_RES_MID_MEMORY = 3, 4, 5, 6
@@ -155,6 +155,7 @@ class GsConfig(C.Structure):
         ("plugin_weights", i64 * GS_NUM_PLUGINS),
         ("loadaware", GsLoadAwareArgs), ("fit", GsFitArgs), ("numa", GsNumaArgs),
         ("seed", u64), ("batch_size", u32), ("cand_cap", u32),
+        ("sample_nodes", i32), ("percentage_of_nodes_to_score", i32),
     ]
 
 
@@ -168,6 +169,7 @@ class GsStats(C.Structure):
         ("eval_launches", u64), ("eval_pairs", u64),
         ("eval_ms", C.c_double), ("cand_ms", C.c_double), ("commit_ms", C.c_double), ("exchange_ms", C.c_double),
         ("node_row_bytes", u64), ("shard_begin", u32), ("shard_end", u32),
+        ("next_start_node_index", u32), ("pad0", u32),
     ]
 
 
@@ -227,6 +229,7 @@ SIGNATURES = {
     "gs_numa_allocations_release": (C.c_int, [P, P, P, u32]),
     "gs_numa_allocation_get": (C.c_int, [P, u32, u64, C.POINTER(GsPodAllocation)]),
     "gs_numa_args_default": (None, [C.POINTER(GsNumaArgs)]),
+    "gs_num_feasible_nodes_to_find": (u32, [u32, i32]),
 }
 
 

@@ -83,7 +83,8 @@ def numa_args(defaultCPUBindPolicy: str | None = None, scoringStrategy: dict | N
 
 def make_config(num_nodes: int, la: abi.GsLoadAwareArgs | None = None, fit: abi.GsFitArgs | None = None,
                 enabled: int = abi.GS_ENABLE_LA_FIT, weights=(1, 1, 1), seed: int = 0x6B6F6F7264, device: int = 0,
-                batch_size: int = 0, cand_cap: int = 0, numa: abi.GsNumaArgs | None = None) -> abi.GsConfig:
+                batch_size: int = 0, cand_cap: int = 0, numa: abi.GsNumaArgs | None = None,
+                percentage_of_nodes_to_score: int | None = None) -> abi.GsConfig:
     """One scheduler profile: NodeResourcesFit + LoadAwareScheduling (+ NodeNUMAResource) with score weights."""
     cfg = abi.GsConfig()
     cfg.abi_version = abi.GS_ABI_VERSION
@@ -99,4 +100,8 @@ def make_config(num_nodes: int, la: abi.GsLoadAwareArgs | None = None, fit: abi.
     cfg.seed = seed
     cfg.batch_size = batch_size
     cfg.cand_cap = cand_cap
+    # None: every node is checked (percentageOfNodesToScore = 100, the parity harness); else the reference's
+    # node sampling with this percentage (0 = adaptive)
+    cfg.sample_nodes = 0 if percentage_of_nodes_to_score is None else 1
+    cfg.percentage_of_nodes_to_score = percentage_of_nodes_to_score or 0
     return cfg

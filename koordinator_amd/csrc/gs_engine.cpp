@@ -71,6 +71,8 @@ struct gs_ctx {
   uint32_t N = 0, npad = 0;
   hipStream_t st = nullptr;
   hipStream_t st2 = nullptr;                // side stream: eval_kernel beside eval_numa_kernel
+  uint32_t window_k = 0;                    // node sampling: numFeasibleNodesToFind(N) (0 = every node)
+  uint32_t next_start = 0;                  // [upstream] Scheduler.nextStartNodeIndex
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   // device mirror
   int64_t* d_i64 = nullptr;
@@ -735,6 +737,9 @@ CommitArgs commit_args(gs_ctx* c, int b) {
   a.own0 = c->n0;
   a.own1 = c->n1;
   a.S = c->nranks == 1 ? c->d_S : nullptr;
+  a.window_k = c->window_k;
+  a.start = c->next_start;
+  a.nnodes = c->N;
   return a;
 }
 
@@ -763,7 +768,8 @@ int launch_batch(gs_ctx* c, int b, const int32_t* prev) {
   HIP_TRY(c, launch_eval(c->mv, c->d_pods, b, c->pf, c->n0, c->n1, c->d_S, c->ld, prod_cols, c->d_numa_idx, c->numa_n,
                          c->d_aff, c->st, c->st2, c->ev_fork, c->ev_join));
   HIP_TRY(c, hipEventRecord(c->ev[1], c->st));
-  HIP_TRY(c, launch_cand(c->d_S, c->ld, len, c->n0, b, c->max_score, d_lists, d_hdrs, c->st));
+  if (!c->window_k)   // node sampling selects over the rotation window, not the candidate levels
+    HIP_TRY(c, launch_cand(c->d_S, c->ld, len, c->n0, b, c->max_score, d_lists, d_hdrs, c->st));
   HIP_TRY(c, hipEventRecord(c->ev[2], c->st));
   if (c->nranks > 1) {
     int rc = exchange(c, c->d_xchg_send, c->d_xchg_recv, c->xchg_bytes);
@@ -774,7 +780,7 @@ int launch_batch(gs_ctx* c, int b, const int32_t* prev) {
   HIP_TRY(c, hipEventRecord(c->ev[3], c->st));
   HIP_TRY(c, launch_commit(a, c->st));
   HIP_TRY(c, hipEventRecord(c->ev[4], c->st));
-  HIP_TRY(c, hipMemcpyAsync(c->h_committed, c->d_committed, 8, hipMemcpyDeviceToHost, c->st));
+  HIP_TRY(c, hipMemcpyAsync(c->h_committed, c->d_committed, 16, hipMemcpyDeviceToHost, c->st));
   HIP_TRY(c, hipMemcpyAsync(c->h_out, c->d_out, sizeof(PlacementDev) * b, hipMemcpyDeviceToHost, c->st));
   HIP_TRY(c, hipEventRecord(c->ev[5], c->st));
   return GS_OK;
@@ -793,6 +799,11 @@ int finish_batch(gs_ctx* c, int b, bool clobbered, int* committed_out) {
   c->stats.batches += 1;
   int committed = c->h_committed[0];
   if (committed < 0) return fail(c, GS_ESTATE, "commit pass of a batch was voided unexpectedly");
+  if (c->window_k) {
+    if (committed == 0) return fail(c, GS_ESTATE, "node-sampling commit made no progress");
+    c->next_start = (uint32_t)c->h_committed[2];
+    c->stats.next_start_node_index = c->next_start;
+  }
   if (committed == 0 && clobbered) return GS_REDO;
   if (committed == 0) {
     CommitArgs a = commit_args(c, b);
@@ -852,7 +863,7 @@ int finish_batch(gs_ctx* c, int b, bool clobbered, int* committed_out) {
     HIP_TRY(c, hipEventRecord(c->ev[3], c->st));
     HIP_TRY(c, launch_commit(a, c->st));
     HIP_TRY(c, hipEventRecord(c->ev[4], c->st));
-    HIP_TRY(c, hipMemcpyAsync(c->h_committed, c->d_committed, 8, hipMemcpyDeviceToHost, c->st));
+    HIP_TRY(c, hipMemcpyAsync(c->h_committed, c->d_committed, 16, hipMemcpyDeviceToHost, c->st));
     HIP_TRY(c, hipStreamSynchronize(c->st));
     c->stats.commit_ms += ev_ms(c->ev[3], c->ev[4]);
     committed = c->h_committed[0];
@@ -869,6 +880,16 @@ int finish_batch(gs_ctx* c, int b, bool clobbered, int* committed_out) {
 
 // ================================================================================================
 extern "C" {
+
+uint32_t gs_num_feasible_nodes_to_find(uint32_t num_all_nodes, int32_t pct) {
+  // [upstream] schedule_one.go numFeasibleNodesToFind: minFeasibleNodesToFind = 100,
+  // minFeasibleNodesPercentageToFind = 5, adaptive 50 - N/125 % (int32 arithmetic)
+  const int32_t n = (int32_t)num_all_nodes;
+  if (n < 100 || pct >= 100) return num_all_nodes;
+  int32_t p = pct > 0 ? pct : std::max<int32_t>(5, 50 - n / 125);
+  const int32_t k = n * p / 100;
+  return k < 100 ? 100u : (uint32_t)k;
+}
 
 const char* gs_version(void) { return "libgpuscore 0.1 (gfx950, ABI 1)"; }
 
@@ -953,6 +974,8 @@ int gs_create(const gs_config* cfg, gs_ctx** out) {
     delete c;
     return GS_EINVAL;
   }
+  if (cfg->sample_nodes != 0 && cfg->sample_nodes != 1) { delete c; return GS_EINVAL; }
+  c->window_k = cfg->sample_nodes ? gs_num_feasible_nodes_to_find(cfg->num_nodes, cfg->percentage_of_nodes_to_score) : 0;
   c->B = cfg->batch_size ? (int)cfg->batch_size : MAX_BATCH;
   if (c->B < 1 || c->B > MAX_BATCH || (cfg->cand_cap && cfg->cand_cap != (uint32_t)LCAP)) {
     fprintf(stderr, "gpuscore: batch_size must be in [1,%d] and cand_cap %d\n", MAX_BATCH, LCAP);
@@ -996,7 +1019,7 @@ int gs_create(const gs_config* cfg, gs_ctx** out) {
   if ((e = hipMalloc(&c->d_xchg_send, xb)) != hipSuccess) return bail("hipMalloc", e);
   c->xchg_bytes = xb;
   if ((e = hipMalloc(&c->d_out, sizeof(PlacementDev) * c->B)) != hipSuccess) return bail("hipMalloc", e);
-  if ((e = hipMalloc(&c->d_committed, 8)) != hipSuccess) return bail("hipMalloc", e);
+  if ((e = hipMalloc(&c->d_committed, 16)) != hipSuccess) return bail("hipMalloc", e);
   if ((e = hipMalloc(&c->d_rowstat, sizeof(RowStat) * (1 + MAX_RANKS))) != hipSuccess) return bail("hipMalloc", e);
   if ((e = hipMalloc(&c->d_sel, 4 * (1 + MAX_RANKS))) != hipSuccess) return bail("hipMalloc", e);
   c->stage_cap = std::min<uint32_t>(c->N, 65536);
@@ -1008,7 +1031,7 @@ int gs_create(const gs_config* cfg, gs_ctx** out) {
   if ((e = hipHostMalloc(&c->h_pods, sizeof(PodVec) * c->B, hipHostMallocDefault)) != hipSuccess) return bail("hipHostMalloc", e);
   if ((e = hipHostMalloc(&c->h_seq, 8 * c->B, hipHostMallocDefault)) != hipSuccess) return bail("hipHostMalloc", e);
   if ((e = hipHostMalloc(&c->h_out, sizeof(PlacementDev) * c->B, hipHostMallocDefault)) != hipSuccess) return bail("hipHostMalloc", e);
-  if ((e = hipHostMalloc(&c->h_committed, 8, hipHostMallocDefault)) != hipSuccess) return bail("hipHostMalloc", e);
+  if ((e = hipHostMalloc(&c->h_committed, 16, hipHostMallocDefault)) != hipSuccess) return bail("hipHostMalloc", e);
   if ((e = hipHostMalloc(&c->h_xchg_send, xb, hipHostMallocDefault)) != hipSuccess) return bail("hipHostMalloc", e);
   (void)hipMemset(c->d_S, 0xff, (size_t)c->B * c->ld * 2);
   {
@@ -1020,11 +1043,11 @@ int gs_create(const gs_config* cfg, gs_ctx** out) {
     if ((e = hipMalloc(&s1.d_pods, sizeof(PodVec) * c->B)) != hipSuccess) return bail("hipMalloc", e);
     if ((e = hipMalloc(&s1.d_seq, 8 * c->B)) != hipSuccess) return bail("hipMalloc", e);
     if ((e = hipMalloc(&s1.d_out, sizeof(PlacementDev) * c->B)) != hipSuccess) return bail("hipMalloc", e);
-    if ((e = hipMalloc(&s1.d_committed, 8)) != hipSuccess) return bail("hipMalloc", e);
+    if ((e = hipMalloc(&s1.d_committed, 16)) != hipSuccess) return bail("hipMalloc", e);
     if ((e = hipHostMalloc(&s1.h_pods, sizeof(PodVec) * c->B, hipHostMallocDefault)) != hipSuccess) return bail("hipHostMalloc", e);
     if ((e = hipHostMalloc(&s1.h_seq, 8 * c->B, hipHostMallocDefault)) != hipSuccess) return bail("hipHostMalloc", e);
     if ((e = hipHostMalloc(&s1.h_out, sizeof(PlacementDev) * c->B, hipHostMallocDefault)) != hipSuccess) return bail("hipHostMalloc", e);
-    if ((e = hipHostMalloc(&s1.h_committed, 8, hipHostMallocDefault)) != hipSuccess) return bail("hipHostMalloc", e);
+    if ((e = hipHostMalloc(&s1.h_committed, 16, hipHostMallocDefault)) != hipSuccess) return bail("hipHostMalloc", e);
     for (auto& ev : s1.ev)
       if ((e = hipEventCreate(&ev)) != hipSuccess) return bail("hipEventCreate", e);
   }
@@ -1434,6 +1457,7 @@ int gs_comm_unique_id(uint8_t out[128]) {
 
 int gs_comm_init_rccl(gs_ctx* c, const uint8_t id[128], int nranks, int rank) {
   if (!c || !id || nranks < 1 || nranks > MAX_RANKS || rank < 0 || rank >= nranks) return GS_EINVAL;
+  if (c->window_k && nranks > 1) return fail(c, GS_EUNSUPPORTED, "node sampling runs on one GPU");
   if (nranks > 1) {
     ncclUniqueId uid;
     std::memcpy(&uid, id, 128);
@@ -1450,6 +1474,7 @@ int gs_comm_init_rccl(gs_ctx* c, const uint8_t id[128], int nranks, int rank) {
 
 int gs_comm_init_callback(gs_ctx* c, int nranks, int rank, gs_allgather_fn fn, void* user) {
   if (!c || !fn || nranks < 1 || nranks > MAX_RANKS || rank < 0 || rank >= nranks) return GS_EINVAL;
+  if (c->window_k && nranks > 1) return fail(c, GS_EUNSUPPORTED, "node sampling runs on one GPU");
   c->cb = fn;
   c->cb_user = user;
   c->nranks = nranks;
@@ -1462,6 +1487,7 @@ int gs_comm_init_callback(gs_ctx* c, int nranks, int rank, gs_allgather_fn fn, v
 int gs_get_stats(gs_ctx* c, gs_stats* out) {
   if (!c || !out) return GS_EINVAL;
   *out = c->stats;
+  out->next_start_node_index = c->next_start;
   return GS_OK;
 }
 

@@ -85,7 +85,12 @@ struct CommitArgs {
   uint32_t ld;
   uint32_t own0, own1;       // this rank's shard [own0, own1)
   const int16_t* S;          // batch-start score rows (one shard only: in-kernel full-row resolution; else nullptr)
-  const int32_t* prev;       // speculative pass: the previous batch's committed[2]; run only if prev[1] == 1
+  const int32_t* prev;       // speculative pass: the previous batch's committed[4]; run only if prev[1] == 1
+  // node sampling (gs_config.sample_nodes, one shard): window_k = numFeasibleNodesToFind(N) (0 = every node);
+  // the batch starts at nextStartNodeIndex `start` (prev[2] for a speculative pass) and leaves it in committed[2]
+  uint32_t window_k;
+  uint32_t start;
+  uint32_t nnodes;
 };
 
 hipError_t set_kernel_attributes();

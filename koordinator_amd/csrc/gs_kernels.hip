@@ -625,7 +625,11 @@ __global__ void __launch_bounds__(256) commit_kernel(CommitArgs a) {
     return;
   }
 
+  __shared__ uint32_t s_start;                         // nextStartNodeIndex (node sampling)
+  __shared__ int32_t s_wred[3][8];                     // window selection: block scans / reductions
+  __shared__ int32_t s_wend, s_wproc, s_wfound;
   if (tid == 0) {
+    s_start = a.window_k ? (a.prev ? (uint32_t)a.prev[2] : a.start) : 0u;
     s_topo_id = -1;
     s_fk = a.forced_node >= 0 ? 0 : -1;
     s_fnode = a.forced_node;
@@ -666,8 +670,157 @@ __global__ void __launch_bounds__(256) commit_kernel(CommitArgs a) {
   bool host_cut = false;   // the batch ended at a pod whose cpuset Reserve the host performs
   __syncthreads();
 
+  // wave 0: the winner's slot in the dirty set (its batch-start row, CPU state and Filter-time affinity fetched
+  // from HBM when fresh: one load per lane, all issued before a single wait), and the decision for pod k
+  auto fetch_winner = [&](int k, uint32_t winner, int M, int F, int64_t T) {
+    int slot = hash_find(hkey, hval, winner);
+    const bool fresh = slot < 0;
+    if (fresh) {
+      slot = nd;
+      if (lane == 0) {
+        uint32_t h = (winner * 2654435761u) & (HASH - 1);
+        while (hkey[h] >= 0) h = (h + 1) & (HASH - 1);
+        hkey[h] = (int32_t)winner;
+        hval[h] = slot;
+      }
+      ++nd;
+      // one load per lane, all issued before a single wait (the per-lane source/destination map is built once)
+      int64_t v = 0;
+      if (f_kind == 1) v = reinterpret_cast<const int64_t*>(f_src)[winner];
+      else if (f_kind == 2) v = reinterpret_cast<const int32_t*>(f_src)[winner];
+      else if (f_kind == 3) {   // the batch-start Filter's affinity for this pair (own shard, NUMA-policy nodes)
+        const bool own = f_src && winner >= a.own0 && winner < a.own1;
+        v = own ? (int64_t)reinterpret_cast<const uint8_t*>(f_src)[(size_t)k * a.ld + (winner - a.own0)] : -1;
+      } else if (f_kind == 4) v = (int64_t)winner;   // Row.node, Row.pad = 0
+      if (f_kind) {
+        unsigned char* dst = f_region == 0 ? reinterpret_cast<unsigned char*>(&orow)
+                           : f_region == 1 ? reinterpret_cast<unsigned char*>(&cst[slot])
+                                           : reinterpret_cast<unsigned char*>(&s_aff);
+        if (f_size == 8) *reinterpret_cast<int64_t*>(dst + f_off) = v;
+        else *reinterpret_cast<int32_t*>(dst + f_off) = (int32_t)v;
+      }
+    }
+    if (lane == 0) {
+      s_action = 0; s_slot = slot; s_fresh = fresh; s_winner = winner; s_M = M; s_F = F; s_T = T;
+      if (!fresh || !numa_on) s_aff = -1;   // a dirty row changed since the batch-start Filter
+    }
+  };
+  // Node sampling ([upstream] findNodesThatPassFilters, parallelism-1 order): positions i = 0.. from s_start in
+  // rotation order; a node's verdict for pod k is its batch-start score S[k][n] unless an earlier pod of the batch
+  // landed on it (its current score dsc). The window is the first K = window_k feasible positions; the (K+1)-th
+  // feasible position ends the search uncounted (processedNodes = its position, else N). selectHost: max and
+  // ties over the window, the jp-th tie in window order. All threads; 8 consecutive positions per thread.
+  auto block_scan = [&](int v, int slot, int* total) -> int {   // exclusive prefix over tid order
+    int incl = v;
+    for (int off = 1; off < 64; off <<= 1) {
+      const int u = __shfl_up(incl, off);
+      if (lane >= off) incl += u;
+    }
+    if (lane == 63) s_wred[slot][wave] = incl;
+    __syncthreads();
+    int base = 0, tot = 0;
+    for (int w = 0; w < 4; ++w) { const int x = s_wred[slot][w]; if (w < wave) base += x; tot += x; }
+    __syncthreads();
+    *total = tot;
+    return base + incl - v;
+  };
+  auto window_select = [&](int k) {
+    constexpr int WCH = 8;
+    const uint32_t N = a.nnodes, K = a.window_k, st0 = s_start;
+    const int16_t* row = a.S + (size_t)k * a.ld;
+    auto verdict = [&](uint32_t i) -> int {   // score of position i for pod k (-1: infeasible)
+      uint32_t n = st0 + i;
+      if (n >= N) n -= N;
+      const int sl = hash_find(hkey, hval, n);
+      return sl >= 0 ? (int)dsc[k * B + sl] : (int)row[n - a.own0];
+    };
+    if (tid == 0) { s_wend = (int)N - 1; s_wproc = (int)N; }
+    int found = 0, lmax = -1, lcnt = 0;
+    for (uint32_t base = 0; base < N; base += 256 * WCH) {
+      int v[WCH], c = 0;
+#pragma unroll
+      for (int j = 0; j < WCH; ++j) {
+        const uint32_t i = base + (uint32_t)tid * WCH + j;
+        v[j] = i < N ? verdict(i) : -1;
+        c += v[j] >= 0 ? 1 : 0;
+      }
+      int total = 0;
+      int idx = found + block_scan(c, 0, &total);   // window index of this thread's first feasible position
+#pragma unroll
+      for (int j = 0; j < WCH; ++j) {
+        if (v[j] < 0) continue;
+        const uint32_t i = base + (uint32_t)tid * WCH + j;
+        if ((uint32_t)idx < K) {
+          if (v[j] > lmax) { lmax = v[j]; lcnt = 1; }
+          else if (v[j] == lmax) ++lcnt;
+          if ((uint32_t)idx == K - 1) s_wend = (int)i;
+        } else if ((uint32_t)idx == K) {
+          s_wproc = (int)i;
+        }
+        ++idx;
+      }
+      found += total;
+      if ((uint32_t)found > K) break;   // block-uniform
+    }
+    // M, T over the window
+    const int wm = wave_max(lmax);
+    if (lane == 0) s_wred[1][wave] = wm;
+    __syncthreads();
+    const int M = max(max(s_wred[1][0], s_wred[1][1]), max(s_wred[1][2], s_wred[1][3]));
+    const int tl = wave_sum(lmax == M ? lcnt : 0);
+    __syncthreads();
+    if (lane == 0) s_wred[2][wave] = tl;
+    __syncthreads();
+    const int64_t T = (int64_t)s_wred[2][0] + s_wred[2][1] + s_wred[2][2] + s_wred[2][3];
+    const int F = (int)min((uint32_t)found, K);
+    const uint32_t wend = (uint32_t)s_wend, proc = (uint32_t)s_wproc;
+    if (M < 0) {   // FitError: nothing assumed; every node was processed
+      if (tid == 0) {
+        a.out[k] = PlacementDev{-1, (uint32_t)F, 0, 0, 0, 0, 0, {0, 0, 0, 0}, {0, 0, 0, 0}};
+        s_action = 1;
+        s_start = (st0 + proc) % N;
+      }
+      __syncthreads();
+      return;
+    }
+    // the jp-th tie at M in window order
+    const int64_t jp = tiebreak_position(a.seed, a.seq[k], T);
+    int64_t before = 0;
+    if (tid == 0) s_fnode = -1;
+    for (uint32_t base = 0; base <= wend; base += 256 * WCH) {
+      int c = 0;
+#pragma unroll
+      for (int j = 0; j < WCH; ++j) {
+        const uint32_t i = base + (uint32_t)tid * WCH + j;
+        c += (i <= wend && verdict(i) == M) ? 1 : 0;
+      }
+      int total = 0;
+      const int64_t ex = before + block_scan(c, 0, &total);
+      if (c > 0 && jp > ex && jp <= ex + c) {
+        int64_t need = jp - ex;
+        for (int j = 0; j < WCH; ++j) {
+          const uint32_t i = base + (uint32_t)tid * WCH + j;
+          if (i <= wend && verdict(i) == M && --need == 0) {
+            uint32_t n = st0 + i;
+            s_fnode = (int)(n >= N ? n - N : n);
+            break;
+          }
+        }
+      }
+      before += total;
+      if (before >= jp) break;   // block-uniform
+    }
+    __syncthreads();
+    if (tid == 0) {
+      s_action = s_fnode >= 0 ? 0 : 2;   // 2: unreachable (the tie exists), the host fails loudly
+      s_winner = (uint32_t)s_fnode;
+      s_M = M; s_F = F; s_T = T;
+      s_start = (st0 + proc) % N;
+    }
+    __syncthreads();
+  };
   for (int k = 0; k < B; ++k) {
-   if (k % HCH == 0) {
+   if (k % HCH == 0 && !a.window_k) {
      for (int e = tid; e < HCH * nhl; e += 256) {
        int kk = e / nhl, l = e % nhl;
        if (k + kk < B) {
@@ -690,6 +843,12 @@ __global__ void __launch_bounds__(256) commit_kernel(CommitArgs a) {
      __syncthreads();
    }
    for (;;) {   // one pass; a second, forced one after an in-kernel full-row resolution
+   if (a.window_k) {   // node sampling: findNodesThatPassFilters over the rotation window, then selectHost
+     window_select(k);
+     if (wave == 0 && s_action == 0) fetch_winner(k, s_winner, s_M, s_F, s_T);
+     __syncthreads();
+     break;
+   }
    if (wave == 0) do {   // ===================== wave 0: selectHost for pod k =====================
     const int kc = k % HCH;
     const int r_l = lane / MAXLEV, j_l = lane % MAXLEV;
@@ -865,38 +1024,7 @@ __global__ void __launch_bounds__(256) commit_kernel(CommitArgs a) {
       winner = __shfl(cand, __ffsll((long long)got) - 1);
     }
     STAMP(5);
-    // ---- slot of the winner in the dirty set (batch-start row fetched from HBM when fresh)
-    int slot = hash_find(hkey, hval, winner);
-    const bool fresh = slot < 0;
-    if (fresh) {
-      slot = nd;
-      if (lane == 0) {
-        uint32_t h = (winner * 2654435761u) & (HASH - 1);
-        while (hkey[h] >= 0) h = (h + 1) & (HASH - 1);
-        hkey[h] = (int32_t)winner;
-        hval[h] = slot;
-      }
-      ++nd;
-      // one load per lane, all issued before a single wait (the per-lane source/destination map is built once)
-      int64_t v = 0;
-      if (f_kind == 1) v = reinterpret_cast<const int64_t*>(f_src)[winner];
-      else if (f_kind == 2) v = reinterpret_cast<const int32_t*>(f_src)[winner];
-      else if (f_kind == 3) {   // the batch-start Filter's affinity for this pair (own shard, NUMA-policy nodes)
-        const bool own = f_src && winner >= a.own0 && winner < a.own1;
-        v = own ? (int64_t)reinterpret_cast<const uint8_t*>(f_src)[(size_t)k * a.ld + (winner - a.own0)] : -1;
-      } else if (f_kind == 4) v = (int64_t)winner;   // Row.node, Row.pad = 0
-      if (f_kind) {
-        unsigned char* dst = f_region == 0 ? reinterpret_cast<unsigned char*>(&orow)
-                           : f_region == 1 ? reinterpret_cast<unsigned char*>(&cst[slot])
-                                           : reinterpret_cast<unsigned char*>(&s_aff);
-        if (f_size == 8) *reinterpret_cast<int64_t*>(dst + f_off) = v;
-        else *reinterpret_cast<int32_t*>(dst + f_off) = (int32_t)v;
-      }
-    }
-    if (lane == 0) {
-      s_action = 0; s_slot = slot; s_fresh = fresh; s_winner = winner; s_M = M; s_F = F; s_T = T;
-      if (!fresh || !numa_on) s_aff = -1;   // a dirty row changed since the batch-start Filter
-    }
+    fetch_winner(k, winner, M, F, T);
     STAMP(6);
    } while (0);
     __syncthreads();
@@ -1093,6 +1221,7 @@ __global__ void __launch_bounds__(256) commit_kernel(CommitArgs a) {
   if (tid == 0) {
     a.committed[0] = committed;
     a.committed[1] = (committed == B && !host_cut) ? 1 : 0;
+    a.committed[2] = (int32_t)s_start;
   }
   if (ST && tid == 0)
     for (int i = 0; i < 12; ++i) a.stamps[i] += st_acc[i];

@@ -116,6 +116,7 @@ struct or_cluster {
   std::vector<std::shared_ptr<orn::CPUTopology>> topologies;
   std::vector<orn::NodeNUMA> numa;
   bool reverse_hint_order = false;
+  uint32_t next_start = 0;   // [upstream] Scheduler.nextStartNodeIndex
 };
 
 namespace {
@@ -849,6 +850,22 @@ int or_take_cpus_test(int sockets, int nodes_per_socket, int cores_per_node, int
   return ok ? 0 : -1;
 }
 
+// [upstream] Scheduler.numFeasibleNodesToFind (schedule_one.go): minFeasibleNodesToFind = 100,
+// minFeasibleNodesPercentageToFind = 5, adaptive percentage 50 - N/125 when pct <= 0 (int32 arithmetic).
+uint32_t or_num_feasible_nodes_to_find(uint32_t num_all_nodes, int32_t pct) {
+  const int32_t n = (int32_t)num_all_nodes;
+  if (n < 100 || pct >= 100) return num_all_nodes;
+  int32_t adaptive = pct;
+  if (adaptive <= 0) {
+    adaptive = 50 - n / 125;
+    if (adaptive < 5) adaptive = 5;
+  }
+  const int32_t nodes = n * adaptive / 100;
+  return nodes < 100 ? 100u : (uint32_t)nodes;
+}
+
+uint32_t or_next_start_node_index(const or_cluster* c) { return c ? c->next_start : 0; }
+
 int32_t or_tiebreak_intn(uint64_t seed, uint64_t seq, int64_t cnt) {
   TieBreakRand rnd(seed, seq);
   return rnd.intn(cnt);
@@ -892,6 +909,7 @@ int or_schedule_replay(or_cluster* c, const gs_pod* pods, uint32_t npods, const 
     }
     if (given && given[p] >= 0) {
       if (given[p] >= N) return GS_EINVAL;
+      if (c->cfg.sample_nodes) return GS_EUNSUPPORTED;   // a replayed pod's processedNodes is unknown
       selected = given[p];
       const NodeState& s = c->nodes[selected];
       uint16_t code = 0;
@@ -903,8 +921,6 @@ int or_schedule_replay(or_cluster* c, const gs_pod* pods, uint32_t npods, const 
       if (code) return GS_ESTATE;
       o.feasible = 0; o.flags = 0; o.node = selected; o.score = 0; o.ties = 0;
     } else {
-    // findNodesThatPassFilters: percentageOfNodesToScore = 100, so every node is checked and
-    // nextStartNodeIndex = (start + N) % N stays put: feasible order = node index order.
     auto check = [&](int n) {
       const NodeState& s = c->nodes[n];
       uint16_t code = 0;
@@ -914,11 +930,29 @@ int or_schedule_replay(or_cluster* c, const gs_pod* pods, uint32_t npods, const 
       if (!code && (c->cfg.enabled & GS_ENABLE_NUMA_FILTER)) code |= numa_filter(*c, st, (uint32_t)n, &affinity[n]);
       feasible[n] = code == 0;
     };
-    if (pool) pool->until(N, check);
-    else for (int n = 0; n < N; ++n) check(n);
     feasible_list.clear();
-    for (int n = 0; n < N; ++n)
-      if (feasible[n]) feasible_list.push_back(n);
+    if (!c->cfg.sample_nodes) {
+      // findNodesThatPassFilters with percentageOfNodesToScore = 100: every node is checked and
+      // nextStartNodeIndex = (start + N) % N stays put: feasible order = node index order.
+      if (pool) pool->until(N, check);
+      else for (int n = 0; n < N; ++n) check(n);
+      for (int n = 0; n < N; ++n)
+        if (feasible[n]) feasible_list.push_back(n);
+    } else {
+      // findNodesThatPassFilters with node sampling, parallelism-1 order: nodes are checked in rotation order
+      // from nextStartNodeIndex; the (K+1)-th feasible node cancels the search uncounted (feasibleNodesLen is
+      // decremented), processedNodes = feasible + diagnosed, nextStartNodeIndex advances by it (mod N)
+      const int K = (int)or_num_feasible_nodes_to_find((uint32_t)N, c->cfg.percentage_of_nodes_to_score);
+      int diagnosed = 0;
+      for (int i = 0; i < N; ++i) {
+        const int n = (int)((c->next_start + (uint32_t)i) % (uint32_t)N);
+        check(n);
+        if (!feasible[n]) { ++diagnosed; continue; }
+        if ((int)feasible_list.size() >= K) break;
+        feasible_list.push_back(n);
+      }
+      c->next_start = (uint32_t)((c->next_start + feasible_list.size() + (uint32_t)diagnosed) % (uint32_t)N);
+    }
     o.feasible = (uint32_t)feasible_list.size();
     o.flags = 0;
     if (feasible_list.empty()) {   // FitError: nothing is assumed

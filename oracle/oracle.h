@@ -43,6 +43,9 @@ int or_fit_score(or_cluster* c, const gs_pod* pod, uint32_t node, int64_t* score
 int or_evaluate(or_cluster* c, const gs_pod* pods, uint32_t npods, int16_t* scores, uint16_t* codes,
                 int16_t* plugin_scores);
 /* nthreads <= 1: serial; otherwise a worker pool emulating parallelize.Until (pkg/util/parallelize/parallelism.go:29-49) */
+/* [upstream] numFeasibleNodesToFind; the scheduler's nextStartNodeIndex (cfg.sample_nodes) */
+uint32_t or_num_feasible_nodes_to_find(uint32_t num_all_nodes, int32_t pct);
+uint32_t or_next_start_node_index(const or_cluster* c);
 int or_schedule(or_cluster* c, const gs_pod* pods, uint32_t npods, const uint64_t* seq, gs_placement* out,
                 int nthreads);
 /* replay: pods with given[p] >= 0 are placed on that node (Filter on it alone for the affinity, Reserve,

@@ -42,6 +42,8 @@ def _load() -> C.CDLL:
         "or_fit_score": (C.c_int, [P, P, C.c_uint32, P]),
         "or_evaluate": (C.c_int, [P, P, C.c_uint32, P, P, P]),
         "or_schedule": (C.c_int, [P, P, C.c_uint32, P, P, C.c_int]),
+        "or_num_feasible_nodes_to_find": (C.c_uint32, [C.c_uint32, C.c_int32]),
+        "or_next_start_node_index": (C.c_uint32, [P]),
         "or_schedule_replay": (C.c_int, [P, P, C.c_uint32, P, P, P, C.c_int]),
         "or_tiebreak_intn": (C.c_int32, [C.c_uint64, C.c_uint64, C.c_int64]),
         "or_topology_register": (C.c_int, [P, P, P]),
@@ -200,6 +202,10 @@ class Oracle:
              "schedule")
         return out
 
+    @property
+    def next_start_node_index(self) -> int:
+        return int(lib().or_next_start_node_index(self._h))
+
     def schedule_replay(self, pods, given, seq=None, nthreads: int = 1):
         """Pods with given[i] >= 0 are placed on that node (Filter there for the affinity, Reserve, assume);
         given[i] == -2 replays a FitError (nothing assumed); given[i] == -1 runs scheduleOne on the replayed state."""
@@ -228,6 +234,10 @@ def estimate_node(node) -> tuple[int, int]:
     n = np.ascontiguousarray(np.atleast_1d(node), dtype=abi.NODE_DTYPE)
     _chk(lib().or_estimate_node(abi.ptr(n), abi.ptr(out)), "estimate_node")
     return int(out[0]), int(out[1])
+
+
+def num_feasible_nodes_to_find(num_all_nodes: int, pct: int) -> int:
+    return int(lib().or_num_feasible_nodes_to_find(num_all_nodes, pct))
 
 
 def tiebreak_intn(seed: int, seq: int, cnt: int) -> int:

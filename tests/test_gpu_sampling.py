@@ -1,0 +1,86 @@
+"""Node sampling on the HIP path ([upstream] findNodesThatPassFilters with percentageOfNodesToScore < 100,
+parallelism-1 rotation order from nextStartNodeIndex; gs_config.sample_nodes): the commit kernel's window
+selection against the oracle, bit-exact — node, max score, ties and feasible count (= the window size) of
+every pod, and nextStartNodeIndex after every call. Needs an MI355X: -m gpu."""
+import numpy as np
+import pytest
+
+from koordinator_amd import abi, config, synth
+from oracle import oracle as orc
+from tests.test_gpu_parity import homogeneous_cluster
+
+pytestmark = pytest.mark.gpu
+
+
+def sampling_pair(c, pct, **kw):
+    from koordinator_amd.engine import Engine
+    cfg = config.make_config(c.num_nodes, percentage_of_nodes_to_score=pct, **kw)
+    e, o = Engine(cfg), orc.Oracle(cfg)
+    if kw.get("enabled", 0) & abi.GS_ENABLE_NUMA_FILTER:
+        e.verify_cpusets(True)
+    synth.load_into(e, c)
+    synth.load_into(o, c)
+    return e, o
+
+
+def check(e, o, pods, lo=0):
+    seq = np.arange(lo, lo + len(pods), dtype=np.uint64)
+    got, want = e.schedule(pods, seq), o.schedule(pods, seq)
+    for f in ("node", "score", "ties", "feasible"):
+        bad = np.nonzero(got[f] != want[f])[0]
+        assert not len(bad), f"{f} differs at pod {lo + bad[0]}: gpu {got[bad[0]]} oracle {want[bad[0]]}"
+    assert e.stats()["next_start_node_index"] == o.next_start_node_index
+    return got
+
+
+def loaded_cluster(nodes, pods, cid):
+    c = synth.make_cluster(nodes, pods, cid)
+    c.pods["requests"][::3, 0] = 60_000     # many infeasible nodes per pod
+    c.pods["requests"][5::17, 0] = 400_000  # FitError: the whole ring is processed
+    c.pods["request_mask"][:] |= 0x1
+    return c
+
+
+@pytest.mark.parametrize("batch", [1, 16, 128])
+def test_sampling_adaptive_matches_oracle(batch):
+    c = loaded_cluster(3000, 600, 11)
+    e, o = sampling_pair(c, 0, batch_size=batch)
+    got = check(e, o, c.pods)
+    k = orc.num_feasible_nodes_to_find(3000, 0)
+    assert got["feasible"].max() == k and (got["node"] < 0).any()
+    assert e.mirror_check() == 0
+
+
+def test_sampling_percentage_across_calls():
+    """pct = 10 over several gs_schedule calls: nextStartNodeIndex carries over, pipelined batches read it on the
+    device from the batch before."""
+    c = loaded_cluster(5000, 900, 12)
+    e, o = sampling_pair(c, 10)
+    for lo in range(0, 900, 300):
+        check(e, o, c.pods[lo:lo + 300], lo)
+    assert e.mirror_check() == 0
+
+
+def test_sampling_numa_profile():
+    c = synth.make_cluster(2000, 300, 13)
+    synth.make_numa(c, numa_policy_pct=60, cpuset_pod_pct=30)
+    e, o = sampling_pair(c, 0, enabled=abi.GS_ENABLE_ALL)
+    got = check(e, o, c.pods)
+    assert (got["flags"] & abi.GS_PLACED_CPUSET).any()
+    assert e.mirror_check() == 0
+
+
+def test_sampling_homogeneous_ties():
+    """Identical nodes: every window node ties; the jp-th tie is located in window (rotation) order."""
+    c = homogeneous_cluster(4000, 200, 14)
+    e, o = sampling_pair(c, 5)
+    got = check(e, o, c.pods)
+    assert got["ties"].max() >= 100
+
+
+def test_sampling_refuses_several_ranks():
+    c = synth.make_cluster(500, 8, 15)
+    e, _ = sampling_pair(c, 0)
+    from koordinator_amd.engine import GpuScoreError
+    with pytest.raises(GpuScoreError, match="one GPU"):
+        e.comm_init_callback(2, 0, lambda send: [send, send])
