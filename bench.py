@@ -67,6 +67,8 @@ def main() -> None:
     ap.add_argument("--cpu-sample-pods", type=int, default=400)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--profile", choices=["c3", "la-fit"], default="c3")
+    ap.add_argument("--sample-pct", type=int, default=None,
+                    help="node sampling (percentageOfNodesToScore; 0 = adaptive) instead of every node (one GPU)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -94,8 +96,11 @@ def main() -> None:
     if numa:
         synth.make_numa(cluster)
     from koordinator_amd import abi
+    if args.sample_pct is not None and world > 1:
+        raise SystemExit("--sample-pct runs on one GPU")
     cfg = config.make_config(n_nodes, device=local_rank, batch_size=args.batch,
-                             enabled=abi.GS_ENABLE_ALL if numa else abi.GS_ENABLE_LA_FIT)
+                             enabled=abi.GS_ENABLE_ALL if numa else abi.GS_ENABLE_LA_FIT,
+                             percentage_of_nodes_to_score=args.sample_pct)
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -182,6 +187,11 @@ def main() -> None:
                              "assume+Reserve"),
                 "nodes": n_nodes, "pods_per_step": P, "batch": args.batch, "parallelism": f"node-shard x{world}",
                 "level_list_cap": 2048,
+                "node_sampling": None if args.sample_pct is None else {
+                    "percentage_of_nodes_to_score": args.sample_pct,
+                    "num_feasible_nodes_to_find": int(abi.load().gs_num_feasible_nodes_to_find(n_nodes, args.sample_pct)),
+                    "note": "findNodesThatPassFilters rotation window (parallelism-1 order); every node is still "
+                            "evaluated by the eval pass, value counts pods x nodes"},
             },
             "roofline": {
                 "bound": "hbm",
