@@ -627,8 +627,9 @@ __global__ void __launch_bounds__(256) commit_kernel(CommitArgs a) {
 
   __shared__ uint32_t s_start;                         // nextStartNodeIndex (node sampling)
   __shared__ int32_t s_wred[3][8];                     // window selection: block scans / reductions
-  __shared__ int32_t s_wend, s_wproc, s_wfound;
+  __shared__ int32_t s_wend, s_wproc, s_ndirty;       // s_ndirty: dirty slots (wave 0's nd, published)
   if (tid == 0) {
+    s_ndirty = 0;
     s_start = a.window_k ? (a.prev ? (uint32_t)a.prev[2] : a.start) : 0u;
     s_topo_id = -1;
     s_fk = a.forced_node >= 0 ? 0 : -1;
@@ -684,6 +685,7 @@ __global__ void __launch_bounds__(256) commit_kernel(CommitArgs a) {
         hval[h] = slot;
       }
       ++nd;
+      if (lane == 0) s_ndirty = nd;
       // one load per lane, all issued before a single wait (the per-lane source/destination map is built once)
       int64_t v = 0;
       if (f_kind == 1) v = reinterpret_cast<const int64_t*>(f_src)[winner];
@@ -725,25 +727,40 @@ __global__ void __launch_bounds__(256) commit_kernel(CommitArgs a) {
     return base + incl - v;
   };
   auto window_select = [&](int k) {
-    constexpr int WCH = 8;
+    // 16 positions per thread (4096 per pass): the first pass's verdicts stay in registers and the tie location
+    // reuses them when the window ends inside it (a window of K feasible nodes usually does)
+    constexpr int WCH = 16;
     const uint32_t N = a.nnodes, K = a.window_k, st0 = s_start;
     const int16_t* row = a.S + (size_t)k * a.ld;
-    auto verdict = [&](uint32_t i) -> int {   // score of position i for pod k (-1: infeasible)
-      uint32_t n = st0 + i;
-      if (n >= N) n -= N;
-      const int sl = hash_find(hkey, hval, n);
-      return sl >= 0 ? (int)dsc[k * B + sl] : (int)row[n - a.own0];
+    auto node_at = [&](uint32_t i) -> uint32_t {
+      const uint32_t n = st0 + i;
+      return n >= N ? n - N : n;
     };
-    if (tid == 0) { s_wend = (int)N - 1; s_wproc = (int)N; }
-    int found = 0, lmax = -1, lcnt = 0;
-    for (uint32_t base = 0; base < N; base += 256 * WCH) {
-      int v[WCH], c = 0;
+    auto load_pass = [&](uint32_t base, int* v) {   // all S loads issued before the dirty-row probes
 #pragma unroll
       for (int j = 0; j < WCH; ++j) {
         const uint32_t i = base + (uint32_t)tid * WCH + j;
-        v[j] = i < N ? verdict(i) : -1;
-        c += v[j] >= 0 ? 1 : 0;
+        v[j] = i < N ? (int)row[node_at(i) - a.own0] : -1;
       }
+      if (s_ndirty > 0) {
+#pragma unroll
+        for (int j = 0; j < WCH; ++j) {
+          const uint32_t i = base + (uint32_t)tid * WCH + j;
+          if (i >= N) continue;
+          const int sl = hash_find(hkey, hval, node_at(i));
+          if (sl >= 0) v[j] = (int)dsc[k * B + sl];
+        }
+      }
+    };
+    if (tid == 0) { s_wend = (int)N - 1; s_wproc = (int)N; }
+    int found = 0, lmax = -1, lcnt = 0, v[WCH];
+    uint32_t passes = 0;
+    for (uint32_t base = 0; base < N; base += 256 * WCH) {
+      load_pass(base, v);
+      ++passes;
+      int c = 0;
+#pragma unroll
+      for (int j = 0; j < WCH; ++j) c += v[j] >= 0 ? 1 : 0;
       int total = 0;
       int idx = found + block_scan(c, 0, &total);   // window index of this thread's first feasible position
 #pragma unroll
@@ -768,7 +785,6 @@ __global__ void __launch_bounds__(256) commit_kernel(CommitArgs a) {
     __syncthreads();
     const int M = max(max(s_wred[1][0], s_wred[1][1]), max(s_wred[1][2], s_wred[1][3]));
     const int tl = wave_sum(lmax == M ? lcnt : 0);
-    __syncthreads();
     if (lane == 0) s_wred[2][wave] = tl;
     __syncthreads();
     const int64_t T = (int64_t)s_wred[2][0] + s_wred[2][1] + s_wred[2][2] + s_wred[2][3];
@@ -783,28 +799,26 @@ __global__ void __launch_bounds__(256) commit_kernel(CommitArgs a) {
       __syncthreads();
       return;
     }
-    // the jp-th tie at M in window order
+    // the jp-th tie at M in window order (registers hold the single pass when the window ended inside it)
     const int64_t jp = tiebreak_position(a.seed, a.seq[k], T);
     int64_t before = 0;
     if (tid == 0) s_fnode = -1;
     for (uint32_t base = 0; base <= wend; base += 256 * WCH) {
+      if (passes > 1) load_pass(base, v);
       int c = 0;
 #pragma unroll
       for (int j = 0; j < WCH; ++j) {
         const uint32_t i = base + (uint32_t)tid * WCH + j;
-        c += (i <= wend && verdict(i) == M) ? 1 : 0;
+        c += (i <= wend && v[j] == M) ? 1 : 0;
       }
       int total = 0;
       const int64_t ex = before + block_scan(c, 0, &total);
       if (c > 0 && jp > ex && jp <= ex + c) {
         int64_t need = jp - ex;
+#pragma unroll
         for (int j = 0; j < WCH; ++j) {
           const uint32_t i = base + (uint32_t)tid * WCH + j;
-          if (i <= wend && verdict(i) == M && --need == 0) {
-            uint32_t n = st0 + i;
-            s_fnode = (int)(n >= N ? n - N : n);
-            break;
-          }
+          if (i <= wend && v[j] == M && --need == 0) s_fnode = (int)node_at(i);
         }
       }
       before += total;

@@ -84,3 +84,18 @@ def test_sampling_refuses_several_ranks():
     from koordinator_amd.engine import GpuScoreError
     with pytest.raises(GpuScoreError, match="one GPU"):
         e.comm_init_callback(2, 0, lambda send: [send, send])
+
+
+@pytest.mark.parametrize("kind", ["homogeneous", "loaded"])
+def test_sampling_window_spans_several_passes(kind):
+    """Windows longer than one 4096-position pass of the commit kernel: the scan continues across passes and the
+    tie location re-reads them."""
+    if kind == "homogeneous":
+        c = homogeneous_cluster(10_000, 120, 16)
+        e, o = sampling_pair(c, 50)   # K = 5000 feasible of 10000: every window spans two passes
+    else:
+        c = loaded_cluster(12_000, 240, 17)
+        e, o = sampling_pair(c, 30)   # K = 3600, sparse feasibility for the 60-core pods
+    got = check(e, o, c.pods)
+    assert got["feasible"].max() > 4096 or (got["feasible"] < 3600).any()
+    assert e.mirror_check() == 0
