@@ -99,3 +99,21 @@ def test_sampling_window_spans_several_passes(kind):
     got = check(e, o, c.pods)
     assert got["feasible"].max() > 4096 or (got["feasible"] < 3600).any()
     assert e.mirror_check() == 0
+
+
+def test_sampling_special_pods_and_host_cuts():
+    """Node sampling with pods that run in a batch of their own (UID in an assign cache, a PodMetric carrying the
+    pod's name, DaemonSet / terminated pods) and with batches cut for a host-side cpuset Reserve (topologies
+    outside the device scope): the start index survives every kind of batch boundary."""
+    c = synth.make_cluster(1500, 300, 18)
+    synth.make_numa(c, numa_policy_pct=40, cpuset_pod_pct=60, mixed=True)
+    pods = c.pods.copy()
+    pods["flags"][5] |= abi.GS_POD_DAEMONSET
+    pods["flags"][6] |= abi.GS_POD_TERMINATED
+    pods["uid"][7] = c.assigned_pods["uid"][0]
+    pods["name_key"][8] = c.pod_metrics["name_key"][0]
+    e, o = sampling_pair(c, 0, enabled=abi.GS_ENABLE_ALL, batch_size=64)
+    check(e, o, pods[:180])
+    check(e, o, pods[180:], 180)
+    assert e.stats()["cuts"] > 0, "no host-side cut exercised"
+    assert e.mirror_check() == 0
