@@ -427,6 +427,36 @@ int gs_comm_init_rccl(gs_ctx* ctx, const uint8_t id[128], int nranks, int rank);
 /* Caller-supplied transport (host buffers): */
 int gs_comm_init_callback(gs_ctx* ctx, int nranks, int rank, gs_allgather_fn fn, void* user);
 
+/* ---- ingest decoders: the annotation / label text the plugins parse per call in the
+ * reference, decoded once on the host into the ABI structs above (pure host functions, no device call) ---- */
+typedef struct gs_kv { const char* key; const char* value; } gs_kv;   /* one map[string]string entry */
+
+/* [upstream] k8s.io/apimachinery@v0.24.15 resource.ParseQuantity -> Quantity.Value() and MilliValue() (both
+ * round up). GS_EINVAL: malformed; GS_EUNSUPPORTED: outside int64. */
+int gs_decode_quantity(const char* s, int64_t* value, int64_t* milli_value);
+/* cpuset.Parse (pkg/util/cpuset/cpuset.go:322-366): Linux CPU list -> bit words (CPU ids < GS_MAX_CPUS). */
+int gs_decode_cpuset(const char* s, uint64_t out[GS_CPU_WORDS]);
+/* Node annotations: node.koordinator.sh/raw-allocatable (GetNodeRawAllocatable,
+ * apis/extension/node_resource_amplification.go:113-125, as EstimateNode reads it: a malformed one is ignored,
+ * loadaware/estimator/default_estimator.go:110-129), scheduling.koordinator.sh/usage-thresholds
+ * (GetCustomUsageThresholds, apis/extension/load_aware.go:51-62; malformed = the args' thresholds,
+ * loadaware/helper.go:102-140), node.koordinator.sh/resource-amplification-ratio
+ * (GetNodeResourceAmplificationRatio, node_resource_amplification.go:61-73; malformed = the
+ * ErrInvalidCPUAmplificationRatio path, nodenumaresource/plugin.go:345-347). Fills the raw_allocatable* and
+ * custom_* fields of *node and (numa != NULL) the node amplification fields of *numa. */
+int gs_decode_node_annotations(const gs_kv* annotations, uint32_t n, gs_node* node, gs_node_numa* numa);
+/* Node labels + the NRT's kubelet CPU manager policy JSON and topology-manager policy (either may be NULL):
+ * GetNodeCPUBindPolicy (apis/extension/numa_aware.go:301-325), getNUMATopologyPolicy
+ * (nodenumaresource/util.go:52-58), GetNUMAAllocateStrategy (util.go:35-41) -> *numa. */
+int gs_decode_node_labels(const gs_kv* labels, uint32_t n, const char* kubelet_cpu_manager_policy,
+                          const char* kubelet_topology_policy, gs_node_numa* numa);
+/* Pod annotation scheduling.koordinator.sh/resource-spec (GetResourceSpec, numa_aware.go:191-202); NULL =
+ * absent. Fills the bind / exclusive policy fields of *pod. */
+int gs_decode_resource_spec(const char* json, gs_pod* pod);
+/* NRT annotation node.koordinator.sh/cpu-topology (GetCPUTopology, numa_aware.go:249-260) -> gs_cpu_topology
+ * (CoreID = socket<<16 | core, nodenumaresource/cpu_topology.go:45); NULL = an empty topology. */
+int gs_decode_cpu_topology(const char* json, gs_cpu_topology* out);
+
 int gs_get_stats(gs_ctx* ctx, gs_stats* out);
 int gs_reset_stats(gs_ctx* ctx);
 /* Blocks until all device work of ctx has completed. */

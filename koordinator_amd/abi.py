@@ -173,6 +173,10 @@ class GsStats(C.Structure):
     ]
 
 
+class GsKv(C.Structure):
+    _fields_ = [("key", C.c_char_p), ("value", C.c_char_p)]
+
+
 ALLGATHER_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t)
 
 # numpy dtypes with the exact C layout (for bulk construction of node/pod arrays)
@@ -230,6 +234,12 @@ SIGNATURES = {
     "gs_numa_allocation_get": (C.c_int, [P, u32, u64, C.POINTER(GsPodAllocation)]),
     "gs_numa_args_default": (None, [C.POINTER(GsNumaArgs)]),
     "gs_num_feasible_nodes_to_find": (u32, [u32, i32]),
+    "gs_decode_quantity": (C.c_int, [C.c_char_p, C.POINTER(i64), C.POINTER(i64)]),
+    "gs_decode_cpuset": (C.c_int, [C.c_char_p, C.POINTER(u64)]),
+    "gs_decode_node_annotations": (C.c_int, [C.POINTER(GsKv), u32, C.POINTER(GsNode), C.POINTER(GsNodeNuma)]),
+    "gs_decode_node_labels": (C.c_int, [C.POINTER(GsKv), u32, C.c_char_p, C.c_char_p, C.POINTER(GsNodeNuma)]),
+    "gs_decode_resource_spec": (C.c_int, [C.c_char_p, C.POINTER(GsPod)]),
+    "gs_decode_cpu_topology": (C.c_int, [C.c_char_p, C.POINTER(GsCpuTopology)]),
 }
 
 

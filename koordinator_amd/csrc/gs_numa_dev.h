@@ -358,9 +358,6 @@ __device__ __forceinline__ NumaOut numa_eval(const NumaRow& r, const PodVec& p, 
     const int km_kind = nil_hints ? 0 : (lm ? 1 : ((has_mem && tot_m_any) ? 2 : 0));
     const bool single = policy == GS_NUMA_POLICY_SINGLE_NUMA_NODE;
     const bool no_lists = kc_kind == 0 && km_kind == 0;   // empty map: one preferred any-numa hint
-    // a list as a sequence of entries: kind 1 = its set bits, kind 2 / absent = a single pseudo entry (bit 31)
-    const uint32_t seq0 = kc_kind == 1 ? lc : 0x80000000u;
-    const uint32_t seq1 = km_kind == 1 ? lm : 0x80000000u;
     const bool use0 = no_lists || kc_kind != 0, use1 = !no_lists && km_kind != 0;
     // mergeFilteredHints (policy.go:128-186) with filterSingleNumaHints for SingleNUMANode
     bool b_has = true, b_pref = false;
@@ -422,6 +419,7 @@ __device__ __forceinline__ NumaOut numa_eval(const NumaRow& r, const PodVec& p, 
         b_score = best_s;
         continue;
       }
+      // a list as a sequence of entries: kind 1 = its set bits, kind 2 / absent = a single pseudo entry (bit 31)
       const uint32_t set0 = kc_kind == 1 ? (pass == 0 ? pre0 : lc) : 0x80000000u;
       const uint32_t set1 = km_kind == 1 ? (pass == 0 ? pre1 : lm) : 0x80000000u;
       for (uint32_t r0 = set0; r0; r0 &= r0 - 1) {
