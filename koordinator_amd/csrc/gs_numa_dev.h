@@ -459,10 +459,14 @@ __device__ __forceinline__ NumaOut numa_eval(const NumaRow& r, const PodVec& p, 
       }
     }
     NP(2);
-    if (prof) {   // merge path counters: [6] fast, [7] preferred pass only, [8] full pass, [9] a wave lane ran a full pass
+    {   // diagnostics: merge path counters: [6] fast, [7] preferred pass only, [8] full pass, [9] a lane of the
+        // wave (among those here with this pair's lane) ran a full pass
       const bool full = !fast && !nil_hints && !b_pref_after0;
-      prof[fast ? 6 : (full ? 8 : 7)] += 1;
-      if (__ballot(full)) prof[9] += 1;
+      const bool wave_full = __ballot(full) != 0;
+      if (prof) {
+        prof[fast ? 6 : (full ? 8 : 7)] += 1;
+        if (wave_full) prof[9] += 1;
+      }
     }
     bool admit = true;
     if (single) {

@@ -214,3 +214,20 @@ def test_decoder_throughput_smoke():
     for _ in range(10_000):
         ingest.node_annotations(ann)
     assert time.perf_counter() - t0 < 5.0
+
+
+def test_quantity_matches_python_restatement():
+    """The C++ Quantity decoder against the independent exact-rational restatement in koordinator_amd.objects
+    (Decimal mantissa x suffix, ceil), on seeded random quantities across every suffix."""
+    from koordinator_amd import objects
+    rng = np.random.default_rng(5)
+    sufs = sorted(objects._SUFFIX)
+    for _ in range(3000):
+        whole = int(rng.integers(0, 10**6))
+        frac = "" if rng.random() < 0.5 else "." + str(int(rng.integers(0, 10**4))).rjust(int(rng.integers(1, 5)), "0")
+        text = f"{whole}{frac}{sufs[int(rng.integers(0, len(sufs)))]}"
+        want_v = objects._ceil(objects.parse_quantity(text))
+        want_mv = objects._ceil(objects.parse_quantity(text) * 1000)
+        if max(abs(want_v), abs(want_mv)) >= 2**63:
+            continue
+        assert ingest.quantity(text) == (want_v, want_mv), text
