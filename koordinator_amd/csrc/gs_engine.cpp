@@ -1052,8 +1052,8 @@ int gs_create(const gs_config* cfg, gs_ctx** out) {
       if ((e = hipEventCreate(&ev)) != hipSuccess) return bail("hipEventCreate", e);
   }
   if (getenv("GS_COMMIT_STAMPS") && getenv("GS_COMMIT_STAMPS")[0] == '1') {
-    if ((e = hipMalloc(&c->d_stamps, 8 * 24)) != hipSuccess) return bail("hipMalloc", e);
-    (void)hipMemset(c->d_stamps, 0, 192);
+    if ((e = hipMalloc(&c->d_stamps, 8 * 25)) != hipSuccess) return bail("hipMalloc", e);
+    (void)hipMemset(c->d_stamps, 0, 200);
   }
   if ((e = hipDeviceSynchronize()) != hipSuccess) return bail("hipDeviceSynchronize", e);
   // 96 B (LoadAware + Fit row), + 192 B NodeNUMAResource columns when enabled
@@ -1065,8 +1065,8 @@ int gs_create(const gs_config* cfg, gs_ctx** out) {
 int gs_destroy(gs_ctx* c) {
   if (!c) return GS_EINVAL;
   if (c->d_stamps) {
-    uint64_t st[24] = {};
-    if (hipMemcpy(st, c->d_stamps, 192, hipMemcpyDeviceToHost) == hipSuccess) {
+    uint64_t st[25] = {};
+    if (hipMemcpy(st, c->d_stamps, 200, hipMemcpyDeviceToHost) == hipSuccess) {
       uint64_t tot = 0;
       for (int i = 0; i < 12; ++i) tot += st[i];
       fprintf(stderr, "gpuscore commit phases (s_memtime ticks, %% of %llu):", (unsigned long long)tot);
@@ -1080,6 +1080,7 @@ int gs_destroy(gs_ctx* c) {
       fprintf(stderr, "  merge paths of those pairs: fast %llu, preferred pass %llu, full pass %llu, wave with a full pass %llu\n",
               (unsigned long long)st[20], (unsigned long long)st[21], (unsigned long long)st[22],
               (unsigned long long)st[23]);
+      fprintf(stderr, "  header staging (inside p0): %.1f%%\n", tot ? 100.0 * st[24] / tot : 0.0);
     }
     (void)hipFree(c->d_stamps);
   }

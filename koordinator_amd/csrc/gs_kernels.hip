@@ -573,7 +573,8 @@ __device__ __noinline__ bool cpuset_reserve(const TopoDev& t, CpuStateDev& cs, c
 template <bool ST>
 __global__ void __launch_bounds__(256) commit_kernel(CommitArgs a) {
   uint64_t st_acc[14] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-  uint64_t np_acc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};   // numa_eval segments of thread 128's policy-row rescoring (ST)
+  uint64_t np_acc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+  uint64_t st_stage = 0;                      // header staging cycles (inside p0)   // numa_eval segments of thread 128's policy-row rescoring (ST)
   uint64_t st_last = ST ? __builtin_amdgcn_s_memtime() : 0;
 #define STAMP(i)                                    \
   do {                                              \
@@ -834,6 +835,7 @@ __global__ void __launch_bounds__(256) commit_kernel(CommitArgs a) {
     __syncthreads();
   };
   for (int k = 0; k < B; ++k) {
+   const uint64_t t_stage0 = ST ? __builtin_amdgcn_s_memtime() : 0;
    if (k % HCH == 0 && !a.window_k) {
      for (int e = tid; e < HCH * nhl; e += 256) {
        int kk = e / nhl, l = e % nhl;
@@ -856,6 +858,7 @@ __global__ void __launch_bounds__(256) commit_kernel(CommitArgs a) {
        if (k + e < B) hs_seq[e] = a.seq[k + e];
      __syncthreads();
    }
+   if (ST) st_stage += __builtin_amdgcn_s_memtime() - t_stage0;   // header staging share of p0
    for (;;) {   // one pass; a second, forced one after an in-kernel full-row resolution
    if (a.window_k) {   // node sampling: findNodesThatPassFilters over the rotation window, then selectHost
      window_select(k);
@@ -1237,8 +1240,10 @@ __global__ void __launch_bounds__(256) commit_kernel(CommitArgs a) {
     a.committed[1] = (committed == B && !host_cut) ? 1 : 0;
     a.committed[2] = (int32_t)s_start;
   }
-  if (ST && tid == 0)
+  if (ST && tid == 0) {
     for (int i = 0; i < 12; ++i) a.stamps[i] += st_acc[i];
+    a.stamps[24] += st_stage;
+  }
   if (ST && tid == 128) {
     a.stamps[12] += st_acc[12];
     a.stamps[13] += st_acc[13];
