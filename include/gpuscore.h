@@ -457,6 +457,61 @@ int gs_decode_resource_spec(const char* json, gs_pod* pod);
  * (CoreID = socket<<16 | core, nodenumaresource/cpu_topology.go:45); NULL = an empty topology. */
 int gs_decode_cpu_topology(const char* json, gs_cpu_topology* out);
 
+/* ---- ElasticQuota admission: the per-pod quota gate in front of the node loop. A host
+ * function over the quota forest, not a device kernel: it reads O(depth) groups per pod, nothing per node.
+ * Quantities per resource dimension d < GS_QUOTA_DIMS in getQuantityValue units
+ * (elasticquota/core/runtime_quota_calculator.go:500-505: cpu in milli, everything else Value()); the caller
+ * fixes the dimension -> resource-name map. A *_mask bit d says resource d is a key of that ResourceList. ---- */
+#define GS_QUOTA_DIMS 8
+typedef struct gs_quota_group {
+  int32_t parent;            /* index of the parent group; -1 = a child of the root quota (ParentName == root) */
+  uint32_t allow_lent;       /* QuotaInfo.AllowLentResource */
+  uint32_t max_mask;         /* keys of CalculateInfo.Max */
+  uint32_t min_mask;         /* keys of CalculateInfo.Min (= AutoScaleMin: scale-min-quota is not restated) */
+  int64_t max[GS_QUOTA_DIMS];
+  int64_t min[GS_QUOTA_DIMS];
+  int64_t guaranteed[GS_QUOTA_DIMS];     /* CalculateInfo.Guaranteed (0 unless ElasticQuotaGuaranteeUsage) */
+  int64_t shared_weight[GS_QUOTA_DIMS];  /* CalculateInfo.SharedWeight (defaults to Max, quota_info.go) */
+  int64_t request[GS_QUOTA_DIMS];        /* sum of the requests of the pods charged to this quota itself */
+  int64_t used[GS_QUOTA_DIMS];           /* CalculateInfo.Used (this quota and, for a parent, its subtree) */
+  int64_t non_preemptible_used[GS_QUOTA_DIMS];
+} gs_quota_group;
+
+/* quotaTree.redistribution + iterationForRedistribution (runtime_quota_calculator.go:106-166): one resource
+ * dimension of one parent's children. request = the children's limited requests. runtime[i] out. */
+int gs_quota_redistribute(const int64_t* request, const int64_t* min, const int64_t* guaranteed,
+                          const int64_t* shared_weight, const uint8_t* allow_lent, uint32_t n, int64_t total,
+                          int64_t* runtime);
+/* GroupQuotaManager.refreshRuntimeNoLock (group_quota_manager.go:264-321) for every group at once, from a settled
+ * request tree: Request = ChildRequest (own + the children's limited requests), floored at Min when lending is
+ * off (recursiveUpdateGroupTreeWithDeltaRequest, :184-224); limited request = min(Request, Max) on Max's keys
+ * (quota_info.go:201-212); each parent's children share the parent's runtime (root: total = cluster total
+ * except system/default used) per dimension of the union of all Max keys (updateResourceKeyNoLock, :558-576).
+ * runtime and limit_request (either may be NULL) are n x GS_QUOTA_DIMS; runtime_mask (n entries, may be NULL)
+ * = the keys of each group's Runtime (that union).
+ * GS_EINVAL on a parent index out of range or a cycle. */
+int gs_quota_refresh_runtime(const gs_quota_group* groups, uint32_t n, const int64_t total[GS_QUOTA_DIMS],
+                             int64_t* runtime, int64_t* limit_request, uint32_t* runtime_mask);
+
+#define GS_QUOTA_RUNTIME 1u          /* ElasticQuotaArgs.EnableRuntimeQuota: the limit is Runtime, else Max */
+#define GS_QUOTA_CHECK_PARENT 2u     /* ElasticQuotaArgs.EnableCheckParentQuota */
+#define GS_QUOTA_NON_PREEMPTIBLE 4u  /* extension.IsPodNonPreemptible(pod) */
+#define GS_QUOTA_ADMIT 0
+#define GS_QUOTA_INSUFFICIENT 1                 /* "Insufficient quotas, ..." (Unschedulable) */
+#define GS_QUOTA_INSUFFICIENT_NON_PREEMPTIBLE 2 /* "Insufficient non-preemptible quotas, ..." (Unschedulable) */
+typedef struct gs_quota_status {
+  int32_t code;        /* GS_QUOTA_ADMIT / _INSUFFICIENT / _INSUFFICIENT_NON_PREEMPTIBLE */
+  int32_t group;       /* the group whose check failed (a parent when the recursive check failed), else -1 */
+  uint32_t exceed_mask;/* exceedDimensions */
+  uint32_t depth;      /* parent hops above the pod's quota for a recursive failure (quotaNameTopo length - 1) */
+} gs_quota_status;
+/* Plugin.PreFilter (elasticquota/plugin.go:210-254) + checkQuotaRecursive (plugin_helper.go:281-297) for one
+ * pod of quota `quota` (-1: no quota label -> admit). runtime: n x GS_QUOTA_DIMS, group i's keys runtime_mask[i]
+ * (from gs_quota_refresh_runtime, or the caller's). pod_request: PodRequestsAndLimits, keys pod_request_mask. */
+int gs_quota_prefilter(const gs_quota_group* groups, uint32_t n, const int64_t* runtime, const uint32_t* runtime_mask,
+                       int32_t quota, const int64_t pod_request[GS_QUOTA_DIMS], uint32_t pod_request_mask,
+                       uint32_t flags, gs_quota_status* out);
+
 int gs_get_stats(gs_ctx* ctx, gs_stats* out);
 int gs_reset_stats(gs_ctx* ctx);
 /* Blocks until all device work of ctx has completed. */
@@ -470,7 +525,7 @@ int gs_debug_mirror_check(gs_ctx* ctx);
 int gs_debug_verify_cpuset(gs_ctx* ctx, int on);
 /* sizeof() of the ABI structs as compiled into the library, in this order: gs_pod, gs_node,
  * gs_node_metric, gs_pod_metric, gs_config, gs_placement, gs_stats, gs_loadaware_args, gs_cpu_topology,
- * gs_node_numa, gs_pod_allocation, gs_numa_args. */
+ * gs_node_numa, gs_pod_allocation, gs_numa_args, gs_quota_group, gs_quota_status. */
 void gs_abi_sizes(uint64_t* out, uint32_t n);
 
 #ifdef __cplusplus

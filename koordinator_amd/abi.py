@@ -177,6 +177,22 @@ class GsKv(C.Structure):
     _fields_ = [("key", C.c_char_p), ("value", C.c_char_p)]
 
 
+GS_QUOTA_DIMS = 8
+GS_QUOTA_RUNTIME, GS_QUOTA_CHECK_PARENT, GS_QUOTA_NON_PREEMPTIBLE = 1, 2, 4
+GS_QUOTA_ADMIT, GS_QUOTA_INSUFFICIENT, GS_QUOTA_INSUFFICIENT_NON_PREEMPTIBLE = 0, 1, 2
+
+
+class GsQuotaGroup(C.Structure):
+    _fields_ = [("parent", i32), ("allow_lent", u32), ("max_mask", u32), ("min_mask", u32),
+                ("max", i64 * GS_QUOTA_DIMS), ("min", i64 * GS_QUOTA_DIMS), ("guaranteed", i64 * GS_QUOTA_DIMS),
+                ("shared_weight", i64 * GS_QUOTA_DIMS), ("request", i64 * GS_QUOTA_DIMS),
+                ("used", i64 * GS_QUOTA_DIMS), ("non_preemptible_used", i64 * GS_QUOTA_DIMS)]
+
+
+class GsQuotaStatus(C.Structure):
+    _fields_ = [("code", i32), ("group", i32), ("exceed_mask", u32), ("depth", u32)]
+
+
 ALLGATHER_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t)
 
 # numpy dtypes with the exact C layout (for bulk construction of node/pod arrays)
@@ -195,7 +211,8 @@ STRUCT_SIZES = {
     "gs_placement": C.sizeof(GsPlacement), "gs_stats": C.sizeof(GsStats),
     "gs_loadaware_args": C.sizeof(GsLoadAwareArgs), "gs_cpu_topology": C.sizeof(GsCpuTopology),
     "gs_node_numa": C.sizeof(GsNodeNuma), "gs_pod_allocation": C.sizeof(GsPodAllocation),
-    "gs_numa_args": C.sizeof(GsNumaArgs),
+    "gs_numa_args": C.sizeof(GsNumaArgs), "gs_quota_group": C.sizeof(GsQuotaGroup),
+    "gs_quota_status": C.sizeof(GsQuotaStatus),
 }
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
@@ -240,6 +257,9 @@ SIGNATURES = {
     "gs_decode_node_labels": (C.c_int, [C.POINTER(GsKv), u32, C.c_char_p, C.c_char_p, C.POINTER(GsNodeNuma)]),
     "gs_decode_resource_spec": (C.c_int, [C.c_char_p, C.POINTER(GsPod)]),
     "gs_decode_cpu_topology": (C.c_int, [C.c_char_p, C.POINTER(GsCpuTopology)]),
+    "gs_quota_redistribute": (C.c_int, [P, P, P, P, P, u32, i64, P]),
+    "gs_quota_refresh_runtime": (C.c_int, [P, u32, P, P, P, P]),
+    "gs_quota_prefilter": (C.c_int, [P, u32, P, P, i32, P, u32, u32, C.POINTER(GsQuotaStatus)]),
 }
 
 

@@ -896,7 +896,8 @@ const char* gs_version(void) { return "libgpuscore 0.1 (gfx950, ABI 1)"; }
 void gs_abi_sizes(uint64_t* out, uint32_t n) {
   const uint64_t s[] = {sizeof(gs_pod), sizeof(gs_node), sizeof(gs_node_metric), sizeof(gs_pod_metric),
                         sizeof(gs_config), sizeof(gs_placement), sizeof(gs_stats), sizeof(gs_loadaware_args),
-                        sizeof(gs_cpu_topology), sizeof(gs_node_numa), sizeof(gs_pod_allocation), sizeof(gs_numa_args)};
+                        sizeof(gs_cpu_topology), sizeof(gs_node_numa), sizeof(gs_pod_allocation), sizeof(gs_numa_args),
+                        sizeof(gs_quota_group), sizeof(gs_quota_status)};
   for (uint32_t i = 0; i < n && i < sizeof(s) / sizeof(s[0]); ++i) out[i] = s[i];
 }
 

@@ -1,0 +1,219 @@
+// gs_quota.cpp — ElasticQuota admission: the per-pod quota gate that runs in PreFilter,
+// before the node loop. It reads the quota forest (O(depth) groups per pod, nothing per node), so it is host
+// code next to the engine, not a device kernel. Restates:
+//   * quotaTree.redistribution / iterationForRedistribution (elasticquota/core/runtime_quota_calculator.go:106-166)
+//     — the min-then-shared-weight water filling of one parent's runtime over its children, per dimension;
+//   * the request tree (group_quota_manager.go:184-224 recursiveUpdateGroupTreeWithDeltaRequest, quota_info.go:
+//     201-212 getLimitRequestNoLock) and the top-down runtime refresh (group_quota_manager.go:264-321), computed
+//     for every group at once from a settled tree;
+//   * Plugin.PreFilter (plugin.go:210-254) and checkQuotaRecursive (plugin_helper.go:281-297).
+#include <algorithm>
+#include <cstdint>
+#include <cstring>
+#include <vector>
+
+#include "../../include/gpuscore.h"
+
+namespace {
+
+constexpr int D = GS_QUOTA_DIMS;
+
+// iterationForRedistribution (runtime_quota_calculator.go:140-166), as a loop instead of tail recursion. Each
+// node's share depends only on (totalRes, totalSharedWeight), so the Go map's iteration order cannot change the
+// result; the share is int64(float64(w)*float64(total)/float64(totalW) + 0.5) — the same three IEEE double
+// operations, truncated toward zero like Go's conversion.
+void iterate(int64_t total, int64_t total_w, std::vector<uint32_t> nodes, const int64_t* request,
+             const int64_t* weight, int64_t* rt) {
+  std::vector<uint32_t> next;
+  while (total_w > 0) {
+    next.clear();
+    int64_t part = 0, next_w = 0;
+    for (uint32_t i : nodes) {
+      const int64_t delta = (int64_t)((double)weight[i] * (double)total / (double)total_w + 0.5);
+      rt[i] += delta;
+      if (rt[i] < request[i]) {
+        next.push_back(i);
+        next_w += weight[i];
+      } else {
+        part += rt[i] - request[i];
+        rt[i] = request[i];
+      }
+    }
+    if (part <= 0 || next.empty()) return;
+    total = part;
+    total_w = next_w;
+    nodes.swap(next);
+  }
+}
+
+// quotaTree.redistribution (runtime_quota_calculator.go:106-138).
+void redistribute(uint32_t n, const int64_t* request, const int64_t* min, const int64_t* guaranteed,
+                  const int64_t* weight, const uint8_t* lent, int64_t total, int64_t* rt) {
+  int64_t to_part = total, total_w = 0;
+  std::vector<uint32_t> adjust;
+  for (uint32_t i = 0; i < n; ++i) {
+    const int64_t m = guaranteed[i] > min[i] ? guaranteed[i] : min[i];   // guarantee above min replaces it
+    if (request[i] > m) {
+      adjust.push_back(i);
+      total_w += weight[i];
+      rt[i] = m;
+    } else {
+      rt[i] = lent[i] ? request[i] : m;   // a quota that does not lend keeps its min
+    }
+    to_part -= rt[i];
+  }
+  if (to_part > 0) iterate(to_part, total_w, std::move(adjust), request, weight, rt);
+}
+
+// depth of every group (root's children: 0); -1 on a bad parent index or a cycle.
+bool depths(const gs_quota_group* g, uint32_t n, std::vector<uint32_t>& depth) {
+  depth.assign(n, 0);
+  for (uint32_t i = 0; i < n; ++i) {
+    uint32_t d = 0;
+    for (int32_t p = g[i].parent; p >= 0; p = g[p].parent) {
+      if ((uint32_t)p >= n || ++d > n) return false;
+    }
+    if (g[i].parent < -1) return false;
+    depth[i] = d;
+  }
+  return true;
+}
+
+// quotav1.LessThanOrEqual(Mask(Add(podRequest, used), names(podRequest)), limit): only keys of the limit that the
+// pod requests are compared (a key missing from `used` is zero). Returns the exceeding dimensions.
+uint32_t exceeds(const int64_t* used, const int64_t* req, uint32_t req_mask, const int64_t* limit,
+                 uint32_t limit_mask) {
+  uint32_t m = 0;
+  for (int d = 0; d < D; ++d)
+    if ((limit_mask >> d & 1u) && (req_mask >> d & 1u) && used[d] + req[d] > limit[d]) m |= 1u << d;
+  return m;
+}
+
+}  // namespace
+
+extern "C" int gs_quota_redistribute(const int64_t* request, const int64_t* min, const int64_t* guaranteed,
+                                     const int64_t* shared_weight, const uint8_t* allow_lent, uint32_t n,
+                                     int64_t total, int64_t* runtime) {
+  if (n == 0) return GS_OK;
+  if (!request || !min || !guaranteed || !shared_weight || !allow_lent || !runtime) return GS_EINVAL;
+  redistribute(n, request, min, guaranteed, shared_weight, allow_lent, total, runtime);
+  return GS_OK;
+}
+
+extern "C" int gs_quota_refresh_runtime(const gs_quota_group* g, uint32_t n, const int64_t total[GS_QUOTA_DIMS],
+                                        int64_t* runtime, int64_t* limit_request, uint32_t* runtime_mask) {
+  if (n && (!g || !total)) return GS_EINVAL;
+  std::vector<uint32_t> depth;
+  if (!depths(g, n, depth)) return GS_EINVAL;
+  uint32_t keys = 0;   // updateResourceKeyNoLock: the union of every quota's Max keys
+  for (uint32_t i = 0; i < n; ++i) keys |= g[i].max_mask;
+  keys &= (1u << D) - 1;
+  if (runtime_mask)
+    for (uint32_t i = 0; i < n; ++i) runtime_mask[i] = keys;
+
+  std::vector<uint32_t> order(n);
+  for (uint32_t i = 0; i < n; ++i) order[i] = i;
+  std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return depth[a] > depth[b]; });
+
+  // bottom-up: ChildRequest = own pods + the children's limited requests; Request = ChildRequest, raised to Min
+  // when the quota does not lend; limited request = min(Request, Max) on Max's keys.
+  std::vector<int64_t> child(size_t(n) * D), limit(size_t(n) * D);
+  for (uint32_t i = 0; i < n; ++i)
+    for (int d = 0; d < D; ++d) child[size_t(i) * D + d] = g[i].request[d];
+  for (uint32_t i : order) {
+    for (int d = 0; d < D; ++d) {
+      int64_t r = child[size_t(i) * D + d];
+      if (r < 0) r = 0;   // addChildRequestNonNegativeNoLock
+      if (!g[i].allow_lent && (g[i].min_mask >> d & 1u) && g[i].min[d] > r) r = g[i].min[d];
+      if ((g[i].max_mask >> d & 1u) && r > g[i].max[d]) r = g[i].max[d];
+      limit[size_t(i) * D + d] = r;
+      if (g[i].parent >= 0) child[size_t(g[i].parent) * D + d] += r;
+    }
+  }
+
+  // top-down: each parent's runtime (the root's: total) is redistributed over its children, per key.
+  std::vector<int64_t> rt(size_t(n) * D, 0);
+  std::vector<std::vector<uint32_t>> kids(n + 1);   // kids[n] = children of the root
+  for (uint32_t i = 0; i < n; ++i) kids[g[i].parent < 0 ? n : (uint32_t)g[i].parent].push_back(i);
+  std::vector<uint32_t> parents;
+  parents.push_back(n);
+  for (uint32_t k = n; k-- > 0;) parents.push_back(order[k]);   // ascending depth: parents before children
+  std::vector<int64_t> req, mn, gu, w, out;
+  std::vector<uint8_t> lent;
+  for (uint32_t p : parents) {
+    const auto& ch = kids[p];
+    if (ch.empty()) continue;
+    const size_t m = ch.size();
+    req.resize(m); mn.resize(m); gu.resize(m); w.resize(m); lent.resize(m); out.resize(m);
+    for (int d = 0; d < D; ++d) {
+      if (!(keys >> d & 1u)) continue;
+      for (size_t j = 0; j < m; ++j) {
+        const gs_quota_group& c = g[ch[j]];
+        req[j] = limit[size_t(ch[j]) * D + d];
+        mn[j] = (c.min_mask >> d & 1u) ? c.min[d] : 0;
+        gu[j] = c.guaranteed[d];
+        w[j] = c.shared_weight[d];
+        lent[j] = c.allow_lent ? 1 : 0;
+      }
+      const int64_t tot = p == n ? total[d] : rt[size_t(p) * D + d];
+      redistribute((uint32_t)m, req.data(), mn.data(), gu.data(), w.data(), lent.data(), tot, out.data());
+      for (size_t j = 0; j < m; ++j) rt[size_t(ch[j]) * D + d] = out[j];
+    }
+  }
+  if (runtime) std::memcpy(runtime, rt.data(), rt.size() * sizeof(int64_t));
+  if (limit_request) std::memcpy(limit_request, limit.data(), limit.size() * sizeof(int64_t));
+  return GS_OK;
+}
+
+extern "C" int gs_quota_prefilter(const gs_quota_group* g, uint32_t n, const int64_t* runtime,
+                                  const uint32_t* runtime_mask, int32_t quota, const int64_t pod_request[GS_QUOTA_DIMS],
+                                  uint32_t pod_request_mask, uint32_t flags, gs_quota_status* out) {
+  if (!out) return GS_EINVAL;
+  out->code = GS_QUOTA_ADMIT;
+  out->group = -1;
+  out->exceed_mask = 0;
+  out->depth = 0;
+  if (quota < 0) return GS_OK;   // no quota label: PreFilter skips (plugin.go:211-215)
+  if ((uint32_t)quota >= n || !g || !pod_request) return GS_EINVAL;
+  const bool use_runtime = flags & GS_QUOTA_RUNTIME;
+  if (use_runtime && (!runtime || !runtime_mask)) return GS_EINVAL;
+  std::vector<uint32_t> depth;
+  if (!depths(g, n, depth)) return GS_EINVAL;
+
+  // getQuotaInfoUsedLimit (plugin_helper.go:314-319): Runtime when runtime quota is on, else Max
+  auto check = [&](uint32_t q) {
+    return use_runtime ? exceeds(g[q].used, pod_request, pod_request_mask, runtime + size_t(q) * D,
+                                   runtime_mask[q])
+                       : exceeds(g[q].used, pod_request, pod_request_mask, g[q].max, g[q].max_mask);
+  };
+  uint32_t m = check((uint32_t)quota);
+  if (m) {
+    out->code = GS_QUOTA_INSUFFICIENT;
+    out->group = quota;
+    out->exceed_mask = m;
+    return GS_OK;
+  }
+  if (flags & GS_QUOTA_NON_PREEMPTIBLE) {   // nonPreemptibleUsed + request within Min (plugin.go:235-244)
+    m = exceeds(g[quota].non_preemptible_used, pod_request, pod_request_mask, g[quota].min, g[quota].min_mask);
+    if (m) {
+      out->code = GS_QUOTA_INSUFFICIENT_NON_PREEMPTIBLE;
+      out->group = quota;
+      out->exceed_mask = m;
+      return GS_OK;
+    }
+  }
+  if (flags & GS_QUOTA_CHECK_PARENT) {   // checkQuotaRecursive: this quota, then every ancestor below the root
+    uint32_t hops = 0;
+    for (int32_t q = quota; q >= 0; q = g[q].parent, ++hops) {
+      m = check((uint32_t)q);
+      if (m) {
+        out->code = GS_QUOTA_INSUFFICIENT;
+        out->group = q;
+        out->exceed_mask = m;
+        out->depth = hops;
+        return GS_OK;
+      }
+    }
+  }
+  return GS_OK;
+}

@@ -1,0 +1,208 @@
+"""ElasticQuota admission, host mirror of the reference plugin's PreFilter gate over libgpuscore's gs_quota_*.
+
+Mirrors elasticquota/plugin.go:210-254 (PreFilter), plugin_helper.go:281-319 (checkQuotaRecursive,
+getQuotaInfoUsedLimit) and the GroupQuotaManager state it reads (core/group_quota_manager.go): quotas form a forest
+under the root quota; pods add request to their quota (and used once assigned, to it and every ancestor); the
+runtime of every quota is refreshed from the cluster total through the C++ water filling
+(core/runtime_quota_calculator.go:106-166). ResourceLists are {name: int} in getQuantityValue units (cpu milli,
+everything else Value()). Status messages follow the reference's text; Quantity.String() is rendered for the
+integral cpu / byte values the scheduler carries (cpu "Nm" or whole cores, other resources as integers).
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass, field
+
+import numpy as np
+
+from . import abi
+
+ROOT = "koordinator-root-quota"   # extension.RootQuotaName
+DEFAULT_RESOURCES = ("cpu", "memory", "nvidia.com/gpu", "ephemeral-storage",
+                     "kubernetes.io/batch-cpu", "kubernetes.io/batch-memory", "pods", "koordinator.sh/gpu")
+
+
+@dataclass
+class Status:
+    code: str                 # "Success" | "Unschedulable"
+    message: str = ""
+    quota: str | None = None  # the quota whose check failed
+    exceed: list = field(default_factory=list)
+
+    def is_success(self) -> bool:
+        return self.code == "Success"
+
+
+def _fmt_quantity(name: str, v: int) -> str:
+    if name == "cpu":
+        return str(v // 1000) if v % 1000 == 0 else f"{v}m"
+    return str(v)
+
+
+def print_resource_list(rl: dict) -> str:
+    """printResourceList (plugin_helper.go:299-312): "name:quantity" sorted, "<empty>" when empty."""
+    if not rl:
+        return "<empty>"
+    return ",".join(sorted(f"{k}:{_fmt_quantity(k, v)}" for k, v in rl.items()))
+
+
+class ElasticQuotaPlugin:
+    def __init__(self, resources=DEFAULT_RESOURCES, enable_runtime_quota=True, enable_check_parent_quota=False,
+                 lib=None):
+        if len(resources) > abi.GS_QUOTA_DIMS:
+            raise ValueError(f"at most {abi.GS_QUOTA_DIMS} resource dimensions")
+        self.lib = lib or abi.load()
+        self.resources = list(resources)
+        self.dim = {r: i for i, r in enumerate(self.resources)}
+        self.enable_runtime_quota = enable_runtime_quota
+        self.enable_check_parent_quota = enable_check_parent_quota
+        self.total: dict = {}
+        self.names: list[str] = []
+        self.index: dict[str, int] = {}
+        self.groups: list[abi.GsQuotaGroup] = []
+        self.parent_names: list[str] = []
+        self.runtime = np.zeros((0, abi.GS_QUOTA_DIMS), np.int64)
+        self.runtime_mask = np.zeros(0, np.uint32)
+
+    # ---- ResourceList <-> dense dimensions ----
+    def _dense(self, rl: dict | None) -> tuple[np.ndarray, int]:
+        out, mask = np.zeros(abi.GS_QUOTA_DIMS, np.int64), 0
+        for k, v in (rl or {}).items():
+            if k not in self.dim:
+                raise KeyError(f"resource {k!r} has no quota dimension (configured: {self.resources})")
+            out[self.dim[k]] = int(v)
+            mask |= 1 << self.dim[k]
+        return out, mask
+
+    def _sparse(self, vals, mask: int) -> dict:
+        return {r: int(vals[d]) for r, d in self.dim.items() if mask >> d & 1}
+
+    # ---- GroupQuotaManager updates ----
+    def update_cluster_total_resource(self, total: dict):
+        """UpdateClusterTotalResource; here already net of the system / default quotas' used."""
+        self.total = dict(total)
+
+    def on_quota_add(self, name, parent=ROOT, max=None, min=None, shared_weight=None, allow_lent=True,
+                     guaranteed=None):
+        """OnQuotaAdd -> NewQuotaInfoFromQuota: SharedWeight defaults to Max."""
+        if name in self.index:
+            raise ValueError(f"quota {name!r} exists")
+        g = abi.GsQuotaGroup()
+        g.allow_lent = 1 if allow_lent else 0
+        for fld, rl in (("max", max), ("min", min), ("shared_weight", max if shared_weight is None else shared_weight),
+                        ("guaranteed", guaranteed)):
+            vals, mask = self._dense(rl)
+            getattr(g, fld)[:] = vals.tolist()
+            if fld in ("max", "min"):
+                setattr(g, fld + "_mask", mask)
+        self.index[name] = len(self.names)
+        self.names.append(name)
+        self.parent_names.append(parent)
+        self.groups.append(g)
+
+    def _chain(self, quota: str):
+        name = quota
+        while name != ROOT:
+            yield self.groups[self.index[name]]
+            name = self.parent_names[self.index[name]]
+
+    def on_pod_add(self, quota: str, request: dict, assigned: bool, non_preemptible: bool = False):
+        """OnPodAdd: the pod's request joins its quota's request; once assigned, its used (and, for a
+        non-preemptible pod, non-preemptible used) joins the quota and every ancestor."""
+        vals, _ = self._dense(request)
+        g = self.groups[self.index[quota]]
+        for d in range(abi.GS_QUOTA_DIMS):
+            g.request[d] += int(vals[d])
+        if assigned:
+            for a in self._chain(quota):
+                for d in range(abi.GS_QUOTA_DIMS):
+                    a.used[d] += int(vals[d])
+                    if non_preemptible:
+                        a.non_preemptible_used[d] += int(vals[d])
+
+    def _array(self):
+        for i, p in enumerate(self.parent_names):
+            self.groups[i].parent = -1 if p == ROOT else self.index[p]
+        arr = (abi.GsQuotaGroup * max(1, len(self.groups)))(*self.groups)
+        return arr
+
+    def refresh_runtime(self) -> dict:
+        """RefreshRuntime for every quota; returns {quota: runtime ResourceList}."""
+        n = len(self.groups)
+        arr = self._array()
+        total, _ = self._dense(self.total)
+        self.runtime = np.zeros((max(n, 1), abi.GS_QUOTA_DIMS), np.int64)
+        self.runtime_mask = np.zeros(max(n, 1), np.uint32)
+        rc = self.lib.gs_quota_refresh_runtime(arr, n, abi.ptr(total), abi.ptr(self.runtime), None,
+                                               abi.ptr(self.runtime_mask))
+        if rc != 0:
+            raise RuntimeError(f"gs_quota_refresh_runtime: {rc}")
+        return {name: self._sparse(self.runtime[i], int(self.runtime_mask[i])) for i, name in enumerate(self.names)}
+
+    def set_runtime(self, quota: str, runtime: dict):
+        """What the reference's tests do with qi.CalculateInfo.Runtime = ... (plugin_test.go:686-689)."""
+        self._ensure_runtime()
+        vals, mask = self._dense(runtime)
+        i = self.index[quota]
+        self.runtime[i] = vals
+        self.runtime_mask[i] = mask
+
+    def _ensure_runtime(self):
+        n = len(self.groups)
+        if self.runtime.shape[0] < n:   # quotas added since the last refresh: no Runtime keys yet
+            rt = np.zeros((n, abi.GS_QUOTA_DIMS), np.int64)
+            rt[:self.runtime.shape[0]] = self.runtime
+            rm = np.zeros(n, np.uint32)
+            rm[:self.runtime_mask.shape[0]] = self.runtime_mask
+            self.runtime, self.runtime_mask = rt, rm
+
+    def get(self, quota: str, what: str) -> dict:
+        g = self.groups[self.index[quota]]
+        mask = {"max": g.max_mask, "min": g.min_mask}.get(what, (1 << abi.GS_QUOTA_DIMS) - 1)
+        vals = list(getattr(g, what))
+        rl = self._sparse(vals, mask)
+        return rl if what in ("max", "min") else {k: v for k, v in rl.items() if v}
+
+    # ---- PreFilter ----
+    def pre_filter(self, quota: str | None, request: dict, non_preemptible: bool = False) -> Status:
+        if not quota:
+            return Status("Success")
+        if quota not in self.index:
+            return Status("Error", f"Could not find the specified ElasticQuota")
+        req, req_mask = self._dense(request)
+        flags = ((abi.GS_QUOTA_RUNTIME if self.enable_runtime_quota else 0)
+                 | (abi.GS_QUOTA_CHECK_PARENT if self.enable_check_parent_quota else 0)
+                 | (abi.GS_QUOTA_NON_PREEMPTIBLE if non_preemptible else 0))
+        n = len(self.groups)
+        arr = self._array()
+        self._ensure_runtime()
+        st = abi.GsQuotaStatus()
+        rc = self.lib.gs_quota_prefilter(arr, n, abi.ptr(self.runtime), abi.ptr(self.runtime_mask),
+                                         self.index[quota], abi.ptr(req), req_mask, flags, C.byref(st))
+        if rc != 0:
+            raise RuntimeError(f"gs_quota_prefilter: {rc}")
+        if st.code == abi.GS_QUOTA_ADMIT:
+            return Status("Success")
+        failed = self.names[st.group]
+        exceed = [r for r, d in self.dim.items() if st.exceed_mask >> d & 1]
+        i = st.group
+        limit = (self._sparse(self.runtime[i], int(self.runtime_mask[i])) if self.enable_runtime_quota
+                 else self.get(failed, "max"))
+        if st.code == abi.GS_QUOTA_INSUFFICIENT_NON_PREEMPTIBLE:
+            msg = (f"Insufficient non-preemptible quotas, quotaName: {failed}, min: "
+                   f"{print_resource_list(self.get(failed, 'min'))}, nonPreemptibleUsed: "
+                   f"{print_resource_list(self.get(failed, 'non_preemptible_used'))}, pod's request: "
+                   f"{print_resource_list(request)}, exceedDimensions: [{' '.join(exceed)}]")
+        elif st.depth == 0:   # the pod's own quota (the first check of plugin.go:229-234)
+            msg = (f"Insufficient quotas, quotaName: {failed}, runtime: {print_resource_list(limit)}, used: "
+                   f"{print_resource_list(self.get(failed, 'used'))}, pod's request: {print_resource_list(request)}, "
+                   f"exceedDimensions: [{' '.join(exceed)}]")
+        else:
+            topo, name = [quota], quota
+            for _ in range(st.depth):
+                name = self.parent_names[self.index[name]]
+                topo.insert(0, name)
+            msg = (f"Insufficient quotas, quotaNameTopo: [{' '.join(topo)}], runtime: {print_resource_list(limit)}, "
+                   f"used: {print_resource_list(self.get(failed, 'used'))}, pod's request: "
+                   f"{print_resource_list(request)}, exceedDimensions: [{' '.join(exceed)}]")
+        return Status("Unschedulable", msg, failed, exceed)
