@@ -177,8 +177,10 @@ extern "C" int gs_quota_prefilter(const gs_quota_group* g, uint32_t n, const int
   if ((uint32_t)quota >= n || !g || !pod_request) return GS_EINVAL;
   const bool use_runtime = flags & GS_QUOTA_RUNTIME;
   if (use_runtime && (!runtime || !runtime_mask)) return GS_EINVAL;
-  std::vector<uint32_t> depth;
-  if (!depths(g, n, depth)) return GS_EINVAL;
+  // validate only this pod's ancestor chain (O(depth) per pod, not the forest)
+  uint32_t hops = 0;
+  for (int32_t p = g[quota].parent; p != -1; p = g[p].parent)
+    if (p < -1 || (uint32_t)p >= n || ++hops > n) return GS_EINVAL;
 
   // getQuotaInfoUsedLimit (plugin_helper.go:314-319): Runtime when runtime quota is on, else Max
   auto check = [&](uint32_t q) {
