@@ -206,3 +206,74 @@ class ElasticQuotaPlugin:
                    f"used: {print_resource_list(self.get(failed, 'used'))}, pod's request: "
                    f"{print_resource_list(request)}, exceedDimensions: [{' '.join(exceed)}]")
         return Status("Unschedulable", msg, failed, exceed)
+
+    # ---- Reserve / Unreserve (GroupQuotaManager.ReservePod / UnreservePod, group_quota_manager.go:791-805) ----
+    def reserve_pod(self, quota: str | None, request: dict, non_preemptible: bool = False, sign: int = 1):
+        """The pod's request joins `used` (and non-preemptible used) of its quota and every ancestor."""
+        if not quota:
+            return
+        vals, _ = self._dense(request)
+        for a in self._chain(quota):
+            for d in range(abi.GS_QUOTA_DIMS):
+                a.used[d] += sign * int(vals[d])
+                if non_preemptible:
+                    a.non_preemptible_used[d] += sign * int(vals[d])
+
+    def unreserve_pod(self, quota: str | None, request: dict, non_preemptible: bool = False):
+        self.reserve_pod(quota, request, non_preemptible, sign=-1)
+
+
+def schedule_with_quota(engine, plugin: ElasticQuotaPlugin, pods, pod_quota, seq=None):
+    """Quota-gated batched scheduleOne: per pod in order, ElasticQuota PreFilter, then (if admitted) the node
+    loop of `engine.schedule` (libgpuscore gs_schedule), then quota Reserve on a placement — the reference's
+    sequential order (PreFilter -> Filter/Score -> selectHost -> Reserve) kept exact while the node loop runs
+    in batches.
+
+    Admitted pods are reserved speculatively (as if placed) so that a run of admitted pods goes to the engine
+    as one batch. The check is monotone in `used` (used + request <= limit), so a pod admitted under
+    speculation stays admitted when an earlier pod of its batch finds no node and is unreserved; only a
+    rejection can depend on the speculation, and only when the batch holds a speculative Reserve on a quota of
+    the rejected pod's chain: then the batch is cut before that pod and it is re-checked once the batch's true
+    placements are reserved; otherwise the rejection is final. Runtime does not change inside a batch (it
+    follows requests, which a Reserve does not touch). pod_quota[i] = (quota name or None, request
+    ResourceList, non_preemptible). Returns (placements, statuses): placements in the engine's dtype with
+    node = -1 for quota-rejected pods, statuses[i] = the PreFilter Status of pod i."""
+    pods = np.ascontiguousarray(pods, dtype=abi.POD_DTYPE)
+    n = len(pods)
+    seq = np.arange(n, dtype=np.uint64) if seq is None else np.ascontiguousarray(seq, dtype=np.uint64)
+    out = np.zeros(n, abi.PLACEMENT_DTYPE)
+    out["node"] = -1
+    statuses: list[Status | None] = [None] * n
+    i = 0
+    chains: dict = {}
+
+    def chain(q):
+        if q not in chains:
+            chains[q] = {id(g) for g in plugin._chain(q)} if q else set()
+        return chains[q]
+
+    while i < n:
+        seg: list[int] = []
+        touched: set = set()               # quotas whose used holds a speculative Reserve of this batch
+        j = i
+        while j < n:
+            q, req, np_ = pod_quota[j]
+            st = plugin.pre_filter(q, req, np_)
+            if not st.is_success() and chain(q) & touched:
+                break                      # may depend on the speculation: re-check after the batch's placements
+            statuses[j] = st
+            if st.is_success():
+                plugin.reserve_pod(q, req, np_)
+                seg.append(j)
+                touched |= chain(q)
+            j += 1
+        if seg:
+            idx = np.array(seg)
+            res = engine.schedule(pods[idx], seq[idx])
+            out[idx] = res
+            for k, p in enumerate(seg):
+                if res["node"][k] < 0:     # no feasible node: the speculative Reserve never happened
+                    q, req, np_ = pod_quota[p]
+                    plugin.unreserve_pod(q, req, np_)
+        i = j
+    return out, statuses
