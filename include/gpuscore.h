@@ -512,6 +512,20 @@ int gs_quota_prefilter(const gs_quota_group* groups, uint32_t n, const int64_t* 
                        int32_t quota, const int64_t pod_request[GS_QUOTA_DIMS], uint32_t pod_request_mask,
                        uint32_t flags, gs_quota_status* out);
 
+/* GroupQuotaManager.ReservePod / UnreservePod (group_quota_manager.go:791-805): request joins (sign = +1) or
+ * leaves (-1) used — and, with GS_QUOTA_NON_PREEMPTIBLE in flags, non-preemptible used — of `quota` and every
+ * ancestor. */
+int gs_quota_reserve(gs_quota_group* groups, uint32_t n, int32_t quota, const int64_t request[GS_QUOTA_DIMS],
+                     uint32_t flags, int32_t sign);
+/* Quota-gated batch admission: gs_quota_prefilter per pod in order (pod j: quota[j], requests[j*GS_QUOTA_DIMS..],
+ * request_mask[j], flags[j]); each admitted pod is reserved speculatively; stops before the first rejected pod
+ * whose ancestor chain holds a speculative Reserve of this call (its verdict may change once a speculatively
+ * reserved pod finds no node and is unreserved; admission is monotone in used, so admitted verdicts stand).
+ * status[0..*consumed) = the decided pods' verdicts. */
+int gs_quota_admit_batch(gs_quota_group* groups, uint32_t n, const int64_t* runtime, const uint32_t* runtime_mask,
+                         const int32_t* quota, const int64_t* requests, const uint32_t* request_mask,
+                         const uint32_t* flags, uint32_t count, gs_quota_status* status, uint32_t* consumed);
+
 int gs_get_stats(gs_ctx* ctx, gs_stats* out);
 int gs_reset_stats(gs_ctx* ctx);
 /* Blocks until all device work of ctx has completed. */

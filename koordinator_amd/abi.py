@@ -260,6 +260,8 @@ SIGNATURES = {
     "gs_quota_redistribute": (C.c_int, [P, P, P, P, P, u32, i64, P]),
     "gs_quota_refresh_runtime": (C.c_int, [P, u32, P, P, P, P]),
     "gs_quota_prefilter": (C.c_int, [P, u32, P, P, i32, P, u32, u32, C.POINTER(GsQuotaStatus)]),
+    "gs_quota_reserve": (C.c_int, [P, u32, i32, P, u32, i32]),
+    "gs_quota_admit_batch": (C.c_int, [P, u32, P, P, P, P, P, P, u32, P, C.POINTER(u32)]),
 }
 
 

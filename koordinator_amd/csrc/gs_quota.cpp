@@ -219,3 +219,51 @@ extern "C" int gs_quota_prefilter(const gs_quota_group* g, uint32_t n, const int
   }
   return GS_OK;
 }
+
+// GroupQuotaManager.ReservePod / UnreservePod (group_quota_manager.go:791-805 -> updatePodUsedNoLock): the pod's
+// request joins (sign -1: leaves) used — and non-preemptible used — of its quota and every ancestor.
+extern "C" int gs_quota_reserve(gs_quota_group* g, uint32_t n, int32_t quota, const int64_t request[GS_QUOTA_DIMS],
+                                uint32_t flags, int32_t sign) {
+  if (quota < 0) return GS_OK;
+  if (!g || !request || (uint32_t)quota >= n || (sign != 1 && sign != -1)) return GS_EINVAL;
+  uint32_t hops = 0;
+  for (int32_t q = quota; q != -1; q = g[q].parent) {
+    if (q < -1 || (uint32_t)q >= n || ++hops > n) return GS_EINVAL;
+    for (int d = 0; d < D; ++d) {
+      g[q].used[d] += sign * request[d];
+      if (flags & GS_QUOTA_NON_PREEMPTIBLE) g[q].non_preemptible_used[d] += sign * request[d];
+    }
+  }
+  return GS_OK;
+}
+
+// The admission loop of a quota-gated batch (koordinator_amd/quota.py schedule_with_quota): PreFilter each pod
+// in order and Reserve every admitted pod speculatively (as if placed), stopping before the first rejected pod
+// whose ancestor chain holds a speculative Reserve of this call (its verdict may depend on a pod that then
+// finds no node; admission is monotone in used, so admitted verdicts stand). *consumed = the pods decided.
+extern "C" int gs_quota_admit_batch(gs_quota_group* g, uint32_t n, const int64_t* runtime,
+                                    const uint32_t* runtime_mask, const int32_t* quota, const int64_t* requests,
+                                    const uint32_t* request_mask, const uint32_t* flags, uint32_t count,
+                                    gs_quota_status* status, uint32_t* consumed) {
+  if (!consumed || (count && (!quota || !requests || !request_mask || !flags || !status))) return GS_EINVAL;
+  *consumed = 0;
+  std::vector<uint8_t> touched(n, 0);
+  for (uint32_t j = 0; j < count; ++j) {
+    const int64_t* req = requests + size_t(j) * D;
+    gs_quota_status st;
+    int rc = gs_quota_prefilter(g, n, runtime, runtime_mask, quota[j], req, request_mask[j], flags[j], &st);
+    if (rc != GS_OK) return rc;
+    if (st.code != GS_QUOTA_ADMIT) {
+      bool overlap = false;
+      for (int32_t q = quota[j]; q != -1 && !overlap; q = g[q].parent) overlap = touched[q];
+      if (overlap) return GS_OK;   // re-checked after the batch's true placements
+    } else if (quota[j] >= 0) {
+      rc = gs_quota_reserve(g, n, quota[j], req, flags[j], 1);
+      if (rc != GS_OK) return rc;
+      for (int32_t q = quota[j]; q != -1; q = g[q].parent) touched[q] = 1;
+    }
+    status[j] = st;
+    *consumed = j + 1;
+  }
+  return GS_OK;
+}

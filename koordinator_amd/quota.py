@@ -95,6 +95,9 @@ class ElasticQuotaPlugin:
             getattr(g, fld)[:] = vals.tolist()
             if fld in ("max", "min"):
                 setattr(g, fld + "_mask", mask)
+        if getattr(self, "_arr", None) is not None:   # detach the views before the forest grows
+            self.groups = [abi.GsQuotaGroup.from_buffer_copy(x) for x in self.groups]
+            self._arr = None
         self.index[name] = len(self.names)
         self.names.append(name)
         self.parent_names.append(parent)
@@ -121,10 +124,15 @@ class ElasticQuotaPlugin:
                         a.non_preemptible_used[d] += int(vals[d])
 
     def _array(self):
-        for i, p in enumerate(self.parent_names):
-            self.groups[i].parent = -1 if p == ROOT else self.index[p]
-        arr = (abi.GsQuotaGroup * max(1, len(self.groups)))(*self.groups)
-        return arr
+        """The forest as one ctypes array; self.groups become views into it, so native Reserve calls and
+        Python-side updates see the same memory."""
+        n = len(self.groups)
+        if getattr(self, "_arr", None) is None or len(self._arr) != max(1, n):
+            for i, p in enumerate(self.parent_names):
+                self.groups[i].parent = -1 if p == ROOT else self.index[p]
+            self._arr = (abi.GsQuotaGroup * max(1, n))(*self.groups)
+            self.groups = [self._arr[i] for i in range(n)]
+        return self._arr
 
     def refresh_runtime(self) -> dict:
         """RefreshRuntime for every quota; returns {quota: runtime ResourceList}."""
@@ -170,9 +178,7 @@ class ElasticQuotaPlugin:
         if quota not in self.index:
             return Status("Error", f"Could not find the specified ElasticQuota")
         req, req_mask = self._dense(request)
-        flags = ((abi.GS_QUOTA_RUNTIME if self.enable_runtime_quota else 0)
-                 | (abi.GS_QUOTA_CHECK_PARENT if self.enable_check_parent_quota else 0)
-                 | (abi.GS_QUOTA_NON_PREEMPTIBLE if non_preemptible else 0))
+        flags = self._flags(non_preemptible)
         n = len(self.groups)
         arr = self._array()
         self._ensure_runtime()
@@ -181,6 +187,15 @@ class ElasticQuotaPlugin:
                                          self.index[quota], abi.ptr(req), req_mask, flags, C.byref(st))
         if rc != 0:
             raise RuntimeError(f"gs_quota_prefilter: {rc}")
+        return self._status(st, quota, request)
+
+    def _flags(self, non_preemptible: bool) -> int:
+        return ((abi.GS_QUOTA_RUNTIME if self.enable_runtime_quota else 0)
+                | (abi.GS_QUOTA_CHECK_PARENT if self.enable_check_parent_quota else 0)
+                | (abi.GS_QUOTA_NON_PREEMPTIBLE if non_preemptible else 0))
+
+    def _status(self, st, quota: str, request: dict) -> Status:
+        """gs_quota_status -> the reference's framework.Status text (plugin.go:229-243, plugin_helper.go:287-291)."""
         if st.code == abi.GS_QUOTA_ADMIT:
             return Status("Success")
         failed = self.names[st.group]
@@ -212,12 +227,12 @@ class ElasticQuotaPlugin:
         """The pod's request joins `used` (and non-preemptible used) of its quota and every ancestor."""
         if not quota:
             return
-        vals, _ = self._dense(request)
-        for a in self._chain(quota):
-            for d in range(abi.GS_QUOTA_DIMS):
-                a.used[d] += sign * int(vals[d])
-                if non_preemptible:
-                    a.non_preemptible_used[d] += sign * int(vals[d])
+        req, _ = self._dense(request)
+        arr = self._array()
+        rc = self.lib.gs_quota_reserve(arr, len(self.groups), self.index[quota], abi.ptr(req),
+                                       self._flags(non_preemptible), sign)
+        if rc != 0:
+            raise RuntimeError(f"gs_quota_reserve: {rc}")
 
     def unreserve_pod(self, quota: str | None, request: dict, non_preemptible: bool = False):
         self.reserve_pod(quota, request, non_preemptible, sign=-1)
@@ -243,37 +258,35 @@ def schedule_with_quota(engine, plugin: ElasticQuotaPlugin, pods, pod_quota, seq
     seq = np.arange(n, dtype=np.uint64) if seq is None else np.ascontiguousarray(seq, dtype=np.uint64)
     out = np.zeros(n, abi.PLACEMENT_DTYPE)
     out["node"] = -1
-    statuses: list[Status | None] = [None] * n
+    qidx = np.array([plugin.index[q] if q else -1 for q, _, _ in pod_quota], np.int32)
+    reqs = np.zeros((max(n, 1), abi.GS_QUOTA_DIMS), np.int64)
+    masks = np.zeros(max(n, 1), np.uint32)
+    for j, (_, req, _) in enumerate(pod_quota):
+        reqs[j], masks[j] = plugin._dense(req)
+    flags = np.array([plugin._flags(np_) for _, _, np_ in pod_quota] or [0], np.uint32)
+    arr = plugin._array()
+    plugin._ensure_runtime()
+    ng = len(plugin.groups)
+    st = (abi.GsQuotaStatus * max(n, 1))()
+    consumed = C.c_uint32()
     i = 0
-    chains: dict = {}
-
-    def chain(q):
-        if q not in chains:
-            chains[q] = {id(g) for g in plugin._chain(q)} if q else set()
-        return chains[q]
-
     while i < n:
-        seg: list[int] = []
-        touched: set = set()               # quotas whose used holds a speculative Reserve of this batch
-        j = i
-        while j < n:
-            q, req, np_ = pod_quota[j]
-            st = plugin.pre_filter(q, req, np_)
-            if not st.is_success() and chain(q) & touched:
-                break                      # may depend on the speculation: re-check after the batch's placements
-            statuses[j] = st
-            if st.is_success():
-                plugin.reserve_pod(q, req, np_)
-                seg.append(j)
-                touched |= chain(q)
-            j += 1
-        if seg:
-            idx = np.array(seg)
-            res = engine.schedule(pods[idx], seq[idx])
-            out[idx] = res
-            for k, p in enumerate(seg):
-                if res["node"][k] < 0:     # no feasible node: the speculative Reserve never happened
-                    q, req, np_ = pod_quota[p]
-                    plugin.unreserve_pod(q, req, np_)
+        rc = plugin.lib.gs_quota_admit_batch(
+            arr, ng, abi.ptr(plugin.runtime), abi.ptr(plugin.runtime_mask), qidx[i:].ctypes.data,
+            reqs[i:].ctypes.data, masks[i:].ctypes.data, flags[i:].ctypes.data, n - i,
+            C.byref(st, i * C.sizeof(abi.GsQuotaStatus)), C.byref(consumed))
+        if rc != 0 or consumed.value == 0:
+            raise RuntimeError(f"gs_quota_admit_batch: rc={rc} consumed={consumed.value}")
+        j = i + consumed.value
+        seg = np.array([p for p in range(i, j) if st[p].code == abi.GS_QUOTA_ADMIT], np.int64)
+        if len(seg):
+            res = engine.schedule(pods[seg], seq[seg])
+            out[seg] = res
+            for k in np.nonzero(res["node"] < 0)[0]:   # no feasible node: the speculative Reserve never happened
+                p = int(seg[k])
+                rc = plugin.lib.gs_quota_reserve(arr, ng, int(qidx[p]), reqs[p].ctypes.data, int(flags[p]), -1)
+                if rc != 0:
+                    raise RuntimeError(f"gs_quota_reserve: {rc}")
         i = j
+    statuses = [plugin._status(st[p], pod_quota[p][0], pod_quota[p][1]) for p in range(n)]
     return out, statuses

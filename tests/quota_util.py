@@ -53,3 +53,43 @@ def sequential(engine, p, pods, pq, seq):
             if nodes[i] >= 0:
                 p.reserve_pod(q, req, np_)
     return nodes, codes
+
+
+def oracle_tree():
+    """The same forest in the Python restatement (oracle/quota.py)."""
+    from oracle import quota as oq
+    t = oq.QuotaTree({"cpu": 400_000, "memory": 800 << 30})
+    t.add(oq.Quota("team-a", max={"cpu": 250_000, "memory": 600 << 30}, min={"cpu": 100_000, "memory": 200 << 30}))
+    t.add(oq.Quota("team-a-1", parent="team-a", max={"cpu": 150_000, "memory": 400 << 30},
+                   min={"cpu": 50_000, "memory": 100 << 30}))
+    t.add(oq.Quota("team-a-2", parent="team-a", max={"cpu": 120_000, "memory": 300 << 30},
+                   min={"cpu": 50_000, "memory": 100 << 30}, allow_lent=False))
+    t.add(oq.Quota("team-b", max={"cpu": 90_000, "memory": 200 << 30}, min={"cpu": 60_000, "memory": 100 << 30}))
+    return t
+
+
+def sequential_oracle(engine, pods, pq, seq, check_parent=True):
+    """One pod at a time with the quota gate of oracle/quota.py (independent of libgpuscore's gs_quota_*)."""
+    from oracle import quota as oq
+    t = oracle_tree()
+    for q, req, _ in pq:
+        if q:
+            t.add_pod(q, req, assigned=False)
+    t.refresh()
+    nodes, codes = np.full(len(pods), -1), []
+    for i in range(len(pods)):
+        q, req, np_ = pq[i]
+        code = oq.pre_filter(t, q, req, non_preemptible=np_, check_parent=check_parent)[0]
+        codes.append("Success" if code == "Success" else "Unschedulable")
+        if code == "Success":
+            nodes[i] = engine.schedule(pods[i:i + 1], seq[i:i + 1])["node"][0]
+            if nodes[i] >= 0 and q:
+                name = q
+                while name != oq.ROOT:
+                    a = t.quotas[name]
+                    a.used = {k: a.used.get(k, 0) + req.get(k, 0) for k in set(a.used) | set(req)}
+                    if np_:
+                        a.non_preemptible_used = {k: a.non_preemptible_used.get(k, 0) + req.get(k, 0)
+                                                  for k in set(a.non_preemptible_used) | set(req)}
+                    name = a.parent
+    return nodes, codes

@@ -31,3 +31,19 @@ def test_gate_matches_sequential_order(seed, check_parent):
     assert rejected > 0 and unplaced > 0            # both the cut and the unreserve repair ran
     for name in ("team-a", "team-a-1", "team-a-2", "team-b"):
         assert p1.get(name, "used") == p2.get(name, "used")
+
+
+@pytest.mark.parametrize("seed,check_parent", [(3, True), (4, False)])
+def test_gate_matches_quota_oracle(seed, check_parent):
+    """Against the independent Python restatement of the quota gate (oracle/quota.py)."""
+    c, cfg = qu.setup(800, 240, seed)
+    seq = np.arange(len(c.pods), dtype=np.uint64)
+    o1, o2 = orc.Oracle(cfg), orc.Oracle(cfg)
+    synth.load_into(o1, c)
+    synth.load_into(o2, c)
+    p1 = qu.plugin(check_parent=check_parent)
+    pq = qu.pod_quotas(c, p1)
+    got, st = schedule_with_quota(o1, p1, c.pods, pq, seq)
+    want_nodes, want_codes = qu.sequential_oracle(o2, c.pods, pq, seq, check_parent)
+    assert [s.code for s in st] == want_codes
+    assert np.array_equal(got["node"], want_nodes)
