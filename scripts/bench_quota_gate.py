@@ -40,7 +40,7 @@ def main():
                            min={"cpu": cap_cpu // 40, "memory": cap_mem // 40})
             for k in range(10):
                 # a few children are tight: their pods hit the quota and get rejected
-                frac = 400 if k == 0 else 120
+                frac = 20_000 if k == 0 else 2_000
                 p.on_quota_add(f"t{t}-{k}", parent=f"t{t}", max={"cpu": cap_cpu // frac, "memory": cap_mem // frac},
                                min={"cpu": cap_cpu // 800, "memory": cap_mem // 800}, allow_lent=k % 3 != 0)
         return p
@@ -84,14 +84,14 @@ def main():
         eng.synchronize()
         dt = time.perf_counter() - t0
         eng.close()
-        return {"pods_per_s": args.steps * P / dt, "placed": placed, "quota_rejected": rejected,
+        return {"pods_per_s": args.steps * P / dt, "placed_per_s": placed / dt, "placed": placed, "quota_rejected": rejected,
                 "engine_calls": len(calls), "mean_engine_batch": float(np.mean(calls)) if calls else None}
 
     ungated = run(False)
     gated = run(True)
     print(json.dumps({"workload": f"C3 {args.nodes} nodes x {args.steps * P} pods, 200 ElasticQuotas (20x10), "
                                   f"check-parent, 25% non-preemptible", "ungated": ungated, "gated": gated,
-                      "gate_overhead_frac": 1 - gated["pods_per_s"] / ungated["pods_per_s"]}))
+                      "note": "pods_per_s counts every decided pod (quota-rejected pods do no node work)"}))
 
 
 if __name__ == "__main__":
