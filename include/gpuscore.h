@@ -504,6 +504,7 @@ typedef struct gs_quota_status {
   int32_t group;       /* the group whose check failed (a parent when the recursive check failed), else -1 */
   uint32_t exceed_mask;/* exceedDimensions */
   uint32_t depth;      /* parent hops above the pod's quota for a recursive failure (quotaNameTopo length - 1) */
+  int64_t used[GS_QUOTA_DIMS];   /* the failing group's used (non-preemptible used for _NON_PREEMPTIBLE) as checked */
 } gs_quota_status;
 /* Plugin.PreFilter (elasticquota/plugin.go:210-254) + checkQuotaRecursive (plugin_helper.go:281-297) for one
  * pod of quota `quota` (-1: no quota label -> admit). runtime: n x GS_QUOTA_DIMS, group i's keys runtime_mask[i]
@@ -518,13 +519,21 @@ int gs_quota_prefilter(const gs_quota_group* groups, uint32_t n, const int64_t* 
 int gs_quota_reserve(gs_quota_group* groups, uint32_t n, int32_t quota, const int64_t request[GS_QUOTA_DIMS],
                      uint32_t flags, int32_t sign);
 /* Quota-gated batch admission: gs_quota_prefilter per pod in order (pod j: quota[j], requests[j*GS_QUOTA_DIMS..],
- * request_mask[j], flags[j]); each admitted pod is reserved speculatively; stops before the first rejected pod
- * whose ancestor chain holds a speculative Reserve of this call (its verdict may change once a speculatively
- * reserved pod finds no node and is unreserved; admission is monotone in used, so admitted verdicts stand).
+ * request_mask[j], flags[j]); each admitted pod is reserved speculatively; a rejected pod is final when it is
+ * also rejected against the certain used (its chain's used minus this call's speculative Reserves), otherwise the
+ * call stops before it (admission is monotone in used, so admitted verdicts stand). Follow each run with
+ * gs_quota_settle_batch.
  * status[0..*consumed) = the decided pods' verdicts. */
 int gs_quota_admit_batch(gs_quota_group* groups, uint32_t n, const int64_t* runtime, const uint32_t* runtime_mask,
                          const int32_t* quota, const int64_t* requests, const uint32_t* request_mask,
                          const uint32_t* flags, uint32_t count, gs_quota_status* status, uint32_t* consumed);
+
+/* Settles a run of gs_quota_admit_batch after the node loop: withdraws its speculative Reserves and replays it
+ * in order with the engine's placements (placed_node[j] >= 0: Reserve), recomputing every status against the
+ * used the one-pod-at-a-time order would have seen. GS_ESTATE if a verdict would change (monotonicity bug). */
+int gs_quota_settle_batch(gs_quota_group* groups, uint32_t n, const int64_t* runtime, const uint32_t* runtime_mask,
+                          const int32_t* quota, const int64_t* requests, const uint32_t* request_mask,
+                          const uint32_t* flags, uint32_t count, const int32_t* placed_node, gs_quota_status* status);
 
 int gs_get_stats(gs_ctx* ctx, gs_stats* out);
 int gs_reset_stats(gs_ctx* ctx);

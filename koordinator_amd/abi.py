@@ -190,7 +190,8 @@ class GsQuotaGroup(C.Structure):
 
 
 class GsQuotaStatus(C.Structure):
-    _fields_ = [("code", i32), ("group", i32), ("exceed_mask", u32), ("depth", u32)]
+    _fields_ = [("code", i32), ("group", i32), ("exceed_mask", u32), ("depth", u32),
+                ("used", i64 * GS_QUOTA_DIMS)]
 
 
 ALLGATHER_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t)
@@ -262,6 +263,7 @@ SIGNATURES = {
     "gs_quota_prefilter": (C.c_int, [P, u32, P, P, i32, P, u32, u32, C.POINTER(GsQuotaStatus)]),
     "gs_quota_reserve": (C.c_int, [P, u32, i32, P, u32, i32]),
     "gs_quota_admit_batch": (C.c_int, [P, u32, P, P, P, P, P, P, u32, P, C.POINTER(u32)]),
+    "gs_quota_settle_batch": (C.c_int, [P, u32, P, P, P, P, P, P, u32, P, P]),
 }
 
 

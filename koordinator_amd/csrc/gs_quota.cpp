@@ -173,6 +173,7 @@ extern "C" int gs_quota_prefilter(const gs_quota_group* g, uint32_t n, const int
   out->group = -1;
   out->exceed_mask = 0;
   out->depth = 0;
+  std::memset(out->used, 0, sizeof(out->used));
   if (quota < 0) return GS_OK;   // no quota label: PreFilter skips (plugin.go:211-215)
   if ((uint32_t)quota >= n || !g || !pod_request) return GS_EINVAL;
   const bool use_runtime = flags & GS_QUOTA_RUNTIME;
@@ -193,6 +194,7 @@ extern "C" int gs_quota_prefilter(const gs_quota_group* g, uint32_t n, const int
     out->code = GS_QUOTA_INSUFFICIENT;
     out->group = quota;
     out->exceed_mask = m;
+    std::memcpy(out->used, g[quota].used, sizeof(out->used));
     return GS_OK;
   }
   if (flags & GS_QUOTA_NON_PREEMPTIBLE) {   // nonPreemptibleUsed + request within Min (plugin.go:235-244)
@@ -201,6 +203,7 @@ extern "C" int gs_quota_prefilter(const gs_quota_group* g, uint32_t n, const int
       out->code = GS_QUOTA_INSUFFICIENT_NON_PREEMPTIBLE;
       out->group = quota;
       out->exceed_mask = m;
+      std::memcpy(out->used, g[quota].non_preemptible_used, sizeof(out->used));
       return GS_OK;
     }
   }
@@ -213,6 +216,7 @@ extern "C" int gs_quota_prefilter(const gs_quota_group* g, uint32_t n, const int
         out->group = q;
         out->exceed_mask = m;
         out->depth = hops;
+        std::memcpy(out->used, g[q].used, sizeof(out->used));
         return GS_OK;
       }
     }
@@ -238,16 +242,27 @@ extern "C" int gs_quota_reserve(gs_quota_group* g, uint32_t n, int32_t quota, co
 }
 
 // The admission loop of a quota-gated batch (koordinator_amd/quota.py schedule_with_quota): PreFilter each pod
-// in order and Reserve every admitted pod speculatively (as if placed), stopping before the first rejected pod
-// whose ancestor chain holds a speculative Reserve of this call (its verdict may depend on a pod that then
-// finds no node; admission is monotone in used, so admitted verdicts stand). *consumed = the pods decided.
+// in order and Reserve every admitted pod speculatively (as if placed). Admission is monotone in used, so an
+// admitted verdict stands whatever the speculative pods' outcomes. A rejection is final when it also holds
+// against the certain used (used minus this call's speculative Reserves on the pod's chain, the least the true
+// used can be); otherwise the loop stops before that pod, to be re-checked once the batch's true placements
+// are reserved. *consumed = the pods decided.
 extern "C" int gs_quota_admit_batch(gs_quota_group* g, uint32_t n, const int64_t* runtime,
                                     const uint32_t* runtime_mask, const int32_t* quota, const int64_t* requests,
                                     const uint32_t* request_mask, const uint32_t* flags, uint32_t count,
                                     gs_quota_status* status, uint32_t* consumed) {
   if (!consumed || (count && (!quota || !requests || !request_mask || !flags || !status))) return GS_EINVAL;
   *consumed = 0;
+  std::vector<int64_t> spec(size_t(n) * 2 * D, 0);   // per group: speculative used, non-preemptible used
   std::vector<uint8_t> touched(n, 0);
+  auto shift = [&](int32_t q0, int64_t sign) {        // remove (-1) / restore (+1) the speculation on a chain
+    for (int32_t q = q0; q != -1; q = g[q].parent)
+      if (touched[q])
+        for (int d = 0; d < D; ++d) {
+          g[q].used[d] += sign * spec[size_t(q) * 2 * D + d];
+          g[q].non_preemptible_used[d] += sign * spec[size_t(q) * 2 * D + D + d];
+        }
+  };
   for (uint32_t j = 0; j < count; ++j) {
     const int64_t* req = requests + size_t(j) * D;
     gs_quota_status st;
@@ -256,14 +271,58 @@ extern "C" int gs_quota_admit_batch(gs_quota_group* g, uint32_t n, const int64_t
     if (st.code != GS_QUOTA_ADMIT) {
       bool overlap = false;
       for (int32_t q = quota[j]; q != -1 && !overlap; q = g[q].parent) overlap = touched[q];
-      if (overlap) return GS_OK;   // re-checked after the batch's true placements
+      if (overlap) {
+        gs_quota_status certain;
+        shift(quota[j], -1);
+        rc = gs_quota_prefilter(g, n, runtime, runtime_mask, quota[j], req, request_mask[j], flags[j], &certain);
+        shift(quota[j], +1);
+        if (rc != GS_OK) return rc;
+        if (certain.code == GS_QUOTA_ADMIT) return GS_OK;   // depends on the speculation: cut here
+        st = certain;                                       // rejected at the least possible used: final
+      }
     } else if (quota[j] >= 0) {
       rc = gs_quota_reserve(g, n, quota[j], req, flags[j], 1);
       if (rc != GS_OK) return rc;
-      for (int32_t q = quota[j]; q != -1; q = g[q].parent) touched[q] = 1;
+      for (int32_t q = quota[j]; q != -1; q = g[q].parent) {
+        touched[q] = 1;
+        for (int d = 0; d < D; ++d) {
+          spec[size_t(q) * 2 * D + d] += req[d];
+          if (flags[j] & GS_QUOTA_NON_PREEMPTIBLE) spec[size_t(q) * 2 * D + D + d] += req[d];
+        }
+      }
     }
     status[j] = st;
     *consumed = j + 1;
+  }
+  return GS_OK;
+}
+
+// Settles a run decided by gs_quota_admit_batch once the engine's placements are known: the speculative Reserves
+// are withdrawn and the run is replayed in order — a placed pod is reserved, an admitted pod with no node is not,
+// and every rejected pod's status is recomputed against the used it would have seen in the one-pod-at-a-time
+// order (a final rejection decided against the certain used keeps its verdict, its detail may change).
+// GS_ESTATE if a replayed verdict differs from the one admit_batch gave (it cannot, by monotonicity).
+extern "C" int gs_quota_settle_batch(gs_quota_group* g, uint32_t n, const int64_t* runtime,
+                                     const uint32_t* runtime_mask, const int32_t* quota, const int64_t* requests,
+                                     const uint32_t* request_mask, const uint32_t* flags, uint32_t count,
+                                     const int32_t* placed_node, gs_quota_status* status) {
+  if (count && (!quota || !requests || !request_mask || !flags || !status || !placed_node)) return GS_EINVAL;
+  for (uint32_t j = 0; j < count; ++j)
+    if (status[j].code == GS_QUOTA_ADMIT && quota[j] >= 0) {
+      int rc = gs_quota_reserve(g, n, quota[j], requests + size_t(j) * D, flags[j], -1);
+      if (rc != GS_OK) return rc;
+    }
+  for (uint32_t j = 0; j < count; ++j) {
+    const int64_t* req = requests + size_t(j) * D;
+    gs_quota_status st;
+    int rc = gs_quota_prefilter(g, n, runtime, runtime_mask, quota[j], req, request_mask[j], flags[j], &st);
+    if (rc != GS_OK) return rc;
+    if ((st.code == GS_QUOTA_ADMIT) != (status[j].code == GS_QUOTA_ADMIT)) return GS_ESTATE;
+    status[j] = st;
+    if (st.code == GS_QUOTA_ADMIT && quota[j] >= 0 && placed_node[j] >= 0) {
+      rc = gs_quota_reserve(g, n, quota[j], req, flags[j], 1);
+      if (rc != GS_OK) return rc;
+    }
   }
   return GS_OK;
 }

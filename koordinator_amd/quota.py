@@ -200,17 +200,18 @@ class ElasticQuotaPlugin:
             return Status("Success")
         failed = self.names[st.group]
         exceed = [r for r, d in self.dim.items() if st.exceed_mask >> d & 1]
+        used = {k: v for k, v in self._sparse(list(st.used), (1 << abi.GS_QUOTA_DIMS) - 1).items() if v}
         i = st.group
         limit = (self._sparse(self.runtime[i], int(self.runtime_mask[i])) if self.enable_runtime_quota
                  else self.get(failed, "max"))
         if st.code == abi.GS_QUOTA_INSUFFICIENT_NON_PREEMPTIBLE:
             msg = (f"Insufficient non-preemptible quotas, quotaName: {failed}, min: "
                    f"{print_resource_list(self.get(failed, 'min'))}, nonPreemptibleUsed: "
-                   f"{print_resource_list(self.get(failed, 'non_preemptible_used'))}, pod's request: "
+                   f"{print_resource_list(used)}, pod's request: "
                    f"{print_resource_list(request)}, exceedDimensions: [{' '.join(exceed)}]")
         elif st.depth == 0:   # the pod's own quota (the first check of plugin.go:229-234)
             msg = (f"Insufficient quotas, quotaName: {failed}, runtime: {print_resource_list(limit)}, used: "
-                   f"{print_resource_list(self.get(failed, 'used'))}, pod's request: {print_resource_list(request)}, "
+                   f"{print_resource_list(used)}, pod's request: {print_resource_list(request)}, "
                    f"exceedDimensions: [{' '.join(exceed)}]")
         else:
             topo, name = [quota], quota
@@ -218,7 +219,7 @@ class ElasticQuotaPlugin:
                 name = self.parent_names[self.index[name]]
                 topo.insert(0, name)
             msg = (f"Insufficient quotas, quotaNameTopo: [{' '.join(topo)}], runtime: {print_resource_list(limit)}, "
-                   f"used: {print_resource_list(self.get(failed, 'used'))}, pod's request: "
+                   f"used: {print_resource_list(used)}, pod's request: "
                    f"{print_resource_list(request)}, exceedDimensions: [{' '.join(exceed)}]")
         return Status("Unschedulable", msg, failed, exceed)
 
@@ -247,9 +248,11 @@ def schedule_with_quota(engine, plugin: ElasticQuotaPlugin, pods, pod_quota, seq
     Admitted pods are reserved speculatively (as if placed) so that a run of admitted pods goes to the engine
     as one batch. The check is monotone in `used` (used + request <= limit), so a pod admitted under
     speculation stays admitted when an earlier pod of its batch finds no node and is unreserved; only a
-    rejection can depend on the speculation, and only when the batch holds a speculative Reserve on a quota of
-    the rejected pod's chain: then the batch is cut before that pod and it is re-checked once the batch's true
-    placements are reserved; otherwise the rejection is final. Runtime does not change inside a batch (it
+    rejection can depend on the speculation: it is final when the pod is also rejected against the certain used
+    (its chain's used minus the run's speculative Reserves), otherwise the run is cut before that pod, which is
+    re-checked once the run's true placements are reserved. After the engine call the run is settled natively
+    (gs_quota_settle_batch): speculation withdrawn, run replayed with the true placements, so statuses and used
+    are those of the one-pod-at-a-time order. Runtime does not change inside a batch (it
     follows requests, which a Reserve does not touch). pod_quota[i] = (quota name or None, request
     ResourceList, non_preemptible). Returns (placements, statuses): placements in the engine's dtype with
     node = -1 for quota-rejected pods, statuses[i] = the PreFilter Status of pod i."""
@@ -282,11 +285,14 @@ def schedule_with_quota(engine, plugin: ElasticQuotaPlugin, pods, pod_quota, seq
         if len(seg):
             res = engine.schedule(pods[seg], seq[seg])
             out[seg] = res
-            for k in np.nonzero(res["node"] < 0)[0]:   # no feasible node: the speculative Reserve never happened
-                p = int(seg[k])
-                rc = plugin.lib.gs_quota_reserve(arr, ng, int(qidx[p]), reqs[p].ctypes.data, int(flags[p]), -1)
-                if rc != 0:
-                    raise RuntimeError(f"gs_quota_reserve: {rc}")
+        # withdraw the speculation and replay the run with the true placements (exact statuses and used)
+        placed = np.ascontiguousarray(out["node"][i:j], dtype=np.int32)
+        rc = plugin.lib.gs_quota_settle_batch(
+            arr, ng, abi.ptr(plugin.runtime), abi.ptr(plugin.runtime_mask), qidx[i:].ctypes.data,
+            reqs[i:].ctypes.data, masks[i:].ctypes.data, flags[i:].ctypes.data, j - i, abi.ptr(placed),
+            C.byref(st, i * C.sizeof(abi.GsQuotaStatus)))
+        if rc != 0:
+            raise RuntimeError(f"gs_quota_settle_batch: {rc}")
         i = j
     statuses = [plugin._status(st[p], pod_quota[p][0], pod_quota[p][1]) for p in range(n)]
     return out, statuses

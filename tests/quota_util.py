@@ -46,7 +46,7 @@ def sequential(engine, p, pods, pq, seq):
     for i in range(len(pods)):
         q, req, np_ = pq[i]
         st = p.pre_filter(q, req, np_)
-        codes.append(st.code)
+        codes.append((st.code, st.message))
         if st.is_success():
             r = engine.schedule(pods[i:i + 1], seq[i:i + 1])
             nodes[i] = r["node"][0]

@@ -25,7 +25,7 @@ def test_gpu_gate_matches_sequential_oracle(batch):
     pq1, pq2 = qu.pod_quotas(c, p1), qu.pod_quotas(c, p2)
     got, st = schedule_with_quota(e, p1, c.pods, pq1, seq)
     want_nodes, want_codes = qu.sequential(o, p2, c.pods, pq2, seq)
-    assert [s.code for s in st] == want_codes
+    assert [(s.code, s.message) for s in st] == want_codes
     bad = np.nonzero(got["node"] != want_nodes)[0]
     assert len(bad) == 0, f"placement differs first at pod {bad[0]}"
     assert e.mirror_check() == 0

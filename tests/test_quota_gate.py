@@ -24,7 +24,7 @@ def test_gate_matches_sequential_order(seed, check_parent):
     pq1, pq2 = qu.pod_quotas(c, p1), qu.pod_quotas(c, p2)
     got, st = schedule_with_quota(o1, p1, c.pods, pq1, seq)
     want_nodes, want_codes = qu.sequential(o2, p2, c.pods, pq2, seq)
-    assert [s.code for s in st] == want_codes
+    assert [(s.code, s.message) for s in st] == want_codes   # verdicts and the reference's status text
     assert np.array_equal(got["node"], want_nodes)
     rejected = sum(s.code != "Success" for s in st)
     unplaced = int(((got["node"] < 0) & np.array([s.code == "Success" for s in st])).sum())
