@@ -7,7 +7,6 @@
 //     201-212 getLimitRequestNoLock) and the top-down runtime refresh (group_quota_manager.go:264-321), computed
 //     for every group at once from a settled tree;
 //   * Plugin.PreFilter (plugin.go:210-254) and checkQuotaRecursive (plugin_helper.go:281-297).
-#include <algorithm>
 #include <cstdint>
 #include <cstring>
 #include <vector>
@@ -22,9 +21,8 @@ constexpr int D = GS_QUOTA_DIMS;
 // node's share depends only on (totalRes, totalSharedWeight), so the Go map's iteration order cannot change the
 // result; the share is int64(float64(w)*float64(total)/float64(totalW) + 0.5) — the same three IEEE double
 // operations, truncated toward zero like Go's conversion.
-void iterate(int64_t total, int64_t total_w, std::vector<uint32_t> nodes, const int64_t* request,
-             const int64_t* weight, int64_t* rt) {
-  std::vector<uint32_t> next;
+void iterate(int64_t total, int64_t total_w, std::vector<uint32_t>& nodes, std::vector<uint32_t>& next,
+             const int64_t* request, const int64_t* weight, int64_t* rt) {
   while (total_w > 0) {
     next.clear();
     int64_t part = 0, next_w = 0;
@@ -50,7 +48,8 @@ void iterate(int64_t total, int64_t total_w, std::vector<uint32_t> nodes, const 
 void redistribute(uint32_t n, const int64_t* request, const int64_t* min, const int64_t* guaranteed,
                   const int64_t* weight, const uint8_t* lent, int64_t total, int64_t* rt) {
   int64_t to_part = total, total_w = 0;
-  std::vector<uint32_t> adjust;
+  thread_local std::vector<uint32_t> adjust, next;   // scratch reused across calls (no per-parent allocation)
+  adjust.clear();
   for (uint32_t i = 0; i < n; ++i) {
     const int64_t m = guaranteed[i] > min[i] ? guaranteed[i] : min[i];   // guarantee above min replaces it
     if (request[i] > m) {
@@ -62,21 +61,7 @@ void redistribute(uint32_t n, const int64_t* request, const int64_t* min, const 
     }
     to_part -= rt[i];
   }
-  if (to_part > 0) iterate(to_part, total_w, std::move(adjust), request, weight, rt);
-}
-
-// depth of every group (root's children: 0); -1 on a bad parent index or a cycle.
-bool depths(const gs_quota_group* g, uint32_t n, std::vector<uint32_t>& depth) {
-  depth.assign(n, 0);
-  for (uint32_t i = 0; i < n; ++i) {
-    uint32_t d = 0;
-    for (int32_t p = g[i].parent; p >= 0; p = g[p].parent) {
-      if ((uint32_t)p >= n || ++d > n) return false;
-    }
-    if (g[i].parent < -1) return false;
-    depth[i] = d;
-  }
-  return true;
+  if (to_part > 0) iterate(to_part, total_w, adjust, next, request, weight, rt);
 }
 
 // quotav1.LessThanOrEqual(Mask(Add(podRequest, used), names(podRequest)), limit): only keys of the limit that the
@@ -103,24 +88,38 @@ extern "C" int gs_quota_redistribute(const int64_t* request, const int64_t* min,
 extern "C" int gs_quota_refresh_runtime(const gs_quota_group* g, uint32_t n, const int64_t total[GS_QUOTA_DIMS],
                                         int64_t* runtime, int64_t* limit_request, uint32_t* runtime_mask) {
   if (n && (!g || !total)) return GS_EINVAL;
-  std::vector<uint32_t> depth;
-  if (!depths(g, n, depth)) return GS_EINVAL;
+  // children in CSR form (slot n = the root), then a BFS from the root: parents before children. A group the
+  // BFS does not reach sits on a cycle.
+  std::vector<uint32_t> off(n + 2, 0), kid(n), order;
+  order.reserve(n);
+  for (uint32_t i = 0; i < n; ++i) {
+    const int32_t p = g[i].parent;
+    if (p < -1 || p >= (int32_t)n) return GS_EINVAL;
+    ++off[(p < 0 ? n : (uint32_t)p) + 1];
+  }
+  for (uint32_t i = 0; i <= n; ++i) off[i + 1] += off[i];
+  {
+    std::vector<uint32_t> fill(off.begin(), off.end() - 1);
+    for (uint32_t i = 0; i < n; ++i) kid[fill[g[i].parent < 0 ? n : (uint32_t)g[i].parent]++] = i;
+  }
+  for (uint32_t k = off[n]; k < off[n + 1]; ++k) order.push_back(kid[k]);
+  for (size_t h = 0; h < order.size(); ++h)
+    for (uint32_t k = off[order[h]]; k < off[order[h] + 1]; ++k) order.push_back(kid[k]);
+  if (order.size() != n) return GS_EINVAL;
+
   uint32_t keys = 0;   // updateResourceKeyNoLock: the union of every quota's Max keys
   for (uint32_t i = 0; i < n; ++i) keys |= g[i].max_mask;
   keys &= (1u << D) - 1;
   if (runtime_mask)
     for (uint32_t i = 0; i < n; ++i) runtime_mask[i] = keys;
 
-  std::vector<uint32_t> order(n);
-  for (uint32_t i = 0; i < n; ++i) order[i] = i;
-  std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return depth[a] > depth[b]; });
-
-  // bottom-up: ChildRequest = own pods + the children's limited requests; Request = ChildRequest, raised to Min
-  // when the quota does not lend; limited request = min(Request, Max) on Max's keys.
+  // bottom-up (reverse BFS): ChildRequest = own pods + the children's limited requests; Request = ChildRequest,
+  // raised to Min when the quota does not lend; limited request = min(Request, Max) on Max's keys.
   std::vector<int64_t> child(size_t(n) * D), limit(size_t(n) * D);
   for (uint32_t i = 0; i < n; ++i)
     for (int d = 0; d < D; ++d) child[size_t(i) * D + d] = g[i].request[d];
-  for (uint32_t i : order) {
+  for (uint32_t h = n; h-- > 0;) {
+    const uint32_t i = order[h];
     for (int d = 0; d < D; ++d) {
       int64_t r = child[size_t(i) * D + d];
       if (r < 0) r = 0;   // addChildRequestNonNegativeNoLock
@@ -131,33 +130,29 @@ extern "C" int gs_quota_refresh_runtime(const gs_quota_group* g, uint32_t n, con
     }
   }
 
-  // top-down: each parent's runtime (the root's: total) is redistributed over its children, per key.
+  // top-down (root, then BFS order): each parent's runtime (the root's: total) is redistributed over its
+  // children, per key.
   std::vector<int64_t> rt(size_t(n) * D, 0);
-  std::vector<std::vector<uint32_t>> kids(n + 1);   // kids[n] = children of the root
-  for (uint32_t i = 0; i < n; ++i) kids[g[i].parent < 0 ? n : (uint32_t)g[i].parent].push_back(i);
-  std::vector<uint32_t> parents;
-  parents.push_back(n);
-  for (uint32_t k = n; k-- > 0;) parents.push_back(order[k]);   // ascending depth: parents before children
   std::vector<int64_t> req, mn, gu, w, out;
   std::vector<uint8_t> lent;
-  for (uint32_t p : parents) {
-    const auto& ch = kids[p];
-    if (ch.empty()) continue;
-    const size_t m = ch.size();
+  for (uint32_t h = 0; h <= n; ++h) {
+    const uint32_t p = h == 0 ? n : order[h - 1];
+    const uint32_t k0 = off[p], m = off[p + 1] - k0;
+    if (m == 0) continue;
     req.resize(m); mn.resize(m); gu.resize(m); w.resize(m); lent.resize(m); out.resize(m);
     for (int d = 0; d < D; ++d) {
       if (!(keys >> d & 1u)) continue;
-      for (size_t j = 0; j < m; ++j) {
-        const gs_quota_group& c = g[ch[j]];
-        req[j] = limit[size_t(ch[j]) * D + d];
-        mn[j] = (c.min_mask >> d & 1u) ? c.min[d] : 0;
-        gu[j] = c.guaranteed[d];
-        w[j] = c.shared_weight[d];
-        lent[j] = c.allow_lent ? 1 : 0;
+      for (uint32_t j = 0; j < m; ++j) {
+        const uint32_t c = kid[k0 + j];
+        req[j] = limit[size_t(c) * D + d];
+        mn[j] = (g[c].min_mask >> d & 1u) ? g[c].min[d] : 0;
+        gu[j] = g[c].guaranteed[d];
+        w[j] = g[c].shared_weight[d];
+        lent[j] = g[c].allow_lent ? 1 : 0;
       }
       const int64_t tot = p == n ? total[d] : rt[size_t(p) * D + d];
-      redistribute((uint32_t)m, req.data(), mn.data(), gu.data(), w.data(), lent.data(), tot, out.data());
-      for (size_t j = 0; j < m; ++j) rt[size_t(ch[j]) * D + d] = out[j];
+      redistribute(m, req.data(), mn.data(), gu.data(), w.data(), lent.data(), tot, out.data());
+      for (uint32_t j = 0; j < m; ++j) rt[size_t(kid[k0 + j]) * D + d] = out[j];
     }
   }
   if (runtime) std::memcpy(runtime, rt.data(), rt.size() * sizeof(int64_t));
