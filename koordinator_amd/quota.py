@@ -123,6 +123,30 @@ class ElasticQuotaPlugin:
                     if non_preemptible:
                         a.non_preemptible_used[d] += int(vals[d])
 
+    def on_pod_delete(self, quota: str, request: dict, assigned: bool, non_preemptible: bool = False):
+        """OnPodDelete: the pod's request leaves its quota (clamped at zero, addRequestNonNegativeNoLock) and,
+        if it was assigned, its used leaves the quota and every ancestor."""
+        vals, _ = self._dense(request)
+        g = self.groups[self.index[quota]]
+        for d in range(abi.GS_QUOTA_DIMS):
+            g.request[d] = max(0, g.request[d] - int(vals[d]))
+        if assigned:
+            self.reserve_pod(quota, request, non_preemptible, sign=-1)
+
+    def on_quota_update(self, name, max=None, min=None, shared_weight=None, allow_lent=None):
+        """OnQuotaUpdate for the spec fields the runtime reads (Max, Min, SharedWeight, AllowLentResource);
+        takes effect at the next refresh_runtime()."""
+        g = self.groups[self.index[name]]
+        if allow_lent is not None:
+            g.allow_lent = 1 if allow_lent else 0
+        for fld, rl in (("max", max), ("min", min), ("shared_weight", shared_weight)):
+            if rl is None:
+                continue
+            vals, mask = self._dense(rl)
+            getattr(g, fld)[:] = vals.tolist()
+            if fld in ("max", "min"):
+                setattr(g, fld + "_mask", mask)
+
     def _array(self):
         """The forest as one ctypes array; self.groups become views into it, so native Reserve calls and
         Python-side updates see the same memory."""

@@ -97,6 +97,20 @@ class QuotaTree:
                     a.non_preemptible_used = _add(a.non_preemptible_used, request)
                 name = a.parent
 
+    def remove_pod(self, quota: str, request: dict, assigned: bool, non_preemptible: bool = False):
+        """OnPodDelete: request leaves the quota (non-negative), used leaves the chain if assigned."""
+        q = self.quotas[quota]
+        q.pod_request = {k: max(0, q.pod_request.get(k, 0) - request.get(k, 0))
+                         for k in set(q.pod_request) | set(request)}
+        if assigned:
+            name = quota
+            while name != ROOT:
+                a = self.quotas[name]
+                a.used = _add(a.used, {k: -v for k, v in request.items()})
+                if non_preemptible:
+                    a.non_preemptible_used = _add(a.non_preemptible_used, {k: -v for k, v in request.items()})
+                name = a.parent
+
     def children(self, name: str) -> list[Quota]:
         return [q for q in self.quotas.values() if q.parent == name]
 

@@ -214,3 +214,43 @@ def test_runtime_conservation(lib):
                 floor = max(specs[name]["min"].get(r, 0), (specs[name]["guaranteed"] or {}).get(r, 0))
                 if specs[name]["allow_lent"]:
                     assert rt[name].get(r, 0) <= max(lim[i, d], floor)
+
+
+@pytest.mark.parametrize("seed", range(10))
+def test_pod_delete_and_quota_update_match_oracle(lib, seed):
+    """OnPodDelete / OnQuotaUpdate events between refreshes: runtime and PreFilter still match the oracle."""
+    rng = random.Random(1000 + seed)
+    names, parents, specs = _random_forest(rng, rng.randrange(2, 16))
+    total = {r: rng.randrange(100_000, 1_000_000) for r in RES}
+    p = ElasticQuotaPlugin(resources=RES, enable_check_parent_quota=True, lib=lib)
+    p.update_cluster_total_resource(total)
+    tree = oq.QuotaTree(total)
+    for name in names:
+        p.on_quota_add(name, parent=parents[name], **specs[name])
+        tree.add(oq.Quota(name, parent=parents[name], **specs[name]))
+    pods = []
+    for _ in range(60):
+        name = rng.choice(names)
+        req = {r: rng.randrange(0, 40_000) for r in RES}
+        a, np_ = rng.random() < 0.6, rng.random() < 0.3
+        p.on_pod_add(name, req, a, np_)
+        tree.add_pod(name, req, a, np_)
+        pods.append((name, req, a, np_))
+    for name, req, a, np_ in rng.sample(pods, 25):
+        p.on_pod_delete(name, req, a, np_)
+        tree.remove_pod(name, req, a, np_)
+    for name in rng.sample(names, max(1, len(names) // 3)):
+        mx = {r: rng.randrange(0, 200_000) for r in RES}
+        p.on_quota_update(name, max=mx, allow_lent=not specs[name]["allow_lent"])
+        q = tree.quotas[name]
+        q.max, q.allow_lent = dict(mx), not specs[name]["allow_lent"]   # SharedWeight keeps its value
+    got = p.refresh_runtime()
+    tree.refresh()
+    for name in names:
+        assert got[name] == tree.quotas[name].runtime, name
+    for _ in range(20):
+        name = rng.choice(names)
+        req = {r: rng.randrange(0, 60_000) for r in RES}
+        st = p.pre_filter(name, req)
+        code, failed, bad, _ = oq.pre_filter(tree, name, req, check_parent=True)
+        assert st.is_success() == (code == "Success") and (st.is_success() or (st.quota, st.exceed) == (failed, bad))
