@@ -272,6 +272,11 @@ int quantity_scaled(const char* s, int scale10, int64_t* out) {
   }
   e10 += scale10;
   if (m == 0) { *out = 0; return GS_OK; }
+  // A negative quantity takes apimachinery's int64Amount or inf.Dec path by its digits and suffix, and the two
+  // round an inexact Value() differently (away from zero vs truncate-then-add-one); resource requests, allocatable
+  // and the annotations decoded here are non-negative in every valid object, so a negative one is refused
+  // instead of being rounded by one rule for both paths.
+  if (neg) return GS_EUNSUPPORTED;
   const __int128 lim = (__int128)INT64_MAX;
   for (int i = 0; i < e2; ++i) { m *= 2; if (m > lim * 1000) return GS_EUNSUPPORTED; }
   __int128 q;
@@ -279,16 +284,16 @@ int quantity_scaled(const char* s, int scale10, int64_t* out) {
     q = m;
     for (int i = 0; i < e10; ++i) { q *= 10; if (q > lim) return GS_EUNSUPPORTED; }
   } else if (-e10 > 36) {
-    *out = neg ? 0 : 1;   // 0 < |value| < 1 after scaling: ceil is 1 above zero, 0 below
+    *out = 1;   // 0 < value < 1 after scaling: ceil is 1
     return GS_OK;
   } else {
     __int128 d = 1;
     for (int i = 0; i < -e10; ++i) d *= 10;
     q = m / d;
-    if (!neg && m % d != 0) q += 1;   // ceil of a positive value; a negative one truncates toward +inf
+    if (m % d != 0) q += 1;   // ceil
   }
   if (q > lim) return GS_EUNSUPPORTED;
-  *out = neg ? -(int64_t)q : (int64_t)q;
+  *out = (int64_t)q;
   return GS_OK;
 }
 

@@ -1190,7 +1190,7 @@ __global__ void __launch_bounds__(256) commit_kernel(CommitArgs a) {
     // batch-start scores (fresh rows) on threads 0..127, current scores on threads 128..255; one call site,
     // so the long pair evaluation exists once in the instruction cache
     {
-      const bool start = tid < 128;
+      const bool start = __builtin_amdgcn_readfirstlane(wave) < 2;   // wave-uniform: the row goes scalar
       const int q = k + 1 + (tid & 127);
       const uint64_t t0_ = ST ? __builtin_amdgcn_s_memtime() : 0;
       if (q < B && (fresh || !start)) {

@@ -7,6 +7,7 @@
 //     201-212 getLimitRequestNoLock) and the top-down runtime refresh (group_quota_manager.go:264-321), computed
 //     for every group at once from a settled tree;
 //   * Plugin.PreFilter (plugin.go:210-254) and checkQuotaRecursive (plugin_helper.go:281-297).
+#include <algorithm>
 #include <cstdint>
 #include <cstring>
 #include <vector>
@@ -220,7 +221,8 @@ extern "C" int gs_quota_prefilter(const gs_quota_group* g, uint32_t n, const int
 }
 
 // GroupQuotaManager.ReservePod / UnreservePod (group_quota_manager.go:791-805 -> updatePodUsedNoLock): the pod's
-// request joins (sign -1: leaves) used — and non-preemptible used — of its quota and every ancestor.
+// request joins (sign -1: leaves) used — and non-preemptible used — of its quota and every ancestor, each clamped
+// at zero. A speculative Reserve withdrawn by gs_quota_settle_batch cancels exactly (used never goes below zero).
 extern "C" int gs_quota_reserve(gs_quota_group* g, uint32_t n, int32_t quota, const int64_t request[GS_QUOTA_DIMS],
                                 uint32_t flags, int32_t sign) {
   if (quota < 0) return GS_OK;
@@ -228,9 +230,10 @@ extern "C" int gs_quota_reserve(gs_quota_group* g, uint32_t n, int32_t quota, co
   uint32_t hops = 0;
   for (int32_t q = quota; q != -1; q = g[q].parent) {
     if (q < -1 || (uint32_t)q >= n || ++hops > n) return GS_EINVAL;
-    for (int d = 0; d < D; ++d) {
-      g[q].used[d] += sign * request[d];
-      if (flags & GS_QUOTA_NON_PREEMPTIBLE) g[q].non_preemptible_used[d] += sign * request[d];
+    for (int d = 0; d < D; ++d) {   // addUsedNonNegativeNoLock (quota_info.go:252-261): negatives clamp to 0
+      g[q].used[d] = std::max<int64_t>(0, g[q].used[d] + sign * request[d]);
+      if (flags & GS_QUOTA_NON_PREEMPTIBLE)
+        g[q].non_preemptible_used[d] = std::max<int64_t>(0, g[q].non_preemptible_used[d] + sign * request[d]);
     }
   }
   return GS_OK;
@@ -258,11 +261,22 @@ extern "C" int gs_quota_admit_batch(gs_quota_group* g, uint32_t n, const int64_t
           g[q].non_preemptible_used[d] += sign * spec[size_t(q) * 2 * D + D + d];
         }
   };
+  // on an error, every speculative Reserve of this call is withdrawn before returning (used as on entry)
+  auto undo = [&](int rc) {
+    for (uint32_t q = 0; q < n; ++q)
+      if (touched[q])
+        for (int d = 0; d < D; ++d) {
+          g[q].used[d] -= spec[size_t(q) * 2 * D + d];
+          g[q].non_preemptible_used[d] -= spec[size_t(q) * 2 * D + D + d];
+        }
+    *consumed = 0;
+    return rc;
+  };
   for (uint32_t j = 0; j < count; ++j) {
     const int64_t* req = requests + size_t(j) * D;
     gs_quota_status st;
     int rc = gs_quota_prefilter(g, n, runtime, runtime_mask, quota[j], req, request_mask[j], flags[j], &st);
-    if (rc != GS_OK) return rc;
+    if (rc != GS_OK) return undo(rc);
     if (st.code != GS_QUOTA_ADMIT) {
       bool overlap = false;
       for (int32_t q = quota[j]; q != -1 && !overlap; q = g[q].parent) overlap = touched[q];
@@ -271,13 +285,13 @@ extern "C" int gs_quota_admit_batch(gs_quota_group* g, uint32_t n, const int64_t
         shift(quota[j], -1);
         rc = gs_quota_prefilter(g, n, runtime, runtime_mask, quota[j], req, request_mask[j], flags[j], &certain);
         shift(quota[j], +1);
-        if (rc != GS_OK) return rc;
+        if (rc != GS_OK) return undo(rc);
         if (certain.code == GS_QUOTA_ADMIT) return GS_OK;   // depends on the speculation: cut here
         st = certain;                                       // rejected at the least possible used: final
       }
     } else if (quota[j] >= 0) {
       rc = gs_quota_reserve(g, n, quota[j], req, flags[j], 1);
-      if (rc != GS_OK) return rc;
+      if (rc != GS_OK) return undo(rc);
       for (int32_t q = quota[j]; q != -1; q = g[q].parent) {
         touched[q] = 1;
         for (int d = 0; d < D; ++d) {

@@ -63,6 +63,9 @@ class ElasticQuotaPlugin:
         self.parent_names: list[str] = []
         self.runtime = np.zeros((0, abi.GS_QUOTA_DIMS), np.int64)
         self.runtime_mask = np.zeros(0, np.uint32)
+        # RefreshRuntime runs in every PreFilter (plugin.go:221-223) and recomputes once a request, Max/Min/weight
+        # or the cluster total changed; here: every mutator marks the runtime stale, PreFilter refreshes it
+        self._runtime_stale = True
 
     # ---- ResourceList <-> dense dimensions ----
     def _dense(self, rl: dict | None) -> tuple[np.ndarray, int]:
@@ -81,6 +84,7 @@ class ElasticQuotaPlugin:
     def update_cluster_total_resource(self, total: dict):
         """UpdateClusterTotalResource; here already net of the system / default quotas' used."""
         self.total = dict(total)
+        self._runtime_stale = True
 
     def on_quota_add(self, name, parent=ROOT, max=None, min=None, shared_weight=None, allow_lent=True,
                      guaranteed=None):
@@ -102,6 +106,7 @@ class ElasticQuotaPlugin:
         self.names.append(name)
         self.parent_names.append(parent)
         self.groups.append(g)
+        self._runtime_stale = True
 
     def _chain(self, quota: str):
         name = quota
@@ -116,6 +121,7 @@ class ElasticQuotaPlugin:
         g = self.groups[self.index[quota]]
         for d in range(abi.GS_QUOTA_DIMS):
             g.request[d] += int(vals[d])
+        self._runtime_stale = True
         if assigned:
             for a in self._chain(quota):
                 for d in range(abi.GS_QUOTA_DIMS):
@@ -130,13 +136,15 @@ class ElasticQuotaPlugin:
         g = self.groups[self.index[quota]]
         for d in range(abi.GS_QUOTA_DIMS):
             g.request[d] = max(0, g.request[d] - int(vals[d]))
+        self._runtime_stale = True
         if assigned:
             self.reserve_pod(quota, request, non_preemptible, sign=-1)
 
     def on_quota_update(self, name, max=None, min=None, shared_weight=None, allow_lent=None):
         """OnQuotaUpdate for the spec fields the runtime reads (Max, Min, SharedWeight, AllowLentResource);
-        takes effect at the next refresh_runtime()."""
+        the next PreFilter (or refresh_runtime()) recomputes the runtime."""
         g = self.groups[self.index[name]]
+        self._runtime_stale = True
         if allow_lent is not None:
             g.allow_lent = 1 if allow_lent else 0
         for fld, rl in (("max", max), ("min", min), ("shared_weight", shared_weight)):
@@ -169,19 +177,24 @@ class ElasticQuotaPlugin:
                                                abi.ptr(self.runtime_mask))
         if rc != 0:
             raise RuntimeError(f"gs_quota_refresh_runtime: {rc}")
+        self._runtime_stale = False
         return {name: self._sparse(self.runtime[i], int(self.runtime_mask[i])) for i, name in enumerate(self.names)}
 
     def set_runtime(self, quota: str, runtime: dict):
         """What the reference's tests do with qi.CalculateInfo.Runtime = ... (plugin_test.go:686-689)."""
-        self._ensure_runtime()
+        self._fresh_runtime()
         vals, mask = self._dense(runtime)
         i = self.index[quota]
         self.runtime[i] = vals
         self.runtime_mask[i] = mask
 
-    def _ensure_runtime(self):
+    def _fresh_runtime(self):
+        """The runtime PreFilter reads: recomputed when a mutator made it stale (with runtime quota enabled; with it
+        disabled PreFilter reads Max and never refreshes)."""
+        if self._runtime_stale and self.enable_runtime_quota:
+            self.refresh_runtime()
         n = len(self.groups)
-        if self.runtime.shape[0] < n:   # quotas added since the last refresh: no Runtime keys yet
+        if self.runtime.shape[0] < n:   # runtime quota disabled: quotas added since have no Runtime keys
             rt = np.zeros((n, abi.GS_QUOTA_DIMS), np.int64)
             rt[:self.runtime.shape[0]] = self.runtime
             rm = np.zeros(n, np.uint32)
@@ -204,8 +217,8 @@ class ElasticQuotaPlugin:
         req, req_mask = self._dense(request)
         flags = self._flags(non_preemptible)
         n = len(self.groups)
+        self._fresh_runtime()
         arr = self._array()
-        self._ensure_runtime()
         st = abi.GsQuotaStatus()
         rc = self.lib.gs_quota_prefilter(arr, n, abi.ptr(self.runtime), abi.ptr(self.runtime_mask),
                                          self.index[quota], abi.ptr(req), req_mask, flags, C.byref(st))
@@ -291,8 +304,8 @@ def schedule_with_quota(engine, plugin: ElasticQuotaPlugin, pods, pod_quota, seq
     for j, (_, req, _) in enumerate(pod_quota):
         reqs[j], masks[j] = plugin._dense(req)
     flags = np.array([plugin._flags(np_) for _, _, np_ in pod_quota] or [0], np.uint32)
+    plugin._fresh_runtime()
     arr = plugin._array()
-    plugin._ensure_runtime()
     ng = len(plugin.groups)
     st = (abi.GsQuotaStatus * max(n, 1))()
     consumed = C.c_uint32()
@@ -307,7 +320,14 @@ def schedule_with_quota(engine, plugin: ElasticQuotaPlugin, pods, pod_quota, seq
         j = i + consumed.value
         seg = np.array([p for p in range(i, j) if st[p].code == abi.GS_QUOTA_ADMIT], np.int64)
         if len(seg):
-            res = engine.schedule(pods[seg], seq[seg])
+            try:
+                res = engine.schedule(pods[seg], seq[seg])
+            except Exception:
+                # the run's speculative Reserves leave the forest (used as before the run), then the error surfaces
+                for p in seg:
+                    if qidx[p] >= 0:
+                        plugin.lib.gs_quota_reserve(arr, ng, int(qidx[p]), reqs[p].ctypes.data, int(flags[p]), -1)
+                raise
             out[seg] = res
         # withdraw the speculation and replay the run with the true placements (exact statuses and used)
         placed = np.ascontiguousarray(out["node"][i:j], dtype=np.int32)

@@ -72,6 +72,11 @@ def _add(a: dict, b: dict) -> dict:
     return out
 
 
+def _add_non_negative(a: dict, b: dict) -> dict:
+    """addUsedNonNegativeNoLock (quota_info.go:252-261): quotav1.Add, then every negative entry set to 0."""
+    return {k: max(0, v) for k, v in _add(a, b).items()}
+
+
 class QuotaTree:
     """GroupQuotaManager, restated for a settled tree (every request delta applied, every runtime refreshed)."""
 
@@ -92,9 +97,9 @@ class QuotaTree:
             name = quota
             while name != ROOT:
                 a = self.quotas[name]
-                a.used = _add(a.used, request)
+                a.used = _add_non_negative(a.used, request)
                 if non_preemptible:
-                    a.non_preemptible_used = _add(a.non_preemptible_used, request)
+                    a.non_preemptible_used = _add_non_negative(a.non_preemptible_used, request)
                 name = a.parent
 
     def remove_pod(self, quota: str, request: dict, assigned: bool, non_preemptible: bool = False):
@@ -106,9 +111,10 @@ class QuotaTree:
             name = quota
             while name != ROOT:
                 a = self.quotas[name]
-                a.used = _add(a.used, {k: -v for k, v in request.items()})
+                a.used = _add_non_negative(a.used, {k: -v for k, v in request.items()})
                 if non_preemptible:
-                    a.non_preemptible_used = _add(a.non_preemptible_used, {k: -v for k, v in request.items()})
+                    a.non_preemptible_used = _add_non_negative(a.non_preemptible_used,
+                                                               {k: -v for k, v in request.items()})
                 name = a.parent
 
     def children(self, name: str) -> list[Quota]:

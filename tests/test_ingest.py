@@ -49,7 +49,7 @@ def test_golden_cpuset_parse(case):
 QUANTITIES = [
     ("1", 1, 1000), ("100m", 1, 100), ("1500m", 2, 1500), ("1.5", 2, 1500), ("0.0001", 1, 1), ("0", 0, 0),
     ("1Ki", 1024, 1024000), ("1Gi", 1 << 30, (1 << 30) * 1000), ("16Gi", 16 << 30, (16 << 30) * 1000),
-    ("5G", 5 * 10**9, 5 * 10**12), ("1e3", 1000, 10**6), ("1E-3", 1, 1), ("-1.5", -1, -1500), ("+2", 2, 2000),
+    ("5G", 5 * 10**9, 5 * 10**12), ("1e3", 1000, 10**6), ("1E-3", 1, 1), ("-0", 0, 0), ("+2", 2, 2000),
     ("128974848", 128974848, 128974848000), ("129e6", 129 * 10**6, 129 * 10**9), ("123Mi", 123 << 20, (123 << 20) * 1000),
     ("0.5Ki", 512, 512000), ("1n", 1, 1), ("250u", 1, 1), ("3k", 3000, 3 * 10**6), (".5", 1, 500),
 ]
@@ -64,6 +64,16 @@ def test_quantity(text, value, milli):
 def test_quantity_malformed(text):
     with pytest.raises(ingest.DecodeError):
         ingest.quantity(text)
+
+
+@pytest.mark.parametrize("text", ["-1.5", "-1", "-100m", "-1Ki", "-0.5"])
+def test_quantity_negative_refused(text):
+    """Negative quantities: apimachinery rounds an inexact negative Value() one way on its int64Amount path and
+    another on its inf.Dec path; no valid request / allocatable / annotation is negative, so the decoder refuses
+    them (parity unpinned: no reference fixture holds a negative quantity)."""
+    with pytest.raises(ingest.DecodeError) as e:
+        ingest.quantity(text)
+    assert e.value.rc == abi.GS_EUNSUPPORTED
 
 
 def test_quantity_outside_int64():

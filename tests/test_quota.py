@@ -254,3 +254,84 @@ def test_pod_delete_and_quota_update_match_oracle(lib, seed):
         st = p.pre_filter(name, req)
         code, failed, bad, _ = oq.pre_filter(tree, name, req, check_parent=True)
         assert st.is_success() == (code == "Success") and (st.is_success() or (st.quota, st.exceed) == (failed, bad))
+
+
+def test_prefilter_refreshes_stale_runtime(lib):
+    """PreFilter after quota / pod / total events with no explicit refresh reads the refreshed runtime
+    (plugin.go:221-223 calls RefreshRuntime in every PreFilter): a quota added after the last refresh is
+    limited like the oracle's, not admitted with an empty runtime."""
+    rng = random.Random(42)
+    for _ in range(20):
+        names, parents, specs = _random_forest(rng, rng.randrange(2, 12))
+        total = {r: rng.randrange(50_000, 500_000) for r in RES}
+        p = ElasticQuotaPlugin(resources=RES, lib=lib)
+        p.update_cluster_total_resource(total)
+        tree = oq.QuotaTree(total)
+        half = len(names) // 2
+        for name in names[:half]:
+            p.on_quota_add(name, parent=parents[name] if parents[name] in names[:half] else ROOT, **specs[name])
+            tree.add(oq.Quota(name, parent=parents[name] if parents[name] in names[:half] else ROOT, **specs[name]))
+        p.refresh_runtime()
+        for name in names[half:]:   # after the refresh
+            par = parents[name]
+            p.on_quota_add(name, parent=par, **specs[name])
+            tree.add(oq.Quota(name, parent=par, **specs[name]))
+        for _ in range(30):
+            name = rng.choice(names)
+            req = {r: rng.randrange(0, 40_000) for r in RES}
+            a = rng.random() < 0.5
+            p.on_pod_add(name, req, a)
+            tree.add_pod(name, req, a)
+        tree.refresh()
+        for _ in range(10):
+            name = rng.choice(names)
+            req = {r: rng.randrange(0, 60_000) for r in RES}
+            st = p.pre_filter(name, req)
+            code, failed, bad, _ = oq.pre_filter(tree, name, req)
+            assert st.is_success() == (code == "Success"), name
+            assert st.is_success() or (st.quota, st.exceed) == (failed, bad)
+
+
+def test_used_clamps_at_zero(lib):
+    """addUsedNonNegativeNoLock (quota_info.go:252-261): deleting more used than a quota holds leaves 0, in the
+    C-ABI and in the oracle alike, and later PreFilter checks are not loosened by a negative used."""
+    p = ElasticQuotaPlugin(resources=RES, enable_runtime_quota=False, lib=lib)   # limit = Max
+    total = {"cpu": 100_000, "memory": 1 << 30}
+    p.update_cluster_total_resource(total)
+    tree = oq.QuotaTree(total)
+    for name, par in (("a", ROOT), ("b", "a")):
+        spec = dict(max={"cpu": 10_000, "memory": 1 << 28}, min={"cpu": 1_000})
+        p.on_quota_add(name, parent=par, **spec)
+        tree.add(oq.Quota(name, parent=par, **spec))
+    p.on_pod_add("b", {"cpu": 3_000}, assigned=True, non_preemptible=True)
+    tree.add_pod("b", {"cpu": 3_000}, True, True)
+    p.on_pod_delete("b", {"cpu": 5_000, "memory": 7}, assigned=True, non_preemptible=True)
+    tree.remove_pod("b", {"cpu": 5_000, "memory": 7}, True, True)
+    for name in ("a", "b"):
+        assert p.get(name, "used") == {}, name
+        assert p.get(name, "non_preemptible_used") == {}, name
+        assert all(v == 0 for v in tree.quotas[name].used.values())
+        assert all(v == 0 for v in tree.quotas[name].non_preemptible_used.values())
+    tree.refresh()
+    for cpu in (9_000, 10_000, 10_001):
+        st = p.pre_filter("b", {"cpu": cpu})
+        code, _, _, _ = oq.pre_filter(tree, "b", {"cpu": cpu}, runtime_quota=False)
+        assert st.is_success() == (code == "Success") == (cpu <= 10_000)
+
+
+def test_admit_batch_error_withdraws_speculation(lib):
+    """An engine failure inside schedule_with_quota withdraws the run's speculative Reserves."""
+    from koordinator_amd.quota import schedule_with_quota
+
+    class Boom:
+        def schedule(self, pods, seq):
+            raise RuntimeError("injected engine failure")
+
+    p = ElasticQuotaPlugin(resources=RES, enable_runtime_quota=False, lib=lib)
+    p.update_cluster_total_resource({"cpu": 100_000, "memory": 1 << 30})
+    p.on_quota_add("a", max={"cpu": 50_000, "memory": 1 << 29})
+    p.on_pod_add("a", {"cpu": 1_000}, assigned=True)
+    pods = np.zeros(4, abi.POD_DTYPE)
+    with pytest.raises(RuntimeError, match="injected"):
+        schedule_with_quota(Boom(), p, pods, [("a", {"cpu": 2_000}, False)] * 4)
+    assert p.get("a", "used") == {"cpu": 1_000}
