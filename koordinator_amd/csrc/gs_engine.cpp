@@ -737,6 +737,7 @@ CommitArgs commit_args(gs_ctx* c, int b) {
   a.own0 = c->n0;
   a.own1 = c->n1;
   a.S = c->nranks == 1 ? c->d_S : nullptr;
+  a.S_own = c->d_S;
   a.window_k = c->window_k;
   a.start = c->next_start;
   a.nnodes = c->N;
@@ -1053,8 +1054,8 @@ int gs_create(const gs_config* cfg, gs_ctx** out) {
       if ((e = hipEventCreate(&ev)) != hipSuccess) return bail("hipEventCreate", e);
   }
   if (getenv("GS_COMMIT_STAMPS") && getenv("GS_COMMIT_STAMPS")[0] == '1') {
-    if ((e = hipMalloc(&c->d_stamps, 8 * 25)) != hipSuccess) return bail("hipMalloc", e);
-    (void)hipMemset(c->d_stamps, 0, 200);
+    if ((e = hipMalloc(&c->d_stamps, 8 * 32)) != hipSuccess) return bail("hipMalloc", e);
+    (void)hipMemset(c->d_stamps, 0, 256);
   }
   if ((e = hipDeviceSynchronize()) != hipSuccess) return bail("hipDeviceSynchronize", e);
   // 96 B (LoadAware + Fit row), + 192 B NodeNUMAResource columns when enabled
@@ -1066,21 +1067,14 @@ int gs_create(const gs_config* cfg, gs_ctx** out) {
 int gs_destroy(gs_ctx* c) {
   if (!c) return GS_EINVAL;
   if (c->d_stamps) {
-    uint64_t st[25] = {};
-    if (hipMemcpy(st, c->d_stamps, 200, hipMemcpyDeviceToHost) == hipSuccess) {
+    uint64_t st[32] = {};
+    if (hipMemcpy(st, c->d_stamps, 256, hipMemcpyDeviceToHost) == hipSuccess) {
       uint64_t tot = 0;
       for (int i = 0; i < 12; ++i) tot += st[i];
       fprintf(stderr, "gpuscore commit phases (s_memtime ticks, %% of %llu):", (unsigned long long)tot);
       for (int i = 0; i < 12; ++i) fprintf(stderr, " p%d=%.1f%%", i, tot ? 100.0 * st[i] / tot : 0.0);
       fprintf(stderr, " | policy-row rescoring: %llu pods, %.0f ticks per pair (thread 128)\n",
               (unsigned long long)st[12], st[12] ? (double)st[13] / st[12] : 0.0);
-      fprintf(stderr, "  numa_eval segments per pair: prelim %.0f hints %.0f merge %.0f alloc %.0f cpuset %.0f score %.0f\n",
-              st[12] ? (double)st[14] / st[12] : 0.0, st[12] ? (double)st[15] / st[12] : 0.0,
-              st[12] ? (double)st[16] / st[12] : 0.0, st[12] ? (double)st[17] / st[12] : 0.0,
-              st[12] ? (double)st[18] / st[12] : 0.0, st[12] ? (double)st[19] / st[12] : 0.0);
-      fprintf(stderr, "  merge paths of those pairs: fast %llu, preferred pass %llu, full pass %llu, wave with a full pass %llu\n",
-              (unsigned long long)st[20], (unsigned long long)st[21], (unsigned long long)st[22],
-              (unsigned long long)st[23]);
       fprintf(stderr, "  header staging (inside p0): %.1f%%\n", tot ? 100.0 * st[24] / tot : 0.0);
     }
     (void)hipFree(c->d_stamps);

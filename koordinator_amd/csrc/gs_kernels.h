@@ -85,6 +85,7 @@ struct CommitArgs {
   uint32_t ld;
   uint32_t own0, own1;       // this rank's shard [own0, own1)
   const int16_t* S;          // batch-start score rows (one shard only: in-kernel full-row resolution; else nullptr)
+  const int16_t* S_own;      // this rank's batch-start score rows (batch-start scores of fresh own-shard rows)
   const int32_t* prev;       // speculative pass: the previous batch's committed[4]; run only if prev[1] == 1
   // node sampling (gs_config.sample_nodes, one shard): window_k = numFeasibleNodesToFind(N) (0 = every node);
   // the batch starts at nextStartNodeIndex `start` (prev[2] for a speculative pass) and leaves it in committed[2]

@@ -134,9 +134,10 @@ struct SlotsLds {
 // LDS_SCALARS: scalar free columns come from r.free[3..6] (the commit's LDS copy) instead of HBM.
 // NUMA_POLICY_NODES = false: NodeNUMAResource's topology-policy path is compiled out (eval_kernel routes those
 // nodes to eval_numa_kernel)
-template <bool FULL, bool LDS_SCALARS, bool NUMA_POLICY_NODES = true>
+// table: the row's NUMA hint table (commit re-scoring of one row for many pods), else computed from the row.
+template <bool FULL, bool LDS_SCALARS, bool NUMA_POLICY_NODES = true, bool TABLE = false>
 __device__ __forceinline__ PairOut eval_pair(const Row& r, const PodVec& p, const Profile& pf, const MirrorView& m,
-                                             uint64_t* prof = nullptr) {
+                                             const HintTable* table = nullptr) {
   PairOut o{0u, 0, 0, 0, 0u};
   // ---- [upstream] noderesources Fit.Filter -> fitsRequest
   if (pf.enabled & 0x1u) {
@@ -163,8 +164,8 @@ __device__ __forceinline__ PairOut eval_pair(const Row& r, const PodVec& p, cons
   // ---- NodeNUMAResource Filter (+ Admit) and Score (gs_numa_dev.h)
   if (pf.enabled & 0x30u) {
     NumaOut no;
-    if (LDS_SCALARS) no = numa_eval<NUMA_POLICY_NODES>(r.nr, p, pf, SlotsLds{r, m}, pf.enabled & 0x10u, pf.enabled & 0x20u,
-                                                       -1, prof);
+    if (LDS_SCALARS) no = numa_eval<NUMA_POLICY_NODES, TABLE>(r.nr, p, pf, SlotsLds{r, m}, pf.enabled & 0x10u,
+                                                              pf.enabled & 0x20u, -1, table);
     else no = numa_eval<NUMA_POLICY_NODES>(r.nr, p, pf, SlotsHbm{r, m}, pf.enabled & 0x10u, pf.enabled & 0x20u);
     if (pf.enabled & 0x10u) o.code |= no.reason << GS_FAIL_NUMA_SHIFT;
     if (!FULL && o.code) return o;
@@ -481,8 +482,8 @@ constexpr int WIN = 2 * MAX_BATCH + 8;
 #define WAVE_FENCE() __builtin_amdgcn_wave_barrier()
 
 __device__ __forceinline__ int32_t row_score(const Row& d, const PodVec& p, const Profile& pf, const MirrorView& m,
-                                             uint64_t* prof = nullptr) {
-  return total_score(eval_pair<false, true>(d, p, pf, m, prof), pf);
+                                             const HintTable* table = nullptr) {
+  return total_score(eval_pair<false, true, true, true>(d, p, pf, m, table), pf);
 }
 
 __device__ __forceinline__ int hash_find(const int32_t* hkey, const int32_t* hval, uint32_t node) {
@@ -573,7 +574,6 @@ __device__ __noinline__ bool cpuset_reserve(const TopoDev& t, CpuStateDev& cs, c
 template <bool ST>
 __global__ void __launch_bounds__(256) commit_kernel(CommitArgs a) {
   uint64_t st_acc[14] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-  uint64_t np_acc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
   uint64_t st_stage = 0;                      // header staging cycles (inside p0)   // numa_eval segments of thread 128's policy-row rescoring (ST)
   uint64_t st_last = ST ? __builtin_amdgcn_s_memtime() : 0;
 #define STAMP(i)                                    \
@@ -618,6 +618,7 @@ __global__ void __launch_bounds__(256) commit_kernel(CommitArgs a) {
   __shared__ int s_topo_id;
   __shared__ int s_aff;                                // known affinity of pod k on its winner row (-1: recompute)
   __shared__ uint64_t s_cpuset[4];                     // CPUs of a device-side cpuset Reserve
+  __shared__ HintTable s_ht, s_ht2;                    // NUMA hint sums of the winner row (new / batch-start state)
   const bool numa_on = (a.pf.enabled & 0x30u) != 0;
   // speculative pass queued behind another batch: only if that one committed every pod with nothing left for
   // the host (committed[1] == 1); otherwise a no-op (committed = -1) the host discards
@@ -1120,21 +1121,28 @@ __global__ void __launch_bounds__(256) commit_kernel(CommitArgs a) {
         if (tid == 0) s_topo_id = tp;
       }
     }
+    const int wv = __builtin_amdgcn_readfirstlane(wave);
+    if (wv == 0 && numa_on && s_aff < 0) {   // hint table of the winner's pre-Reserve state (affinity unknown)
+      const NumaRow nr = fresh ? orow.nr : d.nr;
+      if ((nr.nflags >> NF_POLICY_SHIFT) & 3u) hint_table_fill(s_ht, nr, zone_avail(nr), lane);
+      WAVE_FENCE();
+    }
     if (tid == 0) {
-      if (fresh) d = orow;
+      const Row dr = fresh ? orow : d;   // registers: the Reserve's pair evaluation re-reads row words
+      if (fresh) d = dr;
       const PodVec& pk = pods(k);
       const bool forced = k == s_fk;
       PlacementDev pl{(int32_t)s_winner, (uint32_t)s_F, (int64_t)s_M, (uint32_t)s_T, forced ? 1u : 0u, 0, 0,
                       {0, 0, 0, 0}, {0, 0, 0, 0}};
       s_cut = 0;
-      const uint32_t nf = d.nr.nflags;
+      const uint32_t nf = dr.nr.nflags;
       // Reserve returns at once unless requestCPUBind (util.go:105-122) or the node has a NUMA policy
       const bool maybe_rb = (pk.numa & PN_BIND) || (((nf >> NF_BIND_SHIFT) & 3u) && (pk.req_keys & 1u) && pk.req[0]);
       if (numa_on && !(pk.numa & (PN_SKIP | PN_PREFAIL)) && (maybe_rb || ((nf >> NF_POLICY_SHIFT) & 3u))) {
         // NodeNUMAResource Reserve (plugin.go:375-422) on the pre-assume row: the Filter-time affinity and the
         // NUMA split of Allocate; a cpuset pod's CPUs are selected here (gs_cpuset_dev.h) when the node's
         // topology is in the device scope, else the batch ends with it and the host selects them
-        NumaOut no = numa_eval(d.nr, pk, a.pf, SlotsLds{d, m}, a.pf.enabled & 0x10u, false, s_aff);
+        NumaOut no = numa_eval<true, true>(dr.nr, pk, a.pf, SlotsLds{dr, m}, a.pf.enabled & 0x10u, false, s_aff, &s_ht);
         STAMP(10);
         const bool rb = no.flags & GS_PLACED_CPUSET;
         if (no.reason) pl.flags |= PL_RESERVE_FAILED;   // cannot happen for a feasible winner
@@ -1144,15 +1152,17 @@ __global__ void __launch_bounds__(256) commit_kernel(CommitArgs a) {
 #pragma unroll
           for (int z = 0; z < 4; ++z) { pl.zcpu[z] = no.zcpu[z]; pl.zmem[z] = no.zmem[z]; }
           if (nf & NF_TOPO_VALID) {   // resourceManager.Update -> NodeAllocation.addPodAllocation
+            uint32_t f2 = dr.nr.nflags2;
 #pragma unroll
             for (int z = 0; z < 4; ++z) {
               const bool zc = no.zkeys >> z & 1u, zm = no.zkeys >> (4 + z) & 1u;
               if (!zc && !zm) continue;
-              d.nr.zraw_cpu[z] += no.zcpu[z];
-              d.nr.zraw_mem[z] += no.zmem[z];
-              d.nr.nflags2 |= (1u << (NF2_ENTRY_SHIFT + z)) | (zc ? 1u << (NF2_ACPU_SHIFT + z) : 0u) |
-                              (zm ? 1u << (NF2_AMEM_SHIFT + z) : 0u);
+              d.nr.zraw_cpu[z] = dr.nr.zraw_cpu[z] + no.zcpu[z];
+              d.nr.zraw_mem[z] = dr.nr.zraw_mem[z] + no.zmem[z];
+              f2 |= (1u << (NF2_ENTRY_SHIFT + z)) | (zc ? 1u << (NF2_ACPU_SHIFT + z) : 0u) |
+                    (zm ? 1u << (NF2_AMEM_SHIFT + z) : 0u);
             }
+            d.nr.nflags2 = f2;
           }
           if (rb) {
             CpuStateDev& cs = cst[slot];
@@ -1173,32 +1183,54 @@ __global__ void __launch_bounds__(256) commit_kernel(CommitArgs a) {
         }
       }
       a.out[k] = pl;
-      for (int s = 0; s < 7; ++s) d.free[s] -= pk.req[s];
-      d.nzfree[0] -= pk.nz[0];
-      d.nzfree[1] -= pk.nz[1];
-      d.free_pods -= 1;
-      d.la_free[0] -= pk.est[0];
-      d.la_free[1] -= pk.est[1];
+      for (int s = 0; s < 7; ++s) d.free[s] = dr.free[s] - pk.req[s];
+      d.nzfree[0] = dr.nzfree[0] - pk.nz[0];
+      d.nzfree[1] = dr.nzfree[1] - pk.nz[1];
+      d.free_pods = dr.free_pods - 1;
+      d.la_free[0] = dr.la_free[0] - pk.est[0];
+      d.la_free[1] = dr.la_free[1] - pk.est[1];
       if (pk.flags & PF_PROD) {
-        d.la_pfree[0] -= pk.est[0];
-        d.la_pfree[1] -= pk.est[1];
+        d.la_pfree[0] = dr.la_pfree[0] - pk.est[0];
+        d.la_pfree[1] = dr.la_pfree[1] - pk.est[1];
       }
+    }
+    // NUMA-policy winner row: wave 0 builds the hint table of its new state (one entry per lane) for the
+    // re-scoring lanes; wave 1 that of a fresh row's batch-start state when its batch-start scores are evaluated
+    // (a node outside this rank's shard)
+    if (wv == 0 && numa_on) {
+      WAVE_FENCE();
+      const uint32_t nfw = d.nr.nflags;
+      if ((nfw >> NF_POLICY_SHIFT) & 3u) {
+        const NumaRow nr = d.nr;
+        hint_table_fill(s_ht, nr, zone_avail(nr), lane);
+      }
+    } else if (wv == 1 && numa_on && fresh && !(orow.node >= a.own0 && orow.node < a.own1)) {
+      const NumaRow nr = orow.nr;
+      if ((nr.nflags >> NF_POLICY_SHIFT) & 3u) hint_table_fill(s_ht2, nr, zone_avail(nr), lane);
     }
     __syncthreads();
     if (s_cut) { committed = k + 1; host_cut = true; break; }
     if (tid == 0) STAMP(7);
-    // batch-start scores (fresh rows) on threads 0..127, current scores on threads 128..255; one call site,
-    // so the long pair evaluation exists once in the instruction cache
+    // Re-scoring, pods q = k+1 .. over 4 waves x 32: lanes 0..31 evaluate the winner row's current score
+    // (one row for all lanes: the NUMA hint sums come from the table); lanes 32..63 of a fresh row fetch its
+    // batch-start score from the score rows S when the node is in this rank's shard, else evaluate it.
     {
-      const bool start = __builtin_amdgcn_readfirstlane(wave) < 2;   // wave-uniform: the row goes scalar
-      const int q = k + 1 + (tid & 127);
+      const int sub = lane & 31;
+      const bool cur = lane < 32;
+      const int q = k + 1 + wv * 32 + sub;
       const uint64_t t0_ = ST ? __builtin_amdgcn_s_memtime() : 0;
-      if (q < B && (fresh || !start)) {
-        const Row rr = start ? orow : d;   // registers: the evaluation re-reads row words many times
-        uint64_t* np = (ST && tid == 128 && ((d.nr.nflags >> NF_POLICY_SHIFT) & 3u)) ? np_acc : nullptr;
-        (start ? dso : dsc)[q * B + slot] = (int16_t)row_score(rr, pods(q), a.pf, m, np);
+      const uint32_t node = d.node;
+      const bool own = node >= a.own0 && node < a.own1;
+      const bool load_so = !cur && fresh && own && q < B;
+      int16_t so = 0;
+      if (load_so) so = a.S_own[(size_t)q * a.ld + (node - a.own0)];
+      const bool policy_row = numa_on && ((d.nr.nflags >> NF_POLICY_SHIFT) & 3u);   // (ST stamps)
+      if (q < B && (cur || (fresh && !own))) {
+        const Row rr = cur ? d : orow;   // registers: the evaluation re-reads row words many times
+        (cur ? dsc : dso)[q * B + slot] = (int16_t)row_score(rr, pods(q), a.pf, m, cur ? &s_ht : &s_ht2);
       }
-      if (ST && tid == 128 && ((d.nr.nflags >> NF_POLICY_SHIFT) & 3u)) {
+      if (load_so) dso[q * B + slot] = so;
+      if (ST && tid == 128 && policy_row) {
         st_acc[12] += 1;
         st_acc[13] += __builtin_amdgcn_s_memtime() - t0_;
       }
@@ -1247,7 +1279,6 @@ __global__ void __launch_bounds__(256) commit_kernel(CommitArgs a) {
   if (ST && tid == 128) {
     a.stamps[12] += st_acc[12];
     a.stamps[13] += st_acc[13];
-    for (int i = 0; i < 10; ++i) a.stamps[14 + i] += np_acc[i];
   }
 #undef STAMP
 }

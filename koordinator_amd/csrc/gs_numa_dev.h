@@ -6,11 +6,20 @@
 //  * cpuset feasibility of allocateCPUSet is a count test: with the required-policy prefilter applied every
 //    available CPU lies in a full core (FullPCPUs) or on a distinct core (SpreadByPCPUs), and takeCPUs takes
 //    prefixes of core-ordered lists, so the result satisfies the policy iff per-zone counts are multiples of
-//    CPUsPerCore (FullPCPUs with a NUMA split) — which CPUs are picked is a host-side Reserve concern;
+//    CPUsPerCore (FullPCPUs with a NUMA split) — which CPUs are picked is a Reserve concern (gs_cpuset_dev.h);
 //  * NUMA hints are enumerated over zone-slot masks (zones sorted by node id, so slot masks order and
 //    intersect exactly like node-id masks) in bitmask.IterateBitMasks order; the hint lists of the single
 //    provider are merged in sorted resource-name order (cpu before memory; the reference iterates a Go map,
 //    policy.go:108 — see DESIGN.md) with mergeFilteredHints' exact update rule.
+//
+// SIMT shape. A hint list is a bitmap over the 15 positions of the 4-zone IterateBitMasks order (bitmask.go
+// :206-222): masks 1 2 4 8 | 3 5 9 6 10 12 | 7 11 13 14 | 15. For nz < 4 zones the order is the same sequence
+// with the masks >= 2^nz left out, so one position numbering serves every zone count, positions are sorted by
+// mask size, and single-zone masks sit at positions 0..3. The row-side sums a position needs (zone totals and
+// free amounts of its mask) come from a "hint source": HintRegs computes them from the row's per-zone values
+// (a thread owning a node row: eval kernels, Reserve); HintTable reads them from a table built once per row in
+// LDS (the commit kernel re-scores one row for many pods, one pod per lane). Everything per pod is compares
+// on those sums, so a lane's work does not grow with the number of masks the row has.
 #pragma once
 
 #include "../../include/gpuscore.h"
@@ -86,17 +95,8 @@ __device__ __forceinline__ int32_t numa_pct(int64_t x, int64_t cap) {
   else if (prod + cap <= num) ++q;
   return q;
 }
-// leastRequestedScore / mostRequestedScore (least_allocated.go:49-58, most_allocated.go:45-55)
-__device__ __forceinline__ int32_t lr_score(int64_t req, int64_t cap) {
-  if (cap == 0 || req > cap) return 0;
-  return numa_pct(cap - req, cap);
-}
-__device__ __forceinline__ int32_t mr_score(int64_t req, int64_t cap) {
-  if (cap == 0) return 0;
-  if (req > cap) req = cap;
-  return numa_pct(req, cap);
-}
-// either scorer with one division site (numa_eval inlines its scorers several times)
+// leastRequestedScore / mostRequestedScore (least_allocated.go:49-58, most_allocated.go:45-55) with one
+// division site
 __device__ __forceinline__ int32_t req_score(bool most, int64_t req, int64_t cap) {
   if (cap == 0 || (!most && req > cap)) return 0;
   return numa_pct(most ? (req > cap ? cap : req) : cap - req, cap);
@@ -108,37 +108,294 @@ __device__ __forceinline__ int32_t sdiv(int32_t a, int32_t b) {
   return q;
 }
 
-// IterateBitMasks order over zone slots (bitmask.go:206-222) for 1..4 zones, 4 bits per position:
-//   1 zone: 1 | 2 zones: 1 2 3 | 3 zones: 1 2 4 3 5 6 7 | 4 zones: 1 2 4 8 3 5 9 6 10 12 7 11 13 14 15
-__constant__ uint64_t kMaskOrderPacked[4] = {0x1ull, 0x321ull, 0x7653421ull, 0xFEDB7CA69538421ull};
-
+// ---- IterateBitMasks positions (4-zone order)
+constexpr uint64_t kOrd4 = 0xFEDB7CA69538421ull;   // position mi -> zone-slot mask, 4 bits per position
+__host__ __device__ constexpr uint32_t ord_mask(int mi) { return (uint32_t)(kOrd4 >> (4 * mi)) & 15u; }
+// positions present for nz zones (masks < 2^nz): nz = 1..4
+__device__ __forceinline__ uint32_t ord_valid(int nz) {
+  return nz >= 4 ? 0x7FFFu : nz == 3 ? 0x4B7u : nz == 2 ? 0x13u : nz == 1 ? 0x1u : 0u;
+}
+// mask size of the first position of a non-empty position set (positions are sorted by mask size)
+__device__ __forceinline__ int ord_size_first(uint32_t pos) {
+  const int mi = __ffs(pos) - 1;
+  return mi < 4 ? 1 : mi < 10 ? 2 : mi < 14 ? 3 : 4;
+}
 __device__ __forceinline__ bool narrower(uint32_t a, uint32_t b) {   // bitmask.IsNarrowerThan
   int ca = __popc(a), cb = __popc(b);
   return ca == cb ? a < b : ca < cb;
 }
 
+// Row-side sums of one position: zone totals of the zones listing cpu / memory, and the available (free) amounts
+// of all the mask's zones (cpu after trimNUMANodeResources for the pod's bind policy, see HintVariant).
+struct HintSums {
+  int64_t tc, tm, fc, fm;
+};
+// trimNUMANodeResources (resource_manager.go:140-169) variants of the available cpu per zone: 0 untrimmed (no
+// required bind policy), 1 FullPCPUs, 2 SpreadByPCPUs, 3 another required policy (raw count)
+__device__ __forceinline__ int hint_variant(bool reqflag, int bind) {
+  return !reqflag ? 0 : bind == BIND_FULL ? 1 : bind == BIND_SPREAD ? 2 : 3;
+}
+
+// Per-zone availability of a NUMA-policy row (numa_eval's av_cpu / av_mem / key bits): zone capacity minus the
+// allocated resources of NodeAllocation (cpu amplified by the zone adjustment), floored at 0.
+struct ZoneAvail {
+  int64_t av_cpu[4], av_mem[4];
+  uint32_t avk;   // bit z: allocatable has a cpu key in zone z, bit 4+z: memory key
+};
+__device__ __forceinline__ ZoneAvail zone_avail(const NumaRow& r) {
+  ZoneAvail a;
+  const uint32_t nf = r.nflags, nf2 = r.nflags2;
+  const int nz = (nf >> NF_ZONES_SHIFT) & 7;
+  const double amp = r.amp;
+  a.avk = 0;
+#pragma unroll
+  for (int z = 0; z < 4; ++z) {
+    a.av_cpu[z] = a.av_mem[z] = 0;
+    if (z >= nz) continue;
+    const bool entry = nf2 >> (NF2_ENTRY_SHIFT + z) & 1u;
+    const bool ccpu = nf >> (NF_ZCPU_SHIFT + z) & 1u, cmem = nf >> (NF_ZMEM_SHIFT + z) & 1u;
+    const bool acpu = entry && ((nf2 >> (NF2_ACPU_SHIFT + z) & 1u) || amp > 1.0);
+    const bool amem = entry && (nf2 >> (NF2_AMEM_SHIFT + z) & 1u);
+    const int64_t ac = entry ? r.zraw_cpu[z] + (amp > 1.0 ? (int64_t)r.zadj[z] : 0) : 0;
+    const int64_t am = entry ? r.zraw_mem[z] : 0;
+    if (ccpu) a.av_cpu[z] = r.zcap_cpu[z] - ac > 0 ? r.zcap_cpu[z] - ac : 0;
+    if (cmem) a.av_mem[z] = r.zcap_mem[z] - am > 0 ? r.zcap_mem[z] - am : 0;
+    if (ccpu || acpu) a.avk |= 1u << z;
+    if (cmem || amem) a.avk |= 1u << (4 + z);
+  }
+  return a;
+}
+// available cpu of zone z in variant v (trimNUMANodeResources: min(available, usable CPUs x 1000))
+__device__ __forceinline__ int64_t trimmed_cpu(int64_t av, uint32_t zfree, int v) {
+  if (v == 0 || av == 0) return av;
+  const int raw = cnt_raw(zfree);
+  int n = raw;
+  if (v != 3 && (int64_t)raw * 1000 >= av) n = v == 1 ? (int)((zfree >> 9) & 511u) : (int)((zfree >> 18) & 511u);
+  return (int64_t)n * 1000 < av ? (int64_t)n * 1000 : av;
+}
+
+// Hint source over a row in registers: sums of a position's zones computed from per-zone values.
+struct HintRegs {
+  int64_t zc[4], zm[4], hc[4], hm[4];   // zone totals (listed zones, else 0), available cpu (variant), memory
+  __device__ HintSums sum(int mi) const {
+    const uint32_t mk = ord_mask(mi);
+    HintSums s{0, 0, 0, 0};
+#pragma unroll
+    for (int z = 0; z < 4; ++z)
+      if (mk >> z & 1u) { s.tc += zc[z]; s.tm += zm[z]; s.fc += hc[z]; s.fm += hm[z]; }
+    return s;
+  }
+};
+__device__ __forceinline__ HintRegs hint_regs(const NumaRow& r, const ZoneAvail& a, int v) {
+  HintRegs h;
+  const uint32_t nf = r.nflags;
+#pragma unroll
+  for (int z = 0; z < 4; ++z) {
+    h.zc[z] = (nf >> (NF_ZCPU_SHIFT + z) & 1u) ? r.zcap_cpu[z] : 0;
+    h.zm[z] = (nf >> (NF_ZMEM_SHIFT + z) & 1u) ? r.zcap_mem[z] : 0;
+    h.hc[z] = trimmed_cpu(a.av_cpu[z], r.zfree[z], v);
+    h.hm[z] = a.av_mem[z];
+  }
+  return h;
+}
+
+// Hint source over a table of a row's position sums (built once per row, read by every lane of a wave).
+struct HintTable {
+  int64_t tc[16], tm[16], fm[16];
+  int64_t fc[4][16];                    // per variant
+};
+struct HintTableRef {
+  const HintTable* t;
+  int v;
+  __device__ HintSums sum(int mi) const { return HintSums{t->tc[mi], t->tm[mi], t->fc[v][mi], t->fm[mi]}; }
+};
+// builds entry `e` (0..63) of the table: lanes 0..59 cover position e % 15 of value kind e / 15
+__device__ __forceinline__ void hint_table_fill(HintTable& t, const NumaRow& r, const ZoneAvail& a, int e) {
+  if (e >= 60) return;
+  const int mi = e % 15, kind = e / 15;
+  const uint32_t mk = ord_mask(mi), nf = r.nflags;
+  int64_t tc = 0, tm = 0, fm = 0, f[4] = {0, 0, 0, 0};
+#pragma unroll
+  for (int z = 0; z < 4; ++z) {
+    if (!(mk >> z & 1u)) continue;
+    if (kind == 0) {
+      tc += (nf >> (NF_ZCPU_SHIFT + z) & 1u) ? r.zcap_cpu[z] : 0;
+      tm += (nf >> (NF_ZMEM_SHIFT + z) & 1u) ? r.zcap_mem[z] : 0;
+      fm += a.av_mem[z];
+    } else {
+      // kind 1..3: variants 0 and kind (FullPCPUs / SpreadByPCPUs / raw) of the available cpu
+      f[0] += a.av_cpu[z];
+      f[1] += trimmed_cpu(a.av_cpu[z], r.zfree[z], kind);
+    }
+  }
+  if (kind == 0) { t.tc[mi] = tc; t.tm[mi] = tm; t.fm[mi] = fm; }
+  else {
+    if (kind == 1) t.fc[0][mi] = f[0];
+    t.fc[kind][mi] = f[1];
+  }
+}
+
+// numaScorer.score(requested = total - available (floored at 0), total, pod) of a hint (resource_manager.go
+// :454-457): zone totals carry only cpu / memory. (The sums already exclude zones that do not list a resource.)
+__device__ __forceinline__ int32_t hint_score(const HintSums& s, int64_t pcpu, int64_t mem, const Profile& pf) {
+  int32_t ns = 0, ws = 0;
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int32_t w = pf.numa_w[k];
+    if (!w) continue;
+    const int64_t al = k == 0 ? s.tc : s.tm;
+    if (al == 0) continue;
+    const int64_t f = k == 0 ? s.fc : s.fm;
+    const int64_t used = al - f > 0 ? al - f : 0;
+    ns += req_score(pf.numa_hint_most, used + (k == 0 ? pcpu : mem), al) * w;
+    ws += w;
+  }
+  return ws ? sdiv(ns, ws) : 0;
+}
+
+// GetPodTopologyHints + topologyManager policy Merge + admit (topology_hint.go:41-67, resource_manager.go
+// :418-532, policy.go:68-186, policy_*.go). Returns the admit verdict; aff_has / aff = the merged affinity.
+template <class Src>
+__device__ __forceinline__ bool hints_merge(const Src& src, int nz, int policy, bool nil_hints, bool has_cpu,
+                                            bool has_mem, int64_t pcpu, int64_t mem, bool tot_c_any, bool tot_m_any,
+                                            const Profile& pf, bool& aff_has, uint32_t& aff) {
+  const uint32_t valid = ord_valid(nz);
+  // generateHints (resource_manager.go:499-532) for every position: total >= request (the size minimum) and
+  // free >= request (a hint)
+  uint32_t totc = 0, totm = 0, lc = 0, lm = 0;
+  if (!nil_hints) {
+#pragma unroll 1
+    for (int mi = 0; mi < 15; ++mi) {
+      if (!(valid >> mi & 1u)) continue;
+      const HintSums s = src.sum(mi);
+      if (s.tc >= pcpu) { totc |= 1u << mi; if (s.fc >= pcpu) lc |= 1u << mi; }
+      if (s.tm >= mem) { totm |= 1u << mi; if (s.fm >= mem) lm |= 1u << mi; }
+    }
+    if (!has_cpu) totc = lc = 0;
+    if (!has_mem) totm = lm = 0;
+  }
+  const int min_c = totc ? ord_size_first(totc) : nz, min_m = totm ? ord_size_first(totm) : nz;
+  // filterProvidersHints (policy.go:98-126): lists in resource-name order cpu, memory.
+  // kind: 0 absent, 1 hints, 2 the empty-list marker {nil, false}
+  const int kc = nil_hints ? 0 : (lc ? 1 : ((has_cpu && tot_c_any) ? 2 : 0));
+  const int km = nil_hints ? 0 : (lm ? 1 : ((has_mem && tot_m_any) ? 2 : 0));
+  const bool single = policy == GS_NUMA_POLICY_SINGLE_NUMA_NODE;
+  const bool no_lists = kc == 0 && km == 0;   // empty map: one preferred any-numa hint
+  const bool use0 = no_lists || kc != 0, use1 = !no_lists && km != 0;
+  const uint32_t full_mask = (1u << nz) - 1u;
+  bool b_pref = false;
+  uint32_t b_mask = full_mask;
+  int32_t b_score = 0;
+  // hint scores of positions, evaluated once each when a comparison needs them, packed 7 bits per position
+  uint64_t sc_lo = 0, sc_hi = 0;
+  uint32_t have = 0;
+  auto score_at = [&](int mi) -> int32_t {
+    if (!(have >> mi & 1u)) {
+      const uint64_t s = (uint64_t)hint_score(src.sum(mi), pcpu, mem, pf);
+      if (mi < 9) sc_lo |= s << (7 * mi);
+      else sc_hi |= s << (7 * (mi - 9));
+      have |= 1u << mi;
+    }
+    return (int32_t)((mi < 9 ? sc_lo >> (7 * mi) : sc_hi >> (7 * (mi - 9))) & 127u);
+  };
+  // Fast path (exact): when every present list has single-zone preferred hints (min size 1), a preferred merged
+  // hint is only produced by equal single-bit masks, so the preferred, narrowest candidates are the single zones
+  // present in every list (positions 0..nz-1), visited in ascending zone order; mergeFilteredHints keeps the first
+  // one of maximal score.
+  uint32_t both = full_mask;
+  bool fast = !no_lists && kc != 2 && km != 2;
+  if (fast && kc == 1) { fast = min_c == 1; both &= lc; }
+  if (fast && km == 1) { fast = min_m == 1; both &= lm; }
+  fast = fast && both != 0;
+  if (fast) {
+    int best_s = -1;
+    for (uint32_t rr = both; rr; rr &= rr - 1) {
+      const int z = __ffs(rr) - 1;
+      const int sz = score_at(z);
+      if (sz > best_s) { best_s = sz; b_mask = 1u << z; }
+    }
+    b_pref = true;
+    b_score = best_s;
+  } else {
+    // Preferred-first merge (exact): the first preferred merged hint is always taken and a non-preferred one never
+    // replaces a preferred best, so the permutation scan equals the scan over the pairs of preferred entries alone
+    // whenever one of them merges to a non-empty mask (pass 0); only otherwise does the full scan run (pass 1,
+    // where no pair is preferred). Both visit pairs in policy.go's order.
+    uint32_t pre0 = 0, pre1 = 0;
+    for (uint32_t rr = lc; rr; rr &= rr - 1) {
+      const int mi = __ffs(rr) - 1;
+      if (__popc(ord_mask(mi)) == min_c) pre0 |= 1u << mi;
+    }
+    for (uint32_t rr = lm; rr; rr &= rr - 1) {
+      const int mi = __ffs(rr) - 1;
+      if (__popc(ord_mask(mi)) == min_m) pre1 |= 1u << mi;
+    }
+    for (int pass = 0; pass < 2; ++pass) {
+      if (pass == 1) {
+        if (b_pref) break;
+        b_mask = full_mask;
+        b_score = 0;
+      }
+      // a list as a sequence of entries: kind 1 = its set bits, kind 2 / absent = a single pseudo entry (bit 31)
+      const uint32_t set0 = kc == 1 ? (pass == 0 ? pre0 : lc) : 0x80000000u;
+      const uint32_t set1 = km == 1 ? (pass == 0 ? pre1 : lm) : 0x80000000u;
+      for (uint32_t r0 = set0; r0; r0 &= r0 - 1) {
+        const int i0 = __ffs(r0) - 1;
+        const bool h0 = kc == 1;
+        const uint32_t m0 = h0 ? ord_mask(i0) : 0u;
+        const bool p0 = h0 ? __popc(m0) == min_c : kc == 0;
+        if (use0 && single && !(p0 && (!h0 || __popc(m0) == 1))) continue;
+        for (uint32_t r1 = set1; r1; r1 &= r1 - 1) {
+          const int i1 = __ffs(r1) - 1;
+          const bool h1 = use1 && km == 1;
+          const uint32_t m1 = h1 ? ord_mask(i1) : 0u;
+          const bool p1 = h1 ? __popc(m1) == min_m : !use1;
+          if (use1 && single && !(p1 && (!h1 || __popc(m1) == 1))) continue;
+          uint32_t mg = full_mask;
+          bool pg = true;
+          if (use0) { mg &= h0 ? m0 : full_mask; pg = pg && p0; }
+          if (use1) { mg &= h1 ? m1 : full_mask; pg = pg && p1; }
+          if (mg == 0) continue;
+          if (!pg && b_pref) continue;
+          // candidates that cannot replace the best skip their score: a wider mask never does, nor an equally wide
+          // one that is not narrower unless its score is higher (the score is only needed then)
+          const bool nar = narrower(mg, b_mask);
+          if (!(pg && !b_pref) && !nar && __popc(mg) != __popc(b_mask)) continue;
+          int32_t sg = 0;
+          if (use0 && h0 && m0 == mg) sg = score_at(i0);
+          if (use1 && h1 && m1 == mg) { const int32_t s1 = score_at(i1); if (s1 > sg) sg = s1; }
+          if (pg && !b_pref) { b_mask = mg; b_pref = true; b_score = sg; continue; }
+          if (!nar) {
+            if (sg > b_score) { b_mask = mg; b_pref = pg; b_score = sg; }
+            continue;
+          }
+          b_mask = mg; b_pref = pg; b_score = sg;
+        }
+      }
+    }
+  }
+  aff_has = true;
+  aff = b_mask;
+  if (single) {
+    if (b_mask == full_mask) aff_has = false;   // policy_single_numa_node.go:70-73
+    return b_pref;
+  }
+  if (policy == GS_NUMA_POLICY_RESTRICTED) return b_pref;
+  return true;
+}
+
 // One (pod, node) evaluation. do_filter: run Filter (incl. the topology manager Admit that sets the affinity);
-// do_score: Score with that affinity (none when the filter is off, as in the reference without a Filter call);
-// want_alloc: fill the Reserve allocation.
+// do_score: Score with that affinity (none when the filter is off, as in the reference without a Filter call).
 // `alloc[s]`/`free[s]` give NodeInfo.Allocatable / Allocatable-Requested for slots 0..2 and the scalars.
 // POLICY_NODES = false compiles only the path of nodes without a NUMA topology policy (the caller routes
 // policy nodes to a kernel of their own); such a call on a policy node returns with reason 0 and no score.
 // known_aff >= 0: the affinity this pair's Filter produced on the same row state (NumaOut.aff; Reserve of a
 // row untouched since the batch-start evaluation): hint generation and merge are skipped.
-template <bool POLICY_NODES = true, class Slots>
+// TABLE: the row's hint sums come from `table` (the commit kernel), else they are computed from the row's zones.
+template <bool POLICY_NODES = true, bool TABLE = false, class Slots>
 __device__ __forceinline__ NumaOut numa_eval(const NumaRow& r, const PodVec& p, const Profile& pf, const Slots& sl,
                                              bool do_filter, bool do_score, int known_aff = -1,
-                                             uint64_t* prof = nullptr) {
-  // prof (diagnostics): s_memtime cycles per segment accumulated into prof[0..5]
-  uint64_t t_np = prof ? __builtin_amdgcn_s_memtime() : 0;
-#define NP(i)                                          \
-  do {                                                 \
-    if (prof) {                                        \
-      const uint64_t t_ = __builtin_amdgcn_s_memtime(); \
-      prof[i] += t_ - t_np;                            \
-      t_np = t_;                                       \
-    }                                                  \
-  } while (0)
+                                             const HintTable* table = nullptr) {
   NumaOut o{};
   const uint32_t pn = p.numa;
   if (pn & PN_PREFAIL) { o.reason = GS_NUMA_INVALID_REQUESTED_CPUS; return o; }
@@ -222,262 +479,25 @@ __device__ __forceinline__ NumaOut numa_eval(const NumaRow& r, const PodVec& p, 
   }
 
   // ---- NUMA-policy node
-  NP(0);
   if (!POLICY_NODES) return o;
   const int nz = (nf >> NF_ZONES_SHIFT) & 7;
   if (do_filter && nz == 0) { o.reason = GS_NUMA_MISSING_NUMA_RESOURCES; return o; }
-  const uint32_t nf2 = r.nflags2;
-  int64_t av_cpu[4], av_mem[4];
-  uint32_t avk = 0;   // bit z: cpu key, bit 4+z: memory key
-#pragma unroll
-  for (int z = 0; z < 4; ++z) {
-    av_cpu[z] = av_mem[z] = 0;
-    if (z >= nz) continue;
-    const bool entry = nf2 >> (NF2_ENTRY_SHIFT + z) & 1u;
-    const bool ccpu = nf >> (NF_ZCPU_SHIFT + z) & 1u, cmem = nf >> (NF_ZMEM_SHIFT + z) & 1u;
-    const bool acpu = entry && ((nf2 >> (NF2_ACPU_SHIFT + z) & 1u) || amp > 1.0);
-    const bool amem = entry && (nf2 >> (NF2_AMEM_SHIFT + z) & 1u);
-    int64_t ac = entry ? r.zraw_cpu[z] + (amp > 1.0 ? (int64_t)r.zadj[z] : 0) : 0;
-    int64_t am = entry ? r.zraw_mem[z] : 0;
-    if (ccpu) av_cpu[z] = r.zcap_cpu[z] - ac > 0 ? r.zcap_cpu[z] - ac : 0;
-    if (cmem) av_mem[z] = r.zcap_mem[z] - am > 0 ? r.zcap_mem[z] - am : 0;
-    if (ccpu || acpu) avk |= 1u << z;
-    if (cmem || amem) avk |= 1u << (4 + z);
-  }
-  const uint32_t full_mask = (1u << nz) - 1u;
+  const ZoneAvail za = zone_avail(r);
   bool aff_has = false;
   uint32_t aff = 0;
   if (do_filter && known_aff >= 0) {
     aff_has = known_aff & 0x10;
     aff = (uint32_t)known_aff & 15u;
   } else if (do_filter) {
-    // GetPodTopologyHints (topology_hint.go:41-67) -> GetTopologyHints (resource_manager.go:122-138)
-    bool nil_hints = false;
-    int64_t hv_cpu[4];
-#pragma unroll
-    for (int z = 0; z < 4; ++z) hv_cpu[z] = av_cpu[z];
-    if (reqflag) {   // trimNUMANodeResources (resource_manager.go:140-169)
-      if (topo && !valid) {
-        nil_hints = true;
-      } else {
-#pragma unroll
-        for (int z = 0; z < 4; ++z) {
-          if (z >= nz || hv_cpu[z] == 0) continue;
-          int raw = cnt_raw(r.zfree[z]);
-          int n = ((int64_t)raw * 1000 >= hv_cpu[z]) ? cnt_sel(r.zfree[z], bind, true) : raw;
-          if ((int64_t)n * 1000 < hv_cpu[z]) hv_cpu[z] = (int64_t)n * 1000;
-        }
-      }
-    }
-    // hint lists as bitmaps over IterateBitMasks positions (bit mi = the mi-th mask of the order), hint scores
-    // (<= 100) packed 7 bits per position: no dynamically indexed arrays, nothing spills to scratch
-    const uint64_t order = kMaskOrderPacked[nz - 1];
-    uint32_t lc = 0, lm = 0;
-    uint64_t sc_lo = 0, sc_hi = 0;
-    int min_c = nz, min_m = nz;
-    bool tot_c_any = false, tot_m_any = false;
-    // numaScorer.score(requested = total - available (non-negative), total, pod) of the hint over mask mk
-    // (resource_manager.go:454-457); evaluated only for the hints the merge below can compare
-    auto mask_score = [&](uint32_t mk) -> uint64_t {
-      int64_t tc = 0, tm = 0, fc = 0, fm = 0;
-      bool kc = false, km = false;
-#pragma unroll
-      for (int z = 0; z < 4; ++z) {
-        if (!(mk >> z & 1u)) continue;
-        if (nf >> (NF_ZCPU_SHIFT + z) & 1u) { tc += r.zcap_cpu[z]; kc = true; }
-        if (nf >> (NF_ZMEM_SHIFT + z) & 1u) { tm += r.zcap_mem[z]; km = true; }
-        fc += hv_cpu[z];
-        fm += av_mem[z];
-      }
-      int32_t ns = 0, ws = 0;
-#pragma unroll
-      for (int s = 0; s < 2; ++s) {
-        int32_t w = pf.numa_w[s];
-        if (!w) continue;
-        const int64_t al = s == 0 ? (kc ? tc : 0) : (km ? tm : 0);
-        if (al == 0) continue;
-        const int64_t used = s == 0 ? (kc ? (tc - fc > 0 ? tc - fc : 0) : 0) : (km ? (tm - fm > 0 ? tm - fm : 0) : 0);
-        const int64_t rq = used + (s == 0 ? pcpu : mem);
-        ns += req_score(pf.numa_hint_most, rq, al) * w;
-        ws += w;
-      }
-      return (uint64_t)(ws ? sdiv(ns, ws) : 0);
-    };
-    if (!nil_hints) {
-      const int nmasks = (1 << nz) - 1;
-      for (int mi = 0; mi < nmasks; ++mi) {
-        if (mi == nz) {
-          // all single-zone masks seen (order positions 0..nz-1): if they already settle the fast merge below
-          // (preferred single-zone hints in every list, a zone common to all), larger masks cannot change
-          // the kinds, minima or candidates it uses, and their hints are never compared
-          const int kc1 = lc ? 1 : ((has_cpu && tot_c_any) ? 2 : 0);
-          const int km1 = lm ? 1 : ((has_mem && tot_m_any) ? 2 : 0);
-          uint32_t bp = (1u << nz) - 1u;
-          if (kc1 == 1) bp &= lc;
-          if (km1 == 1) bp &= lm;
-          if ((kc1 | km1) != 0 && kc1 != 2 && km1 != 2 && (kc1 != 1 || min_c == 1) && (km1 != 1 || min_m == 1) && bp)
-            break;
-        }
-        const uint32_t mk = (uint32_t)(order >> (4 * mi)) & 15u;
-        int64_t tc = 0, tm = 0, fc = 0, fm = 0;
-        bool kc = false, km = false;
-#pragma unroll
-        for (int z = 0; z < 4; ++z) {
-          if (!(mk >> z & 1u)) continue;
-          if (nf >> (NF_ZCPU_SHIFT + z) & 1u) { tc += r.zcap_cpu[z]; kc = true; }
-          if (nf >> (NF_ZMEM_SHIFT + z) & 1u) { tm += r.zcap_mem[z]; km = true; }
-          fc += hv_cpu[z];
-          fm += av_mem[z];
-        }
-        const int cnt = __popc(mk);
-        // generateHints: memory group first, then cpu (resource_manager.go:464-476, 499-532)
-        if (has_mem) {
-          if (km) tot_m_any = true;
-          if (tm >= mem) {
-            if (cnt < min_m) min_m = cnt;
-            if (fm >= mem) lm |= 1u << mi;
-          }
-        }
-        if (has_cpu) {
-          if (kc) tot_c_any = true;
-          if (tc >= pcpu) {
-            if (cnt < min_c) min_c = cnt;
-            if (fc >= pcpu) lc |= 1u << mi;
-          }
-        }
-      }
-    }
-    NP(1);
-    auto mask_at = [&](int mi) -> uint32_t { return (uint32_t)(order >> (4 * mi)) & 15u; };
-    auto score_at = [&](int mi) -> int32_t {
-      return (int32_t)((mi < 9 ? sc_lo >> (7 * mi) : sc_hi >> (7 * (mi - 9))) & 127u);
-    };
-    // filterProvidersHints (policy.go:98-126): lists in resource-name order cpu, memory.
-    // kind: 0 absent, 1 hints, 2 the empty-list marker {nil, false}
-    const int kc_kind = nil_hints ? 0 : (lc ? 1 : ((has_cpu && tot_c_any) ? 2 : 0));
-    const int km_kind = nil_hints ? 0 : (lm ? 1 : ((has_mem && tot_m_any) ? 2 : 0));
-    const bool single = policy == GS_NUMA_POLICY_SINGLE_NUMA_NODE;
-    const bool no_lists = kc_kind == 0 && km_kind == 0;   // empty map: one preferred any-numa hint
-    const bool use0 = no_lists || kc_kind != 0, use1 = !no_lists && km_kind != 0;
-    // mergeFilteredHints (policy.go:128-186) with filterSingleNumaHints for SingleNUMANode
-    bool b_has = true, b_pref = false;
-    uint32_t b_mask = full_mask;
-    int32_t b_score = 0;
-    // Fast path (exact): when every present list has single-zone preferred hints (min size 1), a preferred
-    // merged hint is only produced by equal single-bit masks, so the preferred, narrowest candidates are the
-    // single zones z present in every list, visited in ascending z; mergeFilteredHints then keeps the first
-    // one of maximal score. (The 1-bit masks occupy order positions 0..nz-1.)
-    const uint32_t ones = (1u << nz) - 1u;
-    uint32_t both = 0xFu;
-    bool fast = !no_lists && (kc_kind == 1 || kc_kind == 0) && (km_kind == 1 || km_kind == 0);
-    if (fast && kc_kind == 1) { fast = min_c == 1; both &= lc & ones; }
-    if (fast && km_kind == 1) { fast = min_m == 1; both &= lm & ones; }
-    fast = fast && both != 0;
-    // Preferred-first merge (exact): the first preferred merged hint is always taken and a non-preferred one
-    // never replaces a preferred best, so the permutation scan's result equals the scan over the pairs of
-    // preferred entries alone whenever one of them merges to a non-empty mask (pass 0, at most 6 x 6 pairs);
-    // only otherwise does the full scan run (pass 1). Both visit pairs in policy.go's order.
-    uint32_t pre0 = 0, pre1 = 0;
-    if (!fast && !nil_hints) {
-      for (uint32_t rr = lc; rr; rr &= rr - 1) {
-        const int mi = __ffs(rr) - 1;
-        if (__popc(mask_at(mi)) == min_c) pre0 |= 1u << mi;
-      }
-      for (uint32_t rr = lm; rr; rr &= rr - 1) {
-        const int mi = __ffs(rr) - 1;
-        if (__popc(mask_at(mi)) == min_m) pre1 |= 1u << mi;
-      }
-    }
-    bool b_pref_after0 = false;   // diagnostics: pass 0 settled the merge
-    for (int pass = 0; pass < 2; ++pass) {
-      if (pass == 1) {
-        b_pref_after0 = b_pref;
-        if (fast || b_pref) break;
-        b_mask = full_mask;
-        b_pref = false;
-        b_score = 0;
-      }
-      // scores of the hints this pass compares (single-zone candidates, preferred entries, then the rest)
-      if (!nil_hints) {
-        const uint32_t need = pass == 1 ? (lc | lm) & ~(pre0 | pre1) : (fast ? both : (pre0 | pre1));
-        for (uint32_t rr = need; rr; rr &= rr - 1) {
-          const int mi = __ffs(rr) - 1;
-          const uint64_t hs = mask_score(mask_at(mi));
-          if (mi < 9) sc_lo |= hs << (7 * mi);
-          else sc_hi |= hs << (7 * (mi - 9));
-        }
-      }
-      if (fast) {
-        int best_z = 0, best_s = -1;
-        for (uint32_t rr = both; rr; rr &= rr - 1) {
-          const int z = __ffs(rr) - 1;
-          const int sz = score_at(z);
-          if (sz > best_s) { best_s = sz; best_z = z; }
-        }
-        b_mask = 1u << best_z;
-        b_pref = true;
-        b_score = best_s;
-        continue;
-      }
-      // a list as a sequence of entries: kind 1 = its set bits, kind 2 / absent = a single pseudo entry (bit 31)
-      const uint32_t set0 = kc_kind == 1 ? (pass == 0 ? pre0 : lc) : 0x80000000u;
-      const uint32_t set1 = km_kind == 1 ? (pass == 0 ? pre1 : lm) : 0x80000000u;
-      for (uint32_t r0 = set0; r0; r0 &= r0 - 1) {
-        const int i0 = __ffs(r0) - 1;
-        bool h0 = false, p0 = true;
-        uint32_t m0 = 0;
-        int32_t s0 = 0;
-        if (kc_kind == 1) { h0 = true; m0 = mask_at(i0); p0 = __popc(m0) == min_c; s0 = score_at(i0); }
-        else if (kc_kind == 2) { p0 = false; }
-        if (use0 && single && !(p0 && (!h0 || __popc(m0) == 1))) continue;
-        for (uint32_t r1 = set1; r1; r1 &= r1 - 1) {
-          const int i1 = __ffs(r1) - 1;
-          bool h1 = false, p1 = true;
-          uint32_t m1 = 0;
-          int32_t s1 = 0;
-          if (use1) {
-            if (km_kind == 1) { h1 = true; m1 = mask_at(i1); p1 = __popc(m1) == min_m; s1 = score_at(i1); }
-            else { p1 = false; }
-            if (single && !(p1 && (!h1 || __popc(m1) == 1))) continue;
-          }
-          uint32_t mg = full_mask;
-          bool pg = true;
-          if (use0) { mg &= h0 ? m0 : full_mask; pg = pg && p0; }
-          if (use1) { mg &= h1 ? m1 : full_mask; pg = pg && p1; }
-          if (mg == 0) continue;
-          int32_t sg = 0;
-          if (use0 && h0 && m0 == mg && s0 > sg) sg = s0;
-          if (use1 && h1 && m1 == mg && s1 > sg) sg = s1;
-          if (pg && !b_pref) { b_mask = mg; b_pref = pg; b_score = sg; continue; }
-          if (!pg && b_pref) continue;
-          if (!narrower(mg, b_mask)) {
-            if (__popc(mg) == __popc(b_mask) && sg > b_score) { b_mask = mg; b_pref = pg; b_score = sg; }
-            continue;
-          }
-          b_mask = mg; b_pref = pg; b_score = sg;
-        }
-      }
-    }
-    NP(2);
-    {   // diagnostics: merge path counters: [6] fast, [7] preferred pass only, [8] full pass, [9] a lane of the
-        // wave (among those here with this pair's lane) ran a full pass
-      const bool full = !fast && !nil_hints && !b_pref_after0;
-      const bool wave_full = __ballot(full) != 0;
-      if (prof) {
-        prof[fast ? 6 : (full ? 8 : 7)] += 1;
-        if (wave_full) prof[9] += 1;
-      }
-    }
-    bool admit = true;
-    if (single) {
-      if (b_mask == full_mask) b_has = false;   // policy_single_numa_node.go:70-73
-      admit = b_pref;
-    } else if (policy == GS_NUMA_POLICY_RESTRICTED) {
-      admit = b_pref;
-    }
+    const bool nil_hints = reqflag && topo && !valid;
+    const int v = hint_variant(reqflag, bind);
+    const bool tca = (nf >> NF_ZCPU_SHIFT) & ((1u << nz) - 1u), tma = (nf >> NF_ZMEM_SHIFT) & ((1u << nz) - 1u);
+    bool admit;
+    if (TABLE) admit = hints_merge(HintTableRef{table, v}, nz, policy, nil_hints, has_cpu, has_mem, pcpu, mem, tca, tma,
+                                   pf, aff_has, aff);
+    else admit = hints_merge(hint_regs(r, za, v), nz, policy, nil_hints, has_cpu, has_mem, pcpu, mem, tca, tma, pf,
+                             aff_has, aff);
     if (!admit) { o.reason = GS_NUMA_AFFINITY_ERROR; return o; }
-    aff_has = b_has;
-    aff = b_mask;
   }
   // resourceManager.Allocate with the affinity (resource_manager.go:171-193)
   bool fail = false;
@@ -487,22 +507,21 @@ __device__ __forceinline__ NumaOut numa_eval(const NumaRow& r, const PodVec& p, 
 #pragma unroll
     for (int z = 0; z < 4; ++z) {
       if (!(aff >> z & 1u)) continue;
-      if (has_cpu && (avk >> z & 1u)) {
+      if (has_cpu && (za.avk >> z & 1u)) {
         ic = true;
-        int64_t a = av_cpu[z], got = a > rc ? rc : a;
+        int64_t a = za.av_cpu[z], got = a > rc ? rc : a;
         rc -= got;
         if (got) { o.zkeys |= 1u << z; o.zcpu[z] = got; }
       }
-      if (has_mem && (avk >> (4 + z) & 1u)) {
+      if (has_mem && (za.avk >> (4 + z) & 1u)) {
         im = true;
-        int64_t a = av_mem[z], got = a > rm ? rm : a;
+        int64_t a = za.av_mem[z], got = a > rm ? rm : a;
         rm -= got;
         if (got) { o.zkeys |= 1u << (4 + z); o.zmem[z] = got; }
       }
     }
     if ((ic && rc != 0) || (im && rm != 0)) fail = true;
   }
-  NP(3);
   if (!fail && rb) {   // allocateCPUSet (resource_manager.go:273-360), counted
     if (cnt_sel(r.tfree, bind, reqflag) < p.num_cpus) fail = true;
     // satisfiedRequiredCPUBindPolicy: FullPCPUs over full cores is met iff the count is a multiple of CPUsPerCore
@@ -528,9 +547,9 @@ __device__ __forceinline__ NumaOut numa_eval(const NumaRow& r, const PodVec& p, 
   }
   if (o.zkeys) o.flags |= GS_PLACED_NUMA;
   if (aff_has) { o.flags |= aff << GS_PLACED_AFFINITY_SHIFT; o.aff = 0x10u | aff; }
-  NP(4);
   if (do_score) {   // calculateAllocatableAndRequested (scoring.go:118-164)
     if (o.zkeys) {
+      const uint32_t nf2 = r.nflags2;
       int64_t ac = 0, am = 0, rqc = 0, rqm = 0;
 #pragma unroll
       for (int z = 0; z < 4; ++z) {
@@ -559,8 +578,6 @@ __device__ __forceinline__ NumaOut numa_eval(const NumaRow& r, const PodVec& p, 
       o.score = node_score(rb ? amplify_d((int64_t)r.alloc_cpus * 1000, amp) : req_cpu);
     }
   }
-  NP(5);
-#undef NP
   return o;
 }
 
