@@ -107,7 +107,9 @@ hipError_t launch_eval_full(const MirrorView& m, const PodVec* pods, int npods, 
 hipError_t launch_cand(const int16_t* S, uint32_t ld, uint32_t len, uint32_t n0, int npods, int max_score,
                        uint32_t* lists, LevelHdr* hdrs, hipStream_t st);
 size_t commit_smem_bytes(int B);
-hipError_t launch_commit(const CommitArgs& a, hipStream_t st);
+hipError_t launch_commit(const CommitArgs& a, hipStream_t st);        // window_k > 0: lockstep kernel
+hipError_t launch_commit_pipe(const CommitArgs& a, hipStream_t st);   // pipelined roles (gs_commit.hip)
+hipError_t set_commit_pipe_attributes();
 hipError_t launch_row_stats(const int16_t* S, uint32_t len, RowStat* out, hipStream_t st);
 hipError_t launch_row_select(const int16_t* S, uint32_t len, int score, int64_t target, uint32_t n0, int32_t* out,
                              hipStream_t st);

@@ -18,200 +18,9 @@
 #include <stdint.h>
 #include <stdlib.h>
 
-#include "gs_cpuset_dev.h"
-#include "gs_kernels.h"
-#include "gs_numa_dev.h"
+#include "gs_eval_dev.h"
 
 namespace gs {
-
-// ------------------------------------------------------------------------------------------------
-// exact floor((x*100)/cap) for 0 <= x <= cap, 0 < cap < 2^53
-__device__ __forceinline__ float u64_to_f32(uint64_t v) {
-  return (float)(uint32_t)(v >> 32) * 4294967296.0f + (float)(uint32_t)v;
-}
-
-__device__ __forceinline__ int32_t pct_floor(int64_t x, int64_t cap) {
-  int64_t num = x * 100;
-  float qf = u64_to_f32((uint64_t)num) * __builtin_amdgcn_rcpf(u64_to_f32((uint64_t)cap));
-  int32_t q = (int32_t)qf;
-  q = q > 100 ? 100 : q;
-  int64_t prod = (int64_t)q * cap;
-  if (prod > num) --q;                  // estimate one too high
-  else if (prod + cap <= num) ++q;      // estimate one too low
-  return q;
-}
-
-// leastRequestedScore(requested, capacity) with requested = capacity - free + p  (load_aware.go:388-397,
-// [upstream] least_allocated.go): capacity == 0 -> 0; requested > capacity -> 0.
-__device__ __forceinline__ int32_t least_requested(int64_t free, int64_t p, int64_t cap) {
-  if (cap == 0) return 0;
-  int64_t x = free - p;
-  if (x < 0) return 0;
-  return pct_floor(x, cap);
-}
-
-// exact a / b for 0 <= a < 2^24, 1 <= b < 2^24 (weighted-mean divisions)
-__device__ __forceinline__ int32_t small_div(int32_t a, int32_t b) {
-  int32_t q = (int32_t)((float)a * __builtin_amdgcn_rcpf((float)b));
-  if (q * b > a) --q;
-  else if ((q + 1) * b <= a) ++q;
-  return q;
-}
-
-// A node row: everything one Filter+Score evaluation reads (scalar-resource columns stay in HBM and are
-// read only for pods that request / profiles that weigh scalar resources).
-struct Row {
-  int64_t free[7];      // Allocatable - Requested per slot (slots 3..6 only in the commit's LDS copy)
-  int64_t alloc[2];     // cpu, mem
-  int64_t nzfree[2];
-  int64_t la_cap[2];
-  int64_t la_free[2];
-  int64_t la_pfree[2];
-  int32_t free_pods;
-  uint32_t dflags;
-  uint32_t node;        // global index
-  uint32_t pad;
-  NumaRow nr;           // NodeNUMAResource columns (loaded when the profile enables the plugin)
-};
-constexpr int ROW_I64 = 17;   // int64 words of Row, in the column order of kRowCol
-constexpr int NUMA_I64 = 18;  // NumaRow int64 words: C_ZCAP_CPU0 .. C_NAMP (contiguous columns)
-constexpr int NUMA_I32 = 12;  // NumaRow int32 words: C_NFLAGS .. C_ZADJ0+3 (contiguous columns)
-static_assert(C_NAMP - C_ZCAP_CPU0 + 1 == NUMA_I64, "NUMA i64 columns contiguous");
-static_assert(C_ZADJ0 + 3 - C_NFLAGS + 1 == NUMA_I32, "NUMA i32 columns contiguous");
-
-__constant__ int kRowCol[ROW_I64] = {C_FREE_CPU,     C_FREE_MEM,    C_FREE_EPH,   C_FREE_BCPU,  C_FREE_BMEM,
-                                     C_FREE_MCPU,    C_FREE_MMEM,   C_ALLOC_CPU,  C_ALLOC_MEM,  C_NZFREE_CPU,
-                                     C_NZFREE_MEM,   C_LA_CAP_CPU,  C_LA_CAP_MEM, C_LA_FREE_CPU, C_LA_FREE_MEM,
-                                     C_LA_PFREE_CPU, C_LA_PFREE_MEM};
-// Row words an assume/Reserve changes (written back by the commit kernel)
-__device__ __forceinline__ bool row_word_mutable(int j) { return j < 7 || j == 9 || j == 10 || j >= 13; }
-
-__device__ __forceinline__ void load_row(const MirrorView& m, uint32_t i, bool prod_cols, bool numa, Row& r) {
-  if (numa) load_numa_row(m, i, r.nr);
-  r.free[0] = m.c64(C_FREE_CPU)[i];
-  r.free[1] = m.c64(C_FREE_MEM)[i];
-  r.free[2] = m.c64(C_FREE_EPH)[i];
-  r.alloc[0] = m.c64(C_ALLOC_CPU)[i];
-  r.alloc[1] = m.c64(C_ALLOC_MEM)[i];
-  r.nzfree[0] = m.c64(C_NZFREE_CPU)[i];
-  r.nzfree[1] = m.c64(C_NZFREE_MEM)[i];
-  r.la_cap[0] = m.c64(C_LA_CAP_CPU)[i];
-  r.la_cap[1] = m.c64(C_LA_CAP_MEM)[i];
-  r.la_free[0] = m.c64(C_LA_FREE_CPU)[i];
-  r.la_free[1] = m.c64(C_LA_FREE_MEM)[i];
-  if (prod_cols) {
-    r.la_pfree[0] = m.c64(C_LA_PFREE_CPU)[i];
-    r.la_pfree[1] = m.c64(C_LA_PFREE_MEM)[i];
-  } else {
-    r.la_pfree[0] = r.la_pfree[1] = 0;
-  }
-  r.free_pods = m.c32(C_FREE_PODS)[i];
-  r.dflags = (uint32_t)m.c32(C_DFLAGS)[i];
-  r.node = i;
-}
-
-struct PairOut {
-  uint32_t code;
-  int32_t fit, la, numa;
-  uint32_t aff;         // NodeNUMAResource Filter-time affinity (NumaOut.aff)
-};
-
-// NodeInfo slot views for numa_eval: Allocatable and Allocatable - Requested per resource slot
-struct SlotsHbm {
-  const Row& r;
-  const MirrorView& m;
-  __device__ int64_t alloc(int s) const { return s < 2 ? r.alloc[s] : m.c64(C_ALLOC_CPU + s)[r.node]; }
-  __device__ int64_t free(int s) const { return s < 3 ? r.free[s] : m.c64(C_FREE_CPU + s)[r.node]; }
-};
-struct SlotsLds {
-  const Row& r;
-  const MirrorView& m;
-  __device__ int64_t alloc(int s) const { return s < 2 ? r.alloc[s] : m.c64(C_ALLOC_CPU + s)[r.node]; }
-  __device__ int64_t free(int s) const { return r.free[s]; }
-};
-
-// Filter (Fit + LoadAware) and Score (Fit LeastAllocated + LoadAware) of one pod on one node.
-// LDS_SCALARS: scalar free columns come from r.free[3..6] (the commit's LDS copy) instead of HBM.
-// NUMA_POLICY_NODES = false: NodeNUMAResource's topology-policy path is compiled out (eval_kernel routes those
-// nodes to eval_numa_kernel)
-// table: the row's NUMA hint table (commit re-scoring of one row for many pods), else computed from the row.
-template <bool FULL, bool LDS_SCALARS, bool NUMA_POLICY_NODES = true, bool TABLE = false>
-__device__ __forceinline__ PairOut eval_pair(const Row& r, const PodVec& p, const Profile& pf, const MirrorView& m,
-                                             const HintTable* table = nullptr) {
-  PairOut o{0u, 0, 0, 0, 0u};
-  // ---- [upstream] noderesources Fit.Filter -> fitsRequest
-  if (pf.enabled & 0x1u) {
-    if (r.free_pods < 1) o.code |= 0x01u;                               // len(Pods)+1 > AllowedPodNumber
-    if (!(p.flags & PF_ALL_ZERO)) {
-      if (p.req[0] > r.free[0]) o.code |= 0x02u;
-      if (p.req[1] > r.free[1]) o.code |= 0x04u;
-      if (p.req[2] > r.free[2]) o.code |= 0x08u;
-      if (p.scalar_mask) {
-        for (int s = 3; s < 7; ++s) {
-          if (!(p.scalar_mask & (1u << s))) continue;
-          int64_t fr = LDS_SCALARS ? r.free[s] : m.c64(C_FREE_CPU + s)[r.node];
-          if (p.req[s] > fr) o.code |= 0x10u;
-        }
-      }
-    }
-  }
-  // ---- LoadAware.Filter (load_aware.go:123-171), usage verdicts precomputed per node
-  if ((pf.enabled & 0x4u) && !(p.flags & PF_DAEMONSET)) {
-    uint32_t bit = (p.flags & PF_PROD) ? DF_LA_FAIL_P : DF_LA_FAIL_NP;
-    if (r.dflags & bit) o.code |= 0x20u;
-  }
-  if (!FULL && o.code) return o;
-  // ---- NodeNUMAResource Filter (+ Admit) and Score (gs_numa_dev.h)
-  if (pf.enabled & 0x30u) {
-    NumaOut no;
-    if (LDS_SCALARS) no = numa_eval<NUMA_POLICY_NODES, TABLE>(r.nr, p, pf, SlotsLds{r, m}, pf.enabled & 0x10u,
-                                                              pf.enabled & 0x20u, -1, table);
-    else no = numa_eval<NUMA_POLICY_NODES>(r.nr, p, pf, SlotsHbm{r, m}, pf.enabled & 0x10u, pf.enabled & 0x20u);
-    if (pf.enabled & 0x10u) o.code |= no.reason << GS_FAIL_NUMA_SHIFT;
-    if (!FULL && o.code) return o;
-    o.numa = no.reason ? 0 : no.score;
-    o.aff = no.aff;
-  }
-  // ---- Fit.Score, LeastAllocated over NonZeroRequested ([upstream] resource_allocation.go)
-  if (pf.enabled & 0x2u) {
-    int32_t ns = 0, ws = 0;
-    if (pf.fit_w[0] && r.alloc[0] != 0) {
-      ns += least_requested(r.nzfree[0], p.nz[0], r.alloc[0]) * pf.fit_w[0];
-      ws += pf.fit_w[0];
-    }
-    if (pf.fit_w[1] && r.alloc[1] != 0) {
-      ns += least_requested(r.nzfree[1], p.nz[1], r.alloc[1]) * pf.fit_w[1];
-      ws += pf.fit_w[1];
-    }
-    if (pf.fit_scalar_w_mask) {
-      for (int s = 2; s < 7; ++s) {
-        if (!(pf.fit_scalar_w_mask & (1u << s))) continue;
-        int64_t preq = p.req[s];
-        if (s >= 3 && preq == 0) continue;                              // un-requested scalar: bypass
-        int64_t cap = m.c64(C_ALLOC_CPU + s)[r.node];
-        if (cap == 0) continue;
-        int64_t fr = (LDS_SCALARS || s == 2) ? r.free[s] : m.c64(C_FREE_CPU + s)[r.node];
-        ns += least_requested(fr, preq, cap) * pf.fit_w[s];
-        ws += pf.fit_w[s];
-      }
-    }
-    o.fit = ws ? small_div(ns, ws) : 0;
-  }
-  // ---- LoadAware.Score (load_aware.go:269-335): est + la_used vs EstimateNode
-  if ((pf.enabled & 0x8u) && !(r.dflags & DF_LA_ZERO)) {
-    bool prod = p.flags & PF_PROD_SCORE;
-    int32_t ns = 0;
-    if (pf.la_w[0]) ns += least_requested(prod ? r.la_pfree[0] : r.la_free[0], p.est[0], r.la_cap[0]) * pf.la_w[0];
-    if (pf.la_w[1]) ns += least_requested(prod ? r.la_pfree[1] : r.la_free[1], p.est[1], r.la_cap[1]) * pf.la_w[1];
-    o.la = small_div(ns, pf.la_wsum);
-  }
-  return o;
-}
-
-__device__ __forceinline__ int32_t total_score(const PairOut& o, const Profile& pf) {
-  if (o.code) return -1;
-  return o.fit * pf.w_fit + o.la * pf.w_la + o.numa * pf.w_numa;
-}
 
 // ------------------------------------------------------------------------------------------------
 // node-prep: LoadAware expiry (helper.go:36-41) evaluated at `now` for every node.
@@ -437,142 +246,11 @@ __global__ void __launch_bounds__(64 * W) cand_kernel(const int16_t* __restrict_
   if (t == 0) hdrs[k] = s_hdr;
 }
 
-// ------------------------------------------------------------------------------------------------
-// selectHost tie-break: position (1-based, in feasible order) of the selected node among T max ties.
-// Same stream as oracle/oracle.cpp TieBreakRand: R = {1, floor(j/U_0)+1, ...}; answer = max R ∩ [1,T].
-__host__ __device__ inline uint64_t mix64(uint64_t x) {
-  uint64_t z = x + 0x9e3779b97f4a7c15ULL;
-  z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ULL;
-  z = (z ^ (z >> 27)) * 0x94d049bb133111ebULL;
-  return z ^ (z >> 31);
-}
-
-__host__ __device__ inline int64_t tiebreak_position(uint64_t seed, uint64_t seq, int64_t T) {
-  uint64_t key = mix64(seed ^ mix64(seq));
-  int64_t j = 1;
-  for (uint64_t i = 0;; ++i) {
-    uint64_t h = mix64(key + i);
-    double u = (double)((h >> 11) + 1) * 0x1.0p-53;
-    double x = (double)j / u;
-    if (!(x < 4.0e18)) break;
-    int64_t jn = (int64_t)floor(x) + 1;
-    if (jn > T) break;
-    j = jn;
-  }
-  return j;
-}
-
 int64_t host_tiebreak_position(uint64_t seed, uint64_t seq, int64_t T) { return tiebreak_position(seed, seq, T); }
-
-// ------------------------------------------------------------------------------------------------
-// Sequential commit: ONE wave walks the batch's pods in order (no workgroup barriers: LDS traffic of a
-// single wave is in order, so phases only need compiler scheduling fences, and global prefetches of the
-// next pod's headers stay in flight while the current pod is resolved).
-//
-// For pod k the effective score of a node is its batch-start score (S, summarized per shard by the listed
-// levels) unless an earlier pod of the batch landed on it ("dirty"): dirty rows live in LDS and their
-// scores for every later pod are re-evaluated exactly (dso = batch-start score, dsc = current score).
-// The max M is valid when it exceeds every shard's highest unlisted score (`next`); otherwise the batch
-// is cut at k. Ties at M are ordered by node index across shards (shards are contiguous ranges).
-constexpr int NUMA_PPT = 2;   // pods per thread in eval_numa_kernel (full batches)
-constexpr int HASH = 1024;
-constexpr int POD_STRIDE = 136;   // LDS bytes per pod vector in the commit kernel (sizeof(PodVec) + 8)
-static_assert(POD_STRIDE >= (int)sizeof(PodVec) && POD_STRIDE % 8 == 0, "pod stride");
-constexpr int WIN = 2 * MAX_BATCH + 8;
-#define WAVE_FENCE() __builtin_amdgcn_wave_barrier()
-
-__device__ __forceinline__ int32_t row_score(const Row& d, const PodVec& p, const Profile& pf, const MirrorView& m,
-                                             const HintTable* table = nullptr) {
-  return total_score(eval_pair<false, true, true, true>(d, p, pf, m, table), pf);
-}
-
-__device__ __forceinline__ int hash_find(const int32_t* hkey, const int32_t* hval, uint32_t node) {
-  uint32_t h = (node * 2654435761u) & (HASH - 1);
-  for (int probe = 0; probe < HASH; ++probe) {
-    int kk = hkey[h];
-    if (kk == (int)node) return hval[h];
-    if (kk < 0) return -1;
-    h = (h + 1) & (HASH - 1);
-  }
-  return -1;
-}
-
-__device__ __forceinline__ const LevelHdr* hdr_ptr(const CommitArgs& a, int r, int k) {
-  return reinterpret_cast<const LevelHdr*>(a.xbase + (size_t)r * a.xblock + (size_t)a.bmax * LCAP * 4) + k;
-}
-__device__ __forceinline__ const uint32_t* list_ptr(const CommitArgs& a, int r, int k) {
-  return reinterpret_cast<const uint32_t*>(a.xbase + (size_t)r * a.xblock) + (size_t)k * LCAP;
-}
-
-__device__ __forceinline__ int wave_max(int v) {
-  for (int off = 32; off > 0; off >>= 1) v = max(v, __shfl_xor(v, off));
-  return v;
-}
-__device__ __forceinline__ int wave_sum(int v) {
-  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
-  return v;
-}
-
-// sort n (<= 128) distinct node ids in place, tmp as scratch (one wave)
-__device__ __forceinline__ void wave_rank_sort(uint32_t* v, int n, uint32_t* tmp, int lane) {
-  for (int i = lane; i < n; i += 64) {
-    uint32_t x = v[i];
-    int r = 0;
-    for (int u = 0; u < n; ++u) r += v[u] < x;
-    tmp[r] = x;
-  }
-  WAVE_FENCE();
-  for (int i = lane; i < n; i += 64) v[i] = tmp[i];
-  WAVE_FENCE();
-}
-
-// Device-side cpuset Reserve of one pod on its winner row (one thread): allocateCPUSet with the NUMA split of
-// Allocate (resource_manager.go:273-360, gs_cpuset_dev.h), then NodeAllocation.addPodAllocation
-// (node_allocation.go:82-110) on the CPU state and the row's available-CPU summaries, as numa_derive
-// (gs_numa_host.cpp) would recompute them. false: allocateCPUSet errors (the host fails loudly).
-// Arguments live in LDS or registers (zone split by value, cpuset into an LDS array): nothing of the caller's
-// frame has its address taken, so the commit kernel keeps its Reserve state out of scratch.
-__device__ __noinline__ bool cpuset_reserve(const TopoDev& t, CpuStateDev& cs, const PodVec& p, uint32_t nf,
-                                            uint32_t zkeys, int64_t zc0, int64_t zc1, int64_t zc2, int64_t zc3,
-                                            NumaRow& nr, uint64_t* cpuset) {
-  const int64_t zcpu[4] = {zc0, zc1, zc2, zc3};
-  // getCPUBindPolicy (util.go:85-103)
-  const uint32_t pn = p.numa;
-  const int st_req = (pn >> PN_REQ_SHIFT) & 7, nb = (nf >> NF_BIND_SHIFT) & 3;
-  int bind = (pn >> PN_PREF_SHIFT) & 7;
-  bool required = false;
-  if (st_req != BIND_UNSET) { bind = st_req; required = true; }
-  else if (nb == GS_NODE_CPU_BIND_SPREAD_BY_PCPUS) { bind = BIND_SPREAD; required = true; }
-  else if (nb == GS_NODE_CPU_BIND_FULL_PCPUS_ONLY) { bind = BIND_FULL; required = true; }
-  const int ep = (pn & PN_BIND) ? (int)((pn >> PN_EXCL_SHIFT) & 3u) : GS_CPU_EXCLUSIVE_NONE;
-  uint64_t R[TD_POS];
-  if (!td_allocate_cpuset(t, cs, p.num_cpus, bind, required, ep, zkeys, zcpu, R)) return false;
-  const uint64_t cores = td_any(R);
-  for (int j = 0; j < TD_POS; ++j) cs.un[j] |= R[j];
-  if (ep == GS_CPU_EXCLUSIVE_PCPU_LEVEL) cs.xc |= cores;
-  else if (ep == GS_CPU_EXCLUSIVE_NUMA_NODE_LEVEL)
-    for (uint64_t b = cores; b; b &= b - 1) cs.meta |= 1u << t.core_node[td_ctz(b)];
-  nr.alloc_cpus += td_cnt(R, ~0ull);
-  nr.tfree = (uint32_t)td_counts(t, cs, ~0ull);
-  const int nz = (nf >> NF_ZONES_SHIFT) & 7;
-  for (int z = 0; z < 4; ++z) {
-    const int n = td_zone_node(cs, z);
-    if (z >= nz || n >= t.nnodes) continue;   // a zone the topology lacks keeps its zero summaries
-    const uint64_t zc = ((cs.zal >> (16 * z)) & 0xFFFFull) + (uint64_t)td_cnt(R, t.node_cores[n]);
-    cs.zal = (cs.zal & ~(0xFFFFull << (16 * z))) | (zc << (16 * z));
-    nr.zfree[z] = (uint32_t)td_counts(t, cs, t.node_cores[n]);
-    if (nr.amp > 1.0) {
-      const int64_t c = (int64_t)zc * 1000;
-      nr.zadj[z] = (int32_t)(amplify_d(c, nr.amp) - c);
-    }
-  }
-  td_to_cpus(t, R, cpuset);
-  return true;
-}
 
 // ST: diagnostic build with s_memtime phase stamps (accumulated per phase, written to a.stamps)
 template <bool ST>
-__global__ void __launch_bounds__(256) commit_kernel(CommitArgs a) {
+__global__ void __launch_bounds__(COMMIT_THREADS) commit_kernel(CommitArgs a) {
   uint64_t st_acc[14] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
   uint64_t st_stage = 0;                      // header staging cycles (inside p0)   // numa_eval segments of thread 128's policy-row rescoring (ST)
   uint64_t st_last = ST ? __builtin_amdgcn_s_memtime() : 0;
@@ -595,8 +273,10 @@ __global__ void __launch_bounds__(256) commit_kernel(CommitArgs a) {
   Row* drows = reinterpret_cast<Row*>(cm + (size_t)B * POD_STRIDE);          // B dirty slots
   int16_t* dsc = reinterpret_cast<int16_t*>(drows + B);                      // [pod][slot] current score
   int16_t* dso = dsc + B * B;                                                // [pod][slot] batch-start score
-  int32_t* hkey = reinterpret_cast<int32_t*>(
-      (reinterpret_cast<uintptr_t>(dso + B * B) + 15) & ~(uintptr_t)15);     // HASH
+  // offsets from the LDS base, not integer-cast pointers: the address space stays visible to the compiler (an
+  // integer round trip turns every access into a flat load that waits on outstanding global loads)
+  const size_t hoff = ((size_t)B * POD_STRIDE + (size_t)B * sizeof(Row) + (size_t)B * B * 4 + 15) & ~(size_t)15;
+  int32_t* hkey = reinterpret_cast<int32_t*>(cm + hoff);                     // HASH
   int32_t* hval = hkey + HASH;                                               // HASH
   CpuStateDev* cst = reinterpret_cast<CpuStateDev*>(hval + HASH);            // B dirty slots: CPU state
 
@@ -610,7 +290,7 @@ __global__ void __launch_bounds__(256) commit_kernel(CommitArgs a) {
   // a pod resolved from its whole score row (host slow path for pod 0, or in-kernel on one shard): its selectHost
   __shared__ int s_fk, s_fnode, s_fscore, s_ffeas, s_Md, s_Fd, s_ndc;
   __shared__ int64_t s_fties;
-  __shared__ int s_red[8];
+  __shared__ int s_red[2 * COMMIT_WAVES];
   __shared__ uint32_t s_winner;
   __shared__ int64_t s_T;
   __shared__ int s_cut;                                // the pod just committed needs host-side Reserve
@@ -628,7 +308,7 @@ __global__ void __launch_bounds__(256) commit_kernel(CommitArgs a) {
   }
 
   __shared__ uint32_t s_start;                         // nextStartNodeIndex (node sampling)
-  __shared__ int32_t s_wred[3][8];                     // window selection: block scans / reductions
+  __shared__ int32_t s_wred[3][COMMIT_WAVES];                     // window selection: block scans / reductions
   __shared__ int32_t s_wend, s_wproc, s_ndirty;       // s_ndirty: dirty slots (wave 0's nd, published)
   if (tid == 0) {
     s_ndirty = 0;
@@ -659,8 +339,8 @@ __global__ void __launch_bounds__(256) commit_kernel(CommitArgs a) {
       f_kind = 2; f_src = a.m.c32(C_NFLAGS + (lane - 50)); f_off = offsetof(Row, nr.nflags) + (lane - 50) * 4; f_size = 4;
     }
   }
-  for (int i = tid; i < B; i += 256) pods(i) = a.pods[i];
-  for (int i = tid; i < HASH; i += 256) { hkey[i] = -1; hval[i] = -1; }
+  for (int i = tid; i < B; i += COMMIT_THREADS) pods(i) = a.pods[i];
+  for (int i = tid; i < HASH; i += COMMIT_THREADS) { hkey[i] = -1; hval[i] = -1; }
   const MirrorView& m = a.m;
   const int nhl = R * MAXLEV;                    // header lanes: lane = r*MAXLEV + j
   // LevelHdrs and seq of HCH pods at a time are staged in LDS (one HBM round trip per chunk)
@@ -723,7 +403,7 @@ __global__ void __launch_bounds__(256) commit_kernel(CommitArgs a) {
     if (lane == 63) s_wred[slot][wave] = incl;
     __syncthreads();
     int base = 0, tot = 0;
-    for (int w = 0; w < 4; ++w) { const int x = s_wred[slot][w]; if (w < wave) base += x; tot += x; }
+    for (int w = 0; w < COMMIT_WAVES; ++w) { const int x = s_wred[slot][w]; if (w < wave) base += x; tot += x; }
     __syncthreads();
     *total = tot;
     return base + incl - v;
@@ -757,7 +437,7 @@ __global__ void __launch_bounds__(256) commit_kernel(CommitArgs a) {
     if (tid == 0) { s_wend = (int)N - 1; s_wproc = (int)N; }
     int found = 0, lmax = -1, lcnt = 0, v[WCH];
     uint32_t passes = 0;
-    for (uint32_t base = 0; base < N; base += 256 * WCH) {
+    for (uint32_t base = 0; base < N; base += COMMIT_THREADS * WCH) {
       load_pass(base, v);
       ++passes;
       int c = 0;
@@ -785,11 +465,13 @@ __global__ void __launch_bounds__(256) commit_kernel(CommitArgs a) {
     const int wm = wave_max(lmax);
     if (lane == 0) s_wred[1][wave] = wm;
     __syncthreads();
-    const int M = max(max(s_wred[1][0], s_wred[1][1]), max(s_wred[1][2], s_wred[1][3]));
+    int M = s_wred[1][0];
+    for (int w = 1; w < COMMIT_WAVES; ++w) M = max(M, s_wred[1][w]);
     const int tl = wave_sum(lmax == M ? lcnt : 0);
     if (lane == 0) s_wred[2][wave] = tl;
     __syncthreads();
-    const int64_t T = (int64_t)s_wred[2][0] + s_wred[2][1] + s_wred[2][2] + s_wred[2][3];
+    int64_t T = 0;
+    for (int w = 0; w < COMMIT_WAVES; ++w) T += s_wred[2][w];
     const int F = (int)min((uint32_t)found, K);
     const uint32_t wend = (uint32_t)s_wend, proc = (uint32_t)s_wproc;
     if (M < 0) {   // FitError: nothing assumed; every node was processed
@@ -805,7 +487,7 @@ __global__ void __launch_bounds__(256) commit_kernel(CommitArgs a) {
     const int64_t jp = tiebreak_position(a.seed, a.seq[k], T);
     int64_t before = 0;
     if (tid == 0) s_fnode = -1;
-    for (uint32_t base = 0; base <= wend; base += 256 * WCH) {
+    for (uint32_t base = 0; base <= wend; base += COMMIT_THREADS * WCH) {
       if (passes > 1) load_pass(base, v);
       int c = 0;
 #pragma unroll
@@ -838,7 +520,7 @@ __global__ void __launch_bounds__(256) commit_kernel(CommitArgs a) {
   for (int k = 0; k < B; ++k) {
    const uint64_t t_stage0 = ST ? __builtin_amdgcn_s_memtime() : 0;
    if (k % HCH == 0 && !a.window_k) {
-     for (int e = tid; e < HCH * nhl; e += 256) {
+     for (int e = tid; e < HCH * nhl; e += COMMIT_THREADS) {
        int kk = e / nhl, l = e % nhl;
        if (k + kk < B) {
          const LevelHdr* h = hdr_ptr(a, l / MAXLEV, k + kk);
@@ -846,7 +528,7 @@ __global__ void __launch_bounds__(256) commit_kernel(CommitArgs a) {
          hs_count[kk][l] = h->count[l % MAXLEV];
        }
      }
-     for (int e = tid; e < HCH * R; e += 256) {
+     for (int e = tid; e < HCH * R; e += COMMIT_THREADS) {
        int kk = e / R, r = e % R;
        if (k + kk < B) {
          const LevelHdr* h = hdr_ptr(a, r, k + kk);
@@ -855,7 +537,7 @@ __global__ void __launch_bounds__(256) commit_kernel(CommitArgs a) {
          hs_next[kk][r] = h->next;
        }
      }
-     for (int e = tid; e < HCH; e += 256)
+     for (int e = tid; e < HCH; e += COMMIT_THREADS)
        if (k + e < B) hs_seq[e] = a.seq[k + e];
      __syncthreads();
    }
@@ -1051,7 +733,7 @@ __global__ void __launch_bounds__(256) commit_kernel(CommitArgs a) {
     // current scores for dirty rows; max, ties and feasible count, then the j*-th tie in node order
     {
       const int16_t* row = a.S + (size_t)k * a.ld;
-      const uint32_t len = a.own1 - a.own0, chunk = (len + 255) / 256;
+      const uint32_t len = a.own1 - a.own0, chunk = (len + COMMIT_THREADS - 1) / COMMIT_THREADS;
       const uint32_t i0 = min(len, (uint32_t)tid * chunk), i1 = min(len, i0 + chunk);
       int lmax = -1, lfeas = 0;
       for (uint32_t i = i0; i < i1; ++i) {
@@ -1061,10 +743,10 @@ __global__ void __launch_bounds__(256) commit_kernel(CommitArgs a) {
       }
       lmax = wave_max(lmax);
       lfeas = wave_sum(lfeas);
-      if (lane == 0) { s_red[wave] = lmax; s_red[4 + wave] = lfeas; }
+      if (lane == 0) { s_red[wave] = lmax; s_red[COMMIT_WAVES + wave] = lfeas; }
       __syncthreads();
-      const int M = max(max(max(s_red[0], s_red[1]), max(s_red[2], s_red[3])), s_Md);
-      const int F = s_red[4] + s_red[5] + s_red[6] + s_red[7] + s_Fd;
+      int M = s_Md, F = s_Fd;
+      for (int w = 0; w < COMMIT_WAVES; ++w) { M = max(M, s_red[w]); F += s_red[COMMIT_WAVES + w]; }
       __syncthreads();
       int cnt = 0;
       if (M >= 0) {
@@ -1084,7 +766,8 @@ __global__ void __launch_bounds__(256) commit_kernel(CommitArgs a) {
       __syncthreads();
       int base = 0;
       for (int w = 0; w < wave; ++w) base += s_red[w];
-      const int64_t T = (int64_t)s_red[0] + s_red[1] + s_red[2] + s_red[3];
+      int64_t T = 0;
+      for (int w = 0; w < COMMIT_WAVES; ++w) T += s_red[w];
       const int64_t jp = T > 0 ? tiebreak_position(a.seed, hs_seq[k % HCH], T) : 0;
       const int64_t excl = base + incl - cnt;
       if (tid == 0) s_fnode = -1;
@@ -1116,7 +799,7 @@ __global__ void __launch_bounds__(256) commit_kernel(CommitArgs a) {
           ((pq.numa & PN_BIND) || ((nfl >> NF_BIND_SHIFT) & 3u))) {
         const uint64_t* src = reinterpret_cast<const uint64_t*>(a.topos + tp);
         uint64_t* dst = reinterpret_cast<uint64_t*>(&s_topo);
-        for (int i = tid; i < (int)(sizeof(TopoDev) / 8); i += 256) dst[i] = src[i];
+        for (int i = tid; i < (int)(sizeof(TopoDev) / 8); i += COMMIT_THREADS) dst[i] = src[i];
         __syncthreads();
         if (tid == 0) s_topo_id = tp;
       }
@@ -1211,13 +894,14 @@ __global__ void __launch_bounds__(256) commit_kernel(CommitArgs a) {
     __syncthreads();
     if (s_cut) { committed = k + 1; host_cut = true; break; }
     if (tid == 0) STAMP(7);
-    // Re-scoring, pods q = k+1 .. over 4 waves x 32: lanes 0..31 evaluate the winner row's current score
-    // (one row for all lanes: the NUMA hint sums come from the table); lanes 32..63 of a fresh row fetch its
-    // batch-start score from the score rows S when the node is in this rank's shard, else evaluate it.
+    // Re-scoring, pods q = k+1 .. over the waves, RS_PODS per wave: lanes 0..RS_PODS-1 evaluate the winner row's
+    // current score (one row for all lanes: the NUMA hint sums come from the table); lanes 32.. of a fresh row fetch
+    // its batch-start score from the score rows S when the node is in this rank's shard, else evaluate it.
     {
+      constexpr int RS_PODS = MAX_BATCH / COMMIT_WAVES;
       const int sub = lane & 31;
       const bool cur = lane < 32;
-      const int q = k + 1 + wv * 32 + sub;
+      const int q = sub < RS_PODS ? k + 1 + wv * RS_PODS + sub : B;
       const uint64_t t0_ = ST ? __builtin_amdgcn_s_memtime() : 0;
       const uint32_t node = d.node;
       const bool own = node >= a.own0 && node < a.own1;
@@ -1225,9 +909,13 @@ __global__ void __launch_bounds__(256) commit_kernel(CommitArgs a) {
       int16_t so = 0;
       if (load_so) so = a.S_own[(size_t)q * a.ld + (node - a.own0)];
       const bool policy_row = numa_on && ((d.nr.nflags >> NF_POLICY_SHIFT) & 3u);   // (ST stamps)
-      if (q < B && (cur || (fresh && !own))) {
-        const Row rr = cur ? d : orow;   // registers: the evaluation re-reads row words many times
-        (cur ? dsc : dso)[q * B + slot] = (int16_t)row_score(rr, pods(q), a.pf, m, cur ? &s_ht : &s_ht2);
+      if (q < B && cur) {   // the row is wave-uniform (LDS at a uniform slot): its words can live in SGPRs
+        const Row rr = d;
+        dsc[q * B + slot] = (int16_t)row_score(rr, pods(q), a.pf, m, &s_ht);
+      }
+      if (fresh && !own && q < B && !cur) {   // several ranks only
+        const Row rr = orow;
+        dso[q * B + slot] = (int16_t)row_score(rr, pods(q), a.pf, m, &s_ht2);
       }
       if (load_so) dso[q * B + slot] = so;
       if (ST && tid == 128 && policy_row) {
@@ -1250,16 +938,16 @@ __global__ void __launch_bounds__(256) commit_kernel(CommitArgs a) {
   }
   __syncthreads();
   nd = s_nd;
-  for (int e = tid; e < nd * ROW_I64; e += 256) {
+  for (int e = tid; e < nd * ROW_I64; e += COMMIT_THREADS) {
     int s = e / ROW_I64, j = e % ROW_I64;
     if (row_word_mutable(j)) m.c64(kRowCol[j])[drows[s].node] = reinterpret_cast<const int64_t*>(&drows[s])[j];
   }
-  for (int s = tid; s < nd; s += 256) m.c32(C_FREE_PODS)[drows[s].node] = drows[s].free_pods;
+  for (int s = tid; s < nd; s += COMMIT_THREADS) m.c32(C_FREE_PODS)[drows[s].node] = drows[s].free_pods;
   // NUMA words Reserve changes: ZRAW (8 i64), NFLAGS2 .. ZADJ3 (11 i32), CPU state (6 i64 + meta)
   constexpr int NW = 8 + 11 + 6 + 1;
   static_assert(C_ZADJ0 + 3 - C_NFLAGS2 + 1 == 11, "NUMA i32 write-back columns contiguous");
   if (numa_on)
-    for (int e = tid; e < nd * NW; e += 256) {
+    for (int e = tid; e < nd * NW; e += COMMIT_THREADS) {
       const int sl = e / NW, j = e % NW;
       const uint32_t node = drows[sl].node;
       if (j < 8) m.c64(C_ZRAW_CPU0 + j)[node] = (&drows[sl].nr.zraw_cpu[0])[j];
@@ -1451,10 +1139,12 @@ size_t commit_smem_bytes(int B) {
 }
 
 hipError_t launch_commit(const CommitArgs& a, hipStream_t st) {
+  static const bool lockstep = getenv("GS_COMMIT_LOCKSTEP") && getenv("GS_COMMIT_LOCKSTEP")[0] == '1';
+  if (!a.window_k && !lockstep) return launch_commit_pipe(a, st);
   if (a.stamps)
-    hipLaunchKernelGGL(commit_kernel<true>, dim3(1), dim3(256), commit_smem_bytes(a.npods), st, a);
+    hipLaunchKernelGGL(commit_kernel<true>, dim3(1), dim3(COMMIT_THREADS), commit_smem_bytes(a.npods), st, a);
   else
-    hipLaunchKernelGGL(commit_kernel<false>, dim3(1), dim3(256), commit_smem_bytes(a.npods), st, a);
+    hipLaunchKernelGGL(commit_kernel<false>, dim3(1), dim3(COMMIT_THREADS), commit_smem_bytes(a.npods), st, a);
   return hipGetLastError();
 }
 
@@ -1477,7 +1167,9 @@ hipError_t launch_scatter_rows(const MirrorView& m, const uint32_t* idx, const i
 }
 
 hipError_t set_kernel_attributes() {
-  hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(commit_kernel<false>),
+  hipError_t e = set_commit_pipe_attributes();
+  if (e != hipSuccess) return e;
+  e = hipFuncSetAttribute(reinterpret_cast<const void*>(commit_kernel<false>),
                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)commit_smem_bytes(MAX_BATCH));
   if (e != hipSuccess) return e;
   e = hipFuncSetAttribute(reinterpret_cast<const void*>(commit_kernel<true>),
