@@ -77,13 +77,10 @@ __global__ void __launch_bounds__(256) commit_pipe_kernel(CommitArgs a) {
   __shared__ int32_t rset[2][PIPE_RSN], rset_n[2];
   __shared__ uint64_t sseq[MAX_BATCH];
   // wave 0 selection scratch
-  __shared__ int32_t sh_score[MAX_RANKS * MAXLEV], sh_count[MAX_RANKS * MAXLEV], sh_dec[MAX_RANKS * MAXLEV];
-  __shared__ uint32_t dnew[MAX_BATCH], tmp[MAX_BATCH];
-  __shared__ uint32_t win[WIN];
-  __shared__ int32_t pre_old[WIN + 1];
+  __shared__ int32_t sh_score[MAX_RANKS * MAXLEV], sh_dec[MAX_RANKS * MAXLEV];   // several shards: decrements
   __shared__ Row orow[2];                 // batch-start copy of a fresh row outside this rank's shard (by parity)
   __shared__ TopoDev s_topo;              // topology of the last cpuset Reserve (bit-plane form)
-  __shared__ HintTable s_ht[2], s_hto[2], s_htpre;   // new state / batch-start state (by parity) / pre-Reserve
+  __shared__ HintTable s_ht[2], s_hto[2];  // new state / batch-start state of the winner row (by parity)
   __shared__ uint64_t s_cpuset[4];
   __shared__ int32_t s_aff;               // Filter-time affinity of the pair (fresh own-shard row; -1 unknown)
   // hand-off between the roles (by parity of the pod): the slot pod p landed on (-1 none), its batch-start
@@ -100,14 +97,18 @@ __global__ void __launch_bounds__(256) commit_pipe_kernel(CommitArgs a) {
   }
 
   // ---- prologue: pods, hash, pod 0's prefetch
-  uint64_t st_acc[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+  uint64_t st_acc[18] = {};
   uint64_t st_last = ST ? __builtin_amdgcn_s_memtime() : 0;
+// (diagnostic build: nothing moves across a stamp, and a phase's outstanding memory operations complete inside it)
 #define STAMP(i)                                    \
   do {                                              \
     if (ST) {                                       \
+      __builtin_amdgcn_sched_barrier(0);            \
+      __builtin_amdgcn_s_waitcnt(0);                \
       uint64_t t_ = __builtin_amdgcn_s_memtime();   \
       st_acc[i] += t_ - st_last;                    \
       st_last = t_;                                 \
+      __builtin_amdgcn_sched_barrier(0);            \
     }                                               \
   } while (0)
   for (int i = tid; i < B; i += 256) { pods(i) = a.pods[i]; sseq[i] = a.seq[i]; }
@@ -137,6 +138,10 @@ __global__ void __launch_bounds__(256) commit_pipe_kernel(CommitArgs a) {
 
   if (wv == 0) {
     // ===================================== wave 0: the selector =====================================
+    // Dirty slot s's node id lives in a register of lane s % 64 (dn0: slots 0..63, dn1: slots 64..127), so the
+    // selection reads LDS in one round (level headers, the pod's scores on the dirty slots, tie-break positions,
+    // the list window) and does the rest with ballots, DPP reductions and readlane broadcasts.
+    uint32_t dn0 = 0xffffffffu, dn1 = 0xffffffffu;
     int nd = 0;                  // dirty slots
     int topo_id = -1;            // s_topo holds this registered topology
     const int nhl = R * MAXLEV;  // header lanes: lane = r*MAXLEV + j
@@ -159,6 +164,11 @@ __global__ void __launch_bounds__(256) commit_pipe_kernel(CommitArgs a) {
         f_kind = 2; f_src = m.c32(C_NFLAGS + (lane - 50)); f_off = offsetof(Row, nr.nflags) + (lane - 50) * 4; f_size = 4;
       }
     }
+    // node ids of the dirty slots selected by two lane bitmaps, in lane order
+    auto each_node = [&](uint64_t m0, uint64_t m1, auto&& fn) {
+      for (uint64_t b = m0; b; b &= b - 1) fn((uint32_t)__builtin_amdgcn_readlane((int)dn0, __builtin_ctzll(b)));
+      for (uint64_t b = m1; b; b &= b - 1) fn((uint32_t)__builtin_amdgcn_readlane((int)dn1, __builtin_ctzll(b)));
+    };
     int committed = B;
     bool host_cut = false;
     for (int p = 0; p < B; ++p) {
@@ -171,30 +181,48 @@ __global__ void __launch_bounds__(256) commit_pipe_kernel(CommitArgs a) {
       int M = -1, F = 0;
       int64_t T = 0;
       bool slowpath = p == 0 && a.forced_node >= 0;   // pod 0 resolved by the host's full-row path
+      // ---- one round of LDS loads
       const int r_l = lane / MAXLEV, j_l = lane % MAXLEV;
-      const bool lvl = lane < nhl && j_l < hsh[par][r_l < MAX_RANKS ? r_l : 0].nlev;
+      const int nlev_l = lane < nhl ? hsh[par][r_l].nlev : 0;
+      const bool lvl = lane < nhl && j_l < nlev_l;
       const int hs = lvl ? hsh[par][r_l].score[j_l] : -1, hc = lvl ? hsh[par][r_l].count[j_l] : 0;
       const int feas_l = lane < R ? hsh[par][lane].feasible : 0, next_l = lane < R ? hsh[par][lane].next : -1;
-      if (lane < nhl) { sh_score[lane] = hs; sh_count[lane] = hc; sh_dec[lane] = 0; }
-      WAVE_FENCE();
-      // ---- dirty rows: batch-start / current scores of pod p, listed-level decrements
-      int Md = -1, Fd = 0;
-      for (int s = lane; s < nd; s += 64) {
-        const int sc = dsc[p * B + s], so = dso[p * B + s];
-        Md = max(Md, sc);
-        Fd += (sc >= 0 ? 1 : 0) - (so >= 0 ? 1 : 0);
-        if (so >= 0) {
-          const int base = (int)(drows[s].node / a.shard_size) * MAXLEV;
+      int sc0 = -1, so0 = -1, sc1 = -1, so1 = -1;
+      if (lane < nd) { sc0 = dsc[p * B + lane]; so0 = dso[p * B + lane]; }
+      if (lane + 64 < nd) { sc1 = dsc[p * B + 64 + lane]; so1 = dso[p * B + 64 + lane]; }
+      const int rn = rset_n[par], rna = rn < 0 ? -rn : rn;
+      const int32_t rv = lane < rna ? rset[par][lane] : 0x7fffffff;
+      const int sh0 = (int)(dn0 / a.shard_size), sh1 = (int)(dn1 / a.shard_size);   // shard of each dirty node
+      STAMP(12);
+      // ---- listed-level decrements: a dirty row whose batch-start score is a listed level of its shard left it
+      int clean = 0;
+      if (R == 1) {
+        int dec_l = 0;   // decrement of level `lane`
+#pragma unroll
+        for (int j = 0; j < MAXLEV; ++j) {
+          const int sj = __builtin_amdgcn_readlane(hs, j);
+          const int dj = __popcll(__ballot(so0 >= 0 && so0 == sj)) + __popcll(__ballot(so1 >= 0 && so1 == sj));
+          if (lane == j) dec_l = dj;
+        }
+        clean = lvl ? hc - dec_l : 0;
+      } else {
+        if (lane < nhl) { sh_score[lane] = hs; sh_dec[lane] = 0; }
+        WAVE_FENCE();
+        for (int e = 0; e < 2; ++e) {
+          const int so = e ? so1 : so0;
+          if (so < 0) continue;
+          const int base = (e ? sh1 : sh0) * MAXLEV;
           for (int j = 0; j < MAXLEV; ++j)
             if (sh_score[base + j] == so) { atomicAdd(&sh_dec[base + j], 1); break; }
         }
+        WAVE_FENCE();
+        clean = lvl ? hc - sh_dec[lane] : 0;
       }
-      Md = wave_max(Md);
-      Fd = wave_sum(Fd);
-      WAVE_FENCE();
-      const int clean = lvl ? hc - sh_dec[lane] : 0;
+      const int Md = wave_max(max(sc0, sc1));
+      const int Fd = wave_sum((sc0 >= 0) - (so0 >= 0) + (sc1 >= 0) - (so1 >= 0));
       M = max(wave_max(clean > 0 ? hs : -1), Md);
       F = Fd + wave_sum(lane < R ? feas_l : 0);
+      STAMP(13);
       bool full_row = false;
       if (slowpath) {
         M = a.forced_score;
@@ -209,130 +237,113 @@ __global__ void __launch_bounds__(256) commit_pipe_kernel(CommitArgs a) {
       } else if (M < 0) {
         action = 1;   // FitError: no feasible node anywhere
       } else {
-        // ---- tie set at M: clean listed nodes + dirty rows now at M ("dnew") - dirty rows listed at M ("old")
+        // ---- tie set at M: clean listed nodes + dirty rows now at M ("new") - dirty rows listed at M ("old")
+        const bool nw0 = sc0 == M, nw1 = sc1 == M;
+        const int ndn = __popcll(__ballot(nw0)) + __popcll(__ballot(nw1));
         const int cm_lane = (lvl && hs == M) ? clean : 0;
-        int ndn = 0;
-        for (int s0 = 0; s0 < nd; s0 += 64) {
-          const int s = s0 + lane;
-          const bool isn = s < nd && dsc[p * B + s] == M;
-          const uint64_t bn = __ballot(isn);
-          if (isn) dnew[ndn + __popcll(bn & lt_mask)] = drows[s].node;
-          ndn += __popcll(bn);
-        }
-        WAVE_FENCE();
         T = (int64_t)wave_sum(cm_lane) + ndn;
-        // tie-break position: the largest prefetched R entry <= T
-        int64_t jp;
+        int64_t jp;   // tie-break position: the largest prefetched R entry <= T
         {
-          const int rn = rset_n[par], na = rn < 0 ? -rn : rn;
-          const int32_t rv = lane < na ? rset[par][lane] : 0x7fffffff;
-          const uint64_t le = __ballot(lane < na && (int64_t)rv <= T);
+          const uint64_t le = __ballot(lane < rna && (int64_t)rv <= T);
           const int top = 63 - __clzll((long long)le);
-          jp = __shfl(rv, top);
-          if (rn < 0 && top == na - 1) jp = tiebreak_position(a.seed, sseq[p], T);   // past the prefetched entries
+          jp = __builtin_amdgcn_readlane(rv, top);
+          if (rn < 0 && top == rna - 1) jp = tiebreak_position(a.seed, sseq[p], T);   // past the prefetched entries
         }
-        if (ndn > 1) wave_rank_sort(dnew, ndn, tmp, lane);
-        // per shard: clean ties + dirty ties (lane r < R), owning shard r* by prefix
-        int here = 0;
-        {
-          int c = 0;
-          for (int j = 0; j < MAXLEV; ++j) c += __shfl(cm_lane, (lane < R ? lane : 0) * MAXLEV + j);
-          if (lane < R) {
-            const uint32_t sb = (uint32_t)lane * a.shard_size, se = sb + a.shard_size;
-            int dn = 0;
-            for (int u = 0; u < ndn; ++u) dn += dnew[u] >= sb && dnew[u] < se;
-            here = c + dn;
+        // owning shard r*: per shard, clean listed ties + dirty rows now at M, by prefix in shard order
+        int rstar = 0;
+        if (R > 1) {
+          int64_t before = 0;
+          for (int r = 0; r < R; ++r) {
+            const int here = wave_sum(r_l == r ? cm_lane : 0) + __popcll(__ballot(nw0 && sh0 == r)) +
+                             __popcll(__ballot(nw1 && sh1 == r));
+            if (before + here >= jp || r == R - 1) { rstar = r; break; }
+            before += here;
           }
+          jp -= before;
         }
-        int incl = here;
-        for (int off = 1; off < 64; off <<= 1) {
-          const int v = __shfl_up(incl, off);
-          if (lane >= off) incl += v;
-        }
-        const uint64_t hit = __ballot(lane < R && incl >= jp);
-        const int rstar = hit ? (__ffsll((long long)hit) - 1) : (R - 1);
-        jp -= __shfl(incl - here, rstar);
-        // level-M segment of r*'s list
+        // level-M segment of r*'s list: offset = listed nodes of r* above M, len = listed nodes at M
         int off = 0, len = 0;
         for (int j = 0; j < MAXLEV; ++j) {
-          const int sc = sh_score[rstar * MAXLEV + j];
-          if (sc < 0) break;
-          if (sc == M) { len = sh_count[rstar * MAXLEV + j]; break; }
-          off += sh_count[rstar * MAXLEV + j];
+          const int sj = __builtin_amdgcn_readlane(hs, rstar * MAXLEV + j);
+          const int cj = __builtin_amdgcn_readlane(hc, rstar * MAXLEV + j);
+          if (sj < 0) break;
+          if (sj == M) { len = cj; break; }
+          off += cj;
         }
         const uint32_t sb = (uint32_t)rstar * a.shard_size, se = sb + a.shard_size;
-        int nn_lo = 0;
-        while (nn_lo < ndn && dnew[nn_lo] < sb) ++nn_lo;
-        int nn_hi = nn_lo;
-        while (nn_hi < ndn && dnew[nn_hi] < se) ++nn_hi;
-        // dirty rows of r* listed at M (batch-start score M)
-        int ndo_r = 0;
-        for (int s = lane; s < nd; s += 64) {
-          const uint32_t node = drows[s].node;
-          ndo_r += (dso[p * B + s] == M && node >= sb && node < se) ? 1 : 0;
-        }
-        ndo_r = wave_sum(ndo_r);
-        const int lo = (int)max<int64_t>(0, jp - 2 - (nn_hi - nn_lo));
-        const int hi = (int)min<int64_t>(len - 1, jp - 1 + ndo_r);
-        const int W = hi - lo + 1;
-        // ---- the jp-th node of (listed level-M nodes of r* - old) U dnew, node order, over window L[lo..hi]
-        // (list entries below PIPE_PL come from the prefetched head)
+        const bool in0 = dn0 >= sb && dn0 < se, in1 = dn1 >= sb && dn1 < se;
+        const uint64_t new0 = __ballot(nw0 && in0), new1 = __ballot(nw1 && in1);
+        const uint64_t old0 = __ballot(so0 == M && in0), old1 = __ballot(so1 == M && in1);
+        const int nnew = __popcll(new0) + __popcll(new1), nold = __popcll(old0) + __popcll(old1);
+        const int lo = (int)max<int64_t>(0, jp - 2 - nnew);
+        const int hi = (int)min<int64_t>(len - 1, jp - 1 + nold);
+        const int W = hi - lo + 1;   // <= nold + nnew + 2
+        STAMP(14);
+        // ---- the jp-th node of (listed level-M nodes of r* - old) U new, node order, over window L[lo..hi]
+        // (list entries below PIPE_PL come from the prefetched head); window position i in lane i % 64 of chunk i / 64
         const uint32_t* L = list_ptr(a, rstar, p);
+        constexpr int WCH = (2 * MAX_BATCH + 2 + 63) / 64;
+        uint32_t xw[WCH];
+        bool ow[WCH];
         uint32_t cand = 0xffffffffu;
+        int base_old = 0;
         if (len > 0) {
-          for (int i = lane; i < W; i += 64) {
-            const int e = off + lo + i;
-            win[i] = e < PIPE_PL ? plh[par][rstar][e] : L[e];
+#pragma unroll
+          for (int c = 0; c < WCH; ++c) {
+            const int i = c * 64 + lane, e = off + lo + i;
+            xw[c] = 0xffffffffu;
+            if (c * 64 < W && i < W) xw[c] = e < PIPE_PL ? plh[par][rstar][e] : L[e];
           }
-          WAVE_FENCE();
-          // old rows before the window, then a running count over the window (membership via the hash)
-          int base_old = 0;
-          for (int s = lane; s < nd; s += 64) {
-            const uint32_t node = drows[s].node;
-            base_old += (dso[p * B + s] == M && node >= sb && node < win[0]) ? 1 : 0;
-          }
-          base_old = wave_sum(base_old);
+          const uint32_t win0 = (uint32_t)__builtin_amdgcn_readlane((int)xw[0], 0);
+#pragma unroll
+          for (int c = 0; c < WCH; ++c) ow[c] = false;
+          each_node(old0, old1, [&](uint32_t n) {
+            base_old += n < win0 ? 1 : 0;
+#pragma unroll
+            for (int c = 0; c < WCH; ++c) ow[c] |= xw[c] == n;
+          });
           int running = base_old;
-          for (int i0 = 0; i0 < W; i0 += 64) {
-            const int i = i0 + lane;
-            const uint32_t x = i < W ? win[i] : 0xffffffffu;
-            bool isold = false;
-            if (i < W) {
-              const int sl = hash_find(hkey, hval, x);
-              isold = sl >= 0 && dso[p * B + sl] == M;
-            }
-            const uint64_t bo = __ballot(isold);
+#pragma unroll
+          for (int c = 0; c < WCH; ++c) {
+            if (c * 64 >= W) break;
+            const int i = c * 64 + lane;
+            const bool valid = i < W;
+            const uint64_t bo = __ballot(valid && ow[c]);
             const int older = running + __popcll(bo & lt_mask);
-            if (i < W) {
-              pre_old[i] = older;
-              int newer = 0;
-              for (int u = nn_lo; u < nn_hi; ++u) newer += dnew[u] < x;
-              if (!isold && (int64_t)(lo + i - older + newer + 1) == jp) cand = x;
-            }
+            int newer = 0;
+            each_node(new0, new1, [&](uint32_t n) { newer += n < xw[c] ? 1 : 0; });
+            if (valid && !ow[c] && (int64_t)(lo + i - older + newer + 1) == jp) cand = xw[c];
             running += __popcll(bo);
           }
-          if (lane == 0) pre_old[W] = running;
-          WAVE_FENCE();
         }
-        for (int u0 = nn_lo + lane; u0 < nn_hi; u0 += 64) {
-          const uint32_t n = dnew[u0];
-          int64_t ltn = -1;   // #listed level-M nodes < n, when it can decide position jp
+        // a new node is the jp-th when its insertion point in the window decides position jp
+        each_node(new0, new1, [&](uint32_t n) {
+          int u = 0;   // rank among the new nodes
+          each_node(new0, new1, [&](uint32_t n2) { u += n2 < n ? 1 : 0; });
+          int64_t ltn = -1;   // # listed level-M nodes < n, when it can decide position jp
           int older = 0;
           if (len == 0) {
             ltn = 0;
           } else {
-            int pp = 0, qq = W;   // lower_bound(win, n)
-            while (pp < qq) { const int mid = (pp + qq) >> 1; if (win[mid] < n) pp = mid + 1; else qq = mid; }
+            int pp = 0;
+#pragma unroll
+            for (int c = 0; c < WCH; ++c) {
+              if (c * 64 >= W) break;
+              const bool valid = c * 64 + lane < W;
+              pp += __popcll(__ballot(valid && xw[c] < n));
+              older += __popcll(__ballot(valid && ow[c] && xw[c] < n));
+            }
+            older += base_old;
             if (pp == 0) ltn = (lo == 0) ? 0 : -1;
             else if (pp == W) ltn = (hi == len - 1) ? len : -1;
             else ltn = lo + pp;
-            older = pre_old[pp];
           }
-          if (ltn >= 0 && ltn - older + (u0 - nn_lo) + 1 == jp) cand = n;
-        }
+          if (ltn >= 0 && ltn - older + u + 1 == jp) cand = n;
+        });
+        STAMP(15);
         const uint64_t got = __ballot(cand != 0xffffffffu);
         if (!got) action = 2;   // unreachable for a valid max: cut, exact re-run on the host
-        else winner = __shfl(cand, __ffsll((long long)got) - 1);
+        else winner = (uint32_t)__builtin_amdgcn_readlane((int)cand, __ffsll((long long)got) - 1);
       }
       if (full_row) {
         // ---- exact full-row resolution of pod p on the single shard: batch-start scores S[p][*] for clean nodes,
@@ -359,12 +370,8 @@ __global__ void __launch_bounds__(256) commit_pipe_kernel(CommitArgs a) {
             const uint32_t n = drows[s].node;
             if (n >= a.own0 + i0 && n < a.own0 + i1 && dsc[p * B + s] == M) ++cnt;
           }
-          int incl = cnt;
-          for (int off = 1; off < 64; off <<= 1) {
-            const int v = __shfl_up(incl, off);
-            if (lane >= off) incl += v;
-          }
-          T = __shfl(incl, 63);
+          const int incl = wave_incl_scan(cnt);
+          T = __builtin_amdgcn_readlane(incl, 63);
           const int64_t jp = tiebreak_position(a.seed, sseq[p], T);
           const int64_t excl = incl - cnt;
           int64_t found = -1;
@@ -378,7 +385,7 @@ __global__ void __launch_bounds__(256) commit_pipe_kernel(CommitArgs a) {
           }
           const uint64_t got = __ballot(found >= 0);
           if (!got) action = 2;
-          else winner = (uint32_t)__shfl(found, __ffsll((long long)got) - 1);
+          else winner = (uint32_t)__builtin_amdgcn_readlane((int)found, __ffsll((long long)got) - 1);
           slowpath = true;
         }
       }
@@ -404,13 +411,15 @@ __global__ void __launch_bounds__(256) commit_pipe_kernel(CommitArgs a) {
         continue;
       }
       // ------------------------------------------------------------ fetch the winner into its dirty slot
-      int slot = hash_find(hkey, hval, winner);
+      const uint64_t hit0 = __ballot(dn0 == winner), hit1 = __ballot(dn1 == winner);
+      int slot = hit0 ? __builtin_ctzll(hit0) : hit1 ? 64 + __builtin_ctzll(hit1) : -1;
       const bool fresh = slot < 0;
       const bool own = winner >= a.own0 && winner < a.own1;
       const bool eval_so = fresh && !own;   // batch-start scores outside this rank's shard are evaluated
       if (fresh) {
         slot = nd;
-        if (lane == 0) {
+        if (lane == (nd & 63)) { if (nd < 64) dn0 = winner; else dn1 = winner; }
+        if (lane == 0) {   // the node -> slot hash (full-row resolution)
           uint32_t h = (winner * 2654435761u) & (HASH - 1);
           while (hkey[h] >= 0) h = (h + 1) & (HASH - 1);
           hkey[h] = (int32_t)winner;
@@ -425,10 +434,10 @@ __global__ void __launch_bounds__(256) commit_pipe_kernel(CommitArgs a) {
           v = own ? (int64_t)reinterpret_cast<const uint8_t*>(f_src)[(size_t)p * a.ld + (winner - a.own0)] : -1;
         } else if (f_kind == 4) v = (int64_t)winner;   // Row.node, Row.pad = 0
         // batch-start scores of the later pods on this row (own shard): S[q][winner], q = p+1 ..
-        int16_t so0 = 0, so1 = 0;
+        int16_t so0v = 0, so1v = 0;
         const int q0 = p + 1 + lane, q1 = q0 + 64;
-        if (own && q0 < B) so0 = a.S_own[(size_t)q0 * a.ld + (winner - a.own0)];
-        if (own && q1 < B) so1 = a.S_own[(size_t)q1 * a.ld + (winner - a.own0)];
+        if (own && q0 < B) so0v = a.S_own[(size_t)q0 * a.ld + (winner - a.own0)];
+        if (own && q1 < B) so1v = a.S_own[(size_t)q1 * a.ld + (winner - a.own0)];
         if (f_kind) {
           unsigned char* dst = f_region == 0 ? reinterpret_cast<unsigned char*>(&drows[slot])
                              : f_region == 1 ? reinterpret_cast<unsigned char*>(&cst[slot])
@@ -441,8 +450,8 @@ __global__ void __launch_bounds__(256) commit_pipe_kernel(CommitArgs a) {
             else *reinterpret_cast<int32_t*>(d2 + f_off) = (int32_t)v;
           }
         }
-        if (own && q0 < B) dso[q0 * B + slot] = so0;
-        if (own && q1 < B) dso[q1 * B + slot] = so1;
+        if (own && q0 < B) dso[q0 * B + slot] = so0v;
+        if (own && q1 < B) dso[q1 * B + slot] = so1v;
       }
       if (lane == 0 && (!fresh || !numa_on)) s_aff = -1;   // a dirty row changed since the batch-start Filter
       WAVE_FENCE();
@@ -455,8 +464,7 @@ __global__ void __launch_bounds__(256) commit_pipe_kernel(CommitArgs a) {
       Row& d = drows[slot];
       const PodVec& pk = pods(p);
       // ------------------------------------------------------------ Reserve
-      if (numa_on) {
-        // stage the winner's topology in LDS for a device-side cpuset Reserve
+      if (numa_on) {   // stage the winner's topology in LDS for a device-side cpuset Reserve
         const int tp = cst[slot].topo;
         const uint32_t nfl = d.nr.nflags;
         if (tp >= 0 && tp != topo_id && !(pk.numa & (PN_SKIP | PN_PREFAIL)) &&
@@ -466,98 +474,99 @@ __global__ void __launch_bounds__(256) commit_pipe_kernel(CommitArgs a) {
           for (int i = lane; i < (int)(sizeof(TopoDev) / 8); i += 64) dst[i] = src[i];
           topo_id = tp;
         }
-        // the hint table of the pre-Reserve state when the Filter-time affinity is unknown
-        if (s_aff < 0 && ((nfl >> NF_POLICY_SHIFT) & 3u)) {
-          const NumaRow nr = d.nr;
-          hint_table_fill(s_htpre, nr, zone_avail(nr), lane);
-        }
         WAVE_FENCE();
       }
       STAMP(3);
       int cut = 0;
-      if (lane == 0) {
-        const Row dr = d;   // registers: the Reserve's pair evaluation re-reads row words
-        PlacementDev pl{(int32_t)winner, (uint32_t)F, (int64_t)M, (uint32_t)T, slowpath ? 1u : 0u, 0, 0,
-                        {0, 0, 0, 0}, {0, 0, 0, 0}};
+      {
+        const Row dr = d;   // wave-uniform copy: the Reserve's pair evaluation re-reads row words
         const uint32_t nf = dr.nr.nflags;
         // Reserve returns at once unless requestCPUBind (util.go:105-122) or the node has a NUMA policy
         const bool maybe_rb = (pk.numa & PN_BIND) || (((nf >> NF_BIND_SHIFT) & 3u) && (pk.req_keys & 1u) && pk.req[0]);
-        if (numa_on && !(pk.numa & (PN_SKIP | PN_PREFAIL)) && (maybe_rb || ((nf >> NF_POLICY_SHIFT) & 3u))) {
-          // NodeNUMAResource Reserve (plugin.go:375-422) on the pre-assume row: the Filter-time affinity and the
-          // NUMA split of Allocate; a cpuset pod's CPUs are selected here (gs_cpuset_dev.h) when the node's
-          // topology is in the device scope, else the batch ends with it and the host selects them
-          const NumaOut no = numa_eval<true, true>(dr.nr, pk, a.pf, SlotsLds{dr, m}, a.pf.enabled & 0x10u, false,
-                                                   s_aff, &s_htpre);
-          const bool rb = no.flags & GS_PLACED_CPUSET;
-          if (no.reason) pl.flags |= PL_RESERVE_FAILED;   // cannot happen for a feasible winner
-          if (rb || ((nf >> NF_POLICY_SHIFT) & 3u)) {
-            pl.flags |= no.flags;
-            pl.zkeys = no.zkeys;
+        const bool numa_reserve =
+            numa_on && !(pk.numa & (PN_SKIP | PN_PREFAIL)) && (maybe_rb || ((nf >> NF_POLICY_SHIFT) & 3u));
+        // NodeNUMAResource Reserve (plugin.go:375-422) on the pre-assume row: the Filter-time affinity and the NUMA
+        // split of Allocate (the whole wave evaluates the pair); a cpuset pod's CPUs are selected by lane 0
+        // (gs_cpuset_dev.h) when the node's topology is in the device scope, else the batch ends with it and the
+        // host selects them
+        NumaOut no{};
+        if (numa_reserve)
+          no = numa_eval<true, false, true>(dr.nr, pk, a.pf, SlotsLds{dr, m}, a.pf.enabled & 0x10u, false, s_aff);
+        if (lane == 0) {
+          PlacementDev pl{(int32_t)winner, (uint32_t)F, (int64_t)M, (uint32_t)T, slowpath ? 1u : 0u, 0, 0,
+                          {0, 0, 0, 0}, {0, 0, 0, 0}};
+          if (numa_reserve) {
+            const bool rb = no.flags & GS_PLACED_CPUSET;
+            if (no.reason) pl.flags |= PL_RESERVE_FAILED;   // cannot happen for a feasible winner
+            if (rb || ((nf >> NF_POLICY_SHIFT) & 3u)) {
+              pl.flags |= no.flags;
+              pl.zkeys = no.zkeys;
 #pragma unroll
-            for (int z = 0; z < 4; ++z) { pl.zcpu[z] = no.zcpu[z]; pl.zmem[z] = no.zmem[z]; }
-            if (nf & NF_TOPO_VALID) {   // resourceManager.Update -> NodeAllocation.addPodAllocation
-              uint32_t f2 = dr.nr.nflags2;
+              for (int z = 0; z < 4; ++z) { pl.zcpu[z] = no.zcpu[z]; pl.zmem[z] = no.zmem[z]; }
+              if (nf & NF_TOPO_VALID) {   // resourceManager.Update -> NodeAllocation.addPodAllocation
+                uint32_t f2 = dr.nr.nflags2;
 #pragma unroll
-              for (int z = 0; z < 4; ++z) {
-                const bool zc = no.zkeys >> z & 1u, zm = no.zkeys >> (4 + z) & 1u;
-                if (!zc && !zm) continue;
-                d.nr.zraw_cpu[z] = dr.nr.zraw_cpu[z] + no.zcpu[z];
-                d.nr.zraw_mem[z] = dr.nr.zraw_mem[z] + no.zmem[z];
-                f2 |= (1u << (NF2_ENTRY_SHIFT + z)) | (zc ? 1u << (NF2_ACPU_SHIFT + z) : 0u) |
-                      (zm ? 1u << (NF2_AMEM_SHIFT + z) : 0u);
-              }
-              d.nr.nflags2 = f2;
-            }
-            if (rb) {
-              CpuStateDev& cs = cst[slot];
-              if (cs.topo >= 0 && cs.topo == topo_id) {
-                if (cpuset_reserve(s_topo, cs, pk, nf, no.zkeys, no.zcpu[0], no.zcpu[1], no.zcpu[2], no.zcpu[3],
-                                   d.nr, s_cpuset)) {
-                  pl.flags |= PL_DEVICE_CPUSET;
-#pragma unroll
-                  for (int j = 0; j < 4; ++j) pl.cpuset[j] = s_cpuset[j];
-                } else {
-                  pl.flags |= PL_RESERVE_FAILED;
+                for (int z = 0; z < 4; ++z) {
+                  const bool zc = no.zkeys >> z & 1u, zm = no.zkeys >> (4 + z) & 1u;
+                  if (!zc && !zm) continue;
+                  d.nr.zraw_cpu[z] = dr.nr.zraw_cpu[z] + no.zcpu[z];
+                  d.nr.zraw_mem[z] = dr.nr.zraw_mem[z] + no.zmem[z];
+                  f2 |= (1u << (NF2_ENTRY_SHIFT + z)) | (zc ? 1u << (NF2_ACPU_SHIFT + z) : 0u) |
+                        (zm ? 1u << (NF2_AMEM_SHIFT + z) : 0u);
                 }
-              } else {
-                cut = 1;
+                d.nr.nflags2 = f2;
+              }
+              if (rb) {
+                CpuStateDev& cs = cst[slot];
+                if (cs.topo >= 0 && cs.topo == topo_id) {
+                  if (cpuset_reserve((const GS_LDS TopoDev*)&s_topo, (GS_LDS CpuStateDev*)&cs, pk, nf, no.zkeys,
+                                     no.zcpu[0], no.zcpu[1], no.zcpu[2], no.zcpu[3], (GS_LDS NumaRow*)&d.nr,
+                                     (GS_LDS uint64_t*)s_cpuset)) {
+                    pl.flags |= PL_DEVICE_CPUSET;
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) pl.cpuset[j] = s_cpuset[j];
+                  } else {
+                    pl.flags |= PL_RESERVE_FAILED;
+                  }
+                } else {
+                  cut = 1;
+                }
               }
             }
           }
-        }
-        a.out[p] = pl;
-        for (int s = 0; s < 7; ++s) d.free[s] = dr.free[s] - pk.req[s];
-        d.nzfree[0] = dr.nzfree[0] - pk.nz[0];
-        d.nzfree[1] = dr.nzfree[1] - pk.nz[1];
-        d.free_pods = dr.free_pods - 1;
-        d.la_free[0] = dr.la_free[0] - pk.est[0];
-        d.la_free[1] = dr.la_free[1] - pk.est[1];
-        if (pk.flags & PF_PROD) {
-          d.la_pfree[0] = dr.la_pfree[0] - pk.est[0];
-          d.la_pfree[1] = dr.la_pfree[1] - pk.est[1];
+          a.out[p] = pl;
+          for (int s = 0; s < 7; ++s) d.free[s] = dr.free[s] - pk.req[s];
+          d.nzfree[0] = dr.nzfree[0] - pk.nz[0];
+          d.nzfree[1] = dr.nzfree[1] - pk.nz[1];
+          d.free_pods = dr.free_pods - 1;
+          d.la_free[0] = dr.la_free[0] - pk.est[0];
+          d.la_free[1] = dr.la_free[1] - pk.est[1];
+          if (pk.flags & PF_PROD) {
+            d.la_pfree[0] = dr.la_pfree[0] - pk.est[0];
+            d.la_pfree[1] = dr.la_pfree[1] - pk.est[1];
+          }
         }
       }
-      cut = __shfl(cut, 0);
+      cut = __builtin_amdgcn_readlane(cut, 0);
       WAVE_FENCE();
       STAMP(4);
       // ------------------------------------------------------------ the new state's hint table, re-score for p+1
-      if (numa_on) {
-        const NumaRow nr = d.nr;
-        if ((nr.nflags >> NF_POLICY_SHIFT) & 3u) hint_table_fill(s_ht[par], nr, zone_avail(nr), lane);
-        if (eval_so) {
-          const NumaRow no = orow[par].nr;
-          if ((no.nflags >> NF_POLICY_SHIFT) & 3u) hint_table_fill(s_hto[par], no, zone_avail(no), lane);
-        }
-        WAVE_FENCE();
-      }
       const bool last = p == B - 1 || cut;
-      if (!last) {
-        if (lane == 0) {
-          const Row rr = d;
-          dsc[(p + 1) * B + slot] = (int16_t)row_score(rr, pods(p + 1), a.pf, m, &s_ht[par]);
-        } else if (lane == 1 && eval_so) {
-          const Row rr = orow[par];
-          dso[(p + 1) * B + slot] = (int16_t)row_score(rr, pods(p + 1), a.pf, m, &s_hto[par]);
+      {
+        const Row rr = d;   // the row after assume + Reserve (wave-uniform)
+        if (numa_on) {
+          if ((rr.nr.nflags >> NF_POLICY_SHIFT) & 3u) hint_table_fill(s_ht[par], rr.nr, zone_avail(rr.nr), lane);
+          if (eval_so) {
+            const NumaRow no = orow[par].nr;
+            if ((no.nflags >> NF_POLICY_SHIFT) & 3u) hint_table_fill(s_hto[par], no, zone_avail(no), lane);
+          }
+        }
+        if (!last) {   // the whole wave evaluates the pair (current score; batch-start score when evaluated)
+          for (int it = 0; it < (eval_so ? 2 : 1); ++it) {   // one call site: one inlined copy of the evaluation
+            const Row ru = it ? orow[par] : rr;
+            const int32_t x = row_score_wave(ru, pods(p + 1), a.pf, m, nullptr);
+            if (lane == 0) (it ? dso : dsc)[(p + 1) * B + slot] = (int16_t)x;
+          }
         }
       }
       if (lane == 0) {
@@ -590,13 +599,12 @@ __global__ void __launch_bounds__(256) commit_pipe_kernel(CommitArgs a) {
         if (s >= 0 && n > 0) {
           const int ch = (n + RS_WAVES - 1) / RS_WAVES;
           const int q = p + 1 + wr * ch + lane;
-          if (lane < ch && q < B) {
-            const Row rr = drows[s];   // wave-uniform
-            dsc[q * B + s] = (int16_t)row_score(rr, pods(q), a.pf, m, &s_ht[pr]);
-          }
-          if (s_weval[pr] && lane < ch && q < B) {
-            const Row rr = orow[pr];
-            dso[q * B + s] = (int16_t)row_score(rr, pods(q), a.pf, m, &s_hto[pr]);
+          const int nit = s_weval[pr] ? 2 : 1;   // current scores; batch-start scores when evaluated
+          for (int it = 0; it < nit; ++it) {       // one call site: one inlined copy of the evaluation
+            if (lane < ch && q < B) {
+              const Row rr = it ? orow[pr] : drows[s];   // wave-uniform
+              (it ? dso : dsc)[q * B + s] = (int16_t)row_score(rr, pods(q), a.pf, m, it ? &s_hto[pr] : &s_ht[pr]);
+            }
           }
         }
       }
@@ -636,7 +644,8 @@ __global__ void __launch_bounds__(256) commit_pipe_kernel(CommitArgs a) {
   if (ST) {   // per-phase cycle sums of wave 0 (lane 0) and wave 1 (lane 0)
     if (tid == 0)
       for (int i = 0; i < 7; ++i) atomicAdd(reinterpret_cast<unsigned long long*>(&a.stamps[i]), st_acc[i]);
-    if (tid == 0) atomicAdd(reinterpret_cast<unsigned long long*>(&a.stamps[11]), st_acc[11]);
+    if (tid == 0)
+      for (int i = 11; i < 18; ++i) atomicAdd(reinterpret_cast<unsigned long long*>(&a.stamps[i]), st_acc[i]);
     if (tid == 64)
       for (int i = 7; i < 11; ++i) atomicAdd(reinterpret_cast<unsigned long long*>(&a.stamps[i]), st_acc[i]);
   }

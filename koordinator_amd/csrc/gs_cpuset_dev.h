@@ -18,9 +18,9 @@
 #include "../../include/gpuscore.h"
 
 #if defined(__HIP__)
-#define GS_HD __host__ __device__
+#define GS_HD __host__ __device__ inline __attribute__((always_inline))
 #else
-#define GS_HD
+#define GS_HD inline
 #endif
 
 namespace gs {
@@ -56,16 +56,16 @@ enum : uint32_t {
   CM_MOST = 1u << 24,    // NUMAAllocateStrategy MostAllocated (GetNUMAAllocateStrategy, util.go:35-41)
 };
 
-GS_HD inline int td_pc(uint64_t x) { return __builtin_popcountll(x); }
-GS_HD inline int td_ctz(uint64_t x) { return __builtin_ctzll(x); }
-GS_HD inline int td_cnt(const uint64_t* P, uint64_t m) {
+GS_HD int td_pc(uint64_t x) { return __builtin_popcountll(x); }
+GS_HD int td_ctz(uint64_t x) { return __builtin_ctzll(x); }
+GS_HD int td_cnt(const uint64_t* P, uint64_t m) {
   return td_pc(P[0] & m) + td_pc(P[1] & m) + td_pc(P[2] & m) + td_pc(P[3] & m);
 }
-GS_HD inline uint64_t td_any(const uint64_t* P) { return P[0] | P[1] | P[2] | P[3]; }
-GS_HD inline uint64_t td_all(const TopoDev& t) { return t.ncores >= 64 ? ~0ull : ((1ull << t.ncores) - 1ull); }
+GS_HD uint64_t td_any(const uint64_t* P) { return P[0] | P[1] | P[2] | P[3]; }
+GS_HD uint64_t td_all(const TopoDev& t) { return t.ncores >= 64 ? ~0ull : ((1ull << t.ncores) - 1ull); }
 
 // E[v] = cores with exactly v CPUs set in P (v = 0..4), bit-sliced
-GS_HD inline void td_exact(const uint64_t* P, uint64_t* E) {
+GS_HD void td_exact(const uint64_t* P, uint64_t* E) {
   const uint64_t s0 = P[0] ^ P[1], c0 = P[0] & P[1], s1 = P[2] ^ P[3], c1 = P[2] & P[3];
   const uint64_t b0 = s0 ^ s1, t1 = s0 & s1;
   const uint64_t b1 = c0 ^ c1 ^ t1, b2 = (c0 & c1) | (c0 & t1) | (c1 & t1);
@@ -77,7 +77,7 @@ GS_HD inline void td_exact(const uint64_t* P, uint64_t* E) {
 }
 
 // position of the r-th set CPU of core k in P (-1: none)
-GS_HD inline int td_rth(const uint64_t* P, int k, int r) {
+GS_HD int td_rth(const uint64_t* P, int k, int r) {
   for (int j = 0; j < TD_POS; ++j)
     if ((P[j] >> k) & 1u) {
       if (r == 0) return j;
@@ -285,7 +285,7 @@ struct DAcc {
 };
 
 // Go 1.18 sort.Slice on <= 12 elements: gap-6 pass + insertion sort (as gs_numa_host.cpp go_sort_small)
-GS_HD inline void td_go_sort(int* id, int* sz, int n, bool desc) {
+GS_HD void td_go_sort(int* id, int* sz, int n, bool desc) {
   for (int i = 6; i < n; ++i)
     if (desc ? sz[i] > sz[i - 6] : sz[i] < sz[i - 6]) {
       int x = id[i]; id[i] = id[i - 6]; id[i - 6] = x;
@@ -299,7 +299,7 @@ GS_HD inline void td_go_sort(int* id, int* sz, int n, bool desc) {
 }
 
 // takeCPUs (cpu_accumulator.go:87-232); avail = planes of the CPUs it may take. false: the reference errors.
-GS_HD inline bool td_take_cpus(const TopoDev& t, const uint64_t* avail, uint64_t xc, uint32_t xn, int needed,
+GS_HD bool td_take_cpus(const TopoDev& t, const uint64_t* avail, uint64_t xc, uint32_t xn, int needed,
                                int bind, int ep, bool most, uint64_t* out) {
   DAcc a(t, avail, xc, xn, needed, ep, most);
   for (int j = 0; j < TD_POS; ++j) out[j] = 0;
@@ -373,14 +373,14 @@ GS_HD inline bool td_take_cpus(const TopoDev& t, const uint64_t* avail, uint64_t
 }
 
 // available CPUs (getAvailableCPUs, node_allocation.go:142-162, maxRefCount <= 1) as planes
-GS_HD inline void td_available(const TopoDev& t, const CpuStateDev& cs, uint64_t* P) {
+GS_HD void td_available(const TopoDev& t, const CpuStateDev& cs, uint64_t* P) {
   for (int j = 0; j < TD_POS; ++j) P[j] = t.pos_cores[j] & ~cs.un[j];
 }
-GS_HD inline int td_zone_node(const CpuStateDev& cs, int z) { return (int)((cs.meta >> (CM_ZIDX_SHIFT + 4 * z)) & 15u); }
+GS_HD int td_zone_node(const CpuStateDev& cs, int z) { return (int)((cs.meta >> (CM_ZIDX_SHIFT + 4 * z)) & 15u); }
 
 // allocateCPUSet (resource_manager.go:273-360) given the NUMA split Allocate produced (PlacementDev zkeys /
 // zcpu). false: the reference errors (cannot follow a feasible Filter; the host fails loudly).
-GS_HD inline bool td_allocate_cpuset(const TopoDev& t, const CpuStateDev& cs, int num_cpus, int bind, bool required,
+GS_HD bool td_allocate_cpuset(const TopoDev& t, const CpuStateDev& cs, int num_cpus, int bind, bool required,
                                      int ep, uint32_t zkeys, const int64_t* zcpu, uint64_t* out) {
   uint64_t P[TD_POS];
   td_available(t, cs, P);
@@ -435,7 +435,7 @@ GS_HD inline bool td_allocate_cpuset(const TopoDev& t, const CpuStateDev& cs, in
 
 // available-CPU counts of the cores `m` (raw | full-core CPUs << 9 | cores with a free CPU << 18), packed
 // as gs_numa_host.cpp count_available
-GS_HD inline int32_t td_counts(const TopoDev& t, const CpuStateDev& cs, uint64_t m) {
+GS_HD int32_t td_counts(const TopoDev& t, const CpuStateDev& cs, uint64_t m) {
   uint64_t P[TD_POS], E[5];
   td_available(t, cs, P);
   for (int j = 0; j < TD_POS; ++j) P[j] &= m;
@@ -447,7 +447,7 @@ GS_HD inline int32_t td_counts(const TopoDev& t, const CpuStateDev& cs, uint64_t
 }
 
 // the cpuset as a 256-bit CPU mask
-GS_HD inline void td_to_cpus(const TopoDev& t, const uint64_t* R, uint64_t* w) {
+GS_HD void td_to_cpus(const TopoDev& t, const uint64_t* R, uint64_t* w) {
   w[0] = w[1] = w[2] = w[3] = 0;
   for (int j = 0; j < TD_POS; ++j)
     for (uint64_t b = R[j]; b; b &= b - 1) {

@@ -136,6 +136,7 @@ struct gs_ctx {
   void* cb_user = nullptr;
   gs_stats stats{};
   uint64_t* d_stamps = nullptr;   // GS_COMMIT_STAMPS=1: commit-kernel phase cycle sums
+  uint64_t stats_all_pods = 0;     // pods placed by gs_schedule over the context's life (stamp averages)
   // NodeNUMAResource: per-node TopologyOptions + NodeAllocation mirror, registered CPU topologies
   std::vector<NumaNode> numa;
   std::vector<std::shared_ptr<TopoClass>> topos;
@@ -1073,6 +1074,9 @@ int gs_destroy(gs_ctx* c) {
       for (int i = 0; i < 12; ++i) tot += st[i];
       fprintf(stderr, "gpuscore commit phases (s_memtime ticks, %% of %llu):", (unsigned long long)tot);
       for (int i = 0; i < 12; ++i) fprintf(stderr, " p%d=%.1f%%", i, tot ? 100.0 * st[i] / tot : 0.0);
+      fprintf(stderr, "\n  raw ticks per committed pod (%llu pods):", (unsigned long long)c->stats_all_pods);
+      for (int i = 0; i < 18; ++i)
+        fprintf(stderr, " s%d=%.0f", i, c->stats_all_pods ? (double)st[i] / (double)c->stats_all_pods : 0.0);
       fprintf(stderr, " | policy-row rescoring: %llu pods, %.0f ticks per pair (thread 128)\n",
               (unsigned long long)st[12], st[12] ? (double)st[13] / st[12] : 0.0);
       fprintf(stderr, "  header staging (inside p0): %.1f%%\n", tot ? 100.0 * st[24] / tot : 0.0);
@@ -1319,6 +1323,7 @@ int gs_schedule(gs_ctx* c, const gs_pod* pods, uint32_t npods, const uint64_t* s
       apply_placement(c, pods[i + k], pd.node, cur_special);
     }
     c->stats.pods += committed;
+    c->stats_all_pods += committed;
     i += committed;
     inflight = false;
     if (spec) {

@@ -126,7 +126,7 @@ struct SlotsLds {
 // NUMA_POLICY_NODES = false: NodeNUMAResource's topology-policy path is compiled out (eval_kernel routes those
 // nodes to eval_numa_kernel)
 // table: the row's NUMA hint table (commit re-scoring of one row for many pods), else computed from the row.
-template <bool FULL, bool LDS_SCALARS, bool NUMA_POLICY_NODES = true, bool TABLE = false>
+template <bool FULL, bool LDS_SCALARS, bool NUMA_POLICY_NODES = true, bool TABLE = false, bool WAVE = false>
 __device__ __forceinline__ PairOut eval_pair(const Row& r, const PodVec& p, const Profile& pf, const MirrorView& m,
                                              const HintTable* table = nullptr) {
   PairOut o{0u, 0, 0, 0, 0u};
@@ -155,7 +155,7 @@ __device__ __forceinline__ PairOut eval_pair(const Row& r, const PodVec& p, cons
   // ---- NodeNUMAResource Filter (+ Admit) and Score (gs_numa_dev.h)
   if (pf.enabled & 0x30u) {
     NumaOut no;
-    if (LDS_SCALARS) no = numa_eval<NUMA_POLICY_NODES, TABLE>(r.nr, p, pf, SlotsLds{r, m}, pf.enabled & 0x10u,
+    if (LDS_SCALARS) no = numa_eval<NUMA_POLICY_NODES, TABLE, WAVE>(r.nr, p, pf, SlotsLds{r, m}, pf.enabled & 0x10u,
                                                               pf.enabled & 0x20u, -1, table);
     else no = numa_eval<NUMA_POLICY_NODES>(r.nr, p, pf, SlotsHbm{r, m}, pf.enabled & 0x10u, pf.enabled & 0x20u);
     if (pf.enabled & 0x10u) o.code |= no.reason << GS_FAIL_NUMA_SHIFT;
@@ -254,6 +254,12 @@ __device__ __forceinline__ int32_t row_score(const Row& d, const PodVec& p, cons
   return total_score(eval_pair<false, true, true, true>(d, p, pf, m, table), pf);
 }
 
+// one pair evaluated by all 64 lanes of a wave (row, pod and table wave-uniform); every lane gets the score
+__device__ __forceinline__ int32_t row_score_wave(const Row& d, const PodVec& p, const Profile& pf, const MirrorView& m,
+                                                  const HintTable* table) {
+  return total_score(eval_pair<false, true, true, true, true>(d, p, pf, m, table), pf);
+}
+
 __device__ __forceinline__ int hash_find(const int32_t* hkey, const int32_t* hval, uint32_t node) {
   uint32_t h = (node * 2654435761u) & (HASH - 1);
   for (int probe = 0; probe < HASH; ++probe) {
@@ -272,12 +278,37 @@ __device__ __forceinline__ const uint32_t* list_ptr(const CommitArgs& a, int r, 
   return reinterpret_cast<const uint32_t*>(a.xbase + (size_t)r * a.xblock) + (size_t)k * LCAP;
 }
 
+// Wave64 reductions and scan over DPP row operations (no LDS round trip, unlike __shfl_*: ds_bpermute). All 64
+// lanes must be active. quad_perm [1,0,3,2], [2,3,0,1], row_half_mirror, row_mirror reduce within a 16-lane row;
+// row_bcast15 (rows 1, 3) and row_bcast31 (rows 2, 3) carry the rows into lane 63.
+#define GS_DPP(old, v, ctrl, rmask) __builtin_amdgcn_update_dpp((old), (v), (ctrl), (rmask), 0xF, false)
 __device__ __forceinline__ int wave_max(int v) {
-  for (int off = 32; off > 0; off >>= 1) v = max(v, __shfl_xor(v, off));
-  return v;
+  constexpr int lo = -2147483647 - 1;
+  v = max(v, GS_DPP(lo, v, 0xB1, 0xF));
+  v = max(v, GS_DPP(lo, v, 0x4E, 0xF));
+  v = max(v, GS_DPP(lo, v, 0x141, 0xF));
+  v = max(v, GS_DPP(lo, v, 0x140, 0xF));
+  v = max(v, GS_DPP(lo, v, 0x142, 0xA));
+  v = max(v, GS_DPP(lo, v, 0x143, 0xC));
+  return __builtin_amdgcn_readlane(v, 63);
 }
 __device__ __forceinline__ int wave_sum(int v) {
-  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+  v += GS_DPP(0, v, 0xB1, 0xF);
+  v += GS_DPP(0, v, 0x4E, 0xF);
+  v += GS_DPP(0, v, 0x141, 0xF);
+  v += GS_DPP(0, v, 0x140, 0xF);
+  v += GS_DPP(0, v, 0x142, 0xA);
+  v += GS_DPP(0, v, 0x143, 0xC);
+  return __builtin_amdgcn_readlane(v, 63);
+}
+// inclusive prefix sum over lanes: row_shr 1, 2, 4, 8 within rows, then the row carries
+__device__ __forceinline__ int wave_incl_scan(int v) {
+  v += GS_DPP(0, v, 0x111, 0xF);
+  v += GS_DPP(0, v, 0x112, 0xF);
+  v += GS_DPP(0, v, 0x114, 0xF);
+  v += GS_DPP(0, v, 0x118, 0xF);
+  v += GS_DPP(0, v, 0x142, 0xA);
+  v += GS_DPP(0, v, 0x143, 0xC);
   return v;
 }
 
@@ -300,9 +331,16 @@ __device__ __forceinline__ void wave_rank_sort(uint32_t* v, int n, uint32_t* tmp
 // (gs_numa_host.cpp) would recompute them. false: allocateCPUSet errors (the host fails loudly).
 // Arguments live in LDS or registers (zone split by value, cpuset into an LDS array): nothing of the caller's
 // frame has its address taken, so the commit kernel keeps its Reserve state out of scratch.
-__device__ __forceinline__ bool cpuset_reserve(const TopoDev& t, CpuStateDev& cs, const PodVec& p, uint32_t nf,
-                                            uint32_t zkeys, int64_t zc0, int64_t zc1, int64_t zc2, int64_t zc3,
-                                            NumaRow& nr, uint64_t* cpuset) {
+#define GS_LDS __attribute__((address_space(3)))
+// Not inlined: its register pressure stays out of the commit loop. The LDS operands arrive as address-space-3
+// pointers and everything below is inlined here, so every access stays a ds_* instruction (a generic pointer would
+// make them flat loads that wait for outstanding global loads).
+__device__ __noinline__ bool cpuset_reserve(const GS_LDS TopoDev* tp, GS_LDS CpuStateDev* csp, const PodVec& p,
+                                            uint32_t nf, uint32_t zkeys, int64_t zc0, int64_t zc1, int64_t zc2,
+                                            int64_t zc3, GS_LDS NumaRow* nrp, GS_LDS uint64_t* cpuset) {
+  const TopoDev& t = *(const TopoDev*)tp;
+  CpuStateDev& cs = *(CpuStateDev*)csp;
+  NumaRow& nr = *(NumaRow*)nrp;
   const int64_t zcpu[4] = {zc0, zc1, zc2, zc3};
   // getCPUBindPolicy (util.go:85-103)
   const uint32_t pn = p.numa;
@@ -334,7 +372,9 @@ __device__ __forceinline__ bool cpuset_reserve(const TopoDev& t, CpuStateDev& cs
       nr.zadj[z] = (int32_t)(amplify_d(c, nr.amp) - c);
     }
   }
-  td_to_cpus(t, R, cpuset);
+  uint64_t w[4];
+  td_to_cpus(t, R, w);
+  for (int j = 0; j < 4; ++j) cpuset[j] = w[j];
   return true;
 }
 

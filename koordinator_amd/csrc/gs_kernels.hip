@@ -850,8 +850,9 @@ __global__ void __launch_bounds__(COMMIT_THREADS) commit_kernel(CommitArgs a) {
           if (rb) {
             CpuStateDev& cs = cst[slot];
             if (cs.topo >= 0 && cs.topo == s_topo_id) {
-              if (cpuset_reserve(s_topo, cs, pk, nf, no.zkeys, no.zcpu[0], no.zcpu[1], no.zcpu[2], no.zcpu[3],
-                                 d.nr, s_cpuset)) {
+              if (cpuset_reserve((const GS_LDS TopoDev*)&s_topo, (GS_LDS CpuStateDev*)&cs, pk, nf, no.zkeys, no.zcpu[0],
+                                 no.zcpu[1], no.zcpu[2], no.zcpu[3],
+                                 (GS_LDS NumaRow*)&d.nr, (GS_LDS uint64_t*)s_cpuset)) {
                 pl.flags |= PL_DEVICE_CPUSET;
 #pragma unroll
                 for (int j = 0; j < 4; ++j) pl.cpuset[j] = s_cpuset[j];

@@ -253,27 +253,14 @@ __device__ __forceinline__ int32_t hint_score(const HintSums& s, int64_t pcpu, i
   return ws ? sdiv(ns, ws) : 0;
 }
 
-// GetPodTopologyHints + topologyManager policy Merge + admit (topology_hint.go:41-67, resource_manager.go
-// :418-532, policy.go:68-186, policy_*.go). Returns the admit verdict; aff_has / aff = the merged affinity.
-template <class Src>
-__device__ __forceinline__ bool hints_merge(const Src& src, int nz, int policy, bool nil_hints, bool has_cpu,
-                                            bool has_mem, int64_t pcpu, int64_t mem, bool tot_c_any, bool tot_m_any,
-                                            const Profile& pf, bool& aff_has, uint32_t& aff) {
-  const uint32_t valid = ord_valid(nz);
-  // generateHints (resource_manager.go:499-532) for every position: total >= request (the size minimum) and
-  // free >= request (a hint)
-  uint32_t totc = 0, totm = 0, lc = 0, lm = 0;
-  if (!nil_hints) {
-#pragma unroll 1
-    for (int mi = 0; mi < 15; ++mi) {
-      if (!(valid >> mi & 1u)) continue;
-      const HintSums s = src.sum(mi);
-      if (s.tc >= pcpu) { totc |= 1u << mi; if (s.fc >= pcpu) lc |= 1u << mi; }
-      if (s.tm >= mem) { totm |= 1u << mi; if (s.fm >= mem) lm |= 1u << mi; }
-    }
-    if (!has_cpu) totc = lc = 0;
-    if (!has_mem) totm = lm = 0;
-  }
+// topologyManager policy Merge + admit over the provider's hint lists (policy.go:68-186, policy_*.go), given as
+// position bitmaps (lc cpu, lm memory) with the positions whose total covers the request (totc, totm); score_at(mi)
+// = the hint score of position mi. Returns the admit verdict; aff_has / aff = the merged affinity.
+template <class ScoreAt>
+__device__ __forceinline__ bool merge_hint_lists(uint32_t totc, uint32_t lc, uint32_t totm, uint32_t lm, int nz,
+                                                 int policy, bool nil_hints, bool has_cpu, bool has_mem,
+                                                 bool tot_c_any, bool tot_m_any, ScoreAt&& score_at, bool& aff_has,
+                                                 uint32_t& aff) {
   const int min_c = totc ? ord_size_first(totc) : nz, min_m = totm ? ord_size_first(totm) : nz;
   // filterProvidersHints (policy.go:98-126): lists in resource-name order cpu, memory.
   // kind: 0 absent, 1 hints, 2 the empty-list marker {nil, false}
@@ -286,18 +273,6 @@ __device__ __forceinline__ bool hints_merge(const Src& src, int nz, int policy, 
   bool b_pref = false;
   uint32_t b_mask = full_mask;
   int32_t b_score = 0;
-  // hint scores of positions, evaluated once each when a comparison needs them, packed 7 bits per position
-  uint64_t sc_lo = 0, sc_hi = 0;
-  uint32_t have = 0;
-  auto score_at = [&](int mi) -> int32_t {
-    if (!(have >> mi & 1u)) {
-      const uint64_t s = (uint64_t)hint_score(src.sum(mi), pcpu, mem, pf);
-      if (mi < 9) sc_lo |= s << (7 * mi);
-      else sc_hi |= s << (7 * (mi - 9));
-      have |= 1u << mi;
-    }
-    return (int32_t)((mi < 9 ? sc_lo >> (7 * mi) : sc_hi >> (7 * (mi - 9))) & 127u);
-  };
   // Fast path (exact): when every present list has single-zone preferred hints (min size 1), a preferred merged
   // hint is only produced by equal single-bit masks, so the preferred, narrowest candidates are the single zones
   // present in every list (positions 0..nz-1), visited in ascending zone order; mergeFilteredHints keeps the first
@@ -384,6 +359,59 @@ __device__ __forceinline__ bool hints_merge(const Src& src, int nz, int policy, 
   return true;
 }
 
+// GetPodTopologyHints (topology_hint.go:41-67 -> resource_manager.go:418-532: generateHints for every position,
+// total >= request = the size minimum, free >= request = a hint) + merge_hint_lists, one pair per lane. Hint scores
+// are evaluated once each when a comparison needs them, packed 7 bits per position.
+template <class Src>
+__device__ __forceinline__ bool hints_merge(const Src& src, int nz, int policy, bool nil_hints, bool has_cpu,
+                                            bool has_mem, int64_t pcpu, int64_t mem, bool tot_c_any, bool tot_m_any,
+                                            const Profile& pf, bool& aff_has, uint32_t& aff) {
+  const uint32_t valid = ord_valid(nz);
+  uint32_t totc = 0, totm = 0, lc = 0, lm = 0;
+  if (!nil_hints) {
+#pragma unroll 1
+    for (int mi = 0; mi < 15; ++mi) {
+      if (!(valid >> mi & 1u)) continue;
+      const HintSums s = src.sum(mi);
+      if (s.tc >= pcpu) { totc |= 1u << mi; if (s.fc >= pcpu) lc |= 1u << mi; }
+      if (s.tm >= mem) { totm |= 1u << mi; if (s.fm >= mem) lm |= 1u << mi; }
+    }
+    if (!has_cpu) totc = lc = 0;
+    if (!has_mem) totm = lm = 0;
+  }
+  uint64_t sc_lo = 0, sc_hi = 0;
+  uint32_t have = 0;
+  auto score_at = [&](int mi) -> int32_t {
+    if (!(have >> mi & 1u)) {
+      const uint64_t s = (uint64_t)hint_score(src.sum(mi), pcpu, mem, pf);
+      if (mi < 9) sc_lo |= s << (7 * mi);
+      else sc_hi |= s << (7 * (mi - 9));
+      have |= 1u << mi;
+    }
+    return (int32_t)((mi < 9 ? sc_lo >> (7 * mi) : sc_hi >> (7 * (mi - 9))) & 127u);
+  };
+  return merge_hint_lists(totc, lc, totm, lm, nz, policy, nil_hints, has_cpu, has_mem, tot_c_any, tot_m_any, score_at,
+                          aff_has, aff);
+}
+
+// The same for ONE pair evaluated by all 64 lanes of a wave with wave-uniform inputs: lane mi < 15 takes position
+// mi (its sums from the row's zone values, compares, hint score), the lists are ballots, and the merge reads
+// scores from the lanes. No LDS traffic.
+__device__ __forceinline__ bool hints_merge_wave(const HintRegs& h, int nz, int policy, bool nil_hints, bool has_cpu,
+                                                 bool has_mem, int64_t pcpu, int64_t mem, bool tot_c_any,
+                                                 bool tot_m_any, const Profile& pf, bool& aff_has, uint32_t& aff) {
+  const int lane = (int)__lane_id();
+  const bool on = !nil_hints && lane < 15 && (ord_valid(nz) >> lane & 1u);
+  const HintSums s = h.sum(lane < 15 ? lane : 0);
+  const bool tc = on && has_cpu && s.tc >= pcpu, tm = on && has_mem && s.tm >= mem;
+  const uint32_t totc = (uint32_t)__ballot(tc), lc = (uint32_t)__ballot(tc && s.fc >= pcpu);
+  const uint32_t totm = (uint32_t)__ballot(tm), lm = (uint32_t)__ballot(tm && s.fm >= mem);
+  const int32_t sc = on ? hint_score(s, pcpu, mem, pf) : 0;
+  auto score_at = [&](int mi) -> int32_t { return __builtin_amdgcn_readlane(sc, mi); };
+  return merge_hint_lists(totc, lc, totm, lm, nz, policy, nil_hints, has_cpu, has_mem, tot_c_any, tot_m_any, score_at,
+                          aff_has, aff);
+}
+
 // One (pod, node) evaluation. do_filter: run Filter (incl. the topology manager Admit that sets the affinity);
 // do_score: Score with that affinity (none when the filter is off, as in the reference without a Filter call).
 // `alloc[s]`/`free[s]` give NodeInfo.Allocatable / Allocatable-Requested for slots 0..2 and the scalars.
@@ -392,7 +420,8 @@ __device__ __forceinline__ bool hints_merge(const Src& src, int nz, int policy, 
 // known_aff >= 0: the affinity this pair's Filter produced on the same row state (NumaOut.aff; Reserve of a
 // row untouched since the batch-start evaluation): hint generation and merge are skipped.
 // TABLE: the row's hint sums come from `table` (the commit kernel), else they are computed from the row's zones.
-template <bool POLICY_NODES = true, bool TABLE = false, class Slots>
+// WAVE: one pair evaluated by a whole wave with wave-uniform inputs (hints_merge_wave over the row's registers).
+template <bool POLICY_NODES = true, bool TABLE = false, bool WAVE = false, class Slots>
 __device__ __forceinline__ NumaOut numa_eval(const NumaRow& r, const PodVec& p, const Profile& pf, const Slots& sl,
                                              bool do_filter, bool do_score, int known_aff = -1,
                                              const HintTable* table = nullptr) {
@@ -493,7 +522,9 @@ __device__ __forceinline__ NumaOut numa_eval(const NumaRow& r, const PodVec& p, 
     const int v = hint_variant(reqflag, bind);
     const bool tca = (nf >> NF_ZCPU_SHIFT) & ((1u << nz) - 1u), tma = (nf >> NF_ZMEM_SHIFT) & ((1u << nz) - 1u);
     bool admit;
-    if (TABLE) admit = hints_merge(HintTableRef{table, v}, nz, policy, nil_hints, has_cpu, has_mem, pcpu, mem, tca, tma,
+    if (WAVE) admit = hints_merge_wave(hint_regs(r, za, v), nz, policy, nil_hints, has_cpu, has_mem, pcpu, mem, tca, tma,
+                                       pf, aff_has, aff);
+    else if (TABLE) admit = hints_merge(HintTableRef{table, v}, nz, policy, nil_hints, has_cpu, has_mem, pcpu, mem, tca, tma,
                                    pf, aff_has, aff);
     else admit = hints_merge(hint_regs(r, za, v), nz, policy, nil_hints, has_cpu, has_mem, pcpu, mem, tca, tma, pf,
                              aff_has, aff);
