@@ -3,8 +3,9 @@
 A step = one pass of the hot path over one batch of synthetic pending pods: the scheduleOne loop
 (NodeResourcesFit + LoadAwareScheduling + NodeNUMAResource Filter over every node, their Scores, selectHost,
 assume + Reserve incl. NUMA allocation and cpuset selection) for `--pods-per-step` pods, sequentially, against
-the 50k-node synthetic C3 cluster (weak scaling: 50k nodes per GPU, node-sharded, RCCL all-gather of per-shard
-candidate lists per batch). `--profile la-fit` drops NodeNUMAResource (the C2 plugin set).
+the 50k-node synthetic C3 cluster. Several GPUs: strong scaling by default (the metric's 50k nodes in total,
+node-sharded, RCCL all-gather of per-shard candidate lists per batch, the commit replicated); `--scaling weak`
+gives every GPU 50k nodes. `--profile la-fit` drops NodeNUMAResource (the C2 plugin set).
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
@@ -28,31 +29,57 @@ METRIC = "pod×node Filter+Score evals/sec + pods/sec at 50k nodes, 1/2/4/8 GPUs
 HBM_PEAK_GBPS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md)
 
 
-def cpu_baseline(cluster, cfg, sample_pods: int, threads: int) -> dict:
-    """The CPU restatement of the reference Go path (oracle, kind "port") on a bounded sample."""
+def cpu_baseline(cluster, cfg, pods, seq, given, sample_start: int, sample_pods: int, threads: int) -> dict:
+    """The CPU restatement of the reference Go path (oracle, kind "port") on the state the GPU's timed region started
+    from: the oracle replays the GPU's placements of pods [0, sample_start) (the warm-up steps), then runs the full
+    scheduleOne on the next pods — an untimed warm-up chunk, then 5 timed chunks (median pods/s) with Filter / Score /
+    selectHost / Reserve timed separately, then a single-thread chunk."""
     from oracle import oracle as orc
-    o = orc.Oracle(cfg)
     from koordinator_amd import synth
+    o = orc.Oracle(cfg)
     synth.load_into(o, cluster)
-    pods = cluster.pods[:sample_pods]
+    if sample_start:
+        o.schedule_replay(pods[:sample_start], given[:sample_start], seq[:sample_start], nthreads=threads)
+    i = sample_start
+    warm = max(8, sample_pods // 10)
+    o.schedule(pods[i:i + warm], seq[i:i + warm], nthreads=threads)
+    i += warm
+    o.phase_times()
+    chunk = max(1, (sample_pods - warm) // 5)
+    rates, secs = [], 0.0
+    for _ in range(5):
+        t0 = time.perf_counter()
+        o.schedule(pods[i:i + chunk], seq[i:i + chunk], nthreads=threads)
+        dt = time.perf_counter() - t0
+        rates.append(chunk / dt)
+        secs += dt
+        i += chunk
+    phases = o.phase_times()
+    n1 = max(4, chunk // 8)
     t0 = time.perf_counter()
-    o.schedule(pods, nthreads=threads)
-    dt = time.perf_counter() - t0
-    return {"evals_per_s": sample_pods * cluster.num_nodes / dt, "pods_per_s": sample_pods / dt, "seconds": dt}
+    o.schedule(pods[i:i + n1], seq[i:i + n1], nthreads=1)
+    r1 = n1 / (time.perf_counter() - t0)
+    pods_per_s = float(np.median(rates))
+    return {"pods_per_s": pods_per_s, "evals_per_s": pods_per_s * cluster.num_nodes, "seconds": secs,
+            "chunks": 5, "chunk_pods": chunk, "chunk_pods_per_s": rates,
+            "phase_share": {k: v / max(secs, 1e-12) for k, v in phases.items()},
+            "single_thread_pods_per_s": r1, "single_thread_evals_per_s": r1 * cluster.num_nodes,
+            "sample": f"pods {sample_start}..{i + n1} of the timed workload on the GPU's state at the start of the timed "
+                      f"region (oracle replay of the {sample_start} warm-up placements); {warm} warm-up pods, 5 x "
+                      f"{chunk} timed pods at {threads} threads (median), {n1} pods at 1 thread"}
 
 
 PMC_FILE = os.path.join(ROOT, "profiles", "pmc_latest.json")
 
 
-def pmc_traffic() -> tuple[float | None, str | None]:
-    """HBM bytes per eval pass from the committed rocprofv3 PMC summary (scripts/gpu_profile.sh ->
-    scripts/pmc_summary.py): counters cannot be read from inside this process, so the figure is the one measured
-    by the separate --pmc passes over this same bench command."""
+def pmc_summary() -> tuple[dict | None, str | None]:
+    """Per-kernel HBM bytes per launch from the committed rocprofv3 PMC summary (scripts/gpu_profile.sh ->
+    scripts/pmc_summary.py; separate --pmc FETCH_SIZE / WRITE_SIZE passes over a 1-step run of this bench): counters
+    cannot be read from inside this process."""
     try:
         with open(PMC_FILE) as f:
-            d = json.load(f)
-        return float(d["eval_pass"]["hbm_bytes_per_launch"]), os.path.relpath(PMC_FILE, ROOT)
-    except (OSError, KeyError, ValueError):
+            return json.load(f), os.path.relpath(PMC_FILE, ROOT)
+    except (OSError, ValueError):
         return None, None
 
 
@@ -61,7 +88,9 @@ def main() -> None:
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--nodes-per-gpu", type=int, default=50_000)
+    ap.add_argument("--nodes", type=int, default=50_000,
+                    help="cluster nodes (strong scaling: in total, the metric's 50k; weak: per GPU)")
+    ap.add_argument("--scaling", choices=["strong", "weak"], default="strong")
     ap.add_argument("--pods-per-step", type=int, default=2048)
     ap.add_argument("--batch", type=int, default=128)
     ap.add_argument("--cpu-sample-pods", type=int, default=400)
@@ -89,7 +118,7 @@ def main() -> None:
     from koordinator_amd import config, synth
     from koordinator_amd.engine import Engine, unique_id
 
-    n_nodes = args.nodes_per_gpu * world
+    n_nodes = args.nodes if args.scaling == "strong" else args.nodes * world
     total_pods = (args.warmup + args.steps) * args.pods_per_step
     cluster = synth.make_cluster(n_nodes, total_pods, config_id=2)
     numa = args.profile == "c3"
@@ -102,22 +131,6 @@ def main() -> None:
                              enabled=abi.GS_ENABLE_ALL if numa else abi.GS_ENABLE_LA_FIT,
                              percentage_of_nodes_to_score=args.sample_pct)
 
-    cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        threads = min(os.cpu_count() or 1, int(os.environ.get("OMP_NUM_THREADS", "16")), 16)
-        r16 = cpu_baseline(cluster, cfg, args.cpu_sample_pods, threads)
-        r1 = cpu_baseline(cluster, cfg, max(20, args.cpu_sample_pods // 8), 1)
-        nall = len(os.sched_getaffinity(0)) or 1
-        rall = cpu_baseline(cluster, cfg, args.cpu_sample_pods, nall) if nall > threads else r16
-        cpu = {"value": r16["evals_per_s"], "unit": "evals/s", "cores": threads, "kind": "port",
-               "sample": f"first {args.cpu_sample_pods} pods of the same {n_nodes}-node cluster, sequential "
-                         f"scheduleOne with Filter/Score fanned out over {threads} threads "
-                         f"(parallelize.Until emulation, parallelism={threads}); CPU restatement of the "
-                         f"reference Go path (oracle/), not the Go binary",
-               "pods_per_s": r16["pods_per_s"], "seconds": r16["seconds"],
-               "single_thread_evals_per_s": r1["evals_per_s"],
-               "all_cores": {"threads": nall, "evals_per_s": rall["evals_per_s"], "pods_per_s": rall["pods_per_s"]}}
-
     eng = Engine(cfg)
     if world > 1:
         uid = [unique_id() if rank == 0 else None]
@@ -127,9 +140,11 @@ def main() -> None:
 
     pods = cluster.pods
     seq = np.arange(total_pods, dtype=np.uint64)
+    given = np.full(total_pods, -1, np.int32)   # the GPU's placements (the CPU baseline replays the warm-up ones)
     P = args.pods_per_step
     for w in range(args.warmup):
-        eng.schedule(pods[w * P:(w + 1) * P], seq[w * P:(w + 1) * P])
+        out = eng.schedule(pods[w * P:(w + 1) * P], seq[w * P:(w + 1) * P])
+        given[w * P:(w + 1) * P] = np.where(out["node"] >= 0, out["node"], -2)
     eng.synchronize()
     eng.reset_stats()
 
@@ -155,12 +170,56 @@ def main() -> None:
     pods_timed = args.steps * P
     evals = pods_timed * n_nodes
     value = evals / dt
+    bpe = st["node_row_bytes"]
+    # BASELINE.md §4 / SURVEY §8(d): roofline.achieved = evals/s over the timed steps x algorithmic bytes per eval
+    achieved = value * bpe / 1e9
+    batches = max(1, st["batches"])
     launches = max(1, st["eval_launches"])
-    avg_launch_ms = st["eval_ms"] / launches
+    eval_us = st["eval_ms"] / launches * 1e3
     pairs_per_launch = st["eval_pairs"] / launches
-    bytes_per_launch = pairs_per_launch * st["node_row_bytes"]
-    achieved = bytes_per_launch / (avg_launch_ms * 1e-3) / 1e9 if avg_launch_ms > 0 else 0.0
-    traffic, traffic_src = pmc_traffic() if numa else (None, None)
+    eval_achieved = pairs_per_launch * bpe / (eval_us * 1e-6) / 1e9 if eval_us > 0 else 0.0
+    step_ms = dt / args.steps * 1e3
+    pmc, pmc_src = pmc_summary() if numa else (None, None)
+    kpmc = (pmc or {}).get("kernels", {})
+
+    def pmc_bytes(prefix):
+        ks = [k for k in kpmc if k.startswith(prefix)]
+        return sum(kpmc[k]["hbm_bytes_per_launch"] for k in ks) if ks else None
+
+    traffic_step = None
+    if kpmc:
+        steps_in_pmc = max(1, kpmc.get("gs::commit_pipe_kernel<false>", kpmc.get("gs::commit_kernel<false>", {}))
+                           .get("dispatches", batches / args.steps) / max(1.0, batches / args.steps))
+        traffic_step = sum(v["hbm_bytes_per_launch"] * v["dispatches"] for k, v in kpmc.items()
+                           if k.startswith("gs::")) / steps_in_pmc
+    kernels = {
+        "eval_pass": {"kernels": "eval_kernel + eval_numa_kernel (concurrent streams), one launch each per batch",
+                      "avg_launch_us": eval_us, "pairs_per_launch": pairs_per_launch,
+                      "achieved_GBps": eval_achieved, "frac": eval_achieved / HBM_PEAK_GBPS,
+                      "pmc_bytes_per_launch": pmc_bytes("gs::eval"),
+                      "share_of_step": st["eval_ms"] / args.steps / step_ms},
+        "cand_kernel": {"avg_launch_us": st["cand_ms"] / batches * 1e3, "pmc_bytes_per_launch": pmc_bytes("gs::cand"),
+                        "share_of_step": st["cand_ms"] / args.steps / step_ms},
+        "commit_kernel": {"bound": "latency: one workgroup walks the batch's pods in order (selectHost, Reserve, "
+                                   "re-scoring of the rows earlier pods landed on)",
+                          "avg_launch_us": st["commit_ms"] / batches * 1e3,
+                          "us_per_pod": st["commit_ms"] * 1e3 / max(1, st["pods"]),
+                          "pmc_bytes_per_launch": pmc_bytes("gs::commit"),
+                          "share_of_step": st["commit_ms"] / args.steps / step_ms},
+    }
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        threads = min(os.cpu_count() or 1, int(os.environ.get("OMP_NUM_THREADS", "16")), 16)
+        sample_start = args.warmup * P
+        r = cpu_baseline(cluster, cfg, pods, seq, given, sample_start, args.cpu_sample_pods, threads)
+        cpu = {"value": r["evals_per_s"], "unit": "evals/s", "cores": threads, "kind": "port",
+               "sample": r["sample"] + f"; sequential scheduleOne with Filter/Score fanned out over {threads} threads "
+                         "(parallelize.Until emulation, parallelism=16 = the reference default and this box's CPU "
+                         "share); CPU restatement of the reference Go path (oracle/), not the Go binary",
+               "pods_per_s": r["pods_per_s"], "seconds": r["seconds"], "chunk_pods_per_s": r["chunk_pods_per_s"],
+               "phase_share": r["phase_share"], "single_thread_evals_per_s": r["single_thread_evals_per_s"],
+               "single_thread_pods_per_s": r["single_thread_pods_per_s"]}
 
     if rank == 0:
         line = {
@@ -170,22 +229,24 @@ def main() -> None:
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
-            "ms_per_step": dt / args.steps * 1e3,
+            "ms_per_step": step_ms,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": args.scaling,
             "vs_baseline": None,
             "dtype": "int64",
             "data": "synthetic",
             "pods_per_s": pods_timed / dt,
             "config": {
-                "workload": (f"C3: {n_nodes} nodes ({args.nodes_per_gpu}/GPU) x {P} pods/step, sequential scheduleOne "
-                             "with NodeResourcesFit(LeastAllocated) + LoadAwareScheduling + NodeNUMAResource filter+"
-                             "score (30% NUMA-policy nodes, 20% LSE/LSR cpuset pods), selectHost, assume+Reserve"
+                "workload": (f"C3: {n_nodes} nodes ({args.scaling} scaling over {world} GPU) x {P} pods/step, "
+                             "sequential scheduleOne with NodeResourcesFit(LeastAllocated) + LoadAwareScheduling + "
+                             "NodeNUMAResource filter+score (30% NUMA-policy nodes, 20% LSE/LSR cpuset pods), "
+                             "selectHost, assume+Reserve"
                              if numa else
-                             f"C2 plugin set at C3 scale: {n_nodes} nodes ({args.nodes_per_gpu}/GPU) x {P} pods/step, "
-                             "NodeResourcesFit(LeastAllocated)+LoadAwareScheduling filter+score, selectHost, "
-                             "assume+Reserve"),
-                "nodes": n_nodes, "pods_per_step": P, "batch": args.batch, "parallelism": f"node-shard x{world}",
+                             f"C2 plugin set at C3 scale: {n_nodes} nodes ({args.scaling} scaling over {world} GPU) x "
+                             f"{P} pods/step, NodeResourcesFit(LeastAllocated)+LoadAwareScheduling filter+score, "
+                             "selectHost, assume+Reserve"),
+                "nodes": n_nodes, "pods_per_step": P, "batch": args.batch,
+                "parallelism": f"node-shard x{world}, commit replicated on every rank",
                 "level_list_cap": 2048,
                 "node_sampling": None if args.sample_pct is None else {
                     "percentage_of_nodes_to_score": args.sample_pct,
@@ -199,17 +260,14 @@ def main() -> None:
                 "peak": HBM_PEAK_GBPS,
                 "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBPS,
-                "traffic": traffic,
-                "traffic_unit": "bytes per eval pass (2 x FETCH_SIZE + WRITE_SIZE, gfx950 correction)",
-                "traffic_source": traffic_src,
-                "kernel": "eval pass = eval_kernel + eval_numa_kernel (one launch each per batch)",
-                "bytes_per_eval": st["node_row_bytes"],
-                "avg_launch_us": avg_launch_ms * 1e3,
-                "pairs_per_launch": pairs_per_launch,
-                "note": f"algorithmic bytes = {st['node_row_bytes']} B node row per pod x node eval (un-batched "
-                        "convention); eval_kernel reads each row once per group of 16 pods (eval_numa_kernel: "
-                        "once per 2 pods), so frac > 1 would mean reuse; avg_launch_us is the HIP-event time of the "
-                        "pass on the library stream",
+                "traffic": traffic_step,
+                "traffic_unit": "HBM bytes per step, all gs:: kernels (rocprofv3 PMC: 2 x FETCH_SIZE + WRITE_SIZE, "
+                                "gfx950 correction)",
+                "traffic_source": pmc_src,
+                "bytes_per_eval": bpe,
+                "convention": "BASELINE.md §4 / SURVEY §8(d): achieved = evals/s over the driver-timed steps x "
+                              "bytes_per_eval (the node row one un-batched pod x node evaluation reads)",
+                "kernels": kernels,
             },
             "breakdown_ms": {"eval": st["eval_ms"], "cand": st["cand_ms"], "commit": st["commit_ms"],
                              "exchange": st["exchange_ms"], "batches": st["batches"], "cuts": st["cuts"],

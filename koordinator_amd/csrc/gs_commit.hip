@@ -97,7 +97,7 @@ __global__ void __launch_bounds__(256) commit_pipe_kernel(CommitArgs a) {
   }
 
   // ---- prologue: pods, hash, pod 0's prefetch
-  uint64_t st_acc[18] = {};
+  uint64_t st_acc[27] = {};
   uint64_t st_last = ST ? __builtin_amdgcn_s_memtime() : 0;
 // (diagnostic build: nothing moves across a stamp, and a phase's outstanding memory operations complete inside it)
 #define STAMP(i)                                    \
@@ -344,50 +344,126 @@ __global__ void __launch_bounds__(256) commit_pipe_kernel(CommitArgs a) {
         const uint64_t got = __ballot(cand != 0xffffffffu);
         if (!got) action = 2;   // unreachable for a valid max: cut, exact re-run on the host
         else winner = (uint32_t)__builtin_amdgcn_readlane((int)cand, __ffsll((long long)got) - 1);
+        STAMP(16);
       }
+      STAMP(17);
+      if (ST) { st_acc[18] += full_row ? 1 : 0; st_acc[19] += action == 1 ? 1 : 0; st_acc[20] += slowpath ? 1 : 0; }
       if (full_row) {
         // ---- exact full-row resolution of pod p on the single shard: batch-start scores S[p][*] for clean nodes,
         // current scores for dirty rows; max, ties and feasible count, then the jp-th tie in node order
+        // (coalesced 16-B loads, lane l holds nodes [8l, 8l+8) of each 512-node block). A dirty row's batch-start
+        // score is dso (= S on the single shard), so the clean ties at a score are the raw ties minus the dirty rows
+        // listed at it; the dirty-slot hash is only probed when every raw node at the row's maximum is dirty.
         const int16_t* row = a.S + (size_t)p * a.ld;
         const uint32_t len = a.own1 - a.own0;
-        int lmax = -1, lfeas = 0;
-        for (uint32_t i = lane; i < len; i += 64) {
-          const int x = row[i];
-          lfeas += x >= 0 ? 1 : 0;
-          if (x > lmax && hash_find(hkey, hval, a.own0 + i) < 0) lmax = x;
+        constexpr int VB = 8;   // blocks in flight per step
+        auto load_blk = [&](uint32_t i0, int16_t (&x)[8]) {
+          if (i0 + 8 <= len) {
+            const uint4 v = *reinterpret_cast<const uint4*>(row + i0);
+            const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+            for (int k = 0; k < 8; ++k) x[k] = (int16_t)(w[k >> 1] >> (16 * (k & 1)));
+          } else {
+#pragma unroll
+            for (int k = 0; k < 8; ++k) x[k] = i0 + k < len ? row[i0 + k] : (int16_t)-1;
+          }
+        };
+        int lmax = -1, lcnt = 0, lfeas = 0;
+        for (uint32_t b0 = 0; b0 < len; b0 += 512u * VB) {
+          int16_t x[VB][8];
+#pragma unroll
+          for (int u = 0; u < VB; ++u) load_blk(b0 + 512u * u + 8u * lane, x[u]);
+#pragma unroll
+          for (int u = 0; u < VB; ++u)
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+              const int xv = x[u][k];
+              lfeas += xv >= 0 ? 1 : 0;
+              lcnt = xv > lmax ? 1 : lcnt + (xv == lmax ? 1 : 0);
+              lmax = xv > lmax ? xv : lmax;
+            }
         }
-        M = max(wave_max(lmax), Md);
         F = wave_sum(lfeas) + Fd;
+        int Mc = wave_max(lmax);
+        int64_t Tc = Mc >= 0 ? (int64_t)wave_sum(lmax == Mc ? lcnt : 0) - __popcll(__ballot(so0 == Mc)) -
+                                   __popcll(__ballot(so1 == Mc))
+                             : 0;
+        if (Mc >= 0 && Tc <= 0) {   // every raw node at the maximum is dirty: the clean maximum, probing the hash
+          lmax = -1;
+          lcnt = 0;
+          for (uint32_t b0 = 0; b0 < len; b0 += 512u * VB) {
+            int16_t x[VB][8];
+#pragma unroll
+            for (int u = 0; u < VB; ++u) load_blk(b0 + 512u * u + 8u * lane, x[u]);
+#pragma unroll
+            for (int u = 0; u < VB; ++u)
+#pragma unroll
+              for (int k = 0; k < 8; ++k) {
+                const int xv = x[u][k];
+                if (xv >= 0 && xv >= lmax && hash_find(hkey, hval, a.own0 + b0 + 512u * u + 8u * lane + k) < 0) {
+                  lcnt = xv > lmax ? 1 : lcnt + 1;
+                  lmax = xv;
+                }
+              }
+          }
+          Mc = wave_max(lmax);
+          Tc = Mc >= 0 ? (int64_t)wave_sum(lmax == Mc ? lcnt : 0) : 0;
+        }
+        M = max(Mc, Md);
         if (M < 0) {
           action = 1;
         } else {
-          const uint32_t chunk = (len + 63) / 64;
-          const uint32_t i0 = min(len, (uint32_t)lane * chunk), i1 = min(len, i0 + chunk);
-          int cnt = 0;
-          for (uint32_t i = i0; i < i1; ++i)
-            if (row[i] == M && hash_find(hkey, hval, a.own0 + i) < 0) ++cnt;
-          for (int s = 0; s < nd; ++s) {
-            const uint32_t n = drows[s].node;
-            if (n >= a.own0 + i0 && n < a.own0 + i1 && dsc[p * B + s] == M) ++cnt;
-          }
-          const int incl = wave_incl_scan(cnt);
-          T = __builtin_amdgcn_readlane(incl, 63);
+          const uint64_t new0 = __ballot(sc0 == M), new1 = __ballot(sc1 == M);   // dirty rows now at M
+          const uint64_t old0 = __ballot(so0 == M), old1 = __ballot(so1 == M);   // dirty rows listed at M in S
+          T = (Mc == M ? Tc : 0) + __popcll(new0) + __popcll(new1);
           const int64_t jp = tiebreak_position(a.seed, sseq[p], T);
-          const int64_t excl = incl - cnt;
+          // the jp-th tie in node order: raw nodes at M, less the dirty rows listed there, plus the dirty rows now at M
+          int64_t run = 0;
           int64_t found = -1;
-          if (jp > excl && jp <= excl + cnt) {   // this lane's chunk holds the jp-th tie
-            int64_t need = jp - excl;
-            for (uint32_t i = i0; i < i1; ++i) {
-              const int sl = hash_find(hkey, hval, a.own0 + i);
-              const bool tie = sl >= 0 ? dsc[p * B + sl] == M : row[i] == M;
-              if (tie && --need == 0) { found = (int64_t)(a.own0 + i); break; }
+          for (uint32_t b0 = 0; b0 < len && found == -1; b0 += 512u * VB) {
+            int16_t x[VB][8];
+#pragma unroll
+            for (int u = 0; u < VB; ++u) load_blk(b0 + 512u * u + 8u * lane, x[u]);
+#pragma unroll
+            for (int u = 0; u < VB; ++u) {
+              const uint32_t i0 = b0 + 512u * u;
+              uint32_t fl = 0;
+#pragma unroll
+              for (int k = 0; k < 8; ++k) fl |= (x[u][k] == M ? 1u : 0u) << k;
+              // the block's ties: raw ties at M, less the dirty rows listed at M, plus the dirty rows now at M
+              const bool in0 = dn0 - a.own0 - i0 < 512u, in1 = dn1 - a.own0 - i0 < 512u;
+              const uint64_t bn0 = new0 & __ballot(in0), bn1 = new1 & __ballot(in1);
+              const uint64_t bo0 = old0 & __ballot(in0), bo1 = old1 & __ballot(in1);
+              const int tot = wave_sum(__popc(fl)) + __popcll(bn0) + __popcll(bn1) - __popcll(bo0) - __popcll(bo1);
+              if (found == -1 && run + tot >= jp) {   // the jp-th tie is in this block: exact per-node flags
+                each_node(bo0, bo1, [&](uint32_t nn) {
+                  const uint32_t o = nn - a.own0 - i0;
+                  if ((uint32_t)lane == (o >> 3)) fl &= ~(1u << (o & 7u));
+                });
+                each_node(bn0, bn1, [&](uint32_t nn) {
+                  const uint32_t o = nn - a.own0 - i0;
+                  if ((uint32_t)lane == (o >> 3)) fl |= 1u << (o & 7u);
+                });
+                const int c = __popc(fl);
+                const int incl = wave_incl_scan(c);
+                int64_t need = jp - (run + incl - c);
+                int64_t f = -1;
+                if (need >= 1 && need <= c) {
+                  uint32_t bits = fl;
+                  while (--need) bits &= bits - 1;
+                  f = (int64_t)(a.own0 + i0 + 8u * lane + (uint32_t)__builtin_ctz(bits));
+                }
+                const uint64_t got = __ballot(f >= 0);
+                found = got ? (int64_t)__builtin_amdgcn_readlane((int)f, __ffsll((long long)got) - 1) : -2;
+              }
+              run += tot;
             }
           }
-          const uint64_t got = __ballot(found >= 0);
-          if (!got) action = 2;
-          else winner = (uint32_t)__builtin_amdgcn_readlane((int)found, __ffsll((long long)got) - 1);
+          if (found < 0) action = 2;
+          else winner = (uint32_t)found;
           slowpath = true;
         }
+        STAMP(26);
       }
       if (slowpath && action == 0 && (int32_t)winner < 0) action = 2;   // unreachable for a valid max
       STAMP(0);
@@ -492,6 +568,8 @@ __global__ void __launch_bounds__(256) commit_pipe_kernel(CommitArgs a) {
         NumaOut no{};
         if (numa_reserve)
           no = numa_eval<true, false, true>(dr.nr, pk, a.pf, SlotsLds{dr, m}, a.pf.enabled & 0x10u, false, s_aff);
+        STAMP(24);
+        if (ST) st_acc[25] += (pk.numa & PN_BIND) ? 1 : 0;
         if (lane == 0) {
           PlacementDev pl{(int32_t)winner, (uint32_t)F, (int64_t)M, (uint32_t)T, slowpath ? 1u : 0u, 0, 0,
                           {0, 0, 0, 0}, {0, 0, 0, 0}};
@@ -561,6 +639,8 @@ __global__ void __launch_bounds__(256) commit_pipe_kernel(CommitArgs a) {
             if ((no.nflags >> NF_POLICY_SHIFT) & 3u) hint_table_fill(s_hto[par], no, zone_avail(no), lane);
           }
         }
+        if (ST) { st_acc[22] += ((rr.nr.nflags >> NF_POLICY_SHIFT) & 3u) ? 1 : 0; st_acc[23] += fresh ? 1 : 0; }
+        STAMP(21);
         if (!last) {   // the whole wave evaluates the pair (current score; batch-start score when evaluated)
           for (int it = 0; it < (eval_so ? 2 : 1); ++it) {   // one call site: one inlined copy of the evaluation
             const Row ru = it ? orow[par] : rr;
@@ -645,7 +725,7 @@ __global__ void __launch_bounds__(256) commit_pipe_kernel(CommitArgs a) {
     if (tid == 0)
       for (int i = 0; i < 7; ++i) atomicAdd(reinterpret_cast<unsigned long long*>(&a.stamps[i]), st_acc[i]);
     if (tid == 0)
-      for (int i = 11; i < 18; ++i) atomicAdd(reinterpret_cast<unsigned long long*>(&a.stamps[i]), st_acc[i]);
+      for (int i = 11; i < 27; ++i) atomicAdd(reinterpret_cast<unsigned long long*>(&a.stamps[i]), st_acc[i]);
     if (tid == 64)
       for (int i = 7; i < 11; ++i) atomicAdd(reinterpret_cast<unsigned long long*>(&a.stamps[i]), st_acc[i]);
   }

@@ -71,6 +71,7 @@ struct gs_ctx {
   uint32_t N = 0, npad = 0;
   hipStream_t st = nullptr;
   hipStream_t st2 = nullptr;                // side stream: eval_kernel beside eval_numa_kernel
+  hipStream_t st_ev = nullptr;              // eval passes: a batch's eval runs beside the previous batch's commit
   uint32_t window_k = 0;                    // node sampling: numFeasibleNodesToFind(N) (0 = every node)
   uint32_t next_start = 0;                  // [upstream] Scheduler.nextStartNodeIndex
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
@@ -107,6 +108,9 @@ struct gs_ctx {
   // double-buffered per-batch buffers (slot 0 = the fields above when bound): the next batch is enqueued
   // speculatively before the current one is read back (gs_schedule)
   struct Slot {
+    int16_t* d_S = nullptr;         // score rows and Filter-time affinities of the slot's batch
+    uint8_t* d_aff = nullptr;
+    hipEvent_t ev_go = nullptr, ev_evdone = nullptr;
     PodVec* d_pods = nullptr;
     uint64_t* d_seq = nullptr;
     PlacementDev* d_out = nullptr;
@@ -707,6 +711,7 @@ double ev_ms(hipEvent_t a, hipEvent_t b) {
 
 void bind_slot(gs_ctx* c, int s) {
   const gs_ctx::Slot& x = c->slot[s];
+  c->d_S = x.d_S; c->d_aff = x.d_aff;
   c->d_pods = x.d_pods; c->d_seq = x.d_seq; c->d_out = x.d_out; c->d_committed = x.d_committed;
   c->h_pods = x.h_pods; c->h_seq = x.h_seq; c->h_out = x.h_out; c->h_committed = x.h_committed;
   for (int i = 0; i < 6; ++i) c->ev[i] = x.ev[i];
@@ -746,20 +751,26 @@ CommitArgs commit_args(gs_ctx* c, int b) {
 }
 
 // Enqueue one device pass over pods [0, b) of the bound slot's staged batch, and its read-back; no host wait.
-// prev != nullptr: a speculative pass behind the batch that wrote `prev` on the same stream — its commit kernel
-// does nothing unless that batch committed every pod and needs no host-side Reserve (prev[1] == 1).
-int launch_batch(gs_ctx* c, int b, const int32_t* prev) {
+// The eval pass runs on st_ev, the rest on st. prev != nullptr: a speculative pass behind the batch that wrote `prev`
+// (its placements prev_out, prev_b pods): its eval pass runs beside that batch's commit, on the mirror as it was
+// before it, and the rows that batch landed on are re-evaluated on st once it committed (patch_kernel); its commit
+// kernel does nothing unless that batch committed every pod and needs no host-side Reserve (prev[1] == 1).
+int launch_batch(gs_ctx* c, int b, const int32_t* prev, const PlacementDev* prev_out = nullptr, int prev_b = 0) {
   uint32_t* d_lists = reinterpret_cast<uint32_t*>(c->d_xchg_send);
   LevelHdr* d_hdrs = reinterpret_cast<LevelHdr*>(c->d_xchg_send + lists_bytes(c->B));
   int prod_cols = 0;
   for (int i = 0; i < b; ++i) prod_cols |= (c->h_pods[i].flags & PF_PROD_SCORE) ? 1 : 0;
   uint32_t len = c->n1 - c->n0;
-  HIP_TRY(c, hipEventRecord(c->ev[0], c->st));
   if (c->numa_on && c->numa_idx_stale) {
     std::vector<uint32_t> idx;
     for (uint32_t n = c->n0; n < c->n1; ++n)
       if (c->numa[n].cfg.numa_topology_policy != GS_NUMA_POLICY_NONE) idx.push_back(n);
-    if (c->d_numa_idx) { HIP_TRY(c, hipStreamSynchronize(c->st)); (void)hipFree(c->d_numa_idx); c->d_numa_idx = nullptr; }
+    if (c->d_numa_idx) {
+      HIP_TRY(c, hipStreamSynchronize(c->st));
+      HIP_TRY(c, hipStreamSynchronize(c->st_ev));
+      (void)hipFree(c->d_numa_idx);
+      c->d_numa_idx = nullptr;
+    }
     c->numa_n = (uint32_t)idx.size();
     if (c->numa_n) {
       HIP_TRY(c, hipMalloc(&c->d_numa_idx, 4 * idx.size()));
@@ -767,9 +778,16 @@ int launch_batch(gs_ctx* c, int b, const int32_t* prev) {
     }
     c->numa_idx_stale = false;
   }
+  const gs_ctx::Slot& sl = c->slot[c->cur_slot];
+  HIP_TRY(c, hipEventRecord(c->ev[0], c->st_ev));
   HIP_TRY(c, launch_eval(c->mv, c->d_pods, b, c->pf, c->n0, c->n1, c->d_S, c->ld, prod_cols, c->d_numa_idx, c->numa_n,
-                         c->d_aff, c->st, c->st2, c->ev_fork, c->ev_join));
-  HIP_TRY(c, hipEventRecord(c->ev[1], c->st));
+                         c->d_aff, c->st_ev, c->st2, c->ev_fork, c->ev_join));
+  HIP_TRY(c, hipEventRecord(c->ev[1], c->st_ev));
+  HIP_TRY(c, hipEventRecord(sl.ev_evdone, c->st_ev));
+  HIP_TRY(c, hipStreamWaitEvent(c->st, sl.ev_evdone, 0));
+  if (prev)
+    HIP_TRY(c, launch_patch(c->mv, c->d_pods, b, c->pf, c->n0, c->n1, c->d_S, c->ld, prod_cols, c->d_aff, prev_out, prev,
+                            prev_b, c->st));
   if (!c->window_k)   // node sampling selects over the rotation window, not the candidate levels
     HIP_TRY(c, launch_cand(c->d_S, c->ld, len, c->n0, b, c->max_score, d_lists, d_hdrs, c->st));
   HIP_TRY(c, hipEventRecord(c->ev[2], c->st));
@@ -1001,6 +1019,7 @@ int gs_create(const gs_config* cfg, gs_ctx** out) {
   if ((e = set_kernel_attributes()) != hipSuccess) return bail("hipFuncSetAttribute", e);
   if ((e = hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking)) != hipSuccess) return bail("hipStreamCreate", e);
   if ((e = hipStreamCreateWithFlags(&c->st2, hipStreamNonBlocking)) != hipSuccess) return bail("hipStreamCreate", e);
+  if ((e = hipStreamCreateWithFlags(&c->st_ev, hipStreamNonBlocking)) != hipSuccess) return bail("hipStreamCreate", e);
   if ((e = hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming)) != hipSuccess) return bail("hipEventCreate", e);
   if ((e = hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming)) != hipSuccess) return bail("hipEventCreate", e);
   for (auto& ev : c->ev)
@@ -1038,11 +1057,19 @@ int gs_create(const gs_config* cfg, gs_ctx** out) {
   if ((e = hipHostMalloc(&c->h_xchg_send, xb, hipHostMallocDefault)) != hipSuccess) return bail("hipHostMalloc", e);
   (void)hipMemset(c->d_S, 0xff, (size_t)c->B * c->ld * 2);
   {
+    for (auto& sl : c->slot) {
+      if ((e = hipEventCreateWithFlags(&sl.ev_go, hipEventDisableTiming)) != hipSuccess) return bail("hipEventCreate", e);
+      if ((e = hipEventCreateWithFlags(&sl.ev_evdone, hipEventDisableTiming)) != hipSuccess) return bail("hipEventCreate", e);
+    }
     gs_ctx::Slot& s0 = c->slot[0];
+    s0.d_S = c->d_S; s0.d_aff = c->d_aff;
     s0.d_pods = c->d_pods; s0.d_seq = c->d_seq; s0.d_out = c->d_out; s0.d_committed = c->d_committed;
     s0.h_pods = c->h_pods; s0.h_seq = c->h_seq; s0.h_out = c->h_out; s0.h_committed = c->h_committed;
     for (int i = 0; i < 6; ++i) s0.ev[i] = c->ev[i];
     gs_ctx::Slot& s1 = c->slot[1];
+    if ((e = hipMalloc(&s1.d_S, (size_t)c->B * c->ld * 2)) != hipSuccess) return bail("hipMalloc S", e);
+    if ((e = hipMalloc(&s1.d_aff, (size_t)c->B * c->ld)) != hipSuccess) return bail("hipMalloc aff", e);
+    (void)hipMemset(s1.d_S, 0xff, (size_t)c->B * c->ld * 2);
     if ((e = hipMalloc(&s1.d_pods, sizeof(PodVec) * c->B)) != hipSuccess) return bail("hipMalloc", e);
     if ((e = hipMalloc(&s1.d_seq, 8 * c->B)) != hipSuccess) return bail("hipMalloc", e);
     if ((e = hipMalloc(&s1.d_out, sizeof(PlacementDev) * c->B)) != hipSuccess) return bail("hipMalloc", e);
@@ -1075,20 +1102,30 @@ int gs_destroy(gs_ctx* c) {
       fprintf(stderr, "gpuscore commit phases (s_memtime ticks, %% of %llu):", (unsigned long long)tot);
       for (int i = 0; i < 12; ++i) fprintf(stderr, " p%d=%.1f%%", i, tot ? 100.0 * st[i] / tot : 0.0);
       fprintf(stderr, "\n  raw ticks per committed pod (%llu pods):", (unsigned long long)c->stats_all_pods);
-      for (int i = 0; i < 18; ++i)
+      for (int i = 0; i < 22; ++i)
         fprintf(stderr, " s%d=%.0f", i, c->stats_all_pods ? (double)st[i] / (double)c->stats_all_pods : 0.0);
+      fprintf(stderr, "\n  pods through full-row resolution %llu, FitError %llu, slow path %llu",
+              (unsigned long long)st[18], (unsigned long long)st[19], (unsigned long long)st[20]);
+      fprintf(stderr, ", winners on NUMA-policy rows %llu, fresh winners %llu, cpuset pods %llu | s24 (Reserve pair "
+              "evaluation) %.0f", (unsigned long long)st[22], (unsigned long long)st[23], (unsigned long long)st[25],
+              c->stats_all_pods ? (double)st[24] / (double)c->stats_all_pods : 0.0);
+      fprintf(stderr, " | s26 (full-row resolution, per such pod) %.0f", st[18] ? (double)st[26] / (double)st[18] : 0.0);
       fprintf(stderr, " | policy-row rescoring: %llu pods, %.0f ticks per pair (thread 128)\n",
               (unsigned long long)st[12], st[12] ? (double)st[13] / st[12] : 0.0);
-      fprintf(stderr, "  header staging (inside p0): %.1f%%\n", tot ? 100.0 * st[24] / tot : 0.0);
     }
     (void)hipFree(c->d_stamps);
   }
   if (c->comm) ncclCommDestroy(c->comm);
   if (c->st) (void)hipStreamSynchronize(c->st);
+  if (c->st_ev) (void)hipStreamSynchronize(c->st_ev);
   if (c->slot[0].d_pods) bind_slot(c, 0);
   {
     gs_ctx::Slot& s1 = c->slot[1];
-    void* d1[] = {s1.d_pods, s1.d_seq, s1.d_out, s1.d_committed};
+    for (auto& sl : c->slot) {
+      if (sl.ev_go) (void)hipEventDestroy(sl.ev_go);
+      if (sl.ev_evdone) (void)hipEventDestroy(sl.ev_evdone);
+    }
+    void* d1[] = {s1.d_pods, s1.d_seq, s1.d_out, s1.d_committed, s1.d_S, s1.d_aff};
     for (void* p : d1)
       if (p) (void)hipFree(p);
     void* h1[] = {s1.h_pods, s1.h_seq, s1.h_out, s1.h_committed};
@@ -1108,6 +1145,7 @@ int gs_destroy(gs_ctx* c) {
     if (p) (void)hipHostFree(p);
   for (auto& ev : c->ev)
     if (ev) (void)hipEventDestroy(ev);
+  if (c->st_ev) (void)hipStreamDestroy(c->st_ev);
   if (c->st2) (void)hipStreamSynchronize(c->st2);
   if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
   if (c->ev_join) (void)hipEventDestroy(c->ev_join);
@@ -1235,13 +1273,20 @@ int batch_len(const gs_ctx* c, const gs_pod* pods, uint32_t i, uint32_t npods, b
 }
 
 // PreFilter of pods [i, i+b) into the bound slot, and their upload
-int stage_batch(gs_ctx* c, const gs_pod* pods, const uint64_t* seq, uint32_t i, int b) {
+// (uploads on st_ev, where the batch's eval pass runs; a non-speculative batch's eval first waits for everything
+// enqueued on st — row deltas, node prep, the previous commit — a speculative one only for the eval pass before it)
+int stage_batch(gs_ctx* c, const gs_pod* pods, const uint64_t* seq, uint32_t i, int b, bool speculative) {
   for (int j = 0; j < b; ++j) {
     c->h_pods[j] = prep_pod(c, pods[i + j]);
     c->h_seq[j] = seq ? seq[i + j] : (uint64_t)(i + j);
   }
-  HIP_TRY(c, hipMemcpyAsync(c->d_pods, c->h_pods, sizeof(PodVec) * b, hipMemcpyHostToDevice, c->st));
-  HIP_TRY(c, hipMemcpyAsync(c->d_seq, c->h_seq, 8 * b, hipMemcpyHostToDevice, c->st));
+  if (!speculative) {
+    const gs_ctx::Slot& sl = c->slot[c->cur_slot];
+    HIP_TRY(c, hipEventRecord(sl.ev_go, c->st));
+    HIP_TRY(c, hipStreamWaitEvent(c->st_ev, sl.ev_go, 0));
+  }
+  HIP_TRY(c, hipMemcpyAsync(c->d_pods, c->h_pods, sizeof(PodVec) * b, hipMemcpyHostToDevice, c->st_ev));
+  HIP_TRY(c, hipMemcpyAsync(c->d_seq, c->h_seq, 8 * b, hipMemcpyHostToDevice, c->st_ev));
   return GS_OK;
 }
 
@@ -1271,14 +1316,14 @@ int gs_schedule(gs_ctx* c, const gs_pod* pods, uint32_t npods, const uint64_t* s
   uint32_t i = 0;
   bool inflight = false, cur_special = false, spec_ok = true;
   int cur_b = 0;
-  auto drain = [&]() { (void)hipStreamSynchronize(c->st); };
+  auto drain = [&]() { (void)hipStreamSynchronize(c->st); (void)hipStreamSynchronize(c->st_ev); };
   while (i < npods) {
     if (!inflight) {
       if ((rc = flush_rows(c))) return rc;
       if (c->prep_stale && (rc = node_prep(c))) return rc;
       cur_b = batch_len(c, pods, i, npods, &cur_special);
       // (a cpuset pod whose node is outside the device cpuset scope ends the batch inside the commit kernel)
-      if ((rc = stage_batch(c, pods, seq, i, cur_b))) return rc;
+      if ((rc = stage_batch(c, pods, seq, i, cur_b, false))) return rc;
       if ((rc = launch_batch(c, cur_b, nullptr))) return rc;
     }
     bool spec = false;
@@ -1289,10 +1334,11 @@ int gs_schedule(gs_ctx* c, const gs_pod* pods, uint32_t npods, const uint64_t* s
       nb = batch_len(c, pods, j, npods, &sf);
       if (!sf && !uid_overlap(pods + i, cur_b, pods + j, nb)) {
         const int32_t* prev = c->d_committed;
+        const PlacementDev* prev_out = c->d_out;
         const int here = c->cur_slot;
         bind_slot(c, 1 - here);
-        rc = stage_batch(c, pods, seq, j, nb);
-        if (!rc) rc = launch_batch(c, nb, prev);
+        rc = stage_batch(c, pods, seq, j, nb, true);
+        if (!rc) rc = launch_batch(c, nb, prev, prev_out, cur_b);
         bind_slot(c, here);
         if (rc) { drain(); return rc; }
         spec = true;
@@ -1301,8 +1347,9 @@ int gs_schedule(gs_ctx* c, const gs_pod* pods, uint32_t npods, const uint64_t* s
     spec_ok = true;
     int committed = 0;
     rc = finish_batch(c, cur_b, spec, &committed);
-    if (rc == GS_REDO) {   // pod 0 needs the full-row path, the speculative pass (void) overwrote its rows: re-run
+    if (rc == GS_REDO) {   // pod 0 needs the full-row path, the speculative pass (void) overwrote its lists: re-run
       drain();
+      if ((rc = stage_batch(c, pods, seq, i, cur_b, false))) return rc;
       if ((rc = launch_batch(c, cur_b, nullptr))) return rc;
       inflight = true;
       spec_ok = false;
@@ -1504,6 +1551,7 @@ int gs_reset_stats(gs_ctx* c) {
 
 int gs_synchronize(gs_ctx* c) {
   if (!c) return GS_EINVAL;
+  HIP_TRY(c, hipStreamSynchronize(c->st_ev));
   HIP_TRY(c, hipStreamSynchronize(c->st));
   return GS_OK;
 }

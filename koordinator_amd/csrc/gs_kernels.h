@@ -102,6 +102,11 @@ hipError_t launch_eval(const MirrorView& m, const PodVec* pods, int npods, const
                        int16_t* S, uint32_t ld, int prod_cols, const uint32_t* numa_idx, uint32_t numa_n,
                        uint8_t* aff, hipStream_t st, hipStream_t st2 = nullptr, hipEvent_t fork = nullptr,
                        hipEvent_t join = nullptr);
+// the previous batch's winner rows of this shard re-evaluated for every pod of this batch (its eval pass ran beside
+// the previous batch's commit)
+hipError_t launch_patch(const MirrorView& m, const PodVec* pods, int npods, const Profile& pf, uint32_t n0, uint32_t n1,
+                        int16_t* S, uint32_t ld, int prod_cols, uint8_t* aff, const PlacementDev* prev_out,
+                        const int32_t* prev_committed, int prev_npods, hipStream_t st);
 hipError_t launch_eval_full(const MirrorView& m, const PodVec* pods, int npods, const Profile& pf, uint32_t N,
                             int16_t* scores, uint16_t* codes, int16_t* plugin, int prod_cols, hipStream_t st);
 hipError_t launch_cand(const int16_t* S, uint32_t ld, uint32_t len, uint32_t n0, int npods, int max_score,

@@ -88,6 +88,30 @@ __global__ void __launch_bounds__(256) eval_numa_kernel(MirrorView m, const PodV
   }
 }
 
+// Patch of a batch's score rows evaluated concurrently with the previous batch's commit (which writes the rows
+// its pods landed on back to HBM at its end): the previous batch's winner rows of this shard are evaluated again,
+// on their committed state, for every pod of this batch (same pair evaluation as eval_kernel / eval_numa_kernel).
+// Block k: the row pod k of the previous batch landed on.
+__global__ void __launch_bounds__(128) patch_kernel(MirrorView m, const PodVec* __restrict__ pods, int npods, Profile pf,
+                                                     uint32_t n0, uint32_t n1, int16_t* __restrict__ S, uint32_t ld,
+                                                     int prod_cols, uint8_t* __restrict__ aff,
+                                                     const PlacementDev* __restrict__ prev_out,
+                                                     const int32_t* __restrict__ prev_committed) {
+  const int k = blockIdx.x;
+  if (k >= prev_committed[0]) return;   // pods the previous batch placed (a voided pass: -1)
+  const int32_t node = prev_out[k].node;
+  if (node < 0 || (uint32_t)node < n0 || (uint32_t)node >= n1) return;
+  const bool numa = (pf.enabled & 0x30u) != 0;
+  for (int q = threadIdx.x; q < npods; q += 128) {
+    Row r;
+    load_row(m, (uint32_t)node, prod_cols, numa, r);
+    const PairOut o = eval_pair<false, false, true>(r, pods[q], pf, m);
+    S[(size_t)q * ld + ((uint32_t)node - n0)] = (int16_t)total_score(o, pf);
+    if (numa && ((r.nr.nflags >> NF_POLICY_SHIFT) & 3u))
+      aff[(size_t)q * ld + ((uint32_t)node - n0)] = (uint8_t)(o.code ? 0u : o.aff);
+  }
+}
+
 // Diagnostic variant (gs_evaluate): every plugin's verdict and score for every pair.
 __global__ void __launch_bounds__(256) eval_full_kernel(MirrorView m, const PodVec* __restrict__ pods, int npods,
                                                         Profile pf, uint32_t N, int16_t* scores, uint16_t* codes,
@@ -1101,6 +1125,15 @@ hipError_t launch_eval(const MirrorView& m, const PodVec* pods, int npods, const
   } else {
     hipLaunchKernelGGL(eval_kernel<false>, dim3(gx, gy), dim3(256), 0, st, m, pods, npods, pf, n0, n1, S, ld, prod_cols);
   }
+  return hipGetLastError();
+}
+
+hipError_t launch_patch(const MirrorView& m, const PodVec* pods, int npods, const Profile& pf, uint32_t n0, uint32_t n1,
+                        int16_t* S, uint32_t ld, int prod_cols, uint8_t* aff, const PlacementDev* prev_out,
+                        const int32_t* prev_committed, int prev_npods, hipStream_t st) {
+  if (prev_npods <= 0 || npods <= 0) return hipSuccess;
+  hipLaunchKernelGGL(patch_kernel, dim3(prev_npods), dim3(128), 0, st, m, pods, npods, pf, n0, n1, S, ld, prod_cols, aff,
+                     prev_out, prev_committed);
   return hipGetLastError();
 }
 

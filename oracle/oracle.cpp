@@ -14,6 +14,7 @@
 #include <memory>
 #include <algorithm>
 #include <mutex>
+#include <chrono>
 #include <thread>
 #include <vector>
 
@@ -117,6 +118,7 @@ struct or_cluster {
   std::vector<orn::NodeNUMA> numa;
   bool reverse_hint_order = false;
   uint32_t next_start = 0;   // [upstream] Scheduler.nextStartNodeIndex
+  double phase_s[4] = {0, 0, 0, 0};   // or_phase_times
 };
 
 namespace {
@@ -898,7 +900,15 @@ int or_schedule_replay(or_cluster* c, const gs_pod* pods, uint32_t npods, const 
   feasible_list.reserve(N);
   std::unique_ptr<Pool> pool;
   if (nthreads > 1) pool.reset(new Pool(nthreads));
+  using clk = std::chrono::steady_clock;
+  auto lap = [](clk::time_point& t0) {   // seconds since t0, t0 advanced
+    const clk::time_point t = clk::now();
+    const double d = std::chrono::duration<double>(t - t0).count();
+    t0 = t;
+    return d;
+  };
   for (uint32_t p = 0; p < npods; ++p) {
+    clk::time_point tp = clk::now();
     const gs_pod& pod = pods[p];
     const orn::PreState st = orn::prefilter(c->numa_args, pod);
     gs_placement& o = out[p];
@@ -938,6 +948,7 @@ int or_schedule_replay(or_cluster* c, const gs_pod* pods, uint32_t npods, const 
       else for (int n = 0; n < N; ++n) check(n);
       for (int n = 0; n < N; ++n)
         if (feasible[n]) feasible_list.push_back(n);
+      c->phase_s[0] += lap(tp);
     } else {
       // findNodesThatPassFilters with node sampling, parallelism-1 order: nodes are checked in rotation order
       // from nextStartNodeIndex; the (K+1)-th feasible node cancels the search uncounted (feasibleNodesLen is
@@ -972,6 +983,7 @@ int or_schedule_replay(or_cluster* c, const gs_pod* pods, uint32_t npods, const 
     int F = (int)feasible_list.size();
     if (pool) pool->until(F, score_one);
     else for (int i = 0; i < F; ++i) score_one(i);
+    c->phase_s[1] += lap(tp);
     // selectHost ([upstream] schedule_one.go)
     TieBreakRand rnd(c->cfg.seed, seq ? seq[p] : p);
     selected = feasible_list[0];
@@ -987,6 +999,7 @@ int or_schedule_replay(or_cluster* c, const gs_pod* pods, uint32_t npods, const 
       }
     }
     o.node = selected; o.score = max_score; o.ties = (uint32_t)cnt;
+    c->phase_s[2] += lap(tp);
     }
     // Reserve: NodeNUMAResource (plugin.go:375-422) on the pre-assume NodeInfo
     if (c->cfg.enabled & (GS_ENABLE_NUMA_FILTER | GS_ENABLE_NUMA_SCORE)) {
@@ -1012,7 +1025,16 @@ int or_schedule_replay(or_cluster* c, const gs_pod* pods, uint32_t npods, const 
     // Reserve: LoadAware podAssignCache.assign(node, pod) with timestamp = now (load_aware.go:260-263)
     if (!(pod.flags & GS_POD_TERMINATED))
       c->nodes[selected].assigned[pod.uid] = AssignInfo{c->now, pod};
+    c->phase_s[3] += lap(tp);
   }
+  return GS_OK;
+}
+
+// seconds spent per scheduleOne phase since the last call: Filter (findNodesThatPassFilters), Score
+// (prioritizeNodes), selectHost, Reserve + assume (cpu_baseline breakdown)
+int or_phase_times(or_cluster* c, double out[4]) {
+  if (!c || !out) return GS_EINVAL;
+  for (int i = 0; i < 4; ++i) { out[i] = c->phase_s[i]; c->phase_s[i] = 0; }
   return GS_OK;
 }
 

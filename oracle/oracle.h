@@ -65,6 +65,8 @@ int or_set_hint_order(or_cluster* c, int reverse);
 int or_take_cpus_test(int sockets, int nodes_per_socket, int cores_per_node, int cpus_per_core, int max_ref,
                       const uint64_t* available, const int32_t* alloc_ref, const int32_t* alloc_excl, int needed,
                       int bind, int excl, int strategy, uint64_t* result);
+/* seconds per scheduleOne phase since the last call: Filter, Score, selectHost, Reserve + assume (then reset) */
+int or_phase_times(or_cluster* c, double out[4]);
 /* the selectHost tie-break stream: Intn(cnt) of pod stream `seq` (see oracle.cpp TieBreakRand) */
 int32_t or_tiebreak_intn(uint64_t seed, uint64_t seq, int64_t cnt);
 

@@ -46,6 +46,7 @@ def _load() -> C.CDLL:
         "or_next_start_node_index": (C.c_uint32, [P]),
         "or_schedule_replay": (C.c_int, [P, P, C.c_uint32, P, P, P, C.c_int]),
         "or_tiebreak_intn": (C.c_int32, [C.c_uint64, C.c_uint64, C.c_int64]),
+        "or_phase_times": (C.c_int, [P, P]),
         "or_topology_register": (C.c_int, [P, P, P]),
         "or_nodes_numa_upsert": (C.c_int, [P, P, P, C.c_uint32]),
         "or_numa_allocations_update": (C.c_int, [P, P, P, C.c_uint32]),
@@ -201,6 +202,12 @@ class Oracle:
         _chk(lib().or_schedule(self._h, abi.ptr(pods), len(pods), abi.ptr(seq), abi.ptr(out), int(nthreads)),
              "schedule")
         return out
+
+    def phase_times(self) -> dict:
+        """Seconds per scheduleOne phase since the last call (then reset): filter, score, select, reserve."""
+        out = np.zeros(4, np.float64)
+        _chk(lib().or_phase_times(self._h, abi.ptr(out)), "phase_times")
+        return dict(zip(("filter", "score", "select", "reserve"), out.tolist()))
 
     @property
     def next_start_node_index(self) -> int:
