@@ -546,6 +546,14 @@ int gs_debug_mirror_check(gs_ctx* ctx);
 /* Diagnostics: on != 0 makes gs_schedule re-run the host takeCPUs (cpu_accumulator.go:87-232) for every cpuset
  * the commit kernel selected and fail with GS_ESTATE on any difference. */
 int gs_debug_verify_cpuset(gs_ctx* ctx, int on);
+/* Diagnostics: s_memtime cycles of the commit kernel's per-pair evaluation on mirror rows. Probe i evaluates
+ * node nodes[i]: mode 0 with pod pod_of[i] on a whole wave (the selector's re-score), mode 2 likewise with the
+ * lane-parallel evaluation, mode 1 with pods 0..npods-1 (npods <= 64) one per lane over the row's hint table (the
+ * re-scoring waves). scores: n (modes 0, 2) or n*64 (mode 1) total scores (-1 infeasible); cycles: 2n, the
+ * warm-instruction-cache evaluation of probe i at [i], the cold first one at [n + i]; mode 2 also leaves the
+ * s_memtime stamps of its 8 phases at [2n + 8i ..] (cycles: 10n entries). */
+int gs_debug_pair_probe(gs_ctx* ctx, const gs_pod* pods, uint32_t npods, const uint32_t* nodes, const int32_t* pod_of,
+                        uint32_t n, int mode, int32_t* scores, uint64_t* cycles);
 /* sizeof() of the ABI structs as compiled into the library, in this order: gs_pod, gs_node,
  * gs_node_metric, gs_pod_metric, gs_config, gs_placement, gs_stats, gs_loadaware_args, gs_cpu_topology,
  * gs_node_numa, gs_pod_allocation, gs_numa_args, gs_quota_group, gs_quota_status. */

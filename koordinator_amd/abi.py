@@ -244,6 +244,7 @@ SIGNATURES = {
     "gs_synchronize": (C.c_int, [P]),
     "gs_debug_mirror_check": (C.c_int, [P]),
     "gs_debug_verify_cpuset": (C.c_int, [P, C.c_int]),
+    "gs_debug_pair_probe": (C.c_int, [P, P, C.c_uint32, P, P, C.c_uint32, C.c_int, P, P]),
     "gs_abi_sizes": (None, [C.POINTER(u64), u32]),
     "gs_topology_register": (C.c_int, [P, C.POINTER(GsCpuTopology), C.POINTER(i32)]),
     "gs_nodes_numa_upsert": (C.c_int, [P, P, P, u32]),

@@ -92,7 +92,7 @@ __global__ void __launch_bounds__(256) commit_pipe_kernel(CommitArgs a) {
   // speculative pass queued behind another batch: only if that one committed every pod with nothing left for
   // the host (committed[1] == 1); otherwise a no-op (committed = -1) the host discards
   if (a.prev && a.prev[1] != 1) {
-    if (tid == 0) { a.committed[0] = -1; a.committed[1] = 0; }
+    if (tid == 0) { a.committed[0] = -1; a.committed[1] = 0; a.committed[3] = 0; }
     return;
   }
 
@@ -720,6 +720,7 @@ __global__ void __launch_bounds__(256) commit_pipe_kernel(CommitArgs a) {
     a.committed[0] = s_committed;
     a.committed[1] = (s_committed == B && !s_hostcut) ? 1 : 0;
     a.committed[2] = 0;
+    a.committed[3] = 0;
   }
   if (ST) {   // per-phase cycle sums of wave 0 (lane 0) and wave 1 (lane 0)
     if (tid == 0)

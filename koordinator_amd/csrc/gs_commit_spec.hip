@@ -1,0 +1,885 @@
+// gs_commit_spec.hip — the sequential commit of a batch as a speculative pipeline on one CU (gfx950, one shard).
+//
+// Same contract and results as commit_pipe_kernel (gs_commit.hip): the batch's pods in queue order, each one
+// selectHost over its batch-start score levels and the rows earlier pods of the batch landed on ("dirty" rows,
+// re-scored exactly), then assume + Reserve ([upstream] scheduleOne: selectHost, assume; LoadAware /
+// NodeNUMAResource Reserve).
+//
+// Why speculative. One wave issues about one instruction per 4-8 cycles, and the exact chain per pod — selection,
+// Reserve of the winner, the winner row's new score for the next pod — is several thousand instructions long. The
+// new score is only needed to know whether the row the previous pod landed on competes again; it rarely does (the
+// row just lost capacity). So the selection of pod q runs as soon as pod q-1 is decided, with the rows whose new
+// scores are not yet known ("pending") left out, and is verified once they are: pod q stands iff every pending
+// row's exact score for q is below q's maximum M_q (then its Feasible count gains the pending rows that are
+// feasible). Otherwise the pipeline rolls back to q (undo log of the Reserves after it) and decides q again with
+// every score exact. Verified decisions are exactly those of the sequential loop.
+//
+// Roles (8 waves):
+//   wave 0       decide (selectHost over levels + ready dirty rows, pending rows excluded) and verify, in order;
+//                rollback. Highest issue priority.
+//   wave 1       Reserve of decided pods in order: fetch a fresh winner row into its slot, log the slot's state,
+//                apply assume + Reserve (NUMA split, cpuset), build the row's hint table, queue its re-scoring.
+//   waves 2..7   re-scoring jobs: a reserved row's new score for 64 later pods, one pod per lane.
+// All hand-offs are LDS words (release / acquire); every wait is bounded (an expired wait ends the batch at the
+// verified prefix with GS_COMMIT_TIMEOUT in committed[3], so a bug cannot hang the GPU).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "gs_eval_dev.h"
+
+namespace gs {
+
+constexpr int SP_WAVES = 8, SP_THREADS = 64 * SP_WAVES;
+constexpr int SP_LAG = 8;        // decided - verified <= SP_LAG (undo log depth)
+constexpr int SP_TABLES = 4;     // hint tables of reserved rows in flight
+constexpr int SP_JOBQ = 32;      // re-scoring job ring
+constexpr int SP_HASH = 256;     // node -> slot (full-row resolution)
+constexpr int SP_FRESH = 1, SP_FITERR = 2, SP_SLOW = 4;   // DecRec.flags
+constexpr uint32_t SP_SPIN_LIMIT = 1u << 24;
+
+struct DecRec {          // one decided pod
+  int32_t winner;        // node (-1: FitError)
+  int32_t slot;          // dirty slot it lands on
+  int32_t M, T, F;       // max score, ties, feasible count with the pending rows left out
+  int32_t nd_before;     // dirty slots before this decision
+  int32_t prev_pend;     // the slot's previous version (a landing on an existing slot)
+  uint32_t flags;
+  uint64_t pend0, pend1; // pending slots at decision time
+};
+struct UndoRec {         // a slot's state before a Reserve
+  Row row;
+  CpuStateDev cs;
+  int32_t slot, pad;
+};
+struct Job {
+  int32_t slot, q, range, tbl;
+};
+
+__device__ __forceinline__ void sp_sleep() { __builtin_amdgcn_s_sleep(2); }
+
+size_t spec_smem_bytes(int B) {
+  size_t b = (size_t)B * POD_STRIDE;                  // pods
+  b += (size_t)B * sizeof(Row);                       // dirty rows
+  b += (size_t)B * B * 2 * 2;                         // dsc, dso
+  b = (b + 15) & ~(size_t)15;
+  b += (size_t)B * sizeof(CpuStateDev);               // cpu state of the dirty rows
+  b += (size_t)B * sizeof(DecRec);
+  b += (size_t)SP_LAG * sizeof(UndoRec);
+  b += (size_t)SP_TABLES * sizeof(HintTable);
+  b += (size_t)B * 4 * 5;                              // final_F, done_ver, has_row, rescored, jobs_left
+  b += (size_t)SP_HASH * 8;
+  b += (size_t)SP_JOBQ * sizeof(Job);
+  return b + 64;
+}
+
+__global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
+  extern __shared__ __align__(16) unsigned char cm[];
+  const int B = a.npods;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const MirrorView& m = a.m;
+  const bool numa_on = (a.pf.enabled & 0x30u) != 0;
+  const uint64_t lt_mask = (1ull << lane) - 1ull;
+  // ---- LDS carve-up
+  unsigned char* cur = cm;
+  auto take = [&](size_t bytes) { unsigned char* p = cur; cur += (bytes + 15) & ~(size_t)15; return p; };
+  unsigned char* pods_b = take((size_t)B * POD_STRIDE);
+  auto pods = [&](int i) -> PodVec& { return *reinterpret_cast<PodVec*>(pods_b + (size_t)i * POD_STRIDE); };
+  Row* drows = reinterpret_cast<Row*>(take((size_t)B * sizeof(Row)));
+  int16_t* dsc = reinterpret_cast<int16_t*>(take((size_t)B * B * 2));   // [pod][slot] current score
+  int16_t* dso = reinterpret_cast<int16_t*>(take((size_t)B * B * 2));   // [pod][slot] batch-start score
+  CpuStateDev* cst = reinterpret_cast<CpuStateDev*>(take((size_t)B * sizeof(CpuStateDev)));
+  DecRec* dec = reinterpret_cast<DecRec*>(take((size_t)B * sizeof(DecRec)));
+  UndoRec* undo = reinterpret_cast<UndoRec*>(take((size_t)SP_LAG * sizeof(UndoRec)));
+  HintTable* tables = reinterpret_cast<HintTable*>(take((size_t)SP_TABLES * sizeof(HintTable)));
+  int32_t* final_F = reinterpret_cast<int32_t*>(take((size_t)B * 4));
+  int32_t* done_ver = reinterpret_cast<int32_t*>(take((size_t)B * 4));   // slot: version whose re-scoring is complete
+  int32_t* has_row = reinterpret_cast<int32_t*>(take((size_t)B * 4));    // slot: row fetched into LDS
+  int32_t* rescored = reinterpret_cast<int32_t*>(take((size_t)B * 4));   // pod: Reserve + re-scoring complete
+  int32_t* jobs_left = reinterpret_cast<int32_t*>(take((size_t)B * 4));
+  int32_t* hkey = reinterpret_cast<int32_t*>(take((size_t)SP_HASH * 4));
+  int32_t* hval = reinterpret_cast<int32_t*>(take((size_t)SP_HASH * 4));
+  Job* jobq = reinterpret_cast<Job*>(take((size_t)SP_JOBQ * sizeof(Job)));
+  __shared__ TopoDev s_topo;        // wave 1: topology of the last cpuset Reserve
+  __shared__ HintTable s_ht0;       // wave 0: rollback re-scoring
+  __shared__ uint64_t s_cpuset[4];
+  __shared__ int32_t s_aff;
+  __shared__ int32_t s_decided, s_reserved, s_stop, s_parked, s_finish, s_cut_at, s_err;
+  __shared__ int32_t s_jq_head, s_jq_tail;
+  __shared__ int32_t s_committed, s_hostcut, s_nd, s_endwhy;
+  __shared__ uint64_t sseq[MAX_BATCH];
+
+  if (a.prev && a.prev[1] != 1) {   // speculative pass behind a batch that left work for the host: no-op
+    if (tid == 0) { a.committed[0] = -1; a.committed[1] = 0; a.committed[3] = 0; }
+    return;
+  }
+  for (int i = tid; i < B; i += SP_THREADS) {
+    pods(i) = a.pods[i];
+    sseq[i] = a.seq[i];
+    done_ver[i] = -1;
+    has_row[i] = 0;
+    rescored[i] = 0;
+    jobs_left[i] = 0;
+  }
+  for (int i = tid; i < SP_HASH; i += SP_THREADS) { hkey[i] = -1; hval[i] = -1; }
+  if (tid == 0) {
+    s_decided = 0; s_reserved = 0; s_stop = 0; s_parked = 0; s_finish = 0; s_cut_at = -1; s_err = 0;
+    s_jq_head = 0; s_jq_tail = 0; s_committed = 0; s_hostcut = 0; s_nd = 0;
+  }
+  __syncthreads();
+
+  auto ld_acq = [](const int32_t* p) { return __atomic_load_n(p, __ATOMIC_ACQUIRE); };
+  auto st_rel = [](int32_t* p, int32_t v) { __atomic_store_n(p, v, __ATOMIC_RELEASE); };
+
+  if (wv == 0) {
+    // =============================================== decide + verify ===============================================
+    __builtin_amdgcn_s_setprio(3);
+    uint32_t dn0 = 0xffffffffu, dn1 = 0xffffffffu;   // slot s's node in lane s % 64 of dn0 / dn1
+    int32_t pv0 = -1, pv1 = -1;                      // slot s's latest decided version (pod index)
+    int nd = 0, q = 0, v = 0, wm = 0, end_at = B, end_why = 0;
+    int committed = 0;
+    bool host_cut = false, err = false;
+    auto each_node = [&](uint64_t m0, uint64_t m1, auto&& fn) {
+      for (uint64_t b = m0; b; b &= b - 1) fn((uint32_t)__builtin_amdgcn_readlane((int)dn0, __builtin_ctzll(b)));
+      for (uint64_t b = m1; b; b &= b - 1) fn((uint32_t)__builtin_amdgcn_readlane((int)dn1, __builtin_ctzll(b)));
+    };
+    auto hash_insert = [&](uint32_t node, int slot) {
+      uint32_t h = (node * 2654435761u) & (SP_HASH - 1);
+      while (hkey[h] >= 0) h = (h + 1) & (SP_HASH - 1);
+      hkey[h] = (int32_t)node;
+      hval[h] = slot;
+    };
+    auto sp_hash_find = [&](uint32_t node) -> int {
+      uint32_t h = (node * 2654435761u) & (SP_HASH - 1);
+      for (int probe = 0; probe < SP_HASH; ++probe) {
+        const int kk = hkey[h];
+        if (kk == (int)node) return hval[h];
+        if (kk < 0) return -1;
+        h = (h + 1) & (SP_HASH - 1);
+      }
+      return -1;
+    };
+    // header of pod p (lanes 0..7: level j score / count) and the head of its level list (lane i: entry i)
+    auto load_hdr = [&](int p, int& hs, int& hc, int& nlev, int& feas, int& next, uint32_t& lh) {
+      const LevelHdr* h = hdr_ptr(a, 0, p);
+      nlev = h->nlev;
+      feas = h->feasible;
+      next = h->next;
+      hs = lane < MAXLEV ? h->score[lane] : -1;
+      hc = lane < MAXLEV ? h->count[lane] : 0;
+      lh = lane < 32 ? list_ptr(a, 0, p)[lane] : 0xffffffffu;
+    };
+    int n_hs = -1, n_hc = 0, n_nlev = 0, n_feas = 0, n_next = -1;
+    uint32_t n_lh = 0xffffffffu;
+    load_hdr(0, n_hs, n_hc, n_nlev, n_feas, n_next, n_lh);
+    uint32_t spins = 0;
+    while (!err) {
+      // ------------------------------------------------ verification, in order
+      while (wm < q && ld_acq(&rescored[wm])) ++wm;
+      bool rolled = false;
+      while (v < q && v <= wm) {
+        const DecRec d = dec[v];
+        int mis = 0, fadd = 0;
+        if ((d.pend0 >> lane) & 1ull) {
+          const int sc = dsc[v * B + lane];
+          mis |= sc >= 0 && sc >= d.M;
+          fadd += sc >= 0;
+        }
+        if ((d.pend1 >> lane) & 1ull) {
+          const int sc = dsc[v * B + 64 + lane];
+          mis |= sc >= 0 && sc >= d.M;
+          fadd += sc >= 0;
+        }
+        if (__ballot(mis)) {
+          // ---------------- rollback to v: park the other waves, undo the Reserves of pods >= v, restore versions
+          st_rel(&s_stop, 1);
+          spins = 0;
+          while (ld_acq(&s_parked) < SP_WAVES - 1) {
+            if (++spins > SP_SPIN_LIMIT) { err = true; break; }
+            sp_sleep();
+          }
+          if (err) break;
+          const int r = ld_acq(&s_reserved);
+          for (int qq = r - 1; qq >= v; --qq) {
+            if (dec[qq].flags & SP_FITERR) continue;
+            const UndoRec& u = undo[qq % SP_LAG];
+            const int sl = u.slot;
+            const uint64_t* src = reinterpret_cast<const uint64_t*>(&u.row);
+            uint64_t* dst = reinterpret_cast<uint64_t*>(&drows[sl]);
+            for (int i = lane; i < (int)(sizeof(Row) / 8); i += 64) dst[i] = src[i];
+            const uint64_t* s2 = reinterpret_cast<const uint64_t*>(&u.cs);
+            uint64_t* d2 = reinterpret_cast<uint64_t*>(&cst[sl]);
+            for (int i = lane; i < (int)(sizeof(CpuStateDev) / 8); i += 64) d2[i] = s2[i];
+            WAVE_FENCE();
+          }
+          // versions of the slots that survive, newest undone landing first
+          uint64_t redo0 = 0, redo1 = 0;   // surviving slots whose row was restored: re-score them for pods >= v
+          for (int qq = q - 1; qq >= v; --qq) {
+            const DecRec& e = dec[qq];
+            if ((e.flags & (SP_FITERR | SP_FRESH)) || e.slot >= dec[v].nd_before) continue;
+            const int sl = e.slot;
+            if (lane == (sl & 63)) { if (sl < 64) pv0 = e.prev_pend; else pv1 = e.prev_pend; }
+            if (qq < r) { if (sl < 64) redo0 |= 1ull << sl; else redo1 |= 1ull << (sl - 64); }
+          }
+          const int ndv = dec[v].nd_before;
+          if (lane >= ndv) { dn0 = 0xffffffffu; pv0 = -1; }
+          if (lane + 64 >= ndv) { dn1 = 0xffffffffu; pv1 = -1; }
+          for (int s = ndv + lane; s < nd; s += 64) { has_row[s] = 0; done_ver[s] = -1; }
+          nd = ndv;
+          for (int i = lane; i < SP_HASH; i += 64) { hkey[i] = -1; hval[i] = -1; }
+          WAVE_FENCE();
+          for (int s = 0; s < nd; ++s) {   // (readlane in uniform control flow: the source register is whole)
+            const uint32_t nn = s < 64 ? (uint32_t)__builtin_amdgcn_readlane((int)dn0, s)
+                                       : (uint32_t)__builtin_amdgcn_readlane((int)dn1, s - 64);
+            if (lane == 0) hash_insert(nn, s);
+          }
+          WAVE_FENCE();
+          // re-score the restored rows for pods v.. (their dsc entries after the undone landing are stale)
+          for (int pass = 0; pass < 2; ++pass) {
+            for (uint64_t bb = pass ? redo1 : redo0; bb; bb &= bb - 1) {
+              const int sl = (pass ? 64 : 0) + __builtin_ctzll(bb);
+              const Row rr = drows[sl];
+              if (numa_on && ((rr.nr.nflags >> NF_POLICY_SHIFT) & 3u)) hint_table_fill(s_ht0, rr.nr, zone_avail(rr.nr), lane);
+              WAVE_FENCE();
+              for (int q2 = v + lane; q2 < B; q2 += 64) dsc[q2 * B + sl] = (int16_t)row_score(rr, pods(q2), a.pf, m, &s_ht0);
+              WAVE_FENCE();
+            }
+          }
+          const int32_t myv0 = pv0, myv1 = pv1;
+          if (lane < nd) done_ver[lane] = myv0;
+          if (lane + 64 < nd) done_ver[lane + 64] = myv1;
+          for (int qq = v + lane; qq < B; qq += 64) { rescored[qq] = 0; jobs_left[qq] = 0; }
+          if (lane == 0) {
+            s_jq_head = 0;
+            s_jq_tail = 0;
+            s_cut_at = -1;
+            s_reserved = v;
+            s_decided = v;
+            s_parked = 0;
+          }
+          WAVE_FENCE();
+          q = v;
+          wm = v;
+          end_at = B;
+          end_why = 0;
+          if (lane == 0) st_rel(&s_stop, 0);
+          n_hs = -1;   // reload pod v's header
+          load_hdr(v, n_hs, n_hc, n_nlev, n_feas, n_next, n_lh);
+          rolled = true;
+          break;
+        }
+        const int F = d.F + wave_sum(fadd);
+        if (lane == 0) final_F[v] = F;
+        ++v;
+      }
+      {   // a Reserve that needs the host's cpuset selection ends the batch right after its pod
+        const int cut_at = ld_acq(&s_cut_at);
+        if (!rolled && cut_at >= 0 && v > cut_at) { committed = cut_at + 1; host_cut = true; }
+      }
+      if (err) break;
+      if (host_cut) break;
+      if (rolled) continue;
+      if (v == end_at && v == q) { committed = v; break; }
+      // ------------------------------------------------ decide pod q
+      if (q >= end_at || q - v >= SP_LAG || ld_acq(&s_cut_at) >= 0) {
+        if (++spins > SP_SPIN_LIMIT) { err = true; break; }
+        sp_sleep();
+        continue;
+      }
+      spins = 0;
+      const int p = q;
+      const int hs = n_hs, hc = n_hc, nlev = n_nlev, feas = n_feas, next = n_next;
+      const uint32_t lh = n_lh;
+      // dirty slots: ready (exact current score) or pending (left out)
+      const int dv0 = lane < nd ? ld_acq(&done_ver[lane]) : -1;
+      const int dv1 = lane + 64 < nd ? ld_acq(&done_ver[lane + 64]) : -1;
+      const bool rdy0 = lane < nd && dv0 == pv0, rdy1 = lane + 64 < nd && dv1 == pv1;
+      const uint64_t pend0 = __ballot(lane < nd && !rdy0), pend1 = __ballot(lane + 64 < nd && !rdy1);
+      if ((a.dbg & 1u) && (pend0 | pend1)) {   // diagnostics: no speculation, wait for the pending rows
+        if (++spins > SP_SPIN_LIMIT) { err = true; break; }
+        sp_sleep();
+        continue;
+      }
+      if (p + 1 < B) load_hdr(p + 1, n_hs, n_hc, n_nlev, n_feas, n_next, n_lh);   // consumed by the next decision
+      int sc0 = -1, so0 = -1, sc1 = -1, so1 = -1;
+      if (lane < nd) { so0 = dso[p * B + lane]; if (rdy0) sc0 = dsc[p * B + lane]; }
+      if (lane + 64 < nd) { so1 = dso[p * B + 64 + lane]; if (rdy1) sc1 = dsc[p * B + 64 + lane]; }
+      // action 0 commit, 1 FitError, 2 stop deciding before p
+      int action = 0;
+      uint32_t winner = 0xffffffffu;
+      int M = -1, F = 0;
+      int64_t T = 0;
+      bool slowpath = p == 0 && a.forced_node >= 0;
+      const bool lvl = lane < MAXLEV && lane < nlev;
+      // listed levels minus the dirty rows listed there (their batch-start score)
+      int dec_l = 0;
+#pragma unroll
+      for (int j = 0; j < MAXLEV; ++j) {
+        const int sj = __builtin_amdgcn_readlane(hs, j);
+        const int dj = __popcll(__ballot(so0 >= 0 && so0 == sj)) + __popcll(__ballot(so1 >= 0 && so1 == sj));
+        if (lane == j) dec_l = dj;
+      }
+      const int clean = lvl ? hc - dec_l : 0;
+      const int Md = wave_max(max(sc0, sc1));
+      const int Fd = wave_sum((sc0 >= 0) - (so0 >= 0) + (sc1 >= 0) - (so1 >= 0));
+      M = max(wave_max(clean > 0 ? hs : -1), Md);
+      F = Fd + feas;
+      bool full_row = false;
+      if (slowpath) {
+        M = a.forced_score;
+        F = a.forced_feasible;
+        T = a.forced_ties;
+        winner = (uint32_t)a.forced_node;
+      } else if (M <= next) {
+        full_row = a.S != nullptr;
+        if (!full_row) { action = 2; end_why = 3; }
+      } else if (M < 0) {
+        action = 1;
+      } else {
+        const bool nw0 = sc0 == M, nw1 = sc1 == M;
+        const int cm_lane = (lvl && hs == M) ? clean : 0;
+        T = (int64_t)wave_sum(cm_lane) + __popcll(__ballot(nw0)) + __popcll(__ballot(nw1));
+        const int64_t jp = tiebreak_position(a.seed, sseq[p], T);
+        int off = 0, len = 0;
+        for (int j = 0; j < MAXLEV; ++j) {
+          const int sj = __builtin_amdgcn_readlane(hs, j);
+          const int cj = __builtin_amdgcn_readlane(hc, j);
+          if (sj < 0) break;
+          if (sj == M) { len = cj; break; }
+          off += cj;
+        }
+        const uint64_t new0 = __ballot(nw0), new1 = __ballot(nw1);
+        const uint64_t old0 = __ballot(so0 == M && lane < nd), old1 = __ballot(so1 == M && lane + 64 < nd);
+        const int nnew = __popcll(new0) + __popcll(new1), nold = __popcll(old0) + __popcll(old1);
+        const int lo = (int)max<int64_t>(0, jp - 2 - nnew);
+        const int hi = (int)min<int64_t>(len - 1, jp - 1 + nold);
+        const int W = hi - lo + 1;
+        const uint32_t* L = list_ptr(a, 0, p);
+        constexpr int WCH = (2 * MAX_BATCH + 2 + 63) / 64;
+        uint32_t xw[WCH];
+        bool ow[WCH];
+        uint32_t cand = 0xffffffffu;
+        int base_old = 0;
+        if (len > 0) {
+#pragma unroll
+          for (int c = 0; c < WCH; ++c) {
+            const int i = c * 64 + lane, e = off + lo + i;
+            const uint32_t fromh = (uint32_t)__shfl((int)lh, e & 31);
+            xw[c] = 0xffffffffu;
+            if (c * 64 < W && i < W) xw[c] = e < 32 ? fromh : L[e];
+          }
+          const uint32_t win0 = (uint32_t)__builtin_amdgcn_readlane((int)xw[0], 0);
+#pragma unroll
+          for (int c = 0; c < WCH; ++c) ow[c] = false;
+          each_node(old0, old1, [&](uint32_t n) {
+            base_old += n < win0 ? 1 : 0;
+#pragma unroll
+            for (int c = 0; c < WCH; ++c) ow[c] |= xw[c] == n;
+          });
+          int running = base_old;
+#pragma unroll
+          for (int c = 0; c < WCH; ++c) {
+            if (c * 64 >= W) break;
+            const int i = c * 64 + lane;
+            const bool valid = i < W;
+            const uint64_t bo = __ballot(valid && ow[c]);
+            const int older = running + __popcll(bo & lt_mask);
+            int newer = 0;
+            each_node(new0, new1, [&](uint32_t n) { newer += n < xw[c] ? 1 : 0; });
+            if (valid && !ow[c] && (int64_t)(lo + i - older + newer + 1) == jp) cand = xw[c];
+            running += __popcll(bo);
+          }
+        }
+        each_node(new0, new1, [&](uint32_t n) {
+          int u = 0;
+          each_node(new0, new1, [&](uint32_t n2) { u += n2 < n ? 1 : 0; });
+          int64_t ltn = -1;
+          int older = 0;
+          if (len == 0) {
+            ltn = 0;
+          } else {
+            int pp = 0;
+#pragma unroll
+            for (int c = 0; c < WCH; ++c) {
+              if (c * 64 >= W) break;
+              const bool valid = c * 64 + lane < W;
+              pp += __popcll(__ballot(valid && xw[c] < n));
+              older += __popcll(__ballot(valid && ow[c] && xw[c] < n));
+            }
+            older += base_old;
+            if (pp == 0) ltn = (lo == 0) ? 0 : -1;
+            else if (pp == W) ltn = (hi == len - 1) ? len : -1;
+            else ltn = lo + pp;
+          }
+          if (ltn >= 0 && ltn - older + u + 1 == jp) cand = n;
+        });
+        const uint64_t got = __ballot(cand != 0xffffffffu);
+        if (!got) { action = 2; end_why = 1; }
+        else winner = (uint32_t)__builtin_amdgcn_readlane((int)cand, __ffsll((long long)got) - 1);
+      }
+      if (full_row) {
+        // exact resolution of pod p from its whole score row: batch-start S[p][*] for clean nodes, the current
+        // score for ready dirty rows, pending rows left out (verified later like any decision)
+        const int16_t* row = a.S + (size_t)p * a.ld;
+        const uint32_t len = a.own1 - a.own0;
+        constexpr int VB = 8;
+        auto load_blk = [&](uint32_t i0, int16_t (&x)[8]) {
+          if (i0 + 8 <= len) {
+            const uint4 vv = *reinterpret_cast<const uint4*>(row + i0);
+            const uint32_t w[4] = {vv.x, vv.y, vv.z, vv.w};
+#pragma unroll
+            for (int k = 0; k < 8; ++k) x[k] = (int16_t)(w[k >> 1] >> (16 * (k & 1)));
+          } else {
+#pragma unroll
+            for (int k = 0; k < 8; ++k) x[k] = i0 + k < len ? row[i0 + k] : (int16_t)-1;
+          }
+        };
+        int lmax = -1, lcnt = 0, lfeas = 0;
+        for (uint32_t b0 = 0; b0 < len; b0 += 512u * VB) {
+          int16_t x[VB][8];
+#pragma unroll
+          for (int u = 0; u < VB; ++u) load_blk(b0 + 512u * u + 8u * lane, x[u]);
+#pragma unroll
+          for (int u = 0; u < VB; ++u)
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+              const int xv = x[u][k];
+              lfeas += xv >= 0 ? 1 : 0;
+              lcnt = xv > lmax ? 1 : lcnt + (xv == lmax ? 1 : 0);
+              lmax = xv > lmax ? xv : lmax;
+            }
+        }
+        F = wave_sum(lfeas) + Fd;
+        int Mc = wave_max(lmax);
+        int64_t Tc = Mc >= 0 ? (int64_t)wave_sum(lmax == Mc ? lcnt : 0) - __popcll(__ballot(lane < nd && so0 == Mc)) -
+                                   __popcll(__ballot(lane + 64 < nd && so1 == Mc))
+                             : 0;
+        if (Mc >= 0 && Tc <= 0) {
+          lmax = -1;
+          lcnt = 0;
+          for (uint32_t b0 = 0; b0 < len; b0 += 512u * VB) {
+            int16_t x[VB][8];
+#pragma unroll
+            for (int u = 0; u < VB; ++u) load_blk(b0 + 512u * u + 8u * lane, x[u]);
+#pragma unroll
+            for (int u = 0; u < VB; ++u)
+#pragma unroll
+              for (int k = 0; k < 8; ++k) {
+                const int xv = x[u][k];
+                if (xv >= 0 && xv >= lmax && sp_hash_find(a.own0 + b0 + 512u * u + 8u * lane + k) < 0) {
+                  lcnt = xv > lmax ? 1 : lcnt + 1;
+                  lmax = xv;
+                }
+              }
+          }
+          Mc = wave_max(lmax);
+          Tc = Mc >= 0 ? (int64_t)wave_sum(lmax == Mc ? lcnt : 0) : 0;
+        }
+        M = max(Mc, Md);
+        if (M < 0) {
+          action = 1;
+        } else {
+          const uint64_t new0 = __ballot(sc0 == M), new1 = __ballot(sc1 == M);
+          const uint64_t old0 = __ballot(lane < nd && so0 == M), old1 = __ballot(lane + 64 < nd && so1 == M);
+          T = (Mc == M ? Tc : 0) + __popcll(new0) + __popcll(new1);
+          const int64_t jp = tiebreak_position(a.seed, sseq[p], T);
+          int64_t run = 0;
+          int64_t found = -1;
+          for (uint32_t b0 = 0; b0 < len && found == -1; b0 += 512u * VB) {
+            int16_t x[VB][8];
+#pragma unroll
+            for (int u = 0; u < VB; ++u) load_blk(b0 + 512u * u + 8u * lane, x[u]);
+#pragma unroll
+            for (int u = 0; u < VB; ++u) {
+              const uint32_t i0 = b0 + 512u * u;
+              uint32_t fl = 0;
+#pragma unroll
+              for (int k = 0; k < 8; ++k) fl |= (x[u][k] == M ? 1u : 0u) << k;
+              const bool in0 = dn0 - a.own0 - i0 < 512u, in1 = dn1 - a.own0 - i0 < 512u;
+              const uint64_t bn0 = new0 & __ballot(in0), bn1 = new1 & __ballot(in1);
+              const uint64_t bo0 = old0 & __ballot(in0), bo1 = old1 & __ballot(in1);
+              const int tot = wave_sum(__popc(fl)) + __popcll(bn0) + __popcll(bn1) - __popcll(bo0) - __popcll(bo1);
+              if (found == -1 && run + tot >= jp) {
+                each_node(bo0, bo1, [&](uint32_t nn) {
+                  const uint32_t o = nn - a.own0 - i0;
+                  if ((uint32_t)lane == (o >> 3)) fl &= ~(1u << (o & 7u));
+                });
+                each_node(bn0, bn1, [&](uint32_t nn) {
+                  const uint32_t o = nn - a.own0 - i0;
+                  if ((uint32_t)lane == (o >> 3)) fl |= 1u << (o & 7u);
+                });
+                const int c = __popc(fl);
+                const int incl = wave_incl_scan(c);
+                int64_t need = jp - (run + incl - c);
+                int64_t f = -1;
+                if (need >= 1 && need <= c) {
+                  uint32_t bits = fl;
+                  while (--need) bits &= bits - 1;
+                  f = (int64_t)(a.own0 + i0 + 8u * lane + (uint32_t)__builtin_ctz(bits));
+                }
+                const uint64_t gg = __ballot(f >= 0);
+                found = gg ? (int64_t)__builtin_amdgcn_readlane((int)f, __ffsll((long long)gg) - 1) : -2;
+              }
+              run += tot;
+            }
+          }
+          if (found < 0) {
+            action = 2;
+            end_why = 2;
+            const int osl = old0 ? __builtin_ctzll(old0) : old1 ? 64 + __builtin_ctzll(old1) : -1;
+            const uint32_t onode = osl < 0 ? 0u : (uint32_t)__builtin_amdgcn_readlane((int)(osl < 64 ? dn0 : dn1), osl & 63);
+            const int ohash = osl < 0 ? -9 : sp_hash_find(onode);
+            const int osv = osl < 0 ? -9 : (int)a.S[(size_t)p * a.ld + (onode - a.own0)];
+            const int odso = osl < 0 ? -9 : (int)dso[p * B + osl];
+            if (lane == 0)   // diagnostics (GS_DEBUG_CUTS): the inconsistent tie count
+              a.out[p] = PlacementDev{-7, (uint32_t)run, (int64_t)M | ((int64_t)Mc << 20) | ((int64_t)Md << 40), (uint32_t)T,
+                                      (uint32_t)Tc, (uint32_t)(__popcll(new0) + __popcll(new1)),
+                                      (uint32_t)(__popcll(old0) + __popcll(old1)), {(int64_t)jp, (int64_t)nd, (int64_t)__popcll(pend0), 0}, {0, 0, 0, 0},
+                                      {(uint64_t)osl, (uint64_t)onode, (uint64_t)(int64_t)ohash,
+                                       (uint64_t)(((int64_t)osv << 32) | (uint32_t)odso)}};
+          }
+          else winner = (uint32_t)found;
+          slowpath = true;
+        }
+      }
+      if (action == 0 && (int32_t)winner < 0) { action = 2; end_why = 4; }
+      if (action == 2) {   // stop deciding here: the batch ends at p once everything before it is verified
+        end_at = p;
+        continue;
+      }
+      // ---- record the decision, claim / version the winner's slot
+      DecRec d{};
+      d.winner = action == 1 ? -1 : (int32_t)winner;
+      d.M = action == 1 ? -1 : M;
+      d.T = (int32_t)T;
+      d.F = F;
+      d.nd_before = nd;
+      d.pend0 = pend0;
+      d.pend1 = pend1;
+      d.flags = (action == 1 ? SP_FITERR : 0u) | (slowpath ? SP_SLOW : 0u);
+      d.slot = -1;
+      d.prev_pend = -1;
+      if (action == 0) {
+        const uint64_t hit0 = __ballot(dn0 == winner), hit1 = __ballot(dn1 == winner);
+        int slot = hit0 ? __builtin_ctzll(hit0) : hit1 ? 64 + __builtin_ctzll(hit1) : -1;
+        if (slot < 0) {   // fresh row: a new slot, its batch-start scores for the later pods
+          slot = nd;
+          d.flags |= SP_FRESH;
+          if (lane == (nd & 63)) { if (nd < 64) { dn0 = winner; pv0 = p; } else { dn1 = winner; pv1 = p; } }
+          const int q0 = p + 1 + lane, q1 = q0 + 64;
+          const int16_t s0v = q0 < B ? a.S_own[(size_t)q0 * a.ld + (winner - a.own0)] : (int16_t)0;
+          const int16_t s1v = q1 < B ? a.S_own[(size_t)q1 * a.ld + (winner - a.own0)] : (int16_t)0;
+          if (lane == 0) {
+            hash_insert(winner, slot);
+            done_ver[slot] = -1;
+          }
+          if (q0 < B) dso[q0 * B + slot] = s0v;
+          if (q1 < B) dso[q1 * B + slot] = s1v;
+          ++nd;
+        } else {          // a ready dirty row lands another pod: pending again
+          const int32_t prevv = slot < 64 ? __builtin_amdgcn_readlane(pv0, slot) : __builtin_amdgcn_readlane(pv1, slot - 64);
+          d.prev_pend = prevv;
+          if (lane == (slot & 63)) { if (slot < 64) pv0 = p; else pv1 = p; }
+        }
+        d.slot = slot;
+      }
+      if (lane == 0) dec[p] = d;
+      WAVE_FENCE();
+      if (lane == 0) st_rel(&s_decided, p + 1);
+      ++q;
+    }
+    if (lane == 0) {
+      s_committed = committed;
+      s_endwhy = committed < B ? (end_why << 16 | (host_cut ? 0x8000 : 0) | (end_at & 0xfff)) : 0;
+      s_hostcut = host_cut ? 1 : 0;
+      s_nd = nd;
+      if (err) s_err = 1;
+      st_rel(&s_finish, 1);
+    }
+  } else if (wv == 1) {
+    // =================================================== Reserve ===================================================
+    int topo_id = -1;
+    int f_kind = 0, f_region = 0, f_off = 0, f_size = 8;
+    const void* f_src = nullptr;
+    if (lane < ROW_I64) { f_kind = 1; f_src = m.c64(kRowCol[lane]); f_off = lane * 8; }
+    else if (lane == ROW_I64) { f_kind = 2; f_src = m.c32(C_FREE_PODS); f_off = offsetof(Row, free_pods); f_size = 4; }
+    else if (lane == ROW_I64 + 1) { f_kind = 2; f_src = m.c32(C_DFLAGS); f_off = offsetof(Row, dflags); f_size = 4; }
+    else if (lane == ROW_I64 + 2) { f_kind = 4; f_off = offsetof(Row, node); }
+    else if (numa_on) {
+      if (lane >= 20 && lane < 26) { f_kind = 1; f_src = m.c64(C_CPU_UN0 + (lane - 20)); f_region = 1; f_off = (lane - 20) * 8; }
+      else if (lane == 26) { f_kind = 2; f_src = m.c32(C_CPU_META); f_region = 1; f_off = offsetof(CpuStateDev, meta); f_size = 4; }
+      else if (lane == 27) { f_kind = 2; f_src = m.c32(C_TOPO_DEV); f_region = 1; f_off = offsetof(CpuStateDev, topo); f_size = 4; }
+      else if (lane == 28) { f_kind = 3; f_src = a.aff; f_region = 2; f_size = 4; }
+      else if (lane >= 32 && lane < 32 + NUMA_I64) {
+        f_kind = 1; f_src = m.c64(C_ZCAP_CPU0 + (lane - 32)); f_off = offsetof(Row, nr) + (lane - 32) * 8;
+      } else if (lane >= 50 && lane < 50 + NUMA_I32) {
+        f_kind = 2; f_src = m.c32(C_NFLAGS + (lane - 50)); f_off = offsetof(Row, nr.nflags) + (lane - 50) * 4; f_size = 4;
+      }
+    }
+    int q = 0;
+    uint32_t spins = 0;
+    for (;;) {
+      if (ld_acq(&s_stop)) {   // rollback: park until wave 0 has repaired the state, then resume at s_reserved
+        if (lane == 0) __atomic_fetch_add(&s_parked, 1, __ATOMIC_ACQ_REL);
+        while (ld_acq(&s_stop) && !ld_acq(&s_finish)) sp_sleep();
+        q = ld_acq(&s_reserved);
+        topo_id = -1;
+        continue;
+      }
+      if (ld_acq(&s_finish)) break;
+      if (q >= ld_acq(&s_decided) || ld_acq(&s_cut_at) >= 0) {
+        if (++spins > SP_SPIN_LIMIT) break;
+        sp_sleep();
+        continue;
+      }
+      spins = 0;
+      const DecRec d = dec[q];
+      const PodVec& pk = pods(q);
+      if (d.flags & SP_FITERR) {
+        if (lane == 0) {
+          a.out[q] = PlacementDev{-1, (uint32_t)d.F, 0, 0, 0, 0, 0, {0, 0, 0, 0}, {0, 0, 0, 0}};
+          rescored[q] = 1;
+          __atomic_store_n(&s_reserved, q + 1, __ATOMIC_RELEASE);
+        }
+        WAVE_FENCE();
+        ++q;
+        continue;
+      }
+      const int slot = d.slot;
+      const uint32_t winner = (uint32_t)d.winner;
+      const bool fresh = d.flags & SP_FRESH;
+      if (fresh) {   // fetch the row: one load per lane, then LDS
+        int64_t vv = 0;
+        if (f_kind == 1) vv = reinterpret_cast<const int64_t*>(f_src)[winner];
+        else if (f_kind == 2) vv = reinterpret_cast<const int32_t*>(f_src)[winner];
+        else if (f_kind == 3) vv = (int64_t)reinterpret_cast<const uint8_t*>(f_src)[(size_t)q * a.ld + (winner - a.own0)];
+        else if (f_kind == 4) vv = (int64_t)winner;
+        if (f_kind) {
+          unsigned char* dst = f_region == 0 ? reinterpret_cast<unsigned char*>(&drows[slot])
+                             : f_region == 1 ? reinterpret_cast<unsigned char*>(&cst[slot])
+                                             : reinterpret_cast<unsigned char*>(&s_aff);
+          if (f_size == 8) *reinterpret_cast<int64_t*>(dst + f_off) = vv;
+          else *reinterpret_cast<int32_t*>(dst + f_off) = (int32_t)vv;
+        }
+        if (lane == 0) has_row[slot] = 1;
+      } else {
+        // the slot's previous version must be fully re-scored before its row changes
+        bool stop = false;
+        while (ld_acq(&done_ver[slot]) < d.prev_pend) {
+          if (ld_acq(&s_stop) || ld_acq(&s_finish)) { stop = true; break; }
+          sp_sleep();
+        }
+        if (stop) continue;
+      }
+      if (lane == 0 && (!fresh || !numa_on)) s_aff = -1;
+      WAVE_FENCE();
+      {   // undo log: the slot's state before this Reserve
+        UndoRec& u = undo[q % SP_LAG];
+        const uint64_t* src = reinterpret_cast<const uint64_t*>(&drows[slot]);
+        uint64_t* dst = reinterpret_cast<uint64_t*>(&u.row);
+        for (int i = lane; i < (int)(sizeof(Row) / 8); i += 64) dst[i] = src[i];
+        const uint64_t* s2 = reinterpret_cast<const uint64_t*>(&cst[slot]);
+        uint64_t* d2 = reinterpret_cast<uint64_t*>(&u.cs);
+        for (int i = lane; i < (int)(sizeof(CpuStateDev) / 8); i += 64) d2[i] = s2[i];
+        if (lane == 0) u.slot = slot;
+      }
+      WAVE_FENCE();
+      Row& dr_ = drows[slot];
+      if (numa_on) {
+        const int tp = cst[slot].topo;
+        const uint32_t nfl = dr_.nr.nflags;
+        if (tp >= 0 && tp != topo_id && !(pk.numa & (PN_SKIP | PN_PREFAIL)) &&
+            ((pk.numa & PN_BIND) || ((nfl >> NF_BIND_SHIFT) & 3u))) {
+          const uint64_t* src = reinterpret_cast<const uint64_t*>(a.topos + tp);
+          uint64_t* dst = reinterpret_cast<uint64_t*>(&s_topo);
+          for (int i = lane; i < (int)(sizeof(TopoDev) / 8); i += 64) dst[i] = src[i];
+          topo_id = tp;
+        }
+        WAVE_FENCE();
+      }
+      int cut = 0;
+      {
+        const Row dr = dr_;
+        const uint32_t nf = dr.nr.nflags;
+        const bool maybe_rb = (pk.numa & PN_BIND) || (((nf >> NF_BIND_SHIFT) & 3u) && (pk.req_keys & 1u) && pk.req[0]);
+        const bool numa_reserve =
+            numa_on && !(pk.numa & (PN_SKIP | PN_PREFAIL)) && (maybe_rb || ((nf >> NF_POLICY_SHIFT) & 3u));
+        NumaOut no{};
+        if (numa_reserve)
+          no = numa_eval<true, false, true>(dr.nr, pk, a.pf, SlotsLds{dr, m}, a.pf.enabled & 0x10u, false, s_aff);
+        if (lane == 0) {
+          PlacementDev pl{(int32_t)winner, (uint32_t)d.F, (int64_t)d.M, (uint32_t)d.T, (d.flags & SP_SLOW) ? 1u : 0u,
+                          0, 0, {0, 0, 0, 0}, {0, 0, 0, 0}};
+          if (numa_reserve) {
+            const bool rb = no.flags & GS_PLACED_CPUSET;
+            if (no.reason) pl.flags |= PL_RESERVE_FAILED;
+            if (rb || ((nf >> NF_POLICY_SHIFT) & 3u)) {
+              pl.flags |= no.flags;
+              pl.zkeys = no.zkeys;
+#pragma unroll
+              for (int z = 0; z < 4; ++z) { pl.zcpu[z] = no.zcpu[z]; pl.zmem[z] = no.zmem[z]; }
+              if (nf & NF_TOPO_VALID) {
+                uint32_t f2 = dr.nr.nflags2;
+#pragma unroll
+                for (int z = 0; z < 4; ++z) {
+                  const bool zc = no.zkeys >> z & 1u, zm = no.zkeys >> (4 + z) & 1u;
+                  if (!zc && !zm) continue;
+                  dr_.nr.zraw_cpu[z] = dr.nr.zraw_cpu[z] + no.zcpu[z];
+                  dr_.nr.zraw_mem[z] = dr.nr.zraw_mem[z] + no.zmem[z];
+                  f2 |= (1u << (NF2_ENTRY_SHIFT + z)) | (zc ? 1u << (NF2_ACPU_SHIFT + z) : 0u) |
+                        (zm ? 1u << (NF2_AMEM_SHIFT + z) : 0u);
+                }
+                dr_.nr.nflags2 = f2;
+              }
+              if (rb) {
+                CpuStateDev& cs = cst[slot];
+                if (cs.topo >= 0 && cs.topo == topo_id) {
+                  if (cpuset_reserve((const GS_LDS TopoDev*)&s_topo, (GS_LDS CpuStateDev*)&cs, pk, nf, no.zkeys,
+                                     no.zcpu[0], no.zcpu[1], no.zcpu[2], no.zcpu[3], (GS_LDS NumaRow*)&dr_.nr,
+                                     (GS_LDS uint64_t*)s_cpuset)) {
+                    pl.flags |= PL_DEVICE_CPUSET;
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) pl.cpuset[j] = s_cpuset[j];
+                  } else {
+                    pl.flags |= PL_RESERVE_FAILED;
+                  }
+                } else {
+                  cut = 1;
+                }
+              }
+            }
+          }
+          a.out[q] = pl;
+          for (int s = 0; s < 7; ++s) dr_.free[s] = dr.free[s] - pk.req[s];
+          dr_.nzfree[0] = dr.nzfree[0] - pk.nz[0];
+          dr_.nzfree[1] = dr.nzfree[1] - pk.nz[1];
+          dr_.free_pods = dr.free_pods - 1;
+          dr_.la_free[0] = dr.la_free[0] - pk.est[0];
+          dr_.la_free[1] = dr.la_free[1] - pk.est[1];
+          if (pk.flags & PF_PROD) {
+            dr_.la_pfree[0] = dr.la_pfree[0] - pk.est[0];
+            dr_.la_pfree[1] = dr.la_pfree[1] - pk.est[1];
+          }
+        }
+      }
+      cut = __builtin_amdgcn_readlane(cut, 0);
+      WAVE_FENCE();
+      // ---- the row's re-scoring: hint table of its new state, jobs of 64 later pods
+      const int nlater = B - (q + 1);
+      const int njobs = (nlater + 63) / 64;
+      if (njobs == 0) {
+        if (lane == 0) {
+          done_ver[slot] = q;
+          rescored[q] = 1;
+        }
+      } else {
+        const int tb = q % SP_TABLES;
+        // the table's previous user (pod q - SP_TABLES) must be done
+        bool stop = false;
+        if (q >= SP_TABLES) {
+          while (!ld_acq(&rescored[q - SP_TABLES])) {
+            if (ld_acq(&s_stop) || ld_acq(&s_finish)) { stop = true; break; }
+            sp_sleep();
+          }
+        }
+        if (!stop) {
+          const Row rr = dr_;
+          if (numa_on && ((rr.nr.nflags >> NF_POLICY_SHIFT) & 3u)) hint_table_fill(tables[tb], rr.nr, zone_avail(rr.nr), lane);
+          WAVE_FENCE();
+          if (lane == 0) {
+            jobs_left[q] = njobs;
+            int t = s_jq_tail;
+            for (int j = 0; j < njobs; ++j, ++t) jobq[t % SP_JOBQ] = Job{slot, q, j, tb};
+            __atomic_store_n(&s_jq_tail, t, __ATOMIC_RELEASE);
+          }
+        } else {
+          // rollback began while this pod waited: it will be undone (its undo record is logged)
+        }
+      }
+      WAVE_FENCE();
+      if (lane == 0) {
+        if (cut) __atomic_store_n(&s_cut_at, q, __ATOMIC_RELEASE);
+        __atomic_store_n(&s_reserved, q + 1, __ATOMIC_RELEASE);
+      }
+      WAVE_FENCE();
+      ++q;
+    }
+  } else {
+    // ============================================== re-scoring jobs ==============================================
+    uint32_t spins = 0;
+    for (;;) {
+      if (ld_acq(&s_stop)) {
+        if (lane == 0) __atomic_fetch_add(&s_parked, 1, __ATOMIC_ACQ_REL);
+        while (ld_acq(&s_stop) && !ld_acq(&s_finish)) sp_sleep();
+        continue;
+      }
+      if (ld_acq(&s_finish)) break;
+      int h = -1;
+      if (lane == 0) {
+        const int hd = __atomic_load_n(&s_jq_head, __ATOMIC_ACQUIRE);
+        if (hd < __atomic_load_n(&s_jq_tail, __ATOMIC_ACQUIRE)) {
+          int expect = hd;
+          if (__atomic_compare_exchange_n(&s_jq_head, &expect, hd + 1, false, __ATOMIC_ACQ_REL, __ATOMIC_ACQUIRE)) h = hd;
+        }
+      }
+      h = __builtin_amdgcn_readfirstlane(h);
+      if (h < 0) {
+        if (++spins > SP_SPIN_LIMIT) break;
+        sp_sleep();
+        continue;
+      }
+      spins = 0;
+      const Job jb = jobq[h % SP_JOBQ];
+      const Row rr = drows[jb.slot];
+      const int q2 = jb.q + 1 + jb.range * 64 + lane;
+      if (q2 < B) dsc[q2 * B + jb.slot] = (int16_t)row_score(rr, pods(q2), a.pf, m, &tables[jb.tbl]);
+      WAVE_FENCE();
+      if (lane == 0) {
+        if (__atomic_fetch_sub(&jobs_left[jb.q], 1, __ATOMIC_ACQ_REL) == 1) {
+          __atomic_store_n(&done_ver[jb.slot], jb.q, __ATOMIC_RELEASE);
+          __atomic_store_n(&rescored[jb.q], 1, __ATOMIC_RELEASE);
+        }
+      }
+      WAVE_FENCE();
+    }
+  }
+  __syncthreads();
+  // ---- write back the fetched dirty rows; final Feasible counts
+  const int nd = s_nd, committed = s_committed;
+  for (int e = tid; e < nd * ROW_I64; e += SP_THREADS) {
+    const int s = e / ROW_I64, j = e % ROW_I64;
+    if (has_row[s] && row_word_mutable(j)) m.c64(kRowCol[j])[drows[s].node] = reinterpret_cast<const int64_t*>(&drows[s])[j];
+  }
+  for (int s = tid; s < nd; s += SP_THREADS)
+    if (has_row[s]) m.c32(C_FREE_PODS)[drows[s].node] = drows[s].free_pods;
+  constexpr int NW = 8 + 11 + 6 + 1;
+  if (numa_on)
+    for (int e = tid; e < nd * NW; e += SP_THREADS) {
+      const int sl = e / NW, j = e % NW;
+      if (!has_row[sl]) continue;
+      const uint32_t node = drows[sl].node;
+      if (j < 8) m.c64(C_ZRAW_CPU0 + j)[node] = (&drows[sl].nr.zraw_cpu[0])[j];
+      else if (j < 19) m.c32(C_NFLAGS2 + (j - 8))[node] = reinterpret_cast<const int32_t*>(&drows[sl].nr.nflags2)[j - 8];
+      else if (j < 25) m.c64(C_CPU_UN0 + (j - 19))[node] = reinterpret_cast<const int64_t*>(&cst[sl])[j - 19];
+      else m.c32(C_CPU_META)[node] = (int32_t)cst[sl].meta;
+    }
+  for (int i = tid; i < committed; i += SP_THREADS) a.out[i].feasible = (uint32_t)final_F[i];
+  if (tid == 0) {
+    a.committed[0] = committed;
+    a.committed[1] = (committed == B && !s_hostcut && !s_err) ? 1 : 0;
+    a.committed[2] = s_endwhy;   // diagnostics: why a batch ended early (GS_DEBUG_CUTS)
+    a.committed[3] = s_err ? 1 : 0;
+  }
+}
+
+hipError_t launch_commit_spec(const CommitArgs& a, hipStream_t st) {
+  hipLaunchKernelGGL(commit_spec_kernel, dim3(1), dim3(SP_THREADS), spec_smem_bytes(a.npods), st, a);
+  return hipGetLastError();
+}
+
+hipError_t set_commit_spec_attributes() {
+  return hipFuncSetAttribute(reinterpret_cast<const void*>(commit_spec_kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
+                             (int)spec_smem_bytes(MAX_BATCH));
+}
+
+}  // namespace gs

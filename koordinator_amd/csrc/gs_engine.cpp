@@ -747,6 +747,8 @@ CommitArgs commit_args(gs_ctx* c, int b) {
   a.window_k = c->window_k;
   a.start = c->next_start;
   a.nnodes = c->N;
+  static const bool nospec = getenv("GS_SPEC_WAIT") && getenv("GS_SPEC_WAIT")[0] == '1';
+  a.dbg = nospec ? 1u : 0u;
   return a;
 }
 
@@ -819,6 +821,7 @@ int finish_batch(gs_ctx* c, int b, bool clobbered, int* committed_out) {
   c->stats.batches += 1;
   int committed = c->h_committed[0];
   if (committed < 0) return fail(c, GS_ESTATE, "commit pass of a batch was voided unexpectedly");
+  if (c->h_committed[3]) return fail(c, GS_EDEVICE, "commit kernel: a pipeline wait expired (internal error)");
   if (c->window_k) {
     if (committed == 0) return fail(c, GS_ESTATE, "node-sampling commit made no progress");
     c->next_start = (uint32_t)c->h_committed[2];
@@ -891,7 +894,19 @@ int finish_batch(gs_ctx* c, int b, bool clobbered, int* committed_out) {
     HIP_TRY(c, hipMemcpyAsync(c->h_out, c->d_out, sizeof(PlacementDev) * committed, hipMemcpyDeviceToHost, c->st));
     HIP_TRY(c, hipStreamSynchronize(c->st));
   }
-  if (committed < b) c->stats.cuts += 1;
+  if (committed < b) {
+    c->stats.cuts += 1;
+    static const bool dbg = getenv("GS_DEBUG_CUTS") && getenv("GS_DEBUG_CUTS")[0] == '1';
+    if (dbg) {
+      const PlacementDev& x = c->h_out[committed];
+      fprintf(stderr, "gpuscore: batch of %d ended after %d pods (code %#x) [%d run %u M %lld Mc %lld Md %lld T %u Tc %d new %u old %u jp %lld nd %lld pend %lld]\n",
+              b, committed, c->h_committed[2], x.node, x.feasible, (long long)(x.score & 0xfffff),
+              (long long)((x.score >> 20) & 0xfffff), (long long)(x.score >> 40), x.ties, (int)x.flags, x.zkeys, x.pad,
+              (long long)x.zcpu[0], (long long)x.zcpu[1], (long long)x.zcpu[2]);
+      fprintf(stderr, "   old slot %lld node %llu hash %lld S %d dso %d\n", (long long)x.cpuset[0],
+              (unsigned long long)x.cpuset[1], (long long)x.cpuset[2], (int)(x.cpuset[3] >> 32), (int)(int32_t)x.cpuset[3]);
+    }
+  }
   *committed_out = committed;
   return GS_OK;
 }
@@ -1559,6 +1574,49 @@ int gs_synchronize(gs_ctx* c) {
 int gs_debug_verify_cpuset(gs_ctx* c, int on) {
   if (!c) return GS_EINVAL;
   c->verify_cpuset = on != 0;
+  return GS_OK;
+}
+
+// Cycle cost of the commit kernel's pair evaluations on mirror rows (gs_probe.hip): n probes, probe i on node
+// nodes[i] with pod pod_of[i] (modes 0, 2) or with pods 0..min(npods,64)-1 one per lane (mode 1).
+int gs_debug_pair_probe(gs_ctx* c, const gs_pod* pods, uint32_t npods, const uint32_t* nodes, const int32_t* pod_of,
+                        uint32_t n, int mode, int32_t* scores, uint64_t* cycles) {
+  if (!c || !pods || !nodes || !pod_of || !scores || !cycles || npods == 0 || npods > 64 || mode < 0 || mode > 2)
+    return GS_EINVAL;
+  int rc = ready(c);
+  if (rc) return rc;
+  if ((rc = flush_rows(c))) return rc;
+  if (c->prep_stale && (rc = node_prep(c))) return rc;
+  for (uint32_t i = 0; i < n; ++i)
+    if (nodes[i] >= c->N || pod_of[i] < 0 || (uint32_t)pod_of[i] >= npods) return GS_EINVAL;
+  std::vector<PodVec> pv(npods);
+  int prod_cols = 0;
+  for (uint32_t i = 0; i < npods; ++i) {
+    if ((rc = validate_pod(c, pods[i]))) return rc;
+    pv[i] = prep_pod(c, pods[i]);
+    prod_cols |= (pv[i].flags & PF_PROD_SCORE) ? 1 : 0;
+  }
+  PodVec* d_p = nullptr;
+  uint32_t* d_n = nullptr;
+  int32_t *d_o = nullptr, *d_s = nullptr;
+  uint64_t* d_c = nullptr;
+  const size_t ns = (size_t)n * (mode == 1 ? 64 : 1);
+  hipError_t e = hipMalloc(&d_p, sizeof(PodVec) * npods);
+  if (e == hipSuccess) e = hipMalloc(&d_n, 4 * n);
+  if (e == hipSuccess) e = hipMalloc(&d_o, 4 * n);
+  if (e == hipSuccess) e = hipMalloc(&d_s, 4 * ns);
+  if (e == hipSuccess) e = hipMalloc(&d_c, 80 * n);
+  if (e == hipSuccess) e = hipMemset(d_c, 0, 80 * n);
+  if (e == hipSuccess) e = hipMemcpy(d_p, pv.data(), sizeof(PodVec) * npods, hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hipMemcpy(d_n, nodes, 4 * n, hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hipMemcpy(d_o, pod_of, 4 * n, hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hipStreamSynchronize(c->st);
+  if (e == hipSuccess) e = launch_probe(mode, c->mv, c->pf, d_p, (int)npods, d_n, d_o, n, prod_cols, d_s, d_c, c->st);
+  if (e == hipSuccess) e = hipStreamSynchronize(c->st);
+  if (e == hipSuccess) e = hipMemcpy(scores, d_s, 4 * ns, hipMemcpyDeviceToHost);
+  if (e == hipSuccess) e = hipMemcpy(cycles, d_c, 80 * n, hipMemcpyDeviceToHost);
+  (void)hipFree(d_p); (void)hipFree(d_n); (void)hipFree(d_o); (void)hipFree(d_s); (void)hipFree(d_c);
+  if (e != hipSuccess) return fail(c, GS_EDEVICE, "probe: %s", hipGetErrorString(e));
   return GS_OK;
 }
 

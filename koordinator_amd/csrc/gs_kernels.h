@@ -92,6 +92,7 @@ struct CommitArgs {
   uint32_t window_k;
   uint32_t start;
   uint32_t nnodes;
+  uint32_t dbg;              // diagnostics: bit 0 = the speculative commit waits for every pending row (no speculation)
 };
 
 hipError_t set_kernel_attributes();
@@ -115,11 +116,17 @@ size_t commit_smem_bytes(int B);
 hipError_t launch_commit(const CommitArgs& a, hipStream_t st);        // window_k > 0: lockstep kernel
 hipError_t launch_commit_pipe(const CommitArgs& a, hipStream_t st);   // pipelined roles (gs_commit.hip)
 hipError_t set_commit_pipe_attributes();
+hipError_t launch_commit_spec(const CommitArgs& a, hipStream_t st);   // speculative pipeline (gs_commit_spec.hip)
+hipError_t set_commit_spec_attributes();
 hipError_t launch_row_stats(const int16_t* S, uint32_t len, RowStat* out, hipStream_t st);
 hipError_t launch_row_select(const int16_t* S, uint32_t len, int score, int64_t target, uint32_t n0, int32_t* out,
                              hipStream_t st);
 hipError_t launch_scatter_rows(const MirrorView& m, const uint32_t* idx, const int64_t* rows, uint32_t nrows,
                                hipStream_t st);
 int64_t host_tiebreak_position(uint64_t seed, uint64_t seq, int64_t T);
+// diagnostics (gs_probe.hip): cycles of one pair evaluation as the commit kernel runs it
+hipError_t launch_probe(int mode, const MirrorView& m, const Profile& pf, const PodVec* pods, int npods,
+                        const uint32_t* nodes, const int32_t* pod_of, uint32_t n, int prod_cols, int32_t* scores,
+                        uint64_t* cycles, hipStream_t st);
 
 }  // namespace gs

@@ -327,7 +327,7 @@ __global__ void __launch_bounds__(COMMIT_THREADS) commit_kernel(CommitArgs a) {
   // speculative pass queued behind another batch: only if that one committed every pod with nothing left for
   // the host (committed[1] == 1); otherwise a no-op (committed = -1) the host discards
   if (a.prev && a.prev[1] != 1) {
-    if (tid == 0) { a.committed[0] = -1; a.committed[1] = 0; }
+    if (tid == 0) { a.committed[0] = -1; a.committed[1] = 0; a.committed[3] = 0; }
     return;
   }
 
@@ -984,6 +984,7 @@ __global__ void __launch_bounds__(COMMIT_THREADS) commit_kernel(CommitArgs a) {
     a.committed[0] = committed;
     a.committed[1] = (committed == B && !host_cut) ? 1 : 0;
     a.committed[2] = (int32_t)s_start;
+    a.committed[3] = 0;
   }
   if (ST && tid == 0) {
     for (int i = 0; i < 12; ++i) a.stamps[i] += st_acc[i];
@@ -1174,6 +1175,9 @@ size_t commit_smem_bytes(int B) {
 
 hipError_t launch_commit(const CommitArgs& a, hipStream_t st) {
   static const bool lockstep = getenv("GS_COMMIT_LOCKSTEP") && getenv("GS_COMMIT_LOCKSTEP")[0] == '1';
+  static const char* kind = getenv("GS_COMMIT_KERNEL");   // "pipe": the non-speculative pipelined kernel
+  const bool spec_ok = !(kind && kind[0] == 'p') && !a.stamps && a.nranks == 1 && a.S != nullptr;
+  if (!a.window_k && !lockstep && spec_ok) return launch_commit_spec(a, st);
   if (!a.window_k && !lockstep) return launch_commit_pipe(a, st);
   if (a.stamps)
     hipLaunchKernelGGL(commit_kernel<true>, dim3(1), dim3(COMMIT_THREADS), commit_smem_bytes(a.npods), st, a);
@@ -1202,6 +1206,8 @@ hipError_t launch_scatter_rows(const MirrorView& m, const uint32_t* idx, const i
 
 hipError_t set_kernel_attributes() {
   hipError_t e = set_commit_pipe_attributes();
+  if (e != hipSuccess) return e;
+  e = set_commit_spec_attributes();
   if (e != hipSuccess) return e;
   e = hipFuncSetAttribute(reinterpret_cast<const void*>(commit_kernel<false>),
                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)commit_smem_bytes(MAX_BATCH));

@@ -180,6 +180,19 @@ class Engine:
             self._chk(rc, "gs_debug_mirror_check")
         return rc
 
+    def pair_probe(self, pods, nodes, pod_of, mode: int):
+        """Diagnostics: (scores, cycles) of the commit kernel's pair evaluation on mirror rows (gs_debug_pair_probe)."""
+        pods = np.ascontiguousarray(pods, dtype=abi.POD_DTYPE)
+        nodes = np.ascontiguousarray(nodes, dtype=np.uint32)
+        pod_of = np.ascontiguousarray(pod_of, dtype=np.int32)
+        n = len(nodes)
+        scores = np.zeros(n * (64 if mode == 1 else 1), np.int32)
+        cycles = np.zeros(10 * n, np.uint64)
+        self._chk(lib().gs_debug_pair_probe(self._h, abi.ptr(pods), len(pods), abi.ptr(nodes), abi.ptr(pod_of), n, mode,
+                                            abi.ptr(scores), abi.ptr(cycles)), "gs_debug_pair_probe")
+        self.last_probe_stamps = cycles[2 * n:].reshape(n, 8).astype(np.int64)
+        return (scores.reshape(n, 64) if mode == 1 else scores), cycles[:n], cycles[n:2 * n]
+
     def verify_cpusets(self, on: bool = True):
         """Re-run the host takeCPUs for every cpuset the commit kernel selects (schedule fails on a difference)."""
         self._chk(lib().gs_debug_verify_cpuset(self._h, int(on)), "gs_debug_verify_cpuset")
