@@ -286,6 +286,10 @@ typedef struct gs_config {
 #define GS_FAIL_FIT_EPHEMERAL 0x08u
 #define GS_FAIL_FIT_SCALAR 0x10u
 #define GS_FAIL_LOADAWARE 0x20u     /* "node(s) ... usage exceed threshold" (load_aware.go:45-46) */
+/* details of a GS_FAIL_LOADAWARE: the resource the reason names is memory (else cpu), and the aggregated-usage
+ * form of the reason (ErrReasonAggregatedUsageExceedThreshold); gs_reason_string renders them */
+#define GS_FAIL_LA_MEMORY 0x400u
+#define GS_FAIL_LA_AGGREGATED 0x800u
 /* NodeNUMAResource: the first failing check of the plugin, as a 4-bit reason at GS_FAIL_NUMA_SHIFT */
 #define GS_FAIL_NUMA_SHIFT 6
 #define GS_FAIL_NUMA_MASK 0x3C0u
@@ -535,6 +539,13 @@ int gs_quota_settle_batch(gs_quota_group* groups, uint32_t n, const int64_t* run
                           const int32_t* quota, const int64_t* requests, const uint32_t* request_mask,
                           const uint32_t* flags, uint32_t count, const int32_t* placed_node, gs_quota_status* status);
 
+/* Recovery after a failed call (any return < 0 from gs_schedule / gs_evaluate / an upsert): the host state is the
+ * truth — placements of the failed gs_schedule call past the last completed batch were not assumed (gs_stats.pods
+ * counts the pods that were) — and the HBM mirror may hold a partial batch. gs_reset drains the device queues and
+ * rebuilds every mirror row from the host state (the reference's informer snapshot). GS_EDEVICE: the device is
+ * unusable; destroy the context and create a new one. */
+int gs_reset(gs_ctx* ctx);
+
 int gs_get_stats(gs_ctx* ctx, gs_stats* out);
 int gs_reset_stats(gs_ctx* ctx);
 /* Blocks until all device work of ctx has completed. */
@@ -546,6 +557,20 @@ int gs_debug_mirror_check(gs_ctx* ctx);
 /* Diagnostics: on != 0 makes gs_schedule re-run the host takeCPUs (cpu_accumulator.go:87-232) for every cpuset
  * the commit kernel selected and fail with GS_ESTATE on any difference. */
 int gs_debug_verify_cpuset(gs_ctx* ctx, int on);
+/* The reference's Filter status for a GS_FAIL_* code of gs_evaluate (codes[]): the first failing plugin in the
+ * profile's Filter order (NodeResourcesFit, LoadAwareScheduling, NodeNUMAResource), its message as
+ * framework.Status.Message() prints it (the Fit reasons joined by ", ", [upstream] fit.go; load_aware.go:45-46 with
+ * the resource; nodenumaresource/plugin.go:48-55, topology_hint.go:36, topologymanager/manager.go:70,
+ * resource_manager.go:292 for the reasons the device reports) written to buf (NUL-terminated, truncated to len).
+ * scalar_names: the names of resource slots 3..6 for "Insufficient <name>" (NULL: the kubernetes.io/batch-cpu,
+ * batch-memory, mid-cpu, mid-memory defaults). Returns the framework.Code: 0 Success (code 0), 1 Unschedulable,
+ * 2 UnschedulableAndUnresolvable; GS_EINVAL for a malformed code.
+ * Scalar resources: the code does not say which requested scalar was short, so every slot of scalar_mask is
+ * named (pass the pod's gs_pod.scalar_mask; 0 names none). GS_NUMA_ADMIT_ALLOCATE_FAILED renders the allocator's
+ * cpuset-count error; when the reference's Allocate fails earlier, on the hint's NUMA amounts, it prints
+ * "Insufficient NUMA <resource>" instead (the device code does not carry which; parity unpinned). */
+int gs_reason_string(uint32_t code, uint32_t scalar_mask, const char* const* scalar_names, char* buf, size_t len);
+
 /* Diagnostics: s_memtime cycles of the commit kernel's per-pair evaluation on mirror rows. Probe i evaluates
  * node nodes[i]: mode 0 with pod pod_of[i] on a whole wave (the selector's re-score), mode 2 likewise with the
  * lane-parallel evaluation, mode 1 with pods 0..npods-1 (npods <= 64) one per lane over the row's hint table (the

@@ -41,6 +41,18 @@ NUMA_POLICY = {"": 0, "BestEffort": 1, "Restricted": 2, "SingleNUMANode": 3}
 NUMA_ALLOC = {"": 0, "MostAllocated": 1, "LeastAllocated": 2, "DistributeEvenly": 3}
 GS_SCORING_LEAST_ALLOCATED, GS_SCORING_MOST_ALLOCATED = 0, 1
 GS_FAIL_NUMA_SHIFT, GS_FAIL_NUMA_MASK = 6, 0x3C0
+GS_FAIL_LA_MEMORY, GS_FAIL_LA_AGGREGATED = 0x400, 0x800
+# gs_numa_reason (the NodeNUMAResource reason in bits GS_FAIL_NUMA_MASK)
+(GS_NUMA_OK, GS_NUMA_INVALID_REQUESTED_CPUS, GS_NUMA_INVALID_AMP_RATIO, GS_NUMA_AVAILABLE_CPUS_ERROR,
+ GS_NUMA_INSUFFICIENT_AMP_CPU, GS_NUMA_INVALID_TOPOLOGY, GS_NUMA_BIND_POLICY_CONFLICT, GS_NUMA_SMT_ALIGNMENT,
+ GS_NUMA_ALLOCATE_FAILED, GS_NUMA_MISSING_NUMA_RESOURCES, GS_NUMA_AFFINITY_ERROR, GS_NUMA_ADMIT_ALLOCATE_FAILED) = range(12)
+
+
+def reason_string(code: int, scalar_mask: int = 0) -> tuple[int, str]:
+    """(framework.Code, message) of the reference's Filter status for a gs_evaluate failure code (gs_reason_string)."""
+    buf = C.create_string_buffer(512)
+    st = load().gs_reason_string(int(code), int(scalar_mask), None, buf, len(buf))
+    return st, buf.value.decode()
 NUMA_REASONS = ["OK", "InvalidRequestedCPUs", "InvalidAmplificationRatio", "AvailableCPUsError",
                 "InsufficientAmplifiedCPU", "InvalidCPUTopology", "CPUBindPolicyConflict", "SMTAlignment",
                 "AllocateFailed", "MissingNUMAResources", "NUMATopologyAffinity", "AdmitAllocateFailed"]
@@ -245,6 +257,8 @@ SIGNATURES = {
     "gs_debug_mirror_check": (C.c_int, [P]),
     "gs_debug_verify_cpuset": (C.c_int, [P, C.c_int]),
     "gs_debug_pair_probe": (C.c_int, [P, P, C.c_uint32, P, P, C.c_uint32, C.c_int, P, P]),
+    "gs_reason_string": (C.c_int, [C.c_uint32, C.c_uint32, P, C.c_char_p, C.c_size_t]),
+    "gs_reset": (C.c_int, [P]),
     "gs_abi_sizes": (None, [C.POINTER(u64), u32]),
     "gs_topology_register": (C.c_int, [P, C.POINTER(GsCpuTopology), C.POINTER(i32)]),
     "gs_nodes_numa_upsert": (C.c_int, [P, P, P, u32]),

@@ -8,7 +8,7 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 OUT = os.path.join(HERE, "libgpuscore.so")
-SOURCES = ["gs_engine.cpp", "gs_numa_host.cpp", "gs_ingest.cpp", "gs_quota.cpp", "gs_kernels.hip", "gs_commit.hip", "gs_commit_spec.hip", "gs_probe.hip"]
+SOURCES = ["gs_engine.cpp", "gs_numa_host.cpp", "gs_ingest.cpp", "gs_quota.cpp", "gs_reasons.cpp", "gs_kernels.hip", "gs_commit.hip", "gs_commit_spec.hip", "gs_probe.hip"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off",
          "-fno-fast-math", "-Wall"]

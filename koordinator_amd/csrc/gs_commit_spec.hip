@@ -17,9 +17,10 @@
 // Roles (8 waves):
 //   wave 0       decide (selectHost over levels + ready dirty rows, pending rows excluded) and verify, in order;
 //                rollback. Highest issue priority.
-//   wave 1       Reserve of decided pods in order: fetch a fresh winner row into its slot, log the slot's state,
-//                apply assume + Reserve (NUMA split, cpuset), build the row's hint table, queue its re-scoring.
-//   waves 2..7   re-scoring jobs: a reserved row's new score for 64 later pods, one pod per lane.
+//   wave 1       Reserve of decided pods in order: fetch a fresh winner row into its slot (prefetched one pod ahead),
+//                log the slot's state, apply assume + Reserve (NUMA split, cpuset), queue the row's re-scoring.
+//   waves 2..7   re-scoring jobs: a reserved row's new score for 64 later pods, one pod per lane (each wave builds
+//                the row's hint table itself).
 // All hand-offs are LDS words (release / acquire); every wait is bounded (an expired wait ends the batch at the
 // verified prefix with GS_COMMIT_TIMEOUT in committed[3], so a bug cannot hang the GPU).
 #include <hip/hip_runtime.h>
@@ -31,7 +32,7 @@ namespace gs {
 
 constexpr int SP_WAVES = 8, SP_THREADS = 64 * SP_WAVES;
 constexpr int SP_LAG = 8;        // decided - verified <= SP_LAG (undo log depth)
-constexpr int SP_TABLES = 4;     // hint tables of reserved rows in flight
+constexpr int SP_TABLES = SP_WAVES - 2;   // one hint table per re-scoring wave
 constexpr int SP_JOBQ = 32;      // re-scoring job ring
 constexpr int SP_HASH = 256;     // node -> slot (full-row resolution)
 constexpr int SP_FRESH = 1, SP_FITERR = 2, SP_SLOW = 4;   // DecRec.flags
@@ -72,7 +73,22 @@ size_t spec_smem_bytes(int B) {
   return b + 64;
 }
 
+// ST: diagnostic build — per-role cycle sums (s_memtime) into a.stamps: 0 decide, 1 verify, 2 wave 0 waiting,
+// 3 rollbacks, 4 rollback cycles, 5 Reserve busy, 6 Reserve waiting, 7 re-scoring busy, 8 re-scoring waiting,
+// 9 decisions, 10 full-row decisions, 11 full-row cycles, 12 wave 0 total
+template <bool ST>
 __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
+  uint64_t st_acc[15] = {};
+  uint64_t st_last = ST ? __builtin_amdgcn_s_memtime() : 0;
+  const uint64_t st_t0 = st_last;
+#define SPM(i)                                          \
+  do {                                                  \
+    if (ST) {                                           \
+      const uint64_t t_ = __builtin_amdgcn_s_memtime(); \
+      st_acc[i] += t_ - st_last;                        \
+      st_last = t_;                                     \
+    }                                                   \
+  } while (0)
   extern __shared__ __align__(16) unsigned char cm[];
   const int B = a.npods;
   const int tid = threadIdx.x, lane = tid & 63;
@@ -160,13 +176,16 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
       return -1;
     };
     // header of pod p (lanes 0..7: level j score / count) and the head of its level list (lane i: entry i)
+    // (all LEVALL levels: the LevelHdr's first MAXLEV and the LevelExt's rest)
     auto load_hdr = [&](int p, int& hs, int& hc, int& nlev, int& feas, int& next, uint32_t& lh) {
       const LevelHdr* h = hdr_ptr(a, 0, p);
-      nlev = h->nlev;
+      const LevelExt* x = reinterpret_cast<const LevelExt*>(a.xbase + (size_t)a.bmax * LCAP * 4 +
+                                                            (size_t)a.bmax * sizeof(LevelHdr)) + p;
+      nlev = x->nlev;
       feas = h->feasible;
-      next = h->next;
-      hs = lane < MAXLEV ? h->score[lane] : -1;
-      hc = lane < MAXLEV ? h->count[lane] : 0;
+      next = x->next;
+      hs = lane < MAXLEV ? h->score[lane] : lane < LEVALL ? x->score[lane - MAXLEV] : -1;
+      hc = lane < MAXLEV ? h->count[lane] : lane < LEVALL ? x->count[lane - MAXLEV] : 0;
       lh = lane < 32 ? list_ptr(a, 0, p)[lane] : 0xffffffffu;
     };
     int n_hs = -1, n_hc = 0, n_nlev = 0, n_feas = 0, n_next = -1;
@@ -174,6 +193,7 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
     load_hdr(0, n_hs, n_hc, n_nlev, n_feas, n_next, n_lh);
     uint32_t spins = 0;
     while (!err) {
+      SPM(2);
       // ------------------------------------------------ verification, in order
       while (wm < q && ld_acq(&rescored[wm])) ++wm;
       bool rolled = false;
@@ -266,6 +286,8 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
           n_hs = -1;   // reload pod v's header
           load_hdr(v, n_hs, n_hc, n_nlev, n_feas, n_next, n_lh);
           rolled = true;
+          if (ST) st_acc[3] += 1;
+          SPM(4);
           break;
         }
         const int F = d.F + wave_sum(fadd);
@@ -280,6 +302,7 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
       if (host_cut) break;
       if (rolled) continue;
       if (v == end_at && v == q) { committed = v; break; }
+      SPM(1);
       // ------------------------------------------------ decide pod q
       if (q >= end_at || q - v >= SP_LAG || ld_acq(&s_cut_at) >= 0) {
         if (++spins > SP_SPIN_LIMIT) { err = true; break; }
@@ -310,19 +333,17 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
       int M = -1, F = 0;
       int64_t T = 0;
       bool slowpath = p == 0 && a.forced_node >= 0;
-      const bool lvl = lane < MAXLEV && lane < nlev;
-      // listed levels minus the dirty rows listed there (their batch-start score)
-      int dec_l = 0;
-#pragma unroll
-      for (int j = 0; j < MAXLEV; ++j) {
-        const int sj = __builtin_amdgcn_readlane(hs, j);
-        const int dj = __popcll(__ballot(so0 >= 0 && so0 == sj)) + __popcll(__ballot(so1 >= 0 && so1 == sj));
-        if (lane == j) dec_l = dj;
+      // the highest listed level that still holds a clean node: listed count minus the dirty rows listed there (their
+      // batch-start score), from the top (usually the first level)
+      int ctop = 0, Mclean = -1;
+      for (int j = 0; j < nlev; ++j) {
+        const int sj = __builtin_amdgcn_readlane(hs, j), cj = __builtin_amdgcn_readlane(hc, j);
+        const int dj = __popcll(__ballot(so0 == sj)) + __popcll(__ballot(so1 == sj));
+        if (cj > dj) { ctop = cj - dj; Mclean = sj; break; }
       }
-      const int clean = lvl ? hc - dec_l : 0;
       const int Md = wave_max(max(sc0, sc1));
       const int Fd = wave_sum((sc0 >= 0) - (so0 >= 0) + (sc1 >= 0) - (so1 >= 0));
-      M = max(wave_max(clean > 0 ? hs : -1), Md);
+      M = max(Mclean, Md);
       F = Fd + feas;
       bool full_row = false;
       if (slowpath) {
@@ -330,24 +351,24 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
         F = a.forced_feasible;
         T = a.forced_ties;
         winner = (uint32_t)a.forced_node;
+      } else if (M < 0 && next < 0) {
+        action = 1;   // every feasible node is listed, none clean, no dirty row feasible: FitError
       } else if (M <= next) {
         full_row = a.S != nullptr;
         if (!full_row) { action = 2; end_why = 3; }
+        if (ST) st_acc[M < 0 ? 13 : 14] += 1;
       } else if (M < 0) {
         action = 1;
       } else {
         const bool nw0 = sc0 == M, nw1 = sc1 == M;
-        const int cm_lane = (lvl && hs == M) ? clean : 0;
-        T = (int64_t)wave_sum(cm_lane) + __popcll(__ballot(nw0)) + __popcll(__ballot(nw1));
+        // clean listed ties: only at the top clean level (a higher M is a dirty row's: every listed node there is dirty)
+        T = (int64_t)(M == Mclean ? ctop : 0) + __popcll(__ballot(nw0)) + __popcll(__ballot(nw1));
         const int64_t jp = tiebreak_position(a.seed, sseq[p], T);
-        int off = 0, len = 0;
-        for (int j = 0; j < MAXLEV; ++j) {
-          const int sj = __builtin_amdgcn_readlane(hs, j);
-          const int cj = __builtin_amdgcn_readlane(hc, j);
-          if (sj < 0) break;
-          if (sj == M) { len = cj; break; }
-          off += cj;
-        }
+        // level M's segment of the list: offset = listed nodes above it, len = listed nodes at it (0: not listed)
+        const uint64_t atm = __ballot(lane < nlev && hs == M);
+        const int jm = atm ? __builtin_ctzll(atm) : nlev;
+        const int len = atm ? __builtin_amdgcn_readlane(hc, jm) : 0;
+        const int off = wave_sum(lane < jm && lane < nlev ? hc : 0);
         const uint64_t new0 = __ballot(nw0), new1 = __ballot(nw1);
         const uint64_t old0 = __ballot(so0 == M && lane < nd), old1 = __ballot(so1 == M && lane + 64 < nd);
         const int nnew = __popcll(new0) + __popcll(new1), nold = __popcll(old0) + __popcll(old1);
@@ -417,6 +438,8 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
         if (!got) { action = 2; end_why = 1; }
         else winner = (uint32_t)__builtin_amdgcn_readlane((int)cand, __ffsll((long long)got) - 1);
       }
+      if (ST) st_acc[10] += full_row ? 1 : 0;
+      SPM(0);
       if (full_row) {
         // exact resolution of pod p from its whole score row: batch-start S[p][*] for clean nodes, the current
         // score for ready dirty rows, pending rows left out (verified later like any decision)
@@ -542,6 +565,7 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
           slowpath = true;
         }
       }
+      if (full_row) SPM(11);
       if (action == 0 && (int32_t)winner < 0) { action = 2; end_why = 4; }
       if (action == 2) {   // stop deciding here: the batch ends at p once everything before it is verified
         end_at = p;
@@ -587,7 +611,10 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
       WAVE_FENCE();
       if (lane == 0) st_rel(&s_decided, p + 1);
       ++q;
+      if (ST) st_acc[9] += 1;
+      SPM(0);
     }
+    if (ST) st_acc[12] = __builtin_amdgcn_s_memtime() - st_t0;
     if (lane == 0) {
       s_committed = committed;
       s_endwhy = committed < B ? (end_why << 16 | (host_cut ? 0x8000 : 0) | (end_at & 0xfff)) : 0;
@@ -616,7 +643,17 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
         f_kind = 2; f_src = m.c32(C_NFLAGS + (lane - 50)); f_off = offsetof(Row, nr.nflags) + (lane - 50) * 4; f_size = 4;
       }
     }
-    int q = 0;
+    // one load per lane of the fetch map for a fresh winner row of pod qq
+    auto fetch = [&](int qq, uint32_t node) -> int64_t {
+      int64_t vv = 0;
+      if (f_kind == 1) vv = reinterpret_cast<const int64_t*>(f_src)[node];
+      else if (f_kind == 2) vv = reinterpret_cast<const int32_t*>(f_src)[node];
+      else if (f_kind == 3) vv = (int64_t)reinterpret_cast<const uint8_t*>(f_src)[(size_t)qq * a.ld + (node - a.own0)];
+      else if (f_kind == 4) vv = (int64_t)node;
+      return vv;
+    };
+    int q = 0, pf_q = -1;   // pf_q: the pod whose fresh winner row is in flight in pf_v
+    int64_t pf_v = 0;
     uint32_t spins = 0;
     for (;;) {
       if (ld_acq(&s_stop)) {   // rollback: park until wave 0 has repaired the state, then resume at s_reserved
@@ -624,15 +661,18 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
         while (ld_acq(&s_stop) && !ld_acq(&s_finish)) sp_sleep();
         q = ld_acq(&s_reserved);
         topo_id = -1;
+        pf_q = -1;
         continue;
       }
       if (ld_acq(&s_finish)) break;
       if (q >= ld_acq(&s_decided) || ld_acq(&s_cut_at) >= 0) {
         if (++spins > SP_SPIN_LIMIT) break;
         sp_sleep();
+        SPM(6);
         continue;
       }
       spins = 0;
+      SPM(6);
       const DecRec d = dec[q];
       const PodVec& pk = pods(q);
       if (d.flags & SP_FITERR) {
@@ -648,12 +688,13 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
       const int slot = d.slot;
       const uint32_t winner = (uint32_t)d.winner;
       const bool fresh = d.flags & SP_FRESH;
-      if (fresh) {   // fetch the row: one load per lane, then LDS
-        int64_t vv = 0;
-        if (f_kind == 1) vv = reinterpret_cast<const int64_t*>(f_src)[winner];
-        else if (f_kind == 2) vv = reinterpret_cast<const int32_t*>(f_src)[winner];
-        else if (f_kind == 3) vv = (int64_t)reinterpret_cast<const uint8_t*>(f_src)[(size_t)q * a.ld + (winner - a.own0)];
-        else if (f_kind == 4) vv = (int64_t)winner;
+      if (fresh) {   // the row: one load per lane (issued one pod ahead when pod q was already decided), then LDS
+        const int64_t vv = pf_q == q ? pf_v : fetch(q, winner);
+        pf_q = -1;
+        if (q + 1 < ld_acq(&s_decided)) {   // prefetch the next pod's fresh winner row
+          const DecRec& dn = dec[q + 1];
+          if ((dn.flags & (SP_FRESH | SP_FITERR)) == SP_FRESH) { pf_v = fetch(q + 1, (uint32_t)dn.winner); pf_q = q + 1; }
+        }
         if (f_kind) {
           unsigned char* dst = f_region == 0 ? reinterpret_cast<unsigned char*>(&drows[slot])
                              : f_region == 1 ? reinterpret_cast<unsigned char*>(&cst[slot])
@@ -773,27 +814,11 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
           rescored[q] = 1;
         }
       } else {
-        const int tb = q % SP_TABLES;
-        // the table's previous user (pod q - SP_TABLES) must be done
-        bool stop = false;
-        if (q >= SP_TABLES) {
-          while (!ld_acq(&rescored[q - SP_TABLES])) {
-            if (ld_acq(&s_stop) || ld_acq(&s_finish)) { stop = true; break; }
-            sp_sleep();
-          }
-        }
-        if (!stop) {
-          const Row rr = dr_;
-          if (numa_on && ((rr.nr.nflags >> NF_POLICY_SHIFT) & 3u)) hint_table_fill(tables[tb], rr.nr, zone_avail(rr.nr), lane);
-          WAVE_FENCE();
-          if (lane == 0) {
-            jobs_left[q] = njobs;
-            int t = s_jq_tail;
-            for (int j = 0; j < njobs; ++j, ++t) jobq[t % SP_JOBQ] = Job{slot, q, j, tb};
-            __atomic_store_n(&s_jq_tail, t, __ATOMIC_RELEASE);
-          }
-        } else {
-          // rollback began while this pod waited: it will be undone (its undo record is logged)
+        if (lane == 0) {
+          jobs_left[q] = njobs;
+          int t = s_jq_tail;
+          for (int j = 0; j < njobs; ++j, ++t) jobq[t % SP_JOBQ] = Job{slot, q, j, 0};
+          __atomic_store_n(&s_jq_tail, t, __ATOMIC_RELEASE);
         }
       }
       WAVE_FENCE();
@@ -803,6 +828,7 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
       }
       WAVE_FENCE();
       ++q;
+      SPM(5);
     }
   } else {
     // ============================================== re-scoring jobs ==============================================
@@ -826,13 +852,18 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
       if (h < 0) {
         if (++spins > SP_SPIN_LIMIT) break;
         sp_sleep();
+        SPM(8);
         continue;
       }
       spins = 0;
+      SPM(8);
       const Job jb = jobq[h % SP_JOBQ];
       const Row rr = drows[jb.slot];
+      HintTable& tab = tables[wv - 2];
+      if (numa_on && ((rr.nr.nflags >> NF_POLICY_SHIFT) & 3u)) hint_table_fill(tab, rr.nr, zone_avail(rr.nr), lane);
+      WAVE_FENCE();
       const int q2 = jb.q + 1 + jb.range * 64 + lane;
-      if (q2 < B) dsc[q2 * B + jb.slot] = (int16_t)row_score(rr, pods(q2), a.pf, m, &tables[jb.tbl]);
+      if (q2 < B) dsc[q2 * B + jb.slot] = (int16_t)row_score(rr, pods(q2), a.pf, m, &tab);
       WAVE_FENCE();
       if (lane == 0) {
         if (__atomic_fetch_sub(&jobs_left[jb.q], 1, __ATOMIC_ACQ_REL) == 1) {
@@ -841,6 +872,7 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
         }
       }
       WAVE_FENCE();
+      SPM(7);
     }
   }
   __syncthreads();
@@ -864,6 +896,10 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
       else m.c32(C_CPU_META)[node] = (int32_t)cst[sl].meta;
     }
   for (int i = tid; i < committed; i += SP_THREADS) a.out[i].feasible = (uint32_t)final_F[i];
+  if (ST && lane == 0)
+    for (int i = 0; i < 15; ++i)
+      if (st_acc[i]) atomicAdd(reinterpret_cast<unsigned long long*>(&a.stamps[i]), (unsigned long long)st_acc[i]);
+#undef SPM
   if (tid == 0) {
     a.committed[0] = committed;
     a.committed[1] = (committed == B && !s_hostcut && !s_err) ? 1 : 0;
@@ -873,13 +909,19 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
 }
 
 hipError_t launch_commit_spec(const CommitArgs& a, hipStream_t st) {
-  hipLaunchKernelGGL(commit_spec_kernel, dim3(1), dim3(SP_THREADS), spec_smem_bytes(a.npods), st, a);
+  if (a.stamps)
+    hipLaunchKernelGGL(commit_spec_kernel<true>, dim3(1), dim3(SP_THREADS), spec_smem_bytes(a.npods), st, a);
+  else
+    hipLaunchKernelGGL(commit_spec_kernel<false>, dim3(1), dim3(SP_THREADS), spec_smem_bytes(a.npods), st, a);
   return hipGetLastError();
 }
 
 hipError_t set_commit_spec_attributes() {
-  return hipFuncSetAttribute(reinterpret_cast<const void*>(commit_spec_kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
-                             (int)spec_smem_bytes(MAX_BATCH));
+  hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(commit_spec_kernel<false>),
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)spec_smem_bytes(MAX_BATCH));
+  if (e != hipSuccess) return e;
+  return hipFuncSetAttribute(reinterpret_cast<const void*>(commit_spec_kernel<true>),
+                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)spec_smem_bytes(MAX_BATCH));
 }
 
 }  // namespace gs

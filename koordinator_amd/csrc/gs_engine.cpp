@@ -240,7 +240,8 @@ struct Thr {
   uint32_t mask = 0;
 };
 
-bool usage_exceeds(const Thr& th, const Vec2& used, const gs_node& n) {
+// 0: within the thresholds; else 1 + the first exceeding resource in the order cpu, memory
+int usage_exceeds(const Thr& th, const Vec2& used, const gs_node& n) {
   for (int r = 0; r < 2; ++r) {
     if (!(th.mask & (1u << r)) || th.v[r] == 0) continue;
     int64_t total = estimate_node(n, r);
@@ -248,9 +249,9 @@ bool usage_exceeds(const Thr& th, const Vec2& used, const gs_node& n) {
     int64_t u = used.get(r);
     double mu = (double)(r == 0 ? u : u * 1000), mt = (double)(r == 0 ? total : total * 1000);
     int64_t pct = (int64_t)std::round(mu / mt * 100);   // load_aware.go:214,248
-    if (pct >= th.v[r]) return true;
+    if (pct >= th.v[r]) return 1 + r;
   }
-  return false;
+  return 0;
 }
 
 struct LaDerived {
@@ -296,7 +297,8 @@ LaDerived derive_loadaware(const gs_loadaware_args& a, const HostNode& hn) {
   if (m.exists && th.mask && m.has_node_metric) {
     Vec2 u;
     bool have = has_agg ? target_agg(m, agg_dur, agg_type, &u) : (u = usage_of(m.node_usage), true);
-    if (have && usage_exceeds(th, u, n)) d.sflags |= SF_FAIL_NP;
+    const int ex = have ? usage_exceeds(th, u, n) : 0;
+    if (ex) d.sflags |= SF_FAIL_NP | (ex == 2 ? SF_NP_MEM : 0u) | (has_agg ? SF_NP_AGG : 0u);
   }
   // prod verdict: filterProdUsage (load_aware.go:226-254)
   if (prod.mask) {
@@ -309,7 +311,8 @@ LaDerived derive_loadaware(const gs_loadaware_args& a, const HostNode& hn) {
       for (const auto& kv : pm)
         for (int r = 0; r < 2; ++r)
           if (kv.second.has(r)) sum.add(r, kv.second.v[r]);
-      if (usage_exceeds(prod, sum, n)) d.sflags |= SF_FAIL_P;
+      const int ex = usage_exceeds(prod, sum, n);
+      if (ex) d.sflags |= SF_FAIL_P | (ex == 2 ? SF_P_MEM : 0u);
     }
   }
   // ---- Score-side usage (load_aware.go:291-327, 337-376), for both prodPod modes
@@ -687,10 +690,10 @@ void set_shard(gs_ctx* c) {
   c->stats.shard_end = c->n1;
 }
 
-// one rank's exchange block: [B x LCAP listed node ids | B LevelHdr], padded to 256 B
+// one rank's exchange block: [B x LCAP listed node ids | B LevelHdr | B LevelExt], padded to 256 B
 size_t lists_bytes(int B) { return (size_t)B * LCAP * 4; }
 size_t xchg_block_bytes(int B) {
-  size_t raw = lists_bytes(B) + (size_t)B * sizeof(LevelHdr);
+  size_t raw = lists_bytes(B) + (size_t)B * (sizeof(LevelHdr) + sizeof(LevelExt));
   return (raw + 255) / 256 * 256;
 }
 
@@ -760,6 +763,7 @@ CommitArgs commit_args(gs_ctx* c, int b) {
 int launch_batch(gs_ctx* c, int b, const int32_t* prev, const PlacementDev* prev_out = nullptr, int prev_b = 0) {
   uint32_t* d_lists = reinterpret_cast<uint32_t*>(c->d_xchg_send);
   LevelHdr* d_hdrs = reinterpret_cast<LevelHdr*>(c->d_xchg_send + lists_bytes(c->B));
+  LevelExt* d_ext = reinterpret_cast<LevelExt*>(c->d_xchg_send + lists_bytes(c->B) + (size_t)c->B * sizeof(LevelHdr));
   int prod_cols = 0;
   for (int i = 0; i < b; ++i) prod_cols |= (c->h_pods[i].flags & PF_PROD_SCORE) ? 1 : 0;
   uint32_t len = c->n1 - c->n0;
@@ -791,7 +795,7 @@ int launch_batch(gs_ctx* c, int b, const int32_t* prev, const PlacementDev* prev
     HIP_TRY(c, launch_patch(c->mv, c->d_pods, b, c->pf, c->n0, c->n1, c->d_S, c->ld, prod_cols, c->d_aff, prev_out, prev,
                             prev_b, c->st));
   if (!c->window_k)   // node sampling selects over the rotation window, not the candidate levels
-    HIP_TRY(c, launch_cand(c->d_S, c->ld, len, c->n0, b, c->max_score, d_lists, d_hdrs, c->st));
+    HIP_TRY(c, launch_cand(c->d_S, c->ld, len, c->n0, b, c->max_score, d_lists, d_hdrs, d_ext, c->st));
   HIP_TRY(c, hipEventRecord(c->ev[2], c->st));
   if (c->nranks > 1) {
     int rc = exchange(c, c->d_xchg_send, c->d_xchg_recv, c->xchg_bytes);
@@ -1109,6 +1113,24 @@ int gs_create(const gs_config* cfg, gs_ctx** out) {
 
 int gs_destroy(gs_ctx* c) {
   if (!c) return GS_EINVAL;
+  if (c->d_stamps) {
+    uint64_t st[32] = {};
+    if (hipMemcpy(st, c->d_stamps, 256, hipMemcpyDeviceToHost) == hipSuccess) {
+      static const char* kind = getenv("GS_COMMIT_KERNEL");
+      if (c->nranks == 1 && !(kind && kind[0] == 'p') && !c->window_k) {   // speculative commit kernel
+        const double np = c->stats_all_pods ? (double)c->stats_all_pods : 1.0;
+        fprintf(stderr, "gpuscore spec commit, cycles per committed pod (%llu pods): decide %.0f verify %.0f wave0-wait %.0f "
+                "rollback %.0f (%llu rollbacks) | Reserve busy %.0f wait %.0f | re-scoring busy %.0f wait %.0f (6 waves) | "
+                "decisions %llu, full-row %llu (%.0f cycles each; M<0 %llu, M>=0 %llu) | wave 0 total %.0f\n",
+                (unsigned long long)c->stats_all_pods, st[0] / np, st[1] / np, st[2] / np, st[4] / np,
+                (unsigned long long)st[3], st[5] / np, st[6] / np, st[7] / np, st[8] / np, (unsigned long long)st[9],
+                (unsigned long long)st[10], st[10] ? (double)st[11] / st[10] : 0.0, (unsigned long long)st[13],
+                (unsigned long long)st[14], st[12] / np);
+        (void)hipFree(c->d_stamps);
+        c->d_stamps = nullptr;
+      }
+    }
+  }
   if (c->d_stamps) {
     uint64_t st[32] = {};
     if (hipMemcpy(st, c->d_stamps, 256, hipMemcpyDeviceToHost) == hipSuccess) {
@@ -1568,6 +1590,27 @@ int gs_synchronize(gs_ctx* c) {
   if (!c) return GS_EINVAL;
   HIP_TRY(c, hipStreamSynchronize(c->st_ev));
   HIP_TRY(c, hipStreamSynchronize(c->st));
+  return GS_OK;
+}
+
+// Device-error recovery (a GPU error becomes framework.Error, then the mirror is rebuilt from the
+// host snapshot): drain the streams, re-derive every node row from the host state into HBM, re-run node prep.
+int gs_reset(gs_ctx* c) {
+  if (!c) return GS_EINVAL;
+  (void)hipStreamSynchronize(c->st);
+  (void)hipStreamSynchronize(c->st_ev);
+  (void)hipStreamSynchronize(c->st2);
+  (void)hipGetLastError();
+  for (uint32_t i = 0; i < c->N; ++i)
+    if (c->nodes[i].valid) mark_dirty(c, i);
+  c->numa_idx_stale = true;
+  int rc = flush_rows(c);
+  if (rc) return rc;
+  if ((rc = node_prep(c))) return rc;
+  hipError_t e = hipStreamSynchronize(c->st);
+  if (e != hipSuccess) return fail(c, GS_EDEVICE, "reset: the device is unusable (%s): destroy and recreate the context",
+                                   hipGetErrorString(e));
+  c->err.clear();
   return GS_OK;
 }
 

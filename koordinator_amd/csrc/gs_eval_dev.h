@@ -148,8 +148,9 @@ __device__ __forceinline__ PairOut eval_pair(const Row& r, const PodVec& p, cons
   }
   // ---- LoadAware.Filter (load_aware.go:123-171), usage verdicts precomputed per node
   if ((pf.enabled & 0x4u) && !(p.flags & PF_DAEMONSET)) {
-    uint32_t bit = (p.flags & PF_PROD) ? DF_LA_FAIL_P : DF_LA_FAIL_NP;
-    if (r.dflags & bit) o.code |= 0x20u;
+    const bool prod = p.flags & PF_PROD;
+    if (r.dflags & (prod ? DF_LA_FAIL_P : DF_LA_FAIL_NP))   // + the reason's resource / aggregated form
+      o.code |= 0x20u | ((r.dflags >> (prod ? DF_P_DETAIL_SHIFT : DF_NP_DETAIL_SHIFT)) & 3u) << 10;
   }
   if (!FULL && o.code) return o;
   // ---- NodeNUMAResource Filter (+ Admit) and Score (gs_numa_dev.h)

@@ -44,6 +44,18 @@ struct LevelHdr {
 };
 static_assert(sizeof(LevelHdr) == 80, "LevelHdr layout");
 
+// Levels 8.. of the same summary (up to LEVALL levels in all; the lists hold their nodes after level 7's): read by
+// the speculative commit kernel, whose pods then find k+1 listed nodes without the full-row path (C3: the top 8
+// levels hold a median of 14 nodes, the top 24 at least 136).
+constexpr int LEVALL = 32, LEVX = LEVALL - MAXLEV;
+struct LevelExt {
+  int32_t nlev;              // listed levels in all (<= LEVALL)
+  int32_t next;              // highest score of a feasible node that is NOT listed (-1: none)
+  int32_t score[LEVX];       // levels MAXLEV.. (descending; -1 past nlev)
+  int32_t count[LEVX];
+};
+static_assert(sizeof(LevelExt) == 200, "LevelExt layout");
+
 struct PlacementDev {   // gs_placement + the NodeNUMAResource Reserve the device applied / the host must apply
   int32_t node;
   uint32_t feasible;
@@ -68,7 +80,8 @@ struct CommitArgs {
   int npods;
   int nranks;
   uint32_t shard_size;       // ceil(N / nranks): shard of node i = i / shard_size
-  const uint8_t* xbase;      // rank r block at xbase + r*xblock: [npods_max x LCAP u32 lists | LevelHdr x npods_max]
+  const uint8_t* xbase;      // rank r block at xbase + r*xblock: [npods_max x LCAP u32 lists | LevelHdr x npods_max |
+                             //  LevelExt x npods_max]
   size_t xblock;
   int bmax;                  // pods per block layout (lists/hdrs are laid out for bmax pods)
   Profile pf;
@@ -111,7 +124,7 @@ hipError_t launch_patch(const MirrorView& m, const PodVec* pods, int npods, cons
 hipError_t launch_eval_full(const MirrorView& m, const PodVec* pods, int npods, const Profile& pf, uint32_t N,
                             int16_t* scores, uint16_t* codes, int16_t* plugin, int prod_cols, hipStream_t st);
 hipError_t launch_cand(const int16_t* S, uint32_t ld, uint32_t len, uint32_t n0, int npods, int max_score,
-                       uint32_t* lists, LevelHdr* hdrs, hipStream_t st);
+                       uint32_t* lists, LevelHdr* hdrs, LevelExt* ext, hipStream_t st);
 size_t commit_smem_bytes(int B);
 hipError_t launch_commit(const CommitArgs& a, hipStream_t st);        // window_k > 0: lockstep kernel
 hipError_t launch_commit_pipe(const CommitArgs& a, hipStream_t st);   // pipelined roles (gs_commit.hip)

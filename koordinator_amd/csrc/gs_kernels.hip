@@ -34,8 +34,13 @@ __global__ void __launch_bounds__(256) node_prep_kernel(MirrorView m, uint32_t n
   bool skip_filter = !exists || (filter_expired && has_exp && expired);
   uint32_t df = 0;
   if (!skip_filter) {
-    if (sf & SF_FAIL_NP) df |= DF_LA_FAIL_NP;
-    if ((sf & SF_PROD_THR) ? (sf & SF_FAIL_P) : (sf & SF_FAIL_NP)) df |= DF_LA_FAIL_P;
+    const uint32_t npd = ((sf & SF_NP_MEM) ? 1u : 0u) | ((sf & SF_NP_AGG) ? 2u : 0u);   // reason details
+    if (sf & SF_FAIL_NP) df |= DF_LA_FAIL_NP | npd << DF_NP_DETAIL_SHIFT;
+    if (sf & SF_PROD_THR) {
+      if (sf & SF_FAIL_P) df |= DF_LA_FAIL_P | (((sf & SF_P_MEM) ? 1u : 0u) << DF_P_DETAIL_SHIFT);
+    } else if (sf & SF_FAIL_NP) {
+      df |= DF_LA_FAIL_P | npd << DF_P_DETAIL_SHIFT;
+    }
   }
   if (!exists || (has_exp && expired)) df |= DF_LA_ZERO;
   m.c32(C_DFLAGS)[i] = (int32_t)df;
@@ -140,7 +145,7 @@ __global__ void __launch_bounds__(256) eval_full_kernel(MirrorView m, const PodV
 template <int W>
 __global__ void __launch_bounds__(64 * W) cand_kernel(const int16_t* __restrict__ S, uint32_t ld, uint32_t len,
                                                       uint32_t n0, int max_score, uint32_t* __restrict__ lists,
-                                                      LevelHdr* __restrict__ hdrs) {
+                                                      LevelHdr* __restrict__ hdrs, LevelExt* __restrict__ ext) {
   constexpr int CAND_THREADS = 64 * W;
   extern __shared__ __align__(16) uint32_t smem[];
   const int nbins = max_score + 1;
@@ -149,8 +154,8 @@ __global__ void __launch_bounds__(64 * W) cand_kernel(const int16_t* __restrict_
   int8_t* slot_of = reinterpret_cast<int8_t*>(comb + nbins);     // [nbins]
   __shared__ uint32_t segsum[CAND_THREADS];
   __shared__ uint32_t s_total;
-  __shared__ LevelHdr s_hdr;
-  __shared__ uint32_t s_woff[W][MAXLEV];
+  __shared__ int32_t s_nlev, s_next, s_score[LEVALL], s_count[LEVALL];
+  __shared__ uint32_t s_woff[W][LEVALL];
   const int k = blockIdx.x;
   const int t = threadIdx.x, wave = t >> 6, lane = t & 63;
   const int16_t* row = S + (size_t)k * ld;
@@ -191,10 +196,7 @@ __global__ void __launch_bounds__(64 * W) cand_kernel(const int16_t* __restrict_
     // levels from the top until the pod's position in the batch is covered: pod k can find at most k of
     // the listed nodes dirtied by earlier pods, so k+1 listed nodes always leave a clean one.
     const uint32_t target = (uint32_t)k + 1;
-    LevelHdr h;
-    h.nlev = 0;
-    h.feasible = (int32_t)s_total;
-    h.next = -1;
+    int nlev = 0, next = -1;
     uint32_t cum = 0;
     bool stop = false;
     for (int sg = CAND_THREADS - 1; sg >= 0 && !stop; --sg) {
@@ -202,72 +204,86 @@ __global__ void __launch_bounds__(64 * W) cand_kernel(const int16_t* __restrict_
       for (int b = min(nbins, (sg + 1) * per) - 1; b >= sg * per; --b) {
         uint32_t c = comb[b];
         if (!c) continue;
-        if (h.nlev == MAXLEV || cum + c > (uint32_t)LCAP || cum >= target) {
-          h.next = b;
+        if (nlev == LEVALL || cum + c > (uint32_t)LCAP || cum >= target) {
+          next = b;
           stop = true;
           break;
         }
-        h.score[h.nlev] = b;
-        h.count[h.nlev] = (int32_t)c;
-        slot_of[b] = (int8_t)h.nlev;
-        ++h.nlev;
+        s_score[nlev] = b;
+        s_count[nlev] = (int32_t)c;
+        slot_of[b] = (int8_t)nlev;
+        ++nlev;
         cum += c;
       }
     }
-    for (int j = h.nlev; j < MAXLEV; ++j) { h.score[j] = -1; h.count[j] = 0; }
-    h.total = (int32_t)cum;
-    s_hdr = h;
+    for (int j = nlev; j < LEVALL; ++j) { s_score[j] = -1; s_count[j] = 0; }
+    s_nlev = nlev;
+    s_next = next;
   }
   __syncthreads();
-  const int nlev = s_hdr.nlev;
-  if (t < W * MAXLEV) {
-    int w = t / MAXLEV, j = t % MAXLEV;
+  const int nlev = s_nlev;
+  for (int e = t; e < W * LEVALL; e += CAND_THREADS) {
+    const int w = e / LEVALL, j = e % LEVALL;
     uint32_t off = 0;
     if (j < nlev) {
-      for (int jj = 0; jj < j; ++jj) off += s_hdr.count[jj];
-      for (int ww = 0; ww < w; ++ww) off += whist[ww * nbins + s_hdr.score[j]];
+      for (int jj = 0; jj < j; ++jj) off += s_count[jj];
+      for (int ww = 0; ww < w; ++ww) off += whist[ww * nbins + s_score[j]];
     }
     s_woff[w][j] = off;
   }
   __syncthreads();
-  // pass 2: order-preserving compaction of the listed levels (node order = (lane, element) order)
+  // pass 2: order-preserving compaction of the listed levels (node order = (lane, element) order), level by level
+  // over the levels present in each 512-node step
   uint32_t* out = lists + (size_t)k * LCAP;
   if (nlev > 0) {
-    uint32_t run[MAXLEV];
-#pragma unroll
-    for (int j = 0; j < MAXLEV; ++j) run[j] = s_woff[wave][j];
+    uint32_t run_l = lane < LEVALL ? s_woff[wave][lane] : 0;   // level `lane`'s next output position (this wave)
     for (uint32_t base = wb; base < we; base += 512) {
       int4 q = row4[(base + lane * 8) / 8];
       const int16_t* e = reinterpret_cast<const int16_t*>(&q);
       int slot[8];
-      bool any = false;
+      uint32_t present = 0;
 #pragma unroll
       for (int x = 0; x < 8; ++x) {
         slot[x] = e[x] >= 0 ? slot_of[e[x]] : -1;
-        any |= slot[x] >= 0;
+        if (slot[x] >= 0) present |= 1u << slot[x];
       }
-      if (!__ballot(any)) continue;
-#pragma unroll
-      for (int j = 0; j < MAXLEV; ++j) {
-        if (j >= nlev) break;
+      // levels present anywhere in the step (OR over the wave)
+      uint32_t pw = present;
+      for (int o = 1; o < 64; o <<= 1) pw |= (uint32_t)__shfl_xor((int)pw, o);
+      for (; pw; pw &= pw - 1) {
+        const int j = __ffs(pw) - 1;
         int c = 0;
 #pragma unroll
         for (int x = 0; x < 8; ++x) c += slot[x] == j;
-        if (!__ballot(c > 0)) continue;
         int incl = c;
         for (int o = 1; o < 64; o <<= 1) {
           int v = __shfl_up(incl, o);
           if (lane >= o) incl += v;
         }
-        int pos = run[j] + incl - c;
+        int pos = (int)__shfl((int)run_l, j) + incl - c;
 #pragma unroll
         for (int x = 0; x < 8; ++x)
           if (slot[x] == j) out[pos++] = n0 + base + lane * 8 + x;
-        run[j] += __shfl(incl, 63);
+        const int tot = __shfl(incl, 63);
+        if (lane == j) run_l += tot;
       }
     }
   }
-  if (t == 0) hdrs[k] = s_hdr;
+  if (t == 0) {
+    LevelHdr h;
+    h.nlev = nlev < MAXLEV ? nlev : MAXLEV;
+    h.feasible = (int32_t)s_total;
+    h.next = nlev > MAXLEV ? s_score[MAXLEV] : s_next;
+    int32_t tot = 0;
+    for (int j = 0; j < MAXLEV; ++j) { h.score[j] = s_score[j]; h.count[j] = s_count[j]; tot += s_count[j]; }
+    h.total = tot;
+    hdrs[k] = h;
+    LevelExt x;
+    x.nlev = nlev;
+    x.next = s_next;
+    for (int j = 0; j < LEVX; ++j) { x.score[j] = s_score[MAXLEV + j]; x.count[j] = s_count[MAXLEV + j]; }
+    ext[k] = x;
+  }
 }
 
 int64_t host_tiebreak_position(uint64_t seed, uint64_t seq, int64_t T) { return tiebreak_position(seed, seq, T); }
@@ -1155,13 +1171,13 @@ static size_t cand_smem_bytes(int max_score, int waves) {
 static bool cand_wide(int max_score) { return false && cand_smem_bytes(max_score, 16) <= 48 * 1024; }
 
 hipError_t launch_cand(const int16_t* S, uint32_t ld, uint32_t len, uint32_t n0, int npods, int max_score,
-                       uint32_t* lists, LevelHdr* hdrs, hipStream_t st) {
+                       uint32_t* lists, LevelHdr* hdrs, LevelExt* ext, hipStream_t st) {
   if (cand_wide(max_score))
     hipLaunchKernelGGL(cand_kernel<16>, dim3(npods), dim3(1024), cand_smem_bytes(max_score, 16), st, S, ld, len, n0,
-                       max_score, lists, hdrs);
+                       max_score, lists, hdrs, ext);
   else
     hipLaunchKernelGGL(cand_kernel<4>, dim3(npods), dim3(256), cand_smem_bytes(max_score, 4), st, S, ld, len, n0,
-                       max_score, lists, hdrs);
+                       max_score, lists, hdrs, ext);
   return hipGetLastError();
 }
 
@@ -1176,7 +1192,7 @@ size_t commit_smem_bytes(int B) {
 hipError_t launch_commit(const CommitArgs& a, hipStream_t st) {
   static const bool lockstep = getenv("GS_COMMIT_LOCKSTEP") && getenv("GS_COMMIT_LOCKSTEP")[0] == '1';
   static const char* kind = getenv("GS_COMMIT_KERNEL");   // "pipe": the non-speculative pipelined kernel
-  const bool spec_ok = !(kind && kind[0] == 'p') && !a.stamps && a.nranks == 1 && a.S != nullptr;
+  const bool spec_ok = !(kind && kind[0] == 'p') && a.nranks == 1 && a.S != nullptr;
   if (!a.window_k && !lockstep && spec_ok) return launch_commit_spec(a, st);
   if (!a.window_k && !lockstep) return launch_commit_pipe(a, st);
   if (a.stamps)

@@ -92,12 +92,17 @@ enum : uint32_t {
   SF_FAIL_P = 1u << 3,        // filterProdUsage -> Unschedulable (load_aware.go:226-254)
   SF_PROD_THR = 1u << 4,      // len(filterProfile.ProdUsageThresholds) > 0
   SF_VALID = 1u << 5,         // row populated
+  SF_NP_MEM = 1u << 6,        // SF_FAIL_NP names memory (else cpu)
+  SF_NP_AGG = 1u << 7,        // SF_FAIL_NP comes from the aggregated-usage profile
+  SF_P_MEM = 1u << 8,         // SF_FAIL_P names memory
 };
 // C_DFLAGS bits
 enum : uint32_t {
   DF_LA_FAIL_NP = 1u << 0,    // LoadAware.Filter fails a non-Prod (or DaemonSet-free) pod
   DF_LA_FAIL_P = 1u << 1,     // LoadAware.Filter fails a Prod pod
   DF_LA_ZERO = 1u << 2,       // LoadAware.Score returns 0 (metric missing / expired)
+  DF_NP_DETAIL_SHIFT = 3,     // 2 bits: GS_FAIL_LA_MEMORY / GS_FAIL_LA_AGGREGATED >> 10 of the non-Prod verdict
+  DF_P_DETAIL_SHIFT = 5,      // 2 bits: the same for the Prod verdict
 };
 
 // per-pod vector (PreFilter output), 128 B

@@ -171,6 +171,10 @@ class Engine:
     def reset_stats(self):
         self._chk(lib().gs_reset_stats(self._h), "gs_reset_stats")
 
+    def reset(self):
+        """Rebuild the HBM mirror from the host state after a failed call (gs_reset)."""
+        self._chk(lib().gs_reset(self._h), "gs_reset")
+
     def synchronize(self):
         self._chk(lib().gs_synchronize(self._h), "gs_synchronize")
 

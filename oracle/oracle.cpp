@@ -292,9 +292,11 @@ int64_t least_requested_score(int64_t requested, int64_t capacity) {
 
 // ---- loadaware/load_aware.go -----------------------------------------------------------------
 
-// filterNodeUsage (load_aware.go:173-224); returns true on Unschedulable
-bool filter_node_usage(const NodeState& s, const FilterProfile& p) {
-  if (!s.metric.has_node_metric) return false;
+// filterNodeUsage (load_aware.go:173-224); returns 0 or the GS_FAIL_LOADAWARE code with the reason's details
+// (the resource named in "node(s) %s usage exceed threshold", the aggregated form); resources are visited in
+// the fixed order cpu, memory (the reference ranges over a Go map: with both over, the named one is unpinned)
+uint32_t filter_node_usage(const NodeState& s, const FilterProfile& p) {
+  if (!s.metric.has_node_metric) return 0;
   const Thresholds& th = p.has_agg ? p.agg : p.usage;
   for (int r = 0; r < 2; ++r) {
     if (!(th.mask & (1u << r))) continue;
@@ -310,14 +312,15 @@ bool filter_node_usage(const NodeState& s, const FilterProfile& p) {
     }
     int64_t used = usage.get(r);
     int64_t pct = (int64_t)std::round((double)milli_value(r, used) / (double)milli_value(r, total) * 100);
-    if (pct >= threshold) return true;
+    if (pct >= threshold)
+      return GS_FAIL_LOADAWARE | (r == 1 ? GS_FAIL_LA_MEMORY : 0u) | (p.has_agg ? GS_FAIL_LA_AGGREGATED : 0u);
   }
-  return false;
+  return 0;
 }
 
 // filterProdUsage (load_aware.go:226-254)
-bool filter_prod_usage(const NodeState& s, const Thresholds& prod) {
-  if (s.pods_metric.empty()) return false;
+uint32_t filter_prod_usage(const NodeState& s, const Thresholds& prod) {
+  if (s.pods_metric.empty()) return 0;
   auto pm = build_pod_metric_map(s, true);
   ResList prod_usages, unused;
   sum_pod_usages(pm, nullptr, &prod_usages, &unused);
@@ -329,24 +332,24 @@ bool filter_prod_usage(const NodeState& s, const Thresholds& prod) {
     if (total == 0) continue;
     int64_t used = prod_usages.get(r);
     int64_t pct = (int64_t)std::round((double)milli_value(r, used) / (double)milli_value(r, total) * 100);
-    if (pct >= threshold) return true;
+    if (pct >= threshold) return GS_FAIL_LOADAWARE | (r == 1 ? GS_FAIL_LA_MEMORY : 0u);
   }
-  return false;
+  return 0;
 }
 
-// Plugin.Filter (load_aware.go:123-171); true = Unschedulable
-bool loadaware_filter(const or_cluster& c, const gs_pod& pod, const NodeState& s) {
+// Plugin.Filter (load_aware.go:123-171); 0 or the GS_FAIL_LOADAWARE code (Unschedulable) with its details
+uint32_t loadaware_filter(const or_cluster& c, const gs_pod& pod, const NodeState& s) {
   const gs_loadaware_args& a = c.cfg.loadaware;
-  if (pod.flags & GS_POD_DAEMONSET) return false;
-  if (!s.metric.exists) return false;  // NotFound: skip the node (load_aware.go:138-140)
+  if (pod.flags & GS_POD_DAEMONSET) return 0;
+  if (!s.metric.exists) return 0;  // NotFound: skip the node (load_aware.go:138-140)
   if (a.filter_expired_node_metrics && a.has_node_metric_expiration &&
       is_node_metric_expired(s, a.node_metric_expiration_seconds, c.now))
-    return false;
+    return 0;
   FilterProfile p = filter_profile(s.node, a);
   if (p.prod.mask != 0 && pod.priority_class == GS_PRIO_PROD) return filter_prod_usage(s, p.prod);
   const Thresholds& th = p.has_agg ? p.agg : p.usage;
   if (th.mask != 0) return filter_node_usage(s, p);
-  return false;
+  return 0;
 }
 
 // estimatedAssignedPodUsed (load_aware.go:337-376)
@@ -503,7 +506,7 @@ PairResult eval_pair(const or_cluster& c, const gs_pod& pod, const orn::PreState
   PairResult res{0, 0, 0, 0};
   uint32_t en = c.cfg.enabled;
   if (en & GS_ENABLE_FIT_FILTER) res.code |= (uint16_t)fit_filter(pod, s.node);
-  if ((en & GS_ENABLE_LA_FILTER) && loadaware_filter(c, pod, s)) res.code |= GS_FAIL_LOADAWARE;
+  if (en & GS_ENABLE_LA_FILTER) res.code |= loadaware_filter(c, pod, s);
   orn::Hint aff;
   if (en & GS_ENABLE_NUMA_FILTER) res.code |= numa_filter(c, st, i, &aff);
   if (en & GS_ENABLE_FIT_SCORE) res.fit = fit_score(c.cfg.fit, pod, s.node);
@@ -924,7 +927,7 @@ int or_schedule_replay(or_cluster* c, const gs_pod* pods, uint32_t npods, const 
       const NodeState& s = c->nodes[selected];
       uint16_t code = 0;
       if (c->cfg.enabled & GS_ENABLE_FIT_FILTER) code |= (uint16_t)fit_filter(pod, s.node);
-      if ((c->cfg.enabled & GS_ENABLE_LA_FILTER) && loadaware_filter(*c, pod, s)) code |= GS_FAIL_LOADAWARE;
+      if (c->cfg.enabled & GS_ENABLE_LA_FILTER) code |= loadaware_filter(*c, pod, s);
       affinity[selected] = orn::Hint{};
       if (!code && (c->cfg.enabled & GS_ENABLE_NUMA_FILTER))
         code |= numa_filter(*c, st, (uint32_t)selected, &affinity[selected]);
@@ -935,7 +938,7 @@ int or_schedule_replay(or_cluster* c, const gs_pod* pods, uint32_t npods, const 
       const NodeState& s = c->nodes[n];
       uint16_t code = 0;
       if (c->cfg.enabled & GS_ENABLE_FIT_FILTER) code |= (uint16_t)fit_filter(pod, s.node);
-      if ((c->cfg.enabled & GS_ENABLE_LA_FILTER) && loadaware_filter(*c, pod, s)) code |= GS_FAIL_LOADAWARE;
+      if (c->cfg.enabled & GS_ENABLE_LA_FILTER) code |= loadaware_filter(*c, pod, s);
       affinity[n] = orn::Hint{};
       if (!code && (c->cfg.enabled & GS_ENABLE_NUMA_FILTER)) code |= numa_filter(*c, st, (uint32_t)n, &affinity[n]);
       feasible[n] = code == 0;

@@ -105,24 +105,27 @@ filter_usage = [
      "metric": metric(node_usage=usage("60", "256Gi")), "want_fail": False},
     {"src": f"{LA}:302-306", "name": "filter node missing NodeMetrics", "metric": None, "want_fail": False},
     {"src": f"{LA}:307-333", "name": "filter exceed cpu usage",
-     "metric": metric(node_usage=usage("70", "256Gi")), "want_fail": True},
+     "metric": metric(node_usage=usage("70", "256Gi")), "want_fail": True,
+     "want_msg": "node(s) cpu usage exceed threshold"},
     {"src": f"{LA}:334-380", "name": "filter exceed p95 cpu usage",
      "args": {"aggregated": {"usageThresholds": {"cpu": 60}, "usageAggregationType": "p95",
                              "usageAggregatedDurationSeconds": 300}},
      "metric": metric(node_usage=usage("30", "100Gi"),
                       aggregated=[{"duration_s": 300, "usage": {"p95": usage("70", "256Gi")}}]),
-     "want_fail": True},
+     "want_fail": True, "want_msg": "node(s) cpu aggregated usage exceed threshold"},
     {"src": f"{LA}:381-407", "name": "filter exceed memory usage",
-     "metric": metric(node_usage=usage("30", "500Gi")), "want_fail": True},
+     "metric": metric(node_usage=usage("30", "500Gi")), "want_fail": True,
+     "want_msg": "node(s) memory usage exceed threshold"},
     {"src": f"{LA}:408-437", "name": "filter exceed memory usage by custom usage thresholds",
      "custom": {"usageThresholds": {"memory": 60}},
-     "metric": metric(node_usage=usage("30", "316Gi")), "want_fail": True},
+     "metric": metric(node_usage=usage("30", "316Gi")), "want_fail": True,
+     "want_msg": "node(s) memory usage exceed threshold"},
     {"src": f"{LA}:438-482", "name": "filter exceed p95 cpu usage by custom usage",
      "custom": {"aggregatedUsage": {"usageThresholds": {"cpu": 60}, "usageAggregationType": "p95",
                                     "usageAggregatedDurationSeconds": 300}},
      "metric": metric(node_usage=usage("30", "100Gi"),
                       aggregated=[{"duration_s": 300, "usage": {"p95": usage("70", "256Gi")}}]),
-     "want_fail": True},
+     "want_fail": True, "want_msg": "node(s) cpu aggregated usage exceed threshold"},
     {"src": f"{LA}:483-509", "name": "disable filter exceed memory usage",
      "args": {"usageThresholds": {"memory": 0}},
      "metric": metric(node_usage=usage("30", "500Gi")), "want_fail": False},
@@ -133,21 +136,22 @@ filter_usage = [
     {"src": f"{LA}:557-609", "name": "filter prod cpu usage",
      "args": {"usageThresholds": {"cpu": 100, "memory": 100}, "prodUsageThresholds": {"cpu": 50, "memory": 100}},
      "metric": metric(node_usage=usage("63", "500Gi"), pods_metric=PROD_METRICS),
-     "lister": PROD_PODS, "pod": PROD_TEST_POD, "want_fail": True},
+     "lister": PROD_PODS, "pod": PROD_TEST_POD, "want_fail": True, "want_msg": "node(s) cpu usage exceed threshold"},
     {"src": f"{LA}:610-662", "name": "filter prod memory usage",
      "args": {"usageThresholds": {"cpu": 100, "memory": 100}, "prodUsageThresholds": {"cpu": 100, "memory": 50}},
      "metric": metric(node_usage=usage("63", "500Gi"), pods_metric=PROD_METRICS),
-     "lister": PROD_PODS, "pod": PROD_TEST_POD, "want_fail": True},
+     "lister": PROD_PODS, "pod": PROD_TEST_POD, "want_fail": True, "want_msg": "node(s) memory usage exceed threshold"},
     {"src": f"{LA}:663-719", "name": "filter prod memory usage with custom usage configuration",
      "args": {"usageThresholds": {"cpu": 100, "memory": 100}, "prodUsageThresholds": {"cpu": 100, "memory": 100}},
      "custom": {"prodUsageThresholds": {"cpu": 100, "memory": 50}},
      "metric": metric(node_usage=usage("63", "500Gi"), pods_metric=PROD_METRICS),
-     "lister": PROD_PODS, "pod": PROD_TEST_POD, "want_fail": True},
+     "lister": PROD_PODS, "pod": PROD_TEST_POD, "want_fail": True, "want_msg": "node(s) memory usage exceed threshold"},
     {"src": f"{LA}:720-746", "name": "filter daemonset pod exceed cpu usage",
      "metric": metric(node_usage=usage("70", "256Gi")),
      "pod": {"namespace": "default", "name": "test-pod", "priority": 9999, "daemonset": True},
      "want_fail": False},
 ]
+# want_msg: the wantStatus message of the case (load_aware_test.go:335,383,411,442,490,642,705,772)
 for case in filter_usage:   # TestFilterUsage runs with FilterExpiredNodeMetrics = false (:748)
     case.setdefault("args", {})["filterExpiredNodeMetrics"] = False
 

@@ -91,3 +91,33 @@ def test_pod_decoding_quantities():
     be = objects.make_pod({"containers": [{}]})
     assert be["priority_class"] == abi.GS_PRIO_BATCH   # BestEffort -> BE -> Batch
     assert list(be["nonzero_requests"]) == [100, 200 << 20]
+
+
+def test_reason_strings():
+    """gs_reason_string renders the reference's Filter statuses: NodeNUMAResource's Err* constants
+    (nodenumaresource/plugin.go:48-55) and the reasons of util.go:117, topology_hint.go:36, manager.go:70,
+    resource_manager.go:292, with their framework codes; upstream Fit reasons joined like Status.Message()."""
+    S = abi.GS_FAIL_NUMA_SHIFT
+    want = {
+        abi.GS_NUMA_INVALID_REQUESTED_CPUS: (2, "the requested CPUs must be integer"),
+        abi.GS_NUMA_INVALID_AMP_RATIO: (2, "node(s) invalid CPU amplification ratio"),
+        abi.GS_NUMA_AVAILABLE_CPUS_ERROR: (2, "node(s) invalid CPU Topology"),
+        abi.GS_NUMA_INSUFFICIENT_AMP_CPU: (1, "Insufficient amplified cpu"),
+        abi.GS_NUMA_INVALID_TOPOLOGY: (2, "node(s) invalid CPU Topology"),
+        abi.GS_NUMA_BIND_POLICY_CONFLICT: (2, "node(s) cpu bind policy conflicts with pod's required cpu bind policy"),
+        abi.GS_NUMA_SMT_ALIGNMENT: (2, "node(s) requested cpus not multiple cpus per core"),
+        abi.GS_NUMA_ALLOCATE_FAILED: (1, "not enough cpus available to satisfy request"),
+        abi.GS_NUMA_MISSING_NUMA_RESOURCES: (2, "node(s) missing NUMA resources"),
+        abi.GS_NUMA_AFFINITY_ERROR: (1, "node(s) NUMA Topology affinity error"),
+    }
+    for r, w in want.items():
+        assert abi.reason_string(r << S) == w, r
+    assert abi.reason_string(0) == (0, "")
+    assert abi.reason_string(abi.GS_FAIL_FIT_CPU | abi.GS_FAIL_FIT_MEMORY | abi.GS_FAIL_LOADAWARE) == \
+        (1, "Insufficient cpu, Insufficient memory")           # the first failing plugin only
+    assert abi.reason_string(abi.GS_FAIL_FIT_PODS) == (1, "Too many pods")
+    assert abi.reason_string(abi.GS_FAIL_FIT_SCALAR, 1 << 3) == (1, "Insufficient kubernetes.io/batch-cpu")
+    assert abi.reason_string(abi.GS_FAIL_LOADAWARE | abi.GS_FAIL_LA_MEMORY) == (1, "node(s) memory usage exceed threshold")
+    assert abi.reason_string(abi.GS_FAIL_LOADAWARE | abi.GS_FAIL_LA_AGGREGATED) == \
+        (1, "node(s) cpu aggregated usage exceed threshold")
+    assert abi.reason_string(1 << 15)[0] < 0 and abi.reason_string(abi.GS_FAIL_LA_MEMORY)[0] < 0

@@ -226,3 +226,18 @@ def test_two_ranks_on_one_gpu_callback_transport():
         for f in ("node", "score", "ties", "feasible"):
             assert np.array_equal(res[r][f], want[f]), (r, f)
     assert engines[0].stats()["shard_end"] == engines[1].stats()["shard_begin"]
+
+
+def test_reset_rebuilds_mirror():
+    """gs_reset (device-error recovery) rebuilds the HBM mirror from the host state: scheduling continues
+    bit-exact with the oracle."""
+    c = synth.make_cluster(1500, 256, 1)
+    synth.make_numa(c)
+    e, o = pair(c, enabled=abi.GS_ENABLE_ALL)
+    seq = np.arange(256, dtype=np.uint64)
+    got1, want1 = e.schedule(c.pods[:128], seq[:128]), o.schedule(c.pods[:128], seq[:128])
+    e.reset()
+    assert e.mirror_check() == 0
+    got2, want2 = e.schedule(c.pods[128:], seq[128:]), o.schedule(c.pods[128:], seq[128:])
+    for f in ("node", "score", "ties", "feasible"):
+        assert np.array_equal(np.concatenate([got1[f], got2[f]]), np.concatenate([want1[f], want2[f]])), f

@@ -32,3 +32,13 @@ def test_loadaware_filter(case):
 def test_loadaware_score(case):
     eng, pod = gu.build(case, orc.Oracle)
     assert eng.loadaware_score(pod, 0) == case["want"], case["src"]
+
+
+@pytest.mark.parametrize("case", [c for c in G["filter_usage"] if c.get("want_msg")], ids=lambda c: c["name"])
+def test_loadaware_filter_reason(case):
+    """The failure code's reason text (gs_reason_string over the oracle's code) is the wantStatus message of the
+    reference test (load_aware_test.go), and Unschedulable."""
+    eng, pod = gu.build(case, orc.Oracle)
+    _, codes, _ = eng.evaluate(np.array([pod], abi.POD_DTYPE))
+    st, msg = abi.reason_string(int(codes[0, 0]))
+    assert (st, msg) == (1, case["want_msg"]), case["src"]
