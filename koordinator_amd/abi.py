@@ -38,6 +38,7 @@ CPU_BIND = {"": 0, "Default": 1, "FullPCPUs": 2, "SpreadByPCPUs": 3, "Constraine
 CPU_EXCLUSIVE = {"": 0, "None": 0, "PCPULevel": 1, "NUMANodeLevel": 2}
 NODE_CPU_BIND = {"": 0, "None": 0, "FullPCPUsOnly": 1, "SpreadByPCPUs": 2}
 NUMA_POLICY = {"": 0, "BestEffort": 1, "Restricted": 2, "SingleNUMANode": 3}
+GS_NUMA_POLICY_NONE, GS_NUMA_POLICY_BEST_EFFORT, GS_NUMA_POLICY_RESTRICTED, GS_NUMA_POLICY_SINGLE_NUMA_NODE = 0, 1, 2, 3
 NUMA_ALLOC = {"": 0, "MostAllocated": 1, "LeastAllocated": 2, "DistributeEvenly": 3}
 GS_SCORING_LEAST_ALLOCATED, GS_SCORING_MOST_ALLOCATED = 0, 1
 GS_FAIL_NUMA_SHIFT, GS_FAIL_NUMA_MASK = 6, 0x3C0

@@ -75,6 +75,8 @@ struct gs_ctx {
   uint32_t window_k = 0;                    // node sampling: numFeasibleNodesToFind(N) (0 = every node)
   uint32_t next_start = 0;                  // [upstream] Scheduler.nextStartNodeIndex
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+  std::vector<hipEvent_t> x_ev;             // RCCL all-gather start / end events not yet accounted (exchange_ms)
+  int x_pending = 0;
   // device mirror
   int64_t* d_i64 = nullptr;
   int32_t* d_i32 = nullptr;
@@ -530,11 +532,35 @@ int ready(gs_ctx* c) {
   return GS_OK;
 }
 
+double ev_ms(hipEvent_t a, hipEvent_t b) {
+  float ms = 0;
+  if (hipEventElapsedTime(&ms, a, b) != hipSuccess) return 0;
+  return ms;
+}
+
+// exchange_ms of RCCL all-gathers: completion time from events around each collective on the stream, added up
+// once the batch's work has completed (finish_batch)
+void flush_exchange_times(gs_ctx* c) {
+  for (int i = 0; i < c->x_pending; ++i) c->stats.exchange_ms += ev_ms(c->x_ev[2 * i], c->x_ev[2 * i + 1]);
+  c->x_pending = 0;
+}
+
 int exchange(gs_ctx* c, const void* d_send, void* d_recv, size_t bytes) {
   auto t0 = std::chrono::steady_clock::now();
   if (c->comm) {
+    if (c->x_pending * 2 + 2 > (int)c->x_ev.size()) {
+      for (int k = 0; k < 2; ++k) {
+        hipEvent_t ev;
+        HIP_TRY(c, hipEventCreate(&ev));
+        c->x_ev.push_back(ev);
+      }
+    }
+    HIP_TRY(c, hipEventRecord(c->x_ev[2 * c->x_pending], c->st));
     ncclResult_t r = ncclAllGather(d_send, d_recv, bytes, ncclUint8, c->comm, c->st);
     if (r != ncclSuccess) return fail(c, GS_ECOMM, "ncclAllGather: %s", ncclGetErrorString(r));
+    HIP_TRY(c, hipEventRecord(c->x_ev[2 * c->x_pending + 1], c->st));
+    ++c->x_pending;
+    return GS_OK;
   } else if (c->cb) {
     if (bytes > c->xchg_bytes) return fail(c, GS_EINVAL, "exchange payload too large");
     HIP_TRY(c, hipMemcpyAsync(c->h_xchg_send, d_send, bytes, hipMemcpyDeviceToHost, c->st));
@@ -706,11 +732,6 @@ int alloc_exchange(gs_ctx* c) {
   return GS_OK;
 }
 
-double ev_ms(hipEvent_t a, hipEvent_t b) {
-  float ms = 0;
-  if (hipEventElapsedTime(&ms, a, b) != hipSuccess) return 0;
-  return ms;
-}
 
 void bind_slot(gs_ctx* c, int s) {
   const gs_ctx::Slot& x = c->slot[s];
@@ -817,6 +838,7 @@ int launch_batch(gs_ctx* c, int b, const int32_t* prev, const PlacementDev* prev
 int finish_batch(gs_ctx* c, int b, bool clobbered, int* committed_out) {
   uint32_t len = c->n1 - c->n0;
   HIP_TRY(c, hipEventSynchronize(c->ev[5]));
+  flush_exchange_times(c);
   c->stats.eval_ms += ev_ms(c->ev[0], c->ev[1]);
   c->stats.cand_ms += ev_ms(c->ev[1], c->ev[2]);
   c->stats.commit_ms += ev_ms(c->ev[3], c->ev[4]);
@@ -898,6 +920,7 @@ int finish_batch(gs_ctx* c, int b, bool clobbered, int* committed_out) {
     HIP_TRY(c, hipMemcpyAsync(c->h_out, c->d_out, sizeof(PlacementDev) * committed, hipMemcpyDeviceToHost, c->st));
     HIP_TRY(c, hipStreamSynchronize(c->st));
   }
+  flush_exchange_times(c);
   if (committed < b) {
     c->stats.cuts += 1;
     static const bool dbg = getenv("GS_DEBUG_CUTS") && getenv("GS_DEBUG_CUTS")[0] == '1';
@@ -1153,6 +1176,7 @@ int gs_destroy(gs_ctx* c) {
     (void)hipFree(c->d_stamps);
   }
   if (c->comm) ncclCommDestroy(c->comm);
+  for (hipEvent_t ev : c->x_ev) (void)hipEventDestroy(ev);
   if (c->st) (void)hipStreamSynchronize(c->st);
   if (c->st_ev) (void)hipStreamSynchronize(c->st_ev);
   if (c->slot[0].d_pods) bind_slot(c, 0);

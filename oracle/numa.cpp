@@ -980,10 +980,9 @@ Hint merge_filtered(uint64_t def, const std::vector<std::vector<Hint>>& lists) {
 }
 
 // policy.Merge -> (best, admit)
-bool policy_merge(int policy, const std::vector<int>& numa_nodes, const HintsMap& hm, bool reverse, Hint* best) {
-  uint64_t def = 0;
-  for (int id : numa_nodes) def |= 1ull << id;
-  auto filtered = filter_providers(hm, reverse);
+// the policy's Merge over filterProvidersHints' lists (policy_best_effort.go:43-48, policy_restricted.go:42-47,
+// policy_single_numa_node.go:48-78): the merged hint; the admit verdict
+bool policy_merge_filtered(int policy, uint64_t def, std::vector<std::vector<Hint>> filtered, Hint* best) {
   if (policy == GS_NUMA_POLICY_SINGLE_NUMA_NODE) {   // policy_single_numa_node.go:48-78
     for (auto& l : filtered) {
       std::vector<Hint> keep;
@@ -1000,6 +999,12 @@ bool policy_merge(int policy, const std::vector<int>& numa_nodes, const HintsMap
   *best = merge_filtered(def, filtered);
   if (policy == GS_NUMA_POLICY_RESTRICTED) return best->preferred;   // policy_restricted.go:42-47
   return true;                                                       // policy_best_effort.go:43-48
+}
+
+bool policy_merge(int policy, const std::vector<int>& numa_nodes, const HintsMap& hm, bool reverse, Hint* best) {
+  uint64_t def = 0;
+  for (int id : numa_nodes) def |= 1ull << id;
+  return policy_merge_filtered(policy, def, filter_providers(hm, reverse), best);
 }
 
 }  // namespace
@@ -1159,3 +1164,34 @@ int reserve(const NumaArgs& a, const PreState& st, NodeNUMA& n, const gs_pod& po
 }
 
 }  // namespace orn
+
+// ---- test entry: the topology-manager Merge over explicit hint lists (policy_test.go vectors) ----------------
+// lists as filterProvidersHints produced them: nlists lists, list i holding lens[i] hints (has_mask, mask,
+// preferred) taken in order from the flat arrays. Returns the admit verdict; *out = the merged hint.
+extern "C" int or_policy_merge(int policy, uint64_t numa_mask, int nlists, const int32_t* lens, const uint8_t* has_mask,
+                               const uint64_t* masks, const uint8_t* preferred, uint8_t* out_has_mask,
+                               uint64_t* out_mask, uint8_t* out_preferred) {
+  if (policy == GS_NUMA_POLICY_NONE) {   // policy_none.go:40-42: an empty hint, admitted
+    *out_has_mask = 0; *out_mask = 0; *out_preferred = 0;
+    return 1;
+  }
+  std::vector<std::vector<orn::Hint>> lists(nlists);
+  int k = 0;
+  for (int i = 0; i < nlists; ++i)
+    for (int j = 0; j < lens[i]; ++j, ++k) lists[i].push_back(orn::Hint{has_mask[k] != 0, masks[k], preferred[k] != 0, 0});
+  orn::Hint best;
+  const bool admit = orn::policy_merge_filtered(policy, numa_mask, lists, &best);
+  *out_has_mask = best.has_mask ? 1 : 0;
+  *out_mask = best.has_mask ? best.mask : 0;
+  *out_preferred = best.preferred ? 1 : 0;
+  return admit ? 1 : 0;
+}
+
+// bitmask.IterateBitMasks (bitmask.go:206-222): the masks of every non-empty subset of `bits` in visit order
+extern "C" int or_iterate_bitmasks(const int32_t* bits, int nbits, uint64_t* out, int cap) {
+  std::vector<int> b(bits, bits + nbits);
+  int n = 0;
+  orn::iterate_bitmasks(b, [&](uint64_t m) { if (n < cap) out[n] = m; ++n; });
+  return n;
+}
+

@@ -54,6 +54,8 @@ def _load() -> C.CDLL:
         "or_numa_allocation_get": (C.c_int, [P, C.c_uint32, C.c_uint64, P]),
         "or_set_hint_order": (C.c_int, [P, C.c_int]),
         "or_take_cpus_test": (C.c_int, [C.c_int] * 5 + [P, P, P] + [C.c_int] * 4 + [P]),
+        "or_policy_merge": (C.c_int, [C.c_int, C.c_uint64, C.c_int, P, P, P, P, P, P, P]),
+        "or_iterate_bitmasks": (C.c_int, [P, C.c_int, P, C.c_int]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -263,3 +265,29 @@ def take_cpus_test(topology, max_ref, available, alloc_ref, alloc_excl, needed, 
                                  int(needed), int(bind), int(excl), int(strategy), abi.ptr(out))
     cpus = [c for c in range(256) if (int(out[c >> 6]) >> (c & 63)) & 1]
     return rc == 0, cpus
+
+
+def policy_merge(policy: int, numa_nodes, lists) -> tuple[dict, bool]:
+    """topologymanager Policy.Merge over filterProvidersHints' lists (each a list of {"mask": bits|None,
+    "preferred": bool}) -> (merged hint, admit)."""
+    lens = np.array([len(l) for l in lists], np.int32)
+    flat = [h for l in lists for h in l]
+    has = np.array([h["mask"] is not None for h in flat], np.uint8)
+    masks = np.array([sum(1 << b for b in (h["mask"] or [])) for h in flat], np.uint64)
+    pref = np.array([bool(h["preferred"]) for h in flat], np.uint8)
+    oh, om, op = np.zeros(1, np.uint8), np.zeros(1, np.uint64), np.zeros(1, np.uint8)
+    nm = sum(1 << b for b in numa_nodes)
+    admit = lib().or_policy_merge(policy, nm, len(lists), lens.ctypes.data, has.ctypes.data, masks.ctypes.data,
+                                  pref.ctypes.data, oh.ctypes.data, om.ctypes.data, op.ctypes.data)
+    bits = [b for b in range(64) if int(om[0]) >> b & 1] if oh[0] else None
+    return {"mask": bits, "preferred": bool(op[0])}, bool(admit)
+
+
+def iterate_bitmasks(bits) -> list[int]:
+    """bitmask.IterateBitMasks visit order (masks as integers)."""
+    b = np.array(bits, np.int32)
+    n = lib().or_iterate_bitmasks(b.ctypes.data, len(b), None, 0)
+    out = np.zeros(max(n, 1), np.uint64)
+    lib().or_iterate_bitmasks(b.ctypes.data, len(b), out.ctypes.data, n)
+    return [int(x) for x in out[:n]]
+
