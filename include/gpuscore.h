@@ -424,6 +424,114 @@ int gs_numa_allocation_get(gs_ctx* ctx, uint32_t node, uint64_t uid, gs_pod_allo
 /* v1beta2.SetDefaults_NodeNUMAResourceArgs (defaults.go:101-136) */
 void gs_numa_args_default(gs_numa_args* a);
 
+/* ---- Reservation + DeviceShare ----
+ * The two plugins of the shipped profile that normalize their scores (config/manager/scheduler-config.yaml:80-89:
+ * DeviceShare weight 1, Reservation weight 5000). Scope on the device path: GPU devices (the GPU device type of
+ * deviceshare/utils.go:47-56; no RDMA / FPGA, no joint allocation, no VF or PCIe hints, no device hint selectors);
+ * reservations holding cpu / memory / ephemeral / the scalar slots (no cpuset or device reservations, no host
+ * ports, no preemption nomination). A pod uses the extension path when it requests GPUs or matches a reservation
+ * (or requires one); it is then scheduled alone, through the normalizing select kernel. Every other pod keeps the
+ * batched path: for it both plugins score 0 everywhere (DefaultNormalizeScore keeps an all-zero list) and the
+ * reservations it does not match enter its NodeInfo through the unmatched restore, which the mirror rows carry. */
+enum gs_gpu_res { GS_GPU_CORE = 0, GS_GPU_MEMORY_RATIO = 1, GS_GPU_MEMORY = 2, GS_NUM_GPU_RES = 3 };
+/* pod / node resource names of the GPU device type (apis/extension/device_share.go; deviceshare/utils.go:47-56) */
+enum gs_gpu_name {
+  GS_GPU_NAME_NVIDIA = 0,        /* "nvidia.com/gpu" */
+  GS_GPU_NAME_KOORD_GPU = 1,     /* "koordinator.sh/gpu" */
+  GS_GPU_NAME_CORE = 2,          /* "koordinator.sh/gpu-core" */
+  GS_GPU_NAME_MEMORY = 3,        /* "koordinator.sh/gpu-memory" (bytes) */
+  GS_GPU_NAME_MEMORY_RATIO = 4,  /* "koordinator.sh/gpu-memory-ratio" */
+  GS_NUM_GPU_NAMES = 5
+};
+#define GS_MAX_GPUS 8
+
+typedef struct gs_gpu_device {     /* one GPU minor of the node's Device object (deviceshare/device_cache.go:38-56) */
+  int32_t minor;
+  int32_t has_info;                /* a DeviceInfo exists for the minor (filterNodeDevice, device_allocator.go:139-163) */
+  int64_t total[GS_NUM_GPU_RES];   /* deviceTotal[gpu][minor] (all zero: an unhealthy device) */
+  int64_t used[GS_NUM_GPU_RES];    /* deviceUsed[gpu][minor] */
+} gs_gpu_device;
+
+typedef struct gs_node_devices {
+  int32_t has_device;              /* nodeDeviceCache.getNodeDevice(node) != nil (else DeviceShare passes / scores 0) */
+  int32_t num_gpus;                /* <= GS_MAX_GPUS, distinct minors */
+  gs_gpu_device gpus[GS_MAX_GPUS];
+  int64_t allocatable[GS_NUM_GPU_NAMES];  /* NodeInfo.Allocatable.ScalarResources of the GPU names ([upstream] Fit) */
+  int64_t requested[GS_NUM_GPU_NAMES];    /* NodeInfo.Requested.ScalarResources of the GPU names */
+} gs_node_devices;
+
+enum gs_reservation_policy {       /* schedulingv1alpha1.ReservationAllocatePolicy */
+  GS_RSV_POLICY_DEFAULT = 0, GS_RSV_POLICY_ALIGNED = 1, GS_RSV_POLICY_RESTRICTED = 2
+};
+typedef struct gs_reservation {    /* frameworkext.ReservationInfo (frameworkext/reservation_info.go:80-115) */
+  uint64_t uid;
+  uint64_t owner_key;              /* ReservationInfo.Match(pod) <=> gs_pod_ext.reservation_owner == owner_key
+                                      (the caller evaluates the owner matchers; 0 matches no pod) */
+  uint32_t node;                   /* Status.NodeName as a node index */
+  int32_t allocate_policy;         /* gs_reservation_policy */
+  int64_t order;                   /* label scheduling.koordinator.sh/reservation-order parsed (0: absent or invalid) */
+  int32_t available;               /* IsAvailable() && ParseError == nil */
+  int32_t unschedulable;           /* IsUnschedulable() */
+  int32_t allocate_once;           /* IsAllocateOnce() */
+  int32_t assigned_pods;           /* len(AssignedPods) */
+  int64_t allocatable[GS_NUM_RES]; /* Allocatable = the reserve pod's requests (ReservationRequests) */
+  int64_t allocated[GS_NUM_RES];   /* Allocated */
+  uint32_t allocatable_mask;       /* keys of Allocatable */
+  uint32_t allocated_mask;         /* keys of Allocated */
+  uint32_t resource_names_mask;    /* ResourceNames (restricted options applied) */
+  uint32_t pad0;
+} gs_reservation;
+
+typedef struct gs_pod_ext {        /* per-pod inputs of the two plugins' PreFilter */
+  uint64_t reservation_owner;      /* owner key the pod presents to ReservationInfo.Match (0: none) */
+  int32_t reservation_required;    /* reservationutil.GetRequiredReservationAffinity(pod) != nil (hasAffinity) */
+  uint32_t gpu_request_mask;       /* bit n: PodRequestsAndLimits holds GPU name n with a non-zero value */
+  int64_t gpu_requests[GS_NUM_GPU_NAMES];
+} gs_pod_ext;
+
+#define GS_EXT_DEVICESHARE 0x1u    /* DeviceShare Filter + Score + Reserve */
+#define GS_EXT_RESERVATION 0x2u    /* Reservation BeforePreFilter restore + Filter + PreScore + Score + Reserve */
+typedef struct gs_ext_args {
+  uint32_t enabled;                /* GS_EXT_* */
+  int32_t device_scoring_type;     /* DeviceShareArgs.ScoringStrategy.Type (gs_scoring_type) */
+  int64_t device_weights[GS_NUM_GPU_RES]; /* ScoringStrategy.Resources over gpu-core, gpu-memory-ratio, gpu-memory
+                                             (v1beta2 default: gpu-memory-ratio = 1, defaults.go:187-203) */
+  int64_t weight_deviceshare;      /* profile score weights */
+  int64_t weight_reservation;
+} gs_ext_args;
+
+#define GS_EXT_FAIL_DEVICE 0x1000u      /* DeviceShare Filter: "Insufficient gpu devices" and the Prepare errors */
+#define GS_EXT_FAIL_RESERVATION 0x2000u /* Reservation Filter (reservation affinity: no satisfying reservation) */
+#define GS_EXT_FAIL_POD 0x4000u         /* the pod fails a PreFilter (invalid device request) on every node */
+
+typedef struct gs_ext_placement {
+  uint64_t reservation_uid;        /* the nominated reservation the pod was assumed into (0: none) */
+  uint32_t gpu_minor_mask;         /* GPU minors the DeviceShare Reserve allocated (bit = minor) */
+  int32_t gpu_count;
+  int64_t gpu_per_instance[GS_NUM_GPU_RES]; /* the DeviceAllocation.Resources of each minor */
+  int32_t deviceshare_score;       /* normalized plugin scores of the selected node (before weighting) */
+  int32_t reservation_score;
+  uint32_t fail_code;              /* a pod failing PreFilter: GS_EXT_FAIL_POD */
+  uint32_t pad0;
+} gs_ext_placement;
+
+/* v1beta2.SetDefaults_DeviceShareArgs (defaults.go:187-203) + the shipped profile weights */
+void gs_ext_args_default(gs_ext_args* a);
+int gs_ext_configure(gs_ctx* ctx, const gs_ext_args* args);
+/* Device informer (deviceshare/eventhandler_device.go): the node's GPU Device object + NodeInfo scalars. */
+int gs_node_devices_upsert(gs_ctx* ctx, const uint32_t* idx, const gs_node_devices* dev, uint32_t n);
+int gs_node_devices_get(gs_ctx* ctx, uint32_t node, gs_node_devices* out);
+/* Reservation informer (reservation/eventhandler.go, cache.go): add / update by uid, delete by uid. NodeInfo
+ * (gs_nodes_upsert) is the caller's snapshot and already holds the reserve pods. */
+int gs_reservations_upsert(gs_ctx* ctx, const gs_reservation* r, uint32_t n);
+int gs_reservations_remove(gs_ctx* ctx, const uint64_t* uids, uint32_t n);
+int gs_reservation_get(gs_ctx* ctx, uint64_t uid, gs_reservation* out);   /* 1 = found, 0 = none */
+/* gs_schedule with the Reservation / DeviceShare plugins: ext[i] (ext may be NULL: no pod uses them) holds pod i's
+ * plugin inputs; ext_out[i] (may be NULL) receives the reservation and GPU minors the Reserve assumed. Pods on the
+ * extension path need one rank and no node sampling (GS_EUNSUPPORTED otherwise). */
+int gs_schedule_ext(gs_ctx* ctx, const gs_pod* pods, const gs_pod_ext* ext, uint32_t npods, const uint64_t* seq,
+                    gs_placement* out, gs_ext_placement* ext_out);
+
 /* Multi-GPU: nodes are sharded in contiguous ranges [r*ceil(N/R), (r+1)*ceil(N/R)); every rank keeps the full
  * mirror (replicated deltas) and evaluates only its shard. Native RCCL over xGMI: */
 int gs_comm_unique_id(uint8_t out[128]);

@@ -207,6 +207,50 @@ class GsQuotaStatus(C.Structure):
                 ("used", i64 * GS_QUOTA_DIMS)]
 
 
+# ---- Reservation + DeviceShare ----
+GS_NUM_GPU_RES = 3
+GS_GPU_CORE, GS_GPU_MEMORY_RATIO, GS_GPU_MEMORY = 0, 1, 2
+GS_NUM_GPU_NAMES = 5
+GPU_NAMES = {"nvidia.com/gpu": 0, "koordinator.sh/gpu": 1, "koordinator.sh/gpu-core": 2,
+             "koordinator.sh/gpu-memory": 3, "koordinator.sh/gpu-memory-ratio": 4}
+GS_MAX_GPUS = 8
+RSV_POLICY = {"": 0, "Default": 0, "Aligned": 1, "Restricted": 2}
+GS_EXT_DEVICESHARE, GS_EXT_RESERVATION = 0x1, 0x2
+GS_EXT_FAIL_DEVICE, GS_EXT_FAIL_RESERVATION, GS_EXT_FAIL_POD = 0x1000, 0x2000, 0x4000
+
+
+class GsGpuDevice(C.Structure):
+    _fields_ = [("minor", i32), ("has_info", i32), ("total", i64 * GS_NUM_GPU_RES), ("used", i64 * GS_NUM_GPU_RES)]
+
+
+class GsNodeDevices(C.Structure):
+    _fields_ = [("has_device", i32), ("num_gpus", i32), ("gpus", GsGpuDevice * GS_MAX_GPUS),
+                ("allocatable", i64 * GS_NUM_GPU_NAMES), ("requested", i64 * GS_NUM_GPU_NAMES)]
+
+
+class GsReservation(C.Structure):
+    _fields_ = [("uid", u64), ("owner_key", u64), ("node", u32), ("allocate_policy", i32), ("order", i64),
+                ("available", i32), ("unschedulable", i32), ("allocate_once", i32), ("assigned_pods", i32),
+                ("allocatable", i64 * GS_NUM_RES), ("allocated", i64 * GS_NUM_RES), ("allocatable_mask", u32),
+                ("allocated_mask", u32), ("resource_names_mask", u32), ("pad0", u32)]
+
+
+class GsPodExt(C.Structure):
+    _fields_ = [("reservation_owner", u64), ("reservation_required", i32), ("gpu_request_mask", u32),
+                ("gpu_requests", i64 * GS_NUM_GPU_NAMES)]
+
+
+class GsExtArgs(C.Structure):
+    _fields_ = [("enabled", u32), ("device_scoring_type", i32), ("device_weights", i64 * GS_NUM_GPU_RES),
+                ("weight_deviceshare", i64), ("weight_reservation", i64)]
+
+
+class GsExtPlacement(C.Structure):
+    _fields_ = [("reservation_uid", u64), ("gpu_minor_mask", u32), ("gpu_count", i32),
+                ("gpu_per_instance", i64 * GS_NUM_GPU_RES), ("deviceshare_score", i32), ("reservation_score", i32),
+                ("fail_code", u32), ("pad0", u32)]
+
+
 ALLGATHER_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t)
 
 # numpy dtypes with the exact C layout (for bulk construction of node/pod arrays)
@@ -218,6 +262,10 @@ PLACEMENT_DTYPE = np.dtype(GsPlacement)
 TOPOLOGY_DTYPE = np.dtype(GsCpuTopology)
 NODE_NUMA_DTYPE = np.dtype(GsNodeNuma)
 POD_ALLOCATION_DTYPE = np.dtype(GsPodAllocation)
+NODE_DEVICES_DTYPE = np.dtype(GsNodeDevices)
+RESERVATION_DTYPE = np.dtype(GsReservation)
+POD_EXT_DTYPE = np.dtype(GsPodExt)
+EXT_PLACEMENT_DTYPE = np.dtype(GsExtPlacement)
 
 STRUCT_SIZES = {
     "gs_pod": C.sizeof(GsPod), "gs_node": C.sizeof(GsNode), "gs_node_metric": C.sizeof(GsNodeMetric),
@@ -226,7 +274,9 @@ STRUCT_SIZES = {
     "gs_loadaware_args": C.sizeof(GsLoadAwareArgs), "gs_cpu_topology": C.sizeof(GsCpuTopology),
     "gs_node_numa": C.sizeof(GsNodeNuma), "gs_pod_allocation": C.sizeof(GsPodAllocation),
     "gs_numa_args": C.sizeof(GsNumaArgs), "gs_quota_group": C.sizeof(GsQuotaGroup),
-    "gs_quota_status": C.sizeof(GsQuotaStatus),
+    "gs_quota_status": C.sizeof(GsQuotaStatus), "gs_node_devices": C.sizeof(GsNodeDevices),
+    "gs_reservation": C.sizeof(GsReservation), "gs_pod_ext": C.sizeof(GsPodExt), "gs_ext_args": C.sizeof(GsExtArgs),
+    "gs_ext_placement": C.sizeof(GsExtPlacement),
 }
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
@@ -280,6 +330,14 @@ SIGNATURES = {
     "gs_quota_reserve": (C.c_int, [P, u32, i32, P, u32, i32]),
     "gs_quota_admit_batch": (C.c_int, [P, u32, P, P, P, P, P, P, u32, P, C.POINTER(u32)]),
     "gs_quota_settle_batch": (C.c_int, [P, u32, P, P, P, P, P, P, u32, P, P]),
+    "gs_ext_args_default": (None, [C.POINTER(GsExtArgs)]),
+    "gs_ext_configure": (C.c_int, [P, C.POINTER(GsExtArgs)]),
+    "gs_node_devices_upsert": (C.c_int, [P, P, P, u32]),
+    "gs_node_devices_get": (C.c_int, [P, u32, C.POINTER(GsNodeDevices)]),
+    "gs_reservations_upsert": (C.c_int, [P, P, u32]),
+    "gs_reservations_remove": (C.c_int, [P, P, u32]),
+    "gs_reservation_get": (C.c_int, [P, u64, C.POINTER(GsReservation)]),
+    "gs_schedule_ext": (C.c_int, [P, P, P, u32, P, P, P]),
 }
 
 

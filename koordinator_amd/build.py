@@ -8,7 +8,9 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 OUT = os.path.join(HERE, "libgpuscore.so")
-SOURCES = ["gs_engine.cpp", "gs_numa_host.cpp", "gs_ingest.cpp", "gs_quota.cpp", "gs_reasons.cpp", "gs_kernels.hip", "gs_commit.hip", "gs_commit_spec.hip", "gs_probe.hip"]
+SOURCES = ["gs_engine.cpp", "gs_numa_host.cpp", "gs_ingest.cpp", "gs_quota.cpp", "gs_reasons.cpp", "gs_kernels.hip",
+           "gs_commit.hip", "gs_commit_spec.hip", "gs_probe.hip", "gs_ext.hip"]
+OBJ = os.path.join(HERE, "build")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off",
          "-fno-fast-math", "-Wall"]
@@ -22,10 +24,37 @@ def needs_build() -> bool:
     return any(os.path.getmtime(d) > t for d in deps)
 
 
+def _objects(force: bool, verbose: bool) -> list[str]:
+    """One object per source, compiled in parallel; a source is recompiled when it, or any header, is newer."""
+    from concurrent.futures import ThreadPoolExecutor
+    os.makedirs(OBJ, exist_ok=True)
+    hdrs = [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".h")]
+    hdrs.append(os.path.join(HERE, "..", "include", "gpuscore.h"))
+    newest_hdr = max(os.path.getmtime(h) for h in hdrs)
+    jobs, objs = [], []
+    for src in SOURCES:
+        sp = os.path.join(CSRC, src)
+        op = os.path.join(OBJ, src + ".o")
+        objs.append(op)
+        if force or not os.path.exists(op) or os.path.getmtime(op) < max(os.path.getmtime(sp), newest_hdr):
+            flags = [f for f in FLAGS if f != "-shared"]
+            jobs.append([HIPCC, *flags, "-c", "-o", op + ".tmp", sp])
+    def run(cmd):
+        if verbose:
+            print(" ".join(cmd), file=sys.stderr)
+        subprocess.check_call(cmd)
+        os.replace(cmd[cmd.index("-o") + 1], cmd[cmd.index("-o") + 1][:-4])
+    workers = max(1, min(len(jobs), int(os.environ.get("MAX_JOBS", "8"))))
+    with ThreadPoolExecutor(workers) as ex:
+        list(ex.map(run, jobs))
+    return objs
+
+
 def build(force: bool = False, verbose: bool = False) -> str:
     if not force and not needs_build():
         return OUT
-    cmd = [HIPCC, *FLAGS, "-o", OUT + ".tmp", *[os.path.join(CSRC, s) for s in SOURCES], "-L/opt/rocm/lib", "-lrccl"]
+    objs = _objects(force, verbose)
+    cmd = [HIPCC, "--offload-arch=gfx950", "-shared", "-fPIC", "-o", OUT + ".tmp", *objs, "-L/opt/rocm/lib", "-lrccl"]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.check_call(cmd)

@@ -15,12 +15,14 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <map>
 #include <string>
 #include <unordered_map>
 #include <unordered_set>
 #include <vector>
 
 #include "../../include/gpuscore.h"
+#include "gs_ext.h"
 #include "gs_kernels.h"
 #include "gs_numa_host.h"
 
@@ -158,6 +160,31 @@ struct gs_ctx {
   TopoDev* d_topos = nullptr;
   uint8_t* d_aff = nullptr;       // [pod][ld] Filter-time NUMA affinity of policy nodes (eval -> commit Reserve)
   bool verify_cpuset = false;
+  // Reservation + DeviceShare (gs_ext.hip): host mirror of the nodes' GPU devices and of the reservation cache
+  gs_ext_args ext{};
+  std::vector<gs_node_devices> devs;             // per node (has_device = 0: no Device object)
+  std::vector<uint8_t> dev_dirty;
+  std::vector<uint32_t> dev_dirty_list;
+  std::map<uint64_t, gs_reservation> rsv;        // reservationCache by uid (uid order = the harness's iteration order)
+  std::vector<std::vector<uint64_t>> rsv_node;   // uids per node, ascending
+  std::unordered_map<uint64_t, std::vector<uint64_t>> rsv_owner;   // owner key -> uids
+  DevNode* d_dev = nullptr;
+  ExtPod* d_xpod = nullptr;
+  ExtRec* d_xrec = nullptr;
+  ExtRes* d_xres = nullptr;
+  int32_t* d_xtot = nullptr;
+  int16_t* d_xds = nullptr;
+  int16_t* d_xrs = nullptr;
+  int32_t* d_xnom = nullptr;
+  int32_t* d_xT = nullptr;
+  ExtOut* d_xout = nullptr;
+  ExtPod* h_xpod = nullptr;
+  ExtOut* h_xout = nullptr;
+  int32_t* h_xnom = nullptr;
+  std::vector<ExtRec> xrec;
+  std::vector<ExtRes> xres;
+  std::vector<uint64_t> xres_uid;
+  uint32_t xrec_cap = 0, xres_cap = 0;
 };
 
 namespace {
@@ -381,8 +408,12 @@ LaDerived derive_loadaware(const gs_loadaware_args& a, const HostNode& hn) {
   return d;
 }
 
-void derive_row(const gs_ctx* c, const HostNode& hn, int64_t* row) {
-  const gs_node& n = hn.node;
+gs_node reservation_view(const gs_ctx* c, uint32_t i, uint64_t owner);
+
+void derive_row(const gs_ctx* c, uint32_t i, int64_t* row) {
+  const HostNode& hn = c->nodes[i];
+  // NodeInfo as a pod that matches none of the node's reservations sees it (reservation/transformer.go:266-292)
+  const gs_node n = reservation_view(c, i, 0);
   for (int s = 0; s < 7; ++s) {
     row[C_FREE_CPU + s] = n.allocatable[s] - n.requested[s];
     row[C_ALLOC_CPU + s] = n.allocatable[s];
@@ -402,6 +433,59 @@ void derive_row(const gs_ctx* c, const HostNode& hn, int64_t* row) {
   row[NUM_I64_COLS + C_FREE_PODS] = fp;
   row[NUM_I64_COLS + C_SFLAGS] = (int64_t)(d.sflags | (hn.valid ? SF_VALID : 0));
   row[NUM_I64_COLS + C_DFLAGS] = 0;
+}
+
+// ---- Reservation restore (reservation/transformer.go:50-292) on the host mirror ----------------------------------
+// A reservation enters a pod's NodeInfo in BeforePreFilter: available ones (IsAvailable, no parse error, not an
+// allocate-once reservation already used) that the pod matches are removed with their reserve pod (RemovePod); the
+// others with assigned pods are "unmatched" and trimmed to their remaining resources (updateNodeInfoRequested).
+bool rsv_usable(const gs_reservation& r) { return r.available && !(r.allocate_once && r.assigned_pods > 0); }
+bool rsv_matches(const gs_reservation& r, uint64_t owner) {
+  return owner != 0 && !r.unschedulable && r.owner_key == owner && rsv_usable(r);
+}
+
+// one-container pod requests -> (Requested delta per slot, NonZeroRequested delta): [upstream] calculateResource with
+// schedutil.GetNonzeroRequests (100m / 200Mi for an absent cpu / memory key)
+void rsv_request_delta(const int64_t* v, uint32_t mask, int64_t sign, int64_t* req, int64_t* nz) {
+  for (int s = 0; s < GS_NUM_RES; ++s)
+    if (mask >> s & 1u) req[s] += sign * v[s];
+  nz[0] += sign * ((mask & 1u) ? v[0] : 100);
+  nz[1] += sign * ((mask & 2u) ? v[1] : 200LL * 1024 * 1024);
+}
+// SubtractWithNonNegativeResult(Allocatable, Allocated): values and keys
+uint32_t rsv_remained(const gs_reservation& r, int64_t* rem) {
+  const uint32_t keys = r.allocatable_mask | r.allocated_mask;
+  for (int s = 0; s < GS_NUM_RES; ++s) {
+    const int64_t a = (r.allocatable_mask >> s & 1u) ? r.allocatable[s] : 0;
+    const int64_t u = (r.allocated_mask >> s & 1u) ? r.allocated[s] : 0;
+    rem[s] = (keys >> s & 1u) ? std::max<int64_t>(0, a - u) : 0;
+  }
+  return keys;
+}
+bool all_zero(const int64_t* v) {
+  for (int s = 0; s < GS_NUM_RES; ++s)
+    if (v[s]) return false;
+  return true;
+}
+// restoreUnmatchedReservations on a NodeInfo copy
+void rsv_trim_unmatched(const gs_reservation& r, gs_node& n) {
+  rsv_request_delta(r.allocatable, r.allocatable_mask, -1, n.requested, n.nonzero_requested);
+  int64_t rem[GS_NUM_RES];
+  const uint32_t keys = rsv_remained(r, rem);
+  if (!all_zero(rem)) rsv_request_delta(rem, keys, +1, n.requested, n.nonzero_requested);
+}
+
+// NodeInfo of node i as a pod with owner key `owner` sees it after the unmatched trim (podRequested; the matched
+// reservations are not removed here)
+gs_node reservation_view(const gs_ctx* c, uint32_t i, uint64_t owner) {
+  gs_node n = c->nodes[i].node;
+  if (c->rsv_node.empty() || !(c->ext.enabled & GS_EXT_RESERVATION)) return n;
+  for (uint64_t uid : c->rsv_node[i]) {
+    const gs_reservation& r = c->rsv.at(uid);
+    if (!rsv_usable(r) || rsv_matches(r, owner) || r.assigned_pods <= 0) continue;
+    rsv_trim_unmatched(r, n);
+  }
+  return n;
 }
 
 void derive_row_numa(const gs_ctx* c, uint32_t i, int64_t* row) {
@@ -503,7 +587,7 @@ int flush_rows(gs_ctx* c) {
     for (uint32_t j = 0; j < n; ++j) {
       uint32_t i = c->dirty_list[done + j];
       c->h_stage_idx[j] = i;
-      derive_row(c, c->nodes[i], c->h_stage_rows + (size_t)j * ROW_WORDS);
+      derive_row(c, i, c->h_stage_rows + (size_t)j * ROW_WORDS);
       derive_row_numa(c, i, c->h_stage_rows + (size_t)j * ROW_WORDS);
       c->row_dirty[i] = 0;
     }
@@ -938,6 +1022,362 @@ int finish_batch(gs_ctx* c, int b, bool clobbered, int* committed_out) {
   return GS_OK;
 }
 
+// ---- Reservation + DeviceShare: one extension pod (gs_ext.hip) ------------------------------------------------
+
+// GetPodDeviceRequests for the GPU type (deviceshare/utils.go:147-252): ValidateDeviceRequest + ConvertDeviceRequest.
+// 0: ok (mask 0 = no GPU request), -1: invalid (PreFilter UnschedulableAndUnresolvable)
+int gpu_request_of(const gs_pod_ext& e, int64_t req[3], uint32_t* mask) {
+  req[0] = req[1] = req[2] = 0;
+  *mask = 0;
+  const uint32_t m = e.gpu_request_mask & 0x1Fu;
+  if (!m) return 0;
+  for (int n : {GS_GPU_NAME_KOORD_GPU, GS_GPU_NAME_CORE, GS_GPU_NAME_MEMORY_RATIO})   // ValidatePercentageResource
+    if ((m >> n & 1u) && e.gpu_requests[n] > 100 && e.gpu_requests[n] % 100 != 0) return -1;
+  const int64_t* q = e.gpu_requests;
+  switch (m) {   // ValidDeviceResourceCombinations -> ResourceCombinationsMapper
+    case 1u << GS_GPU_NAME_NVIDIA: req[0] = req[1] = q[GS_GPU_NAME_NVIDIA] * 100; *mask = 3; return 0;
+    case 1u << GS_GPU_NAME_KOORD_GPU: req[0] = req[1] = q[GS_GPU_NAME_KOORD_GPU]; *mask = 3; return 0;
+    case 1u << GS_GPU_NAME_MEMORY: req[2] = q[GS_GPU_NAME_MEMORY]; *mask = 4; return 0;
+    case 1u << GS_GPU_NAME_MEMORY_RATIO: req[1] = q[GS_GPU_NAME_MEMORY_RATIO]; *mask = 2; return 0;
+    case (1u << GS_GPU_NAME_CORE) | (1u << GS_GPU_NAME_MEMORY):
+      req[0] = q[GS_GPU_NAME_CORE]; req[2] = q[GS_GPU_NAME_MEMORY]; *mask = 5; return 0;
+    case (1u << GS_GPU_NAME_CORE) | (1u << GS_GPU_NAME_MEMORY_RATIO):
+      req[0] = q[GS_GPU_NAME_CORE]; req[1] = q[GS_GPU_NAME_MEMORY_RATIO]; *mask = 3; return 0;
+    default: return -1;
+  }
+}
+
+DevNode dev_image(const gs_node_devices& d) {
+  DevNode o{};
+  o.has_device = d.has_device;
+  o.num_gpus = d.has_device ? d.num_gpus : 0;
+  for (int n = 0; n < GS_NUM_GPU_NAMES; ++n) o.fit_free[n] = d.allocatable[n] - d.requested[n];
+  for (int g = 0; g < o.num_gpus; ++g) {
+    o.g[g].minor = d.gpus[g].minor;
+    o.g[g].has_info = d.gpus[g].has_info;
+    for (int r = 0; r < 3; ++r) {
+      o.g[g].total[r] = d.gpus[g].total[r];
+      o.g[g].free[r] = std::max<int64_t>(0, d.gpus[g].total[r] - d.gpus[g].used[r]);
+    }
+  }
+  return o;
+}
+
+int ext_alloc(gs_ctx* c) {
+  if (c->d_dev) return GS_OK;
+  HIP_TRY(c, hipMalloc(&c->d_dev, sizeof(DevNode) * std::max<uint32_t>(1, c->N)));
+  std::vector<DevNode> img(c->N);
+  for (uint32_t i = 0; i < c->N; ++i) img[i] = dev_image(c->devs[i]);
+  HIP_TRY(c, hipMemcpy(c->d_dev, img.data(), sizeof(DevNode) * c->N, hipMemcpyHostToDevice));
+  c->dev_dirty_list.clear();
+  std::fill(c->dev_dirty.begin(), c->dev_dirty.end(), 0);
+  HIP_TRY(c, hipMalloc(&c->d_xpod, sizeof(ExtPod)));
+  HIP_TRY(c, hipMalloc(&c->d_xtot, 4 * (size_t)c->ld));
+  HIP_TRY(c, hipMalloc(&c->d_xT, 4 * (size_t)c->ld));
+  HIP_TRY(c, hipMalloc(&c->d_xds, 2 * (size_t)c->ld));
+  HIP_TRY(c, hipMalloc(&c->d_xrs, 2 * (size_t)c->ld));
+  HIP_TRY(c, hipMalloc(&c->d_xout, sizeof(ExtOut)));
+  HIP_TRY(c, hipHostMalloc(&c->h_xpod, sizeof(ExtPod), hipHostMallocDefault));
+  HIP_TRY(c, hipHostMalloc(&c->h_xout, sizeof(ExtOut), hipHostMallocDefault));
+  return GS_OK;
+}
+
+int ext_flush_devices(gs_ctx* c) {
+  if (c->dev_dirty_list.empty()) return GS_OK;
+  if (!c->d_dev) return ext_alloc(c);
+  for (uint32_t i : c->dev_dirty_list) {
+    const DevNode img = dev_image(c->devs[i]);
+    HIP_TRY(c, hipMemcpy(c->d_dev + i, &img, sizeof(DevNode), hipMemcpyHostToDevice));
+    c->dev_dirty[i] = 0;
+  }
+  c->dev_dirty_list.clear();
+  return GS_OK;
+}
+
+void dev_mark(gs_ctx* c, uint32_t i) {
+  if (!c->dev_dirty[i]) { c->dev_dirty[i] = 1; c->dev_dirty_list.push_back(i); }
+}
+
+// the pod's matched reservations grouped by node (node order, uid order within a node)
+void matched_of(const gs_ctx* c, uint64_t owner, std::vector<std::pair<uint32_t, uint64_t>>* out) {
+  out->clear();
+  if (!owner || !(c->ext.enabled & GS_EXT_RESERVATION)) return;
+  auto it = c->rsv_owner.find(owner);
+  if (it == c->rsv_owner.end()) return;
+  for (uint64_t uid : it->second) {
+    const gs_reservation& r = c->rsv.at(uid);
+    if (rsv_matches(r, owner)) out->push_back({r.node, uid});
+  }
+  std::sort(out->begin(), out->end());
+}
+
+bool is_ext_pod(const gs_ctx* c, const gs_pod_ext& e) {
+  if ((c->ext.enabled & GS_EXT_DEVICESHARE) && (e.gpu_request_mask & 0x1Fu)) return true;
+  if (!(c->ext.enabled & GS_EXT_RESERVATION)) return false;
+  if (e.reservation_required) return true;
+  std::vector<std::pair<uint32_t, uint64_t>> m;
+  matched_of(c, e.reservation_owner, &m);
+  return !m.empty();
+}
+
+// DeviceShare Reserve (deviceshare/plugin.go:377-430) on the host mirror: defaultAllocateDevices with the scorer
+// (device_allocator.go:397-467; minors by device score descending, then minor)
+int ext_device_reserve(gs_ctx* c, uint32_t node, const int64_t preq[3], uint32_t pmask, gs_ext_placement* eo) {
+  gs_node_devices& d = c->devs[node];
+  if (!d.has_device) return GS_OK;
+  const DevNode img = dev_image(d);
+  int64_t total_mem = -1;
+  for (int g = 0; g < img.num_gpus; ++g)
+    if (img.g[g].total[0] | img.g[g].total[1] | img.g[g].total[2]) { total_mem = img.g[g].total[2]; break; }
+  if (img.num_gpus <= 0 || total_mem < 0) return fail(c, GS_ESTATE, "DeviceShare Reserve: no GPU on node %u", node);
+  int64_t core = preq[0], ratio = preq[1], mem = preq[2];
+  if (pmask & 4u) ratio = (int64_t)((double)mem / (double)total_mem * 100.0);
+  else mem = ratio * total_mem / 100;
+  uint32_t m = pmask | 6u;
+  int64_t count = 1;
+  if (ratio > 100 && ratio % 100 == 0) { count = ratio / 100; core /= count; mem /= count; ratio /= count; m = 7u; }
+  const int64_t inst[3] = {core, ratio, mem};
+  struct Cand { int g; int64_t score; };
+  std::vector<Cand> cs;
+  for (int g = 0; g < img.num_gpus; ++g) {
+    if (!img.g[g].has_info) continue;
+    int64_t ns = 0, ws = 0;   // scoreDevice (deviceshare/scoring.go:186-211)
+    for (int r = 0; r < 3; ++r) {
+      const int64_t w = c->ext.device_weights[r], t = img.g[g].total[r], f = img.g[g].free[r];
+      if (!w || t == 0) continue;
+      int64_t rq = t;
+      if (t >= f) rq = t - f + ((m >> r & 1u) ? inst[r] : 0);
+      int64_t sc;
+      if (c->ext.device_scoring_type == GS_SCORING_MOST_ALLOCATED) sc = (std::min(rq, t) * 100) / t;
+      else sc = rq > t ? 0 : ((t - rq) * 100) / t;
+      ns += sc * w;
+      ws += w;
+    }
+    cs.push_back({g, ws ? ns / ws : 0});
+  }
+  std::stable_sort(cs.begin(), cs.end(), [&](const Cand& a, const Cand& b) {
+    if (a.score != b.score) return a.score > b.score;
+    return img.g[a.g].minor < img.g[b.g].minor;
+  });
+  std::vector<int> take;
+  for (const Cand& x : cs) {
+    const DevGpu& g = img.g[x.g];
+    if (!(g.free[0] | g.free[1] | g.free[2])) continue;
+    bool ok = true;
+    for (int r = 0; r < 3; ++r) ok &= !(m >> r & 1u) || inst[r] <= g.free[r];
+    if (!ok) continue;
+    take.push_back(x.g);
+    if ((int64_t)take.size() == count) break;
+  }
+  if ((int64_t)take.size() < count)
+    return fail(c, GS_ESTATE, "DeviceShare Reserve: allocation failed on node %u after a feasible Filter", node);
+  for (int g : take) {
+    for (int r = 0; r < 3; ++r)
+      if (m >> r & 1u) d.gpus[g].used[r] += inst[r];
+    eo->gpu_minor_mask |= 1u << (d.gpus[g].minor & 31);
+  }
+  eo->gpu_count = (int32_t)count;
+  for (int r = 0; r < 3; ++r) eo->gpu_per_instance[r] = (m >> r & 1u) ? inst[r] : 0;
+  dev_mark(c, node);
+  return GS_OK;
+}
+
+// scheduleOne of one extension pod: eval pass (B = 1) -> ext_nodes -> ext_matched -> ext_select, then the Reserve
+// of NodeNUMAResource (no-op on the supported nodes), DeviceShare and Reservation, and assume.
+int ext_schedule_one(gs_ctx* c, const gs_pod& pod, const gs_pod_ext& e, uint64_t seq, gs_placement* out,
+                     gs_ext_placement* eo) {
+  *out = gs_placement{-1, 0, 0, 0, 0};
+  *eo = gs_ext_placement{};
+  if (c->nranks > 1 || c->window_k)
+    return fail(c, GS_EUNSUPPORTED, "Reservation / DeviceShare pods need one rank and no node sampling");
+  const bool ds_on = c->ext.enabled & GS_EXT_DEVICESHARE, rs_on = c->ext.enabled & GS_EXT_RESERVATION;
+  int64_t greq[3];
+  uint32_t gmask = 0;
+  if (ds_on && gpu_request_of(e, greq, &gmask) < 0) {   // DeviceShare PreFilter: UnschedulableAndUnresolvable
+    eo->fail_code = GS_EXT_FAIL_POD;
+    c->stats.pods += 1;
+    return GS_OK;
+  }
+  if (!ds_on) { greq[0] = greq[1] = greq[2] = 0; gmask = 0; }
+  std::vector<std::pair<uint32_t, uint64_t>> matched;
+  if (rs_on) matched_of(c, e.reservation_owner, &matched);
+  if (gmask && !matched.empty())
+    return fail(c, GS_EUNSUPPORTED, "a pod that requests GPUs and matches reservations is not on the device path");
+  PodVec v = prep_pod(c, pod);
+  if (c->numa_on && (v.numa & PN_BIND))
+    return fail(c, GS_EUNSUPPORTED, "cpuset-bound Reservation / DeviceShare pods are not on the device path");
+  if (rs_on && e.reservation_required && matched.empty()) {   // PreFilter: ErrReasonReservationAffinity
+    c->stats.pods += 1;
+    return GS_OK;
+  }
+  int rc;
+  if ((rc = ext_alloc(c))) return rc;
+  if ((rc = ext_flush_devices(c))) return rc;
+  if ((rc = flush_rows(c))) return rc;
+  if (c->prep_stale && (rc = node_prep(c))) return rc;
+  // ---- BeforePreFilter: per-node restore records (reservation/transformer.go:50-235)
+  c->xrec.clear();
+  c->xres.clear();
+  c->xres_uid.clear();
+  for (size_t a = 0; a < matched.size();) {
+    const uint32_t node = matched[a].first;
+    size_t b = a;
+    while (b < matched.size() && matched[b].first == node) ++b;
+    if (b - a > (size_t)EXT_MAX_RES_PER_NODE)
+      return fail(c, GS_EUNSUPPORTED, "more than %d matched reservations on node %u", EXT_MAX_RES_PER_NODE, node);
+    ExtRec rec{};
+    rec.node = node;
+    rec.nres = (int32_t)(b - a);
+    rec.first = (int32_t)c->xres.size();
+    rec.dpods = rec.nres;
+    rec.order_min = INT64_MAX;
+    const gs_node mirror = reservation_view(c, node, 0);
+    const gs_node podreq = reservation_view(c, node, e.reservation_owner);
+    for (int s = 0; s < 7; ++s) {
+      rec.pod_requested[s] = podreq.requested[s];
+      rec.allocatable[s] = podreq.allocatable[s];
+    }
+    gs_node restored = podreq;
+    for (size_t k = a; k < b; ++k) {
+      const gs_reservation& r = c->rsv.at(matched[k].second);
+      rsv_request_delta(r.allocatable, r.allocatable_mask, -1, restored.requested, restored.nonzero_requested);
+      ExtRes x{};
+      int64_t rem[GS_NUM_RES];
+      (void)rsv_remained(r, rem);
+      for (int s = 0; s < 7; ++s) {
+        x.alloc[s] = (r.allocatable_mask >> s & 1u) ? r.allocatable[s] : 0;
+        x.allocated[s] = (r.allocated_mask >> s & 1u) ? r.allocated[s] : 0;
+        rec.r_allocated[s] += x.allocated[s];
+        // SubtractWithNonNegativeResult(Allocatable, Mask(Allocated, ResourceNames)) (Restricted policy)
+        const int64_t am = (r.resource_names_mask >> s & 1u) ? x.allocated[s] : 0;
+        x.remained_nn[s] = std::max<int64_t>(0, x.alloc[s] - am);
+      }
+      x.order = r.order;
+      x.alloc_mask = r.allocatable_mask;
+      x.allocated_mask = r.allocated_mask;
+      x.names = r.resource_names_mask;
+      x.policy = r.allocate_policy;
+      x.skip = (r.allocate_once && r.assigned_pods > 0) ? 1 : 0;
+      if (r.order != 0 && rec.order_min > r.order) rec.order_min = r.order;
+      c->xres.push_back(x);
+      c->xres_uid.push_back(r.uid);
+    }
+    for (int s = 0; s < 7; ++s) rec.dfree[s] = mirror.requested[s] - restored.requested[s];
+    rec.dnz[0] = mirror.nonzero_requested[0] - restored.nonzero_requested[0];
+    rec.dnz[1] = mirror.nonzero_requested[1] - restored.nonzero_requested[1];
+    rec.restored_pods = podreq.pod_count - rec.nres;
+    rec.allowed_pods = podreq.allowed_pod_number;
+    c->xrec.push_back(rec);
+    a = b;
+  }
+  const int nrec = (int)c->xrec.size();
+  if ((uint32_t)nrec > c->xrec_cap) {
+    if (c->d_xrec) (void)hipFree(c->d_xrec);
+    if (c->d_xnom) (void)hipFree(c->d_xnom);
+    if (c->h_xnom) (void)hipHostFree(c->h_xnom);
+    c->xrec_cap = std::max<uint32_t>(64, (uint32_t)nrec * 2);
+    HIP_TRY(c, hipMalloc(&c->d_xrec, sizeof(ExtRec) * c->xrec_cap));
+    HIP_TRY(c, hipMalloc(&c->d_xnom, 4 * c->xrec_cap));
+    HIP_TRY(c, hipHostMalloc(&c->h_xnom, 4 * c->xrec_cap, hipHostMallocDefault));
+  }
+  if (c->xres.size() > c->xres_cap) {
+    if (c->d_xres) (void)hipFree(c->d_xres);
+    c->xres_cap = std::max<uint32_t>(64, (uint32_t)c->xres.size() * 2);
+    HIP_TRY(c, hipMalloc(&c->d_xres, sizeof(ExtRes) * c->xres_cap));
+  }
+  ExtPod& xp = *c->h_xpod;
+  xp = ExtPod{};
+  for (int r = 0; r < 3; ++r) { xp.gpu_req[r] = greq[r]; xp.dev_w[r] = c->ext.device_weights[r]; }
+  xp.gpu_mask = gmask;
+  xp.gpu_names = gmask ? (e.gpu_request_mask & 0x1Fu) : 0u;
+  for (int n = 0; n < GS_NUM_GPU_NAMES; ++n) xp.gpu_name_req[n] = (xp.gpu_names >> n & 1u) ? e.gpu_requests[n] : 0;
+  xp.w_ds = c->ext.weight_deviceshare;
+  xp.w_rs = c->ext.weight_reservation;
+  for (int s = 0; s < 7; ++s) xp.pod_req[s] = pod.requests[s];
+  xp.pod_mask = pod.request_mask & 0x7Fu;
+  xp.required = rs_on && e.reservation_required;
+  xp.nrec = nrec;
+  xp.ds_on = ds_on;
+  xp.rs_on = rs_on;
+  xp.dev_most = c->ext.device_scoring_type == GS_SCORING_MOST_ALLOCATED;
+  xp.seq = seq;
+  // GPU names are scalar requests: the Fit filter's all-zero short cut no longer applies
+  if (xp.gpu_names) v.flags &= ~PF_ALL_ZERO;
+  c->h_pods[0] = v;
+  c->h_seq[0] = seq;
+  // numa_idx (the eval pass's NUMA-policy work list) as launch_batch keeps it
+  if (c->numa_on && c->numa_idx_stale) {
+    std::vector<uint32_t> idx;
+    for (uint32_t n = c->n0; n < c->n1; ++n)
+      if (c->numa[n].cfg.numa_topology_policy != GS_NUMA_POLICY_NONE) idx.push_back(n);
+    HIP_TRY(c, hipStreamSynchronize(c->st));
+    HIP_TRY(c, hipStreamSynchronize(c->st_ev));
+    if (c->d_numa_idx) { (void)hipFree(c->d_numa_idx); c->d_numa_idx = nullptr; }
+    c->numa_n = (uint32_t)idx.size();
+    if (c->numa_n) {
+      HIP_TRY(c, hipMalloc(&c->d_numa_idx, 4 * idx.size()));
+      HIP_TRY(c, hipMemcpy(c->d_numa_idx, idx.data(), 4 * idx.size(), hipMemcpyHostToDevice));
+    }
+    c->numa_idx_stale = false;
+  }
+  if (c->numa_on && c->numa_n)   // the NUMA-policy Reserve (zone split by the Filter-time hint) is not on this path
+    return fail(c, GS_EUNSUPPORTED, "Reservation / DeviceShare pods with NUMA-policy nodes in the cluster");
+  const int prod_cols = (v.flags & PF_PROD_SCORE) ? 1 : 0;
+  HIP_TRY(c, hipMemcpyAsync(c->d_pods, c->h_pods, sizeof(PodVec), hipMemcpyHostToDevice, c->st));
+  HIP_TRY(c, hipMemcpyAsync(c->d_xpod, c->h_xpod, sizeof(ExtPod), hipMemcpyHostToDevice, c->st));
+  if (nrec) {
+    HIP_TRY(c, hipMemcpyAsync(c->d_xrec, c->xrec.data(), sizeof(ExtRec) * nrec, hipMemcpyHostToDevice, c->st));
+    HIP_TRY(c, hipMemcpyAsync(c->d_xres, c->xres.data(), sizeof(ExtRes) * c->xres.size(), hipMemcpyHostToDevice, c->st));
+  }
+  HIP_TRY(c, hipEventRecord(c->ev[0], c->st));
+  HIP_TRY(c, launch_eval(c->mv, c->d_pods, 1, c->pf, c->n0, c->n1, c->d_S, c->ld, prod_cols, c->d_numa_idx, c->numa_n,
+                         c->d_aff, c->st));
+  HIP_TRY(c, hipEventRecord(c->ev[1], c->st));
+  HIP_TRY(c, launch_ext_nodes(c->d_dev, c->d_S, c->n0, c->n1, c->d_xpod, c->d_xtot, c->d_xds, c->d_xrs, c->st));
+  HIP_TRY(c, launch_ext_matched(c->mv, c->d_pods, c->pf, prod_cols, c->d_xpod, c->d_xrec, c->d_xres, nrec, c->d_xtot,
+                                c->d_xrs, c->d_xnom, c->st));
+  HIP_TRY(c, launch_ext_select(c->d_xtot, c->d_xds, c->d_xrs, c->d_xrec, c->n0, c->n1, c->d_xpod, c->cfg.seed, c->d_xT,
+                               c->d_xout, c->st));
+  HIP_TRY(c, hipEventRecord(c->ev[4], c->st));
+  HIP_TRY(c, hipMemcpyAsync(c->h_xout, c->d_xout, sizeof(ExtOut), hipMemcpyDeviceToHost, c->st));
+  if (nrec) HIP_TRY(c, hipMemcpyAsync(c->h_xnom, c->d_xnom, 4 * nrec, hipMemcpyDeviceToHost, c->st));
+  HIP_TRY(c, hipStreamSynchronize(c->st));
+  c->stats.eval_ms += ev_ms(c->ev[0], c->ev[1]);
+  c->stats.commit_ms += ev_ms(c->ev[1], c->ev[4]);
+  c->stats.eval_launches += 1;
+  c->stats.eval_pairs += c->n1 - c->n0;
+  c->stats.batches += 1;
+  c->stats.pods += 1;
+  const ExtOut xo = *c->h_xout;
+  out->feasible = xo.feasible;
+  if (xo.node < 0) return GS_OK;
+  out->node = xo.node;
+  out->score = xo.score;
+  out->ties = xo.ties;
+  eo->deviceshare_score = xo.ds_norm;
+  eo->reservation_score = xo.rs_norm;
+  const uint32_t node = (uint32_t)xo.node;
+  // ---- Reserve
+  if (gmask && (rc = ext_device_reserve(c, node, greq, gmask, eo))) return rc;
+  if (rs_on && xo.rec >= 0) {   // Reservation.Reserve -> reservationCache.assumePod (AddAssignedPod, reservation_info.go:379-388)
+    const int nom = c->h_xnom[xo.rec];
+    if (nom >= 0) {
+      gs_reservation& r = c->rsv.at(c->xres_uid[c->xrec[xo.rec].first + nom]);
+      for (int s = 0; s < 7; ++s)
+        if ((r.resource_names_mask >> s & 1u) && (pod.request_mask >> s & 1u)) {
+          r.allocated[s] = ((r.allocated_mask >> s & 1u) ? r.allocated[s] : 0) + pod.requests[s];
+          r.allocated_mask |= 1u << s;
+        }
+      r.assigned_pods += 1;
+      eo->reservation_uid = r.uid;
+    }
+  }
+  for (int n = 0; n < GS_NUM_GPU_NAMES; ++n)   // NodeInfo.AddPod of the GPU-name scalars
+    if (xp.gpu_names >> n & 1u) { c->devs[node].requested[n] += e.gpu_requests[n]; dev_mark(c, node); }
+  apply_placement(c, pod, xo.node, true);
+  return GS_OK;
+}
+
 }  // namespace
 
 // ================================================================================================
@@ -959,7 +1399,8 @@ void gs_abi_sizes(uint64_t* out, uint32_t n) {
   const uint64_t s[] = {sizeof(gs_pod), sizeof(gs_node), sizeof(gs_node_metric), sizeof(gs_pod_metric),
                         sizeof(gs_config), sizeof(gs_placement), sizeof(gs_stats), sizeof(gs_loadaware_args),
                         sizeof(gs_cpu_topology), sizeof(gs_node_numa), sizeof(gs_pod_allocation), sizeof(gs_numa_args),
-                        sizeof(gs_quota_group), sizeof(gs_quota_status)};
+                        sizeof(gs_quota_group), sizeof(gs_quota_status), sizeof(gs_node_devices),
+                        sizeof(gs_reservation), sizeof(gs_pod_ext), sizeof(gs_ext_args), sizeof(gs_ext_placement)};
   for (uint32_t i = 0; i < n && i < sizeof(s) / sizeof(s[0]); ++i) out[i] = s[i];
 }
 
@@ -1050,6 +1491,11 @@ int gs_create(const gs_config* cfg, gs_ctx** out) {
   c->nodes.resize(c->N);
   c->numa.resize(c->N);
   c->row_dirty.assign(c->N, 0);
+  c->devs.assign(c->N, gs_node_devices{});
+  c->dev_dirty.assign(c->N, 0);
+  c->rsv_node.assign(c->N, {});
+  gs_ext_args_default(&c->ext);
+  c->ext.enabled = 0;   // the extension plugins are off until gs_ext_configure
   set_shard(c);
   auto bail = [&](const char* what, hipError_t e) {
     fprintf(stderr, "gpuscore: %s: %s\n", what, hipGetErrorString(e));
@@ -1136,6 +1582,11 @@ int gs_create(const gs_config* cfg, gs_ctx** out) {
 
 int gs_destroy(gs_ctx* c) {
   if (!c) return GS_EINVAL;
+  for (void* p : {(void*)c->d_dev, (void*)c->d_xpod, (void*)c->d_xrec, (void*)c->d_xres, (void*)c->d_xtot,
+                  (void*)c->d_xds, (void*)c->d_xrs, (void*)c->d_xnom, (void*)c->d_xT, (void*)c->d_xout})
+    if (p) (void)hipFree(p);
+  for (void* p : {(void*)c->h_xpod, (void*)c->h_xout, (void*)c->h_xnom})
+    if (p) (void)hipHostFree(p);
   if (c->d_stamps) {
     uint64_t st[32] = {};
     if (hipMemcpy(st, c->d_stamps, 256, hipMemcpyDeviceToHost) == hipSuccess) {
@@ -1628,7 +2079,10 @@ int gs_reset(gs_ctx* c) {
   for (uint32_t i = 0; i < c->N; ++i)
     if (c->nodes[i].valid) mark_dirty(c, i);
   c->numa_idx_stale = true;
+  if (c->d_dev)
+    for (uint32_t i = 0; i < c->N; ++i) dev_mark(c, i);
   int rc = flush_rows(c);
+  if (!rc) rc = ext_flush_devices(c);
   if (rc) return rc;
   if ((rc = node_prep(c))) return rc;
   hipError_t e = hipStreamSynchronize(c->st);
@@ -1700,7 +2154,7 @@ int gs_debug_mirror_check(gs_ctx* c) {
   int bad = 0;
   std::vector<int64_t> row(ROW_WORDS);
   for (uint32_t i = 0; i < c->N; ++i) {
-    derive_row(c, c->nodes[i], row.data());
+    derive_row(c, i, row.data());
     bool ok = true;
     derive_row_numa(c, i, row.data());
     for (int k = 0; k < NUM_I64_COLS; ++k) ok &= d64[(size_t)k * c->npad + i] == row[k];
@@ -1712,6 +2166,155 @@ int gs_debug_mirror_check(gs_ctx* c) {
     }
   }
   return bad;
+}
+
+}  // extern "C"
+
+// ---- Reservation + DeviceShare ----------------------------------------------------------------
+extern "C" {
+
+void gs_ext_args_default(gs_ext_args* a) {
+  if (!a) return;
+  std::memset(a, 0, sizeof(*a));
+  a->enabled = GS_EXT_DEVICESHARE | GS_EXT_RESERVATION;
+  a->device_scoring_type = GS_SCORING_LEAST_ALLOCATED;   // v1beta2 SetDefaults_DeviceShareArgs (defaults.go:187-203)
+  a->device_weights[GS_GPU_MEMORY_RATIO] = 1;            // (its rdma weight has no GPU counterpart)
+  a->weight_deviceshare = 1;                              // config/manager/scheduler-config.yaml:80-89
+  a->weight_reservation = 5000;
+}
+
+int gs_ext_configure(gs_ctx* c, const gs_ext_args* a) {
+  if (!c || !a) return GS_EINVAL;
+  if (a->enabled & ~(GS_EXT_DEVICESHARE | GS_EXT_RESERVATION)) return fail(c, GS_EINVAL, "unknown extension plugin bits");
+  if (a->device_scoring_type != GS_SCORING_LEAST_ALLOCATED && a->device_scoring_type != GS_SCORING_MOST_ALLOCATED)
+    return fail(c, GS_EINVAL, "DeviceShare scoring strategy not supported");
+  for (int r = 0; r < GS_NUM_GPU_RES; ++r)
+    if (a->device_weights[r] < 0 || a->device_weights[r] > 100) return fail(c, GS_EINVAL, "DeviceShare weight out of range");
+  if (a->weight_deviceshare < 0 || a->weight_reservation < 0 || a->weight_deviceshare > 100000 ||
+      a->weight_reservation > 100000)
+    return fail(c, GS_EINVAL, "extension plugin weights out of range");
+  const bool rs_changed = (c->ext.enabled ^ a->enabled) & GS_EXT_RESERVATION;
+  c->ext = *a;
+  if (rs_changed)   // the mirror rows carry the unmatched restore only with the Reservation plugin on
+    for (uint32_t i = 0; i < c->N; ++i)
+      if (c->nodes[i].valid) mark_dirty(c, i);
+  return GS_OK;
+}
+
+int gs_node_devices_upsert(gs_ctx* c, const uint32_t* idx, const gs_node_devices* d, uint32_t n) {
+  if (!c || (n && !d)) return GS_EINVAL;
+  for (uint32_t k = 0; k < n; ++k) {
+    const uint32_t i = idx ? idx[k] : k;
+    if (i >= c->N) return fail(c, GS_EINVAL, "node index %u out of range", i);
+    if (d[k].num_gpus < 0 || d[k].num_gpus > GS_MAX_GPUS) return fail(c, GS_EINVAL, "num_gpus out of range");
+    for (int g = 0; g < d[k].num_gpus; ++g) {
+      for (int h = 0; h < g; ++h)
+        if (d[k].gpus[h].minor == d[k].gpus[g].minor) return fail(c, GS_EINVAL, "duplicate GPU minor on node %u", i);
+      if (d[k].gpus[g].minor < 0 || d[k].gpus[g].minor > 31) return fail(c, GS_EUNSUPPORTED, "GPU minor outside 0..31");
+      for (int r = 0; r < GS_NUM_GPU_RES; ++r)
+        if (d[k].gpus[g].total[r] < 0 || d[k].gpus[g].used[r] < 0 || d[k].gpus[g].total[r] >= (1LL << 53))
+          return fail(c, GS_EUNSUPPORTED, "GPU quantity outside [0, 2^53)");
+    }
+    c->devs[i] = d[k];
+    dev_mark(c, i);
+  }
+  return GS_OK;
+}
+
+int gs_node_devices_get(gs_ctx* c, uint32_t node, gs_node_devices* out) {
+  if (!c || !out || node >= c->N) return GS_EINVAL;
+  *out = c->devs[node];
+  return GS_OK;
+}
+
+namespace {
+void rsv_unindex(gs_ctx* c, const gs_reservation& r) {
+  auto& v = c->rsv_node[r.node];
+  v.erase(std::remove(v.begin(), v.end(), r.uid), v.end());
+  auto it = c->rsv_owner.find(r.owner_key);
+  if (it != c->rsv_owner.end()) {
+    auto& o = it->second;
+    o.erase(std::remove(o.begin(), o.end(), r.uid), o.end());
+    if (o.empty()) c->rsv_owner.erase(it);
+  }
+  mark_dirty(c, r.node);
+}
+}  // namespace
+
+int gs_reservations_upsert(gs_ctx* c, const gs_reservation* r, uint32_t n) {
+  if (!c || (n && !r)) return GS_EINVAL;
+  for (uint32_t k = 0; k < n; ++k) {
+    const gs_reservation& x = r[k];
+    if (x.node >= c->N) return fail(c, GS_EINVAL, "reservation node %u out of range", x.node);
+    if (x.allocate_policy < GS_RSV_POLICY_DEFAULT || x.allocate_policy > GS_RSV_POLICY_RESTRICTED)
+      return fail(c, GS_EINVAL, "reservation allocate policy out of range");
+    if ((x.allocatable_mask | x.allocated_mask | x.resource_names_mask) & ~0x7Fu)
+      return fail(c, GS_EINVAL, "reservation resource keys outside slots 0..6");
+    for (int s = 0; s < GS_NUM_RES; ++s)
+      if (x.allocatable[s] < 0 || x.allocated[s] < 0 || x.allocatable[s] >= (1LL << 50) || x.allocated[s] >= (1LL << 50))
+        return fail(c, GS_EUNSUPPORTED, "reservation quantity outside [0, 2^50)");
+    auto it = c->rsv.find(x.uid);
+    if (it != c->rsv.end()) rsv_unindex(c, it->second);
+    c->rsv[x.uid] = x;
+    auto& v = c->rsv_node[x.node];
+    v.insert(std::lower_bound(v.begin(), v.end(), x.uid), x.uid);
+    if (x.owner_key) {
+      auto& o = c->rsv_owner[x.owner_key];
+      o.insert(std::lower_bound(o.begin(), o.end(), x.uid), x.uid);
+    }
+    mark_dirty(c, x.node);
+  }
+  return GS_OK;
+}
+
+int gs_reservations_remove(gs_ctx* c, const uint64_t* uids, uint32_t n) {
+  if (!c || (n && !uids)) return GS_EINVAL;
+  for (uint32_t k = 0; k < n; ++k) {
+    auto it = c->rsv.find(uids[k]);
+    if (it == c->rsv.end()) continue;
+    rsv_unindex(c, it->second);
+    c->rsv.erase(it);
+  }
+  return GS_OK;
+}
+
+int gs_reservation_get(gs_ctx* c, uint64_t uid, gs_reservation* out) {
+  if (!c || !out) return GS_EINVAL;
+  auto it = c->rsv.find(uid);
+  if (it == c->rsv.end()) return 0;
+  *out = it->second;
+  return 1;
+}
+
+int gs_schedule_ext(gs_ctx* c, const gs_pod* pods, const gs_pod_ext* ext, uint32_t npods, const uint64_t* seq,
+                    gs_placement* out, gs_ext_placement* ext_out) {
+  if (!c || (npods && (!pods || !out))) return GS_EINVAL;
+  int rc = ready(c);
+  if (rc) return rc;
+  for (uint32_t i = 0; i < npods; ++i)
+    if ((rc = validate_pod(c, pods[i]))) return rc;
+  uint32_t i = 0;
+  while (i < npods) {
+    // a run of plain pods goes through the batched path (both plugins score 0 for them; the mirror rows carry the
+    // unmatched restore), an extension pod through the normalizing path
+    uint32_t j = i;
+    while (j < npods && !(ext && c->ext.enabled && is_ext_pod(c, ext[j]))) ++j;
+    if (j > i) {
+      std::vector<uint64_t> sq;
+      if (!seq) { sq.resize(j - i); for (uint32_t k = i; k < j; ++k) sq[k - i] = k; }
+      if ((rc = gs_schedule(c, pods + i, j - i, seq ? seq + i : sq.data(), out + i))) return rc;
+      if (ext_out) std::memset(ext_out + i, 0, sizeof(gs_ext_placement) * (j - i));
+      i = j;
+      continue;
+    }
+    gs_ext_placement eo{};
+    if ((rc = ext_schedule_one(c, pods[i], ext[i], seq ? seq[i] : i, &out[i], &eo))) return rc;
+    if (ext_out) ext_out[i] = eo;
+    ++i;
+  }
+  rc = flush_rows(c);
+  if (!rc) rc = ext_flush_devices(c);
+  return rc;
 }
 
 }  // extern "C"

@@ -1,0 +1,360 @@
+// gs_ext.hip — Reservation + DeviceShare kernels for one extension pod (see gs_ext.h).
+//
+// Reference: deviceshare/plugin.go:272-322 (Filter), deviceshare/scoring.go:34-89,186-308 (Score),
+// deviceshare/device_allocator.go:99-163,397-467,513-536 (Allocate / score), devicehandler_gpu.go:38-85 (desired
+// per-instance request), reservation/transformer.go:50-292 (restore), reservation/plugin.go:311-496 (Filter, fitsNode),
+// reservation/nominator.go:140-190 + scoring.go:42-203 (nomination, PreScore, Score),
+// [upstream] pluginhelper.DefaultNormalizeScore, schedule_one.go selectHost.
+#include <hip/hip_runtime.h>
+
+#include "gs_eval_dev.h"
+#include "gs_ext.h"
+
+namespace gs {
+namespace {
+
+constexpr int64_t kMaxNodeScore = 100;
+
+__device__ __forceinline__ int64_t ds_least(int64_t req, int64_t cap) {
+  return (cap == 0 || req > cap) ? 0 : (cap - req) * kMaxNodeScore / cap;
+}
+__device__ __forceinline__ int64_t ds_most(int64_t req, int64_t cap) {
+  if (cap == 0) return 0;
+  if (req > cap) req = cap;
+  return req * kMaxNodeScore / cap;
+}
+
+// GPUHandler.CalcDesiredRequestsAndCount: per-instance request (all three keys after fillGPUTotalMem) and count;
+// false = Prepare fails (no GPU minors / no healthy GPU)
+__device__ __forceinline__ bool gpu_desired(const DevNode& d, const ExtPod& p, int64_t inst[3], uint32_t* mask,
+                                            int64_t* count) {
+  if (d.num_gpus <= 0) return false;
+  int64_t total_mem = -1;
+  for (int g = 0; g < d.num_gpus; ++g) {
+    if (d.g[g].total[0] | d.g[g].total[1] | d.g[g].total[2]) { total_mem = d.g[g].total[2]; break; }
+  }
+  if (total_mem < 0) return false;
+  int64_t core = p.gpu_req[0], ratio = p.gpu_req[1], mem = p.gpu_req[2];
+  if (p.gpu_mask & 4u) ratio = (int64_t)((double)mem / (double)total_mem * 100.0);   // memoryBytesToRatio
+  else mem = ratio * total_mem / 100;                                                   // memoryRatioToBytes
+  uint32_t m = p.gpu_mask | 6u;
+  int64_t n = 1;
+  if (ratio > 100 && ratio % 100 == 0) {
+    n = ratio / 100;
+    core /= n; mem /= n; ratio /= n;
+    m = 7u;
+  }
+  inst[0] = core; inst[1] = ratio; inst[2] = mem;
+  *mask = m;
+  *count = n;
+  return true;
+}
+
+__device__ __forceinline__ bool fits_inst(const int64_t inst[3], uint32_t mask, const DevGpu& g) {
+  for (int r = 0; r < 3; ++r)
+    if ((mask >> r & 1u) && inst[r] > g.free[r]) return false;
+  return true;
+}
+
+// one node: GPU Fit scalars, DeviceShare Filter and raw Score
+__device__ __forceinline__ void eval_device(const DevNode& d, const ExtPod& p, bool* ok, int32_t* raw) {
+  *ok = true;
+  *raw = 0;
+  for (int n = 0; n < 5; ++n)   // [upstream] fitsRequest over the pod's GPU-name scalars
+    if ((p.gpu_names >> n & 1u) && p.gpu_name_req[n] > d.fit_free[n]) { *ok = false; return; }
+  if (!d.has_device) return;    // no Device object: DeviceShare passes and scores 0
+  int64_t inst[3];
+  uint32_t mask;
+  int64_t count;
+  if (!gpu_desired(d, p, inst, &mask, &count)) { *ok = false; return; }
+  // nodeDevice.filter: a node whose GPUs are all fully used drops the type
+  bool all_zero = true;
+  for (int g = 0; g < d.num_gpus; ++g) all_zero &= !(d.g[g].free[0] | d.g[g].free[1] | d.g[g].free[2]);
+  int64_t ok_n = 0, tot[3] = {0, 0, 0}, fr[3] = {0, 0, 0};
+  if (!all_zero) {
+    for (int g = 0; g < d.num_gpus; ++g) {
+      const DevGpu& x = d.g[g];
+      if (!x.has_info) continue;
+      for (int r = 0; r < 3; ++r) { tot[r] += x.total[r]; fr[r] += x.free[r]; }
+      if (!(x.free[0] | x.free[1] | x.free[2])) continue;
+      if (fits_inst(inst, mask, x)) ++ok_n;
+    }
+  }
+  if (ok_n < count) { *ok = false; return; }
+  // allocator.score -> scoreNode (summed totals / frees of the candidate minors)
+  int64_t ns = 0, ws = 0;
+  for (int r = 0; r < 3; ++r) {
+    if (!p.dev_w[r] || tot[r] == 0) continue;
+    int64_t rq = tot[r];
+    if (tot[r] >= fr[r]) rq = tot[r] - fr[r] + ((mask >> r & 1u) ? inst[r] : 0);
+    ns += (p.dev_most ? ds_most(rq, tot[r]) : ds_least(rq, tot[r])) * p.dev_w[r];
+    ws += p.dev_w[r];
+  }
+  *raw = ws ? (int32_t)(ns / ws) : 0;
+}
+
+__global__ __launch_bounds__(256) void ext_nodes_kernel(const DevNode* __restrict__ dev, const int16_t* __restrict__ S,
+                                                         uint32_t n0, uint32_t n1, const ExtPod* __restrict__ pp,
+                                                         int32_t* tot, int16_t* ds, int16_t* rs) {
+  const uint32_t i = n0 + blockIdx.x * 256 + threadIdx.x;
+  if (i >= n1) return;
+  const ExtPod& p = *pp;
+  int32_t t = S[i - n0];
+  int32_t raw = 0;
+  if (t >= 0 && p.gpu_mask) {
+    bool ok;
+    eval_device(dev[i], p, &ok, &raw);
+    if (!ok) t = -1;
+  }
+  if (p.required) t = -1;       // reservation affinity: only nodes with a matched reservation (ext_matched_kernel)
+  tot[i - n0] = t;
+  ds[i - n0] = (int16_t)(t >= 0 ? raw : 0);
+  rs[i - n0] = 0;
+}
+
+// fitsNode (plugin.go:444-496), preemptible = 0: number of insufficient resources
+__device__ int fits_node(const ExtPod& p, const ExtRec& rc, const ExtRes* r) {
+  int bad = 0;
+  if (rc.restored_pods - rc.nres + 1 > rc.allowed_pods) ++bad;
+  const uint32_t scalars = p.pod_mask & GS_SCALAR_RES_MASK;
+  if (!p.pod_req[0] && !p.pod_req[1] && !p.pod_req[2] && !scalars) return bad;
+  for (int s = 0; s < 7; ++s) {
+    if (s >= 3 && !(scalars >> s & 1u)) continue;
+    const int64_t rem = r ? r->alloc[s] - r->allocated[s] : 0;
+    const int64_t avail = rc.allocatable[s] - (rc.pod_requested[s] - rem - rc.r_allocated[s]);
+    if (p.pod_req[s] > avail) ++bad;
+  }
+  return bad;
+}
+
+// filterWithReservations over one reservation (plugin.go:377-440)
+__device__ bool reservation_fits(const ExtPod& p, const ExtRec& rc, const ExtRes& r) {
+  if (!(r.names & p.pod_mask)) return false;
+  const bool node_fits = fits_node(p, rc, &r) == 0;
+  if (r.policy == GS_RSV_POLICY_DEFAULT || r.policy == GS_RSV_POLICY_ALIGNED) return node_fits;
+  if (r.policy == GS_RSV_POLICY_RESTRICTED) {
+    if (!node_fits) return false;
+    for (int s = 0; s < 7; ++s)
+      if ((p.pod_mask >> s & 1u) && (r.names >> s & 1u) && p.pod_req[s] > r.remained_nn[s]) return false;
+    return true;
+  }
+  return false;
+}
+
+__device__ __forceinline__ int64_t milli(int s, int64_t v) { return s == 0 ? v : v * 1000; }
+
+// scoreReservation (scoring.go:183-203) with allocated = Allocated
+__device__ int64_t score_reservation(const ExtPod& p, const ExtRes& r) {
+  int64_t s = 0, w = 0;
+  for (int k = 0; k < 7; ++k) {
+    if (!(r.alloc_mask >> k & 1u) || r.alloc[k] == 0) continue;
+    ++w;
+    const int64_t req = ((p.pod_mask >> k & 1u) ? p.pod_req[k] : 0) + ((r.allocated_mask >> k & 1u) ? r.allocated[k] : 0);
+    if (req <= r.alloc[k]) s += kMaxNodeScore * milli(k, req) / milli(k, r.alloc[k]);
+  }
+  return w ? s / w : 0;
+}
+
+__global__ __launch_bounds__(64) void ext_matched_kernel(MirrorView m, const PodVec* __restrict__ pods, Profile pf,
+                                                          int prod_cols, const ExtPod* __restrict__ pp,
+                                                          const ExtRec* __restrict__ recs,
+                                                          const ExtRes* __restrict__ res, int nrec, int32_t* tot,
+                                                          int16_t* rs, int32_t* nominated) {
+  const int k = blockIdx.x * 64 + threadIdx.x;
+  if (k >= nrec) return;
+  const ExtPod& p = *pp;
+  const ExtRec& rc = recs[k];
+  const uint32_t i = rc.node;
+  // the restored NodeInfo of the pod (BeforePreFilter): the mirror row plus the matched restore deltas
+  Row r;
+  load_row(m, i, prod_cols != 0, (pf.enabled & 0x30u) != 0, r);
+  for (int s = 3; s < 7; ++s) r.free[s] = m.c64(C_FREE_CPU + s)[i];
+  for (int s = 0; s < 7; ++s) r.free[s] += rc.dfree[s];
+  r.nzfree[0] += rc.dnz[0];
+  r.nzfree[1] += rc.dnz[1];
+  r.free_pods += rc.dpods;
+  const PairOut o = eval_pair<false, true>(r, pods[0], pf, m);
+  int32_t t = total_score(o, pf);
+  // Reservation Filter: a required pod needs a satisfying matched reservation (filterWithReservations)
+  if (t >= 0 && p.required) {
+    bool any = false;
+    for (int j = 0; j < rc.nres && !any; ++j) any = reservation_fits(p, rc, res[rc.first + j]);
+    if (!any) t = -1;
+  }
+  // NominateReservation
+  int nom = -1;
+  if (t >= 0) {
+    int64_t best_order = INT64_MAX;
+    for (int j = 0; j < rc.nres; ++j) {
+      const ExtRes& x = res[rc.first + j];
+      if (x.skip || !reservation_fits(p, rc, x)) continue;
+      if (x.order != 0 && best_order > x.order) { best_order = x.order; nom = j; }
+    }
+    if (nom < 0) {
+      int64_t bs = INT64_MIN;
+      for (int j = 0; j < rc.nres; ++j) {
+        const ExtRes& x = res[rc.first + j];
+        if (x.skip || !reservation_fits(p, rc, x)) continue;
+        const int64_t s = score_reservation(p, x);
+        if (s > bs) { bs = s; nom = j; }
+      }
+    }
+  }
+  tot[i] = t;
+  rs[i] = (int16_t)((t >= 0 && nom >= 0) ? score_reservation(p, res[rc.first + nom]) : 0);
+  nominated[k] = nom;
+}
+
+constexpr int SEL_THREADS = 1024;
+
+__device__ __forceinline__ int64_t block_reduce_max(int64_t v, int64_t* sh) {
+  for (int o = 32; o > 0; o >>= 1) v = max(v, (int64_t)__shfl_xor(v, o));
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  __syncthreads();
+  if (l == 0) sh[w] = v;
+  __syncthreads();
+  if (threadIdx.x < 64) {
+    int64_t x = threadIdx.x < SEL_THREADS / 64 ? sh[threadIdx.x] : INT64_MIN;
+    for (int o = 32; o > 0; o >>= 1) x = max(x, (int64_t)__shfl_xor(x, o));
+    if (threadIdx.x == 0) sh[16] = x;
+  }
+  __syncthreads();
+  return sh[16];
+}
+__device__ __forceinline__ int64_t block_reduce_sum(int64_t v, int64_t* sh) {
+  for (int o = 32; o > 0; o >>= 1) v += (int64_t)__shfl_xor(v, o);
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  __syncthreads();
+  if (l == 0) sh[w] = v;
+  __syncthreads();
+  if (threadIdx.x < 64) {
+    int64_t x = threadIdx.x < SEL_THREADS / 64 ? sh[threadIdx.x] : 0;
+    for (int o = 32; o > 0; o >>= 1) x += (int64_t)__shfl_xor(x, o);
+    if (threadIdx.x == 0) sh[16] = x;
+  }
+  __syncthreads();
+  return sh[16];
+}
+
+// One workgroup: each thread owns a contiguous chunk of the row (node order), so the j*-th tie is located with one
+// exclusive scan of per-thread tie counts.
+__global__ __launch_bounds__(SEL_THREADS) void ext_select_kernel(const int32_t* __restrict__ tot,
+                                                                 const int16_t* __restrict__ ds,
+                                                                 const int16_t* __restrict__ rs,
+                                                                 const ExtRec* __restrict__ recs, uint32_t n0,
+                                                                 uint32_t n1, const ExtPod* __restrict__ pp,
+                                                                 uint64_t seed, int32_t* T, ExtOut* out) {
+  __shared__ int64_t sh[17];
+  __shared__ int32_t pref_sh;
+  __shared__ int64_t scan[SEL_THREADS];
+  const ExtPod& p = *pp;
+  const uint32_t len = n1 - n0;
+  const uint32_t chunk = (len + SEL_THREADS - 1) / SEL_THREADS;
+  const uint32_t b = min(len, threadIdx.x * chunk), e = min(len, b + chunk);
+  // PreScore: the preferred node = the first feasible node (node order) with the lowest reservation order
+  if (threadIdx.x == 0) {
+    int32_t pref = -1;
+    int64_t so = INT64_MAX;
+    if (p.rs_on)
+      for (int k = 0; k < p.nrec; ++k) {
+        const ExtRec& rc = recs[k];
+        if (tot[rc.node - n0] < 0) continue;
+        if (rc.order_min != INT64_MAX && rc.order_min != 0 && so > rc.order_min) { so = rc.order_min; pref = (int32_t)rc.node; }
+      }
+    pref_sh = pref;
+  }
+  __syncthreads();
+  const int32_t pref = pref_sh;
+  int64_t mds = 0, mrs = 0, feas = 0;
+  for (uint32_t j = b; j < e; ++j) {
+    if (tot[j] < 0) continue;
+    ++feas;
+    mds = max(mds, (int64_t)ds[j]);
+    mrs = max(mrs, (int64_t)((int32_t)(j + n0) == pref ? 1000 : rs[j]));
+  }
+  const int64_t MDS = block_reduce_max(mds, sh);
+  const int64_t MRS = block_reduce_max(mrs, sh);
+  const int64_t F = block_reduce_sum(feas, sh);
+  // weighted totals with DefaultNormalizeScore(MaxNodeScore, false) of both plugins
+  int64_t mt = -1;
+  for (uint32_t j = b; j < e; ++j) {
+    int32_t t = tot[j];
+    if (t >= 0) {
+      int64_t x = t;
+      if (p.ds_on) x += (MDS ? kMaxNodeScore * ds[j] / MDS : (int64_t)ds[j]) * p.w_ds;
+      if (p.rs_on) {
+        const int64_t r = (int32_t)(j + n0) == pref ? 1000 : rs[j];
+        x += (MRS ? kMaxNodeScore * r / MRS : r) * p.w_rs;
+      }
+      t = (int32_t)x;
+      mt = max(mt, x);
+    }
+    T[j] = t;
+  }
+  const int64_t M = block_reduce_max(mt, sh);
+  int64_t cnt = 0;
+  if (M >= 0)
+    for (uint32_t j = b; j < e; ++j) cnt += T[j] == M;
+  scan[threadIdx.x] = cnt;
+  __syncthreads();
+  for (int o = 1; o < SEL_THREADS; o <<= 1) {   // inclusive Hillis-Steele scan
+    int64_t v = threadIdx.x >= (unsigned)o ? scan[threadIdx.x - o] : 0;
+    __syncthreads();
+    scan[threadIdx.x] += v;
+    __syncthreads();
+  }
+  const int64_t ties = scan[SEL_THREADS - 1];
+  if (M < 0) {
+    if (threadIdx.x == 0) *out = ExtOut{-1, (uint32_t)F, 0, 0, -1, 0, 0, pref, 0};
+    return;
+  }
+  const int64_t jstar = tiebreak_position(seed, p.seq, ties);
+  const int64_t before = scan[threadIdx.x] - cnt;
+  if (jstar > before && jstar <= before + cnt) {
+    int64_t c = before;
+    for (uint32_t j = b; j < e; ++j) {
+      if (T[j] != M) continue;
+      if (++c == jstar) {
+        const int32_t node = (int32_t)(j + n0);
+        int32_t rec = -1;
+        for (int k = 0; k < p.nrec; ++k)
+          if ((int32_t)recs[k].node == node) rec = k;
+        const int64_t dsn = MDS ? kMaxNodeScore * ds[j] / MDS : ds[j];
+        const int64_t rr = node == pref ? 1000 : rs[j];
+        const int64_t rsn = MRS ? kMaxNodeScore * rr / MRS : rr;
+        *out = ExtOut{node, (uint32_t)F, M, (uint32_t)ties, rec, (int32_t)(p.ds_on ? dsn : 0),
+                      (int32_t)(p.rs_on ? rsn : 0), pref, 0};
+        break;
+      }
+    }
+  }
+}
+
+}  // namespace
+
+hipError_t launch_ext_nodes(const DevNode* dev, const int16_t* S, uint32_t n0, uint32_t n1, const ExtPod* pod,
+                            int32_t* tot, int16_t* ds, int16_t* rs, hipStream_t st) {
+  const uint32_t len = n1 - n0;
+  if (!len) return hipSuccess;
+  hipLaunchKernelGGL(ext_nodes_kernel, dim3((len + 255) / 256), dim3(256), 0, st, dev, S, n0, n1, pod, tot, ds, rs);
+  return hipGetLastError();
+}
+
+hipError_t launch_ext_matched(const MirrorView& m, const PodVec* pods, const Profile& pf, int prod_cols,
+                              const ExtPod* pod, const ExtRec* recs, const ExtRes* res, int nrec, int32_t* tot,
+                              int16_t* rs, int32_t* nominated, hipStream_t st) {
+  if (nrec <= 0) return hipSuccess;
+  hipLaunchKernelGGL(ext_matched_kernel, dim3((nrec + 63) / 64), dim3(64), 0, st, m, pods, pf, prod_cols, pod, recs, res,
+                     nrec, tot, rs, nominated);
+  return hipGetLastError();
+}
+
+hipError_t launch_ext_select(const int32_t* tot, const int16_t* ds, const int16_t* rs, const ExtRec* recs, uint32_t n0,
+                             uint32_t n1, const ExtPod* pod, uint64_t seed, int32_t* scratch, ExtOut* out,
+                             hipStream_t st) {
+  hipLaunchKernelGGL(ext_select_kernel, dim3(1), dim3(SEL_THREADS), 0, st, tot, ds, rs, recs, n0, n1, pod, seed, scratch,
+                     out);
+  return hipGetLastError();
+}
+
+}  // namespace gs

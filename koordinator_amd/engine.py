@@ -112,6 +112,48 @@ class Engine:
         self._chk(lib().gs_schedule(self._h, abi.ptr(pods), len(pods), abi.ptr(seq), abi.ptr(out)), "gs_schedule")
         return out
 
+    # ---- Reservation + DeviceShare
+    def ext_configure(self, args: abi.GsExtArgs):
+        self._chk(lib().gs_ext_configure(self._h, C.byref(args)), "gs_ext_configure")
+
+    def upsert_devices(self, devs, idx=None):
+        devs = np.ascontiguousarray(devs, dtype=abi.NODE_DEVICES_DTYPE)
+        if idx is not None:
+            idx = np.ascontiguousarray(idx, dtype=np.uint32)
+        self._chk(lib().gs_node_devices_upsert(self._h, abi.ptr(idx), abi.ptr(devs), len(devs)), "gs_node_devices_upsert")
+
+    def devices(self, node: int):
+        out = abi.GsNodeDevices()
+        self._chk(lib().gs_node_devices_get(self._h, node, C.byref(out)), "gs_node_devices_get")
+        return np.frombuffer(bytes(out), dtype=abi.NODE_DEVICES_DTYPE)[0]
+
+    def upsert_reservations(self, rsv):
+        rsv = np.ascontiguousarray(rsv, dtype=abi.RESERVATION_DTYPE)
+        self._chk(lib().gs_reservations_upsert(self._h, abi.ptr(rsv), len(rsv)), "gs_reservations_upsert")
+
+    def remove_reservations(self, uids):
+        uids = np.ascontiguousarray(uids, dtype=np.uint64)
+        self._chk(lib().gs_reservations_remove(self._h, abi.ptr(uids), len(uids)), "gs_reservations_remove")
+
+    def reservation(self, uid: int):
+        out = abi.GsReservation()
+        rc = lib().gs_reservation_get(self._h, uid, C.byref(out))
+        self._chk(min(rc, 0), "gs_reservation_get")
+        return np.frombuffer(bytes(out), dtype=abi.RESERVATION_DTYPE)[0] if rc == 1 else None
+
+    def schedule_ext(self, pods, ext, seq=None):
+        pods = np.ascontiguousarray(pods, dtype=abi.POD_DTYPE)
+        ext = np.ascontiguousarray(ext, dtype=abi.POD_EXT_DTYPE)
+        assert len(ext) == len(pods)
+        if seq is None:
+            seq = np.arange(len(pods), dtype=np.uint64)
+        seq = np.ascontiguousarray(seq, dtype=np.uint64)
+        out = np.zeros(len(pods), abi.PLACEMENT_DTYPE)
+        eo = np.zeros(len(pods), abi.EXT_PLACEMENT_DTYPE)
+        self._chk(lib().gs_schedule_ext(self._h, abi.ptr(pods), abi.ptr(ext), len(pods), abi.ptr(seq), abi.ptr(out),
+                                        abi.ptr(eo)), "gs_schedule_ext")
+        return out, eo
+
     # ---- NodeNUMAResource state
     def register_topology(self, topo) -> int:
         t = abi.GsCpuTopology.from_buffer_copy(np.ascontiguousarray(np.atleast_1d(topo), abi.TOPOLOGY_DTYPE).tobytes())

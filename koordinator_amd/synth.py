@@ -70,6 +70,7 @@ class Cluster:
     assigned_ts: np.ndarray
     pods: np.ndarray         # POD_DTYPE[P] pending, in scheduling order
     numa: dict | None = None # NodeNUMAResource state: topologies, node_numa, allocations (make_numa)
+    ext: dict | None = None  # Reservation + DeviceShare state (make_ext)
 
     @property
     def num_nodes(self) -> int:
@@ -319,3 +320,125 @@ def load_into(engine, c: Cluster) -> None:
         engine.upsert_numa(recs)
         if len(c.numa["allocs"]):
             engine.update_allocations(c.numa["alloc_nodes"], c.numa["allocs"])
+
+
+def make_ext(c: Cluster, seed: int | None = None, gpu_node_pct: int = 20, gpus_per_node: int = 8,
+             rsv_node_pct: int = 5, owners: int = 40, owner_pod_pct: int = 10, required_pct: int = 2,
+             gpu_pod_pct: int = 10) -> Cluster:
+    """Reservation + DeviceShare state for config C5: GPU Device objects on gpu_node_pct% of the nodes
+    (8 GPUs of 80 GiB, partly used), 1-2 reservations on rsv_node_pct% of the nodes (owner groups, Default /
+    Restricted policies, some allocate-once, some already used by assigned pods, 10% with a reservation-order label),
+    and per-pod plugin inputs: owner-group pods (owner_pod_pct%, required_pct% with reservation affinity) and GPU
+    pods (gpu_pod_pct%: gpu-core + gpu-memory-ratio, nvidia.com/gpu, gpu-memory-ratio alone or gpu-memory, 1% with an
+    invalid gpu-core). NodeInfo (c.nodes) already holds the reserve pods and the pods assigned to them."""
+    s = Stream((BASE_SEED + 0x5C5) if seed is None else seed)
+    N = c.num_nodes
+    P = len(c.pods)
+    # ---- GPU devices
+    devs = np.zeros(N, abi.NODE_DEVICES_DTYPE)
+    gpu_node = s.randint(1, N, 0, 99) < gpu_node_pct
+    G = gpus_per_node
+    mem = 80 * GiB
+    used_steps = s.randint(2, N * G, 0, 7).reshape(N, G)            # used ratio in 0, 25, 50, 75, 100 (more idle)
+    used_ratio = np.array([0, 0, 0, 25, 50, 75, 100, 100], np.int64)[used_steps]
+    unhealthy = s.randint(3, N * G, 0, 99).reshape(N, G) == 0        # 1% of devices report zero resources
+    for i in np.nonzero(gpu_node)[0]:
+        d = devs[i]
+        d["has_device"] = 1
+        d["num_gpus"] = G
+        tot_core = tot_ratio = tot_mem = 0
+        u_core = u_ratio = u_mem = 0
+        for g in range(G):
+            gg = d["gpus"][g]
+            gg["minor"] = g
+            gg["has_info"] = 1
+            if unhealthy[i, g]:
+                continue
+            gg["total"] = (100, 100, mem)
+            ur = int(used_ratio[i, g])
+            gg["used"] = (ur, ur, ur * mem // 100)
+            tot_core += 100; tot_ratio += 100; tot_mem += mem
+            u_core += ur; u_ratio += ur; u_mem += ur * mem // 100
+        d["allocatable"] = (G, tot_core, tot_core, tot_mem, tot_ratio)
+        d["requested"] = (int((used_ratio[i] == 100).sum()), u_core, u_core, u_mem, u_ratio)
+    # ---- reservations
+    has_r = s.randint(4, N, 0, 99) < rsv_node_pct
+    nr = np.where(has_r, s.randint(5, N, 1, 2), 0)
+    R = int(nr.sum())
+    rnode = np.repeat(np.arange(N, dtype=np.uint32), nr)
+    rsv = np.zeros(R, abi.RESERVATION_DTYPE)
+    rsv["uid"] = s.u64(6, R) | np.uint64(1)
+    rsv["owner_key"] = (s.randint(7, R, 1, owners)).astype(np.uint64)
+    rsv["node"] = rnode
+    pol = s.randint(8, R, 0, 9)
+    rsv["allocate_policy"] = np.where(pol < 7, abi.RSV_POLICY["Default"], abi.RSV_POLICY["Restricted"])
+    rsv["order"] = np.where(s.randint(9, R, 0, 9) == 0, s.randint(10, R, 1, 1000), 0)
+    rsv["available"] = 1
+    rsv["unschedulable"] = (s.randint(11, R, 0, 49) == 0).astype(np.int32)
+    rsv["allocate_once"] = (s.randint(12, R, 0, 4) == 0).astype(np.int32)
+    rcpu = np.array([2000, 4000, 8000, 16000], np.int64)[s.randint(13, R, 0, 3)]
+    rmem = np.array([4, 8, 16, 32], np.int64)[s.randint(14, R, 0, 3)] * GiB
+    alloc = np.zeros((R, abi.GS_NUM_RES), np.int64)
+    alloc[:, 0], alloc[:, 1] = rcpu, rmem
+    rsv["allocatable"] = alloc
+    rsv["allocatable_mask"] = 3
+    rsv["resource_names_mask"] = 3
+    used = s.randint(15, R, 0, 9) < 3                                  # 30% already used by 1-2 assigned pods
+    npods = np.where(used, s.randint(16, R, 1, 2), 0)
+    allocated = np.zeros((R, abi.GS_NUM_RES), np.int64)
+    allocated[:, 0] = np.where(used, s.randint(17, R, 1, 10) * rcpu // 10 // 100 * 100, 0)
+    allocated[:, 1] = np.where(used, s.randint(18, R, 1, 10) * rmem // 10 // MiB * MiB, 0)
+    rsv["allocated"] = allocated
+    rsv["allocated_mask"] = np.where(used, 3, 0).astype(np.uint32)
+    rsv["assigned_pods"] = npods
+    # NodeInfo holds the reserve pod (its requests = Allocatable) and the pods assigned to the reservation
+    nodes = c.nodes
+    for k in range(R):
+        i = int(rnode[k])
+        for sl in (0, 1):
+            nodes["requested"][i, sl] += alloc[k, sl] + allocated[k, sl]
+            nodes["nonzero_requested"][i, sl] += alloc[k, sl] + allocated[k, sl]
+        nodes["pod_count"][i] += 1 + int(npods[k])
+    # ---- per-pod plugin inputs
+    ext = np.zeros(P, abi.POD_EXT_DTYPE)
+    kind = s.randint(20, P, 0, 99)
+    own = kind < owner_pod_pct
+    ext["reservation_owner"] = np.where(own, s.randint(21, P, 1, owners), 0).astype(np.uint64)
+    ext["reservation_required"] = (own & (s.randint(22, P, 0, 99) < required_pct * 100 // max(1, owner_pod_pct))).astype(np.int32)
+    gp = (kind >= owner_pod_pct) & (kind < owner_pod_pct + gpu_pod_pct)
+    gk = s.randint(23, P, 0, 99)
+    amount = np.array([25, 50, 100, 100, 200, 400], np.int64)[s.randint(24, P, 0, 5)]
+    nv = s.randint(25, P, 1, 2)
+    masks = np.zeros(P, np.uint32)
+    reqs = np.zeros((P, abi.GS_NUM_GPU_NAMES), np.int64)
+    CO, RA, ME, NV = (abi.GPU_NAMES["koordinator.sh/gpu-core"], abi.GPU_NAMES["koordinator.sh/gpu-memory-ratio"],
+                      abi.GPU_NAMES["koordinator.sh/gpu-memory"], abi.GPU_NAMES["nvidia.com/gpu"])
+    for p in np.nonzero(gp)[0]:
+        if gk[p] < 50:
+            reqs[p, CO] = reqs[p, RA] = amount[p]
+            masks[p] = (1 << CO) | (1 << RA)
+        elif gk[p] < 80:
+            reqs[p, NV] = nv[p]
+            masks[p] = 1 << NV
+        elif gk[p] < 90:
+            reqs[p, RA] = min(amount[p], 100)
+            masks[p] = 1 << RA
+        elif gk[p] < 99:
+            reqs[p, CO] = 50
+            reqs[p, ME] = 40 * GiB
+            masks[p] = (1 << CO) | (1 << ME)
+        else:
+            reqs[p, CO] = reqs[p, RA] = 150                          # invalid percentage: PreFilter fails
+            masks[p] = (1 << CO) | (1 << RA)
+    ext["gpu_request_mask"] = masks
+    ext["gpu_requests"] = reqs
+    c.ext = {"devices": devs, "reservations": rsv, "pod_ext": ext}
+    return c
+
+
+def load_ext_into(engine, c: Cluster, args) -> None:
+    """Push the Reservation / DeviceShare state of make_ext into an Engine / Oracle."""
+    engine.ext_configure(args)
+    engine.upsert_devices(c.ext["devices"])
+    if len(c.ext["reservations"]):
+        engine.upsert_reservations(c.ext["reservations"])

@@ -119,6 +119,10 @@ struct or_cluster {
   bool reverse_hint_order = false;
   uint32_t next_start = 0;   // [upstream] Scheduler.nextStartNodeIndex
   double phase_s[4] = {0, 0, 0, 0};   // or_phase_times
+  // Reservation + DeviceShare (the "extension plugins" section at the end of this file)
+  gs_ext_args ext{};
+  std::map<uint64_t, gs_reservation> reservations;   // reservationCache, by uid (reservation/cache.go)
+  std::vector<gs_node_devices> devices;               // nodeDeviceCache (has_device == 0: no Device object)
 };
 
 namespace {
@@ -630,6 +634,8 @@ or_cluster* or_create(const gs_config* cfg) {
   c->nodes.resize(cfg->num_nodes);
   c->numa.resize(cfg->num_nodes);
   c->numa_args = numa_args_of(cfg->numa);
+  c->devices.resize(cfg->num_nodes);
+  std::memset(c->devices.data(), 0, sizeof(gs_node_devices) * c->devices.size());
   return c;
 }
 
@@ -1038,6 +1044,689 @@ int or_schedule_replay(or_cluster* c, const gs_pod* pods, uint32_t npods, const 
 int or_phase_times(or_cluster* c, double out[4]) {
   if (!c || !out) return GS_EINVAL;
   for (int i = 0; i < 4; ++i) { out[i] = c->phase_s[i]; c->phase_s[i] = 0; }
+  return GS_OK;
+}
+
+}  // extern "C"
+
+// =============================================================================================
+// Extension plugins: Reservation + DeviceShare. Restated with
+// ResourceList-shaped maps keyed by resource slot / GPU resource name; reservations iterate in uid order
+// (the reference walks a Go map, reservation/cache.go forEachAvailableReservationOnNode — the harness fixes the
+// order, as for the NUMA hint providers).
+// =============================================================================================
+namespace {
+
+// corev1.ResourceList over the node resource slots (key presence kept: quotav1 semantics depend on it)
+struct RList {
+  std::map<int, int64_t> m;
+  int64_t get(int r) const { auto it = m.find(r); return it == m.end() ? 0 : it->second; }
+  bool has(int r) const { return m.count(r) != 0; }
+  bool is_zero() const { for (auto& kv : m) if (kv.second != 0) return false; return true; }   // quotav1.IsZero
+};
+RList rlist_of(const int64_t* v, uint32_t mask) {
+  RList l;
+  for (int r = 0; r < GS_NUM_RES; ++r)
+    if (mask & (1u << r)) l.m[r] = v[r];
+  return l;
+}
+RList rl_add(const RList& a, const RList& b) {   // quotav1.Add
+  RList o = a;
+  for (auto& kv : b.m) o.m[kv.first] = a.get(kv.first) + kv.second;
+  return o;
+}
+RList rl_sub(const RList& a, const RList& b) {   // quotav1.Subtract
+  RList o = a;
+  for (auto& kv : b.m) o.m[kv.first] = a.get(kv.first) - kv.second;
+  return o;
+}
+RList rl_sub_nonneg(const RList& a, const RList& b) {   // quotav1.SubtractWithNonNegativeResult
+  RList o;
+  for (auto& kv : a.m) o.m[kv.first] = std::max<int64_t>(0, kv.second - b.get(kv.first));
+  for (auto& kv : b.m)
+    if (!a.has(kv.first)) o.m[kv.first] = std::max<int64_t>(0, -kv.second);
+  return o;
+}
+RList rl_mask(const RList& a, uint32_t names) {   // quotav1.Mask
+  RList o;
+  for (auto& kv : a.m)
+    if (names & (1u << kv.first)) o.m[kv.first] = kv.second;
+  return o;
+}
+uint32_t rl_names(const RList& a) { uint32_t n = 0; for (auto& kv : a.m) n |= 1u << kv.first; return n; }
+RList rl_remove_zeros(const RList& a) { RList o; for (auto& kv : a.m) if (kv.second) o.m[kv.first] = kv.second; return o; }
+
+// [upstream] schedutil.GetNonzeroRequests of a container with these requests: cpu 100m / memory 200MiB when unset
+void nonzero_of(const RList& req, int64_t* cpu, int64_t* mem) {
+  *cpu = req.has(GS_RES_CPU) ? req.get(GS_RES_CPU) : 100;
+  *mem = req.has(GS_RES_MEMORY) ? req.get(GS_RES_MEMORY) : 200LL * 1024 * 1024;
+}
+
+// transformer.go:294-307 updateNodeInfoRequested (a one-container pod with `req`)
+void update_requested(gs_node& n, const RList& req, int64_t sign) {
+  for (auto& kv : req.m) n.requested[kv.first] += sign * kv.second;
+  int64_t c, m;
+  nonzero_of(req, &c, &m);
+  n.nonzero_requested[0] += sign * c;
+  n.nonzero_requested[1] += sign * m;
+}
+
+struct NodeRState {               // reservation/plugin.go nodeReservationState
+  std::vector<const gs_reservation*> matched;
+  gs_node restored{};             // NodeInfo after BeforePreFilter
+  gs_node pod_requested{};        // Requested after the unmatched trim (podRequested)
+  RList r_allocated;              // Σ matched Allocated
+  bool has = false;
+};
+
+// ---- DeviceShare (deviceshare/*.go), GPU device type ----
+struct GpuReq {                   // ConvertDeviceRequest result: keys of gs_gpu_res present
+  int64_t v[GS_NUM_GPU_RES] = {0, 0, 0};
+  uint32_t mask = 0;
+};
+// GetPodDeviceRequests (utils.go:232-252) for the GPU type: 0 ok (req->mask == 0: no GPU request), <0 invalid
+int gpu_pod_request(const gs_pod_ext& e, GpuReq* req) {
+  *req = GpuReq{};
+  const uint32_t m = e.gpu_request_mask & 0x1Fu;   // after RemoveZeros (the caller passes non-zero keys only)
+  if (!m) return 0;
+  for (int n = 0; n < GS_NUM_GPU_NAMES; ++n) {     // ValidatePercentageResource for koord gpu, core, ratio
+    if (!(m & (1u << n))) continue;
+    const int64_t q = e.gpu_requests[n];
+    if ((n == GS_GPU_NAME_KOORD_GPU || n == GS_GPU_NAME_CORE || n == GS_GPU_NAME_MEMORY_RATIO) && q > 100 && q % 100)
+      return -1;
+  }
+  const uint32_t NV = 1u << GS_GPU_NAME_NVIDIA, KG = 1u << GS_GPU_NAME_KOORD_GPU, CO = 1u << GS_GPU_NAME_CORE,
+                 ME = 1u << GS_GPU_NAME_MEMORY, RA = 1u << GS_GPU_NAME_MEMORY_RATIO;
+  // ValidDeviceResourceCombinations (utils.go:69-79) + ResourceCombinationsMapper (:89-144)
+  if (m == NV) {
+    req->v[GS_GPU_CORE] = req->v[GS_GPU_MEMORY_RATIO] = e.gpu_requests[GS_GPU_NAME_NVIDIA] * 100;
+    req->mask = 3;
+  } else if (m == KG) {
+    req->v[GS_GPU_CORE] = req->v[GS_GPU_MEMORY_RATIO] = e.gpu_requests[GS_GPU_NAME_KOORD_GPU];
+    req->mask = 3;
+  } else if (m == ME) {
+    req->v[GS_GPU_MEMORY] = e.gpu_requests[GS_GPU_NAME_MEMORY]; req->mask = 4;
+  } else if (m == RA) {
+    req->v[GS_GPU_MEMORY_RATIO] = e.gpu_requests[GS_GPU_NAME_MEMORY_RATIO]; req->mask = 2;
+  } else if (m == (CO | ME)) {
+    req->v[GS_GPU_CORE] = e.gpu_requests[GS_GPU_NAME_CORE];
+    req->v[GS_GPU_MEMORY] = e.gpu_requests[GS_GPU_NAME_MEMORY]; req->mask = 5;
+  } else if (m == (CO | RA)) {
+    req->v[GS_GPU_CORE] = e.gpu_requests[GS_GPU_NAME_CORE];
+    req->v[GS_GPU_MEMORY_RATIO] = e.gpu_requests[GS_GPU_NAME_MEMORY_RATIO]; req->mask = 3;
+  } else {
+    return -1;
+  }
+  return 0;
+}
+
+struct GpuRes {                   // one device's ResourceList over gs_gpu_res (all three keys, as a Device reports)
+  int64_t v[GS_NUM_GPU_RES] = {0, 0, 0};
+  bool zero() const { return !v[0] && !v[1] && !v[2]; }
+};
+struct NodeDev {                  // nodeDevice after filterNodeDevice (device_allocator.go:139-163): minors with info
+  std::map<int, GpuRes> total, free;
+};
+NodeDev filtered_node_device(const gs_node_devices& d) {
+  NodeDev o;
+  std::map<int, GpuRes> free_all;   // resetDeviceFree (device_cache.go:157-174)
+  bool all_zero = true;
+  for (int g = 0; g < d.num_gpus && g < GS_MAX_GPUS; ++g) {
+    GpuRes f;
+    for (int r = 0; r < GS_NUM_GPU_RES; ++r) f.v[r] = std::max<int64_t>(0, d.gpus[g].total[r] - d.gpus[g].used[r]);
+    free_all[d.gpus[g].minor] = f;
+    if (!f.zero()) all_zero = false;
+  }
+  if (all_zero) return o;           // nodeDevice.filter: freeDevices.isZero() -> the type is dropped (device_cache.go:361)
+  for (int g = 0; g < d.num_gpus && g < GS_MAX_GPUS; ++g) {
+    if (!d.gpus[g].has_info) continue;
+    GpuRes t;
+    for (int r = 0; r < GS_NUM_GPU_RES; ++r) t.v[r] = d.gpus[g].total[r];
+    o.total[d.gpus[g].minor] = t;
+    o.free[d.gpus[g].minor] = free_all[d.gpus[g].minor];
+  }
+  return o;
+}
+
+// GPUHandler.CalcDesiredRequestsAndCount (devicehandler_gpu.go:38-64): per-instance request (keys: mask) and count.
+// <0: UnschedulableAndUnresolvable (no GPU devices / no healthy GPU)
+int gpu_desired(const gs_node_devices& d, const GpuReq& pod, GpuReq* inst, int64_t* count) {
+  if (d.num_gpus <= 0) return -1;                       // len(deviceTotal[gpu]) == 0
+  int64_t total_mem = -1;                               // fillGPUTotalMem: the first healthy device (all GPUs of a
+  for (int g = 0; g < d.num_gpus && g < GS_MAX_GPUS; ++g) {   // node are one model: the same memory)
+    bool z = !d.gpus[g].total[0] && !d.gpus[g].total[1] && !d.gpus[g].total[2];
+    if (!z) { total_mem = d.gpus[g].total[GS_GPU_MEMORY]; break; }
+  }
+  if (total_mem < 0) return -2;
+  GpuReq r = pod;
+  if (r.mask & (1u << GS_GPU_MEMORY)) {
+    r.v[GS_GPU_MEMORY_RATIO] = (int64_t)((double)r.v[GS_GPU_MEMORY] / (double)total_mem * 100);   // memoryBytesToRatio
+  } else {
+    r.v[GS_GPU_MEMORY] = r.v[GS_GPU_MEMORY_RATIO] * total_mem / 100;                           // memoryRatioToBytes
+  }
+  r.mask |= (1u << GS_GPU_MEMORY) | (1u << GS_GPU_MEMORY_RATIO);
+  *count = 1;
+  const int64_t ratio = r.v[GS_GPU_MEMORY_RATIO];
+  if (ratio > 100 && ratio % 100 == 0) {
+    const int64_t n = ratio / 100;
+    *count = n;
+    GpuReq o;
+    o.v[GS_GPU_CORE] = r.v[GS_GPU_CORE] / n;
+    o.v[GS_GPU_MEMORY] = r.v[GS_GPU_MEMORY] / n;
+    o.v[GS_GPU_MEMORY_RATIO] = ratio / n;
+    o.mask = 7;
+    r = o;
+  }
+  *inst = r;
+  return 0;
+}
+
+bool le_request(const GpuReq& req, const GpuRes& free) {   // quotav1.LessThanOrEqual(request, free) over request keys
+  for (int r = 0; r < GS_NUM_GPU_RES; ++r)
+    if ((req.mask & (1u << r)) && req.v[r] > free.v[r]) return false;
+  return true;
+}
+
+int64_t ds_least(int64_t req, int64_t cap) { return cap == 0 || req > cap ? 0 : (cap - req) * kMaxNodeScore / cap; }
+int64_t ds_most(int64_t req, int64_t cap) {
+  if (cap == 0) return 0;
+  if (req > cap) req = cap;
+  return req * kMaxNodeScore / cap;
+}
+// resourceAllocationScorer (scoring.go:186-243): requested = total - free + request (total >= free)
+int64_t ds_scorer(const gs_ext_args& a, const int64_t* total, const int64_t* free, const GpuReq& req) {
+  int64_t ns = 0, ws = 0;
+  for (int r = 0; r < GS_NUM_GPU_RES; ++r) {
+    if (!a.device_weights[r]) continue;       // resourceToWeightMap keys
+    if (total[r] == 0) continue;
+    int64_t rq = total[r];
+    if (total[r] >= free[r]) rq = total[r] - free[r] + ((req.mask & (1u << r)) ? req.v[r] : 0);
+    ns += (a.device_scoring_type == GS_SCORING_MOST_ALLOCATED ? ds_most(rq, total[r]) : ds_least(rq, total[r])) *
+          a.device_weights[r];
+    ws += a.device_weights[r];
+  }
+  return ws ? ns / ws : 0;
+}
+
+// DeviceShare Filter (plugin.go:272-322) on a node with a Device object: 0 ok, else GS_EXT_FAIL_DEVICE
+uint32_t ds_filter(const gs_node_devices& d, const GpuReq& pod) {
+  GpuReq inst;
+  int64_t count;
+  if (gpu_desired(d, pod, &inst, &count) < 0) return GS_EXT_FAIL_DEVICE;
+  NodeDev nd = filtered_node_device(d);
+  int64_t ok = 0;                              // defaultAllocateDevices (device_allocator.go:397-467), no scorer
+  for (auto& kv : nd.free) {
+    if (kv.second.zero()) continue;
+    if (!le_request(inst, kv.second)) continue;
+    if (++ok == count) break;
+  }
+  return ok < count ? GS_EXT_FAIL_DEVICE : 0u;
+}
+
+// DeviceShare Score (scoring.go:34-89) -> allocator.score (device_allocator.go:513-536)
+int64_t ds_score(const gs_ext_args& a, const gs_node_devices& d, const GpuReq& pod) {
+  GpuReq inst;
+  int64_t count;
+  if (gpu_desired(d, pod, &inst, &count) < 0) return 0;
+  NodeDev nd = filtered_node_device(d);
+  if (nd.total.empty()) return 0;
+  int64_t tot[GS_NUM_GPU_RES] = {0, 0, 0}, fr[GS_NUM_GPU_RES] = {0, 0, 0};
+  for (auto& kv : nd.total)
+    for (int r = 0; r < GS_NUM_GPU_RES; ++r) tot[r] += kv.second.v[r];
+  for (auto& kv : nd.free)
+    for (int r = 0; r < GS_NUM_GPU_RES; ++r) fr[r] += kv.second.v[r];
+  return ds_scorer(a, tot, fr, inst);
+}
+
+// DeviceShare Reserve (plugin.go:377-430): defaultAllocateDevices with the scorer; minors sorted by device score
+// descending, then minor (sortDeviceResourcesByMinor, device_resources.go:187-208). Returns the minors.
+int ds_reserve(const gs_ext_args& a, gs_node_devices& d, const GpuReq& pod, gs_ext_placement* eo) {
+  GpuReq inst;
+  int64_t count;
+  if (gpu_desired(d, pod, &inst, &count) < 0) return -1;
+  NodeDev nd = filtered_node_device(d);
+  struct Pair { int minor; int64_t score; GpuRes free; };
+  std::vector<Pair> ps;
+  for (auto& kv : nd.free) ps.push_back({kv.first, ds_scorer(a, nd.total[kv.first].v, kv.second.v, inst), kv.second});
+  std::stable_sort(ps.begin(), ps.end(), [](const Pair& x, const Pair& y) {
+    if (x.score != y.score) return x.score > y.score;
+    return x.minor < y.minor;
+  });
+  std::vector<int> minors;
+  for (auto& p : ps) {
+    if (p.free.zero() || !le_request(inst, p.free)) continue;
+    minors.push_back(p.minor);
+    if ((int64_t)minors.size() == count) break;
+  }
+  if ((int64_t)minors.size() < count) return -1;
+  for (int mnr : minors) {                     // nodeDevice.updateCacheUsed -> updateDeviceUsed (device_cache.go:176-201)
+    for (int g = 0; g < d.num_gpus; ++g) {
+      if (d.gpus[g].minor != mnr) continue;
+      for (int r = 0; r < GS_NUM_GPU_RES; ++r)
+        if (inst.mask & (1u << r)) d.gpus[g].used[r] += inst.v[r];
+    }
+    eo->gpu_minor_mask |= 1u << mnr;
+  }
+  eo->gpu_count = (int32_t)count;
+  for (int r = 0; r < GS_NUM_GPU_RES; ++r) eo->gpu_per_instance[r] = (inst.mask & (1u << r)) ? inst.v[r] : 0;
+  return 0;
+}
+
+// ---- Reservation (reservation/*.go) ----
+bool rsv_usable(const gs_reservation& r) {   // transformer.go:102-111
+  if (!r.available) return false;
+  if (r.allocate_once && r.assigned_pods > 0) return false;
+  return true;
+}
+RList rsv_allocatable(const gs_reservation& r) { return rlist_of(r.allocatable, r.allocatable_mask); }
+RList rsv_allocated(const gs_reservation& r) { return rlist_of(r.allocated, r.allocated_mask); }
+
+// scoreReservation (scoring.go:183-203): MostAllocated over the non-zero Allocatable, milli values
+int64_t score_reservation(const gs_pod& pod, const gs_reservation& r, const RList& allocated) {
+  RList requested = rl_add(rlist_of(pod.requests, pod.request_mask), allocated);
+  RList resources = rl_remove_zeros(rsv_allocatable(r));
+  const int64_t w = (int64_t)resources.m.size();
+  if (w <= 0) return 0;
+  int64_t s = 0;
+  for (auto& kv : resources.m) {
+    const int64_t req = requested.get(kv.first);
+    if (req <= kv.second) s += kMaxNodeScore * milli_value(kv.first, req) / milli_value(kv.first, kv.second);
+  }
+  return s / w;
+}
+
+// fitsNode (plugin.go:444-496) with preemptible = 0: the insufficient resource count
+int fits_node(const gs_pod& pod, const gs_node& restored, const NodeRState& ns, const gs_reservation* r) {
+  int bad = 0;
+  if (restored.pod_count - (int64_t)ns.matched.size() + 1 > restored.allowed_pod_number) ++bad;
+  const uint32_t scalars = pod.request_mask & GS_SCALAR_RES_MASK;
+  if (!pod.requests[0] && !pod.requests[1] && !pod.requests[2] && !scalars) return bad;
+  RList rem = r ? rl_sub(rsv_allocatable(*r), rsv_allocated(*r)) : RList{};
+  for (int s = 0; s < GS_NUM_RES; ++s) {
+    if (s >= 3 && !(scalars & (1u << s))) continue;
+    if (s == GS_RES_RESERVED) continue;
+    const int64_t avail = restored.allocatable[s] - (ns.pod_requested.requested[s] - rem.get(s) - ns.r_allocated.get(s));
+    if (pod.requests[s] > avail) ++bad;
+  }
+  return bad;
+}
+
+// filterWithReservations (plugin.go:377-440): true = some reservation satisfies the pod
+bool filter_with_reservations(const gs_pod& pod, const NodeRState& ns, const std::vector<const gs_reservation*>& rs) {
+  const uint32_t pod_names = pod.request_mask;
+  for (const gs_reservation* r : rs) {
+    if (!(r->resource_names_mask & pod_names)) continue;
+    const bool node_fits = fits_node(pod, ns.restored, ns, r) == 0;
+    if (r->allocate_policy == GS_RSV_POLICY_DEFAULT || r->allocate_policy == GS_RSV_POLICY_ALIGNED) {
+      if (node_fits) return true;
+    } else if (r->allocate_policy == GS_RSV_POLICY_RESTRICTED) {
+      RList allocated = rl_mask(rsv_allocated(*r), r->resource_names_mask);
+      RList remained = rl_sub_nonneg(rsv_allocatable(*r), allocated);
+      RList req = rl_mask(rlist_of(pod.requests, pod.request_mask), r->resource_names_mask);
+      bool fits = true;
+      for (auto& kv : req.m)
+        if (kv.second > remained.get(kv.first)) fits = false;
+      if (fits && node_fits) return true;
+    }
+  }
+  return false;
+}
+
+// NominateReservation (nominator.go:140-190): filter each matched reservation (FilterReservation, plugin.go:503-530),
+// then the lowest order label, else the highest ScoreReservation (ties: the first in reservation order)
+const gs_reservation* nominate(const gs_pod& pod, const NodeRState& ns) {
+  std::vector<const gs_reservation*> ok;
+  for (const gs_reservation* r : ns.matched) {
+    if (r->allocate_once && r->assigned_pods > 0) continue;
+    if (!filter_with_reservations(pod, ns, {r})) continue;
+    ok.push_back(r);
+  }
+  if (ok.empty()) return nullptr;
+  const gs_reservation* best = nullptr;
+  int64_t order = INT64_MAX;
+  for (const gs_reservation* r : ok)   // findMostPreferredReservationByOrder (scoring.go:162-181)
+    if (r->order != 0 && order > r->order) { order = r->order; best = r; }
+  if (best) return best;
+  int64_t bs = INT64_MIN;
+  for (const gs_reservation* r : ok) {
+    const int64_t s = score_reservation(pod, *r, rsv_allocated(*r));
+    if (s > bs) { bs = s; best = r; }
+  }
+  return best;
+}
+
+// [upstream] pluginhelper.DefaultNormalizeScore(MaxNodeScore, false) / frameworkext.DefaultReservationNormalizeScore
+void default_normalize(int64_t max_priority, bool reverse, std::vector<int64_t>& s) {
+  int64_t mx = 0;
+  for (int64_t v : s) mx = std::max(mx, v);
+  if (mx == 0) {
+    if (reverse) for (auto& v : s) v = max_priority;
+    return;
+  }
+  for (auto& v : s) {
+    v = max_priority * v / mx;
+    if (reverse) v = max_priority - v;
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+void or_ext_args_default(gs_ext_args* a) {
+  std::memset(a, 0, sizeof(*a));
+  a->enabled = GS_EXT_DEVICESHARE | GS_EXT_RESERVATION;
+  a->device_scoring_type = GS_SCORING_LEAST_ALLOCATED;
+  a->device_weights[GS_GPU_MEMORY_RATIO] = 1;
+  a->weight_deviceshare = 1;
+  a->weight_reservation = 5000;
+}
+
+int or_ext_configure(or_cluster* c, const gs_ext_args* a) {
+  if (!c || !a) return GS_EINVAL;
+  c->ext = *a;
+  return GS_OK;
+}
+
+int or_node_devices_upsert(or_cluster* c, const uint32_t* idx, const gs_node_devices* d, uint32_t n) {
+  if (!c || (n && !d)) return GS_EINVAL;
+  for (uint32_t i = 0; i < n; ++i) {
+    const uint32_t k = idx ? idx[i] : i;
+    if (k >= c->devices.size() || d[i].num_gpus < 0 || d[i].num_gpus > GS_MAX_GPUS) return GS_EINVAL;
+    c->devices[k] = d[i];
+  }
+  return GS_OK;
+}
+
+int or_node_devices_get(or_cluster* c, uint32_t node, gs_node_devices* out) {
+  if (!c || !out || node >= c->devices.size()) return GS_EINVAL;
+  *out = c->devices[node];
+  return GS_OK;
+}
+
+int or_reservations_upsert(or_cluster* c, const gs_reservation* r, uint32_t n) {
+  if (!c || (n && !r)) return GS_EINVAL;
+  for (uint32_t i = 0; i < n; ++i) {
+    if (r[i].node >= c->nodes.size()) return GS_EINVAL;
+    c->reservations[r[i].uid] = r[i];
+  }
+  return GS_OK;
+}
+
+int or_reservations_remove(or_cluster* c, const uint64_t* uids, uint32_t n) {
+  if (!c || (n && !uids)) return GS_EINVAL;
+  for (uint32_t i = 0; i < n; ++i) c->reservations.erase(uids[i]);
+  return GS_OK;
+}
+
+int or_reservation_get(or_cluster* c, uint64_t uid, gs_reservation* out) {
+  if (!c || !out) return GS_EINVAL;
+  auto it = c->reservations.find(uid);
+  if (it == c->reservations.end()) return 0;
+  *out = it->second;
+  return 1;
+}
+
+int64_t or_score_reservation(const gs_pod* pod, const gs_reservation* r) {
+  return score_reservation(*pod, *r, rsv_allocated(*r));
+}
+
+int or_default_normalize_score(int64_t max_priority, int reverse, int64_t* scores, uint32_t n) {
+  std::vector<int64_t> s(scores, scores + n);
+  default_normalize(max_priority, reverse != 0, s);
+  for (uint32_t i = 0; i < n; ++i) scores[i] = s[i];
+  return GS_OK;
+}
+
+// Reservation PreScore + Score of one pod over `nnodes` nodes: node k's matched reservations are rsv[off[k]..off[k+1]),
+// its restored NodeInfo nodes[k] and its podRequested view pod_requested[k] (fitsNode). raw[k] = Score (1000 for
+// PreScore's preferred node, else the nominated reservation's scoreReservation, else 0).
+int or_reservation_node_scores(const gs_pod* pod, const gs_reservation* rsv, const uint32_t* off, uint32_t nnodes,
+                               const gs_node* nodes, const gs_node* pod_requested, int64_t* raw) {
+  if (!pod || !off || !nodes || !pod_requested || !raw) return GS_EINVAL;
+  int preferred = -1;
+  int64_t sel = INT64_MAX;
+  std::vector<NodeRState> ns(nnodes);
+  for (uint32_t k = 0; k < nnodes; ++k) {
+    ns[k].restored = nodes[k];
+    ns[k].pod_requested = pod_requested[k];
+    int64_t order = INT64_MAX;
+    for (uint32_t j = off[k]; j < off[k + 1]; ++j) {
+      ns[k].matched.push_back(&rsv[j]);
+      ns[k].r_allocated = rl_add(ns[k].r_allocated, rsv_allocated(rsv[j]));
+      if (rsv[j].order != 0 && order > rsv[j].order) order = rsv[j].order;
+    }
+    if (order != INT64_MAX && sel > order) { sel = order; preferred = (int)k; }
+  }
+  for (uint32_t k = 0; k < nnodes; ++k) {
+    raw[k] = 0;
+    if ((int)k == preferred) { raw[k] = 1000; continue; }
+    const gs_reservation* r = ns[k].matched.empty() ? nullptr : nominate(*pod, ns[k]);
+    if (r) raw[k] = score_reservation(*pod, *r, rsv_allocated(*r));
+  }
+  return GS_OK;
+}
+
+// DeviceShare Score of one pod on one node (PreFilter conversion + allocator.score)
+int64_t or_device_score(const gs_ext_args* a, const gs_node_devices* d, const gs_pod_ext* e) {
+  GpuReq q;
+  if (gpu_pod_request(*e, &q) < 0 || !q.mask || !d->has_device) return 0;
+  return ds_score(*a, *d, q);
+}
+
+// DeviceShare Filter of one pod on one node: 0 = pass, else GS_EXT_FAIL_DEVICE / GS_EXT_FAIL_POD
+uint32_t or_device_filter(const gs_node_devices* d, const gs_pod_ext* e) {
+  GpuReq q;
+  if (gpu_pod_request(*e, &q) < 0) return GS_EXT_FAIL_POD;
+  if (!q.mask || !d->has_device) return 0;
+  return ds_filter(*d, q);
+}
+
+int64_t or_device_score_node(const gs_ext_args* a, const int64_t* total, const int64_t* free, const int64_t* request,
+                             uint32_t request_mask) {
+  GpuReq q;
+  for (int r = 0; r < GS_NUM_GPU_RES; ++r) q.v[r] = request[r];
+  q.mask = request_mask;
+  return ds_scorer(*a, total, free, q);
+}
+
+// scheduleOne with the extension plugins (one pod at a time, every node checked, no replay).
+int or_schedule_ext(or_cluster* c, const gs_pod* pods, const gs_pod_ext* ext, uint32_t npods, const uint64_t* seq,
+                    gs_placement* out, gs_ext_placement* ext_out) {
+  if (!c || !out || (npods && !pods)) return GS_EINVAL;
+  if (c->cfg.sample_nodes) return GS_EUNSUPPORTED;
+  const int N = (int)c->nodes.size();
+  for (int n = 0; n < N; ++n)
+    if (!c->nodes[n].has_node) return GS_ESTATE;
+  const uint32_t en = c->cfg.enabled;
+  const bool ds_on = c->ext.enabled & GS_EXT_DEVICESHARE, rs_on = c->ext.enabled & GS_EXT_RESERVATION;
+  std::vector<int64_t> base(N), dsr(N), rsr(N);
+  std::vector<uint8_t> feasible(N);
+  std::vector<orn::Hint> affinity(N);
+  std::vector<NodeRState> rstate(N);
+  std::vector<const gs_reservation*> nominated(N);
+  // reservations by node, uid order
+  std::vector<std::vector<gs_reservation*>> by_node(N);
+  for (auto& kv : c->reservations) by_node[kv.second.node].push_back(&kv.second);
+  for (uint32_t p = 0; p < npods; ++p) {
+    const gs_pod& pod = pods[p];
+    gs_pod_ext e{};
+    if (ext) e = ext[p];
+    gs_placement& o = out[p];
+    gs_ext_placement eo{};
+    o = gs_placement{-1, 0, 0, 0, 0};
+    GpuReq gpu;
+    if (ds_on && gpu_pod_request(e, &gpu) < 0) {   // DeviceShare PreFilter: UnschedulableAndUnresolvable
+      eo.fail_code = GS_EXT_FAIL_POD;
+      if (ext_out) ext_out[p] = eo;
+      continue;
+    }
+    if (!ds_on) gpu = GpuReq{};
+    const bool gpu_pod = gpu.mask != 0;
+    const uint32_t gpu_names = gpu_pod ? (e.gpu_request_mask & 0x1Fu) : 0u;
+    const orn::PreState st = orn::prefilter(c->numa_args, pod);
+    // Reservation BeforePreFilter (transformer.go:50-235)
+    bool any_state = false;
+    for (int n = 0; n < N; ++n) {
+      NodeRState& ns = rstate[n];
+      ns = NodeRState{};
+      ns.restored = c->nodes[n].node;
+      if (!rs_on) continue;
+      std::vector<const gs_reservation*> unmatched;
+      for (const gs_reservation* r : by_node[n]) {
+        if (!rsv_usable(*r)) continue;
+        if (!r->unschedulable && e.reservation_owner != 0 && r->owner_key == e.reservation_owner) ns.matched.push_back(r);
+        else if (r->assigned_pods > 0) unmatched.push_back(r);
+      }
+      if (ns.matched.empty() && unmatched.empty()) continue;
+      if (e.reservation_required && ns.matched.empty()) continue;
+      for (const gs_reservation* r : unmatched) {   // restoreUnmatchedReservations (:266-292)
+        update_requested(ns.restored, rsv_allocatable(*r), -1);
+        RList rem = rl_sub_nonneg(rsv_allocatable(*r), rsv_allocated(*r));
+        if (!rem.is_zero()) update_requested(ns.restored, rem, +1);
+      }
+      ns.pod_requested = ns.restored;
+      for (const gs_reservation* r : ns.matched) {   // restoreMatchedReservation (:241-264): RemovePod(reservePod)
+        update_requested(ns.restored, rsv_allocatable(*r), -1);
+        ns.restored.pod_count -= 1;
+        ns.r_allocated = rl_add(ns.r_allocated, rsv_allocated(*r));
+      }
+      ns.has = true;
+      any_state = true;
+    }
+    if (rs_on && e.reservation_required && !any_state) {   // PreFilter: ErrReasonReservationAffinity
+      if (ext_out) ext_out[p] = eo;
+      continue;
+    }
+    // Filter
+    std::vector<int> fl;
+    for (int n = 0; n < N; ++n) {
+      const NodeState& s = c->nodes[n];
+      const gs_node& nd = rstate[n].restored;
+      uint32_t code = 0;
+      if (en & GS_ENABLE_FIT_FILTER) {
+        code |= fit_filter(pod, nd);
+        if (gpu_pod) {   // the GPU names are scalar resources of the pod ([upstream] fit.go fitsRequest)
+          const gs_node_devices& d = c->devices[n];
+          if (!pod.requests[0] && !pod.requests[1] && !pod.requests[2] && !(pod.request_mask & GS_SCALAR_RES_MASK)) {
+            // fit_filter returned early on an all-zero request: the scalar GPU names make it non-zero
+            if (pod.requests[0] > nd.allocatable[0] - nd.requested[0]) code |= GS_FAIL_FIT_CPU;
+            if (pod.requests[1] > nd.allocatable[1] - nd.requested[1]) code |= GS_FAIL_FIT_MEMORY;
+            if (pod.requests[2] > nd.allocatable[2] - nd.requested[2]) code |= GS_FAIL_FIT_EPHEMERAL;
+          }
+          for (int g = 0; g < GS_NUM_GPU_NAMES; ++g) {
+            if (!(gpu_names & (1u << g))) continue;
+            const int64_t a = d.allocatable[g], r = d.requested[g];
+            if (e.gpu_requests[g] > a - r) code |= GS_FAIL_FIT_SCALAR;
+          }
+        }
+      }
+      if (en & GS_ENABLE_LA_FILTER) code |= loadaware_filter(*c, pod, s);
+      affinity[n] = orn::Hint{};
+      if (!code && (en & GS_ENABLE_NUMA_FILTER)) {
+        bool has = false;
+        int reason = orn::filter(c->numa_args, st, c->numa[n], node_view(nd), &affinity[n], &has, c->reverse_hint_order);
+        if (!has) affinity[n] = orn::Hint{};
+        code |= (uint32_t)reason << GS_FAIL_NUMA_SHIFT;
+      }
+      if (!code && gpu_pod && c->devices[n].has_device) code |= ds_filter(c->devices[n], gpu);
+      if (!code && rs_on) {   // Reservation Filter (plugin.go:311-375), non-reserve pods
+        const NodeRState& ns = rstate[n];
+        if (ns.matched.empty()) {
+          if (e.reservation_required) code |= GS_EXT_FAIL_RESERVATION;
+        } else if (e.reservation_required && !filter_with_reservations(pod, ns, ns.matched)) {
+          code |= GS_EXT_FAIL_RESERVATION;
+        }
+      }
+      feasible[n] = code == 0;
+      if (!code) fl.push_back(n);
+    }
+    o.feasible = (uint32_t)fl.size();
+    if (fl.empty()) {
+      if (ext_out) ext_out[p] = eo;
+      continue;
+    }
+    // PreScore (Reservation, scoring.go:42-101): nominations + the preferred node (lowest order, first in feasible order)
+    int preferred = -1;
+    int64_t sel_order = INT64_MAX;
+    for (int n : fl) {
+      nominated[n] = nullptr;
+      const NodeRState& ns = rstate[n];
+      if (!rs_on || ns.matched.empty()) continue;
+      int64_t order = INT64_MAX;
+      for (const gs_reservation* r : ns.matched)
+        if (r->order != 0 && order > r->order) order = r->order;
+      if (order != INT64_MAX && order != 0 && sel_order > order) { sel_order = order; preferred = n; }
+      nominated[n] = nominate(pod, ns);
+    }
+    // Score + NormalizeScore + weights
+    const int F = (int)fl.size();
+    std::vector<int64_t> dsl(F), rsl(F);
+    for (int i = 0; i < F; ++i) {
+      const int n = fl[i];
+      const gs_node& nd = rstate[n].restored;
+      PairResult r{0, 0, 0, 0};
+      if (en & GS_ENABLE_FIT_SCORE) r.fit = fit_score(c->cfg.fit, pod, nd);
+      if (en & GS_ENABLE_LA_SCORE) r.la = loadaware_score(*c, pod, c->nodes[n]);
+      if (en & GS_ENABLE_NUMA_SCORE) r.numa = orn::score(c->numa_args, st, c->numa[n], node_view(nd), affinity[n]);
+      base[n] = weighted_total(*c, r);
+      dsl[i] = (gpu_pod && c->devices[n].has_device) ? ds_score(c->ext, c->devices[n], gpu) : 0;
+      int64_t rs = 0;
+      if (rs_on) {
+        if (n == preferred) rs = 1000;   // mostPreferredScore
+        else if (nominated[n]) rs = score_reservation(pod, *nominated[n], rsv_allocated(*nominated[n]));
+      }
+      rsl[i] = rs;
+    }
+    if (ds_on) default_normalize(kMaxNodeScore, false, dsl);
+    if (rs_on) default_normalize(kMaxNodeScore, false, rsl);
+    std::vector<int64_t> total(F);
+    for (int i = 0; i < F; ++i)
+      total[i] = base[fl[i]] + (ds_on ? dsl[i] * c->ext.weight_deviceshare : 0) +
+                 (rs_on ? rsl[i] * c->ext.weight_reservation : 0);
+    // selectHost
+    TieBreakRand rnd(c->cfg.seed, seq ? seq[p] : p);
+    int si = 0;
+    int64_t mx = total[0], cnt = 1;
+    for (int i = 1; i < F; ++i) {
+      if (total[i] > mx) { mx = total[i]; si = i; cnt = 1; }
+      else if (total[i] == mx) { ++cnt; if (rnd.intn(cnt) == 0) si = i; }
+    }
+    const int selected = fl[si];
+    o.node = selected; o.score = mx; o.ties = (uint32_t)cnt;
+    eo.deviceshare_score = (int32_t)dsl[si];
+    eo.reservation_score = (int32_t)rsl[si];
+    // Reserve: NodeNUMAResource, DeviceShare, Reservation; then assume
+    if (en & (GS_ENABLE_NUMA_FILTER | GS_ENABLE_NUMA_SCORE)) {
+      orn::PodAllocation pa;
+      if (orn::reserve(c->numa_args, st, c->numa[selected], pod, affinity[selected], &pa) != 0) return GS_ESTATE;
+      if (!pa.numa.empty()) o.flags |= GS_PLACED_NUMA;
+      if (!pa.cpus.empty()) o.flags |= GS_PLACED_CPUSET;
+    }
+    gs_node_devices& dv = c->devices[selected];
+    if (gpu_pod && dv.has_device && ds_reserve(c->ext, dv, gpu, &eo) != 0) return GS_ESTATE;
+    if (rs_on) {
+      const gs_reservation* nr = nominated[selected];
+      if (nr) {   // reservationCache.assumePod -> ReservationInfo.AddAssignedPod (reservation_info.go:379-388)
+        gs_reservation& rr = c->reservations[nr->uid];
+        RList add = rl_mask(rlist_of(pod.requests, pod.request_mask), rr.resource_names_mask);
+        RList na = rl_add(rsv_allocated(rr), add);
+        for (auto& kv : na.m) rr.allocated[kv.first] = kv.second;
+        rr.allocated_mask |= rl_names(na);
+        rr.assigned_pods += 1;
+        eo.reservation_uid = rr.uid;
+      }
+    }
+    gs_node& nd = c->nodes[selected].node;   // NodeInfo.AddPod
+    for (int r = 0; r < GS_NUM_RES; ++r) nd.requested[r] += pod.requests[r];
+    nd.nonzero_requested[0] += pod.nonzero_requests[0];
+    nd.nonzero_requested[1] += pod.nonzero_requests[1];
+    nd.pod_count += 1;
+    for (int g = 0; g < GS_NUM_GPU_NAMES; ++g)
+      if (gpu_names & (1u << g)) dv.requested[g] += e.gpu_requests[g];
+    if (!(pod.flags & GS_POD_TERMINATED)) c->nodes[selected].assigned[pod.uid] = AssignInfo{c->now, pod};
+    if (ext_out) ext_out[p] = eo;
+  }
   return GS_OK;
 }
 

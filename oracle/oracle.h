@@ -70,6 +70,26 @@ int or_phase_times(or_cluster* c, double out[4]);
 /* the selectHost tie-break stream: Intn(cnt) of pod stream `seq` (see oracle.cpp TieBreakRand) */
 int32_t or_tiebreak_intn(uint64_t seed, uint64_t seq, int64_t cnt);
 
+/* Reservation + DeviceShare (mirrors gs_ext_configure / gs_node_devices_* / gs_reservations_* / gs_schedule_ext) */
+void or_ext_args_default(gs_ext_args* a);
+int or_ext_configure(or_cluster* c, const gs_ext_args* a);
+int or_node_devices_upsert(or_cluster* c, const uint32_t* idx, const gs_node_devices* d, uint32_t n);
+int or_node_devices_get(or_cluster* c, uint32_t node, gs_node_devices* out);
+int or_reservations_upsert(or_cluster* c, const gs_reservation* r, uint32_t n);
+int or_reservations_remove(or_cluster* c, const uint64_t* uids, uint32_t n);
+int or_reservation_get(or_cluster* c, uint64_t uid, gs_reservation* out);
+int or_schedule_ext(or_cluster* c, const gs_pod* pods, const gs_pod_ext* ext, uint32_t npods, const uint64_t* seq,
+                    gs_placement* out, gs_ext_placement* ext_out);
+/* plugin-level restatements for the reference's unit vectors */
+int64_t or_score_reservation(const gs_pod* pod, const gs_reservation* r);   /* scoreReservation (scoring.go:183-203) */
+int or_default_normalize_score(int64_t max_priority, int reverse, int64_t* scores, uint32_t n);
+int or_reservation_node_scores(const gs_pod* pod, const gs_reservation* rsv, const uint32_t* off, uint32_t nnodes,
+                               const gs_node* nodes, const gs_node* pod_requested, int64_t* raw);
+int64_t or_device_score(const gs_ext_args* a, const gs_node_devices* d, const gs_pod_ext* e);
+uint32_t or_device_filter(const gs_node_devices* d, const gs_pod_ext* e);
+int64_t or_device_score_node(const gs_ext_args* a, const int64_t* total, const int64_t* free, const int64_t* request,
+                             uint32_t request_mask);   /* resourceAllocationScorer.scoreNode (deviceshare/scoring.go:213-243) */
+
 #ifdef __cplusplus
 }
 #endif

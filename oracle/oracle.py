@@ -56,6 +56,20 @@ def _load() -> C.CDLL:
         "or_take_cpus_test": (C.c_int, [C.c_int] * 5 + [P, P, P] + [C.c_int] * 4 + [P]),
         "or_policy_merge": (C.c_int, [C.c_int, C.c_uint64, C.c_int, P, P, P, P, P, P, P]),
         "or_iterate_bitmasks": (C.c_int, [P, C.c_int, P, C.c_int]),
+        "or_ext_args_default": (None, [C.POINTER(abi.GsExtArgs)]),
+        "or_ext_configure": (C.c_int, [P, C.POINTER(abi.GsExtArgs)]),
+        "or_node_devices_upsert": (C.c_int, [P, P, P, C.c_uint32]),
+        "or_node_devices_get": (C.c_int, [P, C.c_uint32, P]),
+        "or_reservations_upsert": (C.c_int, [P, P, C.c_uint32]),
+        "or_reservations_remove": (C.c_int, [P, P, C.c_uint32]),
+        "or_reservation_get": (C.c_int, [P, C.c_uint64, P]),
+        "or_schedule_ext": (C.c_int, [P, P, P, C.c_uint32, P, P, P]),
+        "or_score_reservation": (C.c_int64, [P, P]),
+        "or_default_normalize_score": (C.c_int, [C.c_int64, C.c_int, P, C.c_uint32]),
+        "or_reservation_node_scores": (C.c_int, [P, P, P, C.c_uint32, P, P, P]),
+        "or_device_score": (C.c_int64, [C.POINTER(abi.GsExtArgs), P, P]),
+        "or_device_filter": (C.c_uint32, [P, P]),
+        "or_device_score_node": (C.c_int64, [C.POINTER(abi.GsExtArgs), P, P, P, C.c_uint32]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -215,6 +229,46 @@ class Oracle:
     def next_start_node_index(self) -> int:
         return int(lib().or_next_start_node_index(self._h))
 
+    # ---- Reservation + DeviceShare
+    def ext_configure(self, args: abi.GsExtArgs):
+        _chk(lib().or_ext_configure(self._h, C.byref(args)), "ext_configure")
+
+    def upsert_devices(self, devs, idx=None):
+        devs = np.ascontiguousarray(devs, dtype=abi.NODE_DEVICES_DTYPE)
+        if idx is not None:
+            idx = np.ascontiguousarray(idx, dtype=np.uint32)
+        _chk(lib().or_node_devices_upsert(self._h, abi.ptr(idx), abi.ptr(devs), len(devs)), "node_devices_upsert")
+
+    def devices(self, node: int):
+        out = np.zeros(1, abi.NODE_DEVICES_DTYPE)
+        _chk(lib().or_node_devices_get(self._h, node, abi.ptr(out)), "node_devices_get")
+        return out[0]
+
+    def upsert_reservations(self, rsv):
+        rsv = np.ascontiguousarray(rsv, dtype=abi.RESERVATION_DTYPE)
+        _chk(lib().or_reservations_upsert(self._h, abi.ptr(rsv), len(rsv)), "reservations_upsert")
+
+    def remove_reservations(self, uids):
+        uids = np.ascontiguousarray(uids, dtype=np.uint64)
+        _chk(lib().or_reservations_remove(self._h, abi.ptr(uids), len(uids)), "reservations_remove")
+
+    def reservation(self, uid: int):
+        out = np.zeros(1, abi.RESERVATION_DTYPE)
+        rc = lib().or_reservation_get(self._h, uid, abi.ptr(out))
+        return out[0] if rc == 1 else None
+
+    def schedule_ext(self, pods, ext, seq=None):
+        pods = np.ascontiguousarray(pods, dtype=abi.POD_DTYPE)
+        ext = np.ascontiguousarray(ext, dtype=abi.POD_EXT_DTYPE)
+        if seq is None:
+            seq = np.arange(len(pods), dtype=np.uint64)
+        seq = np.ascontiguousarray(seq, dtype=np.uint64)
+        out = np.zeros(len(pods), abi.PLACEMENT_DTYPE)
+        eo = np.zeros(len(pods), abi.EXT_PLACEMENT_DTYPE)
+        _chk(lib().or_schedule_ext(self._h, abi.ptr(pods), abi.ptr(ext), len(pods), abi.ptr(seq), abi.ptr(out),
+                                   abi.ptr(eo)), "schedule_ext")
+        return out, eo
+
     def schedule_replay(self, pods, given, seq=None, nthreads: int = 1):
         """Pods with given[i] >= 0 are placed on that node (Filter there for the affinity, Reserve, assume);
         given[i] == -2 replays a FitError (nothing assumed); given[i] == -1 runs scheduleOne on the replayed state."""
@@ -228,6 +282,60 @@ class Oracle:
         _chk(lib().or_schedule_replay(self._h, abi.ptr(pods), len(pods), abi.ptr(seq), abi.ptr(given),
                                       abi.ptr(out), int(nthreads)), "schedule_replay")
         return out
+
+
+def ext_args_default() -> abi.GsExtArgs:
+    a = abi.GsExtArgs()
+    lib().or_ext_args_default(C.byref(a))
+    return a
+
+
+def score_reservation(pod, rsv) -> int:
+    """scoreReservation (reservation/scoring.go:183-203)."""
+    p = np.ascontiguousarray(np.atleast_1d(pod), abi.POD_DTYPE)
+    r = np.ascontiguousarray(np.atleast_1d(rsv), abi.RESERVATION_DTYPE)
+    return int(lib().or_score_reservation(abi.ptr(p), abi.ptr(r)))
+
+
+def default_normalize_score(max_priority: int, reverse: bool, scores) -> list[int]:
+    s = np.ascontiguousarray(scores, dtype=np.int64)
+    _chk(lib().or_default_normalize_score(max_priority, int(reverse), abi.ptr(s), len(s)), "normalize")
+    return s.tolist()
+
+
+def reservation_node_scores(pod, rsv_per_node, nodes, pod_requested) -> list[int]:
+    """Reservation PreScore + Score (reservation/scoring.go:42-160, nominator.go:140-190) per node."""
+    p = np.ascontiguousarray(np.atleast_1d(pod), abi.POD_DTYPE)
+    flat = [r for rs in rsv_per_node for r in rs]
+    rs = np.ascontiguousarray(np.array(flat, dtype=abi.RESERVATION_DTYPE) if flat else np.zeros(1, abi.RESERVATION_DTYPE))
+    off = np.zeros(len(rsv_per_node) + 1, np.uint32)
+    off[1:] = np.cumsum([len(x) for x in rsv_per_node])
+    nd = np.ascontiguousarray(nodes, abi.NODE_DTYPE)
+    pr = np.ascontiguousarray(pod_requested, abi.NODE_DTYPE)
+    raw = np.zeros(len(rsv_per_node), np.int64)
+    _chk(lib().or_reservation_node_scores(abi.ptr(p), abi.ptr(rs), abi.ptr(off), len(rsv_per_node), abi.ptr(nd),
+                                          abi.ptr(pr), abi.ptr(raw)), "reservation_node_scores")
+    return raw.tolist()
+
+
+def device_score(args: abi.GsExtArgs, devs, ext) -> int:
+    d = np.ascontiguousarray(np.atleast_1d(devs), abi.NODE_DEVICES_DTYPE)
+    e = np.ascontiguousarray(np.atleast_1d(ext), abi.POD_EXT_DTYPE)
+    return int(lib().or_device_score(C.byref(args), abi.ptr(d), abi.ptr(e)))
+
+
+def device_filter(devs, ext) -> int:
+    d = np.ascontiguousarray(np.atleast_1d(devs), abi.NODE_DEVICES_DTYPE)
+    e = np.ascontiguousarray(np.atleast_1d(ext), abi.POD_EXT_DTYPE)
+    return int(lib().or_device_filter(abi.ptr(d), abi.ptr(e)))
+
+
+def device_score_node(args: abi.GsExtArgs, total, free, request, request_mask) -> int:
+    """resourceAllocationScorer.scoreNode (deviceshare/scoring.go:213-243) over gpu-core, gpu-memory-ratio, gpu-memory."""
+    t = np.ascontiguousarray(total, np.int64)
+    f = np.ascontiguousarray(free, np.int64)
+    q = np.ascontiguousarray(request, np.int64)
+    return int(lib().or_device_score_node(C.byref(args), abi.ptr(t), abi.ptr(f), abi.ptr(q), request_mask))
 
 
 def estimate_pod(args: abi.GsLoadAwareArgs, pod) -> tuple[int, int, int]:

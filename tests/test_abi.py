@@ -31,11 +31,12 @@ def test_exports_every_header_symbol(lib):
 
 
 def test_struct_sizes_match_library(lib):
-    arr = (C.c_uint64 * 14)()
-    lib.gs_abi_sizes(arr, 14)
     names = ["gs_pod", "gs_node", "gs_node_metric", "gs_pod_metric", "gs_config", "gs_placement", "gs_stats",
              "gs_loadaware_args", "gs_cpu_topology", "gs_node_numa", "gs_pod_allocation", "gs_numa_args",
-             "gs_quota_group", "gs_quota_status"]
+             "gs_quota_group", "gs_quota_status", "gs_node_devices", "gs_reservation", "gs_pod_ext", "gs_ext_args",
+             "gs_ext_placement"]
+    arr = (C.c_uint64 * len(names))()
+    lib.gs_abi_sizes(arr, len(names))
     for name, size in zip(names, arr):
         assert abi.STRUCT_SIZES[name] == size, name
 

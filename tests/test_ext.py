@@ -1,0 +1,186 @@
+"""Reservation + DeviceShare on the CPU: the oracle restatement against the reference's own
+test vectors (tests/golden/ext.json, tests/golden/make_golden_ext.py), and properties of or_schedule_ext on C5-like
+clusters (no GPU needed)."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from koordinator_amd import abi, config, synth
+from oracle import oracle as orc
+
+G = json.load(open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "ext.json")))
+KEYS = {"cpu": 0, "memory": 1}
+GR = {"core": abi.GS_GPU_CORE, "ratio": abi.GS_GPU_MEMORY_RATIO, "memory": abi.GS_GPU_MEMORY}
+
+
+def pod_of(d):
+    p = np.zeros(1, abi.POD_DTYPE)[0]
+    p["requests"][0], p["requests"][1] = d["cpu"], d["memory"]
+    p["request_mask"] = sum(1 << KEYS[k] for k in d["keys"])
+    return p
+
+
+def rsv_of(d, order=0, uid=1):
+    r = np.zeros(1, abi.RESERVATION_DTYPE)[0]
+    r["uid"] = uid
+    r["available"] = 1
+    r["allocatable"][0], r["allocatable"][1] = d["cpu"], d["memory"]
+    r["allocatable_mask"] = r["resource_names_mask"] = 3
+    r["order"] = order
+    if "allocated" in d:
+        r["allocated"][0], r["allocated"][1] = d["allocated"]["cpu"], d["allocated"]["memory"]
+        r["allocated_mask"] = 3
+    return r
+
+
+@pytest.mark.parametrize("case", G["reservation_score"], ids=lambda c: c["name"])
+def test_golden_reservation_score(case):
+    pod = pod_of(case["pod"])
+    rs = [rsv_of(r, uid=k + 1) for k, r in enumerate(case["reservations"])]
+    empty = np.zeros(1, abi.NODE_DTYPE)   # the test node: empty Status, no pods
+    raw = orc.reservation_node_scores(pod, [rs], empty, empty)
+    assert raw[0] == case["want"], case["src"]
+
+
+def test_golden_reservation_order_and_normalize():
+    case = G["reservation_order"]
+    pod = pod_of(case["pod"])
+    rs = [[rsv_of(case["reservation"], order=o, uid=k + 1)] for k, o in enumerate(case["orders"])]
+    empty = np.zeros(len(rs), abi.NODE_DTYPE)
+    raw = orc.reservation_node_scores(pod, rs, empty, empty)
+    assert raw == case["want_scores"], case["src"]
+    assert orc.default_normalize_score(100, False, raw) == case["want_normalized"], case["src"]
+
+
+def test_default_normalize_score_edge_cases():
+    assert orc.default_normalize_score(100, False, [0, 0]) == [0, 0]
+    assert orc.default_normalize_score(100, True, [0, 0]) == [100, 100]
+    assert orc.default_normalize_score(100, True, [5, 10]) == [50, 0]
+
+
+def ext_args(strategy=None):
+    a = orc.ext_args_default()
+    if strategy == "MostAllocated":
+        a.device_scoring_type = abi.GS_SCORING_MOST_ALLOCATED
+    return a
+
+
+@pytest.mark.parametrize("case", G["device_score"], ids=lambda c: c["name"])
+def test_golden_device_score(case):
+    d = np.zeros(1, abi.NODE_DEVICES_DTYPE)[0]
+    if case["gpus"] is not None:
+        d["has_device"] = 1
+        d["num_gpus"] = len(case["gpus"])
+        for g, x in enumerate(case["gpus"]):
+            d["gpus"][g]["minor"] = x["minor"]
+            d["gpus"][g]["has_info"] = 1
+            for k, v in x["total"].items():
+                d["gpus"][g]["total"][GR[k]] = v
+            for k, v in (x["used"] or {}).items():
+                d["gpus"][g]["used"][GR[k]] = v
+    else:
+        d["has_device"] = 1     # a Device object without GPUs: Prepare fails, Score reports 0
+    e = np.zeros(1, abi.POD_EXT_DTYPE)[0]
+    CO, RA = abi.GPU_NAMES["koordinator.sh/gpu-core"], abi.GPU_NAMES["koordinator.sh/gpu-memory-ratio"]
+    e["gpu_requests"][CO] = case["request"]["core"]
+    e["gpu_requests"][RA] = case["request"]["ratio"]
+    e["gpu_request_mask"] = (1 << CO) | (1 << RA)
+    assert orc.device_score(ext_args(case.get("strategy")), d, e) == case["want"], case["src"]
+
+
+@pytest.mark.parametrize("case", G["score_device"], ids=lambda c: c["name"])
+def test_golden_score_device(case):
+    vec = lambda m: [m.get(k, 0) for k in ("core", "ratio", "memory")]
+    mask = sum(1 << GR[k] for k in case["request"])
+    got = orc.device_score_node(ext_args(case.get("strategy")), vec(case["total"]), vec(case["free"]),
+                                vec(case["request"]), mask)
+    assert got == case["want"], case["src"]
+
+
+def test_device_request_validation():
+    """ValidateDeviceRequest / ValidDeviceResourceCombinations (deviceshare/utils.go:147-175)."""
+    d = np.zeros(1, abi.NODE_DEVICES_DTYPE)[0]
+    e = np.zeros(1, abi.POD_EXT_DTYPE)[0]
+    CO, RA, NV = (abi.GPU_NAMES[n] for n in ("koordinator.sh/gpu-core", "koordinator.sh/gpu-memory-ratio",
+                                             "nvidia.com/gpu"))
+    e["gpu_requests"][CO] = e["gpu_requests"][RA] = 150          # > 100 and not a multiple of 100
+    e["gpu_request_mask"] = (1 << CO) | (1 << RA)
+    assert orc.device_filter(d, e) == abi.GS_EXT_FAIL_POD
+    e["gpu_request_mask"] = (1 << CO) | (1 << NV)                 # not a valid combination
+    assert orc.device_filter(d, e) == abi.GS_EXT_FAIL_POD
+    e["gpu_request_mask"] = 1 << CO                               # gpu-core alone: not a valid combination
+    assert orc.device_filter(d, e) == abi.GS_EXT_FAIL_POD
+
+
+def c5(nodes=800, pods=300, **kw):
+    c = synth.make_cluster(nodes, pods, config_id=5)
+    synth.make_ext(c, **kw)
+    return c
+
+
+def oracle_for(c, strategy=None, enabled=abi.GS_ENABLE_LA_FIT):
+    cfg = config.make_config(c.num_nodes, enabled=enabled)
+    o = orc.Oracle(cfg)
+    synth.load_into(o, c)
+    synth.load_ext_into(o, c, ext_args(strategy))
+    return o
+
+
+def test_ext_off_equals_plain_schedule():
+    """With both plugins off, or_schedule_ext is or_schedule (no reservations restored, nothing normalized)."""
+    c = c5(600, 200)
+    cfg = config.make_config(c.num_nodes, enabled=abi.GS_ENABLE_LA_FIT)
+    o1, o2 = orc.Oracle(cfg), orc.Oracle(cfg)
+    synth.load_into(o1, c)
+    synth.load_into(o2, c)
+    a = ext_args()
+    a.enabled = 0
+    o2.ext_configure(a)
+    p1 = o1.schedule(c.pods)
+    p2, _ = o2.schedule_ext(c.pods, c.ext["pod_ext"])
+    assert np.array_equal(p1, p2)
+
+
+def test_c5_properties():
+    c = c5(800, 400, owner_pod_pct=30, required_pct=5, rsv_node_pct=20)
+    CO, RA = abi.GPU_NAMES["koordinator.sh/gpu-core"], abi.GPU_NAMES["koordinator.sh/gpu-memory-ratio"]
+    for p in (3, 77):   # invalid gpu-core percentage: DeviceShare PreFilter fails
+        c.ext["pod_ext"][p]["reservation_owner"] = 0
+        c.ext["pod_ext"][p]["gpu_request_mask"] = (1 << CO) | (1 << RA)
+        c.ext["pod_ext"][p]["gpu_requests"][CO] = c.ext["pod_ext"][p]["gpu_requests"][RA] = 250
+    o = oracle_for(c)
+    dev0 = c.ext["devices"].copy()
+    out, eo = o.schedule_ext(c.pods, c.ext["pod_ext"])
+    pe = c.ext["pod_ext"]
+    rsv = {int(r["uid"]): r for r in c.ext["reservations"]}
+    gpu = pe["gpu_request_mask"] > 0
+    placed = out["node"] >= 0
+    # GPU pods land on GPU nodes and get their minors; pods that fail PreFilter are unschedulable
+    bad = eo["fail_code"] == abi.GS_EXT_FAIL_POD
+    assert bad.any() and (out["node"][bad] == -1).all()
+    ok_gpu = gpu & placed
+    assert ok_gpu.sum() > 10
+    assert (c.ext["devices"]["has_device"][out["node"][ok_gpu]] == 1).all()
+    assert (eo["gpu_count"][ok_gpu] >= 1).all()
+    # required pods only land on nodes holding a matched reservation, and are assumed into it
+    req = (pe["reservation_required"] == 1) & placed
+    for p in np.nonzero(req)[0]:
+        u = int(eo["reservation_uid"][p])
+        assert u and rsv[u]["node"] == out["node"][p] and rsv[u]["owner_key"] == pe["reservation_owner"][p]
+    # every assumed reservation belongs to the pod's owner and node
+    for p in np.nonzero(eo["reservation_uid"])[0]:
+        r = rsv[int(eo["reservation_uid"][p])]
+        assert r["owner_key"] == pe["reservation_owner"][p] and r["node"] == out["node"][p]
+    # the reservation cache accounting follows the assumed pods
+    for u, r in rsv.items():
+        n = int((eo["reservation_uid"] == u).sum())
+        cur = o.reservation(u)
+        assert cur["assigned_pods"] == r["assigned_pods"] + n
+    # devices: the used GPU resources grew by exactly the per-instance requests of the pods placed on them
+    for i in np.unique(out["node"][ok_gpu]):
+        d1 = o.devices(int(i))
+        grew = int(d1["gpus"]["used"][:, abi.GS_GPU_MEMORY_RATIO].sum() - dev0[i]["gpus"]["used"][:, abi.GS_GPU_MEMORY_RATIO].sum())
+        sel = ok_gpu & (out["node"] == i)
+        assert grew == int((eo["gpu_count"][sel] * eo["gpu_per_instance"][sel][:, abi.GS_GPU_MEMORY_RATIO]).sum())

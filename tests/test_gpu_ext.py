@@ -1,0 +1,88 @@
+"""Reservation + DeviceShare on the HIP path (gs_schedule_ext) against the oracle (or_schedule_ext), bit-exact:
+placement, max score, tie count, feasible count, the reservation each pod was assumed into, the GPU minors and
+per-instance resources DeviceShare's Reserve allocated, both normalized plugin scores, and the final reservation and
+device state. Needs an MI355X: -m gpu."""
+import numpy as np
+import pytest
+
+from koordinator_amd import abi, config, synth
+from oracle import oracle as orc
+
+pytestmark = pytest.mark.gpu
+
+
+def run_pair(c, strategy=None, enabled=abi.GS_ENABLE_LA_FIT, chunks=1):
+    from koordinator_amd.engine import Engine
+    cfg = config.make_config(c.num_nodes, enabled=enabled)
+    a = orc.ext_args_default()
+    if strategy == "MostAllocated":
+        a.device_scoring_type = abi.GS_SCORING_MOST_ALLOCATED
+    e, o = Engine(cfg), orc.Oracle(cfg)
+    for x in (e, o):
+        synth.load_into(x, c)
+        synth.load_ext_into(x, c, a)
+    P = len(c.pods)
+    seq = np.arange(P, dtype=np.uint64)
+    outs = []
+    for k in range(chunks):
+        sl = slice(k * P // chunks, (k + 1) * P // chunks)
+        outs.append(e.schedule_ext(c.pods[sl], c.ext["pod_ext"][sl], seq[sl]))
+    ge = np.concatenate([x[0] for x in outs]), np.concatenate([x[1] for x in outs])
+    oe = o.schedule_ext(c.pods, c.ext["pod_ext"], seq)
+    return e, o, ge, oe
+
+
+def check(c, e, o, ge, oe):
+    (gp, gx), (op, ox) = ge, oe
+    for f in ("node", "feasible"):
+        bad = np.nonzero(gp[f] != op[f])[0]
+        assert not len(bad), f"{f} differs at pods {bad[:10]}: gpu {gp[bad[:5]]} oracle {op[bad[:5]]}"
+    placed = op["node"] >= 0
+    assert np.array_equal(gp["score"][placed], op["score"][placed])
+    assert np.array_equal(gp["ties"][placed], op["ties"][placed])
+    for f in ("reservation_uid", "gpu_minor_mask", "gpu_count", "gpu_per_instance", "deviceshare_score",
+              "reservation_score", "fail_code"):
+        bad = np.nonzero((gx[f] != ox[f]).reshape(len(gx), -1).any(axis=1))[0]
+        assert not len(bad), f"ext {f} differs at pods {bad[:10]}"
+    for r in c.ext["reservations"]:
+        a, b = e.reservation(int(r["uid"])), o.reservation(int(r["uid"]))
+        assert a["assigned_pods"] == b["assigned_pods"] and np.array_equal(a["allocated"], b["allocated"])
+    for i in np.nonzero(c.ext["devices"]["has_device"])[0]:
+        a, b = e.devices(int(i)), o.devices(int(i))
+        assert np.array_equal(a["gpus"]["used"], b["gpus"]["used"]) and np.array_equal(a["requested"], b["requested"])
+    assert e.mirror_check() == 0
+    return placed
+
+
+def test_c5_small_matches_oracle():
+    c = synth.make_cluster(3000, 900, config_id=5)
+    synth.make_ext(c)
+    e, o, ge, oe = run_pair(c, chunks=3)
+    placed = check(c, e, o, ge, oe)
+    gx = ge[1]
+    assert placed.sum() > 800 and (gx["gpu_count"] > 0).sum() > 40 and (gx["reservation_uid"] > 0).sum() > 5
+
+
+def test_c5_dense_reservations_required_restricted():
+    c = synth.make_cluster(2000, 700, config_id=6)
+    synth.make_ext(c, rsv_node_pct=40, owners=10, owner_pod_pct=50, required_pct=10, gpu_pod_pct=5)
+    e, o, ge, oe = run_pair(c)
+    check(c, e, o, ge, oe)
+    assert (ge[1]["reservation_uid"] > 0).sum() > 50
+    assert (ge[1]["reservation_score"] > 0).any()
+
+
+def test_c5_gpu_heavy_most_allocated():
+    c = synth.make_cluster(1500, 600, config_id=7)
+    synth.make_ext(c, gpu_node_pct=50, gpu_pod_pct=60, owner_pod_pct=5)
+    e, o, ge, oe = run_pair(c, strategy="MostAllocated")
+    check(c, e, o, ge, oe)
+    assert (ge[1]["gpu_count"] > 1).any() and (ge[0]["node"] < 0).any()
+
+
+def test_c5_with_numa_profile_without_policy_nodes():
+    c = synth.make_cluster(1200, 400, config_id=8)
+    synth.make_numa(c, numa_policy_pct=0, cpuset_pod_pct=0)
+    synth.make_ext(c)
+    e, o, ge, oe = run_pair(c, enabled=abi.GS_ENABLE_ALL)
+    check(c, e, o, ge, oe)
