@@ -69,6 +69,23 @@ def cpu_baseline(cluster, cfg, pods, seq, given, sample_start: int, sample_pods:
                       f"{chunk} timed pods at {threads} threads (median), {n1} pods at 1 thread"}
 
 
+def cpu_baseline_c5(cluster, cfg, ext_args, pods, seq, sample_pods: int) -> dict:
+    """C5: the oracle's one-thread scheduleOne with the Reservation / DeviceShare restatement (or_schedule_ext) on the
+    first pods of the workload from the fresh cluster state (the ext restatement has no replay mode)."""
+    from oracle import oracle as orc
+    from koordinator_amd import synth
+    o = orc.Oracle(cfg)
+    synth.load_into(o, cluster)
+    synth.load_ext_into(o, cluster, ext_args)
+    n = max(8, sample_pods)
+    t0 = time.perf_counter()
+    o.schedule_ext(pods[:n], cluster.ext["pod_ext"][:n], seq[:n])
+    dt = time.perf_counter() - t0
+    return {"pods_per_s": n / dt, "evals_per_s": n / dt * cluster.num_nodes, "seconds": dt,
+            "sample": f"pods 0..{n} of the workload on the fresh cluster, one thread (or_schedule_ext: Fit + LoadAware + "
+                      "DeviceShare + Reservation restatement)"}
+
+
 PMC_FILE = os.path.join(ROOT, "profiles", "pmc_latest.json")
 
 
@@ -95,7 +112,8 @@ def main() -> None:
     ap.add_argument("--batch", type=int, default=128)
     ap.add_argument("--cpu-sample-pods", type=int, default=400)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--profile", choices=["c3", "la-fit"], default="c3")
+    ap.add_argument("--profile", choices=["c3", "la-fit", "c5"], default="c3",
+                    help="c5: 100k nodes, LoadAware + Fit + DeviceShare + Reservation (SURVEY 8(d) C5, see --nodes)")
     ap.add_argument("--sample-pct", type=int, default=None,
                     help="node sampling (percentageOfNodesToScore; 0 = adaptive) instead of every node (one GPU)")
     args = ap.parse_args()
@@ -120,10 +138,15 @@ def main() -> None:
 
     n_nodes = args.nodes if args.scaling == "strong" else args.nodes * world
     total_pods = (args.warmup + args.steps) * args.pods_per_step
-    cluster = synth.make_cluster(n_nodes, total_pods, config_id=2)
+    c5 = args.profile == "c5"
+    if c5 and world > 1:
+        raise SystemExit("--profile c5 runs on one GPU (extension pods need one rank)")
+    cluster = synth.make_cluster(n_nodes, total_pods, config_id=5 if c5 else 2)
     numa = args.profile == "c3"
     if numa:
         synth.make_numa(cluster)
+    if c5:
+        synth.make_ext(cluster)
     from koordinator_amd import abi
     if args.sample_pct is not None and world > 1:
         raise SystemExit("--sample-pct runs on one GPU")
@@ -137,13 +160,24 @@ def main() -> None:
         dist.broadcast_object_list(uid, src=0)
         eng.comm_init_rccl(uid[0], world, rank)
     synth.load_into(eng, cluster)
+    ext_args = None
+    if c5:
+        ext_args = abi.GsExtArgs()
+        abi.load().gs_ext_args_default(abi.C.byref(ext_args))
+        synth.load_ext_into(eng, cluster, ext_args)
+        pod_ext = cluster.ext["pod_ext"]
+
+    def run(lo, hi):
+        if c5:
+            return eng.schedule_ext(pods[lo:hi], pod_ext[lo:hi], seq[lo:hi])[0]
+        return eng.schedule(pods[lo:hi], seq[lo:hi])
 
     pods = cluster.pods
     seq = np.arange(total_pods, dtype=np.uint64)
     given = np.full(total_pods, -1, np.int32)   # the GPU's placements (the CPU baseline replays the warm-up ones)
     P = args.pods_per_step
     for w in range(args.warmup):
-        out = eng.schedule(pods[w * P:(w + 1) * P], seq[w * P:(w + 1) * P])
+        out = run(w * P, (w + 1) * P)
         given[w * P:(w + 1) * P] = np.where(out["node"] >= 0, out["node"], -2)
     eng.synchronize()
     eng.reset_stats()
@@ -154,7 +188,7 @@ def main() -> None:
     t0 = time.perf_counter()
     placed = 0
     for s in range(args.warmup, args.warmup + args.steps):
-        out = eng.schedule(pods[s * P:(s + 1) * P], seq[s * P:(s + 1) * P])
+        out = run(s * P, (s + 1) * P)
         placed += int((out["node"] >= 0).sum())
     eng.synchronize()
     torch.cuda.synchronize()
@@ -209,7 +243,11 @@ def main() -> None:
     }
 
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and c5:
+        r = cpu_baseline_c5(cluster, cfg, ext_args, pods, seq, args.cpu_sample_pods // 4)
+        cpu = {"value": r["evals_per_s"], "unit": "evals/s", "cores": 1, "kind": "port", "pods_per_s": r["pods_per_s"],
+               "seconds": r["seconds"], "sample": r["sample"]}
+    elif rank == 0 and world == 1 and not args.no_cpu_baseline:
         threads = min(os.cpu_count() or 1, int(os.environ.get("OMP_NUM_THREADS", "16")), 16)
         sample_start = args.warmup * P
         r = cpu_baseline(cluster, cfg, pods, seq, given, sample_start, args.cpu_sample_pods, threads)
@@ -237,7 +275,11 @@ def main() -> None:
             "data": "synthetic",
             "pods_per_s": pods_timed / dt,
             "config": {
-                "workload": (f"C3: {n_nodes} nodes ({args.scaling} scaling over {world} GPU) x {P} pods/step, "
+                "workload": (f"C5: {n_nodes} nodes ({world} GPU) x {P} pods/step, NodeResourcesFit(LeastAllocated) + "
+                             "LoadAwareScheduling + DeviceShare (GPU) + Reservation filter+score with normalize, selectHost, "
+                             "assume+Reserve; 20% GPU nodes, 5% nodes with reservations, ~10% owner pods, ~10% GPU pods"
+                             if c5 else
+                             f"C3: {n_nodes} nodes ({args.scaling} scaling over {world} GPU) x {P} pods/step, "
                              "sequential scheduleOne with NodeResourcesFit(LeastAllocated) + LoadAwareScheduling + "
                              "NodeNUMAResource filter+score (30% NUMA-policy nodes, 20% LSE/LSR cpuset pods), "
                              "selectHost, assume+Reserve"

@@ -1073,7 +1073,7 @@ int ext_alloc(gs_ctx* c) {
   std::fill(c->dev_dirty.begin(), c->dev_dirty.end(), 0);
   HIP_TRY(c, hipMalloc(&c->d_xpod, sizeof(ExtPod)));
   HIP_TRY(c, hipMalloc(&c->d_xtot, 4 * (size_t)c->ld));
-  HIP_TRY(c, hipMalloc(&c->d_xT, 4 * (size_t)c->ld));
+  HIP_TRY(c, hipMalloc(&c->d_xT, 4 * ext_select_scratch_words(c->ld)));
   HIP_TRY(c, hipMalloc(&c->d_xds, 2 * (size_t)c->ld));
   HIP_TRY(c, hipMalloc(&c->d_xrs, 2 * (size_t)c->ld));
   HIP_TRY(c, hipMalloc(&c->d_xout, sizeof(ExtOut)));
@@ -1335,7 +1335,7 @@ int ext_schedule_one(gs_ctx* c, const gs_pod& pod, const gs_pod_ext& e, uint64_t
   HIP_TRY(c, hipEventRecord(c->ev[1], c->st));
   HIP_TRY(c, launch_ext_nodes(c->d_dev, c->d_S, c->n0, c->n1, c->d_xpod, c->d_xtot, c->d_xds, c->d_xrs, c->st));
   HIP_TRY(c, launch_ext_matched(c->mv, c->d_pods, c->pf, prod_cols, c->d_xpod, c->d_xrec, c->d_xres, nrec, c->d_xtot,
-                                c->d_xrs, c->d_xnom, c->st));
+                                c->d_xrs, c->d_xnom, c->d_xT, c->n1 - c->n0, c->st));
   HIP_TRY(c, launch_ext_select(c->d_xtot, c->d_xds, c->d_xrs, c->d_xrec, c->n0, c->n1, c->d_xpod, c->cfg.seed, c->d_xT,
                                c->d_xout, c->st));
   HIP_TRY(c, hipEventRecord(c->ev[4], c->st));
@@ -1359,10 +1359,16 @@ int ext_schedule_one(gs_ctx* c, const gs_pod& pod, const gs_pod_ext& e, uint64_t
   const uint32_t node = (uint32_t)xo.node;
   // ---- Reserve
   if (gmask && (rc = ext_device_reserve(c, node, greq, gmask, eo))) return rc;
-  if (rs_on && xo.rec >= 0) {   // Reservation.Reserve -> reservationCache.assumePod (AddAssignedPod, reservation_info.go:379-388)
-    const int nom = c->h_xnom[xo.rec];
+  int rec_i = -1;   // the chosen node's matched record (records are in node order)
+  {
+    auto it = std::lower_bound(c->xrec.begin(), c->xrec.end(), node,
+                               [](const ExtRec& r, uint32_t n) { return r.node < n; });
+    if (it != c->xrec.end() && it->node == node) rec_i = (int)(it - c->xrec.begin());
+  }
+  if (rs_on && rec_i >= 0) {   // Reservation.Reserve -> reservationCache.assumePod (AddAssignedPod, reservation_info.go:379-388)
+    const int nom = c->h_xnom[rec_i];
     if (nom >= 0) {
-      gs_reservation& r = c->rsv.at(c->xres_uid[c->xrec[xo.rec].first + nom]);
+      gs_reservation& r = c->rsv.at(c->xres_uid[c->xrec[rec_i].first + nom]);
       for (int s = 0; s < 7; ++s)
         if ((r.resource_names_mask >> s & 1u) && (pod.request_mask >> s & 1u)) {
           r.allocated[s] = ((r.allocated_mask >> s & 1u) ? r.allocated[s] : 0) + pod.requests[s];

@@ -1,12 +1,13 @@
 // gs_ext.h — Reservation + DeviceShare on the device: the HBM image of the nodes' GPU
 // devices, the per-pod matched-reservation records the host's BeforePreFilter builds, and the launch interface of
-// the three kernels of one extension pod (gs_ext.hip):
+// the kernels of one extension pod (gs_ext.hip):
 //   ext_nodes_kernel    every node of the shard: the GPU Fit scalars, DeviceShare Filter + raw Score on the batch-start
 //                       score row of the pod (eval pass), the Reservation affinity verdict of unmatched nodes;
 //   ext_matched_kernel  the nodes holding reservations the pod matches: the restored NodeInfo re-evaluated (Fit,
 //                       LoadAware, NodeNUMAResource), Reservation Filter, NominateReservation and its raw Score;
-//   ext_select_kernel   one workgroup: PreScore's preferred node, both DefaultNormalizeScore passes, the weighted
-//                       totals, selectHost (max, ties, feasible, the tie-break position) over the whole row.
+//   ext select passes   PreScore's preferred node, both DefaultNormalizeScore passes, the weighted totals,
+//                       selectHost (max, ties, feasible, the tie-break position) over the whole row: three coalesced
+//                       grid passes with global atomics, the last block locating the j*-th tie.
 #pragma once
 #include <stdint.h>
 
@@ -86,7 +87,8 @@ hipError_t launch_ext_nodes(const DevNode* dev, const int16_t* S, uint32_t n0, u
                             int32_t* tot, int16_t* ds, int16_t* rs, hipStream_t st);
 hipError_t launch_ext_matched(const MirrorView& m, const PodVec* pods, const Profile& pf, int prod_cols,
                               const ExtPod* pod, const ExtRec* recs, const ExtRes* res, int nrec, int32_t* tot,
-                              int16_t* rs, int32_t* nominated, hipStream_t st);
+                              int16_t* rs, int32_t* nominated, int32_t* scratch, uint32_t len, hipStream_t st);
+size_t ext_select_scratch_words(uint32_t len);   // int32 words of launch_ext_select's scratch
 hipError_t launch_ext_select(const int32_t* tot, const int16_t* ds, const int16_t* rs, const ExtRec* recs, uint32_t n0,
                              uint32_t n1, const ExtPod* pod, uint64_t seed, int32_t* scratch, ExtOut* out,
                              hipStream_t st);

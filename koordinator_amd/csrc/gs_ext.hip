@@ -155,14 +155,14 @@ __device__ int64_t score_reservation(const ExtPod& p, const ExtRes& r) {
   return w ? s / w : 0;
 }
 
-__global__ __launch_bounds__(64) void ext_matched_kernel(MirrorView m, const PodVec* __restrict__ pods, Profile pf,
-                                                          int prod_cols, const ExtPod* __restrict__ pp,
-                                                          const ExtRec* __restrict__ recs,
-                                                          const ExtRes* __restrict__ res, int nrec, int32_t* tot,
-                                                          int16_t* rs, int32_t* nominated) {
-  const int k = blockIdx.x * 64 + threadIdx.x;
-  if (k >= nrec) return;
-  const ExtPod& p = *pp;
+constexpr int SEL_BLOCK = 256;
+enum { ACC_DS = 0, ACC_RS = 1, ACC_FEAS = 2, ACC_MAX = 3, ACC_DONE = 4, ACC_TIES = 5, ACC_PREF = 6, ACC_WORDS = 8 };
+
+// one matched node (record k): the restored row re-evaluated, Reservation Filter, NominateReservation, raw Score
+__device__ __forceinline__ void matched_one(const MirrorView& m, const PodVec* __restrict__ pods, const Profile& pf,
+                                            int prod_cols, const ExtPod& p, const ExtRec* __restrict__ recs,
+                                            const ExtRes* __restrict__ res, int k, int32_t* tot, int16_t* rs,
+                                            int32_t* nominated) {
   const ExtRec& rc = recs[k];
   const uint32_t i = rc.node;
   // the restored NodeInfo of the pod (BeforePreFilter): the mirror row plus the matched restore deltas
@@ -205,128 +205,190 @@ __global__ __launch_bounds__(64) void ext_matched_kernel(MirrorView m, const Pod
   nominated[k] = nom;
 }
 
-constexpr int SEL_THREADS = 1024;
-
-__device__ __forceinline__ int64_t block_reduce_max(int64_t v, int64_t* sh) {
-  for (int o = 32; o > 0; o >>= 1) v = max(v, (int64_t)__shfl_xor(v, o));
-  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
-  __syncthreads();
-  if (l == 0) sh[w] = v;
-  __syncthreads();
-  if (threadIdx.x < 64) {
-    int64_t x = threadIdx.x < SEL_THREADS / 64 ? sh[threadIdx.x] : INT64_MIN;
-    for (int o = 32; o > 0; o >>= 1) x = max(x, (int64_t)__shfl_xor(x, o));
-    if (threadIdx.x == 0) sh[16] = x;
-  }
-  __syncthreads();
-  return sh[16];
-}
-__device__ __forceinline__ int64_t block_reduce_sum(int64_t v, int64_t* sh) {
-  for (int o = 32; o > 0; o >>= 1) v += (int64_t)__shfl_xor(v, o);
-  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
-  __syncthreads();
-  if (l == 0) sh[w] = v;
-  __syncthreads();
-  if (threadIdx.x < 64) {
-    int64_t x = threadIdx.x < SEL_THREADS / 64 ? sh[threadIdx.x] : 0;
-    for (int o = 32; o > 0; o >>= 1) x += (int64_t)__shfl_xor(x, o);
-    if (threadIdx.x == 0) sh[16] = x;
-  }
-  __syncthreads();
-  return sh[16];
-}
-
-// One workgroup: each thread owns a contiguous chunk of the row (node order), so the j*-th tie is located with one
-// exclusive scan of per-thread tie counts.
-__global__ __launch_bounds__(SEL_THREADS) void ext_select_kernel(const int32_t* __restrict__ tot,
-                                                                 const int16_t* __restrict__ ds,
-                                                                 const int16_t* __restrict__ rs,
-                                                                 const ExtRec* __restrict__ recs, uint32_t n0,
-                                                                 uint32_t n1, const ExtPod* __restrict__ pp,
-                                                                 uint64_t seed, int32_t* T, ExtOut* out) {
-  __shared__ int64_t sh[17];
-  __shared__ int32_t pref_sh;
-  __shared__ int64_t scan[SEL_THREADS];
+// One workgroup over the matched records, then PreScore's preferred node: the first feasible matched node (node
+// order) with the lowest reservation order (findMostPreferredReservationByOrder, scoring.go:89-99) -> acc[ACC_PREF].
+__global__ __launch_bounds__(SEL_BLOCK) void ext_matched_kernel(MirrorView m, const PodVec* __restrict__ pods,
+                                                                Profile pf, int prod_cols, const ExtPod* __restrict__ pp,
+                                                                const ExtRec* __restrict__ recs,
+                                                                const ExtRes* __restrict__ res, int nrec, int32_t* tot,
+                                                                int16_t* rs, int32_t* nominated, int32_t* acc) {
+  __shared__ int64_t so_sh[SEL_BLOCK];
+  __shared__ int32_t node_sh[SEL_BLOCK];
   const ExtPod& p = *pp;
-  const uint32_t len = n1 - n0;
-  const uint32_t chunk = (len + SEL_THREADS - 1) / SEL_THREADS;
-  const uint32_t b = min(len, threadIdx.x * chunk), e = min(len, b + chunk);
-  // PreScore: the preferred node = the first feasible node (node order) with the lowest reservation order
-  if (threadIdx.x == 0) {
-    int32_t pref = -1;
-    int64_t so = INT64_MAX;
-    if (p.rs_on)
-      for (int k = 0; k < p.nrec; ++k) {
-        const ExtRec& rc = recs[k];
-        if (tot[rc.node - n0] < 0) continue;
-        if (rc.order_min != INT64_MAX && rc.order_min != 0 && so > rc.order_min) { so = rc.order_min; pref = (int32_t)rc.node; }
-      }
-    pref_sh = pref;
-  }
-  __syncthreads();
-  const int32_t pref = pref_sh;
-  int64_t mds = 0, mrs = 0, feas = 0;
-  for (uint32_t j = b; j < e; ++j) {
-    if (tot[j] < 0) continue;
-    ++feas;
-    mds = max(mds, (int64_t)ds[j]);
-    mrs = max(mrs, (int64_t)((int32_t)(j + n0) == pref ? 1000 : rs[j]));
-  }
-  const int64_t MDS = block_reduce_max(mds, sh);
-  const int64_t MRS = block_reduce_max(mrs, sh);
-  const int64_t F = block_reduce_sum(feas, sh);
-  // weighted totals with DefaultNormalizeScore(MaxNodeScore, false) of both plugins
-  int64_t mt = -1;
-  for (uint32_t j = b; j < e; ++j) {
-    int32_t t = tot[j];
-    if (t >= 0) {
-      int64_t x = t;
-      if (p.ds_on) x += (MDS ? kMaxNodeScore * ds[j] / MDS : (int64_t)ds[j]) * p.w_ds;
-      if (p.rs_on) {
-        const int64_t r = (int32_t)(j + n0) == pref ? 1000 : rs[j];
-        x += (MRS ? kMaxNodeScore * r / MRS : r) * p.w_rs;
-      }
-      t = (int32_t)x;
-      mt = max(mt, x);
+  int64_t so = INT64_MAX;
+  int32_t pn = -1;
+  for (int k = threadIdx.x; k < nrec; k += SEL_BLOCK) {
+    matched_one(m, pods, pf, prod_cols, p, recs, res, k, tot, rs, nominated);
+    const ExtRec& rc = recs[k];
+    if (tot[rc.node] >= 0 && rc.order_min != INT64_MAX && rc.order_min != 0 &&
+        (rc.order_min < so || (rc.order_min == so && (int32_t)rc.node < pn))) {
+      so = rc.order_min;
+      pn = (int32_t)rc.node;
     }
-    T[j] = t;
   }
-  const int64_t M = block_reduce_max(mt, sh);
-  int64_t cnt = 0;
-  if (M >= 0)
-    for (uint32_t j = b; j < e; ++j) cnt += T[j] == M;
-  scan[threadIdx.x] = cnt;
+  so_sh[threadIdx.x] = so;
+  node_sh[threadIdx.x] = pn;
   __syncthreads();
-  for (int o = 1; o < SEL_THREADS; o <<= 1) {   // inclusive Hillis-Steele scan
-    int64_t v = threadIdx.x >= (unsigned)o ? scan[threadIdx.x - o] : 0;
-    __syncthreads();
-    scan[threadIdx.x] += v;
+  for (int o = SEL_BLOCK / 2; o > 0; o >>= 1) {
+    if (threadIdx.x < (unsigned)o) {
+      const int64_t a = so_sh[threadIdx.x], b = so_sh[threadIdx.x + o];
+      const int32_t na = node_sh[threadIdx.x], nb = node_sh[threadIdx.x + o];
+      if (b < a || (b == a && nb >= 0 && (na < 0 || nb < na))) { so_sh[threadIdx.x] = b; node_sh[threadIdx.x] = nb; }
+    }
     __syncthreads();
   }
-  const int64_t ties = scan[SEL_THREADS - 1];
+  if (threadIdx.x == 0) acc[ACC_PREF] = p.rs_on ? node_sh[0] : -1;
+}
+
+// ---- normalizing select over the whole row, in four grid passes (coalesced; no grid-wide barrier):
+//   ext_acc_kernel    per-block max of the DeviceShare / Reservation raw scores (PreScore's preferred node counted at
+//                     mostPreferredScore) and the feasible count -> global atomics
+//   ext_total_kernel  weighted totals T[j] with both DefaultNormalizeScore passes, per-block max -> atomicMax
+//   ext_ties_kernel   per-block tie counts at the max (blocks cover contiguous node ranges); the last block to finish
+//                     scans the block counts, finds the block of the j*-th tie (selectHost) and the node in it
+
+__device__ __forceinline__ int32_t block_max_i32(int32_t v, int32_t* sh) {
+  v = wave_max(v);
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) sh[w] = v;
+  __syncthreads();
+  int32_t m = sh[0];
+  for (int i = 1; i < SEL_BLOCK / 64; ++i) m = max(m, sh[i]);
+  __syncthreads();
+  return m;
+}
+__device__ __forceinline__ int32_t block_sum_i32(int32_t v, int32_t* sh) {
+  v = wave_sum(v);
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) sh[w] = v;
+  __syncthreads();
+  int32_t m = 0;
+  for (int i = 0; i < SEL_BLOCK / 64; ++i) m += sh[i];
+  __syncthreads();
+  return m;
+}
+
+__global__ __launch_bounds__(SEL_BLOCK) void ext_acc_kernel(const int32_t* __restrict__ tot,
+                                                            const int16_t* __restrict__ ds,
+                                                            const int16_t* __restrict__ rs,
+                                                            const ExtRec* __restrict__ recs, uint32_t n0, uint32_t len,
+                                                            const ExtPod* __restrict__ pp, int32_t* acc) {
+  __shared__ int32_t sh[SEL_BLOCK / 64];
+  const int32_t pref = acc[ACC_PREF];
+  const uint32_t j = blockIdx.x * SEL_BLOCK + threadIdx.x;
+  int32_t f = 0, d = 0, r = 0;
+  if (j < len && tot[j] >= 0) {
+    f = 1;
+    d = ds[j];
+    r = (int32_t)(j + n0) == pref ? 1000 : rs[j];
+  }
+  d = block_max_i32(d, sh);
+  r = block_max_i32(r, sh);
+  f = block_sum_i32(f, sh);
+  if (threadIdx.x == 0) {
+    if (d) atomicMax(&acc[ACC_DS], d);
+    if (r) atomicMax(&acc[ACC_RS], r);
+    if (f) atomicAdd(&acc[ACC_FEAS], f);
+  }
+}
+
+__global__ __launch_bounds__(SEL_BLOCK) void ext_total_kernel(const int32_t* __restrict__ tot,
+                                                              const int16_t* __restrict__ ds,
+                                                              const int16_t* __restrict__ rs,
+                                                              const ExtRec* __restrict__ recs, uint32_t n0, uint32_t len,
+                                                              const ExtPod* __restrict__ pp, int32_t* T, int32_t* acc) {
+  __shared__ int32_t sh[SEL_BLOCK / 64];
+  const ExtPod& p = *pp;
+  const int32_t pref_sh = acc[ACC_PREF];
+  const int64_t MDS = acc[ACC_DS], MRS = acc[ACC_RS];
+  const uint32_t j = blockIdx.x * SEL_BLOCK + threadIdx.x;
+  int32_t t = -1;
+  if (j < len && tot[j] >= 0) {
+    int64_t x = tot[j];
+    if (p.ds_on) x += (MDS ? kMaxNodeScore * ds[j] / MDS : (int64_t)ds[j]) * p.w_ds;
+    if (p.rs_on) {
+      const int64_t r = (int32_t)(j + n0) == pref_sh ? 1000 : rs[j];
+      x += (MRS ? kMaxNodeScore * r / MRS : r) * p.w_rs;
+    }
+    t = (int32_t)x;
+  }
+  if (j < len) T[j] = t;
+  const int32_t m = block_max_i32(t, sh);
+  if (threadIdx.x == 0 && m >= 0) atomicMax(&acc[ACC_MAX], m + 1);
+}
+
+__global__ __launch_bounds__(SEL_BLOCK) void ext_ties_kernel(const int32_t* __restrict__ T,
+                                                             const int16_t* __restrict__ ds,
+                                                             const int16_t* __restrict__ rs, uint32_t n0, uint32_t len,
+                                                             const ExtPod* __restrict__ pp, uint64_t seed, int32_t* acc,
+                                                             int32_t* bcnt, ExtOut* out) {
+  __shared__ int32_t sh[SEL_BLOCK / 64];
+  __shared__ int32_t last;
+  __shared__ int64_t jstar_sh;
+  __shared__ int32_t found_block, found_rank;
+  const ExtPod& p = *pp;
+  const int32_t M = acc[ACC_MAX] - 1;
+  const uint32_t j = blockIdx.x * SEL_BLOCK + threadIdx.x;
+  const int32_t c = block_sum_i32((M >= 0 && j < len && T[j] == M) ? 1 : 0, sh);
+  if (threadIdx.x == 0) {
+    bcnt[blockIdx.x] = c;
+    __threadfence();
+    last = atomicAdd(&acc[ACC_DONE], 1) == (int)gridDim.x - 1;
+  }
+  __syncthreads();
+  if (!last) return;
+  __threadfence();
+  const int32_t F = __atomic_load_n(&acc[ACC_FEAS], __ATOMIC_RELAXED);
+  const int32_t pref = acc[ACC_PREF];
   if (M < 0) {
     if (threadIdx.x == 0) *out = ExtOut{-1, (uint32_t)F, 0, 0, -1, 0, 0, pref, 0};
     return;
   }
-  const int64_t jstar = tiebreak_position(seed, p.seq, ties);
-  const int64_t before = scan[threadIdx.x] - cnt;
-  if (jstar > before && jstar <= before + cnt) {
-    int64_t c = before;
-    for (uint32_t j = b; j < e; ++j) {
-      if (T[j] != M) continue;
-      if (++c == jstar) {
-        const int32_t node = (int32_t)(j + n0);
-        int32_t rec = -1;
-        for (int k = 0; k < p.nrec; ++k)
-          if ((int32_t)recs[k].node == node) rec = k;
-        const int64_t dsn = MDS ? kMaxNodeScore * ds[j] / MDS : ds[j];
-        const int64_t rr = node == pref ? 1000 : rs[j];
-        const int64_t rsn = MRS ? kMaxNodeScore * rr / MRS : rr;
-        *out = ExtOut{node, (uint32_t)F, M, (uint32_t)ties, rec, (int32_t)(p.ds_on ? dsn : 0),
-                      (int32_t)(p.rs_on ? rsn : 0), pref, 0};
-        break;
-      }
+  // the last block: thread t owns block counts [t*per, (t+1)*per); a block scan gives every range its tie offset
+  const uint32_t nb = gridDim.x, per = (nb + SEL_BLOCK - 1) / SEL_BLOCK;
+  const uint32_t b0 = min(nb, threadIdx.x * per), b1 = min(nb, b0 + per);
+  int32_t mine = 0;
+  for (uint32_t b = b0; b < b1; ++b) mine += __atomic_load_n(&bcnt[b], __ATOMIC_RELAXED);
+  const int incl = wave_incl_scan(mine);
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 63) sh[w] = incl;
+  __syncthreads();
+  int32_t before = incl - mine, ties = 0;
+  for (int i = 0; i < SEL_BLOCK / 64; ++i) {
+    if (i < w) before += sh[i];
+    ties += sh[i];
+  }
+  if (threadIdx.x == 0) {
+    jstar_sh = tiebreak_position(seed, p.seq, ties);
+    acc[ACC_TIES] = ties;
+  }
+  __syncthreads();
+  const int64_t jstar = jstar_sh;
+  if (jstar > before && jstar <= before + mine) {
+    int64_t cum = before;
+    for (uint32_t b = b0; b < b1; ++b) {
+      const int32_t cb = __atomic_load_n(&bcnt[b], __ATOMIC_RELAXED);
+      if (jstar <= cum + cb) { found_block = (int32_t)b; found_rank = (int32_t)(jstar - cum); break; }
+      cum += cb;
     }
+  }
+  __syncthreads();
+  const uint32_t jj = (uint32_t)found_block * SEL_BLOCK + threadIdx.x;
+  const int is_tie = (jj < len && __atomic_load_n(&T[jj], __ATOMIC_RELAXED) == M) ? 1 : 0;
+  const int tincl = wave_incl_scan(is_tie);
+  __syncthreads();
+  if ((threadIdx.x & 63) == 63) sh[w] = tincl;
+  __syncthreads();
+  int rank = tincl;
+  for (int i = 0; i < w; ++i) rank += sh[i];
+  if (is_tie && rank == found_rank) {
+    const int32_t node = (int32_t)(jj + n0);
+    const int64_t MDS = acc[ACC_DS], MRS = acc[ACC_RS];
+    const int64_t dsn = MDS ? kMaxNodeScore * ds[jj] / MDS : ds[jj];
+    const int64_t rr = node == pref ? 1000 : rs[jj];
+    const int64_t rsn = MRS ? kMaxNodeScore * rr / MRS : rr;
+    *out = ExtOut{node, (uint32_t)F, M, (uint32_t)ties, -1, (int32_t)(p.ds_on ? dsn : 0), (int32_t)(p.rs_on ? rsn : 0),
+                  pref, 0};
   }
 }
 
@@ -342,19 +404,31 @@ hipError_t launch_ext_nodes(const DevNode* dev, const int16_t* S, uint32_t n0, u
 
 hipError_t launch_ext_matched(const MirrorView& m, const PodVec* pods, const Profile& pf, int prod_cols,
                               const ExtPod* pod, const ExtRec* recs, const ExtRes* res, int nrec, int32_t* tot,
-                              int16_t* rs, int32_t* nominated, hipStream_t st) {
-  if (nrec <= 0) return hipSuccess;
-  hipLaunchKernelGGL(ext_matched_kernel, dim3((nrec + 63) / 64), dim3(64), 0, st, m, pods, pf, prod_cols, pod, recs, res,
-                     nrec, tot, rs, nominated);
+                              int16_t* rs, int32_t* nominated, int32_t* scratch, uint32_t len, hipStream_t st) {
+  // scratch: T[len] | acc[ACC_WORDS] | bcnt[blocks]; the accumulators are reset here, before the select passes
+  int32_t* acc = scratch + len;
+  hipError_t e = hipMemsetAsync(acc, 0, sizeof(int32_t) * ACC_WORDS, st);   // acc[ACC_MAX] holds max + 1
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(ext_matched_kernel, dim3(1), dim3(SEL_BLOCK), 0, st, m, pods, pf, prod_cols, pod, recs, res, nrec,
+                     tot, rs, nominated, acc);
   return hipGetLastError();
 }
 
 hipError_t launch_ext_select(const int32_t* tot, const int16_t* ds, const int16_t* rs, const ExtRec* recs, uint32_t n0,
                              uint32_t n1, const ExtPod* pod, uint64_t seed, int32_t* scratch, ExtOut* out,
                              hipStream_t st) {
-  hipLaunchKernelGGL(ext_select_kernel, dim3(1), dim3(SEL_THREADS), 0, st, tot, ds, rs, recs, n0, n1, pod, seed, scratch,
+  const uint32_t len = n1 - n0;
+  const uint32_t blocks = (len + SEL_BLOCK - 1) / SEL_BLOCK;
+  int32_t* T = scratch;
+  int32_t* acc = scratch + len;
+  int32_t* bcnt = acc + ACC_WORDS;
+  hipLaunchKernelGGL(ext_acc_kernel, dim3(blocks), dim3(SEL_BLOCK), 0, st, tot, ds, rs, recs, n0, len, pod, acc);
+  hipLaunchKernelGGL(ext_total_kernel, dim3(blocks), dim3(SEL_BLOCK), 0, st, tot, ds, rs, recs, n0, len, pod, T, acc);
+  hipLaunchKernelGGL(ext_ties_kernel, dim3(blocks), dim3(SEL_BLOCK), 0, st, T, ds, rs, n0, len, pod, seed, acc, bcnt,
                      out);
   return hipGetLastError();
 }
+
+size_t ext_select_scratch_words(uint32_t len) { return len + ACC_WORDS + (len + SEL_BLOCK - 1) / SEL_BLOCK + 64; }
 
 }  // namespace gs
