@@ -392,6 +392,15 @@ int gs_node_metrics_upsert(gs_ctx* ctx, const uint32_t* idx, const gs_node_metri
 int gs_pods_assign(gs_ctx* ctx, const uint32_t* node_idx, const gs_pod* pods, const int64_t* timestamps_ns,
                    uint32_t n);
 int gs_pods_unassign(gs_ctx* ctx, const uint32_t* node_idx, const gs_pod* pods, uint32_t n);
+/* podAssignCache's pod informer handlers OnAdd / OnUpdate / OnDelete (loadaware/pod_assign_cache.go:82-117):
+ * node_idx[i] = pod.Spec.NodeName as a node index (-1: "", a pending pod), the GS_POD_TERMINATED flag =
+ * util.IsPodTerminated(pod); assign stamps the injected now (timeNowFn). */
+#define GS_POD_EVENT_ADD 0
+#define GS_POD_EVENT_UPDATE 1
+#define GS_POD_EVENT_DELETE 2
+int gs_pods_on_event(gs_ctx* ctx, int event, const int32_t* node_idx, const gs_pod* pods, uint32_t n);
+/* podAssignCache.podInfoItems[node] in uid order: up to cap (uid, timestamp) entries; returns the entry count. */
+int gs_assign_cache_get(gs_ctx* ctx, uint32_t node, uint64_t* uids, int64_t* timestamps, uint32_t cap);
 
 /* Filter + Score of every pod against every node of the current snapshot, no selection, no state change:
  * [upstream] RunFilterPlugins (Fit.Filter fit.go, LoadAware.Filter load_aware.go:123-171) and

@@ -216,6 +216,7 @@ GPU_NAMES = {"nvidia.com/gpu": 0, "koordinator.sh/gpu": 1, "koordinator.sh/gpu-c
 GS_MAX_GPUS = 8
 RSV_POLICY = {"": 0, "Default": 0, "Aligned": 1, "Restricted": 2}
 GS_EXT_DEVICESHARE, GS_EXT_RESERVATION = 0x1, 0x2
+GS_POD_EVENT_ADD, GS_POD_EVENT_UPDATE, GS_POD_EVENT_DELETE = 0, 1, 2
 GS_EXT_FAIL_DEVICE, GS_EXT_FAIL_RESERVATION, GS_EXT_FAIL_POD = 0x1000, 0x2000, 0x4000
 
 
@@ -330,6 +331,8 @@ SIGNATURES = {
     "gs_quota_reserve": (C.c_int, [P, u32, i32, P, u32, i32]),
     "gs_quota_admit_batch": (C.c_int, [P, u32, P, P, P, P, P, P, u32, P, C.POINTER(u32)]),
     "gs_quota_settle_batch": (C.c_int, [P, u32, P, P, P, P, P, P, u32, P, P]),
+    "gs_pods_on_event": (C.c_int, [P, C.c_int, P, P, u32]),
+    "gs_assign_cache_get": (C.c_int, [P, u32, P, P, u32]),
     "gs_ext_args_default": (None, [C.POINTER(GsExtArgs)]),
     "gs_ext_configure": (C.c_int, [P, C.POINTER(GsExtArgs)]),
     "gs_node_devices_upsert": (C.c_int, [P, P, P, u32]),

@@ -1741,6 +1741,34 @@ int gs_pods_unassign(gs_ctx* c, const uint32_t* node_idx, const gs_pod* pods, ui
   return flush_rows(c);
 }
 
+int gs_pods_on_event(gs_ctx* c, int event, const int32_t* node_idx, const gs_pod* pods, uint32_t n) {
+  if (!c || (n && (!node_idx || !pods))) return GS_EINVAL;
+  if (event < GS_POD_EVENT_ADD || event > GS_POD_EVENT_DELETE) return fail(c, GS_EINVAL, "unknown pod event %d", event);
+  for (uint32_t j = 0; j < n; ++j) {
+    const int32_t i = node_idx[j];
+    if (i >= (int32_t)c->N) return fail(c, GS_EINVAL, "node index %d >= %u", i, c->N);
+    if (i < 0) continue;                                      // nodeName == "": assign / unAssign return early
+    const bool terminated = pods[j].flags & GS_POD_TERMINATED;
+    const bool assign = event == GS_POD_EVENT_ADD || (event == GS_POD_EVENT_UPDATE && !terminated);
+    int rc = assign ? gs_pods_assign(c, (const uint32_t*)&node_idx[j], &pods[j], nullptr, 1)
+                    : gs_pods_unassign(c, (const uint32_t*)&node_idx[j], &pods[j], 1);
+    if (rc) return rc;
+  }
+  return GS_OK;
+}
+
+int gs_assign_cache_get(gs_ctx* c, uint32_t node, uint64_t* uids, int64_t* ts, uint32_t cap) {
+  if (!c || node >= c->N) return GS_EINVAL;
+  std::vector<std::pair<uint64_t, int64_t>> v;
+  for (const auto& kv : c->nodes[node].assigned) v.push_back({kv.first, kv.second.ts});
+  std::sort(v.begin(), v.end());
+  for (uint32_t k = 0; k < v.size() && k < cap; ++k) {
+    if (uids) uids[k] = v[k].first;
+    if (ts) ts[k] = v[k].second;
+  }
+  return (int)v.size();
+}
+
 int gs_evaluate(gs_ctx* c, const gs_pod* pods, uint32_t npods, int16_t* scores, uint16_t* codes,
                 int16_t* plugin_scores) {
   if (!c || (npods && !pods)) return GS_EINVAL;

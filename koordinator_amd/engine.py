@@ -112,6 +112,19 @@ class Engine:
         self._chk(lib().gs_schedule(self._h, abi.ptr(pods), len(pods), abi.ptr(seq), abi.ptr(out)), "gs_schedule")
         return out
 
+    def pod_event(self, event: int, node_idx, pods):
+        """podAssignCache OnAdd / OnUpdate / OnDelete (node_idx -1 = pod.Spec.NodeName == "")."""
+        pods = np.ascontiguousarray(pods, dtype=abi.POD_DTYPE)
+        idx = np.ascontiguousarray(node_idx, dtype=np.int32)
+        self._chk(lib().gs_pods_on_event(self._h, event, abi.ptr(idx), abi.ptr(pods), len(pods)), "gs_pods_on_event")
+
+    def assign_cache(self, node: int) -> list[tuple[int, int]]:
+        u = np.zeros(256, np.uint64)
+        t = np.zeros(256, np.int64)
+        n = lib().gs_assign_cache_get(self._h, node, abi.ptr(u), abi.ptr(t), 256)
+        self._chk(min(n, 0), "gs_assign_cache_get")
+        return list(zip(u[:n].tolist(), t[:n].tolist()))
+
     # ---- Reservation + DeviceShare
     def ext_configure(self, args: abi.GsExtArgs):
         self._chk(lib().gs_ext_configure(self._h, C.byref(args)), "gs_ext_configure")

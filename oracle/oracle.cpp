@@ -695,6 +695,42 @@ int or_pods_unassign(or_cluster* c, const uint32_t* node_idx, const gs_pod* pods
   return GS_OK;
 }
 
+// podAssignCache.OnAdd / OnUpdate / OnDelete (pod_assign_cache.go:82-117) over assign / unAssign (:53-80)
+int or_pods_on_event(or_cluster* c, int event, const int32_t* node_idx, const gs_pod* pods, uint32_t n) {
+  if (!c || (n && (!node_idx || !pods))) return GS_EINVAL;
+  for (uint32_t j = 0; j < n; ++j) {
+    const int32_t i = node_idx[j];
+    if (i >= (int32_t)c->nodes.size()) return GS_EINVAL;
+    const bool terminated = pods[j].flags & GS_POD_TERMINATED;
+    bool do_assign;
+    if (event == GS_POD_EVENT_ADD) do_assign = true;
+    else if (event == GS_POD_EVENT_UPDATE) do_assign = !terminated;
+    else if (event == GS_POD_EVENT_DELETE) do_assign = false;
+    else return GS_EINVAL;
+    if (i < 0) continue;   // nodeName == ""
+    if (do_assign) {
+      if (terminated) continue;
+      c->nodes[i].assigned[pods[j].uid] = AssignInfo{c->now, pods[j]};
+    } else {
+      c->nodes[i].assigned.erase(pods[j].uid);
+    }
+  }
+  return GS_OK;
+}
+
+int or_assign_cache_get(or_cluster* c, uint32_t node, uint64_t* uids, int64_t* ts, uint32_t cap) {
+  if (!c || node >= c->nodes.size()) return GS_EINVAL;
+  uint32_t k = 0;
+  for (const auto& kv : c->nodes[node].assigned) {   // std::map: uid order
+    if (k < cap) {
+      if (uids) uids[k] = kv.first;
+      if (ts) ts[k] = kv.second.timestamp;
+    }
+    ++k;
+  }
+  return (int)k;
+}
+
 int or_estimate_pod(const gs_loadaware_args* a, const gs_pod* pod, int64_t out[2], uint32_t* out_mask) {
   if (!a || !pod || !out) return GS_EINVAL;
   ResList e = estimate_pod(*a, *pod);
@@ -859,6 +895,87 @@ int or_take_cpus_test(int sockets, int nodes_per_socket, int cores_per_node, int
   for (int w = 0; w < GS_CPU_WORDS; ++w) result[w] = 0;
   for (int cpu : out) result[cpu >> 6] |= 1ull << (cpu & 63);
   return ok ? 0 : -1;
+}
+
+// NodeAllocation (node_allocation.go:32-177) on a buildCPUTopologyForTest topology (the CoreID = socket<<16 | core
+// form node_allocation_test.go uses): a script of ops. op 0: addCPUs(uid, set, excl); op 1: release(uid);
+// op 2: getAvailableCPUs(maxRef = arg, reserved = none, preferred = set) -> out (4 words per op).
+// refcount[cpu] (256 entries, may be NULL) = allocatedCPUs[cpu].RefCount after the script (-1: no entry).
+int or_node_allocation_script(int sockets, int nodes_per_socket, int cores_per_node, int cpus_per_core, int nops,
+                              const int32_t* op, const uint64_t* uid, const uint64_t* set, const int32_t* arg,
+                              uint64_t* out, int32_t* refcount) {
+  auto topo = orn::build_test_topology(sockets, nodes_per_socket, cores_per_node, cpus_per_core);
+  orn::NodeAllocation na;
+  for (int k = 0; k < nops; ++k) {
+    orn::CPUSet cs;
+    for (int cpu = 0; cpu < GS_MAX_CPUS; ++cpu)
+      if (set[4 * k + (cpu >> 6)] >> (cpu & 63) & 1) cs.insert(cpu);
+    for (int w = 0; w < 4; ++w) out[4 * k + w] = 0;
+    if (op[k] == 0) {
+      orn::PodAllocation pa;
+      pa.uid = uid[k];
+      pa.cpus = cs;
+      pa.excl = arg[k];
+      na.add(pa, topo.get());
+    } else if (op[k] == 1) {
+      na.release(uid[k]);
+    } else if (op[k] == 2) {
+      orn::CPUSet avail;
+      orn::CPUDetails alloc;
+      na.available_cpus(*topo, arg[k], orn::CPUSet{}, cs, &avail, &alloc);
+      for (int cpu : avail) out[4 * k + (cpu >> 6)] |= 1ull << (cpu & 63);
+    } else {
+      return GS_EINVAL;
+    }
+  }
+  if (refcount)
+    for (int cpu = 0; cpu < GS_MAX_CPUS; ++cpu) {
+      auto it = na.allocated_cpus.find(cpu);
+      refcount[cpu] = it == na.allocated_cpus.end() ? -1 : it->second.ref;
+    }
+  return GS_OK;
+}
+
+// getAvailableNUMANodeResources (node_allocation.go:141-177) for two NUMA nodes of a buildCPUTopologyForTest topology:
+// zone resources zone_cpu/zone_mem, AmplificationRatios[cpu] = amp (<= 1: none), allocatedResources[0] cpu =
+// alloc_cpu0 (0: no entry), the first n_cpuset CPUs in allocatedCPUs. avail / alloc: [zone][cpu, mem], masks bit
+// 2*zone + r = key present (alloc_mask bit 4 = zone entry present).
+int or_available_numa_test(int sockets, int nodes_per_socket, int cores_per_node, int cpus_per_core, double amp,
+                           int64_t zone_cpu, int64_t zone_mem, int64_t alloc_cpu0, int n_cpuset, int64_t* avail,
+                           uint32_t* avail_mask, int64_t* alloc, uint32_t* alloc_mask) {
+  orn::TopologyOptions o;
+  o.present = true;
+  o.topo = orn::build_test_topology(sockets, nodes_per_socket, cores_per_node, cpus_per_core);
+  o.max_ref = 1;
+  o.amp_ratio = amp;
+  for (int z = 0; z < 2; ++z) {
+    orn::NUMANodeResource r;
+    r.node = z;
+    r.res.set(GS_RES_CPU, zone_cpu);
+    r.res.set(GS_RES_MEMORY, zone_mem);
+    o.numa.push_back(r);
+  }
+  orn::NodeAllocation na;
+  if (alloc_cpu0) {
+    orn::NUMANodeResource r;
+    r.node = 0;
+    r.res.set(GS_RES_CPU, alloc_cpu0);
+    na.allocated_res[0] = r;
+  }
+  for (int cpu = 0; cpu < n_cpuset; ++cpu) na.allocated_cpus[cpu] = o.topo->details[cpu];
+  std::map<int, orn::RL> ta, tl;
+  na.available_numa(o, &ta, &tl);
+  *avail_mask = *alloc_mask = 0;
+  for (int z = 0; z < 2; ++z)
+    for (int r = 0; r < 2; ++r) {
+      avail[2 * z + r] = alloc[2 * z + r] = 0;
+      if (ta.count(z) && ta[z].has(r)) { avail[2 * z + r] = ta[z].v[r]; *avail_mask |= 1u << (2 * z + r); }
+      if (tl.count(z)) {
+        *alloc_mask |= 1u << (4 + z);
+        if (tl[z].has(r)) { alloc[2 * z + r] = tl[z].v[r]; *alloc_mask |= 1u << (2 * z + r); }
+      }
+    }
+  return GS_OK;
 }
 
 // [upstream] Scheduler.numFeasibleNodesToFind (schedule_one.go): minFeasibleNodesToFind = 100,

@@ -30,6 +30,8 @@ int or_node_metrics_upsert(or_cluster* c, const uint32_t* idx, const gs_node_met
                            const gs_pod_metric* pm, const uint32_t* pm_offsets);
 int or_pods_assign(or_cluster* c, const uint32_t* node_idx, const gs_pod* pods, const int64_t* ts, uint32_t n);
 int or_pods_unassign(or_cluster* c, const uint32_t* node_idx, const gs_pod* pods, uint32_t n);
+int or_pods_on_event(or_cluster* c, int event, const int32_t* node_idx, const gs_pod* pods, uint32_t n);
+int or_assign_cache_get(or_cluster* c, uint32_t node, uint64_t* uids, int64_t* ts, uint32_t cap);
 
 /* plugin-level restatements */
 int or_estimate_pod(const gs_loadaware_args* a, const gs_pod* pod, int64_t out[2], uint32_t* out_mask);
@@ -65,6 +67,13 @@ int or_set_hint_order(or_cluster* c, int reverse);
 int or_take_cpus_test(int sockets, int nodes_per_socket, int cores_per_node, int cpus_per_core, int max_ref,
                       const uint64_t* available, const int32_t* alloc_ref, const int32_t* alloc_excl, int needed,
                       int bind, int excl, int strategy, uint64_t* result);
+/* NodeAllocation scripts and getAvailableNUMANodeResources on test topologies (node_allocation_test.go vectors) */
+int or_node_allocation_script(int sockets, int nodes_per_socket, int cores_per_node, int cpus_per_core, int nops,
+                              const int32_t* op, const uint64_t* uid, const uint64_t* set, const int32_t* arg,
+                              uint64_t* out, int32_t* refcount);
+int or_available_numa_test(int sockets, int nodes_per_socket, int cores_per_node, int cpus_per_core, double amp,
+                           int64_t zone_cpu, int64_t zone_mem, int64_t alloc_cpu0, int n_cpuset, int64_t* avail,
+                           uint32_t* avail_mask, int64_t* alloc, uint32_t* alloc_mask);
 /* seconds per scheduleOne phase since the last call: Filter, Score, selectHost, Reserve + assume (then reset) */
 int or_phase_times(or_cluster* c, double out[4]);
 /* the selectHost tie-break stream: Intn(cnt) of pod stream `seq` (see oracle.cpp TieBreakRand) */

@@ -56,6 +56,11 @@ def _load() -> C.CDLL:
         "or_take_cpus_test": (C.c_int, [C.c_int] * 5 + [P, P, P] + [C.c_int] * 4 + [P]),
         "or_policy_merge": (C.c_int, [C.c_int, C.c_uint64, C.c_int, P, P, P, P, P, P, P]),
         "or_iterate_bitmasks": (C.c_int, [P, C.c_int, P, C.c_int]),
+        "or_pods_on_event": (C.c_int, [P, C.c_int, P, P, C.c_uint32]),
+        "or_assign_cache_get": (C.c_int, [P, C.c_uint32, P, P, C.c_uint32]),
+        "or_node_allocation_script": (C.c_int, [C.c_int] * 5 + [P, P, P, P, P, P]),
+        "or_available_numa_test": (C.c_int, [C.c_int] * 4 + [C.c_double, C.c_int64, C.c_int64, C.c_int64, C.c_int,
+                                                              P, P, P, P]),
         "or_ext_args_default": (None, [C.POINTER(abi.GsExtArgs)]),
         "or_ext_configure": (C.c_int, [P, C.POINTER(abi.GsExtArgs)]),
         "or_node_devices_upsert": (C.c_int, [P, P, P, C.c_uint32]),
@@ -229,6 +234,18 @@ class Oracle:
     def next_start_node_index(self) -> int:
         return int(lib().or_next_start_node_index(self._h))
 
+    def pod_event(self, event: int, node_idx, pods):
+        pods = np.ascontiguousarray(pods, dtype=abi.POD_DTYPE)
+        idx = np.ascontiguousarray(node_idx, dtype=np.int32)
+        _chk(lib().or_pods_on_event(self._h, event, abi.ptr(idx), abi.ptr(pods), len(pods)), "pods_on_event")
+
+    def assign_cache(self, node: int) -> list[tuple[int, int]]:
+        u = np.zeros(256, np.uint64)
+        t = np.zeros(256, np.int64)
+        n = lib().or_assign_cache_get(self._h, node, abi.ptr(u), abi.ptr(t), 256)
+        _chk(min(n, 0), "assign_cache_get")
+        return list(zip(u[:n].tolist(), t[:n].tolist()))
+
     # ---- Reservation + DeviceShare
     def ext_configure(self, args: abi.GsExtArgs):
         _chk(lib().or_ext_configure(self._h, C.byref(args)), "ext_configure")
@@ -282,6 +299,45 @@ class Oracle:
         _chk(lib().or_schedule_replay(self._h, abi.ptr(pods), len(pods), abi.ptr(seq), abi.ptr(given),
                                       abi.ptr(out), int(nthreads)), "schedule_replay")
         return out
+
+
+def node_allocation_script(topology, ops):
+    """ops: [("add", uid, cpus, excl) | ("release", uid) | ("available", max_ref, preferred_cpus)]; returns the
+    available-CPU lists of the "available" ops and the final RefCount per CPU (dict, allocated CPUs only)."""
+    n = len(ops)
+    op = np.zeros(n, np.int32)
+    uid = np.zeros(n, np.uint64)
+    sets = np.zeros((n, 4), np.uint64)
+    arg = np.zeros(n, np.int32)
+    for k, o in enumerate(ops):
+        cpus = o[2] if o[0] in ("add", "available") else []
+        if o[0] == "add":
+            op[k], uid[k], arg[k] = 0, o[1], o[3]
+        elif o[0] == "release":
+            op[k], uid[k] = 1, o[1]
+        else:
+            op[k], arg[k] = 2, o[1]
+        for c in cpus:
+            sets[k, c >> 6] |= np.uint64(1 << (c & 63))
+    out = np.zeros((n, 4), np.uint64)
+    ref = np.zeros(256, np.int32)
+    _chk(lib().or_node_allocation_script(*topology, n, abi.ptr(op), abi.ptr(uid), abi.ptr(sets), abi.ptr(arg),
+                                         abi.ptr(out), abi.ptr(ref)), "node_allocation_script")
+    avail = [[c for c in range(256) if int(out[k, c >> 6]) >> (c & 63) & 1] for k in range(n) if ops[k][0] == "available"]
+    return avail, {c: int(ref[c]) for c in range(256) if ref[c] >= 0}
+
+
+def available_numa_test(topology, amp, zone_cpu, zone_mem, alloc_cpu0, n_cpuset):
+    av = np.zeros(4, np.int64)
+    al = np.zeros(4, np.int64)
+    am = np.zeros(1, np.uint32)
+    lm = np.zeros(1, np.uint32)
+    _chk(lib().or_available_numa_test(*topology, amp, zone_cpu, zone_mem, alloc_cpu0, n_cpuset, abi.ptr(av),
+                                      abi.ptr(am), abi.ptr(al), abi.ptr(lm)), "available_numa_test")
+    avail = {z: {r: int(av[2 * z + r]) for r in range(2) if am[0] >> (2 * z + r) & 1} for z in range(2)}
+    alloc = {z: {r: int(al[2 * z + r]) for r in range(2) if lm[0] >> (2 * z + r) & 1}
+             for z in range(2) if lm[0] >> (4 + z) & 1}
+    return avail, alloc
 
 
 def ext_args_default() -> abi.GsExtArgs:

@@ -6,6 +6,7 @@ fails the run) and re-runs the full scheduleOne over all 100k nodes for a sample
 node, max score, tie count and feasible count must be identical. About 32 FitError pods are re-checked in full
 (the others are replayed as FitErrors: a wrong one would shift the state every later sampled pod sees)."""
 import os
+import time
 
 import numpy as np
 import pytest
@@ -36,6 +37,7 @@ def _replay_check(c, cfg, got, sample):
 
 def test_c3_100k_nodes_50k_pods_replay_parity():
     from koordinator_amd.engine import Engine
+    t0 = time.perf_counter()
     c = synth.make_cluster(100_000, 50_000, 3)
     synth.make_numa(c)
     cfg = config.make_config(c.num_nodes, enabled=abi.GS_ENABLE_ALL)
@@ -44,7 +46,48 @@ def test_c3_100k_nodes_50k_pods_replay_parity():
     got = e.schedule(c.pods)
     assert e.mirror_check() == 0
     P = len(c.pods)
-    sample = np.unique(np.concatenate([np.arange(48), np.linspace(48, P - 1, 48).astype(np.int64)]))
+    sample = np.unique(np.concatenate([np.arange(48), np.arange(48, P, 64)]))   # every 64th pod
     n = _replay_check(c, cfg, got, sample)
     placed = int((got["node"] >= 0).sum())
-    print(f"100k x 50k: {placed} placed, {n} pods re-scheduled by the oracle and identical; stats {e.stats()}")
+    print(f"100k x 50k: {placed} placed, {n} pods re-scheduled by the oracle and identical; "
+          f"wall {time.perf_counter() - t0:.1f} s; stats {e.stats()}")
+
+
+def test_c3_bench_config_50k_nodes_replay_parity():
+    """Exactly the bench's workload (bench.py defaults: C3 cluster of config id 2, 50,000 nodes, 2048-pod calls,
+    batch 128): 10 calls (20,480 pods), every 64th pod re-scheduled by the oracle over all 50k nodes."""
+    from koordinator_amd.engine import Engine
+    t0 = time.perf_counter()
+    P, step = 20_480, 2048
+    c = synth.make_cluster(50_000, P, config_id=2)
+    synth.make_numa(c)
+    cfg = config.make_config(c.num_nodes, batch_size=128, enabled=abi.GS_ENABLE_ALL)
+    e = Engine(cfg)
+    synth.load_into(e, c)
+    seq = np.arange(P, dtype=np.uint64)
+    got = np.concatenate([e.schedule(c.pods[k:k + step], seq[k:k + step]) for k in range(0, P, step)])
+    assert e.mirror_check() == 0
+    n = _replay_check(c, cfg, got, np.arange(0, P, 64))
+    print(f"C3 bench config 50k x {P}: {int((got['node'] >= 0).sum())} placed, {n} pods re-checked in full; "
+          f"wall {time.perf_counter() - t0:.1f} s")
+
+
+def test_c2_5k_nodes_10k_pods_full_parity():
+    """C2: 5,000 nodes x 10,000 pods, NodeResourcesFit + LoadAwareScheduling; every pod's node, max
+    score, tie count and feasible count compared with the oracle's full sequential scheduleOne."""
+    from koordinator_amd.engine import Engine
+    t0 = time.perf_counter()
+    c = synth.make_cluster(5_000, 10_000, config_id=1)
+    cfg = config.make_config(c.num_nodes, enabled=abi.GS_ENABLE_LA_FIT)
+    e = Engine(cfg)
+    synth.load_into(e, c)
+    got = e.schedule(c.pods)
+    assert e.mirror_check() == 0
+    o = orc.Oracle(cfg)
+    synth.load_into(o, c)
+    want = o.schedule(c.pods, nthreads=THREADS)
+    for f in ("node", "score", "ties", "feasible"):
+        bad = np.nonzero(got[f] != want[f])[0]
+        assert len(bad) == 0, f"{f} differs at pods {bad[:5]}"
+    print(f"C2 5k x 10k: {int((got['node'] >= 0).sum())} placed, all 10,000 decisions identical; "
+          f"wall {time.perf_counter() - t0:.1f} s")
