@@ -507,6 +507,10 @@ typedef struct gs_ext_args {
                                              (v1beta2 default: gpu-memory-ratio = 1, defaults.go:187-203) */
   int64_t weight_deviceshare;      /* profile score weights */
   int64_t weight_reservation;
+  uint32_t fit_ignored_gpu_names;  /* [upstream] NodeResourcesFitArgs.IgnoredResources / IgnoredResourceGroups on the GPU
+                                      names (extended resources): bit n = name n is ignored, or its domain (the text
+                                      before '/') is an ignored group; Fit then skips its scalar check */
+  uint32_t pad0;
 } gs_ext_args;
 
 #define GS_EXT_FAIL_DEVICE 0x1000u      /* DeviceShare Filter: "Insufficient gpu devices" and the Prepare errors */

@@ -243,7 +243,8 @@ class GsPodExt(C.Structure):
 
 class GsExtArgs(C.Structure):
     _fields_ = [("enabled", u32), ("device_scoring_type", i32), ("device_weights", i64 * GS_NUM_GPU_RES),
-                ("weight_deviceshare", i64), ("weight_reservation", i64)]
+                ("weight_deviceshare", i64), ("weight_reservation", i64), ("fit_ignored_gpu_names", u32),
+                ("pad0", u32)]
 
 
 class GsExtPlacement(C.Structure):

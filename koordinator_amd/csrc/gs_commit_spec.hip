@@ -58,18 +58,21 @@ struct Job {
 
 __device__ __forceinline__ void sp_sleep() { __builtin_amdgcn_s_sleep(2); }
 
-size_t spec_smem_bytes(int B) {
-  size_t b = (size_t)B * POD_STRIDE;                  // pods
-  b += (size_t)B * sizeof(Row);                       // dirty rows
-  b += (size_t)B * B * 2 * 2;                         // dsc, dso
-  b = (b + 15) & ~(size_t)15;
-  b += (size_t)B * sizeof(CpuStateDev);               // cpu state of the dirty rows
-  b += (size_t)B * sizeof(DecRec);
-  b += (size_t)SP_LAG * sizeof(UndoRec);
-  b += (size_t)SP_TABLES * sizeof(HintTable);
-  b += (size_t)B * 4 * 5;                              // final_F, done_ver, has_row, rescored, jobs_left
-  b += (size_t)SP_HASH * 8;
-  b += (size_t)SP_JOBQ * sizeof(Job);
+size_t spec_smem_bytes(int B) {   // the kernel's LDS carve-up, piece by piece with take()'s 16-B rounding
+  size_t b = 0;
+  auto take = [&](size_t bytes) { b += (bytes + 15) & ~(size_t)15; };
+  take((size_t)B * POD_STRIDE);                     // pods
+  take((size_t)B * sizeof(Row));                    // dirty rows
+  take((size_t)B * B * 2);                          // dsc
+  take((size_t)B * B * 2);                          // dso
+  take((size_t)B * sizeof(CpuStateDev));            // cpu state of the dirty rows
+  take((size_t)B * sizeof(DecRec));
+  take((size_t)SP_LAG * sizeof(UndoRec));
+  take((size_t)SP_TABLES * sizeof(HintTable));
+  for (int i = 0; i < 5; ++i) take((size_t)B * 4);  // final_F, done_ver, has_row, rescored, jobs_left
+  take((size_t)SP_HASH * 4);                        // hkey
+  take((size_t)SP_HASH * 4);                        // hval
+  take((size_t)SP_JOBQ * sizeof(Job));
   return b + 64;
 }
 
@@ -78,7 +81,7 @@ size_t spec_smem_bytes(int B) {
 // 9 decisions, 10 full-row decisions, 11 full-row cycles, 12 wave 0 total
 template <bool ST>
 __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
-  uint64_t st_acc[15] = {};
+  uint64_t st_acc[18] = {};
   uint64_t st_last = ST ? __builtin_amdgcn_s_memtime() : 0;
   const uint64_t st_t0 = st_last;
 #define SPM(i)                                          \
@@ -155,6 +158,7 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
     int nd = 0, q = 0, v = 0, wm = 0, end_at = B, end_why = 0;
     int committed = 0;
     bool host_cut = false, err = false;
+    int err_code = 0;   // which bounded wait expired (reported in committed[3])
     auto each_node = [&](uint64_t m0, uint64_t m1, auto&& fn) {
       for (uint64_t b = m0; b; b &= b - 1) fn((uint32_t)__builtin_amdgcn_readlane((int)dn0, __builtin_ctzll(b)));
       for (uint64_t b = m1; b; b &= b - 1) fn((uint32_t)__builtin_amdgcn_readlane((int)dn1, __builtin_ctzll(b)));
@@ -215,7 +219,7 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
           st_rel(&s_stop, 1);
           spins = 0;
           while (ld_acq(&s_parked) < SP_WAVES - 1) {
-            if (++spins > SP_SPIN_LIMIT) { err = true; break; }
+            if (++spins > SP_SPIN_LIMIT) { err = true; err_code = 1; break; }
             sp_sleep();
           }
           if (err) break;
@@ -305,7 +309,7 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
       SPM(1);
       // ------------------------------------------------ decide pod q
       if (q >= end_at || q - v >= SP_LAG || ld_acq(&s_cut_at) >= 0) {
-        if (++spins > SP_SPIN_LIMIT) { err = true; break; }
+        if (++spins > SP_SPIN_LIMIT) { err = true; err_code = 2; break; }
         sp_sleep();
         continue;
       }
@@ -319,7 +323,7 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
       const bool rdy0 = lane < nd && dv0 == pv0, rdy1 = lane + 64 < nd && dv1 == pv1;
       const uint64_t pend0 = __ballot(lane < nd && !rdy0), pend1 = __ballot(lane + 64 < nd && !rdy1);
       if ((a.dbg & 1u) && (pend0 | pend1)) {   // diagnostics: no speculation, wait for the pending rows
-        if (++spins > SP_SPIN_LIMIT) { err = true; break; }
+        if (++spins > SP_SPIN_LIMIT) { err = true; err_code = 3; break; }
         sp_sleep();
         continue;
       }
@@ -614,13 +618,20 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
       if (ST) st_acc[9] += 1;
       SPM(0);
     }
+    if (!err && committed > 0) {   // every committed pod's Reserve is in place before the waves stop
+      uint32_t w = 0;
+      while (ld_acq(&s_reserved) < committed) {
+        if (++w > SP_SPIN_LIMIT) { err = true; err_code = 4; break; }
+        sp_sleep();
+      }
+    }
     if (ST) st_acc[12] = __builtin_amdgcn_s_memtime() - st_t0;
     if (lane == 0) {
       s_committed = committed;
       s_endwhy = committed < B ? (end_why << 16 | (host_cut ? 0x8000 : 0) | (end_at & 0xfff)) : 0;
       s_hostcut = host_cut ? 1 : 0;
       s_nd = nd;
-      if (err) s_err = 1;
+      if (err) s_err = err_code ? err_code : 9;
       st_rel(&s_finish, 1);
     }
   } else if (wv == 1) {
@@ -725,6 +736,7 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
         if (lane == 0) u.slot = slot;
       }
       WAVE_FENCE();
+      SPM(15);   // row fetch + undo log
       Row& dr_ = drows[slot];
       if (numa_on) {
         const int tp = cst[slot].topo;
@@ -748,6 +760,7 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
         NumaOut no{};
         if (numa_reserve)
           no = numa_eval<true, false, true>(dr.nr, pk, a.pf, SlotsLds{dr, m}, a.pf.enabled & 0x10u, false, s_aff);
+        SPM(16);   // topology staging + the Reserve's NUMA Allocate (numa_eval)
         if (lane == 0) {
           PlacementDev pl{(int32_t)winner, (uint32_t)d.F, (int64_t)d.M, (uint32_t)d.T, (d.flags & SP_SLOW) ? 1u : 0u,
                           0, 0, {0, 0, 0, 0}, {0, 0, 0, 0}};
@@ -805,6 +818,7 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
       }
       cut = __builtin_amdgcn_readlane(cut, 0);
       WAVE_FENCE();
+      SPM(17);   // lane 0: placement record, zone split, cpuset_reserve, assume deltas
       // ---- the row's re-scoring: hint table of its new state, jobs of 64 later pods
       const int nlater = B - (q + 1);
       const int njobs = (nlater + 63) / 64;
@@ -897,14 +911,14 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
     }
   for (int i = tid; i < committed; i += SP_THREADS) a.out[i].feasible = (uint32_t)final_F[i];
   if (ST && lane == 0)
-    for (int i = 0; i < 15; ++i)
+    for (int i = 0; i < 18; ++i)
       if (st_acc[i]) atomicAdd(reinterpret_cast<unsigned long long*>(&a.stamps[i]), (unsigned long long)st_acc[i]);
 #undef SPM
   if (tid == 0) {
     a.committed[0] = committed;
     a.committed[1] = (committed == B && !s_hostcut && !s_err) ? 1 : 0;
     a.committed[2] = s_endwhy;   // diagnostics: why a batch ended early (GS_DEBUG_CUTS)
-    a.committed[3] = s_err ? 1 : 0;
+    a.committed[3] = s_err;
   }
 }
 

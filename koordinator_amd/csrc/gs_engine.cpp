@@ -931,7 +931,8 @@ int finish_batch(gs_ctx* c, int b, bool clobbered, int* committed_out) {
   c->stats.batches += 1;
   int committed = c->h_committed[0];
   if (committed < 0) return fail(c, GS_ESTATE, "commit pass of a batch was voided unexpectedly");
-  if (c->h_committed[3]) return fail(c, GS_EDEVICE, "commit kernel: a pipeline wait expired (internal error)");
+  if (c->h_committed[3])
+    return fail(c, GS_EDEVICE, "commit kernel: a pipeline wait expired (internal error, site %d)", c->h_committed[3]);
   if (c->window_k) {
     if (committed == 0) return fail(c, GS_ESTATE, "node-sampling commit made no progress");
     c->next_start = (uint32_t)c->h_committed[2];
@@ -1289,7 +1290,8 @@ int ext_schedule_one(gs_ctx* c, const gs_pod& pod, const gs_pod_ext& e, uint64_t
   xp = ExtPod{};
   for (int r = 0; r < 3; ++r) { xp.gpu_req[r] = greq[r]; xp.dev_w[r] = c->ext.device_weights[r]; }
   xp.gpu_mask = gmask;
-  xp.gpu_names = gmask ? (e.gpu_request_mask & 0x1Fu) : 0u;
+  const uint32_t gpu_names_all = gmask ? (e.gpu_request_mask & 0x1Fu) : 0u;   // NodeInfo.AddPod adds them all
+  xp.gpu_names = gpu_names_all & ~c->ext.fit_ignored_gpu_names;               // Fit checks the non-ignored ones
   for (int n = 0; n < GS_NUM_GPU_NAMES; ++n) xp.gpu_name_req[n] = (xp.gpu_names >> n & 1u) ? e.gpu_requests[n] : 0;
   xp.w_ds = c->ext.weight_deviceshare;
   xp.w_rs = c->ext.weight_reservation;
@@ -1302,7 +1304,7 @@ int ext_schedule_one(gs_ctx* c, const gs_pod& pod, const gs_pod_ext& e, uint64_t
   xp.dev_most = c->ext.device_scoring_type == GS_SCORING_MOST_ALLOCATED;
   xp.seq = seq;
   // GPU names are scalar requests: the Fit filter's all-zero short cut no longer applies
-  if (xp.gpu_names) v.flags &= ~PF_ALL_ZERO;
+  if (gpu_names_all) v.flags &= ~PF_ALL_ZERO;
   c->h_pods[0] = v;
   c->h_seq[0] = seq;
   // numa_idx (the eval pass's NUMA-policy work list) as launch_batch keeps it
@@ -1379,7 +1381,7 @@ int ext_schedule_one(gs_ctx* c, const gs_pod& pod, const gs_pod_ext& e, uint64_t
     }
   }
   for (int n = 0; n < GS_NUM_GPU_NAMES; ++n)   // NodeInfo.AddPod of the GPU-name scalars
-    if (xp.gpu_names >> n & 1u) { c->devs[node].requested[n] += e.gpu_requests[n]; dev_mark(c, node); }
+    if (gpu_names_all >> n & 1u) { c->devs[node].requested[n] += e.gpu_requests[n]; dev_mark(c, node); }
   apply_placement(c, pod, xo.node, true);
   return GS_OK;
 }
@@ -1606,6 +1608,8 @@ int gs_destroy(gs_ctx* c) {
                 (unsigned long long)st[3], st[5] / np, st[6] / np, st[7] / np, st[8] / np, (unsigned long long)st[9],
                 (unsigned long long)st[10], st[10] ? (double)st[11] / st[10] : 0.0, (unsigned long long)st[13],
                 (unsigned long long)st[14], st[12] / np);
+        fprintf(stderr, "gpuscore spec commit, Reserve wave per committed pod: fetch+undo %.0f numa_eval %.0f "
+                "lane0 (zone split, cpuset, assume) %.0f rest %.0f\n", st[15] / np, st[16] / np, st[17] / np, st[5] / np);
         (void)hipFree(c->d_stamps);
         c->d_stamps = nullptr;
       }
@@ -2220,6 +2224,7 @@ void gs_ext_args_default(gs_ext_args* a) {
 int gs_ext_configure(gs_ctx* c, const gs_ext_args* a) {
   if (!c || !a) return GS_EINVAL;
   if (a->enabled & ~(GS_EXT_DEVICESHARE | GS_EXT_RESERVATION)) return fail(c, GS_EINVAL, "unknown extension plugin bits");
+  if (a->fit_ignored_gpu_names & ~0x1Fu) return fail(c, GS_EINVAL, "fit_ignored_gpu_names outside the GPU names");
   if (a->device_scoring_type != GS_SCORING_LEAST_ALLOCATED && a->device_scoring_type != GS_SCORING_MOST_ALLOCATED)
     return fail(c, GS_EINVAL, "DeviceShare scoring strategy not supported");
   for (int r = 0; r < GS_NUM_GPU_RES; ++r)

@@ -107,13 +107,23 @@ __global__ void __launch_bounds__(128) patch_kernel(MirrorView m, const PodVec* 
   const int32_t node = prev_out[k].node;
   if (node < 0 || (uint32_t)node < n0 || (uint32_t)node >= n1) return;
   const bool numa = (pf.enabled & 0x30u) != 0;
+  // the row once per block (scalar slots included), and for a NUMA-policy row its hint table (the sums of every
+  // zone subset, built by 60 lanes), which every pod of the batch then reads instead of recomputing the hints
+  __shared__ Row s_row;
+  __shared__ HintTable s_tab;
+  if (threadIdx.x == 0) {
+    load_row(m, (uint32_t)node, prod_cols, numa, s_row);
+    for (int sl = 3; sl < 7; ++sl) s_row.free[sl] = m.c64(C_FREE_CPU + sl)[node];
+  }
+  __syncthreads();
+  const bool policy = numa && ((s_row.nr.nflags >> NF_POLICY_SHIFT) & 3u);
+  if (policy && threadIdx.x < 64) hint_table_fill(s_tab, s_row.nr, zone_avail(s_row.nr), (int)threadIdx.x);
+  __syncthreads();
+  const Row r = s_row;
   for (int q = threadIdx.x; q < npods; q += 128) {
-    Row r;
-    load_row(m, (uint32_t)node, prod_cols, numa, r);
-    const PairOut o = eval_pair<false, false, true>(r, pods[q], pf, m);
+    const PairOut o = eval_pair<false, true, true, true>(r, pods[q], pf, m, &s_tab);
     S[(size_t)q * ld + ((uint32_t)node - n0)] = (int16_t)total_score(o, pf);
-    if (numa && ((r.nr.nflags >> NF_POLICY_SHIFT) & 3u))
-      aff[(size_t)q * ld + ((uint32_t)node - n0)] = (uint8_t)(o.code ? 0u : o.aff);
+    if (policy) aff[(size_t)q * ld + ((uint32_t)node - n0)] = (uint8_t)(o.code ? 0u : o.aff);
   }
 }
 
@@ -168,13 +178,19 @@ __global__ void __launch_bounds__(64 * W) cand_kernel(const int16_t* __restrict_
   const uint32_t seg = (lenv / 512 + W - 1) / W * 512;
   const uint32_t wb = min(lenv, wave * seg), we = min(lenv, wb + seg);
   const int4* row4 = reinterpret_cast<const int4*>(row);
-  // pass 1: per-wave histograms of feasible scores
-  for (uint32_t i = wb + lane * 8; i < we; i += 512) {
-    int4 q = row4[i / 8];
-    const int16_t* e = reinterpret_cast<const int16_t*>(&q);
+  // pass 1: per-wave histograms of feasible scores; 4 loads in flight per lane (the pass is load-latency bound:
+  // one workgroup streams a whole row)
+  for (uint32_t i = wb + lane * 8; i < we; i += 4 * 512) {
+    int4 q[4];
 #pragma unroll
-    for (int x = 0; x < 8; ++x)
-      if (e[x] >= 0) atomicAdd(&whist[wave * nbins + e[x]], 1u);
+    for (int u = 0; u < 4; ++u) q[u] = i + u * 512 < we ? row4[(i + u * 512) / 8] : make_int4(-1, -1, -1, -1);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int16_t* e = reinterpret_cast<const int16_t*>(&q[u]);
+#pragma unroll
+      for (int x = 0; x < 8; ++x)
+        if (e[x] >= 0) atomicAdd(&whist[wave * nbins + e[x]], 1u);
+    }
   }
   __syncthreads();
   const int per = (nbins + CAND_THREADS - 1) / CAND_THREADS;
@@ -237,8 +253,10 @@ __global__ void __launch_bounds__(64 * W) cand_kernel(const int16_t* __restrict_
   uint32_t* out = lists + (size_t)k * LCAP;
   if (nlev > 0) {
     uint32_t run_l = lane < LEVALL ? s_woff[wave][lane] : 0;   // level `lane`'s next output position (this wave)
+    int4 qn = wb < we ? row4[(wb + lane * 8) / 8] : make_int4(-1, -1, -1, -1);
     for (uint32_t base = wb; base < we; base += 512) {
-      int4 q = row4[(base + lane * 8) / 8];
+      int4 q = qn;   // the next step's load is issued before this step's scans
+      if (base + 512 < we) qn = row4[(base + 512 + lane * 8) / 8];
       const int16_t* e = reinterpret_cast<const int16_t*>(&q);
       int slot[8];
       uint32_t present = 0;

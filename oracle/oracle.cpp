@@ -1733,6 +1733,7 @@ int or_schedule_ext(or_cluster* c, const gs_pod* pods, const gs_pod_ext* ext, ui
           }
           for (int g = 0; g < GS_NUM_GPU_NAMES; ++g) {
             if (!(gpu_names & (1u << g))) continue;
+            if (c->ext.fit_ignored_gpu_names & (1u << g)) continue;   // IgnoredResources / IgnoredResourceGroups
             const int64_t a = d.allocatable[g], r = d.requested[g];
             if (e.gpu_requests[g] > a - r) code |= GS_FAIL_FIT_SCALAR;
           }

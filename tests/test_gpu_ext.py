@@ -11,12 +11,13 @@ from oracle import oracle as orc
 pytestmark = pytest.mark.gpu
 
 
-def run_pair(c, strategy=None, enabled=abi.GS_ENABLE_LA_FIT, chunks=1):
+def run_pair(c, strategy=None, enabled=abi.GS_ENABLE_LA_FIT, chunks=1, ignored=0):
     from koordinator_amd.engine import Engine
     cfg = config.make_config(c.num_nodes, enabled=enabled)
     a = orc.ext_args_default()
     if strategy == "MostAllocated":
         a.device_scoring_type = abi.GS_SCORING_MOST_ALLOCATED
+    a.fit_ignored_gpu_names = ignored
     e, o = Engine(cfg), orc.Oracle(cfg)
     for x in (e, o):
         synth.load_into(x, c)
@@ -86,3 +87,17 @@ def test_c5_with_numa_profile_without_policy_nodes():
     synth.make_ext(c)
     e, o, ge, oe = run_pair(c, enabled=abi.GS_ENABLE_ALL)
     check(c, e, o, ge, oe)
+
+
+def test_c5_fit_ignored_resource_group():
+    """NodeResourcesFitArgs.IgnoredResourceGroups = ["koordinator.sh"]: Fit skips the koordinator.sh/* GPU names
+    (DeviceShare still filters on the devices); nvidia.com/gpu stays checked."""
+    c = synth.make_cluster(1500, 500, config_id=10)
+    synth.make_ext(c, gpu_node_pct=30, gpu_pod_pct=40)
+    # NodeInfo scalars that would fail Fit for every koordinator.sh request
+    c.ext["devices"]["allocatable"][:, 1:] = 0
+    ign = sum(1 << abi.GPU_NAMES[n] for n in ("koordinator.sh/gpu", "koordinator.sh/gpu-core",
+                                              "koordinator.sh/gpu-memory", "koordinator.sh/gpu-memory-ratio"))
+    e, o, ge, oe = run_pair(c, ignored=ign)
+    check(c, e, o, ge, oe)
+    assert (ge[1]["gpu_count"] > 0).sum() > 20
