@@ -31,7 +31,7 @@
 namespace gs {
 
 constexpr int SP_WAVES = 8, SP_THREADS = 64 * SP_WAVES;
-constexpr int SP_LAG = 8;        // decided - verified <= SP_LAG (undo log depth)
+constexpr int SP_LAG = 16;       // decided - verified <= SP_LAG (undo log depth)
 constexpr int SP_TABLES = SP_WAVES - 2;   // one hint table per re-scoring wave
 constexpr int SP_JOBQ = 32;      // re-scoring job ring
 constexpr int SP_HASH = 256;     // node -> slot (full-row resolution)
@@ -81,7 +81,7 @@ size_t spec_smem_bytes(int B) {   // the kernel's LDS carve-up, piece by piece w
 // 9 decisions, 10 full-row decisions, 11 full-row cycles, 12 wave 0 total
 template <bool ST>
 __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
-  uint64_t st_acc[18] = {};
+  uint64_t st_acc[28] = {};
   uint64_t st_last = ST ? __builtin_amdgcn_s_memtime() : 0;
   const uint64_t st_t0 = st_last;
 #define SPM(i)                                          \
@@ -141,6 +141,7 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
     jobs_left[i] = 0;
   }
   for (int i = tid; i < SP_HASH; i += SP_THREADS) { hkey[i] = -1; hval[i] = -1; }
+  for (int i = tid; i < B; i += SP_THREADS) tiebreak_records(a.seed, a.seq[i], a.tb + (size_t)i * TB_N);
   if (tid == 0) {
     s_decided = 0; s_reserved = 0; s_stop = 0; s_parked = 0; s_finish = 0; s_cut_at = -1; s_err = 0;
     s_jq_head = 0; s_jq_tail = 0; s_committed = 0; s_hostcut = 0; s_nd = 0;
@@ -181,7 +182,7 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
     };
     // header of pod p (lanes 0..7: level j score / count) and the head of its level list (lane i: entry i)
     // (all LEVALL levels: the LevelHdr's first MAXLEV and the LevelExt's rest)
-    auto load_hdr = [&](int p, int& hs, int& hc, int& nlev, int& feas, int& next, uint32_t& lh) {
+    auto load_hdr = [&](int p, int& hs, int& hc, int& nlev, int& feas, int& next, uint32_t& lh, int32_t& tbv) {
       const LevelHdr* h = hdr_ptr(a, 0, p);
       const LevelExt* x = reinterpret_cast<const LevelExt*>(a.xbase + (size_t)a.bmax * LCAP * 4 +
                                                             (size_t)a.bmax * sizeof(LevelHdr)) + p;
@@ -190,11 +191,31 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
       next = x->next;
       hs = lane < MAXLEV ? h->score[lane] : lane < LEVALL ? x->score[lane - MAXLEV] : -1;
       hc = lane < MAXLEV ? h->count[lane] : lane < LEVALL ? x->count[lane - MAXLEV] : 0;
-      lh = lane < 32 ? list_ptr(a, 0, p)[lane] : 0xffffffffu;
+      lh = list_ptr(a, 0, p)[lane];
+      tbv = a.tb[(size_t)p * TB_N + (lane & (TB_N - 1))];
+    };
+    // tiebreak_position(a.seed, sseq[p], T) from pod p's records (tbv, lane k: entry k)
+    auto tb_pos = [&](int p, int32_t tbv, int64_t T) -> int64_t {
+      const int32_t lim = __builtin_amdgcn_readlane(tbv, TB_N - 1);
+      if (T > (int64_t)lim) return tiebreak_position(a.seed, sseq[p], T);
+      const int cnt = __popcll(__ballot(lane < TB_N - 1 && tbv != INT32_MAX && (int64_t)tbv <= T));
+      return cnt ? (int64_t)__builtin_amdgcn_readlane(tbv, cnt - 1) : 1;
+    };
+    // a fresh slot's batch-start scores for the later pods (S_own column loads), issued when the slot is created and
+    // stored into dso by the next decision (the loads' latency hides behind the verification in between)
+    int ps_slot = -1, ps_p = 0;
+    int16_t ps_v0 = 0, ps_v1 = 0;
+    auto flush_fresh = [&]() {
+      if (ps_slot < 0) return;
+      const int q0 = ps_p + 1 + lane, q1 = q0 + 64;
+      if (q0 < B) dso[q0 * B + ps_slot] = ps_v0;
+      if (q1 < B) dso[q1 * B + ps_slot] = ps_v1;
+      ps_slot = -1;
     };
     int n_hs = -1, n_hc = 0, n_nlev = 0, n_feas = 0, n_next = -1;
     uint32_t n_lh = 0xffffffffu;
-    load_hdr(0, n_hs, n_hc, n_nlev, n_feas, n_next, n_lh);
+    int32_t n_tb = 1;
+    load_hdr(0, n_hs, n_hc, n_nlev, n_feas, n_next, n_lh, n_tb);
     uint32_t spins = 0;
     while (!err) {
       SPM(2);
@@ -246,6 +267,7 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
             if (qq < r) { if (sl < 64) redo0 |= 1ull << sl; else redo1 |= 1ull << (sl - 64); }
           }
           const int ndv = dec[v].nd_before;
+          ps_slot = -1;   // a pending fresh slot is the last decision's: >= ndv, undone
           if (lane >= ndv) { dn0 = 0xffffffffu; pv0 = -1; }
           if (lane + 64 >= ndv) { dn1 = 0xffffffffu; pv1 = -1; }
           for (int s = ndv + lane; s < nd; s += 64) { has_row[s] = 0; done_ver[s] = -1; }
@@ -288,7 +310,7 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
           end_why = 0;
           if (lane == 0) st_rel(&s_stop, 0);
           n_hs = -1;   // reload pod v's header
-          load_hdr(v, n_hs, n_hc, n_nlev, n_feas, n_next, n_lh);
+          load_hdr(v, n_hs, n_hc, n_nlev, n_feas, n_next, n_lh, n_tb);
           rolled = true;
           if (ST) st_acc[3] += 1;
           SPM(4);
@@ -311,12 +333,14 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
       if (q >= end_at || q - v >= SP_LAG || ld_acq(&s_cut_at) >= 0) {
         if (++spins > SP_SPIN_LIMIT) { err = true; err_code = 2; break; }
         sp_sleep();
+        if (q >= end_at) SPM(23);   // waiting at the batch's end
         continue;
       }
       spins = 0;
       const int p = q;
       const int hs = n_hs, hc = n_hc, nlev = n_nlev, feas = n_feas, next = n_next;
       const uint32_t lh = n_lh;
+      const int32_t tbv = n_tb;
       // dirty slots: ready (exact current score) or pending (left out)
       const int dv0 = lane < nd ? ld_acq(&done_ver[lane]) : -1;
       const int dv1 = lane + 64 < nd ? ld_acq(&done_ver[lane + 64]) : -1;
@@ -327,8 +351,9 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
         sp_sleep();
         continue;
       }
-      if (p + 1 < B) load_hdr(p + 1, n_hs, n_hc, n_nlev, n_feas, n_next, n_lh);   // consumed by the next decision
+      if (p + 1 < B) load_hdr(p + 1, n_hs, n_hc, n_nlev, n_feas, n_next, n_lh, n_tb);   // consumed by the next decision
       int sc0 = -1, so0 = -1, sc1 = -1, so1 = -1;
+      flush_fresh();
       if (lane < nd) { so0 = dso[p * B + lane]; if (rdy0) sc0 = dsc[p * B + lane]; }
       if (lane + 64 < nd) { so1 = dso[p * B + 64 + lane]; if (rdy1) sc1 = dsc[p * B + 64 + lane]; }
       // action 0 commit, 1 FitError, 2 stop deciding before p
@@ -349,6 +374,7 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
       const int Fd = wave_sum((sc0 >= 0) - (so0 >= 0) + (sc1 >= 0) - (so1 >= 0));
       M = max(Mclean, Md);
       F = Fd + feas;
+      SPM(18);   // decide: dirty-slot state, level scan
       bool full_row = false;
       if (slowpath) {
         M = a.forced_score;
@@ -367,7 +393,7 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
         const bool nw0 = sc0 == M, nw1 = sc1 == M;
         // clean listed ties: only at the top clean level (a higher M is a dirty row's: every listed node there is dirty)
         T = (int64_t)(M == Mclean ? ctop : 0) + __popcll(__ballot(nw0)) + __popcll(__ballot(nw1));
-        const int64_t jp = tiebreak_position(a.seed, sseq[p], T);
+        const int64_t jp = tb_pos(p, tbv, T);
         // level M's segment of the list: offset = listed nodes above it, len = listed nodes at it (0: not listed)
         const uint64_t atm = __ballot(lane < nlev && hs == M);
         const int jm = atm ? __builtin_ctzll(atm) : nlev;
@@ -389,10 +415,11 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
 #pragma unroll
           for (int c = 0; c < WCH; ++c) {
             const int i = c * 64 + lane, e = off + lo + i;
-            const uint32_t fromh = (uint32_t)__shfl((int)lh, e & 31);
+            const uint32_t fromh = (uint32_t)__shfl((int)lh, e & 63);
             xw[c] = 0xffffffffu;
-            if (c * 64 < W && i < W) xw[c] = e < 32 ? fromh : L[e];
+            if (c * 64 < W && i < W) xw[c] = e < 64 ? fromh : L[e];
           }
+          if (ST) { st_acc[24] += off + hi >= 32 ? 1 : 0; st_acc[25] += off + hi >= 64 ? 1 : 0; }
           const uint32_t win0 = (uint32_t)__builtin_amdgcn_readlane((int)xw[0], 0);
 #pragma unroll
           for (int c = 0; c < WCH; ++c) ow[c] = false;
@@ -443,7 +470,7 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
         else winner = (uint32_t)__builtin_amdgcn_readlane((int)cand, __ffsll((long long)got) - 1);
       }
       if (ST) st_acc[10] += full_row ? 1 : 0;
-      SPM(0);
+      SPM(19);   // decide: tie-break position, winner among listed + dirty ties
       if (full_row) {
         // exact resolution of pod p from its whole score row: batch-start S[p][*] for clean nodes, the current
         // score for ready dirty rows, pending rows left out (verified later like any decision)
@@ -509,7 +536,7 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
           const uint64_t new0 = __ballot(sc0 == M), new1 = __ballot(sc1 == M);
           const uint64_t old0 = __ballot(lane < nd && so0 == M), old1 = __ballot(lane + 64 < nd && so1 == M);
           T = (Mc == M ? Tc : 0) + __popcll(new0) + __popcll(new1);
-          const int64_t jp = tiebreak_position(a.seed, sseq[p], T);
+          const int64_t jp = tb_pos(p, tbv, T);
           int64_t run = 0;
           int64_t found = -1;
           for (uint32_t b0 = 0; b0 < len && found == -1; b0 += 512u * VB) {
@@ -595,15 +622,16 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
           d.flags |= SP_FRESH;
           if (lane == (nd & 63)) { if (nd < 64) { dn0 = winner; pv0 = p; } else { dn1 = winner; pv1 = p; } }
           const int q0 = p + 1 + lane, q1 = q0 + 64;
-          const int16_t s0v = q0 < B ? a.S_own[(size_t)q0 * a.ld + (winner - a.own0)] : (int16_t)0;
-          const int16_t s1v = q1 < B ? a.S_own[(size_t)q1 * a.ld + (winner - a.own0)] : (int16_t)0;
+          ps_v0 = q0 < B ? a.S_own[(size_t)q0 * a.ld + (winner - a.own0)] : (int16_t)0;
+          ps_v1 = q1 < B ? a.S_own[(size_t)q1 * a.ld + (winner - a.own0)] : (int16_t)0;
+          ps_slot = slot;
+          ps_p = p;
           if (lane == 0) {
             hash_insert(winner, slot);
             done_ver[slot] = -1;
           }
-          if (q0 < B) dso[q0 * B + slot] = s0v;
-          if (q1 < B) dso[q1 * B + slot] = s1v;
           ++nd;
+          SPM(20);   // decide: fresh slot's batch-start scores (S_own loads)
         } else {          // a ready dirty row lands another pod: pending again
           const int32_t prevv = slot < 64 ? __builtin_amdgcn_readlane(pv0, slot) : __builtin_amdgcn_readlane(pv1, slot - 64);
           d.prev_pend = prevv;
@@ -679,6 +707,7 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
       if (q >= ld_acq(&s_decided) || ld_acq(&s_cut_at) >= 0) {
         if (++spins > SP_SPIN_LIMIT) break;
         sp_sleep();
+        if (q == 0) SPM(26);   // waiting for the batch's first decision
         SPM(6);
         continue;
       }
@@ -714,6 +743,7 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
           else *reinterpret_cast<int32_t*>(dst + f_off) = (int32_t)vv;
         }
         if (lane == 0) has_row[slot] = 1;
+        SPM(21);   // fresh row fetch
       } else {
         // the slot's previous version must be fully re-scored before its row changes
         bool stop = false;
@@ -722,6 +752,7 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
           sp_sleep();
         }
         if (stop) continue;
+        SPM(22);   // landed-again slot: wait for its previous re-scoring
       }
       if (lane == 0 && (!fresh || !numa_on)) s_aff = -1;
       WAVE_FENCE();
@@ -819,6 +850,10 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
       cut = __builtin_amdgcn_readlane(cut, 0);
       WAVE_FENCE();
       SPM(17);   // lane 0: placement record, zone split, cpuset_reserve, assume deltas
+      if (pf_q != q + 1 && q + 1 < ld_acq(&s_decided)) {   // the next pod was decided meanwhile: prefetch its row now
+        const DecRec& dn = dec[q + 1];
+        if ((dn.flags & (SP_FRESH | SP_FITERR)) == SP_FRESH) { pf_v = fetch(q + 1, (uint32_t)dn.winner); pf_q = q + 1; }
+      }
       // ---- the row's re-scoring: hint table of its new state, jobs of 64 later pods
       const int nlater = B - (q + 1);
       const int njobs = (nlater + 63) / 64;
@@ -911,7 +946,7 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
     }
   for (int i = tid; i < committed; i += SP_THREADS) a.out[i].feasible = (uint32_t)final_F[i];
   if (ST && lane == 0)
-    for (int i = 0; i < 18; ++i)
+    for (int i = 0; i < 28; ++i)
       if (st_acc[i]) atomicAdd(reinterpret_cast<unsigned long long*>(&a.stamps[i]), (unsigned long long)st_acc[i]);
 #undef SPM
   if (tid == 0) {

@@ -94,6 +94,7 @@ struct gs_ctx {
   size_t xchg_bytes = 0;
   PlacementDev* d_out = nullptr;
   int32_t* d_committed = nullptr;
+  int32_t* d_tb = nullptr;          // speculative commit: tie-break records of the batch's pods
   RowStat* d_rowstat = nullptr;
   int32_t* d_sel = nullptr;
   uint32_t* d_stage_idx = nullptr;
@@ -857,6 +858,7 @@ CommitArgs commit_args(gs_ctx* c, int b) {
   a.nnodes = c->N;
   static const bool nospec = getenv("GS_SPEC_WAIT") && getenv("GS_SPEC_WAIT")[0] == '1';
   a.dbg = nospec ? 1u : 0u;
+  a.tb = c->d_tb;
   return a;
 }
 
@@ -1538,6 +1540,7 @@ int gs_create(const gs_config* cfg, gs_ctx** out) {
   c->xchg_bytes = xb;
   if ((e = hipMalloc(&c->d_out, sizeof(PlacementDev) * c->B)) != hipSuccess) return bail("hipMalloc", e);
   if ((e = hipMalloc(&c->d_committed, 16)) != hipSuccess) return bail("hipMalloc", e);
+  if ((e = hipMalloc(&c->d_tb, sizeof(int32_t) * TB_N * c->B)) != hipSuccess) return bail("hipMalloc", e);
   if ((e = hipMalloc(&c->d_rowstat, sizeof(RowStat) * (1 + MAX_RANKS))) != hipSuccess) return bail("hipMalloc", e);
   if ((e = hipMalloc(&c->d_sel, 4 * (1 + MAX_RANKS))) != hipSuccess) return bail("hipMalloc", e);
   c->stage_cap = std::min<uint32_t>(c->N, 65536);
@@ -1609,7 +1612,12 @@ int gs_destroy(gs_ctx* c) {
                 (unsigned long long)st[10], st[10] ? (double)st[11] / st[10] : 0.0, (unsigned long long)st[13],
                 (unsigned long long)st[14], st[12] / np);
         fprintf(stderr, "gpuscore spec commit, Reserve wave per committed pod: fetch+undo %.0f numa_eval %.0f "
-                "lane0 (zone split, cpuset, assume) %.0f rest %.0f\n", st[15] / np, st[16] / np, st[17] / np, st[5] / np);
+                "lane0 (zone split, cpuset, assume) %.0f rest %.0f (fresh fetch %.0f, landed-again wait %.0f)\n", st[15] / np,
+                st[16] / np, st[17] / np, st[5] / np, st[21] / np, st[22] / np);
+        fprintf(stderr, "gpuscore spec commit, decide per committed pod: level scan %.0f winner %.0f fresh-slot S loads %.0f "
+                "record %.0f; list window beyond entry 32: %llu, beyond 64: %llu; wave 0 waiting at batch end %.0f; Reserve waiting "
+                "for the first decision %.0f\n", st[18] / np, st[19] / np, st[20] / np, st[0] / np,
+                (unsigned long long)st[24], (unsigned long long)st[25], st[23] / np, st[26] / np);
         (void)hipFree(c->d_stamps);
         c->d_stamps = nullptr;
       }
@@ -1658,7 +1666,7 @@ int gs_destroy(gs_ctx* c) {
   }
   void* dev[] = {c->d_i64, c->d_i32, c->d_pods, c->d_seq, c->d_S, c->d_xchg_send, c->d_xchg_recv, c->d_out,
                  c->d_committed, c->d_rowstat, c->d_sel, c->d_stage_idx, c->d_stage_rows, c->d_numa_idx,
-                 c->d_topos, c->d_aff};
+                 c->d_topos, c->d_aff, c->d_tb};
   for (void* p : dev)
     if (p) (void)hipFree(p);
   void* host[] = {c->h_pods, c->h_seq, c->h_out, c->h_committed, c->h_stage_idx, c->h_stage_rows, c->h_xchg_send,

@@ -231,6 +231,29 @@ __host__ __device__ inline int64_t tiebreak_position(uint64_t seed, uint64_t seq
   return j;
 }
 
+// the positions tiebreak_position's walk visits for (seed, seq), ascending (they do not depend on T), for a lane-parallel
+// lookup: out[0..TB_N-2] records (INT32_MAX past the walk's end), out[TB_N-1] = the largest T they decide
+__host__ __device__ inline void tiebreak_records(uint64_t seed, uint64_t seq, int32_t* out) {
+  const uint64_t key = mix64(seed ^ mix64(seq));
+  int64_t j = 1;
+  int k = 0;
+  int32_t lim = INT32_MAX;   // the walk ended: every T
+  out[k++] = 1;
+  for (uint64_t i = 0;; ++i) {
+    if (k == TB_N - 1) { lim = (int32_t)j; break; }   // records full: T up to the last one
+    const uint64_t h = mix64(key + i);
+    const double u = (double)((h >> 11) + 1) * 0x1.0p-53;
+    const double x = (double)j / u;
+    if (!(x < 4.0e18)) break;
+    const int64_t jn = (int64_t)floor(x) + 1;
+    if (jn >= (int64_t)INT32_MAX) { lim = INT32_MAX - 1; break; }   // the next record is past int32
+    j = jn;
+    out[k++] = (int32_t)j;
+  }
+  for (; k < TB_N - 1; ++k) out[k] = INT32_MAX;
+  out[TB_N - 1] = lim;
+}
+
 
 // ------------------------------------------------------------------------------------------------
 // Sequential commit: ONE wave walks the batch's pods in order (no workgroup barriers: LDS traffic of a
@@ -339,12 +362,23 @@ __device__ __forceinline__ void wave_rank_sort(uint32_t* v, int n, uint32_t* tmp
 __device__ __noinline__ bool cpuset_reserve(const GS_LDS TopoDev* tp, GS_LDS CpuStateDev* csp, const PodVec& p,
                                             uint32_t nf, uint32_t zkeys, int64_t zc0, int64_t zc1, int64_t zc2,
                                             int64_t zc3, GS_LDS NumaRow* nrp, GS_LDS uint64_t* cpuset) {
+  // every operand is wave-uniform (one Reserve at a time): say so, so that the selection runs on the scalar unit
+  auto u32 = [](uint32_t x) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)x); };
+  auto u64 = [&](int64_t x) {
+    return (int64_t)(((uint64_t)u32((uint32_t)((uint64_t)x >> 32)) << 32) | u32((uint32_t)(uint64_t)x));
+  };
+  tp = (const GS_LDS TopoDev*)(size_t)u32((uint32_t)(size_t)tp);
+  csp = (GS_LDS CpuStateDev*)(size_t)u32((uint32_t)(size_t)csp);
+  nrp = (GS_LDS NumaRow*)(size_t)u32((uint32_t)(size_t)nrp);
+  cpuset = (GS_LDS uint64_t*)(size_t)u32((uint32_t)(size_t)cpuset);
+  nf = u32(nf);
+  zkeys = u32(zkeys);
   const TopoDev& t = *(const TopoDev*)tp;
   CpuStateDev& cs = *(CpuStateDev*)csp;
   NumaRow& nr = *(NumaRow*)nrp;
-  const int64_t zcpu[4] = {zc0, zc1, zc2, zc3};
+  const int64_t zcpu[4] = {u64(zc0), u64(zc1), u64(zc2), u64(zc3)};
   // getCPUBindPolicy (util.go:85-103)
-  const uint32_t pn = p.numa;
+  const uint32_t pn = u32(p.numa);
   const int st_req = (pn >> PN_REQ_SHIFT) & 7, nb = (nf >> NF_BIND_SHIFT) & 3;
   int bind = (pn >> PN_PREF_SHIFT) & 7;
   bool required = false;
@@ -353,21 +387,21 @@ __device__ __noinline__ bool cpuset_reserve(const GS_LDS TopoDev* tp, GS_LDS Cpu
   else if (nb == GS_NODE_CPU_BIND_FULL_PCPUS_ONLY) { bind = BIND_FULL; required = true; }
   const int ep = (pn & PN_BIND) ? (int)((pn >> PN_EXCL_SHIFT) & 3u) : GS_CPU_EXCLUSIVE_NONE;
   uint64_t R[TD_POS];
-  if (!td_allocate_cpuset(t, cs, p.num_cpus, bind, required, ep, zkeys, zcpu, R)) return false;
+  if (!td_allocate_cpuset(t, cs, (int)u32((uint32_t)p.num_cpus), bind, required, ep, zkeys, zcpu, R)) return false;
   const uint64_t cores = td_any(R);
   for (int j = 0; j < TD_POS; ++j) cs.un[j] |= R[j];
   if (ep == GS_CPU_EXCLUSIVE_PCPU_LEVEL) cs.xc |= cores;
   else if (ep == GS_CPU_EXCLUSIVE_NUMA_NODE_LEVEL)
-    for (uint64_t b = cores; b; b &= b - 1) cs.meta |= 1u << t.core_node[td_ctz(b)];
+    for (uint64_t b = cores; b; b &= b - 1) cs.meta |= 1u << TU32(t.core_node[td_ctz(b)]);
   nr.alloc_cpus += td_cnt(R, ~0ull);
   nr.tfree = (uint32_t)td_counts(t, cs, ~0ull);
   const int nz = (nf >> NF_ZONES_SHIFT) & 7;
   for (int z = 0; z < 4; ++z) {
     const int n = td_zone_node(cs, z);
-    if (z >= nz || n >= t.nnodes) continue;   // a zone the topology lacks keeps its zero summaries
-    const uint64_t zc = ((cs.zal >> (16 * z)) & 0xFFFFull) + (uint64_t)td_cnt(R, t.node_cores[n]);
+    if (z >= nz || n >= TU32(t.nnodes)) continue;   // a zone the topology lacks keeps its zero summaries
+    const uint64_t zc = ((TU64(cs.zal) >> (16 * z)) & 0xFFFFull) + (uint64_t)td_cnt(R, TU64(t.node_cores[n]));
     cs.zal = (cs.zal & ~(0xFFFFull << (16 * z))) | (zc << (16 * z));
-    nr.zfree[z] = (uint32_t)td_counts(t, cs, t.node_cores[n]);
+    nr.zfree[z] = (uint32_t)td_counts(t, cs, TU64(t.node_cores[n]));
     if (nr.amp > 1.0) {
       const int64_t c = (int64_t)zc * 1000;
       nr.zadj[z] = (int32_t)(amplify_d(c, nr.amp) - c);

@@ -106,7 +106,11 @@ struct CommitArgs {
   uint32_t start;
   uint32_t nnodes;
   uint32_t dbg;              // diagnostics: bit 0 = the speculative commit waits for every pending row (no speculation)
+  int32_t* tb;               // [npods x TB_N] selectHost tie-break records of each pod (speculative commit scratch)
 };
+// tiebreak_position(seed, seq, T) as a lookup: entries 0..TB_N-2 are the positions the reservoir walk visits
+// (ascending, independent of T; INT32_MAX past the walk's end), entry TB_N-1 the largest T the entries decide
+constexpr int TB_N = 32;
 
 hipError_t set_kernel_attributes();
 hipError_t launch_node_prep(const MirrorView& m, uint32_t n0, uint32_t n1, int64_t now, int32_t filter_expired,
