@@ -74,6 +74,7 @@ struct gs_ctx {
   hipStream_t st = nullptr;
   hipStream_t st2 = nullptr;                // side stream: eval_kernel beside eval_numa_kernel
   hipStream_t st_ev = nullptr;              // eval passes: a batch's eval runs beside the previous batch's commit
+  hipStream_t st_rb = nullptr;              // a batch's placement readback, off the stream the next batch runs on
   uint32_t window_k = 0;                    // node sampling: numFeasibleNodesToFind(N) (0 = every node)
   uint32_t next_start = 0;                  // [upstream] Scheduler.nextStartNodeIndex
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
@@ -913,9 +914,12 @@ int launch_batch(gs_ctx* c, int b, const int32_t* prev, const PlacementDev* prev
   HIP_TRY(c, hipEventRecord(c->ev[3], c->st));
   HIP_TRY(c, launch_commit(a, c->st));
   HIP_TRY(c, hipEventRecord(c->ev[4], c->st));
-  HIP_TRY(c, hipMemcpyAsync(c->h_committed, c->d_committed, 16, hipMemcpyDeviceToHost, c->st));
-  HIP_TRY(c, hipMemcpyAsync(c->h_out, c->d_out, sizeof(PlacementDev) * b, hipMemcpyDeviceToHost, c->st));
-  HIP_TRY(c, hipEventRecord(c->ev[5], c->st));
+  // readback on its own stream: the speculative next batch's patch / cand start right after the commit (the slot's
+  // buffers are rewritten only after finish_batch has waited for ev[5])
+  HIP_TRY(c, hipStreamWaitEvent(c->st_rb, c->ev[4], 0));
+  HIP_TRY(c, hipMemcpyAsync(c->h_committed, c->d_committed, 16, hipMemcpyDeviceToHost, c->st_rb));
+  HIP_TRY(c, hipMemcpyAsync(c->h_out, c->d_out, sizeof(PlacementDev) * b, hipMemcpyDeviceToHost, c->st_rb));
+  HIP_TRY(c, hipEventRecord(c->ev[5], c->st_rb));
   return GS_OK;
 }
 
@@ -1518,6 +1522,7 @@ int gs_create(const gs_config* cfg, gs_ctx** out) {
   if ((e = hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking)) != hipSuccess) return bail("hipStreamCreate", e);
   if ((e = hipStreamCreateWithFlags(&c->st2, hipStreamNonBlocking)) != hipSuccess) return bail("hipStreamCreate", e);
   if ((e = hipStreamCreateWithFlags(&c->st_ev, hipStreamNonBlocking)) != hipSuccess) return bail("hipStreamCreate", e);
+  if ((e = hipStreamCreateWithFlags(&c->st_rb, hipStreamNonBlocking)) != hipSuccess) return bail("hipStreamCreate", e);
   if ((e = hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming)) != hipSuccess) return bail("hipEventCreate", e);
   if ((e = hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming)) != hipSuccess) return bail("hipEventCreate", e);
   for (auto& ev : c->ev)
@@ -1583,6 +1588,7 @@ int gs_create(const gs_config* cfg, gs_ctx** out) {
   if (getenv("GS_COMMIT_STAMPS") && getenv("GS_COMMIT_STAMPS")[0] == '1') {
     if ((e = hipMalloc(&c->d_stamps, 8 * 32)) != hipSuccess) return bail("hipMalloc", e);
     (void)hipMemset(c->d_stamps, 0, 256);
+    set_cand_stamps(c->d_stamps + 27);
   }
   if ((e = hipDeviceSynchronize()) != hipSuccess) return bail("hipDeviceSynchronize", e);
   // 96 B (LoadAware + Fit row), + 192 B NodeNUMAResource columns when enabled
@@ -1618,6 +1624,9 @@ int gs_destroy(gs_ctx* c) {
                 "record %.0f; list window beyond entry 32: %llu, beyond 64: %llu; wave 0 waiting at batch end %.0f; Reserve waiting "
                 "for the first decision %.0f\n", st[18] / np, st[19] / np, st[20] / np, st[0] / np,
                 (unsigned long long)st[24], (unsigned long long)st[25], st[23] / np, st[26] / np);
+        const double nb = c->stats.batches ? (double)c->stats.batches * c->B : 1.0;
+        fprintf(stderr, "gpuscore cand_kernel, wave-0 cycles per pod row: pass 1 %.0f, level sums %.0f, level pick %.0f, "
+                "offsets %.0f, pass 2 %.0f\n", st[27] / nb, st[28] / nb, st[29] / nb, st[30] / nb, st[31] / nb);
         (void)hipFree(c->d_stamps);
         c->d_stamps = nullptr;
       }
@@ -1676,6 +1685,7 @@ int gs_destroy(gs_ctx* c) {
   for (auto& ev : c->ev)
     if (ev) (void)hipEventDestroy(ev);
   if (c->st_ev) (void)hipStreamDestroy(c->st_ev);
+  if (c->st_rb) (void)hipStreamDestroy(c->st_rb);
   if (c->st2) (void)hipStreamSynchronize(c->st2);
   if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
   if (c->ev_join) (void)hipEventDestroy(c->ev_join);

@@ -326,6 +326,15 @@ __device__ __forceinline__ int wave_sum(int v) {
   return __builtin_amdgcn_readlane(v, 63);
 }
 // inclusive prefix sum over lanes: row_shr 1, 2, 4, 8 within rows, then the row carries
+__device__ __forceinline__ int wave_or(int v) {
+  v |= GS_DPP(0, v, 0xB1, 0xF);
+  v |= GS_DPP(0, v, 0x4E, 0xF);
+  v |= GS_DPP(0, v, 0x141, 0xF);
+  v |= GS_DPP(0, v, 0x140, 0xF);
+  v |= GS_DPP(0, v, 0x142, 0xA);
+  v |= GS_DPP(0, v, 0x143, 0xC);
+  return __builtin_amdgcn_readlane(v, 63);
+}
 __device__ __forceinline__ int wave_incl_scan(int v) {
   v += GS_DPP(0, v, 0x111, 0xF);
   v += GS_DPP(0, v, 0x112, 0xF);

@@ -127,6 +127,7 @@ hipError_t launch_patch(const MirrorView& m, const PodVec* pods, int npods, cons
                         const int32_t* prev_committed, int prev_npods, hipStream_t st);
 hipError_t launch_eval_full(const MirrorView& m, const PodVec* pods, int npods, const Profile& pf, uint32_t N,
                             int16_t* scores, uint16_t* codes, int16_t* plugin, int prod_cols, hipStream_t st);
+void set_cand_stamps(uint64_t* p);   // diagnostics: cand_kernel phase cycles (nullptr: off)
 hipError_t launch_cand(const int16_t* S, uint32_t ld, uint32_t len, uint32_t n0, int npods, int max_score,
                        uint32_t* lists, LevelHdr* hdrs, LevelExt* ext, hipStream_t st);
 size_t commit_smem_bytes(int B);

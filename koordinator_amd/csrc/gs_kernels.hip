@@ -155,8 +155,17 @@ __global__ void __launch_bounds__(256) eval_full_kernel(MirrorView m, const PodV
 template <int W>
 __global__ void __launch_bounds__(64 * W) cand_kernel(const int16_t* __restrict__ S, uint32_t ld, uint32_t len,
                                                       uint32_t n0, int max_score, uint32_t* __restrict__ lists,
-                                                      LevelHdr* __restrict__ hdrs, LevelExt* __restrict__ ext) {
+                                                      LevelHdr* __restrict__ hdrs, LevelExt* __restrict__ ext,
+                                                      uint64_t* stamps) {
   constexpr int CAND_THREADS = 64 * W;
+  // diagnostics (stamps != nullptr): wave 0's cycles per phase, summed over the pods
+  uint64_t ct_last = stamps ? __builtin_amdgcn_s_memtime() : 0;
+  auto CT = [&](int i) {
+    if (!stamps) return;
+    const uint64_t t_ = __builtin_amdgcn_s_memtime();
+    if (threadIdx.x == 0) atomicAdd(reinterpret_cast<unsigned long long*>(&stamps[i]), (unsigned long long)(t_ - ct_last));
+    ct_last = t_;
+  };
   extern __shared__ __align__(16) uint32_t smem[];
   const int nbins = max_score + 1;
   uint32_t* whist = smem;                                        // [W][nbins]
@@ -166,6 +175,8 @@ __global__ void __launch_bounds__(64 * W) cand_kernel(const int16_t* __restrict_
   __shared__ uint32_t s_total;
   __shared__ int32_t s_nlev, s_next, s_score[LEVALL], s_count[LEVALL];
   __shared__ uint32_t s_woff[W][LEVALL];
+  constexpr int STEPCAP = 128;                 // 512-entry steps per wave with a recorded maximum
+  __shared__ int16_t s_stepmax[W][STEPCAP];    // highest score of each of the wave's steps (pass 2 skips the rest)
   const int k = blockIdx.x;
   const int t = threadIdx.x, wave = t >> 6, lane = t & 63;
   const int16_t* row = S + (size_t)k * ld;
@@ -187,12 +198,19 @@ __global__ void __launch_bounds__(64 * W) cand_kernel(const int16_t* __restrict_
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const int16_t* e = reinterpret_cast<const int16_t*>(&q[u]);
+      int mx = -1;
 #pragma unroll
-      for (int x = 0; x < 8; ++x)
+      for (int x = 0; x < 8; ++x) {
         if (e[x] >= 0) atomicAdd(&whist[wave * nbins + e[x]], 1u);
+        mx = max(mx, (int)e[x]);
+      }
+      mx = wave_max(mx);
+      const uint32_t st = (i - lane * 8 + u * 512 - wb) / 512;
+      if (lane == 0 && st < (uint32_t)STEPCAP) s_stepmax[wave][st] = (int16_t)mx;
     }
   }
   __syncthreads();
+  CT(0);
   const int per = (nbins + CAND_THREADS - 1) / CAND_THREADS;
   {
     uint32_t s = 0;
@@ -208,35 +226,48 @@ __global__ void __launch_bounds__(64 * W) cand_kernel(const int16_t* __restrict_
     if (s) atomicAdd(&s_total, s);
   }
   __syncthreads();
-  if (t == 0) {
+  CT(1);
+  if (wave == 0) {
     // levels from the top until the pod's position in the batch is covered: pod k can find at most k of
-    // the listed nodes dirtied by earlier pods, so k+1 listed nodes always leave a clean one.
+    // the listed nodes dirtied by earlier pods, so k+1 listed nodes always leave a clean one. Wave 0 walks the
+    // bins 64 at a time from the top (lane l: bin hi - l); a level stops the list when the levels before it are
+    // LEVALL, or it would pass LCAP, or the nodes before it cover the target.
     const uint32_t target = (uint32_t)k + 1;
+    const uint64_t lt = (1ull << lane) - 1ull;
     int nlev = 0, next = -1;
     uint32_t cum = 0;
-    bool stop = false;
-    for (int sg = CAND_THREADS - 1; sg >= 0 && !stop; --sg) {
-      if (!segsum[sg]) continue;
-      for (int b = min(nbins, (sg + 1) * per) - 1; b >= sg * per; --b) {
-        uint32_t c = comb[b];
-        if (!c) continue;
-        if (nlev == LEVALL || cum + c > (uint32_t)LCAP || cum >= target) {
-          next = b;
-          stop = true;
-          break;
-        }
-        s_score[nlev] = b;
-        s_count[nlev] = (int32_t)c;
-        slot_of[b] = (int8_t)nlev;
-        ++nlev;
-        cum += c;
+    for (int hi = nbins - 1; hi >= 0; hi -= 64) {
+      const int b = hi - lane;
+      const uint32_t c = b >= 0 ? comb[b] : 0u;
+      const bool nz = c != 0;
+      const uint64_t nzm = __ballot(nz);
+      if (!nzm) continue;
+      const uint32_t cb = cum + (uint32_t)(wave_incl_scan((int)c) - (int)c);
+      const int nb = nlev + __popcll(nzm & lt);
+      const bool stop = nz && (nb == LEVALL || cb + c > (uint32_t)LCAP || cb >= target);
+      const uint64_t sm = __ballot(stop);
+      const int ls = sm ? __builtin_ctzll(sm) : 64;
+      if (nz && lane < ls) {
+        s_score[nb] = b;
+        s_count[nb] = (int32_t)c;
+        slot_of[b] = (int8_t)nb;
       }
+      if (sm) {
+        next = __builtin_amdgcn_readlane(b, ls);
+        nlev += __popcll(nzm & ((1ull << ls) - 1ull));
+        break;
+      }
+      nlev += __popcll(nzm);
+      cum += (uint32_t)wave_sum((int)c);
     }
-    for (int j = nlev; j < LEVALL; ++j) { s_score[j] = -1; s_count[j] = 0; }
-    s_nlev = nlev;
-    s_next = next;
+    for (int j = nlev + lane; j < LEVALL; j += 64) { s_score[j] = -1; s_count[j] = 0; }
+    if (lane == 0) {
+      s_nlev = nlev;
+      s_next = next;
+    }
   }
   __syncthreads();
+  CT(2);
   const int nlev = s_nlev;
   for (int e = t; e < W * LEVALL; e += CAND_THREADS) {
     const int w = e / LEVALL, j = e % LEVALL;
@@ -248,15 +279,27 @@ __global__ void __launch_bounds__(64 * W) cand_kernel(const int16_t* __restrict_
     s_woff[w][j] = off;
   }
   __syncthreads();
+  CT(3);
   // pass 2: order-preserving compaction of the listed levels (node order = (lane, element) order), level by level
   // over the levels present in each 512-node step
   uint32_t* out = lists + (size_t)k * LCAP;
   if (nlev > 0) {
     uint32_t run_l = lane < LEVALL ? s_woff[wave][lane] : 0;   // level `lane`'s next output position (this wave)
-    int4 qn = wb < we ? row4[(wb + lane * 8) / 8] : make_int4(-1, -1, -1, -1);
-    for (uint32_t base = wb; base < we; base += 512) {
+    // steps whose highest score is below the lowest listed level hold no listed node: not read again
+    const int thr = s_score[nlev - 1];
+    auto next_step = [&](uint32_t b) {
+      for (; b < we; b += 512) {
+        const uint32_t st = (b - wb) / 512;
+        if (st >= (uint32_t)STEPCAP || s_stepmax[wave][st] >= thr) break;
+      }
+      return b;
+    };
+    uint32_t base = next_step(wb);
+    int4 qn = base < we ? row4[(base + lane * 8) / 8] : make_int4(-1, -1, -1, -1);
+    for (uint32_t nb; base < we; base = nb) {
       int4 q = qn;   // the next step's load is issued before this step's scans
-      if (base + 512 < we) qn = row4[(base + 512 + lane * 8) / 8];
+      nb = next_step(base + 512);
+      if (nb < we) qn = row4[(nb + lane * 8) / 8];
       const int16_t* e = reinterpret_cast<const int16_t*>(&q);
       int slot[8];
       uint32_t present = 0;
@@ -266,27 +309,23 @@ __global__ void __launch_bounds__(64 * W) cand_kernel(const int16_t* __restrict_
         if (slot[x] >= 0) present |= 1u << slot[x];
       }
       // levels present anywhere in the step (OR over the wave)
-      uint32_t pw = present;
-      for (int o = 1; o < 64; o <<= 1) pw |= (uint32_t)__shfl_xor((int)pw, o);
+      uint32_t pw = (uint32_t)wave_or((int)present);
       for (; pw; pw &= pw - 1) {
         const int j = __ffs(pw) - 1;
         int c = 0;
 #pragma unroll
         for (int x = 0; x < 8; ++x) c += slot[x] == j;
-        int incl = c;
-        for (int o = 1; o < 64; o <<= 1) {
-          int v = __shfl_up(incl, o);
-          if (lane >= o) incl += v;
-        }
-        int pos = (int)__shfl((int)run_l, j) + incl - c;
+        const int incl = wave_incl_scan(c);
+        int pos = __builtin_amdgcn_readlane((int)run_l, j) + incl - c;
 #pragma unroll
         for (int x = 0; x < 8; ++x)
           if (slot[x] == j) out[pos++] = n0 + base + lane * 8 + x;
-        const int tot = __shfl(incl, 63);
+        const int tot = __builtin_amdgcn_readlane(incl, 63);
         if (lane == j) run_l += tot;
       }
     }
   }
+  CT(4);
   if (t == 0) {
     LevelHdr h;
     h.nlev = nlev < MAXLEV ? nlev : MAXLEV;
@@ -1186,16 +1225,22 @@ static size_t cand_smem_bytes(int max_score, int waves) {
 }
 // The 16-wave variant measured slower on MI355X (its serial level scan walks 4x more segments): kept for
 // experiments, not selected.
-static bool cand_wide(int max_score) { return false && cand_smem_bytes(max_score, 16) <= 48 * 1024; }
+static bool cand_wide(int max_score) {
+  static const int env = getenv("GS_CAND_WIDE") ? atoi(getenv("GS_CAND_WIDE")) : 0;
+  return env == 1 && cand_smem_bytes(max_score, 16) <= 48 * 1024;
+}
+
+static uint64_t* g_cand_stamps = nullptr;
+void set_cand_stamps(uint64_t* p) { g_cand_stamps = p; }
 
 hipError_t launch_cand(const int16_t* S, uint32_t ld, uint32_t len, uint32_t n0, int npods, int max_score,
                        uint32_t* lists, LevelHdr* hdrs, LevelExt* ext, hipStream_t st) {
   if (cand_wide(max_score))
     hipLaunchKernelGGL(cand_kernel<16>, dim3(npods), dim3(1024), cand_smem_bytes(max_score, 16), st, S, ld, len, n0,
-                       max_score, lists, hdrs, ext);
+                       max_score, lists, hdrs, ext, g_cand_stamps);
   else
     hipLaunchKernelGGL(cand_kernel<4>, dim3(npods), dim3(256), cand_smem_bytes(max_score, 4), st, S, ld, len, n0,
-                       max_score, lists, hdrs, ext);
+                       max_score, lists, hdrs, ext, g_cand_stamps);
   return hipGetLastError();
 }
 
