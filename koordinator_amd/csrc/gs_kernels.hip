@@ -189,12 +189,19 @@ __global__ void __launch_bounds__(64 * W) cand_kernel(const int16_t* __restrict_
   const uint32_t seg = (lenv / 512 + W - 1) / W * 512;
   const uint32_t wb = min(lenv, wave * seg), we = min(lenv, wb + seg);
   const int4* row4 = reinterpret_cast<const int4*>(row);
-  // pass 1: per-wave histograms of feasible scores; 4 loads in flight per lane (the pass is load-latency bound:
-  // one workgroup streams a whole row)
+  // pass 1: per-wave histograms of feasible scores; 4 loads in flight per lane, the next group's loads issued
+  // before this group's atomics (the pass is load-latency bound: one workgroup streams a whole row)
+  auto load4 = [&](uint32_t i, int4 (&q)[4]) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) q[u] = i + u * 512 < we ? row4[(i + u * 512) / 8] : make_int4(-1, -1, -1, -1);
+  };
+  int4 qn[4];
+  load4(wb + lane * 8, qn);
   for (uint32_t i = wb + lane * 8; i < we; i += 4 * 512) {
     int4 q[4];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) q[u] = i + u * 512 < we ? row4[(i + u * 512) / 8] : make_int4(-1, -1, -1, -1);
+    for (int u = 0; u < 4; ++u) q[u] = qn[u];
+    if (i + 4 * 512 < we) load4(i + 4 * 512, qn);
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const int16_t* e = reinterpret_cast<const int16_t*>(&q[u]);
@@ -294,18 +301,31 @@ __global__ void __launch_bounds__(64 * W) cand_kernel(const int16_t* __restrict_
       }
       return b;
     };
-    uint32_t base = next_step(wb);
-    int4 qn = base < we ? row4[(base + lane * 8) / 8] : make_int4(-1, -1, -1, -1);
-    for (uint32_t nb; base < we; base = nb) {
-      int4 q = qn;   // the next step's load is issued before this step's scans
-      nb = next_step(base + 512);
-      if (nb < we) qn = row4[(nb + lane * 8) / 8];
+    // the next 3 steps' loads are in flight while a step is scanned
+    constexpr int PD = 4;
+    uint32_t bq[PD];
+    int4 vq[PD];
+    uint32_t nb = next_step(wb);
+#pragma unroll
+    for (int u = 0; u < PD; ++u) {
+      bq[u] = nb;
+      vq[u] = nb < we ? row4[(nb + lane * 8) / 8] : make_int4(-1, -1, -1, -1);
+      nb = nb < we ? next_step(nb + 512) : we;
+    }
+    while (bq[0] < we) {
+      const uint32_t base = bq[0];
+      const int4 q = vq[0];
+#pragma unroll
+      for (int u = 0; u + 1 < PD; ++u) { bq[u] = bq[u + 1]; vq[u] = vq[u + 1]; }
+      bq[PD - 1] = nb;
+      vq[PD - 1] = nb < we ? row4[(nb + lane * 8) / 8] : make_int4(-1, -1, -1, -1);
+      nb = nb < we ? next_step(nb + 512) : we;
       const int16_t* e = reinterpret_cast<const int16_t*>(&q);
       int slot[8];
       uint32_t present = 0;
 #pragma unroll
       for (int x = 0; x < 8; ++x) {
-        slot[x] = e[x] >= 0 ? slot_of[e[x]] : -1;
+        slot[x] = e[x] >= thr ? slot_of[e[x]] : -1;   // every non-empty bin >= thr is a listed level
         if (slot[x] >= 0) present |= 1u << slot[x];
       }
       // levels present anywhere in the step (OR over the wave)
