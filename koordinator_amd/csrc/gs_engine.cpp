@@ -914,12 +914,14 @@ int launch_batch(gs_ctx* c, int b, const int32_t* prev, const PlacementDev* prev
   HIP_TRY(c, hipEventRecord(c->ev[3], c->st));
   HIP_TRY(c, launch_commit(a, c->st));
   HIP_TRY(c, hipEventRecord(c->ev[4], c->st));
-  // readback on its own stream: the speculative next batch's patch / cand start right after the commit (the slot's
-  // buffers are rewritten only after finish_batch has waited for ev[5])
-  HIP_TRY(c, hipStreamWaitEvent(c->st_rb, c->ev[4], 0));
-  HIP_TRY(c, hipMemcpyAsync(c->h_committed, c->d_committed, 16, hipMemcpyDeviceToHost, c->st_rb));
-  HIP_TRY(c, hipMemcpyAsync(c->h_out, c->d_out, sizeof(PlacementDev) * b, hipMemcpyDeviceToHost, c->st_rb));
-  HIP_TRY(c, hipEventRecord(c->ev[5], c->st_rb));
+  // full batches: readback on its own stream, so that the speculative next batch's patch / cand start right after the
+  // commit (the slot's buffers are rewritten only after finish_batch has waited for ev[5]). Short batches (the host
+  // waits on each one) keep it in order on st: the extra queue hop costs more than it hides there.
+  hipStream_t rb = b >= 32 ? c->st_rb : c->st;
+  if (rb != c->st) HIP_TRY(c, hipStreamWaitEvent(rb, c->ev[4], 0));
+  HIP_TRY(c, hipMemcpyAsync(c->h_committed, c->d_committed, 16, hipMemcpyDeviceToHost, rb));
+  HIP_TRY(c, hipMemcpyAsync(c->h_out, c->d_out, sizeof(PlacementDev) * b, hipMemcpyDeviceToHost, rb));
+  HIP_TRY(c, hipEventRecord(c->ev[5], rb));
   return GS_OK;
 }
 

@@ -18,6 +18,9 @@
 #include <stdint.h>
 #include <stdlib.h>
 
+#include <cstdio>
+#include <vector>
+
 #include "gs_eval_dev.h"
 
 namespace gs {
@@ -364,6 +367,45 @@ __global__ void __launch_bounds__(64 * W) cand_kernel(const int16_t* __restrict_
 }
 
 int64_t host_tiebreak_position(uint64_t seed, uint64_t seq, int64_t T) { return tiebreak_position(seed, seq, T); }
+
+// selectHost tie-break lookup of the speculative commit (tiebreak_records + the lane-parallel count in
+// gs_commit_spec.hip tb_pos) against tiebreak_position, on the host: random (seed, seq) and T at, around and
+// between the records, the records' limit and beyond it. Returns the number of mismatches.
+extern "C" int gsx_tiebreak_selftest(uint64_t seed, int iters, char* msg, size_t len) {
+  uint64_t st = seed * 0x9E3779B97F4A7C15ull + 1;
+  auto rnd = [&]() { st += 0x9E3779B97F4A7C15ull; return mix64(st); };
+  int bad = 0;
+  if (msg && len) msg[0] = 0;
+  for (int it = 0; it < iters; ++it) {
+    const uint64_t sd = rnd(), sq = rnd();
+    int32_t r[TB_N];
+    tiebreak_records(sd, sq, r);
+    const int32_t lim = r[TB_N - 1];
+    std::vector<int64_t> Ts = {1, 2, 3, (int64_t)(rnd() % 1000) + 1, (int64_t)(rnd() % 200000) + 1,
+                               (int64_t)(rnd() % (1ull << 31)) + 1, (int64_t)lim, (int64_t)lim + 1};
+    for (int k = 0; k < TB_N - 1 && r[k] != INT32_MAX; ++k)
+      for (int64_t d = -1; d <= 1; ++d) Ts.push_back((int64_t)r[k] + d);
+    for (int64_t T : Ts) {
+      if (T < 1) continue;
+      int64_t got;
+      if (T > (int64_t)lim) {
+        got = tiebreak_position(sd, sq, T);   // the kernel's fallback
+      } else {
+        int cnt = 0;
+        for (int k = 0; k < TB_N - 1; ++k) cnt += (r[k] != INT32_MAX && (int64_t)r[k] <= T) ? 1 : 0;
+        got = cnt ? (int64_t)r[cnt - 1] : 1;
+      }
+      const int64_t want = tiebreak_position(sd, sq, T);
+      if (got != want) {
+        if (!bad && msg && len)
+          snprintf(msg, len, "seed %llu seq %llu T %lld: lookup %lld, walk %lld", (unsigned long long)sd,
+                   (unsigned long long)sq, (long long)T, (long long)got, (long long)want);
+        ++bad;
+      }
+    }
+  }
+  return bad;
+}
 
 // ST: diagnostic build with s_memtime phase stamps (accumulated per phase, written to a.stamps)
 template <bool ST>
