@@ -265,7 +265,7 @@ __host__ __device__ inline void tiebreak_records(uint64_t seed, uint64_t seq, in
 // scores for every later pod are re-evaluated exactly (dso = batch-start score, dsc = current score).
 // The max M is valid when it exceeds every shard's highest unlisted score (`next`); otherwise the batch
 // is cut at k. Ties at M are ordered by node index across shards (shards are contiguous ranges).
-constexpr int NUMA_PPT = 2;   // pods per thread in eval_numa_kernel (full batches)
+constexpr int NUMA_PPT = 4;   // pods per thread in eval_numa_kernel (full batches): half the row traffic of 2 at the same pass time
 constexpr int COMMIT_WAVES = 4, COMMIT_THREADS = 64 * COMMIT_WAVES;   // commit workgroup
 constexpr int HASH = 1024;
 constexpr int POD_STRIDE = 136;   // LDS bytes per pod vector in the commit kernel (sizeof(PodVec) + 8)
