@@ -9,6 +9,8 @@ gives every GPU 50k nodes. `--profile la-fit` drops NodeNUMAResource (the C2 plu
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
+    (rehearsal of the sharded flow on a one-GPU box: N processes on device 0, all-gather over gloo through the
+     library's host-callback transport: ... bench.py --gpus N --transport gloo --share-gpu)
 
 Prints ONE JSON line on rank 0 (value = whole-job pod x node evaluations per second).
 """
@@ -86,6 +88,33 @@ def cpu_baseline_c5(cluster, cfg, ext_args, pods, seq, sample_pods: int) -> dict
                       "DeviceShare + Reservation restatement)"}
 
 
+def host_cpus() -> dict:
+    """The host CPUs the CPU baseline runs on: logical CPUs of the machine (nproc), the ones this process may run on
+    (affinity), the cgroup CPU quota (a box's share of the machine), and the CPU model."""
+    info = {"nproc": os.cpu_count(), "affinity": len(os.sched_getaffinity(0)), "cgroup_quota_cpus": None,
+            "model": None}
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+            if q != "max":
+                info["cgroup_quota_cpus"] = int(q) / int(per)
+    except (OSError, ValueError):
+        pass
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    info["model"] = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    usable = info["affinity"]
+    if info["cgroup_quota_cpus"]:
+        usable = min(usable, max(1, int(info["cgroup_quota_cpus"])))
+    info["usable"] = usable
+    return info
+
+
 PMC_FILE = os.path.join(ROOT, "profiles", "pmc_latest.json")
 
 
@@ -116,6 +145,9 @@ def main() -> None:
                     help="c5: 100k nodes, LoadAware + Fit + DeviceShare + Reservation (SURVEY 8(d) C5, see --nodes)")
     ap.add_argument("--sample-pct", type=int, default=None,
                     help="node sampling (percentageOfNodesToScore; 0 = adaptive) instead of every node (one GPU)")
+    ap.add_argument("--transport", choices=["rccl", "gloo"], default="rccl",
+                    help="several ranks: RCCL all-gather (production) or gloo through the host-callback transport")
+    ap.add_argument("--share-gpu", action="store_true", help="every rank on device 0 (gloo rehearsal on one GPU)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -128,10 +160,17 @@ def main() -> None:
     import torch.distributed as dist
     if not torch.cuda.is_available():
         raise SystemExit("bench.py needs an MI355X (no GPU visible)")
-    torch.cuda.set_device(local_rank)
+    gloo = world > 1 and args.transport == "gloo"
+    if args.share_gpu and not gloo:
+        raise SystemExit("--share-gpu needs --transport gloo (RCCL takes one GPU per rank)")
+    device = 0 if args.share_gpu else local_rank
+    torch.cuda.set_device(device)
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        if gloo:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
 
     from koordinator_amd import config, synth
     from koordinator_amd.engine import Engine, unique_id
@@ -150,12 +189,19 @@ def main() -> None:
     from koordinator_amd import abi
     if args.sample_pct is not None and world > 1:
         raise SystemExit("--sample-pct runs on one GPU")
-    cfg = config.make_config(n_nodes, device=local_rank, batch_size=args.batch,
+    cfg = config.make_config(n_nodes, device=device, batch_size=args.batch,
                              enabled=abi.GS_ENABLE_ALL if numa else abi.GS_ENABLE_LA_FIT,
                              percentage_of_nodes_to_score=args.sample_pct)
 
     eng = Engine(cfg)
-    if world > 1:
+    if gloo:
+        def allgather(data: bytes):
+            t = torch.frombuffer(bytearray(data), dtype=torch.uint8)
+            out = [torch.empty_like(t) for _ in range(world)]
+            dist.all_gather(out, t)
+            return [x.numpy().tobytes() for x in out]
+        eng.comm_init_callback(world, rank, allgather)
+    elif world > 1:
         uid = [unique_id() if rank == 0 else None]
         dist.broadcast_object_list(uid, src=0)
         eng.comm_init_rccl(uid[0], world, rank)
@@ -196,7 +242,7 @@ def main() -> None:
         dist.barrier()
     dt = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([dt], device="cuda", dtype=torch.float64)
+        t = torch.tensor([dt], device="cpu" if gloo else "cuda", dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
 
@@ -252,10 +298,20 @@ def main() -> None:
         cpu = {"value": r["evals_per_s"], "unit": "evals/s", "cores": 1, "kind": "port", "pods_per_s": r["pods_per_s"],
                "seconds": r["seconds"], "sample": r["sample"]}
     elif rank == 0 and world == 1 and not args.no_cpu_baseline:
-        threads = min(os.cpu_count() or 1, int(os.environ.get("OMP_NUM_THREADS", "16")), 16)
+        hc = host_cpus()
+        threads = min(hc["usable"], 16)
         sample_start = args.warmup * P
         r = cpu_baseline(cluster, cfg, pods, seq, given, sample_start, args.cpu_sample_pods, threads)
-        cpu = {"value": r["evals_per_s"], "unit": "evals/s", "cores": threads, "kind": "port",
+        # run B: every usable host core; the same as run A when the box's CPU share is 16 or less
+        rb = None
+        if hc["usable"] > threads:
+            rb = cpu_baseline(cluster, cfg, pods, seq, given, sample_start, args.cpu_sample_pods, hc["usable"])
+        cpu = {"value": r["evals_per_s"], "unit": "evals/s", "cores": threads, "kind": "port", "host": hc,
+               "all_cores": ({"cores": hc["usable"], "value": rb["evals_per_s"], "pods_per_s": rb["pods_per_s"],
+                              "chunk_pods_per_s": rb["chunk_pods_per_s"]} if rb else
+                             {"cores": threads, "note": f"all usable host cores = {hc['usable']} (affinity "
+                                                        f"{hc['affinity']}, cgroup quota {hc['cgroup_quota_cpus']}): "
+                                                        "run A is already every usable core"}),
                "sample": r["sample"] + f"; sequential scheduleOne with Filter/Score fanned out over {threads} threads "
                          "(parallelize.Until emulation, parallelism=16 = the reference default and this box's CPU "
                          "share); CPU restatement of the reference Go path (oracle/), not the Go binary",
@@ -292,7 +348,9 @@ def main() -> None:
                              f"{P} pods/step, NodeResourcesFit(LeastAllocated)+LoadAwareScheduling filter+score, "
                              "selectHost, assume+Reserve"),
                 "nodes": n_nodes, "pods_per_step": P, "batch": args.batch,
-                "parallelism": f"node-shard x{world}, commit replicated on every rank",
+                "parallelism": f"node-shard x{world}, commit replicated on every rank" +
+                               (" (gloo host-callback all-gather, every rank on one GPU: a rehearsal, not a scaling "
+                                "point)" if args.share_gpu else ""),
                 "level_list_cap": 2048,
                 "node_sampling": None if args.sample_pct is None else {
                     "percentage_of_nodes_to_score": args.sample_pct,

@@ -347,7 +347,7 @@ typedef struct gs_stats {
   double eval_ms;            /* summed device time of the fused filter+score kernel (HIP events) */
   double cand_ms;            /* summed device time of candidate extraction */
   double commit_ms;          /* summed device time of the sequential commit kernel */
-  double exchange_ms;        /* host wall time in the all-gather (multi-GPU) */
+  double exchange_ms;        /* all-gather time (multi-GPU): RCCL from stream events around each collective, the host-callback transport as host wall time */
   uint64_t node_row_bytes;   /* bytes one pod x node evaluation reads from the node mirror */
   uint32_t shard_begin, shard_end; /* this rank's node range */
   uint32_t next_start_node_index;  /* [upstream] Scheduler.nextStartNodeIndex after the last scheduled pod */

@@ -21,8 +21,19 @@
 //                log the slot's state, apply assume + Reserve (NUMA split, cpuset), queue the row's re-scoring.
 //   waves 2..7   re-scoring jobs: a reserved row's new score for 64 later pods, one pod per lane (each wave builds
 //                the row's hint table itself).
-// All hand-offs are LDS words (release / acquire); every wait is bounded (an expired wait ends the batch at the
-// verified prefix with GS_COMMIT_TIMEOUT in committed[3], so a bug cannot hang the GPU).
+// All hand-offs are LDS words (release / acquire); every wait is bounded: an expired wait (any wave) ends the kernel
+// with a site code in committed[3], nothing committed and nothing written back (the host fails the call with
+// GS_EDEVICE; HBM and host mirror both keep the batch-start state), so a bug cannot hang the GPU.
+//
+// Several shards (a.nranks > 1): the levels are the all-gathered shards' levels merged into one list per pod
+// (merge_levels_kernel), and every rank runs this kernel on them over its full mirror replica. A fresh winner row
+// outside the rank's shard has no batch-start score row here (S_own is the own shard's), so its batch-start scores
+// for the later pods are unknown (SO_UNKNOWN in dso) until a re-scoring wave has evaluated the row as it stood at
+// batch start (the HBM mirror: rows are written back at the kernel's end) — a "batch-start job" queued by the
+// Reserve wave. Meanwhile a decision finds such a node in the pod's list head (its listed level: exact), or records
+// it as unknown: the decision treated the node as clean and unlisted, which stands iff its batch-start score turns
+// out below the decided maximum; the verification checks that (and takes the node's batch-start feasibility out of
+// the Feasible count) once the creating pod is complete — same rule as a pending row.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -33,10 +44,12 @@ namespace gs {
 constexpr int SP_WAVES = 8, SP_THREADS = 64 * SP_WAVES;
 constexpr int SP_LAG = 16;       // decided - verified <= SP_LAG (undo log depth)
 constexpr int SP_TABLES = SP_WAVES - 2;   // one hint table per re-scoring wave
-constexpr int SP_JOBQ = 32;      // re-scoring job ring
+constexpr int SP_JOBQ = 64;      // re-scoring job ring (<= 3 jobs per pod, <= SP_LAG + 2 pods in flight)
 constexpr int SP_HASH = 256;     // node -> slot (full-row resolution)
-constexpr int SP_FRESH = 1, SP_FITERR = 2, SP_SLOW = 4;   // DecRec.flags
+constexpr int SP_FRESH = 1, SP_FITERR = 2, SP_SLOW = 4, SP_OFFSHARD = 8;   // DecRec.flags
 constexpr uint32_t SP_SPIN_LIMIT = 1u << 24;
+constexpr int16_t SO_UNKNOWN = -2;    // dso: batch-start score of an off-shard fresh row not evaluated yet
+constexpr int16_t SO_UNLISTED = -3;   // a decision's view of such a row not in the pod's list head
 
 struct DecRec {          // one decided pod
   int32_t winner;        // node (-1: FitError)
@@ -46,6 +59,7 @@ struct DecRec {          // one decided pod
   int32_t prev_pend;     // the slot's previous version (a landing on an existing slot)
   uint32_t flags;
   uint64_t pend0, pend1; // pending slots at decision time
+  uint64_t unk0, unk1;   // slots whose batch-start score was unknown at decision time (several shards)
 };
 struct UndoRec {         // a slot's state before a Reserve
   Row row;
@@ -69,7 +83,7 @@ size_t spec_smem_bytes(int B) {   // the kernel's LDS carve-up, piece by piece w
   take((size_t)B * sizeof(DecRec));
   take((size_t)SP_LAG * sizeof(UndoRec));
   take((size_t)SP_TABLES * sizeof(HintTable));
-  for (int i = 0; i < 5; ++i) take((size_t)B * 4);  // final_F, done_ver, has_row, rescored, jobs_left
+  for (int i = 0; i < 6; ++i) take((size_t)B * 4);  // final_F, done_ver, has_row, rescored, jobs_left, jobs_all
   take((size_t)SP_HASH * 4);                        // hkey
   take((size_t)SP_HASH * 4);                        // hval
   take((size_t)SP_JOBQ * sizeof(Job));
@@ -98,6 +112,7 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   const MirrorView& m = a.m;
   const bool numa_on = (a.pf.enabled & 0x30u) != 0;
+  const bool multi = a.nranks > 1;   // merged levels of several shards; rows outside [own0, own1) have no S_own
   const uint64_t lt_mask = (1ull << lane) - 1ull;
   // ---- LDS carve-up
   unsigned char* cur = cm;
@@ -115,7 +130,8 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
   int32_t* done_ver = reinterpret_cast<int32_t*>(take((size_t)B * 4));   // slot: version whose re-scoring is complete
   int32_t* has_row = reinterpret_cast<int32_t*>(take((size_t)B * 4));    // slot: row fetched into LDS
   int32_t* rescored = reinterpret_cast<int32_t*>(take((size_t)B * 4));   // pod: Reserve + re-scoring complete
-  int32_t* jobs_left = reinterpret_cast<int32_t*>(take((size_t)B * 4));
+  int32_t* jobs_left = reinterpret_cast<int32_t*>(take((size_t)B * 4));  // pod: re-scoring jobs not done (-> done_ver)
+  int32_t* jobs_all = reinterpret_cast<int32_t*>(take((size_t)B * 4));   // pod: every job not done (-> rescored)
   int32_t* hkey = reinterpret_cast<int32_t*>(take((size_t)SP_HASH * 4));
   int32_t* hval = reinterpret_cast<int32_t*>(take((size_t)SP_HASH * 4));
   Job* jobq = reinterpret_cast<Job*>(take((size_t)SP_JOBQ * sizeof(Job)));
@@ -124,6 +140,7 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
   __shared__ uint64_t s_cpuset[4];
   __shared__ int32_t s_aff;
   __shared__ int32_t s_decided, s_reserved, s_stop, s_parked, s_finish, s_cut_at, s_err;
+  __shared__ int32_t s_werr;        // a Reserve / re-scoring wave's bounded wait expired (its site code)
   __shared__ int32_t s_jq_head, s_jq_tail;
   __shared__ int32_t s_committed, s_hostcut, s_nd, s_endwhy;
   __shared__ uint64_t sseq[MAX_BATCH];
@@ -139,11 +156,12 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
     has_row[i] = 0;
     rescored[i] = 0;
     jobs_left[i] = 0;
+    jobs_all[i] = 0;
   }
   for (int i = tid; i < SP_HASH; i += SP_THREADS) { hkey[i] = -1; hval[i] = -1; }
   for (int i = tid; i < B; i += SP_THREADS) tiebreak_records(a.seed, a.seq[i], a.tb + (size_t)i * TB_N);
   if (tid == 0) {
-    s_decided = 0; s_reserved = 0; s_stop = 0; s_parked = 0; s_finish = 0; s_cut_at = -1; s_err = 0;
+    s_decided = 0; s_reserved = 0; s_stop = 0; s_parked = 0; s_finish = 0; s_cut_at = -1; s_err = 0; s_werr = 0;
     s_jq_head = 0; s_jq_tail = 0; s_committed = 0; s_hostcut = 0; s_nd = 0;
   }
   __syncthreads();
@@ -235,6 +253,18 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
           mis |= sc >= 0 && sc >= d.M;
           fadd += sc >= 0;
         }
+        // unknown batch-start scores (several shards): known now (the creating pod is complete); the decision counted
+        // the node as clean and unlisted
+        if ((d.unk0 >> lane) & 1ull) {
+          const int so = dso[v * B + lane];
+          mis |= so >= 0 && so >= d.M;
+          fadd -= so >= 0;
+        }
+        if ((d.unk1 >> lane) & 1ull) {
+          const int so = dso[v * B + 64 + lane];
+          mis |= so >= 0 && so >= d.M;
+          fadd -= so >= 0;
+        }
         if (__ballot(mis)) {
           // ---------------- rollback to v: park the other waves, undo the Reserves of pods >= v, restore versions
           st_rel(&s_stop, 1);
@@ -294,7 +324,7 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
           const int32_t myv0 = pv0, myv1 = pv1;
           if (lane < nd) done_ver[lane] = myv0;
           if (lane + 64 < nd) done_ver[lane + 64] = myv1;
-          for (int qq = v + lane; qq < B; qq += 64) { rescored[qq] = 0; jobs_left[qq] = 0; }
+          for (int qq = v + lane; qq < B; qq += 64) { rescored[qq] = 0; jobs_left[qq] = 0; jobs_all[qq] = 0; }
           if (lane == 0) {
             s_jq_head = 0;
             s_jq_tail = 0;
@@ -332,6 +362,7 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
       // ------------------------------------------------ decide pod q
       if (q >= end_at || q - v >= SP_LAG || ld_acq(&s_cut_at) >= 0) {
         if (++spins > SP_SPIN_LIMIT) { err = true; err_code = 2; break; }
+        if (const int we = ld_acq(&s_werr)) { err = true; err_code = we; break; }
         sp_sleep();
         if (q >= end_at) SPM(23);   // waiting at the batch's end
         continue;
@@ -356,6 +387,32 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
       flush_fresh();
       if (lane < nd) { so0 = dso[p * B + lane]; if (rdy0) sc0 = dsc[p * B + lane]; }
       if (lane + 64 < nd) { so1 = dso[p * B + 64 + lane]; if (rdy1) sc1 = dsc[p * B + 64 + lane]; }
+      uint64_t unk0 = 0, unk1 = 0;
+      if (multi) {
+        // off-shard fresh rows whose batch-start job has not finished: a node in the list head has its listed level
+        // as batch-start score (exact); any other is unknown, counted as clean and unlisted (checked at verification)
+        const uint64_t u0 = __ballot(lane < nd && so0 == SO_UNKNOWN), u1 = __ballot(lane + 64 < nd && so1 == SO_UNKNOWN);
+        if (u0 | u1) {
+          const int incl = wave_incl_scan(lane < nlev ? hc : 0);   // list end of level `lane`
+          const int listed = __builtin_amdgcn_readlane(incl, 63);
+          for (int pass = 0; pass < 2; ++pass)
+            for (uint64_t bb = pass ? u1 : u0; bb; bb &= bb - 1) {
+              const int s = __builtin_ctzll(bb);
+              const uint32_t nn = (uint32_t)__builtin_amdgcn_readlane((int)(pass ? dn1 : dn0), s);
+              const uint64_t f = __ballot(lane < listed && lh == nn);
+              int sv = SO_UNLISTED;
+              if (f) {
+                const int e = __builtin_ctzll(f);
+                sv = __builtin_amdgcn_readlane(hs, __popcll(__ballot(lane < nlev && incl <= e)));
+              } else if (pass) {
+                unk1 |= 1ull << s;
+              } else {
+                unk0 |= 1ull << s;
+              }
+              if (lane == s) { if (pass) so1 = sv; else so0 = sv; }
+            }
+        }
+      }
       // action 0 commit, 1 FitError, 2 stop deciding before p
       int action = 0;
       uint32_t winner = 0xffffffffu;
@@ -611,6 +668,8 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
       d.nd_before = nd;
       d.pend0 = pend0;
       d.pend1 = pend1;
+      d.unk0 = unk0;
+      d.unk1 = unk1;
       d.flags = (action == 1 ? SP_FITERR : 0u) | (slowpath ? SP_SLOW : 0u);
       d.slot = -1;
       d.prev_pend = -1;
@@ -622,10 +681,16 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
           d.flags |= SP_FRESH;
           if (lane == (nd & 63)) { if (nd < 64) { dn0 = winner; pv0 = p; } else { dn1 = winner; pv1 = p; } }
           const int q0 = p + 1 + lane, q1 = q0 + 64;
-          ps_v0 = q0 < B ? a.S_own[(size_t)q0 * a.ld + (winner - a.own0)] : (int16_t)0;
-          ps_v1 = q1 < B ? a.S_own[(size_t)q1 * a.ld + (winner - a.own0)] : (int16_t)0;
-          ps_slot = slot;
-          ps_p = p;
+          if (winner - a.own0 < a.own1 - a.own0) {
+            ps_v0 = q0 < B ? a.S_own[(size_t)q0 * a.ld + (winner - a.own0)] : (int16_t)0;
+            ps_v1 = q1 < B ? a.S_own[(size_t)q1 * a.ld + (winner - a.own0)] : (int16_t)0;
+            ps_slot = slot;
+            ps_p = p;
+          } else {   // another shard's row: unknown until the Reserve wave's batch-start job has evaluated it
+            d.flags |= SP_OFFSHARD;
+            if (q0 < B) dso[q0 * B + slot] = SO_UNKNOWN;
+            if (q1 < B) dso[q1 * B + slot] = SO_UNKNOWN;
+          }
           if (lane == 0) {
             hash_insert(winner, slot);
             done_ver[slot] = -1;
@@ -650,6 +715,7 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
       uint32_t w = 0;
       while (ld_acq(&s_reserved) < committed) {
         if (++w > SP_SPIN_LIMIT) { err = true; err_code = 4; break; }
+        if (const int we = ld_acq(&s_werr)) { err = true; err_code = we; break; }
         sp_sleep();
       }
     }
@@ -687,13 +753,29 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
       int64_t vv = 0;
       if (f_kind == 1) vv = reinterpret_cast<const int64_t*>(f_src)[node];
       else if (f_kind == 2) vv = reinterpret_cast<const int32_t*>(f_src)[node];
-      else if (f_kind == 3) vv = (int64_t)reinterpret_cast<const uint8_t*>(f_src)[(size_t)qq * a.ld + (node - a.own0)];
+      else if (f_kind == 3)   // the Filter-time affinity, known for the own shard's rows only (-1: recomputed)
+        vv = node - a.own0 < a.own1 - a.own0
+                 ? (int64_t)reinterpret_cast<const uint8_t*>(f_src)[(size_t)qq * a.ld + (node - a.own0)]
+                 : (int64_t)-1;
       else if (f_kind == 4) vv = (int64_t)node;
       return vv;
     };
     int q = 0, pf_q = -1;   // pf_q: the pod whose fresh winner row is in flight in pf_v
     int64_t pf_v = 0;
     uint32_t spins = 0;
+    // room for n more jobs in the ring (this wave is its only producer); false: a rollback or the end intervened
+    auto room = [&](int n) -> bool {
+      uint32_t w = 0;
+      while (s_jq_tail - ld_acq(&s_jq_head) + n > SP_JOBQ) {
+        if (ld_acq(&s_stop) || ld_acq(&s_finish)) return false;
+        if (++w > SP_SPIN_LIMIT) {
+          if (lane == 0) __atomic_store_n(&s_werr, 7, __ATOMIC_RELEASE);
+          return false;
+        }
+        sp_sleep();
+      }
+      return true;
+    };
     for (;;) {
       if (ld_acq(&s_stop)) {   // rollback: park until wave 0 has repaired the state, then resume at s_reserved
         if (lane == 0) __atomic_fetch_add(&s_parked, 1, __ATOMIC_ACQ_REL);
@@ -705,7 +787,10 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
       }
       if (ld_acq(&s_finish)) break;
       if (q >= ld_acq(&s_decided) || ld_acq(&s_cut_at) >= 0) {
-        if (++spins > SP_SPIN_LIMIT) break;
+        if (++spins > SP_SPIN_LIMIT) {
+          if (lane == 0) __atomic_store_n(&s_werr, 5, __ATOMIC_RELEASE);
+          break;
+        }
         sp_sleep();
         if (q == 0) SPM(26);   // waiting for the batch's first decision
         SPM(6);
@@ -753,6 +838,21 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
         }
         if (stop) continue;
         SPM(22);   // landed-again slot: wait for its previous re-scoring
+      }
+      const int nlater = B - (q + 1);
+      const int njobs = (nlater + 63) / 64;
+      const bool xjob = (d.flags & SP_OFFSHARD) && njobs > 0;
+      // ring room for this pod's jobs before the Reserve changes anything (a rollback may end the wait; it only grows)
+      if (!room(njobs + (xjob ? 1 : 0))) continue;
+      if (xjob) {   // another shard's row: its batch-start job goes first, ahead of the row's re-scoring jobs
+        if (lane == 0) {
+          jobs_left[q] = njobs;
+          jobs_all[q] = njobs + 1;
+          const int t = s_jq_tail;
+          jobq[t % SP_JOBQ] = Job{slot, q, -1, (int32_t)winner};
+          __atomic_store_n(&s_jq_tail, t + 1, __ATOMIC_RELEASE);
+        }
+        WAVE_FENCE();
       }
       if (lane == 0 && (!fresh || !numa_on)) s_aff = -1;
       WAVE_FENCE();
@@ -855,8 +955,6 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
         if ((dn.flags & (SP_FRESH | SP_FITERR)) == SP_FRESH) { pf_v = fetch(q + 1, (uint32_t)dn.winner); pf_q = q + 1; }
       }
       // ---- the row's re-scoring: hint table of its new state, jobs of 64 later pods
-      const int nlater = B - (q + 1);
-      const int njobs = (nlater + 63) / 64;
       if (njobs == 0) {
         if (lane == 0) {
           done_ver[slot] = q;
@@ -864,7 +962,10 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
         }
       } else {
         if (lane == 0) {
-          jobs_left[q] = njobs;
+          if (!xjob) {
+            jobs_left[q] = njobs;
+            jobs_all[q] = njobs;
+          }
           int t = s_jq_tail;
           for (int j = 0; j < njobs; ++j, ++t) jobq[t % SP_JOBQ] = Job{slot, q, j, 0};
           __atomic_store_n(&s_jq_tail, t, __ATOMIC_RELEASE);
@@ -899,7 +1000,10 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
       }
       h = __builtin_amdgcn_readfirstlane(h);
       if (h < 0) {
-        if (++spins > SP_SPIN_LIMIT) break;
+        if (++spins > SP_SPIN_LIMIT) {
+          if (lane == 0) __atomic_store_n(&s_werr, 6, __ATOMIC_RELEASE);
+          break;
+        }
         sp_sleep();
         SPM(8);
         continue;
@@ -907,26 +1011,44 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
       spins = 0;
       SPM(8);
       const Job jb = jobq[h % SP_JOBQ];
-      const Row rr = drows[jb.slot];
       HintTable& tab = tables[wv - 2];
+      if (jb.range < 0) {
+        // batch-start job (several shards): another shard's fresh row as it stood at batch start — the HBM mirror,
+        // written back only at the kernel's end — evaluated for every later pod: its dso entries
+        const uint32_t node = (uint32_t)__builtin_amdgcn_readfirstlane(jb.tbl);
+        Row rr;
+        load_row(m, node, true, numa_on, rr);
+        for (int s = 3; s < 7; ++s) rr.free[s] = m.c64(C_FREE_CPU + s)[node];
+        if (numa_on && ((rr.nr.nflags >> NF_POLICY_SHIFT) & 3u)) hint_table_fill(tab, rr.nr, zone_avail(rr.nr), lane);
+        WAVE_FENCE();
+        for (int q2 = jb.q + 1 + lane; q2 < B; q2 += 64) dso[q2 * B + jb.slot] = (int16_t)row_score(rr, pods(q2), a.pf, m, &tab);
+        WAVE_FENCE();
+        if (lane == 0 && __atomic_fetch_sub(&jobs_all[jb.q], 1, __ATOMIC_ACQ_REL) == 1)
+          __atomic_store_n(&rescored[jb.q], 1, __ATOMIC_RELEASE);
+        WAVE_FENCE();
+        SPM(7);
+        continue;
+      }
+      const Row rr = drows[jb.slot];
       if (numa_on && ((rr.nr.nflags >> NF_POLICY_SHIFT) & 3u)) hint_table_fill(tab, rr.nr, zone_avail(rr.nr), lane);
       WAVE_FENCE();
       const int q2 = jb.q + 1 + jb.range * 64 + lane;
       if (q2 < B) dsc[q2 * B + jb.slot] = (int16_t)row_score(rr, pods(q2), a.pf, m, &tab);
       WAVE_FENCE();
       if (lane == 0) {
-        if (__atomic_fetch_sub(&jobs_left[jb.q], 1, __ATOMIC_ACQ_REL) == 1) {
+        if (__atomic_fetch_sub(&jobs_left[jb.q], 1, __ATOMIC_ACQ_REL) == 1)
           __atomic_store_n(&done_ver[jb.slot], jb.q, __ATOMIC_RELEASE);
+        if (__atomic_fetch_sub(&jobs_all[jb.q], 1, __ATOMIC_ACQ_REL) == 1)
           __atomic_store_n(&rescored[jb.q], 1, __ATOMIC_RELEASE);
-        }
       }
       WAVE_FENCE();
       SPM(7);
     }
   }
   __syncthreads();
-  // ---- write back the fetched dirty rows; final Feasible counts
-  const int nd = s_nd, committed = s_committed;
+  // ---- write back the fetched dirty rows; final Feasible counts. After an expired wait nothing is written back and
+  // nothing is committed: the HBM mirror keeps its batch-start state, which is the host's (it applies no placement)
+  const int nd = s_err ? 0 : s_nd, committed = s_err ? 0 : s_committed;
   for (int e = tid; e < nd * ROW_I64; e += SP_THREADS) {
     const int s = e / ROW_I64, j = e % ROW_I64;
     if (has_row[s] && row_word_mutable(j)) m.c64(kRowCol[j])[drows[s].node] = reinterpret_cast<const int64_t*>(&drows[s])[j];

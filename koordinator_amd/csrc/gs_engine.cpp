@@ -92,6 +92,7 @@ struct gs_ctx {
   uint32_t ld = 0;
   uint8_t* d_xchg_send = nullptr;   // local lists + headers (contiguous, all-gathered)
   uint8_t* d_xchg_recv = nullptr;   // R blocks
+  uint8_t* d_xmerged = nullptr;     // several ranks, speculative commit: the R blocks' levels merged into one block
   size_t xchg_bytes = 0;
   PlacementDev* d_out = nullptr;
   int32_t* d_committed = nullptr;
@@ -624,11 +625,21 @@ double ev_ms(hipEvent_t a, hipEvent_t b) {
   return ms;
 }
 
-// exchange_ms of RCCL all-gathers: completion time from events around each collective on the stream, added up
-// once the batch's work has completed (finish_batch)
+// exchange_ms of RCCL all-gathers: completion time from events around each collective on the stream, added up once
+// a collective's end event has completed (finish_batch); the pairs of a speculative batch still in flight stay pending
 void flush_exchange_times(gs_ctx* c) {
-  for (int i = 0; i < c->x_pending; ++i) c->stats.exchange_ms += ev_ms(c->x_ev[2 * i], c->x_ev[2 * i + 1]);
-  c->x_pending = 0;
+  int keep = 0;
+  for (int i = 0; i < c->x_pending; ++i) {
+    hipEvent_t a = c->x_ev[2 * i], b = c->x_ev[2 * i + 1];
+    if (hipEventQuery(b) == hipSuccess) {
+      c->stats.exchange_ms += ev_ms(a, b);
+    } else {   // still in flight: keep the pair (moved to the front)
+      std::swap(c->x_ev[2 * keep], c->x_ev[2 * i]);
+      std::swap(c->x_ev[2 * keep + 1], c->x_ev[2 * i + 1]);
+      ++keep;
+    }
+  }
+  c->x_pending = keep;
 }
 
 int exchange(gs_ctx* c, const void* d_send, void* d_recv, size_t bytes) {
@@ -815,6 +826,8 @@ int alloc_exchange(gs_ctx* c) {
   if (c->h_xchg_recv) { (void)hipHostFree(c->h_xchg_recv); c->h_xchg_recv = nullptr; }
   HIP_TRY(c, hipMalloc(&c->d_xchg_recv, c->xchg_bytes * c->nranks + 64));
   HIP_TRY(c, hipHostMalloc(&c->h_xchg_recv, c->xchg_bytes * c->nranks + 64, hipHostMallocDefault));
+  if (c->d_xmerged) { (void)hipFree(c->d_xmerged); c->d_xmerged = nullptr; }
+  HIP_TRY(c, hipMalloc(&c->d_xmerged, c->xchg_bytes + 64));
   return GS_OK;
 }
 
@@ -838,7 +851,8 @@ CommitArgs commit_args(gs_ctx* c, int b) {
   a.npods = b;
   a.nranks = c->nranks;
   a.shard_size = (c->N + c->nranks - 1) / c->nranks;
-  a.xbase = c->nranks > 1 ? c->d_xchg_recv : c->d_xchg_send;
+  // several ranks: the speculative commit reads the merged levels, the pipelined / lockstep kernels every rank block
+  a.xbase = c->nranks == 1 ? c->d_xchg_send : commit_spec_selected(c->window_k) ? c->d_xmerged : c->d_xchg_recv;
   a.xblock = c->xchg_bytes;
   a.bmax = c->B;
   a.pf = c->pf;
@@ -908,6 +922,8 @@ int launch_batch(gs_ctx* c, int b, const int32_t* prev, const PlacementDev* prev
   if (c->nranks > 1) {
     int rc = exchange(c, c->d_xchg_send, c->d_xchg_recv, c->xchg_bytes);
     if (rc) return rc;
+    if (commit_spec_selected(c->window_k))
+      HIP_TRY(c, launch_merge_levels(c->d_xchg_recv, c->xchg_bytes, c->nranks, b, c->B, c->d_xmerged, c->st));
   }
   CommitArgs a = commit_args(c, b);
   a.prev = prev;
@@ -1610,7 +1626,7 @@ int gs_destroy(gs_ctx* c) {
     uint64_t st[32] = {};
     if (hipMemcpy(st, c->d_stamps, 256, hipMemcpyDeviceToHost) == hipSuccess) {
       static const char* kind = getenv("GS_COMMIT_KERNEL");
-      if (c->nranks == 1 && !(kind && kind[0] == 'p') && !c->window_k) {   // speculative commit kernel
+      if (!(kind && kind[0] == 'p') && !c->window_k) {   // speculative commit kernel
         const double np = c->stats_all_pods ? (double)c->stats_all_pods : 1.0;
         fprintf(stderr, "gpuscore spec commit, cycles per committed pod (%llu pods): decide %.0f verify %.0f wave0-wait %.0f "
                 "rollback %.0f (%llu rollbacks) | Reserve busy %.0f wait %.0f | re-scoring busy %.0f wait %.0f (6 waves) | "
@@ -1659,6 +1675,7 @@ int gs_destroy(gs_ctx* c) {
   for (hipEvent_t ev : c->x_ev) (void)hipEventDestroy(ev);
   if (c->st) (void)hipStreamSynchronize(c->st);
   if (c->st_ev) (void)hipStreamSynchronize(c->st_ev);
+  if (c->st_rb) (void)hipStreamSynchronize(c->st_rb);   // readbacks into the pinned buffers freed below
   if (c->slot[0].d_pods) bind_slot(c, 0);
   {
     gs_ctx::Slot& s1 = c->slot[1];
@@ -1675,7 +1692,7 @@ int gs_destroy(gs_ctx* c) {
     for (auto& ev : s1.ev)
       if (ev) (void)hipEventDestroy(ev);
   }
-  void* dev[] = {c->d_i64, c->d_i32, c->d_pods, c->d_seq, c->d_S, c->d_xchg_send, c->d_xchg_recv, c->d_out,
+  void* dev[] = {c->d_i64, c->d_i32, c->d_pods, c->d_seq, c->d_S, c->d_xchg_send, c->d_xchg_recv, c->d_xmerged, c->d_out,
                  c->d_committed, c->d_rowstat, c->d_sel, c->d_stage_idx, c->d_stage_rows, c->d_numa_idx,
                  c->d_topos, c->d_aff, c->d_tb};
   for (void* p : dev)
@@ -1886,7 +1903,11 @@ int gs_schedule(gs_ctx* c, const gs_pod* pods, uint32_t npods, const uint64_t* s
   uint32_t i = 0;
   bool inflight = false, cur_special = false, spec_ok = true;
   int cur_b = 0;
-  auto drain = [&]() { (void)hipStreamSynchronize(c->st); (void)hipStreamSynchronize(c->st_ev); };
+  auto drain = [&]() {
+    (void)hipStreamSynchronize(c->st);
+    (void)hipStreamSynchronize(c->st_ev);
+    (void)hipStreamSynchronize(c->st_rb);   // a voided or in-flight batch's readback into the pinned buffers
+  };
   while (i < npods) {
     if (!inflight) {
       if ((rc = flush_rows(c))) return rc;
@@ -2123,6 +2144,7 @@ int gs_synchronize(gs_ctx* c) {
   if (!c) return GS_EINVAL;
   HIP_TRY(c, hipStreamSynchronize(c->st_ev));
   HIP_TRY(c, hipStreamSynchronize(c->st));
+  HIP_TRY(c, hipStreamSynchronize(c->st_rb));
   return GS_OK;
 }
 
@@ -2133,6 +2155,7 @@ int gs_reset(gs_ctx* c) {
   (void)hipStreamSynchronize(c->st);
   (void)hipStreamSynchronize(c->st_ev);
   (void)hipStreamSynchronize(c->st2);
+  (void)hipStreamSynchronize(c->st_rb);
   (void)hipGetLastError();
   for (uint32_t i = 0; i < c->N; ++i)
     if (c->nodes[i].valid) mark_dirty(c, i);

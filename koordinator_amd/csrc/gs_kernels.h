@@ -130,7 +130,12 @@ hipError_t launch_eval_full(const MirrorView& m, const PodVec* pods, int npods, 
 void set_cand_stamps(uint64_t* p);   // diagnostics: cand_kernel phase cycles (nullptr: off)
 hipError_t launch_cand(const int16_t* S, uint32_t ld, uint32_t len, uint32_t n0, int npods, int max_score,
                        uint32_t* lists, LevelHdr* hdrs, LevelExt* ext, hipStream_t st);
+// several shards: per pod, the all-gathered rank blocks' levels merged into one block of the single-rank layout (the
+// speculative commit's input)
+hipError_t launch_merge_levels(const uint8_t* xin, size_t xblock, int nranks, int npods, int bmax, uint8_t* xout,
+                               hipStream_t st);
 size_t commit_smem_bytes(int B);
+bool commit_spec_selected(uint32_t window_k);   // the speculative commit kernel runs (else pipelined / lockstep)
 hipError_t launch_commit(const CommitArgs& a, hipStream_t st);        // window_k > 0: lockstep kernel
 hipError_t launch_commit_pipe(const CommitArgs& a, hipStream_t st);   // pipelined roles (gs_commit.hip)
 hipError_t set_commit_pipe_attributes();

@@ -366,6 +366,108 @@ __global__ void __launch_bounds__(64 * W) cand_kernel(const int16_t* __restrict_
   }
 }
 
+// ------------------------------------------------------------------------------------------------
+// Several shards: the all-gathered candidate levels of every shard merged into ONE block of the single-rank layout, so
+// that the speculative commit runs over one list per pod as on one shard. Kept: the distinct scores above every shard's
+// `next` (each such level is complete on every shard), in descending order, while they fit LEVALL levels and LCAP
+// nodes; a level's nodes in shard order, i.e. node order (shards are contiguous ranges, each shard's level segment is
+// ascending). The merged `next` is the highest score not kept (every shard's `next`, or the first dropped level).
+// Block k = pod k; thread e = (shard e / LEVALL, level e % LEVALL).
+__global__ void __launch_bounds__(256) merge_levels_kernel(const uint8_t* __restrict__ xin, size_t xblock, int R,
+                                                           int bmax, uint8_t* __restrict__ xout) {
+  constexpr int NEMAX = MAX_RANKS * LEVALL;
+  static_assert(NEMAX <= 256, "one thread per shard level");
+  __shared__ int32_t e_score[NEMAX], e_count[NEMAX], e_rep[NEMAX];
+  __shared__ int32_t s_next[MAX_RANKS], s_feas[MAX_RANKS];
+  __shared__ int32_t m_score[LEVALL], m_count[LEVALL];
+  __shared__ int32_t s_nlev, s_drop;
+  const int k = blockIdx.x, t = threadIdx.x, NE = R * LEVALL;
+  const size_t hoff = (size_t)bmax * LCAP * 4, xoff = hoff + (size_t)bmax * sizeof(LevelHdr);
+  if (t == 0) { s_nlev = 0; s_drop = -1; }
+  if (t < LEVALL) { m_score[t] = -1; m_count[t] = 0; }
+  int off = 0;   // this level's offset in its shard's list
+  if (t < NE) {
+    const int r = t / LEVALL, j = t % LEVALL;
+    const LevelHdr* h = reinterpret_cast<const LevelHdr*>(xin + r * xblock + hoff) + k;
+    const LevelExt* x = reinterpret_cast<const LevelExt*>(xin + r * xblock + xoff) + k;
+    const int nl = x->nlev;
+    int s = -1, c = 0;
+    if (j < nl) {
+      s = j < MAXLEV ? h->score[j] : x->score[j - MAXLEV];
+      c = j < MAXLEV ? h->count[j] : x->count[j - MAXLEV];
+    }
+    e_score[t] = s;
+    e_count[t] = c;
+    if (j == 0) { s_next[r] = x->next; s_feas[r] = h->feasible; }
+  }
+  __syncthreads();
+  int mnext = -1, feas = 0;
+  for (int r = 0; r < R; ++r) { mnext = max(mnext, s_next[r]); feas += s_feas[r]; }
+  int s = -1;
+  if (t < NE) {
+    s = e_score[t];
+    const int r = t / LEVALL, j = t % LEVALL;
+    for (int jj = 0; jj < j; ++jj) off += e_count[r * LEVALL + jj];
+    bool rep = s > mnext;   // the first shard holding score s represents its merged level
+    for (int u = 0; u < t && rep; ++u) rep = e_score[u] != s;
+    e_rep[t] = rep;
+  }
+  __syncthreads();
+  int pos = -1;
+  if (t < NE && s > mnext) {
+
+    int rank = 0, cum = 0, before = 0, tot = 0;
+    for (int u = 0; u < NE; ++u) {
+      const int su = e_score[u];
+      if (su > s) { cum += e_count[u]; rank += e_rep[u]; }
+      else if (su == s) { tot += e_count[u]; if (u < t) before += e_count[u]; }
+    }
+    if (rank < LEVALL && cum + tot <= LCAP) {
+      pos = cum + before;
+      if (e_rep[t]) { m_score[rank] = s; m_count[rank] = tot; atomicAdd(&s_nlev, 1); }
+    } else if (e_rep[t]) {
+      atomicMax(&s_drop, s);
+    }
+  }
+  __syncthreads();
+  // the kept levels' nodes: entry by entry, every thread copying
+  uint32_t* out = reinterpret_cast<uint32_t*>(xout) + (size_t)k * LCAP;
+  __shared__ int32_t s_pos[NEMAX], s_off[NEMAX];
+  if (t < NE) { s_pos[t] = pos; s_off[t] = off; }
+  __syncthreads();
+  for (int u = 0; u < NE; ++u) {
+    const int pu = s_pos[u];
+    if (pu < 0) continue;
+    const uint32_t* in = reinterpret_cast<const uint32_t*>(xin + (u / LEVALL) * xblock) + (size_t)k * LCAP + s_off[u];
+    const int cu = e_count[u];
+    for (int x = t; x < cu; x += 256) out[pu + x] = in[x];
+  }
+  if (t == 0) {
+    const int nlev = s_nlev, next = max(mnext, s_drop);
+    LevelHdr h;
+    h.nlev = nlev < MAXLEV ? nlev : MAXLEV;
+    h.feasible = feas;
+    h.next = nlev > MAXLEV ? m_score[MAXLEV] : next;
+    int32_t tot = 0;
+    for (int j = 0; j < MAXLEV; ++j) { h.score[j] = m_score[j]; h.count[j] = m_count[j]; tot += m_count[j]; }
+    h.total = tot;
+    reinterpret_cast<LevelHdr*>(xout + hoff)[k] = h;
+    LevelExt x;
+    x.nlev = nlev;
+    x.next = next;
+    for (int j = 0; j < LEVX; ++j) { x.score[j] = m_score[MAXLEV + j]; x.count[j] = m_count[MAXLEV + j]; }
+    reinterpret_cast<LevelExt*>(xout + xoff)[k] = x;
+  }
+}
+
+hipError_t launch_merge_levels(const uint8_t* xin, size_t xblock, int nranks, int npods, int bmax, uint8_t* xout,
+                               hipStream_t st) {
+  if (npods <= 0) return hipSuccess;
+  if (nranks < 2 || nranks > MAX_RANKS) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(merge_levels_kernel, dim3(npods), dim3(256), 0, st, xin, xblock, nranks, bmax, xout);
+  return hipGetLastError();
+}
+
 int64_t host_tiebreak_position(uint64_t seed, uint64_t seq, int64_t T) { return tiebreak_position(seed, seq, T); }
 
 // selectHost tie-break lookup of the speculative commit (tiebreak_records + the lane-parallel count in
@@ -1314,11 +1416,16 @@ size_t commit_smem_bytes(int B) {
   return b;
 }
 
-hipError_t launch_commit(const CommitArgs& a, hipStream_t st) {
+bool commit_spec_selected(uint32_t window_k) {
   static const bool lockstep = getenv("GS_COMMIT_LOCKSTEP") && getenv("GS_COMMIT_LOCKSTEP")[0] == '1';
   static const char* kind = getenv("GS_COMMIT_KERNEL");   // "pipe": the non-speculative pipelined kernel
-  const bool spec_ok = !(kind && kind[0] == 'p') && a.nranks == 1 && a.S != nullptr;
-  if (!a.window_k && !lockstep && spec_ok) return launch_commit_spec(a, st);
+  return !window_k && !lockstep && !(kind && kind[0] == 'p');
+}
+
+hipError_t launch_commit(const CommitArgs& a, hipStream_t st) {
+  static const bool lockstep = getenv("GS_COMMIT_LOCKSTEP") && getenv("GS_COMMIT_LOCKSTEP")[0] == '1';
+  // several shards: the speculative kernel reads the merged levels (launch_merge_levels), the others every rank block
+  if (commit_spec_selected(a.window_k)) return launch_commit_spec(a, st);
   if (!a.window_k && !lockstep) return launch_commit_pipe(a, st);
   if (a.stamps)
     hipLaunchKernelGGL(commit_kernel<true>, dim3(1), dim3(COMMIT_THREADS), commit_smem_bytes(a.npods), st, a);

@@ -1,0 +1,113 @@
+"""C4: the 100k-node cluster node-sharded over 2 and 4 PROCESSES on the box's one GPU. Every rank
+evaluates its shard, the per-shard candidate levels are all-gathered (torch.distributed gloo through the library's
+host-callback transport, gs_comm_init_callback — RCCL's ncclAllGather carries the same bytes in production), merged
+on the device, and every rank runs the replicated speculative commit. All ranks must return identical placements
+and keep identical mirrors; the placements are checked against the CPU oracle by replay (the oracle's Filter on
+every chosen node, then Reserve; every 64th pod re-scheduled in full over all 100k nodes). Both plugin sets: C2's
+(NodeResourcesFit + LoadAwareScheduling) and C3's (+ NodeNUMAResource with NUMA splits and cpusets).
+Needs an MI355X: -m gpu."""
+import multiprocessing as mp
+import os
+import socket
+import time
+
+import numpy as np
+import pytest
+
+from tests.test_gpu_fullsize import _replay_check
+
+pytestmark = pytest.mark.gpu
+
+NODES = 100_000
+
+
+def _cluster(numa: bool, pods: int):
+    from koordinator_amd import synth
+    c = synth.make_cluster(NODES, pods, 4)
+    if numa:
+        synth.make_numa(c)
+    return c
+
+
+def _cfg(c, numa: bool):
+    from koordinator_amd import abi, config
+    return config.make_config(c.num_nodes, enabled=abi.GS_ENABLE_ALL if numa else abi.GS_ENABLE_LA_FIT)
+
+
+def _worker(rank: int, world: int, port: int, numa: bool, pods: int, q):
+    try:
+        import torch
+        import torch.distributed as dist
+        os.environ["MASTER_ADDR"] = "127.0.0.1"
+        os.environ["MASTER_PORT"] = str(port)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        from koordinator_amd.engine import Engine
+        c = _cluster(numa, pods)
+        e = Engine(_cfg(c, numa))
+
+        def allgather(data: bytes):
+            t = torch.frombuffer(bytearray(data), dtype=torch.uint8)
+            out = [torch.empty_like(t) for _ in range(world)]
+            dist.all_gather(out, t)
+            return [x.numpy().tobytes() for x in out]
+
+        e.comm_init_callback(world, rank, allgather)
+        from koordinator_amd import synth
+        synth.load_into(e, c)
+        dist.barrier()
+        t0 = time.perf_counter()
+        got = np.concatenate([e.schedule(c.pods[k:k + 4096], np.arange(k, min(k + 4096, pods), dtype=np.uint64))
+                              for k in range(0, pods, 4096)])
+        wall = time.perf_counter() - t0
+        st = e.stats()
+        q.put((rank, got.tobytes(), e.mirror_check(), wall, st["shard_begin"], st["shard_end"], st["cuts"]))
+        dist.barrier()
+        dist.destroy_process_group()
+    except Exception as ex:  # report instead of hanging the parent
+        q.put((rank, repr(ex), -1, 0.0, 0, 0, 0))
+
+
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+@pytest.mark.parametrize("world,numa,pods", [(2, False, 20_480), (4, False, 20_480), (2, True, 20_480),
+                                             (4, True, 50_000)],
+                         ids=["2proc-c2set", "4proc-c2set", "2proc-c3", "4proc-c3-50k"])
+def test_c4_sharded_processes_replay_parity(world, numa, pods):
+    from koordinator_amd import abi
+    t0 = time.perf_counter()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, numa, pods, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = {}
+    try:
+        for _ in range(world):
+            r, data, mirror_bad, wall, s0, s1, cuts = q.get(timeout=300)
+            assert mirror_bad >= 0, f"rank {r}: {data}"
+            res[r] = (np.frombuffer(data, abi.PLACEMENT_DTYPE), mirror_bad, wall, s0, s1, cuts)
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+            if p.exitcode is None:
+                p.kill()
+    for p in procs:
+        assert p.exitcode == 0
+    for r in range(world):
+        assert res[r][1] == 0, f"rank {r}: HBM mirror diverged from its host mirror"
+        assert res[r][4] == res[(r + 1) % world][3] or r == world - 1, "contiguous shards"
+        for f in ("node", "score", "ties", "feasible", "flags"):
+            assert np.array_equal(res[r][0][f], res[0][0][f]), f"rank {r}: {f} differs from rank 0"
+    got = res[0][0]
+    c = _cluster(numa, pods)
+    n = _replay_check(c, _cfg(c, numa), got, np.arange(0, pods, 64))
+    walls = [res[r][2] for r in range(world)]
+    print(f"C4 {world} processes x {NODES} nodes, {pods} pods ({'C3' if numa else 'C2 set'}): "
+          f"{int((got['node'] >= 0).sum())} placed, {n} re-checked in full, identical on every rank; schedule wall "
+          f"{max(walls):.1f} s ({pods / max(walls):.0f} pods/s through gloo), cuts {res[0][5]}; "
+          f"test wall {time.perf_counter() - t0:.1f} s")
