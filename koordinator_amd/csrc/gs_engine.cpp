@@ -94,6 +94,7 @@ struct gs_ctx {
   uint8_t* d_xchg_recv = nullptr;   // R blocks
   uint8_t* d_xmerged = nullptr;     // several ranks, speculative commit: the R blocks' levels merged into one block
   size_t xchg_bytes = 0;
+  int lstride = LCAP;               // listed nodes per pod in the local / exchanged blocks (XCAP: several ranks, spec)
   PlacementDev* d_out = nullptr;
   int32_t* d_committed = nullptr;
   int32_t* d_tb = nullptr;          // speculative commit: tie-break records of the batch's pods
@@ -813,21 +814,24 @@ void set_shard(gs_ctx* c) {
   c->stats.shard_end = c->n1;
 }
 
-// one rank's exchange block: [B x LCAP listed node ids | B LevelHdr | B LevelExt], padded to 256 B
-size_t lists_bytes(int B) { return (size_t)B * LCAP * 4; }
-size_t xchg_block_bytes(int B) {
-  size_t raw = lists_bytes(B) + (size_t)B * (sizeof(LevelHdr) + sizeof(LevelExt));
+// one rank's exchange block: [B x lstride listed node ids | B LevelHdr | B LevelExt], padded to 256 B
+size_t lists_bytes(int B, int lstride) { return (size_t)B * lstride * 4; }
+size_t xchg_block_bytes(int B, int lstride) {
+  size_t raw = lists_bytes(B, lstride) + (size_t)B * (sizeof(LevelHdr) + sizeof(LevelExt));
   return (raw + 255) / 256 * 256;
 }
 
 int alloc_exchange(gs_ctx* c) {
-  c->xchg_bytes = xchg_block_bytes(c->B);
+  // the speculative commit merges the shards' lists: XCAP listed nodes per (pod, shard) are enough for a pod at batch
+  // position k (k + 1 per shard), and the all-gathered block is 8x smaller; the other kernels read LCAP-wide blocks
+  c->lstride = commit_spec_selected(c->window_k) ? XCAP : LCAP;
+  c->xchg_bytes = xchg_block_bytes(c->B, c->lstride);
   if (c->d_xchg_recv) { (void)hipFree(c->d_xchg_recv); c->d_xchg_recv = nullptr; }
   if (c->h_xchg_recv) { (void)hipHostFree(c->h_xchg_recv); c->h_xchg_recv = nullptr; }
   HIP_TRY(c, hipMalloc(&c->d_xchg_recv, c->xchg_bytes * c->nranks + 64));
   HIP_TRY(c, hipHostMalloc(&c->h_xchg_recv, c->xchg_bytes * c->nranks + 64, hipHostMallocDefault));
   if (c->d_xmerged) { (void)hipFree(c->d_xmerged); c->d_xmerged = nullptr; }
-  HIP_TRY(c, hipMalloc(&c->d_xmerged, c->xchg_bytes + 64));
+  HIP_TRY(c, hipMalloc(&c->d_xmerged, xchg_block_bytes(c->B, LCAP) + 64));
   return GS_OK;
 }
 
@@ -884,8 +888,9 @@ CommitArgs commit_args(gs_ctx* c, int b) {
 // kernel does nothing unless that batch committed every pod and needs no host-side Reserve (prev[1] == 1).
 int launch_batch(gs_ctx* c, int b, const int32_t* prev, const PlacementDev* prev_out = nullptr, int prev_b = 0) {
   uint32_t* d_lists = reinterpret_cast<uint32_t*>(c->d_xchg_send);
-  LevelHdr* d_hdrs = reinterpret_cast<LevelHdr*>(c->d_xchg_send + lists_bytes(c->B));
-  LevelExt* d_ext = reinterpret_cast<LevelExt*>(c->d_xchg_send + lists_bytes(c->B) + (size_t)c->B * sizeof(LevelHdr));
+  LevelHdr* d_hdrs = reinterpret_cast<LevelHdr*>(c->d_xchg_send + lists_bytes(c->B, c->lstride));
+  LevelExt* d_ext =
+      reinterpret_cast<LevelExt*>(c->d_xchg_send + lists_bytes(c->B, c->lstride) + (size_t)c->B * sizeof(LevelHdr));
   int prod_cols = 0;
   for (int i = 0; i < b; ++i) prod_cols |= (c->h_pods[i].flags & PF_PROD_SCORE) ? 1 : 0;
   uint32_t len = c->n1 - c->n0;
@@ -917,13 +922,14 @@ int launch_batch(gs_ctx* c, int b, const int32_t* prev, const PlacementDev* prev
     HIP_TRY(c, launch_patch(c->mv, c->d_pods, b, c->pf, c->n0, c->n1, c->d_S, c->ld, prod_cols, c->d_aff, prev_out, prev,
                             prev_b, c->st));
   if (!c->window_k)   // node sampling selects over the rotation window, not the candidate levels
-    HIP_TRY(c, launch_cand(c->d_S, c->ld, len, c->n0, b, c->max_score, d_lists, d_hdrs, d_ext, c->st));
+    HIP_TRY(c, launch_cand(c->d_S, c->ld, len, c->n0, b, c->max_score, c->lstride, d_lists, d_hdrs, d_ext, c->st));
   HIP_TRY(c, hipEventRecord(c->ev[2], c->st));
   if (c->nranks > 1) {
     int rc = exchange(c, c->d_xchg_send, c->d_xchg_recv, c->xchg_bytes);
     if (rc) return rc;
     if (commit_spec_selected(c->window_k))
-      HIP_TRY(c, launch_merge_levels(c->d_xchg_recv, c->xchg_bytes, c->nranks, b, c->B, c->d_xmerged, c->st));
+      HIP_TRY(c, launch_merge_levels(c->d_xchg_recv, c->xchg_bytes, c->nranks, b, c->B, c->lstride, c->d_xmerged,
+                                     c->st));
   }
   CommitArgs a = commit_args(c, b);
   a.prev = prev;
@@ -1558,7 +1564,7 @@ int gs_create(const gs_config* cfg, gs_ctx** out) {
   if ((e = hipMalloc(&c->d_seq, 8 * c->B)) != hipSuccess) return bail("hipMalloc", e);
   if ((e = hipMalloc(&c->d_S, (size_t)c->B * c->ld * 2)) != hipSuccess) return bail("hipMalloc S", e);
   if ((e = hipMalloc(&c->d_aff, (size_t)c->B * c->ld)) != hipSuccess) return bail("hipMalloc aff", e);
-  size_t xb = xchg_block_bytes(c->B);
+  size_t xb = xchg_block_bytes(c->B, LCAP);
   if ((e = hipMalloc(&c->d_xchg_send, xb)) != hipSuccess) return bail("hipMalloc", e);
   c->xchg_bytes = xb;
   if ((e = hipMalloc(&c->d_out, sizeof(PlacementDev) * c->B)) != hipSuccess) return bail("hipMalloc", e);

@@ -13,6 +13,8 @@ constexpr int MAX_BATCH = 128;       // pods per device pass (commit-kernel LDS 
 constexpr int MAX_RANKS = 8;
 constexpr int MAXLEV = 8;            // score levels listed per (pod, shard)
 constexpr int LCAP = 2048;           // listed nodes per (pod, shard)
+constexpr int XCAP = 256;            // listed nodes per (pod, shard) when the lists are all-gathered for the speculative
+                                     // commit (the exchange block is 8x smaller; merged: <= MAX_RANKS x XCAP = LCAP)
 constexpr int PODS_PER_BLOCK = 16;   // eval kernel: pods per workgroup (grid.y = ceil(B / 16))
 constexpr int MAX_SCORE_LIMIT = 2047; // cand kernel keeps one histogram per wave in LDS
 constexpr int ROW_WORDS = NUM_I64_COLS + NUM_I32_COLS;  // staging row: i64 columns, then i32 widened
@@ -128,12 +130,13 @@ hipError_t launch_patch(const MirrorView& m, const PodVec* pods, int npods, cons
 hipError_t launch_eval_full(const MirrorView& m, const PodVec* pods, int npods, const Profile& pf, uint32_t N,
                             int16_t* scores, uint16_t* codes, int16_t* plugin, int prod_cols, hipStream_t st);
 void set_cand_stamps(uint64_t* p);   // diagnostics: cand_kernel phase cycles (nullptr: off)
-hipError_t launch_cand(const int16_t* S, uint32_t ld, uint32_t len, uint32_t n0, int npods, int max_score,
+// lcap: listed nodes per pod (<= LCAP), also the lists' stride
+hipError_t launch_cand(const int16_t* S, uint32_t ld, uint32_t len, uint32_t n0, int npods, int max_score, int lcap,
                        uint32_t* lists, LevelHdr* hdrs, LevelExt* ext, hipStream_t st);
 // several shards: per pod, the all-gathered rank blocks' levels merged into one block of the single-rank layout (the
 // speculative commit's input)
-hipError_t launch_merge_levels(const uint8_t* xin, size_t xblock, int nranks, int npods, int bmax, uint8_t* xout,
-                               hipStream_t st);
+hipError_t launch_merge_levels(const uint8_t* xin, size_t xblock, int nranks, int npods, int bmax, int lstride,
+                               uint8_t* xout, hipStream_t st);
 size_t commit_smem_bytes(int B);
 bool commit_spec_selected(uint32_t window_k);   // the speculative commit kernel runs (else pipelined / lockstep)
 hipError_t launch_commit(const CommitArgs& a, hipStream_t st);        // window_k > 0: lockstep kernel

@@ -157,7 +157,7 @@ __global__ void __launch_bounds__(256) eval_full_kernel(MirrorView m, const PodV
 // with small score ranges (more bandwidth per row when batches are short), else 4.
 template <int W>
 __global__ void __launch_bounds__(64 * W) cand_kernel(const int16_t* __restrict__ S, uint32_t ld, uint32_t len,
-                                                      uint32_t n0, int max_score, uint32_t* __restrict__ lists,
+                                                      uint32_t n0, int max_score, int lcap, uint32_t* __restrict__ lists,
                                                       LevelHdr* __restrict__ hdrs, LevelExt* __restrict__ ext,
                                                       uint64_t* stamps) {
   constexpr int CAND_THREADS = 64 * W;
@@ -241,7 +241,8 @@ __global__ void __launch_bounds__(64 * W) cand_kernel(const int16_t* __restrict_
     // levels from the top until the pod's position in the batch is covered: pod k can find at most k of
     // the listed nodes dirtied by earlier pods, so k+1 listed nodes always leave a clean one. Wave 0 walks the
     // bins 64 at a time from the top (lane l: bin hi - l); a level stops the list when the levels before it are
-    // LEVALL, or it would pass LCAP, or the nodes before it cover the target.
+    // LEVALL, or it would pass lcap (LCAP; XCAP when the lists are all-gathered), or the nodes before it cover the
+    // target.
     const uint32_t target = (uint32_t)k + 1;
     const uint64_t lt = (1ull << lane) - 1ull;
     int nlev = 0, next = -1;
@@ -254,7 +255,7 @@ __global__ void __launch_bounds__(64 * W) cand_kernel(const int16_t* __restrict_
       if (!nzm) continue;
       const uint32_t cb = cum + (uint32_t)(wave_incl_scan((int)c) - (int)c);
       const int nb = nlev + __popcll(nzm & lt);
-      const bool stop = nz && (nb == LEVALL || cb + c > (uint32_t)LCAP || cb >= target);
+      const bool stop = nz && (nb == LEVALL || cb + c > (uint32_t)lcap || cb >= target);
       const uint64_t sm = __ballot(stop);
       const int ls = sm ? __builtin_ctzll(sm) : 64;
       if (nz && lane < ls) {
@@ -292,7 +293,7 @@ __global__ void __launch_bounds__(64 * W) cand_kernel(const int16_t* __restrict_
   CT(3);
   // pass 2: order-preserving compaction of the listed levels (node order = (lane, element) order), level by level
   // over the levels present in each 512-node step
-  uint32_t* out = lists + (size_t)k * LCAP;
+  uint32_t* out = lists + (size_t)k * lcap;
   if (nlev > 0) {
     uint32_t run_l = lane < LEVALL ? s_woff[wave][lane] : 0;   // level `lane`'s next output position (this wave)
     // steps whose highest score is below the lowest listed level hold no listed node: not read again
@@ -374,7 +375,7 @@ __global__ void __launch_bounds__(64 * W) cand_kernel(const int16_t* __restrict_
 // ascending). The merged `next` is the highest score not kept (every shard's `next`, or the first dropped level).
 // Block k = pod k; thread e = (shard e / LEVALL, level e % LEVALL).
 __global__ void __launch_bounds__(256) merge_levels_kernel(const uint8_t* __restrict__ xin, size_t xblock, int R,
-                                                           int bmax, uint8_t* __restrict__ xout) {
+                                                           int bmax, int lstride, uint8_t* __restrict__ xout) {
   constexpr int NEMAX = MAX_RANKS * LEVALL;
   static_assert(NEMAX <= 256, "one thread per shard level");
   __shared__ int32_t e_score[NEMAX], e_count[NEMAX], e_rep[NEMAX];
@@ -382,14 +383,16 @@ __global__ void __launch_bounds__(256) merge_levels_kernel(const uint8_t* __rest
   __shared__ int32_t m_score[LEVALL], m_count[LEVALL];
   __shared__ int32_t s_nlev, s_drop;
   const int k = blockIdx.x, t = threadIdx.x, NE = R * LEVALL;
+  // rank blocks: lists at lstride entries per pod; the merged block has the single-rank layout (LCAP per pod)
+  const size_t ihoff = (size_t)bmax * lstride * 4, ixoff = ihoff + (size_t)bmax * sizeof(LevelHdr);
   const size_t hoff = (size_t)bmax * LCAP * 4, xoff = hoff + (size_t)bmax * sizeof(LevelHdr);
   if (t == 0) { s_nlev = 0; s_drop = -1; }
   if (t < LEVALL) { m_score[t] = -1; m_count[t] = 0; }
   int off = 0;   // this level's offset in its shard's list
   if (t < NE) {
     const int r = t / LEVALL, j = t % LEVALL;
-    const LevelHdr* h = reinterpret_cast<const LevelHdr*>(xin + r * xblock + hoff) + k;
-    const LevelExt* x = reinterpret_cast<const LevelExt*>(xin + r * xblock + xoff) + k;
+    const LevelHdr* h = reinterpret_cast<const LevelHdr*>(xin + r * xblock + ihoff) + k;
+    const LevelExt* x = reinterpret_cast<const LevelExt*>(xin + r * xblock + ixoff) + k;
     const int nl = x->nlev;
     int s = -1, c = 0;
     if (j < nl) {
@@ -438,7 +441,7 @@ __global__ void __launch_bounds__(256) merge_levels_kernel(const uint8_t* __rest
   for (int u = 0; u < NE; ++u) {
     const int pu = s_pos[u];
     if (pu < 0) continue;
-    const uint32_t* in = reinterpret_cast<const uint32_t*>(xin + (u / LEVALL) * xblock) + (size_t)k * LCAP + s_off[u];
+    const uint32_t* in = reinterpret_cast<const uint32_t*>(xin + (u / LEVALL) * xblock) + (size_t)k * lstride + s_off[u];
     const int cu = e_count[u];
     for (int x = t; x < cu; x += 256) out[pu + x] = in[x];
   }
@@ -460,11 +463,11 @@ __global__ void __launch_bounds__(256) merge_levels_kernel(const uint8_t* __rest
   }
 }
 
-hipError_t launch_merge_levels(const uint8_t* xin, size_t xblock, int nranks, int npods, int bmax, uint8_t* xout,
-                               hipStream_t st) {
+hipError_t launch_merge_levels(const uint8_t* xin, size_t xblock, int nranks, int npods, int bmax, int lstride,
+                               uint8_t* xout, hipStream_t st) {
   if (npods <= 0) return hipSuccess;
-  if (nranks < 2 || nranks > MAX_RANKS) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(merge_levels_kernel, dim3(npods), dim3(256), 0, st, xin, xblock, nranks, bmax, xout);
+  if (nranks < 2 || nranks > MAX_RANKS || lstride > LCAP || nranks * lstride > LCAP) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(merge_levels_kernel, dim3(npods), dim3(256), 0, st, xin, xblock, nranks, bmax, lstride, xout);
   return hipGetLastError();
 }
 
@@ -1397,14 +1400,15 @@ static bool cand_wide(int max_score) {
 static uint64_t* g_cand_stamps = nullptr;
 void set_cand_stamps(uint64_t* p) { g_cand_stamps = p; }
 
-hipError_t launch_cand(const int16_t* S, uint32_t ld, uint32_t len, uint32_t n0, int npods, int max_score,
+hipError_t launch_cand(const int16_t* S, uint32_t ld, uint32_t len, uint32_t n0, int npods, int max_score, int lcap,
                        uint32_t* lists, LevelHdr* hdrs, LevelExt* ext, hipStream_t st) {
+  if (lcap < 1 || lcap > LCAP) return hipErrorInvalidValue;
   if (cand_wide(max_score))
     hipLaunchKernelGGL(cand_kernel<16>, dim3(npods), dim3(1024), cand_smem_bytes(max_score, 16), st, S, ld, len, n0,
-                       max_score, lists, hdrs, ext, g_cand_stamps);
+                       max_score, lcap, lists, hdrs, ext, g_cand_stamps);
   else
     hipLaunchKernelGGL(cand_kernel<4>, dim3(npods), dim3(256), cand_smem_bytes(max_score, 4), st, S, ld, len, n0,
-                       max_score, lists, hdrs, ext, g_cand_stamps);
+                       max_score, lcap, lists, hdrs, ext, g_cand_stamps);
   return hipGetLastError();
 }
 
