@@ -570,6 +570,23 @@ int gs_decode_cpuset(const char* s, uint64_t out[GS_CPU_WORDS]);
  * ErrInvalidCPUAmplificationRatio path, nodenumaresource/plugin.go:345-347). Fills the raw_allocatable* and
  * custom_* fields of *node and (numa != NULL) the node amplification fields of *numa. */
 int gs_decode_node_annotations(const gs_kv* annotations, uint32_t n, gs_node* node, gs_node_numa* numa);
+/* Node reservation, annotation node.koordinator.sh/reservation (NodeReservation, apis/extension/node_reservation.go
+ * :37-68): the scheduler's node transformer TransformNodeWithNodeReservation (pkg/util/transformer/node_transformer.go
+ * :66-68) = TrimNodeAllocatableByNodeReservation (pkg/util/node.go:121-151) applied in place to node->allocatable and
+ * allowed_pod_number (the caller fills them with node.Status.Allocatable first): with applyPolicy "" or "Default" the
+ * reserved resources (GetNodeReservationResources, node.go:102-119: cpu = |reservedCPUs| when that is set) are
+ * subtracted, floored at 0 (quotav1.SubtractWithNonNegativeResult), batch-cpu / batch-memory kept. Returns 1 when the
+ * allocatable changed, 0 when not (absent or undecodable annotation, ReservedCPUsOnly, nothing reserved, an
+ * unparsable reservedCPUs: the reference leaves Allocatable as it is), GS_EUNSUPPORTED for a negative quantity. */
+int gs_node_reservation_trim(const gs_kv* annotations, uint32_t n, gs_node* node);
+/* GetReservedCPUs (node_reservation.go:70-90): the reservation's reservedCPUs as bit words and numReservedCPUs
+ * (ceil of a positive reserved cpu quantity, 0 when reservedCPUs is set). 1: reservedCPUs is set but unparsable. */
+int gs_node_reserved_cpus(const gs_kv* annotations, uint32_t n, uint64_t cpus[GS_CPU_WORDS], int32_t* num_reserved_cpus);
+/* TopologyOptions.ReservedCPUs (nodenumaresource/topology_options.go:90-146) from the NRT annotations: kubelet-managed
+ * pods' cpusets (node.koordinator.sh/pod-cpu-allocs) | kubelet reservedCPUs (kubelet.koordinator.sh/cpu-manager-policy)
+ * | the node reservation's reservedCPUs | an exclusive system-QoS cpuset (node.koordinator.sh/system-qos-resource); a
+ * part that does not decode adds nothing (the reference logs it). -> gs_node_numa.reserved_cpus. */
+int gs_decode_nrt_reserved_cpus(const gs_kv* nrt_annotations, uint32_t n, uint64_t out[GS_CPU_WORDS]);
 /* Node labels + the NRT's kubelet CPU manager policy JSON and topology-manager policy (either may be NULL):
  * GetNodeCPUBindPolicy (apis/extension/numa_aware.go:301-325), getNUMATopologyPolicy
  * (nodenumaresource/util.go:52-58), GetNUMAAllocateStrategy (util.go:35-41) -> *numa. */

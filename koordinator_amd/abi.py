@@ -323,6 +323,9 @@ SIGNATURES = {
     "gs_decode_quantity": (C.c_int, [C.c_char_p, C.POINTER(i64), C.POINTER(i64)]),
     "gs_decode_cpuset": (C.c_int, [C.c_char_p, C.POINTER(u64)]),
     "gs_decode_node_annotations": (C.c_int, [C.POINTER(GsKv), u32, C.POINTER(GsNode), C.POINTER(GsNodeNuma)]),
+    "gs_node_reservation_trim": (C.c_int, [C.POINTER(GsKv), u32, C.POINTER(GsNode)]),
+    "gs_node_reserved_cpus": (C.c_int, [C.POINTER(GsKv), u32, C.POINTER(u64), C.POINTER(C.c_int32)]),
+    "gs_decode_nrt_reserved_cpus": (C.c_int, [C.POINTER(GsKv), u32, C.POINTER(u64)]),
     "gs_decode_node_labels": (C.c_int, [C.POINTER(GsKv), u32, C.c_char_p, C.c_char_p, C.POINTER(GsNodeNuma)]),
     "gs_decode_resource_spec": (C.c_int, [C.c_char_p, C.POINTER(GsPod)]),
     "gs_decode_cpu_topology": (C.c_int, [C.c_char_p, C.POINTER(GsCpuTopology)]),

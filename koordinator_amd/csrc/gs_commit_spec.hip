@@ -15,12 +15,16 @@
 // every score exact. Verified decisions are exactly those of the sequential loop.
 //
 // Roles (8 waves):
-//   wave 0       decide (selectHost over levels + ready dirty rows, pending rows excluded) and verify, in order;
-//                rollback. Highest issue priority.
-//   wave 1       Reserve of decided pods in order: fetch a fresh winner row into its slot (prefetched one pod ahead),
-//                log the slot's state, apply assume + Reserve (NUMA split, cpuset), queue the row's re-scoring.
-//   waves 2..7   re-scoring jobs: a reserved row's new score for 64 later pods, one pod per lane (each wave builds
-//                the row's hint table itself).
+//   wave 0       decide (selectHost over levels + ready dirty rows, pending rows excluded), in order; performs the
+//                rollbacks the verifier requests. Highest issue priority: it sets the pipeline's pace.
+//   wave 1       verify the decisions in order (pending rows' exact re-scores below the decided maximum), the final
+//                Feasible counts, and the batch's end; a miss requests a rollback from wave 0.
+//   waves 2, 3   Reserve of decided pods, wave 2 the even pods and wave 3 the odd ones: fetch a fresh winner row into
+//                its slot (prefetched one pod of its parity ahead), log the slot's state, apply assume + Reserve (NUMA
+//                split, cpuset), queue the row's re-scoring on the wave's own job ring. A pod landing on a row an
+//                earlier pod landed on waits until that version is re-scored (so the other wave's Reserve is in).
+//   waves 4..7   re-scoring jobs from both rings: a reserved row's new score for 64 later pods, one pod per lane
+//                (each wave builds the row's hint table itself).
 // All hand-offs are LDS words (release / acquire); every wait is bounded: an expired wait (any wave) ends the kernel
 // with a site code in committed[3], nothing committed and nothing written back (the host fails the call with
 // GS_EDEVICE; HBM and host mirror both keep the batch-start state), so a bug cannot hang the GPU.
@@ -43,8 +47,9 @@ namespace gs {
 
 constexpr int SP_WAVES = 8, SP_THREADS = 64 * SP_WAVES;
 constexpr int SP_LAG = 16;       // decided - verified <= SP_LAG (undo log depth)
-constexpr int SP_TABLES = SP_WAVES - 2;   // one hint table per re-scoring wave
-constexpr int SP_JOBQ = 64;      // re-scoring job ring (<= 3 jobs per pod, <= SP_LAG + 2 pods in flight)
+constexpr int SP_RES0 = 2, SP_NRES = 2;   // Reserve waves 2, 3 (pod parity)
+constexpr int SP_RS0 = SP_RES0 + SP_NRES, SP_TABLES = SP_WAVES - SP_RS0;   // re-scoring waves, one hint table each
+constexpr int SP_JOBQ = 32;      // job ring per Reserve wave (<= 3 jobs per pod, <= SP_LAG / 2 + 2 pods in flight)
 constexpr int SP_HASH = 256;     // node -> slot (full-row resolution)
 constexpr int SP_FRESH = 1, SP_FITERR = 2, SP_SLOW = 4, SP_OFFSHARD = 8;   // DecRec.flags
 constexpr uint32_t SP_SPIN_LIMIT = 1u << 24;
@@ -72,7 +77,7 @@ struct Job {
 
 __device__ __forceinline__ void sp_sleep() { __builtin_amdgcn_s_sleep(2); }
 
-size_t spec_smem_bytes(int B) {   // the kernel's LDS carve-up, piece by piece with take()'s 16-B rounding
+size_t spec_smem_bytes(int B) {   // the kernel's LDS carve-up, piece by piece with take()'s 16-B rounding (same order)
   size_t b = 0;
   auto take = [&](size_t bytes) { b += (bytes + 15) & ~(size_t)15; };
   take((size_t)B * POD_STRIDE);                     // pods
@@ -83,10 +88,10 @@ size_t spec_smem_bytes(int B) {   // the kernel's LDS carve-up, piece by piece w
   take((size_t)B * sizeof(DecRec));
   take((size_t)SP_LAG * sizeof(UndoRec));
   take((size_t)SP_TABLES * sizeof(HintTable));
-  for (int i = 0; i < 6; ++i) take((size_t)B * 4);  // final_F, done_ver, has_row, rescored, jobs_left, jobs_all
+  for (int i = 0; i < 7; ++i) take((size_t)B * 4);  // final_F, done_ver, has_row, rescored, jobs_left, jobs_all, resv
   take((size_t)SP_HASH * 4);                        // hkey
   take((size_t)SP_HASH * 4);                        // hval
-  take((size_t)SP_JOBQ * sizeof(Job));
+  take((size_t)SP_NRES * SP_JOBQ * sizeof(Job));
   return b + 64;
 }
 
@@ -132,16 +137,23 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
   int32_t* rescored = reinterpret_cast<int32_t*>(take((size_t)B * 4));   // pod: Reserve + re-scoring complete
   int32_t* jobs_left = reinterpret_cast<int32_t*>(take((size_t)B * 4));  // pod: re-scoring jobs not done (-> done_ver)
   int32_t* jobs_all = reinterpret_cast<int32_t*>(take((size_t)B * 4));   // pod: every job not done (-> rescored)
+  int32_t* resv = reinterpret_cast<int32_t*>(take((size_t)B * 4));       // pod: its Reserve is applied (or FitError)
   int32_t* hkey = reinterpret_cast<int32_t*>(take((size_t)SP_HASH * 4));
   int32_t* hval = reinterpret_cast<int32_t*>(take((size_t)SP_HASH * 4));
-  Job* jobq = reinterpret_cast<Job*>(take((size_t)SP_JOBQ * sizeof(Job)));
-  __shared__ TopoDev s_topo;        // wave 1: topology of the last cpuset Reserve
+  Job* jobq = reinterpret_cast<Job*>(take((size_t)SP_NRES * SP_JOBQ * sizeof(Job)));   // [Reserve wave][ring]
+  __shared__ TopoDev s_topo[SP_NRES];     // per Reserve wave: topology of its last cpuset Reserve
   __shared__ HintTable s_ht0;       // wave 0: rollback re-scoring
-  __shared__ uint64_t s_cpuset[4];
-  __shared__ int32_t s_aff;
-  __shared__ int32_t s_decided, s_reserved, s_stop, s_parked, s_finish, s_cut_at, s_err;
-  __shared__ int32_t s_werr;        // a Reserve / re-scoring wave's bounded wait expired (its site code)
-  __shared__ int32_t s_jq_head, s_jq_tail;
+  __shared__ uint64_t s_cpuset[SP_NRES][4];
+  __shared__ int32_t s_aff[SP_NRES];
+  __shared__ int32_t s_decided, s_stop, s_parked, s_finish, s_cut_at, s_err;
+  __shared__ int32_t s_werr;        // a verify / Reserve / re-scoring wave's bounded wait expired (its site code)
+  __shared__ int32_t s_jq_head[SP_NRES], s_jq_tail[SP_NRES];
+  __shared__ int32_t s_verified;    // verifier: pods verified (wave 0 decides at most SP_LAG ahead of it)
+  __shared__ int32_t s_rb_req;      // verifier -> wave 0: v + 1 = roll back to pod v (0: none)
+  __shared__ int32_t s_rb_at;       // the last rollback's pod (where the parked waves resume)
+  __shared__ int32_t s_end_at;      // wave 0: decisions end before this pod (B: every pod)
+  __shared__ int32_t s_vend;        // verifier: the batch's committed count (-1: not yet), s_vcut: a host cut ends it
+  __shared__ int32_t s_vcut;
   __shared__ int32_t s_committed, s_hostcut, s_nd, s_endwhy;
   __shared__ uint64_t sseq[MAX_BATCH];
 
@@ -157,12 +169,15 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
     rescored[i] = 0;
     jobs_left[i] = 0;
     jobs_all[i] = 0;
+    resv[i] = 0;
   }
   for (int i = tid; i < SP_HASH; i += SP_THREADS) { hkey[i] = -1; hval[i] = -1; }
   for (int i = tid; i < B; i += SP_THREADS) tiebreak_records(a.seed, a.seq[i], a.tb + (size_t)i * TB_N);
   if (tid == 0) {
-    s_decided = 0; s_reserved = 0; s_stop = 0; s_parked = 0; s_finish = 0; s_cut_at = -1; s_err = 0; s_werr = 0;
-    s_jq_head = 0; s_jq_tail = 0; s_committed = 0; s_hostcut = 0; s_nd = 0;
+    s_decided = 0; s_stop = 0; s_parked = 0; s_finish = 0; s_cut_at = -1; s_err = 0; s_werr = 0;
+    for (int k = 0; k < SP_NRES; ++k) { s_jq_head[k] = 0; s_jq_tail[k] = 0; }
+    s_verified = 0; s_rb_req = 0; s_end_at = B; s_vend = -1; s_vcut = 0;
+    s_committed = 0; s_hostcut = 0; s_nd = 0;
   }
   __syncthreads();
 
@@ -170,11 +185,11 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
   auto st_rel = [](int32_t* p, int32_t v) { __atomic_store_n(p, v, __ATOMIC_RELEASE); };
 
   if (wv == 0) {
-    // =============================================== decide + verify ===============================================
+    // ==================================================== decide ====================================================
     __builtin_amdgcn_s_setprio(3);
     uint32_t dn0 = 0xffffffffu, dn1 = 0xffffffffu;   // slot s's node in lane s % 64 of dn0 / dn1
     int32_t pv0 = -1, pv1 = -1;                      // slot s's latest decided version (pod index)
-    int nd = 0, q = 0, v = 0, wm = 0, end_at = B, end_why = 0;
+    int nd = 0, q = 0, end_at = B, end_why = 0;
     int committed = 0;
     bool host_cut = false, err = false;
     int err_code = 0;   // which bounded wait expired (reported in committed[3])
@@ -237,130 +252,105 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
     uint32_t spins = 0;
     while (!err) {
       SPM(2);
-      // ------------------------------------------------ verification, in order
-      while (wm < q && ld_acq(&rescored[wm])) ++wm;
-      bool rolled = false;
-      while (v < q && v <= wm) {
-        const DecRec d = dec[v];
-        int mis = 0, fadd = 0;
-        if ((d.pend0 >> lane) & 1ull) {
-          const int sc = dsc[v * B + lane];
-          mis |= sc >= 0 && sc >= d.M;
-          fadd += sc >= 0;
+      // ------------------------------------------------ a rollback the verifier requested: to pod v
+      if (const int rq = ld_acq(&s_rb_req)) {
+        const int v = rq - 1;
+        // park the other waves, undo the Reserves of pods >= v (newest first: the two Reserve waves finish pods out of
+        // order, so by their flags), restore the slot versions
+        st_rel(&s_stop, 1);
+        spins = 0;
+        while (ld_acq(&s_parked) < SP_WAVES - 1) {
+          if (++spins > SP_SPIN_LIMIT) { err = true; err_code = 1; break; }
+          sp_sleep();
         }
-        if ((d.pend1 >> lane) & 1ull) {
-          const int sc = dsc[v * B + 64 + lane];
-          mis |= sc >= 0 && sc >= d.M;
-          fadd += sc >= 0;
+        if (err) break;
+        for (int qq = q - 1; qq >= v; --qq) {
+          if (!resv[qq] || (dec[qq].flags & SP_FITERR)) continue;
+          const UndoRec& u = undo[qq % SP_LAG];
+          const int sl = u.slot;
+          const uint64_t* src = reinterpret_cast<const uint64_t*>(&u.row);
+          uint64_t* dst = reinterpret_cast<uint64_t*>(&drows[sl]);
+          for (int i = lane; i < (int)(sizeof(Row) / 8); i += 64) dst[i] = src[i];
+          const uint64_t* s2 = reinterpret_cast<const uint64_t*>(&u.cs);
+          uint64_t* d2 = reinterpret_cast<uint64_t*>(&cst[sl]);
+          for (int i = lane; i < (int)(sizeof(CpuStateDev) / 8); i += 64) d2[i] = s2[i];
+          WAVE_FENCE();
         }
-        // unknown batch-start scores (several shards): known now (the creating pod is complete); the decision counted
-        // the node as clean and unlisted
-        if ((d.unk0 >> lane) & 1ull) {
-          const int so = dso[v * B + lane];
-          mis |= so >= 0 && so >= d.M;
-          fadd -= so >= 0;
+        // versions of the slots that survive, newest undone landing first
+        uint64_t redo0 = 0, redo1 = 0;   // surviving slots whose row was restored: re-score them for pods >= v
+        for (int qq = q - 1; qq >= v; --qq) {
+          const DecRec& e = dec[qq];
+          if ((e.flags & (SP_FITERR | SP_FRESH)) || e.slot >= dec[v].nd_before) continue;
+          const int sl = e.slot;
+          if (lane == (sl & 63)) { if (sl < 64) pv0 = e.prev_pend; else pv1 = e.prev_pend; }
+          if (resv[qq]) { if (sl < 64) redo0 |= 1ull << sl; else redo1 |= 1ull << (sl - 64); }
         }
-        if ((d.unk1 >> lane) & 1ull) {
-          const int so = dso[v * B + 64 + lane];
-          mis |= so >= 0 && so >= d.M;
-          fadd -= so >= 0;
+        const int ndv = dec[v].nd_before;
+        ps_slot = -1;   // a pending fresh slot is the last decision's: >= ndv, undone
+        if (lane >= ndv) { dn0 = 0xffffffffu; pv0 = -1; }
+        if (lane + 64 >= ndv) { dn1 = 0xffffffffu; pv1 = -1; }
+        for (int s = ndv + lane; s < nd; s += 64) { has_row[s] = 0; done_ver[s] = -1; }
+        nd = ndv;
+        for (int i = lane; i < SP_HASH; i += 64) { hkey[i] = -1; hval[i] = -1; }
+        WAVE_FENCE();
+        for (int s = 0; s < nd; ++s) {   // (readlane in uniform control flow: the source register is whole)
+          const uint32_t nn = s < 64 ? (uint32_t)__builtin_amdgcn_readlane((int)dn0, s)
+                                     : (uint32_t)__builtin_amdgcn_readlane((int)dn1, s - 64);
+          if (lane == 0) hash_insert(nn, s);
         }
-        if (__ballot(mis)) {
-          // ---------------- rollback to v: park the other waves, undo the Reserves of pods >= v, restore versions
-          st_rel(&s_stop, 1);
-          spins = 0;
-          while (ld_acq(&s_parked) < SP_WAVES - 1) {
-            if (++spins > SP_SPIN_LIMIT) { err = true; err_code = 1; break; }
-            sp_sleep();
-          }
-          if (err) break;
-          const int r = ld_acq(&s_reserved);
-          for (int qq = r - 1; qq >= v; --qq) {
-            if (dec[qq].flags & SP_FITERR) continue;
-            const UndoRec& u = undo[qq % SP_LAG];
-            const int sl = u.slot;
-            const uint64_t* src = reinterpret_cast<const uint64_t*>(&u.row);
-            uint64_t* dst = reinterpret_cast<uint64_t*>(&drows[sl]);
-            for (int i = lane; i < (int)(sizeof(Row) / 8); i += 64) dst[i] = src[i];
-            const uint64_t* s2 = reinterpret_cast<const uint64_t*>(&u.cs);
-            uint64_t* d2 = reinterpret_cast<uint64_t*>(&cst[sl]);
-            for (int i = lane; i < (int)(sizeof(CpuStateDev) / 8); i += 64) d2[i] = s2[i];
+        WAVE_FENCE();
+        // re-score the restored rows for pods v.. (their dsc entries after the undone landing are stale)
+        for (int pass = 0; pass < 2; ++pass) {
+          for (uint64_t bb = pass ? redo1 : redo0; bb; bb &= bb - 1) {
+            const int sl = (pass ? 64 : 0) + __builtin_ctzll(bb);
+            const Row rr = drows[sl];
+            if (numa_on && ((rr.nr.nflags >> NF_POLICY_SHIFT) & 3u)) hint_table_fill(s_ht0, rr.nr, zone_avail(rr.nr), lane);
+            WAVE_FENCE();
+            for (int q2 = v + lane; q2 < B; q2 += 64) dsc[q2 * B + sl] = (int16_t)row_score(rr, pods(q2), a.pf, m, &s_ht0);
             WAVE_FENCE();
           }
-          // versions of the slots that survive, newest undone landing first
-          uint64_t redo0 = 0, redo1 = 0;   // surviving slots whose row was restored: re-score them for pods >= v
-          for (int qq = q - 1; qq >= v; --qq) {
-            const DecRec& e = dec[qq];
-            if ((e.flags & (SP_FITERR | SP_FRESH)) || e.slot >= dec[v].nd_before) continue;
-            const int sl = e.slot;
-            if (lane == (sl & 63)) { if (sl < 64) pv0 = e.prev_pend; else pv1 = e.prev_pend; }
-            if (qq < r) { if (sl < 64) redo0 |= 1ull << sl; else redo1 |= 1ull << (sl - 64); }
-          }
-          const int ndv = dec[v].nd_before;
-          ps_slot = -1;   // a pending fresh slot is the last decision's: >= ndv, undone
-          if (lane >= ndv) { dn0 = 0xffffffffu; pv0 = -1; }
-          if (lane + 64 >= ndv) { dn1 = 0xffffffffu; pv1 = -1; }
-          for (int s = ndv + lane; s < nd; s += 64) { has_row[s] = 0; done_ver[s] = -1; }
-          nd = ndv;
-          for (int i = lane; i < SP_HASH; i += 64) { hkey[i] = -1; hval[i] = -1; }
-          WAVE_FENCE();
-          for (int s = 0; s < nd; ++s) {   // (readlane in uniform control flow: the source register is whole)
-            const uint32_t nn = s < 64 ? (uint32_t)__builtin_amdgcn_readlane((int)dn0, s)
-                                       : (uint32_t)__builtin_amdgcn_readlane((int)dn1, s - 64);
-            if (lane == 0) hash_insert(nn, s);
-          }
-          WAVE_FENCE();
-          // re-score the restored rows for pods v.. (their dsc entries after the undone landing are stale)
-          for (int pass = 0; pass < 2; ++pass) {
-            for (uint64_t bb = pass ? redo1 : redo0; bb; bb &= bb - 1) {
-              const int sl = (pass ? 64 : 0) + __builtin_ctzll(bb);
-              const Row rr = drows[sl];
-              if (numa_on && ((rr.nr.nflags >> NF_POLICY_SHIFT) & 3u)) hint_table_fill(s_ht0, rr.nr, zone_avail(rr.nr), lane);
-              WAVE_FENCE();
-              for (int q2 = v + lane; q2 < B; q2 += 64) dsc[q2 * B + sl] = (int16_t)row_score(rr, pods(q2), a.pf, m, &s_ht0);
-              WAVE_FENCE();
-            }
-          }
-          const int32_t myv0 = pv0, myv1 = pv1;
-          if (lane < nd) done_ver[lane] = myv0;
-          if (lane + 64 < nd) done_ver[lane + 64] = myv1;
-          for (int qq = v + lane; qq < B; qq += 64) { rescored[qq] = 0; jobs_left[qq] = 0; jobs_all[qq] = 0; }
-          if (lane == 0) {
-            s_jq_head = 0;
-            s_jq_tail = 0;
-            s_cut_at = -1;
-            s_reserved = v;
-            s_decided = v;
-            s_parked = 0;
-          }
-          WAVE_FENCE();
-          q = v;
-          wm = v;
-          end_at = B;
-          end_why = 0;
-          if (lane == 0) st_rel(&s_stop, 0);
-          n_hs = -1;   // reload pod v's header
-          load_hdr(v, n_hs, n_hc, n_nlev, n_feas, n_next, n_lh, n_tb);
-          rolled = true;
-          if (ST) st_acc[3] += 1;
-          SPM(4);
+        }
+        const int32_t myv0 = pv0, myv1 = pv1;
+        if (lane < nd) done_ver[lane] = myv0;
+        if (lane + 64 < nd) done_ver[lane + 64] = myv1;
+        for (int qq = v + lane; qq < B; qq += 64) {
+          rescored[qq] = 0;
+          jobs_left[qq] = 0;
+          jobs_all[qq] = 0;
+          resv[qq] = 0;
+        }
+        if (lane == 0) {
+          for (int k = 0; k < SP_NRES; ++k) { s_jq_head[k] = 0; s_jq_tail[k] = 0; }
+          s_cut_at = -1;
+          s_decided = v;
+          s_verified = v;
+          s_rb_at = v;
+          s_end_at = B;
+          s_parked = 0;
+          s_rb_req = 0;
+        }
+        WAVE_FENCE();
+        q = v;
+        end_at = B;
+        end_why = 0;
+        if (lane == 0) st_rel(&s_stop, 0);
+        n_hs = -1;   // reload pod v's header
+        load_hdr(v, n_hs, n_hc, n_nlev, n_feas, n_next, n_lh, n_tb);
+        if (ST) st_acc[3] += 1;
+        SPM(4);
+        continue;
+      }
+      {   // the verifier has verified every pod before the batch's end (or a host cut)
+        const int vend = ld_acq(&s_vend);
+        if (vend >= 0) {
+          committed = vend;
+          host_cut = ld_acq(&s_vcut) != 0;
           break;
         }
-        const int F = d.F + wave_sum(fadd);
-        if (lane == 0) final_F[v] = F;
-        ++v;
       }
-      {   // a Reserve that needs the host's cpuset selection ends the batch right after its pod
-        const int cut_at = ld_acq(&s_cut_at);
-        if (!rolled && cut_at >= 0 && v > cut_at) { committed = cut_at + 1; host_cut = true; }
-      }
-      if (err) break;
-      if (host_cut) break;
-      if (rolled) continue;
-      if (v == end_at && v == q) { committed = v; break; }
       SPM(1);
       // ------------------------------------------------ decide pod q
-      if (q >= end_at || q - v >= SP_LAG || ld_acq(&s_cut_at) >= 0) {
+      if (q >= end_at || q - ld_acq(&s_verified) >= SP_LAG || ld_acq(&s_cut_at) >= 0) {
         if (++spins > SP_SPIN_LIMIT) { err = true; err_code = 2; break; }
         if (const int we = ld_acq(&s_werr)) { err = true; err_code = we; break; }
         sp_sleep();
@@ -657,6 +647,7 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
       if (action == 0 && (int32_t)winner < 0) { action = 2; end_why = 4; }
       if (action == 2) {   // stop deciding here: the batch ends at p once everything before it is verified
         end_at = p;
+        if (lane == 0) st_rel(&s_end_at, p);
         continue;
       }
       // ---- record the decision, claim / version the winner's slot
@@ -713,10 +704,19 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
     }
     if (!err && committed > 0) {   // every committed pod's Reserve is in place before the waves stop
       uint32_t w = 0;
-      while (ld_acq(&s_reserved) < committed) {
+      for (;;) {
+        bool all = true;
+        for (int qq = lane; qq < committed; qq += 64) all = all && ld_acq(&resv[qq]) != 0;
+        if (!__ballot(!all)) break;
         if (++w > SP_SPIN_LIMIT) { err = true; err_code = 4; break; }
         if (const int we = ld_acq(&s_werr)) { err = true; err_code = we; break; }
         sp_sleep();
+      }
+      // the last pod's Reserve can cut after the verifier has passed it (nothing waits for its re-scoring)
+      const int ca = ld_acq(&s_cut_at);
+      if (!err && ca >= 0 && ca < committed) {
+        committed = ca + 1;
+        host_cut = true;
       }
     }
     if (ST) st_acc[12] = __builtin_amdgcn_s_memtime() - st_t0;
@@ -729,7 +729,93 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
       st_rel(&s_finish, 1);
     }
   } else if (wv == 1) {
+    // ==================================================== verify ====================================================
+    // pod v stands iff every row pending at its decision now scores below its maximum for it (and every row whose
+    // batch-start score was unknown scored below it at batch start); the rows it excluded that are feasible join its
+    // Feasible count. A miss asks wave 0 to roll back to v. Verifying v needs the re-scoring of every pod before it
+    // (rescored[]), which also means their Reserves (and batch-start jobs) are complete.
+    int v = 0, wm = 0;
+    uint32_t spins = 0;
+    for (;;) {
+      if (ld_acq(&s_stop)) {   // a rollback: park; wave 0 resets the verified count to the rollback's pod
+        if (lane == 0) __atomic_fetch_add(&s_parked, 1, __ATOMIC_ACQ_REL);
+        while (ld_acq(&s_stop) && !ld_acq(&s_finish)) sp_sleep();
+        v = ld_acq(&s_verified);
+        wm = v;
+        SPM(2);
+        continue;
+      }
+      if (ld_acq(&s_finish)) break;
+      if (ld_acq(&s_rb_req) || ld_acq(&s_vend) >= 0) { sp_sleep(); SPM(2); continue; }   // wave 0 acts on it
+      const int qd = ld_acq(&s_decided);
+      while (wm < qd && ld_acq(&rescored[wm])) ++wm;
+      bool moved = false, req = false;
+      while (v < qd && v <= wm) {
+        const DecRec d = dec[v];
+        int mis = 0, fadd = 0;
+        if ((d.pend0 >> lane) & 1ull) {
+          const int sc = dsc[v * B + lane];
+          mis |= sc >= 0 && sc >= d.M;
+          fadd += sc >= 0;
+        }
+        if ((d.pend1 >> lane) & 1ull) {
+          const int sc = dsc[v * B + 64 + lane];
+          mis |= sc >= 0 && sc >= d.M;
+          fadd += sc >= 0;
+        }
+        // unknown batch-start scores (several shards): known now (the creating pod is complete); the decision counted
+        // the node as clean and unlisted
+        if ((d.unk0 >> lane) & 1ull) {
+          const int so = dso[v * B + lane];
+          mis |= so >= 0 && so >= d.M;
+          fadd -= so >= 0;
+        }
+        if ((d.unk1 >> lane) & 1ull) {
+          const int so = dso[v * B + 64 + lane];
+          mis |= so >= 0 && so >= d.M;
+          fadd -= so >= 0;
+        }
+        if (__ballot(mis)) {
+          if (lane == 0) st_rel(&s_rb_req, v + 1);
+          req = true;
+          break;
+        }
+        const int F = d.F + wave_sum(fadd);
+        if (lane == 0) final_F[v] = F;
+        ++v;
+        moved = true;
+        if (lane == 0) st_rel(&s_verified, v);
+      }
+      if (req) { SPM(1); continue; }
+      if (moved) SPM(1);
+      {   // a Reserve that needs the host's cpuset selection ends the batch right after its pod
+        const int cut_at = ld_acq(&s_cut_at);
+        if (cut_at >= 0 && v > cut_at) {
+          if (lane == 0) { s_vcut = 1; st_rel(&s_vend, cut_at + 1); }
+          continue;
+        }
+      }
+      if (v == ld_acq(&s_end_at)) {   // every pod before the end of the decisions is verified
+        if (lane == 0) st_rel(&s_vend, v);
+        continue;
+      }
+      if (moved) { spins = 0; continue; }
+      if (++spins > SP_SPIN_LIMIT) {
+        if (lane == 0) __atomic_store_n(&s_werr, 8, __ATOMIC_RELEASE);
+        break;
+      }
+      sp_sleep();
+      SPM(2);
+    }
+  } else if (wv < SP_RS0) {
     // =================================================== Reserve ===================================================
+    const int wr = wv - SP_RES0;   // this wave's pods: q % SP_NRES == wr
+    TopoDev& s_topo_w = s_topo[wr];
+    uint64_t* s_cpuset_w = s_cpuset[wr];
+    int32_t& s_aff_w = s_aff[wr];
+    Job* jq = jobq + wr * SP_JOBQ;
+    int32_t& jq_tail = s_jq_tail[wr];
+    int32_t& jq_head = s_jq_head[wr];
     int topo_id = -1;
     int f_kind = 0, f_region = 0, f_off = 0, f_size = 8;
     const void* f_src = nullptr;
@@ -760,13 +846,13 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
       else if (f_kind == 4) vv = (int64_t)node;
       return vv;
     };
-    int q = 0, pf_q = -1;   // pf_q: the pod whose fresh winner row is in flight in pf_v
+    int q = wr, pf_q = -1;   // pf_q: the pod whose fresh winner row is in flight in pf_v
     int64_t pf_v = 0;
     uint32_t spins = 0;
-    // room for n more jobs in the ring (this wave is its only producer); false: a rollback or the end intervened
+    // room for n more jobs in this wave's ring (it is the only producer); false: a rollback or the end intervened
     auto room = [&](int n) -> bool {
       uint32_t w = 0;
-      while (s_jq_tail - ld_acq(&s_jq_head) + n > SP_JOBQ) {
+      while (jq_tail - ld_acq(&jq_head) + n > SP_JOBQ) {
         if (ld_acq(&s_stop) || ld_acq(&s_finish)) return false;
         if (++w > SP_SPIN_LIMIT) {
           if (lane == 0) __atomic_store_n(&s_werr, 7, __ATOMIC_RELEASE);
@@ -777,16 +863,18 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
       return true;
     };
     for (;;) {
-      if (ld_acq(&s_stop)) {   // rollback: park until wave 0 has repaired the state, then resume at s_reserved
+      if (ld_acq(&s_stop)) {   // rollback: park until wave 0 has repaired the state, resume at its pod of our parity
         if (lane == 0) __atomic_fetch_add(&s_parked, 1, __ATOMIC_ACQ_REL);
         while (ld_acq(&s_stop) && !ld_acq(&s_finish)) sp_sleep();
-        q = ld_acq(&s_reserved);
+        const int v = ld_acq(&s_rb_at);
+        q = v + ((wr - v) & (SP_NRES - 1));
         topo_id = -1;
         pf_q = -1;
         continue;
       }
       if (ld_acq(&s_finish)) break;
-      if (q >= ld_acq(&s_decided) || ld_acq(&s_cut_at) >= 0) {
+      const int cut_now = ld_acq(&s_cut_at);
+      if (q >= ld_acq(&s_decided) || (cut_now >= 0 && q > cut_now)) {
         if (++spins > SP_SPIN_LIMIT) {
           if (lane == 0) __atomic_store_n(&s_werr, 5, __ATOMIC_RELEASE);
           break;
@@ -803,11 +891,11 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
       if (d.flags & SP_FITERR) {
         if (lane == 0) {
           a.out[q] = PlacementDev{-1, (uint32_t)d.F, 0, 0, 0, 0, 0, {0, 0, 0, 0}, {0, 0, 0, 0}};
-          rescored[q] = 1;
-          __atomic_store_n(&s_reserved, q + 1, __ATOMIC_RELEASE);
+          __atomic_store_n(&rescored[q], 1, __ATOMIC_RELEASE);
+          __atomic_store_n(&resv[q], 1, __ATOMIC_RELEASE);
         }
         WAVE_FENCE();
-        ++q;
+        q += SP_NRES;
         continue;
       }
       const int slot = d.slot;
@@ -816,14 +904,15 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
       if (fresh) {   // the row: one load per lane (issued one pod ahead when pod q was already decided), then LDS
         const int64_t vv = pf_q == q ? pf_v : fetch(q, winner);
         pf_q = -1;
-        if (q + 1 < ld_acq(&s_decided)) {   // prefetch the next pod's fresh winner row
-          const DecRec& dn = dec[q + 1];
-          if ((dn.flags & (SP_FRESH | SP_FITERR)) == SP_FRESH) { pf_v = fetch(q + 1, (uint32_t)dn.winner); pf_q = q + 1; }
+        const int qn = q + SP_NRES;   // this wave's next pod
+        if (qn < ld_acq(&s_decided)) {   // prefetch its fresh winner row
+          const DecRec& dn = dec[qn];
+          if ((dn.flags & (SP_FRESH | SP_FITERR)) == SP_FRESH) { pf_v = fetch(qn, (uint32_t)dn.winner); pf_q = qn; }
         }
         if (f_kind) {
           unsigned char* dst = f_region == 0 ? reinterpret_cast<unsigned char*>(&drows[slot])
                              : f_region == 1 ? reinterpret_cast<unsigned char*>(&cst[slot])
-                                             : reinterpret_cast<unsigned char*>(&s_aff);
+                                             : reinterpret_cast<unsigned char*>(&s_aff_w);
           if (f_size == 8) *reinterpret_cast<int64_t*>(dst + f_off) = vv;
           else *reinterpret_cast<int32_t*>(dst + f_off) = (int32_t)vv;
         }
@@ -848,13 +937,13 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
         if (lane == 0) {
           jobs_left[q] = njobs;
           jobs_all[q] = njobs + 1;
-          const int t = s_jq_tail;
-          jobq[t % SP_JOBQ] = Job{slot, q, -1, (int32_t)winner};
-          __atomic_store_n(&s_jq_tail, t + 1, __ATOMIC_RELEASE);
+          const int t = jq_tail;
+          jq[t % SP_JOBQ] = Job{slot, q, -1, (int32_t)winner};
+          __atomic_store_n(&jq_tail, t + 1, __ATOMIC_RELEASE);
         }
         WAVE_FENCE();
       }
-      if (lane == 0 && (!fresh || !numa_on)) s_aff = -1;
+      if (lane == 0 && (!fresh || !numa_on)) s_aff_w = -1;
       WAVE_FENCE();
       {   // undo log: the slot's state before this Reserve
         UndoRec& u = undo[q % SP_LAG];
@@ -875,7 +964,7 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
         if (tp >= 0 && tp != topo_id && !(pk.numa & (PN_SKIP | PN_PREFAIL)) &&
             ((pk.numa & PN_BIND) || ((nfl >> NF_BIND_SHIFT) & 3u))) {
           const uint64_t* src = reinterpret_cast<const uint64_t*>(a.topos + tp);
-          uint64_t* dst = reinterpret_cast<uint64_t*>(&s_topo);
+          uint64_t* dst = reinterpret_cast<uint64_t*>(&s_topo_w);
           for (int i = lane; i < (int)(sizeof(TopoDev) / 8); i += 64) dst[i] = src[i];
           topo_id = tp;
         }
@@ -890,7 +979,7 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
             numa_on && !(pk.numa & (PN_SKIP | PN_PREFAIL)) && (maybe_rb || ((nf >> NF_POLICY_SHIFT) & 3u));
         NumaOut no{};
         if (numa_reserve)
-          no = numa_eval<true, false, true>(dr.nr, pk, a.pf, SlotsLds{dr, m}, a.pf.enabled & 0x10u, false, s_aff);
+          no = numa_eval<true, false, true>(dr.nr, pk, a.pf, SlotsLds{dr, m}, a.pf.enabled & 0x10u, false, s_aff_w);
         SPM(16);   // topology staging + the Reserve's NUMA Allocate (numa_eval)
         if (lane == 0) {
           PlacementDev pl{(int32_t)winner, (uint32_t)d.F, (int64_t)d.M, (uint32_t)d.T, (d.flags & SP_SLOW) ? 1u : 0u,
@@ -919,12 +1008,12 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
               if (rb) {
                 CpuStateDev& cs = cst[slot];
                 if (cs.topo >= 0 && cs.topo == topo_id) {
-                  if (cpuset_reserve((const GS_LDS TopoDev*)&s_topo, (GS_LDS CpuStateDev*)&cs, pk, nf, no.zkeys,
+                  if (cpuset_reserve((const GS_LDS TopoDev*)&s_topo_w, (GS_LDS CpuStateDev*)&cs, pk, nf, no.zkeys,
                                      no.zcpu[0], no.zcpu[1], no.zcpu[2], no.zcpu[3], (GS_LDS NumaRow*)&dr_.nr,
-                                     (GS_LDS uint64_t*)s_cpuset)) {
+                                     (GS_LDS uint64_t*)s_cpuset_w)) {
                     pl.flags |= PL_DEVICE_CPUSET;
 #pragma unroll
-                    for (int j = 0; j < 4; ++j) pl.cpuset[j] = s_cpuset[j];
+                    for (int j = 0; j < 4; ++j) pl.cpuset[j] = s_cpuset_w[j];
                   } else {
                     pl.flags |= PL_RESERVE_FAILED;
                   }
@@ -950,15 +1039,27 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
       cut = __builtin_amdgcn_readlane(cut, 0);
       WAVE_FENCE();
       SPM(17);   // lane 0: placement record, zone split, cpuset_reserve, assume deltas
-      if (pf_q != q + 1 && q + 1 < ld_acq(&s_decided)) {   // the next pod was decided meanwhile: prefetch its row now
-        const DecRec& dn = dec[q + 1];
-        if ((dn.flags & (SP_FRESH | SP_FITERR)) == SP_FRESH) { pf_v = fetch(q + 1, (uint32_t)dn.winner); pf_q = q + 1; }
+      if (pf_q != q + SP_NRES && q + SP_NRES < ld_acq(&s_decided)) {   // our next pod was decided meanwhile: its row
+        const DecRec& dn = dec[q + SP_NRES];
+        if ((dn.flags & (SP_FRESH | SP_FITERR)) == SP_FRESH) {
+          pf_v = fetch(q + SP_NRES, (uint32_t)dn.winner);
+          pf_q = q + SP_NRES;
+        }
       }
+      // a pod whose cpuset the host must select ends the batch after it: published before its re-scoring can complete
+      // (the verifier passes a pod only once the pod before it is re-scored); the first such pod in queue order wins
+      if (lane == 0 && cut) {
+        int cur = ld_acq(&s_cut_at);
+        while ((cur < 0 || q < cur) &&
+               !__atomic_compare_exchange_n(&s_cut_at, &cur, q, false, __ATOMIC_ACQ_REL, __ATOMIC_ACQUIRE)) {
+        }
+      }
+      WAVE_FENCE();
       // ---- the row's re-scoring: hint table of its new state, jobs of 64 later pods
       if (njobs == 0) {
         if (lane == 0) {
-          done_ver[slot] = q;
-          rescored[q] = 1;
+          __atomic_store_n(&done_ver[slot], q, __ATOMIC_RELEASE);
+          __atomic_store_n(&rescored[q], 1, __ATOMIC_RELEASE);
         }
       } else {
         if (lane == 0) {
@@ -966,23 +1067,21 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
             jobs_left[q] = njobs;
             jobs_all[q] = njobs;
           }
-          int t = s_jq_tail;
-          for (int j = 0; j < njobs; ++j, ++t) jobq[t % SP_JOBQ] = Job{slot, q, j, 0};
-          __atomic_store_n(&s_jq_tail, t, __ATOMIC_RELEASE);
+          int t = jq_tail;
+          for (int j = 0; j < njobs; ++j, ++t) jq[t % SP_JOBQ] = Job{slot, q, j, 0};
+          __atomic_store_n(&jq_tail, t, __ATOMIC_RELEASE);
         }
       }
       WAVE_FENCE();
-      if (lane == 0) {
-        if (cut) __atomic_store_n(&s_cut_at, q, __ATOMIC_RELEASE);
-        __atomic_store_n(&s_reserved, q + 1, __ATOMIC_RELEASE);
-      }
+      if (lane == 0) __atomic_store_n(&resv[q], 1, __ATOMIC_RELEASE);
       WAVE_FENCE();
-      ++q;
+      q += SP_NRES;
       SPM(5);
     }
   } else {
     // ============================================== re-scoring jobs ==============================================
     uint32_t spins = 0;
+    int ring = wv % SP_NRES;
     for (;;) {
       if (ld_acq(&s_stop)) {
         if (lane == 0) __atomic_fetch_add(&s_parked, 1, __ATOMIC_ACQ_REL);
@@ -990,15 +1089,24 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
         continue;
       }
       if (ld_acq(&s_finish)) break;
+      // a job from either Reserve wave's ring (the preferred one alternating). The entry is read before the head moves
+      // past it: until then its producer cannot reuse the slot
       int h = -1;
+      Job jl{0, 0, 0, 0};
       if (lane == 0) {
-        const int hd = __atomic_load_n(&s_jq_head, __ATOMIC_ACQUIRE);
-        if (hd < __atomic_load_n(&s_jq_tail, __ATOMIC_ACQUIRE)) {
-          int expect = hd;
-          if (__atomic_compare_exchange_n(&s_jq_head, &expect, hd + 1, false, __ATOMIC_ACQ_REL, __ATOMIC_ACQUIRE)) h = hd;
+        for (int i = 0; i < SP_NRES && h < 0; ++i) {
+          const int k = (ring + i) % SP_NRES;
+          const int hd = __atomic_load_n(&s_jq_head[k], __ATOMIC_ACQUIRE);
+          if (hd < __atomic_load_n(&s_jq_tail[k], __ATOMIC_ACQUIRE)) {
+            jl = jobq[k * SP_JOBQ + hd % SP_JOBQ];
+            int expect = hd;
+            if (__atomic_compare_exchange_n(&s_jq_head[k], &expect, hd + 1, false, __ATOMIC_ACQ_REL, __ATOMIC_ACQUIRE))
+              h = k;
+          }
         }
       }
       h = __builtin_amdgcn_readfirstlane(h);
+      ring = (ring + 1) % SP_NRES;
       if (h < 0) {
         if (++spins > SP_SPIN_LIMIT) {
           if (lane == 0) __atomic_store_n(&s_werr, 6, __ATOMIC_RELEASE);
@@ -1010,8 +1118,9 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
       }
       spins = 0;
       SPM(8);
-      const Job jb = jobq[h % SP_JOBQ];
-      HintTable& tab = tables[wv - 2];
+      const Job jb{__builtin_amdgcn_readfirstlane(jl.slot), __builtin_amdgcn_readfirstlane(jl.q),
+                   __builtin_amdgcn_readfirstlane(jl.range), __builtin_amdgcn_readfirstlane(jl.tbl)};
+      HintTable& tab = tables[wv - SP_RS0];
       if (jb.range < 0) {
         // batch-start job (several shards): another shard's fresh row as it stood at batch start — the HBM mirror,
         // written back only at the kernel's end — evaluated for every later pod: its dso entries
@@ -1043,6 +1152,23 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
       }
       WAVE_FENCE();
       SPM(7);
+    }
+  }
+  __syncthreads();
+  // ---- a host cut ends the batch after its pod, but the other Reserve wave may have reserved a later decided pod
+  // meanwhile: those Reserves are undone (newest first) before the write-back
+  if (wv == 0 && s_hostcut && !s_err) {
+    for (int qq = s_decided - 1; qq >= s_committed; --qq) {
+      if (!resv[qq] || (dec[qq].flags & SP_FITERR)) continue;
+      const UndoRec& u = undo[qq % SP_LAG];
+      const int sl = u.slot;
+      const uint64_t* src = reinterpret_cast<const uint64_t*>(&u.row);
+      uint64_t* dst = reinterpret_cast<uint64_t*>(&drows[sl]);
+      for (int i = lane; i < (int)(sizeof(Row) / 8); i += 64) dst[i] = src[i];
+      const uint64_t* s2 = reinterpret_cast<const uint64_t*>(&u.cs);
+      uint64_t* d2 = reinterpret_cast<uint64_t*>(&cst[sl]);
+      for (int i = lane; i < (int)(sizeof(CpuStateDev) / 8); i += 64) d2[i] = s2[i];
+      WAVE_FENCE();
     }
   }
   __syncthreads();

@@ -1634,9 +1634,10 @@ int gs_destroy(gs_ctx* c) {
       static const char* kind = getenv("GS_COMMIT_KERNEL");
       if (!(kind && kind[0] == 'p') && !c->window_k) {   // speculative commit kernel
         const double np = c->stats_all_pods ? (double)c->stats_all_pods : 1.0;
-        fprintf(stderr, "gpuscore spec commit, cycles per committed pod (%llu pods): decide %.0f verify %.0f wave0-wait %.0f "
-                "rollback %.0f (%llu rollbacks) | Reserve busy %.0f wait %.0f | re-scoring busy %.0f wait %.0f (6 waves) | "
-                "decisions %llu, full-row %llu (%.0f cycles each; M<0 %llu, M>=0 %llu) | wave 0 total %.0f\n",
+        fprintf(stderr, "gpuscore spec commit, cycles per committed pod (%llu pods): decide %.0f verify %.0f wave0+verifier-wait "
+                "%.0f rollback %.0f (%llu rollbacks) | Reserve busy %.0f wait %.0f (2 waves, summed) | re-scoring busy %.0f "
+                "wait %.0f (4 waves, summed) | decisions %llu, full-row %llu (%.0f cycles each; M<0 %llu, M>=0 %llu) | wave 0 "
+                "total %.0f\n",
                 (unsigned long long)c->stats_all_pods, st[0] / np, st[1] / np, st[2] / np, st[4] / np,
                 (unsigned long long)st[3], st[5] / np, st[6] / np, st[7] / np, st[8] / np, (unsigned long long)st[9],
                 (unsigned long long)st[10], st[10] ? (double)st[11] / st[10] : 0.0, (unsigned long long)st[13],

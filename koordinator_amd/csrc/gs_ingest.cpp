@@ -392,6 +392,52 @@ int agg_type(const std::string& s, int32_t* out) {
   return GS_OK;
 }
 
+
+// NodeReservation (apis/extension/node_reservation.go:37-44) as encoding/json.Unmarshal fills it from the annotation
+// node.koordinator.sh/reservation (GetNodeReservation, :59-68): present = the annotation is non-empty and decodes.
+struct NodeRsv {
+  bool present = false;
+  std::vector<std::pair<std::string, const JVal*>> resources;   // ResourceList entries (Quantity JSON)
+  std::string reserved_cpus, apply_policy;
+  JVal doc;
+};
+bool node_reservation(const gs_kv* kv, uint32_t n, NodeRsv* r) {
+  const char* s = find_kv(kv, n, "node.koordinator.sh/reservation");
+  if (!s || !*s) return true;                       // absent / "": nil reservation
+  if (!parse_json(s, &r->doc)) return false;
+  if (r->doc.kind == JVal::NUL) { r->present = true; return true; }   // "null": an empty reservation
+  if (r->doc.kind != JVal::OBJ) return false;
+  if (const JVal* res = r->doc.get("resources")) {
+    if (res->kind == JVal::OBJ) {
+      for (const auto& e : res->obj) {
+        int64_t x;
+        const int rc = quantity_json(e.second, e.first == "cpu" ? 3 : 0, &x);
+        if (rc == GS_EINVAL) return false;          // Quantity.UnmarshalJSON error
+        r->resources.emplace_back(e.first, &e.second);
+      }
+    } else if (res->kind != JVal::NUL) {
+      return false;
+    }
+  }
+  for (const char* f : {"reservedCPUs", "applyPolicy"}) {
+    const JVal* v = r->doc.get(f);
+    if (!v || v->kind == JVal::NUL) continue;
+    if (v->kind != JVal::STR) return false;
+    (f[0] == 'r' ? r->reserved_cpus : r->apply_policy) = v->text;
+  }
+  r->present = true;
+  return true;
+}
+
+int res_slot(const std::string& name) {   // gs_resource slot of a resource name, -1: none in gs_node
+  static const char* names[7] = {"cpu", "memory", "ephemeral-storage", "kubernetes.io/batch-cpu",
+                                          "kubernetes.io/batch-memory", "kubernetes.io/mid-cpu",
+                                          "kubernetes.io/mid-memory"};
+  for (int i = 0; i < 7; ++i)
+    if (name == names[i]) return i;
+  return -1;
+}
+
 }  // namespace
 
 extern "C" {
@@ -542,6 +588,126 @@ int gs_decode_node_annotations(const gs_kv* kv, uint32_t n, gs_node* node, gs_no
       else numa->node_amplification_invalid = 1;
     }
   }
+  return GS_OK;
+}
+
+int gs_node_reservation_trim(const gs_kv* kv, uint32_t n, gs_node* node) {
+  if ((n && !kv) || !node) return GS_EINVAL;
+  NodeRsv r;
+  if (!node_reservation(kv, n, &r) || !r.present) return 0;                   // GetNodeReservation error / nil
+  if (!(r.apply_policy.empty() || r.apply_policy == "Default")) return 0;     // ReservedCPUsOnly: no trim
+  // GetNodeReservationResources (pkg/util/node.go:102-119): the resources, cpu replaced by |reservedCPUs|
+  int64_t red[GS_NUM_RES] = {0, 0, 0, 0, 0, 0, 0}, pods = 0;
+  bool nonzero = false;
+  for (const auto& e : r.resources) {
+    const int sl = res_slot(e.first);
+    int64_t x = 0;
+    const int rc = quantity_json(*e.second, sl == GS_RES_CPU ? 3 : 0, &x);
+    if (rc) return rc;   // a negative reserved quantity (it would raise allocatable): refused, see quantity_scaled
+    nonzero |= x != 0;
+    if (sl >= 0) red[sl] = x;
+    else if (e.first == "pods") pods = x;
+  }
+  if (!r.reserved_cpus.empty()) {
+    uint64_t w[GS_CPU_WORDS];
+    if (gs_decode_cpuset(r.reserved_cpus.c_str(), w) != GS_OK) return 0;      // cpuset.Parse error: no trim
+    int cnt = 0;
+    for (int i = 0; i < GS_CPU_WORDS; ++i) cnt += __builtin_popcountll(w[i]);
+    // resourceList[cpu] = MustParse(strconv.Itoa(cpus.Size())); the map now always holds cpu
+    bool had_nonzero_other = false;
+    for (const auto& e : r.resources) {
+      if (e.first == "cpu") continue;
+      int64_t x = 0;
+      (void)quantity_json(*e.second, 0, &x);
+      had_nonzero_other |= x != 0;
+    }
+    red[GS_RES_CPU] = (int64_t)cnt * 1000;
+    nonzero = had_nonzero_other || cnt != 0;
+  }
+  if (!nonzero) return 0;                                                     // quotav1.IsZero
+  // SubtractWithNonNegativeResult, then batch-cpu / batch-memory restored (node.go:140-148)
+  int changed = 0;
+  for (int sl = 0; sl < 7; ++sl) {   // (slot 7 is reserved)
+    if (sl == GS_RES_BATCH_CPU || sl == GS_RES_BATCH_MEMORY) continue;
+    const int64_t t = node->allocatable[sl] - red[sl] > 0 ? node->allocatable[sl] - red[sl] : 0;
+    changed |= t != node->allocatable[sl];
+    node->allocatable[sl] = t;
+  }
+  const int64_t tp = node->allowed_pod_number - pods > 0 ? node->allowed_pod_number - pods : 0;
+  changed |= tp != node->allowed_pod_number;
+  node->allowed_pod_number = tp;
+  return changed;
+}
+
+int gs_node_reserved_cpus(const gs_kv* kv, uint32_t n, uint64_t cpus[GS_CPU_WORDS], int32_t* num_reserved_cpus) {
+  if ((n && !kv) || !cpus) return GS_EINVAL;
+  for (int i = 0; i < GS_CPU_WORDS; ++i) cpus[i] = 0;
+  if (num_reserved_cpus) *num_reserved_cpus = 0;
+  NodeRsv r;
+  if (!node_reservation(kv, n, &r) || !r.present) return GS_OK;
+  int32_t num = 0;
+  for (const auto& e : r.resources) {
+    if (e.first != "cpu") continue;
+    int64_t milli = 0;
+    if (quantity_json(*e.second, 3, &milli) == GS_OK && milli > 0) num = (int32_t)((milli + 999) / 1000);
+  }
+  if (!r.reserved_cpus.empty()) num = 0;
+  if (num_reserved_cpus) *num_reserved_cpus = num;
+  if (r.reserved_cpus.empty()) return GS_OK;
+  return gs_decode_cpuset(r.reserved_cpus.c_str(), cpus) == GS_OK ? GS_OK : 1;   // 1: unparsable (no CPUs)
+}
+
+int gs_decode_nrt_reserved_cpus(const gs_kv* kv, uint32_t n, uint64_t out[GS_CPU_WORDS]) {
+  if ((n && !kv) || !out) return GS_EINVAL;
+  uint64_t w[GS_CPU_WORDS] = {0, 0, 0, 0};
+  auto unite = [&](const std::string& list) {   // cpuset.Parse; an error is logged by the reference: nothing added
+    uint64_t c[GS_CPU_WORDS];
+    if (gs_decode_cpuset(list.c_str(), c) != GS_OK) return;
+    for (int i = 0; i < GS_CPU_WORDS; ++i) w[i] |= c[i];
+  };
+  // getPodAllocsCPUSet (topology_options.go:155-171) over GetPodCPUAllocs (numa_aware.go:262-273)
+  if (const char* s = find_kv(kv, n, "node.koordinator.sh/pod-cpu-allocs")) {
+    JVal v;
+    if (parse_json(s, &v) && v.kind == JVal::ARR) {
+      bool good = true;
+      for (const auto& a : v.arr) good = good && (a.kind == JVal::OBJ || a.kind == JVal::NUL);
+      for (size_t i = 0; good && i < v.arr.size(); ++i) {
+        const JVal& a = v.arr[i];
+        if (a.kind != JVal::OBJ) continue;
+        const JVal* mk = a.get("managedByKubelet");
+        const JVal* uid = a.get("uid");
+        const JVal* cs = a.get("cpuset");
+        const bool managed = mk && mk->kind == JVal::BOOL && mk->b;
+        if (!managed || !uid || uid->kind != JVal::STR || uid->text.empty() || !cs || cs->kind != JVal::STR ||
+            cs->text.empty())
+          continue;
+        unite(cs->text);
+      }
+    }
+  }
+  // kubelet's reserved CPUs (GetKubeletCPUManagerPolicy, numa_aware.go:301-312)
+  if (const char* s = find_kv(kv, n, "kubelet.koordinator.sh/cpu-manager-policy")) {
+    JVal v;
+    if (parse_json(s, &v) && v.kind == JVal::OBJ)
+      if (const JVal* rc = v.get("reservedCPUs"))
+        if (rc->kind == JVal::STR) unite(rc->text);
+  }
+  // the node reservation's reservedCPUs (GetReservedCPUs, node_reservation.go:70-90)
+  {
+    NodeRsv r;
+    if (node_reservation(kv, n, &r) && r.present && !r.reserved_cpus.empty()) unite(r.reserved_cpus);
+  }
+  // an exclusive system-QoS cpuset (GetSystemQOSResource, system_qos.go:35-53)
+  if (const char* s = find_kv(kv, n, "node.koordinator.sh/system-qos-resource")) {
+    JVal v;
+    if (parse_json(s, &v) && v.kind == JVal::OBJ) {
+      const JVal* ex = v.get("cpusetExclusive");
+      const bool exclusive = !ex || ex->kind == JVal::NUL || (ex->kind == JVal::BOOL && ex->b);
+      const JVal* cs = v.get("cpuset");
+      if (exclusive && cs && cs->kind == JVal::STR) unite(cs->text);
+    }
+  }
+  memcpy(out, w, sizeof w);
   return GS_OK;
 }
 

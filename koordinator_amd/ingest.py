@@ -55,6 +55,34 @@ def node_annotations(annotations: dict, node=None, numa=None):
     return node, numa
 
 
+def node_reservation_trim(annotations: dict, node) -> bool:
+    """TransformNodeWithNodeReservation on node.allocatable / allowed_pod_number in place; True when trimmed"""
+    arr, n = _kv(annotations)
+    rc = abi.load().gs_node_reservation_trim(arr, n, C.byref(node))
+    if rc < 0:
+        raise DecodeError("node reservation", rc)
+    return rc == 1
+
+
+def node_reserved_cpus(annotations: dict) -> tuple[list[int], int, bool]:
+    """GetReservedCPUs -> (reserved cpu ids, numReservedCPUs, reservedCPUs parsed)"""
+    w = (C.c_uint64 * abi.GS_CPU_WORDS)()
+    num = C.c_int32()
+    arr, n = _kv(annotations)
+    rc = abi.load().gs_node_reserved_cpus(arr, n, w, C.byref(num))
+    if rc < 0:
+        raise DecodeError("node reserved cpus", rc)
+    return [c for c in range(abi.GS_MAX_CPUS) if (w[c >> 6] >> (c & 63)) & 1], num.value, rc == 0
+
+
+def nrt_reserved_cpus(annotations: dict) -> list[int]:
+    """TopologyOptions.ReservedCPUs from the NRT annotations"""
+    w = (C.c_uint64 * abi.GS_CPU_WORDS)()
+    arr, n = _kv(annotations)
+    _chk(abi.load().gs_decode_nrt_reserved_cpus(arr, n, w), "nrt reserved cpus")
+    return [c for c in range(abi.GS_MAX_CPUS) if (w[c >> 6] >> (c & 63)) & 1]
+
+
 def node_labels(labels: dict, kubelet_cpu_manager_policy: str | None = None,
                 kubelet_topology_policy: str | None = None, numa=None):
     numa = numa if numa is not None else abi.GsNodeNuma()

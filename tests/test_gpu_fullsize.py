@@ -19,6 +19,15 @@ pytestmark = pytest.mark.gpu
 THREADS = min(16, os.cpu_count() or 1)
 
 
+def _save(name: str, got, extra: dict):
+    """The GPU placements for the offline every-pod check (scripts/full_parity.py; committed under
+    tests/golden/fullsize/)."""
+    import json
+    os.makedirs("gpurun_out", exist_ok=True)
+    np.savez_compressed(os.path.join("gpurun_out", f"placements_{name}.npz"),
+                        placements=np.ascontiguousarray(got).view(np.uint8), meta=json.dumps(extra))
+
+
 def _replay_check(c, cfg, got, sample):
     o = orc.Oracle(cfg)
     synth.load_into(o, c)
@@ -45,6 +54,7 @@ def test_c3_100k_nodes_50k_pods_replay_parity():
     synth.load_into(e, c)
     got = e.schedule(c.pods)
     assert e.mirror_check() == 0
+    _save("northstar", got, {"stats": {k: (float(v) if isinstance(v, float) else int(v)) for k, v in e.stats().items()}})
     P = len(c.pods)
     sample = np.unique(np.concatenate([np.arange(48), np.arange(48, P, 64)]))   # every 64th pod
     n = _replay_check(c, cfg, got, sample)
@@ -67,6 +77,7 @@ def test_c3_bench_config_50k_nodes_replay_parity():
     seq = np.arange(P, dtype=np.uint64)
     got = np.concatenate([e.schedule(c.pods[k:k + step], seq[k:k + step]) for k in range(0, P, step)])
     assert e.mirror_check() == 0
+    _save("bench", got, {"stats": {k: (float(v) if isinstance(v, float) else int(v)) for k, v in e.stats().items()}})
     n = _replay_check(c, cfg, got, np.arange(0, P, 64))
     print(f"C3 bench config 50k x {P}: {int((got['node'] >= 0).sum())} placed, {n} pods re-checked in full; "
           f"wall {time.perf_counter() - t0:.1f} s")
