@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define GS_ABI_VERSION 3u
+#define GS_ABI_VERSION 4u
 
 /* ---- resource slots (corev1.ResourceName restricted to the hot-path set) ---- */
 enum gs_resource {
@@ -453,6 +453,11 @@ enum gs_gpu_name {
   GS_NUM_GPU_NAMES = 5
 };
 #define GS_MAX_GPUS 8
+/* Extended resources outside the 7 fixed slots and the GPU names ([upstream] v1helper.IsExtendedResourceName, any
+ * vendor domain): the caller registers up to GS_MAX_XRES names and passes NodeInfo scalars / pod requests by index. A
+ * pod requesting one takes the extension path, where Fit's fitsRequest checks it (IgnoredResources /
+ * IgnoredResourceGroups through gs_ext_args.fit_ignored_xres). */
+#define GS_MAX_XRES 8
 
 typedef struct gs_gpu_device {     /* one GPU minor of the node's Device object (deviceshare/device_cache.go:38-56) */
   int32_t minor;
@@ -467,6 +472,10 @@ typedef struct gs_node_devices {
   gs_gpu_device gpus[GS_MAX_GPUS];
   int64_t allocatable[GS_NUM_GPU_NAMES];  /* NodeInfo.Allocatable.ScalarResources of the GPU names ([upstream] Fit) */
   int64_t requested[GS_NUM_GPU_NAMES];    /* NodeInfo.Requested.ScalarResources of the GPU names */
+  /* NodeInfo scalars of the caller's other extended resources (any vendor/name outside the 7 fixed slots and the GPU
+   * names; index x = the caller's registered name x, 0 when the node does not report it) */
+  int64_t xres_allocatable[GS_MAX_XRES];
+  int64_t xres_requested[GS_MAX_XRES];
 } gs_node_devices;
 
 enum gs_reservation_policy {       /* schedulingv1alpha1.ReservationAllocatePolicy */
@@ -496,6 +505,9 @@ typedef struct gs_pod_ext {        /* per-pod inputs of the two plugins' PreFilt
   int32_t reservation_required;    /* reservationutil.GetRequiredReservationAffinity(pod) != nil (hasAffinity) */
   uint32_t gpu_request_mask;       /* bit n: PodRequestsAndLimits holds GPU name n with a non-zero value */
   int64_t gpu_requests[GS_NUM_GPU_NAMES];
+  uint32_t xres_request_mask;      /* bit x: the pod requests registered extended resource x (a key of its requests) */
+  uint32_t pad0;
+  int64_t xres_requests[GS_MAX_XRES];   /* [upstream] Fit fitsRequest checks them like any scalar resource */
 } gs_pod_ext;
 
 #define GS_EXT_DEVICESHARE 0x1u    /* DeviceShare Filter + Score + Reserve */
@@ -510,7 +522,9 @@ typedef struct gs_ext_args {
   uint32_t fit_ignored_gpu_names;  /* [upstream] NodeResourcesFitArgs.IgnoredResources / IgnoredResourceGroups on the GPU
                                       names (extended resources): bit n = name n is ignored, or its domain (the text
                                       before '/') is an ignored group; Fit then skips its scalar check */
-  uint32_t pad0;
+  uint32_t fit_ignored_xres;       /* the same for the registered extended resources (bit x). Their Fit Score weight
+                                      is 0 (ScoringStrategy.Resources lists only slot resources): a profile weighing
+                                      one is outside this ABI */
 } gs_ext_args;
 
 #define GS_EXT_FAIL_DEVICE 0x1000u      /* DeviceShare Filter: "Insufficient gpu devices" and the Prepare errors */

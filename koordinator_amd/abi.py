@@ -10,7 +10,7 @@ import os
 
 import numpy as np
 
-GS_ABI_VERSION = 3
+GS_ABI_VERSION = 4
 GS_NUM_RES = 8
 GS_RES_CPU, GS_RES_MEMORY, GS_RES_EPHEMERAL = 0, 1, 2
 GS_RES_BATCH_CPU, GS_RES_BATCH_MEMORY, GS_RES_MID_CPU, GS_RES_MID_MEMORY = 3, 4, 5, 6
@@ -214,6 +214,7 @@ GS_NUM_GPU_NAMES = 5
 GPU_NAMES = {"nvidia.com/gpu": 0, "koordinator.sh/gpu": 1, "koordinator.sh/gpu-core": 2,
              "koordinator.sh/gpu-memory": 3, "koordinator.sh/gpu-memory-ratio": 4}
 GS_MAX_GPUS = 8
+GS_MAX_XRES = 8   # registered extended resources (any vendor name outside the fixed slots / GPU names)
 RSV_POLICY = {"": 0, "Default": 0, "Aligned": 1, "Restricted": 2}
 GS_EXT_DEVICESHARE, GS_EXT_RESERVATION = 0x1, 0x2
 GS_POD_EVENT_ADD, GS_POD_EVENT_UPDATE, GS_POD_EVENT_DELETE = 0, 1, 2
@@ -226,7 +227,8 @@ class GsGpuDevice(C.Structure):
 
 class GsNodeDevices(C.Structure):
     _fields_ = [("has_device", i32), ("num_gpus", i32), ("gpus", GsGpuDevice * GS_MAX_GPUS),
-                ("allocatable", i64 * GS_NUM_GPU_NAMES), ("requested", i64 * GS_NUM_GPU_NAMES)]
+                ("allocatable", i64 * GS_NUM_GPU_NAMES), ("requested", i64 * GS_NUM_GPU_NAMES),
+                ("xres_allocatable", i64 * GS_MAX_XRES), ("xres_requested", i64 * GS_MAX_XRES)]
 
 
 class GsReservation(C.Structure):
@@ -238,13 +240,14 @@ class GsReservation(C.Structure):
 
 class GsPodExt(C.Structure):
     _fields_ = [("reservation_owner", u64), ("reservation_required", i32), ("gpu_request_mask", u32),
-                ("gpu_requests", i64 * GS_NUM_GPU_NAMES)]
+                ("gpu_requests", i64 * GS_NUM_GPU_NAMES), ("xres_request_mask", u32), ("pad0", u32),
+                ("xres_requests", i64 * GS_MAX_XRES)]
 
 
 class GsExtArgs(C.Structure):
     _fields_ = [("enabled", u32), ("device_scoring_type", i32), ("device_weights", i64 * GS_NUM_GPU_RES),
                 ("weight_deviceshare", i64), ("weight_reservation", i64), ("fit_ignored_gpu_names", u32),
-                ("pad0", u32)]
+                ("fit_ignored_xres", u32)]
 
 
 class GsExtPlacement(C.Structure):

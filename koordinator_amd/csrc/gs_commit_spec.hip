@@ -321,7 +321,7 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
         }
         if (lane == 0) {
           for (int k = 0; k < SP_NRES; ++k) { s_jq_head[k] = 0; s_jq_tail[k] = 0; }
-          s_cut_at = -1;
+          if (s_cut_at >= v) s_cut_at = -1;   // a cut before v stands (its pod is not undone)
           s_decided = v;
           s_verified = v;
           s_rb_at = v;
@@ -449,72 +449,79 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
         const uint64_t new0 = __ballot(nw0), new1 = __ballot(nw1);
         const uint64_t old0 = __ballot(so0 == M && lane < nd), old1 = __ballot(so1 == M && lane + 64 < nd);
         const int nnew = __popcll(new0) + __popcll(new1), nold = __popcll(old0) + __popcll(old1);
-        const int lo = (int)max<int64_t>(0, jp - 2 - nnew);
-        const int hi = (int)min<int64_t>(len - 1, jp - 1 + nold);
-        const int W = hi - lo + 1;
-        const uint32_t* L = list_ptr(a, 0, p);
-        constexpr int WCH = (2 * MAX_BATCH + 2 + 63) / 64;
-        uint32_t xw[WCH];
-        bool ow[WCH];
-        uint32_t cand = 0xffffffffu;
-        int base_old = 0;
-        if (len > 0) {
+        if (nnew == 0 && nold == 0) {
+          // no dirty row at M (then level M is listed: M is its clean level): the jp-th listed node of level M
+          const int e = off + (int)jp - 1;
+          winner = e < 64 ? (uint32_t)__builtin_amdgcn_readlane((int)lh, e) : list_ptr(a, 0, p)[e];
+          if (ST) { st_acc[24] += e >= 32 ? 1 : 0; st_acc[25] += e >= 64 ? 1 : 0; }
+        } else {
+          const int lo = (int)max<int64_t>(0, jp - 2 - nnew);
+          const int hi = (int)min<int64_t>(len - 1, jp - 1 + nold);
+          const int W = hi - lo + 1;
+          const uint32_t* L = list_ptr(a, 0, p);
+          constexpr int WCH = (2 * MAX_BATCH + 2 + 63) / 64;
+          uint32_t xw[WCH];
+          bool ow[WCH];
+          uint32_t cand = 0xffffffffu;
+          int base_old = 0;
+          if (len > 0) {
 #pragma unroll
-          for (int c = 0; c < WCH; ++c) {
-            const int i = c * 64 + lane, e = off + lo + i;
-            const uint32_t fromh = (uint32_t)__shfl((int)lh, e & 63);
-            xw[c] = 0xffffffffu;
-            if (c * 64 < W && i < W) xw[c] = e < 64 ? fromh : L[e];
-          }
-          if (ST) { st_acc[24] += off + hi >= 32 ? 1 : 0; st_acc[25] += off + hi >= 64 ? 1 : 0; }
-          const uint32_t win0 = (uint32_t)__builtin_amdgcn_readlane((int)xw[0], 0);
+            for (int c = 0; c < WCH; ++c) {
+              const int i = c * 64 + lane, e = off + lo + i;
+              const uint32_t fromh = (uint32_t)__shfl((int)lh, e & 63);
+              xw[c] = 0xffffffffu;
+              if (c * 64 < W && i < W) xw[c] = e < 64 ? fromh : L[e];
+            }
+            if (ST) { st_acc[24] += off + hi >= 32 ? 1 : 0; st_acc[25] += off + hi >= 64 ? 1 : 0; }
+            const uint32_t win0 = (uint32_t)__builtin_amdgcn_readlane((int)xw[0], 0);
 #pragma unroll
-          for (int c = 0; c < WCH; ++c) ow[c] = false;
-          each_node(old0, old1, [&](uint32_t n) {
-            base_old += n < win0 ? 1 : 0;
+            for (int c = 0; c < WCH; ++c) ow[c] = false;
+            each_node(old0, old1, [&](uint32_t n) {
+              base_old += n < win0 ? 1 : 0;
 #pragma unroll
-            for (int c = 0; c < WCH; ++c) ow[c] |= xw[c] == n;
-          });
-          int running = base_old;
-#pragma unroll
-          for (int c = 0; c < WCH; ++c) {
-            if (c * 64 >= W) break;
-            const int i = c * 64 + lane;
-            const bool valid = i < W;
-            const uint64_t bo = __ballot(valid && ow[c]);
-            const int older = running + __popcll(bo & lt_mask);
-            int newer = 0;
-            each_node(new0, new1, [&](uint32_t n) { newer += n < xw[c] ? 1 : 0; });
-            if (valid && !ow[c] && (int64_t)(lo + i - older + newer + 1) == jp) cand = xw[c];
-            running += __popcll(bo);
-          }
-        }
-        each_node(new0, new1, [&](uint32_t n) {
-          int u = 0;
-          each_node(new0, new1, [&](uint32_t n2) { u += n2 < n ? 1 : 0; });
-          int64_t ltn = -1;
-          int older = 0;
-          if (len == 0) {
-            ltn = 0;
-          } else {
-            int pp = 0;
+              for (int c = 0; c < WCH; ++c) ow[c] |= xw[c] == n;
+            });
+            int running = base_old;
 #pragma unroll
             for (int c = 0; c < WCH; ++c) {
               if (c * 64 >= W) break;
-              const bool valid = c * 64 + lane < W;
-              pp += __popcll(__ballot(valid && xw[c] < n));
-              older += __popcll(__ballot(valid && ow[c] && xw[c] < n));
+              const int i = c * 64 + lane;
+              const bool valid = i < W;
+              const uint64_t bo = __ballot(valid && ow[c]);
+              const int older = running + __popcll(bo & lt_mask);
+              int newer = 0;
+              each_node(new0, new1, [&](uint32_t n) { newer += n < xw[c] ? 1 : 0; });
+              if (valid && !ow[c] && (int64_t)(lo + i - older + newer + 1) == jp) cand = xw[c];
+              running += __popcll(bo);
             }
-            older += base_old;
-            if (pp == 0) ltn = (lo == 0) ? 0 : -1;
-            else if (pp == W) ltn = (hi == len - 1) ? len : -1;
-            else ltn = lo + pp;
           }
-          if (ltn >= 0 && ltn - older + u + 1 == jp) cand = n;
-        });
-        const uint64_t got = __ballot(cand != 0xffffffffu);
-        if (!got) { action = 2; end_why = 1; }
-        else winner = (uint32_t)__builtin_amdgcn_readlane((int)cand, __ffsll((long long)got) - 1);
+          each_node(new0, new1, [&](uint32_t n) {
+            int u = 0;
+            each_node(new0, new1, [&](uint32_t n2) { u += n2 < n ? 1 : 0; });
+            int64_t ltn = -1;
+            int older = 0;
+            if (len == 0) {
+              ltn = 0;
+            } else {
+              int pp = 0;
+#pragma unroll
+              for (int c = 0; c < WCH; ++c) {
+                if (c * 64 >= W) break;
+                const bool valid = c * 64 + lane < W;
+                pp += __popcll(__ballot(valid && xw[c] < n));
+                older += __popcll(__ballot(valid && ow[c] && xw[c] < n));
+              }
+              older += base_old;
+              if (pp == 0) ltn = (lo == 0) ? 0 : -1;
+              else if (pp == W) ltn = (hi == len - 1) ? len : -1;
+              else ltn = lo + pp;
+            }
+            if (ltn >= 0 && ltn - older + u + 1 == jp) cand = n;
+          });
+          const uint64_t got = __ballot(cand != 0xffffffffu);
+          if (!got) { action = 2; end_why = 1; }
+          else winner = (uint32_t)__builtin_amdgcn_readlane((int)cand, __ffsll((long long)got) - 1);
+        }
       }
       if (ST) st_acc[10] += full_row ? 1 : 0;
       SPM(19);   // decide: tie-break position, winner among listed + dirty ties
@@ -751,6 +758,9 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
       while (wm < qd && ld_acq(&rescored[wm])) ++wm;
       bool moved = false, req = false;
       while (v < qd && v <= wm) {
+        // nothing past a host cut is verified: the batch ends after the cut pod whatever the later decisions
+        const int cut_v = ld_acq(&s_cut_at);
+        if (cut_v >= 0 && v > cut_v) break;
         const DecRec d = dec[v];
         int mis = 0, fadd = 0;
         if ((d.pend0 >> lane) & 1ull) {

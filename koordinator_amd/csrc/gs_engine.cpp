@@ -1083,6 +1083,7 @@ DevNode dev_image(const gs_node_devices& d) {
   o.has_device = d.has_device;
   o.num_gpus = d.has_device ? d.num_gpus : 0;
   for (int n = 0; n < GS_NUM_GPU_NAMES; ++n) o.fit_free[n] = d.allocatable[n] - d.requested[n];
+  for (int x = 0; x < GS_MAX_XRES; ++x) o.fit_free[GS_NUM_GPU_NAMES + x] = d.xres_allocatable[x] - d.xres_requested[x];
   for (int g = 0; g < o.num_gpus; ++g) {
     o.g[g].minor = d.gpus[g].minor;
     o.g[g].has_info = d.gpus[g].has_info;
@@ -1143,6 +1144,7 @@ void matched_of(const gs_ctx* c, uint64_t owner, std::vector<std::pair<uint32_t,
 }
 
 bool is_ext_pod(const gs_ctx* c, const gs_pod_ext& e) {
+  if (e.xres_request_mask & ((1u << GS_MAX_XRES) - 1u)) return true;   // Fit over a registered extended resource
   if ((c->ext.enabled & GS_EXT_DEVICESHARE) && (e.gpu_request_mask & 0x1Fu)) return true;
   if (!(c->ext.enabled & GS_EXT_RESERVATION)) return false;
   if (e.reservation_required) return true;
@@ -1234,6 +1236,9 @@ int ext_schedule_one(gs_ctx* c, const gs_pod& pod, const gs_pod_ext& e, uint64_t
   if (rs_on) matched_of(c, e.reservation_owner, &matched);
   if (gmask && !matched.empty())
     return fail(c, GS_EUNSUPPORTED, "a pod that requests GPUs and matches reservations is not on the device path");
+  for (int x = 0; x < GS_MAX_XRES; ++x)
+    if (e.xres_requests[x] < 0 || !in_range(e.xres_requests[x]))
+      return fail(c, GS_EUNSUPPORTED, "extended resource request outside [0, 2^53)");
   PodVec v = prep_pod(c, pod);
   if (c->numa_on && (v.numa & PN_BIND))
     return fail(c, GS_EUNSUPPORTED, "cpuset-bound Reservation / DeviceShare pods are not on the device path");
@@ -1323,6 +1328,11 @@ int ext_schedule_one(gs_ctx* c, const gs_pod& pod, const gs_pod_ext& e, uint64_t
   const uint32_t gpu_names_all = gmask ? (e.gpu_request_mask & 0x1Fu) : 0u;   // NodeInfo.AddPod adds them all
   xp.gpu_names = gpu_names_all & ~c->ext.fit_ignored_gpu_names;               // Fit checks the non-ignored ones
   for (int n = 0; n < GS_NUM_GPU_NAMES; ++n) xp.gpu_name_req[n] = (xp.gpu_names >> n & 1u) ? e.gpu_requests[n] : 0;
+  const uint32_t xres_all = e.xres_request_mask & ((1u << GS_MAX_XRES) - 1u);
+  const uint32_t xres_fit = xres_all & ~c->ext.fit_ignored_xres;
+  xp.gpu_names |= xres_fit << GS_NUM_GPU_NAMES;
+  for (int x = 0; x < GS_MAX_XRES; ++x)
+    xp.gpu_name_req[GS_NUM_GPU_NAMES + x] = (xres_fit >> x & 1u) ? e.xres_requests[x] : 0;
   xp.w_ds = c->ext.weight_deviceshare;
   xp.w_rs = c->ext.weight_reservation;
   for (int s = 0; s < 7; ++s) xp.pod_req[s] = pod.requests[s];
@@ -1334,7 +1344,7 @@ int ext_schedule_one(gs_ctx* c, const gs_pod& pod, const gs_pod_ext& e, uint64_t
   xp.dev_most = c->ext.device_scoring_type == GS_SCORING_MOST_ALLOCATED;
   xp.seq = seq;
   // GPU names are scalar requests: the Fit filter's all-zero short cut no longer applies
-  if (gpu_names_all) v.flags &= ~PF_ALL_ZERO;
+  if (gpu_names_all || xres_all) v.flags &= ~PF_ALL_ZERO;
   c->h_pods[0] = v;
   c->h_seq[0] = seq;
   // numa_idx (the eval pass's NUMA-policy work list) as launch_batch keeps it
@@ -1412,6 +1422,8 @@ int ext_schedule_one(gs_ctx* c, const gs_pod& pod, const gs_pod_ext& e, uint64_t
   }
   for (int n = 0; n < GS_NUM_GPU_NAMES; ++n)   // NodeInfo.AddPod of the GPU-name scalars
     if (gpu_names_all >> n & 1u) { c->devs[node].requested[n] += e.gpu_requests[n]; dev_mark(c, node); }
+  for (int x = 0; x < GS_MAX_XRES; ++x)         // ... and of the registered extended resources
+    if (xres_all >> x & 1u) { c->devs[node].xres_requested[x] += e.xres_requests[x]; dev_mark(c, node); }
   apply_placement(c, pod, xo.node, true);
   return GS_OK;
 }
@@ -2275,6 +2287,8 @@ int gs_ext_configure(gs_ctx* c, const gs_ext_args* a) {
   if (!c || !a) return GS_EINVAL;
   if (a->enabled & ~(GS_EXT_DEVICESHARE | GS_EXT_RESERVATION)) return fail(c, GS_EINVAL, "unknown extension plugin bits");
   if (a->fit_ignored_gpu_names & ~0x1Fu) return fail(c, GS_EINVAL, "fit_ignored_gpu_names outside the GPU names");
+  if (a->fit_ignored_xres & ~((1u << GS_MAX_XRES) - 1u))
+    return fail(c, GS_EINVAL, "fit_ignored_xres outside the registered extended resources");
   if (a->device_scoring_type != GS_SCORING_LEAST_ALLOCATED && a->device_scoring_type != GS_SCORING_MOST_ALLOCATED)
     return fail(c, GS_EINVAL, "DeviceShare scoring strategy not supported");
   for (int r = 0; r < GS_NUM_GPU_RES; ++r)
@@ -2304,6 +2318,9 @@ int gs_node_devices_upsert(gs_ctx* c, const uint32_t* idx, const gs_node_devices
         if (d[k].gpus[g].total[r] < 0 || d[k].gpus[g].used[r] < 0 || d[k].gpus[g].total[r] >= (1LL << 53))
           return fail(c, GS_EUNSUPPORTED, "GPU quantity outside [0, 2^53)");
     }
+    for (int x = 0; x < GS_MAX_XRES; ++x)
+      if (!in_range(d[k].xres_allocatable[x]) || !in_range(d[k].xres_requested[x]))
+        return fail(c, GS_EUNSUPPORTED, "extended resource quantity outside the exact range (-2^53, 2^53)");
     c->devs[i] = d[k];
     dev_mark(c, i);
   }
@@ -2387,7 +2404,7 @@ int gs_schedule_ext(gs_ctx* c, const gs_pod* pods, const gs_pod_ext* ext, uint32
     // a run of plain pods goes through the batched path (both plugins score 0 for them; the mirror rows carry the
     // unmatched restore), an extension pod through the normalizing path
     uint32_t j = i;
-    while (j < npods && !(ext && c->ext.enabled && is_ext_pod(c, ext[j]))) ++j;
+    while (j < npods && !(ext && (c->ext.enabled || ext[j].xres_request_mask) && is_ext_pod(c, ext[j]))) ++j;
     if (j > i) {
       std::vector<uint64_t> sq;
       if (!seq) { sq.resize(j - i); for (uint32_t k = i; k < j; ++k) sq[k - i] = k; }

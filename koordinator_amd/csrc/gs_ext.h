@@ -11,6 +11,7 @@
 #pragma once
 #include <stdint.h>
 
+#include "../../include/gpuscore.h"
 #include "gs_kernels.h"
 
 namespace gs {
@@ -24,13 +25,15 @@ struct DevGpu {                 // one GPU minor after filterNodeDevice (has_inf
   int32_t minor;
   int32_t has_info;
 };
+constexpr int EXT_FIT_NAMES = GS_NUM_GPU_NAMES + GS_MAX_XRES;   // Fit scalars of the extension path: GPU names, then
+                                                                  // the registered extended resources
 struct DevNode {                // gs_node_devices, as the kernels read it
   int32_t has_device;
   int32_t num_gpus;
-  int64_t fit_free[5];          // NodeInfo Allocatable - Requested of the GPU resource names ([upstream] Fit)
+  int64_t fit_free[EXT_FIT_NAMES];   // NodeInfo Allocatable - Requested of those names ([upstream] Fit)
   DevGpu g[EXT_GPUS];
 };
-static_assert(sizeof(DevNode) == 8 + 40 + EXT_GPUS * 56, "DevNode layout");
+static_assert(sizeof(DevNode) == 8 + 8 * EXT_FIT_NAMES + EXT_GPUS * 56, "DevNode layout");
 
 struct ExtRes {                 // one matched reservation (ReservationInfo fields the Filter / Score read)
   int64_t alloc[7];             // Allocatable per slot (0 where absent)
@@ -58,12 +61,12 @@ struct ExtRec {                 // a node with matched reservations: the restore
 
 struct ExtPod {                 // per-pod constants of the three kernels
   int64_t gpu_req[3];           // ConvertDeviceRequest (gpu-core, gpu-memory-ratio, gpu-memory)
-  int64_t gpu_name_req[5];      // the pod's GPU-name requests (Fit scalars)
+  int64_t gpu_name_req[EXT_FIT_NAMES];   // the pod's GPU-name and registered extended-resource requests (Fit scalars)
   int64_t dev_w[3];
   int64_t w_ds, w_rs;
   int64_t pod_req[7];           // PodRequestsAndLimits per slot (Reservation fitsNode / score)
   uint32_t gpu_mask;            // keys of gpu_req (0: no GPU request; DeviceShare skips)
-  uint32_t gpu_names;           // keys of gpu_name_req
+  uint32_t gpu_names;           // keys of gpu_name_req (checked by Fit: the ignored ones left out)
   uint32_t pod_mask;            // keys of pod_req
   int32_t required;             // reservation affinity
   int32_t nrec;

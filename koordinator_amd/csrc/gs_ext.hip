@@ -60,7 +60,7 @@ __device__ __forceinline__ bool fits_inst(const int64_t inst[3], uint32_t mask, 
 __device__ __forceinline__ void eval_device(const DevNode& d, const ExtPod& p, bool* ok, int32_t* raw) {
   *ok = true;
   *raw = 0;
-  for (int n = 0; n < 5; ++n)   // [upstream] fitsRequest over the pod's GPU-name scalars
+  for (int n = 0; n < EXT_FIT_NAMES; ++n)   // [upstream] fitsRequest over the pod's GPU-name / extended scalars
     if ((p.gpu_names >> n & 1u) && p.gpu_name_req[n] > d.fit_free[n]) { *ok = false; return; }
   if (!d.has_device) return;    // no Device object: DeviceShare passes and scores 0
   int64_t inst[3];

@@ -276,7 +276,7 @@ class ElasticQuotaPlugin:
         self.reserve_pod(quota, request, non_preemptible, sign=-1)
 
 
-def schedule_with_quota(engine, plugin: ElasticQuotaPlugin, pods, pod_quota, seq=None):
+def schedule_with_quota(engine, plugin: ElasticQuotaPlugin, pods, pod_quota, seq=None, pod_ext=None):
     """Quota-gated batched scheduleOne: per pod in order, ElasticQuota PreFilter, then (if admitted) the node
     loop of `engine.schedule` (libgpuscore gs_schedule), then quota Reserve on a placement — the reference's
     sequential order (PreFilter -> Filter/Score -> selectHost -> Reserve) kept exact while the node loop runs
@@ -292,12 +292,15 @@ def schedule_with_quota(engine, plugin: ElasticQuotaPlugin, pods, pod_quota, seq
     are those of the one-pod-at-a-time order. Runtime does not change inside a batch (it
     follows requests, which a Reserve does not touch). pod_quota[i] = (quota name or None, request
     ResourceList, non_preemptible). Returns (placements, statuses): placements in the engine's dtype with
-    node = -1 for quota-rejected pods, statuses[i] = the PreFilter Status of pod i."""
+    node = -1 for quota-rejected pods, statuses[i] = the PreFilter Status of pod i. pod_ext (gs_pod_ext per pod):
+    the runs go through engine.schedule_ext (Reservation + DeviceShare, config C5) and the result is
+    (placements, ext placements, statuses)."""
     pods = np.ascontiguousarray(pods, dtype=abi.POD_DTYPE)
     n = len(pods)
     seq = np.arange(n, dtype=np.uint64) if seq is None else np.ascontiguousarray(seq, dtype=np.uint64)
     out = np.zeros(n, abi.PLACEMENT_DTYPE)
     out["node"] = -1
+    xout = np.zeros(n, abi.EXT_PLACEMENT_DTYPE) if pod_ext is not None else None
     qidx = np.array([plugin.index[q] if q else -1 for q, _, _ in pod_quota], np.int32)
     reqs = np.zeros((max(n, 1), abi.GS_QUOTA_DIMS), np.int64)
     masks = np.zeros(max(n, 1), np.uint32)
@@ -321,7 +324,11 @@ def schedule_with_quota(engine, plugin: ElasticQuotaPlugin, pods, pod_quota, seq
         seg = np.array([p for p in range(i, j) if st[p].code == abi.GS_QUOTA_ADMIT], np.int64)
         if len(seg):
             try:
-                res = engine.schedule(pods[seg], seq[seg])
+                if pod_ext is None:
+                    res = engine.schedule(pods[seg], seq[seg])
+                else:
+                    res, xres = engine.schedule_ext(pods[seg], pod_ext[seg], seq[seg])
+                    xout[seg] = xres
             except Exception:
                 # the run's speculative Reserves leave the forest (used as before the run), then the error surfaces
                 for p in seg:
@@ -339,4 +346,4 @@ def schedule_with_quota(engine, plugin: ElasticQuotaPlugin, pods, pod_quota, seq
             raise RuntimeError(f"gs_quota_settle_batch: {rc}")
         i = j
     statuses = [plugin._status(st[p], pod_quota[p][0], pod_quota[p][1]) for p in range(n)]
-    return out, statuses
+    return (out, statuses) if pod_ext is None else (out, xout, statuses)

@@ -324,13 +324,16 @@ def load_into(engine, c: Cluster) -> None:
 
 def make_ext(c: Cluster, seed: int | None = None, gpu_node_pct: int = 20, gpus_per_node: int = 8,
              rsv_node_pct: int = 5, owners: int = 40, owner_pod_pct: int = 10, required_pct: int = 2,
-             gpu_pod_pct: int = 10) -> Cluster:
+             gpu_pod_pct: int = 10, xres_node_pct: int = 0, xres_pod_pct: int = 0) -> Cluster:
     """Reservation + DeviceShare state for config C5: GPU Device objects on gpu_node_pct% of the nodes
     (8 GPUs of 80 GiB, partly used), 1-2 reservations on rsv_node_pct% of the nodes (owner groups, Default /
     Restricted policies, some allocate-once, some already used by assigned pods, 10% with a reservation-order label),
     and per-pod plugin inputs: owner-group pods (owner_pod_pct%, required_pct% with reservation affinity) and GPU
     pods (gpu_pod_pct%: gpu-core + gpu-memory-ratio, nvidia.com/gpu, gpu-memory-ratio alone or gpu-memory, 1% with an
-    invalid gpu-core). NodeInfo (c.nodes) already holds the reserve pods and the pods assigned to them."""
+    invalid gpu-core). NodeInfo (c.nodes) already holds the reserve pods and the pods assigned to them.
+    xres_node_pct / xres_pod_pct: two registered extended resources (x0 "example.com/fpga": 1-4 per node, pods ask 1;
+    x1 "example.com/shared-nic": 1000 per node, pods ask 100-400) on that share of nodes / pods, 1% of the pods asking
+    for both (Fit's scalar check over names outside the fixed slots)."""
     s = Stream((BASE_SEED + 0x5C5) if seed is None else seed)
     N = c.num_nodes
     P = len(c.pods)
@@ -432,6 +435,21 @@ def make_ext(c: Cluster, seed: int | None = None, gpu_node_pct: int = 20, gpus_p
             masks[p] = (1 << CO) | (1 << RA)
     ext["gpu_request_mask"] = masks
     ext["gpu_requests"] = reqs
+    if xres_node_pct:
+        xn = s.randint(30, N, 0, 99) < xres_node_pct
+        fp = s.randint(31, N, 1, 4)
+        devs["xres_allocatable"][:, 0] = np.where(xn, fp, 0)
+        devs["xres_requested"][:, 0] = np.where(xn, np.minimum(s.randint(32, N, 0, 2), fp), 0)
+        devs["xres_allocatable"][:, 1] = np.where(xn, 1000, 0)
+        devs["xres_requested"][:, 1] = np.where(xn, s.randint(33, N, 0, 9) * 100, 0)
+    if xres_pod_pct:
+        xk = s.randint(34, P, 0, 999)
+        xp0 = xk < xres_pod_pct * 5
+        xp1 = (xk >= xres_pod_pct * 5) & (xk < xres_pod_pct * 10)
+        both = xk >= 990
+        ext["xres_requests"][:, 0] = np.where(xp0 | both, 1, 0)
+        ext["xres_requests"][:, 1] = np.where(xp1 | both, s.randint(35, P, 1, 4) * 100, 0)
+        ext["xres_request_mask"] = (np.where(xp0 | both, 1, 0) | np.where(xp1 | both, 2, 0)).astype(np.uint32)
     c.ext = {"devices": devs, "reservations": rsv, "pod_ext": ext}
     return c
 

@@ -1681,6 +1681,7 @@ int or_schedule_ext(or_cluster* c, const gs_pod* pods, const gs_pod_ext* ext, ui
     if (!ds_on) gpu = GpuReq{};
     const bool gpu_pod = gpu.mask != 0;
     const uint32_t gpu_names = gpu_pod ? (e.gpu_request_mask & 0x1Fu) : 0u;
+    const uint32_t xres_names = e.xres_request_mask & ((1u << GS_MAX_XRES) - 1u);   // the caller's extended resources
     const orn::PreState st = orn::prefilter(c->numa_args, pod);
     // Reservation BeforePreFilter (transformer.go:50-235)
     bool any_state = false;
@@ -1723,7 +1724,7 @@ int or_schedule_ext(or_cluster* c, const gs_pod* pods, const gs_pod_ext* ext, ui
       uint32_t code = 0;
       if (en & GS_ENABLE_FIT_FILTER) {
         code |= fit_filter(pod, nd);
-        if (gpu_pod) {   // the GPU names are scalar resources of the pod ([upstream] fit.go fitsRequest)
+        if (gpu_pod || xres_names) {   // GPU names / extended resources are scalars ([upstream] fit.go fitsRequest)
           const gs_node_devices& d = c->devices[n];
           if (!pod.requests[0] && !pod.requests[1] && !pod.requests[2] && !(pod.request_mask & GS_SCALAR_RES_MASK)) {
             // fit_filter returned early on an all-zero request: the scalar GPU names make it non-zero
@@ -1736,6 +1737,10 @@ int or_schedule_ext(or_cluster* c, const gs_pod* pods, const gs_pod_ext* ext, ui
             if (c->ext.fit_ignored_gpu_names & (1u << g)) continue;   // IgnoredResources / IgnoredResourceGroups
             const int64_t a = d.allocatable[g], r = d.requested[g];
             if (e.gpu_requests[g] > a - r) code |= GS_FAIL_FIT_SCALAR;
+          }
+          for (int x = 0; x < GS_MAX_XRES; ++x) {
+            if (!(xres_names & (1u << x)) || (c->ext.fit_ignored_xres & (1u << x))) continue;
+            if (e.xres_requests[x] > d.xres_allocatable[x] - d.xres_requested[x]) code |= GS_FAIL_FIT_SCALAR;
           }
         }
       }
@@ -1842,6 +1847,8 @@ int or_schedule_ext(or_cluster* c, const gs_pod* pods, const gs_pod_ext* ext, ui
     nd.pod_count += 1;
     for (int g = 0; g < GS_NUM_GPU_NAMES; ++g)
       if (gpu_names & (1u << g)) dv.requested[g] += e.gpu_requests[g];
+    for (int x = 0; x < GS_MAX_XRES; ++x)
+      if (xres_names & (1u << x)) dv.xres_requested[x] += e.xres_requests[x];
     if (!(pod.flags & GS_POD_TERMINATED)) c->nodes[selected].assigned[pod.uid] = AssignInfo{c->now, pod};
     if (ext_out) ext_out[p] = eo;
   }

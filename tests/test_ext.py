@@ -184,3 +184,43 @@ def test_c5_properties():
         grew = int(d1["gpus"]["used"][:, abi.GS_GPU_MEMORY_RATIO].sum() - dev0[i]["gpus"]["used"][:, abi.GS_GPU_MEMORY_RATIO].sum())
         sel = ok_gpu & (out["node"] == i)
         assert grew == int((eo["gpu_count"][sel] * eo["gpu_per_instance"][sel][:, abi.GS_GPU_MEMORY_RATIO]).sum())
+
+
+def _xres_cluster(ignored: int = 0):
+    c = synth.make_cluster(400, 300, config_id=12)
+    synth.make_ext(c, xres_node_pct=40, xres_pod_pct=20, gpu_pod_pct=5, owner_pod_pct=5)
+    cfg = config.make_config(c.num_nodes, enabled=abi.GS_ENABLE_LA_FIT)
+    a = orc.ext_args_default()
+    a.fit_ignored_xres = ignored
+    o = orc.Oracle(cfg)
+    synth.load_into(o, c)
+    synth.load_ext_into(o, c, a)
+    return c, o
+
+
+def test_extended_resources_fit_properties():
+    """Registered extended resources (names outside the fixed slots, [upstream] fit.go fitsRequest over
+    podRequest.ScalarResources; parity unpinned: no reference test holds it): every placement fits the node's
+    Allocatable - Requested of each requested name at its time, a request no node can hold is a FitError, and with the
+    names in IgnoredResources the same request is placed."""
+    c, o = _xres_cluster()
+    ext = c.ext["pod_ext"].copy()
+    ext["xres_request_mask"][7] |= 1
+    ext["xres_requests"][7, 0] = 99               # more than any node reports
+    out, eo = o.schedule_ext(c.pods, ext)
+    alloc = c.ext["devices"]["xres_allocatable"].copy()
+    req = c.ext["devices"]["xres_requested"].copy()
+    asked = 0
+    for i in range(len(c.pods)):
+        n, m = int(out["node"][i]), int(ext["xres_request_mask"][i])
+        if n < 0:
+            continue
+        for x in range(2):
+            if m >> x & 1:
+                asked += 1
+                assert ext["xres_requests"][i, x] <= alloc[n, x] - req[n, x], (i, x)
+                req[n, x] += ext["xres_requests"][i, x]
+    assert asked > 20 and out["node"][7] == -1
+    c2, o2 = _xres_cluster(ignored=0x3)
+    out2, _ = o2.schedule_ext(c2.pods, ext)
+    assert out2["node"][7] >= 0

@@ -101,3 +101,26 @@ def test_c5_fit_ignored_resource_group():
     e, o, ge, oe = run_pair(c, ignored=ign)
     check(c, e, o, ge, oe)
     assert (ge[1]["gpu_count"] > 0).sum() > 20
+
+
+@pytest.mark.parametrize("ignored", [0, 0x1], ids=["checked", "x0-ignored"])
+def test_c5_registered_extended_resources(ignored):
+    """Extended resources outside the fixed slots and the GPU names (gs_pod_ext.xres_*): Fit's scalar check on the
+    extension path, IgnoredResources per name, NodeInfo.AddPod of them on the host mirror."""
+    c = synth.make_cluster(1500, 500, config_id=12)
+    synth.make_ext(c, xres_node_pct=40, xres_pod_pct=20)
+    from koordinator_amd.engine import Engine
+    cfg = config.make_config(c.num_nodes, enabled=abi.GS_ENABLE_LA_FIT)
+    a = orc.ext_args_default()
+    a.fit_ignored_xres = ignored
+    e, o = Engine(cfg), orc.Oracle(cfg)
+    for x in (e, o):
+        synth.load_into(x, c)
+        synth.load_ext_into(x, c, a)
+    seq = np.arange(len(c.pods), dtype=np.uint64)
+    ge = e.schedule_ext(c.pods, c.ext["pod_ext"], seq)
+    oe = o.schedule_ext(c.pods, c.ext["pod_ext"], seq)
+    check(c, e, o, ge, oe)
+    for i in np.nonzero(c.ext["devices"]["xres_allocatable"][:, 0])[0][:50]:
+        assert np.array_equal(e.devices(int(i))["xres_requested"], o.devices(int(i))["xres_requested"])
+    assert (c.ext["pod_ext"]["xres_request_mask"] != 0).sum() > 50
