@@ -47,6 +47,9 @@ def check(c, e, o, ge, oe):
         assert not len(bad), f"ext {f} differs at pods {bad[:10]}"
     for r in c.ext["reservations"]:
         a, b = e.reservation(int(r["uid"])), o.reservation(int(r["uid"]))
+        if a is None or b is None:   # removed by an update between calls: removed on both sides
+            assert a is None and b is None
+            continue
         assert a["assigned_pods"] == b["assigned_pods"] and np.array_equal(a["allocated"], b["allocated"])
     for i in np.nonzero(c.ext["devices"]["has_device"])[0]:
         a, b = e.devices(int(i)), o.devices(int(i))
