@@ -731,6 +731,27 @@ int gs_reason_string(uint32_t code, uint32_t scalar_mask, const char* const* sca
  * s_memtime stamps of its 8 phases at [2n + 8i ..] (cycles: 10n entries). */
 int gs_debug_pair_probe(gs_ctx* ctx, const gs_pod* pods, uint32_t npods, const uint32_t* nodes, const int32_t* pod_of,
                         uint32_t n, int mode, int32_t* scores, uint64_t* cycles);
+/* Diagnostics: the device's topology-manager Merge + admit (frameworkext/topologymanager/policy.go:68-186 and
+ * policy_{best_effort,restricted,single_numa_node}.go, as every NUMA-policy pair evaluation runs it) on given hint
+ * lists, one gs_merge_case each. The lists are those NodeNUMAResource's hint provider produces
+ * (resource_manager.go:418-532 generateHints), in filterProvidersHints' resource order cpu, memory: positions of the
+ * IterateBitMasks order over nz NUMA nodes (bit i = the i-th mask), lc / lm = the masks listed as hints, totc / totm =
+ * the masks whose total covers the request (a hint is Preferred iff its size is the smallest of tot*), tot_*_any =
+ * totc / totm non-empty; a resource the pod does not request (has_* = 0) or nil_hints (no provider output) adds no
+ * list, an empty lc / lm with tot_*_any adds the reference's {nil, false} marker. score[i]: the hint score of
+ * position i (numaScorer). out: admit, whether an affinity is set, and its mask. */
+typedef struct gs_merge_case {
+  uint32_t lc, totc, lm, totm;
+  int32_t nz, policy;
+  int32_t nil_hints, has_cpu, has_mem, tot_c_any, tot_m_any;
+  int32_t score[15];
+} gs_merge_case;
+typedef struct gs_merge_result {
+  int32_t admit, aff_has;
+  uint32_t aff;
+  int32_t pad;
+} gs_merge_result;
+int gs_debug_numa_merge(gs_ctx* ctx, const gs_merge_case* cases, uint32_t n, gs_merge_result* out);
 /* sizeof() of the ABI structs as compiled into the library, in this order: gs_pod, gs_node,
  * gs_node_metric, gs_pod_metric, gs_config, gs_placement, gs_stats, gs_loadaware_args, gs_cpu_topology,
  * gs_node_numa, gs_pod_allocation, gs_numa_args, gs_quota_group, gs_quota_status. */

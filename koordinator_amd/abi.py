@@ -259,6 +259,18 @@ class GsExtPlacement(C.Structure):
 ALLGATHER_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t)
 
 # numpy dtypes with the exact C layout (for bulk construction of node/pod arrays)
+class GsMergeCase(C.Structure):
+    _fields_ = [("lc", u32), ("totc", u32), ("lm", u32), ("totm", u32), ("nz", i32), ("policy", i32),
+                ("nil_hints", i32), ("has_cpu", i32), ("has_mem", i32), ("tot_c_any", i32), ("tot_m_any", i32),
+                ("score", i32 * 15)]
+
+
+class GsMergeResult(C.Structure):
+    _fields_ = [("admit", i32), ("aff_has", i32), ("aff", u32), ("pad", i32)]
+
+
+MERGE_CASE_DTYPE = np.dtype(GsMergeCase)
+MERGE_RESULT_DTYPE = np.dtype(GsMergeResult)
 POD_DTYPE = np.dtype(GsPod)
 NODE_DTYPE = np.dtype(GsNode)
 METRIC_DTYPE = np.dtype(GsNodeMetric)
@@ -313,6 +325,7 @@ SIGNATURES = {
     "gs_debug_mirror_check": (C.c_int, [P]),
     "gs_debug_verify_cpuset": (C.c_int, [P, C.c_int]),
     "gs_debug_pair_probe": (C.c_int, [P, P, C.c_uint32, P, P, C.c_uint32, C.c_int, P, P]),
+    "gs_debug_numa_merge": (C.c_int, [P, P, u32, P]),
     "gs_reason_string": (C.c_int, [C.c_uint32, C.c_uint32, P, C.c_char_p, C.c_size_t]),
     "gs_reset": (C.c_int, [P]),
     "gs_abi_sizes": (None, [C.POINTER(u64), u32]),

@@ -1376,7 +1376,7 @@ int ext_schedule_one(gs_ctx* c, const gs_pod& pod, const gs_pod_ext& e, uint64_t
                          c->d_aff, c->st));
   HIP_TRY(c, hipEventRecord(c->ev[1], c->st));
   HIP_TRY(c, launch_ext_nodes(c->d_dev, c->d_S, c->n0, c->n1, c->d_xpod, c->d_xtot, c->d_xds, c->d_xrs, c->st));
-  HIP_TRY(c, launch_ext_matched(c->mv, c->d_pods, c->pf, prod_cols, c->d_xpod, c->d_xrec, c->d_xres, nrec, c->d_xtot,
+  HIP_TRY(c, launch_ext_matched(c->mv, c->d_pods, c->pf, prod_cols, c->d_dev, c->d_xpod, c->d_xrec, c->d_xres, nrec, c->d_xtot,
                                 c->d_xrs, c->d_xnom, c->d_xT, c->n1 - c->n0, c->st));
   HIP_TRY(c, launch_ext_select(c->d_xtot, c->d_xds, c->d_xrs, c->d_xrec, c->n0, c->n1, c->d_xpod, c->cfg.seed, c->d_xT,
                                c->d_xout, c->st));
@@ -2238,6 +2238,31 @@ int gs_debug_pair_probe(gs_ctx* c, const gs_pod* pods, uint32_t npods, const uin
   if (e == hipSuccess) e = hipMemcpy(cycles, d_c, 80 * n, hipMemcpyDeviceToHost);
   (void)hipFree(d_p); (void)hipFree(d_n); (void)hipFree(d_o); (void)hipFree(d_s); (void)hipFree(d_c);
   if (e != hipSuccess) return fail(c, GS_EDEVICE, "probe: %s", hipGetErrorString(e));
+  return GS_OK;
+}
+
+// The device merge on given hint lists (gs_probe.hip merge_probe_kernel).
+int gs_debug_numa_merge(gs_ctx* c, const gs_merge_case* cases, uint32_t n, gs_merge_result* out) {
+  if (!c || (n && (!cases || !out))) return GS_EINVAL;
+  for (uint32_t i = 0; i < n; ++i)
+    if (cases[i].nz < 1 || cases[i].nz > 4 || cases[i].policy < GS_NUMA_POLICY_NONE ||
+        cases[i].policy > GS_NUMA_POLICY_SINGLE_NUMA_NODE)
+      return GS_EINVAL;
+  if (!n) return GS_OK;
+  int rc = ready(c);
+  if (rc) return rc;
+  gs_merge_case* d_c = nullptr;
+  gs_merge_result* d_o = nullptr;
+  hipError_t e = hipMalloc(&d_c, sizeof(gs_merge_case) * n);
+  if (e == hipSuccess) e = hipMalloc(&d_o, sizeof(gs_merge_result) * n);
+  if (e == hipSuccess) e = hipMemcpy(d_c, cases, sizeof(gs_merge_case) * n, hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hipStreamSynchronize(c->st);
+  if (e == hipSuccess) e = launch_merge_probe(d_c, (int)n, d_o, c->st);
+  if (e == hipSuccess) e = hipStreamSynchronize(c->st);
+  if (e == hipSuccess) e = hipMemcpy(out, d_o, sizeof(gs_merge_result) * n, hipMemcpyDeviceToHost);
+  (void)hipFree(d_c);
+  (void)hipFree(d_o);
+  if (e != hipSuccess) return fail(c, GS_EDEVICE, "merge probe: %s", hipGetErrorString(e));
   return GS_OK;
 }
 

@@ -89,7 +89,7 @@ struct ExtOut {
 hipError_t launch_ext_nodes(const DevNode* dev, const int16_t* S, uint32_t n0, uint32_t n1, const ExtPod* pod,
                             int32_t* tot, int16_t* ds, int16_t* rs, hipStream_t st);
 hipError_t launch_ext_matched(const MirrorView& m, const PodVec* pods, const Profile& pf, int prod_cols,
-                              const ExtPod* pod, const ExtRec* recs, const ExtRes* res, int nrec, int32_t* tot,
+                              const DevNode* dev, const ExtPod* pod, const ExtRec* recs, const ExtRes* res, int nrec, int32_t* tot,
                               int16_t* rs, int32_t* nominated, int32_t* scratch, uint32_t len, hipStream_t st);
 size_t ext_select_scratch_words(uint32_t len);   // int32 words of launch_ext_select's scratch
 hipError_t launch_ext_select(const int32_t* tot, const int16_t* ds, const int16_t* rs, const ExtRec* recs, uint32_t n0,

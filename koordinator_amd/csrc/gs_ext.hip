@@ -57,12 +57,18 @@ __device__ __forceinline__ bool fits_inst(const int64_t inst[3], uint32_t mask, 
 }
 
 // one node: GPU Fit scalars, DeviceShare Filter and raw Score
+// [upstream] fitsRequest over the pod's GPU-name / registered extended scalars (every node, matched ones included)
+__device__ __forceinline__ bool fit_names_ok(const DevNode& d, const ExtPod& p) {
+  for (int n = 0; n < EXT_FIT_NAMES; ++n)
+    if ((p.gpu_names >> n & 1u) && p.gpu_name_req[n] > d.fit_free[n]) return false;
+  return true;
+}
+
 __device__ __forceinline__ void eval_device(const DevNode& d, const ExtPod& p, bool* ok, int32_t* raw) {
   *ok = true;
   *raw = 0;
-  for (int n = 0; n < EXT_FIT_NAMES; ++n)   // [upstream] fitsRequest over the pod's GPU-name / extended scalars
-    if ((p.gpu_names >> n & 1u) && p.gpu_name_req[n] > d.fit_free[n]) { *ok = false; return; }
-  if (!d.has_device) return;    // no Device object: DeviceShare passes and scores 0
+  if (!fit_names_ok(d, p)) { *ok = false; return; }
+  if (!d.has_device || !p.gpu_mask) return;   // no Device object / no GPU request: DeviceShare passes, scores 0
   int64_t inst[3];
   uint32_t mask;
   int64_t count;
@@ -101,7 +107,7 @@ __global__ __launch_bounds__(256) void ext_nodes_kernel(const DevNode* __restric
   const ExtPod& p = *pp;
   int32_t t = S[i - n0];
   int32_t raw = 0;
-  if (t >= 0 && p.gpu_mask) {
+  if (t >= 0 && (p.gpu_mask || p.gpu_names)) {
     bool ok;
     eval_device(dev[i], p, &ok, &raw);
     if (!ok) t = -1;
@@ -160,7 +166,8 @@ enum { ACC_DS = 0, ACC_RS = 1, ACC_FEAS = 2, ACC_MAX = 3, ACC_DONE = 4, ACC_TIES
 
 // one matched node (record k): the restored row re-evaluated, Reservation Filter, NominateReservation, raw Score
 __device__ __forceinline__ void matched_one(const MirrorView& m, const PodVec* __restrict__ pods, const Profile& pf,
-                                            int prod_cols, const ExtPod& p, const ExtRec* __restrict__ recs,
+                                            int prod_cols, const DevNode* __restrict__ dev, const ExtPod& p,
+                                            const ExtRec* __restrict__ recs,
                                             const ExtRes* __restrict__ res, int k, int32_t* tot, int16_t* rs,
                                             int32_t* nominated) {
   const ExtRec& rc = recs[k];
@@ -175,6 +182,7 @@ __device__ __forceinline__ void matched_one(const MirrorView& m, const PodVec* _
   r.free_pods += rc.dpods;
   const PairOut o = eval_pair<false, true>(r, pods[0], pf, m);
   int32_t t = total_score(o, pf);
+  if (t >= 0 && p.gpu_names && !fit_names_ok(dev[i], p)) t = -1;   // Fit's scalars are not restored by reservations
   // Reservation Filter: a required pod needs a satisfying matched reservation (filterWithReservations)
   if (t >= 0 && p.required) {
     bool any = false;
@@ -208,7 +216,8 @@ __device__ __forceinline__ void matched_one(const MirrorView& m, const PodVec* _
 // One workgroup over the matched records, then PreScore's preferred node: the first feasible matched node (node
 // order) with the lowest reservation order (findMostPreferredReservationByOrder, scoring.go:89-99) -> acc[ACC_PREF].
 __global__ __launch_bounds__(SEL_BLOCK) void ext_matched_kernel(MirrorView m, const PodVec* __restrict__ pods,
-                                                                Profile pf, int prod_cols, const ExtPod* __restrict__ pp,
+                                                                Profile pf, int prod_cols, const DevNode* __restrict__ dev,
+                                                                const ExtPod* __restrict__ pp,
                                                                 const ExtRec* __restrict__ recs,
                                                                 const ExtRes* __restrict__ res, int nrec, int32_t* tot,
                                                                 int16_t* rs, int32_t* nominated, int32_t* acc) {
@@ -218,7 +227,7 @@ __global__ __launch_bounds__(SEL_BLOCK) void ext_matched_kernel(MirrorView m, co
   int64_t so = INT64_MAX;
   int32_t pn = -1;
   for (int k = threadIdx.x; k < nrec; k += SEL_BLOCK) {
-    matched_one(m, pods, pf, prod_cols, p, recs, res, k, tot, rs, nominated);
+    matched_one(m, pods, pf, prod_cols, dev, p, recs, res, k, tot, rs, nominated);
     const ExtRec& rc = recs[k];
     if (tot[rc.node] >= 0 && rc.order_min != INT64_MAX && rc.order_min != 0 &&
         (rc.order_min < so || (rc.order_min == so && (int32_t)rc.node < pn))) {
@@ -403,13 +412,13 @@ hipError_t launch_ext_nodes(const DevNode* dev, const int16_t* S, uint32_t n0, u
 }
 
 hipError_t launch_ext_matched(const MirrorView& m, const PodVec* pods, const Profile& pf, int prod_cols,
-                              const ExtPod* pod, const ExtRec* recs, const ExtRes* res, int nrec, int32_t* tot,
+                              const DevNode* dev, const ExtPod* pod, const ExtRec* recs, const ExtRes* res, int nrec, int32_t* tot,
                               int16_t* rs, int32_t* nominated, int32_t* scratch, uint32_t len, hipStream_t st) {
   // scratch: T[len] | acc[ACC_WORDS] | bcnt[blocks]; the accumulators are reset here, before the select passes
   int32_t* acc = scratch + len;
   hipError_t e = hipMemsetAsync(acc, 0, sizeof(int32_t) * ACC_WORDS, st);   // acc[ACC_MAX] holds max + 1
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(ext_matched_kernel, dim3(1), dim3(SEL_BLOCK), 0, st, m, pods, pf, prod_cols, pod, recs, res, nrec,
+  hipLaunchKernelGGL(ext_matched_kernel, dim3(1), dim3(SEL_BLOCK), 0, st, m, pods, pf, prod_cols, dev, pod, recs, res, nrec,
                      tot, rs, nominated, acc);
   return hipGetLastError();
 }

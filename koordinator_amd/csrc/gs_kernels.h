@@ -154,5 +154,6 @@ int64_t host_tiebreak_position(uint64_t seed, uint64_t seq, int64_t T);
 hipError_t launch_probe(int mode, const MirrorView& m, const Profile& pf, const PodVec* pods, int npods,
                         const uint32_t* nodes, const int32_t* pod_of, uint32_t n, int prod_cols, int32_t* scores,
                         uint64_t* cycles, hipStream_t st);
+hipError_t launch_merge_probe(const gs_merge_case* cases, int n, gs_merge_result* out, hipStream_t st);
 
 }  // namespace gs

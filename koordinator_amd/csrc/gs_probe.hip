@@ -89,4 +89,24 @@ hipError_t launch_probe(int mode, const MirrorView& m, const Profile& pf, const 
   return hipGetLastError();
 }
 
+// The device's topology-manager Merge (gs_numa_dev.h merge_hint_lists, the code every NUMA-policy pair evaluation runs)
+// on given inputs, one case per thread: the policy_test.go vectors driven through the device merge directly.
+__global__ void __launch_bounds__(64) merge_probe_kernel(const gs_merge_case* __restrict__ cs, int n,
+                                                         gs_merge_result* __restrict__ out) {
+  const int i = blockIdx.x * 64 + threadIdx.x;
+  if (i >= n) return;
+  const gs_merge_case c = cs[i];
+  auto score_at = [&](int mi) -> int32_t { return c.score[mi]; };
+  bool aff_has = false;
+  uint32_t aff = 0;
+  const bool admit = merge_hint_lists(c.totc, c.lc, c.totm, c.lm, c.nz, c.policy, c.nil_hints != 0, c.has_cpu != 0,
+                                      c.has_mem != 0, c.tot_c_any != 0, c.tot_m_any != 0, score_at, aff_has, aff);
+  out[i] = gs_merge_result{admit ? 1 : 0, aff_has ? 1 : 0, aff, 0};
+}
+
+hipError_t launch_merge_probe(const gs_merge_case* cases, int n, gs_merge_result* out, hipStream_t st) {
+  hipLaunchKernelGGL(merge_probe_kernel, dim3((n + 63) / 64), dim3(64), 0, st, cases, n, out);
+  return hipGetLastError();
+}
+
 }  // namespace gs

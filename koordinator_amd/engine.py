@@ -239,6 +239,13 @@ class Engine:
             self._chk(rc, "gs_debug_mirror_check")
         return rc
 
+    def numa_merge(self, cases):
+        """Diagnostics: the device's topology-manager Merge on gs_merge_case records (gs_debug_numa_merge)."""
+        cases = np.ascontiguousarray(cases, dtype=abi.MERGE_CASE_DTYPE)
+        out = np.zeros(len(cases), abi.MERGE_RESULT_DTYPE)
+        self._chk(lib().gs_debug_numa_merge(self._h, abi.ptr(cases), len(cases), abi.ptr(out)), "gs_debug_numa_merge")
+        return out
+
     def pair_probe(self, pods, nodes, pod_of, mode: int):
         """Diagnostics: (scores, cycles) of the commit kernel's pair evaluation on mirror rows (gs_debug_pair_probe)."""
         pods = np.ascontiguousarray(pods, dtype=abi.POD_DTYPE)
