@@ -148,6 +148,7 @@ def main() -> None:
     ap.add_argument("--transport", choices=["rccl", "gloo"], default="rccl",
                     help="several ranks: RCCL all-gather (production) or gloo through the host-callback transport")
     ap.add_argument("--share-gpu", action="store_true", help="every rank on device 0 (gloo rehearsal on one GPU)")
+    ap.add_argument("--sync", action="store_true", help="one blocking gs_schedule per step (no submission ahead)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -233,9 +234,20 @@ def main() -> None:
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     placed = 0
-    for s in range(args.warmup, args.warmup + args.steps):
-        out = run(s * P, (s + 1) * P)
-        placed += int((out["node"] >= 0).sum())
+    if args.sync or c5 or world > 1 or args.sample_pct is not None:
+        for s in range(args.warmup, args.warmup + args.steps):
+            out = run(s * P, (s + 1) * P)
+            placed += int((out["node"] >= 0).sum())
+    else:
+        # each step's pods are submitted before the previous step is waited for (gs_schedule_submit): the batch
+        # pipeline runs on across steps, as a scheduler draining its queue chunk by chunk
+        s0 = args.warmup
+        h = eng.schedule_submit(pods[s0 * P:(s0 + 1) * P], seq[s0 * P:(s0 + 1) * P])
+        for s in range(s0 + 1, args.warmup + args.steps + 1):
+            h2 = eng.schedule_submit(pods[s * P:(s + 1) * P], seq[s * P:(s + 1) * P]) if s < args.warmup + args.steps else None
+            out = eng.schedule_wait(h)
+            placed += int((out["node"] >= 0).sum())
+            h = h2
     eng.synchronize()
     torch.cuda.synchronize()
     if world > 1:
@@ -348,6 +360,9 @@ def main() -> None:
                              f"{P} pods/step, NodeResourcesFit(LeastAllocated)+LoadAwareScheduling filter+score, "
                              "selectHost, assume+Reserve"),
                 "nodes": n_nodes, "pods_per_step": P, "batch": args.batch,
+                "submission": "blocking gs_schedule per step" if (args.sync or c5 or world > 1 or
+                                                                  args.sample_pct is not None)
+                              else "gs_schedule_submit one step ahead (the batch pipeline runs across steps)",
                 "parallelism": f"node-shard x{world}, commit replicated on every rank" +
                                (" (gloo host-callback all-gather, every rank on one GPU: a rehearsal, not a scaling "
                                 "point)" if args.share_gpu else ""),

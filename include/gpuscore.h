@@ -417,6 +417,18 @@ int gs_evaluate(gs_ctx* ctx, const gs_pod* pods, uint32_t npods, int16_t* scores
  * assume (NodeInfo.AddPod) -> Reserve (LoadAware podAssignCache.assign, timestamp = now).
  * seq[i] keys pod i's tie-break stream. Multi-GPU: every rank passes the same pods and gets the same out[]. */
 int gs_schedule(gs_ctx* ctx, const gs_pod* pods, uint32_t npods, const uint64_t* seq, gs_placement* out);
+/* gs_schedule, asynchronously: the pods join the scheduling stream behind every earlier submission (the queue order
+ * across submissions is the order of the calls; results are those of one gs_schedule over their concatenation), and
+ * the batch pipeline keeps running across submissions — while one submission's last batch commits, the next one's
+ * first batch is evaluated and the host applies the finished batch's placements. pods / seq are copied; out must stay
+ * valid until gs_schedule_wait(ticket) returns. Every other call on ctx first waits until all submissions are complete
+ * (a scheduler submits the next queue chunk, then waits for the previous one). One rank, no node sampling. Returns
+ * GS_OK and the submission's ticket, or an error (invalid pod, no mirror yet) with nothing submitted. */
+int gs_schedule_submit(gs_ctx* ctx, const gs_pod* pods, uint32_t npods, const uint64_t* seq, gs_placement* out,
+                       uint64_t* ticket);
+/* Blocks until submission `ticket` is complete: its gs_schedule result. An error fails every later submission
+ * (GS_ESTATE), leaving the context as a failed gs_schedule would. */
+int gs_schedule_wait(gs_ctx* ctx, uint64_t ticket);
 
 /* ---- NodeNUMAResource state ---- */
 /* Register a CPUTopology; returns its id in *id (identical topologies may share one id). */

@@ -316,6 +316,8 @@ SIGNATURES = {
     "gs_pods_unassign": (C.c_int, [P, P, P, u32]),
     "gs_evaluate": (C.c_int, [P, P, u32, P, P, P]),
     "gs_schedule": (C.c_int, [P, P, u32, P, P]),
+    "gs_schedule_submit": (C.c_int, [P, P, u32, P, P, C.POINTER(u64)]),
+    "gs_schedule_wait": (C.c_int, [P, u64]),
     "gs_comm_unique_id": (C.c_int, [P]),
     "gs_comm_init_rccl": (C.c_int, [P, P, C.c_int, C.c_int]),
     "gs_comm_init_callback": (C.c_int, [P, C.c_int, C.c_int, ALLGATHER_FN, P]),

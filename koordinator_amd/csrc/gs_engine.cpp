@@ -20,6 +20,11 @@
 #include <unordered_map>
 #include <unordered_set>
 #include <vector>
+#include <condition_variable>
+#include <deque>
+#include <memory>
+#include <mutex>
+#include <thread>
 
 #include "../../include/gpuscore.h"
 #include "gs_ext.h"
@@ -67,9 +72,31 @@ Vec2 usage_of(const gs_usage& u) {
 
 }  // namespace
 
+// ---- asynchronous submissions (gs_schedule_submit / gs_schedule_wait): a worker thread runs schedule_stream over
+// the submitted runs in order, taking the next run while the current one's last batch is in flight
+struct AsyncRun {
+  std::vector<gs_pod> pods;
+  std::vector<uint64_t> seq;
+  gs_placement* out = nullptr;
+  uint64_t ticket = 0;
+  int rc = 1;   // 1: not complete
+  std::string err;
+};
+struct AsyncQueue {
+  std::thread th;
+  std::mutex mu;
+  std::condition_variable cv_work, cv_done;
+  std::deque<std::shared_ptr<AsyncRun>> pending;                  // submitted, not yet taken by the worker
+  std::unordered_map<uint64_t, std::shared_ptr<AsyncRun>> runs;   // submitted, not yet waited for
+  uint64_t next_ticket = 1;
+  bool busy = false, stop = false;
+};
+
+
 struct gs_ctx {
   gs_config cfg{};
   std::string err;
+  std::unique_ptr<AsyncQueue> aq;   // gs_schedule_submit's worker (created by the first submission)
   uint32_t N = 0, npad = 0;
   hipStream_t st = nullptr;
   hipStream_t st2 = nullptr;                // side stream: eval_kernel beside eval_numa_kernel
@@ -190,6 +217,9 @@ struct gs_ctx {
   std::vector<uint64_t> xres_uid;
   uint32_t xrec_cap = 0, xres_cap = 0;
 };
+
+int quiesce(gs_ctx* c);   // the async submissions' worker is idle (gs_schedule_submit)
+void async_stop(gs_ctx* c);
 
 namespace {
 
@@ -557,21 +587,37 @@ PodVec prep_pod(const gs_ctx* c, const gs_pod& p) {
   return v;
 }
 
-int validate_pod(gs_ctx* c, const gs_pod& p) {
+// a pod the device path takes (msg: why not); no context state written (gs_schedule_submit runs it beside the worker)
+int validate_pod_msg(bool numa_on, const gs_pod& p, char* msg, size_t len) {
   for (int s = 0; s < GS_NUM_RES; ++s)
-    if (!in_range(p.requests[s]) || p.requests[s] < 0 || !in_range(p.limits[s]) || p.limits[s] < 0)
-      return fail(c, GS_EUNSUPPORTED, "pod resource slot %d outside the exact range [0, 2^53)", s);
-  if (p.requests[GS_RES_RESERVED] || (p.request_mask & 0x80u)) return fail(c, GS_EINVAL, "resource slot 7 is reserved");
-  if (c->numa_on) {
+    if (!in_range(p.requests[s]) || p.requests[s] < 0 || !in_range(p.limits[s]) || p.limits[s] < 0) {
+      snprintf(msg, len, "pod resource slot %d outside the exact range [0, 2^53)", s);
+      return GS_EUNSUPPORTED;
+    }
+  if (p.requests[GS_RES_RESERVED] || (p.request_mask & 0x80u)) {
+    snprintf(msg, len, "resource slot 7 is reserved");
+    return GS_EINVAL;
+  }
+  if (numa_on) {
     for (int s = 2; s < 7; ++s)
-      if ((p.request_mask >> s & 1) && p.requests[s] == 0)
-        return fail(c, GS_EUNSUPPORTED, "NodeNUMAResource: a zero-valued request key other than cpu/memory (slot %d) "
-                    "is not supported on the device path", s);
+      if ((p.request_mask >> s & 1) && p.requests[s] == 0) {
+        snprintf(msg, len, "NodeNUMAResource: a zero-valued request key other than cpu/memory (slot %d) is not "
+                 "supported on the device path", s);
+        return GS_EUNSUPPORTED;
+      }
     if (p.required_cpu_bind_policy < 0 || p.required_cpu_bind_policy > 4 || p.preferred_cpu_bind_policy < 0 ||
-        p.preferred_cpu_bind_policy > 4 || p.preferred_cpu_exclusive_policy < 0 || p.preferred_cpu_exclusive_policy > 2)
-      return fail(c, GS_EINVAL, "pod cpu bind / exclusive policy out of range");
+        p.preferred_cpu_bind_policy > 4 || p.preferred_cpu_exclusive_policy < 0 || p.preferred_cpu_exclusive_policy > 2) {
+      snprintf(msg, len, "pod cpu bind / exclusive policy out of range");
+      return GS_EINVAL;
+    }
   }
   return GS_OK;
+}
+
+int validate_pod(gs_ctx* c, const gs_pod& p) {
+  char msg[256];
+  const int rc = validate_pod_msg(c->numa_on, p, msg, sizeof msg);
+  return rc ? fail(c, rc, "%s", msg) : GS_OK;
 }
 
 void mark_dirty(gs_ctx* c, uint32_t i) {
@@ -1635,6 +1681,7 @@ int gs_create(const gs_config* cfg, gs_ctx** out) {
 
 int gs_destroy(gs_ctx* c) {
   if (!c) return GS_EINVAL;
+  async_stop(c);
   for (void* p : {(void*)c->d_dev, (void*)c->d_xpod, (void*)c->d_xrec, (void*)c->d_xres, (void*)c->d_xtot,
                   (void*)c->d_xds, (void*)c->d_xrs, (void*)c->d_xnom, (void*)c->d_xT, (void*)c->d_xout})
     if (p) (void)hipFree(p);
@@ -1733,10 +1780,15 @@ int gs_destroy(gs_ctx* c) {
   return GS_OK;
 }
 
-const char* gs_last_error(gs_ctx* c) { return c ? c->err.c_str() : "nil context"; }
+const char* gs_last_error(gs_ctx* c) {
+  if (!c) return "nil context";
+  quiesce(c);
+  return c->err.c_str();
+}
 
 int gs_set_now(gs_ctx* c, int64_t now) {
   if (!c) return GS_EINVAL;
+  quiesce(c);
   if (now != c->now) c->prep_stale = true;
   c->now = now;
   return GS_OK;
@@ -1744,6 +1796,7 @@ int gs_set_now(gs_ctx* c, int64_t now) {
 
 int gs_nodes_upsert(gs_ctx* c, const uint32_t* idx, const gs_node* nodes, uint32_t n) {
   if (!c || (!nodes && n)) return GS_EINVAL;
+  quiesce(c);
   for (uint32_t j = 0; j < n; ++j) {
     uint32_t i = idx ? idx[j] : j;
     if (i >= c->N) return fail(c, GS_EINVAL, "node index %u >= %u", i, c->N);
@@ -1759,6 +1812,7 @@ int gs_nodes_upsert(gs_ctx* c, const uint32_t* idx, const gs_node* nodes, uint32
 int gs_node_metrics_upsert(gs_ctx* c, const uint32_t* idx, const gs_node_metric* m, uint32_t n,
                            const gs_pod_metric* pm, const uint32_t* off) {
   if (!c || (!m && n)) return GS_EINVAL;
+  quiesce(c);
   for (uint32_t j = 0; j < n; ++j) {
     uint32_t i = idx ? idx[j] : j;
     if (i >= c->N) return fail(c, GS_EINVAL, "node index %u >= %u", i, c->N);
@@ -1777,6 +1831,7 @@ int gs_node_metrics_upsert(gs_ctx* c, const uint32_t* idx, const gs_node_metric*
 
 int gs_pods_assign(gs_ctx* c, const uint32_t* node_idx, const gs_pod* pods, const int64_t* ts, uint32_t n) {
   if (!c || (n && (!node_idx || !pods))) return GS_EINVAL;
+  quiesce(c);
   for (uint32_t j = 0; j < n; ++j) {
     uint32_t i = node_idx[j];
     if (i >= c->N) return fail(c, GS_EINVAL, "node index %u >= %u", i, c->N);
@@ -1790,6 +1845,7 @@ int gs_pods_assign(gs_ctx* c, const uint32_t* node_idx, const gs_pod* pods, cons
 
 int gs_pods_unassign(gs_ctx* c, const uint32_t* node_idx, const gs_pod* pods, uint32_t n) {
   if (!c || (n && (!node_idx || !pods))) return GS_EINVAL;
+  quiesce(c);
   for (uint32_t j = 0; j < n; ++j) {
     uint32_t i = node_idx[j];
     if (i >= c->N) return fail(c, GS_EINVAL, "node index %u >= %u", i, c->N);
@@ -1803,6 +1859,7 @@ int gs_pods_unassign(gs_ctx* c, const uint32_t* node_idx, const gs_pod* pods, ui
 
 int gs_pods_on_event(gs_ctx* c, int event, const int32_t* node_idx, const gs_pod* pods, uint32_t n) {
   if (!c || (n && (!node_idx || !pods))) return GS_EINVAL;
+  quiesce(c);
   if (event < GS_POD_EVENT_ADD || event > GS_POD_EVENT_DELETE) return fail(c, GS_EINVAL, "unknown pod event %d", event);
   for (uint32_t j = 0; j < n; ++j) {
     const int32_t i = node_idx[j];
@@ -1819,6 +1876,7 @@ int gs_pods_on_event(gs_ctx* c, int event, const int32_t* node_idx, const gs_pod
 
 int gs_assign_cache_get(gs_ctx* c, uint32_t node, uint64_t* uids, int64_t* ts, uint32_t cap) {
   if (!c || node >= c->N) return GS_EINVAL;
+  quiesce(c);
   std::vector<std::pair<uint64_t, int64_t>> v;
   for (const auto& kv : c->nodes[node].assigned) v.push_back({kv.first, kv.second.ts});
   std::sort(v.begin(), v.end());
@@ -1832,6 +1890,7 @@ int gs_assign_cache_get(gs_ctx* c, uint32_t node, uint64_t* uids, int64_t* ts, u
 int gs_evaluate(gs_ctx* c, const gs_pod* pods, uint32_t npods, int16_t* scores, uint16_t* codes,
                 int16_t* plugin_scores) {
   if (!c || (npods && !pods)) return GS_EINVAL;
+  quiesce(c);
   int rc = ready(c);
   if (rc) return rc;
   if ((rc = flush_rows(c))) return rc;
@@ -1906,99 +1965,287 @@ bool uid_overlap(const gs_pod* a, int na, const gs_pod* b, int nb) {
 }
 }  // namespace
 
-int gs_schedule(gs_ctx* c, const gs_pod* pods, uint32_t npods, const uint64_t* seq, gs_placement* out) {
-  if (!c || (npods && (!pods || !out))) return GS_EINVAL;
-  int rc = ready(c);
-  if (rc) return rc;
-  for (uint32_t i = 0; i < npods; ++i)
-    if ((rc = validate_pod(c, pods[i]))) return rc;
-  // Pipelining: while batch [i, i+b) runs, the next batch is staged and enqueued behind it on the stream
-  // (other slot). Its commit kernel checks on the device that the batch before committed all its pods with no
-  // host-side Reserve pending, else it is a no-op; the host only keeps it when the same holds on its side.
-  // Every rank takes the same decisions (replicated host state), so speculative exchanges pair up; with the
-  // host-callback transport the speculative pass's exchange waits for the current batch (no overlap, same result).
+extern "C++" {
+namespace {
+// A contiguous run of the pod stream: one gs_schedule call or one gs_schedule_submit.
+struct PodRun {
+  const gs_pod* pods = nullptr;
+  const uint64_t* seq = nullptr;
+  gs_placement* out = nullptr;
+  uint32_t n = 0;
+  void* tag = nullptr;
+};
+
+// The scheduleOne loop over the pod stream, batch by batch. Pipelining: while batch [i, i+b) runs, the next batch is
+// staged and enqueued behind it on the stream (other slot). Its commit kernel checks on the device that the batch
+// before committed all its pods with no host-side Reserve pending, else it is a no-op; the host only keeps it when the
+// same holds on its side. The next batch may be the first of the next run (next_run: the run after the current one
+// if it is already known), so the pipeline continues across runs. Every rank takes the same decisions (replicated
+// host state), so speculative exchanges pair up; with the host-callback transport the speculative pass's exchange
+// waits for the current batch (no overlap, same result). run_done(run, rc): the run's placements are all written
+// (rc 0), or it failed; on an error the current run gets the error and a run already taken from next_run GS_ESTATE.
+template <class Next, class Done>
+int schedule_stream(gs_ctx* c, PodRun run, Next&& next_run, Done&& run_done) {
   static const bool no_spec = getenv("GS_NO_PIPELINE") && getenv("GS_NO_PIPELINE")[0] == '1';
   const bool can_spec = !no_spec;
-  uint32_t i = 0;
-  bool inflight = false, cur_special = false, spec_ok = true;
-  int cur_b = 0;
+  PodRun nxt{};
+  bool have_nxt = false;
   auto drain = [&]() {
     (void)hipStreamSynchronize(c->st);
     (void)hipStreamSynchronize(c->st_ev);
     (void)hipStreamSynchronize(c->st_rb);   // a voided or in-flight batch's readback into the pinned buffers
   };
-  while (i < npods) {
-    if (!inflight) {
-      if ((rc = flush_rows(c))) return rc;
-      if (c->prep_stale && (rc = node_prep(c))) return rc;
-      cur_b = batch_len(c, pods, i, npods, &cur_special);
-      // (a cpuset pod whose node is outside the device cpuset scope ends the batch inside the commit kernel)
-      if ((rc = stage_batch(c, pods, seq, i, cur_b, false))) return rc;
-      if ((rc = launch_batch(c, cur_b, nullptr))) return rc;
-    }
-    bool spec = false;
-    int nb = 0;
-    const uint32_t j = i + cur_b;
-    if (can_spec && spec_ok && !cur_special && j < npods && c->dirty_list.empty() && !c->prep_stale) {
-      bool sf = false;
-      nb = batch_len(c, pods, j, npods, &sf);
-      if (!sf && !uid_overlap(pods + i, cur_b, pods + j, nb)) {
-        const int32_t* prev = c->d_committed;
-        const PlacementDev* prev_out = c->d_out;
-        const int here = c->cur_slot;
-        bind_slot(c, 1 - here);
-        rc = stage_batch(c, pods, seq, j, nb, true);
-        if (!rc) rc = launch_batch(c, nb, prev, prev_out, cur_b);
-        bind_slot(c, here);
-        if (rc) { drain(); return rc; }
-        spec = true;
+  auto body = [&]() -> int {
+    int rc = GS_OK;
+    uint32_t i = 0;
+    bool inflight = false, cur_special = false, spec_ok = true;
+    int cur_b = 0;
+    for (;;) {
+      if (i == run.n) {   // the run is complete; the next one (its first batch may be in flight already)
+        run_done(run, GS_OK);
+        if (!have_nxt) have_nxt = next_run(&nxt);
+        if (!have_nxt) break;
+        run = nxt;
+        have_nxt = false;
+        i = 0;
+        continue;
       }
-    }
-    spec_ok = true;
-    int committed = 0;
-    rc = finish_batch(c, cur_b, spec, &committed);
-    if (rc == GS_REDO) {   // pod 0 needs the full-row path, the speculative pass (void) overwrote its lists: re-run
-      drain();
-      if ((rc = stage_batch(c, pods, seq, i, cur_b, false))) return rc;
-      if ((rc = launch_batch(c, cur_b, nullptr))) return rc;
-      inflight = true;
-      spec_ok = false;
-      continue;
-    }
-    if (rc) { if (spec) drain(); return rc; }
-    const bool host_work = c->h_committed[1] != 1;   // the device-side continuation flag the speculative pass read
-    for (int k = 0; k < committed; ++k) {
-      const PlacementDev& pd = c->h_out[k];
-      gs_placement& o = out[i + k];
-      o.node = pd.node;
-      o.feasible = pd.feasible;
-      o.score = pd.node >= 0 ? pd.score : 0;
-      o.ties = pd.node >= 0 ? pd.ties : 0;
-      o.flags = pd.flags & ~PL_INTERNAL_FLAGS;
-      if (pd.flags & GS_PLACED_SLOWPATH) c->stats.slowpath_pods += 1;   // resolved from its whole score row
-      if ((rc = numa_reserve(c, pods[i + k], c->h_pods[k], pd))) { if (spec) drain(); return rc; }
-      apply_placement(c, pods[i + k], pd.node, cur_special);
-    }
-    c->stats.pods += committed;
-    c->stats_all_pods += committed;
-    i += committed;
-    inflight = false;
-    if (spec) {
-      if (!host_work && committed == cur_b) {
-        if (!c->dirty_list.empty() || c->prep_stale) {
-          drain();
-          return fail(c, GS_ESTATE, "speculative batch ran while host rows were pending");
-        }
-        bind_slot(c, 1 - c->cur_slot);
-        cur_b = nb;
-        cur_special = false;
-        inflight = true;
+      const gs_pod* pods = run.pods;
+      if (!inflight) {
+        if ((rc = flush_rows(c))) return rc;
+        if (c->prep_stale && (rc = node_prep(c))) return rc;
+        cur_b = batch_len(c, pods, i, run.n, &cur_special);
+        // (a cpuset pod whose node is outside the device cpuset scope ends the batch inside the commit kernel)
+        if ((rc = stage_batch(c, pods, run.seq, i, cur_b, false))) return rc;
+        if ((rc = launch_batch(c, cur_b, nullptr))) return rc;
+      }
+      // the batch after this one: in this run, or the first of the next run
+      const gs_pod* np = nullptr;
+      const uint64_t* ns = nullptr;
+      uint32_t nj = 0, nn = 0;
+      const uint32_t j = i + cur_b;
+      if (j < run.n) {
+        np = pods; ns = run.seq; nj = j; nn = run.n;
       } else {
-        drain();   // its commit kernel was a no-op
+        if (!have_nxt) have_nxt = next_run(&nxt);
+        if (have_nxt && nxt.n) { np = nxt.pods; ns = nxt.seq; nn = nxt.n; }
       }
+      bool spec = false;
+      int nb = 0;
+      if (can_spec && spec_ok && !cur_special && np && c->dirty_list.empty() && !c->prep_stale) {
+        bool sf = false;
+        nb = batch_len(c, np, nj, nn, &sf);
+        if (!sf && !uid_overlap(pods + i, cur_b, np + nj, nb)) {
+          const int32_t* prev = c->d_committed;
+          const PlacementDev* prev_out = c->d_out;
+          const int here = c->cur_slot;
+          bind_slot(c, 1 - here);
+          rc = stage_batch(c, np, ns, nj, nb, true);
+          if (!rc) rc = launch_batch(c, nb, prev, prev_out, cur_b);
+          bind_slot(c, here);
+          if (rc) { drain(); return rc; }
+          spec = true;
+        }
+      }
+      spec_ok = true;
+      int committed = 0;
+      rc = finish_batch(c, cur_b, spec, &committed);
+      if (rc == GS_REDO) {   // pod 0 needs the full-row path, the speculative pass (void) overwrote its lists: re-run
+        drain();
+        if ((rc = stage_batch(c, pods, run.seq, i, cur_b, false))) return rc;
+        if ((rc = launch_batch(c, cur_b, nullptr))) return rc;
+        inflight = true;
+        spec_ok = false;
+        continue;
+      }
+      if (rc) { if (spec) drain(); return rc; }
+      const bool host_work = c->h_committed[1] != 1;   // the device-side continuation flag the speculative pass read
+      for (int k = 0; k < committed; ++k) {
+        const PlacementDev& pd = c->h_out[k];
+        gs_placement& o = run.out[i + k];
+        o.node = pd.node;
+        o.feasible = pd.feasible;
+        o.score = pd.node >= 0 ? pd.score : 0;
+        o.ties = pd.node >= 0 ? pd.ties : 0;
+        o.flags = pd.flags & ~PL_INTERNAL_FLAGS;
+        if (pd.flags & GS_PLACED_SLOWPATH) c->stats.slowpath_pods += 1;   // resolved from its whole score row
+        if ((rc = numa_reserve(c, pods[i + k], c->h_pods[k], pd))) { if (spec) drain(); return rc; }
+        apply_placement(c, pods[i + k], pd.node, cur_special);
+      }
+      c->stats.pods += committed;
+      c->stats_all_pods += committed;
+      i += committed;
+      inflight = false;
+      if (spec) {
+        if (!host_work && committed == cur_b) {
+          if (!c->dirty_list.empty() || c->prep_stale) {
+            drain();
+            return fail(c, GS_ESTATE, "speculative batch ran while host rows were pending");
+          }
+          bind_slot(c, 1 - c->cur_slot);
+          cur_b = nb;
+          cur_special = false;
+          inflight = true;   // (when it is the next run's first batch, i == run.n: the top of the loop moves there)
+        } else {
+          drain();   // its commit kernel was a no-op
+        }
+      }
+    }
+    return flush_rows(c);
+  };
+  const int rc = body();
+  if (rc) {
+    run_done(run, rc);
+    if (have_nxt) run_done(nxt, GS_ESTATE);
+  }
+  return rc;
+}
+
+}  // namespace
+
+namespace {
+void async_worker(gs_ctx* c) {
+  AsyncQueue& q = *c->aq;
+  (void)hipSetDevice(c->cfg.device);
+  std::unique_lock<std::mutex> lk(q.mu);
+  for (;;) {
+    q.cv_work.wait(lk, [&] { return q.stop || !q.pending.empty(); });
+    if (q.pending.empty()) return;   // stop
+    std::shared_ptr<AsyncRun> first = q.pending.front();
+    q.pending.pop_front();
+    q.busy = true;
+    lk.unlock();
+    std::vector<std::shared_ptr<AsyncRun>> taken{first};   // keeps the runs alive while the loop reads them
+    auto as_run = [](const std::shared_ptr<AsyncRun>& r) {
+      PodRun p;
+      p.pods = r->pods.data();
+      p.seq = r->seq.data();
+      p.out = r->out;
+      p.n = (uint32_t)r->pods.size();
+      p.tag = r.get();
+      return p;
+    };
+    auto next = [&](PodRun* out) -> bool {
+      std::lock_guard<std::mutex> g(q.mu);
+      if (q.pending.empty()) return false;
+      taken.push_back(q.pending.front());
+      q.pending.pop_front();
+      *out = as_run(taken.back());
+      return true;
+    };
+    auto done = [&](const PodRun& r, int rc) {
+      AsyncRun* a = static_cast<AsyncRun*>(r.tag);
+      std::lock_guard<std::mutex> g(q.mu);
+      a->rc = rc;
+      if (rc) a->err = c->err;
+      q.cv_done.notify_all();
+    };
+    const int rc = schedule_stream(c, as_run(first), next, done);
+    lk.lock();
+    if (rc) {   // an error fails every later submission (the stream's order is broken)
+      for (auto& r : q.pending) {
+        r->rc = GS_ESTATE;
+        r->err = "an earlier gs_schedule_submit failed: " + c->err;
+      }
+      q.pending.clear();
+    }
+    q.busy = false;
+    q.cv_done.notify_all();
+  }
+}
+}  // namespace
+
+// Every other call on the context waits until the submitted runs are complete (the worker is idle).
+int quiesce(gs_ctx* c) {
+  if (!c || !c->aq) return GS_OK;
+  AsyncQueue& q = *c->aq;
+  std::unique_lock<std::mutex> lk(q.mu);
+  q.cv_done.wait(lk, [&] { return q.pending.empty() && !q.busy; });
+  return GS_OK;
+}
+
+void async_stop(gs_ctx* c) {
+  if (!c->aq) return;
+  quiesce(c);
+  {
+    std::lock_guard<std::mutex> g(c->aq->mu);
+    c->aq->stop = true;
+  }
+  c->aq->cv_work.notify_all();
+  if (c->aq->th.joinable()) c->aq->th.join();
+  c->aq.reset();
+}
+
+}  // extern "C++"
+
+int gs_schedule(gs_ctx* c, const gs_pod* pods, uint32_t npods, const uint64_t* seq, gs_placement* out) {
+  if (!c || (npods && (!pods || !out))) return GS_EINVAL;
+  quiesce(c);
+  int rc = ready(c);
+  if (rc) return rc;
+  for (uint32_t i = 0; i < npods; ++i)
+    if ((rc = validate_pod(c, pods[i]))) return rc;
+  PodRun run;
+  run.pods = pods;
+  run.seq = seq;
+  run.out = out;
+  run.n = npods;
+  return schedule_stream(c, run, [](PodRun*) { return false; }, [](const PodRun&, int) {});
+}
+
+int gs_schedule_submit(gs_ctx* c, const gs_pod* pods, uint32_t npods, const uint64_t* seq, gs_placement* out,
+                       uint64_t* ticket) {
+  if (!c || !ticket || (npods && (!pods || !out))) return GS_EINVAL;
+  if (c->nranks > 1) return fail(c, GS_EUNSUPPORTED, "gs_schedule_submit: one rank (use gs_schedule with several)");
+  if (c->window_k) return fail(c, GS_EUNSUPPORTED, "gs_schedule_submit: not with node sampling");
+  auto r = std::make_shared<AsyncRun>();
+  // checks that write nothing (the worker may be running): on an error, wait for it, then report
+  for (uint32_t i = 0; i < c->N; ++i)
+    if (!c->nodes[i].valid) {
+      quiesce(c);
+      return fail(c, GS_ESTATE, "node %u was never upserted", i);
+    }
+  char msg[256];
+  for (uint32_t i = 0; i < npods; ++i) {
+    const int rc = validate_pod_msg(c->numa_on, pods[i], msg, sizeof msg);
+    if (rc) {
+      quiesce(c);
+      return fail(c, rc, "%s", msg);
     }
   }
-  return flush_rows(c);
+  r->pods.assign(pods, pods + npods);
+  r->seq.resize(npods);
+  for (uint32_t i = 0; i < npods; ++i) r->seq[i] = seq ? seq[i] : (uint64_t)i;
+  r->out = out;
+  if (!c->aq) {
+    c->aq = std::make_unique<AsyncQueue>();
+    c->aq->th = std::thread(async_worker, c);
+  }
+  {
+    std::lock_guard<std::mutex> g(c->aq->mu);
+    r->ticket = c->aq->next_ticket++;
+    c->aq->runs[r->ticket] = r;
+    c->aq->pending.push_back(r);
+  }
+  c->aq->cv_work.notify_all();
+  *ticket = r->ticket;
+  return GS_OK;
+}
+
+int gs_schedule_wait(gs_ctx* c, uint64_t ticket) {
+  if (!c || !c->aq) return GS_EINVAL;
+  AsyncQueue& q = *c->aq;
+  std::unique_lock<std::mutex> lk(q.mu);
+  auto it = q.runs.find(ticket);
+  if (it == q.runs.end()) return GS_EINVAL;
+  std::shared_ptr<AsyncRun> r = it->second;
+  q.cv_done.wait(lk, [&] { return r->rc != 1; });
+  q.runs.erase(it);
+  if (r->rc) {
+    q.cv_done.wait(lk, [&] { return q.pending.empty() && !q.busy; });   // the worker has stopped writing c->err
+    c->err = r->err;
+  }
+  return r->rc;
 }
 
 void gs_numa_args_default(gs_numa_args* a) {
@@ -2013,6 +2260,7 @@ void gs_numa_args_default(gs_numa_args* a) {
 
 int gs_topology_register(gs_ctx* c, const gs_cpu_topology* t, int32_t* id) {
   if (!c || !t || !id) return GS_EINVAL;
+  quiesce(c);
   const char* err = nullptr;
   auto topo = make_topo(*t, &err);
   if (!topo) return fail(c, GS_EUNSUPPORTED, "gs_topology_register: %s", err ? err : "invalid topology");
@@ -2030,6 +2278,7 @@ int gs_topology_register(gs_ctx* c, const gs_cpu_topology* t, int32_t* id) {
 
 int gs_nodes_numa_upsert(gs_ctx* c, const uint32_t* idx, const gs_node_numa* nn, uint32_t n) {
   if (!c || (!nn && n)) return GS_EINVAL;
+  quiesce(c);
   for (uint32_t j = 0; j < n; ++j) {
     uint32_t i = idx ? idx[j] : j;
     if (i >= c->N) return fail(c, GS_EINVAL, "node index %u >= %u", i, c->N);
@@ -2058,6 +2307,7 @@ int gs_nodes_numa_upsert(gs_ctx* c, const uint32_t* idx, const gs_node_numa* nn,
 
 int gs_numa_allocations_update(gs_ctx* c, const uint32_t* node_idx, const gs_pod_allocation* a, uint32_t n) {
   if (!c || (n && (!node_idx || !a))) return GS_EINVAL;
+  quiesce(c);
   for (uint32_t j = 0; j < n; ++j) {
     uint32_t i = node_idx[j];
     if (i >= c->N) return fail(c, GS_EINVAL, "node index %u >= %u", i, c->N);
@@ -2079,6 +2329,7 @@ int gs_numa_allocations_update(gs_ctx* c, const uint32_t* node_idx, const gs_pod
 
 int gs_numa_allocations_release(gs_ctx* c, const uint32_t* node_idx, const uint64_t* uids, uint32_t n) {
   if (!c || (n && (!node_idx || !uids))) return GS_EINVAL;
+  quiesce(c);
   for (uint32_t j = 0; j < n; ++j) {
     uint32_t i = node_idx[j];
     if (i >= c->N) return fail(c, GS_EINVAL, "node index %u >= %u", i, c->N);
@@ -2092,6 +2343,7 @@ int gs_numa_allocations_release(gs_ctx* c, const uint32_t* node_idx, const uint6
 
 int gs_numa_allocation_get(gs_ctx* c, uint32_t node, uint64_t uid, gs_pod_allocation* out) {
   if (!c || !out || node >= c->N) return GS_EINVAL;
+  quiesce(c);
   const NumaNode& st = c->numa[node];
   auto it = st.pods.find(uid);
   if (it == st.pods.end()) return 0;
@@ -2115,6 +2367,7 @@ int gs_comm_unique_id(uint8_t out[128]) {
 
 int gs_comm_init_rccl(gs_ctx* c, const uint8_t id[128], int nranks, int rank) {
   if (!c || !id || nranks < 1 || nranks > MAX_RANKS || rank < 0 || rank >= nranks) return GS_EINVAL;
+  quiesce(c);
   if (c->window_k && nranks > 1) return fail(c, GS_EUNSUPPORTED, "node sampling runs on one GPU");
   if (nranks > 1) {
     ncclUniqueId uid;
@@ -2132,6 +2385,7 @@ int gs_comm_init_rccl(gs_ctx* c, const uint8_t id[128], int nranks, int rank) {
 
 int gs_comm_init_callback(gs_ctx* c, int nranks, int rank, gs_allgather_fn fn, void* user) {
   if (!c || !fn || nranks < 1 || nranks > MAX_RANKS || rank < 0 || rank >= nranks) return GS_EINVAL;
+  quiesce(c);
   if (c->window_k && nranks > 1) return fail(c, GS_EUNSUPPORTED, "node sampling runs on one GPU");
   c->cb = fn;
   c->cb_user = user;
@@ -2144,6 +2398,7 @@ int gs_comm_init_callback(gs_ctx* c, int nranks, int rank, gs_allgather_fn fn, v
 
 int gs_get_stats(gs_ctx* c, gs_stats* out) {
   if (!c || !out) return GS_EINVAL;
+  quiesce(c);
   *out = c->stats;
   out->next_start_node_index = c->next_start;
   return GS_OK;
@@ -2151,6 +2406,7 @@ int gs_get_stats(gs_ctx* c, gs_stats* out) {
 
 int gs_reset_stats(gs_ctx* c) {
   if (!c) return GS_EINVAL;
+  quiesce(c);
   uint64_t rb = c->stats.node_row_bytes;   // keep
   c->stats = gs_stats{};
   c->stats.node_row_bytes = rb;
@@ -2161,6 +2417,7 @@ int gs_reset_stats(gs_ctx* c) {
 
 int gs_synchronize(gs_ctx* c) {
   if (!c) return GS_EINVAL;
+  quiesce(c);
   HIP_TRY(c, hipStreamSynchronize(c->st_ev));
   HIP_TRY(c, hipStreamSynchronize(c->st));
   HIP_TRY(c, hipStreamSynchronize(c->st_rb));
@@ -2171,6 +2428,7 @@ int gs_synchronize(gs_ctx* c) {
 // host snapshot): drain the streams, re-derive every node row from the host state into HBM, re-run node prep.
 int gs_reset(gs_ctx* c) {
   if (!c) return GS_EINVAL;
+  quiesce(c);
   (void)hipStreamSynchronize(c->st);
   (void)hipStreamSynchronize(c->st_ev);
   (void)hipStreamSynchronize(c->st2);
@@ -2194,6 +2452,7 @@ int gs_reset(gs_ctx* c) {
 
 int gs_debug_verify_cpuset(gs_ctx* c, int on) {
   if (!c) return GS_EINVAL;
+  quiesce(c);
   c->verify_cpuset = on != 0;
   return GS_OK;
 }
@@ -2204,6 +2463,7 @@ int gs_debug_pair_probe(gs_ctx* c, const gs_pod* pods, uint32_t npods, const uin
                         uint32_t n, int mode, int32_t* scores, uint64_t* cycles) {
   if (!c || !pods || !nodes || !pod_of || !scores || !cycles || npods == 0 || npods > 64 || mode < 0 || mode > 2)
     return GS_EINVAL;
+  quiesce(c);
   int rc = ready(c);
   if (rc) return rc;
   if ((rc = flush_rows(c))) return rc;
@@ -2244,13 +2504,12 @@ int gs_debug_pair_probe(gs_ctx* c, const gs_pod* pods, uint32_t npods, const uin
 // The device merge on given hint lists (gs_probe.hip merge_probe_kernel).
 int gs_debug_numa_merge(gs_ctx* c, const gs_merge_case* cases, uint32_t n, gs_merge_result* out) {
   if (!c || (n && (!cases || !out))) return GS_EINVAL;
+  quiesce(c);
   for (uint32_t i = 0; i < n; ++i)
     if (cases[i].nz < 1 || cases[i].nz > 4 || cases[i].policy < GS_NUMA_POLICY_NONE ||
         cases[i].policy > GS_NUMA_POLICY_SINGLE_NUMA_NODE)
       return GS_EINVAL;
-  if (!n) return GS_OK;
-  int rc = ready(c);
-  if (rc) return rc;
+  if (!n) return GS_OK;   // (no mirror state involved: the merge's inputs are the cases)
   gs_merge_case* d_c = nullptr;
   gs_merge_result* d_o = nullptr;
   hipError_t e = hipMalloc(&d_c, sizeof(gs_merge_case) * n);
@@ -2269,6 +2528,7 @@ int gs_debug_numa_merge(gs_ctx* c, const gs_merge_case* cases, uint32_t n, gs_me
 // Compares every HBM mirror row against a fresh host derivation; returns the number of mismatching rows.
 int gs_debug_mirror_check(gs_ctx* c) {
   if (!c) return GS_EINVAL;
+  quiesce(c);
   int rc = flush_rows(c);
   if (rc) return rc;
   std::vector<int64_t> d64((size_t)c->npad * NUM_I64_COLS);
@@ -2310,6 +2570,7 @@ void gs_ext_args_default(gs_ext_args* a) {
 
 int gs_ext_configure(gs_ctx* c, const gs_ext_args* a) {
   if (!c || !a) return GS_EINVAL;
+  quiesce(c);
   if (a->enabled & ~(GS_EXT_DEVICESHARE | GS_EXT_RESERVATION)) return fail(c, GS_EINVAL, "unknown extension plugin bits");
   if (a->fit_ignored_gpu_names & ~0x1Fu) return fail(c, GS_EINVAL, "fit_ignored_gpu_names outside the GPU names");
   if (a->fit_ignored_xres & ~((1u << GS_MAX_XRES) - 1u))
@@ -2331,6 +2592,7 @@ int gs_ext_configure(gs_ctx* c, const gs_ext_args* a) {
 
 int gs_node_devices_upsert(gs_ctx* c, const uint32_t* idx, const gs_node_devices* d, uint32_t n) {
   if (!c || (n && !d)) return GS_EINVAL;
+  quiesce(c);
   for (uint32_t k = 0; k < n; ++k) {
     const uint32_t i = idx ? idx[k] : k;
     if (i >= c->N) return fail(c, GS_EINVAL, "node index %u out of range", i);
@@ -2354,6 +2616,7 @@ int gs_node_devices_upsert(gs_ctx* c, const uint32_t* idx, const gs_node_devices
 
 int gs_node_devices_get(gs_ctx* c, uint32_t node, gs_node_devices* out) {
   if (!c || !out || node >= c->N) return GS_EINVAL;
+  quiesce(c);
   *out = c->devs[node];
   return GS_OK;
 }
@@ -2374,6 +2637,7 @@ void rsv_unindex(gs_ctx* c, const gs_reservation& r) {
 
 int gs_reservations_upsert(gs_ctx* c, const gs_reservation* r, uint32_t n) {
   if (!c || (n && !r)) return GS_EINVAL;
+  quiesce(c);
   for (uint32_t k = 0; k < n; ++k) {
     const gs_reservation& x = r[k];
     if (x.node >= c->N) return fail(c, GS_EINVAL, "reservation node %u out of range", x.node);
@@ -2400,6 +2664,7 @@ int gs_reservations_upsert(gs_ctx* c, const gs_reservation* r, uint32_t n) {
 
 int gs_reservations_remove(gs_ctx* c, const uint64_t* uids, uint32_t n) {
   if (!c || (n && !uids)) return GS_EINVAL;
+  quiesce(c);
   for (uint32_t k = 0; k < n; ++k) {
     auto it = c->rsv.find(uids[k]);
     if (it == c->rsv.end()) continue;
@@ -2411,6 +2676,7 @@ int gs_reservations_remove(gs_ctx* c, const uint64_t* uids, uint32_t n) {
 
 int gs_reservation_get(gs_ctx* c, uint64_t uid, gs_reservation* out) {
   if (!c || !out) return GS_EINVAL;
+  quiesce(c);
   auto it = c->rsv.find(uid);
   if (it == c->rsv.end()) return 0;
   *out = it->second;
@@ -2420,6 +2686,7 @@ int gs_reservation_get(gs_ctx* c, uint64_t uid, gs_reservation* out) {
 int gs_schedule_ext(gs_ctx* c, const gs_pod* pods, const gs_pod_ext* ext, uint32_t npods, const uint64_t* seq,
                     gs_placement* out, gs_ext_placement* ext_out) {
   if (!c || (npods && (!pods || !out))) return GS_EINVAL;
+  quiesce(c);
   int rc = ready(c);
   if (rc) return rc;
   for (uint32_t i = 0; i < npods; ++i)

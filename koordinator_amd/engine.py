@@ -112,6 +112,23 @@ class Engine:
         self._chk(lib().gs_schedule(self._h, abi.ptr(pods), len(pods), abi.ptr(seq), abi.ptr(out)), "gs_schedule")
         return out
 
+    def schedule_submit(self, pods, seq=None):
+        """gs_schedule_submit: returns a handle for schedule_wait (the placements array, filled once it completes)."""
+        pods = np.ascontiguousarray(pods, dtype=abi.POD_DTYPE)
+        if seq is None:
+            seq = np.arange(len(pods), dtype=np.uint64)
+        seq = np.ascontiguousarray(seq, dtype=np.uint64)
+        out = np.zeros(len(pods), abi.PLACEMENT_DTYPE)
+        t = C.c_uint64(0)
+        self._chk(lib().gs_schedule_submit(self._h, abi.ptr(pods), len(pods), abi.ptr(seq), abi.ptr(out), C.byref(t)),
+                  "gs_schedule_submit")
+        return (t.value, out)
+
+    def schedule_wait(self, handle):
+        t, out = handle
+        self._chk(lib().gs_schedule_wait(self._h, t), "gs_schedule_wait")
+        return out
+
     def pod_event(self, event: int, node_idx, pods):
         """podAssignCache OnAdd / OnUpdate / OnDelete (node_idx -1 = pod.Spec.NodeName == "")."""
         pods = np.ascontiguousarray(pods, dtype=abi.POD_DTYPE)
