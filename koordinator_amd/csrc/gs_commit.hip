@@ -507,7 +507,9 @@ __global__ void __launch_bounds__(256) commit_pipe_kernel(CommitArgs a) {
         if (f_kind == 1) v = reinterpret_cast<const int64_t*>(f_src)[winner];
         else if (f_kind == 2) v = reinterpret_cast<const int32_t*>(f_src)[winner];
         else if (f_kind == 3) {   // the batch-start Filter's affinity for this pair (own shard, NUMA-policy nodes)
-          v = own ? (int64_t)reinterpret_cast<const uint8_t*>(f_src)[(size_t)p * a.ld + (winner - a.own0)] : -1;
+          const uint8_t b8 = own ? reinterpret_cast<const uint8_t*>(f_src)[(size_t)p * a.ld + (winner - a.own0)]
+                                 : AFF_RECOMPUTE;
+          v = b8 == AFF_RECOMPUTE ? (int64_t)-1 : (int64_t)b8;   // (a patched row's: recomputed)
         } else if (f_kind == 4) v = (int64_t)winner;   // Row.node, Row.pad = 0
         // batch-start scores of the later pods on this row (own shard): S[q][winner], q = p+1 ..
         int16_t so0v = 0, so1v = 0;

@@ -49,10 +49,16 @@ constexpr int SP_WAVES = 8, SP_THREADS = 64 * SP_WAVES;
 constexpr int SP_LAG = 16;       // decided - verified <= SP_LAG (undo log depth)
 constexpr int SP_RES0 = 2, SP_NRES = 2;   // Reserve waves 2, 3 (pod parity)
 constexpr int SP_RS0 = SP_RES0 + SP_NRES, SP_TABLES = SP_WAVES - SP_RS0;   // re-scoring waves, one hint table each
+// Role -> wave index. The CU runs wave w on SIMD w % 4, two waves per SIMD: the selector (wave 0) shares its SIMD with
+// the verifier, the lightest role, instead of a busy re-scoring wave; the Reserve and re-scoring waves fill SIMDs 1-3.
+constexpr int SP_W_VERIFY = 4;
+__device__ __forceinline__ int sp_reserve_index(int wv) { return wv == 2 ? 0 : wv == 3 ? 1 : -1; }
+__device__ __forceinline__ int sp_rescore_index(int wv) { return wv == 1 ? 0 : wv >= 5 ? wv - 4 : -1; }
 constexpr int SP_JOBQ = 32;      // job ring per Reserve wave (<= 3 jobs per pod, <= SP_LAG / 2 + 2 pods in flight)
 constexpr int SP_HASH = 256;     // node -> slot (full-row resolution)
 constexpr int SP_FRESH = 1, SP_FITERR = 2, SP_SLOW = 4, SP_OFFSHARD = 8;   // DecRec.flags
 constexpr uint32_t SP_SPIN_LIMIT = 1u << 24;
+constexpr int SP_NST = 40, SP_STRIDE = 64;   // diagnostics: stamps per wave, the wave's region in a.stamps
 constexpr int16_t SO_UNKNOWN = -2;    // dso: batch-start score of an off-shard fresh row not evaluated yet
 constexpr int16_t SO_UNLISTED = -3;   // a decision's view of such a row not in the pod's list head
 
@@ -77,32 +83,44 @@ struct Job {
 
 __device__ __forceinline__ void sp_sleep() { __builtin_amdgcn_s_sleep(2); }
 
-size_t spec_smem_bytes(int B) {   // the kernel's LDS carve-up, piece by piece with take()'s 16-B rounding (same order)
-  size_t b = 0;
-  auto take = [&](size_t bytes) { b += (bytes + 15) & ~(size_t)15; };
-  take((size_t)B * POD_STRIDE);                     // pods
-  take((size_t)B * sizeof(Row));                    // dirty rows
-  take((size_t)B * B * 2);                          // dsc
-  take((size_t)B * B * 2);                          // dso
-  take((size_t)B * sizeof(CpuStateDev));            // cpu state of the dirty rows
-  take((size_t)B * sizeof(DecRec));
-  take((size_t)SP_LAG * sizeof(UndoRec));
-  take((size_t)SP_TABLES * sizeof(HintTable));
-  for (int i = 0; i < 7; ++i) take((size_t)B * 4);  // final_F, done_ver, has_row, rescored, jobs_left, jobs_all, resv
-  take((size_t)SP_HASH * 4);                        // hkey
-  take((size_t)SP_HASH * 4);                        // hval
-  take((size_t)SP_NRES * SP_JOBQ * sizeof(Job));
-  return b + 64;
-}
+// The kernel's LDS, at fixed offsets sized for MAX_BATCH pods whatever the batch: every array is at a link-time
+// constant address and [pod][slot] rows have the constant stride SB, so no register holds a carve-up pointer and
+// index arithmetic is a shift (the selector wave is instruction-bound; the carve-up pointers used to be SGPRs spilled
+// to VGPR lanes).
+constexpr int SB = MAX_BATCH;
+struct alignas(16) SpecLds {
+  alignas(16) unsigned char pods_b[SB * POD_STRIDE];
+  alignas(16) Row drows[SB];                 // dirty rows
+  alignas(16) int16_t dsc[SB * SB];          // [pod][slot] current score
+  alignas(16) int16_t dso[SB * SB];          // [pod][slot] batch-start score
+  alignas(16) CpuStateDev cst[SB];           // cpu state of the dirty rows
+  alignas(16) DecRec dec[SB];
+  alignas(16) UndoRec undo[SP_LAG];
+  alignas(16) HintTable tables[SP_TABLES];
+  alignas(16) int32_t final_F[SB], done_ver[SB], has_row[SB], rescored[SB], jobs_left[SB], jobs_all[SB], resv[SB];
+  alignas(16) int32_t hkey[SP_HASH], hval[SP_HASH];
+  alignas(16) Job jobq[SP_NRES * SP_JOBQ];
+};
 
-// ST: diagnostic build — per-role cycle sums (s_memtime) into a.stamps: 0 decide, 1 verify, 2 wave 0 waiting,
-// 3 rollbacks, 4 rollback cycles, 5 Reserve busy, 6 Reserve waiting, 7 re-scoring busy, 8 re-scoring waiting,
-// 9 decisions, 10 full-row decisions, 11 full-row cycles, 12 wave 0 total
-template <bool ST>
-__global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
-  uint64_t st_acc[28] = {};
-  uint64_t st_last = ST ? __builtin_amdgcn_s_memtime() : 0;
-  const uint64_t st_t0 = st_last;
+size_t spec_smem_bytes(int) { return sizeof(SpecLds); }
+
+// LDS hand-off words between the roles (namespace scope: the role functions below and the kernel share them)
+__shared__ TopoDev s_topo[SP_NRES];     // per Reserve wave: topology of its last cpuset Reserve
+__shared__ HintTable s_ht0;       // wave 0: rollback re-scoring
+__shared__ uint64_t s_cpuset[SP_NRES][4];
+__shared__ int32_t s_aff[SP_NRES];
+__shared__ int32_t s_decided, s_stop, s_parked, s_finish, s_cut_at, s_err;
+__shared__ int32_t s_werr;        // a verify / Reserve / re-scoring wave's bounded wait expired (its site code)
+__shared__ int32_t s_jq_head[SP_NRES], s_jq_tail[SP_NRES];
+__shared__ int32_t s_verified;    // verifier: pods verified (wave 0 decides at most SP_LAG ahead of it)
+__shared__ int32_t s_rb_req;      // verifier -> wave 0: v + 1 = roll back to pod v (0: none)
+__shared__ int32_t s_rb_at;       // the last rollback's pod (where the parked waves resume)
+__shared__ int32_t s_end_at;      // wave 0: decisions end before this pod (B: every pod)
+__shared__ int32_t s_vend;        // verifier: the batch's committed count (-1: not yet), s_vcut: a host cut ends it
+__shared__ int32_t s_vcut;
+__shared__ int32_t s_committed, s_hostcut, s_nd, s_endwhy;
+__shared__ uint64_t sseq[MAX_BATCH];
+
 #define SPM(i)                                          \
   do {                                                  \
     if (ST) {                                           \
@@ -111,7 +129,19 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
       st_last = t_;                                     \
     }                                                   \
   } while (0)
-  extern __shared__ __align__(16) unsigned char cm[];
+
+__device__ __forceinline__ int32_t ld_acq(const int32_t* p) { return __atomic_load_n(p, __ATOMIC_ACQUIRE); }
+__device__ __forceinline__ void st_rel(int32_t* p, int32_t v) { __atomic_store_n(p, v, __ATOMIC_RELEASE); }
+
+
+// ST: diagnostic build — per-role cycle sums (s_memtime) into a.stamps: 0 decide, 1 verify, 2 wave 0 waiting,
+// 3 rollbacks, 4 rollback cycles, 5 Reserve busy, 6 Reserve waiting, 7 re-scoring busy, 8 re-scoring waiting,
+// 9 decisions, 10 full-row decisions, 11 full-row cycles, 12 wave 0 total
+template <bool ST>
+__global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
+  uint64_t st_acc[SP_NST] = {};
+  uint64_t st_last = ST ? __builtin_amdgcn_s_memtime() : 0;
+  const uint64_t st_t0 = st_last;
   const int B = a.npods;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -119,43 +149,27 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
   const bool numa_on = (a.pf.enabled & 0x30u) != 0;
   const bool multi = a.nranks > 1;   // merged levels of several shards; rows outside [own0, own1) have no S_own
   const uint64_t lt_mask = (1ull << lane) - 1ull;
-  // ---- LDS carve-up
-  unsigned char* cur = cm;
-  auto take = [&](size_t bytes) { unsigned char* p = cur; cur += (bytes + 15) & ~(size_t)15; return p; };
-  unsigned char* pods_b = take((size_t)B * POD_STRIDE);
-  auto pods = [&](int i) -> PodVec& { return *reinterpret_cast<PodVec*>(pods_b + (size_t)i * POD_STRIDE); };
-  Row* drows = reinterpret_cast<Row*>(take((size_t)B * sizeof(Row)));
-  int16_t* dsc = reinterpret_cast<int16_t*>(take((size_t)B * B * 2));   // [pod][slot] current score
-  int16_t* dso = reinterpret_cast<int16_t*>(take((size_t)B * B * 2));   // [pod][slot] batch-start score
-  CpuStateDev* cst = reinterpret_cast<CpuStateDev*>(take((size_t)B * sizeof(CpuStateDev)));
-  DecRec* dec = reinterpret_cast<DecRec*>(take((size_t)B * sizeof(DecRec)));
-  UndoRec* undo = reinterpret_cast<UndoRec*>(take((size_t)SP_LAG * sizeof(UndoRec)));
-  HintTable* tables = reinterpret_cast<HintTable*>(take((size_t)SP_TABLES * sizeof(HintTable)));
-  int32_t* final_F = reinterpret_cast<int32_t*>(take((size_t)B * 4));
-  int32_t* done_ver = reinterpret_cast<int32_t*>(take((size_t)B * 4));   // slot: version whose re-scoring is complete
-  int32_t* has_row = reinterpret_cast<int32_t*>(take((size_t)B * 4));    // slot: row fetched into LDS
-  int32_t* rescored = reinterpret_cast<int32_t*>(take((size_t)B * 4));   // pod: Reserve + re-scoring complete
-  int32_t* jobs_left = reinterpret_cast<int32_t*>(take((size_t)B * 4));  // pod: re-scoring jobs not done (-> done_ver)
-  int32_t* jobs_all = reinterpret_cast<int32_t*>(take((size_t)B * 4));   // pod: every job not done (-> rescored)
-  int32_t* resv = reinterpret_cast<int32_t*>(take((size_t)B * 4));       // pod: its Reserve is applied (or FitError)
-  int32_t* hkey = reinterpret_cast<int32_t*>(take((size_t)SP_HASH * 4));
-  int32_t* hval = reinterpret_cast<int32_t*>(take((size_t)SP_HASH * 4));
-  Job* jobq = reinterpret_cast<Job*>(take((size_t)SP_NRES * SP_JOBQ * sizeof(Job)));   // [Reserve wave][ring]
-  __shared__ TopoDev s_topo[SP_NRES];     // per Reserve wave: topology of its last cpuset Reserve
-  __shared__ HintTable s_ht0;       // wave 0: rollback re-scoring
-  __shared__ uint64_t s_cpuset[SP_NRES][4];
-  __shared__ int32_t s_aff[SP_NRES];
-  __shared__ int32_t s_decided, s_stop, s_parked, s_finish, s_cut_at, s_err;
-  __shared__ int32_t s_werr;        // a verify / Reserve / re-scoring wave's bounded wait expired (its site code)
-  __shared__ int32_t s_jq_head[SP_NRES], s_jq_tail[SP_NRES];
-  __shared__ int32_t s_verified;    // verifier: pods verified (wave 0 decides at most SP_LAG ahead of it)
-  __shared__ int32_t s_rb_req;      // verifier -> wave 0: v + 1 = roll back to pod v (0: none)
-  __shared__ int32_t s_rb_at;       // the last rollback's pod (where the parked waves resume)
-  __shared__ int32_t s_end_at;      // wave 0: decisions end before this pod (B: every pod)
-  __shared__ int32_t s_vend;        // verifier: the batch's committed count (-1: not yet), s_vcut: a host cut ends it
-  __shared__ int32_t s_vcut;
-  __shared__ int32_t s_committed, s_hostcut, s_nd, s_endwhy;
-  __shared__ uint64_t sseq[MAX_BATCH];
+  // ---- LDS (fixed layout, SpecLds)
+  extern __shared__ __align__(16) unsigned char cm[];
+  SpecLds& L = *reinterpret_cast<SpecLds*>(cm);
+  auto pods = [&](int i) -> PodVec& { return *reinterpret_cast<PodVec*>(L.pods_b + (size_t)i * POD_STRIDE); };
+  Row* drows = L.drows;
+  int16_t* dsc = L.dsc;   // [pod][slot], stride SB
+  int16_t* dso = L.dso;
+  CpuStateDev* cst = L.cst;
+  DecRec* dec = L.dec;
+  UndoRec* undo = L.undo;
+  HintTable* tables = L.tables;
+  int32_t* final_F = L.final_F;
+  int32_t* done_ver = L.done_ver;   // slot: version whose re-scoring is complete
+  int32_t* has_row = L.has_row;     // slot: row fetched into LDS
+  int32_t* rescored = L.rescored;   // pod: Reserve + re-scoring complete
+  int32_t* jobs_left = L.jobs_left; // pod: re-scoring jobs not done (-> done_ver)
+  int32_t* jobs_all = L.jobs_all;   // pod: every job not done (-> rescored)
+  int32_t* resv = L.resv;           // pod: its Reserve is applied (or FitError)
+  int32_t* hkey = L.hkey;
+  int32_t* hval = L.hval;
+  Job* jobq = L.jobq;               // [Reserve wave][ring]
 
   if (a.prev && a.prev[1] != 1) {   // speculative pass behind a batch that left work for the host: no-op
     if (tid == 0) { a.committed[0] = -1; a.committed[1] = 0; a.committed[3] = 0; }
@@ -181,8 +195,6 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
   }
   __syncthreads();
 
-  auto ld_acq = [](const int32_t* p) { return __atomic_load_n(p, __ATOMIC_ACQUIRE); };
-  auto st_rel = [](int32_t* p, int32_t v) { __atomic_store_n(p, v, __ATOMIC_RELEASE); };
 
   if (wv == 0) {
     // ==================================================== decide ====================================================
@@ -241,8 +253,8 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
     auto flush_fresh = [&]() {
       if (ps_slot < 0) return;
       const int q0 = ps_p + 1 + lane, q1 = q0 + 64;
-      if (q0 < B) dso[q0 * B + ps_slot] = ps_v0;
-      if (q1 < B) dso[q1 * B + ps_slot] = ps_v1;
+      if (q0 < B) dso[q0 * SB + ps_slot] = ps_v0;
+      if (q1 < B) dso[q1 * SB + ps_slot] = ps_v1;
       ps_slot = -1;
     };
     int n_hs = -1, n_hc = 0, n_nlev = 0, n_feas = 0, n_next = -1;
@@ -306,7 +318,7 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
             const Row rr = drows[sl];
             if (numa_on && ((rr.nr.nflags >> NF_POLICY_SHIFT) & 3u)) hint_table_fill(s_ht0, rr.nr, zone_avail(rr.nr), lane);
             WAVE_FENCE();
-            for (int q2 = v + lane; q2 < B; q2 += 64) dsc[q2 * B + sl] = (int16_t)row_score(rr, pods(q2), a.pf, m, &s_ht0);
+            for (int q2 = v + lane; q2 < B; q2 += 64) dsc[q2 * SB + sl] = (int16_t)row_score(rr, pods(q2), a.pf, m, &s_ht0);
             WAVE_FENCE();
           }
         }
@@ -348,7 +360,7 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
           break;
         }
       }
-      SPM(1);
+      SPM(27);   // rollback / batch-end checks
       // ------------------------------------------------ decide pod q
       if (q >= end_at || q - ld_acq(&s_verified) >= SP_LAG || ld_acq(&s_cut_at) >= 0) {
         if (++spins > SP_SPIN_LIMIT) { err = true; err_code = 2; break; }
@@ -358,6 +370,7 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
         continue;
       }
       spins = 0;
+      if (ST) st_acc[35] += nd;
       const int p = q;
       const int hs = n_hs, hc = n_hc, nlev = n_nlev, feas = n_feas, next = n_next;
       const uint32_t lh = n_lh;
@@ -372,11 +385,13 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
         sp_sleep();
         continue;
       }
+      SPM(28);   // dirty-slot state (versions, ballots)
       if (p + 1 < B) load_hdr(p + 1, n_hs, n_hc, n_nlev, n_feas, n_next, n_lh, n_tb);   // consumed by the next decision
       int sc0 = -1, so0 = -1, sc1 = -1, so1 = -1;
       flush_fresh();
-      if (lane < nd) { so0 = dso[p * B + lane]; if (rdy0) sc0 = dsc[p * B + lane]; }
-      if (lane + 64 < nd) { so1 = dso[p * B + 64 + lane]; if (rdy1) sc1 = dsc[p * B + 64 + lane]; }
+      if (lane < nd) { so0 = dso[p * SB + lane]; if (rdy0) sc0 = dsc[p * SB + lane]; }
+      if (lane + 64 < nd) { so1 = dso[p * SB + 64 + lane]; if (rdy1) sc1 = dsc[p * SB + 64 + lane]; }
+      SPM(29);   // next header's loads issued, pending fresh slot stored, dirty scores loaded
       uint64_t unk0 = 0, unk1 = 0;
       if (multi) {
         // off-shard fresh rows whose batch-start job has not finished: a node in the list head has its listed level
@@ -455,9 +470,11 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
           winner = e < 64 ? (uint32_t)__builtin_amdgcn_readlane((int)lh, e) : list_ptr(a, 0, p)[e];
           if (ST) { st_acc[24] += e >= 32 ? 1 : 0; st_acc[25] += e >= 64 ? 1 : 0; }
         } else {
+          if (ST) { st_acc[31] += 1; st_acc[32] += nold; st_acc[33] += nnew; }
           const int lo = (int)max<int64_t>(0, jp - 2 - nnew);
           const int hi = (int)min<int64_t>(len - 1, jp - 1 + nold);
           const int W = hi - lo + 1;
+          if (ST) st_acc[34] += W > 0 ? W : 0;
           const uint32_t* L = list_ptr(a, 0, p);
           constexpr int WCH = (2 * MAX_BATCH + 2 + 63) / 64;
           uint32_t xw[WCH];
@@ -638,7 +655,7 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
             const uint32_t onode = osl < 0 ? 0u : (uint32_t)__builtin_amdgcn_readlane((int)(osl < 64 ? dn0 : dn1), osl & 63);
             const int ohash = osl < 0 ? -9 : sp_hash_find(onode);
             const int osv = osl < 0 ? -9 : (int)a.S[(size_t)p * a.ld + (onode - a.own0)];
-            const int odso = osl < 0 ? -9 : (int)dso[p * B + osl];
+            const int odso = osl < 0 ? -9 : (int)dso[p * SB + osl];
             if (lane == 0)   // diagnostics (GS_DEBUG_CUTS): the inconsistent tie count
               a.out[p] = PlacementDev{-7, (uint32_t)run, (int64_t)M | ((int64_t)Mc << 20) | ((int64_t)Md << 40), (uint32_t)T,
                                       (uint32_t)Tc, (uint32_t)(__popcll(new0) + __popcll(new1)),
@@ -686,8 +703,8 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
             ps_p = p;
           } else {   // another shard's row: unknown until the Reserve wave's batch-start job has evaluated it
             d.flags |= SP_OFFSHARD;
-            if (q0 < B) dso[q0 * B + slot] = SO_UNKNOWN;
-            if (q1 < B) dso[q1 * B + slot] = SO_UNKNOWN;
+            if (q0 < B) dso[q0 * SB + slot] = SO_UNKNOWN;
+            if (q1 < B) dso[q1 * SB + slot] = SO_UNKNOWN;
           }
           if (lane == 0) {
             hash_insert(winner, slot);
@@ -735,7 +752,7 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
       if (err) s_err = err_code ? err_code : 9;
       st_rel(&s_finish, 1);
     }
-  } else if (wv == 1) {
+  } else if (wv == SP_W_VERIFY) {
     // ==================================================== verify ====================================================
     // pod v stands iff every row pending at its decision now scores below its maximum for it (and every row whose
     // batch-start score was unknown scored below it at batch start); the rows it excluded that are feasible join its
@@ -764,24 +781,24 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
         const DecRec d = dec[v];
         int mis = 0, fadd = 0;
         if ((d.pend0 >> lane) & 1ull) {
-          const int sc = dsc[v * B + lane];
+          const int sc = dsc[v * SB + lane];
           mis |= sc >= 0 && sc >= d.M;
           fadd += sc >= 0;
         }
         if ((d.pend1 >> lane) & 1ull) {
-          const int sc = dsc[v * B + 64 + lane];
+          const int sc = dsc[v * SB + 64 + lane];
           mis |= sc >= 0 && sc >= d.M;
           fadd += sc >= 0;
         }
         // unknown batch-start scores (several shards): known now (the creating pod is complete); the decision counted
         // the node as clean and unlisted
         if ((d.unk0 >> lane) & 1ull) {
-          const int so = dso[v * B + lane];
+          const int so = dso[v * SB + lane];
           mis |= so >= 0 && so >= d.M;
           fadd -= so >= 0;
         }
         if ((d.unk1 >> lane) & 1ull) {
-          const int so = dso[v * B + 64 + lane];
+          const int so = dso[v * SB + 64 + lane];
           mis |= so >= 0 && so >= d.M;
           fadd -= so >= 0;
         }
@@ -817,9 +834,9 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
       sp_sleep();
       SPM(2);
     }
-  } else if (wv < SP_RS0) {
+  } else if (sp_reserve_index(wv) >= 0) {
     // =================================================== Reserve ===================================================
-    const int wr = wv - SP_RES0;   // this wave's pods: q % SP_NRES == wr
+    const int wr = sp_reserve_index(wv);   // this wave's pods: q % SP_NRES == wr
     TopoDev& s_topo_w = s_topo[wr];
     uint64_t* s_cpuset_w = s_cpuset[wr];
     int32_t& s_aff_w = s_aff[wr];
@@ -849,10 +866,12 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
       int64_t vv = 0;
       if (f_kind == 1) vv = reinterpret_cast<const int64_t*>(f_src)[node];
       else if (f_kind == 2) vv = reinterpret_cast<const int32_t*>(f_src)[node];
-      else if (f_kind == 3)   // the Filter-time affinity, known for the own shard's rows only (-1: recomputed)
-        vv = node - a.own0 < a.own1 - a.own0
-                 ? (int64_t)reinterpret_cast<const uint8_t*>(f_src)[(size_t)qq * a.ld + (node - a.own0)]
-                 : (int64_t)-1;
+      else if (f_kind == 3) {   // the Filter-time affinity, known for the own shard's unpatched rows (-1: recomputed)
+        const uint8_t b = node - a.own0 < a.own1 - a.own0
+                              ? reinterpret_cast<const uint8_t*>(f_src)[(size_t)qq * a.ld + (node - a.own0)]
+                              : AFF_RECOMPUTE;
+        vv = b == AFF_RECOMPUTE ? (int64_t)-1 : (int64_t)b;
+      }
       else if (f_kind == 4) vv = (int64_t)node;
       return vv;
     };
@@ -1091,7 +1110,8 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
   } else {
     // ============================================== re-scoring jobs ==============================================
     uint32_t spins = 0;
-    int ring = wv % SP_NRES;
+    const int ri = sp_rescore_index(wv);
+    int ring = ri % SP_NRES;
     for (;;) {
       if (ld_acq(&s_stop)) {
         if (lane == 0) __atomic_fetch_add(&s_parked, 1, __ATOMIC_ACQ_REL);
@@ -1130,7 +1150,7 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
       SPM(8);
       const Job jb{__builtin_amdgcn_readfirstlane(jl.slot), __builtin_amdgcn_readfirstlane(jl.q),
                    __builtin_amdgcn_readfirstlane(jl.range), __builtin_amdgcn_readfirstlane(jl.tbl)};
-      HintTable& tab = tables[wv - SP_RS0];
+      HintTable& tab = tables[ri];
       if (jb.range < 0) {
         // batch-start job (several shards): another shard's fresh row as it stood at batch start — the HBM mirror,
         // written back only at the kernel's end — evaluated for every later pod: its dso entries
@@ -1140,7 +1160,7 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
         for (int s = 3; s < 7; ++s) rr.free[s] = m.c64(C_FREE_CPU + s)[node];
         if (numa_on && ((rr.nr.nflags >> NF_POLICY_SHIFT) & 3u)) hint_table_fill(tab, rr.nr, zone_avail(rr.nr), lane);
         WAVE_FENCE();
-        for (int q2 = jb.q + 1 + lane; q2 < B; q2 += 64) dso[q2 * B + jb.slot] = (int16_t)row_score(rr, pods(q2), a.pf, m, &tab);
+        for (int q2 = jb.q + 1 + lane; q2 < B; q2 += 64) dso[q2 * SB + jb.slot] = (int16_t)row_score(rr, pods(q2), a.pf, m, &tab);
         WAVE_FENCE();
         if (lane == 0 && __atomic_fetch_sub(&jobs_all[jb.q], 1, __ATOMIC_ACQ_REL) == 1)
           __atomic_store_n(&rescored[jb.q], 1, __ATOMIC_RELEASE);
@@ -1152,7 +1172,7 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
       if (numa_on && ((rr.nr.nflags >> NF_POLICY_SHIFT) & 3u)) hint_table_fill(tab, rr.nr, zone_avail(rr.nr), lane);
       WAVE_FENCE();
       const int q2 = jb.q + 1 + jb.range * 64 + lane;
-      if (q2 < B) dsc[q2 * B + jb.slot] = (int16_t)row_score(rr, pods(q2), a.pf, m, &tab);
+      if (q2 < B) dsc[q2 * SB + jb.slot] = (int16_t)row_score(rr, pods(q2), a.pf, m, &tab);
       WAVE_FENCE();
       if (lane == 0) {
         if (__atomic_fetch_sub(&jobs_left[jb.q], 1, __ATOMIC_ACQ_REL) == 1)
@@ -1203,10 +1223,10 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
       else m.c32(C_CPU_META)[node] = (int32_t)cst[sl].meta;
     }
   for (int i = tid; i < committed; i += SP_THREADS) a.out[i].feasible = (uint32_t)final_F[i];
-  if (ST && lane == 0)
-    for (int i = 0; i < 28; ++i)
-      if (st_acc[i]) atomicAdd(reinterpret_cast<unsigned long long*>(&a.stamps[i]), (unsigned long long)st_acc[i]);
-#undef SPM
+  if (ST && lane == 0)   // per wave: region wv of SP_STRIDE entries
+    for (int i = 0; i < SP_NST; ++i)
+      if (st_acc[i])
+        atomicAdd(reinterpret_cast<unsigned long long*>(&a.stamps[wv * SP_STRIDE + i]), (unsigned long long)st_acc[i]);
   if (tid == 0) {
     a.committed[0] = committed;
     a.committed[1] = (committed == B && !s_hostcut && !s_err) ? 1 : 0;
@@ -1230,5 +1250,7 @@ hipError_t set_commit_spec_attributes() {
   return hipFuncSetAttribute(reinterpret_cast<const void*>(commit_spec_kernel<true>),
                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)spec_smem_bytes(MAX_BATCH));
 }
+
+#undef SPM
 
 }  // namespace gs

@@ -964,9 +964,12 @@ int launch_batch(gs_ctx* c, int b, const int32_t* prev, const PlacementDev* prev
   HIP_TRY(c, hipEventRecord(c->ev[1], c->st_ev));
   HIP_TRY(c, hipEventRecord(sl.ev_evdone, c->st_ev));
   HIP_TRY(c, hipStreamWaitEvent(c->st, sl.ev_evdone, 0));
-  if (prev)
-    HIP_TRY(c, launch_patch(c->mv, c->d_pods, b, c->pf, c->n0, c->n1, c->d_S, c->ld, prod_cols, c->d_aff, prev_out, prev,
-                            prev_b, c->st));
+  if (prev) {
+    static const bool twice = getenv("GS_PATCH_TWICE") && getenv("GS_PATCH_TWICE")[0] == '1';   // diagnostics
+    for (int k = 0; k < (twice ? 2 : 1); ++k)
+      HIP_TRY(c, launch_patch(c->mv, c->d_pods, b, c->pf, c->n0, c->n1, c->d_S, c->ld, prod_cols, c->d_aff, prev_out,
+                              prev, prev_b, c->st));
+  }
   if (!c->window_k)   // node sampling selects over the rotation window, not the candidate levels
     HIP_TRY(c, launch_cand(c->d_S, c->ld, len, c->n0, b, c->max_score, c->lstride, d_lists, d_hdrs, d_ext, c->st));
   HIP_TRY(c, hipEventRecord(c->ev[2], c->st));
@@ -1601,9 +1604,15 @@ int gs_create(const gs_config* cfg, gs_ctx** out) {
   hipError_t e;
   if ((e = hipSetDevice(cfg->device)) != hipSuccess) return bail("hipSetDevice", e);
   if ((e = set_kernel_attributes()) != hipSuccess) return bail("hipFuncSetAttribute", e);
-  if ((e = hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking)) != hipSuccess) return bail("hipStreamCreate", e);
-  if ((e = hipStreamCreateWithFlags(&c->st2, hipStreamNonBlocking)) != hipSuccess) return bail("hipStreamCreate", e);
-  if ((e = hipStreamCreateWithFlags(&c->st_ev, hipStreamNonBlocking)) != hipSuccess) return bail("hipStreamCreate", e);
+  // priorities: the commit chain (patch, cand, commit on st) before the next batch's eval pass (st_ev, st2), which
+  // otherwise fills every CU while patch / cand wait for slots
+  int prio_lo = 0, prio_hi = 0;
+  if ((e = hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi)) != hipSuccess) return bail("hipDeviceGetStreamPriorityRange", e);
+  static const bool same_prio = getenv("GS_STREAM_PRIO") && getenv("GS_STREAM_PRIO")[0] == '0';
+  if (same_prio) prio_hi = prio_lo;
+  if ((e = hipStreamCreateWithPriority(&c->st, hipStreamNonBlocking, prio_hi)) != hipSuccess) return bail("hipStreamCreate", e);
+  if ((e = hipStreamCreateWithPriority(&c->st2, hipStreamNonBlocking, prio_lo)) != hipSuccess) return bail("hipStreamCreate", e);
+  if ((e = hipStreamCreateWithPriority(&c->st_ev, hipStreamNonBlocking, prio_lo)) != hipSuccess) return bail("hipStreamCreate", e);
   if ((e = hipStreamCreateWithFlags(&c->st_rb, hipStreamNonBlocking)) != hipSuccess) return bail("hipStreamCreate", e);
   if ((e = hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming)) != hipSuccess) return bail("hipEventCreate", e);
   if ((e = hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming)) != hipSuccess) return bail("hipEventCreate", e);
@@ -1668,9 +1677,11 @@ int gs_create(const gs_config* cfg, gs_ctx** out) {
       if ((e = hipEventCreate(&ev)) != hipSuccess) return bail("hipEventCreate", e);
   }
   if (getenv("GS_COMMIT_STAMPS") && getenv("GS_COMMIT_STAMPS")[0] == '1') {
-    if ((e = hipMalloc(&c->d_stamps, 8 * 32)) != hipSuccess) return bail("hipMalloc", e);
-    (void)hipMemset(c->d_stamps, 0, 256);
-    set_cand_stamps(c->d_stamps + 27);
+    // 8 waves x 64 entries (commit_spec_kernel: one region per wave; the other commit kernels: region 0), then the
+    // cand kernel's 8 at entry 512
+    if ((e = hipMalloc(&c->d_stamps, 8 * 520)) != hipSuccess) return bail("hipMalloc", e);
+    (void)hipMemset(c->d_stamps, 0, 8 * 520);
+    set_cand_stamps(c->d_stamps + 512);
   }
   if ((e = hipDeviceSynchronize()) != hipSuccess) return bail("hipDeviceSynchronize", e);
   // 96 B (LoadAware + Fit row), + 192 B NodeNUMAResource columns when enabled
@@ -1688,29 +1699,31 @@ int gs_destroy(gs_ctx* c) {
   for (void* p : {(void*)c->h_xpod, (void*)c->h_xout, (void*)c->h_xnom})
     if (p) (void)hipHostFree(p);
   if (c->d_stamps) {
-    uint64_t st[32] = {};
-    if (hipMemcpy(st, c->d_stamps, 256, hipMemcpyDeviceToHost) == hipSuccess) {
+    std::vector<uint64_t> sa(520);
+    if (hipMemcpy(sa.data(), c->d_stamps, 8 * 520, hipMemcpyDeviceToHost) == hipSuccess) {
       static const char* kind = getenv("GS_COMMIT_KERNEL");
-      if (!(kind && kind[0] == 'p') && !c->window_k) {   // speculative commit kernel
+      if (!(kind && kind[0] == 'p') && !c->window_k) {   // speculative commit kernel: one stamp region per wave
         const double np = c->stats_all_pods ? (double)c->stats_all_pods : 1.0;
-        fprintf(stderr, "gpuscore spec commit, cycles per committed pod (%llu pods): decide %.0f verify %.0f wave0+verifier-wait "
-                "%.0f rollback %.0f (%llu rollbacks) | Reserve busy %.0f wait %.0f (2 waves, summed) | re-scoring busy %.0f "
-                "wait %.0f (4 waves, summed) | decisions %llu, full-row %llu (%.0f cycles each; M<0 %llu, M>=0 %llu) | wave 0 "
-                "total %.0f\n",
-                (unsigned long long)c->stats_all_pods, st[0] / np, st[1] / np, st[2] / np, st[4] / np,
-                (unsigned long long)st[3], st[5] / np, st[6] / np, st[7] / np, st[8] / np, (unsigned long long)st[9],
-                (unsigned long long)st[10], st[10] ? (double)st[11] / st[10] : 0.0, (unsigned long long)st[13],
-                (unsigned long long)st[14], st[12] / np);
-        fprintf(stderr, "gpuscore spec commit, Reserve wave per committed pod: fetch+undo %.0f numa_eval %.0f "
-                "lane0 (zone split, cpuset, assume) %.0f rest %.0f (fresh fetch %.0f, landed-again wait %.0f)\n", st[15] / np,
-                st[16] / np, st[17] / np, st[5] / np, st[21] / np, st[22] / np);
-        fprintf(stderr, "gpuscore spec commit, decide per committed pod: level scan %.0f winner %.0f fresh-slot S loads %.0f "
-                "record %.0f; list window beyond entry 32: %llu, beyond 64: %llu; wave 0 waiting at batch end %.0f; Reserve waiting "
-                "for the first decision %.0f\n", st[18] / np, st[19] / np, st[20] / np, st[0] / np,
-                (unsigned long long)st[24], (unsigned long long)st[25], st[23] / np, st[26] / np);
+        auto W = [&](int w, int i) { return (double)sa[w * 64 + i] / np; };
+        fprintf(stderr, "gpuscore spec commit, cycles per committed pod (%llu pods, %llu decisions, %llu rollbacks, %.0f "
+                "rollback cycles, full-row %llu):\n", (unsigned long long)c->stats_all_pods, (unsigned long long)sa[9],
+                (unsigned long long)sa[3], W(0, 4), (unsigned long long)sa[10]);
+        fprintf(stderr, "  wave 0 total %.0f: checks %.0f | dirty state %.0f | hdr+fresh store+dirty loads %.0f | level scan "
+                "%.0f | winner %.0f | fresh slot %.0f | record %.0f | waiting %.0f (at batch end %.0f) | full-row %.0f\n",
+                W(0, 12), W(0, 27), W(0, 28), W(0, 29), W(0, 18), W(0, 19), W(0, 20), W(0, 0), W(0, 2), W(0, 23), W(0, 11));
+        const double ng = sa[31] ? (double)sa[31] : 1.0;
+        fprintf(stderr, "  winner general path: %llu decisions (%.1f%%), avg old %.1f new %.1f window %.1f; avg dirty slots "
+                "%.1f; list window beyond 32: %llu, beyond 64: %llu\n", (unsigned long long)sa[31], 100.0 * sa[31] / np,
+                sa[32] / ng, sa[33] / ng, sa[34] / ng, sa[35] / np, (unsigned long long)sa[24], (unsigned long long)sa[25]);
+        fprintf(stderr, "  wave 4 (verify): busy %.0f waiting %.0f\n", W(4, 1), W(4, 2));
+        for (int w = 2; w < 4; ++w)
+          fprintf(stderr, "  wave %d (Reserve): fetch+undo %.0f numa_eval %.0f lane0 %.0f rest %.0f (fresh fetch %.0f, landed-"
+                  "again wait %.0f) waiting %.0f (first decision %.0f)\n", w, W(w, 15), W(w, 16), W(w, 17), W(w, 5), W(w, 21),
+                  W(w, 22), W(w, 6), W(w, 26));
+        for (int w : {1, 5, 6, 7}) fprintf(stderr, "  wave %d (re-scoring): busy %.0f waiting %.0f\n", w, W(w, 7), W(w, 8));
         const double nb = c->stats.batches ? (double)c->stats.batches * c->B : 1.0;
         fprintf(stderr, "gpuscore cand_kernel, wave-0 cycles per pod row: pass 1 %.0f, level sums %.0f, level pick %.0f, "
-                "offsets %.0f, pass 2 %.0f\n", st[27] / nb, st[28] / nb, st[29] / nb, st[30] / nb, st[31] / nb);
+                "offsets %.0f, pass 2 %.0f\n", sa[512] / nb, sa[513] / nb, sa[514] / nb, sa[515] / nb, sa[516] / nb);
         (void)hipFree(c->d_stamps);
         c->d_stamps = nullptr;
       }

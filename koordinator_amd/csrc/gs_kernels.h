@@ -18,6 +18,7 @@ constexpr int XCAP = 256;            // listed nodes per (pod, shard) when the l
 constexpr int PODS_PER_BLOCK = 16;   // eval kernel: pods per workgroup (grid.y = ceil(B / 16))
 constexpr int MAX_SCORE_LIMIT = 2047; // cand kernel keeps one histogram per wave in LDS
 constexpr int ROW_WORDS = NUM_I64_COLS + NUM_I32_COLS;  // staging row: i64 columns, then i32 widened
+constexpr uint8_t AFF_RECOMPUTE = 0xFF;   // aff[][] entry the Reserve recomputes (a row patched after the eval pass)
 
 // The HBM mirror: column c of the int64 table starts at i64 + c*npad.
 struct MirrorView {

@@ -22,6 +22,7 @@
 #include <vector>
 
 #include "gs_eval_dev.h"
+#include "gs_pair_wave.h"
 
 namespace gs {
 
@@ -127,6 +128,41 @@ __global__ void __launch_bounds__(128) patch_kernel(MirrorView m, const PodVec* 
     const PairOut o = eval_pair<false, true, true, true>(r, pods[q], pf, m, &s_tab);
     S[(size_t)q * ld + ((uint32_t)node - n0)] = (int16_t)total_score(o, pf);
     if (policy) aff[(size_t)q * ld + ((uint32_t)node - n0)] = (uint8_t)(o.code ? 0u : o.aff);
+  }
+}
+
+// The same patch with one wave per (row, pod) pair, lane-parallel (pair_score_wave): the kernel's time is the
+// slowest pair's, and a pair evaluated by one lane runs the rare long paths (the full topology-manager merge) as one
+// scalar chain, while a wave spreads them over its lanes. Block = one landed row x PW_PODS pods. The Filter-time
+// affinity of a patched NUMA-policy row is left to the Reserve (AFF_RECOMPUTE: numa_eval recomputes it there).
+constexpr int PW_PODS = 16;
+__global__ void __launch_bounds__(64 * PW_PODS) patch_wave_kernel(MirrorView m, const PodVec* __restrict__ pods,
+                                                                  int npods, Profile pf, uint32_t n0, uint32_t n1,
+                                                                  int16_t* __restrict__ S, uint32_t ld, int prod_cols,
+                                                                  uint8_t* __restrict__ aff,
+                                                                  const PlacementDev* __restrict__ prev_out,
+                                                                  const int32_t* __restrict__ prev_committed) {
+  const int k = blockIdx.x;
+  if (k >= prev_committed[0]) return;   // pods the previous batch placed (a voided pass: -1)
+  const int32_t node = prev_out[k].node;
+  if (node < 0 || (uint32_t)node < n0 || (uint32_t)node >= n1) return;
+  const bool numa = (pf.enabled & 0x30u) != 0;
+  __shared__ Row s_row;
+  __shared__ PodVec s_pod[PW_PODS];
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int q = blockIdx.y * PW_PODS + w;
+  if (threadIdx.x == 0) {
+    load_row(m, (uint32_t)node, prod_cols, numa, s_row);
+    for (int sl = 3; sl < 7; ++sl) s_row.free[sl] = m.c64(C_FREE_CPU + sl)[node];
+  }
+  if (q < npods && lane < (int)(sizeof(PodVec) / 8))
+    reinterpret_cast<uint64_t*>(&s_pod[w])[lane] = reinterpret_cast<const uint64_t*>(&pods[q])[lane];
+  __syncthreads();
+  if (q >= npods) return;
+  const int32_t sc = pair_score_wave(s_row, s_pod[w], pf, m);
+  if (lane == 0) {
+    S[(size_t)q * ld + ((uint32_t)node - n0)] = (int16_t)sc;
+    if (numa && ((s_row.nr.nflags >> NF_POLICY_SHIFT) & 3u)) aff[(size_t)q * ld + ((uint32_t)node - n0)] = AFF_RECOMPUTE;
   }
 }
 
@@ -638,7 +674,9 @@ __global__ void __launch_bounds__(COMMIT_THREADS) commit_kernel(CommitArgs a) {
       else if (f_kind == 2) v = reinterpret_cast<const int32_t*>(f_src)[winner];
       else if (f_kind == 3) {   // the batch-start Filter's affinity for this pair (own shard, NUMA-policy nodes)
         const bool own = f_src && winner >= a.own0 && winner < a.own1;
-        v = own ? (int64_t)reinterpret_cast<const uint8_t*>(f_src)[(size_t)k * a.ld + (winner - a.own0)] : -1;
+        const uint8_t b8 = own ? reinterpret_cast<const uint8_t*>(f_src)[(size_t)k * a.ld + (winner - a.own0)]
+                               : AFF_RECOMPUTE;
+        v = b8 == AFF_RECOMPUTE ? (int64_t)-1 : (int64_t)b8;   // (a patched row's: recomputed)
       } else if (f_kind == 4) v = (int64_t)winner;   // Row.node, Row.pad = 0
       if (f_kind) {
         unsigned char* dst = f_region == 0 ? reinterpret_cast<unsigned char*>(&orow)
@@ -1373,8 +1411,14 @@ hipError_t launch_patch(const MirrorView& m, const PodVec* pods, int npods, cons
                         int16_t* S, uint32_t ld, int prod_cols, uint8_t* aff, const PlacementDev* prev_out,
                         const int32_t* prev_committed, int prev_npods, hipStream_t st) {
   if (prev_npods <= 0 || npods <= 0) return hipSuccess;
-  hipLaunchKernelGGL(patch_kernel, dim3(prev_npods), dim3(128), 0, st, m, pods, npods, pf, n0, n1, S, ld, prod_cols, aff,
-                     prev_out, prev_committed);
+  // one lane per pair (default: 63 us per C3 batch); GS_PATCH_WAVE=1: one wave per pair (measured 91 us)
+  static const bool wave = getenv("GS_PATCH_WAVE") && getenv("GS_PATCH_WAVE")[0] == '1';
+  if (!wave)
+    hipLaunchKernelGGL(patch_kernel, dim3(prev_npods), dim3(128), 0, st, m, pods, npods, pf, n0, n1, S, ld, prod_cols,
+                       aff, prev_out, prev_committed);
+  else
+    hipLaunchKernelGGL(patch_wave_kernel, dim3(prev_npods, (npods + PW_PODS - 1) / PW_PODS), dim3(64 * PW_PODS), 0, st,
+                       m, pods, npods, pf, n0, n1, S, ld, prod_cols, aff, prev_out, prev_committed);
   return hipGetLastError();
 }
 

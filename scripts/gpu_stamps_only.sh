@@ -6,7 +6,7 @@ export TMPDIR=/tmp
 GS_COMMIT_STAMPS=1 timeout -k 10 300 python -u bench.py --steps 5 --warmup 1 --no-cpu-baseline ${BENCH_ARGS} \
     > gpurun_out/stamps.json 2> gpurun_out/stamps.err
 rc=$?
-grep gpuscore gpurun_out/stamps.err
+grep -A12 gpuscore gpurun_out/stamps.err
 python - <<'PY'
 import json
 d = json.loads(open("gpurun_out/stamps.json").read().strip().splitlines()[-1])
