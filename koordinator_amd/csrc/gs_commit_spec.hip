@@ -469,6 +469,31 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
           const int e = off + (int)jp - 1;
           winner = e < 64 ? (uint32_t)__builtin_amdgcn_readlane((int)lh, e) : list_ptr(a, 0, p)[e];
           if (ST) { st_acc[24] += e >= 32 ? 1 : 0; st_acc[25] += e >= 64 ? 1 : 0; }
+        } else if (nnew == 0 && nold <= 61) {
+          // only listed nodes at M, some of them dirty rows no longer at M ("old"; the common case): the jp-th of the
+          // others in list order lies in the window [jp-2, jp-1+nold] of level M's segment (<= 64 entries, one per
+          // lane); old nodes before the window are those with a lower node id (the segment is in node order)
+          if (ST) { st_acc[36] += 1; st_acc[32] += nold; }
+          const int lo = (int)max<int64_t>(0, jp - 2);
+          const int hi = (int)min<int64_t>(len - 1, jp - 1 + nold);
+          const int W = hi - lo + 1;
+          const int e = off + lo + lane;
+          const uint32_t fromh = (uint32_t)__shfl((int)lh, e & 63);
+          uint32_t x = 0xffffffffu;
+          if (lane < W) x = e < 64 ? fromh : list_ptr(a, 0, p)[e];
+          const uint32_t win0 = (uint32_t)__builtin_amdgcn_readlane((int)x, 0);
+          bool ow = false;
+          int base_old = 0;
+          each_node(old0, old1, [&](uint32_t n) {
+            base_old += n < win0 ? 1 : 0;
+            ow |= x == n;
+          });
+          const uint64_t bo = __ballot(lane < W && ow);
+          const int older = base_old + __popcll(bo & lt_mask);
+          const uint64_t hit = __ballot(lane < W && !ow && (int64_t)(lo + lane - older + 1) == jp);
+          if (ST) { st_acc[24] += off + hi >= 32 ? 1 : 0; st_acc[25] += off + hi >= 64 ? 1 : 0; }
+          if (!hit) { action = 2; end_why = 1; }
+          else winner = (uint32_t)__builtin_amdgcn_readlane((int)x, __builtin_ctzll(hit));
         } else {
           if (ST) { st_acc[31] += 1; st_acc[32] += nold; st_acc[33] += nnew; }
           const int lo = (int)max<int64_t>(0, jp - 2 - nnew);

@@ -1712,9 +1712,11 @@ int gs_destroy(gs_ctx* c) {
                 "%.0f | winner %.0f | fresh slot %.0f | record %.0f | waiting %.0f (at batch end %.0f) | full-row %.0f\n",
                 W(0, 12), W(0, 27), W(0, 28), W(0, 29), W(0, 18), W(0, 19), W(0, 20), W(0, 0), W(0, 2), W(0, 23), W(0, 11));
         const double ng = sa[31] ? (double)sa[31] : 1.0;
-        fprintf(stderr, "  winner general path: %llu decisions (%.1f%%), avg old %.1f new %.1f window %.1f; avg dirty slots "
-                "%.1f; list window beyond 32: %llu, beyond 64: %llu\n", (unsigned long long)sa[31], 100.0 * sa[31] / np,
-                sa[32] / ng, sa[33] / ng, sa[34] / ng, sa[35] / np, (unsigned long long)sa[24], (unsigned long long)sa[25]);
+        fprintf(stderr, "  winner: old-nodes-only path %llu decisions (%.1f%%), general path %llu (%.1f%%): avg old %.1f new "
+                "%.1f window %.1f; avg dirty slots %.1f; list window beyond 32: %llu, beyond 64: %llu\n",
+                (unsigned long long)sa[36], 100.0 * sa[36] / np, (unsigned long long)sa[31], 100.0 * sa[31] / np,
+                sa[32] / (ng + sa[36]), sa[33] / ng, sa[34] / ng, sa[35] / np, (unsigned long long)sa[24],
+                (unsigned long long)sa[25]);
         fprintf(stderr, "  wave 4 (verify): busy %.0f waiting %.0f\n", W(4, 1), W(4, 2));
         for (int w = 2; w < 4; ++w)
           fprintf(stderr, "  wave %d (Reserve): fetch+undo %.0f numa_eval %.0f lane0 %.0f rest %.0f (fresh fetch %.0f, landed-"
