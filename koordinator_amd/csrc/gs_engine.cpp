@@ -176,6 +176,10 @@ struct gs_ctx {
   gs_stats stats{};
   uint64_t* d_stamps = nullptr;   // GS_COMMIT_STAMPS=1: commit-kernel phase cycle sums
   uint64_t stats_all_pods = 0;     // pods placed by gs_schedule over the context's life (stamp averages)
+  // GS_HOST_TIMING=1: host time per batch of schedule_stream, by phase (printed by gs_destroy)
+  bool host_timing = false;
+  double ht_wait = 0, ht_apply = 0, ht_stage = 0, ht_launch = 0, ht_max_busy = 0;
+  uint64_t ht_batches = 0, ht_busy_hist[8] = {};
   // NodeNUMAResource: per-node TopologyOptions + NodeAllocation mirror, registered CPU topologies
   std::vector<NumaNode> numa;
   std::vector<std::shared_ptr<TopoClass>> topos;
@@ -1610,9 +1614,29 @@ int gs_create(const gs_config* cfg, gs_ctx** out) {
   if ((e = hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi)) != hipSuccess) return bail("hipDeviceGetStreamPriorityRange", e);
   static const bool same_prio = getenv("GS_STREAM_PRIO") && getenv("GS_STREAM_PRIO")[0] == '0';
   if (same_prio) prio_hi = prio_lo;
-  if ((e = hipStreamCreateWithPriority(&c->st, hipStreamNonBlocking, prio_hi)) != hipSuccess) return bail("hipStreamCreate", e);
-  if ((e = hipStreamCreateWithPriority(&c->st2, hipStreamNonBlocking, prio_lo)) != hipSuccess) return bail("hipStreamCreate", e);
-  if ((e = hipStreamCreateWithPriority(&c->st_ev, hipStreamNonBlocking, prio_lo)) != hipSuccess) return bail("hipStreamCreate", e);
+  // CU partition: the commit chain (st: patch, cand, the one-workgroup commit kernel) on its own CUs, the next batch's
+  // eval pass (st_ev, st2) on the others, so that no eval wave shares the commit kernel's CU (measured: the commit
+  // runs ~25% slower with eval waves beside it). GS_COMMIT_CUS = CUs of the commit chain (0: no partition).
+  int ncu = 0;
+  (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, cfg->device);
+  const char* cus_env = getenv("GS_COMMIT_CUS");
+  // (measured on C3, pods/s: no partition 120k, 8 CUs 129k, 32 CUs 141-148k, 64 CUs 143-147k; the commit kernel alone on
+  // 4 CUs of a stream of its own, patch / cand with the eval pass: 138k, the cross-stream hops cost more than they save)
+  const int commit_cus = cus_env ? atoi(cus_env) : 32;
+  if (commit_cus > 0 && ncu > 2 * commit_cus) {
+    std::vector<uint32_t> m_commit((ncu + 31) / 32, 0u), m_eval((ncu + 31) / 32, 0u);
+    for (int k = 0; k < ncu; ++k) (k < commit_cus ? m_commit : m_eval)[k / 32] |= 1u << (k % 32);
+    if ((e = hipExtStreamCreateWithCUMask(&c->st, (uint32_t)m_commit.size(), m_commit.data())) != hipSuccess)
+      return bail("hipExtStreamCreateWithCUMask", e);
+    if ((e = hipExtStreamCreateWithCUMask(&c->st2, (uint32_t)m_eval.size(), m_eval.data())) != hipSuccess)
+      return bail("hipExtStreamCreateWithCUMask", e);
+    if ((e = hipExtStreamCreateWithCUMask(&c->st_ev, (uint32_t)m_eval.size(), m_eval.data())) != hipSuccess)
+      return bail("hipExtStreamCreateWithCUMask", e);
+  } else {
+    if ((e = hipStreamCreateWithPriority(&c->st, hipStreamNonBlocking, prio_hi)) != hipSuccess) return bail("hipStreamCreate", e);
+    if ((e = hipStreamCreateWithPriority(&c->st2, hipStreamNonBlocking, prio_lo)) != hipSuccess) return bail("hipStreamCreate", e);
+    if ((e = hipStreamCreateWithPriority(&c->st_ev, hipStreamNonBlocking, prio_lo)) != hipSuccess) return bail("hipStreamCreate", e);
+  }
   if ((e = hipStreamCreateWithFlags(&c->st_rb, hipStreamNonBlocking)) != hipSuccess) return bail("hipStreamCreate", e);
   if ((e = hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming)) != hipSuccess) return bail("hipEventCreate", e);
   if ((e = hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming)) != hipSuccess) return bail("hipEventCreate", e);
@@ -1676,6 +1700,7 @@ int gs_create(const gs_config* cfg, gs_ctx** out) {
     for (auto& ev : s1.ev)
       if ((e = hipEventCreate(&ev)) != hipSuccess) return bail("hipEventCreate", e);
   }
+  c->host_timing = getenv("GS_HOST_TIMING") && getenv("GS_HOST_TIMING")[0] == '1';
   if (getenv("GS_COMMIT_STAMPS") && getenv("GS_COMMIT_STAMPS")[0] == '1') {
     // 8 waves x 64 entries (commit_spec_kernel: one region per wave; the other commit kernels: region 0), then the
     // cand kernel's 8 at entry 512
@@ -1693,6 +1718,15 @@ int gs_create(const gs_config* cfg, gs_ctx** out) {
 int gs_destroy(gs_ctx* c) {
   if (!c) return GS_EINVAL;
   async_stop(c);
+  if (c->host_timing && c->ht_batches) {
+    const double n = (double)c->ht_batches;
+    fprintf(stderr, "gpuscore host per batch (us, %llu batches): waiting for the batch %.0f | applying placements %.0f | "
+            "staging the next %.0f | enqueueing it %.0f | busy max %.0f; busy histogram (100-us bins):",
+            (unsigned long long)c->ht_batches, c->ht_wait / n, c->ht_apply / n, c->ht_stage / n, c->ht_launch / n,
+            c->ht_max_busy);
+    for (int k = 0; k < 8; ++k) fprintf(stderr, " %llu", (unsigned long long)c->ht_busy_hist[k]);
+    fprintf(stderr, "\n");
+  }
   for (void* p : {(void*)c->d_dev, (void*)c->d_xpod, (void*)c->d_xrec, (void*)c->d_xres, (void*)c->d_xtot,
                   (void*)c->d_xds, (void*)c->d_xrs, (void*)c->d_xnom, (void*)c->d_xT, (void*)c->d_xout})
     if (p) (void)hipFree(p);
@@ -2010,13 +2044,49 @@ int schedule_stream(gs_ctx* c, PodRun run, Next&& next_run, Done&& run_done) {
     (void)hipStreamSynchronize(c->st_ev);
     (void)hipStreamSynchronize(c->st_rb);   // a voided or in-flight batch's readback into the pinned buffers
   };
+  // A batch whose successor is already running on the device has its placements applied on the host only after the
+  // batch after that is enqueued (its eval pass then overlaps the successor's commit; applying 128 placements takes
+  // ~230 us of host time that otherwise delays it): its outputs are copied out of the slot, which that batch reuses.
+  struct Pending {
+    int n = 0;
+    bool special = false;
+    const gs_pod* pods = nullptr;
+    gs_placement* out = nullptr;
+    std::vector<PlacementDev> h_out;
+    std::vector<PodVec> h_pods;
+  } pend;
+  auto apply_batch = [&](const gs_pod* pods, gs_placement* outp, int n, const PlacementDev* hout, const PodVec* hpods,
+                         bool special) -> int {
+    for (int k = 0; k < n; ++k) {
+      const PlacementDev& pd = hout[k];
+      gs_placement& o = outp[k];
+      o.node = pd.node;
+      o.feasible = pd.feasible;
+      o.score = pd.node >= 0 ? pd.score : 0;
+      o.ties = pd.node >= 0 ? pd.ties : 0;
+      o.flags = pd.flags & ~PL_INTERNAL_FLAGS;
+      if (pd.flags & GS_PLACED_SLOWPATH) c->stats.slowpath_pods += 1;   // resolved from its whole score row
+      if (int rc = numa_reserve(c, pods[k], hpods[k], pd)) return rc;
+      apply_placement(c, pods[k], pd.node, special);
+    }
+    return GS_OK;
+  };
+  auto apply_pending = [&]() -> int {
+    if (!pend.n) return GS_OK;
+    const int n = pend.n;
+    pend.n = 0;
+    return apply_batch(pend.pods, pend.out, n, pend.h_out.data(), pend.h_pods.data(), pend.special);
+  };
   auto body = [&]() -> int {
     int rc = GS_OK;
     uint32_t i = 0;
     bool inflight = false, cur_special = false, spec_ok = true;
     int cur_b = 0;
+    const gs_pod* prev_pods = nullptr;   // the pending batch's pods (a UID there must not start the next batch early)
+    int prev_n = 0;
     for (;;) {
       if (i == run.n) {   // the run is complete; the next one (its first batch may be in flight already)
+        if ((rc = apply_pending())) return rc;
         run_done(run, GS_OK);
         if (!have_nxt) have_nxt = next_run(&nxt);
         if (!have_nxt) break;
@@ -2047,24 +2117,47 @@ int schedule_stream(gs_ctx* c, PodRun run, Next&& next_run, Done&& run_done) {
       }
       bool spec = false;
       int nb = 0;
+      using hclk = std::chrono::steady_clock;
+      const auto t_a = hclk::now();
+      double busy = 0;
       if (can_spec && spec_ok && !cur_special && np && c->dirty_list.empty() && !c->prep_stale) {
         bool sf = false;
         nb = batch_len(c, np, nj, nn, &sf);
-        if (!sf && !uid_overlap(pods + i, cur_b, np + nj, nb)) {
+        if (!sf && !uid_overlap(pods + i, cur_b, np + nj, nb) &&
+            !(pend.n && uid_overlap(prev_pods, prev_n, np + nj, nb))) {
           const int32_t* prev = c->d_committed;
           const PlacementDev* prev_out = c->d_out;
           const int here = c->cur_slot;
           bind_slot(c, 1 - here);
           rc = stage_batch(c, np, ns, nj, nb, true);
+          const auto t_b = hclk::now();
           if (!rc) rc = launch_batch(c, nb, prev, prev_out, cur_b);
+          if (c->host_timing) {
+            const double st = std::chrono::duration<double, std::micro>(t_b - t_a).count();
+            const double la = std::chrono::duration<double, std::micro>(hclk::now() - t_b).count();
+            c->ht_stage += st;
+            c->ht_launch += la;
+            busy += st + la;
+          }
           bind_slot(c, here);
           if (rc) { drain(); return rc; }
           spec = true;
         }
       }
+      {   // the batch before this one, committed on the device: its placements on the host now
+        const auto t_p = hclk::now();
+        if ((rc = apply_pending())) { if (spec) drain(); return rc; }
+        if (c->host_timing) {
+          const double ap = std::chrono::duration<double, std::micro>(hclk::now() - t_p).count();
+          c->ht_apply += ap;
+          busy += ap;
+        }
+      }
       spec_ok = true;
       int committed = 0;
+      const auto t_w = hclk::now();
       rc = finish_batch(c, cur_b, spec, &committed);
+      const auto t_f = hclk::now();
       if (rc == GS_REDO) {   // pod 0 needs the full-row path, the speculative pass (void) overwrote its lists: re-run
         drain();
         if ((rc = stage_batch(c, pods, run.seq, i, cur_b, false))) return rc;
@@ -2075,17 +2168,30 @@ int schedule_stream(gs_ctx* c, PodRun run, Next&& next_run, Done&& run_done) {
       }
       if (rc) { if (spec) drain(); return rc; }
       const bool host_work = c->h_committed[1] != 1;   // the device-side continuation flag the speculative pass read
-      for (int k = 0; k < committed; ++k) {
-        const PlacementDev& pd = c->h_out[k];
-        gs_placement& o = run.out[i + k];
-        o.node = pd.node;
-        o.feasible = pd.feasible;
-        o.score = pd.node >= 0 ? pd.score : 0;
-        o.ties = pd.node >= 0 ? pd.ties : 0;
-        o.flags = pd.flags & ~PL_INTERNAL_FLAGS;
-        if (pd.flags & GS_PLACED_SLOWPATH) c->stats.slowpath_pods += 1;   // resolved from its whole score row
-        if ((rc = numa_reserve(c, pods[i + k], c->h_pods[k], pd))) { if (spec) drain(); return rc; }
-        apply_placement(c, pods[i + k], pd.node, cur_special);
+      const bool defer = spec && !host_work && committed == cur_b && !cur_special && c->dirty_list.empty() &&
+                         !c->prep_stale;
+      if (defer) {   // its successor runs: applied once the batch after that is enqueued
+        pend.n = committed;
+        pend.special = cur_special;
+        pend.pods = pods + i;
+        pend.out = run.out + i;
+        pend.h_out.assign(c->h_out, c->h_out + committed);
+        pend.h_pods.assign(c->h_pods, c->h_pods + committed);
+        prev_pods = pods + i;
+        prev_n = committed;
+      } else if ((rc = apply_batch(pods + i, run.out + i, committed, c->h_out, c->h_pods, cur_special))) {
+        if (spec) drain();
+        return rc;
+      }
+      if (c->host_timing) {
+        const double wt = std::chrono::duration<double, std::micro>(t_f - t_w).count();
+        const double ap = std::chrono::duration<double, std::micro>(hclk::now() - t_f).count();
+        c->ht_wait += wt;
+        c->ht_apply += ap;
+        busy += ap;
+        c->ht_batches += 1;
+        c->ht_max_busy = std::max(c->ht_max_busy, busy);
+        c->ht_busy_hist[std::min(7, (int)(busy / 100.0))] += 1;   // 100-us bins
       }
       c->stats.pods += committed;
       c->stats_all_pods += committed;
@@ -2106,10 +2212,12 @@ int schedule_stream(gs_ctx* c, PodRun run, Next&& next_run, Done&& run_done) {
         }
       }
     }
+    if ((rc = apply_pending())) return rc;
     return flush_rows(c);
   };
-  const int rc = body();
+  int rc = body();
   if (rc) {
+    (void)apply_pending();   // placements the device committed before the failure
     run_done(run, rc);
     if (have_nxt) run_done(nxt, GS_ESTATE);
   }
