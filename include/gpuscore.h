@@ -392,6 +392,11 @@ int gs_node_metrics_upsert(gs_ctx* ctx, const uint32_t* idx, const gs_node_metri
 int gs_pods_assign(gs_ctx* ctx, const uint32_t* node_idx, const gs_pod* pods, const int64_t* timestamps_ns,
                    uint32_t n);
 int gs_pods_unassign(gs_ctx* ctx, const uint32_t* node_idx, const gs_pod* pods, uint32_t n);
+/* The scheduler cache's ForgetPod of assumed pods (gs_schedule placed them) once their Reserve is undone: a rejected
+ * Permit or a failed binding cycle ([upstream] schedule_one.go: RunReservePluginsUnreserve + Cache.ForgetPod):
+ * NodeInfo.RemovePod, LoadAware Unreserve (podAssignCache.unAssign, load_aware.go:265-267) and NodeNUMAResource
+ * Unreserve (resourceManager.Release, nodenumaresource/plugin.go:467-476). node_idx[i]: the node pod i was assumed on. */
+int gs_pods_forget(gs_ctx* ctx, const uint32_t* node_idx, const gs_pod* pods, uint32_t n);
 /* podAssignCache's pod informer handlers OnAdd / OnUpdate / OnDelete (loadaware/pod_assign_cache.go:82-117):
  * node_idx[i] = pod.Spec.NodeName as a node index (-1: "", a pending pod), the GS_POD_TERMINATED flag =
  * util.IsPodTerminated(pod); assign stamps the injected now (timeNowFn). */
@@ -764,6 +769,81 @@ typedef struct gs_merge_result {
   int32_t pad;
 } gs_merge_result;
 int gs_debug_numa_merge(gs_ctx* ctx, const gs_merge_case* cases, uint32_t n, gs_merge_result* out);
+/* ---- Coscheduling: the PodGroupManager of pkg/scheduler/plugins/coscheduling/core/core.go over its
+ * gang cache (gang.go, gang_cache.go) as host state. A per-pod gate in front of gs_schedule (PreFilter) and the Permit /
+ * PostFilter / Unreserve / PostBind decisions on assumed pods; a rejected pod's Reserve is undone by gs_pods_forget.
+ * Gangs are keyed by the caller's 64-bit key of GetId(namespace, name), pods by UID (koordinator_amd/gang.py). */
+#define GS_GANG_STRICT 0
+#define GS_GANG_NONSTRICT 1
+#define GS_GANG_ONCE_SATISFIED 0        /* extension.GangMatchPolicyOnceSatisfied (the default) */
+#define GS_GANG_ONLY_WAITING 1
+#define GS_GANG_WAITING_AND_RUNNING 2
+#define GS_GANG_GROUP_MAX 8
+typedef struct gs_gang_args {           /* CoschedulingArgs */
+  int64_t default_timeout_ns;           /* DefaultTimeout (600 s) */
+  int32_t skip_check_schedule_cycle;    /* SkipCheckScheduleCycle */
+  int32_t pad;
+} gs_gang_args;
+typedef struct gs_gang_spec {           /* a PodGroup, or a pod's gang annotations, decoded (gang.go:112-232) */
+  uint64_t gang_id;
+  int32_t min_member;                   /* Spec.MinMember / the min-available annotation (< 0: illegal: no init) */
+  int32_t total_children;               /* the total-number annotation (-1: absent or not an integer) */
+  int32_t mode;                         /* GS_GANG_STRICT / _NONSTRICT (-1: absent or illegal: Strict) */
+  int32_t match_policy;                 /* GS_GANG_* policy (-1: absent or illegal: once-satisfied) */
+  int64_t wait_time_ns;                 /* ScheduleTimeoutSeconds / the wait-time annotation (-1: absent or illegal) */
+  int64_t create_time_ns;
+  uint32_t group_n, pad;                /* the gang-groups annotation (0: the gang alone) */
+  uint64_t group[GS_GANG_GROUP_MAX];
+} gs_gang_spec;
+typedef struct gs_gang_info {
+  int32_t has_init, min_member, total_children, mode, match_policy, schedule_cycle, schedule_cycle_valid,
+      once_resource_satisfied, children, waiting, bound, pad;
+  int64_t wait_time_ns;
+} gs_gang_info;
+#define GS_GANG_PREFILTER_OK 0
+#define GS_GANG_PREFILTER_NOT_FOUND 1           /* "can't find gang" */
+#define GS_GANG_PREFILTER_NOT_INIT 2            /* "gang has not init" */
+#define GS_GANG_PREFILTER_NOT_ENOUGH_CHILDREN 3 /* "gang child pod not collect enough" */
+#define GS_GANG_PREFILTER_CYCLE_INVALID 4       /* "gang scheduleCycle not valid" */
+#define GS_GANG_PREFILTER_CYCLE_TOO_LARGE 5     /* "pod's schedule cycle too large" */
+#define GS_GANG_PERMIT_SUCCESS 0
+#define GS_GANG_PERMIT_WAIT 1
+#define GS_GANG_PERMIT_NOT_FOUND 2
+typedef struct gs_gang_mgr gs_gang_mgr;
+void gs_gang_args_default(gs_gang_args* a);
+int gs_gang_mgr_create(const gs_gang_args* args, gs_gang_mgr** out);
+int gs_gang_mgr_destroy(gs_gang_mgr* m);
+int gs_gang_mgr_clone(const gs_gang_mgr* m, gs_gang_mgr** out);      /* a copy of the whole state (speculation) */
+int gs_gang_mgr_assign(gs_gang_mgr* dst, const gs_gang_mgr* src);    /* dst := src */
+int gs_gang_podgroup_upsert(gs_gang_mgr* m, const gs_gang_spec* s);  /* onPodGroupAdd / Update: tryInitByPodGroup */
+int gs_gang_podgroup_delete(gs_gang_mgr* m, uint64_t gang_id);
+/* onPodAdd / onPodUpdate of a gang pod (gang_cache.go:85-120); annot: the pod's gang annotations when it has no PodGroup
+ * label (NULL otherwise); assigned: Spec.NodeName is set. */
+int gs_gang_pod_add(gs_gang_mgr* m, uint64_t gang_id, uint64_t uid, int assigned, const gs_gang_spec* annot);
+int gs_gang_pod_delete(gs_gang_mgr* m, uint64_t gang_id, uint64_t uid);
+/* PreFilter (core.go:221-272); gang_id 0: not a gang pod. Returns a GS_GANG_PREFILTER_* code (not OK:
+ * UnschedulableAndUnresolvable, then PostFilter). nominated: Status.NominatedNodeName is set. */
+int gs_gang_prefilter(gs_gang_mgr* m, uint64_t gang_id, uint64_t uid, int nominated);
+/* Permit (core.go:312-339, coscheduling.go:190-210) of an assumed pod: GS_GANG_PERMIT_SUCCESS with allowed[] = the gang
+ * group's waiting pods that go on to bind, _WAIT (deadline now_ns + *wait_ns), or _NOT_FOUND. */
+int gs_gang_permit(gs_gang_mgr* m, uint64_t gang_id, uint64_t uid, int64_t now_ns, int64_t* wait_ns, uint64_t* allowed,
+                   uint32_t cap, uint32_t* n_allowed);
+int gs_gang_post_bind(gs_gang_mgr* m, uint64_t gang_id, uint64_t uid);   /* PostBind (core.go:397-447) */
+/* PostFilter (core.go:277-307) of a gang pod that found no node: rejected[] = waiting pods to Unreserve. */
+int gs_gang_post_filter(gs_gang_mgr* m, uint64_t gang_id, uint64_t uid, uint64_t* rejected, uint32_t cap,
+                        uint32_t* n_rejected);
+/* Unreserve (core.go:344-361) of a rejected / failed assumed gang pod: rejected[] = further waiting pods to Unreserve. */
+int gs_gang_unreserve(gs_gang_mgr* m, uint64_t gang_id, uint64_t uid, uint64_t* rejected, uint32_t cap,
+                      uint32_t* n_rejected);
+/* The framework's Permit timeout at now_ns: rejected[] = waiting pods past their deadline (Unreserve follows). */
+int gs_gang_expire(gs_gang_mgr* m, int64_t now_ns, uint64_t* rejected, uint32_t cap, uint32_t* n_rejected);
+int gs_gang_get(const gs_gang_mgr* m, uint64_t gang_id, gs_gang_info* out);   /* 1: found, 0: no such gang */
+int gs_gang_child_cycle(const gs_gang_mgr* m, uint64_t gang_id, uint64_t uid); /* ChildrenScheduleRoundMap (-1: none) */
+int gs_gang_waiting_pods(const gs_gang_mgr* m, uint64_t* uids, uint32_t cap, uint32_t* n);
+/* Test hook (the reference's tests set gang fields directly): what 0 ScheduleCycleValid, 1 the pod's schedule cycle,
+ * 2 OnceResourceSatisfied, 3 GangMatchPolicy (3: a value outside the three), 4 SkipCheckScheduleCycle. */
+int gs_gang_debug_set(gs_gang_mgr* m, uint64_t gang_id, uint64_t uid, int what, int value);
+
 /* sizeof() of the ABI structs as compiled into the library, in this order: gs_pod, gs_node,
  * gs_node_metric, gs_pod_metric, gs_config, gs_placement, gs_stats, gs_loadaware_args, gs_cpu_topology,
  * gs_node_numa, gs_pod_allocation, gs_numa_args, gs_quota_group, gs_quota_status. */

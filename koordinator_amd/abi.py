@@ -269,6 +269,21 @@ class GsMergeResult(C.Structure):
     _fields_ = [("admit", i32), ("aff_has", i32), ("aff", u32), ("pad", i32)]
 
 
+class GsGangArgs(C.Structure):
+    _fields_ = [("default_timeout_ns", i64), ("skip_check_schedule_cycle", i32), ("pad", i32)]
+
+
+class GsGangSpec(C.Structure):
+    _fields_ = [("gang_id", u64), ("min_member", i32), ("total_children", i32), ("mode", i32), ("match_policy", i32),
+                ("wait_time_ns", i64), ("create_time_ns", i64), ("group_n", u32), ("pad", u32), ("group", u64 * 8)]
+
+
+class GsGangInfo(C.Structure):
+    _fields_ = [(n, i32) for n in ("has_init", "min_member", "total_children", "mode", "match_policy", "schedule_cycle",
+                                   "schedule_cycle_valid", "once_resource_satisfied", "children", "waiting", "bound",
+                                   "pad")] + [("wait_time_ns", i64)]
+
+
 MERGE_CASE_DTYPE = np.dtype(GsMergeCase)
 MERGE_RESULT_DTYPE = np.dtype(GsMergeResult)
 POD_DTYPE = np.dtype(GsPod)
@@ -314,6 +329,7 @@ SIGNATURES = {
     "gs_node_metrics_upsert": (C.c_int, [P, P, P, u32, P, P]),
     "gs_pods_assign": (C.c_int, [P, P, P, P, u32]),
     "gs_pods_unassign": (C.c_int, [P, P, P, u32]),
+    "gs_pods_forget": (C.c_int, [P, P, P, u32]),
     "gs_evaluate": (C.c_int, [P, P, u32, P, P, P]),
     "gs_schedule": (C.c_int, [P, P, u32, P, P]),
     "gs_schedule_submit": (C.c_int, [P, P, u32, P, P, C.POINTER(u64)]),
@@ -328,6 +344,25 @@ SIGNATURES = {
     "gs_debug_verify_cpuset": (C.c_int, [P, C.c_int]),
     "gs_debug_pair_probe": (C.c_int, [P, P, C.c_uint32, P, P, C.c_uint32, C.c_int, P, P]),
     "gs_debug_numa_merge": (C.c_int, [P, P, u32, P]),
+    "gs_gang_args_default": (None, [C.POINTER(GsGangArgs)]),
+    "gs_gang_mgr_create": (C.c_int, [C.POINTER(GsGangArgs), C.POINTER(P)]),
+    "gs_gang_mgr_destroy": (C.c_int, [P]),
+    "gs_gang_mgr_clone": (C.c_int, [P, C.POINTER(P)]),
+    "gs_gang_mgr_assign": (C.c_int, [P, P]),
+    "gs_gang_podgroup_upsert": (C.c_int, [P, C.POINTER(GsGangSpec)]),
+    "gs_gang_podgroup_delete": (C.c_int, [P, u64]),
+    "gs_gang_pod_add": (C.c_int, [P, u64, u64, C.c_int, C.POINTER(GsGangSpec)]),
+    "gs_gang_pod_delete": (C.c_int, [P, u64, u64]),
+    "gs_gang_prefilter": (C.c_int, [P, u64, u64, C.c_int]),
+    "gs_gang_permit": (C.c_int, [P, u64, u64, i64, C.POINTER(i64), P, u32, C.POINTER(u32)]),
+    "gs_gang_post_bind": (C.c_int, [P, u64, u64]),
+    "gs_gang_post_filter": (C.c_int, [P, u64, u64, P, u32, C.POINTER(u32)]),
+    "gs_gang_unreserve": (C.c_int, [P, u64, u64, P, u32, C.POINTER(u32)]),
+    "gs_gang_expire": (C.c_int, [P, i64, P, u32, C.POINTER(u32)]),
+    "gs_gang_get": (C.c_int, [P, u64, C.POINTER(GsGangInfo)]),
+    "gs_gang_child_cycle": (C.c_int, [P, u64, u64]),
+    "gs_gang_waiting_pods": (C.c_int, [P, P, u32, C.POINTER(u32)]),
+    "gs_gang_debug_set": (C.c_int, [P, u64, u64, C.c_int, C.c_int]),
     "gs_reason_string": (C.c_int, [C.c_uint32, C.c_uint32, P, C.c_char_p, C.c_size_t]),
     "gs_reset": (C.c_int, [P]),
     "gs_abi_sizes": (None, [C.POINTER(u64), u32]),

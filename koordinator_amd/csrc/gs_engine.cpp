@@ -1906,6 +1906,35 @@ int gs_pods_unassign(gs_ctx* c, const uint32_t* node_idx, const gs_pod* pods, ui
   return flush_rows(c);
 }
 
+// The scheduler cache's ForgetPod of an assumed pod after the Unreserve plugins ([upstream] scheduleOne's binding-cycle
+// failure path): NodeInfo.RemovePod, LoadAware Unreserve (podAssignCache.unAssign, load_aware.go:265-267) and
+// NodeNUMAResource Unreserve (resourceManager.Release, plugin.go:467-476).
+int gs_pods_forget(gs_ctx* c, const uint32_t* node_idx, const gs_pod* pods, uint32_t n) {
+  if (!c || (n && (!node_idx || !pods))) return GS_EINVAL;
+  quiesce(c);
+  for (uint32_t j = 0; j < n; ++j)
+    if (node_idx[j] >= c->N) return fail(c, GS_EINVAL, "node index %u >= %u", node_idx[j], c->N);
+  for (uint32_t j = 0; j < n; ++j) {
+    const uint32_t i = node_idx[j];
+    const gs_pod& p = pods[j];
+    HostNode& hn = c->nodes[i];
+    for (int s = 0; s < GS_NUM_RES; ++s) hn.node.requested[s] -= p.requests[s];
+    hn.node.nonzero_requested[0] -= p.nonzero_requests[0];
+    hn.node.nonzero_requested[1] -= p.nonzero_requests[1];
+    hn.node.pod_count -= 1;
+    hn.assigned.erase(p.uid);
+    auto it = c->uid_node.find(p.uid);
+    if (it != c->uid_node.end() && it->second == i) c->uid_node.erase(it);
+    if (c->numa_on) {
+      numa_release(c->numa[i], p.uid);
+      auto nt = c->numa_uid_node.find(p.uid);
+      if (nt != c->numa_uid_node.end() && nt->second == i) c->numa_uid_node.erase(nt);
+    }
+    mark_dirty(c, i);
+  }
+  return flush_rows(c);
+}
+
 int gs_pods_on_event(gs_ctx* c, int event, const int32_t* node_idx, const gs_pod* pods, uint32_t n) {
   if (!c || (n && (!node_idx || !pods))) return GS_EINVAL;
   quiesce(c);

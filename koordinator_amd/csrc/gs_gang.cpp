@@ -1,0 +1,372 @@
+// gs_gang.cpp — Coscheduling's gang state: the PodGroupManager of
+// pkg/scheduler/plugins/coscheduling/core/core.go over the gang cache (gang.go, gang_cache.go), as host state of the
+// library. It touches no node: PreFilter is a per-pod gate in front of gs_schedule, Permit / PostFilter / Unreserve
+// decide which assumed pods wait, bind or are rejected, and the caller undoes a rejected pod's Reserve with
+// gs_pods_forget (koordinator_amd/gang.py drives both in the reference's per-pod order over batched gs_schedule calls).
+//
+// Keys: a gang is GetId(namespace, name) and a pod its UID, both as the caller's 64-bit keys. The framework's waiting
+// pods (framework.WaitingPod, the pods that got Wait at Permit) of gang pods are tracked here with their Permit deadline.
+// Where the reference iterates a Go map (IterateOverWaitingPods), pods are visited in UID order; no result depends on it.
+#include <algorithm>
+#include <cstring>
+#include <map>
+#include <set>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/gpuscore.h"
+
+namespace {
+
+struct Gang {
+  bool has_init = false;
+  int min = 0, total = 0;
+  int mode = GS_GANG_STRICT;
+  int policy = GS_GANG_ONCE_SATISFIED;
+  int64_t wait_ns = 0;
+  int64_t create_ns = 0;
+  std::vector<uint64_t> group;
+  bool from_annotation = true;   // GangFromPodAnnotation (NewGang's default)
+  std::set<uint64_t> children, waiting, bound;   // Children, WaitingForBindChildren, BoundChildren
+  bool once = false;             // OnceResourceSatisfied
+  bool cycle_valid = true;       // ScheduleCycleValid
+  int cycle = 1;                 // ScheduleCycle
+  std::unordered_map<uint64_t, int> child_cycle;   // ChildrenScheduleRoundMap
+
+  bool valid_for_permit() const {   // isGangValidForPermit (gang.go:480-496)
+    if (!has_init) return false;
+    const int w = (int)waiting.size(), b = (int)bound.size();
+    if (policy == GS_GANG_ONLY_WAITING) return w >= min;
+    if (policy == GS_GANG_WAITING_AND_RUNNING) return w + b >= min;
+    return w >= min || once;
+  }
+  void add_bound(uint64_t uid) {    // addBoundPod (gang.go:466-477)
+    waiting.erase(uid);
+    bound.insert(uid);
+    if ((int)bound.size() >= min) once = true;
+  }
+};
+
+}  // namespace
+
+struct gs_gang_mgr {
+  gs_gang_args args{};
+  std::map<uint64_t, Gang> gangs;
+  std::map<uint64_t, std::pair<uint64_t, int64_t>> fw_waiting;   // pod uid -> (gang id, Permit deadline)
+
+  Gang* get(uint64_t id, bool create) {   // getGangFromCacheByGangId (gang_cache.go:48-63) + NewGang (gang.go:92-110)
+    auto it = gangs.find(id);
+    if (it != gangs.end()) return &it->second;
+    if (!create) return nullptr;
+    Gang& g = gangs[id];
+    g.group = {id};
+    return &g;
+  }
+  // rejectGangGroupById (core.go:363-394): the waiting pods of the gang group are rejected (their Unreserve follows)
+  void reject_group(uint64_t id, std::vector<uint64_t>* rejected) {
+    Gang* g = get(id, false);
+    if (!g) return;
+    const std::set<uint64_t> grp(g->group.begin(), g->group.end());
+    int n = 0;
+    for (auto it = fw_waiting.begin(); it != fw_waiting.end();) {
+      if (grp.count(it->second.first)) {
+        rejected->push_back(it->first);
+        it = fw_waiting.erase(it);
+        ++n;
+      } else {
+        ++it;
+      }
+    }
+    if (!n) return;
+    for (uint64_t gid : grp)
+      if (Gang* x = get(gid, false)) x->cycle_valid = false;
+  }
+};
+
+namespace {
+
+int copy_out(const std::vector<uint64_t>& v, uint64_t* out, uint32_t cap, uint32_t* n) {
+  if (n) *n = (uint32_t)v.size();
+  if (v.size() > cap) return GS_EINVAL;
+  if (out)
+    for (size_t k = 0; k < v.size(); ++k) out[k] = v[k];
+  return GS_OK;
+}
+
+// tryInitByPodGroup (gang.go:180-232) / tryInitByPodConfig (gang.go:112-178) on a decoded spec
+void init_gang(Gang& g, const gs_gang_spec& s, bool from_podgroup, int64_t default_timeout) {
+  g.min = s.min_member;
+  int64_t total = s.total_children;
+  if (total < 0 || (total != 0 && total < g.min)) total = g.min;   // unparsable, or below the minimum
+  g.total = (int)total;
+  g.mode = (s.mode == GS_GANG_NONSTRICT) ? GS_GANG_NONSTRICT : GS_GANG_STRICT;
+  g.policy = (s.match_policy == GS_GANG_ONLY_WAITING || s.match_policy == GS_GANG_WAITING_AND_RUNNING)
+                 ? s.match_policy
+                 : GS_GANG_ONCE_SATISFIED;
+  g.create_ns = s.create_time_ns;
+  // GetWaitTimeDuration: ScheduleTimeoutSeconds >= 0 (PodGroup); the annotation's duration when > 0
+  const bool ok_wait = from_podgroup ? s.wait_time_ns >= 0 : s.wait_time_ns > 0;
+  g.wait_ns = ok_wait ? s.wait_time_ns : default_timeout;
+  g.group.clear();
+  for (uint32_t k = 0; k < s.group_n && k < GS_GANG_GROUP_MAX; ++k) g.group.push_back(s.group[k]);
+  if (g.group.empty()) g.group.push_back(s.gang_id);
+  g.from_annotation = !from_podgroup;
+  g.has_init = true;
+}
+
+}  // namespace
+
+extern "C" {
+
+void gs_gang_args_default(gs_gang_args* a) {
+  if (!a) return;
+  std::memset(a, 0, sizeof(*a));
+  a->default_timeout_ns = 600LL * 1000000000LL;   // CoschedulingArgs.DefaultTimeout (config/v1beta2/defaults.go: 600 s)
+}
+
+int gs_gang_mgr_create(const gs_gang_args* args, gs_gang_mgr** out) {
+  if (!out) return GS_EINVAL;
+  auto* m = new gs_gang_mgr();
+  if (args) m->args = *args;
+  else gs_gang_args_default(&m->args);
+  *out = m;
+  return GS_OK;
+}
+
+int gs_gang_mgr_destroy(gs_gang_mgr* m) {
+  delete m;
+  return GS_OK;
+}
+
+int gs_gang_mgr_clone(const gs_gang_mgr* m, gs_gang_mgr** out) {
+  if (!m || !out) return GS_EINVAL;
+  *out = new gs_gang_mgr(*m);
+  return GS_OK;
+}
+
+int gs_gang_mgr_assign(gs_gang_mgr* dst, const gs_gang_mgr* src) {
+  if (!dst || !src) return GS_EINVAL;
+  *dst = *src;
+  return GS_OK;
+}
+
+// onPodGroupAdd / onPodGroupUpdate (gang_cache.go:150-182)
+int gs_gang_podgroup_upsert(gs_gang_mgr* m, const gs_gang_spec* s) {
+  if (!m || !s || !s->gang_id || s->group_n > GS_GANG_GROUP_MAX) return GS_EINVAL;
+  init_gang(*m->get(s->gang_id, true), *s, true, m->args.default_timeout_ns);
+  return GS_OK;
+}
+
+// onPodGroupDelete (gang_cache.go:184-197)
+int gs_gang_podgroup_delete(gs_gang_mgr* m, uint64_t gang_id) {
+  if (!m) return GS_EINVAL;
+  m->gangs.erase(gang_id);
+  return GS_OK;
+}
+
+// onPodAdd / onPodUpdate of a gang pod (gang_cache.go:85-120). annot: the pod's gang annotations when the pod has no
+// PodGroup label (the gang is then initialized from the first pod carrying a legal min number); assigned: Spec.NodeName
+// is set (an already bound member).
+int gs_gang_pod_add(gs_gang_mgr* m, uint64_t gang_id, uint64_t uid, int assigned, const gs_gang_spec* annot) {
+  if (!m || !gang_id || (annot && annot->group_n > GS_GANG_GROUP_MAX)) return GS_EINVAL;
+  Gang& g = *m->get(gang_id, true);
+  if (annot && !g.has_init && annot->min_member >= 0) init_gang(g, *annot, false, m->args.default_timeout_ns);
+  g.children.insert(uid);
+  if (assigned) {
+    g.add_bound(uid);
+    g.once = true;   // setResourceSatisfied
+  }
+  return GS_OK;
+}
+
+// onPodDelete (gang_cache.go:122-148, gang.deletePod)
+int gs_gang_pod_delete(gs_gang_mgr* m, uint64_t gang_id, uint64_t uid) {
+  if (!m) return GS_EINVAL;
+  Gang* g = m->get(gang_id, false);
+  if (!g) return GS_OK;
+  g->children.erase(uid);
+  g->waiting.erase(uid);
+  g->bound.erase(uid);
+  g->child_cycle.erase(uid);
+  m->fw_waiting.erase(uid);
+  if (g->from_annotation && g->children.empty()) m->gangs.erase(gang_id);
+  return GS_OK;
+}
+
+// PodGroupManager.PreFilter (core.go:221-272); gang_id 0: the pod needs no gang. Returns the GS_GANG_PREFILTER_* code
+// (the reference's error message for each is rendered by koordinator_amd/gang.py).
+int gs_gang_prefilter(gs_gang_mgr* m, uint64_t gang_id, uint64_t uid, int nominated) {
+  if (!m) return GS_EINVAL;
+  if (!gang_id) return GS_GANG_PREFILTER_OK;
+  Gang* g = m->get(gang_id, false);
+  if (!g) return GS_GANG_PREFILTER_NOT_FOUND;
+  if (!g->has_init) return GS_GANG_PREFILTER_NOT_INIT;
+  if (g->policy == GS_GANG_ONCE_SATISFIED && g->once) return GS_GANG_PREFILTER_OK;
+  if ((int)g->children.size() < g->min) return GS_GANG_PREFILTER_NOT_ENOUGH_CHILDREN;
+  if (m->args.skip_check_schedule_cycle) return GS_GANG_PREFILTER_OK;
+  {   // trySetScheduleCycleValid (gang.go:435-452)
+    int num = 0;
+    for (const auto& kv : g->child_cycle) num += kv.second == g->cycle;
+    if (num == g->total) {
+      g->cycle_valid = true;
+      g->cycle += 1;
+    }
+  }
+  const int gcycle = g->cycle;
+  int rc = GS_GANG_PREFILTER_OK;
+  if (g->mode == GS_GANG_STRICT && !nominated) {
+    auto it = g->child_cycle.find(uid);
+    const int pcycle = it == g->child_cycle.end() ? 0 : it->second;
+    if (!g->cycle_valid) rc = GS_GANG_PREFILTER_CYCLE_INVALID;
+    else if (pcycle >= gcycle) rc = GS_GANG_PREFILTER_CYCLE_TOO_LARGE;
+  }
+  g->child_cycle[uid] = gcycle;   // the deferred setChildScheduleCycle
+  return rc;
+}
+
+// PodGroupManager.Permit (core.go:312-339) + Coscheduling.Permit (coscheduling.go:190-210): GS_GANG_PERMIT_SUCCESS (the
+// gang group's waiting pods are allowed: allowed[]), _WAIT (the pod waits until wait_ns after now_ns, *wait_ns), or
+// _NOT_FOUND (Unschedulable "Gang not found"). gang_id 0: success, nothing else.
+int gs_gang_permit(gs_gang_mgr* m, uint64_t gang_id, uint64_t uid, int64_t now_ns, int64_t* wait_ns, uint64_t* allowed,
+                   uint32_t cap, uint32_t* n_allowed) {
+  if (!m) return GS_EINVAL;
+  if (n_allowed) *n_allowed = 0;
+  if (wait_ns) *wait_ns = 0;
+  if (!gang_id) return GS_GANG_PERMIT_SUCCESS;
+  Gang* g = m->get(gang_id, false);
+  if (!g) return GS_GANG_PERMIT_NOT_FOUND;
+  g->waiting.insert(uid);   // addAssumedPod
+  for (uint64_t gid : g->group) {
+    const Gang* x = m->get(gid, false);
+    if (!x || !x->valid_for_permit()) {
+      if (wait_ns) *wait_ns = g->wait_ns;
+      m->fw_waiting[uid] = {gang_id, now_ns + g->wait_ns};
+      return GS_GANG_PERMIT_WAIT;
+    }
+  }
+  // AllowGangGroup (core.go:488-508): every waiting pod of the gang group goes on to bind
+  const std::set<uint64_t> grp(g->group.begin(), g->group.end());
+  std::vector<uint64_t> out;
+  for (auto it = m->fw_waiting.begin(); it != m->fw_waiting.end();) {
+    if (grp.count(it->second.first)) {
+      out.push_back(it->first);
+      it = m->fw_waiting.erase(it);
+    } else {
+      ++it;
+    }
+  }
+  const int rc = copy_out(out, allowed, cap, n_allowed);
+  return rc ? rc : GS_GANG_PERMIT_SUCCESS;
+}
+
+// PodGroupManager.PostBind (core.go:397-447): the gang's bound children (the PodGroup status patch is the caller's)
+int gs_gang_post_bind(gs_gang_mgr* m, uint64_t gang_id, uint64_t uid) {
+  if (!m) return GS_EINVAL;
+  if (!gang_id) return GS_OK;
+  if (Gang* g = m->get(gang_id, false)) g->add_bound(uid);
+  return GS_OK;
+}
+
+// PodGroupManager.PostFilter (core.go:277-307) after a gang pod found no node (or failed PreFilter): Strict mode rejects
+// the gang group's waiting pods (rejected[]; the caller runs their Unreserve) and invalidates its schedule cycle.
+int gs_gang_post_filter(gs_gang_mgr* m, uint64_t gang_id, uint64_t uid, uint64_t* rejected, uint32_t cap,
+                        uint32_t* n_rejected) {
+  if (!m) return GS_EINVAL;
+  (void)uid;
+  if (n_rejected) *n_rejected = 0;
+  if (!gang_id) return GS_OK;
+  Gang* g = m->get(gang_id, false);
+  if (!g) return GS_OK;
+  if (g->policy == GS_GANG_ONCE_SATISFIED && g->once) return GS_OK;
+  std::vector<uint64_t> out;
+  if (g->mode == GS_GANG_STRICT) m->reject_group(gang_id, &out);
+  return copy_out(out, rejected, cap, n_rejected);
+}
+
+// PodGroupManager.Unreserve (core.go:344-361) of an assumed gang pod (a rejected waiting pod, or one whose binding
+// cycle failed): it leaves the gang's assumed pods; Strict mode rejects the rest of the gang group's waiting pods.
+int gs_gang_unreserve(gs_gang_mgr* m, uint64_t gang_id, uint64_t uid, uint64_t* rejected, uint32_t cap,
+                      uint32_t* n_rejected) {
+  if (!m) return GS_EINVAL;
+  if (n_rejected) *n_rejected = 0;
+  if (!gang_id) return GS_OK;
+  Gang* g = m->get(gang_id, false);
+  if (!g) return GS_OK;
+  g->waiting.erase(uid);   // delAssumedPod
+  m->fw_waiting.erase(uid);
+  std::vector<uint64_t> out;
+  if (!(g->policy == GS_GANG_ONCE_SATISFIED && g->once) && g->mode == GS_GANG_STRICT) m->reject_group(gang_id, &out);
+  return copy_out(out, rejected, cap, n_rejected);
+}
+
+// The framework's Permit timeout: waiting pods whose deadline is <= now_ns are rejected (their Unreserve follows).
+int gs_gang_expire(gs_gang_mgr* m, int64_t now_ns, uint64_t* rejected, uint32_t cap, uint32_t* n_rejected) {
+  if (!m) return GS_EINVAL;
+  std::vector<uint64_t> out;
+  for (auto it = m->fw_waiting.begin(); it != m->fw_waiting.end();) {
+    if (it->second.second <= now_ns) {
+      out.push_back(it->first);
+      it = m->fw_waiting.erase(it);
+    } else {
+      ++it;
+    }
+  }
+  return copy_out(out, rejected, cap, n_rejected);
+}
+
+int gs_gang_get(const gs_gang_mgr* m, uint64_t gang_id, gs_gang_info* out) {
+  if (!m || !out) return GS_EINVAL;
+  auto it = m->gangs.find(gang_id);
+  if (it == m->gangs.end()) return 0;
+  const Gang& g = it->second;
+  std::memset(out, 0, sizeof(*out));
+  out->has_init = g.has_init;
+  out->min_member = g.min;
+  out->total_children = g.total;
+  out->mode = g.mode;
+  out->match_policy = g.policy;
+  out->schedule_cycle = g.cycle;
+  out->schedule_cycle_valid = g.cycle_valid;
+  out->once_resource_satisfied = g.once;
+  out->children = (int32_t)g.children.size();
+  out->waiting = (int32_t)g.waiting.size();
+  out->bound = (int32_t)g.bound.size();
+  out->wait_time_ns = g.wait_ns;
+  return 1;
+}
+
+// ChildrenScheduleRoundMap[uid] (GetChildScheduleCycle); -1: no entry
+int gs_gang_child_cycle(const gs_gang_mgr* m, uint64_t gang_id, uint64_t uid) {
+  if (!m) return GS_EINVAL;
+  auto it = m->gangs.find(gang_id);
+  if (it == m->gangs.end()) return -1;
+  auto c = it->second.child_cycle.find(uid);
+  return c == it->second.child_cycle.end() ? -1 : c->second;
+}
+
+// Test hook (the reference's tests set these fields directly): what 0 ScheduleCycleValid, 1 ChildrenScheduleRoundMap[uid],
+// 2 OnceResourceSatisfied, 3 GangMatchPolicy (3: a value outside the three policies), 4 args.SkipCheckScheduleCycle
+int gs_gang_debug_set(gs_gang_mgr* m, uint64_t gang_id, uint64_t uid, int what, int value) {
+  if (!m) return GS_EINVAL;
+  if (what == 4) { m->args.skip_check_schedule_cycle = value; return GS_OK; }
+  Gang* g = m->get(gang_id, false);
+  if (!g) return GS_EINVAL;
+  switch (what) {
+    case 0: g->cycle_valid = value != 0; break;
+    case 1: g->child_cycle[uid] = value; break;
+    case 2: g->once = value != 0; break;
+    case 3: g->policy = value; break;
+    default: return GS_EINVAL;
+  }
+  return GS_OK;
+}
+
+// The framework's waiting pods of gangs (uids ascending)
+int gs_gang_waiting_pods(const gs_gang_mgr* m, uint64_t* uids, uint32_t cap, uint32_t* n) {
+  if (!m) return GS_EINVAL;
+  std::vector<uint64_t> v;
+  for (const auto& kv : m->fw_waiting) v.push_back(kv.first);
+  return copy_out(v, uids, cap, n);
+}
+
+}  // extern "C"

@@ -93,6 +93,12 @@ class Engine:
         pods = np.ascontiguousarray(pods, dtype=abi.POD_DTYPE)
         self._chk(lib().gs_pods_unassign(self._h, abi.ptr(node_idx), abi.ptr(pods), len(pods)), "gs_pods_unassign")
 
+    def forget(self, node_idx, pods):
+        """gs_pods_forget: ForgetPod of assumed pods after Unreserve (NodeInfo, podAssignCache, NUMA allocation)."""
+        node_idx = np.ascontiguousarray(node_idx, dtype=np.uint32)
+        pods = np.ascontiguousarray(pods, dtype=abi.POD_DTYPE)
+        self._chk(lib().gs_pods_forget(self._h, abi.ptr(node_idx), abi.ptr(pods), len(pods)), "gs_pods_forget")
+
     def evaluate(self, pods):
         pods = np.ascontiguousarray(pods, dtype=abi.POD_DTYPE)
         P, N = len(pods), self.n

@@ -695,6 +695,24 @@ int or_pods_unassign(or_cluster* c, const uint32_t* node_idx, const gs_pod* pods
   return GS_OK;
 }
 
+// ForgetPod of an assumed pod after Unreserve: NodeInfo.RemovePod ([upstream] framework/types.go), LoadAware
+// podAssignCache.unAssign (load_aware.go:265-267), NodeNUMAResource resourceManager.Release (plugin.go:467-476)
+int or_pods_forget(or_cluster* c, const uint32_t* node_idx, const gs_pod* pods, uint32_t n) {
+  if (!c || (n && (!node_idx || !pods))) return GS_EINVAL;
+  for (uint32_t i = 0; i < n; ++i)
+    if (node_idx[i] >= c->nodes.size()) return GS_EINVAL;
+  for (uint32_t i = 0; i < n; ++i) {
+    gs_node& nd = c->nodes[node_idx[i]].node;
+    for (int r = 0; r < GS_NUM_RES; ++r) nd.requested[r] -= pods[i].requests[r];
+    nd.nonzero_requested[0] -= pods[i].nonzero_requests[0];
+    nd.nonzero_requested[1] -= pods[i].nonzero_requests[1];
+    nd.pod_count -= 1;
+    c->nodes[node_idx[i]].assigned.erase(pods[i].uid);
+    if (node_idx[i] < c->numa.size()) c->numa[node_idx[i]].alloc.release(pods[i].uid);
+  }
+  return GS_OK;
+}
+
 // podAssignCache.OnAdd / OnUpdate / OnDelete (pod_assign_cache.go:82-117) over assign / unAssign (:53-80)
 int or_pods_on_event(or_cluster* c, int event, const int32_t* node_idx, const gs_pod* pods, uint32_t n) {
   if (!c || (n && (!node_idx || !pods))) return GS_EINVAL;

@@ -30,6 +30,7 @@ int or_node_metrics_upsert(or_cluster* c, const uint32_t* idx, const gs_node_met
                            const gs_pod_metric* pm, const uint32_t* pm_offsets);
 int or_pods_assign(or_cluster* c, const uint32_t* node_idx, const gs_pod* pods, const int64_t* ts, uint32_t n);
 int or_pods_unassign(or_cluster* c, const uint32_t* node_idx, const gs_pod* pods, uint32_t n);
+int or_pods_forget(or_cluster* c, const uint32_t* node_idx, const gs_pod* pods, uint32_t n);
 int or_pods_on_event(or_cluster* c, int event, const int32_t* node_idx, const gs_pod* pods, uint32_t n);
 int or_assign_cache_get(or_cluster* c, uint32_t node, uint64_t* uids, int64_t* ts, uint32_t cap);
 

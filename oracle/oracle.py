@@ -34,6 +34,7 @@ def _load() -> C.CDLL:
         "or_node_metrics_upsert": (C.c_int, [P, P, P, C.c_uint32, P, P]),
         "or_pods_assign": (C.c_int, [P, P, P, P, C.c_uint32]),
         "or_pods_unassign": (C.c_int, [P, P, P, C.c_uint32]),
+        "or_pods_forget": (C.c_int, [P, P, P, C.c_uint32]),
         "or_estimate_pod": (C.c_int, [C.POINTER(abi.GsLoadAwareArgs), P, P, P]),
         "or_estimate_node": (C.c_int, [P, P]),
         "or_loadaware_filter": (C.c_int, [P, P, C.c_uint32, P]),
@@ -145,6 +146,11 @@ class Oracle:
         node_idx = np.ascontiguousarray(node_idx, dtype=np.uint32)
         pods = np.ascontiguousarray(pods, dtype=abi.POD_DTYPE)
         _chk(lib().or_pods_unassign(self._h, abi.ptr(node_idx), abi.ptr(pods), len(pods)), "unassign")
+
+    def forget(self, node_idx, pods):
+        node_idx = np.ascontiguousarray(node_idx, dtype=np.uint32)
+        pods = np.ascontiguousarray(pods, dtype=abi.POD_DTYPE)
+        _chk(lib().or_pods_forget(self._h, abi.ptr(node_idx), abi.ptr(pods), len(pods)), "forget")
 
     # plugin-level
     def loadaware_filter(self, pod, node: int) -> bool:
