@@ -178,6 +178,7 @@ struct gs_ctx {
   uint64_t stats_all_pods = 0;     // pods placed by gs_schedule over the context's life (stamp averages)
   // GS_HOST_TIMING=1: host time per batch of schedule_stream, by phase (printed by gs_destroy)
   bool host_timing = false;
+  bool cu_partition = false;   // GS_COMMIT_CUS > 0: commit chain and eval pass on disjoint CUs
   double ht_wait = 0, ht_apply = 0, ht_stage = 0, ht_launch = 0, ht_max_busy = 0;
   uint64_t ht_batches = 0, ht_busy_hist[8] = {};
   // NodeNUMAResource: per-node TopologyOptions + NodeAllocation mirror, registered CPU topologies
@@ -189,6 +190,8 @@ struct gs_ctx {
   // the shard's nodes with a NUMA topology policy (eval_numa_kernel's work list), rebuilt when policies change
   uint32_t* d_numa_idx = nullptr;
   uint32_t numa_n = 0;
+  MirrorView slab_mv{nullptr, nullptr, 0};   // the eval pass's dense copy of the NUMA-policy rows (gather_numa_kernel)
+  uint32_t slab_cap = 0;
   bool numa_idx_stale = true;
   // registered topologies in bit-plane form (the commit kernel's cpuset Reserve), and the host re-check of
   // every device-chosen cpuset (GS_VERIFY_CPUSET=1)
@@ -959,12 +962,23 @@ int launch_batch(gs_ctx* c, int b, const int32_t* prev, const PlacementDev* prev
       HIP_TRY(c, hipMalloc(&c->d_numa_idx, 4 * idx.size()));
       HIP_TRY(c, hipMemcpy(c->d_numa_idx, idx.data(), 4 * idx.size(), hipMemcpyHostToDevice));
     }
+    static const bool no_slab = getenv("GS_NUMA_SLAB") && getenv("GS_NUMA_SLAB")[0] == '0';
+    if (!no_slab && c->numa_n > c->slab_cap) {   // columns of numa_n entries (rounded), the mirror's numbering
+      HIP_TRY(c, hipStreamSynchronize(c->st_ev));
+      if (c->slab_mv.i64) (void)hipFree(c->slab_mv.i64);
+      if (c->slab_mv.i32) (void)hipFree(c->slab_mv.i32);
+      c->slab_mv = MirrorView{nullptr, nullptr, 0};
+      c->slab_cap = (c->numa_n + 1023) & ~1023u;
+      HIP_TRY(c, hipMalloc(&c->slab_mv.i64, (size_t)NUM_I64_COLS * c->slab_cap * 8));
+      HIP_TRY(c, hipMalloc(&c->slab_mv.i32, (size_t)NUM_I32_COLS * c->slab_cap * 4));
+      c->slab_mv.npad = c->slab_cap;
+    }
     c->numa_idx_stale = false;
   }
   const gs_ctx::Slot& sl = c->slot[c->cur_slot];
   HIP_TRY(c, hipEventRecord(c->ev[0], c->st_ev));
   HIP_TRY(c, launch_eval(c->mv, c->d_pods, b, c->pf, c->n0, c->n1, c->d_S, c->ld, prod_cols, c->d_numa_idx, c->numa_n,
-                         c->d_aff, c->st_ev, c->st2, c->ev_fork, c->ev_join));
+                         c->d_aff, c->st_ev, c->st2, c->ev_fork, c->ev_join, c->slab_mv.i64 ? &c->slab_mv : nullptr));
   HIP_TRY(c, hipEventRecord(c->ev[1], c->st_ev));
   HIP_TRY(c, hipEventRecord(sl.ev_evdone, c->st_ev));
   HIP_TRY(c, hipStreamWaitEvent(c->st, sl.ev_evdone, 0));
@@ -1620,14 +1634,17 @@ int gs_create(const gs_config* cfg, gs_ctx** out) {
   int ncu = 0;
   (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, cfg->device);
   const char* cus_env = getenv("GS_COMMIT_CUS");
-  // (measured on C3, pods/s: no partition 120k, 8 CUs 129k, 32 CUs 141-148k, 64 CUs 143-147k; the commit kernel alone on
-  // 4 CUs of a stream of its own, patch / cand with the eval pass: 138k, the cross-stream hops cost more than they save)
-  const int commit_cus = cus_env ? atoi(cus_env) : 32;
+  // (measured on C3 with the deferred placement application, pods/s: no partition 120k, 8 CUs 129k, 32 CUs 141-148k,
+  // 64 CUs 143-147k; the commit kernel alone on 4 CUs of a stream of its own: 138k. Off by default: CU-masked streams
+  // are blocking streams (hipExtStreamCreateWithCUMask has no flags), and a 1-pod-batch test hung in gs_destroy's
+  // hipFree with them; without the partition the deferral is not used either (it only pays with the partition).)
+  const int commit_cus = cus_env ? atoi(cus_env) : 0;
   if (commit_cus > 0 && ncu > 2 * commit_cus) {
     std::vector<uint32_t> m_commit((ncu + 31) / 32, 0u), m_eval((ncu + 31) / 32, 0u);
     for (int k = 0; k < ncu; ++k) (k < commit_cus ? m_commit : m_eval)[k / 32] |= 1u << (k % 32);
     if ((e = hipExtStreamCreateWithCUMask(&c->st, (uint32_t)m_commit.size(), m_commit.data())) != hipSuccess)
       return bail("hipExtStreamCreateWithCUMask", e);
+    c->cu_partition = true;
     if ((e = hipExtStreamCreateWithCUMask(&c->st2, (uint32_t)m_eval.size(), m_eval.data())) != hipSuccess)
       return bail("hipExtStreamCreateWithCUMask", e);
     if ((e = hipExtStreamCreateWithCUMask(&c->st_ev, (uint32_t)m_eval.size(), m_eval.data())) != hipSuccess)
@@ -1820,6 +1837,8 @@ int gs_destroy(gs_ctx* c) {
     if (ev) (void)hipEventDestroy(ev);
   if (c->st_ev) (void)hipStreamDestroy(c->st_ev);
   if (c->st_rb) (void)hipStreamDestroy(c->st_rb);
+  if (c->slab_mv.i64) (void)hipFree(c->slab_mv.i64);
+  if (c->slab_mv.i32) (void)hipFree(c->slab_mv.i32);
   if (c->st2) (void)hipStreamSynchronize(c->st2);
   if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
   if (c->ev_join) (void)hipEventDestroy(c->ev_join);
@@ -2197,8 +2216,8 @@ int schedule_stream(gs_ctx* c, PodRun run, Next&& next_run, Done&& run_done) {
       }
       if (rc) { if (spec) drain(); return rc; }
       const bool host_work = c->h_committed[1] != 1;   // the device-side continuation flag the speculative pass read
-      const bool defer = spec && !host_work && committed == cur_b && !cur_special && c->dirty_list.empty() &&
-                         !c->prep_stale;
+      const bool defer = c->cu_partition && spec && !host_work && committed == cur_b && !cur_special &&
+                         c->dirty_list.empty() && !c->prep_stale;
       if (defer) {   // its successor runs: applied once the batch after that is enqueued
         pend.n = committed;
         pend.special = cur_special;

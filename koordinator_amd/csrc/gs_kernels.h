@@ -122,7 +122,8 @@ hipError_t launch_node_prep(const MirrorView& m, uint32_t n0, uint32_t n1, int64
 hipError_t launch_eval(const MirrorView& m, const PodVec* pods, int npods, const Profile& pf, uint32_t n0, uint32_t n1,
                        int16_t* S, uint32_t ld, int prod_cols, const uint32_t* numa_idx, uint32_t numa_n,
                        uint8_t* aff, hipStream_t st, hipStream_t st2 = nullptr, hipEvent_t fork = nullptr,
-                       hipEvent_t join = nullptr);
+                       hipEvent_t join = nullptr,
+                       const MirrorView* slab = nullptr);
 // the previous batch's winner rows of this shard re-evaluated for every pod of this batch (its eval pass ran beside
 // the previous batch's commit)
 hipError_t launch_patch(const MirrorView& m, const PodVec* pods, int npods, const Profile& pf, uint32_t n0, uint32_t n1,

@@ -78,10 +78,11 @@ __global__ void __launch_bounds__(256) eval_kernel(MirrorView m, const PodVec* _
 // the topology-manager merge, Allocate by hint. A thread keeps one node row in registers and evaluates PPT
 // consecutive pods of the batch: the row (gathered through the index list, ~30% of the shard's lines) is read
 // once per PPT pods instead of once per pair, while a full batch still puts ~nidx*B/PPT threads in flight.
+// sv.i64 != nullptr: the rows come from the batch's slab (gather_numa_kernel: entry t = node idx[t], dense columns).
 template <int PPT>
-__global__ void __launch_bounds__(256) eval_numa_kernel(MirrorView m, const PodVec* __restrict__ pods, int npods,
-                                                        Profile pf, const uint32_t* __restrict__ idx, uint32_t nidx,
-                                                        uint32_t n0, int16_t* __restrict__ S, uint32_t ld,
+__global__ void __launch_bounds__(256) eval_numa_kernel(MirrorView m, MirrorView sv, const PodVec* __restrict__ pods,
+                                                        int npods, Profile pf, const uint32_t* __restrict__ idx,
+                                                        uint32_t nidx, uint32_t n0, int16_t* __restrict__ S, uint32_t ld,
                                                         int prod_cols, uint8_t* __restrict__ aff) {
   const uint32_t t = blockIdx.x * 256 + threadIdx.x;
   const int k0 = blockIdx.y * PPT;
@@ -89,12 +90,39 @@ __global__ void __launch_bounds__(256) eval_numa_kernel(MirrorView m, const PodV
   const int k1 = min(npods, k0 + PPT);
   const uint32_t node = idx[t];
   Row row;
-  load_row(m, node, prod_cols, true, row);
+  if (sv.i64) {
+    load_row(sv, t, prod_cols, true, row);
+    row.node = node;   // (eval_pair reads the scalar-slot columns of the mirror by node)
+  } else {
+    load_row(m, node, prod_cols, true, row);
+  }
   for (int k = k0; k < k1; ++k) {
     PairOut o = eval_pair<false, false, true>(row, pods[k], pf, m);
     S[(size_t)k * ld + (node - n0)] = (int16_t)total_score(o, pf);
     aff[(size_t)k * ld + (node - n0)] = (uint8_t)(o.code ? 0u : o.aff);   // read by the commit's Reserve
   }
+}
+
+// The NUMA-policy rows of the batch's eval pass gathered into a dense slab (same column numbering, entry t = node
+// idx[t]): eval_numa_kernel then reads each row once per pod group from whole cache lines instead of the ~30% of every
+// line the ascending index list uses in the mirror (the gather reads the sparse lines once per batch).
+__constant__ int kSlabCol64[] = {C_FREE_CPU,  C_FREE_MEM,  C_FREE_EPH,  C_ALLOC_CPU, C_ALLOC_MEM, C_NZFREE_CPU,
+                                 C_NZFREE_MEM, C_LA_CAP_CPU, C_LA_CAP_MEM, C_LA_FREE_CPU, C_LA_FREE_MEM,
+                                 C_LA_PFREE_CPU, C_LA_PFREE_MEM, C_ZCAP_CPU0, C_ZCAP_CPU0 + 1, C_ZCAP_CPU0 + 2,
+                                 C_ZCAP_CPU0 + 3, C_ZCAP_MEM0, C_ZCAP_MEM0 + 1, C_ZCAP_MEM0 + 2, C_ZCAP_MEM0 + 3,
+                                 C_ZRAW_CPU0, C_ZRAW_CPU0 + 1, C_ZRAW_CPU0 + 2, C_ZRAW_CPU0 + 3, C_ZRAW_MEM0,
+                                 C_ZRAW_MEM0 + 1, C_ZRAW_MEM0 + 2, C_ZRAW_MEM0 + 3, C_AMP, C_NAMP};
+__constant__ int kSlabCol32[] = {C_FREE_PODS, C_DFLAGS, C_ZFREE0, C_ZFREE0 + 1, C_ZFREE0 + 2, C_ZFREE0 + 3, C_ZADJ0,
+                                 C_ZADJ0 + 1, C_ZADJ0 + 2, C_ZADJ0 + 3, C_NFLAGS, C_NFLAGS2, C_ALLOC_CPUS, C_TFREE};
+constexpr int SLAB64 = 31, SLAB32 = 14;
+__global__ void __launch_bounds__(256) gather_numa_kernel(MirrorView m, MirrorView sv, const uint32_t* __restrict__ idx,
+                                                          uint32_t nidx) {
+  const uint32_t t = blockIdx.x * 256 + threadIdx.x;
+  if (t >= nidx) return;
+  const uint32_t node = idx[t];
+  const int c = blockIdx.y;
+  if (c < SLAB64) sv.c64(kSlabCol64[c])[t] = m.c64(kSlabCol64[c])[node];
+  else sv.c32(kSlabCol32[c - SLAB64])[t] = m.c32(kSlabCol32[c - SLAB64])[node];
 }
 
 // Patch of a batch's score rows evaluated concurrently with the previous batch's commit (which writes the rows
@@ -1360,7 +1388,8 @@ hipError_t launch_node_prep(const MirrorView& m, uint32_t n0, uint32_t n1, int64
 
 hipError_t launch_eval(const MirrorView& m, const PodVec* pods, int npods, const Profile& pf, uint32_t n0, uint32_t n1,
                        int16_t* S, uint32_t ld, int prod_cols, const uint32_t* numa_idx, uint32_t numa_n,
-                       uint8_t* aff, hipStream_t st, hipStream_t st2, hipEvent_t fork, hipEvent_t join) {
+                       uint8_t* aff, hipStream_t st, hipStream_t st2, hipEvent_t fork, hipEvent_t join,
+                       const MirrorView* slab) {
   uint32_t len = n1 - n0;
   uint32_t gx = (len + 255) / 256;
   uint32_t gy = (npods + PODS_PER_BLOCK - 1) / PODS_PER_BLOCK;
@@ -1379,18 +1408,25 @@ hipError_t launch_eval(const MirrorView& m, const PodVec* pods, int npods, const
     static const int ppt_env = getenv("GS_NUMA_PPT") ? atoi(getenv("GS_NUMA_PPT")) : NUMA_PPT;
     const int ppt = npods >= 32 ? ppt_env : 1;
     const dim3 g((numa_n + 255) / 256, (npods + ppt - 1) / ppt);
+    // the slab pays once a row is read by several pod groups (full batches)
+    MirrorView sv{nullptr, nullptr, 0};
+    if (slab && slab->i64 && numa_n && npods >= 32) {
+      sv = *slab;
+      hipLaunchKernelGGL(gather_numa_kernel, dim3((numa_n + 255) / 256, SLAB64 + SLAB32), dim3(256), 0, st, m, sv,
+                         numa_idx, numa_n);
+    }
     if (numa_n == 0) {
     } else if (ppt == 2) {
-      hipLaunchKernelGGL(eval_numa_kernel<2>, g, dim3(256), 0, st, m, pods, npods, pf, numa_idx, numa_n, n0, S, ld,
+      hipLaunchKernelGGL(eval_numa_kernel<2>, g, dim3(256), 0, st, m, sv, pods, npods, pf, numa_idx, numa_n, n0, S, ld,
                          prod_cols, aff);
     } else if (ppt == 4) {
-      hipLaunchKernelGGL(eval_numa_kernel<4>, g, dim3(256), 0, st, m, pods, npods, pf, numa_idx, numa_n, n0, S, ld,
+      hipLaunchKernelGGL(eval_numa_kernel<4>, g, dim3(256), 0, st, m, sv, pods, npods, pf, numa_idx, numa_n, n0, S, ld,
                          prod_cols, aff);
     } else if (ppt == 8) {
-      hipLaunchKernelGGL(eval_numa_kernel<8>, g, dim3(256), 0, st, m, pods, npods, pf, numa_idx, numa_n, n0, S, ld,
+      hipLaunchKernelGGL(eval_numa_kernel<8>, g, dim3(256), 0, st, m, sv, pods, npods, pf, numa_idx, numa_n, n0, S, ld,
                          prod_cols, aff);
     } else {
-      hipLaunchKernelGGL(eval_numa_kernel<1>, dim3((numa_n + 255) / 256, npods), dim3(256), 0, st, m, pods, npods,
+      hipLaunchKernelGGL(eval_numa_kernel<1>, dim3((numa_n + 255) / 256, npods), dim3(256), 0, st, m, sv, pods, npods,
                          pf, numa_idx, numa_n, n0, S, ld, prod_cols, aff);
     }
     if ((e = hipGetLastError()) != hipSuccess) return e;
