@@ -410,8 +410,14 @@ def header_symbols(header_path: str | None = None) -> list[str]:
     return sorted(set(re.findall(r"^\s*(?:[A-Za-z_][\w\s\*]*?)\b(gs_\w+)\s*\(", text, re.M)))
 
 
+_LOADED: dict = {}
+
+
 def load(path: str = LIB_PATH) -> C.CDLL:
-    """Load libgpuscore and declare signatures. Raises if the HIP extension is missing."""
+    """Load libgpuscore and declare signatures (once per path). Raises if the HIP extension is missing."""
+    lib = _LOADED.get(path)
+    if lib is not None:
+        return lib
     if not os.path.exists(path):
         raise RuntimeError(f"libgpuscore not built: {path} missing (run __graft_entry__.build())")
     lib = C.CDLL(path)
@@ -419,6 +425,7 @@ def load(path: str = LIB_PATH) -> C.CDLL:
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
+    _LOADED[path] = lib
     return lib
 
 

@@ -2,7 +2,8 @@
 shard, the per-shard candidate levels are all-gathered by torch.distributed (gloo) through the library's
 host-callback transport (gs_comm_init_callback), and each rank runs the replicated commit on the merged levels.
 Placements must equal the CPU oracle's single-process sequential loop. (RCCL is the production transport of the
-same exchange; the driver's multi-GPU bench runs it.) Needs an MI355X: -m gpu."""
+same exchange, used by `bench.py --gpus N`; no RCCL run has executed in this pipeline yet, since the driver has not
+had an 8-GPU node.) Needs an MI355X: -m gpu."""
 import multiprocessing as mp
 import os
 import socket
