@@ -1260,20 +1260,35 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
   }
 }
 
+// With an exclusive commit CU the workgroup declares the CU's whole LDS, and the kernels that run beside it (the
+// next batch's eval pass) declare a few bytes (eval_lds_bytes), so none of their waves is placed on the commit's CU.
+template <bool STAMPS>
+static size_t spec_launch_bytes(int npods) {
+  if (!commit_cu_exclusive()) return spec_smem_bytes(npods);
+  static const size_t dyn = [] {
+    hipFuncAttributes fa{};
+    size_t st = 0;
+    if (hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(commit_spec_kernel<STAMPS>)) == hipSuccess)
+      st = fa.sharedSizeBytes;   // the variant's static LDS
+    return std::max(spec_smem_bytes(MAX_BATCH), (size_t)LDS_PER_CU - st);
+  }();
+  return dyn;
+}
+
 hipError_t launch_commit_spec(const CommitArgs& a, hipStream_t st) {
   if (a.stamps)
-    hipLaunchKernelGGL(commit_spec_kernel<true>, dim3(1), dim3(SP_THREADS), spec_smem_bytes(a.npods), st, a);
+    hipLaunchKernelGGL(commit_spec_kernel<true>, dim3(1), dim3(SP_THREADS), spec_launch_bytes<true>(a.npods), st, a);
   else
-    hipLaunchKernelGGL(commit_spec_kernel<false>, dim3(1), dim3(SP_THREADS), spec_smem_bytes(a.npods), st, a);
+    hipLaunchKernelGGL(commit_spec_kernel<false>, dim3(1), dim3(SP_THREADS), spec_launch_bytes<false>(a.npods), st, a);
   return hipGetLastError();
 }
 
 hipError_t set_commit_spec_attributes() {
   hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(commit_spec_kernel<false>),
-                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)spec_smem_bytes(MAX_BATCH));
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)spec_launch_bytes<false>(MAX_BATCH));
   if (e != hipSuccess) return e;
   return hipFuncSetAttribute(reinterpret_cast<const void*>(commit_spec_kernel<true>),
-                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)spec_smem_bytes(MAX_BATCH));
+                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)spec_launch_bytes<true>(MAX_BATCH));
 }
 
 #undef SPM

@@ -144,6 +144,12 @@ bool commit_spec_selected(uint32_t window_k);   // the speculative commit kernel
 hipError_t launch_commit(const CommitArgs& a, hipStream_t st);        // window_k > 0: lockstep kernel
 hipError_t launch_commit_pipe(const CommitArgs& a, hipStream_t st);   // pipelined roles (gs_commit.hip)
 hipError_t set_commit_pipe_attributes();
+// GS_COMMIT_EXCL=1: the commit's workgroup holds a CU of its own: it declares the whole LDS of the CU and the eval
+// pass that overlaps it declares eval_lds_bytes(), so the dispatcher never places eval waves beside it. Measured
+// neutral on C3 (commit 0.705 vs 0.708 ms per batch): off by default.
+constexpr uint32_t LDS_PER_CU = 160u * 1024u;
+bool commit_cu_exclusive();
+size_t eval_lds_bytes();
 hipError_t launch_commit_spec(const CommitArgs& a, hipStream_t st);   // speculative pipeline (gs_commit_spec.hip)
 hipError_t set_commit_spec_attributes();
 hipError_t launch_row_stats(const int16_t* S, uint32_t len, RowStat* out, hipStream_t st);

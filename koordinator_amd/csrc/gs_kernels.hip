@@ -1386,6 +1386,13 @@ hipError_t launch_node_prep(const MirrorView& m, uint32_t n0, uint32_t n1, int64
   return hipGetLastError();
 }
 
+bool commit_cu_exclusive() {
+  static const bool on = getenv("GS_COMMIT_EXCL") && atoi(getenv("GS_COMMIT_EXCL")) != 0;
+  return on;
+}
+
+size_t eval_lds_bytes() { return commit_cu_exclusive() ? 256 : 0; }
+
 hipError_t launch_eval(const MirrorView& m, const PodVec* pods, int npods, const Profile& pf, uint32_t n0, uint32_t n1,
                        int16_t* S, uint32_t ld, int prod_cols, const uint32_t* numa_idx, uint32_t numa_n,
                        uint8_t* aff, hipStream_t st, hipStream_t st2, hipEvent_t fork, hipEvent_t join,
@@ -1394,6 +1401,7 @@ hipError_t launch_eval(const MirrorView& m, const PodVec* pods, int npods, const
   uint32_t gx = (len + 255) / 256;
   uint32_t gy = (npods + PODS_PER_BLOCK - 1) / PODS_PER_BLOCK;
   if (gx == 0 || gy == 0) return hipSuccess;
+  const size_t xl = eval_lds_bytes();
   if (pf.enabled & 0x30u) {
     // eval_kernel (nodes without a NUMA policy) and eval_numa_kernel write disjoint score entries: with a side
     // stream they run concurrently, eval_kernel's blocks filling the CUs eval_numa_kernel's low-occupancy waves
@@ -1412,25 +1420,25 @@ hipError_t launch_eval(const MirrorView& m, const PodVec* pods, int npods, const
     MirrorView sv{nullptr, nullptr, 0};
     if (slab && slab->i64 && numa_n && npods >= 32) {
       sv = *slab;
-      hipLaunchKernelGGL(gather_numa_kernel, dim3((numa_n + 255) / 256, SLAB64 + SLAB32), dim3(256), 0, st, m, sv,
+      hipLaunchKernelGGL(gather_numa_kernel, dim3((numa_n + 255) / 256, SLAB64 + SLAB32), dim3(256), xl, st, m, sv,
                          numa_idx, numa_n);
     }
     if (numa_n == 0) {
     } else if (ppt == 2) {
-      hipLaunchKernelGGL(eval_numa_kernel<2>, g, dim3(256), 0, st, m, sv, pods, npods, pf, numa_idx, numa_n, n0, S, ld,
+      hipLaunchKernelGGL(eval_numa_kernel<2>, g, dim3(256), xl, st, m, sv, pods, npods, pf, numa_idx, numa_n, n0, S, ld,
                          prod_cols, aff);
     } else if (ppt == 4) {
-      hipLaunchKernelGGL(eval_numa_kernel<4>, g, dim3(256), 0, st, m, sv, pods, npods, pf, numa_idx, numa_n, n0, S, ld,
+      hipLaunchKernelGGL(eval_numa_kernel<4>, g, dim3(256), xl, st, m, sv, pods, npods, pf, numa_idx, numa_n, n0, S, ld,
                          prod_cols, aff);
     } else if (ppt == 8) {
-      hipLaunchKernelGGL(eval_numa_kernel<8>, g, dim3(256), 0, st, m, sv, pods, npods, pf, numa_idx, numa_n, n0, S, ld,
+      hipLaunchKernelGGL(eval_numa_kernel<8>, g, dim3(256), xl, st, m, sv, pods, npods, pf, numa_idx, numa_n, n0, S, ld,
                          prod_cols, aff);
     } else {
-      hipLaunchKernelGGL(eval_numa_kernel<1>, dim3((numa_n + 255) / 256, npods), dim3(256), 0, st, m, sv, pods, npods,
+      hipLaunchKernelGGL(eval_numa_kernel<1>, dim3((numa_n + 255) / 256, npods), dim3(256), xl, st, m, sv, pods, npods,
                          pf, numa_idx, numa_n, n0, S, ld, prod_cols, aff);
     }
     if ((e = hipGetLastError()) != hipSuccess) return e;
-    hipLaunchKernelGGL(eval_kernel<true>, dim3(gx, gy), dim3(256), 0, side ? st2 : st, m, pods, npods, pf, n0, n1, S,
+    hipLaunchKernelGGL(eval_kernel<true>, dim3(gx, gy), dim3(256), xl, side ? st2 : st, m, pods, npods, pf, n0, n1, S,
                        ld, prod_cols);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     if (side) {
@@ -1438,7 +1446,7 @@ hipError_t launch_eval(const MirrorView& m, const PodVec* pods, int npods, const
       if ((e = hipStreamWaitEvent(st, join, 0)) != hipSuccess) return e;
     }
   } else {
-    hipLaunchKernelGGL(eval_kernel<false>, dim3(gx, gy), dim3(256), 0, st, m, pods, npods, pf, n0, n1, S, ld, prod_cols);
+    hipLaunchKernelGGL(eval_kernel<false>, dim3(gx, gy), dim3(256), xl, st, m, pods, npods, pf, n0, n1, S, ld, prod_cols);
   }
   return hipGetLastError();
 }

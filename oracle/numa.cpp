@@ -1102,6 +1102,33 @@ int filter(const NumaArgs& a, const PreState& st, const NodeNUMA& n, const NodeV
   return 0;
 }
 
+// resourceManager.GetTopologyHints (resource_manager.go:122-137) for the pod PreFilter described, on one node, with the
+// options the provider passes (topology_hint.go:41-67). Test hook for resource_manager_test.go
+// TestResourceManagerGetTopologyHint: entries (resource slot, mask, preferred) in hint order; an empty list for a
+// resource is one entry with preferred = 2. Returns 1 for a nil map (an error), 0 otherwise, or the bind status.
+int topology_hints_test(const NumaArgs& a, const PreState& st, const NodeNUMA& n, int32_t* res, uint64_t* masks,
+                        uint8_t* preferred, uint32_t cap, uint32_t* count) {
+  *count = 0;
+  if (st.status) return st.status;
+  bool rb = false;
+  if (int rc = request_cpu_bind(st, n.opts.node_cpu_bind, &rb)) return rc;
+  ResourceOptions ro = resource_options(st, n, rb, Hint{});
+  ro.scorer = true;
+  HintsMap hm = topology_hints(a, n, ro);
+  if (hm.nil) return 1;
+  uint32_t k = 0;
+  auto put = [&](int r, uint64_t m, uint8_t p) {
+    if (k < cap) { res[k] = r; masks[k] = m; preferred[k] = p; }
+    ++k;
+  };
+  for (auto& kv : hm.hints) {
+    if (kv.second.empty()) put(kv.first, 0, 2);
+    for (const Hint& h : kv.second) put(kv.first, h.mask, h.preferred ? 1 : 0);
+  }
+  *count = k;
+  return 0;
+}
+
 int64_t score(const NumaArgs& a, const PreState& st, const NodeNUMA& n, const NodeView& v, const Hint& affinity) {
   if (st.status || st.skip) return 0;
   const TopologyOptions& o = n.opts;

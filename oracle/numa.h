@@ -132,6 +132,8 @@ int filter(const NumaArgs& a, const PreState& st, const NodeNUMA& n, const NodeV
            bool* has_affinity, bool reverse_resource_order = false);
 // Score (scoring.go:55-97) with the Filter-time affinity
 int64_t score(const NumaArgs& a, const PreState& st, const NodeNUMA& n, const NodeView& v, const Hint& affinity);
+int topology_hints_test(const NumaArgs& a, const PreState& st, const NodeNUMA& n, int32_t* res, uint64_t* masks,
+                        uint8_t* preferred, uint32_t cap, uint32_t* count);
 // Reserve (plugin.go:375-422): Allocate + resourceManager.Update. Returns 0 or a negative error.
 int reserve(const NumaArgs& a, const PreState& st, NodeNUMA& n, const gs_pod& pod, const Hint& affinity,
             PodAllocation* out);

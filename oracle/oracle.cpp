@@ -886,6 +886,13 @@ int or_numa_allocation_get(or_cluster* c, uint32_t node, uint64_t uid, gs_pod_al
   return 1;
 }
 
+int or_numa_topology_hints(or_cluster* c, const gs_pod* pod, uint32_t node, int32_t* res, uint64_t* masks,
+                           uint8_t* preferred, uint32_t cap, uint32_t* count) {
+  if (!c || !pod || !count || node >= c->numa.size()) return GS_EINVAL;
+  const orn::PreState st = orn::prefilter(c->numa_args, *pod);
+  return orn::topology_hints_test(c->numa_args, st, c->numa[node], res, masks, preferred, cap, count);
+}
+
 int or_set_hint_order(or_cluster* c, int reverse) {
   if (!c) return GS_EINVAL;
   c->reverse_hint_order = reverse != 0;

@@ -63,6 +63,9 @@ int or_numa_allocations_release(or_cluster* c, const uint32_t* node_idx, const u
 int or_numa_allocation_get(or_cluster* c, uint32_t node, uint64_t uid, gs_pod_allocation* out);
 /* 1: iterate hint resources in reverse name order (exposes Go map-order dependence, policy.go:108) */
 int or_set_hint_order(or_cluster* c, int reverse);
+/* resourceManager.GetTopologyHints of a pod on one node (test hook, numa.cpp topology_hints_test). */
+int or_numa_topology_hints(or_cluster* c, const gs_pod* pod, uint32_t node, int32_t* res, uint64_t* masks,
+                           uint8_t* preferred, uint32_t cap, uint32_t* count);
 /* takeCPUs on a buildCPUTopologyForTest topology (cpu_accumulator_test.go:30-57), for the golden vectors.
  * available: cpuset words; alloc_ref[cpu] >= 0 puts the cpu in allocatedCPUs with that RefCount and alloc_excl[cpu]. */
 int or_take_cpus_test(int sockets, int nodes_per_socket, int cores_per_node, int cpus_per_core, int max_ref,

@@ -54,6 +54,7 @@ def _load() -> C.CDLL:
         "or_numa_allocations_release": (C.c_int, [P, P, P, C.c_uint32]),
         "or_numa_allocation_get": (C.c_int, [P, C.c_uint32, C.c_uint64, P]),
         "or_set_hint_order": (C.c_int, [P, C.c_int]),
+        "or_numa_topology_hints": (C.c_int, [P, P, C.c_uint32, P, P, P, C.c_uint32, P]),
         "or_take_cpus_test": (C.c_int, [C.c_int] * 5 + [P, P, P] + [C.c_int] * 4 + [P]),
         "or_policy_merge": (C.c_int, [C.c_int, C.c_uint64, C.c_int, P, P, P, P, P, P, P]),
         "or_iterate_bitmasks": (C.c_int, [P, C.c_int, P, C.c_int]),
@@ -216,6 +217,27 @@ class Oracle:
         if rc < 0:
             _chk(rc, "allocation_get")
         return out[0] if rc == 1 else None
+
+    def topology_hints(self, pod, node: int = 0):
+        """resourceManager.GetTopologyHints on `node`: None (nil map) or {resource slot: [(mask, preferred), ...]}."""
+        pod = np.ascontiguousarray(np.atleast_1d(pod), dtype=abi.POD_DTYPE)
+        cap = 64
+        res, masks = np.zeros(cap, np.int32), np.zeros(cap, np.uint64)
+        pref, cnt = np.zeros(cap, np.uint8), np.zeros(1, np.uint32)
+        rc = lib().or_numa_topology_hints(self._h, abi.ptr(pod), node, abi.ptr(res), abi.ptr(masks), abi.ptr(pref), cap,
+                                          abi.ptr(cnt))
+        if rc < 0:
+            _chk(rc, "topology_hints")
+        if rc == 1:
+            return None
+        if rc > 0:
+            raise RuntimeError(f"topology_hints: PreFilter / bind status {rc}")
+        out = {}
+        for k in range(int(cnt[0])):
+            lst = out.setdefault(int(res[k]), [])
+            if pref[k] != 2:
+                lst.append((int(masks[k]), bool(pref[k])))
+        return out
 
     def set_hint_order(self, reverse: bool):
         _chk(lib().or_set_hint_order(self._h, int(reverse)), "set_hint_order")

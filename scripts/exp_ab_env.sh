@@ -9,6 +9,7 @@ for k in 1 2 3; do
     rc=$?; [ $rc -eq 0 ] || { echo "rc=$rc"; tail -5 gpurun_out/ab.err; exit $rc; }
     python -c "
 import json; d=json.loads(open('gpurun_out/ab.json').read().strip().splitlines()[-1])
-print('${v:-default}', round(d['pods_per_s']), 'pods/s', round(d['ms_per_step'],3), 'ms/step')"
+b=d['breakdown_ms']
+print('${v:-default}', round(d['pods_per_s']), 'pods/s', round(d['ms_per_step'],3), 'ms/step', 'commit/batch', round(b['commit']/b['batches'],3), 'eval/batch', round(b['eval']/b['batches'],3), 'cand/batch', round(b['cand']/b['batches'],3))"
   done
 done

@@ -372,6 +372,97 @@ for name, lines, node, allocated, pod, want in reserve_cases:
                          "args": default_args, "nodes": [node], "allocations": allocs, "pod": pod, "filter": True,
                          "want_cpuset": want})
 
+# ---- resourceManager.Allocate: resource_manager_test.go TestResourceManagerAllocate ----------------------------
+R = "resource_manager_test.go"
+
+
+def rm_node(policy, ratio=-1.0):
+    """TestResourceManagerAllocate node (resource_manager_test.go:536-580): allocatable cpu 104 / memory 256Gi,
+    CPUTopology (2,1,26,2), NUMANodeResources {cpu 52, memory 128Gi} per NUMA node, the resource manager's default
+    NUMA allocate strategy LeastAllocated (written as the node label here), optional amplification ratio. The Go
+    test hands Allocate its hint directly; here the node's topology policy makes the topology manager produce it
+    (the case's want_affinity asserts it did): SingleNUMANode for the single-node hints, BestEffort for {0,1}."""
+    d = {"cpu_milli": 104000, "memory": 256 * GI, "numa_policy": policy, "topology": [2, 1, 26, 2],
+         "zones": [[0, 52000, 128 * GI], [1, 52000, 128 * GI]], "numa_allocate_strategy": "LeastAllocated"}
+    if ratio > 0:
+        d["node_cpu_ratio"] = ratio
+    return d
+
+
+def rm_cpus(text):
+    """cpuset.MustParse of the test; CPU 104 lies outside the 104-CPU topology (ids 0..103) and is inert in the
+    reference (available = all CPUs minus allocated), so it is dropped"""
+    return [c for c in parse(text) if c < 104]
+
+
+def rm_alloc(cpus, zone_cpu):
+    return [{"node": 0, "uid": 0x123456, "cpus": rm_cpus(cpus) if cpus else [],
+             "numa": [[z, c * 1000, None] for z, c in enumerate(zone_cpu)]}]
+
+
+REQ_FULL = {"qos": "LSR", "prod": True, "required": "FullPCPUs", "preferred": "FullPCPUs"}
+REQ_SPREAD = {"qos": "LSR", "prod": True, "required": "SpreadByPCPUs", "preferred": "SpreadByPCPUs"}
+# (name, lines, node, allocated, pod, want cpuset (None: Allocate fails), want NUMA cpu per zone, want hint)
+rm_cases = [
+    # the test's pod also requests 10Gi gpu-memory, a resource no NUMA node holds (not in the intersection): it only
+    # checks that such a resource is left out; the engine's pods carry no gpu-memory, so it is omitted
+    ("allocate with non-existing resources in NUMA", "45-72", rm_node("SingleNUMANode"), [], {"cpu": 4000},
+     [], {0: 4000}, [0]),
+    ("allocate with insufficient resources", "73-91", rm_node("SingleNUMANode"), [], {"cpu": 54000}, None, None, None),
+    ("allocate with required CPUBindPolicyFullPCPUs", "92-122", rm_node("SingleNUMANode"), [],
+     {"cpu": 4000, **REQ_FULL}, parse("0-3"), {0: 4000}, [0]),
+    ("allocate with required CPUBindPolicyFullPCPUs and allocated", "123-173", rm_node("SingleNUMANode"),
+     rm_alloc("4-104", [48, 52]), {"cpu": 4000, **REQ_FULL}, parse("0-3"), {0: 4000}, [0]),
+    ("failed to allocate with required CPUBindPolicyFullPCPUs and allocated", "174-214", rm_node("SingleNUMANode"),
+     rm_alloc("1,3,5,7-104", [48, 52]), {"cpu": 4000, **REQ_FULL}, None, None, None),
+    ("allocate with required CPUBindPolicySpreadByPCPUs", "215-245", rm_node("SingleNUMANode"), [],
+     {"cpu": 4000, **REQ_SPREAD}, parse("0,2,4,6"), {0: 4000}, [0]),
+    ("allocate with required CPUBindPolicySpreadByPCPUs and allocated", "246-296", rm_node("SingleNUMANode"),
+     rm_alloc("1,3,5,7-104", [48, 52]), {"cpu": 4000, **REQ_SPREAD}, parse("0,2,4,6"), {0: 4000}, [0]),
+    ("failed to allocate with required CPUBindPolicySpreadByPCPUs and allocated", "297-337",
+     rm_node("SingleNUMANode"), rm_alloc("4-104", [48, 52]), {"cpu": 4000, **REQ_SPREAD}, None, None, None),
+    # requests = the amplified 6 CPUs, originalRequests = 4: the engine takes the pod's 4 and the node's ratio
+    ("allocate with required CPUBindPolicySpreadByPCPUs and amplified requests", "338-374",
+     rm_node("SingleNUMANode", 1.5), [], {"cpu": 4000, **REQ_SPREAD}, parse("0,2,4,6"), {0: 4000}, [0]),
+    ("allocate with required CPUBindPolicySpreadByPCPUs and allocated and amplified requests", "375-431",
+     rm_node("SingleNUMANode", 1.5), rm_alloc("1,3,5,7-104", [48, 52]), {"cpu": 4000, **REQ_SPREAD},
+     parse("0,2,4,6"), {0: 4000}, [0]),
+    ("failed to allocate with CPU Share and allocated and amplified ratios", "432-477",
+     rm_node("SingleNUMANode", 1.5), rm_alloc("0-49,52-101", [50, 50]), {"cpu": 4000}, None, None, None),
+    ("allocate by numa hint on mixed cpuset/share node", "478-534", rm_node("BestEffort"),
+     rm_alloc("0-43,53-96", [48, 48]), {"cpu": 8000, **REQ_FULL}, parse("44-47,98-101"), {0: 4000, 1: 4000}, [0, 1]),
+]
+for name, lines, node, allocs, pod, want_cpus, want_numa, want_aff in rm_cases:
+    plugin_cases.append({"kind": "allocate", "src": f"{R}:{lines} TestResourceManagerAllocate", "name": name,
+                         "args": default_args, "nodes": [node], "allocations": allocs, "pod": pod, "filter": True,
+                         "want_placed": want_cpus is not None, "want_cpuset": want_cpus or [],
+                         "want_numa_cpu": {str(k): v for k, v in (want_numa or {}).items()},
+                         "want_affinity": want_aff})
+
+# ---- resourceManager.GetTopologyHints: resource_manager_test.go TestResourceManagerGetTopologyHint ----------------
+# want: resource -> [(NUMA node ids, preferred), ...] in the returned order; [] is an empty (non-nil) list. The last
+# case of the table ("failed to generate hints with insufficient memory and hugepages", :906-968) is not transcribed:
+# its memory verdict comes from the 1Gi hugepages sharing memory's hint loop, and the engine models no hugepages.
+hint_cases = [
+    ("allocate with required CPUBindPolicyFullPCPUs", "601-639", [], REQ_FULL, [([0], True), ([1], True), ([0, 1], False)]),
+    ("allocate with required CPUBindPolicyFullPCPUs and allocated", "640-691", rm_alloc("4-104", [48, 52]), REQ_FULL,
+     [([0], True), ([0, 1], False)]),
+    ("failed to allocate with required CPUBindPolicyFullPCPUs and allocated", "692-728",
+     rm_alloc("1,3,5,7-104", [48, 52]), REQ_FULL, []),
+    ("allocate with required CPUBindPolicySpreadByPCPUs", "729-767", [], REQ_SPREAD, [([0], True), ([1], True), ([0, 1], False)]),
+    ("allocate with required CPUBindPolicySpreadByPCPUs and allocated", "768-819", rm_alloc("1,3,5,7-104", [48, 52]),
+     REQ_SPREAD, [([0], True), ([0, 1], False)]),
+    ("failed to allocate with required CPUBindPolicySpreadByPCPUs and allocated", "820-856",
+     rm_alloc("4-104", [48, 52]), REQ_SPREAD, []),
+    ("failed to allocate with CPU Share and allocated and amplified ratios", "857-905",
+     rm_alloc("0-49,52-101", [50, 50]), {}, [([0, 1], False)]),
+]
+for name, lines, allocs, pol, want in hint_cases:
+    node = rm_node("SingleNUMANode", 1.5 if "amplified" in name else -1.0)
+    plugin_cases.append({"kind": "hints", "src": f"{R}:{lines} TestResourceManagerGetTopologyHint", "name": name,
+                         "args": default_args, "nodes": [node], "allocations": allocs, "pod": {"cpu": 4000, **pol},
+                         "filter": True, "want_hints": {"cpu": [[ids, pref] for ids, pref in want]}})
+
 with open(os.path.join(HERE, "numa_plugin.json"), "w") as f:
     json.dump({"cases": plugin_cases}, f, indent=1)
 print(f"wrote {len(plugin_cases)} NodeNUMAResource plugin cases (Filter, affinity, Reserve)")

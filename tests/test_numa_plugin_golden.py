@@ -1,6 +1,9 @@
 """NodeNUMAResource plugin-level vectors of the reference (tests/golden/numa_plugin.json, transcribed from
 plugin_test.go by make_golden_numa.py): Filter verdicts (TestPlugin_Filter, TestFilterWithAmplifiedCPUs), the
-Filter-time NUMA affinity (TestFilterWithNUMANodeScoring) and the cpuset Reserve allocates (TestPlugin_Reserve).
+Filter-time NUMA affinity (TestFilterWithNUMANodeScoring) and the cpuset Reserve allocates (TestPlugin_Reserve); and
+resourceManager.Allocate (resource_manager_test.go TestResourceManagerAllocate): the NUMA split and the cpuset of the
+hint the test hands Allocate, or Allocate's failure (the pod then finds no node); resourceManager.GetTopologyHints
+(TestResourceManagerGetTopologyHint) on the oracle.
 
 The oracle is checked on the CPU; the same cases run through the HIP path (gs_evaluate codes, and gs_schedule on a
 one-node cluster for the affinity bits and the cpuset the commit kernel selects) under -m gpu."""
@@ -52,6 +55,49 @@ def check_reserve(case, cls):
     a = e.allocation(0, int(pod["uid"]))
     got = [] if a is None else numa.cpus_of(a["cpuset"])
     assert got == case["want_cpuset"], f"{case['src']}: cpuset {got}, want {case['want_cpuset']}"
+
+
+def check_allocate(case, cls):
+    e, pod = nu.build(case, cls)
+    if hasattr(e, "verify_cpusets"):
+        e.verify_cpusets(True)
+    out = e.schedule(np.array([pod], abi.POD_DTYPE), np.zeros(1, np.uint64))
+    placed = int(out["node"][0]) == 0
+    assert placed == case["want_placed"], f"{case['src']}: placed {placed}, want {case['want_placed']}"
+    if not placed:
+        return
+    flags = int(out["flags"][0])
+    aff = [z for z in range(4) if (flags >> (abi.GS_PLACED_AFFINITY_SHIFT + z)) & 1]
+    assert aff == case["want_affinity"], f"{case['src']}: hint {aff}, want {case['want_affinity']}"
+    a = e.allocation(0, int(pod["uid"]))
+    assert a is not None, f"{case['src']}: no allocation recorded"
+    assert numa.cpus_of(a["cpuset"]) == case["want_cpuset"], \
+        f"{case['src']}: cpuset {numa.cpus_of(a['cpuset'])}, want {case['want_cpuset']}"
+    got = {str(int(z["node_id"])): int(z["cpu_milli"]) for z in a["numa"][:int(a["num_numa"])] if z["cpu_milli"]}
+    assert got == case["want_numa_cpu"], f"{case['src']}: NUMA cpu {got}, want {case['want_numa_cpu']}"
+
+
+@pytest.mark.parametrize("case", cases("hints"), ids=ids)
+def test_topology_hints_golden_oracle(case):
+    """resourceManager.GetTopologyHints (oracle only: the device builds the same hints per zone subset inside
+    eval_numa_kernel, where they are pinned through the Filter / affinity / Allocate vectors and full-size parity)."""
+    e, pod = nu.build(case, orc.Oracle)
+    got = e.topology_hints(pod)
+    assert got is not None, f"{case['src']}: nil hints"
+    names = {abi.GS_RES_CPU: "cpu", abi.GS_RES_MEMORY: "memory"}
+    got = {names[r]: [[[z for z in range(4) if m >> z & 1], p] for m, p in lst] for r, lst in got.items()}
+    assert got == case["want_hints"], f"{case['src']}: hints {got}, want {case['want_hints']}"
+
+
+@pytest.mark.parametrize("case", cases("allocate"), ids=ids)
+def test_allocate_golden_oracle(case):
+    check_allocate(case, orc.Oracle)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", cases("allocate"), ids=ids)
+def test_allocate_golden_gpu(case):
+    check_allocate(case, engine_cls())
 
 
 @pytest.mark.parametrize("case", cases("filter"), ids=ids)
