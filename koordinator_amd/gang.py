@@ -146,10 +146,19 @@ class GangManager:
         return lib().gs_gang_child_cycle(self._h, gang_id, uid)
 
 
+class WaitingPods:
+    """Pods left waiting at Permit by earlier passes (the framework's waiting pods): uid -> (gang, node, pod record).
+    Pass the same object to consecutive schedule_with_gangs calls so that a gang spanning several calls is allowed,
+    rejected or forgotten exactly as in one long queue."""
+
+    def __init__(self):
+        self.pods: dict[int, tuple[int, int, np.void]] = {}
+
+
 class _Pass:
     """The per-pod transitions of one scheduling pass (shared by the speculative walk and the replay)."""
 
-    def __init__(self, engine, mgr, pods, gang_ids, nominated, now_ns):
+    def __init__(self, engine, mgr, pods, gang_ids, nominated, now_ns, waiting=None):
         self.engine, self.mgr, self.pods, self.gang, self.nom, self.now = engine, mgr, pods, gang_ids, nominated, now_ns
         n = len(pods)
         self.uid_index = {int(u): k for k, u in enumerate(pods["uid"])}
@@ -157,17 +166,38 @@ class _Pass:
         self.state = np.full(n, ST_UNSCHEDULABLE, np.int8)
         self.prefilter = np.zeros(n, np.int8)
         self.permit = np.full(n, -1, np.int8)
+        self.waiting = waiting if waiting is not None else WaitingPods()   # pods waiting from earlier passes
+        self.carried = {}                                                    # their uid -> new state
+
+    def gang_of(self, uid: int) -> int:
+        k = self.uid_index.get(uid)
+        return int(self.gang[k]) if k is not None else self.waiting.pods[uid][0]
+
+    def bind(self, uid: int):
+        """PostBind of a pod Permit allowed (this pass's, or one waiting from an earlier pass)."""
+        k = self.uid_index.get(uid)
+        if k is not None:
+            self.state[k] = ST_BOUND
+        else:
+            self.carried[uid] = ST_BOUND
+        self.mgr.post_bind(self.gang_of(uid), uid)
 
     def unreserve_chain(self, rejected, forget: bool):
         """Rejected waiting pods: Unreserve (gang) + ForgetPod on the engine, and the rejections that follow."""
         queue = list(rejected)
         while queue:
             uid = queue.pop(0)
-            k = self.uid_index[uid]
-            if forget:
-                self.engine.forget([self.node[k]], self.pods[k:k + 1])
-            self.state[k] = ST_REJECTED
-            queue.extend(self.mgr.unreserve(int(self.gang[k]), uid))
+            k = self.uid_index.get(uid)
+            if k is not None:
+                if forget:
+                    self.engine.forget([self.node[k]], self.pods[k:k + 1])
+                self.state[k] = ST_REJECTED
+            else:
+                g, node, rec = self.waiting.pods[uid]
+                if forget:
+                    self.engine.forget([node], np.array([rec], abi.POD_DTYPE))
+                self.carried[uid] = ST_REJECTED
+            queue.extend(self.mgr.unreserve(self.gang_of(uid), uid))
 
     def before_node_loop(self, k) -> tuple[bool, list[int]]:
         """PreFilter; on a rejection its PostFilter. (passes, waiting pods the PostFilter rejected)"""
@@ -190,9 +220,7 @@ class _Pass:
             self.state[k] = ST_BOUND
             self.mgr.post_bind(g, uid)
             for a in allowed:
-                ka = self.uid_index[a]
-                self.state[ka] = ST_BOUND
-                self.mgr.post_bind(int(self.gang[ka]), a)
+                self.bind(a)
             return []
         if st == PERMIT_WAIT:
             self.state[k] = ST_WAITING
@@ -203,7 +231,7 @@ class _Pass:
 
 
 def schedule_with_gangs(engine, mgr: GangManager, pods, gang_ids, seq=None, nominated=None, now_ns: int = 0,
-                        run_cap: int = 4096):
+                        run_cap: int = 4096, waiting: WaitingPods | None = None):
     """Schedules `pods` in queue order with Coscheduling's PreFilter / Permit / PostFilter / Unreserve around every pod,
     through batched engine calls (engine: Engine or the oracle's Oracle: schedule(pods, seq), forget(nodes, pods)).
     gang_ids[i]: the pod's gang key (0: no gang). Returns (placements, result) where result holds per pod the gang
@@ -213,7 +241,7 @@ def schedule_with_gangs(engine, mgr: GangManager, pods, gang_ids, seq=None, nomi
     gang_ids = np.asarray(gang_ids, np.uint64)
     seq = np.arange(n, dtype=np.uint64) if seq is None else np.ascontiguousarray(seq, dtype=np.uint64)
     nominated = np.zeros(n, bool) if nominated is None else np.asarray(nominated, bool)
-    P = _Pass(engine, mgr, pods, gang_ids, nominated, now_ns)
+    P = _Pass(engine, mgr, pods, gang_ids, nominated, now_ns, waiting)
     out = np.zeros(n, abi.PLACEMENT_DTYPE)
     out["node"] = -1
     i = 0
@@ -236,7 +264,7 @@ def schedule_with_gangs(engine, mgr: GangManager, pods, gang_ids, seq=None, nomi
             if st == PERMIT_SUCCESS:
                 mgr.post_bind(g, uid)
                 for a in allowed:
-                    mgr.post_bind(int(gang_ids[P.uid_index[a]]), a)
+                    mgr.post_bind(P.gang_of(a), a)
             elif st == PERMIT_NOT_FOUND:
                 break   # its Reserve is undone after the run
         got = engine.schedule(pods[run], seq[run]) if run else np.zeros(0, abi.PLACEMENT_DTYPE)
@@ -258,14 +286,26 @@ def schedule_with_gangs(engine, mgr: GangManager, pods, gang_ids, seq=None, nomi
                 r += 1
             P.unreserve_chain(rej, forget=True)
         i = j
-    return out, {"prefilter": P.prefilter, "permit": P.permit, "state": P.state, "node": P.node}
+    # the waiting set after this pass: earlier pods that were allowed or rejected leave it, this pass's waiting join
+    for uid in P.carried:
+        P.waiting.pods.pop(uid, None)
+    for k in np.flatnonzero(P.state == ST_WAITING):
+        P.waiting.pods[int(pods["uid"][k])] = (int(gang_ids[k]), int(P.node[k]), pods[k].copy())
+    return out, {"prefilter": P.prefilter, "permit": P.permit, "state": P.state, "node": P.node,
+                 "carried": dict(P.carried)}
 
 
-def expire(engine, mgr: GangManager, pods, gang_ids, node, state, now_ns: int):
+def expire(engine, mgr: GangManager, pods, gang_ids, node, state, now_ns: int, waiting: WaitingPods | None = None):
     """The framework's Permit timeout at now_ns after a pass: waiting pods past their deadline are rejected, their
-    Unreserve and ForgetPod run (and the rejections Strict gangs add). Updates state in place."""
+    Unreserve and ForgetPod run (and the rejections Strict gangs add). Updates state in place; returns the new states
+    of pods waiting from earlier passes (`waiting`, which is updated too)."""
     pods = np.ascontiguousarray(pods, dtype=abi.POD_DTYPE)
-    P = _Pass(engine, mgr, pods, np.asarray(gang_ids, np.uint64), np.zeros(len(pods), bool), now_ns)
+    P = _Pass(engine, mgr, pods, np.asarray(gang_ids, np.uint64), np.zeros(len(pods), bool), now_ns, waiting)
     P.node[:], P.state[:] = node, state
     P.unreserve_chain(mgr.expire(now_ns), forget=True)
     state[:] = P.state
+    for uid in P.carried:
+        P.waiting.pods.pop(uid, None)
+    for k in np.flatnonzero(P.state == ST_REJECTED):
+        P.waiting.pods.pop(int(pods["uid"][k]), None)
+    return dict(P.carried)

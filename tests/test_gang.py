@@ -288,7 +288,27 @@ def load_gangs(mgr, pgs, pods, gang_ids, library: bool):
             mgr.pod_add(int(gang_ids[k]), int(pods["uid"][k]))
 
 
-def run_pair(make_engine, c, pgs, gang_ids, enabled=abi.GS_ENABLE_LA_FIT):
+def chunked_gangs(e, lm, pods, gang_ids, seq, now_ns, chunk):
+    """schedule_with_gangs over consecutive chunks of the queue with one WaitingPods carried between the calls; the
+    per-pod results are joined and the later calls' verdicts on earlier waiting pods applied."""
+    waiting = gg.WaitingPods()
+    outs, res = [], {f: [] for f in ("prefilter", "permit", "state", "node")}
+    for lo in range(0, len(pods), chunk):
+        o, r = gg.schedule_with_gangs(e, lm, pods[lo:lo + chunk], gang_ids[lo:lo + chunk], seq[lo:lo + chunk],
+                                      now_ns=now_ns, waiting=waiting)
+        outs.append(o)
+        for f in res:
+            res[f].append(r[f])
+        res.setdefault("carried", []).append(r["carried"])
+    gres = {f: np.concatenate(res[f]) for f in ("prefilter", "permit", "state", "node")}
+    idx = {int(u): k for k, u in enumerate(pods["uid"])}
+    for car in res["carried"]:
+        for uid, st in car.items():
+            gres["state"][idx[uid]] = st
+    return np.concatenate(outs), gres
+
+
+def run_pair(make_engine, c, pgs, gang_ids, enabled=abi.GS_ENABLE_LA_FIT, chunk=None):
     cfg = config.make_config(c.num_nodes, enabled=enabled)
     e = make_engine(cfg)
     synth.load_into(e, c)
@@ -298,7 +318,10 @@ def run_pair(make_engine, c, pgs, gang_ids, enabled=abi.GS_ENABLE_LA_FIT):
     load_gangs(lm, pgs, c.pods, gang_ids, True)
     load_gangs(om, pgs, c.pods, gang_ids, False)
     seq = np.arange(len(c.pods), dtype=np.uint64)
-    got, gres = gg.schedule_with_gangs(e, lm, c.pods, gang_ids, seq, now_ns=c.now_ns)
+    if chunk:
+        got, gres = chunked_gangs(e, lm, c.pods, gang_ids, seq, c.now_ns, chunk)
+    else:
+        got, gres = gg.schedule_with_gangs(e, lm, c.pods, gang_ids, seq, now_ns=c.now_ns)
     want, wres = oc.schedule_sequential(o, om, c.pods, gang_ids, seq, now_ns=c.now_ns)
     return e, o, got, gres, want, wres
 
@@ -310,6 +333,15 @@ def check_pair(got, gres, want, wres):
     ran = want["node"] >= 0
     for f in ("node", "score", "ties", "feasible"):
         assert np.array_equal(got[f][ran], want[f][ran]), f
+
+
+@pytest.mark.parametrize("chunk", [37, 128])
+def test_chunked_gangs_carry_waiting_pods_oracle_engine(chunk):
+    """A gang spanning several schedule_with_gangs calls: the waiting pods of earlier calls are allowed, rejected and
+    forgotten by later calls exactly as in the one long queue (WaitingPods carried between the calls)."""
+    c, pgs, gang_ids = gang_workload(seed=11)
+    e, o, got, gres, want, wres = run_pair(lambda cfg: orc.Oracle(cfg), c, pgs, gang_ids, chunk=chunk)
+    check_pair(got, gres, want, wres)
 
 
 def test_batched_gangs_match_sequential_order_oracle_engine():

@@ -35,3 +35,13 @@ def test_gangs_hip_engine_numa_1k_nodes():
     check_pair(got, gres, want, wres)
     assert (wres["state"] == oc.ST_BOUND).sum() > 200
     assert e.mirror_check() == 0
+
+
+@pytest.mark.parametrize("chunk", [37, 128])
+def test_gangs_hip_engine_chunked_calls(chunk):
+    """Gangs spanning several schedule_with_gangs calls (waiting pods carried between the calls) on the HIP engine
+    = the one long queue on the oracle."""
+    c, pgs, gang_ids = gang_workload(seed=11)
+    e, o, got, gres, want, wres = run_pair(_engine, c, pgs, gang_ids, chunk=chunk)
+    check_pair(got, gres, want, wres)
+    assert e.mirror_check() == 0
