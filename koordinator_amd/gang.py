@@ -4,13 +4,14 @@ reference's per-pod order of PreFilter -> node loop -> Reserve -> Permit (PostFi
 waiting pods) over batched gs_schedule calls.
 
 Batching is speculative, like the quota gate: the gang transitions of a run of pods are computed on the host assuming
-every pod that passes PreFilter finds a node; the engine then schedules the run's pods in one call. The assumption is
-checked pod by pod: the first gang pod that found no node (its PostFilter rejects waiting siblings and invalidates the
-schedule cycle, and it is not an assumed pod for later Permits) ends the run there: the pods placed after it are
-forgotten on the engine (gs_pods_forget: NodeInfo, podAssignCache and NUMA state exactly as before them), the gang
-state is restored from the run's snapshot and replayed with the real outcomes up to that pod, and the next run starts
-after it. A run also ends after a pod whose transitions undo Reserves (a PreFilter rejection or a Permit 'Gang not
-found' whose rejections reach assumed pods), so every engine call sees the state the sequential order would."""
+every pod that passes PreFilter finds a node; the engine then schedules the run's pods in one call. The gang state is
+then restored from the run's snapshot and the run replayed pod by pod with the real outcomes, checking the walk's
+assumptions: the run stands while every pod's real PreFilter verdict is the walk's and no transition forgets an
+assumed pod (a PostFilter or Unreserve rejecting waiting siblings, a Permit 'Gang not found'), since a forget changes
+the node state under the run's later pods. At the first break the rest of the run is withdrawn (gs_pods_forget:
+NodeInfo, podAssignCache and NUMA state exactly as before those pods) and the next run starts after that pod, so every
+engine call sees the state the sequential order would. Pods left waiting at Permit can be carried to the next call
+(WaitingPods)."""
 from __future__ import annotations
 
 import ctypes as C
@@ -103,7 +104,7 @@ class GangManager:
         return self._chk(lib().gs_gang_prefilter(self._h, gang_id, uid, int(nominated)), "gs_gang_prefilter")
 
     def _list_call(self, fn, *args):
-        cap = 1024
+        cap = 64
         while True:
             buf = np.zeros(cap, np.uint64)
             n = C.c_uint32(0)
@@ -185,19 +186,22 @@ class _Pass:
     def unreserve_chain(self, rejected, forget: bool):
         """Rejected waiting pods: Unreserve (gang) + ForgetPod on the engine, and the rejections that follow."""
         queue = list(rejected)
+        nodes, recs = [], []   # one ForgetPod call for the whole chain (nothing is scheduled in between)
         while queue:
             uid = queue.pop(0)
             k = self.uid_index.get(uid)
             if k is not None:
-                if forget:
-                    self.engine.forget([self.node[k]], self.pods[k:k + 1])
+                nodes.append(int(self.node[k]))
+                recs.append(self.pods[k])
                 self.state[k] = ST_REJECTED
             else:
                 g, node, rec = self.waiting.pods[uid]
-                if forget:
-                    self.engine.forget([node], np.array([rec], abi.POD_DTYPE))
+                nodes.append(node)
+                recs.append(rec)
                 self.carried[uid] = ST_REJECTED
             queue.extend(self.mgr.unreserve(self.gang_of(uid), uid))
+        if forget and nodes:
+            self.engine.forget(np.array(nodes, np.uint32), np.array(recs, abi.POD_DTYPE))
 
     def before_node_loop(self, k) -> tuple[bool, list[int]]:
         """PreFilter; on a rejection its PostFilter. (passes, waiting pods the PostFilter rejected)"""
@@ -247,14 +251,13 @@ def schedule_with_gangs(engine, mgr: GangManager, pods, gang_ids, seq=None, nomi
     i = 0
     while i < n:
         snap = mgr.clone()
-        run, j, end_effects = [], i, None
+        run, j = [], i
         # speculative walk: every pod that passes PreFilter finds a node
         while j < n and len(run) < run_cap:
             ok, rej = P.before_node_loop(j)
             if not ok:
                 j += 1
                 if rej:   # Unreserves: the engine state changes after this pod
-                    end_effects = rej
                     break
                 continue
             run.append(j)
@@ -268,23 +271,42 @@ def schedule_with_gangs(engine, mgr: GangManager, pods, gang_ids, seq=None, nomi
             elif st == PERMIT_NOT_FOUND:
                 break   # its Reserve is undone after the run
         got = engine.schedule(pods[run], seq[run]) if run else np.zeros(0, abi.PLACEMENT_DTYPE)
-        # the first gang pod without a node breaks the assumption
-        f = next((k for k in range(len(run)) if got["node"][k] < 0 and gang_ids[run[k]] != 0), None)
-        if f is not None:
-            later = [k for k in range(f + 1, len(run)) if got["node"][k] >= 0]
+
+        def drop_from(r0):
+            """Withdraw the run's speculative placements from position r0 on (ForgetPod)."""
+            later = [q for q in range(r0, len(run)) if got["node"][q] >= 0]
             if later:
-                engine.forget(got["node"][later].astype(np.uint32), pods[[run[k] for k in later]])
-            run, got, j, end_effects = run[:f + 1], got[:f + 1], run[f] + 1, None
-        # replay the pods [i, j) with the real outcomes on the snapshot's gang state
+                engine.forget(got["node"][later].astype(np.uint32), pods[[run[q] for q in later]])
+
+        # replay [i, j) with the real outcomes on the snapshot's gang state, checking the walk's assumptions: the run
+        # stands while every pod's real PreFilter verdict is the walk's and no Unreserve forgets a pod (which changes
+        # the node state under the run's later pods); at the first break the rest of the run is withdrawn and the
+        # queue resumes after that pod
         mgr.assign(snap)
-        r = 0
-        for k in range(i, j):
+        r, k = 0, i
+        while k < j:
             ok, rej = P.before_node_loop(k)
+            in_run = r < len(run) and run[r] == k
+            if ok != in_run:
+                drop_from(r)
+                if ok:   # the walk's PreFilter failed where the real one passes: this pod alone
+                    one = engine.schedule(pods[k:k + 1], seq[k:k + 1])
+                    out[k] = one[0]
+                    rej = P.after_node_loop(k, int(one["node"][0]))
+                P.unreserve_chain(rej, forget=True)
+                j = k + 1
+                break
             if ok:
                 out[k] = got[r]
                 rej = P.after_node_loop(k, int(got["node"][r]))
                 r += 1
-            P.unreserve_chain(rej, forget=True)
+            if rej:
+                P.unreserve_chain(rej, forget=True)
+                if r < len(run):
+                    drop_from(r)
+                    j = k + 1
+                    break
+            k += 1
         i = j
     # the waiting set after this pass: earlier pods that were allowed or rejected leave it, this pass's waiting join
     for uid in P.carried:

@@ -72,6 +72,21 @@ def main():
         if gang_ids[i]:
             mgr.pod_add(int(gang_ids[i]), int(pods["uid"][i]))
     states, carried, waiting = [], {}, gg.WaitingPods()
+    calls = {"schedule": 0, "schedule_s": 0.0, "forget": 0}
+    sched, forget = e.schedule, e.forget
+
+    def timed_schedule(p, q):
+        t = time.perf_counter()
+        r = sched(p, q)
+        calls["schedule"] += 1
+        calls["schedule_s"] += time.perf_counter() - t
+        return r
+
+    def counted_forget(nodes, p):
+        calls["forget"] += 1
+        return forget(nodes, p)
+
+    e.schedule, e.forget = timed_schedule, counted_forget
     t0 = time.perf_counter()
     for lo in range(warm, total, args.chunk):
         hi = min(total, lo + args.chunk)
@@ -93,6 +108,8 @@ def main():
         "bound": int(np.count_nonzero(st == gg.ST_BOUND)), "waiting": int(np.count_nonzero(st == gg.ST_WAITING)),
         "rejected": int(np.count_nonzero(st == gg.ST_REJECTED)),
         "unschedulable": int(np.count_nonzero(st == gg.ST_UNSCHEDULABLE)),
+        "engine_calls": calls["schedule"], "engine_s": calls["schedule_s"], "forget_calls": calls["forget"],
+        "total_s": gang_s,
         "config": "C3 (NUMA profile), 2048-pod calls after one 2048-pod warm-up call, batch 128, gangs Strict with "
                   "minMember = gang size, PodGroups known up front; one GPU"}))
 
