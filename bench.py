@@ -139,7 +139,7 @@ def main() -> None:
     ap.add_argument("--scaling", choices=["strong", "weak"], default="strong")
     ap.add_argument("--pods-per-step", type=int, default=2048)
     ap.add_argument("--batch", type=int, default=128)
-    ap.add_argument("--cpu-sample-pods", type=int, default=400)
+    ap.add_argument("--cpu-sample-pods", type=int, default=1100)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--profile", choices=["c3", "la-fit", "c5"], default="c3",
                     help="c5: 100k nodes, LoadAware + Fit + DeviceShare + Reservation (SURVEY 8(d) C5, see --nodes)")
@@ -279,11 +279,14 @@ def main() -> None:
         return sum(kpmc[k]["hbm_bytes_per_launch"] for k in ks) if ks else None
 
     traffic_step = None
+    # one-time setup kernels of the profiled run (the mirror upload, buffer fills): not per-step traffic
+    setup = ("gs::scatter_rows_kernel", "gs::node_prep_kernel")
     if kpmc:
-        steps_in_pmc = max(1, kpmc.get("gs::commit_pipe_kernel<false>", kpmc.get("gs::commit_kernel<false>", {}))
-                           .get("dispatches", batches / args.steps) / max(1.0, batches / args.steps))
+        # the profiled run's step count: commit_spec_kernel launches once per batch
+        commit = kpmc.get("gs::commit_spec_kernel<false>", {})
+        steps_in_pmc = max(1.0, commit.get("dispatches", 0) / max(1.0, batches / args.steps))
         traffic_step = sum(v["hbm_bytes_per_launch"] * v["dispatches"] for k, v in kpmc.items()
-                           if k.startswith("gs::")) / steps_in_pmc
+                           if k.startswith("gs::") and not k.startswith(setup)) / steps_in_pmc
     kernels = {
         "eval_pass": {"kernels": "eval_kernel + eval_numa_kernel (concurrent streams), one launch each per batch",
                       "avg_launch_us": eval_us, "pairs_per_launch": pairs_per_launch,
@@ -380,8 +383,9 @@ def main() -> None:
                 "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBPS,
                 "traffic": traffic_step,
-                "traffic_unit": "HBM bytes per step, all gs:: kernels (rocprofv3 PMC: 2 x FETCH_SIZE + WRITE_SIZE, "
-                                "gfx950 correction)",
+                "traffic_unit": "HBM bytes per step, the per-batch gs:: kernels (rocprofv3 PMC: 2 x FETCH_SIZE + "
+                                "WRITE_SIZE, gfx950 correction; one-time mirror upload / node_prep excluded; steps = "
+                                "commit_spec_kernel dispatches / batches per step)",
                 "traffic_source": pmc_src,
                 "bytes_per_eval": bpe,
                 "convention": "BASELINE.md §4 / SURVEY §8(d): achieved = evals/s over the driver-timed steps x "

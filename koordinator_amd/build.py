@@ -10,7 +10,7 @@ CSRC = os.path.join(HERE, "csrc")
 OUT = os.path.join(HERE, "libgpuscore.so")
 SOURCES = ["gs_engine.cpp", "gs_numa_host.cpp", "gs_ingest.cpp", "gs_quota.cpp", "gs_gang.cpp", "gs_reasons.cpp",
            "gs_kernels.hip",
-           "gs_commit.hip", "gs_commit_spec.hip", "gs_probe.hip", "gs_ext.hip"]
+           "gs_commit_spec.hip", "gs_probe.hip", "gs_ext.hip"]
 OBJ = os.path.join(HERE, "build")
 # host code off the per-pod path whose -O3 build takes minutes in clang (the inlined cpuset selection of the
 # self-test): -O2 (27 s instead of ~210 s)

@@ -1,6 +1,6 @@
 // gs_commit_spec.hip — the sequential commit of a batch as a speculative pipeline on one CU (gfx950, one shard).
 //
-// Same contract and results as commit_pipe_kernel (gs_commit.hip): the batch's pods in queue order, each one
+// Same contract and results as commit_kernel (gs_kernels.hip): the batch's pods in queue order, each one
 // selectHost over its batch-start score levels and the rows earlier pods of the batch landed on ("dirty" rows,
 // re-scored exactly), then assume + Reserve ([upstream] scheduleOne: selectHost, assume; LoadAware /
 // NodeNUMAResource Reserve).
@@ -14,16 +14,17 @@
 // feasible). Otherwise the pipeline rolls back to q (undo log of the Reserves after it) and decides q again with
 // every score exact. Verified decisions are exactly those of the sequential loop.
 //
-// Roles (8 waves):
+// Roles (8 waves; wave w runs on SIMD w % 4, see sp_reserve_index / sp_rescore_index below):
 //   wave 0       decide (selectHost over levels + ready dirty rows, pending rows excluded), in order; performs the
 //                rollbacks the verifier requests. Highest issue priority: it sets the pipeline's pace.
-//   wave 1       verify the decisions in order (pending rows' exact re-scores below the decided maximum), the final
-//                Feasible counts, and the batch's end; a miss requests a rollback from wave 0.
+//   wave 4       verify the decisions in order (pending rows' exact re-scores below the decided maximum), the final
+//                Feasible counts, and the batch's end; a miss requests a rollback from wave 0. (SIMD 0, beside the
+//                selector: the lightest role.)
 //   waves 2, 3   Reserve of decided pods, wave 2 the even pods and wave 3 the odd ones: fetch a fresh winner row into
 //                its slot (prefetched one pod of its parity ahead), log the slot's state, apply assume + Reserve (NUMA
 //                split, cpuset), queue the row's re-scoring on the wave's own job ring. A pod landing on a row an
 //                earlier pod landed on waits until that version is re-scored (so the other wave's Reserve is in).
-//   waves 4..7   re-scoring jobs from both rings: a reserved row's new score for 64 later pods, one pod per lane
+//   waves 1, 5, 6, 7  re-scoring jobs from both rings: a reserved row's new score for 64 later pods, one pod per lane
 //                (each wave builds the row's hint table itself).
 // All hand-offs are LDS words (release / acquire); every wait is bounded: an expired wait (any wave) ends the kernel
 // with a site code in committed[3], nothing committed and nothing written back (the host fails the call with

@@ -178,7 +178,6 @@ struct gs_ctx {
   uint64_t stats_all_pods = 0;     // pods placed by gs_schedule over the context's life (stamp averages)
   // GS_HOST_TIMING=1: host time per batch of schedule_stream, by phase (printed by gs_destroy)
   bool host_timing = false;
-  bool cu_partition = false;   // GS_COMMIT_CUS > 0: commit chain and eval pass on disjoint CUs
   double ht_wait = 0, ht_apply = 0, ht_stage = 0, ht_launch = 0, ht_max_busy = 0;
   uint64_t ht_batches = 0, ht_busy_hist[8] = {};
   // NodeNUMAResource: per-node TopologyOptions + NodeAllocation mirror, registered CPU topologies
@@ -1628,32 +1627,13 @@ int gs_create(const gs_config* cfg, gs_ctx** out) {
   if ((e = hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi)) != hipSuccess) return bail("hipDeviceGetStreamPriorityRange", e);
   static const bool same_prio = getenv("GS_STREAM_PRIO") && getenv("GS_STREAM_PRIO")[0] == '0';
   if (same_prio) prio_hi = prio_lo;
-  // CU partition: the commit chain (st: patch, cand, the one-workgroup commit kernel) on its own CUs, the next batch's
-  // eval pass (st_ev, st2) on the others, so that no eval wave shares the commit kernel's CU (measured: the commit
-  // runs ~25% slower with eval waves beside it). GS_COMMIT_CUS = CUs of the commit chain (0: no partition).
-  int ncu = 0;
-  (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, cfg->device);
-  const char* cus_env = getenv("GS_COMMIT_CUS");
-  // (measured on C3 with the deferred placement application, pods/s: no partition 120k, 8 CUs 129k, 32 CUs 141-148k,
-  // 64 CUs 143-147k; the commit kernel alone on 4 CUs of a stream of its own: 138k. Off by default: CU-masked streams
-  // are blocking streams (hipExtStreamCreateWithCUMask has no flags), and a 1-pod-batch test hung in gs_destroy's
-  // hipFree with them; without the partition the deferral is not used either (it only pays with the partition).)
-  const int commit_cus = cus_env ? atoi(cus_env) : 0;
-  if (commit_cus > 0 && ncu > 2 * commit_cus) {
-    std::vector<uint32_t> m_commit((ncu + 31) / 32, 0u), m_eval((ncu + 31) / 32, 0u);
-    for (int k = 0; k < ncu; ++k) (k < commit_cus ? m_commit : m_eval)[k / 32] |= 1u << (k % 32);
-    if ((e = hipExtStreamCreateWithCUMask(&c->st, (uint32_t)m_commit.size(), m_commit.data())) != hipSuccess)
-      return bail("hipExtStreamCreateWithCUMask", e);
-    c->cu_partition = true;
-    if ((e = hipExtStreamCreateWithCUMask(&c->st2, (uint32_t)m_eval.size(), m_eval.data())) != hipSuccess)
-      return bail("hipExtStreamCreateWithCUMask", e);
-    if ((e = hipExtStreamCreateWithCUMask(&c->st_ev, (uint32_t)m_eval.size(), m_eval.data())) != hipSuccess)
-      return bail("hipExtStreamCreateWithCUMask", e);
-  } else {
-    if ((e = hipStreamCreateWithPriority(&c->st, hipStreamNonBlocking, prio_hi)) != hipSuccess) return bail("hipStreamCreate", e);
-    if ((e = hipStreamCreateWithPriority(&c->st2, hipStreamNonBlocking, prio_lo)) != hipSuccess) return bail("hipStreamCreate", e);
-    if ((e = hipStreamCreateWithPriority(&c->st_ev, hipStreamNonBlocking, prio_lo)) != hipSuccess) return bail("hipStreamCreate", e);
-  }
+  // (Round 3 tried a CU partition here: the commit chain on CU-masked streams, the eval pass on the other CUs, with the
+  // host applying a batch's placements one batch late. CU-masked streams are blocking streams — they synchronise with
+  // the null stream, which hipMemset / hipMemcpy / hipFree use — and a one-pod-batch test hung in gs_destroy's hipFree
+  // with it; the commit measured no faster on a CU of its own (GS_COMMIT_EXCL). Removed)
+  if ((e = hipStreamCreateWithPriority(&c->st, hipStreamNonBlocking, prio_hi)) != hipSuccess) return bail("hipStreamCreate", e);
+  if ((e = hipStreamCreateWithPriority(&c->st2, hipStreamNonBlocking, prio_lo)) != hipSuccess) return bail("hipStreamCreate", e);
+  if ((e = hipStreamCreateWithPriority(&c->st_ev, hipStreamNonBlocking, prio_lo)) != hipSuccess) return bail("hipStreamCreate", e);
   if ((e = hipStreamCreateWithFlags(&c->st_rb, hipStreamNonBlocking)) != hipSuccess) return bail("hipStreamCreate", e);
   if ((e = hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming)) != hipSuccess) return bail("hipEventCreate", e);
   if ((e = hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming)) != hipSuccess) return bail("hipEventCreate", e);
@@ -1752,8 +1732,7 @@ int gs_destroy(gs_ctx* c) {
   if (c->d_stamps) {
     std::vector<uint64_t> sa(520);
     if (hipMemcpy(sa.data(), c->d_stamps, 8 * 520, hipMemcpyDeviceToHost) == hipSuccess) {
-      static const char* kind = getenv("GS_COMMIT_KERNEL");
-      if (!(kind && kind[0] == 'p') && !c->window_k) {   // speculative commit kernel: one stamp region per wave
+      if (!c->window_k) {   // speculative commit kernel: one stamp region per wave
         const double np = c->stats_all_pods ? (double)c->stats_all_pods : 1.0;
         auto W = [&](int w, int i) { return (double)sa[w * 64 + i] / np; };
         fprintf(stderr, "gpuscore spec commit, cycles per committed pod (%llu pods, %llu decisions, %llu rollbacks, %.0f "
@@ -2092,17 +2071,6 @@ int schedule_stream(gs_ctx* c, PodRun run, Next&& next_run, Done&& run_done) {
     (void)hipStreamSynchronize(c->st_ev);
     (void)hipStreamSynchronize(c->st_rb);   // a voided or in-flight batch's readback into the pinned buffers
   };
-  // A batch whose successor is already running on the device has its placements applied on the host only after the
-  // batch after that is enqueued (its eval pass then overlaps the successor's commit; applying 128 placements takes
-  // ~230 us of host time that otherwise delays it): its outputs are copied out of the slot, which that batch reuses.
-  struct Pending {
-    int n = 0;
-    bool special = false;
-    const gs_pod* pods = nullptr;
-    gs_placement* out = nullptr;
-    std::vector<PlacementDev> h_out;
-    std::vector<PodVec> h_pods;
-  } pend;
   auto apply_batch = [&](const gs_pod* pods, gs_placement* outp, int n, const PlacementDev* hout, const PodVec* hpods,
                          bool special) -> int {
     for (int k = 0; k < n; ++k) {
@@ -2119,22 +2087,13 @@ int schedule_stream(gs_ctx* c, PodRun run, Next&& next_run, Done&& run_done) {
     }
     return GS_OK;
   };
-  auto apply_pending = [&]() -> int {
-    if (!pend.n) return GS_OK;
-    const int n = pend.n;
-    pend.n = 0;
-    return apply_batch(pend.pods, pend.out, n, pend.h_out.data(), pend.h_pods.data(), pend.special);
-  };
   auto body = [&]() -> int {
     int rc = GS_OK;
     uint32_t i = 0;
     bool inflight = false, cur_special = false, spec_ok = true;
     int cur_b = 0;
-    const gs_pod* prev_pods = nullptr;   // the pending batch's pods (a UID there must not start the next batch early)
-    int prev_n = 0;
     for (;;) {
       if (i == run.n) {   // the run is complete; the next one (its first batch may be in flight already)
-        if ((rc = apply_pending())) return rc;
         run_done(run, GS_OK);
         if (!have_nxt) have_nxt = next_run(&nxt);
         if (!have_nxt) break;
@@ -2171,8 +2130,7 @@ int schedule_stream(gs_ctx* c, PodRun run, Next&& next_run, Done&& run_done) {
       if (can_spec && spec_ok && !cur_special && np && c->dirty_list.empty() && !c->prep_stale) {
         bool sf = false;
         nb = batch_len(c, np, nj, nn, &sf);
-        if (!sf && !uid_overlap(pods + i, cur_b, np + nj, nb) &&
-            !(pend.n && uid_overlap(prev_pods, prev_n, np + nj, nb))) {
+        if (!sf && !uid_overlap(pods + i, cur_b, np + nj, nb)) {
           const int32_t* prev = c->d_committed;
           const PlacementDev* prev_out = c->d_out;
           const int here = c->cur_slot;
@@ -2192,15 +2150,6 @@ int schedule_stream(gs_ctx* c, PodRun run, Next&& next_run, Done&& run_done) {
           spec = true;
         }
       }
-      {   // the batch before this one, committed on the device: its placements on the host now
-        const auto t_p = hclk::now();
-        if ((rc = apply_pending())) { if (spec) drain(); return rc; }
-        if (c->host_timing) {
-          const double ap = std::chrono::duration<double, std::micro>(hclk::now() - t_p).count();
-          c->ht_apply += ap;
-          busy += ap;
-        }
-      }
       spec_ok = true;
       int committed = 0;
       const auto t_w = hclk::now();
@@ -2216,18 +2165,7 @@ int schedule_stream(gs_ctx* c, PodRun run, Next&& next_run, Done&& run_done) {
       }
       if (rc) { if (spec) drain(); return rc; }
       const bool host_work = c->h_committed[1] != 1;   // the device-side continuation flag the speculative pass read
-      const bool defer = c->cu_partition && spec && !host_work && committed == cur_b && !cur_special &&
-                         c->dirty_list.empty() && !c->prep_stale;
-      if (defer) {   // its successor runs: applied once the batch after that is enqueued
-        pend.n = committed;
-        pend.special = cur_special;
-        pend.pods = pods + i;
-        pend.out = run.out + i;
-        pend.h_out.assign(c->h_out, c->h_out + committed);
-        pend.h_pods.assign(c->h_pods, c->h_pods + committed);
-        prev_pods = pods + i;
-        prev_n = committed;
-      } else if ((rc = apply_batch(pods + i, run.out + i, committed, c->h_out, c->h_pods, cur_special))) {
+      if ((rc = apply_batch(pods + i, run.out + i, committed, c->h_out, c->h_pods, cur_special))) {
         if (spec) drain();
         return rc;
       }
@@ -2260,12 +2198,10 @@ int schedule_stream(gs_ctx* c, PodRun run, Next&& next_run, Done&& run_done) {
         }
       }
     }
-    if ((rc = apply_pending())) return rc;
     return flush_rows(c);
   };
   int rc = body();
   if (rc) {
-    (void)apply_pending();   // placements the device committed before the failure
     run_done(run, rc);
     if (have_nxt) run_done(nxt, GS_ESTATE);
   }

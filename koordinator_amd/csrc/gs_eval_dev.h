@@ -1,4 +1,4 @@
-// gs_eval_dev.h — device code shared by the eval kernels (gs_kernels.hip) and the commit kernel (gs_commit.hip):
+// gs_eval_dev.h — device code shared by the eval kernels (gs_kernels.hip) and the commit kernels (gs_kernels.hip, gs_commit_spec.hip):
 // the node row a pair evaluation reads, the fused Filter + Score of one (pod, node) pair, the selectHost tie-break
 // stream, wave helpers and the device-side cpuset Reserve.
 //

@@ -62,24 +62,29 @@ struct gs_gang_mgr {
     g.group = {id};
     return &g;
   }
-  // rejectGangGroupById (core.go:363-394): the waiting pods of the gang group are rejected (their Unreserve follows)
-  void reject_group(uint64_t id, std::vector<uint64_t>* rejected) {
+  // The framework's waiting pods of the gang group of `id` (uid order)
+  void group_waiting(const Gang& g, std::vector<uint64_t>* out) const {
+    const std::set<uint64_t> grp(g.group.begin(), g.group.end());
+    for (const auto& kv : fw_waiting)
+      if (grp.count(kv.second.first)) out->push_back(kv.first);
+  }
+  // rejectGangGroupById (core.go:363-394): the waiting pods of the gang group are rejected (their Unreserve follows).
+  // Nothing changes when they do not fit the caller's buffer (GS_EINVAL, *n = the count needed).
+  int reject_group(uint64_t id, uint64_t* out, uint32_t cap, uint32_t* n) {
     Gang* g = get(id, false);
-    if (!g) return;
-    const std::set<uint64_t> grp(g->group.begin(), g->group.end());
-    int n = 0;
-    for (auto it = fw_waiting.begin(); it != fw_waiting.end();) {
-      if (grp.count(it->second.first)) {
-        rejected->push_back(it->first);
-        it = fw_waiting.erase(it);
-        ++n;
-      } else {
-        ++it;
-      }
+    if (!g) return GS_OK;
+    std::vector<uint64_t> rej;
+    group_waiting(*g, &rej);
+    if (n) *n = (uint32_t)rej.size();
+    if (rej.size() > cap) return GS_EINVAL;
+    if (rej.empty()) return GS_OK;
+    for (size_t k = 0; k < rej.size(); ++k) {
+      if (out) out[k] = rej[k];
+      fw_waiting.erase(rej[k]);
     }
-    if (!n) return;
-    for (uint64_t gid : grp)
+    for (uint64_t gid : g->group)
       if (Gang* x = get(gid, false)) x->cycle_valid = false;
+    return GS_OK;
   }
 };
 
@@ -235,6 +240,7 @@ int gs_gang_permit(gs_gang_mgr* m, uint64_t gang_id, uint64_t uid, int64_t now_n
   if (!gang_id) return GS_GANG_PERMIT_SUCCESS;
   Gang* g = m->get(gang_id, false);
   if (!g) return GS_GANG_PERMIT_NOT_FOUND;
+  const bool was_waiting = g->waiting.count(uid) != 0;
   g->waiting.insert(uid);   // addAssumedPod
   for (uint64_t gid : g->group) {
     const Gang* x = m->get(gid, false);
@@ -244,19 +250,20 @@ int gs_gang_permit(gs_gang_mgr* m, uint64_t gang_id, uint64_t uid, int64_t now_n
       return GS_GANG_PERMIT_WAIT;
     }
   }
-  // AllowGangGroup (core.go:488-508): every waiting pod of the gang group goes on to bind
-  const std::set<uint64_t> grp(g->group.begin(), g->group.end());
+  // AllowGangGroup (core.go:488-508): every waiting pod of the gang group goes on to bind. The list is sized against
+  // the caller's buffer before any state changes: GS_EINVAL leaves the manager as it was (*n_allowed = the count needed).
   std::vector<uint64_t> out;
-  for (auto it = m->fw_waiting.begin(); it != m->fw_waiting.end();) {
-    if (grp.count(it->second.first)) {
-      out.push_back(it->first);
-      it = m->fw_waiting.erase(it);
-    } else {
-      ++it;
-    }
+  m->group_waiting(*g, &out);
+  if (n_allowed) *n_allowed = (uint32_t)out.size();
+  if (out.size() > cap) {
+    if (!was_waiting) g->waiting.erase(uid);
+    return GS_EINVAL;
   }
-  const int rc = copy_out(out, allowed, cap, n_allowed);
-  return rc ? rc : GS_GANG_PERMIT_SUCCESS;
+  for (size_t k = 0; k < out.size(); ++k) {
+    if (allowed) allowed[k] = out[k];
+    m->fw_waiting.erase(out[k]);
+  }
+  return GS_GANG_PERMIT_SUCCESS;
 }
 
 // PodGroupManager.PostBind (core.go:397-447): the gang's bound children (the PodGroup status patch is the caller's)
@@ -278,9 +285,8 @@ int gs_gang_post_filter(gs_gang_mgr* m, uint64_t gang_id, uint64_t uid, uint64_t
   Gang* g = m->get(gang_id, false);
   if (!g) return GS_OK;
   if (g->policy == GS_GANG_ONCE_SATISFIED && g->once) return GS_OK;
-  std::vector<uint64_t> out;
-  if (g->mode == GS_GANG_STRICT) m->reject_group(gang_id, &out);
-  return copy_out(out, rejected, cap, n_rejected);
+  if (g->mode == GS_GANG_STRICT) return m->reject_group(gang_id, rejected, cap, n_rejected);
+  return GS_OK;
 }
 
 // PodGroupManager.Unreserve (core.go:344-361) of an assumed gang pod (a rejected waiting pod, or one whose binding
@@ -292,26 +298,35 @@ int gs_gang_unreserve(gs_gang_mgr* m, uint64_t gang_id, uint64_t uid, uint64_t* 
   if (!gang_id) return GS_OK;
   Gang* g = m->get(gang_id, false);
   if (!g) return GS_OK;
-  g->waiting.erase(uid);   // delAssumedPod
+  // delAssumedPod; the rejection below is sized first, so GS_EINVAL leaves the manager as it was
+  const bool rejects = !(g->policy == GS_GANG_ONCE_SATISFIED && g->once) && g->mode == GS_GANG_STRICT;
+  if (rejects) {
+    std::vector<uint64_t> rej;
+    m->group_waiting(*g, &rej);
+    size_t need = 0;
+    for (uint64_t r : rej) need += r != uid;
+    if (n_rejected) *n_rejected = (uint32_t)need;
+    if (need > cap) return GS_EINVAL;
+  }
+  g->waiting.erase(uid);
   m->fw_waiting.erase(uid);
-  std::vector<uint64_t> out;
-  if (!(g->policy == GS_GANG_ONCE_SATISFIED && g->once) && g->mode == GS_GANG_STRICT) m->reject_group(gang_id, &out);
-  return copy_out(out, rejected, cap, n_rejected);
+  if (rejects) return m->reject_group(gang_id, rejected, cap, n_rejected);
+  return GS_OK;
 }
 
 // The framework's Permit timeout: waiting pods whose deadline is <= now_ns are rejected (their Unreserve follows).
 int gs_gang_expire(gs_gang_mgr* m, int64_t now_ns, uint64_t* rejected, uint32_t cap, uint32_t* n_rejected) {
   if (!m) return GS_EINVAL;
   std::vector<uint64_t> out;
-  for (auto it = m->fw_waiting.begin(); it != m->fw_waiting.end();) {
-    if (it->second.second <= now_ns) {
-      out.push_back(it->first);
-      it = m->fw_waiting.erase(it);
-    } else {
-      ++it;
-    }
+  for (const auto& kv : m->fw_waiting)
+    if (kv.second.second <= now_ns) out.push_back(kv.first);
+  if (n_rejected) *n_rejected = (uint32_t)out.size();
+  if (out.size() > cap) return GS_EINVAL;   // sized before any change
+  for (size_t k = 0; k < out.size(); ++k) {
+    if (rejected) rejected[k] = out[k];
+    m->fw_waiting.erase(out[k]);
   }
-  return copy_out(out, rejected, cap, n_rejected);
+  return GS_OK;
 }
 
 int gs_gang_get(const gs_gang_mgr* m, uint64_t gang_id, gs_gang_info* out) {

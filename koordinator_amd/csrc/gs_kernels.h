@@ -142,8 +142,6 @@ hipError_t launch_merge_levels(const uint8_t* xin, size_t xblock, int nranks, in
 size_t commit_smem_bytes(int B);
 bool commit_spec_selected(uint32_t window_k);   // the speculative commit kernel runs (else pipelined / lockstep)
 hipError_t launch_commit(const CommitArgs& a, hipStream_t st);        // window_k > 0: lockstep kernel
-hipError_t launch_commit_pipe(const CommitArgs& a, hipStream_t st);   // pipelined roles (gs_commit.hip)
-hipError_t set_commit_pipe_attributes();
 // GS_COMMIT_EXCL=1: the commit's workgroup holds a CU of its own: it declares the whole LDS of the CU and the eval
 // pass that overlaps it declares eval_lds_bytes(), so the dispatcher never places eval waves beside it. Measured
 // neutral on C3 (commit 0.705 vs 0.708 ms per batch): off by default.

@@ -1508,17 +1508,13 @@ size_t commit_smem_bytes(int B) {
   return b;
 }
 
-bool commit_spec_selected(uint32_t window_k) {
-  static const bool lockstep = getenv("GS_COMMIT_LOCKSTEP") && getenv("GS_COMMIT_LOCKSTEP")[0] == '1';
-  static const char* kind = getenv("GS_COMMIT_KERNEL");   // "pipe": the non-speculative pipelined kernel
-  return !window_k && !lockstep && !(kind && kind[0] == 'p');
-}
+// The speculative commit kernel runs every batch except under node sampling, whose rotation window is resolved by
+// commit_kernel (one shard).
+bool commit_spec_selected(uint32_t window_k) { return !window_k; }
 
 hipError_t launch_commit(const CommitArgs& a, hipStream_t st) {
-  static const bool lockstep = getenv("GS_COMMIT_LOCKSTEP") && getenv("GS_COMMIT_LOCKSTEP")[0] == '1';
-  // several shards: the speculative kernel reads the merged levels (launch_merge_levels), the others every rank block
+  // several shards: the speculative kernel reads the merged levels (launch_merge_levels)
   if (commit_spec_selected(a.window_k)) return launch_commit_spec(a, st);
-  if (!a.window_k && !lockstep) return launch_commit_pipe(a, st);
   if (a.stamps)
     hipLaunchKernelGGL(commit_kernel<true>, dim3(1), dim3(COMMIT_THREADS), commit_smem_bytes(a.npods), st, a);
   else
@@ -1545,9 +1541,7 @@ hipError_t launch_scatter_rows(const MirrorView& m, const uint32_t* idx, const i
 }
 
 hipError_t set_kernel_attributes() {
-  hipError_t e = set_commit_pipe_attributes();
-  if (e != hipSuccess) return e;
-  e = set_commit_spec_attributes();
+  hipError_t e = set_commit_spec_attributes();
   if (e != hipSuccess) return e;
   e = hipFuncSetAttribute(reinterpret_cast<const void*>(commit_kernel<false>),
                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)commit_smem_bytes(MAX_BATCH));

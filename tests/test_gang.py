@@ -352,3 +352,62 @@ def test_batched_gangs_match_sequential_order_oracle_engine():
     # the workload exercises every outcome
     assert (st == oc.ST_BOUND).sum() > 20 and (st == oc.ST_WAITING).sum() > 5 and (st == oc.ST_REJECTED).sum() > 3
     assert (wres["prefilter"] != 0).sum() > 5 and ((want["node"] < 0) & (wres["prefilter"] == 0)).sum() > 3
+
+
+def _big_gang(m, library, gid, n, group=()):
+    s = dict(gang_id=gid, min_member=n, mode=gg.STRICT, wait_time_ns=5 * SEC, group=list(group))
+    m.podgroup_upsert(gg.spec(**s) if library else s)
+    uids = [gid * 10000 + k for k in range(n)]
+    for u in uids:
+        m.pod_add(gid, u)
+    return uids
+
+
+@pytest.mark.parametrize("which", ["library", "oracle"])
+def test_large_strict_gang_lists_exceed_first_buffer(which):
+    """A Strict gang of 100 members: Permit's allowed list, PostFilter's and Unreserve's rejection lists and the
+    Permit-timeout list all exceed the driver's first 64-entry buffer. Every pod must come back exactly once and the
+    manager state must equal the restatement's (a call that returned GS_EINVAL with the state already changed lost
+    the pods of the retry)."""
+    lm, om = both_managers()
+    m = lm if which == "library" else om
+    waiting = (lambda: m.waiting_pods()) if which == "library" else (lambda: sorted(om.fw_waiting))
+    # Permit success: the 100th pod allows the 99 waiting ones
+    uids = _big_gang(m, which == "library", 1, 100)
+    for u in uids[:-1]:
+        assert m.permit(1, u, 0)[0] == gg.PERMIT_WAIT
+    st, _, allowed = m.permit(1, uids[-1], 0)
+    assert st == gg.PERMIT_SUCCESS and sorted(allowed) == sorted(uids[:-1])
+    assert waiting() == []
+    # PostFilter: a FitError rejects the 99 waiting pods of another Strict gang
+    uids = _big_gang(m, which == "library", 2, 100)
+    for u in uids[:-1]:
+        m.prefilter(2, u)
+        m.permit(2, u, 0)
+    rej = m.post_filter(2, uids[-1])
+    assert sorted(rej) == sorted(uids[:-1]) and waiting() == []
+    # Unreserve of one waiting pod rejects the other 98
+    uids = _big_gang(m, which == "library", 3, 100)
+    for u in uids[:-1]:
+        m.permit(3, u, 0)
+    rej = m.unreserve(3, uids[0])
+    assert sorted(rej) == sorted(uids[1:-1]) and waiting() == []
+    # Permit timeout: 99 waiting pods expire together
+    uids = _big_gang(m, which == "library", 4, 100)
+    for u in uids[:-1]:
+        m.permit(4, u, 0)
+    assert m.expire(10 * SEC) == sorted(uids[:-1]) and waiting() == []
+
+
+def test_large_gang_library_matches_restatement_state():
+    lm, om = both_managers()
+    for which, m in (("library", lm), ("oracle", om)):
+        uids = _big_gang(m, which == "library", 7, 90, group=[7, 8])
+        uids8 = _big_gang(m, which == "library", 8, 40, group=[7, 8])
+        for u in uids[:-1] + uids8:
+            m.permit(7 if u in uids else 8, u, 0)
+    a, b = lm.permit(7, 70089, 0), om.permit(7, 70089, 0)
+    assert a[0] == b[0] == gg.PERMIT_SUCCESS and sorted(a[2]) == sorted(b[2]) and len(a[2]) == 129
+    for g in (7, 8):
+        li, og = lm.info(g), om.gangs[g]
+        assert (li["waiting"], li["bound"]) == (len(og.waiting), len(og.bound))
