@@ -877,10 +877,11 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
     else if (lane == ROW_I64 + 1) { f_kind = 2; f_src = m.c32(C_DFLAGS); f_off = offsetof(Row, dflags); f_size = 4; }
     else if (lane == ROW_I64 + 2) { f_kind = 4; f_off = offsetof(Row, node); }
     else if (numa_on) {
-      if (lane >= 20 && lane < 26) { f_kind = 1; f_src = m.c64(C_CPU_UN0 + (lane - 20)); f_region = 1; f_off = (lane - 20) * 8; }
-      else if (lane == 26) { f_kind = 2; f_src = m.c32(C_CPU_META); f_region = 1; f_off = offsetof(CpuStateDev, meta); f_size = 4; }
-      else if (lane == 27) { f_kind = 2; f_src = m.c32(C_TOPO_DEV); f_region = 1; f_off = offsetof(CpuStateDev, topo); f_size = 4; }
-      else if (lane == 28) { f_kind = 3; f_src = a.aff; f_region = 2; f_size = 4; }
+      // CpuStateDev's 11 words (C_CPU_UN0 .. C_CPU_XC1), meta, topo; lanes 32..61 the NUMA row
+      if (lane >= 20 && lane < 31) { f_kind = 1; f_src = m.c64(C_CPU_UN0 + (lane - 20)); f_region = 1; f_off = (lane - 20) * 8; }
+      else if (lane == 31) { f_kind = 2; f_src = m.c32(C_CPU_META); f_region = 1; f_off = offsetof(CpuStateDev, meta); f_size = 4; }
+      else if (lane == 62) { f_kind = 2; f_src = m.c32(C_TOPO_DEV); f_region = 1; f_off = offsetof(CpuStateDev, topo); f_size = 4; }
+      else if (lane == 63) { f_kind = 3; f_src = a.aff; f_region = 2; f_size = 4; }
       else if (lane >= 32 && lane < 32 + NUMA_I64) {
         f_kind = 1; f_src = m.c64(C_ZCAP_CPU0 + (lane - 32)); f_off = offsetof(Row, nr) + (lane - 32) * 8;
       } else if (lane >= 50 && lane < 50 + NUMA_I32) {
@@ -1062,7 +1063,7 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
               }
               if (rb) {
                 CpuStateDev& cs = cst[slot];
-                if (cs.topo >= 0 && cs.topo == topo_id) {
+                if (cpuset_on_device(cs, topo_id, pk)) {
                   if (cpuset_reserve((const GS_LDS TopoDev*)&s_topo_w, (GS_LDS CpuStateDev*)&cs, pk, nf, no.zkeys,
                                      no.zcpu[0], no.zcpu[1], no.zcpu[2], no.zcpu[3], (GS_LDS NumaRow*)&dr_.nr,
                                      (GS_LDS uint64_t*)s_cpuset_w)) {
@@ -1237,7 +1238,7 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
   }
   for (int s = tid; s < nd; s += SP_THREADS)
     if (has_row[s]) m.c32(C_FREE_PODS)[drows[s].node] = drows[s].free_pods;
-  constexpr int NW = 8 + 11 + 6 + 1;
+  constexpr int NW = 8 + 11 + 11 + 1;
   if (numa_on)
     for (int e = tid; e < nd * NW; e += SP_THREADS) {
       const int sl = e / NW, j = e % NW;
@@ -1245,7 +1246,7 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
       const uint32_t node = drows[sl].node;
       if (j < 8) m.c64(C_ZRAW_CPU0 + j)[node] = (&drows[sl].nr.zraw_cpu[0])[j];
       else if (j < 19) m.c32(C_NFLAGS2 + (j - 8))[node] = reinterpret_cast<const int32_t*>(&drows[sl].nr.nflags2)[j - 8];
-      else if (j < 25) m.c64(C_CPU_UN0 + (j - 19))[node] = reinterpret_cast<const int64_t*>(&cst[sl])[j - 19];
+      else if (j < 30) m.c64(C_CPU_UN0 + (j - 19))[node] = reinterpret_cast<const int64_t*>(&cst[sl])[j - 19];
       else m.c32(C_CPU_META)[node] = (int32_t)cst[sl].meta;
     }
   for (int i = tid; i < committed; i += SP_THREADS) a.out[i].feasible = (uint32_t)final_F[i];

@@ -4,14 +4,20 @@
 // cpuset pod on the device and keep the batch going. The same code is compiled for the host, where the
 // library self-test (gsx_cpuset_selftest) compares it with the host restatement (gs_numa_host.cpp take_cpus).
 //
-// Scope (TopoDev.ok, "compact" topologies): <= 64 cores of <= 4 CPUs, <= 8 NUMA nodes and sockets, every
-// core and every NUMA node inside one socket; the node's maxRefCount <= 1 (no RefCount ordering). Nodes
-// outside it keep the host path (the commit kernel ends the batch after such a pod).
+// Scope (TopoDev.ok, "compact" topologies): <= 128 cores, <= 8 NUMA nodes and sockets, every core and every NUMA
+// node inside one socket, <= 4 CPUs per core up to 64 cores and <= 2 beyond; the node's maxRefCount <= 2 (RefCount
+// ordering over one "RefCount 1" plane set). Nodes outside it keep the host path (the commit kernel ends the batch
+// after such a pod).
 //
 // Representation: core rank k = position of the core id in ascending order (the reference's core-id
 // tiebreaks), NUMA node / socket index = position of the id in ascending order, CPU position j = rank of
-// the CPU id inside its core. A set of CPUs is 4 planes of 64-bit core masks: plane j, bit k = CPU (k, j).
-// Lists the reference orders by CPU id are materialised as 256-bit CPU masks (cpu_core / cpu_pos map back).
+// the CPU id inside its core. A set of CPUs is a set of planes of core masks: plane j, bit k = CPU (k, j) —
+// 4 planes of 64-bit masks for <= 64 cores, 2 planes of 128-bit masks beyond (TopoDev.wide). Either way a set is
+// 256 bits, stored as 4 packed words (the CPU state columns, the cpuset results); the selection is a template over
+// the two shapes, so the common one never carries 128-bit masks in its registers. Lists the reference orders by
+// CPU id are materialised as 256-bit CPU masks (cpu_core / cpu_pos map back).
+// maxRefCount 2: RC = the available CPUs at RefCount 1; the reference's RefCount orderings (sortCores,
+// sortCPUsByRefCount, freeCPUs' core order) become "RefCount-0 CPUs / cores with fewer RefCount-1 CPUs first".
 #pragma once
 #include <stdint.h>
 
@@ -25,14 +31,17 @@
 
 namespace gs {
 
-constexpr int TD_CORES = 64, TD_NODES = 8, TD_SOCKETS = 8, TD_POS = 4;
+constexpr int TD_CORES = 128, TD_NODES = 8, TD_SOCKETS = 8, TD_POS = 4;
+typedef unsigned __int128 cm_t;   // a 128-bit core mask (bit k = core rank k)
 
 struct TopoDev {
   int32_t ok;                       // the device path applies to this topology
   int32_t num_cpus, ncores, cpc, cpn, cps, nnodes, nsockets;
-  uint64_t node_cores[TD_NODES];    // cores of NUMA node index n
-  uint64_t sock_cores[TD_SOCKETS];  // cores of socket index s
-  uint64_t pos_cores[TD_POS];       // cores with a CPU at position j
+  int32_t wide;                     // ncores > 64: 2 planes of 128 cores (cpc <= 2)
+  int32_t pad0;
+  uint64_t node_cores[TD_NODES][2];     // cores of NUMA node index n (lo, hi word)
+  uint64_t sock_cores[TD_SOCKETS][2];   // cores of socket index s
+  uint64_t pos_cores[TD_POS][2];        // cores with a CPU at position j
   uint8_t core_node[TD_CORES];
   uint8_t node_sock[TD_NODES];
   uint8_t pad[8];
@@ -42,23 +51,29 @@ struct TopoDev {
 };
 static_assert(sizeof(TopoDev) % 8 == 0, "TopoDev is staged to LDS as 64-bit words");
 
-// Per-node CPU state the device Reserve reads and updates (HBM columns C_CPU_UN0.. / C_CPU_META).
+// Per-node CPU state the device Reserve reads and updates (HBM columns C_CPU_UN0 .. C_CPU_XC1, C_CPU_META). The
+// plane sets un / rc are packed words; the layout is the column order of gs_layout.h.
 struct CpuStateDev {
-  uint64_t un[TD_POS];   // not available: allocated (RefCount > 0) or reserved
-  uint64_t xc;           // cores holding an allocated CPU with PCPULevel exclusivity
-  uint64_t zal;          // allocated CPUs per zone slot z (16 bits each)
-  uint32_t meta;         // CM_* below
-  int32_t topo;          // TopoDev index; -1: cpuset selection stays on the host
+  uint64_t un[4];   // not available: RefCount >= maxRefCount, or reserved
+  uint64_t xc;      // cores holding an allocated CPU with PCPULevel exclusivity (ranks 0..63)
+  uint64_t zal;     // allocated CPUs (RefCount > 0) per zone slot z (16 bits each)
+  uint64_t rc[4];   // available CPUs at RefCount 1 (maxRefCount 2; zero otherwise)
+  uint64_t xc1;     // xc, ranks 64..127
+  uint32_t meta;    // CM_* below
+  int32_t topo;     // TopoDev index; -1: cpuset selection stays on the host
 };
+static_assert(sizeof(CpuStateDev) == 96, "CpuStateDev = 11 i64 columns + meta + topo");
 enum : uint32_t {
   CM_XN_MASK = 0xFFu,    // NUMA node indexes holding a NUMANodeLevel-exclusive allocated CPU
   CM_ZIDX_SHIFT = 8,     // 4 x 4 bits: zone slot z -> NUMA node index (0xF: not in the topology)
   CM_MOST = 1u << 24,    // NUMAAllocateStrategy MostAllocated (GetNUMAAllocateStrategy, util.go:35-41)
+  CM_MR2 = 1u << 25,     // maxRefCount 2
+  CM_XSTALE = 1u << 26,  // xc / xn may be inexact: a CPU of an exclusive node was shared (its policy overwritten)
 };
 
 // Wave-uniform reads of the topology / CPU state: on the device these functions run for one Reserve at a time (one
 // active lane or identical operands in every lane), so a value read from LDS is moved to a scalar register and the
-// selection below runs on the scalar unit (64-bit masks natively) instead of one VALU lane.
+// selection below runs on the scalar unit instead of one VALU lane.
 GS_HD int32_t TU32(int32_t x) {
 #if defined(__HIP_DEVICE_COMPILE__)
   return __builtin_amdgcn_readfirstlane(x);
@@ -68,34 +83,77 @@ GS_HD int32_t TU32(int32_t x) {
 }
 GS_HD uint32_t TUU(uint32_t x) { return (uint32_t)TU32((int32_t)x); }
 GS_HD uint64_t TU64(uint64_t x) { return ((uint64_t)TUU((uint32_t)(x >> 32)) << 32) | TUU((uint32_t)x); }
+GS_HD uint64_t cm_lo(cm_t x) { return (uint64_t)x; }
+GS_HD uint64_t cm_hi(cm_t x) { return (uint64_t)(x >> 64); }
 
+// ---- mask operations for both shapes (M = uint64_t: <= 64 cores, M = cm_t: <= 128)
 GS_HD int td_pc(uint64_t x) { return __builtin_popcountll(x); }
+GS_HD int td_pc(cm_t x) { return __builtin_popcountll(cm_lo(x)) + __builtin_popcountll(cm_hi(x)); }
 GS_HD int td_ctz(uint64_t x) { return __builtin_ctzll(x); }
-GS_HD int td_cnt(const uint64_t* P, uint64_t m) {
-  return td_pc(P[0] & m) + td_pc(P[1] & m) + td_pc(P[2] & m) + td_pc(P[3] & m);
-}
-GS_HD uint64_t td_any(const uint64_t* P) { return P[0] | P[1] | P[2] | P[3]; }
-GS_HD uint64_t td_all(const TopoDev& t) { return TU32(t.ncores) >= 64 ? ~0ull : ((1ull << TU32(t.ncores)) - 1ull); }
+GS_HD int td_ctz(cm_t x) { return cm_lo(x) ? __builtin_ctzll(cm_lo(x)) : 64 + __builtin_ctzll(cm_hi(x)); }
+template <class M> GS_HD M td_tm(const uint64_t* w);   // a TopoDev mask
+template <> GS_HD uint64_t td_tm<uint64_t>(const uint64_t* w) { return TU64(w[0]); }
+template <> GS_HD cm_t td_tm<cm_t>(const uint64_t* w) { return ((cm_t)TU64(w[1]) << 64) | (cm_t)TU64(w[0]); }
+template <class M> GS_HD M td_bit(int k) { return (M)1 << k; }
+template <class M> GS_HD bool td_has(M x, int k) { return (int)((x >> k) & 1u) != 0; }
+template <class M> constexpr int td_bits() { return (int)sizeof(M) * 8; }
 
-// E[v] = cores with exactly v CPUs set in P (v = 0..4), bit-sliced
-GS_HD void td_exact(const uint64_t* P, uint64_t* E) {
-  const uint64_t s0 = P[0] ^ P[1], c0 = P[0] & P[1], s1 = P[2] ^ P[3], c1 = P[2] & P[3];
-  const uint64_t b0 = s0 ^ s1, t1 = s0 & s1;
-  const uint64_t b1 = c0 ^ c1 ^ t1, b2 = (c0 & c1) | (c0 & t1) | (c1 & t1);
+template <class M, int NP> GS_HD int td_cnt(const M* P, M m) {
+  int n = 0;
+#pragma unroll
+  for (int j = 0; j < NP; ++j) n += td_pc(P[j] & m);
+  return n;
+}
+template <class M, int NP> GS_HD M td_any(const M* P) {
+  M a = 0;
+#pragma unroll
+  for (int j = 0; j < NP; ++j) a |= P[j];
+  return a;
+}
+template <class M> GS_HD M td_all(const TopoDev& t) {
+  const int n = TU32(t.ncores);
+  return n >= td_bits<M>() ? ~(M)0 : (td_bit<M>(n) - 1);
+}
+
+// packed words <-> planes
+template <class M, int NP> GS_HD void td_unpack(const uint64_t* w, M* P);
+template <> GS_HD void td_unpack<uint64_t, 4>(const uint64_t* w, uint64_t* P) {
+#pragma unroll
+  for (int j = 0; j < 4; ++j) P[j] = TU64(w[j]);
+}
+template <> GS_HD void td_unpack<cm_t, 2>(const uint64_t* w, cm_t* P) {
+  P[0] = ((cm_t)TU64(w[1]) << 64) | TU64(w[0]);
+  P[1] = ((cm_t)TU64(w[3]) << 64) | TU64(w[2]);
+}
+template <class M, int NP> GS_HD void td_pack(const M* P, uint64_t* w);
+template <> GS_HD void td_pack<uint64_t, 4>(const uint64_t* P, uint64_t* w) {
+#pragma unroll
+  for (int j = 0; j < 4; ++j) w[j] = P[j];
+}
+template <> GS_HD void td_pack<cm_t, 2>(const cm_t* P, uint64_t* w) {
+  w[0] = cm_lo(P[0]); w[1] = cm_hi(P[0]); w[2] = cm_lo(P[1]); w[3] = cm_hi(P[1]);
+}
+
+// E[v] = cores with exactly v CPUs set in P (v = 0..4), bit-sliced (planes past NP are empty)
+template <class M, int NP> GS_HD void td_exact(const M* P, M* E) {
+  const M p2 = NP > 2 ? P[NP > 2 ? 2 : 0] : (M)0, p3 = NP > 3 ? P[NP > 3 ? 3 : 0] : (M)0;
+  const M s0 = P[0] ^ P[1], c0 = P[0] & P[1], s1 = p2 ^ p3, c1 = p2 & p3;
+  const M b0 = s0 ^ s1, t1 = s0 & s1;
+  const M b1 = c0 ^ c1 ^ t1, b2 = (c0 & c1) | (c0 & t1) | (c1 & t1);
   E[0] = ~b0 & ~b1 & ~b2;
   E[1] = b0 & ~b1 & ~b2;
   E[2] = ~b0 & b1 & ~b2;
   E[3] = b0 & b1 & ~b2;
   E[4] = ~b0 & ~b1 & b2;
 }
-
 // cores with exactly v CPUs set in P, v a run-time value (no indexed register array: on the device a dynamically
 // indexed local array lives in scratch memory)
-GS_HD uint64_t td_exactly(const uint64_t* P, int v) {
-  uint64_t E[5];
-  td_exact(P, E);
-  return v == 0 ? E[0] : v == 1 ? E[1] : v == 2 ? E[2] : v == 3 ? E[3] : v == 4 ? E[4] : 0ull;
+template <class M, int NP> GS_HD M td_exactly(const M* P, int v) {
+  M E[5];
+  td_exact<M, NP>(P, E);
+  return v == 0 ? E[0] : v == 1 ? E[1] : v == 2 ? E[2] : v == 3 ? E[3] : v == 4 ? E[4] : (M)0;
 }
+
 // 8 run-time-indexed 32-bit entries in four named 64-bit registers (a local array indexed at run time would
 // live in scratch memory on the device)
 struct TdPack8 {
@@ -127,49 +185,69 @@ struct TdMask256 {
   }
 };
 
-// position of the r-th set CPU of core k in P (-1: none)
-GS_HD int td_rth(const uint64_t* P, int k, int r) {
-  for (int j = 0; j < TD_POS; ++j)
-    if ((P[j] >> k) & 1u) {
-      if (r == 0) return j;
-      --r;
-    }
+// position of the r-th CPU of core k in P in (RefCount, CPU id) order: the RefCount-0 CPUs (not in RC) by
+// position, then the RefCount-1 ones (-1: none)
+template <class M, int NP> GS_HD int td_rth(const M* P, const M* RC, int k, int r) {
+  for (int pass = 0; pass < 2; ++pass)
+#pragma unroll
+    for (int j = 0; j < NP; ++j)
+      if (td_has(P[j], k) && (int)td_has(RC[j], k) == pass) {
+        if (r == 0) return j;
+        --r;
+      }
   return -1;
 }
 
-// cpuAccumulator (cpu_accumulator.go:234-330) with maxRefCount <= 1
+// cpuAccumulator (cpu_accumulator.go:234-330) with maxRefCount <= 2
+template <class M, int NP>
 struct DAcc {
   const TopoDev& t;
-  uint64_t A[TD_POS];   // allocatableCPUs
-  uint64_t R[TD_POS];   // result
-  uint64_t xc;          // exclusiveInCores
-  uint32_t xn;          // exclusiveInNUMANodes (node indexes)
+  M A[NP];    // allocatableCPUs
+  M RC[NP];   // CPUs at RefCount 1 (allocatable or not: only A & RC is read)
+  M R[NP];    // result
+  M xc;       // exclusiveInCores
+  uint32_t xn;   // exclusiveInNUMANodes (node indexes)
   int needed, nalloc, ep;
-  bool most, exclusive;
+  bool most, exclusive, refs;
 
-  GS_HD DAcc(const TopoDev& tt, const uint64_t* avail, uint64_t xc0, uint32_t xn0, int n, int e, bool m)
+  GS_HD DAcc(const TopoDev& tt, const M* avail, const M* rc, M xc0, uint32_t xn0, int n, int e, bool m)
       : t(tt), xc(xc0), xn(xn0), needed(n), ep(e), most(m) {
-    for (int j = 0; j < TD_POS; ++j) { A[j] = avail[j]; R[j] = 0; }
-    nalloc = td_cnt(A, ~0ull);
+    M any_rc = 0;
+#pragma unroll
+    for (int j = 0; j < NP; ++j) { A[j] = avail[j]; RC[j] = rc[j]; R[j] = 0; any_rc |= A[j] & RC[j]; }
+    refs = any_rc != 0;
+    nalloc = td_cnt<M, NP>(A, ~(M)0);
     exclusive = e == GS_CPU_EXCLUSIVE_PCPU_LEVEL || e == GS_CPU_EXCLUSIVE_NUMA_NODE_LEVEL;
   }
+  GS_HD M tm(const uint64_t* w) const { return td_tm<M>(w); }
   GS_HD bool sless(int a, int b) const { return most ? a < b : a > b; }
   GS_HD int dir(int x) const { return most ? x : 511 - x; }   // ascending key of the sless order
   GS_HD bool satisfied() const { return needed < 1; }
-  GS_HD uint64_t nodes_cores(uint32_t nodes) const {
-    uint64_t m = 0;
-    for (; nodes; nodes &= nodes - 1) m |= TU64(t.node_cores[td_ctz(nodes)]);
+  GS_HD M nodes_cores(uint32_t nodes) const {
+    M m = 0;
+    for (; nodes; nodes &= nodes - 1) m |= tm(t.node_cores[__builtin_ctz(nodes)]);
     return m;
   }
+  // getCoreRefCount over allocatableCPUs (:776-783): cores whose CPUs in the snapshot S (the allocatable CPUs a list
+  // was built from: the reference sorts a list once, before taking from it) hold exactly v at RefCount 1; with no
+  // RefCount-1 CPU every core is at level 0
+  GS_HD M ref_level(const M* S, int v) const {
+    if (!refs) return v == 0 ? ~(M)0 : (M)0;
+    M P[NP];
+#pragma unroll
+    for (int j = 0; j < NP; ++j) P[j] = S[j] & RC[j];
+    return td_exactly<M, NP>(P, v);
+  }
+  GS_HD int ref_levels() const { return refs ? NP : 0; }
   // filterExclusive predicates: isCPUExclusivePCPULevel / isCPUExclusiveNUMANodeLevel (:318-330)
-  GS_HD uint64_t keep_xp(bool fe) const { return (fe && ep == GS_CPU_EXCLUSIVE_PCPU_LEVEL) ? ~xc : ~0ull; }
-  GS_HD uint64_t keep_xn(bool fe) const {
-    return (fe && ep == GS_CPU_EXCLUSIVE_NUMA_NODE_LEVEL) ? ~nodes_cores(xn) : ~0ull;
+  GS_HD M keep_xp(bool fe) const { return (fe && ep == GS_CPU_EXCLUSIVE_PCPU_LEVEL) ? ~xc : ~(M)0; }
+  GS_HD M keep_xn(bool fe) const {
+    return (fe && ep == GS_CPU_EXCLUSIVE_NUMA_NODE_LEVEL) ? ~nodes_cores(xn) : ~(M)0;
   }
   GS_HD void take(int k, int j) {   // take (:290-304)
-    const uint64_t b = 1ull << k;
+    const M b = td_bit<M>(k);
 #pragma unroll
-    for (int jj = 0; jj < TD_POS; ++jj) {
+    for (int jj = 0; jj < NP; ++jj) {
       if (jj != j) continue;
       R[jj] |= b;
       if (A[jj] & b) { A[jj] &= ~b; --nalloc; }
@@ -183,73 +261,82 @@ struct DAcc {
   // the first `n` allocatable CPUs of core k in CPU order
   GS_HD void take_core(int k, int n) {
 #pragma unroll
-    for (int j = 0; j < TD_POS; ++j)
-      if (n > 0 && ((A[j] >> k) & 1u)) { take(k, j); --n; }
+    for (int j = 0; j < NP; ++j)
+      if (n > 0 && td_has(A[j], k)) { take(k, j); --n; }
   }
-  // head(list, needed) of a full-core list (cores ascending, CPUs ascending)
-  GS_HD void take_head_cores(uint64_t q) {
-    for (; q && needed > 0; q &= q - 1) take_core(td_ctz(q), needed < TU32(t.cpc) ? needed : TU32(t.cpc));
-  }
-  // Takes up to `needed` CPUs, in CPU-id order, out of the pass-r CPUs (the r-th CPU of each core) of the
-  // snapshot S; r < 0: all CPUs of S.
-  GS_HD void take_cpu_order(const uint64_t* S, int r) {
-    TdMask256 W;
-    for (uint64_t b = td_any(S); b; b &= b - 1) {
-      const int k = td_ctz(b);
-      if (r < 0) {
+  // head(list, needed) of a full-core list: cores by (RefCount asc, id) (sortCores, :345-367), CPUs ascending
+  GS_HD void take_head_cores(M q) {
+    const int nl = ref_levels();
+    M S[NP];
 #pragma unroll
-        for (int j = 0; j < TD_POS; ++j)
-          if ((S[j] >> k) & 1u) {
-            W.set_bit(TU32(t.core_cpu[k][j]));
-          }
-      } else {
-        const int j = td_rth(S, k, r);
-        if (j < 0) continue;
-        W.set_bit(TU32(t.core_cpu[k][j]));
+    for (int j = 0; j < NP; ++j) S[j] = A[j];
+    for (int v = 0; v <= nl && needed > 0; ++v)
+      for (M b = q & ref_level(S, v); b && needed > 0; b &= b - 1)
+        take_core(td_ctz(b), needed < TU32(t.cpc) ? needed : TU32(t.cpc));
+  }
+  // Takes up to `needed` CPUs, in (RefCount, CPU id) order, out of the pass-r CPUs (the r-th CPU of each core in
+  // (RefCount, id) order) of the snapshot S; r < 0: all CPUs of S.
+  GS_HD void take_cpu_order(const M* S, int r) {
+    TdMask256 W0, W1;   // RefCount 0 / 1
+    for (M b = td_any<M, NP>(S); b; b &= b - 1) {
+      const int k = td_ctz(b);
+      const int jr = r >= 0 ? td_rth<M, NP>(S, RC, k, r) : -1;
+#pragma unroll
+      for (int j = 0; j < NP; ++j) {
+        if (!td_has(S[j], k) || (r >= 0 && j != jr)) continue;
+        const int c = TU32(t.core_cpu[k][j]);
+        if (td_has(RC[j], k)) W1.set_bit(c);
+        else W0.set_bit(c);
       }
     }
 #pragma unroll
-    for (int w = 0; w < 4; ++w)
-      for (uint64_t x = w == 0 ? W.w0 : w == 1 ? W.w1 : w == 2 ? W.w2 : W.w3; x && needed > 0; x &= x - 1) {
-        const int c = w * 64 + td_ctz(x);
-        take(TU32(t.cpu_core[c]), TU32(t.cpu_pos[c]));
+    for (int g = 0; g < 2; ++g)
+#pragma unroll
+      for (int w = 0; w < 4; ++w) {
+        const TdMask256& W = g ? W1 : W0;
+        for (uint64_t x = w == 0 ? W.w0 : w == 1 ? W.w1 : w == 2 ? W.w2 : W.w3; x && needed > 0; x &= x - 1) {
+          const int c = w * 64 + __builtin_ctzll(x);
+          take(TU32(t.cpu_core[c]), TU32(t.cpu_pos[c]));
+        }
       }
   }
-  // head(spreadCPUs(list), needed) for a list in CPU-id order: the CPUs of cores `m` in A; `first_only`:
-  // the list went through extractCPU (one CPU per core), L = its length
-  GS_HD void take_spread_cpu_list(uint64_t m, bool first_only, int L) {
-    uint64_t S[TD_POS];
-    for (int j = 0; j < TD_POS; ++j) S[j] = A[j] & m;
+  // head(spreadCPUs(list), needed) for a list in (RefCount, CPU id) order (sortCPUsByRefCount, :785-797): the CPUs
+  // of cores `m` in A; `first_only`: the list went through extractCPU (one CPU per core), L = its length
+  GS_HD void take_spread_cpu_list(M m, bool first_only, int L) {
+    M S[NP];
+#pragma unroll
+    for (int j = 0; j < NP; ++j) S[j] = A[j] & m;
     if (!first_only && L <= TU32(t.cpc)) { take_cpu_order(S, -1); return; }   // spreadCPUs keeps short lists as is
-    const int passes = first_only ? 1 : TD_POS;
+    const int passes = first_only ? 1 : NP;
     for (int r = 0; r < passes && needed > 0; ++r) take_cpu_order(S, r);
   }
-  GS_HD uint64_t full_cores(uint64_t keep) const {
-    uint64_t K[TD_POS];
-    for (int j = 0; j < TD_POS; ++j) K[j] = A[j] & keep;
-    return td_exactly(K, TU32(t.cpc)) & td_any(K);
+  GS_HD M full_cores(M keep) const {
+    M K[NP];
+#pragma unroll
+    for (int j = 0; j < NP; ++j) K[j] = A[j] & keep;
+    return td_exactly<M, NP>(K, TU32(t.cpc)) & td_any<M, NP>(K);
   }
   // freeCoresInNode(true, fe) (:370-461): the first NUMA node list with >= needed CPUs (-1: none)
-  GS_HD int pick_full_node(bool fe, uint64_t* cores) const {
-    const uint64_t keep = td_all(t) & keep_xn(fe);
-    const uint64_t full = full_cores(keep);
+  GS_HD int pick_full_node(bool fe, M* cores) const {
+    const M keep = td_all<M>(t) & keep_xn(fe);
+    const M full = full_cores(keep);
     int best = -1, bsz = 0, bsf = 0;
     for (int n = 0; n < TU32(t.nnodes); ++n) {
-      const uint64_t q = full & TU64(t.node_cores[n]);
+      const M q = full & tm(t.node_cores[n]);
       if (!q) continue;
       const int sz = TU32(t.cpc) * td_pc(q);
       if (sz < needed) continue;
-      const int sf = td_cnt(A, keep & TU64(t.sock_cores[TU32(t.node_sock[n])]));
+      const int sf = td_cnt<M, NP>(A, keep & tm(t.sock_cores[TU32(t.node_sock[n])]));
       if (best < 0 || sless(sz, bsz) || (sz == bsz && sless(sf, bsf))) { best = n; bsz = sz; bsf = sf; *cores = q; }
     }
     return best;
   }
   // freeCoresInSocket(true) (:463-527): the first socket list with >= needed CPUs
-  GS_HD int pick_full_socket(uint64_t* cores) const {
-    const uint64_t full = full_cores(~0ull);
+  GS_HD int pick_full_socket(M* cores) const {
+    const M full = full_cores(~(M)0);
     int best = -1, bsz = 0;
     for (int s = 0; s < TU32(t.nsockets); ++s) {
-      const uint64_t q = full & TU64(t.sock_cores[s]);
+      const M q = full & tm(t.sock_cores[s]);
       if (!q) continue;
       const int sz = TU32(t.cpc) * td_pc(q);
       if (sz < needed) continue;
@@ -257,85 +344,82 @@ struct DAcc {
     }
     return best;
   }
-  // freeCPUsInNode(fe) (:529-605): the first NUMA node list with >= needed CPUs
-  GS_HD int pick_cpus_node(bool fe, uint64_t* cores, int* L) const {
-    const uint64_t keep = td_all(t) & keep_xp(fe) & keep_xn(fe);
+  // freeCPUsInNode(fe) (:529-605) / freeCPUsInSocket(fe) (:607-656): the first list with >= needed CPUs
+  GS_HD int pick_cpus(bool node, bool fe, M* cores, int* L) const {
+    const M keep = td_all<M>(t) & keep_xp(fe) & (node ? keep_xn(fe) : ~(M)0);
     int best = -1, bnf = 0, bsf = 0;
-    for (int n = 0; n < TU32(t.nnodes); ++n) {
-      const uint64_t m = keep & TU64(t.node_cores[n]);
-      const int nf = td_cnt(A, m);
+    const int cnt = node ? TU32(t.nnodes) : TU32(t.nsockets);
+    for (int n = 0; n < cnt; ++n) {
+      const M m = keep & tm(node ? t.node_cores[n] : t.sock_cores[n]);
+      const int nf = td_cnt<M, NP>(A, m);
       if (nf == 0) continue;
-      const int len = fe ? td_pc(td_any(A) & m) : nf;
+      const int len = fe ? td_pc(td_any<M, NP>(A) & m) : nf;
       if (len < needed) continue;
-      const int sf = td_cnt(A, keep & TU64(t.sock_cores[TU32(t.node_sock[n])]));
-      if (best < 0 || sless(nf, bnf) || (nf == bnf && sless(sf, bsf))) {
-        best = n; bnf = nf; bsf = sf; *cores = m; *L = len;
+      if (node) {   // NUMA nodes by (free CPUs, socket free CPUs, id)
+        const int sf = td_cnt<M, NP>(A, keep & tm(t.sock_cores[TU32(t.node_sock[n])]));
+        if (best < 0 || sless(nf, bnf) || (nf == bnf && sless(sf, bsf))) {
+          best = n; bnf = nf; bsf = sf; *cores = m; *L = len;
+        }
+      } else if (best < 0 || sless(len, bnf)) {   // sockets by (list length, id)
+        best = n; bnf = len; *cores = m; *L = len;
       }
     }
     return best;
   }
-  // freeCPUsInSocket(fe) (:607-656)
-  GS_HD int pick_cpus_socket(bool fe, uint64_t* cores, int* L) const {
-    const uint64_t keep = td_all(t) & keep_xp(fe);
-    int best = -1, bl = 0;
-    for (int s = 0; s < TU32(t.nsockets); ++s) {
-      const uint64_t m = keep & TU64(t.sock_cores[s]);
-      const int nf = td_cnt(A, m);
-      if (nf == 0) continue;
-      const int len = fe ? td_pc(td_any(A) & m) : nf;
-      if (len < needed) continue;
-      if (best < 0 || sless(len, bl)) { best = s; bl = len; *cores = m; *L = len; }
-    }
-    return best;
-  }
   // head(spreadCPUs(freeCPUs(fe)), needed) (:658-774): cores ordered by (CPUs of the result in the socket
-  // desc, socket free, node free, core size asc, socket id, core id), CPUs of a core ascending
+  // desc, socket free, node free, core size asc, socket id, core RefCount asc, core id), CPUs of a core in
+  // (RefCount, id) order
   GS_HD void take_free_cpus(bool fe) {
-    const uint64_t keep = td_all(t) & keep_xp(fe) & keep_xn(fe);
-    uint64_t S[TD_POS], E[5];
-    for (int j = 0; j < TD_POS; ++j) S[j] = A[j] & keep;
-    const uint64_t cores = td_any(S);
+    const M keep = td_all<M>(t) & keep_xp(fe) & keep_xn(fe);
+    M S[NP], E[5];
+#pragma unroll
+    for (int j = 0; j < NP; ++j) S[j] = A[j] & keep;
+    const M cores = td_any<M, NP>(S);
     if (!cores) return;
-    td_exact(S, E);
-    const int L = td_cnt(S, ~0ull);
+    td_exact<M, NP>(S, E);
+    const int L = td_cnt<M, NP>(S, ~(M)0);
+    const int nl = ref_levels();
     // NUMA nodes by group key (colo desc, socket free, node free), ascending; equal keys merge
     // entry i = (key << 3 | node) of the i-th node in key order (stable)
     TdPack8 ok;
     int nn = 0;
     for (int n = 0; n < TU32(t.nnodes); ++n) {
-      if (!(cores & TU64(t.node_cores[n]))) continue;
-      const uint64_t sm = TU64(t.sock_cores[TU32(t.node_sock[n])]);
-      const int colo = td_cnt(R, sm), sf = td_cnt(S, sm), nf = td_cnt(S, TU64(t.node_cores[n]));
+      if (!(cores & tm(t.node_cores[n]))) continue;
+      const M sm = tm(t.sock_cores[TU32(t.node_sock[n])]);
+      const int colo = td_cnt<M, NP>(R, sm), sf = td_cnt<M, NP>(S, sm), nf = td_cnt<M, NP>(S, tm(t.node_cores[n]));
       const uint32_t kn = ((uint32_t)(511 - colo) << 18) | ((uint32_t)dir(sf) << 9) | (uint32_t)dir(nf);
       int i = nn++;   // insertion after the last key <= kn (stable)
       while (i > 0 && (ok.get(i - 1) >> 3) > kn) { ok.set(i, ok.get(i - 1)); --i; }
       ok.set(i, kn << 3 | (uint32_t)n);
     }
     const bool as_is = L <= TU32(t.cpc);   // spreadCPUs keeps short lists as is
-    const int passes = as_is ? 1 : TD_POS;
+    const int passes = as_is ? 1 : NP;
     for (int r = 0; r < passes; ++r) {
       for (int g = 0; g < nn;) {
-        uint64_t M = 0;
+        M Mg = 0;
         int h = g;
         const uint32_t kg = ok.get(g) >> 3;
-        for (; h < nn && (ok.get(h) >> 3) == kg; ++h) M |= cores & TU64(t.node_cores[ok.get(h) & 7u]);
+        for (; h < nn && (ok.get(h) >> 3) == kg; ++h) Mg |= cores & tm(t.node_cores[ok.get(h) & 7u]);
         g = h;
 #pragma unroll
-        for (int v = 1; v <= TD_POS; ++v) {
+        for (int v = 1; v <= NP; ++v) {
           if (!as_is && v <= r) continue;
-          const uint64_t Mv = M & E[v];
+          const M Mv = Mg & E[v];
           if (!Mv) continue;
           for (int s = 0; s < TU32(t.nsockets); ++s)
-            for (uint64_t q = Mv & TU64(t.sock_cores[s]); q; q &= q - 1) {
-              const int k = td_ctz(q);
-              if (as_is) {
-                for (int j = 0; j < TD_POS && needed > 0; ++j)
-                  if ((S[j] >> k) & 1u) take(k, j);
-              } else {
-                take(k, td_rth(S, k, r));
+            for (int rl = 0; rl <= nl; ++rl)
+              for (M q = Mv & tm(t.sock_cores[s]) & ref_level(S, rl); q; q &= q - 1) {
+                const int k = td_ctz(q);
+                if (as_is) {
+                  for (int pass = 0; pass < 2 && needed > 0; ++pass)
+#pragma unroll
+                    for (int j = 0; j < NP; ++j)
+                      if (needed > 0 && td_has(S[j], k) && (int)td_has(RC[j], k) == pass) take(k, j);
+                } else {
+                  take(k, td_rth<M, NP>(S, RC, k, r));
+                }
+                if (needed < 1) return;
               }
-              if (needed < 1) return;
-            }
         }
       }
     }
@@ -359,35 +443,36 @@ GS_HD void td_go_sort(TdPack8& e, int n, bool desc) {
     }
 }
 
-// takeCPUs (cpu_accumulator.go:87-232); avail = planes of the CPUs it may take. false: the reference errors.
-GS_HD bool td_take_cpus(const TopoDev& t, const uint64_t* avail, uint64_t xc, uint32_t xn, int needed,
-                               int bind, int ep, bool most, uint64_t* out) {
-  DAcc a(t, avail, xc, xn, needed, ep, most);
-  for (int j = 0; j < TD_POS; ++j) out[j] = 0;
+// takeCPUs (cpu_accumulator.go:87-232); avail = planes of the CPUs it may take, rc = the RefCount-1 planes.
+// false: the reference errors.
+template <class M, int NP>
+GS_HD bool td_take_cpus_t(const TopoDev& t, const M* avail, const M* rc, M xc, uint32_t xn, int needed, int bind,
+                          int ep, bool most, M* out) {
+  DAcc<M, NP> a(t, avail, rc, xc, xn, needed, ep, most);
+#pragma unroll
+  for (int j = 0; j < NP; ++j) out[j] = 0;
   if (a.satisfied()) return true;
   if (a.needed > a.nalloc) return false;
   const bool full = bind == GS_CPU_BIND_FULL_PCPUS;
   bool ok = false;
   do {
-    uint64_t m = 0;
+    M m = 0;
     int L = 0;
     if (full || TU32(t.cpc) == 1) {
-      if (a.needed <= TU32(t.cpn) && (a.pick_full_node(true, &m) >= 0 || a.pick_full_node(false, &m) >= 0)) {
-        a.take_head_cores(m);
-        ok = true;
-        break;
-      }
-      if (a.needed <= TU32(t.cps) && a.pick_full_socket(&m) >= 0) {
+      bool got = false;
+      for (int fe = 1; fe >= 0 && !got && a.needed <= TU32(t.cpn); --fe) got = a.pick_full_node(fe != 0, &m) >= 0;
+      if (!got && a.needed <= TU32(t.cps)) got = a.pick_full_socket(&m) >= 0;
+      if (got) {
         a.take_head_cores(m);
         ok = true;
         break;
       }
       // freeCoresInSocket(true) in (size, id) order, then sort.Slice by size desc (:141-155)
-      const uint64_t fc = a.full_cores(~0ull);
+      const M fc = a.full_cores(~(M)0);
       TdPack8 so;   // (size << 3 | socket index)
       int ns = 0;
       for (int s = 0; s < TU32(t.nsockets); ++s) {
-        const uint64_t q = fc & TU64(t.sock_cores[s]);
+        const M q = fc & a.tm(t.sock_cores[s]);
         if (!q) continue;
         const int z = TU32(t.cpc) * td_pc(q);
         int i = ns++;
@@ -401,120 +486,236 @@ GS_HD bool td_take_cpus(const TopoDev& t, const uint64_t* avail, uint64_t xc, ui
         const uint32_t ei = so.get(i);
         const int idi = (int)(ei & 7u), szi = (int)(ei >> 3);
         if (a.needed < szi) { uo.set(nu++, ei); continue; }
-        for (uint64_t b = fc & TU64(t.sock_cores[idi]); b; b &= b - 1) a.take_core(td_ctz(b), TD_POS);
+        for (M b = fc & a.tm(t.sock_cores[idi]); b; b &= b - 1) a.take_core(td_ctz(b), TD_POS);
         ok = a.satisfied();
       }
       if (ok) break;
-      if (a.needed >= TU32(t.cpc)) {   // (:157-176)
+      if (a.needed >= TU32(t.cpc)) {   // (:157-176): the lists' cores in (RefCount, id) order, cpc CPUs at a time
         td_go_sort(uo, nu, false);
-        for (int i = 0; i < nu && !ok; ++i)
-          for (uint64_t b = fc & TU64(t.sock_cores[uo.get(i) & 7u]); b; b &= b - 1) {
-            a.take_core(td_ctz(b), TD_POS);
-            if (a.satisfied()) { ok = true; break; }
-            if (a.needed < TU32(t.cpc)) break;
-          }
+        const int nl = a.ref_levels();
+        for (int i = 0; i < nu && !ok; ++i) {
+          const M sc = fc & a.tm(t.sock_cores[uo.get(i) & 7u]);
+          M S[NP];
+#pragma unroll
+          for (int j = 0; j < NP; ++j) S[j] = a.A[j];
+          bool brk = false;
+          for (int v = 0; v <= nl && !brk; ++v)
+            for (M b = sc & a.ref_level(S, v); b; b &= b - 1) {
+              a.take_core(td_ctz(b), TD_POS);
+              if (a.satisfied()) { ok = true; brk = true; break; }
+              if (a.needed < TU32(t.cpc)) { brk = true; break; }
+            }
+        }
         if (ok) break;
       }
     }
-    if (!full) {   // (:184-215)
-      if (a.needed <= TU32(t.cpn)) {
-        if (a.pick_cpus_node(true, &m, &L) >= 0) { a.take_spread_cpu_list(m, true, L); ok = true; break; }
-        if (a.pick_cpus_node(false, &m, &L) >= 0) { a.take_spread_cpu_list(m, false, L); ok = true; break; }
+    if (!full) {   // (:184-215): node lists (filterExclusive true, false), then socket lists; one call site of each
+      int found = -1;   // (a run-time loop keeps one inlined copy of the list code)
+      for (int k = 0; k < 4 && found < 0; ++k) {
+        const bool node = k < 2;
+        if (a.needed > (node ? TU32(t.cpn) : TU32(t.cps))) continue;
+        if (a.pick_cpus(node, (k & 1) == 0, &m, &L) >= 0) found = k;
       }
-      if (a.needed <= TU32(t.cps)) {
-        if (a.pick_cpus_socket(true, &m, &L) >= 0) { a.take_spread_cpu_list(m, true, L); ok = true; break; }
-        if (a.pick_cpus_socket(false, &m, &L) >= 0) { a.take_spread_cpu_list(m, false, L); ok = true; break; }
-      }
+      if (found >= 0) { a.take_spread_cpu_list(m, (found & 1) == 0, L); ok = true; break; }
     }
-    a.take_free_cpus(true);   // (:217-229)
-    if (a.satisfied()) { ok = true; break; }
-    a.take_free_cpus(false);
-    ok = a.satisfied();
+    for (int fe = 1; fe >= 0 && !ok; --fe) {   // (:217-229)
+      a.take_free_cpus(fe != 0);
+      ok = a.satisfied();
+    }
   } while (false);
   if (!ok) return false;
-  for (int j = 0; j < TD_POS; ++j) out[j] = a.R[j];
+#pragma unroll
+  for (int j = 0; j < NP; ++j) out[j] = a.R[j];
   return true;
 }
 
-// available CPUs (getAvailableCPUs, node_allocation.go:142-162, maxRefCount <= 1) as planes
-GS_HD void td_available(const TopoDev& t, const CpuStateDev& cs, uint64_t* P) {
-  for (int j = 0; j < TD_POS; ++j) P[j] = TU64(t.pos_cores[j]) & ~TU64(cs.un[j]);
-}
+template <class M> GS_HD M td_xc(const CpuStateDev& cs);
+template <> GS_HD uint64_t td_xc<uint64_t>(const CpuStateDev& cs) { return TU64(cs.xc); }
+template <> GS_HD cm_t td_xc<cm_t>(const CpuStateDev& cs) { return ((cm_t)TU64(cs.xc1) << 64) | (cm_t)TU64(cs.xc); }
 GS_HD int td_zone_node(const CpuStateDev& cs, int z) { return (int)((TUU(cs.meta) >> (CM_ZIDX_SHIFT + 4 * z)) & 15u); }
 
+// available CPUs (getAvailableCPUs, node_allocation.go:142-162: RefCount < maxRefCount, not reserved) as planes
+template <class M, int NP> GS_HD void td_available(const TopoDev& t, const CpuStateDev& cs, M* P) {
+  M U[NP];
+  td_unpack<M, NP>(cs.un, U);
+#pragma unroll
+  for (int j = 0; j < NP; ++j) P[j] = td_tm<M>(t.pos_cores[j]) & ~U[j];
+}
+
 // allocateCPUSet (resource_manager.go:273-360) given the NUMA split Allocate produced (PlacementDev zkeys /
-// zcpu). false: the reference errors (cannot follow a feasible Filter; the host fails loudly).
-GS_HD bool td_allocate_cpuset(const TopoDev& t, const CpuStateDev& cs, int num_cpus, int bind, bool required,
-                                     int ep, uint32_t zkeys, const int64_t* zcpu, uint64_t* out) {
-  uint64_t P[TD_POS];
-  td_available(t, cs, P);
+// zcpu), the cpuset as packed words. false: the reference errors (cannot follow a feasible Filter; the host fails
+// loudly).
+template <class M, int NP>
+GS_HD bool td_allocate_cpuset_t(const TopoDev& t, const CpuStateDev& cs, int num_cpus, int bind, bool required, int ep,
+                                uint32_t zkeys, const int64_t* zcpu, uint64_t* out_w) {
+  M P[NP], RC[NP], out[NP];
+  td_available<M, NP>(t, cs, P);
+  td_unpack<M, NP>(cs.rc, RC);
   const bool most = TUU(cs.meta) & CM_MOST;
-  const uint64_t xc = TU64(cs.xc);
+  const M xc = td_xc<M>(cs);
   const uint32_t xn = TUU(cs.meta) & CM_XN_MASK;
   if (required) {   // filterCPUsByRequiredCPUBindPolicy (:534-566)
     if (bind == GS_CPU_BIND_FULL_PCPUS) {
-      const uint64_t f = td_exactly(P, TU32(t.cpc)) & td_any(P);
-      for (int j = 0; j < TD_POS; ++j) P[j] &= f;
+      const M f = td_exactly<M, NP>(P, TU32(t.cpc)) & td_any<M, NP>(P);
+#pragma unroll
+      for (int j = 0; j < NP; ++j) P[j] &= f;
     } else if (bind == GS_CPU_BIND_SPREAD_BY_PCPUS) {
-      uint64_t seen = 0;
-      for (int j = 0; j < TD_POS; ++j) { P[j] &= ~seen; seen |= P[j]; }
+      M seen = 0;
+#pragma unroll
+      for (int j = 0; j < NP; ++j) { P[j] &= ~seen; seen |= P[j]; }
     }
   }
-  for (int j = 0; j < TD_POS; ++j) out[j] = 0;
-  if (td_cnt(P, ~0ull) < num_cpus) return false;
-  int needed = num_cpus;
-  uint64_t got[TD_POS];
-  if (zkeys) {
-    for (int z = 0; z < 4; ++z) {
+#pragma unroll
+  for (int j = 0; j < NP; ++j) out[j] = 0;
+  for (int j = 0; j < 4; ++j) out_w[j] = 0;
+  if (td_cnt<M, NP>(P, ~(M)0) < num_cpus) return false;
+  // takePreferredCPUs per hinted zone (zkeys: the NUMA split), or once over every available CPU; one call site of
+  // the selection (a second inlined copy doubles the function's registers)
+  for (int z = zkeys ? 0 : 4; z < (zkeys ? 4 : 5); ++z) {
+    M in[NP];
+    int num = num_cpus;
+    if (z < 4) {
       if (!((zkeys >> z) & 1u) && !((zkeys >> (4 + z)) & 1u)) continue;
       const int n = td_zone_node(cs, z);
-      const uint64_t m = n < TU32(t.nnodes) ? TU64(t.node_cores[n]) : 0;
-      uint64_t in[TD_POS];
-      for (int j = 0; j < TD_POS; ++j) in[j] = P[j] & m;
-      int num = td_cnt(in, ~0ull);
+      const M m = n < TU32(t.nnodes) ? td_tm<M>(t.node_cores[n]) : (M)0;
+#pragma unroll
+      for (int j = 0; j < NP; ++j) in[j] = P[j] & m;
+      num = td_cnt<M, NP>(in, ~(M)0);
       const int64_t zz = z == 0 ? zcpu[0] : z == 1 ? zcpu[1] : z == 2 ? zcpu[2] : zcpu[3];
       const int want = ((zkeys >> z) & 1u) ? (int)(zz / 1000) : 0;
       if (want < num) num = want;
       if (num <= 0) continue;   // takePreferredCPUs with nothing needed
-      if (!td_take_cpus(t, in, xc, xn, num, bind, ep, most, got)) return false;
-      for (int j = 0; j < TD_POS; ++j) out[j] |= got[j];
+    } else {
+#pragma unroll
+      for (int j = 0; j < NP; ++j) in[j] = P[j];
     }
-    needed -= td_cnt(out, ~0ull);
-    if (needed != 0) return false;
+    M got[NP];
+    if (!td_take_cpus_t<M, NP>(t, in, RC, xc, xn, num, bind, ep, most, got)) return false;
+#pragma unroll
+    for (int j = 0; j < NP; ++j) out[j] |= got[j];
   }
-  if (needed > 0) {
-    uint64_t rest[TD_POS];
-    for (int j = 0; j < TD_POS; ++j) rest[j] = P[j] & ~out[j];
-    if (!td_take_cpus(t, rest, xc, xn, needed, bind, ep, most, got)) return false;
-    for (int j = 0; j < TD_POS; ++j) out[j] |= got[j];
-  }
+  if (zkeys && td_cnt<M, NP>(out, ~(M)0) != num_cpus) return false;
   if (required) {   // satisfiedRequiredCPUBindPolicy (:568-589)
-    const int nc = td_pc(td_any(out)), ncpus = td_cnt(out, ~0ull);
+    const int nc = td_pc(td_any<M, NP>(out)), ncpus = td_cnt<M, NP>(out, ~(M)0);
     if (bind == GS_CPU_BIND_FULL_PCPUS && nc * TU32(t.cpc) != ncpus) return false;
     if (bind == GS_CPU_BIND_SPREAD_BY_PCPUS && nc != ncpus) return false;
   }
+  td_pack<M, NP>(out, out_w);
   return true;
 }
 
-// available-CPU counts of the cores `m` (raw | full-core CPUs << 9 | cores with a free CPU << 18), packed
-// as gs_numa_host.cpp count_available
-GS_HD int32_t td_counts(const TopoDev& t, const CpuStateDev& cs, uint64_t m) {
-  uint64_t P[TD_POS];
-  td_available(t, cs, P);
-  for (int j = 0; j < TD_POS; ++j) P[j] &= m;
-  const int raw = td_cnt(P, ~0ull);
-  const int full = TU32(t.cpc) * td_pc(td_exactly(P, TU32(t.cpc)) & td_any(P));
-  const int spread = td_pc(td_any(P));
+// NodeAllocation.addPodAllocation (node_allocation.go:77-96) of the cpuset R (packed words) with exclusive policy ep
+// on the CPU state: RefCount + 1 on every CPU of R (maxRefCount 1: they leave the available set; 2: those already at
+// RefCount 1 do, the others move to RefCount 1), the exclusive cores / NUMA nodes, the allocated CPUs per zone slot
+// (nz slots). Every CPU of R takes ep as its ExclusivePolicy; when a CPU already allocated is shared on a node with
+// exclusive CPUs, the policy it loses is not known here, and xc / xn are marked stale (CM_XSTALE: a later pod whose
+// selection reads them leaves the device path). Returns the number of newly allocated CPUs (RefCount 0 -> 1).
+template <class M, int NP>
+GS_HD int td_reserve_update_t(const TopoDev& t, CpuStateDev& cs, const uint64_t* R_w, int ep, int nz) {
+  M U[NP], RC[NP], R[NP], NEW[NP];
+  td_unpack<M, NP>(cs.un, U);
+  td_unpack<M, NP>(cs.rc, RC);
+  td_unpack<M, NP>(R_w, R);
+  uint32_t meta = TUU(cs.meta);
+  const bool mr2 = meta & CM_MR2;
+  M shared = 0;
+#pragma unroll
+  for (int j = 0; j < NP; ++j) {
+    NEW[j] = R[j] & ~RC[j];
+    shared |= R[j] & RC[j];
+    if (mr2) {
+      U[j] |= R[j] & RC[j];
+      RC[j] ^= R[j];
+    } else {
+      U[j] |= R[j];
+    }
+  }
+  M xc = td_xc<M>(cs);
+  if (shared && (xc || (meta & CM_XN_MASK))) meta |= CM_XSTALE;
+  const M cores = td_any<M, NP>(R);
+  if (ep == GS_CPU_EXCLUSIVE_PCPU_LEVEL) xc |= cores;
+  else if (ep == GS_CPU_EXCLUSIVE_NUMA_NODE_LEVEL)
+    for (M b = cores; b; b &= b - 1) meta |= 1u << TU32(t.core_node[td_ctz(b)]);
+  uint64_t zal = TU64(cs.zal);
+  for (int z = 0; z < 4; ++z) {
+    const int n = td_zone_node(cs, z);
+    if (z >= nz || n >= TU32(t.nnodes)) continue;   // a zone the topology lacks keeps its zero summaries
+    const uint64_t zc = ((zal >> (16 * z)) & 0xFFFFull) + (uint64_t)td_cnt<M, NP>(NEW, td_tm<M>(t.node_cores[n]));
+    zal = (zal & ~(0xFFFFull << (16 * z))) | (zc << (16 * z));
+  }
+  td_pack<M, NP>(U, cs.un);
+  td_pack<M, NP>(RC, cs.rc);
+  const cm_t x128 = (cm_t)xc;
+  cs.xc = cm_lo(x128);
+  cs.xc1 = cm_hi(x128);
+  cs.zal = zal;
+  cs.meta = meta;
+  return td_cnt<M, NP>(NEW, ~(M)0);
+}
+
+// available-CPU counts of NUMA node index n (-1: every node): raw | full-core CPUs << 9 | cores with a free CPU
+// << 18, packed as gs_numa_host.cpp count_available
+template <class M, int NP> GS_HD int32_t td_counts_t(const TopoDev& t, const CpuStateDev& cs, int n) {
+  M P[NP];
+  td_available<M, NP>(t, cs, P);
+  const M m = n < 0 ? ~(M)0 : td_tm<M>(t.node_cores[n]);
+#pragma unroll
+  for (int j = 0; j < NP; ++j) P[j] &= m;
+  const int raw = td_cnt<M, NP>(P, ~(M)0);
+  const int full = TU32(t.cpc) * td_pc(td_exactly<M, NP>(P, TU32(t.cpc)) & td_any<M, NP>(P));
+  const int spread = td_pc(td_any<M, NP>(P));
   return (int32_t)(raw | (full << 9) | (spread << 18));
 }
 
-// the cpuset as a 256-bit CPU mask
-GS_HD void td_to_cpus(const TopoDev& t, const uint64_t* R, uint64_t* w) {
+// the cpuset (packed words) as a 256-bit CPU mask
+template <class M, int NP> GS_HD void td_to_cpus_t(const TopoDev& t, const uint64_t* R_w, uint64_t* w) {
+  M R[NP];
+  td_unpack<M, NP>(R_w, R);
   TdMask256 W;
 #pragma unroll
-  for (int j = 0; j < TD_POS; ++j)
-    for (uint64_t b = R[j]; b; b &= b - 1) W.set_bit(TU32(t.core_cpu[td_ctz(b)][j]));
+  for (int j = 0; j < NP; ++j)
+    for (M b = R[j]; b; b &= b - 1) W.set_bit(TU32(t.core_cpu[td_ctz(b)][j]));
   w[0] = W.w0; w[1] = W.w1; w[2] = W.w2; w[3] = W.w3;
+}
+
+// ---- the packed-word API: the shape is the topology's (TopoDev.wide)
+GS_HD bool td_allocate_cpuset(const TopoDev& t, const CpuStateDev& cs, int num_cpus, int bind, bool required, int ep,
+                              uint32_t zkeys, const int64_t* zcpu, uint64_t* out_w) {
+  return TU32(t.wide) ? td_allocate_cpuset_t<cm_t, 2>(t, cs, num_cpus, bind, required, ep, zkeys, zcpu, out_w)
+                      : td_allocate_cpuset_t<uint64_t, 4>(t, cs, num_cpus, bind, required, ep, zkeys, zcpu, out_w);
+}
+GS_HD int td_reserve_update(const TopoDev& t, CpuStateDev& cs, const uint64_t* R_w, int ep, int nz) {
+  return TU32(t.wide) ? td_reserve_update_t<cm_t, 2>(t, cs, R_w, ep, nz)
+                      : td_reserve_update_t<uint64_t, 4>(t, cs, R_w, ep, nz);
+}
+GS_HD int32_t td_counts(const TopoDev& t, const CpuStateDev& cs, int n) {
+  return TU32(t.wide) ? td_counts_t<cm_t, 2>(t, cs, n) : td_counts_t<uint64_t, 4>(t, cs, n);
+}
+GS_HD void td_to_cpus(const TopoDev& t, const uint64_t* R_w, uint64_t* w) {
+  if (TU32(t.wide)) td_to_cpus_t<cm_t, 2>(t, R_w, w);
+  else td_to_cpus_t<uint64_t, 4>(t, R_w, w);
+}
+// takeCPUs over the available CPUs of the state (the self-test's entry; the device selects through allocateCPUSet)
+GS_HD bool td_take_cpus(const TopoDev& t, const CpuStateDev& cs, int needed, int bind, int ep, bool most,
+                        uint64_t* out_w) {
+  for (int j = 0; j < 4; ++j) out_w[j] = 0;
+  if (TU32(t.wide)) {
+    cm_t P[2], RC[2], R[2];
+    td_available<cm_t, 2>(t, cs, P);
+    td_unpack<cm_t, 2>(cs.rc, RC);
+    if (!td_take_cpus_t<cm_t, 2>(t, P, RC, td_xc<cm_t>(cs), TUU(cs.meta) & CM_XN_MASK, needed, bind, ep, most, R))
+      return false;
+    td_pack<cm_t, 2>(R, out_w);
+  } else {
+    uint64_t P[4], RC[4], R[4];
+    td_available<uint64_t, 4>(t, cs, P);
+    td_unpack<uint64_t, 4>(cs.rc, RC);
+    if (!td_take_cpus_t<uint64_t, 4>(t, P, RC, td_xc<uint64_t>(cs), TUU(cs.meta) & CM_XN_MASK, needed, bind, ep,
+                                     most, R))
+      return false;
+    td_pack<uint64_t, 4>(R, out_w);
+  }
+  return true;
 }
 
 }  // namespace gs

@@ -358,6 +358,14 @@ __device__ __forceinline__ void wave_rank_sort(uint32_t* v, int n, uint32_t* tmp
   WAVE_FENCE();
 }
 
+// The device Reserve selects this pod's cpuset on this row: its topology is the staged one (in the device scope, so
+// topo >= 0), and the exclusivity state the selection reads is exact (an exclusive pod on a row marked CM_XSTALE —
+// a maxRefCount-2 node whose shared CPUs lost their policy — has its cpuset selected by the host).
+__device__ __forceinline__ bool cpuset_on_device(const CpuStateDev& cs, int staged_topo, const PodVec& p) {
+  const int ep = (p.numa & PN_BIND) ? (int)((p.numa >> PN_EXCL_SHIFT) & 3u) : GS_CPU_EXCLUSIVE_NONE;
+  return cs.topo >= 0 && cs.topo == staged_topo && !((cs.meta & CM_XSTALE) && ep != GS_CPU_EXCLUSIVE_NONE);
+}
+
 // Device-side cpuset Reserve of one pod on its winner row (one thread): allocateCPUSet with the NUMA split of
 // Allocate (resource_manager.go:273-360, gs_cpuset_dev.h), then NodeAllocation.addPodAllocation
 // (node_allocation.go:82-110) on the CPU state and the row's available-CPU summaries, as numa_derive
@@ -395,24 +403,17 @@ __device__ __noinline__ bool cpuset_reserve(const GS_LDS TopoDev* tp, GS_LDS Cpu
   else if (nb == GS_NODE_CPU_BIND_SPREAD_BY_PCPUS) { bind = BIND_SPREAD; required = true; }
   else if (nb == GS_NODE_CPU_BIND_FULL_PCPUS_ONLY) { bind = BIND_FULL; required = true; }
   const int ep = (pn & PN_BIND) ? (int)((pn >> PN_EXCL_SHIFT) & 3u) : GS_CPU_EXCLUSIVE_NONE;
-  uint64_t R[TD_POS];
+  uint64_t R[4];   // the cpuset, packed plane words
   if (!td_allocate_cpuset(t, cs, (int)u32((uint32_t)p.num_cpus), bind, required, ep, zkeys, zcpu, R)) return false;
-  const uint64_t cores = td_any(R);
-  for (int j = 0; j < TD_POS; ++j) cs.un[j] |= R[j];
-  if (ep == GS_CPU_EXCLUSIVE_PCPU_LEVEL) cs.xc |= cores;
-  else if (ep == GS_CPU_EXCLUSIVE_NUMA_NODE_LEVEL)
-    for (uint64_t b = cores; b; b &= b - 1) cs.meta |= 1u << TU32(t.core_node[td_ctz(b)]);
-  nr.alloc_cpus += td_cnt(R, ~0ull);
-  nr.tfree = (uint32_t)td_counts(t, cs, ~0ull);
   const int nz = (nf >> NF_ZONES_SHIFT) & 7;
+  nr.alloc_cpus += td_reserve_update(t, cs, R, ep, nz);
+  nr.tfree = (uint32_t)td_counts(t, cs, -1);
   for (int z = 0; z < 4; ++z) {
     const int n = td_zone_node(cs, z);
     if (z >= nz || n >= TU32(t.nnodes)) continue;   // a zone the topology lacks keeps its zero summaries
-    const uint64_t zc = ((TU64(cs.zal) >> (16 * z)) & 0xFFFFull) + (uint64_t)td_cnt(R, TU64(t.node_cores[n]));
-    cs.zal = (cs.zal & ~(0xFFFFull << (16 * z))) | (zc << (16 * z));
-    nr.zfree[z] = (uint32_t)td_counts(t, cs, TU64(t.node_cores[n]));
+    nr.zfree[z] = (uint32_t)td_counts(t, cs, n);
     if (nr.amp > 1.0) {
-      const int64_t c = (int64_t)zc * 1000;
+      const int64_t c = (int64_t)((TU64(cs.zal) >> (16 * z)) & 0xFFFFull) * 1000;
       nr.zadj[z] = (int32_t)(amplify_d(c, nr.amp) - c);
     }
   }

@@ -657,10 +657,11 @@ __global__ void __launch_bounds__(COMMIT_THREADS) commit_kernel(CommitArgs a) {
   else if (lane == ROW_I64 + 1) { f_kind = 2; f_src = a.m.c32(C_DFLAGS); f_off = offsetof(Row, dflags); f_size = 4; }
   else if (lane == ROW_I64 + 2) { f_kind = 4; f_off = offsetof(Row, node); }
   else if (numa_on) {
-    if (lane >= 20 && lane < 26) { f_kind = 1; f_src = a.m.c64(C_CPU_UN0 + (lane - 20)); f_region = 1; f_off = (lane - 20) * 8; }
-    else if (lane == 26) { f_kind = 2; f_src = a.m.c32(C_CPU_META); f_region = 1; f_off = offsetof(CpuStateDev, meta); f_size = 4; }
-    else if (lane == 27) { f_kind = 2; f_src = a.m.c32(C_TOPO_DEV); f_region = 1; f_off = offsetof(CpuStateDev, topo); f_size = 4; }
-    else if (lane == 28) { f_kind = 3; f_src = a.aff; f_region = 2; f_size = 4; }
+    // CpuStateDev's 11 words (C_CPU_UN0 .. C_CPU_XC1), meta, topo; lanes 32..61 the NUMA row
+    if (lane >= 20 && lane < 31) { f_kind = 1; f_src = a.m.c64(C_CPU_UN0 + (lane - 20)); f_region = 1; f_off = (lane - 20) * 8; }
+    else if (lane == 31) { f_kind = 2; f_src = a.m.c32(C_CPU_META); f_region = 1; f_off = offsetof(CpuStateDev, meta); f_size = 4; }
+    else if (lane == 62) { f_kind = 2; f_src = a.m.c32(C_TOPO_DEV); f_region = 1; f_off = offsetof(CpuStateDev, topo); f_size = 4; }
+    else if (lane == 63) { f_kind = 3; f_src = a.aff; f_region = 2; f_size = 4; }
     else if (lane >= 32 && lane < 32 + NUMA_I64) {
       f_kind = 1; f_src = a.m.c64(C_ZCAP_CPU0 + (lane - 32)); f_off = offsetof(Row, nr) + (lane - 32) * 8;
     } else if (lane >= 50 && lane < 50 + NUMA_I32) {
@@ -1179,7 +1180,7 @@ __global__ void __launch_bounds__(COMMIT_THREADS) commit_kernel(CommitArgs a) {
           }
           if (rb) {
             CpuStateDev& cs = cst[slot];
-            if (cs.topo >= 0 && cs.topo == s_topo_id) {
+            if (cpuset_on_device(cs, s_topo_id, pk)) {
               if (cpuset_reserve((const GS_LDS TopoDev*)&s_topo, (GS_LDS CpuStateDev*)&cs, pk, nf, no.zkeys, no.zcpu[0],
                                  no.zcpu[1], no.zcpu[2], no.zcpu[3],
                                  (GS_LDS NumaRow*)&d.nr, (GS_LDS uint64_t*)s_cpuset)) {
@@ -1274,8 +1275,8 @@ __global__ void __launch_bounds__(COMMIT_THREADS) commit_kernel(CommitArgs a) {
     if (row_word_mutable(j)) m.c64(kRowCol[j])[drows[s].node] = reinterpret_cast<const int64_t*>(&drows[s])[j];
   }
   for (int s = tid; s < nd; s += COMMIT_THREADS) m.c32(C_FREE_PODS)[drows[s].node] = drows[s].free_pods;
-  // NUMA words Reserve changes: ZRAW (8 i64), NFLAGS2 .. ZADJ3 (11 i32), CPU state (6 i64 + meta)
-  constexpr int NW = 8 + 11 + 6 + 1;
+  // NUMA words Reserve changes: ZRAW (8 i64), NFLAGS2 .. ZADJ3 (11 i32), CPU state (11 i64 + meta)
+  constexpr int NW = 8 + 11 + 11 + 1;
   static_assert(C_ZADJ0 + 3 - C_NFLAGS2 + 1 == 11, "NUMA i32 write-back columns contiguous");
   if (numa_on)
     for (int e = tid; e < nd * NW; e += COMMIT_THREADS) {
@@ -1283,7 +1284,7 @@ __global__ void __launch_bounds__(COMMIT_THREADS) commit_kernel(CommitArgs a) {
       const uint32_t node = drows[sl].node;
       if (j < 8) m.c64(C_ZRAW_CPU0 + j)[node] = (&drows[sl].nr.zraw_cpu[0])[j];
       else if (j < 19) m.c32(C_NFLAGS2 + (j - 8))[node] = reinterpret_cast<const int32_t*>(&drows[sl].nr.nflags2)[j - 8];
-      else if (j < 25) m.c64(C_CPU_UN0 + (j - 19))[node] = reinterpret_cast<const int64_t*>(&cst[sl])[j - 19];
+      else if (j < 30) m.c64(C_CPU_UN0 + (j - 19))[node] = reinterpret_cast<const int64_t*>(&cst[sl])[j - 19];
       else m.c32(C_CPU_META)[node] = (int32_t)cst[sl].meta;
     }
   if (tid == 0) {

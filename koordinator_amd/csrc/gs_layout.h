@@ -42,9 +42,12 @@ enum I64Col : int {
   C_AMP = C_ZRAW_MEM0 + 4,         // options.AmplificationRatios[cpu] (f64 bits)
   C_NAMP,                          // node annotation cpu amplification ratio (f64 bits; -1 unset)
   // device-side cpuset Reserve state (gs_cpuset_dev.h CpuStateDev; read by the commit kernel only)
-  C_CPU_UN0,                       // 4 planes: CPUs not available (allocated or reserved) per core rank
-  C_CPU_XC = C_CPU_UN0 + 4,        // cores holding a PCPULevel-exclusive allocated CPU
+  // (the 11 columns C_CPU_UN0 .. C_CPU_XC1 are CpuStateDev's first 11 words, in order)
+  C_CPU_UN0,                       // 4 packed plane words: CPUs not available (RefCount >= maxRefCount, or reserved)
+  C_CPU_XC = C_CPU_UN0 + 4,        // cores holding a PCPULevel-exclusive allocated CPU (ranks 0..63)
   C_CPU_ZAL,                       // allocated CPUs per zone slot (4 x 16 bits)
+  C_CPU_RC0,                       // 4 packed plane words: available CPUs at RefCount 1 (maxRefCount 2)
+  C_CPU_XC1 = C_CPU_RC0 + 4,       // C_CPU_XC, ranks 64..127
   NUM_I64_COLS
 };
 

@@ -4,7 +4,9 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstddef>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <set>
 
@@ -347,6 +349,7 @@ void make_topo_dev(const TopoClass& t, TopoDev* d) {
   uniq(socks);
   if ((int)cores.size() > TD_CORES || (int)nodes.size() > TD_NODES || (int)socks.size() > TD_SOCKETS) return;
   if (t.cpc < 1 || t.cpc > TD_POS || (int)nodes.size() != t.num_nodes) return;   // a NUMA node id in two sockets
+  const bool wide = cores.size() > 64;
   auto idx = [](const std::vector<int>& v, int x) { return (int)(std::lower_bound(v.begin(), v.end(), x) - v.begin()); };
   int core_sock[TD_CORES], core_node[TD_CORES], node_sock[TD_NODES], npos[TD_CORES] = {0};
   std::fill(core_sock, core_sock + TD_CORES, -1);
@@ -355,6 +358,7 @@ void make_topo_dev(const TopoClass& t, TopoDev* d) {
   std::memset(d->core_cpu, 0xff, sizeof(d->core_cpu));
   std::memset(d->cpu_core, 0xff, sizeof(d->cpu_core));
   std::memset(d->cpu_pos, 0xff, sizeof(d->cpu_pos));
+  cm_t node_m[TD_NODES] = {}, sock_m[TD_SOCKETS] = {}, pos_m[TD_POS] = {};
   for (int c = 0; c < t.num_cpus; ++c) {   // ascending CPU id: position j = rank of the CPU inside its core
     const int k = idx(cores, t.core[c]), n = idx(nodes, t.node[c]), s = idx(socks, t.socket[c]);
     if ((core_sock[k] >= 0 && core_sock[k] != s) || (core_node[k] >= 0 && core_node[k] != n) ||
@@ -364,16 +368,21 @@ void make_topo_dev(const TopoClass& t, TopoDev* d) {
     core_node[k] = n;
     node_sock[n] = s;
     const int j = npos[k]++;
-    if (j >= TD_POS) { std::memset(d, 0, sizeof(*d)); return; }
-    const uint64_t b = 1ull << k;
+    // beyond 64 cores the 256 bits of a plane set hold two planes of 128 cores: <= 2 CPUs per core
+    if (j >= TD_POS || (wide && j >= 2)) { std::memset(d, 0, sizeof(*d)); return; }
+    const cm_t b = (cm_t)1 << k;
     d->core_cpu[k][j] = (uint8_t)c;
     d->cpu_core[c] = (uint8_t)k;
     d->cpu_pos[c] = (uint8_t)j;
-    d->pos_cores[j] |= b;
-    d->node_cores[n] |= b;
-    d->sock_cores[s] |= b;
+    pos_m[j] |= b;
+    node_m[n] |= b;
+    sock_m[s] |= b;
     d->core_node[k] = (uint8_t)n;
   }
+  auto put = [](uint64_t* w, cm_t m) { w[0] = cm_lo(m); w[1] = cm_hi(m); };
+  for (int n = 0; n < TD_NODES; ++n) put(d->node_cores[n], node_m[n]);
+  for (int s = 0; s < TD_SOCKETS; ++s) put(d->sock_cores[s], sock_m[s]);
+  for (int j = 0; j < TD_POS; ++j) put(d->pos_cores[j], pos_m[j]);
   for (int n = 0; n < (int)nodes.size(); ++n) d->node_sock[n] = (uint8_t)node_sock[n];
   d->num_cpus = t.num_cpus;
   d->ncores = (int)cores.size();
@@ -382,6 +391,7 @@ void make_topo_dev(const TopoClass& t, TopoDev* d) {
   d->cpc = t.cpc;
   d->cpn = t.cpn;
   d->cps = t.cps;
+  d->wide = wide ? 1 : 0;
   d->ok = 1;
 }
 
@@ -394,6 +404,9 @@ int dev_node_index(const TopoClass& t, int node_id) {
 
 }  // namespace
 
+static_assert(C_CPU_XC1 - C_CPU_UN0 == 10 && offsetof(CpuStateDev, xc1) == 80 && offsetof(CpuStateDev, rc) == 48,
+              "the CPU state columns are CpuStateDev's first 11 words");
+
 void numa_cpu_state(const NumaNode& n, bool default_most, CpuStateDev* cs) {
   std::memset(cs, 0, sizeof(*cs));
   cs->topo = -1;
@@ -401,10 +414,18 @@ void numa_cpu_state(const NumaNode& n, bool default_most, CpuStateDev* cs) {
   if (!t || !t->dev.ok) return;
   const TopoDev& d = t->dev;
   const int mr = n.max_ref();
+  // the plane sets as CPU-indexed packed words: word / bit of CPU (core rank k, position j)
+  auto set_cpu = [&](uint64_t* w, int c) {
+    const int k = d.cpu_core[c], j = d.cpu_pos[c];
+    const int bit = d.wide ? j * 128 + k : j * 64 + k;
+    w[bit >> 6] |= 1ull << (bit & 63);
+  };
+  cm_t xc = 0;
   for (int c = 0; c < t->num_cpus; ++c) {   // getAvailableCPUs (node_allocation.go:142-162)
     const bool taken = n.ref[c] > 0 && n.ref[c] >= mr;
     const bool reserved = (n.cfg.reserved_cpus[c >> 6] >> (c & 63)) & 1;
-    if (taken || reserved) cs->un[d.cpu_pos[c]] |= 1ull << d.cpu_core[c];
+    if (taken || reserved) set_cpu(cs->un, c);
+    else if (mr == 2 && n.ref[c] == 1) set_cpu(cs->rc, c);   // the accumulator's RefCount
   }
   // exclusiveInCores / exclusiveInNUMANodes of newCPUAccumulator (cpu_accumulator.go:256-264): the CoreID /
   // NodeID of every allocated CPU (zero values for CPUs outside the topology)
@@ -414,12 +435,14 @@ void numa_cpu_state(const NumaNode& n, bool default_most, CpuStateDev* cs) {
     const int core = c < t->num_cpus ? t->core[c] : 0, node = c < t->num_cpus ? t->node[c] : 0;
     if (n.excl[c] == GS_CPU_EXCLUSIVE_PCPU_LEVEL) {
       for (int c2 = 0; c2 < t->num_cpus; ++c2)
-        if (t->core[c2] == core) { cs->xc |= 1ull << d.cpu_core[c2]; break; }
+        if (t->core[c2] == core) { xc |= (cm_t)1 << d.cpu_core[c2]; break; }
     } else if (n.excl[c] == GS_CPU_EXCLUSIVE_NUMA_NODE_LEVEL) {
       const int ni = dev_node_index(*t, node);
       if (ni < TD_NODES) xn |= 1u << ni;
     }
   }
+  cs->xc = cm_lo(xc);
+  cs->xc1 = cm_hi(xc);
   const int nz = n.cfg.has_options ? n.cfg.num_zones : 0;
   uint32_t zidx = 0;
   for (int z = 0; z < GS_MAX_NUMA; ++z) {
@@ -436,8 +459,9 @@ void numa_cpu_state(const NumaNode& n, bool default_most, CpuStateDev* cs) {
   }
   int strategy = n.cfg.numa_allocate_strategy;
   if (strategy == GS_NUMA_ALLOC_UNSET) strategy = default_most ? GS_NUMA_ALLOC_MOST_ALLOCATED : GS_NUMA_ALLOC_LEAST_ALLOCATED;
-  cs->meta = xn | (zidx << CM_ZIDX_SHIFT) | (strategy == GS_NUMA_ALLOC_MOST_ALLOCATED ? CM_MOST : 0u);
-  cs->topo = mr <= 1 ? n.cfg.topology : -1;
+  cs->meta = xn | (zidx << CM_ZIDX_SHIFT) | (strategy == GS_NUMA_ALLOC_MOST_ALLOCATED ? CM_MOST : 0u) |
+             (mr == 2 ? CM_MR2 : 0u);
+  cs->topo = mr <= 2 ? n.cfg.topology : -1;
 }
 
 bool take_cpus(const TopoClass& t, int max_ref, const CpuMask& available, const uint16_t* ref, const uint8_t* ex,
@@ -571,9 +595,7 @@ CpuMask numa_available(const NumaNode& n) {
 void numa_derive(const NumaNode& n, bool default_most, int64_t* i64, int64_t* i32) {
   CpuStateDev cs;
   numa_cpu_state(n, default_most, &cs);
-  for (int j = 0; j < TD_POS; ++j) i64[C_CPU_UN0 + j] = (int64_t)cs.un[j];
-  i64[C_CPU_XC] = (int64_t)cs.xc;
-  i64[C_CPU_ZAL] = (int64_t)cs.zal;
+  for (int j = 0; j < 11; ++j) i64[C_CPU_UN0 + j] = reinterpret_cast<const int64_t*>(&cs)[j];
   i32[C_CPU_META] = (int32_t)cs.meta;
   i32[C_TOPO_DEV] = cs.topo;
   const gs_node_numa& g = n.cfg;
@@ -672,9 +694,11 @@ bool numa_allocate_cpuset(const NumaNode& n, int num_cpus, int bind, bool requir
 
 // Self-test of the bit-plane cpuset selection (gs_cpuset_dev.h, the code the commit kernel runs) against the
 // host restatement on random compact topologies (core-major and sibling-interleaved CPU numbering, SMT 1/2/4,
-// 1-2 sockets x 1-4 NUMA nodes), random allocations / exclusivity / reservations and random requests
-// (bind and exclusive policies, strategies, NUMA splits). Returns the number of mismatches; `msg` describes
-// the first one. Test hook, not part of include/gpuscore.h.
+// 1-2 sockets x 1-4 NUMA nodes; a third of them wide: up to 128 cores of SMT 1/2), random allocations with
+// maxRefCount 1 or 2 (RefCounts 0-2), exclusivity and reservations, and random requests (bind and exclusive
+// policies, strategies, NUMA splits); after each selection the device state update (td_reserve_update) is compared
+// with the host's re-derivation of the node after addPodAllocation. Returns the number of mismatches; `msg`
+// describes the first one. Test hook, not part of include/gpuscore.h.
 extern "C" int gsx_cpuset_selftest(uint64_t seed, int iters, char* msg, size_t len) {
   using namespace gs;
   uint64_t s = seed;
@@ -694,7 +718,15 @@ extern "C" int gsx_cpuset_selftest(uint64_t seed, int iters, char* msg, size_t l
   };
   static const int kCpc[] = {1, 2, 2, 4};
   for (int it = 0; it < iters; ++it) {
-    const int sockets = 1 + rnd(2), nps = 1 + rnd(4), cores_pn = 1 + rnd(6), cpc = kCpc[rnd(4)];
+    const bool wide = rnd(3) == 0;
+    int sockets = 1 + rnd(2), nps = 1 + rnd(4), cores_pn = 1 + rnd(6), cpc = kCpc[rnd(4)];
+    if (wide) {   // 65-128 cores, SMT 1 / 2 (the C3 shapes: 2 sockets, 2 or 4 NUMA nodes, 32-128 cores)
+      sockets = 2;
+      nps = 1 + rnd(2);
+      cpc = 1 + rnd(2);
+      const int per = 128 / (sockets * nps);
+      cores_pn = per / 2 + 1 + rnd(per / 2);
+    }
     const bool interleave = rnd(2);
     const int ncores = sockets * nps * cores_pn;
     gs_cpu_topology in;
@@ -715,7 +747,8 @@ extern "C" int gsx_cpuset_selftest(uint64_t seed, int iters, char* msg, size_t l
     if (!t || !t->dev.ok) { report(it, "topology outside the device scope"); continue; }
     NumaNode n;
     n.cfg.has_options = 1;
-    n.cfg.max_ref_count = 1;
+    const int mr = 1 + rnd(2);
+    n.cfg.max_ref_count = mr;
     n.cfg.topology = 0;
     n.topo = t;
     const int nnodes = sockets * nps, nz = nnodes < GS_MAX_NUMA ? nnodes : GS_MAX_NUMA;
@@ -725,10 +758,11 @@ extern "C" int gsx_cpuset_selftest(uint64_t seed, int iters, char* msg, size_t l
       n.cfg.zones[z].mask = GS_USAGE_CPU | GS_USAGE_MEMORY;
     }
     const int density = 1 + rnd(4);
+    const bool some_excl = rnd(2);
     for (int c = 0; c < in.num_cpus; ++c) {
       if (rnd(density + 1) == 0) {
-        n.ref[c] = 1;
-        const int e = rnd(6);
+        n.ref[c] = (uint16_t)(1 + (mr == 2 ? rnd(2) : 0));
+        const int e = some_excl ? rnd(6) : 5;
         n.excl[c] = (uint8_t)(e == 0 ? GS_CPU_EXCLUSIVE_PCPU_LEVEL : e == 1 ? GS_CPU_EXCLUSIVE_NUMA_NODE_LEVEL
                                                                     : GS_CPU_EXCLUSIVE_NONE);
       }
@@ -743,20 +777,26 @@ extern "C" int gsx_cpuset_selftest(uint64_t seed, int iters, char* msg, size_t l
     if (cs.topo != 0) { report(it, "cpu state not device-eligible"); continue; }
     const CpuMask avail = numa_available(n);
     const int na = avail.count();
-    const int needed = 1 + rnd(std::max(1, std::min(na + 2, 24)));
+    const int needed = 1 + rnd(std::max(1, std::min(na + 2, 48)));
     const int bind = rnd(4), ep = rnd(3);
+    const char* shape = wide ? "wide" : "compact";
     // takeCPUs over the whole available set
     CpuMask h;
-    const bool hok = take_cpus(*t, 1, avail, n.ref, n.excl, needed, bind, ep, strategy, &h);
-    uint64_t P[TD_POS], R[TD_POS], w[4];
-    td_available(t->dev, cs, P);
-    const bool dok = td_take_cpus(t->dev, P, cs.xc, cs.meta & CM_XN_MASK, needed, bind, ep,
-                                  strategy == GS_NUMA_ALLOC_MOST_ALLOCATED, R);
+    const bool hok = take_cpus(*t, mr, avail, n.ref, n.excl, needed, bind, ep, strategy, &h);
+    uint64_t R[4], w[4];
+    const bool dok = td_take_cpus(t->dev, cs, needed, bind, ep, strategy == GS_NUMA_ALLOC_MOST_ALLOCATED, R);
     td_to_cpus(t->dev, R, w);
     if (hok != dok || (hok && std::memcmp(w, h.w, sizeof(w)) != 0)) {
-      char b[256];
+      char b[400];
       snprintf(b, sizeof b, "takeCPUs differs (host ok=%d dev ok=%d, need %d bind %d excl %d strategy %d, cpc %d, "
-               "interleave %d)", hok, dok, needed, bind, ep, strategy, cpc, interleave);
+               "interleave %d, %s, %d cores, maxRefCount %d) host %llx %llx dev %llx %llx", hok, dok, needed, bind, ep,
+               strategy, cpc, interleave, shape, ncores, mr, (unsigned long long)h.w[0], (unsigned long long)h.w[1],
+               (unsigned long long)w[0], (unsigned long long)w[1]);
+      if (getenv("GSX_SELFTEST_DUMP")) {
+        fprintf(stderr, "cpu core node ref excl avail:\n");
+        for (int c = 0; c < in.num_cpus; ++c)
+          fprintf(stderr, "  %d %d %d %d %d %d\n", c, in.core_id[c], in.node_id[c], n.ref[c], n.excl[c], avail.has(c));
+      }
       report(it, b);
       continue;
     }
@@ -783,11 +823,12 @@ extern "C" int gsx_cpuset_selftest(uint64_t seed, int iters, char* msg, size_t l
     if (hok2 != dok2 || (hok2 && std::memcmp(w, h2.w, sizeof(w)) != 0)) {
       char b[256];
       snprintf(b, sizeof b, "allocateCPUSet differs (host ok=%d dev ok=%d, need %d bind %d required %d excl %d, "
-               "%zu zones)", hok2, dok2, needed, bind, required, ep, split.size());
+               "%zu zones, %s, %d cores, maxRefCount %d)", hok2, dok2, needed, bind, required, ep, split.size(), shape,
+               ncores, mr);
       report(it, b);
       continue;
     }
-    // post-Reserve counts (the columns the commit kernel recomputes)
+    // the device state update against the host's re-derivation after addPodAllocation
     if (hok2) {
       PodAllocRec rec;
       rec.uid = 1;
@@ -796,13 +837,23 @@ extern "C" int gsx_cpuset_selftest(uint64_t seed, int iters, char* msg, size_t l
       NumaNode n2 = n;
       numa_add(n2, rec);
       CpuStateDev cs2 = cs, want;
-      for (int j = 0; j < TD_POS; ++j) cs2.un[j] |= R[j];
+      const int added = td_reserve_update(t->dev, cs2, R, ep, nz);
       numa_cpu_state(n2, dmost, &want);
       int64_t i64[NUM_I64_COLS] = {0}, i32[NUM_I32_COLS] = {0};
       numa_derive(n2, dmost, i64, i32);
-      if (td_counts(t->dev, cs2, ~0ull) != (int32_t)i32[C_TFREE] ||
-          std::memcmp(cs2.un, want.un, sizeof(want.un)) != 0) {
-        report(it, "post-Reserve availability counts differ");
+      int64_t b64[NUM_I64_COLS] = {0}, b32[NUM_I32_COLS] = {0};
+      numa_derive(n, dmost, b64, b32);
+      const bool stale = cs2.meta & CM_XSTALE;
+      const bool same_x = stale || (cs2.xc == want.xc && cs2.xc1 == want.xc1 &&
+                                    (cs2.meta & CM_XN_MASK) == (want.meta & CM_XN_MASK));
+      if (td_counts(t->dev, cs2, -1) != (int32_t)i32[C_TFREE] ||
+          std::memcmp(cs2.un, want.un, sizeof(want.un)) != 0 || std::memcmp(cs2.rc, want.rc, sizeof(want.rc)) != 0 ||
+          cs2.zal != want.zal || !same_x || added != (int)(i32[C_ALLOC_CPUS] - b32[C_ALLOC_CPUS]) ||
+          (cs2.meta & ~(CM_XN_MASK | CM_XSTALE)) != (want.meta & ~CM_XN_MASK)) {
+        char b[200];
+        snprintf(b, sizeof b, "post-Reserve CPU state differs (%s, %d cores, maxRefCount %d, excl %d)", shape, ncores,
+                 mr, ep);
+        report(it, b);
         continue;
       }
     }

@@ -206,18 +206,27 @@ def make_cluster(num_nodes: int, num_pods: int, config_id: int = 1, seed: int | 
 def make_numa(c: Cluster, seed: int | None = None, numa_policy_pct: int = 30, cpuset_pod_pct: int = 20,
               mixed: bool = False) -> Cluster:
     """Adds the C3 NodeNUMAResource state to a cluster, in place:
-    2 sockets, k in {2, 4} NUMA nodes, SMT2 (logical CPUs = allocatable cores, <= 128); NRT zones split cpu and
-    memory evenly; `numa_policy_pct`% of nodes labelled numa-topology-policy in {SingleNUMANode, Restricted,
+    2 sockets, k in {2, 4} NUMA nodes, 32-128 physical cores (the cluster's cores draw) with SMT2, i.e. 64-256 logical
+    CPUs: the node's CPU quantities (allocatable = the logical CPUs, as the kubelet reports them, requested,
+    non-zero requested, raw allocatable, NodeMetric usage) are doubled so their utilisation is unchanged; NRT zones
+    split cpu and memory evenly; `numa_policy_pct`% of nodes labelled numa-topology-policy in {SingleNUMANode, Restricted,
     BestEffort}; 3% node cpu-bind-policy FullPCPUsOnly, 2% SpreadByPCPUs; 4% cpu amplification 1.5; existing
     cpuset pods on 25% of nodes and NUMA allocations on labelled nodes; `cpuset_pod_pct`% of pending pods LSR/LSE
     Prod with integer CPUs (some with a required bind policy).
-    mixed: also sibling-interleaved CPU numbering (cpu = thread * cores + core), SMT-4 and SMT-1 classes (128
-    SMT-1 cores exceed the device cpuset scope), maxRefCount 2 on 3% of nodes, PCPU- and NUMANode-level
+    mixed: also sibling-interleaved CPU numbering (cpu = thread * cores + core), SMT-4 and SMT-1 classes (256 SMT-1
+    cores exceed the device cpuset scope), maxRefCount 2 on 3% of nodes, PCPU- and NUMANode-level
     exclusive existing allocations and pods."""
     from . import numa as nm
     s = Stream((BASE_SEED + 77) if seed is None else seed)
     N = c.num_nodes
-    cores = c.nodes["allocatable"][:, 0] // 1000
+    # SMT2: the logical CPUs are twice the physical cores
+    zero_nz = c.nodes["nonzero_requested"][:, 0] - c.nodes["requested"][:, 0]
+    c.nodes["allocatable"][:, 0] *= 2
+    c.nodes["requested"][:, 0] *= 2
+    c.nodes["nonzero_requested"][:, 0] = c.nodes["requested"][:, 0] + zero_nz
+    c.nodes["raw_allocatable"][:, 0] *= 2
+    c.metrics["node_usage"]["cpu_milli"] *= 2
+    cores = c.nodes["allocatable"][:, 0] // 1000   # logical CPUs
     k = np.where(s.randint(300, N, 0, 1) == 0, 2, 4)
     # topology classes by (cores, k)
     classes, tid_of = {}, np.zeros(N, np.int32)
@@ -231,7 +240,8 @@ def make_numa(c: Cluster, seed: int | None = None, numa_policy_pct: int = 30, cp
         per_socket = kk // 2
         smt, interleave = 2, False
         if mixed:
-            smt = 4 if ci % 5 == 2 else (1 if ci % 7 == 3 else 2)
+            # (256 logical CPUs as SMT-1 cores: outside the device cpuset scope, the host path)
+            smt = 4 if ci % 5 == 2 else (1 if (ci % 7 == 3 or (nc == 256 and kk == 2)) else 2)
             interleave = ci % 3 == 1
         cores_per_numa = nc // smt // kk
         ncores = 2 * per_socket * cores_per_numa

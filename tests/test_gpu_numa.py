@@ -108,8 +108,8 @@ def test_numa_schedule_dense_policies_and_cpusets():
 
 @pytest.mark.parametrize("batch", [16, 128])
 def test_numa_schedule_mixed_topologies(batch):
-    """Sibling-interleaved CPU numbering, SMT 4, 128-core SMT-1 nodes (outside the device cpuset scope: host
-    takeCPUs and a batch cut), maxRefCount 2 nodes (host path too), PCPU- and NUMANode-level exclusivity."""
+    """Sibling-interleaved CPU numbering, SMT 4, 256-core SMT-1 nodes (outside the device cpuset scope: host
+    takeCPUs and a batch cut), maxRefCount 2 nodes (device RefCount ordering), PCPU- and NUMANode-level exclusivity."""
     c = synth.make_cluster(1500, 300, 7)
     synth.make_numa(c, numa_policy_pct=40, cpuset_pod_pct=60, mixed=True)
     e, o = numa_pair(c, batch_size=batch)
