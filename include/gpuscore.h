@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define GS_ABI_VERSION 4u
+#define GS_ABI_VERSION 5u
 
 /* ---- resource slots (corev1.ResourceName restricted to the hot-path set) ---- */
 enum gs_resource {
@@ -352,6 +352,8 @@ typedef struct gs_stats {
   uint32_t shard_begin, shard_end; /* this rank's node range */
   uint32_t next_start_node_index;  /* [upstream] Scheduler.nextStartNodeIndex after the last scheduled pod */
   uint32_t pad0;
+  uint64_t delta_rows;       /* mirror rows re-derived and copied host -> HBM (incremental snapshot updates) */
+  uint64_t delta_bytes;      /* their host -> device bytes (row index + staged row) */
 } gs_stats;
 
 /* v1beta2.SetDefaults_LoadAwareSchedulingArgs (pkg/scheduler/apis/config/v1beta2/defaults.go:76-99) */
@@ -843,6 +845,39 @@ int gs_gang_waiting_pods(const gs_gang_mgr* m, uint64_t* uids, uint32_t cap, uin
 /* Test hook (the reference's tests set gang fields directly): what 0 ScheduleCycleValid, 1 the pod's schedule cycle,
  * 2 OnceResourceSatisfied, 3 GangMatchPolicy (3: a value outside the three), 4 SkipCheckScheduleCycle. */
 int gs_gang_debug_set(gs_gang_mgr* m, uint64_t gang_id, uint64_t uid, int what, int value);
+
+/* Coscheduling around the batched node loop, natively (the per-pod gate loop of koordinator_amd/gang.py
+ * schedule_with_gangs): the reference runs PreFilter -> node loop -> Reserve -> Permit (PostFilter after a failure,
+ * the Unreserve chain of rejected waiting pods) one pod at a time; a pass runs the gang side of that order over a
+ * queue of n pods between the caller's engine calls.
+ *  - gs_gang_walk: from pod i, the speculative walk (snapshot of the gang state taken first): every pod whose PreFilter
+ *    passes is assumed to find a node and joins the run (run[], *run_n); the walk stops after run_cap pods, after a
+ *    PreFilter failure whose PostFilter rejects waiting pods, or after a Permit "Gang not found"; *j = the pod after it.
+ *  - the caller schedules the run's pods in one engine call (gs_schedule) -> got_node[run_n];
+ *  - gs_gang_replay: restores the snapshot and replays [i, j) pod by pod with the true nodes (PreFilter, PostFilter,
+ *    Reserve -> Permit, PostBind of the pods Permit allows, Unreserve chains), checking the walk: it stops at the first
+ *    pod whose real PreFilter verdict differs from the walk's or whose transitions forget an assumed pod. *r_stop: the
+ *    run positions kept (the caller withdraws the run's later placements with gs_pods_forget), *j_next: the next pod;
+ *    *single >= 0: that pod passes PreFilter where the walk assumed not — the caller schedules it alone and reports its
+ *    node with gs_gang_pass_after_single.
+ * Per-pod results go to the pass's arrays (PreFilter code, Permit status or -1, GS_GANG_ST_*, node); the pods the
+ * Unreserve chains reject are listed for ForgetPod (gs_gang_pass_forgets: uids in rejection order, this queue's pods
+ * and pods waiting from earlier passes), and state changes of pods waiting from earlier passes are listed too
+ * (gs_gang_pass_carried). Restatement: oracle/coscheduling.py schedule_sequential. */
+enum { GS_GANG_ST_UNSCHEDULABLE = 0, GS_GANG_ST_WAITING = 1, GS_GANG_ST_BOUND = 2, GS_GANG_ST_REJECTED = 3 };
+typedef struct gs_gang_pass gs_gang_pass;
+int gs_gang_pass_create(gs_gang_mgr* m, uint32_t n, const uint64_t* gang_ids, const uint64_t* uids,
+                        const uint8_t* nominated, int64_t now_ns, int8_t* prefilter, int8_t* permit, int8_t* state,
+                        int32_t* node, gs_gang_pass** out);
+int gs_gang_pass_destroy(gs_gang_pass* p);
+int gs_gang_walk(gs_gang_pass* p, uint32_t i, uint32_t run_cap, uint32_t* run, uint32_t* run_n, uint32_t* j);
+int gs_gang_replay(gs_gang_pass* p, uint32_t i, uint32_t j, const uint32_t* run, uint32_t run_n,
+                   const int32_t* got_node, uint32_t* r_stop, uint32_t* j_next, int32_t* single);
+int gs_gang_pass_after_single(gs_gang_pass* p, uint32_t k, int32_t node);
+/* the rejected pods to forget since the last call (uids; cleared by the call), and the new states of pods waiting
+ * from earlier passes (uid, GS_GANG_ST_*; cumulative over the pass) */
+int gs_gang_pass_forgets(gs_gang_pass* p, uint64_t* uids, uint32_t cap, uint32_t* n);
+int gs_gang_pass_carried(gs_gang_pass* p, uint64_t* uids, int8_t* states, uint32_t cap, uint32_t* n);
 
 /* sizeof() of the ABI structs as compiled into the library, in this order: gs_pod, gs_node,
  * gs_node_metric, gs_pod_metric, gs_config, gs_placement, gs_stats, gs_loadaware_args, gs_cpu_topology,

@@ -10,7 +10,7 @@ import os
 
 import numpy as np
 
-GS_ABI_VERSION = 4
+GS_ABI_VERSION = 5
 GS_NUM_RES = 8
 GS_RES_CPU, GS_RES_MEMORY, GS_RES_EPHEMERAL = 0, 1, 2
 GS_RES_BATCH_CPU, GS_RES_BATCH_MEMORY, GS_RES_MID_CPU, GS_RES_MID_MEMORY = 3, 4, 5, 6
@@ -182,7 +182,7 @@ class GsStats(C.Structure):
         ("eval_launches", u64), ("eval_pairs", u64),
         ("eval_ms", C.c_double), ("cand_ms", C.c_double), ("commit_ms", C.c_double), ("exchange_ms", C.c_double),
         ("node_row_bytes", u64), ("shard_begin", u32), ("shard_end", u32),
-        ("next_start_node_index", u32), ("pad0", u32),
+        ("next_start_node_index", u32), ("pad0", u32), ("delta_rows", u64), ("delta_bytes", u64),
     ]
 
 
@@ -363,6 +363,13 @@ SIGNATURES = {
     "gs_gang_child_cycle": (C.c_int, [P, u64, u64]),
     "gs_gang_waiting_pods": (C.c_int, [P, P, u32, C.POINTER(u32)]),
     "gs_gang_debug_set": (C.c_int, [P, u64, u64, C.c_int, C.c_int]),
+    "gs_gang_pass_create": (C.c_int, [P, u32, P, P, P, i64, P, P, P, P, C.POINTER(P)]),
+    "gs_gang_pass_destroy": (C.c_int, [P]),
+    "gs_gang_walk": (C.c_int, [P, u32, u32, P, C.POINTER(u32), C.POINTER(u32)]),
+    "gs_gang_replay": (C.c_int, [P, u32, u32, P, u32, P, C.POINTER(u32), C.POINTER(u32), C.POINTER(i32)]),
+    "gs_gang_pass_after_single": (C.c_int, [P, u32, i32]),
+    "gs_gang_pass_forgets": (C.c_int, [P, P, u32, C.POINTER(u32)]),
+    "gs_gang_pass_carried": (C.c_int, [P, P, P, u32, C.POINTER(u32)]),
     "gs_reason_string": (C.c_int, [C.c_uint32, C.c_uint32, P, C.c_char_p, C.c_size_t]),
     "gs_reset": (C.c_int, [P]),
     "gs_abi_sizes": (None, [C.POINTER(u64), u32]),

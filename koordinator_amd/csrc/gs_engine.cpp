@@ -94,6 +94,7 @@ struct AsyncQueue {
 
 
 struct gs_ctx {
+  std::unordered_set<uint64_t> ext_reserved;   // pods placed with an extension-path Reserve (gs_schedule_ext)
   gs_config cfg{};
   std::string err;
   std::unique_ptr<AsyncQueue> aq;   // gs_schedule_submit's worker (created by the first submission)
@@ -650,6 +651,8 @@ int flush_rows(gs_ctx* c) {
     HIP_TRY(c, hipMemcpyAsync(c->d_stage_idx, c->h_stage_idx, n * 4, hipMemcpyHostToDevice, c->st));
     HIP_TRY(c, hipMemcpyAsync(c->d_stage_rows, c->h_stage_rows, (size_t)n * ROW_WORDS * 8, hipMemcpyHostToDevice, c->st));
     HIP_TRY(c, launch_scatter_rows(c->mv, c->d_stage_idx, c->d_stage_rows, n, c->st));
+    c->stats.delta_rows += n;
+    c->stats.delta_bytes += (uint64_t)n * (4 + ROW_WORDS * 8);
     done += n;
   }
   c->dirty_list.clear();
@@ -1490,6 +1493,8 @@ int ext_schedule_one(gs_ctx* c, const gs_pod& pod, const gs_pod_ext& e, uint64_t
     if (gpu_names_all >> n & 1u) { c->devs[node].requested[n] += e.gpu_requests[n]; dev_mark(c, node); }
   for (int x = 0; x < GS_MAX_XRES; ++x)         // ... and of the registered extended resources
     if (xres_all >> x & 1u) { c->devs[node].xres_requested[x] += e.xres_requests[x]; dev_mark(c, node); }
+  if (gmask || (rs_on && rec_i >= 0 && c->h_xnom[rec_i] >= 0) || gpu_names_all || xres_all)
+    c->ext_reserved.insert(pod.uid);   // gs_pods_forget cannot undo these Reserves
   apply_placement(c, pod, xo.node, true);
   return GS_OK;
 }
@@ -1910,8 +1915,14 @@ int gs_pods_unassign(gs_ctx* c, const uint32_t* node_idx, const gs_pod* pods, ui
 int gs_pods_forget(gs_ctx* c, const uint32_t* node_idx, const gs_pod* pods, uint32_t n) {
   if (!c || (n && (!node_idx || !pods))) return GS_EINVAL;
   quiesce(c);
-  for (uint32_t j = 0; j < n; ++j)
+  for (uint32_t j = 0; j < n; ++j) {
     if (node_idx[j] >= c->N) return fail(c, GS_EINVAL, "node index %u >= %u", node_idx[j], c->N);
+    // the extension path's Reserves (DeviceShare minors and GPU-name / extended-resource requests, Reservation
+    // AddAssignedPod) have no Unreserve here: refused before anything changes
+    if (c->ext_reserved.count(pods[j].uid))
+      return fail(c, GS_EUNSUPPORTED, "gs_pods_forget: pod %llu was placed with a DeviceShare / Reservation Reserve "
+                  "(gs_schedule_ext), whose Unreserve this library does not restate", (unsigned long long)pods[j].uid);
+  }
   for (uint32_t j = 0; j < n; ++j) {
     const uint32_t i = node_idx[j];
     const gs_pod& p = pods[j];

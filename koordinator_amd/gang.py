@@ -3,8 +3,9 @@ the PodGroupManager of pkg/scheduler/plugins/coscheduling/core/core.go) and `sch
 reference's per-pod order of PreFilter -> node loop -> Reserve -> Permit (PostFilter on a failure, Unreserve of rejected
 waiting pods) over batched gs_schedule calls.
 
-Batching is speculative, like the quota gate: the gang transitions of a run of pods are computed on the host assuming
-every pod that passes PreFilter finds a node; the engine then schedules the run's pods in one call. The gang state is
+Batching is speculative, like the quota gate: the gang transitions of a run of pods are computed in the library
+(gs_gang_walk) assuming every pod that passes PreFilter finds a node; the engine then schedules the run's pods in one
+call. The gang state is
 then restored from the run's snapshot and the run replayed pod by pod with the real outcomes, checking the walk's
 assumptions: the run stands while every pod's real PreFilter verdict is the walk's and no transition forgets an
 assumed pod (a PostFilter or Unreserve rejecting waiting siblings, a Permit 'Gang not found'), since a forget changes
@@ -239,82 +240,88 @@ def schedule_with_gangs(engine, mgr: GangManager, pods, gang_ids, seq=None, nomi
     """Schedules `pods` in queue order with Coscheduling's PreFilter / Permit / PostFilter / Unreserve around every pod,
     through batched engine calls (engine: Engine or the oracle's Oracle: schedule(pods, seq), forget(nodes, pods)).
     gang_ids[i]: the pod's gang key (0: no gang). Returns (placements, result) where result holds per pod the gang
-    PreFilter code, the Permit status (-1: none), the final state (ST_*) and the node it is assumed / bound on."""
+    PreFilter code, the Permit status (-1: none), the final state (ST_*) and the node it is assumed / bound on.
+
+    The per-pod gate loop runs in the library (gs_gang_walk / gs_gang_replay over a gs_gang_pass): one walk and one
+    replay call per engine call; this function only moves the runs through the engine and forgets withdrawn pods."""
     pods = np.ascontiguousarray(pods, dtype=abi.POD_DTYPE)
     n = len(pods)
-    gang_ids = np.asarray(gang_ids, np.uint64)
+    gang_ids = np.ascontiguousarray(gang_ids, np.uint64)
     seq = np.arange(n, dtype=np.uint64) if seq is None else np.ascontiguousarray(seq, dtype=np.uint64)
-    nominated = np.zeros(n, bool) if nominated is None else np.asarray(nominated, bool)
-    P = _Pass(engine, mgr, pods, gang_ids, nominated, now_ns, waiting)
+    nom = np.zeros(n, np.uint8) if nominated is None else np.ascontiguousarray(nominated, np.uint8)
+    waiting = waiting if waiting is not None else WaitingPods()
+    uids = np.ascontiguousarray(pods["uid"], np.uint64)
+    prefilter = np.zeros(n, np.int8)
+    permit = np.full(n, -1, np.int8)
+    state = np.zeros(n, np.int8)
+    node = np.full(n, -1, np.int32)
+    L = lib()
+    h = C.c_void_p()
+    GangManager._chk(L.gs_gang_pass_create(mgr._h, n, abi.ptr(gang_ids), abi.ptr(uids), abi.ptr(nom), now_ns,
+                                           abi.ptr(prefilter), abi.ptr(permit), abi.ptr(state), abi.ptr(node),
+                                           C.byref(h)), "gs_gang_pass_create")
     out = np.zeros(n, abi.PLACEMENT_DTYPE)
     out["node"] = -1
-    i = 0
-    while i < n:
-        snap = mgr.clone()
-        run, j = [], i
-        # speculative walk: every pod that passes PreFilter finds a node
-        while j < n and len(run) < run_cap:
-            ok, rej = P.before_node_loop(j)
-            if not ok:
-                j += 1
-                if rej:   # Unreserves: the engine state changes after this pod
-                    break
-                continue
-            run.append(j)
-            g, uid = int(gang_ids[j]), int(pods["uid"][j])
-            st, _, allowed = mgr.permit(g, uid, now_ns)
-            j += 1
-            if st == PERMIT_SUCCESS:
-                mgr.post_bind(g, uid)
-                for a in allowed:
-                    mgr.post_bind(P.gang_of(a), a)
-            elif st == PERMIT_NOT_FOUND:
-                break   # its Reserve is undone after the run
-        got = engine.schedule(pods[run], seq[run]) if run else np.zeros(0, abi.PLACEMENT_DTYPE)
+    run = np.zeros(max(1, min(run_cap, n)), np.uint32)
+    fbuf = np.zeros(n + len(waiting.pods) + 1, np.uint64)
+    index = {}
 
-        def drop_from(r0):
-            """Withdraw the run's speculative placements from position r0 on (ForgetPod)."""
-            later = [q for q in range(r0, len(run)) if got["node"][q] >= 0]
-            if later:
-                engine.forget(got["node"][later].astype(np.uint32), pods[[run[q] for q in later]])
+    def where(uid: int):
+        """the node and pod record of a pod to forget: this queue's, or one waiting from an earlier pass"""
+        if not index:
+            index.update((int(u), k) for k, u in enumerate(uids))
+        k = index.get(uid)
+        if k is not None:
+            return int(node[k]), pods[k]
+        _, nd, rec = waiting.pods[uid]
+        return nd, rec
 
-        # replay [i, j) with the real outcomes on the snapshot's gang state, checking the walk's assumptions: the run
-        # stands while every pod's real PreFilter verdict is the walk's and no Unreserve forgets a pod (which changes
-        # the node state under the run's later pods); at the first break the rest of the run is withdrawn and the
-        # queue resumes after that pod
-        mgr.assign(snap)
-        r, k = 0, i
-        while k < j:
-            ok, rej = P.before_node_loop(k)
-            in_run = r < len(run) and run[r] == k
-            if ok != in_run:
-                drop_from(r)
-                if ok:   # the walk's PreFilter failed where the real one passes: this pod alone
-                    one = engine.schedule(pods[k:k + 1], seq[k:k + 1])
-                    out[k] = one[0]
-                    rej = P.after_node_loop(k, int(one["node"][0]))
-                P.unreserve_chain(rej, forget=True)
-                j = k + 1
-                break
-            if ok:
-                out[k] = got[r]
-                rej = P.after_node_loop(k, int(got["node"][r]))
-                r += 1
-            if rej:
-                P.unreserve_chain(rej, forget=True)
-                if r < len(run):
-                    drop_from(r)
-                    j = k + 1
-                    break
-            k += 1
-        i = j
+    def forget(nodes: list, recs: list):
+        """ForgetPod of the withdrawn run pods (nodes / recs given) and of the pods the Unreserve chains rejected"""
+        cnt = C.c_uint32(0)
+        GangManager._chk(L.gs_gang_pass_forgets(h, abi.ptr(fbuf), len(fbuf), C.byref(cnt)), "gs_gang_pass_forgets")
+        for u in fbuf[:cnt.value]:
+            nd, rec = where(int(u))
+            nodes.append(nd)
+            recs.append(rec)
+        if nodes:
+            engine.forget(np.array(nodes, np.uint32), np.array(recs, abi.POD_DTYPE))
+
+    try:
+        i = 0
+        rn, j, r_stop, j_next, single = C.c_uint32(), C.c_uint32(), C.c_uint32(), C.c_uint32(), C.c_int32()
+        while i < n:
+            GangManager._chk(L.gs_gang_walk(h, i, run_cap, abi.ptr(run), C.byref(rn), C.byref(j)), "gs_gang_walk")
+            r = run[:rn.value].astype(np.int64)
+            got = engine.schedule(pods[r], seq[r]) if len(r) else np.zeros(0, abi.PLACEMENT_DTYPE)
+            got_node = np.ascontiguousarray(got["node"], np.int32)
+            GangManager._chk(L.gs_gang_replay(h, i, j.value, abi.ptr(run), rn.value, abi.ptr(got_node),
+                                              C.byref(r_stop), C.byref(j_next), C.byref(single)), "gs_gang_replay")
+            kept = r_stop.value
+            out[r[:kept]] = got[:kept]
+            later = [q for q in range(kept, len(r)) if got_node[q] >= 0]   # the run's withdrawn placements
+            forget([int(got_node[q]) for q in later], [pods[r[q]] for q in later])
+            if single.value >= 0:   # the walk's PreFilter failed where the real one passes: this pod alone
+                k = single.value
+                one = engine.schedule(pods[k:k + 1], seq[k:k + 1])
+                out[k] = one[0]
+                GangManager._chk(L.gs_gang_pass_after_single(h, k, int(one["node"][0])), "gs_gang_pass_after_single")
+                forget([], [])
+            i = j_next.value
+        cnt = C.c_uint32(0)
+        cu = np.zeros(max(1, 2 * (n + len(waiting.pods))), np.uint64)
+        cs = np.zeros(len(cu), np.int8)
+        GangManager._chk(L.gs_gang_pass_carried(h, abi.ptr(cu), abi.ptr(cs), len(cu), C.byref(cnt)),
+                         "gs_gang_pass_carried")
+        carried = {int(u): int(x) for u, x in zip(cu[:cnt.value], cs[:cnt.value])}
+    finally:
+        L.gs_gang_pass_destroy(h)
     # the waiting set after this pass: earlier pods that were allowed or rejected leave it, this pass's waiting join
-    for uid in P.carried:
-        P.waiting.pods.pop(uid, None)
-    for k in np.flatnonzero(P.state == ST_WAITING):
-        P.waiting.pods[int(pods["uid"][k])] = (int(gang_ids[k]), int(P.node[k]), pods[k].copy())
-    return out, {"prefilter": P.prefilter, "permit": P.permit, "state": P.state, "node": P.node,
-                 "carried": dict(P.carried)}
+    for uid in carried:
+        waiting.pods.pop(uid, None)
+    for k in np.flatnonzero(state == ST_WAITING):
+        waiting.pods[int(uids[k])] = (int(gang_ids[k]), int(node[k]), pods[k].copy())
+    return out, {"prefilter": prefilter, "permit": permit, "state": state, "node": node, "carried": carried}
 
 
 def expire(engine, mgr: GangManager, pods, gang_ids, node, state, now_ns: int, waiting: WaitingPods | None = None):

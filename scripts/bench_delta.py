@@ -54,6 +54,7 @@ def main() -> None:
     for _ in range(5):
         one_pod()
     base = float(np.median([one_pod() for _ in range(args.rounds)]))
+    e.reset_stats()
     n_touch = max(1, int(args.nodes * args.frac))
     rows, up_s, delta_s = [], [], []
     uid = 1 << 40
@@ -79,6 +80,7 @@ def main() -> None:
         up_s.append(t1 - t0)
         delta_s.append(t1 - t0 + t_sched - base)
         rows.append(n_touch)
+    st = e.stats()
     d = float(np.median(delta_s))
     out = {"metric": "incremental snapshot-update throughput (C5 cluster, LoadAware + Fit rows)",
            "nodes": args.nodes, "rows_per_round": n_touch, "rounds": args.rounds,
@@ -86,6 +88,9 @@ def main() -> None:
            "host_upsert_ms_median": 1e3 * float(np.median(up_s)),
            "one_pod_schedule_ms_base": 1e3 * base, "delta_cost_ms_median": 1e3 * d,
            "rows_per_s": n_touch / d if d > 0 else None,
+           "h2d_bytes_per_row": st["delta_bytes"] / max(1, st["delta_rows"]),
+           "h2d_bytes_per_round": st["delta_bytes"] / max(1, args.rounds),
+           "h2d_rows_total": st["delta_rows"],
            "note": "delta cost = host upserts + (one-pod schedule with the deltas pending - without): host row "
                    "re-derivation, pinned H2D copy of the rows and the scatter kernel"}
     print(json.dumps(out), flush=True)
