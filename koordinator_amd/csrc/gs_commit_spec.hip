@@ -47,7 +47,7 @@
 namespace gs {
 
 constexpr int SP_WAVES = 8, SP_THREADS = 64 * SP_WAVES;
-constexpr int SP_LAG = 16;       // decided - verified <= SP_LAG (undo log depth)
+constexpr int SP_LAG = 12;       // decided - verified <= SP_LAG (undo log depth)
 constexpr int SP_RES0 = 2, SP_NRES = 2;   // Reserve waves 2, 3 (pod parity)
 constexpr int SP_RS0 = SP_RES0 + SP_NRES, SP_TABLES = SP_WAVES - SP_RS0;   // re-scoring waves, one hint table each
 // Role -> wave index. The CU runs wave w on SIMD w % 4, two waves per SIMD: the selector (wave 0) shares its SIMD with
@@ -55,7 +55,7 @@ constexpr int SP_RS0 = SP_RES0 + SP_NRES, SP_TABLES = SP_WAVES - SP_RS0;   // re
 constexpr int SP_W_VERIFY = 4;
 __device__ __forceinline__ int sp_reserve_index(int wv) { return wv == 2 ? 0 : wv == 3 ? 1 : -1; }
 __device__ __forceinline__ int sp_rescore_index(int wv) { return wv == 1 ? 0 : wv >= 5 ? wv - 4 : -1; }
-constexpr int SP_JOBQ = 32;      // job ring per Reserve wave (<= 3 jobs per pod, <= SP_LAG / 2 + 2 pods in flight)
+constexpr int SP_JOBQ = 24;      // job ring per Reserve wave (<= 3 jobs per pod, <= SP_LAG / 2 + 2 pods in flight)
 constexpr int SP_HASH = 256;     // node -> slot (full-row resolution)
 constexpr int SP_FRESH = 1, SP_FITERR = 2, SP_SLOW = 4, SP_OFFSHARD = 8;   // DecRec.flags
 constexpr uint32_t SP_SPIN_LIMIT = 1u << 24;
@@ -99,15 +99,16 @@ struct alignas(16) SpecLds {
   alignas(16) UndoRec undo[SP_LAG];
   alignas(16) HintTable tables[SP_TABLES];
   alignas(16) int32_t final_F[SB], done_ver[SB], has_row[SB], rescored[SB], jobs_left[SB], jobs_all[SB], resv[SB];
-  alignas(16) int32_t hkey[SP_HASH], hval[SP_HASH];
+  alignas(16) int32_t hkey[SP_HASH];
+  alignas(16) int16_t hval[SP_HASH];   // slot of the node in hkey
   alignas(16) Job jobq[SP_NRES * SP_JOBQ];
 };
 
 size_t spec_smem_bytes(int) { return sizeof(SpecLds); }
+// the CU's 160 KiB hold SpecLds and the kernel's static __shared__ words (sseq + ~160 B of hand-off words)
+static_assert(sizeof(SpecLds) + 8 * MAX_BATCH + 160 <= 160 * 1024, "commit_spec_kernel LDS over the CU's 160 KiB");
 
 // LDS hand-off words between the roles (namespace scope: the role functions below and the kernel share them)
-__shared__ TopoDev s_topo[SP_NRES];     // per Reserve wave: topology of its last cpuset Reserve
-__shared__ HintTable s_ht0;       // wave 0: rollback re-scoring
 __shared__ uint64_t s_cpuset[SP_NRES][4];
 __shared__ int32_t s_aff[SP_NRES];
 __shared__ int32_t s_decided, s_stop, s_parked, s_finish, s_cut_at, s_err;
@@ -169,7 +170,7 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
   int32_t* jobs_all = L.jobs_all;   // pod: every job not done (-> rescored)
   int32_t* resv = L.resv;           // pod: its Reserve is applied (or FitError)
   int32_t* hkey = L.hkey;
-  int32_t* hval = L.hval;
+  int16_t* hval = L.hval;
   Job* jobq = L.jobq;               // [Reserve wave][ring]
 
   if (a.prev && a.prev[1] != 1) {   // speculative pass behind a batch that left work for the host: no-op
@@ -214,7 +215,7 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
       uint32_t h = (node * 2654435761u) & (SP_HASH - 1);
       while (hkey[h] >= 0) h = (h + 1) & (SP_HASH - 1);
       hkey[h] = (int32_t)node;
-      hval[h] = slot;
+      hval[h] = (int16_t)slot;
     };
     auto sp_hash_find = [&](uint32_t node) -> int {
       uint32_t h = (node * 2654435761u) & (SP_HASH - 1);
@@ -317,9 +318,10 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
           for (uint64_t bb = pass ? redo1 : redo0; bb; bb &= bb - 1) {
             const int sl = (pass ? 64 : 0) + __builtin_ctzll(bb);
             const Row rr = drows[sl];
-            if (numa_on && ((rr.nr.nflags >> NF_POLICY_SHIFT) & 3u)) hint_table_fill(s_ht0, rr.nr, zone_avail(rr.nr), lane);
+            // (the re-scoring waves are parked: wave 0 borrows the first one's hint table)
+            if (numa_on && ((rr.nr.nflags >> NF_POLICY_SHIFT) & 3u)) hint_table_fill(tables[0], rr.nr, zone_avail(rr.nr), lane);
             WAVE_FENCE();
-            for (int q2 = v + lane; q2 < B; q2 += 64) dsc[q2 * SB + sl] = (int16_t)row_score(rr, pods(q2), a.pf, m, &s_ht0);
+            for (int q2 = v + lane; q2 < B; q2 += 64) dsc[q2 * SB + sl] = (int16_t)row_score(rr, pods(q2), a.pf, m, &tables[0]);
             WAVE_FENCE();
           }
         }
@@ -863,13 +865,11 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
   } else if (sp_reserve_index(wv) >= 0) {
     // =================================================== Reserve ===================================================
     const int wr = sp_reserve_index(wv);   // this wave's pods: q % SP_NRES == wr
-    TopoDev& s_topo_w = s_topo[wr];
     uint64_t* s_cpuset_w = s_cpuset[wr];
     int32_t& s_aff_w = s_aff[wr];
     Job* jq = jobq + wr * SP_JOBQ;
     int32_t& jq_tail = s_jq_tail[wr];
     int32_t& jq_head = s_jq_head[wr];
-    int topo_id = -1;
     int f_kind = 0, f_region = 0, f_off = 0, f_size = 8;
     const void* f_src = nullptr;
     if (lane < ROW_I64) { f_kind = 1; f_src = m.c64(kRowCol[lane]); f_off = lane * 8; }
@@ -924,7 +924,6 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
         while (ld_acq(&s_stop) && !ld_acq(&s_finish)) sp_sleep();
         const int v = ld_acq(&s_rb_at);
         q = v + ((wr - v) & (SP_NRES - 1));
-        topo_id = -1;
         pf_q = -1;
         continue;
       }
@@ -1014,18 +1013,6 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
       WAVE_FENCE();
       SPM(15);   // row fetch + undo log
       Row& dr_ = drows[slot];
-      if (numa_on) {
-        const int tp = cst[slot].topo;
-        const uint32_t nfl = dr_.nr.nflags;
-        if (tp >= 0 && tp != topo_id && !(pk.numa & (PN_SKIP | PN_PREFAIL)) &&
-            ((pk.numa & PN_BIND) || ((nfl >> NF_BIND_SHIFT) & 3u))) {
-          const uint64_t* src = reinterpret_cast<const uint64_t*>(a.topos + tp);
-          uint64_t* dst = reinterpret_cast<uint64_t*>(&s_topo_w);
-          for (int i = lane; i < (int)(sizeof(TopoDev) / 8); i += 64) dst[i] = src[i];
-          topo_id = tp;
-        }
-        WAVE_FENCE();
-      }
       int cut = 0;
       {
         const Row dr = dr_;
@@ -1063,8 +1050,8 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
               }
               if (rb) {
                 CpuStateDev& cs = cst[slot];
-                if (cpuset_on_device(cs, topo_id, pk)) {
-                  if (cpuset_reserve((const GS_LDS TopoDev*)&s_topo_w, (GS_LDS CpuStateDev*)&cs, pk, nf, no.zkeys,
+                if (cpuset_on_device(cs, pk)) {   // (the topology's TopoDev is read from HBM: scalar loads)
+                  if (cpuset_reserve(a.topos + cs.topo, (GS_LDS CpuStateDev*)&cs, pk, nf, no.zkeys,
                                      no.zcpu[0], no.zcpu[1], no.zcpu[2], no.zcpu[3], (GS_LDS NumaRow*)&dr_.nr,
                                      (GS_LDS uint64_t*)s_cpuset_w)) {
                     pl.flags |= PL_DEVICE_CPUSET;

@@ -358,12 +358,12 @@ __device__ __forceinline__ void wave_rank_sort(uint32_t* v, int n, uint32_t* tmp
   WAVE_FENCE();
 }
 
-// The device Reserve selects this pod's cpuset on this row: its topology is the staged one (in the device scope, so
-// topo >= 0), and the exclusivity state the selection reads is exact (an exclusive pod on a row marked CM_XSTALE —
+// The device Reserve selects this pod's cpuset on this row: its topology is in the device scope (topo >= 0), and the
+// exclusivity state the selection reads is exact (an exclusive pod on a row marked CM_XSTALE —
 // a maxRefCount-2 node whose shared CPUs lost their policy — has its cpuset selected by the host).
-__device__ __forceinline__ bool cpuset_on_device(const CpuStateDev& cs, int staged_topo, const PodVec& p) {
+__device__ __forceinline__ bool cpuset_on_device(const CpuStateDev& cs, const PodVec& p) {
   const int ep = (p.numa & PN_BIND) ? (int)((p.numa >> PN_EXCL_SHIFT) & 3u) : GS_CPU_EXCLUSIVE_NONE;
-  return cs.topo >= 0 && cs.topo == staged_topo && !((cs.meta & CM_XSTALE) && ep != GS_CPU_EXCLUSIVE_NONE);
+  return cs.topo >= 0 && !((cs.meta & CM_XSTALE) && ep != GS_CPU_EXCLUSIVE_NONE);
 }
 
 // Device-side cpuset Reserve of one pod on its winner row (one thread): allocateCPUSet with the NUMA split of
@@ -371,12 +371,13 @@ __device__ __forceinline__ bool cpuset_on_device(const CpuStateDev& cs, int stag
 // (node_allocation.go:82-110) on the CPU state and the row's available-CPU summaries, as numa_derive
 // (gs_numa_host.cpp) would recompute them. false: allocateCPUSet errors (the host fails loudly).
 // Arguments live in LDS or registers (zone split by value, cpuset into an LDS array): nothing of the caller's
-// frame has its address taken, so the commit kernel keeps its Reserve state out of scratch.
+// frame has its address taken, so the commit kernel keeps its Reserve state out of scratch. The topology (TopoDev,
+// read-only) is read from HBM at a wave-uniform address: scalar loads.
 #define GS_LDS __attribute__((address_space(3)))
 // Not inlined: its register pressure stays out of the commit loop. The LDS operands arrive as address-space-3
 // pointers and everything below is inlined here, so every access stays a ds_* instruction (a generic pointer would
 // make them flat loads that wait for outstanding global loads).
-__device__ __noinline__ bool cpuset_reserve(const GS_LDS TopoDev* tp, GS_LDS CpuStateDev* csp, const PodVec& p,
+__device__ __noinline__ bool cpuset_reserve(const TopoDev* __restrict__ tp, GS_LDS CpuStateDev* csp, const PodVec& p,
                                             uint32_t nf, uint32_t zkeys, int64_t zc0, int64_t zc1, int64_t zc2,
                                             int64_t zc3, GS_LDS NumaRow* nrp, GS_LDS uint64_t* cpuset) {
   // every operand is wave-uniform (one Reserve at a time): say so, so that the selection runs on the scalar unit
@@ -384,7 +385,7 @@ __device__ __noinline__ bool cpuset_reserve(const GS_LDS TopoDev* tp, GS_LDS Cpu
   auto u64 = [&](int64_t x) {
     return (int64_t)(((uint64_t)u32((uint32_t)((uint64_t)x >> 32)) << 32) | u32((uint32_t)(uint64_t)x));
   };
-  tp = (const GS_LDS TopoDev*)(size_t)u32((uint32_t)(size_t)tp);
+  tp = (const TopoDev*)(((uint64_t)u32((uint32_t)((uint64_t)tp >> 32)) << 32) | u32((uint32_t)(uint64_t)tp));
   csp = (GS_LDS CpuStateDev*)(size_t)u32((uint32_t)(size_t)csp);
   nrp = (GS_LDS NumaRow*)(size_t)u32((uint32_t)(size_t)nrp);
   cpuset = (GS_LDS uint64_t*)(size_t)u32((uint32_t)(size_t)cpuset);

@@ -622,8 +622,6 @@ __global__ void __launch_bounds__(COMMIT_THREADS) commit_kernel(CommitArgs a) {
   __shared__ uint32_t s_winner;
   __shared__ int64_t s_T;
   __shared__ int s_cut;                                // the pod just committed needs host-side Reserve
-  __shared__ TopoDev s_topo;                           // topology of the last cpuset Reserve (bit-plane form)
-  __shared__ int s_topo_id;
   __shared__ int s_aff;                                // known affinity of pod k on its winner row (-1: recompute)
   __shared__ uint64_t s_cpuset[4];                     // CPUs of a device-side cpuset Reserve
   __shared__ HintTable s_ht, s_ht2;                    // NUMA hint sums of the winner row (new / batch-start state)
@@ -641,7 +639,6 @@ __global__ void __launch_bounds__(COMMIT_THREADS) commit_kernel(CommitArgs a) {
   if (tid == 0) {
     s_ndirty = 0;
     s_start = a.window_k ? (a.prev ? (uint32_t)a.prev[2] : a.start) : 0u;
-    s_topo_id = -1;
     s_fk = a.forced_node >= 0 ? 0 : -1;
     s_fnode = a.forced_node;
     s_fscore = a.forced_score;
@@ -1122,19 +1119,6 @@ __global__ void __launch_bounds__(COMMIT_THREADS) commit_kernel(CommitArgs a) {
     const int slot = s_slot;
     const bool fresh = s_fresh;
     Row& d = drows[slot];
-    if (numa_on) {   // stage the winner's topology in LDS for a device-side cpuset Reserve (block-uniform test)
-      const PodVec& pq = pods(k);
-      const int tp = cst[slot].topo;
-      const uint32_t nfl = fresh ? orow.nr.nflags : d.nr.nflags;
-      if (tp >= 0 && tp != s_topo_id && !(pq.numa & (PN_SKIP | PN_PREFAIL)) &&
-          ((pq.numa & PN_BIND) || ((nfl >> NF_BIND_SHIFT) & 3u))) {
-        const uint64_t* src = reinterpret_cast<const uint64_t*>(a.topos + tp);
-        uint64_t* dst = reinterpret_cast<uint64_t*>(&s_topo);
-        for (int i = tid; i < (int)(sizeof(TopoDev) / 8); i += COMMIT_THREADS) dst[i] = src[i];
-        __syncthreads();
-        if (tid == 0) s_topo_id = tp;
-      }
-    }
     const int wv = __builtin_amdgcn_readfirstlane(wave);
     if (wv == 0 && numa_on && s_aff < 0) {   // hint table of the winner's pre-Reserve state (affinity unknown)
       const NumaRow nr = fresh ? orow.nr : d.nr;
@@ -1180,8 +1164,8 @@ __global__ void __launch_bounds__(COMMIT_THREADS) commit_kernel(CommitArgs a) {
           }
           if (rb) {
             CpuStateDev& cs = cst[slot];
-            if (cpuset_on_device(cs, s_topo_id, pk)) {
-              if (cpuset_reserve((const GS_LDS TopoDev*)&s_topo, (GS_LDS CpuStateDev*)&cs, pk, nf, no.zkeys, no.zcpu[0],
+            if (cpuset_on_device(cs, pk)) {   // (the topology's TopoDev is read from HBM: scalar loads)
+              if (cpuset_reserve(a.topos + cs.topo, (GS_LDS CpuStateDev*)&cs, pk, nf, no.zkeys, no.zcpu[0],
                                  no.zcpu[1], no.zcpu[2], no.zcpu[3],
                                  (GS_LDS NumaRow*)&d.nr, (GS_LDS uint64_t*)s_cpuset)) {
                 pl.flags |= PL_DEVICE_CPUSET;
