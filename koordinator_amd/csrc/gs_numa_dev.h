@@ -369,15 +369,29 @@ __device__ __forceinline__ bool hints_merge(const Src& src, int nz, int policy, 
   const uint32_t valid = ord_valid(nz);
   uint32_t totc = 0, totm = 0, lc = 0, lm = 0;
   if (!nil_hints) {
-#pragma unroll 1
-    for (int mi = 0; mi < 15; ++mi) {
-      if (!(valid >> mi & 1u)) continue;
+    auto add = [&](int mi) {
       const HintSums s = src.sum(mi);
       if (s.tc >= pcpu) { totc |= 1u << mi; if (s.fc >= pcpu) lc |= 1u << mi; }
       if (s.tm >= mem) { totm |= 1u << mi; if (s.fm >= mem) lm |= 1u << mi; }
-    }
+    };
+    // The single-zone positions (0..nz-1) first: when each requested resource has a single zone with enough free
+    // resources (and one zone has both), merge_hint_lists takes its exact fast path, which reads nothing of the
+    // multi-zone positions (it needs min size 1 and the single zones of each list); only otherwise are the other
+    // positions summed (> 99.7% of C3's policy pairs stop here).
+#pragma unroll 1
+    for (int mi = 0; mi < nz; ++mi) add(mi);
     if (!has_cpu) totc = lc = 0;
     if (!has_mem) totm = lm = 0;
+    const uint32_t single = (1u << nz) - 1u;
+    const bool fast = (has_cpu || has_mem) && (!has_cpu || lc) && (!has_mem || lm) &&
+                      ((has_cpu ? lc : single) & (has_mem ? lm : single)) != 0;
+    if (!fast) {
+#pragma unroll 1
+      for (int mi = nz; mi < 15; ++mi)
+        if (valid >> mi & 1u) add(mi);
+      if (!has_cpu) totc = lc = 0;
+      if (!has_mem) totm = lm = 0;
+    }
   }
   uint64_t sc_lo = 0, sc_hi = 0;
   uint32_t have = 0;

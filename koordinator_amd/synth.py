@@ -241,7 +241,7 @@ def make_numa(c: Cluster, seed: int | None = None, numa_policy_pct: int = 30, cp
         smt, interleave = 2, False
         if mixed:
             # (256 logical CPUs as SMT-1 cores: outside the device cpuset scope, the host path)
-            smt = 4 if ci % 5 == 2 else (1 if (ci % 7 == 3 or (nc == 256 and kk == 2)) else 2)
+            smt = 1 if (nc == 256 and kk == 2) else 4 if ci % 5 == 2 else (1 if ci % 7 == 3 else 2)
             interleave = ci % 3 == 1
         cores_per_numa = nc // smt // kk
         ncores = 2 * per_socket * cores_per_numa

@@ -6,7 +6,7 @@ Runs in the build container (no GPU): about 4e9 pod x node evaluations for the n
     python scripts/full_parity.py bench       # C3, 50,000 nodes, the bench's 20,480 pods (calls of 2,048)
     python scripts/full_parity.py northstar   # C3, 100,000 nodes x 50,000 pods (one call)
 
-Writes profiles/r03_full_parity_<workload>.json."""
+Writes profiles/<ROUND>_full_parity_<workload>.json (ROUND from the environment, default r04)."""
 from __future__ import annotations
 
 import json
@@ -63,7 +63,7 @@ def main() -> None:
         ok = ok and len(bad) == 0
     res["placed"] = int((got["node"] >= 0).sum())
     res["identical"] = ok
-    out = os.path.join(ROOT, "profiles", f"r03_full_parity_{name}.json")
+    out = os.path.join(ROOT, "profiles", f"{os.environ.get('ROUND', 'r04')}_full_parity_{name}.json")
     with open(out, "w") as f:
         json.dump(res, f, indent=1)
     print(json.dumps(res))

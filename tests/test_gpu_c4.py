@@ -1,4 +1,4 @@
-"""C4: the 100k-node cluster node-sharded over 2 and 4 PROCESSES on the box's one GPU. Every rank
+"""C4: the 100k-node cluster node-sharded over 2, 4 and 8 PROCESSES on the box's one GPU. Every rank
 evaluates its shard, the per-shard candidate levels are all-gathered (torch.distributed gloo through the library's
 host-callback transport, gs_comm_init_callback — RCCL's ncclAllGather carries the same bytes in production), merged
 on the device, and every rank runs the replicated speculative commit. All ranks must return identical placements
@@ -73,9 +73,11 @@ def _free_port() -> int:
         return s.getsockname()[1]
 
 
-@pytest.mark.parametrize("world,numa,pods", [(2, False, 20_480), (4, False, 20_480), (2, True, 20_480),
-                                             (4, True, 50_000)],
-                         ids=["2proc-c2set", "4proc-c2set", "2proc-c3", "4proc-c3-50k"])
+CASES = [(2, False, 20_480), (4, False, 20_480), (2, True, 20_480), (4, True, 50_000), (8, True, 20_480)]
+IDS = ["2proc-c2set", "4proc-c2set", "2proc-c3", "4proc-c3-50k", "8proc-c3"]
+
+
+@pytest.mark.parametrize("world,numa,pods", CASES, ids=IDS)
 def test_c4_sharded_processes_replay_parity(world, numa, pods):
     from koordinator_amd import abi
     t0 = time.perf_counter()
@@ -107,6 +109,14 @@ def test_c4_sharded_processes_replay_parity(world, numa, pods):
     c = _cluster(numa, pods)
     n = _replay_check(c, _cfg(c, numa), got, np.arange(0, pods, 64))
     walls = [res[r][2] for r in range(world)]
+    import json
+    os.makedirs("gpurun_out", exist_ok=True)
+    with open(os.path.join("gpurun_out", f"c4_{world}proc_{'c3' if numa else 'c2set'}_{pods}.json"), "w") as f:
+        json.dump({"ranks": world, "nodes": NODES, "pods": pods, "profile": "C3" if numa else "C2 plugin set",
+                   "transport": "gloo all-gather through gs_comm_init_callback, every rank on the box's one GPU",
+                   "placed": int((got["node"] >= 0).sum()), "rechecked_in_full": n, "identical_on_every_rank": True,
+                   "schedule_wall_s_per_rank": walls, "pods_per_s": pods / max(walls), "cuts": int(res[0][5]),
+                   "shards": [[int(res[r][3]), int(res[r][4])] for r in range(world)]}, f)
     print(f"C4 {world} processes x {NODES} nodes, {pods} pods ({'C3' if numa else 'C2 set'}): "
           f"{int((got['node'] >= 0).sum())} placed, {n} re-checked in full, identical on every rank; schedule wall "
           f"{max(walls):.1f} s ({pods / max(walls):.0f} pods/s through gloo), cuts {res[0][5]}; "
