@@ -984,14 +984,19 @@ int launch_batch(gs_ctx* c, int b, const int32_t* prev, const PlacementDev* prev
   HIP_TRY(c, hipEventRecord(c->ev[1], c->st_ev));
   HIP_TRY(c, hipEventRecord(sl.ev_evdone, c->st_ev));
   HIP_TRY(c, hipStreamWaitEvent(c->st, sl.ev_evdone, 0));
-  if (prev) {
-    static const bool twice = getenv("GS_PATCH_TWICE") && getenv("GS_PATCH_TWICE")[0] == '1';   // diagnostics
-    for (int k = 0; k < (twice ? 2 : 1); ++k)
-      HIP_TRY(c, launch_patch(c->mv, c->d_pods, b, c->pf, c->n0, c->n1, c->d_S, c->ld, prod_cols, c->d_aff, prev_out,
-                              prev, prev_b, c->st));
+  // the rows the previous batch landed on, re-evaluated on their committed state: inside cand_kernel (block k patches
+  // pod k's row before its histogram; one launch less on the commit chain), or by patch_kernel under node sampling
+  // (no candidate levels) or GS_FUSED_PATCH=0
+  static const bool separate = getenv("GS_FUSED_PATCH") && getenv("GS_FUSED_PATCH")[0] == '0';
+  const bool fused = prev && prev_b > 0 && !c->window_k && !separate;
+  if (prev && !fused)
+    HIP_TRY(c, launch_patch(c->mv, c->d_pods, b, c->pf, c->n0, c->n1, c->d_S, c->ld, prod_cols, c->d_aff, prev_out,
+                            prev, prev_b, c->st));
+  if (!c->window_k) {   // node sampling selects over the rotation window, not the candidate levels
+    CandPatch cp{c->mv, c->d_pods, c->pf, c->n0, c->n1, prod_cols, 1, c->d_aff, prev_out, prev};
+    HIP_TRY(c, launch_cand(c->d_S, c->ld, len, c->n0, b, c->max_score, c->lstride, d_lists, d_hdrs, d_ext, c->st,
+                           fused ? &cp : nullptr));
   }
-  if (!c->window_k)   // node sampling selects over the rotation window, not the candidate levels
-    HIP_TRY(c, launch_cand(c->d_S, c->ld, len, c->n0, b, c->max_score, c->lstride, d_lists, d_hdrs, d_ext, c->st));
   HIP_TRY(c, hipEventRecord(c->ev[2], c->st));
   if (c->nranks > 1) {
     int rc = exchange(c, c->d_xchg_send, c->d_xchg_recv, c->xchg_bytes);

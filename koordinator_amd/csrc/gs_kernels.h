@@ -133,8 +133,20 @@ hipError_t launch_eval_full(const MirrorView& m, const PodVec* pods, int npods, 
                             int16_t* scores, uint16_t* codes, int16_t* plugin, int prod_cols, hipStream_t st);
 void set_cand_stamps(uint64_t* p);   // diagnostics: cand_kernel phase cycles (nullptr: off)
 // lcap: listed nodes per pod (<= LCAP), also the lists' stride
-hipError_t launch_cand(const int16_t* S, uint32_t ld, uint32_t len, uint32_t n0, int npods, int max_score, int lcap,
-                       uint32_t* lists, LevelHdr* hdrs, LevelExt* ext, hipStream_t st);
+// The previous batch's landed rows, re-evaluated by cand_kernel's block k for pod k before its histogram (a pass
+// behind a batch whose commit wrote those rows back: the eval pass ran on their state before it); on = 0: none.
+struct CandPatch {
+  MirrorView m;
+  const PodVec* pods;
+  Profile pf;
+  uint32_t n0, n1;
+  int prod_cols, on;
+  uint8_t* aff;
+  const PlacementDev* prev_out;
+  const int32_t* prev_committed;
+};
+hipError_t launch_cand(int16_t* S, uint32_t ld, uint32_t len, uint32_t n0, int npods, int max_score, int lcap,
+                       uint32_t* lists, LevelHdr* hdrs, LevelExt* ext, hipStream_t st, const CandPatch* patch = nullptr);
 // several shards: per pod, the all-gathered rank blocks' levels merged into one block of the single-rank layout (the
 // speculative commit's input)
 hipError_t launch_merge_levels(const uint8_t* xin, size_t xblock, int nranks, int npods, int bmax, int lstride,

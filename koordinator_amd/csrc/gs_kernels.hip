@@ -220,10 +220,10 @@ __global__ void __launch_bounds__(256) eval_full_kernel(MirrorView m, const PodV
 // row so that per-wave histograms give every wave its output offset within each level. W = 16 for profiles
 // with small score ranges (more bandwidth per row when batches are short), else 4.
 template <int W>
-__global__ void __launch_bounds__(64 * W) cand_kernel(const int16_t* __restrict__ S, uint32_t ld, uint32_t len,
+__global__ void __launch_bounds__(64 * W) cand_kernel(int16_t* __restrict__ S, uint32_t ld, uint32_t len,
                                                       uint32_t n0, int max_score, int lcap, uint32_t* __restrict__ lists,
                                                       LevelHdr* __restrict__ hdrs, LevelExt* __restrict__ ext,
-                                                      uint64_t* stamps) {
+                                                      uint64_t* stamps, CandPatch cp) {
   constexpr int CAND_THREADS = 64 * W;
   // diagnostics (stamps != nullptr): wave 0's cycles per phase, summed over the pods
   uint64_t ct_last = stamps ? __builtin_amdgcn_s_memtime() : 0;
@@ -246,6 +246,25 @@ __global__ void __launch_bounds__(64 * W) cand_kernel(const int16_t* __restrict_
   __shared__ int16_t s_stepmax[W][STEPCAP];    // highest score of each of the wave's steps (pass 2 skips the rest)
   const int k = blockIdx.x;
   const int t = threadIdx.x, wave = t >> 6, lane = t & 63;
+  if (cp.on) {
+    // the patch of this pod's score row (patch_kernel's work, one pair per thread): the rows the previous batch landed
+    // on, on their committed state; the histogram below then reads them (this block's row only: no other block
+    // writes it)
+    const bool numa = (cp.pf.enabled & 0x30u) != 0;
+    const int np = cp.prev_committed[0];   // -1: a voided pass
+    for (int j = t; j < np; j += CAND_THREADS) {
+      const int32_t node = cp.prev_out[j].node;
+      if (node < 0 || (uint32_t)node < cp.n0 || (uint32_t)node >= cp.n1) continue;
+      Row r;
+      load_row(cp.m, (uint32_t)node, cp.prod_cols, numa, r);
+      const PairOut o = eval_pair<false, false, true>(r, cp.pods[k], cp.pf, cp.m);
+      const size_t at = (size_t)k * ld + ((uint32_t)node - cp.n0);
+      S[at] = (int16_t)total_score(o, cp.pf);
+      if (numa && ((r.nr.nflags >> NF_POLICY_SHIFT) & 3u)) cp.aff[at] = (uint8_t)(o.code ? 0u : o.aff);
+    }
+    __threadfence_block();
+    __syncthreads();
+  }
   const int16_t* row = S + (size_t)k * ld;
   for (int b = t; b < W * nbins; b += CAND_THREADS) whist[b] = 0;
   if (t == 0) s_total = 0;
@@ -1473,15 +1492,17 @@ static bool cand_wide(int max_score) {
 static uint64_t* g_cand_stamps = nullptr;
 void set_cand_stamps(uint64_t* p) { g_cand_stamps = p; }
 
-hipError_t launch_cand(const int16_t* S, uint32_t ld, uint32_t len, uint32_t n0, int npods, int max_score, int lcap,
-                       uint32_t* lists, LevelHdr* hdrs, LevelExt* ext, hipStream_t st) {
+hipError_t launch_cand(int16_t* S, uint32_t ld, uint32_t len, uint32_t n0, int npods, int max_score, int lcap,
+                       uint32_t* lists, LevelHdr* hdrs, LevelExt* ext, hipStream_t st, const CandPatch* patch) {
   if (lcap < 1 || lcap > LCAP) return hipErrorInvalidValue;
+  CandPatch cp{};
+  if (patch) cp = *patch;
   if (cand_wide(max_score))
     hipLaunchKernelGGL(cand_kernel<16>, dim3(npods), dim3(1024), cand_smem_bytes(max_score, 16), st, S, ld, len, n0,
-                       max_score, lcap, lists, hdrs, ext, g_cand_stamps);
+                       max_score, lcap, lists, hdrs, ext, g_cand_stamps, cp);
   else
     hipLaunchKernelGGL(cand_kernel<4>, dim3(npods), dim3(256), cand_smem_bytes(max_score, 4), st, S, ld, len, n0,
-                       max_score, lcap, lists, hdrs, ext, g_cand_stamps);
+                       max_score, lcap, lists, hdrs, ext, g_cand_stamps, cp);
   return hipGetLastError();
 }
 

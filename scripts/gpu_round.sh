@@ -15,7 +15,7 @@ timeout -k 10 400 python -u bench.py ${BENCH_ARGS:-} > gpurun_out/bench.json 2> 
 rc=$?; echo "BENCH rc=$rc"; cat gpurun_out/bench.json; tail -5 gpurun_out/bench.err
 [ $rc -eq 0 ] || exit $rc
 if [ "${SKIP_PROF:-0}" != 1 ]; then
-  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$PWD/gpurun_out/prof" -o bench -- \
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$PWD/gpurun_out/prof" -o bench -- \
       python -u bench.py --steps 5 --warmup 1 --no-cpu-baseline > gpurun_out/prof.log 2>&1
   rc=$?; echo "PROF rc=$rc"; tail -3 gpurun_out/prof.log
   find gpurun_out/prof -name "*stats*" | head
