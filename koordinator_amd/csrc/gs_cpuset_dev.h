@@ -28,6 +28,14 @@
 #else
 #define GS_HD inline
 #endif
+// The topology tables are read-only for a kernel's lifetime: on the device they are read through the constant address
+// space, so the wave-uniform reads of the selection below are scalar loads (s_load, through the scalar cache) instead
+// of vector loads with a readfirstlane each.
+#if defined(__HIP_DEVICE_COMPILE__)
+#define GS_TOPO_AS __attribute__((address_space(4)))
+#else
+#define GS_TOPO_AS
+#endif
 
 namespace gs {
 
@@ -91,9 +99,19 @@ GS_HD int td_pc(uint64_t x) { return __builtin_popcountll(x); }
 GS_HD int td_pc(cm_t x) { return __builtin_popcountll(cm_lo(x)) + __builtin_popcountll(cm_hi(x)); }
 GS_HD int td_ctz(uint64_t x) { return __builtin_ctzll(x); }
 GS_HD int td_ctz(cm_t x) { return cm_lo(x) ? __builtin_ctzll(cm_lo(x)) : 64 + __builtin_ctzll(cm_hi(x)); }
-template <class M> GS_HD M td_tm(const uint64_t* w);   // a TopoDev mask
-template <> GS_HD uint64_t td_tm<uint64_t>(const uint64_t* w) { return TU64(w[0]); }
-template <> GS_HD cm_t td_tm<cm_t>(const uint64_t* w) { return ((cm_t)TU64(w[1]) << 64) | (cm_t)TU64(w[0]); }
+template <class M> GS_HD M td_tm(const GS_TOPO_AS uint64_t* w);   // a TopoDev mask
+template <> GS_HD uint64_t td_tm<uint64_t>(const GS_TOPO_AS uint64_t* w) { return TU64(w[0]); }
+template <> GS_HD cm_t td_tm<cm_t>(const GS_TOPO_AS uint64_t* w) { return ((cm_t)TU64(w[1]) << 64) | (cm_t)TU64(w[0]); }
+// byte i of a topology table: on the device the aligned dword that holds it (a scalar load; there is no scalar byte
+// load on gfx950)
+GS_HD int td_u8(const GS_TOPO_AS uint8_t* a, int i) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const uint32_t w = reinterpret_cast<const GS_TOPO_AS uint32_t*>(a)[i >> 2];
+  return (int)((w >> (8 * (i & 3))) & 0xffu);
+#else
+  return a[i];
+#endif
+}
 template <class M> GS_HD M td_bit(int k) { return (M)1 << k; }
 template <class M> GS_HD bool td_has(M x, int k) { return (int)((x >> k) & 1u) != 0; }
 template <class M> constexpr int td_bits() { return (int)sizeof(M) * 8; }
@@ -110,7 +128,7 @@ template <class M, int NP> GS_HD M td_any(const M* P) {
   for (int j = 0; j < NP; ++j) a |= P[j];
   return a;
 }
-template <class M> GS_HD M td_all(const TopoDev& t) {
+template <class M> GS_HD M td_all(const GS_TOPO_AS TopoDev& t) {
   const int n = TU32(t.ncores);
   return n >= td_bits<M>() ? ~(M)0 : (td_bit<M>(n) - 1);
 }
@@ -201,7 +219,7 @@ template <class M, int NP> GS_HD int td_rth(const M* P, const M* RC, int k, int 
 // cpuAccumulator (cpu_accumulator.go:234-330) with maxRefCount <= 2
 template <class M, int NP>
 struct DAcc {
-  const TopoDev& t;
+  const GS_TOPO_AS TopoDev& t;
   M A[NP];    // allocatableCPUs
   M RC[NP];   // CPUs at RefCount 1 (allocatable or not: only A & RC is read)
   M R[NP];    // result
@@ -210,7 +228,7 @@ struct DAcc {
   int needed, nalloc, ep;
   bool most, exclusive, refs;
 
-  GS_HD DAcc(const TopoDev& tt, const M* avail, const M* rc, M xc0, uint32_t xn0, int n, int e, bool m)
+  GS_HD DAcc(const GS_TOPO_AS TopoDev& tt, const M* avail, const M* rc, M xc0, uint32_t xn0, int n, int e, bool m)
       : t(tt), xc(xc0), xn(xn0), needed(n), ep(e), most(m) {
     M any_rc = 0;
 #pragma unroll
@@ -219,13 +237,13 @@ struct DAcc {
     nalloc = td_cnt<M, NP>(A, ~(M)0);
     exclusive = e == GS_CPU_EXCLUSIVE_PCPU_LEVEL || e == GS_CPU_EXCLUSIVE_NUMA_NODE_LEVEL;
   }
-  GS_HD M tm(const uint64_t* w) const { return td_tm<M>(w); }
+  GS_HD M tm(const GS_TOPO_AS uint64_t* w) const { return td_tm<M>(w); }
   GS_HD bool sless(int a, int b) const { return most ? a < b : a > b; }
   GS_HD int dir(int x) const { return most ? x : 511 - x; }   // ascending key of the sless order
   GS_HD bool satisfied() const { return needed < 1; }
   GS_HD M nodes_cores(uint32_t nodes) const {
     M m = 0;
-    for (; nodes; nodes &= nodes - 1) m |= tm(t.node_cores[__builtin_ctz(nodes)]);
+    for (; nodes; nodes &= nodes - 1) m |= tm(t.node_cores[TU32(__builtin_ctz(nodes))]);
     return m;
   }
   // getCoreRefCount over allocatableCPUs (:776-783): cores whose CPUs in the snapshot S (the allocatable CPUs a list
@@ -255,7 +273,7 @@ struct DAcc {
     --needed;
     if (exclusive) {
       if (ep == GS_CPU_EXCLUSIVE_PCPU_LEVEL) xc |= b;
-      else xn |= 1u << TU32(t.core_node[k]);
+      else xn |= 1u << td_u8(t.core_node, TU32(k));
     }
   }
   // the first `n` allocatable CPUs of core k in CPU order
@@ -284,7 +302,7 @@ struct DAcc {
 #pragma unroll
       for (int j = 0; j < NP; ++j) {
         if (!td_has(S[j], k) || (r >= 0 && j != jr)) continue;
-        const int c = TU32(t.core_cpu[k][j]);
+        const int c = td_u8(&t.core_cpu[0][0], TU32(k) * TD_POS + TU32(j));
         if (td_has(RC[j], k)) W1.set_bit(c);
         else W0.set_bit(c);
       }
@@ -296,7 +314,7 @@ struct DAcc {
         const TdMask256& W = g ? W1 : W0;
         for (uint64_t x = w == 0 ? W.w0 : w == 1 ? W.w1 : w == 2 ? W.w2 : W.w3; x && needed > 0; x &= x - 1) {
           const int c = w * 64 + __builtin_ctzll(x);
-          take(TU32(t.cpu_core[c]), TU32(t.cpu_pos[c]));
+          take(td_u8(t.cpu_core, TU32(c)), td_u8(t.cpu_pos, TU32(c)));
         }
       }
   }
@@ -322,11 +340,11 @@ struct DAcc {
     const M full = full_cores(keep);
     int best = -1, bsz = 0, bsf = 0;
     for (int n = 0; n < TU32(t.nnodes); ++n) {
-      const M q = full & tm(t.node_cores[n]);
+      const M q = full & tm(t.node_cores[TU32(n)]);
       if (!q) continue;
       const int sz = TU32(t.cpc) * td_pc(q);
       if (sz < needed) continue;
-      const int sf = td_cnt<M, NP>(A, keep & tm(t.sock_cores[TU32(t.node_sock[n])]));
+      const int sf = td_cnt<M, NP>(A, keep & tm(t.sock_cores[td_u8(t.node_sock, TU32(n))]));
       if (best < 0 || sless(sz, bsz) || (sz == bsz && sless(sf, bsf))) { best = n; bsz = sz; bsf = sf; *cores = q; }
     }
     return best;
@@ -336,7 +354,7 @@ struct DAcc {
     const M full = full_cores(~(M)0);
     int best = -1, bsz = 0;
     for (int s = 0; s < TU32(t.nsockets); ++s) {
-      const M q = full & tm(t.sock_cores[s]);
+      const M q = full & tm(t.sock_cores[TU32(s)]);
       if (!q) continue;
       const int sz = TU32(t.cpc) * td_pc(q);
       if (sz < needed) continue;
@@ -350,13 +368,13 @@ struct DAcc {
     int best = -1, bnf = 0, bsf = 0;
     const int cnt = node ? TU32(t.nnodes) : TU32(t.nsockets);
     for (int n = 0; n < cnt; ++n) {
-      const M m = keep & tm(node ? t.node_cores[n] : t.sock_cores[n]);
+      const M m = keep & tm(node ? t.node_cores[TU32(n)] : t.sock_cores[TU32(n)]);
       const int nf = td_cnt<M, NP>(A, m);
       if (nf == 0) continue;
       const int len = fe ? td_pc(td_any<M, NP>(A) & m) : nf;
       if (len < needed) continue;
       if (node) {   // NUMA nodes by (free CPUs, socket free CPUs, id)
-        const int sf = td_cnt<M, NP>(A, keep & tm(t.sock_cores[TU32(t.node_sock[n])]));
+        const int sf = td_cnt<M, NP>(A, keep & tm(t.sock_cores[td_u8(t.node_sock, TU32(n))]));
         if (best < 0 || sless(nf, bnf) || (nf == bnf && sless(sf, bsf))) {
           best = n; bnf = nf; bsf = sf; *cores = m; *L = len;
         }
@@ -384,9 +402,9 @@ struct DAcc {
     TdPack8 ok;
     int nn = 0;
     for (int n = 0; n < TU32(t.nnodes); ++n) {
-      if (!(cores & tm(t.node_cores[n]))) continue;
-      const M sm = tm(t.sock_cores[TU32(t.node_sock[n])]);
-      const int colo = td_cnt<M, NP>(R, sm), sf = td_cnt<M, NP>(S, sm), nf = td_cnt<M, NP>(S, tm(t.node_cores[n]));
+      if (!(cores & tm(t.node_cores[TU32(n)]))) continue;
+      const M sm = tm(t.sock_cores[td_u8(t.node_sock, TU32(n))]);
+      const int colo = td_cnt<M, NP>(R, sm), sf = td_cnt<M, NP>(S, sm), nf = td_cnt<M, NP>(S, tm(t.node_cores[TU32(n)]));
       const uint32_t kn = ((uint32_t)(511 - colo) << 18) | ((uint32_t)dir(sf) << 9) | (uint32_t)dir(nf);
       int i = nn++;   // insertion after the last key <= kn (stable)
       while (i > 0 && (ok.get(i - 1) >> 3) > kn) { ok.set(i, ok.get(i - 1)); --i; }
@@ -399,7 +417,7 @@ struct DAcc {
         M Mg = 0;
         int h = g;
         const uint32_t kg = ok.get(g) >> 3;
-        for (; h < nn && (ok.get(h) >> 3) == kg; ++h) Mg |= cores & tm(t.node_cores[ok.get(h) & 7u]);
+        for (; h < nn && (ok.get(h) >> 3) == kg; ++h) Mg |= cores & tm(t.node_cores[TU32(ok.get(h) & 7u)]);
         g = h;
 #pragma unroll
         for (int v = 1; v <= NP; ++v) {
@@ -408,7 +426,7 @@ struct DAcc {
           if (!Mv) continue;
           for (int s = 0; s < TU32(t.nsockets); ++s)
             for (int rl = 0; rl <= nl; ++rl)
-              for (M q = Mv & tm(t.sock_cores[s]) & ref_level(S, rl); q; q &= q - 1) {
+              for (M q = Mv & tm(t.sock_cores[TU32(s)]) & ref_level(S, rl); q; q &= q - 1) {
                 const int k = td_ctz(q);
                 if (as_is) {
                   for (int pass = 0; pass < 2 && needed > 0; ++pass)
@@ -446,7 +464,7 @@ GS_HD void td_go_sort(TdPack8& e, int n, bool desc) {
 // takeCPUs (cpu_accumulator.go:87-232); avail = planes of the CPUs it may take, rc = the RefCount-1 planes.
 // false: the reference errors.
 template <class M, int NP>
-GS_HD bool td_take_cpus_t(const TopoDev& t, const M* avail, const M* rc, M xc, uint32_t xn, int needed, int bind,
+GS_HD bool td_take_cpus_t(const GS_TOPO_AS TopoDev& t, const M* avail, const M* rc, M xc, uint32_t xn, int needed, int bind,
                           int ep, bool most, M* out) {
   DAcc<M, NP> a(t, avail, rc, xc, xn, needed, ep, most);
 #pragma unroll
@@ -472,7 +490,7 @@ GS_HD bool td_take_cpus_t(const TopoDev& t, const M* avail, const M* rc, M xc, u
       TdPack8 so;   // (size << 3 | socket index)
       int ns = 0;
       for (int s = 0; s < TU32(t.nsockets); ++s) {
-        const M q = fc & a.tm(t.sock_cores[s]);
+        const M q = fc & a.tm(t.sock_cores[TU32(s)]);
         if (!q) continue;
         const int z = TU32(t.cpc) * td_pc(q);
         int i = ns++;
@@ -486,7 +504,7 @@ GS_HD bool td_take_cpus_t(const TopoDev& t, const M* avail, const M* rc, M xc, u
         const uint32_t ei = so.get(i);
         const int idi = (int)(ei & 7u), szi = (int)(ei >> 3);
         if (a.needed < szi) { uo.set(nu++, ei); continue; }
-        for (M b = fc & a.tm(t.sock_cores[idi]); b; b &= b - 1) a.take_core(td_ctz(b), TD_POS);
+        for (M b = fc & a.tm(t.sock_cores[TU32(idi)]); b; b &= b - 1) a.take_core(td_ctz(b), TD_POS);
         ok = a.satisfied();
       }
       if (ok) break;
@@ -494,7 +512,7 @@ GS_HD bool td_take_cpus_t(const TopoDev& t, const M* avail, const M* rc, M xc, u
         td_go_sort(uo, nu, false);
         const int nl = a.ref_levels();
         for (int i = 0; i < nu && !ok; ++i) {
-          const M sc = fc & a.tm(t.sock_cores[uo.get(i) & 7u]);
+          const M sc = fc & a.tm(t.sock_cores[TU32(uo.get(i) & 7u)]);
           M S[NP];
 #pragma unroll
           for (int j = 0; j < NP; ++j) S[j] = a.A[j];
@@ -535,18 +553,18 @@ template <> GS_HD cm_t td_xc<cm_t>(const CpuStateDev& cs) { return ((cm_t)TU64(c
 GS_HD int td_zone_node(const CpuStateDev& cs, int z) { return (int)((TUU(cs.meta) >> (CM_ZIDX_SHIFT + 4 * z)) & 15u); }
 
 // available CPUs (getAvailableCPUs, node_allocation.go:142-162: RefCount < maxRefCount, not reserved) as planes
-template <class M, int NP> GS_HD void td_available(const TopoDev& t, const CpuStateDev& cs, M* P) {
+template <class M, int NP> GS_HD void td_available(const GS_TOPO_AS TopoDev& t, const CpuStateDev& cs, M* P) {
   M U[NP];
   td_unpack<M, NP>(cs.un, U);
 #pragma unroll
-  for (int j = 0; j < NP; ++j) P[j] = td_tm<M>(t.pos_cores[j]) & ~U[j];
+  for (int j = 0; j < NP; ++j) P[j] = td_tm<M>(t.pos_cores[TU32(j)]) & ~U[j];
 }
 
 // allocateCPUSet (resource_manager.go:273-360) given the NUMA split Allocate produced (PlacementDev zkeys /
 // zcpu), the cpuset as packed words. false: the reference errors (cannot follow a feasible Filter; the host fails
 // loudly).
 template <class M, int NP>
-GS_HD bool td_allocate_cpuset_t(const TopoDev& t, const CpuStateDev& cs, int num_cpus, int bind, bool required, int ep,
+GS_HD bool td_allocate_cpuset_t(const GS_TOPO_AS TopoDev& t, const CpuStateDev& cs, int num_cpus, int bind, bool required, int ep,
                                 uint32_t zkeys, const int64_t* zcpu, uint64_t* out_w) {
   M P[NP], RC[NP], out[NP];
   td_available<M, NP>(t, cs, P);
@@ -577,7 +595,7 @@ GS_HD bool td_allocate_cpuset_t(const TopoDev& t, const CpuStateDev& cs, int num
     if (z < 4) {
       if (!((zkeys >> z) & 1u) && !((zkeys >> (4 + z)) & 1u)) continue;
       const int n = td_zone_node(cs, z);
-      const M m = n < TU32(t.nnodes) ? td_tm<M>(t.node_cores[n]) : (M)0;
+      const M m = n < TU32(t.nnodes) ? td_tm<M>(t.node_cores[TU32(n)]) : (M)0;
 #pragma unroll
       for (int j = 0; j < NP; ++j) in[j] = P[j] & m;
       num = td_cnt<M, NP>(in, ~(M)0);
@@ -611,7 +629,7 @@ GS_HD bool td_allocate_cpuset_t(const TopoDev& t, const CpuStateDev& cs, int num
 // exclusive CPUs, the policy it loses is not known here, and xc / xn are marked stale (CM_XSTALE: a later pod whose
 // selection reads them leaves the device path). Returns the number of newly allocated CPUs (RefCount 0 -> 1).
 template <class M, int NP>
-GS_HD int td_reserve_update_t(const TopoDev& t, CpuStateDev& cs, const uint64_t* R_w, int ep, int nz) {
+GS_HD int td_reserve_update_t(const GS_TOPO_AS TopoDev& t, CpuStateDev& cs, const uint64_t* R_w, int ep, int nz) {
   M U[NP], RC[NP], R[NP], NEW[NP];
   td_unpack<M, NP>(cs.un, U);
   td_unpack<M, NP>(cs.rc, RC);
@@ -635,12 +653,12 @@ GS_HD int td_reserve_update_t(const TopoDev& t, CpuStateDev& cs, const uint64_t*
   const M cores = td_any<M, NP>(R);
   if (ep == GS_CPU_EXCLUSIVE_PCPU_LEVEL) xc |= cores;
   else if (ep == GS_CPU_EXCLUSIVE_NUMA_NODE_LEVEL)
-    for (M b = cores; b; b &= b - 1) meta |= 1u << TU32(t.core_node[td_ctz(b)]);
+    for (M b = cores; b; b &= b - 1) meta |= 1u << td_u8(t.core_node, TU32(td_ctz(b)));
   uint64_t zal = TU64(cs.zal);
   for (int z = 0; z < 4; ++z) {
     const int n = td_zone_node(cs, z);
     if (z >= nz || n >= TU32(t.nnodes)) continue;   // a zone the topology lacks keeps its zero summaries
-    const uint64_t zc = ((zal >> (16 * z)) & 0xFFFFull) + (uint64_t)td_cnt<M, NP>(NEW, td_tm<M>(t.node_cores[n]));
+    const uint64_t zc = ((zal >> (16 * z)) & 0xFFFFull) + (uint64_t)td_cnt<M, NP>(NEW, td_tm<M>(t.node_cores[TU32(n)]));
     zal = (zal & ~(0xFFFFull << (16 * z))) | (zc << (16 * z));
   }
   td_pack<M, NP>(U, cs.un);
@@ -655,10 +673,10 @@ GS_HD int td_reserve_update_t(const TopoDev& t, CpuStateDev& cs, const uint64_t*
 
 // available-CPU counts of NUMA node index n (-1: every node): raw | full-core CPUs << 9 | cores with a free CPU
 // << 18, packed as gs_numa_host.cpp count_available
-template <class M, int NP> GS_HD int32_t td_counts_t(const TopoDev& t, const CpuStateDev& cs, int n) {
+template <class M, int NP> GS_HD int32_t td_counts_t(const GS_TOPO_AS TopoDev& t, const CpuStateDev& cs, int n) {
   M P[NP];
   td_available<M, NP>(t, cs, P);
-  const M m = n < 0 ? ~(M)0 : td_tm<M>(t.node_cores[n]);
+  const M m = n < 0 ? ~(M)0 : td_tm<M>(t.node_cores[TU32(n)]);
 #pragma unroll
   for (int j = 0; j < NP; ++j) P[j] &= m;
   const int raw = td_cnt<M, NP>(P, ~(M)0);
@@ -668,36 +686,50 @@ template <class M, int NP> GS_HD int32_t td_counts_t(const TopoDev& t, const Cpu
 }
 
 // the cpuset (packed words) as a 256-bit CPU mask
-template <class M, int NP> GS_HD void td_to_cpus_t(const TopoDev& t, const uint64_t* R_w, uint64_t* w) {
+template <class M, int NP> GS_HD void td_to_cpus_t(const GS_TOPO_AS TopoDev& t, const uint64_t* R_w, uint64_t* w) {
   M R[NP];
   td_unpack<M, NP>(R_w, R);
   TdMask256 W;
 #pragma unroll
   for (int j = 0; j < NP; ++j)
-    for (M b = R[j]; b; b &= b - 1) W.set_bit(TU32(t.core_cpu[td_ctz(b)][j]));
+    for (M b = R[j]; b; b &= b - 1) W.set_bit(td_u8(&t.core_cpu[0][0], TU32(td_ctz(b)) * TD_POS + TU32(j)));
   w[0] = W.w0; w[1] = W.w1; w[2] = W.w2; w[3] = W.w3;
 }
 
+// the topology as the selection reads it (the constant address space on the device)
+GS_HD const GS_TOPO_AS TopoDev& td_topo(const TopoDev& t) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return *(const GS_TOPO_AS TopoDev*)(uint64_t)&t;
+#else
+  return t;
+#endif
+}
+
 // ---- the packed-word API: the shape is the topology's (TopoDev.wide)
-GS_HD bool td_allocate_cpuset(const TopoDev& t, const CpuStateDev& cs, int num_cpus, int bind, bool required, int ep,
+GS_HD bool td_allocate_cpuset(const TopoDev& tg, const CpuStateDev& cs, int num_cpus, int bind, bool required, int ep,
                               uint32_t zkeys, const int64_t* zcpu, uint64_t* out_w) {
+  const GS_TOPO_AS TopoDev& t = td_topo(tg);
   return TU32(t.wide) ? td_allocate_cpuset_t<cm_t, 2>(t, cs, num_cpus, bind, required, ep, zkeys, zcpu, out_w)
                       : td_allocate_cpuset_t<uint64_t, 4>(t, cs, num_cpus, bind, required, ep, zkeys, zcpu, out_w);
 }
-GS_HD int td_reserve_update(const TopoDev& t, CpuStateDev& cs, const uint64_t* R_w, int ep, int nz) {
+GS_HD int td_reserve_update(const TopoDev& tg, CpuStateDev& cs, const uint64_t* R_w, int ep, int nz) {
+  const GS_TOPO_AS TopoDev& t = td_topo(tg);
   return TU32(t.wide) ? td_reserve_update_t<cm_t, 2>(t, cs, R_w, ep, nz)
                       : td_reserve_update_t<uint64_t, 4>(t, cs, R_w, ep, nz);
 }
-GS_HD int32_t td_counts(const TopoDev& t, const CpuStateDev& cs, int n) {
+GS_HD int32_t td_counts(const TopoDev& tg, const CpuStateDev& cs, int n) {
+  const GS_TOPO_AS TopoDev& t = td_topo(tg);
   return TU32(t.wide) ? td_counts_t<cm_t, 2>(t, cs, n) : td_counts_t<uint64_t, 4>(t, cs, n);
 }
-GS_HD void td_to_cpus(const TopoDev& t, const uint64_t* R_w, uint64_t* w) {
+GS_HD void td_to_cpus(const TopoDev& tg, const uint64_t* R_w, uint64_t* w) {
+  const GS_TOPO_AS TopoDev& t = td_topo(tg);
   if (TU32(t.wide)) td_to_cpus_t<cm_t, 2>(t, R_w, w);
   else td_to_cpus_t<uint64_t, 4>(t, R_w, w);
 }
 // takeCPUs over the available CPUs of the state (the self-test's entry; the device selects through allocateCPUSet)
-GS_HD bool td_take_cpus(const TopoDev& t, const CpuStateDev& cs, int needed, int bind, int ep, bool most,
+GS_HD bool td_take_cpus(const TopoDev& tg, const CpuStateDev& cs, int needed, int bind, int ep, bool most,
                         uint64_t* out_w) {
+  const GS_TOPO_AS TopoDev& t = td_topo(tg);
   for (int j = 0; j < 4; ++j) out_w[j] = 0;
   if (TU32(t.wide)) {
     cm_t P[2], RC[2], R[2];

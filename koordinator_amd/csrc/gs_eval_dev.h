@@ -391,7 +391,7 @@ __device__ __noinline__ bool cpuset_reserve(const TopoDev* __restrict__ tp, GS_L
   cpuset = (GS_LDS uint64_t*)(size_t)u32((uint32_t)(size_t)cpuset);
   nf = u32(nf);
   zkeys = u32(zkeys);
-  const TopoDev& t = *(const TopoDev*)tp;
+  const TopoDev& t = *tp;   // (the td_* entry points read it through the constant address space)
   CpuStateDev& cs = *(CpuStateDev*)csp;
   NumaRow& nr = *(NumaRow*)nrp;
   const int64_t zcpu[4] = {u64(zc0), u64(zc1), u64(zc2), u64(zc3)};
@@ -411,7 +411,7 @@ __device__ __noinline__ bool cpuset_reserve(const TopoDev* __restrict__ tp, GS_L
   nr.tfree = (uint32_t)td_counts(t, cs, -1);
   for (int z = 0; z < 4; ++z) {
     const int n = td_zone_node(cs, z);
-    if (z >= nz || n >= TU32(t.nnodes)) continue;   // a zone the topology lacks keeps its zero summaries
+    if (z >= nz || n >= TU32(td_topo(t).nnodes)) continue;   // a zone the topology lacks keeps its zero summaries
     nr.zfree[z] = (uint32_t)td_counts(t, cs, n);
     if (nr.amp > 1.0) {
       const int64_t c = (int64_t)((TU64(cs.zal) >> (16 * z)) & 0xFFFFull) * 1000;
