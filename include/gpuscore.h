@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define GS_ABI_VERSION 5u
+#define GS_ABI_VERSION 6u
 
 /* ---- resource slots (corev1.ResourceName restricted to the hot-path set) ---- */
 enum gs_resource {
@@ -481,6 +481,9 @@ enum gs_gpu_name {
 typedef struct gs_gpu_device {     /* one GPU minor of the node's Device object (deviceshare/device_cache.go:38-56) */
   int32_t minor;
   int32_t has_info;                /* a DeviceInfo exists for the minor (filterNodeDevice, device_allocator.go:139-163) */
+  int32_t numa_node;               /* DeviceInfo.Topology.NodeID (deviceshare/numa_topology.go:46-96); -1: no topology.
+                                      On a node with a NUMA topology policy it must be one of the node's NUMA zones */
+  int32_t pad;
   int64_t total[GS_NUM_GPU_RES];   /* deviceTotal[gpu][minor] (all zero: an unhealthy device) */
   int64_t used[GS_NUM_GPU_RES];    /* deviceUsed[gpu][minor] */
 } gs_gpu_device;

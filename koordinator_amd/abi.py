@@ -10,7 +10,7 @@ import os
 
 import numpy as np
 
-GS_ABI_VERSION = 5
+GS_ABI_VERSION = 6
 GS_NUM_RES = 8
 GS_RES_CPU, GS_RES_MEMORY, GS_RES_EPHEMERAL = 0, 1, 2
 GS_RES_BATCH_CPU, GS_RES_BATCH_MEMORY, GS_RES_MID_CPU, GS_RES_MID_MEMORY = 3, 4, 5, 6
@@ -222,7 +222,8 @@ GS_EXT_FAIL_DEVICE, GS_EXT_FAIL_RESERVATION, GS_EXT_FAIL_POD = 0x1000, 0x2000, 0
 
 
 class GsGpuDevice(C.Structure):
-    _fields_ = [("minor", i32), ("has_info", i32), ("total", i64 * GS_NUM_GPU_RES), ("used", i64 * GS_NUM_GPU_RES)]
+    _fields_ = [("minor", i32), ("has_info", i32), ("numa_node", i32), ("pad", i32), ("total", i64 * GS_NUM_GPU_RES),
+                ("used", i64 * GS_NUM_GPU_RES)]
 
 
 class GsNodeDevices(C.Structure):

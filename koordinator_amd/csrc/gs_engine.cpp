@@ -1152,7 +1152,11 @@ int gpu_request_of(const gs_pod_ext& e, int64_t req[3], uint32_t* mask) {
   }
 }
 
-DevNode dev_image(const gs_node_devices& d) {
+// The HBM image of node i's Device object; a GPU's Topology.NodeID becomes a slot of the node's NUMA zones (the zone
+// masks the topology manager merges), GZ_FOREIGN when it is none of them.
+DevNode dev_image(const gs_ctx* c, uint32_t i) {
+  const gs_node_devices& d = c->devs[i];
+  const gs_node_numa* nn = c->numa_on ? &c->numa[i].cfg : nullptr;
   DevNode o{};
   o.has_device = d.has_device;
   o.num_gpus = d.has_device ? d.num_gpus : 0;
@@ -1160,7 +1164,13 @@ DevNode dev_image(const gs_node_devices& d) {
   for (int x = 0; x < GS_MAX_XRES; ++x) o.fit_free[GS_NUM_GPU_NAMES + x] = d.xres_allocatable[x] - d.xres_requested[x];
   for (int g = 0; g < o.num_gpus; ++g) {
     o.g[g].minor = d.gpus[g].minor;
-    o.g[g].has_info = d.gpus[g].has_info;
+    o.g[g].has_info = d.gpus[g].has_info ? 1 : 0;
+    o.g[g].zone = GZ_NONE;
+    if (d.gpus[g].numa_node >= 0) {
+      o.g[g].zone = GZ_FOREIGN;
+      for (int z = 0; nn && z < nn->num_zones; ++z)
+        if (nn->zones[z].node_id == d.gpus[g].numa_node) o.g[g].zone = (int16_t)z;
+    }
     for (int r = 0; r < 3; ++r) {
       o.g[g].total[r] = d.gpus[g].total[r];
       o.g[g].free[r] = std::max<int64_t>(0, d.gpus[g].total[r] - d.gpus[g].used[r]);
@@ -1173,7 +1183,7 @@ int ext_alloc(gs_ctx* c) {
   if (c->d_dev) return GS_OK;
   HIP_TRY(c, hipMalloc(&c->d_dev, sizeof(DevNode) * std::max<uint32_t>(1, c->N)));
   std::vector<DevNode> img(c->N);
-  for (uint32_t i = 0; i < c->N; ++i) img[i] = dev_image(c->devs[i]);
+  for (uint32_t i = 0; i < c->N; ++i) img[i] = dev_image(c, i);
   HIP_TRY(c, hipMemcpy(c->d_dev, img.data(), sizeof(DevNode) * c->N, hipMemcpyHostToDevice));
   c->dev_dirty_list.clear();
   std::fill(c->dev_dirty.begin(), c->dev_dirty.end(), 0);
@@ -1192,7 +1202,7 @@ int ext_flush_devices(gs_ctx* c) {
   if (c->dev_dirty_list.empty()) return GS_OK;
   if (!c->d_dev) return ext_alloc(c);
   for (uint32_t i : c->dev_dirty_list) {
-    const DevNode img = dev_image(c->devs[i]);
+    const DevNode img = dev_image(c, i);
     HIP_TRY(c, hipMemcpy(c->d_dev + i, &img, sizeof(DevNode), hipMemcpyHostToDevice));
     c->dev_dirty[i] = 0;
   }
@@ -1228,11 +1238,13 @@ bool is_ext_pod(const gs_ctx* c, const gs_pod_ext& e) {
 }
 
 // DeviceShare Reserve (deviceshare/plugin.go:377-430) on the host mirror: defaultAllocateDevices with the scorer
-// (device_allocator.go:397-467; minors by device score descending, then minor)
-int ext_device_reserve(gs_ctx* c, uint32_t node, const int64_t preq[3], uint32_t pmask, gs_ext_placement* eo) {
+// (device_allocator.go:397-467; minors by device score descending, then minor), within the node's NUMA affinity
+// (aff: 0x10 | zone-slot mask, 0 = none; device_allocator.go:148-152)
+int ext_device_reserve(gs_ctx* c, uint32_t node, const int64_t preq[3], uint32_t pmask, gs_ext_placement* eo,
+                       uint32_t aff) {
   gs_node_devices& d = c->devs[node];
   if (!d.has_device) return GS_OK;
-  const DevNode img = dev_image(d);
+  const DevNode img = dev_image(c, node);
   int64_t total_mem = -1;
   for (int g = 0; g < img.num_gpus; ++g)
     if (img.g[g].total[0] | img.g[g].total[1] | img.g[g].total[2]) { total_mem = img.g[g].total[2]; break; }
@@ -1248,6 +1260,7 @@ int ext_device_reserve(gs_ctx* c, uint32_t node, const int64_t preq[3], uint32_t
   std::vector<Cand> cs;
   for (int g = 0; g < img.num_gpus; ++g) {
     if (!img.g[g].has_info) continue;
+    if ((aff & 0x10u) && (img.g[g].zone < 0 || !(aff >> img.g[g].zone & 1u))) continue;
     int64_t ns = 0, ws = 0;   // scoreDevice (deviceshare/scoring.go:186-211)
     for (int r = 0; r < 3; ++r) {
       const int64_t w = c->ext.device_weights[r], t = img.g[g].total[r], f = img.g[g].free[r];
@@ -1335,6 +1348,9 @@ int ext_schedule_one(gs_ctx* c, const gs_pod& pod, const gs_pod_ext& e, uint64_t
     while (b < matched.size() && matched[b].first == node) ++b;
     if (b - a > (size_t)EXT_MAX_RES_PER_NODE)
       return fail(c, GS_EUNSUPPORTED, "more than %d matched reservations on node %u", EXT_MAX_RES_PER_NODE, node);
+    if (c->numa_on && c->numa[node].cfg.numa_topology_policy != GS_NUMA_POLICY_NONE)   // (no NUMA restore of a
+      return fail(c, GS_EUNSUPPORTED,                                                  // reservation's resources)
+                  "a matched reservation on node %u, which has a NUMA topology policy, is not on the device path", node);
     ExtRec rec{};
     rec.node = node;
     rec.nres = (int32_t)(b - a);
@@ -1436,8 +1452,6 @@ int ext_schedule_one(gs_ctx* c, const gs_pod& pod, const gs_pod_ext& e, uint64_t
     }
     c->numa_idx_stale = false;
   }
-  if (c->numa_on && c->numa_n)   // the NUMA-policy Reserve (zone split by the Filter-time hint) is not on this path
-    return fail(c, GS_EUNSUPPORTED, "Reservation / DeviceShare pods with NUMA-policy nodes in the cluster");
   const int prod_cols = (v.flags & PF_PROD_SCORE) ? 1 : 0;
   HIP_TRY(c, hipMemcpyAsync(c->d_pods, c->h_pods, sizeof(PodVec), hipMemcpyHostToDevice, c->st));
   HIP_TRY(c, hipMemcpyAsync(c->d_xpod, c->h_xpod, sizeof(ExtPod), hipMemcpyHostToDevice, c->st));
@@ -1452,8 +1466,14 @@ int ext_schedule_one(gs_ctx* c, const gs_pod& pod, const gs_pod_ext& e, uint64_t
   HIP_TRY(c, launch_ext_nodes(c->d_dev, c->d_S, c->n0, c->n1, c->d_xpod, c->d_xtot, c->d_xds, c->d_xrs, c->st));
   HIP_TRY(c, launch_ext_matched(c->mv, c->d_pods, c->pf, prod_cols, c->d_dev, c->d_xpod, c->d_xrec, c->d_xres, nrec, c->d_xtot,
                                 c->d_xrs, c->d_xnom, c->d_xT, c->n1 - c->n0, c->st));
+  // GPU pods on NUMA-policy nodes: DeviceShare is the topology manager's second hint provider
+  if (gmask && c->numa_on && c->numa_n)
+    HIP_TRY(c, launch_ext_numa(c->mv, c->d_pods, c->pf, prod_cols, c->d_dev, c->d_xpod, c->d_numa_idx, c->numa_n, c->n0,
+                               c->d_xtot, c->d_xds, c->d_aff, c->d_xT, c->n1 - c->n0, c->st));
   HIP_TRY(c, launch_ext_select(c->d_xtot, c->d_xds, c->d_xrs, c->d_xrec, c->n0, c->n1, c->d_xpod, c->cfg.seed, c->d_xT,
                                c->d_xout, c->st));
+  if (c->numa_on)   // NodeNUMAResource Reserve of the selected node along its affinity
+    HIP_TRY(c, launch_ext_reserve_numa(c->mv, c->d_pods, c->pf, prod_cols, c->d_aff, c->n0, c->d_xout, c->st));
   HIP_TRY(c, hipEventRecord(c->ev[4], c->st));
   HIP_TRY(c, hipMemcpyAsync(c->h_xout, c->d_xout, sizeof(ExtOut), hipMemcpyDeviceToHost, c->st));
   if (nrec) HIP_TRY(c, hipMemcpyAsync(c->h_xnom, c->d_xnom, 4 * nrec, hipMemcpyDeviceToHost, c->st));
@@ -1465,6 +1485,10 @@ int ext_schedule_one(gs_ctx* c, const gs_pod& pod, const gs_pod_ext& e, uint64_t
   c->stats.batches += 1;
   c->stats.pods += 1;
   const ExtOut xo = *c->h_xout;
+  if (xo.err & 1u)
+    return fail(c, GS_EUNSUPPORTED, "a GPU's NUMA node is not one of its node's NUMA zones (DeviceShare hints)");
+  if (xo.err & 2u)
+    return fail(c, GS_EUNSUPPORTED, "the topology-manager merge of a GPU pod exceeds its permutation bound");
   out->feasible = xo.feasible;
   if (xo.node < 0) return GS_OK;
   out->node = xo.node;
@@ -1473,8 +1497,17 @@ int ext_schedule_one(gs_ctx* c, const gs_pod& pod, const gs_pod_ext& e, uint64_t
   eo->deviceshare_score = xo.ds_norm;
   eo->reservation_score = xo.rs_norm;
   const uint32_t node = (uint32_t)xo.node;
-  // ---- Reserve
-  if (gmask && (rc = ext_device_reserve(c, node, greq, gmask, eo))) return rc;
+  // ---- Reserve: NodeNUMAResource (the zones the device allocated along the affinity), DeviceShare, Reservation
+  if (c->numa_on) {
+    PlacementDev pd{};
+    pd.node = xo.node;
+    pd.flags = xo.nflags;
+    pd.zkeys = xo.zkeys;
+    for (int z = 0; z < 4; ++z) { pd.zcpu[z] = xo.zcpu[z]; pd.zmem[z] = xo.zmem[z]; }
+    if ((rc = numa_reserve(c, pod, v, pd))) return rc;
+    out->flags = xo.nflags & ~PL_INTERNAL_FLAGS;
+  }
+  if (gmask && (rc = ext_device_reserve(c, node, greq, gmask, eo, xo.aff))) return rc;
   int rec_i = -1;   // the chosen node's matched record (records are in node order)
   {
     auto it = std::lower_bound(c->xrec.begin(), c->xrec.end(), node,
@@ -2422,6 +2455,7 @@ int gs_nodes_numa_upsert(gs_ctx* c, const uint32_t* idx, const gs_node_numa* nn,
     NumaNode& st = c->numa[i];
     if (st.cfg.numa_topology_policy != x.numa_topology_policy) c->numa_idx_stale = true;
     st.cfg = x;
+    if (c->devs[i].has_device) dev_mark(c, i);   // its GPUs' zone slots (dev_image)
     st.topo = !x.has_options ? nullptr : (x.topology >= 0 ? c->topos[x.topology] : c->empty_topo);
     mark_dirty(c, i);
   }

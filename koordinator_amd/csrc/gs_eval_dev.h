@@ -126,9 +126,12 @@ struct SlotsLds {
 // NUMA_POLICY_NODES = false: NodeNUMAResource's topology-policy path is compiled out (eval_kernel routes those
 // nodes to eval_numa_kernel)
 // table: the row's NUMA hint table (commit re-scoring of one row for many pods), else computed from the row.
-template <bool FULL, bool LDS_SCALARS, bool NUMA_POLICY_NODES = true, bool TABLE = false, bool WAVE = false>
+// GPROV / gh / gh_over: DeviceShare as a second NUMA hint provider (numa_eval; the extension path's GPU pods).
+template <bool FULL, bool LDS_SCALARS, bool NUMA_POLICY_NODES = true, bool TABLE = false, bool WAVE = false,
+          bool GPROV = false>
 __device__ __forceinline__ PairOut eval_pair(const Row& r, const PodVec& p, const Profile& pf, const MirrorView& m,
-                                             const HintTable* table = nullptr) {
+                                             const HintTable* table = nullptr, uint32_t gh = 0,
+                                             bool* gh_over = nullptr) {
   PairOut o{0u, 0, 0, 0, 0u};
   // ---- [upstream] noderesources Fit.Filter -> fitsRequest
   if (pf.enabled & 0x1u) {
@@ -156,8 +159,9 @@ __device__ __forceinline__ PairOut eval_pair(const Row& r, const PodVec& p, cons
   // ---- NodeNUMAResource Filter (+ Admit) and Score (gs_numa_dev.h)
   if (pf.enabled & 0x30u) {
     NumaOut no;
-    if (LDS_SCALARS) no = numa_eval<NUMA_POLICY_NODES, TABLE, WAVE>(r.nr, p, pf, SlotsLds{r, m}, pf.enabled & 0x10u,
-                                                              pf.enabled & 0x20u, -1, table);
+    if (LDS_SCALARS) no = numa_eval<NUMA_POLICY_NODES, TABLE, WAVE, GPROV>(r.nr, p, pf, SlotsLds{r, m},
+                                                                     pf.enabled & 0x10u, pf.enabled & 0x20u, -1,
+                                                                     table, gh, gh_over);
     else no = numa_eval<NUMA_POLICY_NODES>(r.nr, p, pf, SlotsHbm{r, m}, pf.enabled & 0x10u, pf.enabled & 0x20u);
     if (pf.enabled & 0x10u) o.code |= no.reason << GS_FAIL_NUMA_SHIFT;
     if (!FULL && o.code) return o;

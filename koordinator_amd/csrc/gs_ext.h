@@ -23,8 +23,11 @@ struct DevGpu {                 // one GPU minor after filterNodeDevice (has_inf
   int64_t total[3];             // gpu-core, gpu-memory-ratio, gpu-memory
   int64_t free[3];              // SubtractWithNonNegativeResult(total, used)
   int32_t minor;
-  int32_t has_info;
+  int16_t has_info;
+  int16_t zone;                 // Topology.NodeID as a slot of the node's NUMA zones; GZ_NONE: no topology,
+                                // GZ_FOREIGN: a NUMA node that is not one of the node's zones
 };
+constexpr int16_t GZ_NONE = -1, GZ_FOREIGN = -2;
 constexpr int EXT_FIT_NAMES = GS_NUM_GPU_NAMES + GS_MAX_XRES;   // Fit scalars of the extension path: GPU names, then
                                                                   // the registered extended resources
 struct DevNode {                // gs_node_devices, as the kernels read it
@@ -84,6 +87,13 @@ struct ExtOut {
   int32_t ds_norm, rs_norm;
   int32_t pref_node;            // PreScore preferred node (-1: none)
   int32_t pad;
+  // NodeNUMAResource Reserve of the chosen node (ext_reserve_numa_kernel): the allocation by the Filter-time hint
+  uint32_t nflags;              // NumaOut.flags (GS_PLACED_NUMA, affinity bits), PL_RESERVE_FAILED
+  uint32_t zkeys;
+  int64_t zcpu[4], zmem[4];
+  uint32_t aff;                 // 0x10 | zone-slot mask, 0: none (DeviceShare Reserve allocates within it)
+  uint32_t err;                 // from ext_numa_kernel: 1 a GPU on a NUMA node outside the zones, 2 a merge past its
+                                // permutation bound (the host fails loudly)
 };
 
 hipError_t launch_ext_nodes(const DevNode* dev, const int16_t* S, uint32_t n0, uint32_t n1, const ExtPod* pod,
@@ -91,6 +101,17 @@ hipError_t launch_ext_nodes(const DevNode* dev, const int16_t* S, uint32_t n0, u
 hipError_t launch_ext_matched(const MirrorView& m, const PodVec* pods, const Profile& pf, int prod_cols,
                               const DevNode* dev, const ExtPod* pod, const ExtRec* recs, const ExtRes* res, int nrec, int32_t* tot,
                               int16_t* rs, int32_t* nominated, int32_t* scratch, uint32_t len, hipStream_t st);
+// GPU pods on the NUMA-topology-policy nodes (idx, absolute node indices): Filter + Score again with DeviceShare as the
+// topology manager's second hint provider, the affinity (aff, the eval pass layout) and DeviceShare Filter / raw Score
+// within it; overwrites tot / ds of those nodes (after launch_ext_matched, before launch_ext_select: its error word
+// lives in the select scratch, whose accumulators launch_ext_matched resets).
+hipError_t launch_ext_numa(const MirrorView& m, const PodVec* pods, const Profile& pf, int prod_cols, const DevNode* dev,
+                           const ExtPod* pod, const uint32_t* idx, uint32_t nidx, uint32_t n0, int32_t* tot, int16_t* ds,
+                           uint8_t* aff, int32_t* scratch, uint32_t len, hipStream_t st);
+// NodeNUMAResource Reserve of the selected node along its Filter-time affinity (aff) -> ExtOut.nflags / zkeys / zcpu /
+// zmem / aff
+hipError_t launch_ext_reserve_numa(const MirrorView& m, const PodVec* pods, const Profile& pf, int prod_cols,
+                                   const uint8_t* aff, uint32_t n0, ExtOut* out, hipStream_t st);
 size_t ext_select_scratch_words(uint32_t len);   // int32 words of launch_ext_select's scratch
 hipError_t launch_ext_select(const int32_t* tot, const int16_t* ds, const int16_t* rs, const ExtRec* recs, uint32_t n0,
                              uint32_t n1, const ExtPod* pod, uint64_t seed, int32_t* scratch, ExtOut* out,

@@ -64,7 +64,14 @@ __device__ __forceinline__ bool fit_names_ok(const DevNode& d, const ExtPod& p) 
   return true;
 }
 
-__device__ __forceinline__ void eval_device(const DevNode& d, const ExtPod& p, bool* ok, int32_t* raw) {
+// aff: the node's NUMA affinity (0x10 | zone-slot mask; 0 = none): filterNodeDevice keeps only the minors whose
+// Topology is on it (device_allocator.go:139-163)
+__device__ __forceinline__ bool on_aff(const DevGpu& x, uint32_t aff) {
+  return !(aff & 0x10u) || (x.zone >= 0 && (aff >> x.zone & 1u));
+}
+
+__device__ __forceinline__ void eval_device(const DevNode& d, const ExtPod& p, bool* ok, int32_t* raw,
+                                            uint32_t aff = 0) {
   *ok = true;
   *raw = 0;
   if (!fit_names_ok(d, p)) { *ok = false; return; }
@@ -80,7 +87,7 @@ __device__ __forceinline__ void eval_device(const DevNode& d, const ExtPod& p, b
   if (!all_zero) {
     for (int g = 0; g < d.num_gpus; ++g) {
       const DevGpu& x = d.g[g];
-      if (!x.has_info) continue;
+      if (!x.has_info || !on_aff(x, aff)) continue;
       for (int r = 0; r < 3; ++r) { tot[r] += x.total[r]; fr[r] += x.free[r]; }
       if (!(x.free[0] | x.free[1] | x.free[2])) continue;
       if (fits_inst(inst, mask, x)) ++ok_n;
@@ -116,6 +123,45 @@ __global__ __launch_bounds__(256) void ext_nodes_kernel(const DevNode* __restric
   tot[i - n0] = t;
   ds[i - n0] = (int16_t)(t >= 0 ? raw : 0);
   rs[i - n0] = 0;
+}
+
+// DeviceShare GetPodTopologyHints (topology_hint.go:108-214) on one node with nz NUMA zones, packed as GH_* (gs_numa_dev.h).
+// IterateBitMasks over the zones holding GPUs with a Topology visits exactly the positions whose mask lies within that
+// zone set, in position order. *bad: a GPU on a NUMA node outside the node's zones.
+__device__ uint32_t gpu_hint_word(const DevNode& d, const ExtPod& p, int nz, bool* bad) {
+  if (!d.has_device || !p.gpu_mask) return 0;
+  uint32_t zs = 0;   // numaTopology.nodes
+  for (int g = 0; g < d.num_gpus; ++g) {
+    if (!d.g[g].has_info) continue;
+    if (d.g[g].zone == GZ_FOREIGN) *bad = true;
+    if (d.g[g].zone >= 0) zs |= 1u << d.g[g].zone;
+  }
+  int64_t inst[3];
+  uint32_t mask;
+  int64_t count;
+  if (!zs || !gpu_desired(d, p, inst, &mask, &count)) return 0;   // no mask visited / Prepare fails: no hints
+  bool all_zero = true;
+  for (int g = 0; g < d.num_gpus; ++g) all_zero &= !(d.g[g].free[0] | d.g[g].free[1] | d.g[g].free[2]);
+  const uint32_t valid = ord_valid(nz);
+  int minsz = -1;
+  uint32_t list = 0;
+  for (int mi = 0; mi < 15; ++mi) {
+    const uint32_t mk = ord_mask(mi);
+    if (!(valid >> mi & 1u) || (mk & ~zs)) continue;
+    int64_t total = 0, ok_n = 0;   // calcTotalDevicesByNUMA; the allocation within the mask
+    for (int g = 0; g < d.num_gpus; ++g) {
+      const DevGpu& x = d.g[g];
+      if (!x.has_info || x.zone < 0 || !(mk >> x.zone & 1u)) continue;
+      ++total;
+      if (!all_zero && (x.free[0] | x.free[1] | x.free[2]) && fits_inst(inst, mask, x)) ++ok_n;
+    }
+    if (total < count) continue;
+    if (minsz < 0) minsz = __popc(zs);
+    if (__popc(mk) < minsz) minsz = __popc(mk);
+    if (ok_n >= count) list |= 1u << mi;
+  }
+  if (minsz < 0) return 0;   // minAffinitySize nil: an empty map
+  return list | ((uint32_t)minsz << GH_MIN_SHIFT) | ((uint32_t)__popc(mask) << GH_R_SHIFT);
 }
 
 // fitsNode (plugin.go:444-496), preemptible = 0: number of insufficient resources
@@ -162,7 +208,59 @@ __device__ int64_t score_reservation(const ExtPod& p, const ExtRes& r) {
 }
 
 constexpr int SEL_BLOCK = 256;
-enum { ACC_DS = 0, ACC_RS = 1, ACC_FEAS = 2, ACC_MAX = 3, ACC_DONE = 4, ACC_TIES = 5, ACC_PREF = 6, ACC_WORDS = 8 };
+enum { ACC_DS = 0, ACC_RS = 1, ACC_FEAS = 2, ACC_MAX = 3, ACC_DONE = 4, ACC_TIES = 5, ACC_PREF = 6, ACC_ERR = 7,
+       ACC_WORDS = 8 };
+
+// GPU pods on NUMA-policy nodes: the pair again with DeviceShare as the second hint provider (the eval pass merged
+// NodeNUMAResource's hints alone), then Fit's GPU scalars and DeviceShare Filter / raw Score within the affinity
+// (the topology manager's Admit -> DeviceShare.Allocate, topology_hint.go:57-106; Filter / Score, plugin.go:272-322,
+// scoring.go:34-89, read the same store entry).
+__global__ __launch_bounds__(256) void ext_numa_kernel(MirrorView m, const PodVec* __restrict__ pods, Profile pf,
+                                                       int prod_cols, const DevNode* __restrict__ dev,
+                                                       const ExtPod* __restrict__ pp, const uint32_t* __restrict__ idx,
+                                                       uint32_t nidx, uint32_t n0, int32_t* tot, int16_t* ds,
+                                                       uint8_t* aff, int32_t* acc) {
+  const uint32_t t = blockIdx.x * 256 + threadIdx.x;
+  if (t >= nidx) return;
+  const ExtPod& p = *pp;
+  const uint32_t i = idx[t];
+  Row r;
+  load_row(m, i, prod_cols != 0, true, r);
+  for (int s = 3; s < 7; ++s) r.free[s] = m.c64(C_FREE_CPU + s)[i];
+  const int nz = (r.nr.nflags >> NF_ZONES_SHIFT) & 7;
+  bool bad = false, over = false;
+  const uint32_t gh = gpu_hint_word(dev[i], p, nz, &bad);
+  const PairOut o = eval_pair<false, true, true, false, false, true>(r, pods[0], pf, m, nullptr, gh, &over);
+  int32_t t_sc = total_score(o, pf);
+  int32_t raw = 0;
+  if (t_sc >= 0 && (p.gpu_mask || p.gpu_names)) {
+    bool ok;
+    eval_device(dev[i], p, &ok, &raw, o.aff);
+    if (!ok) t_sc = -1;
+  }
+  if (p.required) t_sc = -1;
+  tot[i - n0] = t_sc;
+  ds[i - n0] = (int16_t)(t_sc >= 0 ? raw : 0);
+  aff[i - n0] = (uint8_t)(o.code ? 0u : o.aff);
+  if (bad || over) atomicOr(&acc[ACC_ERR], (bad ? 1 : 0) | (over ? 2 : 0));
+}
+
+// NodeNUMAResource Reserve (plugin.go:375-422) of the selected node: Allocate along its Filter-time affinity
+__global__ __launch_bounds__(64) void ext_reserve_numa_kernel(MirrorView m, const PodVec* __restrict__ pods, Profile pf,
+                                                              int prod_cols, const uint8_t* __restrict__ aff, uint32_t n0,
+                                                              ExtOut* out) {
+  if (threadIdx.x != 0) return;
+  const int32_t node = out->node;
+  if (node < 0) return;
+  Row r;
+  load_row(m, (uint32_t)node, prod_cols != 0, true, r);
+  for (int s = 3; s < 7; ++s) r.free[s] = m.c64(C_FREE_CPU + s)[node];
+  const NumaOut no = numa_eval<true>(r.nr, pods[0], pf, SlotsLds{r, m}, true, false, aff[node - n0]);
+  out->nflags = no.flags | (no.reason ? PL_RESERVE_FAILED : 0u);
+  out->zkeys = no.zkeys;
+  for (int z = 0; z < 4; ++z) { out->zcpu[z] = no.zcpu[z]; out->zmem[z] = no.zmem[z]; }
+  out->aff = no.aff;
+}
 
 // one matched node (record k): the restored row re-evaluated, Reservation Filter, NominateReservation, raw Score
 __device__ __forceinline__ void matched_one(const MirrorView& m, const PodVec* __restrict__ pods, const Profile& pf,
@@ -349,8 +447,13 @@ __global__ __launch_bounds__(SEL_BLOCK) void ext_ties_kernel(const int32_t* __re
   __threadfence();
   const int32_t F = __atomic_load_n(&acc[ACC_FEAS], __ATOMIC_RELAXED);
   const int32_t pref = acc[ACC_PREF];
+  const uint32_t err = (uint32_t)__atomic_load_n(&acc[ACC_ERR], __ATOMIC_RELAXED);
   if (M < 0) {
-    if (threadIdx.x == 0) *out = ExtOut{-1, (uint32_t)F, 0, 0, -1, 0, 0, pref, 0};
+    if (threadIdx.x == 0) {
+      ExtOut o{};
+      o.node = -1; o.feasible = (uint32_t)F; o.rec = -1; o.pref_node = pref; o.err = err;
+      *out = o;
+    }
     return;
   }
   // the last block: thread t owns block counts [t*per, (t+1)*per); a block scan gives every range its tie offset
@@ -396,8 +499,10 @@ __global__ __launch_bounds__(SEL_BLOCK) void ext_ties_kernel(const int32_t* __re
     const int64_t dsn = MDS ? kMaxNodeScore * ds[jj] / MDS : ds[jj];
     const int64_t rr = node == pref ? 1000 : rs[jj];
     const int64_t rsn = MRS ? kMaxNodeScore * rr / MRS : rr;
-    *out = ExtOut{node, (uint32_t)F, M, (uint32_t)ties, -1, (int32_t)(p.ds_on ? dsn : 0), (int32_t)(p.rs_on ? rsn : 0),
-                  pref, 0};
+    ExtOut o{};
+    o.node = node; o.feasible = (uint32_t)F; o.score = M; o.ties = (uint32_t)ties; o.rec = -1;
+    o.ds_norm = (int32_t)(p.ds_on ? dsn : 0); o.rs_norm = (int32_t)(p.rs_on ? rsn : 0); o.pref_node = pref; o.err = err;
+    *out = o;
   }
 }
 
@@ -435,6 +540,21 @@ hipError_t launch_ext_select(const int32_t* tot, const int16_t* ds, const int16_
   hipLaunchKernelGGL(ext_total_kernel, dim3(blocks), dim3(SEL_BLOCK), 0, st, tot, ds, rs, recs, n0, len, pod, T, acc);
   hipLaunchKernelGGL(ext_ties_kernel, dim3(blocks), dim3(SEL_BLOCK), 0, st, T, ds, rs, n0, len, pod, seed, acc, bcnt,
                      out);
+  return hipGetLastError();
+}
+
+hipError_t launch_ext_numa(const MirrorView& m, const PodVec* pods, const Profile& pf, int prod_cols, const DevNode* dev,
+                           const ExtPod* pod, const uint32_t* idx, uint32_t nidx, uint32_t n0, int32_t* tot, int16_t* ds,
+                           uint8_t* aff, int32_t* scratch, uint32_t len, hipStream_t st) {
+  if (!nidx) return hipSuccess;
+  hipLaunchKernelGGL(ext_numa_kernel, dim3((nidx + 255) / 256), dim3(256), 0, st, m, pods, pf, prod_cols, dev, pod, idx,
+                     nidx, n0, tot, ds, aff, scratch + len);
+  return hipGetLastError();
+}
+
+hipError_t launch_ext_reserve_numa(const MirrorView& m, const PodVec* pods, const Profile& pf, int prod_cols,
+                                   const uint8_t* aff, uint32_t n0, ExtOut* out, hipStream_t st) {
+  hipLaunchKernelGGL(ext_reserve_numa_kernel, dim3(1), dim3(64), 0, st, m, pods, pf, prod_cols, aff, n0, out);
   return hipGetLastError();
 }
 

@@ -359,6 +359,154 @@ __device__ __forceinline__ bool merge_hint_lists(uint32_t totc, uint32_t lc, uin
   return true;
 }
 
+// ---- a second hint provider: DeviceShare (deviceshare/topology_hint.go:33-214), the extension path's GPU pods
+// Its hints for one node, packed: bits 0-14 the IterateBitMasks positions that hold a hint (masks over the zones of the
+// node's GPUs with enough devices in total, where the GPU allocation succeeds), bits 16-18 the size minimum over the
+// masks with enough devices (hints of that size are preferred), bits 20-21 the number of resource names of the
+// per-instance request (each gets the same list; 0 = the provider has no hints: its preferred any-numa hint is
+// neutral). No position with r > 0: every list is empty ({nil, not preferred} in filterProvidersHints).
+constexpr uint32_t GH_LIST = 0x7FFFu, GH_MIN_SHIFT = 16, GH_R_SHIFT = 20;
+
+struct HintList {        // one list of filterProvidersHints' output
+  uint32_t set;          // IterateBitMasks positions of its hints, or bit 31 alone: one mask-less hint
+  int8_t min;            // hint size that is preferred (position lists)
+  bool pseudo_pref;      // the mask-less hint's Preferred
+  bool scored;           // NodeNUMAResource's lists carry hint scores (DeviceShare's score 0)
+};
+constexpr int kGenMergeMax = 1 << 16;   // permutations one pass may visit (the caller fails loudly beyond)
+
+// topologyManager Merge over any provider lists (policy.go:128-186, policy_*.go), lists in filterProvidersHints
+// order: the exact permutation scan of mergeFilteredHints in its visiting order, reduced preferred-first like
+// merge_hint_lists (pass 0 over the preferred entries; pass 1, all entries, only when no preferred permutation merges
+// to a non-empty mask). *over: a pass exceeded kGenMergeMax permutations (the result is then not used).
+template <class ScoreAt>
+__device__ __noinline__ bool merge_hint_lists_gen(const HintList* L, int nl, int nz, int policy, ScoreAt&& score_at,
+                                                  bool& aff_has, uint32_t& aff, bool& over) {
+  const bool single = policy == GS_NUMA_POLICY_SINGLE_NUMA_NODE;
+  const uint32_t full_mask = (1u << nz) - 1u;
+  constexpr uint32_t PSEUDO = 0x80000000u;
+  uint32_t s0[6], s1[6];
+  for (int l = 0; l < nl; ++l) {
+    uint32_t all, pref;
+    if (L[l].set == PSEUDO) {
+      all = PSEUDO;
+      pref = L[l].pseudo_pref ? PSEUDO : 0u;
+    } else {
+      all = L[l].set;
+      pref = 0;
+      for (uint32_t rr = all; rr; rr &= rr - 1) {
+        const int mi = __ffs(rr) - 1;
+        if (__popc(ord_mask(mi)) == L[l].min) pref |= 1u << mi;
+      }
+    }
+    if (single) {   // policy_single_numa_node.go:48-78: preferred mask-less or preferred single-zone hints only
+      all = (L[l].set == PSEUDO) ? pref : (L[l].min == 1 ? pref & 0xFu : 0u);
+      pref = all;
+    }
+    s0[l] = pref;
+    s1[l] = all;
+  }
+  bool b_pref = false;
+  uint32_t b_mask = full_mask;
+  int32_t b_score = 0;
+  over = false;
+  for (int pass = 0; pass < 2; ++pass) {
+    if (pass == 1) {
+      if (b_pref) break;
+      b_mask = full_mask;
+      b_score = 0;
+    }
+    const uint32_t* S = pass ? s1 : s0;
+    bool empty = false;
+    for (int l = 0; l < nl; ++l) empty |= S[l] == 0;
+    if (empty) continue;   // a list without entries: no permutation
+    uint32_t rem[6];
+    for (int l = 0; l < nl; ++l) rem[l] = S[l];
+    int visited = 0;
+    while (true) {
+      if (++visited > kGenMergeMax) { over = true; break; }
+      uint32_t mg = full_mask;
+      bool pg = true;
+      for (int l = 0; l < nl; ++l) {
+        const int e = __ffs(rem[l]) - 1;
+        if (e == 31) {
+          pg = pg && L[l].pseudo_pref;
+        } else {
+          mg &= ord_mask(e);
+          pg = pg && __popc(ord_mask(e)) == L[l].min;
+        }
+      }
+      if (mg != 0 && !(!pg && b_pref)) {
+        const bool nar = narrower(mg, b_mask);
+        if ((pg && !b_pref) || nar || __popc(mg) == __popc(b_mask)) {
+          int32_t sg = 0;
+          for (int l = 0; l < nl; ++l) {
+            const int e = __ffs(rem[l]) - 1;
+            if (e != 31 && L[l].scored && ord_mask(e) == mg) { const int32_t x = score_at(e); if (x > sg) sg = x; }
+          }
+          if (pg && !b_pref) { b_mask = mg; b_pref = true; b_score = sg; }
+          else if (nar) { b_mask = mg; b_pref = pg; b_score = sg; }
+          else if (sg > b_score) { b_mask = mg; b_pref = pg; b_score = sg; }
+        }
+      }
+      int l = nl - 1;   // next permutation: the last list varies fastest
+      rem[l] &= rem[l] - 1;
+      while (rem[l] == 0 && l > 0) {
+        rem[l] = S[l];
+        --l;
+        rem[l] &= rem[l] - 1;
+      }
+      if (rem[0] == 0) break;
+    }
+  }
+  aff_has = true;
+  aff = b_mask;
+  if (single) {
+    if (b_mask == full_mask) aff_has = false;
+    return b_pref;
+  }
+  if (policy == GS_NUMA_POLICY_RESTRICTED) return b_pref;
+  return true;
+}
+
+// GetPodTopologyHints of both providers + Merge: NodeNUMAResource's lists from the row (every position summed), then
+// DeviceShare's (gh, above). *over: see merge_hint_lists_gen.
+template <class Src>
+__device__ __noinline__ bool hints_merge_gprov(const Src& src, int nz, int policy, bool nil_hints, bool has_cpu,
+                                               bool has_mem, int64_t pcpu, int64_t mem, bool tot_c_any, bool tot_m_any,
+                                               const Profile& pf, uint32_t gh, bool& aff_has, uint32_t& aff,
+                                               bool& over) {
+  const uint32_t valid = ord_valid(nz);
+  uint32_t totc = 0, totm = 0, lc = 0, lm = 0;
+  if (!nil_hints) {
+    for (int mi = 0; mi < 15; ++mi) {
+      if (!(valid >> mi & 1u)) continue;
+      const HintSums s = src.sum(mi);
+      if (has_cpu && s.tc >= pcpu) { totc |= 1u << mi; if (s.fc >= pcpu) lc |= 1u << mi; }
+      if (has_mem && s.tm >= mem) { totm |= 1u << mi; if (s.fm >= mem) lm |= 1u << mi; }
+    }
+  }
+  HintList L[5];
+  int nl = 0;
+  // NodeNUMAResource (the first provider): cpu, then memory (sorted names); kind as merge_hint_lists reads them
+  const int kc = nil_hints ? 0 : (lc ? 1 : ((has_cpu && tot_c_any) ? 2 : 0));
+  const int km = nil_hints ? 0 : (lm ? 1 : ((has_mem && tot_m_any) ? 2 : 0));
+  if (kc == 0 && km == 0) {
+    L[nl++] = HintList{0x80000000u, 0, true, false};   // no hints: one preferred any-numa hint
+  } else {
+    if (kc == 1) L[nl++] = HintList{lc, (int8_t)ord_size_first(totc), false, true};
+    if (kc == 2) L[nl++] = HintList{0x80000000u, 0, false, false};
+    if (km == 1) L[nl++] = HintList{lm, (int8_t)ord_size_first(totm), false, true};
+    if (km == 2) L[nl++] = HintList{0x80000000u, 0, false, false};
+  }
+  const int r = (int)((gh >> GH_R_SHIFT) & 3u);   // DeviceShare (the second provider): r identical lists
+  const uint32_t gl = gh & GH_LIST & valid;
+  for (int k = 0; k < r; ++k)
+    L[nl++] = gl ? HintList{gl, (int8_t)((gh >> GH_MIN_SHIFT) & 7u), false, false} : HintList{0x80000000u, 0, false, false};
+  auto score_at = [&](int mi) -> int32_t { return hint_score(src.sum(mi), pcpu, mem, pf); };
+  return merge_hint_lists_gen(L, nl, nz, policy, score_at, aff_has, aff, over);
+}
+
 // GetPodTopologyHints (topology_hint.go:41-67 -> resource_manager.go:418-532: generateHints for every position,
 // total >= request = the size minimum, free >= request = a hint) + merge_hint_lists, one pair per lane. Hint scores
 // are evaluated once each when a comparison needs them, packed 7 bits per position.
@@ -435,10 +583,13 @@ __device__ __forceinline__ bool hints_merge_wave(const HintRegs& h, int nz, int 
 // row untouched since the batch-start evaluation): hint generation and merge are skipped.
 // TABLE: the row's hint sums come from `table` (the commit kernel), else they are computed from the row's zones.
 // WAVE: one pair evaluated by a whole wave with wave-uniform inputs (hints_merge_wave over the row's registers).
-template <bool POLICY_NODES = true, bool TABLE = false, bool WAVE = false, class Slots>
+// GPROV: the extension path's GPU pods on NUMA-policy nodes: DeviceShare's hints (gh, GH_* above) merged as the
+// second provider (hints_merge_gprov); *gh_over reports a merge past its permutation bound.
+template <bool POLICY_NODES = true, bool TABLE = false, bool WAVE = false, bool GPROV = false, class Slots>
 __device__ __forceinline__ NumaOut numa_eval(const NumaRow& r, const PodVec& p, const Profile& pf, const Slots& sl,
                                              bool do_filter, bool do_score, int known_aff = -1,
-                                             const HintTable* table = nullptr) {
+                                             const HintTable* table = nullptr, uint32_t gh = 0,
+                                             bool* gh_over = nullptr) {
   NumaOut o{};
   const uint32_t pn = p.numa;
   if (pn & PN_PREFAIL) { o.reason = GS_NUMA_INVALID_REQUESTED_CPUS; return o; }
@@ -536,7 +687,12 @@ __device__ __forceinline__ NumaOut numa_eval(const NumaRow& r, const PodVec& p, 
     const int v = hint_variant(reqflag, bind);
     const bool tca = (nf >> NF_ZCPU_SHIFT) & ((1u << nz) - 1u), tma = (nf >> NF_ZMEM_SHIFT) & ((1u << nz) - 1u);
     bool admit;
-    if (WAVE) admit = hints_merge_wave(hint_regs(r, za, v), nz, policy, nil_hints, has_cpu, has_mem, pcpu, mem, tca, tma,
+    if (GPROV) {
+      bool over = false;
+      admit = hints_merge_gprov(hint_regs(r, za, v), nz, policy, nil_hints, has_cpu, has_mem, pcpu, mem, tca, tma, pf,
+                                gh, aff_has, aff, over);
+      if (over && gh_over) *gh_over = true;
+    } else if (WAVE) admit = hints_merge_wave(hint_regs(r, za, v), nz, policy, nil_hints, has_cpu, has_mem, pcpu, mem, tca, tma,
                                        pf, aff_has, aff);
     else if (TABLE) admit = hints_merge(HintTableRef{table, v}, nz, policy, nil_hints, has_cpu, has_mem, pcpu, mem, tca, tma,
                                    pf, aff_has, aff);

@@ -355,16 +355,21 @@ def make_ext(c: Cluster, seed: int | None = None, gpu_node_pct: int = 20, gpus_p
     used_steps = s.randint(2, N * G, 0, 7).reshape(N, G)            # used ratio in 0, 25, 50, 75, 100 (more idle)
     used_ratio = np.array([0, 0, 0, 25, 50, 75, 100, 100], np.int64)[used_steps]
     unhealthy = s.randint(3, N * G, 0, 99).reshape(N, G) == 0        # 1% of devices report zero resources
+    nn = c.numa["node_numa"] if c.numa is not None else None
     for i in np.nonzero(gpu_node)[0]:
         d = devs[i]
         d["has_device"] = 1
         d["num_gpus"] = G
         tot_core = tot_ratio = tot_mem = 0
         u_core = u_ratio = u_mem = 0
+        # Topology.NodeID: the GPUs spread evenly over the node's NUMA zones in minor order (two NUMA nodes without
+        # NRT zones), as fakeDeviceCR (deviceshare/device_allocator_test.go:49-57) places 8 GPUs on 2 nodes
+        nz = int(nn["num_zones"][i]) if nn is not None else 0
         for g in range(G):
             gg = d["gpus"][g]
             gg["minor"] = g
             gg["has_info"] = 1
+            gg["numa_node"] = int(nn["zones"][i][g * nz // G]["node_id"]) if nz else g * 2 // G
             if unhealthy[i, g]:
                 continue
             gg["total"] = (100, 100, mem)

@@ -1001,10 +1001,15 @@ bool policy_merge_filtered(int policy, uint64_t def, std::vector<std::vector<Hin
   return true;                                                       // policy_best_effort.go:43-48
 }
 
-bool policy_merge(int policy, const std::vector<int>& numa_nodes, const HintsMap& hm, bool reverse, Hint* best) {
+// topologyManager.calculateAffinity (manager.go:82-90): every provider's lists (filterProvidersHints), then Merge
+bool policy_merge(int policy, const std::vector<int>& numa_nodes, const HintsMap& hm, bool reverse, Hint* best,
+                  const std::vector<std::vector<Hint>>* provider2 = nullptr) {
   uint64_t def = 0;
   for (int id : numa_nodes) def |= 1ull << id;
-  return policy_merge_filtered(policy, def, filter_providers(hm, reverse), best);
+  std::vector<std::vector<Hint>> lists = filter_providers(hm, reverse);
+  if (provider2)
+    for (const auto& l : *provider2) lists.push_back(l.empty() ? std::vector<Hint>{Hint{false, 0, false, 0}} : l);
+  return policy_merge_filtered(policy, def, lists, best);
 }
 
 }  // namespace
@@ -1062,7 +1067,7 @@ int filter_amplified(const NodeNUMA& n, const NodeView& v, int64_t pod_milli, bo
 }  // namespace
 
 int filter(const NumaArgs& a, const PreState& st, const NodeNUMA& n, const NodeView& v, Hint* affinity,
-           bool* has_affinity, bool reverse) {
+           bool* has_affinity, bool reverse, const std::vector<std::vector<Hint>>* provider2) {
   *has_affinity = false;
   if (st.status) return st.status;
   if (st.skip) return 0;
@@ -1092,7 +1097,7 @@ int filter(const NumaArgs& a, const PreState& st, const NodeNUMA& n, const NodeV
     ro.scorer = true;
     HintsMap hm = topology_hints(a, n, ro);   // GetPodTopologyHints (topology_hint.go:41-67); errors -> nil
     Hint best;
-    if (!policy_merge(o.numa_policy, ids, hm, reverse, &best)) return GS_NUMA_AFFINITY_ERROR;
+    if (!policy_merge(o.numa_policy, ids, hm, reverse, &best, provider2)) return GS_NUMA_AFFINITY_ERROR;
     *affinity = best;
     *has_affinity = true;
     ResourceOptions ro2 = resource_options(st, n, rb, best);   // provider Allocate (topology_hint.go:69-96)

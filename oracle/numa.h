@@ -127,9 +127,13 @@ struct NodeView {        // what the plugin reads from NodeInfo
 };
 
 PreState prefilter(const NumaArgs& a, const gs_pod& pod);
-// Filter (plugin.go:275-338); returns gs_numa_reason; *affinity = the store entry the Admit wrote (if any)
+// Filter (plugin.go:275-338); returns gs_numa_reason; *affinity = the store entry the Admit wrote (if any).
+// provider2: the hint lists of the second NUMATopologyHintProvider (DeviceShare, after NodeNUMAResource in the
+// profile's plugin order, framework_extender.go:138-140), as filterProvidersHints appends them (an empty list = no
+// possible affinity; nullptr or no lists = a provider without hints, whose preferred any-numa hint is neutral).
 int filter(const NumaArgs& a, const PreState& st, const NodeNUMA& n, const NodeView& v, Hint* affinity,
-           bool* has_affinity, bool reverse_resource_order = false);
+           bool* has_affinity, bool reverse_resource_order = false,
+           const std::vector<std::vector<Hint>>* provider2 = nullptr);
 // Score (scoring.go:55-97) with the Filter-time affinity
 int64_t score(const NumaArgs& a, const PreState& st, const NodeNUMA& n, const NodeView& v, const Hint& affinity);
 int topology_hints_test(const NumaArgs& a, const PreState& st, const NodeNUMA& n, int32_t* res, uint64_t* masks,

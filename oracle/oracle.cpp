@@ -1309,7 +1309,13 @@ struct GpuRes {                   // one device's ResourceList over gs_gpu_res (
 struct NodeDev {                  // nodeDevice after filterNodeDevice (device_allocator.go:139-163): minors with info
   std::map<int, GpuRes> total, free;
 };
-NodeDev filtered_node_device(const gs_node_devices& d) {
+// numaNodes: the allocator's NUMA affinity (the topology manager's store entry; nullptr / no mask = none): only the
+// minors whose Topology.NodeID it holds are candidates (device_allocator.go:148-152)
+bool on_numa(const gs_gpu_device& g, const orn::Hint* numa) {
+  if (!numa || !numa->has_mask) return true;
+  return g.numa_node >= 0 && g.numa_node < 64 && (numa->mask >> g.numa_node & 1u);
+}
+NodeDev filtered_node_device(const gs_node_devices& d, const orn::Hint* numa = nullptr) {
   NodeDev o;
   std::map<int, GpuRes> free_all;   // resetDeviceFree (device_cache.go:157-174)
   bool all_zero = true;
@@ -1321,7 +1327,7 @@ NodeDev filtered_node_device(const gs_node_devices& d) {
   }
   if (all_zero) return o;           // nodeDevice.filter: freeDevices.isZero() -> the type is dropped (device_cache.go:361)
   for (int g = 0; g < d.num_gpus && g < GS_MAX_GPUS; ++g) {
-    if (!d.gpus[g].has_info) continue;
+    if (!d.gpus[g].has_info || !on_numa(d.gpus[g], numa)) continue;
     GpuRes t;
     for (int r = 0; r < GS_NUM_GPU_RES; ++r) t.v[r] = d.gpus[g].total[r];
     o.total[d.gpus[g].minor] = t;
@@ -1391,11 +1397,13 @@ int64_t ds_scorer(const gs_ext_args& a, const int64_t* total, const int64_t* fre
 }
 
 // DeviceShare Filter (plugin.go:272-322) on a node with a Device object: 0 ok, else GS_EXT_FAIL_DEVICE
-uint32_t ds_filter(const gs_node_devices& d, const GpuReq& pod) {
+// (numa: the node's NUMA affinity; the same check is DeviceShare.Allocate in the topology manager's Admit,
+// topology_hint.go:57-106)
+uint32_t ds_filter(const gs_node_devices& d, const GpuReq& pod, const orn::Hint* numa = nullptr) {
   GpuReq inst;
   int64_t count;
   if (gpu_desired(d, pod, &inst, &count) < 0) return GS_EXT_FAIL_DEVICE;
-  NodeDev nd = filtered_node_device(d);
+  NodeDev nd = filtered_node_device(d, numa);
   int64_t ok = 0;                              // defaultAllocateDevices (device_allocator.go:397-467), no scorer
   for (auto& kv : nd.free) {
     if (kv.second.zero()) continue;
@@ -1406,11 +1414,11 @@ uint32_t ds_filter(const gs_node_devices& d, const GpuReq& pod) {
 }
 
 // DeviceShare Score (scoring.go:34-89) -> allocator.score (device_allocator.go:513-536)
-int64_t ds_score(const gs_ext_args& a, const gs_node_devices& d, const GpuReq& pod) {
+int64_t ds_score(const gs_ext_args& a, const gs_node_devices& d, const GpuReq& pod, const orn::Hint* numa = nullptr) {
   GpuReq inst;
   int64_t count;
   if (gpu_desired(d, pod, &inst, &count) < 0) return 0;
-  NodeDev nd = filtered_node_device(d);
+  NodeDev nd = filtered_node_device(d, numa);
   if (nd.total.empty()) return 0;
   int64_t tot[GS_NUM_GPU_RES] = {0, 0, 0}, fr[GS_NUM_GPU_RES] = {0, 0, 0};
   for (auto& kv : nd.total)
@@ -1422,11 +1430,12 @@ int64_t ds_score(const gs_ext_args& a, const gs_node_devices& d, const GpuReq& p
 
 // DeviceShare Reserve (plugin.go:377-430): defaultAllocateDevices with the scorer; minors sorted by device score
 // descending, then minor (sortDeviceResourcesByMinor, device_resources.go:187-208). Returns the minors.
-int ds_reserve(const gs_ext_args& a, gs_node_devices& d, const GpuReq& pod, gs_ext_placement* eo) {
+int ds_reserve(const gs_ext_args& a, gs_node_devices& d, const GpuReq& pod, gs_ext_placement* eo,
+               const orn::Hint* numa = nullptr) {
   GpuReq inst;
   int64_t count;
   if (gpu_desired(d, pod, &inst, &count) < 0) return -1;
-  NodeDev nd = filtered_node_device(d);
+  NodeDev nd = filtered_node_device(d, numa);
   struct Pair { int minor; int64_t score; GpuRes free; };
   std::vector<Pair> ps;
   for (auto& kv : nd.free) ps.push_back({kv.first, ds_scorer(a, nd.total[kv.first].v, kv.second.v, inst), kv.second});
@@ -1452,6 +1461,59 @@ int ds_reserve(const gs_ext_args& a, gs_node_devices& d, const GpuReq& pod, gs_e
   eo->gpu_count = (int32_t)count;
   for (int r = 0; r < GS_NUM_GPU_RES; ++r) eo->gpu_per_instance[r] = (inst.mask & (1u << r)) ? inst.v[r] : 0;
   return 0;
+}
+
+// DeviceShare as a NUMATopologyHintProvider: GetPodTopologyHints -> generateTopologyHints (topology_hint.go:33-55,
+// 108-214), GPU type. false: the provider returns no hints (no Device object, Prepare fails, or no mask holds enough
+// devices: an empty map, i.e. filterProvidersHints' preferred any-numa hint). true: *lists = one list per resource name
+// of the per-instance request (gpu-core / gpu-memory-ratio / gpu-memory: identical lists, possibly empty), *names =
+// those names (gs_gpu_res bits).
+bool ds_topology_hints(const gs_node_devices& d, const GpuReq& pod, std::vector<std::vector<orn::Hint>>* lists,
+                       uint32_t* names = nullptr) {
+  lists->clear();
+  if (names) *names = 0;
+  if (!d.has_device || !pod.mask) return false;
+  std::vector<int> ids;   // numaTopology.nodes keys (devices with a Topology), sorted (topology_hint.go:123-127)
+  for (int g = 0; g < d.num_gpus && g < GS_MAX_GPUS; ++g)
+    if (d.gpus[g].has_info && d.gpus[g].numa_node >= 0 && d.gpus[g].numa_node < 64) ids.push_back(d.gpus[g].numa_node);
+  std::sort(ids.begin(), ids.end());
+  ids.erase(std::unique(ids.begin(), ids.end()), ids.end());
+  GpuReq inst;
+  int64_t count;
+  if (gpu_desired(d, pod, &inst, &count) < 0) return false;   // allocator.Prepare fails for every mask
+  int min_size = -1;
+  std::vector<orn::Hint> hs;
+  // bitmask.IterateBitMasks (util/bitmask/bitmask.go:206-222): sizes 1..n, combinations in lexicographic order
+  std::vector<int> acc;
+  std::function<void(size_t, int)> it = [&](size_t from, int size) {
+    if ((int)acc.size() == size) {
+      uint64_t m = 0;
+      for (int id : acc) m |= 1ull << id;
+      int64_t total = 0;   // calcTotalDevicesByNUMA (topology_hint.go:216-227)
+      for (int g = 0; g < d.num_gpus && g < GS_MAX_GPUS; ++g)
+        if (d.gpus[g].has_info && d.gpus[g].numa_node >= 0 && d.gpus[g].numa_node < 64 && (m >> d.gpus[g].numa_node & 1u))
+          ++total;
+      if (total < count) return;
+      if (min_size < 0) min_size = (int)ids.size();   // minAffinitySize: len(numaNodes), then the smallest mask
+      if (size < min_size) min_size = size;
+      const orn::Hint aff{true, m, false, 0};
+      if (ds_filter(d, pod, &aff) != 0) return;   // allocator.Allocate within the mask
+      hs.push_back(aff);
+      return;
+    }
+    for (size_t i = from; i < ids.size(); ++i) {
+      acc.push_back(ids[i]);
+      it(i + 1, size);
+      acc.pop_back();
+    }
+  };
+  for (int k = 1; k <= (int)ids.size(); ++k) it(0, k);
+  if (min_size < 0) return false;   // minAffinitySize nil: no resource name gets a list
+  for (orn::Hint& h : hs) h.preferred = __builtin_popcountll(h.mask) == min_size;
+  for (int r = 0; r < GS_NUM_GPU_RES; ++r)   // one (identical) list per name: their order does not matter
+    if (inst.mask >> r & 1u) lists->push_back(hs);
+  if (names) *names = inst.mask;
+  return true;
 }
 
 // ---- Reservation (reservation/*.go) ----
@@ -1664,6 +1726,34 @@ uint32_t or_device_filter(const gs_node_devices* d, const gs_pod_ext* e) {
   return ds_filter(*d, q);
 }
 
+// DeviceShare GetPodTopologyHints on one node (topology_hint_test.go TestPlugin_GetPodTopologyHints, GPU cases):
+// returns -1 invalid request, 0 no hints (an empty map), 1 hints: *names = resource names (gs_gpu_res bits) that each
+// get the list (masks[k], preferred[k]) k < *count (over NUMA node ids)
+int or_device_topology_hints(const gs_node_devices* d, const gs_pod_ext* e, uint64_t* masks, uint8_t* preferred,
+                             uint32_t cap, uint32_t* count, uint32_t* names) {
+  *count = 0;
+  *names = 0;
+  GpuReq q;
+  if (gpu_pod_request(*e, &q) < 0) return -1;
+  std::vector<std::vector<orn::Hint>> lists;
+  if (!ds_topology_hints(*d, q, &lists, names)) return 0;
+  const std::vector<orn::Hint>& l = lists[0];
+  for (size_t k = 0; k < l.size(); ++k)
+    if (k < cap) { masks[k] = l[k].mask; preferred[k] = l[k].preferred ? 1 : 0; }
+  *count = (uint32_t)l.size();
+  return 1;
+}
+
+// DeviceShare.Allocate with an affinity (topology_hint.go:57-106; TestPlugin_Allocate GPU cases): 0 ok, else
+// GS_EXT_FAIL_DEVICE / GS_EXT_FAIL_POD
+uint32_t or_device_allocate(const gs_node_devices* d, const gs_pod_ext* e, int has_mask, uint64_t mask) {
+  GpuReq q;
+  if (gpu_pod_request(*e, &q) < 0) return GS_EXT_FAIL_POD;
+  if (!q.mask || !d->has_device) return 0;
+  const orn::Hint aff{has_mask != 0, mask, false, 0};
+  return ds_filter(*d, q, &aff);
+}
+
 int64_t or_device_score_node(const gs_ext_args* a, const int64_t* total, const int64_t* free, const int64_t* request,
                              uint32_t request_mask) {
   GpuReq q;
@@ -1773,11 +1863,14 @@ int or_schedule_ext(or_cluster* c, const gs_pod* pods, const gs_pod_ext* ext, ui
       affinity[n] = orn::Hint{};
       if (!code && (en & GS_ENABLE_NUMA_FILTER)) {
         bool has = false;
-        int reason = orn::filter(c->numa_args, st, c->numa[n], node_view(nd), &affinity[n], &has, c->reverse_hint_order);
+        std::vector<std::vector<orn::Hint>> p2;   // DeviceShare's hints (the second provider) on NUMA-policy nodes
+        if (gpu_pod && c->numa[n].opts.numa_policy != GS_NUMA_POLICY_NONE) ds_topology_hints(c->devices[n], gpu, &p2);
+        int reason = orn::filter(c->numa_args, st, c->numa[n], node_view(nd), &affinity[n], &has, c->reverse_hint_order,
+                                 &p2);
         if (!has) affinity[n] = orn::Hint{};
         code |= (uint32_t)reason << GS_FAIL_NUMA_SHIFT;
       }
-      if (!code && gpu_pod && c->devices[n].has_device) code |= ds_filter(c->devices[n], gpu);
+      if (!code && gpu_pod && c->devices[n].has_device) code |= ds_filter(c->devices[n], gpu, &affinity[n]);
       if (!code && rs_on) {   // Reservation Filter (plugin.go:311-375), non-reserve pods
         const NodeRState& ns = rstate[n];
         if (ns.matched.empty()) {
@@ -1818,7 +1911,7 @@ int or_schedule_ext(or_cluster* c, const gs_pod* pods, const gs_pod_ext* ext, ui
       if (en & GS_ENABLE_LA_SCORE) r.la = loadaware_score(*c, pod, c->nodes[n]);
       if (en & GS_ENABLE_NUMA_SCORE) r.numa = orn::score(c->numa_args, st, c->numa[n], node_view(nd), affinity[n]);
       base[n] = weighted_total(*c, r);
-      dsl[i] = (gpu_pod && c->devices[n].has_device) ? ds_score(c->ext, c->devices[n], gpu) : 0;
+      dsl[i] = (gpu_pod && c->devices[n].has_device) ? ds_score(c->ext, c->devices[n], gpu, &affinity[n]) : 0;
       int64_t rs = 0;
       if (rs_on) {
         if (n == preferred) rs = 1000;   // mostPreferredScore
@@ -1852,7 +1945,7 @@ int or_schedule_ext(or_cluster* c, const gs_pod* pods, const gs_pod_ext* ext, ui
       if (!pa.cpus.empty()) o.flags |= GS_PLACED_CPUSET;
     }
     gs_node_devices& dv = c->devices[selected];
-    if (gpu_pod && dv.has_device && ds_reserve(c->ext, dv, gpu, &eo) != 0) return GS_ESTATE;
+    if (gpu_pod && dv.has_device && ds_reserve(c->ext, dv, gpu, &eo, &affinity[selected]) != 0) return GS_ESTATE;
     if (rs_on) {
       const gs_reservation* nr = nominated[selected];
       if (nr) {   // reservationCache.assumePod -> ReservationInfo.AddAssignedPod (reservation_info.go:379-388)

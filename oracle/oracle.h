@@ -100,6 +100,9 @@ int or_reservation_node_scores(const gs_pod* pod, const gs_reservation* rsv, con
                                const gs_node* nodes, const gs_node* pod_requested, int64_t* raw);
 int64_t or_device_score(const gs_ext_args* a, const gs_node_devices* d, const gs_pod_ext* e);
 uint32_t or_device_filter(const gs_node_devices* d, const gs_pod_ext* e);
+int or_device_topology_hints(const gs_node_devices* d, const gs_pod_ext* e, uint64_t* masks, uint8_t* preferred,
+                             uint32_t cap, uint32_t* count, uint32_t* names);
+uint32_t or_device_allocate(const gs_node_devices* d, const gs_pod_ext* e, int has_mask, uint64_t mask);
 int64_t or_device_score_node(const gs_ext_args* a, const int64_t* total, const int64_t* free, const int64_t* request,
                              uint32_t request_mask);   /* resourceAllocationScorer.scoreNode (deviceshare/scoring.go:213-243) */
 

@@ -76,6 +76,8 @@ def _load() -> C.CDLL:
         "or_reservation_node_scores": (C.c_int, [P, P, P, C.c_uint32, P, P, P]),
         "or_device_score": (C.c_int64, [C.POINTER(abi.GsExtArgs), P, P]),
         "or_device_filter": (C.c_uint32, [P, P]),
+        "or_device_topology_hints": (C.c_int, [P, P, P, P, C.c_uint32, P, P]),
+        "or_device_allocate": (C.c_uint32, [P, P, C.c_int, C.c_uint64]),
         "or_device_score_node": (C.c_int64, [C.POINTER(abi.GsExtArgs), P, P, P, C.c_uint32]),
     }
     for name, (res, args) in sig.items():
@@ -412,6 +414,35 @@ def device_filter(devs, ext) -> int:
     d = np.ascontiguousarray(np.atleast_1d(devs), abi.NODE_DEVICES_DTYPE)
     e = np.ascontiguousarray(np.atleast_1d(ext), abi.POD_EXT_DTYPE)
     return int(lib().or_device_filter(abi.ptr(d), abi.ptr(e)))
+
+
+def device_topology_hints(devs, ext):
+    """DeviceShare GetPodTopologyHints on one node (topology_hint.go:33-214, GPU type): None for an invalid request,
+    {} for no hints, else {resource name: [(NUMA node ids, preferred), ...]} (identical lists per name)."""
+    d = np.ascontiguousarray(np.atleast_1d(devs), abi.NODE_DEVICES_DTYPE)
+    e = np.ascontiguousarray(np.atleast_1d(ext), abi.POD_EXT_DTYPE)
+    masks = np.zeros(64, np.uint64)
+    pref = np.zeros(64, np.uint8)
+    cnt, names = C.c_uint32(), C.c_uint32()
+    rc = lib().or_device_topology_hints(abi.ptr(d), abi.ptr(e), abi.ptr(masks), abi.ptr(pref), 64, C.addressof(cnt),
+                                        C.addressof(names))
+    if rc < 0:
+        return None
+    if rc == 0:
+        return {}
+    lst = [([b for b in range(64) if int(masks[k]) >> b & 1], bool(pref[k])) for k in range(cnt.value)]
+    keys = {0: "koordinator.sh/gpu-core", 1: "koordinator.sh/gpu-memory-ratio", 2: "koordinator.sh/gpu-memory"}
+    return {keys[r]: list(lst) for r in range(3) if names.value >> r & 1}
+
+
+def device_allocate(devs, ext, numa_nodes=None) -> int:
+    """DeviceShare.Allocate with a NUMA affinity (topology_hint.go:57-106): 0 ok, else the failure code."""
+    d = np.ascontiguousarray(np.atleast_1d(devs), abi.NODE_DEVICES_DTYPE)
+    e = np.ascontiguousarray(np.atleast_1d(ext), abi.POD_EXT_DTYPE)
+    m = 0
+    for b in (numa_nodes or []):
+        m |= 1 << b
+    return int(lib().or_device_allocate(abi.ptr(d), abi.ptr(e), int(numa_nodes is not None), m))
 
 
 def device_score_node(args: abi.GsExtArgs, total, free, request, request_mask) -> int:

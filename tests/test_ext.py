@@ -90,6 +90,49 @@ def test_golden_device_score(case):
     assert orc.device_score(ext_args(case.get("strategy")), d, e) == case["want"], case["src"]
 
 
+DN = json.load(open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "devnuma.json")))
+GPU_NAME_OF = {"core": "koordinator.sh/gpu-core", "ratio": "koordinator.sh/gpu-memory-ratio",
+               "memory": "koordinator.sh/gpu-memory"}
+
+
+def devices_of(gpus):
+    """gs_node_devices of a Device object's GPUs (minor, NUMA node, total, used)."""
+    d = np.zeros(1, abi.NODE_DEVICES_DTYPE)[0]
+    d["has_device"] = 1
+    d["num_gpus"] = len(gpus)
+    for g, x in enumerate(gpus):
+        d["gpus"][g]["minor"] = x["minor"]
+        d["gpus"][g]["has_info"] = 1
+        d["gpus"][g]["numa_node"] = x["numa_node"]
+        for k, v in x["total"].items():
+            d["gpus"][g]["total"][GR[k]] = v
+        for k, v in x["used"].items():
+            d["gpus"][g]["used"][GR[k]] = v
+    return d
+
+
+def gpu_ext_of(req):
+    e = np.zeros(1, abi.POD_EXT_DTYPE)[0]
+    for k, v in req.items():
+        n = abi.GPU_NAMES[GPU_NAME_OF[k]]
+        e["gpu_requests"][n] = v
+        e["gpu_request_mask"] |= 1 << n
+    return e
+
+
+@pytest.mark.parametrize("case", DN["topology_hints"], ids=lambda c: c["name"])
+def test_golden_device_topology_hints(case):
+    got = orc.device_topology_hints(devices_of(case["gpus"]), gpu_ext_of(case["request"]))
+    want = {k: [(m, p) for m, p in v] for k, v in case["want"].items()}
+    assert got == want, case["src"]
+
+
+@pytest.mark.parametrize("case", DN["allocate"], ids=lambda c: c["name"])
+def test_golden_device_allocate(case):
+    rc = orc.device_allocate(devices_of(case["gpus"]), gpu_ext_of(case["request"]), case["numa_nodes"])
+    assert (rc == 0) == case["ok"], case["src"]
+
+
 @pytest.mark.parametrize("case", G["score_device"], ids=lambda c: c["name"])
 def test_golden_score_device(case):
     vec = lambda m: [m.get(k, 0) for k in ("core", "ratio", "memory")]
@@ -224,3 +267,32 @@ def test_extended_resources_fit_properties():
     c2, o2 = _xres_cluster(ignored=0x3)
     out2, _ = o2.schedule_ext(c2.pods, ext)
     assert out2["node"][7] >= 0
+
+
+def test_numa_policy_gpu_pods_allocate_within_affinity():
+    """or_schedule_ext on a cluster with NUMA-policy nodes: a GPU pod placed on a policy node under SingleNUMANode gets
+    GPUs of a single NUMA node, the one its NUMA allocation uses (DeviceShare's hints merged with NodeNUMAResource's)."""
+    c = synth.make_cluster(400, 160, config_id=21)
+    synth.make_numa(c, numa_policy_pct=100, cpuset_pod_pct=0)
+    synth.make_ext(c, gpu_node_pct=60, gpu_pod_pct=60, owner_pod_pct=0)
+    cfg = config.make_config(c.num_nodes, enabled=abi.GS_ENABLE_ALL)
+    o = orc.Oracle(cfg)
+    synth.load_into(o, c)
+    synth.load_ext_into(o, c, orc.ext_args_default())
+    seq = np.arange(len(c.pods), dtype=np.uint64)
+    out, ext = o.schedule_ext(c.pods, c.ext["pod_ext"], seq)
+    nn = c.numa["node_numa"]
+    single = 0
+    for j in np.nonzero((out["node"] >= 0) & (ext["gpu_count"] > 0))[0]:
+        i = int(out["node"][j])
+        if nn["numa_topology_policy"][i] != abi.NUMA_POLICY["SingleNUMANode"]:
+            continue
+        a = o.allocation(i, int(c.pods["uid"][j]))
+        if a is None:   # no cpu / memory request: NodeNUMAResource skips the pod (no Admit, no affinity)
+            continue
+        zones = {int(a["numa"][k]["node_id"]) for k in range(int(a["num_numa"]))}
+        gnuma = {int(g["numa_node"]) for g in c.ext["devices"][i]["gpus"][:8]
+                 if int(ext["gpu_minor_mask"][j]) >> int(g["minor"]) & 1}
+        assert len(zones) == 1 and gnuma == zones, (j, zones, gnuma)
+        single += 1
+    assert single > 5

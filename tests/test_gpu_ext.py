@@ -127,3 +127,26 @@ def test_c5_registered_extended_resources(ignored):
     for i in np.nonzero(c.ext["devices"]["xres_allocatable"][:, 0])[0][:50]:
         assert np.array_equal(e.devices(int(i))["xres_requested"], o.devices(int(i))["xres_requested"])
     assert (c.ext["pod_ext"]["xres_request_mask"] != 0).sum() > 50
+
+
+@pytest.mark.parametrize("policy_pct", [40, 100], ids=["policy40", "policy100"])
+def test_c5_numa_policy_nodes_deviceshare_hints(policy_pct):
+    """GPU pods on nodes with a NUMA topology policy: DeviceShare is the topology manager's second hint provider
+    (deviceshare/topology_hint.go:33-214), merged with NodeNUMAResource's hints; the Filter-time affinity restricts
+    DeviceShare's Allocate / Score / Reserve to the GPUs on its NUMA nodes, and NodeNUMAResource's Reserve allocates
+    the zones along it. Placements, GPU minors, NUMA allocations and the final state bit-exact against the oracle."""
+    c = synth.make_cluster(1500, 600, config_id=13 + policy_pct)
+    synth.make_numa(c, numa_policy_pct=policy_pct, cpuset_pod_pct=0)
+    synth.make_ext(c, gpu_node_pct=50, gpu_pod_pct=50, owner_pod_pct=0)
+    e, o, ge, oe = run_pair(c, enabled=abi.GS_ENABLE_ALL)
+    placed = check(c, e, o, ge, oe)
+    assert np.array_equal(ge[0]["flags"][placed] & 6, oe[0]["flags"][placed] & 6)
+    pol = c.numa["node_numa"]["numa_topology_policy"] != 0
+    node = ge[0]["node"]
+    on_pol = placed & pol[np.maximum(node, 0)]
+    gpu_on_pol = on_pol & (ge[1]["gpu_count"] > 0)
+    assert gpu_on_pol.sum() > 20 and ((ge[0]["flags"] & 2) != 0)[gpu_on_pol].sum() > 10
+    for j in np.nonzero(on_pol)[0]:
+        uid = int(c.pods["uid"][j])
+        a, b = e.allocation(int(node[j]), uid), o.allocation(int(node[j]), uid)
+        assert (a is None) == (b is None) and (a is None or a.tobytes() == b.tobytes()), j
