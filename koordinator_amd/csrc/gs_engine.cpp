@@ -207,6 +207,10 @@ struct gs_ctx {
   std::vector<std::vector<uint64_t>> rsv_node;   // uids per node, ascending
   std::unordered_map<uint64_t, std::vector<uint64_t>> rsv_owner;   // owner key -> uids
   DevNode* d_dev = nullptr;
+  DevNode* h_dev_stage = nullptr;   // ext_flush_devices staging (pinned / device)
+  DevNode* d_dev_stage = nullptr;
+  uint32_t* h_dev_idx = nullptr;
+  uint32_t* d_dev_idx = nullptr;
   ExtPod* d_xpod = nullptr;
   ExtRec* d_xrec = nullptr;
   ExtRes* d_xres = nullptr;
@@ -1198,13 +1202,29 @@ int ext_alloc(gs_ctx* c) {
   return GS_OK;
 }
 
+// the dirty nodes' Device images: staged in pinned memory, one copy and one scatter per EXT_DEV_STAGE nodes
 int ext_flush_devices(gs_ctx* c) {
   if (c->dev_dirty_list.empty()) return GS_OK;
   if (!c->d_dev) return ext_alloc(c);
-  for (uint32_t i : c->dev_dirty_list) {
-    const DevNode img = dev_image(c, i);
-    HIP_TRY(c, hipMemcpy(c->d_dev + i, &img, sizeof(DevNode), hipMemcpyHostToDevice));
-    c->dev_dirty[i] = 0;
+  if (!c->h_dev_stage) {
+    HIP_TRY(c, hipHostMalloc(&c->h_dev_stage, sizeof(DevNode) * EXT_DEV_STAGE, hipHostMallocDefault));
+    HIP_TRY(c, hipHostMalloc(&c->h_dev_idx, 4 * EXT_DEV_STAGE, hipHostMallocDefault));
+    HIP_TRY(c, hipMalloc(&c->d_dev_stage, sizeof(DevNode) * EXT_DEV_STAGE));
+    HIP_TRY(c, hipMalloc(&c->d_dev_idx, 4 * EXT_DEV_STAGE));
+  }
+  for (size_t done = 0; done < c->dev_dirty_list.size();) {
+    const uint32_t n = (uint32_t)std::min<size_t>(EXT_DEV_STAGE, c->dev_dirty_list.size() - done);
+    HIP_TRY(c, hipStreamSynchronize(c->st));   // the previous scatter has consumed the staging buffers
+    for (uint32_t j = 0; j < n; ++j) {
+      const uint32_t i = c->dev_dirty_list[done + j];
+      c->h_dev_stage[j] = dev_image(c, i);
+      c->h_dev_idx[j] = i;
+      c->dev_dirty[i] = 0;
+    }
+    HIP_TRY(c, hipMemcpyAsync(c->d_dev_idx, c->h_dev_idx, 4 * n, hipMemcpyHostToDevice, c->st));
+    HIP_TRY(c, hipMemcpyAsync(c->d_dev_stage, c->h_dev_stage, sizeof(DevNode) * n, hipMemcpyHostToDevice, c->st));
+    HIP_TRY(c, launch_scatter_devnodes(c->d_dev, c->d_dev_idx, c->d_dev_stage, n, c->st));
+    done += n;
   }
   c->dev_dirty_list.clear();
   return GS_OK;
@@ -1767,6 +1787,8 @@ int gs_destroy(gs_ctx* c) {
     for (int k = 0; k < 8; ++k) fprintf(stderr, " %llu", (unsigned long long)c->ht_busy_hist[k]);
     fprintf(stderr, "\n");
   }
+  for (void* p : {(void*)c->d_dev_stage, (void*)c->d_dev_idx}) if (p) (void)hipFree(p);
+  for (void* p : {(void*)c->h_dev_stage, (void*)c->h_dev_idx}) if (p) (void)hipHostFree(p);
   for (void* p : {(void*)c->d_dev, (void*)c->d_xpod, (void*)c->d_xrec, (void*)c->d_xres, (void*)c->d_xtot,
                   (void*)c->d_xds, (void*)c->d_xrs, (void*)c->d_xnom, (void*)c->d_xT, (void*)c->d_xout})
     if (p) (void)hipFree(p);

@@ -18,6 +18,7 @@ namespace gs {
 
 constexpr int EXT_GPUS = 8;
 constexpr int EXT_MAX_RES_PER_NODE = 8;   // matched reservations of one pod on one node (device path)
+constexpr int EXT_DEV_STAGE = 1024;       // Device images per staged update (ext_flush_devices)
 
 struct DevGpu {                 // one GPU minor after filterNodeDevice (has_info = 0: not a candidate)
   int64_t total[3];             // gpu-core, gpu-memory-ratio, gpu-memory
@@ -113,6 +114,8 @@ hipError_t launch_ext_numa(const MirrorView& m, const PodVec* pods, const Profil
 hipError_t launch_ext_reserve_numa(const MirrorView& m, const PodVec* pods, const Profile& pf, int prod_cols,
                                    const uint8_t* aff, uint32_t n0, ExtOut* out, hipStream_t st);
 size_t ext_select_scratch_words(uint32_t len);   // int32 words of launch_ext_select's scratch
+// dev[idx[j]] = img[j], j < n (staged Device image updates)
+hipError_t launch_scatter_devnodes(DevNode* dev, const uint32_t* idx, const DevNode* img, uint32_t n, hipStream_t st);
 hipError_t launch_ext_select(const int32_t* tot, const int16_t* ds, const int16_t* rs, const ExtRec* recs, uint32_t n0,
                              uint32_t n1, const ExtPod* pod, uint64_t seed, int32_t* scratch, ExtOut* out,
                              hipStream_t st);

@@ -506,7 +506,23 @@ __global__ __launch_bounds__(SEL_BLOCK) void ext_ties_kernel(const int32_t* __re
   }
 }
 
+constexpr int DEV_WORDS = (int)(sizeof(DevNode) / 8);
+static_assert(sizeof(DevNode) % 8 == 0, "DevNode words");
+__global__ __launch_bounds__(256) void scatter_devnodes_kernel(DevNode* dev, const uint32_t* __restrict__ idx,
+                                                               const DevNode* __restrict__ img, uint32_t n) {
+  const uint32_t t = blockIdx.x * 256 + threadIdx.x;
+  if (t >= n * DEV_WORDS) return;
+  const uint32_t j = t / DEV_WORDS, w = t % DEV_WORDS;
+  reinterpret_cast<int64_t*>(dev + idx[j])[w] = reinterpret_cast<const int64_t*>(img + j)[w];
+}
+
 }  // namespace
+
+hipError_t launch_scatter_devnodes(DevNode* dev, const uint32_t* idx, const DevNode* img, uint32_t n, hipStream_t st) {
+  if (!n) return hipSuccess;
+  hipLaunchKernelGGL(scatter_devnodes_kernel, dim3((n * DEV_WORDS + 255) / 256), dim3(256), 0, st, dev, idx, img, n);
+  return hipGetLastError();
+}
 
 hipError_t launch_ext_nodes(const DevNode* dev, const int16_t* S, uint32_t n0, uint32_t n1, const ExtPod* pod,
                             int32_t* tot, int16_t* ds, int16_t* rs, hipStream_t st) {
