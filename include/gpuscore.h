@@ -767,6 +767,11 @@ typedef struct gs_merge_case {
   int32_t nz, policy;
   int32_t nil_hints, has_cpu, has_mem, tot_c_any, tot_m_any;
   int32_t score[15];
+  /* A second provider (DeviceShare, deviceshare/topology_hint.go:33-214), merged after these lists: bits 0-14 its hint
+   * positions, bits 16-18 the preferred size, bits 20-21 the number of identical lists (one per resource name; 0 = no
+   * second provider: the two-list merge every pair evaluation runs); no position with lists = each list empty. */
+  uint32_t gpu_hints;
+  int32_t pad;
 } gs_merge_case;
 typedef struct gs_merge_result {
   int32_t admit, aff_has;

@@ -263,7 +263,7 @@ ALLGATHER_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_size
 class GsMergeCase(C.Structure):
     _fields_ = [("lc", u32), ("totc", u32), ("lm", u32), ("totm", u32), ("nz", i32), ("policy", i32),
                 ("nil_hints", i32), ("has_cpu", i32), ("has_mem", i32), ("tot_c_any", i32), ("tot_m_any", i32),
-                ("score", i32 * 15)]
+                ("score", i32 * 15), ("gpu_hints", u32), ("pad", i32)]
 
 
 class GsMergeResult(C.Structure):

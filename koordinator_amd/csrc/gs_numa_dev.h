@@ -373,19 +373,32 @@ struct HintList {        // one list of filterProvidersHints' output
   bool pseudo_pref;      // the mask-less hint's Preferred
   bool scored;           // NodeNUMAResource's lists carry hint scores (DeviceShare's score 0)
 };
-constexpr int kGenMergeMax = 1 << 16;   // permutations one pass may visit (the caller fails loudly beyond)
+constexpr int kGenMergeMax = 1 << 16;   // search steps one pass may take (the caller fails loudly beyond)
 
 // topologyManager Merge over any provider lists (policy.go:128-186, policy_*.go), lists in filterProvidersHints
-// order: the exact permutation scan of mergeFilteredHints in its visiting order, reduced preferred-first like
-// merge_hint_lists (pass 0 over the preferred entries; pass 1, all entries, only when no preferred permutation merges
-// to a non-empty mask). *over: a pass exceeded kGenMergeMax permutations (the result is then not used).
+// order, exact. mergeFilteredHints visits the permutations in lexicographic order with a non-associative update
+// (a preferred hint beats a non-preferred one; then a narrower mask wins, an equally wide one only with a higher
+// score), so the result depends on the order — but only through few candidates:
+//  * preferred-first (as merge_hint_lists): pass 0 over the preferred entries; pass 1, all entries, only when no
+//    preferred permutation merges to a non-empty mask (then every candidate is non-preferred);
+//  * within a pass, once a candidate of the smallest non-empty size p* appears it replaces the best (it is narrower
+//    than anything wider, or the first preferred one), and wider candidates never replace it afterwards: the result is
+//    the update folded over the size-p* candidates alone, in order — a narrower mask (smaller value) always replaces,
+//    another only with a higher score;
+//  * the depth-first walk over the lists skips a subtree whose reachable merged masks (bit sets over the 16 masks,
+//    from a backward pass) hold no size-p* mask, or, below the last scored list (the scores are then fixed), none
+//    that could replace the current best.
+// HintList::scored lists carry score_at(position) (NodeNUMAResource's hint scores; DeviceShare's are 0).
+// *over: a pass took more than kGenMergeMax steps (the result is then not used).
 template <class ScoreAt>
 __device__ __noinline__ bool merge_hint_lists_gen(const HintList* L, int nl, int nz, int policy, ScoreAt&& score_at,
                                                   bool& aff_has, uint32_t& aff, bool& over) {
   const bool single = policy == GS_NUMA_POLICY_SINGLE_NUMA_NODE;
   const uint32_t full_mask = (1u << nz) - 1u;
   constexpr uint32_t PSEUDO = 0x80000000u;
+  auto em = [&](int e) -> uint32_t { return e == 31 ? full_mask : ord_mask(e); };
   uint32_t s0[6], s1[6];
+  int nsc = 0;   // lists [0, nsc) hold every scored one
   for (int l = 0; l < nl; ++l) {
     uint32_t all, pref;
     if (L[l].set == PSEUDO) {
@@ -395,8 +408,8 @@ __device__ __noinline__ bool merge_hint_lists_gen(const HintList* L, int nl, int
       all = L[l].set;
       pref = 0;
       for (uint32_t rr = all; rr; rr &= rr - 1) {
-        const int mi = __ffs(rr) - 1;
-        if (__popc(ord_mask(mi)) == L[l].min) pref |= 1u << mi;
+        const int mi = __builtin_ctz(rr);
+        if (__builtin_popcount(ord_mask(mi)) == L[l].min) pref |= 1u << mi;
       }
     }
     if (single) {   // policy_single_numa_node.go:48-78: preferred mask-less or preferred single-zone hints only
@@ -405,58 +418,90 @@ __device__ __noinline__ bool merge_hint_lists_gen(const HintList* L, int nl, int
     }
     s0[l] = pref;
     s1[l] = all;
+    if (L[l].scored) nsc = l + 1;
   }
+  int16_t scache[15];
+  for (int i = 0; i < 15; ++i) scache[i] = -1;
+  int ent[6];
+  auto s_of = [&](uint32_t x) -> int32_t {   // the merged hint's score: the scored entries whose mask equals it
+    int32_t sx = 0;
+    for (int l = 0; l < nsc; ++l) {
+      const int e = ent[l];
+      if (!L[l].scored || e == 31 || ord_mask(e) != x) continue;
+      if (scache[e] < 0) scache[e] = (int16_t)score_at(e);
+      if (scache[e] > sx) sx = scache[e];
+    }
+    return sx;
+  };
   bool b_pref = false;
   uint32_t b_mask = full_mask;
-  int32_t b_score = 0;
   over = false;
   for (int pass = 0; pass < 2; ++pass) {
-    if (pass == 1) {
-      if (b_pref) break;
-      b_mask = full_mask;
-      b_score = 0;
-    }
+    if (pass == 1 && b_pref) break;
     const uint32_t* S = pass ? s1 : s0;
     bool empty = false;
     for (int l = 0; l < nl; ++l) empty |= S[l] == 0;
     if (empty) continue;   // a list without entries: no permutation
-    uint32_t rem[6];
-    for (int l = 0; l < nl; ++l) rem[l] = S[l];
-    int visited = 0;
-    while (true) {
-      if (++visited > kGenMergeMax) { over = true; break; }
-      uint32_t mg = full_mask;
-      bool pg = true;
-      for (int l = 0; l < nl; ++l) {
-        const int e = __ffs(rem[l]) - 1;
-        if (e == 31) {
-          pg = pg && L[l].pseudo_pref;
-        } else {
-          mg &= ord_mask(e);
-          pg = pg && __popc(ord_mask(e)) == L[l].min;
-        }
+    uint32_t fw = 1u << full_mask;   // merged masks reachable after each list (bit x = mask x)
+    for (int l = 0; l < nl; ++l) {
+      uint32_t nx = 0;
+      for (uint32_t yy = fw; yy; yy &= yy - 1)
+        for (uint32_t ee = S[l]; ee; ee &= ee - 1) nx |= 1u << ((uint32_t)__builtin_ctz(yy) & em(__builtin_ctz(ee)));
+      fw = nx;
+    }
+    const uint32_t fin = fw & ~1u;
+    if (!fin) continue;
+    int pstar = 5;
+    for (uint32_t xx = fin; xx; xx &= xx - 1) pstar = min(pstar, __builtin_popcount((uint32_t)__builtin_ctz(xx)));
+    uint32_t P = 0;
+    for (uint32_t xx = fin; xx; xx &= xx - 1)
+      if (__builtin_popcount((uint32_t)__builtin_ctz(xx)) == pstar) P |= 1u << __builtin_ctz(xx);
+    uint16_t rb[6][16];   // rb[l][y]: merged masks reachable from the partial merge y before list l
+    for (int y = 0; y < 16; ++y) rb[nl][y] = (uint16_t)(1u << y);
+    for (int l = nl - 1; l >= 0; --l)
+      for (int y = 0; y < 16; ++y) {
+        uint32_t acc = 0;
+        for (uint32_t ee = S[l]; ee; ee &= ee - 1) acc |= rb[l + 1][(uint32_t)y & em(__builtin_ctz(ee))];
+        rb[l][y] = (uint16_t)acc;
       }
-      if (mg != 0 && !(!pg && b_pref)) {
-        const bool nar = narrower(mg, b_mask);
-        if ((pg && !b_pref) || nar || __popc(mg) == __popc(b_mask)) {
-          int32_t sg = 0;
-          for (int l = 0; l < nl; ++l) {
-            const int e = __ffs(rem[l]) - 1;
-            if (e != 31 && L[l].scored && ord_mask(e) == mg) { const int32_t x = score_at(e); if (x > sg) sg = x; }
-          }
-          if (pg && !b_pref) { b_mask = mg; b_pref = true; b_score = sg; }
-          else if (nar) { b_mask = mg; b_pref = pg; b_score = sg; }
-          else if (sg > b_score) { b_mask = mg; b_pref = pg; b_score = sg; }
-        }
+    bool have = false;
+    uint32_t b = 0;
+    int32_t sb = 0;
+    auto pruned = [&](int l, uint32_t y) -> bool {
+      const uint32_t cand = rb[l][y] & P;
+      if (!cand) return true;
+      if (!have || l < nsc) return false;
+      for (uint32_t xx = cand; xx; xx &= xx - 1) {
+        const uint32_t x = (uint32_t)__builtin_ctz(xx);
+        if (x < b || s_of(x) > sb) return false;
       }
-      int l = nl - 1;   // next permutation: the last list varies fastest
+      return true;
+    };
+    uint32_t rem[6], yv[6];
+    int l = 0, steps = 0;
+    yv[0] = full_mask;
+    rem[0] = S[0];
+    while (l >= 0) {
+      if (rem[l] == 0) { --l; continue; }
+      const int e = __builtin_ctz(rem[l]);
       rem[l] &= rem[l] - 1;
-      while (rem[l] == 0 && l > 0) {
-        rem[l] = S[l];
-        --l;
-        rem[l] &= rem[l] - 1;
+      if (++steps > kGenMergeMax) { over = true; break; }
+      ent[l] = e;
+      const uint32_t y = yv[l] & em(e);
+      if (pruned(l + 1, y)) continue;
+      if (l + 1 == nl) {   // a size-p* candidate that replaces the best (or the first one)
+        const int32_t sx = s_of(y);
+        if (!have || y < b || sx > sb) { have = true; b = y; sb = sx; }
+        continue;
       }
-      if (rem[0] == 0) break;
+      ++l;
+      yv[l] = y;
+      rem[l] = S[l];
+    }
+    if (over) break;
+    if (have) {
+      b_mask = b;
+      if (pass == 0) b_pref = true;
     }
   }
   aff_has = true;
@@ -469,8 +514,32 @@ __device__ __noinline__ bool merge_hint_lists_gen(const HintList* L, int nl, int
   return true;
 }
 
+// filterProvidersHints' lists of both providers: NodeNUMAResource's (cpu, then memory: the sorted names; kinds as
+// merge_hint_lists reads them) from its position bitmaps, then DeviceShare's r identical lists (gh, GH_* above).
+// Returns the number of lists (<= 5).
+__device__ __forceinline__ int gen_lists(uint32_t totc, uint32_t lc, uint32_t totm, uint32_t lm, uint32_t valid,
+                                         bool nil_hints, bool has_cpu, bool has_mem, bool tot_c_any, bool tot_m_any,
+                                         uint32_t gh, HintList* L) {
+  int nl = 0;
+  const int kc = nil_hints ? 0 : (lc ? 1 : ((has_cpu && tot_c_any) ? 2 : 0));
+  const int km = nil_hints ? 0 : (lm ? 1 : ((has_mem && tot_m_any) ? 2 : 0));
+  if (kc == 0 && km == 0) {
+    L[nl++] = HintList{0x80000000u, 0, true, false};   // no hints: one preferred any-numa hint
+  } else {
+    if (kc == 1) L[nl++] = HintList{lc, (int8_t)ord_size_first(totc), false, true};
+    if (kc == 2) L[nl++] = HintList{0x80000000u, 0, false, false};
+    if (km == 1) L[nl++] = HintList{lm, (int8_t)ord_size_first(totm), false, true};
+    if (km == 2) L[nl++] = HintList{0x80000000u, 0, false, false};
+  }
+  const int r = (int)((gh >> GH_R_SHIFT) & 3u);
+  const uint32_t gl = gh & GH_LIST & valid;
+  for (int k = 0; k < r; ++k)
+    L[nl++] = gl ? HintList{gl, (int8_t)((gh >> GH_MIN_SHIFT) & 7u), false, false} : HintList{0x80000000u, 0, false, false};
+  return nl;
+}
+
 // GetPodTopologyHints of both providers + Merge: NodeNUMAResource's lists from the row (every position summed), then
-// DeviceShare's (gh, above). *over: see merge_hint_lists_gen.
+// DeviceShare's (gh). *over: see merge_hint_lists_gen.
 template <class Src>
 __device__ __noinline__ bool hints_merge_gprov(const Src& src, int nz, int policy, bool nil_hints, bool has_cpu,
                                                bool has_mem, int64_t pcpu, int64_t mem, bool tot_c_any, bool tot_m_any,
@@ -487,22 +556,7 @@ __device__ __noinline__ bool hints_merge_gprov(const Src& src, int nz, int polic
     }
   }
   HintList L[5];
-  int nl = 0;
-  // NodeNUMAResource (the first provider): cpu, then memory (sorted names); kind as merge_hint_lists reads them
-  const int kc = nil_hints ? 0 : (lc ? 1 : ((has_cpu && tot_c_any) ? 2 : 0));
-  const int km = nil_hints ? 0 : (lm ? 1 : ((has_mem && tot_m_any) ? 2 : 0));
-  if (kc == 0 && km == 0) {
-    L[nl++] = HintList{0x80000000u, 0, true, false};   // no hints: one preferred any-numa hint
-  } else {
-    if (kc == 1) L[nl++] = HintList{lc, (int8_t)ord_size_first(totc), false, true};
-    if (kc == 2) L[nl++] = HintList{0x80000000u, 0, false, false};
-    if (km == 1) L[nl++] = HintList{lm, (int8_t)ord_size_first(totm), false, true};
-    if (km == 2) L[nl++] = HintList{0x80000000u, 0, false, false};
-  }
-  const int r = (int)((gh >> GH_R_SHIFT) & 3u);   // DeviceShare (the second provider): r identical lists
-  const uint32_t gl = gh & GH_LIST & valid;
-  for (int k = 0; k < r; ++k)
-    L[nl++] = gl ? HintList{gl, (int8_t)((gh >> GH_MIN_SHIFT) & 7u), false, false} : HintList{0x80000000u, 0, false, false};
+  const int nl = gen_lists(totc, lc, totm, lm, valid, nil_hints, has_cpu, has_mem, tot_c_any, tot_m_any, gh, L);
   auto score_at = [&](int mi) -> int32_t { return hint_score(src.sum(mi), pcpu, mem, pf); };
   return merge_hint_lists_gen(L, nl, nz, policy, score_at, aff_has, aff, over);
 }

@@ -97,11 +97,19 @@ __global__ void __launch_bounds__(64) merge_probe_kernel(const gs_merge_case* __
   if (i >= n) return;
   const gs_merge_case c = cs[i];
   auto score_at = [&](int mi) -> int32_t { return c.score[mi]; };
-  bool aff_has = false;
+  bool aff_has = false, over = false;
   uint32_t aff = 0;
-  const bool admit = merge_hint_lists(c.totc, c.lc, c.totm, c.lm, c.nz, c.policy, c.nil_hints != 0, c.has_cpu != 0,
-                                      c.has_mem != 0, c.tot_c_any != 0, c.tot_m_any != 0, score_at, aff_has, aff);
-  out[i] = gs_merge_result{admit ? 1 : 0, aff_has ? 1 : 0, aff, 0};
+  bool admit;
+  if (c.gpu_hints) {   // both providers: the extension path's general merge (merge_hint_lists_gen)
+    HintList L[5];
+    const int nl = gen_lists(c.totc, c.lc, c.totm, c.lm, ord_valid(c.nz), c.nil_hints != 0, c.has_cpu != 0,
+                             c.has_mem != 0, c.tot_c_any != 0, c.tot_m_any != 0, c.gpu_hints, L);
+    admit = merge_hint_lists_gen(L, nl, c.nz, c.policy, score_at, aff_has, aff, over);
+  } else {
+    admit = merge_hint_lists(c.totc, c.lc, c.totm, c.lm, c.nz, c.policy, c.nil_hints != 0, c.has_cpu != 0,
+                             c.has_mem != 0, c.tot_c_any != 0, c.tot_m_any != 0, score_at, aff_has, aff);
+  }
+  out[i] = gs_merge_result{admit ? 1 : 0, aff_has ? 1 : 0, aff, over ? 1 : 0};
 }
 
 hipError_t launch_merge_probe(const gs_merge_case* cases, int n, gs_merge_result* out, hipStream_t st) {

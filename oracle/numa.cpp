@@ -1219,6 +1219,28 @@ extern "C" int or_policy_merge(int policy, uint64_t numa_mask, int nlists, const
   return admit ? 1 : 0;
 }
 
+// The same with per-hint scores (NUMATopologyHint.Score, which mergeFilteredHints compares between equally wide masks)
+extern "C" int or_policy_merge_scored(int policy, uint64_t numa_mask, int nlists, const int32_t* lens,
+                                      const uint8_t* has_mask, const uint64_t* masks, const uint8_t* preferred,
+                                      const int64_t* scores, uint8_t* out_has_mask, uint64_t* out_mask,
+                                      uint8_t* out_preferred) {
+  if (policy == GS_NUMA_POLICY_NONE) {
+    *out_has_mask = 0; *out_mask = 0; *out_preferred = 0;
+    return 1;
+  }
+  std::vector<std::vector<orn::Hint>> lists(nlists);
+  int k = 0;
+  for (int i = 0; i < nlists; ++i)
+    for (int j = 0; j < lens[i]; ++j, ++k)
+      lists[i].push_back(orn::Hint{has_mask[k] != 0, masks[k], preferred[k] != 0, scores[k]});
+  orn::Hint best;
+  const bool admit = orn::policy_merge_filtered(policy, numa_mask, lists, &best);
+  *out_has_mask = best.has_mask ? 1 : 0;
+  *out_mask = best.has_mask ? best.mask : 0;
+  *out_preferred = best.preferred ? 1 : 0;
+  return admit ? 1 : 0;
+}
+
 // bitmask.IterateBitMasks (bitmask.go:206-222): the masks of every non-empty subset of `bits` in visit order
 extern "C" int or_iterate_bitmasks(const int32_t* bits, int nbits, uint64_t* out, int cap) {
   std::vector<int> b(bits, bits + nbits);

@@ -57,6 +57,7 @@ def _load() -> C.CDLL:
         "or_numa_topology_hints": (C.c_int, [P, P, C.c_uint32, P, P, P, C.c_uint32, P]),
         "or_take_cpus_test": (C.c_int, [C.c_int] * 5 + [P, P, P] + [C.c_int] * 4 + [P]),
         "or_policy_merge": (C.c_int, [C.c_int, C.c_uint64, C.c_int, P, P, P, P, P, P, P]),
+        "or_policy_merge_scored": (C.c_int, [C.c_int, C.c_uint64, C.c_int, P, P, P, P, P, P, P, P]),
         "or_iterate_bitmasks": (C.c_int, [P, C.c_int, P, C.c_int]),
         "or_pods_on_event": (C.c_int, [P, C.c_int, P, P, C.c_uint32]),
         "or_assign_cache_get": (C.c_int, [P, C.c_uint32, P, P, C.c_uint32]),
@@ -492,16 +493,18 @@ def take_cpus_test(topology, max_ref, available, alloc_ref, alloc_excl, needed, 
 
 def policy_merge(policy: int, numa_nodes, lists) -> tuple[dict, bool]:
     """topologymanager Policy.Merge over filterProvidersHints' lists (each a list of {"mask": bits|None,
-    "preferred": bool}) -> (merged hint, admit)."""
+    "preferred": bool, "score": int (optional, 0)}) -> (merged hint, admit)."""
     lens = np.array([len(l) for l in lists], np.int32)
     flat = [h for l in lists for h in l]
     has = np.array([h["mask"] is not None for h in flat], np.uint8)
     masks = np.array([sum(1 << b for b in (h["mask"] or [])) for h in flat], np.uint64)
     pref = np.array([bool(h["preferred"]) for h in flat], np.uint8)
+    scores = np.array([int(h.get("score", 0)) for h in flat], np.int64)
     oh, om, op = np.zeros(1, np.uint8), np.zeros(1, np.uint64), np.zeros(1, np.uint8)
     nm = sum(1 << b for b in numa_nodes)
-    admit = lib().or_policy_merge(policy, nm, len(lists), lens.ctypes.data, has.ctypes.data, masks.ctypes.data,
-                                  pref.ctypes.data, oh.ctypes.data, om.ctypes.data, op.ctypes.data)
+    admit = lib().or_policy_merge_scored(policy, nm, len(lists), lens.ctypes.data, has.ctypes.data, masks.ctypes.data,
+                                         pref.ctypes.data, scores.ctypes.data, oh.ctypes.data, om.ctypes.data,
+                                         op.ctypes.data)
     bits = [b for b in range(64) if int(om[0]) >> b & 1] if oh[0] else None
     return {"mask": bits, "preferred": bool(op[0])}, bool(admit)
 

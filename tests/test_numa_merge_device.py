@@ -156,3 +156,75 @@ def test_device_merge_reference_vectors():
             bad.append((pol, c["name"], got, w))
     assert not bad, bad
     print(f"device merge: {len(ok)} reference cases identical, {len(skipped)} outside the input domain: {skipped}")
+
+
+def _gen_case(rng):
+    """A random gs_merge_case with DeviceShare as the second provider (gpu_hints) and the filterProvidersHints lists it
+    stands for: NodeNUMAResource's cpu / memory lists (hint scores), then r identical GPU lists (score 0)."""
+    rec = np.zeros(1, abi.MERGE_CASE_DTYPE)[0]
+    nz = int(rng.integers(1, 5))
+    valid = [i for i, m in enumerate(KORD4) if m < (1 << nz)]
+    rec["nz"], rec["policy"] = nz, int(rng.choice([abi.GS_NUMA_POLICY_BEST_EFFORT, abi.GS_NUMA_POLICY_RESTRICTED,
+                                                    abi.GS_NUMA_POLICY_SINGLE_NUMA_NODE]))
+    rec["score"] = rng.integers(0, 101, 15)
+    rec["nil_hints"] = int(rng.random() < 0.05)
+
+    def pick():
+        return sum(1 << i for i in valid if rng.random() < 0.5)
+    for res in ("c", "m"):
+        has = rng.random() < 0.85
+        l = pick()
+        tot = l | pick()
+        if rng.random() < 0.1:
+            l = 0   # covered in total but never free: the {nil, false} marker
+        if not has:
+            l = tot = 0   # a resource the pod does not request has no positions
+        rec["l" + res], rec["tot" + res] = l, tot
+        rec["has_cpu" if res == "c" else "has_mem"] = int(has)
+        rec["tot_c_any" if res == "c" else "tot_m_any"] = int(tot != 0)
+    r = int(rng.choice([2, 3]))
+    gl = 0 if rng.random() < 0.1 else pick()
+    sizes = [bin(KORD4[i]).count("1") for i in range(15) if gl >> i & 1]
+    gmin = int(rng.integers(1, (min(sizes) if sizes else nz) + 1))
+    rec["gpu_hints"] = gl | (gmin << 16) | (r << 20)
+    lists = []
+    if not rec["nil_hints"]:
+        for l, tot, has in ((rec["lc"], rec["totc"], rec["has_cpu"]), (rec["lm"], rec["totm"], rec["has_mem"])):
+            if not has or not tot:
+                continue
+            if l == 0:
+                lists.append([{"mask": None, "preferred": False}])
+                continue
+            smin = min(bin(KORD4[i]).count("1") for i in range(15) if tot >> i & 1)
+            lists.append([{"mask": [z for z in range(4) if KORD4[i] >> z & 1],
+                           "preferred": bin(KORD4[i]).count("1") == smin, "score": int(rec["score"][i])}
+                          for i in range(15) if l >> i & 1])
+    if not lists:
+        lists.append([{"mask": None, "preferred": True}])   # NodeNUMAResource without hints
+    g = ([{"mask": [z for z in range(4) if KORD4[i] >> z & 1], "preferred": bin(KORD4[i]).count("1") == gmin}
+          for i in range(15) if gl >> i & 1] or [{"mask": None, "preferred": False}])
+    lists += [g] * r
+    return rec, lists
+
+
+@pytest.mark.gpu
+def test_device_merge_with_deviceshare_provider_matches_reference():
+    """merge_hint_lists_gen (the extension path's merge over NodeNUMAResource's and DeviceShare's hint lists) on random
+    list sets against the reference's permutation scan (oracle, mergeFilteredHints with hint scores), bit-exact."""
+    from koordinator_amd import config
+    from koordinator_amd.engine import Engine
+    rng = np.random.default_rng(20260)
+    cases = [_gen_case(rng) for _ in range(4000)]
+    recs = np.array([c[0] for c in cases], abi.MERGE_CASE_DTYPE)
+    e = Engine(config.make_config(4, enabled=abi.GS_ENABLE_ALL))
+    got = e.numa_merge(recs)
+    assert (got["pad"] == 0).all()   # no search past its bound
+    for k, (rec, lists) in enumerate(cases):
+        nz = int(rec["nz"])
+        hint, admit = orc.policy_merge(int(rec["policy"]), list(range(nz)), lists)
+        want_has = hint["mask"] is not None
+        want_aff = _bits(hint["mask"]) if want_has else 0
+        g = got[k]
+        assert (bool(g["admit"]), bool(g["aff_has"])) == (admit, want_has), (k, rec, lists, hint)
+        if want_has:
+            assert int(g["aff"]) == want_aff, (k, rec, lists, hint)
