@@ -193,6 +193,7 @@ struct gs_ctx {
   MirrorView slab_mv{nullptr, nullptr, 0};   // the eval pass's dense copy of the NUMA-policy rows (gather_numa_kernel)
   uint32_t slab_cap = 0;
   bool numa_idx_stale = true;
+  int64_t prep_now = INT64_MIN;             // `now` of the last full node_prep pass
   // registered topologies in bit-plane form (the commit kernel's cpuset Reserve), and the host re-check of
   // every device-chosen cpuset (GS_VERIFY_CPUSET=1)
   TopoDev* d_topos = nullptr;
@@ -207,10 +208,8 @@ struct gs_ctx {
   std::vector<std::vector<uint64_t>> rsv_node;   // uids per node, ascending
   std::unordered_map<uint64_t, std::vector<uint64_t>> rsv_owner;   // owner key -> uids
   DevNode* d_dev = nullptr;
-  DevNode* h_dev_stage = nullptr;   // ext_flush_devices staging (pinned / device)
+  DevNode* h_dev_stage = nullptr;   // ext_flush_devices staging (pinned / device): images, then node indices
   DevNode* d_dev_stage = nullptr;
-  uint32_t* h_dev_idx = nullptr;
-  uint32_t* d_dev_idx = nullptr;
   ExtPod* d_xpod = nullptr;
   ExtRec* d_xrec = nullptr;
   ExtRes* d_xres = nullptr;
@@ -220,7 +219,11 @@ struct gs_ctx {
   int32_t* d_xnom = nullptr;
   int32_t* d_xT = nullptr;
   ExtOut* d_xout = nullptr;
-  ExtPod* h_xpod = nullptr;
+  ExtPod* h_xpod = nullptr;          // (the host half of d_xin's first section)
+  unsigned char* h_xin = nullptr;    // one extension pod's inputs, staged for ONE copy: ExtPod | PodVec | ExtRec[] |
+  unsigned char* d_xin = nullptr;    // ExtRes[] (pinned host / device, ext_stage_layout)
+  PodVec* d_xpv = nullptr;
+  size_t xin_off_rec = 0, xin_off_res = 0, xin_bytes = 0;
   ExtOut* h_xout = nullptr;
   int32_t* h_xnom = nullptr;
   std::vector<ExtRec> xrec;
@@ -645,22 +648,32 @@ int flush_rows(gs_ctx* c) {
     uint32_t n = (uint32_t)std::min<size_t>(c->stage_cap, c->dirty_list.size() - done);
     // staging buffers are reused: the previous scatter must have consumed them
     HIP_TRY(c, hipStreamSynchronize(c->st));
+    // one staged block, one copy: the n rows, then their node indices
+    uint32_t* h_idx = reinterpret_cast<uint32_t*>(c->h_stage_rows + (size_t)n * ROW_WORDS);
     for (uint32_t j = 0; j < n; ++j) {
       uint32_t i = c->dirty_list[done + j];
-      c->h_stage_idx[j] = i;
+      h_idx[j] = i;
       derive_row(c, i, c->h_stage_rows + (size_t)j * ROW_WORDS);
       derive_row_numa(c, i, c->h_stage_rows + (size_t)j * ROW_WORDS);
       c->row_dirty[i] = 0;
     }
-    HIP_TRY(c, hipMemcpyAsync(c->d_stage_idx, c->h_stage_idx, n * 4, hipMemcpyHostToDevice, c->st));
-    HIP_TRY(c, hipMemcpyAsync(c->d_stage_rows, c->h_stage_rows, (size_t)n * ROW_WORDS * 8, hipMemcpyHostToDevice, c->st));
-    HIP_TRY(c, launch_scatter_rows(c->mv, c->d_stage_idx, c->d_stage_rows, n, c->st));
+    HIP_TRY(c, hipMemcpyAsync(c->d_stage_rows, c->h_stage_rows, (size_t)n * (ROW_WORDS * 8 + 4), hipMemcpyHostToDevice,
+                              c->st));
+    const uint32_t* d_idx = reinterpret_cast<const uint32_t*>(c->d_stage_rows + (size_t)n * ROW_WORDS);
+    HIP_TRY(c, launch_scatter_rows(c->mv, d_idx, c->d_stage_rows, n, c->st));
+    // the rows' LoadAware verdicts at `now` (node_prep), unless a full pass is due anyway
+    if (!c->prep_stale && c->prep_now == c->now) {
+      const gs_loadaware_args& la = c->cfg.loadaware;
+      HIP_TRY(c, launch_node_prep_idx(c->mv, d_idx, n, c->now, la.filter_expired_node_metrics, la.has_node_metric_expiration,
+                                      la.has_node_metric_expiration ? la.node_metric_expiration_seconds * 1000000000LL : 0,
+                                      c->st));
+    }
     c->stats.delta_rows += n;
     c->stats.delta_bytes += (uint64_t)n * (4 + ROW_WORDS * 8);
     done += n;
   }
   c->dirty_list.clear();
-  c->prep_stale = true;
+  if (c->prep_now != c->now) c->prep_stale = true;
   return GS_OK;
 }
 
@@ -670,6 +683,7 @@ int node_prep(gs_ctx* c) {
   HIP_TRY(c, launch_node_prep(c->mv, 0, c->N, c->now, a.filter_expired_node_metrics, a.has_node_metric_expiration,
                               exp_ns, c->st));
   c->prep_stale = false;
+  c->prep_now = c->now;
   return GS_OK;
 }
 
@@ -1019,8 +1033,7 @@ int launch_batch(gs_ctx* c, int b, const int32_t* prev, const PlacementDev* prev
   // waits on each one) keep it in order on st: the extra queue hop costs more than it hides there.
   hipStream_t rb = b >= 32 ? c->st_rb : c->st;
   if (rb != c->st) HIP_TRY(c, hipStreamWaitEvent(rb, c->ev[4], 0));
-  HIP_TRY(c, hipMemcpyAsync(c->h_committed, c->d_committed, 16, hipMemcpyDeviceToHost, rb));
-  HIP_TRY(c, hipMemcpyAsync(c->h_out, c->d_out, sizeof(PlacementDev) * b, hipMemcpyDeviceToHost, rb));
+  HIP_TRY(c, hipMemcpyAsync(c->h_committed, c->d_committed, 16 + sizeof(PlacementDev) * b, hipMemcpyDeviceToHost, rb));
   HIP_TRY(c, hipEventRecord(c->ev[5], rb));
   return GS_OK;
 }
@@ -1191,14 +1204,40 @@ int ext_alloc(gs_ctx* c) {
   HIP_TRY(c, hipMemcpy(c->d_dev, img.data(), sizeof(DevNode) * c->N, hipMemcpyHostToDevice));
   c->dev_dirty_list.clear();
   std::fill(c->dev_dirty.begin(), c->dev_dirty.end(), 0);
-  HIP_TRY(c, hipMalloc(&c->d_xpod, sizeof(ExtPod)));
   HIP_TRY(c, hipMalloc(&c->d_xtot, 4 * (size_t)c->ld));
   HIP_TRY(c, hipMalloc(&c->d_xT, 4 * ext_select_scratch_words(c->ld)));
   HIP_TRY(c, hipMalloc(&c->d_xds, 2 * (size_t)c->ld));
   HIP_TRY(c, hipMalloc(&c->d_xrs, 2 * (size_t)c->ld));
   HIP_TRY(c, hipMalloc(&c->d_xout, sizeof(ExtOut)));
-  HIP_TRY(c, hipHostMalloc(&c->h_xpod, sizeof(ExtPod), hipHostMallocDefault));
-  HIP_TRY(c, hipHostMalloc(&c->h_xout, sizeof(ExtOut), hipHostMallocDefault));
+  HIP_TRY(c, hipHostMalloc(&c->h_xout, sizeof(ExtOut), hipHostMallocDefault));   // written by ext_finish_kernel
+  return GS_OK;
+}
+
+// The extension pod's input block (pinned host + device, one H2D copy per pod) and the nomination arrays, for at
+// least nrec matched records and nres matched reservations.
+int ext_stage_reserve(gs_ctx* c, uint32_t nrec, uint32_t nres) {
+  if (c->h_xin && nrec <= c->xrec_cap && nres <= c->xres_cap) return GS_OK;
+  c->xrec_cap = std::max<uint32_t>({64, c->xrec_cap, nrec * 2});
+  c->xres_cap = std::max<uint32_t>({64, c->xres_cap, nres * 2});
+  auto al = [](size_t x) { return (x + 15) & ~(size_t)15; };
+  const size_t off_pv = al(sizeof(ExtPod));
+  c->xin_off_rec = off_pv + al(sizeof(PodVec));
+  c->xin_off_res = c->xin_off_rec + al(sizeof(ExtRec) * c->xrec_cap);
+  c->xin_bytes = c->xin_off_res + sizeof(ExtRes) * c->xres_cap;
+  HIP_TRY(c, hipStreamSynchronize(c->st));
+  if (c->h_xin) (void)hipHostFree(c->h_xin);
+  if (c->d_xin) (void)hipFree(c->d_xin);
+  if (c->d_xnom) (void)hipFree(c->d_xnom);
+  if (c->h_xnom) (void)hipHostFree(c->h_xnom);
+  HIP_TRY(c, hipHostMalloc(&c->h_xin, c->xin_bytes, hipHostMallocDefault));
+  HIP_TRY(c, hipMalloc(&c->d_xin, c->xin_bytes));
+  HIP_TRY(c, hipMalloc(&c->d_xnom, 4 * c->xrec_cap));
+  HIP_TRY(c, hipHostMalloc(&c->h_xnom, 4 * c->xrec_cap, hipHostMallocDefault));   // written by ext_finish_kernel
+  c->h_xpod = reinterpret_cast<ExtPod*>(c->h_xin);
+  c->d_xpod = reinterpret_cast<ExtPod*>(c->d_xin);
+  c->d_xpv = reinterpret_cast<PodVec*>(c->d_xin + off_pv);
+  c->d_xrec = reinterpret_cast<ExtRec*>(c->d_xin + c->xin_off_rec);
+  c->d_xres = reinterpret_cast<ExtRes*>(c->d_xin + c->xin_off_res);
   return GS_OK;
 }
 
@@ -1206,24 +1245,23 @@ int ext_alloc(gs_ctx* c) {
 int ext_flush_devices(gs_ctx* c) {
   if (c->dev_dirty_list.empty()) return GS_OK;
   if (!c->d_dev) return ext_alloc(c);
-  if (!c->h_dev_stage) {
-    HIP_TRY(c, hipHostMalloc(&c->h_dev_stage, sizeof(DevNode) * EXT_DEV_STAGE, hipHostMallocDefault));
-    HIP_TRY(c, hipHostMalloc(&c->h_dev_idx, 4 * EXT_DEV_STAGE, hipHostMallocDefault));
-    HIP_TRY(c, hipMalloc(&c->d_dev_stage, sizeof(DevNode) * EXT_DEV_STAGE));
-    HIP_TRY(c, hipMalloc(&c->d_dev_idx, 4 * EXT_DEV_STAGE));
+  if (!c->h_dev_stage) {   // n images, then their node indices: one copy
+    HIP_TRY(c, hipHostMalloc(&c->h_dev_stage, (sizeof(DevNode) + 4) * EXT_DEV_STAGE, hipHostMallocDefault));
+    HIP_TRY(c, hipMalloc(&c->d_dev_stage, (sizeof(DevNode) + 4) * EXT_DEV_STAGE));
   }
   for (size_t done = 0; done < c->dev_dirty_list.size();) {
     const uint32_t n = (uint32_t)std::min<size_t>(EXT_DEV_STAGE, c->dev_dirty_list.size() - done);
     HIP_TRY(c, hipStreamSynchronize(c->st));   // the previous scatter has consumed the staging buffers
+    uint32_t* h_idx = reinterpret_cast<uint32_t*>(c->h_dev_stage + n);
     for (uint32_t j = 0; j < n; ++j) {
       const uint32_t i = c->dev_dirty_list[done + j];
       c->h_dev_stage[j] = dev_image(c, i);
-      c->h_dev_idx[j] = i;
+      h_idx[j] = i;
       c->dev_dirty[i] = 0;
     }
-    HIP_TRY(c, hipMemcpyAsync(c->d_dev_idx, c->h_dev_idx, 4 * n, hipMemcpyHostToDevice, c->st));
-    HIP_TRY(c, hipMemcpyAsync(c->d_dev_stage, c->h_dev_stage, sizeof(DevNode) * n, hipMemcpyHostToDevice, c->st));
-    HIP_TRY(c, launch_scatter_devnodes(c->d_dev, c->d_dev_idx, c->d_dev_stage, n, c->st));
+    HIP_TRY(c, hipMemcpyAsync(c->d_dev_stage, c->h_dev_stage, (sizeof(DevNode) + 4) * n, hipMemcpyHostToDevice, c->st));
+    HIP_TRY(c, launch_scatter_devnodes(c->d_dev, reinterpret_cast<const uint32_t*>(c->d_dev_stage + n), c->d_dev_stage,
+                                       n, c->st));
     done += n;
   }
   c->dev_dirty_list.clear();
@@ -1417,20 +1455,7 @@ int ext_schedule_one(gs_ctx* c, const gs_pod& pod, const gs_pod_ext& e, uint64_t
     a = b;
   }
   const int nrec = (int)c->xrec.size();
-  if ((uint32_t)nrec > c->xrec_cap) {
-    if (c->d_xrec) (void)hipFree(c->d_xrec);
-    if (c->d_xnom) (void)hipFree(c->d_xnom);
-    if (c->h_xnom) (void)hipHostFree(c->h_xnom);
-    c->xrec_cap = std::max<uint32_t>(64, (uint32_t)nrec * 2);
-    HIP_TRY(c, hipMalloc(&c->d_xrec, sizeof(ExtRec) * c->xrec_cap));
-    HIP_TRY(c, hipMalloc(&c->d_xnom, 4 * c->xrec_cap));
-    HIP_TRY(c, hipHostMalloc(&c->h_xnom, 4 * c->xrec_cap, hipHostMallocDefault));
-  }
-  if (c->xres.size() > c->xres_cap) {
-    if (c->d_xres) (void)hipFree(c->d_xres);
-    c->xres_cap = std::max<uint32_t>(64, (uint32_t)c->xres.size() * 2);
-    HIP_TRY(c, hipMalloc(&c->d_xres, sizeof(ExtRes) * c->xres_cap));
-  }
+  if ((rc = ext_stage_reserve(c, (uint32_t)nrec, (uint32_t)c->xres.size()))) return rc;
   ExtPod& xp = *c->h_xpod;
   xp = ExtPod{};
   for (int r = 0; r < 3; ++r) { xp.gpu_req[r] = greq[r]; xp.dev_w[r] = c->ext.device_weights[r]; }
@@ -1455,8 +1480,7 @@ int ext_schedule_one(gs_ctx* c, const gs_pod& pod, const gs_pod_ext& e, uint64_t
   xp.seq = seq;
   // GPU names are scalar requests: the Fit filter's all-zero short cut no longer applies
   if (gpu_names_all || xres_all) v.flags &= ~PF_ALL_ZERO;
-  c->h_pods[0] = v;
-  c->h_seq[0] = seq;
+  *reinterpret_cast<PodVec*>(c->h_xin + ((sizeof(ExtPod) + 15) & ~(size_t)15)) = v;
   // numa_idx (the eval pass's NUMA-policy work list) as launch_batch keeps it
   if (c->numa_on && c->numa_idx_stale) {
     std::vector<uint32_t> idx;
@@ -1473,30 +1497,34 @@ int ext_schedule_one(gs_ctx* c, const gs_pod& pod, const gs_pod_ext& e, uint64_t
     c->numa_idx_stale = false;
   }
   const int prod_cols = (v.flags & PF_PROD_SCORE) ? 1 : 0;
-  HIP_TRY(c, hipMemcpyAsync(c->d_pods, c->h_pods, sizeof(PodVec), hipMemcpyHostToDevice, c->st));
-  HIP_TRY(c, hipMemcpyAsync(c->d_xpod, c->h_xpod, sizeof(ExtPod), hipMemcpyHostToDevice, c->st));
+  // inputs: one copy of the staged block (ExtPod, PodVec, the matched records and reservations)
   if (nrec) {
-    HIP_TRY(c, hipMemcpyAsync(c->d_xrec, c->xrec.data(), sizeof(ExtRec) * nrec, hipMemcpyHostToDevice, c->st));
-    HIP_TRY(c, hipMemcpyAsync(c->d_xres, c->xres.data(), sizeof(ExtRes) * c->xres.size(), hipMemcpyHostToDevice, c->st));
+    std::memcpy(c->h_xin + c->xin_off_rec, c->xrec.data(), sizeof(ExtRec) * nrec);
+    std::memcpy(c->h_xin + c->xin_off_res, c->xres.data(), sizeof(ExtRes) * c->xres.size());
   }
+  const size_t in_bytes = nrec ? c->xin_off_res + sizeof(ExtRes) * c->xres.size() : c->xin_off_rec;
+  HIP_TRY(c, hipMemcpyAsync(c->d_xin, c->h_xin, in_bytes, hipMemcpyHostToDevice, c->st));
   HIP_TRY(c, hipEventRecord(c->ev[0], c->st));
-  HIP_TRY(c, launch_eval(c->mv, c->d_pods, 1, c->pf, c->n0, c->n1, c->d_S, c->ld, prod_cols, c->d_numa_idx, c->numa_n,
+  HIP_TRY(c, launch_eval(c->mv, c->d_xpv, 1, c->pf, c->n0, c->n1, c->d_S, c->ld, prod_cols, c->d_numa_idx, c->numa_n,
                          c->d_aff, c->st));
   HIP_TRY(c, hipEventRecord(c->ev[1], c->st));
-  HIP_TRY(c, launch_ext_nodes(c->d_dev, c->d_S, c->n0, c->n1, c->d_xpod, c->d_xtot, c->d_xds, c->d_xrs, c->st));
-  HIP_TRY(c, launch_ext_matched(c->mv, c->d_pods, c->pf, prod_cols, c->d_dev, c->d_xpod, c->d_xrec, c->d_xres, nrec, c->d_xtot,
-                                c->d_xrs, c->d_xnom, c->d_xT, c->n1 - c->n0, c->st));
+  // (ext_nodes_kernel also resets the select accumulators; ext_matched runs for pods with matched reservations only)
+  HIP_TRY(c, launch_ext_nodes(c->d_dev, c->d_S, c->n0, c->n1, c->d_xpod, c->d_xtot, c->d_xds, c->d_xrs, c->d_xT,
+                              c->st));
+  if (nrec)
+    HIP_TRY(c, launch_ext_matched(c->mv, c->d_xpv, c->pf, prod_cols, c->d_dev, c->d_xpod, c->d_xrec, c->d_xres, nrec,
+                                  c->d_xtot, c->d_xrs, c->d_xnom, c->d_xT, c->n1 - c->n0, c->st));
   // GPU pods on NUMA-policy nodes: DeviceShare is the topology manager's second hint provider
   if (gmask && c->numa_on && c->numa_n)
-    HIP_TRY(c, launch_ext_numa(c->mv, c->d_pods, c->pf, prod_cols, c->d_dev, c->d_xpod, c->d_numa_idx, c->numa_n, c->n0,
+    HIP_TRY(c, launch_ext_numa(c->mv, c->d_xpv, c->pf, prod_cols, c->d_dev, c->d_xpod, c->d_numa_idx, c->numa_n, c->n0,
                                c->d_xtot, c->d_xds, c->d_aff, c->d_xT, c->n1 - c->n0, c->st));
   HIP_TRY(c, launch_ext_select(c->d_xtot, c->d_xds, c->d_xrs, c->d_xrec, c->n0, c->n1, c->d_xpod, c->cfg.seed, c->d_xT,
                                c->d_xout, c->st));
-  if (c->numa_on)   // NodeNUMAResource Reserve of the selected node along its affinity
-    HIP_TRY(c, launch_ext_reserve_numa(c->mv, c->d_pods, c->pf, prod_cols, c->d_aff, c->n0, c->d_xout, c->st));
+  // outputs: the NodeNUMAResource Reserve of the selected node along its affinity, and the result and nominations
+  // written straight into pinned host memory (no copy)
+  HIP_TRY(c, launch_ext_finish(c->mv, c->d_xpv, c->pf, prod_cols, c->d_aff, c->n0, c->numa_on ? 1 : 0, c->d_xout,
+                               c->d_xnom, nrec, c->h_xout, c->h_xnom, c->st));
   HIP_TRY(c, hipEventRecord(c->ev[4], c->st));
-  HIP_TRY(c, hipMemcpyAsync(c->h_xout, c->d_xout, sizeof(ExtOut), hipMemcpyDeviceToHost, c->st));
-  if (nrec) HIP_TRY(c, hipMemcpyAsync(c->h_xnom, c->d_xnom, 4 * nrec, hipMemcpyDeviceToHost, c->st));
   HIP_TRY(c, hipStreamSynchronize(c->st));
   c->stats.eval_ms += ev_ms(c->ev[0], c->ev[1]);
   c->stats.commit_ms += ev_ms(c->ev[1], c->ev[4]);
@@ -1711,28 +1739,31 @@ int gs_create(const gs_config* cfg, gs_ctx** out) {
   c->mv.i32 = c->d_i32;
   c->mv.npad = (uint32_t)np;
   c->ld = c->npad;
-  if ((e = hipMalloc(&c->d_pods, sizeof(PodVec) * c->B)) != hipSuccess) return bail("hipMalloc", e);
-  if ((e = hipMalloc(&c->d_seq, 8 * c->B)) != hipSuccess) return bail("hipMalloc", e);
+  // pods | seq and committed | out share one allocation each: one copy per batch each way
+  static_assert(sizeof(PodVec) % 8 == 0 && sizeof(PlacementDev) % 8 == 0, "staging layout");
+  if ((e = hipMalloc(&c->d_pods, (sizeof(PodVec) + 8) * c->B)) != hipSuccess) return bail("hipMalloc", e);
+  c->d_seq = reinterpret_cast<uint64_t*>(c->d_pods + c->B);
   if ((e = hipMalloc(&c->d_S, (size_t)c->B * c->ld * 2)) != hipSuccess) return bail("hipMalloc S", e);
   if ((e = hipMalloc(&c->d_aff, (size_t)c->B * c->ld)) != hipSuccess) return bail("hipMalloc aff", e);
   size_t xb = xchg_block_bytes(c->B, LCAP);
   if ((e = hipMalloc(&c->d_xchg_send, xb)) != hipSuccess) return bail("hipMalloc", e);
   c->xchg_bytes = xb;
-  if ((e = hipMalloc(&c->d_out, sizeof(PlacementDev) * c->B)) != hipSuccess) return bail("hipMalloc", e);
-  if ((e = hipMalloc(&c->d_committed, 16)) != hipSuccess) return bail("hipMalloc", e);
+  if ((e = hipMalloc(&c->d_committed, 16 + sizeof(PlacementDev) * c->B)) != hipSuccess) return bail("hipMalloc", e);
+  c->d_out = reinterpret_cast<PlacementDev*>(c->d_committed + 4);
   if ((e = hipMalloc(&c->d_tb, sizeof(int32_t) * TB_N * c->B)) != hipSuccess) return bail("hipMalloc", e);
   if ((e = hipMalloc(&c->d_rowstat, sizeof(RowStat) * (1 + MAX_RANKS))) != hipSuccess) return bail("hipMalloc", e);
   if ((e = hipMalloc(&c->d_sel, 4 * (1 + MAX_RANKS))) != hipSuccess) return bail("hipMalloc", e);
   c->stage_cap = std::min<uint32_t>(c->N, 65536);
-  if ((e = hipMalloc(&c->d_stage_idx, 4 * c->stage_cap)) != hipSuccess) return bail("hipMalloc", e);
-  if ((e = hipMalloc(&c->d_stage_rows, (size_t)8 * ROW_WORDS * c->stage_cap)) != hipSuccess) return bail("hipMalloc", e);
-  if ((e = hipHostMalloc(&c->h_stage_idx, 4 * c->stage_cap, hipHostMallocDefault)) != hipSuccess) return bail("hipHostMalloc", e);
-  if ((e = hipHostMalloc(&c->h_stage_rows, (size_t)8 * ROW_WORDS * c->stage_cap, hipHostMallocDefault)) != hipSuccess)
+  // staged rows then their node indices (flush_rows)
+  if ((e = hipMalloc(&c->d_stage_rows, (size_t)(8 * ROW_WORDS + 4) * c->stage_cap)) != hipSuccess) return bail("hipMalloc", e);
+  if ((e = hipHostMalloc(&c->h_stage_rows, (size_t)(8 * ROW_WORDS + 4) * c->stage_cap, hipHostMallocDefault)) != hipSuccess)
     return bail("hipHostMalloc", e);
-  if ((e = hipHostMalloc(&c->h_pods, sizeof(PodVec) * c->B, hipHostMallocDefault)) != hipSuccess) return bail("hipHostMalloc", e);
-  if ((e = hipHostMalloc(&c->h_seq, 8 * c->B, hipHostMallocDefault)) != hipSuccess) return bail("hipHostMalloc", e);
-  if ((e = hipHostMalloc(&c->h_out, sizeof(PlacementDev) * c->B, hipHostMallocDefault)) != hipSuccess) return bail("hipHostMalloc", e);
-  if ((e = hipHostMalloc(&c->h_committed, 16, hipHostMallocDefault)) != hipSuccess) return bail("hipHostMalloc", e);
+  if ((e = hipHostMalloc(&c->h_pods, (sizeof(PodVec) + 8) * c->B, hipHostMallocDefault)) != hipSuccess)
+    return bail("hipHostMalloc", e);
+  c->h_seq = reinterpret_cast<uint64_t*>(c->h_pods + c->B);
+  if ((e = hipHostMalloc(&c->h_committed, 16 + sizeof(PlacementDev) * c->B, hipHostMallocDefault)) != hipSuccess)
+    return bail("hipHostMalloc", e);
+  c->h_out = reinterpret_cast<PlacementDev*>(c->h_committed + 4);
   if ((e = hipHostMalloc(&c->h_xchg_send, xb, hipHostMallocDefault)) != hipSuccess) return bail("hipHostMalloc", e);
   (void)hipMemset(c->d_S, 0xff, (size_t)c->B * c->ld * 2);
   {
@@ -1749,14 +1780,16 @@ int gs_create(const gs_config* cfg, gs_ctx** out) {
     if ((e = hipMalloc(&s1.d_S, (size_t)c->B * c->ld * 2)) != hipSuccess) return bail("hipMalloc S", e);
     if ((e = hipMalloc(&s1.d_aff, (size_t)c->B * c->ld)) != hipSuccess) return bail("hipMalloc aff", e);
     (void)hipMemset(s1.d_S, 0xff, (size_t)c->B * c->ld * 2);
-    if ((e = hipMalloc(&s1.d_pods, sizeof(PodVec) * c->B)) != hipSuccess) return bail("hipMalloc", e);
-    if ((e = hipMalloc(&s1.d_seq, 8 * c->B)) != hipSuccess) return bail("hipMalloc", e);
-    if ((e = hipMalloc(&s1.d_out, sizeof(PlacementDev) * c->B)) != hipSuccess) return bail("hipMalloc", e);
-    if ((e = hipMalloc(&s1.d_committed, 16)) != hipSuccess) return bail("hipMalloc", e);
-    if ((e = hipHostMalloc(&s1.h_pods, sizeof(PodVec) * c->B, hipHostMallocDefault)) != hipSuccess) return bail("hipHostMalloc", e);
-    if ((e = hipHostMalloc(&s1.h_seq, 8 * c->B, hipHostMallocDefault)) != hipSuccess) return bail("hipHostMalloc", e);
-    if ((e = hipHostMalloc(&s1.h_out, sizeof(PlacementDev) * c->B, hipHostMallocDefault)) != hipSuccess) return bail("hipHostMalloc", e);
-    if ((e = hipHostMalloc(&s1.h_committed, 16, hipHostMallocDefault)) != hipSuccess) return bail("hipHostMalloc", e);
+    if ((e = hipMalloc(&s1.d_pods, (sizeof(PodVec) + 8) * c->B)) != hipSuccess) return bail("hipMalloc", e);
+    s1.d_seq = reinterpret_cast<uint64_t*>(s1.d_pods + c->B);
+    if ((e = hipMalloc(&s1.d_committed, 16 + sizeof(PlacementDev) * c->B)) != hipSuccess) return bail("hipMalloc", e);
+    s1.d_out = reinterpret_cast<PlacementDev*>(s1.d_committed + 4);
+    if ((e = hipHostMalloc(&s1.h_pods, (sizeof(PodVec) + 8) * c->B, hipHostMallocDefault)) != hipSuccess)
+      return bail("hipHostMalloc", e);
+    s1.h_seq = reinterpret_cast<uint64_t*>(s1.h_pods + c->B);
+    if ((e = hipHostMalloc(&s1.h_committed, 16 + sizeof(PlacementDev) * c->B, hipHostMallocDefault)) != hipSuccess)
+      return bail("hipHostMalloc", e);
+    s1.h_out = reinterpret_cast<PlacementDev*>(s1.h_committed + 4);
     for (auto& ev : s1.ev)
       if ((e = hipEventCreate(&ev)) != hipSuccess) return bail("hipEventCreate", e);
   }
@@ -1787,12 +1820,12 @@ int gs_destroy(gs_ctx* c) {
     for (int k = 0; k < 8; ++k) fprintf(stderr, " %llu", (unsigned long long)c->ht_busy_hist[k]);
     fprintf(stderr, "\n");
   }
-  for (void* p : {(void*)c->d_dev_stage, (void*)c->d_dev_idx}) if (p) (void)hipFree(p);
-  for (void* p : {(void*)c->h_dev_stage, (void*)c->h_dev_idx}) if (p) (void)hipHostFree(p);
-  for (void* p : {(void*)c->d_dev, (void*)c->d_xpod, (void*)c->d_xrec, (void*)c->d_xres, (void*)c->d_xtot,
+  if (c->d_dev_stage) (void)hipFree(c->d_dev_stage);
+  if (c->h_dev_stage) (void)hipHostFree(c->h_dev_stage);
+  for (void* p : {(void*)c->d_dev, (void*)c->d_xin, (void*)c->d_xtot,
                   (void*)c->d_xds, (void*)c->d_xrs, (void*)c->d_xnom, (void*)c->d_xT, (void*)c->d_xout})
     if (p) (void)hipFree(p);
-  for (void* p : {(void*)c->h_xpod, (void*)c->h_xout, (void*)c->h_xnom})
+  for (void* p : {(void*)c->h_xin, (void*)c->h_xout, (void*)c->h_xnom})
     if (p) (void)hipHostFree(p);
   if (c->d_stamps) {
     std::vector<uint64_t> sa(520);
@@ -1859,21 +1892,21 @@ int gs_destroy(gs_ctx* c) {
       if (sl.ev_go) (void)hipEventDestroy(sl.ev_go);
       if (sl.ev_evdone) (void)hipEventDestroy(sl.ev_evdone);
     }
-    void* d1[] = {s1.d_pods, s1.d_seq, s1.d_out, s1.d_committed, s1.d_S, s1.d_aff};
+    void* d1[] = {s1.d_pods, s1.d_committed, s1.d_S, s1.d_aff};   // (seq / out live inside pods / committed)
     for (void* p : d1)
       if (p) (void)hipFree(p);
-    void* h1[] = {s1.h_pods, s1.h_seq, s1.h_out, s1.h_committed};
+    void* h1[] = {s1.h_pods, s1.h_committed};
     for (void* p : h1)
       if (p) (void)hipHostFree(p);
     for (auto& ev : s1.ev)
       if (ev) (void)hipEventDestroy(ev);
   }
-  void* dev[] = {c->d_i64, c->d_i32, c->d_pods, c->d_seq, c->d_S, c->d_xchg_send, c->d_xchg_recv, c->d_xmerged, c->d_out,
+  void* dev[] = {c->d_i64, c->d_i32, c->d_pods, c->d_S, c->d_xchg_send, c->d_xchg_recv, c->d_xmerged,
                  c->d_committed, c->d_rowstat, c->d_sel, c->d_stage_idx, c->d_stage_rows, c->d_numa_idx,
                  c->d_topos, c->d_aff, c->d_tb};
   for (void* p : dev)
     if (p) (void)hipFree(p);
-  void* host[] = {c->h_pods, c->h_seq, c->h_out, c->h_committed, c->h_stage_idx, c->h_stage_rows, c->h_xchg_send,
+  void* host[] = {c->h_pods, c->h_committed, c->h_stage_idx, c->h_stage_rows, c->h_xchg_send,
                   c->h_xchg_recv};
   for (void* p : host)
     if (p) (void)hipHostFree(p);
@@ -2097,8 +2130,7 @@ int stage_batch(gs_ctx* c, const gs_pod* pods, const uint64_t* seq, uint32_t i, 
     HIP_TRY(c, hipEventRecord(sl.ev_go, c->st));
     HIP_TRY(c, hipStreamWaitEvent(c->st_ev, sl.ev_go, 0));
   }
-  HIP_TRY(c, hipMemcpyAsync(c->d_pods, c->h_pods, sizeof(PodVec) * b, hipMemcpyHostToDevice, c->st_ev));
-  HIP_TRY(c, hipMemcpyAsync(c->d_seq, c->h_seq, 8 * b, hipMemcpyHostToDevice, c->st_ev));
+  HIP_TRY(c, hipMemcpyAsync(c->d_pods, c->h_pods, sizeof(PodVec) * c->B + 8 * b, hipMemcpyHostToDevice, c->st_ev));
   return GS_OK;
 }
 

@@ -97,8 +97,9 @@ struct ExtOut {
                                 // permutation bound (the host fails loudly)
 };
 
+// (also resets the select accumulators in `scratch`, launch_ext_select's scratch of n1 - n0 nodes)
 hipError_t launch_ext_nodes(const DevNode* dev, const int16_t* S, uint32_t n0, uint32_t n1, const ExtPod* pod,
-                            int32_t* tot, int16_t* ds, int16_t* rs, hipStream_t st);
+                            int32_t* tot, int16_t* ds, int16_t* rs, int32_t* scratch, hipStream_t st);
 hipError_t launch_ext_matched(const MirrorView& m, const PodVec* pods, const Profile& pf, int prod_cols,
                               const DevNode* dev, const ExtPod* pod, const ExtRec* recs, const ExtRes* res, int nrec, int32_t* tot,
                               int16_t* rs, int32_t* nominated, int32_t* scratch, uint32_t len, hipStream_t st);
@@ -109,10 +110,12 @@ hipError_t launch_ext_matched(const MirrorView& m, const PodVec* pods, const Pro
 hipError_t launch_ext_numa(const MirrorView& m, const PodVec* pods, const Profile& pf, int prod_cols, const DevNode* dev,
                            const ExtPod* pod, const uint32_t* idx, uint32_t nidx, uint32_t n0, int32_t* tot, int16_t* ds,
                            uint8_t* aff, int32_t* scratch, uint32_t len, hipStream_t st);
-// NodeNUMAResource Reserve of the selected node along its Filter-time affinity (aff) -> ExtOut.nflags / zkeys / zcpu /
-// zmem / aff
-hipError_t launch_ext_reserve_numa(const MirrorView& m, const PodVec* pods, const Profile& pf, int prod_cols,
-                                   const uint8_t* aff, uint32_t n0, ExtOut* out, hipStream_t st);
+// The pod's end: with numa, the NodeNUMAResource Reserve of the selected node along its Filter-time affinity (aff) ->
+// ExtOut.nflags / zkeys / zcpu / zmem / aff; then ExtOut and the nrec nominations written to host_out / host_nom
+// (pinned host memory the host reads after the stream synchronizes: no copy).
+hipError_t launch_ext_finish(const MirrorView& m, const PodVec* pods, const Profile& pf, int prod_cols,
+                             const uint8_t* aff, uint32_t n0, int numa, const ExtOut* out, const int32_t* nom, int nrec,
+                             ExtOut* host_out, int32_t* host_nom, hipStream_t st);
 size_t ext_select_scratch_words(uint32_t len);   // int32 words of launch_ext_select's scratch
 // dev[idx[j]] = img[j], j < n (staged Device image updates)
 hipError_t launch_scatter_devnodes(DevNode* dev, const uint32_t* idx, const DevNode* img, uint32_t n, hipStream_t st);

@@ -106,9 +106,12 @@ __device__ __forceinline__ void eval_device(const DevNode& d, const ExtPod& p, b
   *raw = ws ? (int32_t)(ns / ws) : 0;
 }
 
+constexpr int ACC_WORDS_N = 8;   // (ACC_* below)
 __global__ __launch_bounds__(256) void ext_nodes_kernel(const DevNode* __restrict__ dev, const int16_t* __restrict__ S,
                                                          uint32_t n0, uint32_t n1, const ExtPod* __restrict__ pp,
-                                                         int32_t* tot, int16_t* ds, int16_t* rs) {
+                                                         int32_t* tot, int16_t* ds, int16_t* rs, int32_t* acc) {
+  // the select accumulators start from zero (ACC_PREF: -1, no preferred node unless ext_matched_kernel finds one)
+  if (blockIdx.x == 0 && threadIdx.x < ACC_WORDS_N) acc[threadIdx.x] = threadIdx.x == 6 ? -1 : 0;
   const uint32_t i = n0 + blockIdx.x * 256 + threadIdx.x;
   if (i >= n1) return;
   const ExtPod& p = *pp;
@@ -210,6 +213,7 @@ __device__ int64_t score_reservation(const ExtPod& p, const ExtRes& r) {
 constexpr int SEL_BLOCK = 256;
 enum { ACC_DS = 0, ACC_RS = 1, ACC_FEAS = 2, ACC_MAX = 3, ACC_DONE = 4, ACC_TIES = 5, ACC_PREF = 6, ACC_ERR = 7,
        ACC_WORDS = 8 };
+static_assert(ACC_WORDS == ACC_WORDS_N && ACC_PREF == 6, "accumulator layout (ext_nodes_kernel resets it)");
 
 // GPU pods on NUMA-policy nodes: the pair again with DeviceShare as the second hint provider (the eval pass merged
 // NodeNUMAResource's hints alone), then Fit's GPU scalars and DeviceShare Filter / raw Score within the affinity
@@ -245,21 +249,29 @@ __global__ __launch_bounds__(256) void ext_numa_kernel(MirrorView m, const PodVe
   if (bad || over) atomicOr(&acc[ACC_ERR], (bad ? 1 : 0) | (over ? 2 : 0));
 }
 
-// NodeNUMAResource Reserve (plugin.go:375-422) of the selected node: Allocate along its Filter-time affinity
-__global__ __launch_bounds__(64) void ext_reserve_numa_kernel(MirrorView m, const PodVec* __restrict__ pods, Profile pf,
-                                                              int prod_cols, const uint8_t* __restrict__ aff, uint32_t n0,
-                                                              ExtOut* out) {
-  if (threadIdx.x != 0) return;
-  const int32_t node = out->node;
-  if (node < 0) return;
-  Row r;
-  load_row(m, (uint32_t)node, prod_cols != 0, true, r);
-  for (int s = 3; s < 7; ++s) r.free[s] = m.c64(C_FREE_CPU + s)[node];
-  const NumaOut no = numa_eval<true>(r.nr, pods[0], pf, SlotsLds{r, m}, true, false, aff[node - n0]);
-  out->nflags = no.flags | (no.reason ? PL_RESERVE_FAILED : 0u);
-  out->zkeys = no.zkeys;
-  for (int z = 0; z < 4; ++z) { out->zcpu[z] = no.zcpu[z]; out->zmem[z] = no.zmem[z]; }
-  out->aff = no.aff;
+// The pod's end. NodeNUMAResource Reserve (plugin.go:375-422) of the selected node: Allocate along its Filter-time
+// affinity; then the result and the nominations into pinned host memory.
+__global__ __launch_bounds__(64) void ext_finish_kernel(MirrorView m, const PodVec* __restrict__ pods, Profile pf,
+                                                        int prod_cols, const uint8_t* __restrict__ aff, uint32_t n0,
+                                                        int numa, const ExtOut* __restrict__ dout,
+                                                        const int32_t* __restrict__ nom, int nrec, ExtOut* hout,
+                                                        int32_t* hnom) {
+  for (int k = threadIdx.x; k < nrec; k += 64) hnom[k] = nom[k];
+  if (threadIdx.x == 0) {
+    ExtOut o = *dout;
+    if (numa && o.node >= 0) {
+      Row r;
+      load_row(m, (uint32_t)o.node, prod_cols != 0, true, r);
+      for (int s = 3; s < 7; ++s) r.free[s] = m.c64(C_FREE_CPU + s)[o.node];
+      const NumaOut no = numa_eval<true>(r.nr, pods[0], pf, SlotsLds{r, m}, true, false, aff[o.node - n0]);
+      o.nflags = no.flags | (no.reason ? PL_RESERVE_FAILED : 0u);
+      o.zkeys = no.zkeys;
+      for (int z = 0; z < 4; ++z) { o.zcpu[z] = no.zcpu[z]; o.zmem[z] = no.zmem[z]; }
+      o.aff = no.aff;
+    }
+    *hout = o;
+  }
+  __threadfence_system();
 }
 
 // one matched node (record k): the restored row re-evaluated, Reservation Filter, NominateReservation, raw Score
@@ -525,20 +537,18 @@ hipError_t launch_scatter_devnodes(DevNode* dev, const uint32_t* idx, const DevN
 }
 
 hipError_t launch_ext_nodes(const DevNode* dev, const int16_t* S, uint32_t n0, uint32_t n1, const ExtPod* pod,
-                            int32_t* tot, int16_t* ds, int16_t* rs, hipStream_t st) {
+                            int32_t* tot, int16_t* ds, int16_t* rs, int32_t* scratch, hipStream_t st) {
   const uint32_t len = n1 - n0;
-  if (!len) return hipSuccess;
-  hipLaunchKernelGGL(ext_nodes_kernel, dim3((len + 255) / 256), dim3(256), 0, st, dev, S, n0, n1, pod, tot, ds, rs);
+  hipLaunchKernelGGL(ext_nodes_kernel, dim3(len ? (len + 255) / 256 : 1), dim3(256), 0, st, dev, S, n0, n1, pod, tot,
+                     ds, rs, scratch + len);
   return hipGetLastError();
 }
 
 hipError_t launch_ext_matched(const MirrorView& m, const PodVec* pods, const Profile& pf, int prod_cols,
                               const DevNode* dev, const ExtPod* pod, const ExtRec* recs, const ExtRes* res, int nrec, int32_t* tot,
                               int16_t* rs, int32_t* nominated, int32_t* scratch, uint32_t len, hipStream_t st) {
-  // scratch: T[len] | acc[ACC_WORDS] | bcnt[blocks]; the accumulators are reset here, before the select passes
+  // scratch: T[len] | acc[ACC_WORDS] | bcnt[blocks]; the accumulators were reset by ext_nodes_kernel
   int32_t* acc = scratch + len;
-  hipError_t e = hipMemsetAsync(acc, 0, sizeof(int32_t) * ACC_WORDS, st);   // acc[ACC_MAX] holds max + 1
-  if (e != hipSuccess) return e;
   hipLaunchKernelGGL(ext_matched_kernel, dim3(1), dim3(SEL_BLOCK), 0, st, m, pods, pf, prod_cols, dev, pod, recs, res, nrec,
                      tot, rs, nominated, acc);
   return hipGetLastError();
@@ -568,9 +578,11 @@ hipError_t launch_ext_numa(const MirrorView& m, const PodVec* pods, const Profil
   return hipGetLastError();
 }
 
-hipError_t launch_ext_reserve_numa(const MirrorView& m, const PodVec* pods, const Profile& pf, int prod_cols,
-                                   const uint8_t* aff, uint32_t n0, ExtOut* out, hipStream_t st) {
-  hipLaunchKernelGGL(ext_reserve_numa_kernel, dim3(1), dim3(64), 0, st, m, pods, pf, prod_cols, aff, n0, out);
+hipError_t launch_ext_finish(const MirrorView& m, const PodVec* pods, const Profile& pf, int prod_cols,
+                             const uint8_t* aff, uint32_t n0, int numa, const ExtOut* out, const int32_t* nom, int nrec,
+                             ExtOut* host_out, int32_t* host_nom, hipStream_t st) {
+  hipLaunchKernelGGL(ext_finish_kernel, dim3(1), dim3(64), 0, st, m, pods, pf, prod_cols, aff, n0, numa, out, nom, nrec,
+                     host_out, host_nom);
   return hipGetLastError();
 }
 

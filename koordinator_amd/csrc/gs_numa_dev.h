@@ -112,12 +112,12 @@ __device__ __forceinline__ int32_t sdiv(int32_t a, int32_t b) {
 constexpr uint64_t kOrd4 = 0xFEDB7CA69538421ull;   // position mi -> zone-slot mask, 4 bits per position
 __host__ __device__ constexpr uint32_t ord_mask(int mi) { return (uint32_t)(kOrd4 >> (4 * mi)) & 15u; }
 // positions present for nz zones (masks < 2^nz): nz = 1..4
-__device__ __forceinline__ uint32_t ord_valid(int nz) {
+__host__ __device__ __forceinline__ uint32_t ord_valid(int nz) {
   return nz >= 4 ? 0x7FFFu : nz == 3 ? 0x4B7u : nz == 2 ? 0x13u : nz == 1 ? 0x1u : 0u;
 }
 // mask size of the first position of a non-empty position set (positions are sorted by mask size)
-__device__ __forceinline__ int ord_size_first(uint32_t pos) {
-  const int mi = __ffs(pos) - 1;
+__host__ __device__ __forceinline__ int ord_size_first(uint32_t pos) {
+  const int mi = __builtin_ctz(pos);
   return mi < 4 ? 1 : mi < 10 ? 2 : mi < 14 ? 3 : 4;
 }
 __device__ __forceinline__ bool narrower(uint32_t a, uint32_t b) {   // bitmask.IsNarrowerThan
@@ -391,7 +391,7 @@ constexpr int kGenMergeMax = 1 << 16;   // search steps one pass may take (the c
 // HintList::scored lists carry score_at(position) (NodeNUMAResource's hint scores; DeviceShare's are 0).
 // *over: a pass took more than kGenMergeMax steps (the result is then not used).
 template <class ScoreAt>
-__device__ __noinline__ bool merge_hint_lists_gen(const HintList* L, int nl, int nz, int policy, ScoreAt&& score_at,
+__host__ __device__ __noinline__ bool merge_hint_lists_gen(const HintList* L, int nl, int nz, int policy, ScoreAt&& score_at,
                                                   bool& aff_has, uint32_t& aff, bool& over) {
   const bool single = policy == GS_NUMA_POLICY_SINGLE_NUMA_NODE;
   const uint32_t full_mask = (1u << nz) - 1u;
@@ -517,7 +517,7 @@ __device__ __noinline__ bool merge_hint_lists_gen(const HintList* L, int nl, int
 // filterProvidersHints' lists of both providers: NodeNUMAResource's (cpu, then memory: the sorted names; kinds as
 // merge_hint_lists reads them) from its position bitmaps, then DeviceShare's r identical lists (gh, GH_* above).
 // Returns the number of lists (<= 5).
-__device__ __forceinline__ int gen_lists(uint32_t totc, uint32_t lc, uint32_t totm, uint32_t lm, uint32_t valid,
+__host__ __device__ __forceinline__ int gen_lists(uint32_t totc, uint32_t lc, uint32_t totm, uint32_t lm, uint32_t valid,
                                          bool nil_hints, bool has_cpu, bool has_mem, bool tot_c_any, bool tot_m_any,
                                          uint32_t gh, HintList* L) {
   int nl = 0;

@@ -1,0 +1,17 @@
+#!/bin/bash
+# Extension-path session: merge diagnostic, the extension GPU tests, the C5 bench at 100k nodes + its kernel trace.
+# A failing check (rc 1) does not stop the call; a timeout / fault / abort does.
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+step() {   # name, limit, command...
+  local name=$1 lim=$2; shift 2
+  timeout -k 10 "$lim" "$@" > "gpurun_out/$name.log" 2>&1
+  local rc=$?
+  echo "$name rc=$rc"; tail -${TAIL:-6} "gpurun_out/$name.log"
+  [ $rc -le 1 ] || exit $rc
+}
+[ -x koordinator_amd/build/diag_merge ] && TAIL=20 step diag_merge 60 ./koordinator_amd/build/diag_merge
+step ext_tests 500 python -u -m pytest tests/test_gpu_ext.py tests/test_gpu_c5.py tests/test_numa_merge_device.py -m gpu -v \
+    --timeout 200 --timeout-method thread
+grep -E "FAILED" gpurun_out/ext_tests.log | head
+C5_ARGS="--nodes 100000 --steps 3 --warmup 1" bash scripts/gpu_c5.sh
