@@ -193,7 +193,6 @@ struct gs_ctx {
   MirrorView slab_mv{nullptr, nullptr, 0};   // the eval pass's dense copy of the NUMA-policy rows (gather_numa_kernel)
   uint32_t slab_cap = 0;
   bool numa_idx_stale = true;
-  int64_t prep_now = INT64_MIN;             // `now` of the last full node_prep pass
   // registered topologies in bit-plane form (the commit kernel's cpuset Reserve), and the host re-check of
   // every device-chosen cpuset (GS_VERIFY_CPUSET=1)
   TopoDev* d_topos = nullptr;
@@ -661,19 +660,13 @@ int flush_rows(gs_ctx* c) {
                               c->st));
     const uint32_t* d_idx = reinterpret_cast<const uint32_t*>(c->d_stage_rows + (size_t)n * ROW_WORDS);
     HIP_TRY(c, launch_scatter_rows(c->mv, d_idx, c->d_stage_rows, n, c->st));
-    // the rows' LoadAware verdicts at `now` (node_prep), unless a full pass is due anyway
-    if (!c->prep_stale && c->prep_now == c->now) {
-      const gs_loadaware_args& la = c->cfg.loadaware;
-      HIP_TRY(c, launch_node_prep_idx(c->mv, d_idx, n, c->now, la.filter_expired_node_metrics, la.has_node_metric_expiration,
-                                      la.has_node_metric_expiration ? la.node_metric_expiration_seconds * 1000000000LL : 0,
-                                      c->st));
-    }
+
     c->stats.delta_rows += n;
     c->stats.delta_bytes += (uint64_t)n * (4 + ROW_WORDS * 8);
     done += n;
   }
   c->dirty_list.clear();
-  if (c->prep_now != c->now) c->prep_stale = true;
+  c->prep_stale = true;
   return GS_OK;
 }
 
@@ -683,7 +676,6 @@ int node_prep(gs_ctx* c) {
   HIP_TRY(c, launch_node_prep(c->mv, 0, c->N, c->now, a.filter_expired_node_metrics, a.has_node_metric_expiration,
                               exp_ns, c->st));
   c->prep_stale = false;
-  c->prep_now = c->now;
   return GS_OK;
 }
 
@@ -1033,7 +1025,8 @@ int launch_batch(gs_ctx* c, int b, const int32_t* prev, const PlacementDev* prev
   // waits on each one) keep it in order on st: the extra queue hop costs more than it hides there.
   hipStream_t rb = b >= 32 ? c->st_rb : c->st;
   if (rb != c->st) HIP_TRY(c, hipStreamWaitEvent(rb, c->ev[4], 0));
-  HIP_TRY(c, hipMemcpyAsync(c->h_committed, c->d_committed, 16 + sizeof(PlacementDev) * b, hipMemcpyDeviceToHost, rb));
+  HIP_TRY(c, hipMemcpyAsync(c->h_committed, c->d_committed, 16, hipMemcpyDeviceToHost, rb));
+  HIP_TRY(c, hipMemcpyAsync(c->h_out, c->d_out, sizeof(PlacementDev) * b, hipMemcpyDeviceToHost, rb));
   HIP_TRY(c, hipEventRecord(c->ev[5], rb));
   return GS_OK;
 }
@@ -1739,17 +1732,15 @@ int gs_create(const gs_config* cfg, gs_ctx** out) {
   c->mv.i32 = c->d_i32;
   c->mv.npad = (uint32_t)np;
   c->ld = c->npad;
-  // pods | seq and committed | out share one allocation each: one copy per batch each way
-  static_assert(sizeof(PodVec) % 8 == 0 && sizeof(PlacementDev) % 8 == 0, "staging layout");
-  if ((e = hipMalloc(&c->d_pods, (sizeof(PodVec) + 8) * c->B)) != hipSuccess) return bail("hipMalloc", e);
-  c->d_seq = reinterpret_cast<uint64_t*>(c->d_pods + c->B);
+  if ((e = hipMalloc(&c->d_pods, sizeof(PodVec) * c->B)) != hipSuccess) return bail("hipMalloc", e);
+  if ((e = hipMalloc(&c->d_seq, 8 * c->B)) != hipSuccess) return bail("hipMalloc", e);
   if ((e = hipMalloc(&c->d_S, (size_t)c->B * c->ld * 2)) != hipSuccess) return bail("hipMalloc S", e);
   if ((e = hipMalloc(&c->d_aff, (size_t)c->B * c->ld)) != hipSuccess) return bail("hipMalloc aff", e);
   size_t xb = xchg_block_bytes(c->B, LCAP);
   if ((e = hipMalloc(&c->d_xchg_send, xb)) != hipSuccess) return bail("hipMalloc", e);
   c->xchg_bytes = xb;
-  if ((e = hipMalloc(&c->d_committed, 16 + sizeof(PlacementDev) * c->B)) != hipSuccess) return bail("hipMalloc", e);
-  c->d_out = reinterpret_cast<PlacementDev*>(c->d_committed + 4);
+  if ((e = hipMalloc(&c->d_out, sizeof(PlacementDev) * c->B)) != hipSuccess) return bail("hipMalloc", e);
+  if ((e = hipMalloc(&c->d_committed, 16)) != hipSuccess) return bail("hipMalloc", e);
   if ((e = hipMalloc(&c->d_tb, sizeof(int32_t) * TB_N * c->B)) != hipSuccess) return bail("hipMalloc", e);
   if ((e = hipMalloc(&c->d_rowstat, sizeof(RowStat) * (1 + MAX_RANKS))) != hipSuccess) return bail("hipMalloc", e);
   if ((e = hipMalloc(&c->d_sel, 4 * (1 + MAX_RANKS))) != hipSuccess) return bail("hipMalloc", e);
@@ -1758,12 +1749,10 @@ int gs_create(const gs_config* cfg, gs_ctx** out) {
   if ((e = hipMalloc(&c->d_stage_rows, (size_t)(8 * ROW_WORDS + 4) * c->stage_cap)) != hipSuccess) return bail("hipMalloc", e);
   if ((e = hipHostMalloc(&c->h_stage_rows, (size_t)(8 * ROW_WORDS + 4) * c->stage_cap, hipHostMallocDefault)) != hipSuccess)
     return bail("hipHostMalloc", e);
-  if ((e = hipHostMalloc(&c->h_pods, (sizeof(PodVec) + 8) * c->B, hipHostMallocDefault)) != hipSuccess)
-    return bail("hipHostMalloc", e);
-  c->h_seq = reinterpret_cast<uint64_t*>(c->h_pods + c->B);
-  if ((e = hipHostMalloc(&c->h_committed, 16 + sizeof(PlacementDev) * c->B, hipHostMallocDefault)) != hipSuccess)
-    return bail("hipHostMalloc", e);
-  c->h_out = reinterpret_cast<PlacementDev*>(c->h_committed + 4);
+  if ((e = hipHostMalloc(&c->h_pods, sizeof(PodVec) * c->B, hipHostMallocDefault)) != hipSuccess) return bail("hipHostMalloc", e);
+  if ((e = hipHostMalloc(&c->h_seq, 8 * c->B, hipHostMallocDefault)) != hipSuccess) return bail("hipHostMalloc", e);
+  if ((e = hipHostMalloc(&c->h_out, sizeof(PlacementDev) * c->B, hipHostMallocDefault)) != hipSuccess) return bail("hipHostMalloc", e);
+  if ((e = hipHostMalloc(&c->h_committed, 16, hipHostMallocDefault)) != hipSuccess) return bail("hipHostMalloc", e);
   if ((e = hipHostMalloc(&c->h_xchg_send, xb, hipHostMallocDefault)) != hipSuccess) return bail("hipHostMalloc", e);
   (void)hipMemset(c->d_S, 0xff, (size_t)c->B * c->ld * 2);
   {
@@ -1780,16 +1769,14 @@ int gs_create(const gs_config* cfg, gs_ctx** out) {
     if ((e = hipMalloc(&s1.d_S, (size_t)c->B * c->ld * 2)) != hipSuccess) return bail("hipMalloc S", e);
     if ((e = hipMalloc(&s1.d_aff, (size_t)c->B * c->ld)) != hipSuccess) return bail("hipMalloc aff", e);
     (void)hipMemset(s1.d_S, 0xff, (size_t)c->B * c->ld * 2);
-    if ((e = hipMalloc(&s1.d_pods, (sizeof(PodVec) + 8) * c->B)) != hipSuccess) return bail("hipMalloc", e);
-    s1.d_seq = reinterpret_cast<uint64_t*>(s1.d_pods + c->B);
-    if ((e = hipMalloc(&s1.d_committed, 16 + sizeof(PlacementDev) * c->B)) != hipSuccess) return bail("hipMalloc", e);
-    s1.d_out = reinterpret_cast<PlacementDev*>(s1.d_committed + 4);
-    if ((e = hipHostMalloc(&s1.h_pods, (sizeof(PodVec) + 8) * c->B, hipHostMallocDefault)) != hipSuccess)
-      return bail("hipHostMalloc", e);
-    s1.h_seq = reinterpret_cast<uint64_t*>(s1.h_pods + c->B);
-    if ((e = hipHostMalloc(&s1.h_committed, 16 + sizeof(PlacementDev) * c->B, hipHostMallocDefault)) != hipSuccess)
-      return bail("hipHostMalloc", e);
-    s1.h_out = reinterpret_cast<PlacementDev*>(s1.h_committed + 4);
+    if ((e = hipMalloc(&s1.d_pods, sizeof(PodVec) * c->B)) != hipSuccess) return bail("hipMalloc", e);
+    if ((e = hipMalloc(&s1.d_seq, 8 * c->B)) != hipSuccess) return bail("hipMalloc", e);
+    if ((e = hipMalloc(&s1.d_out, sizeof(PlacementDev) * c->B)) != hipSuccess) return bail("hipMalloc", e);
+    if ((e = hipMalloc(&s1.d_committed, 16)) != hipSuccess) return bail("hipMalloc", e);
+    if ((e = hipHostMalloc(&s1.h_pods, sizeof(PodVec) * c->B, hipHostMallocDefault)) != hipSuccess) return bail("hipHostMalloc", e);
+    if ((e = hipHostMalloc(&s1.h_seq, 8 * c->B, hipHostMallocDefault)) != hipSuccess) return bail("hipHostMalloc", e);
+    if ((e = hipHostMalloc(&s1.h_out, sizeof(PlacementDev) * c->B, hipHostMallocDefault)) != hipSuccess) return bail("hipHostMalloc", e);
+    if ((e = hipHostMalloc(&s1.h_committed, 16, hipHostMallocDefault)) != hipSuccess) return bail("hipHostMalloc", e);
     for (auto& ev : s1.ev)
       if ((e = hipEventCreate(&ev)) != hipSuccess) return bail("hipEventCreate", e);
   }
@@ -1892,21 +1879,21 @@ int gs_destroy(gs_ctx* c) {
       if (sl.ev_go) (void)hipEventDestroy(sl.ev_go);
       if (sl.ev_evdone) (void)hipEventDestroy(sl.ev_evdone);
     }
-    void* d1[] = {s1.d_pods, s1.d_committed, s1.d_S, s1.d_aff};   // (seq / out live inside pods / committed)
+    void* d1[] = {s1.d_pods, s1.d_seq, s1.d_out, s1.d_committed, s1.d_S, s1.d_aff};
     for (void* p : d1)
       if (p) (void)hipFree(p);
-    void* h1[] = {s1.h_pods, s1.h_committed};
+    void* h1[] = {s1.h_pods, s1.h_seq, s1.h_out, s1.h_committed};
     for (void* p : h1)
       if (p) (void)hipHostFree(p);
     for (auto& ev : s1.ev)
       if (ev) (void)hipEventDestroy(ev);
   }
-  void* dev[] = {c->d_i64, c->d_i32, c->d_pods, c->d_S, c->d_xchg_send, c->d_xchg_recv, c->d_xmerged,
+  void* dev[] = {c->d_i64, c->d_i32, c->d_pods, c->d_seq, c->d_S, c->d_xchg_send, c->d_xchg_recv, c->d_xmerged, c->d_out,
                  c->d_committed, c->d_rowstat, c->d_sel, c->d_stage_idx, c->d_stage_rows, c->d_numa_idx,
                  c->d_topos, c->d_aff, c->d_tb};
   for (void* p : dev)
     if (p) (void)hipFree(p);
-  void* host[] = {c->h_pods, c->h_committed, c->h_stage_idx, c->h_stage_rows, c->h_xchg_send,
+  void* host[] = {c->h_pods, c->h_seq, c->h_out, c->h_committed, c->h_stage_idx, c->h_stage_rows, c->h_xchg_send,
                   c->h_xchg_recv};
   for (void* p : host)
     if (p) (void)hipHostFree(p);
@@ -2130,7 +2117,8 @@ int stage_batch(gs_ctx* c, const gs_pod* pods, const uint64_t* seq, uint32_t i, 
     HIP_TRY(c, hipEventRecord(sl.ev_go, c->st));
     HIP_TRY(c, hipStreamWaitEvent(c->st_ev, sl.ev_go, 0));
   }
-  HIP_TRY(c, hipMemcpyAsync(c->d_pods, c->h_pods, sizeof(PodVec) * c->B + 8 * b, hipMemcpyHostToDevice, c->st_ev));
+  HIP_TRY(c, hipMemcpyAsync(c->d_pods, c->h_pods, sizeof(PodVec) * b, hipMemcpyHostToDevice, c->st_ev));
+  HIP_TRY(c, hipMemcpyAsync(c->d_seq, c->h_seq, 8 * b, hipMemcpyHostToDevice, c->st_ev));
   return GS_OK;
 }
 

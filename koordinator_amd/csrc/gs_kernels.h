@@ -118,9 +118,6 @@ constexpr int TB_N = 32;
 hipError_t set_kernel_attributes();
 hipError_t launch_node_prep(const MirrorView& m, uint32_t n0, uint32_t n1, int64_t now, int32_t filter_expired,
                             int32_t has_exp, int64_t exp_ns, hipStream_t st);
-// the same for the rows idx[0..n) (after a delta update rewrote them)
-hipError_t launch_node_prep_idx(const MirrorView& m, const uint32_t* idx, uint32_t n, int64_t now, int32_t filter_expired,
-                                int32_t has_exp, int64_t exp_ns, hipStream_t st);
 // NodeNUMAResource profiles: numa_idx lists the shard's nodes with a NUMA topology policy (ascending)
 hipError_t launch_eval(const MirrorView& m, const PodVec* pods, int npods, const Profile& pf, uint32_t n0, uint32_t n1,
                        int16_t* S, uint32_t ld, int prod_cols, const uint32_t* numa_idx, uint32_t numa_n,

@@ -28,13 +28,10 @@ namespace gs {
 
 // ------------------------------------------------------------------------------------------------
 // node-prep: LoadAware expiry (helper.go:36-41) evaluated at `now` for every node.
-// idx != nullptr: the n0..n1 entries of idx (rows a delta update just rewrote) instead of a node range
 __global__ void __launch_bounds__(256) node_prep_kernel(MirrorView m, uint32_t n0, uint32_t n1, int64_t now,
-                                                        int32_t filter_expired, int32_t has_exp, int64_t exp_ns,
-                                                        const uint32_t* __restrict__ idx) {
+                                                        int32_t filter_expired, int32_t has_exp, int64_t exp_ns) {
   uint32_t i = n0 + blockIdx.x * 256 + threadIdx.x;
   if (i >= n1) return;
-  if (idx) i = idx[i];
   uint32_t sf = (uint32_t)m.c32(C_SFLAGS)[i];
   bool exists = sf & SF_METRIC;
   bool expired = !exists || !(sf & SF_UPDATE_TIME) || (exp_ns > 0 && now - m.c64(C_UPDATE_TIME)[i] >= exp_ns);
@@ -1389,16 +1386,7 @@ hipError_t launch_node_prep(const MirrorView& m, uint32_t n0, uint32_t n1, int64
                             int32_t has_exp, int64_t exp_ns, hipStream_t st) {
   if (n1 <= n0) return hipSuccess;
   uint32_t grid = (n1 - n0 + 255) / 256;
-  hipLaunchKernelGGL(node_prep_kernel, dim3(grid), dim3(256), 0, st, m, n0, n1, now, filter_expired, has_exp, exp_ns,
-                     nullptr);
-  return hipGetLastError();
-}
-
-hipError_t launch_node_prep_idx(const MirrorView& m, const uint32_t* idx, uint32_t n, int64_t now, int32_t filter_expired,
-                                int32_t has_exp, int64_t exp_ns, hipStream_t st) {
-  if (!n) return hipSuccess;
-  hipLaunchKernelGGL(node_prep_kernel, dim3((n + 255) / 256), dim3(256), 0, st, m, 0u, n, now, filter_expired, has_exp,
-                     exp_ns, idx);
+  hipLaunchKernelGGL(node_prep_kernel, dim3(grid), dim3(256), 0, st, m, n0, n1, now, filter_expired, has_exp, exp_ns);
   return hipGetLastError();
 }
 

@@ -8,7 +8,8 @@ rc=$?; echo "C5 rc=$rc"; cat gpurun_out/c5.json; tail -3 gpurun_out/c5.err
 [ $rc -eq 0 ] || exit $rc
 if [ "${SKIP_PROF:-0}" != 1 ]; then
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$PWD/gpurun_out/prof_c5" -o c5 -- \
-      python -u bench.py --profile c5 --steps 2 --warmup 1 --no-cpu-baseline > gpurun_out/prof_c5.log 2>&1
+      python -u bench.py --profile c5 --steps 2 --warmup 1 --no-cpu-baseline ${C5_PROF_ARGS:---nodes 100000} \
+      > gpurun_out/prof_c5.log 2>&1
   rc=$?; echo "PROF_C5 rc=$rc"; tail -3 gpurun_out/prof_c5.log
   find gpurun_out/prof_c5 -name "*stats*" | head
 fi

@@ -10,8 +10,7 @@ step() {   # name, limit, command...
   echo "$name rc=$rc"; tail -${TAIL:-6} "gpurun_out/$name.log"
   [ $rc -le 1 ] || exit $rc
 }
-[ -x koordinator_amd/build/diag_merge ] && TAIL=20 step diag_merge 60 ./koordinator_amd/build/diag_merge
-step ext_tests 500 python -u -m pytest tests/test_gpu_ext.py tests/test_gpu_c5.py tests/test_numa_merge_device.py -m gpu -v \
-    --timeout 200 --timeout-method thread
-grep -E "FAILED" gpurun_out/ext_tests.log | head
+[ -x tools_bin/diag_merge ] && TAIL=20 step diag_merge 60 ./tools_bin/diag_merge
+step gpu_tests 700 python -u -m pytest ${TESTS:-tests} -m gpu -v --timeout 200 --timeout-method thread
+grep -E "FAILED" gpurun_out/gpu_tests.log | head -20
 C5_ARGS="--nodes 100000 --steps 3 --warmup 1" bash scripts/gpu_c5.sh

@@ -35,6 +35,9 @@ def _cfg(c, numa: bool):
 
 
 def _worker(rank: int, world: int, port: int, numa: bool, pods: int, q):
+    import faulthandler
+    import sys
+    faulthandler.dump_traceback_later(100, exit=True, file=sys.stderr)   # a stuck rank names where it is
     try:
         import torch
         import torch.distributed as dist
