@@ -11,6 +11,7 @@
 #include <cstring>
 #include <deque>
 #include <map>
+#include <optional>
 #include <memory>
 #include <set>
 #include <unordered_map>
@@ -57,6 +58,7 @@ struct gs_gang_mgr {
   std::map<uint64_t, std::pair<uint64_t, int64_t>> fw_waiting;   // pod uid -> (gang id, Permit deadline)
 
   Gang* get(uint64_t id, bool create) {   // getGangFromCacheByGangId (gang_cache.go:48-63) + NewGang (gang.go:92-110)
+    if (snap_on) snap_touch(id);   // a speculative walk: the gang's state before its first access is kept
     auto it = gangs.find(id);
     if (it != gangs.end()) return &it->second;
     if (!create) return nullptr;
@@ -95,15 +97,29 @@ struct gs_gang_mgr {
   size_t permit_allows(uint64_t gang_id, uint64_t uid) const;
   size_t post_filter_rejects(uint64_t gang_id) const;
   size_t unreserve_rejects(uint64_t gang_id, uint64_t uid) const;
-  // gs_gang_pass: the snapshot a speculative walk is replayed from
-  std::unique_ptr<gs_gang_mgr> snap;
-  gs_gang_mgr() = default;
-  gs_gang_mgr(const gs_gang_mgr& o) : args(o.args), gangs(o.gangs), fw_waiting(o.fw_waiting) {}
-  gs_gang_mgr& operator=(const gs_gang_mgr& o) {
-    args = o.args;
-    gangs = o.gangs;
-    fw_waiting = o.fw_waiting;
-    return *this;
+  // gs_gang_pass: the state a speculative walk is replayed from, copied on first access per gang (every mutation goes
+  // through get()) instead of the whole cache per walk, and the framework's waiting pods (a short map)
+  bool snap_on = false;
+  std::unordered_map<uint64_t, std::optional<Gang>> snap_gangs;   // nullopt: the gang did not exist
+  std::map<uint64_t, std::pair<uint64_t, int64_t>> snap_fw;
+  void snap_touch(uint64_t id) {
+    if (snap_gangs.count(id)) return;
+    auto it = gangs.find(id);
+    snap_gangs.emplace(id, it == gangs.end() ? std::nullopt : std::optional<Gang>(it->second));
+  }
+  void snap_begin() {
+    snap_gangs.clear();
+    snap_fw = fw_waiting;
+    snap_on = true;
+  }
+  void snap_restore() {
+    for (auto& kv : snap_gangs) {
+      if (kv.second) gangs[kv.first] = std::move(*kv.second);
+      else gangs.erase(kv.first);
+    }
+    fw_waiting = std::move(snap_fw);
+    snap_gangs.clear();
+    snap_on = false;
   }
 };
 
@@ -578,7 +594,7 @@ int gs_gang_pass_destroy(gs_gang_pass* p) {
 int gs_gang_walk(gs_gang_pass* p, uint32_t i, uint32_t run_cap, uint32_t* run, uint32_t* run_n, uint32_t* j_out) {
   if (!p || !run || !run_n || !j_out || i > p->n) return GS_EINVAL;
   gs_gang_mgr& m = *p->m;
-  m.snap = std::make_unique<gs_gang_mgr>(m);
+  m.snap_begin();
   uint32_t j = i, nr = 0;
   while (j < p->n && nr < run_cap) {
     gs_gang_mgr::List rej;
@@ -608,9 +624,8 @@ int gs_gang_replay(gs_gang_pass* p, uint32_t i, uint32_t j, const uint32_t* run,
                    const int32_t* got_node, uint32_t* r_stop, uint32_t* j_next, int32_t* single) {
   if (!p || !r_stop || !j_next || !single || j > p->n || i > j || (run_n && (!run || !got_node))) return GS_EINVAL;
   gs_gang_mgr& m = *p->m;
-  if (!m.snap) return GS_ESTATE;
-  static_cast<gs_gang_mgr&>(m) = *m.snap;
-  m.snap.reset();
+  if (!m.snap_on) return GS_ESTATE;
+  m.snap_restore();
   *single = -1;
   uint32_t r = 0, k = i;
   for (; k < j; ++k) {

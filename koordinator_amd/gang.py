@@ -276,16 +276,17 @@ def schedule_with_gangs(engine, mgr: GangManager, pods, gang_ids, seq=None, nomi
         _, nd, rec = waiting.pods[uid]
         return nd, rec
 
-    def forget(nodes: list, recs: list):
-        """ForgetPod of the withdrawn run pods (nodes / recs given) and of the pods the Unreserve chains rejected"""
+    def forget(nodes, recs):
+        """ForgetPod of the withdrawn run pods (node array / pod records given) and of the pods the Unreserve chains
+        rejected"""
         cnt = C.c_uint32(0)
         GangManager._chk(L.gs_gang_pass_forgets(h, abi.ptr(fbuf), len(fbuf), C.byref(cnt)), "gs_gang_pass_forgets")
-        for u in fbuf[:cnt.value]:
-            nd, rec = where(int(u))
-            nodes.append(nd)
-            recs.append(rec)
-        if nodes:
-            engine.forget(np.array(nodes, np.uint32), np.array(recs, abi.POD_DTYPE))
+        if cnt.value:
+            more = [where(int(u)) for u in fbuf[:cnt.value]]
+            nodes = np.concatenate([nodes, np.array([x[0] for x in more], np.uint32)])
+            recs = np.concatenate([recs, np.array([x[1] for x in more], abi.POD_DTYPE)])
+        if len(nodes):
+            engine.forget(np.ascontiguousarray(nodes, np.uint32), np.ascontiguousarray(recs, abi.POD_DTYPE))
 
     try:
         i = 0
@@ -299,14 +300,14 @@ def schedule_with_gangs(engine, mgr: GangManager, pods, gang_ids, seq=None, nomi
                                               C.byref(r_stop), C.byref(j_next), C.byref(single)), "gs_gang_replay")
             kept = r_stop.value
             out[r[:kept]] = got[:kept]
-            later = [q for q in range(kept, len(r)) if got_node[q] >= 0]   # the run's withdrawn placements
-            forget([int(got_node[q]) for q in later], [pods[r[q]] for q in later])
+            later = kept + np.flatnonzero(got_node[kept:] >= 0)   # the run's withdrawn placements
+            forget(got_node[later].astype(np.uint32), pods[r[later]])
             if single.value >= 0:   # the walk's PreFilter failed where the real one passes: this pod alone
                 k = single.value
                 one = engine.schedule(pods[k:k + 1], seq[k:k + 1])
                 out[k] = one[0]
                 GangManager._chk(L.gs_gang_pass_after_single(h, k, int(one["node"][0])), "gs_gang_pass_after_single")
-                forget([], [])
+                forget(np.zeros(0, np.uint32), np.zeros(0, abi.POD_DTYPE))
             i = j_next.value
         cnt = C.c_uint32(0)
         cu = np.zeros(max(1, 2 * (n + len(waiting.pods))), np.uint64)

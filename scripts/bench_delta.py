@@ -67,7 +67,7 @@ def main() -> None:
         m = c.metrics[idx].copy()
         m["node_usage"]["cpu_milli"] = (m["node_usage"]["cpu_milli"] * 0.9).astype(np.int64)
         m["update_time_ns"] = c.now_ns - 5 * 10**9
-        ap_ = c.pods[:n_touch].copy()
+        ap_ = np.resize(c.pods, n_touch).copy()   # (the cluster's pending pods repeated, fresh uids)
         ap_["uid"] = np.arange(uid, uid + n_touch, dtype=np.uint64)
         uid += n_touch
         ts = np.full(n_touch, c.now_ns - 10**9, np.int64)
