@@ -58,8 +58,9 @@ __device__ __forceinline__ int sp_rescore_index(int wv) { return wv == 1 ? 0 : w
 constexpr int SP_JOBQ = 24;      // job ring per Reserve wave (<= 3 jobs per pod, <= SP_LAG / 2 + 2 pods in flight)
 constexpr int SP_HASH = 256;     // node -> slot (full-row resolution)
 constexpr int SP_FRESH = 1, SP_FITERR = 2, SP_SLOW = 4, SP_OFFSHARD = 8;   // DecRec.flags
+constexpr int SP_PRED_GE = 16, SP_PRED_GT = 32;   // diagnostics (ST): a pending row's pre-landing score >= / > M
 constexpr uint32_t SP_SPIN_LIMIT = 1u << 24;
-constexpr int SP_NST = 40, SP_STRIDE = 64;   // diagnostics: stamps per wave, the wave's region in a.stamps
+constexpr int SP_NST = 48, SP_STRIDE = 64;   // diagnostics: stamps per wave, the wave's region in a.stamps
 constexpr int16_t SO_UNKNOWN = -2;    // dso: batch-start score of an off-shard fresh row not evaluated yet
 constexpr int16_t SO_UNLISTED = -3;   // a decision's view of such a row not in the pod's list head
 
@@ -269,6 +270,10 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
       // ------------------------------------------------ a rollback the verifier requested: to pod v
       if (const int rq = ld_acq(&s_rb_req)) {
         const int v = rq - 1;
+        if (ST) {
+          st_acc[43] += (dec[v].flags & SP_PRED_GE) ? 1 : 0;
+          st_acc[45] += (dec[v].flags & SP_PRED_GT) ? 1 : 0;
+        }
         // park the other waves, undo the Reserves of pods >= v (newest first: the two Reserve waves finish pods out of
         // order, so by their flags), restore the slot versions
         st_rel(&s_stop, 1);
@@ -278,6 +283,8 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
           sp_sleep();
         }
         if (err) break;
+        SPM(37);   // rollback: parking the other waves
+        if (ST) st_acc[41] += q - v;
         for (int qq = q - 1; qq >= v; --qq) {
           if (!resv[qq] || (dec[qq].flags & SP_FITERR)) continue;
           const UndoRec& u = undo[qq % SP_LAG];
@@ -307,12 +314,24 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
         nd = ndv;
         for (int i = lane; i < SP_HASH; i += 64) { hkey[i] = -1; hval[i] = -1; }
         WAVE_FENCE();
-        for (int s = 0; s < nd; ++s) {   // (readlane in uniform control flow: the source register is whole)
-          const uint32_t nn = s < 64 ? (uint32_t)__builtin_amdgcn_readlane((int)dn0, s)
-                                     : (uint32_t)__builtin_amdgcn_readlane((int)dn1, s - 64);
-          if (lane == 0) hash_insert(nn, s);
+        // the surviving slots back into the hash, one lane per slot (LDS compare-and-swap claims a probe position; a
+        // key only moves past occupied positions, so linear-probe lookups find it)
+        for (int half = 0; half < 2; ++half) {
+          bool todo = lane + 64 * half < nd;
+          const uint32_t nn = half ? dn1 : dn0;
+          uint32_t h = (nn * 2654435761u) & (SP_HASH - 1);
+          while (todo) {
+            if (atomicCAS(&hkey[h], -1, (int32_t)nn) == -1) {
+              hval[h] = (int16_t)(lane + 64 * half);
+              todo = false;
+            } else {
+              h = (h + 1) & (SP_HASH - 1);
+            }
+          }
+          WAVE_FENCE();
         }
-        WAVE_FENCE();
+        SPM(38);   // rollback: undo log, slot versions, hash rebuild
+        if (ST) st_acc[40] += __popcll(redo0) + __popcll(redo1);
         // re-score the restored rows for pods v.. (their dsc entries after the undone landing are stale)
         for (int pass = 0; pass < 2; ++pass) {
           for (uint64_t bb = pass ? redo1 : redo0; bb; bb &= bb - 1) {
@@ -325,6 +344,7 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
             WAVE_FENCE();
           }
         }
+        SPM(39);   // rollback: re-scoring the restored rows
         const int32_t myv0 = pv0, myv1 = pv1;
         if (lane < nd) done_ver[lane] = myv0;
         if (lane + 64 < nd) done_ver[lane + 64] = myv1;
@@ -714,6 +734,15 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
       d.unk0 = unk0;
       d.unk1 = unk1;
       d.flags = (action == 1 ? SP_FITERR : 0u) | (slowpath ? SP_SLOW : 0u);
+      if (ST && action == 0 && (pend0 | pend1)) {
+        // would a rule "wait when a pending row scored >= M (> M) for p before its landing" have foreseen the rollbacks?
+        int o0 = -1, o1 = -1;
+        if ((pend0 >> lane) & 1ull) o0 = dec[pv0].prev_pend < 0 ? so0 : (int)dsc[p * SB + lane];
+        if ((pend1 >> lane) & 1ull) o1 = dec[pv1].prev_pend < 0 ? so1 : (int)dsc[p * SB + 64 + lane];
+        const int om = wave_max(max(o0, o1));
+        if (om >= M) { d.flags |= SP_PRED_GE; st_acc[42] += 1; }
+        if (om > M) { d.flags |= SP_PRED_GT; st_acc[44] += 1; }
+      }
       d.slot = -1;
       d.prev_pend = -1;
       if (action == 0) {
@@ -725,8 +754,11 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
           if (lane == (nd & 63)) { if (nd < 64) { dn0 = winner; pv0 = p; } else { dn1 = winner; pv1 = p; } }
           const int q0 = p + 1 + lane, q1 = q0 + 64;
           if (winner - a.own0 < a.own1 - a.own0) {
-            ps_v0 = q0 < B ? a.S_own[(size_t)q0 * a.ld + (winner - a.own0)] : (int16_t)0;
-            ps_v1 = q1 < B ? a.S_own[(size_t)q1 * a.ld + (winner - a.own0)] : (int16_t)0;
+            // both loads issued unconditionally (rows clamped into the batch; flush_fresh stores only q < B): no exec-mask
+            // branch between them, so neither waits for the other, nor for the next header's loads in flight
+            const int16_t* col = a.S_own + (winner - a.own0);
+            ps_v0 = col[(size_t)min(q0, B - 1) * a.ld];
+            ps_v1 = col[(size_t)min(q1, B - 1) * a.ld];
             ps_slot = slot;
             ps_p = p;
           } else {   // another shard's row: unknown until the Reserve wave's batch-start job has evaluated it

@@ -1822,7 +1822,8 @@ int gs_destroy(gs_ctx* c) {
         auto W = [&](int w, int i) { return (double)sa[w * 64 + i] / np; };
         fprintf(stderr, "gpuscore spec commit, cycles per committed pod (%llu pods, %llu decisions, %llu rollbacks, %.0f "
                 "rollback cycles, full-row %llu):\n", (unsigned long long)c->stats_all_pods, (unsigned long long)sa[9],
-                (unsigned long long)sa[3], W(0, 4), (unsigned long long)sa[10]);
+                (unsigned long long)sa[3], W(0, 4) + W(0, 37) + W(0, 38) + W(0, 39),
+                (unsigned long long)sa[10]);
         fprintf(stderr, "  wave 0 total %.0f: checks %.0f | dirty state %.0f | hdr+fresh store+dirty loads %.0f | level scan "
                 "%.0f | winner %.0f | fresh slot %.0f | record %.0f | waiting %.0f (at batch end %.0f) | full-row %.0f\n",
                 W(0, 12), W(0, 27), W(0, 28), W(0, 29), W(0, 18), W(0, 19), W(0, 20), W(0, 0), W(0, 2), W(0, 23), W(0, 11));
@@ -1832,6 +1833,13 @@ int gs_destroy(gs_ctx* c) {
                 (unsigned long long)sa[36], 100.0 * sa[36] / np, (unsigned long long)sa[31], 100.0 * sa[31] / np,
                 sa[32] / (ng + sa[36]), sa[33] / ng, sa[34] / ng, sa[35] / np, (unsigned long long)sa[24],
                 (unsigned long long)sa[25]);
+        const double nr = sa[3] ? (double)sa[3] : 1.0;
+        auto R = [&](int i) { return (double)sa[i] / nr; };
+        fprintf(stderr, "  rollback (cycles per rollback): parking %.0f | undo+hash %.0f | restored-row re-scoring %.0f | "
+                "rest %.0f; restored rows %.2f, depth %.2f decisions\n", R(37), R(38), R(39), R(4), R(40), R(41));
+        fprintf(stderr, "  pending row's pre-landing score >= M: %llu decisions, %llu of the rollbacks; > M: %llu decisions, %llu "
+                "of the rollbacks\n", (unsigned long long)sa[42], (unsigned long long)sa[43], (unsigned long long)sa[44],
+                (unsigned long long)sa[45]);
         fprintf(stderr, "  wave 4 (verify): busy %.0f waiting %.0f\n", W(4, 1), W(4, 2));
         for (int w = 2; w < 4; ++w)
           fprintf(stderr, "  wave %d (Reserve): fetch+undo %.0f numa_eval %.0f lane0 %.0f rest %.0f (fresh fetch %.0f, landed-"
