@@ -84,6 +84,11 @@ struct Job {
 };
 
 __device__ __forceinline__ void sp_sleep() { __builtin_amdgcn_s_sleep(2); }
+__device__ __forceinline__ void sp_prio(uint32_t p) {   // s_setprio takes an immediate
+  if (p == 1) __builtin_amdgcn_s_setprio(1);
+  else if (p == 2) __builtin_amdgcn_s_setprio(2);
+  else if (p == 3) __builtin_amdgcn_s_setprio(3);
+}
 
 // The kernel's LDS, at fixed offsets sized for MAX_BATCH pods whatever the batch: every array is at a link-time
 // constant address and [pod][slot] rows have the constant stride SB, so no register holds a carve-up pointer and
@@ -818,6 +823,7 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
     // batch-start score was unknown scored below it at batch start); the rows it excluded that are feasible join its
     // Feasible count. A miss asks wave 0 to roll back to v. Verifying v needs the re-scoring of every pod before it
     // (rescored[]), which also means their Reserves (and batch-start jobs) are complete.
+    sp_prio((a.dbg >> 8) & 3u);
     int v = 0, wm = 0;
     uint32_t spins = 0;
     for (;;) {
@@ -897,6 +903,7 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
   } else if (sp_reserve_index(wv) >= 0) {
     // =================================================== Reserve ===================================================
     const int wr = sp_reserve_index(wv);   // this wave's pods: q % SP_NRES == wr
+    sp_prio((a.dbg >> 4) & 3u);
     uint64_t* s_cpuset_w = s_cpuset[wr];
     int32_t& s_aff_w = s_aff[wr];
     Job* jq = jobq + wr * SP_JOBQ;
@@ -1157,6 +1164,7 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
     // ============================================== re-scoring jobs ==============================================
     uint32_t spins = 0;
     const int ri = sp_rescore_index(wv);
+    sp_prio((a.dbg >> 6) & 3u);
     int ring = ri % SP_NRES;
     for (;;) {
       if (ld_acq(&s_stop)) {

@@ -156,7 +156,12 @@ struct gs_ctx {
     PlacementDev* h_out = nullptr;
     int32_t* h_committed = nullptr;
     hipEvent_t ev[6] = {};
+    uint8_t* d_lst = nullptr;       // overlapped cand (one shard): the slot's lists + headers, and its histograms
+    uint32_t* d_hist = nullptr;
   } slot[2];
+  bool cand_overlap = false;        // GS_CAND_OVERLAP (default on): cand beside the previous commit, fix_levels after it
+  uint8_t* d_lst = nullptr;         // the bound slot's (cand_overlap)
+  uint32_t* d_hist = nullptr;
   int cur_slot = 0;
   // host mirror
   std::vector<HostNode> nodes;
@@ -907,10 +912,19 @@ void bind_slot(gs_ctx* c, int s) {
   c->d_pods = x.d_pods; c->d_seq = x.d_seq; c->d_out = x.d_out; c->d_committed = x.d_committed;
   c->h_pods = x.h_pods; c->h_seq = x.h_seq; c->h_out = x.h_out; c->h_committed = x.h_committed;
   for (int i = 0; i < 6; ++i) c->ev[i] = x.ev[i];
+  c->d_lst = x.d_lst; c->d_hist = x.d_hist;
   c->cur_slot = s;
 }
 
 constexpr int GS_REDO = 1;   // internal: re-run the batch (its score rows were overwritten by a speculative pass)
+
+// The candidate levels of a one-shard pass without node sampling are built on st_ev right after the eval pass (beside
+// the previous batch's commit, on the stale rows it lands on), then fixed up on st once that commit is done
+// (GS_FUSED_PATCH=0, the separate patch kernel: not overlapped)
+bool cand_overlapped(const gs_ctx* c) {
+  static const bool separate = getenv("GS_FUSED_PATCH") && getenv("GS_FUSED_PATCH")[0] == '0';
+  return c->cand_overlap && c->nranks == 1 && !c->window_k && c->d_lst && !separate;
+}
 
 CommitArgs commit_args(gs_ctx* c, int b) {
   CommitArgs a{};
@@ -921,7 +935,8 @@ CommitArgs commit_args(gs_ctx* c, int b) {
   a.nranks = c->nranks;
   a.shard_size = (c->N + c->nranks - 1) / c->nranks;
   // several ranks: the speculative commit reads the merged levels, the pipelined / lockstep kernels every rank block
-  a.xbase = c->nranks == 1 ? c->d_xchg_send : commit_spec_selected(c->window_k) ? c->d_xmerged : c->d_xchg_recv;
+  a.xbase = c->nranks == 1 ? (cand_overlapped(c) ? c->d_lst : c->d_xchg_send)
+                            : commit_spec_selected(c->window_k) ? c->d_xmerged : c->d_xchg_recv;
   a.xblock = c->xchg_bytes;
   a.bmax = c->B;
   a.pf = c->pf;
@@ -941,7 +956,9 @@ CommitArgs commit_args(gs_ctx* c, int b) {
   a.start = c->next_start;
   a.nnodes = c->N;
   static const bool nospec = getenv("GS_SPEC_WAIT") && getenv("GS_SPEC_WAIT")[0] == '1';
-  a.dbg = nospec ? 1u : 0u;
+  // GS_SPEC_PRIO (experiments): issue priorities of the roles, bits 4-5 Reserve, 6-7 re-scoring, 8-9 verify
+  static const uint32_t prio = getenv("GS_SPEC_PRIO") ? (uint32_t)strtoul(getenv("GS_SPEC_PRIO"), nullptr, 0) & 0x3f0u : 0u;
+  a.dbg = (nospec ? 1u : 0u) | prio;
   a.tb = c->d_tb;
   return a;
 }
@@ -952,10 +969,12 @@ CommitArgs commit_args(gs_ctx* c, int b) {
 // before it, and the rows that batch landed on are re-evaluated on st once it committed (patch_kernel); its commit
 // kernel does nothing unless that batch committed every pod and needs no host-side Reserve (prev[1] == 1).
 int launch_batch(gs_ctx* c, int b, const int32_t* prev, const PlacementDev* prev_out = nullptr, int prev_b = 0) {
-  uint32_t* d_lists = reinterpret_cast<uint32_t*>(c->d_xchg_send);
-  LevelHdr* d_hdrs = reinterpret_cast<LevelHdr*>(c->d_xchg_send + lists_bytes(c->B, c->lstride));
-  LevelExt* d_ext =
-      reinterpret_cast<LevelExt*>(c->d_xchg_send + lists_bytes(c->B, c->lstride) + (size_t)c->B * sizeof(LevelHdr));
+  static const bool separate = getenv("GS_FUSED_PATCH") && getenv("GS_FUSED_PATCH")[0] == '0';
+  const bool ovl = cand_overlapped(c);
+  uint8_t* lblk = ovl ? c->d_lst : c->d_xchg_send;
+  uint32_t* d_lists = reinterpret_cast<uint32_t*>(lblk);
+  LevelHdr* d_hdrs = reinterpret_cast<LevelHdr*>(lblk + lists_bytes(c->B, c->lstride));
+  LevelExt* d_ext = reinterpret_cast<LevelExt*>(lblk + lists_bytes(c->B, c->lstride) + (size_t)c->B * sizeof(LevelHdr));
   int prod_cols = 0;
   for (int i = 0; i < b; ++i) prod_cols |= (c->h_pods[i].flags & PF_PROD_SCORE) ? 1 : 0;
   uint32_t len = c->n1 - c->n0;
@@ -992,22 +1011,38 @@ int launch_batch(gs_ctx* c, int b, const int32_t* prev, const PlacementDev* prev
   HIP_TRY(c, launch_eval(c->mv, c->d_pods, b, c->pf, c->n0, c->n1, c->d_S, c->ld, prod_cols, c->d_numa_idx, c->numa_n,
                          c->d_aff, c->st_ev, c->st2, c->ev_fork, c->ev_join, c->slab_mv.i64 ? &c->slab_mv : nullptr));
   HIP_TRY(c, hipEventRecord(c->ev[1], c->st_ev));
+  const bool fix = ovl && prev && prev_b > 0;
+  if (ovl) {
+    // levels on st_ev beside the previous batch's commit: the rows it lands on are stale here (listed with a margin of
+    // prev_b nodes, histogram kept), fixed up on st below once it committed
+    CandPatch cp{};
+    cp.extra = fix ? prev_b : 0;
+    cp.hist = fix ? c->d_hist : nullptr;
+    HIP_TRY(c, launch_cand(c->d_S, c->ld, len, c->n0, b, c->max_score, c->lstride, d_lists, d_hdrs, d_ext, c->st_ev, &cp));
+  }
   HIP_TRY(c, hipEventRecord(sl.ev_evdone, c->st_ev));
   HIP_TRY(c, hipStreamWaitEvent(c->st, sl.ev_evdone, 0));
+  if (fix) {
+    CandPatch cp{c->mv, c->d_pods, c->pf, c->n0, c->n1, prod_cols, 0, c->d_aff, prev_out, prev};
+    cp.extra = prev_b;
+    cp.hist = c->d_hist;
+    HIP_TRY(c, launch_fix_levels(c->d_S, c->ld, b, c->max_score, c->lstride, d_lists, d_hdrs, d_ext, cp, c->st));
+  }
   // the rows the previous batch landed on, re-evaluated on their committed state: inside cand_kernel (block k patches
   // pod k's row before its histogram; one launch less on the commit chain), or by patch_kernel under node sampling
   // (no candidate levels) or GS_FUSED_PATCH=0
-  static const bool separate = getenv("GS_FUSED_PATCH") && getenv("GS_FUSED_PATCH")[0] == '0';
   const bool fused = prev && prev_b > 0 && !c->window_k && !separate;
-  if (prev && !fused)
+  if (!ovl && prev && !fused)
     HIP_TRY(c, launch_patch(c->mv, c->d_pods, b, c->pf, c->n0, c->n1, c->d_S, c->ld, prod_cols, c->d_aff, prev_out,
                             prev, prev_b, c->st));
-  if (!c->window_k) {   // node sampling selects over the rotation window, not the candidate levels
+  if (!c->window_k && !ovl) {   // node sampling selects over the rotation window, not the candidate levels
     CandPatch cp{c->mv, c->d_pods, c->pf, c->n0, c->n1, prod_cols, 1, c->d_aff, prev_out, prev};
     HIP_TRY(c, launch_cand(c->d_S, c->ld, len, c->n0, b, c->max_score, c->lstride, d_lists, d_hdrs, d_ext, c->st,
                            fused ? &cp : nullptr));
   }
-  HIP_TRY(c, hipEventRecord(c->ev[2], c->st));
+  // GS_EV_MIN=1 (experiment): no timing markers between cand and commit (the interval is then booked as commit)
+  static const bool ev_min = getenv("GS_EV_MIN") && getenv("GS_EV_MIN")[0] == '1';
+  if (!ev_min) HIP_TRY(c, hipEventRecord(c->ev[2], c->st));
   if (c->nranks > 1) {
     int rc = exchange(c, c->d_xchg_send, c->d_xchg_recv, c->xchg_bytes);
     if (rc) return rc;
@@ -1017,7 +1052,7 @@ int launch_batch(gs_ctx* c, int b, const int32_t* prev, const PlacementDev* prev
   }
   CommitArgs a = commit_args(c, b);
   a.prev = prev;
-  HIP_TRY(c, hipEventRecord(c->ev[3], c->st));
+  if (!ev_min) HIP_TRY(c, hipEventRecord(c->ev[3], c->st));
   HIP_TRY(c, launch_commit(a, c->st));
   HIP_TRY(c, hipEventRecord(c->ev[4], c->st));
   // full batches: readback on its own stream, so that the speculative next batch's patch / cand start right after the
@@ -1038,8 +1073,13 @@ int finish_batch(gs_ctx* c, int b, bool clobbered, int* committed_out) {
   HIP_TRY(c, hipEventSynchronize(c->ev[5]));
   flush_exchange_times(c);
   c->stats.eval_ms += ev_ms(c->ev[0], c->ev[1]);
-  c->stats.cand_ms += ev_ms(c->ev[1], c->ev[2]);
-  c->stats.commit_ms += ev_ms(c->ev[3], c->ev[4]);
+  static const bool ev_min = getenv("GS_EV_MIN") && getenv("GS_EV_MIN")[0] == '1';
+  if (ev_min) {
+    c->stats.commit_ms += ev_ms(c->ev[1], c->ev[4]);
+  } else {
+    c->stats.cand_ms += ev_ms(c->ev[1], c->ev[2]);
+    c->stats.commit_ms += ev_ms(c->ev[3], c->ev[4]);
+  }
   c->stats.eval_launches += 1;
   c->stats.eval_pairs += (uint64_t)b * len;
   c->stats.batches += 1;
@@ -1779,6 +1819,14 @@ int gs_create(const gs_config* cfg, gs_ctx** out) {
     if ((e = hipHostMalloc(&s1.h_committed, 16, hipHostMallocDefault)) != hipSuccess) return bail("hipHostMalloc", e);
     for (auto& ev : s1.ev)
       if ((e = hipEventCreate(&ev)) != hipSuccess) return bail("hipEventCreate", e);
+    c->cand_overlap = !(getenv("GS_CAND_OVERLAP") && getenv("GS_CAND_OVERLAP")[0] == '0');
+    if (c->cand_overlap)
+      for (auto& sl : c->slot) {
+        if ((e = hipMalloc(&sl.d_lst, xb)) != hipSuccess) return bail("hipMalloc", e);
+        if ((e = hipMalloc(&sl.d_hist, (size_t)4 * c->B * (MAX_SCORE_LIMIT + 1))) != hipSuccess) return bail("hipMalloc", e);
+      }
+    c->d_lst = s0.d_lst;
+    c->d_hist = s0.d_hist;
   }
   c->host_timing = getenv("GS_HOST_TIMING") && getenv("GS_HOST_TIMING")[0] == '1';
   if (getenv("GS_COMMIT_STAMPS") && getenv("GS_COMMIT_STAMPS")[0] == '1') {
@@ -1849,6 +1897,8 @@ int gs_destroy(gs_ctx* c) {
         const double nb = c->stats.batches ? (double)c->stats.batches * c->B : 1.0;
         fprintf(stderr, "gpuscore cand_kernel, wave-0 cycles per pod row: pass 1 %.0f, level sums %.0f, level pick %.0f, "
                 "offsets %.0f, pass 2 %.0f\n", sa[512] / nb, sa[513] / nb, sa[514] / nb, sa[515] / nb, sa[516] / nb);
+        fprintf(stderr, "gpuscore fix_levels_kernel, thread-0 cycles per pod row: loads+dedupe %.0f, landed rows + level pick "
+                "%.0f, lists %.0f\n", sa[517] / nb, sa[518] / nb, sa[519] / nb);
         (void)hipFree(c->d_stamps);
         c->d_stamps = nullptr;
       }
@@ -1887,6 +1937,14 @@ int gs_destroy(gs_ctx* c) {
       if (sl.ev_go) (void)hipEventDestroy(sl.ev_go);
       if (sl.ev_evdone) (void)hipEventDestroy(sl.ev_evdone);
     }
+      for (auto& sl : c->slot) {
+      if (sl.d_lst) (void)hipFree(sl.d_lst);
+      if (sl.d_hist) (void)hipFree(sl.d_hist);
+      sl.d_lst = nullptr;
+      sl.d_hist = nullptr;
+    }
+    c->d_lst = nullptr;
+    c->d_hist = nullptr;
     void* d1[] = {s1.d_pods, s1.d_seq, s1.d_out, s1.d_committed, s1.d_S, s1.d_aff};
     for (void* p : d1)
       if (p) (void)hipFree(p);

@@ -144,9 +144,18 @@ struct CandPatch {
   uint8_t* aff;
   const PlacementDev* prev_out;
   const int32_t* prev_committed;
+  // stale levels (on = 0, cand overlapped with the previous batch's commit): extra = listed nodes beyond pod k's k+1
+  // (the previous batch's landed rows may leave the levels), hist = [pod][max_score + 1] the row's score histogram out
+  int extra;
+  uint32_t* hist;
 };
 hipError_t launch_cand(int16_t* S, uint32_t ld, uint32_t len, uint32_t n0, int npods, int max_score, int lcap,
                        uint32_t* lists, LevelHdr* hdrs, LevelExt* ext, hipStream_t st, const CandPatch* patch = nullptr);
+// The previous batch's landed rows folded into stale levels (cand_kernel with cp.extra / cp.hist, before that batch's
+// commit ended): the rows re-evaluated (S, aff patched as by cand_kernel's patch), the histogram updated, the levels
+// re-picked and each listed level rewritten as its stale nodes minus the landed rows plus the landed rows now at it
+hipError_t launch_fix_levels(int16_t* S, uint32_t ld, int npods, int max_score, int lcap, uint32_t* lists,
+                             LevelHdr* hdrs, LevelExt* ext, const CandPatch& cp, hipStream_t st);
 // several shards: per pod, the all-gathered rank blocks' levels merged into one block of the single-rank layout (the
 // speculative commit's input)
 hipError_t launch_merge_levels(const uint8_t* xin, size_t xblock, int nranks, int npods, int bmax, int lstride,

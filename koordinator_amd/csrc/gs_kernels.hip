@@ -312,6 +312,7 @@ __global__ void __launch_bounds__(64 * W) cand_kernel(int16_t* __restrict__ S, u
 #pragma unroll
       for (int w = 0; w < W; ++w) h += whist[w * nbins + b];
       comb[b] = h;
+      if (cp.hist) cp.hist[(size_t)k * nbins + b] = h;
       slot_of[b] = -1;
       s += h;
     }
@@ -326,7 +327,7 @@ __global__ void __launch_bounds__(64 * W) cand_kernel(int16_t* __restrict__ S, u
     // bins 64 at a time from the top (lane l: bin hi - l); a level stops the list when the levels before it are
     // LEVALL, or it would pass lcap (LCAP; XCAP when the lists are all-gathered), or the nodes before it cover the
     // target.
-    const uint32_t target = (uint32_t)k + 1;
+    const uint32_t target = (uint32_t)k + 1 + (uint32_t)cp.extra;
     const uint64_t lt = (1ull << lane) - 1ull;
     int nlev = 0, next = -1;
     uint32_t cum = 0;
@@ -446,6 +447,283 @@ __global__ void __launch_bounds__(64 * W) cand_kernel(int16_t* __restrict__ S, u
     x.nlev = nlev;
     x.next = s_next;
     for (int j = 0; j < LEVX; ++j) { x.score[j] = s_score[MAXLEV + j]; x.count[j] = s_count[MAXLEV + j]; }
+    ext[k] = x;
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// Stale levels fixed up once the previous batch has committed: cand_kernel ran beside that batch's commit on rows whose
+// landed nodes ("prev rows") still held their pre-commit scores, listing cp.extra nodes beyond pod k's k+1 and writing
+// its histogram. Block k (pod k): re-evaluate the prev rows on their committed state (S, aff patched), move them in the
+// histogram, and re-pick the levels from the top down. A score above the stale `next` is fully known: every non-prev
+// node there is in the stale lists (levels are whole), every prev node is here; so the new levels stop at the first
+// bin at or below the stale `next`, which is then the new `next` (exact: from the updated histogram). Each new level's
+// nodes: its stale segment minus the prev rows, merged (node order) with the prev rows whose new score it is.
+constexpr int FIX_THREADS = 256;
+__device__ __forceinline__ int lower_bound_u32(const uint32_t* a, int n, uint32_t x) {
+  int lo = 0;
+  while (n > 0) {
+    const int h = n >> 1;
+    if (a[lo + h] < x) { lo += h + 1; n -= h + 1; } else { n = h; }
+  }
+  return lo;
+}
+__global__ void __launch_bounds__(FIX_THREADS) fix_levels_kernel(int16_t* __restrict__ S, uint32_t ld, int max_score,
+                                                                 int lcap, uint32_t* __restrict__ lists,
+                                                                 LevelHdr* __restrict__ hdrs, LevelExt* __restrict__ ext,
+                                                                 CandPatch cp, uint64_t* stamps) {
+  // diagnostics (stamps != nullptr): thread 0's cycles per phase, summed over the pods (entries 5..7 of the cand stamps)
+  uint64_t ct_last = stamps ? __builtin_amdgcn_s_memtime() : 0;
+  auto CT = [&](int i) {
+    if (!stamps) return;
+    const uint64_t t_ = __builtin_amdgcn_s_memtime();
+    if (threadIdx.x == 0) atomicAdd(reinterpret_cast<unsigned long long*>(&stamps[i]), (unsigned long long)(t_ - ct_last));
+    ct_last = t_;
+  };
+  extern __shared__ __align__(16) uint32_t smem[];
+  const int nbins = max_score + 1;
+  uint32_t* hist = smem;                 // [nbins] the row's histogram, prev rows moved
+  uint32_t* olist = smem + nbins;        // [lcap] the stale listed nodes
+  __shared__ uint32_t p_raw[MAX_BATCH], p_node[MAX_BATCH];   // prev rows (raw order; distinct, ascending)
+  __shared__ int32_t p_old[MAX_BATCH], p_new[MAX_BATCH];
+  __shared__ uint64_t kr_old[MAX_BATCH], kr_new[MAX_BATCH], k_old[MAX_BATCH], k_new[MAX_BATCH];
+  __shared__ int32_t o_score[LEVALL], o_count[LEVALL], o_off[LEVALL];
+  __shared__ int32_t n_score[LEVALL], n_count[LEVALL], n_off[LEVALL];
+  __shared__ int32_t s_onlev, s_onext, s_ofeas, s_np, s_fd, s_nlev, s_next, s_top;
+  __shared__ int32_t st_old[LEVALL], st_new[LEVALL];   // new level j: prev rows keyed below (score_j + 1, 0)
+  __shared__ int32_t r_old[MAX_BATCH], r_new[MAX_BATCH], p_sidx[MAX_BATCH];   // per raw entry; raw index by rank
+  __shared__ int32_t s_wd[2];
+  int8_t* lev_of = reinterpret_cast<int8_t*>(olist + lcap);   // [nbins] bin -> new level (-1: not listed)
+  const int k = blockIdx.x, t = threadIdx.x, lane = t & 63;
+  const int npr = min(cp.prev_committed[0], MAX_BATCH);   // -1: a voided pass (its lists are never used)
+  if (npr <= 0) return;
+  // phase 1 (no barrier): wave 3 reads the stale levels, every thread part of the histogram, and thread j < npr
+  // evaluates landed entry j (duplicates too: a node several pods landed on gives the same result each time; its stale
+  // score is read here, before any entry's write below)
+  if (t >= FIX_THREADS - 64) {   // the stale levels: one lane per level (independent loads), offsets by a wave scan
+    const LevelHdr& h = hdrs[k];
+    const LevelExt& x = ext[k];
+    const int onl = x.nlev;
+    const int j = lane;
+    int sc = -1, cnt = 0;
+    if (j < LEVALL) {
+      sc = j < MAXLEV ? h.score[j] : x.score[j - MAXLEV];
+      cnt = j < onl ? (j < MAXLEV ? h.count[j] : x.count[j - MAXLEV]) : 0;
+    }
+    const int incl = wave_incl_scan(cnt);
+    if (j < LEVALL) {
+      o_score[j] = sc;
+      o_count[j] = cnt;
+      o_off[j] = incl - cnt;
+    }
+    if (lane == 0) {
+      s_onlev = onl;
+      s_onext = x.next;
+      s_ofeas = h.feasible;
+      s_fd = 0;
+      s_top = onl > 0 ? h.score[0] : x.next;   // the highest non-empty bin before the landed rows move
+    }
+  }
+  for (int b = t; b < nbins; b += FIX_THREADS) hist[b] = cp.hist[(size_t)k * nbins + b];
+  const bool numa = (cp.pf.enabled & 0x30u) != 0;
+  size_t at = 0;
+  int so = -1, sn = -1, aff_v = -1;
+  bool valid = false;
+  if (t < npr) {
+    const int32_t node = cp.prev_out[t].node;
+    valid = node >= 0 && (uint32_t)node >= cp.n0 && (uint32_t)node < cp.n1;
+    p_raw[t] = valid ? (uint32_t)node : 0xffffffffu;
+    if (valid) {
+      at = (size_t)k * ld + ((uint32_t)node - cp.n0);
+      so = S[at];
+      Row r;
+      load_row(cp.m, (uint32_t)node, cp.prod_cols, numa, r);
+      const PairOut o = eval_pair<false, false, true>(r, cp.pods[k], cp.pf, cp.m);
+      sn = total_score(o, cp.pf);
+      if (numa && ((r.nr.nflags >> NF_POLICY_SHIFT) & 3u)) aff_v = o.code ? 0 : (int)o.aff;
+    }
+    r_old[t] = so;
+    r_new[t] = sn;
+  }
+  __syncthreads();
+  // phase 2: the stale lists into LDS; the patched scores out; landed entries ranked by (node, index)
+  {
+    const int otot = s_onlev > 0 ? o_off[s_onlev - 1] + o_count[s_onlev - 1] : 0;
+    const uint32_t* src = lists + (size_t)k * lcap;
+    for (int e = t; e < otot; e += FIX_THREADS) olist[e] = src[e];
+  }
+  if (valid) {
+    S[at] = (int16_t)sn;
+    if (aff_v >= 0) cp.aff[at] = (uint8_t)aff_v;
+  }
+  if (t < npr) {
+    const uint32_t x = p_raw[t];
+    int rank = 0;
+#pragma unroll 16
+    for (int i = 0; i < MAX_BATCH; ++i) {
+      const uint32_t y = p_raw[i];
+      rank += (i < npr && (y < x || (y == x && i < t))) ? 1 : 0;
+    }
+    p_sidx[rank] = t;
+  }
+  __syncthreads();
+  // the first entry of each node, in node order: the distinct landed rows, moved in the histogram
+  bool keep = false;
+  int idx = 0, wpre = 0;
+  uint32_t xs = 0;
+  if (t < 2 * 64) {
+    if (t < npr) {
+      idx = p_sidx[t];
+      xs = p_raw[idx];
+      keep = xs != 0xffffffffu && (t == 0 || p_raw[p_sidx[t - 1]] != xs);
+    }
+    const uint64_t m = __ballot(keep);
+    wpre = __popcll(m & ((1ull << lane) - 1ull));
+    if (lane == 0) s_wd[t >> 6] = __popcll(m);
+  }
+  __syncthreads();
+  if (keep) {
+    const int pos = (t >= 64 ? s_wd[0] : 0) + wpre;
+    const int o_ = r_old[idx], n_ = r_new[idx];
+    p_node[pos] = xs;
+    p_old[pos] = o_;
+    p_new[pos] = n_;
+    if (o_ >= 0) atomicSub(&hist[o_], 1u);
+    if (n_ >= 0) atomicAdd(&hist[n_], 1u);
+    const int fd = (n_ >= 0 ? 1 : 0) - (o_ >= 0 ? 1 : 0);
+    if (fd) atomicAdd(&s_fd, fd);
+    atomicMax(&s_top, n_);
+  }
+  if (t == 0) s_np = s_wd[0] + s_wd[1];
+  __syncthreads();
+  CT(5);
+  const int np = s_np;
+  if (t < 64) {
+    // levels from the top (cand_kernel's rule for pod k: k+1 nodes, LEVALL levels, lcap nodes), known bins only
+    const uint32_t target = (uint32_t)k + 1;
+    const int onext = s_onext;
+    const uint64_t lt = (1ull << lane) - 1ull;
+    int nlev = 0, next = -1;
+    uint32_t cum = 0;
+    for (int hi = min(s_top, nbins - 1); hi >= 0; hi -= 64) {
+      const int b = hi - lane;
+      const uint32_t c = b >= 0 ? hist[b] : 0u;
+      const bool nz = c != 0;
+      const uint64_t nzm = __ballot(nz);
+      if (!nzm) continue;
+      const uint32_t cb = cum + (uint32_t)(wave_incl_scan((int)c) - (int)c);
+      const int nb = nlev + __popcll(nzm & lt);
+      const bool stop = nz && (nb == LEVALL || cb + c > (uint32_t)lcap || cb >= target || b <= onext);
+      const uint64_t sm = __ballot(stop);
+      const int ls = sm ? __builtin_ctzll(sm) : 64;
+      if (nz && lane < ls) {
+        n_score[nb] = b;
+        n_count[nb] = (int32_t)c;
+      }
+      if (sm) {
+        next = __builtin_amdgcn_readlane(b, ls);
+        nlev += __popcll(nzm & ((1ull << ls) - 1ull));
+        break;
+      }
+      nlev += __popcll(nzm);
+      cum += (uint32_t)wave_sum((int)c);
+    }
+    for (int j = nlev + lane; j < LEVALL; j += 64) { n_score[j] = -1; n_count[j] = 0; }
+    if (lane == 0) {
+      s_nlev = nlev;
+      s_next = next;
+    }
+  }
+  __syncthreads();
+  CT(6);
+  const int nlev = s_nlev;
+  // the prev rows keyed (score + 1, node), ascending, by their stale and by their new score; the new levels' offsets
+  // and a bin -> new level map
+  auto key = [](int sc, uint32_t node) { return (uint64_t)(uint32_t)(sc + 1) << 32 | node; };
+  if (t < np) {
+    kr_old[t] = key(p_old[t], p_node[t]);
+    kr_new[t] = key(p_new[t], p_node[t]);
+  }
+  for (int b = t; b < nbins; b += FIX_THREADS) lev_of[b] = -1;
+  if (t == 0) {
+    int off = 0;
+    for (int j = 0; j < nlev; ++j) { n_off[j] = off; off += n_count[j]; }
+  }
+  __syncthreads();
+  if (t < nlev) lev_of[n_score[t]] = (int8_t)t;
+  if (t < np) {
+    const uint64_t ko = kr_old[t], kn = kr_new[t];
+    int ro = 0, rn = 0;
+    for (int i = 0; i < np; ++i) {
+      ro += kr_old[i] < ko ? 1 : 0;
+      rn += kr_new[i] < kn ? 1 : 0;
+    }
+    k_old[ro] = ko;
+    k_new[rn] = kn;
+  }
+  __syncthreads();
+  auto count_lt = [&](const uint64_t* arr, uint64_t x) {
+    int lo = 0, n = np;
+    while (n > 0) {
+      const int h = n >> 1;
+      if (arr[lo + h] < x) { lo += h + 1; n -= h + 1; } else { n = h; }
+    }
+    return lo;
+  };
+  if (t < nlev) {
+    st_old[t] = count_lt(k_old, key(n_score[t], 0));
+    st_new[t] = count_lt(k_new, key(n_score[t], 0));
+  }
+  __syncthreads();
+  uint32_t* out = lists + (size_t)k * lcap;
+  const int onlev = s_onlev;
+  const int otot = onlev > 0 ? o_off[onlev - 1] + o_count[onlev - 1] : 0;
+  // stale entries of a still-listed level, not prev rows: after the kept entries and the new prev rows of a smaller
+  // node at their level
+  for (int e = t; e < otot; e += FIX_THREADS) {
+    int oj = 0;   // the stale level holding entry e: last o_off <= e
+    for (int step = 16; step; step >>= 1)
+      if (oj + step < onlev && o_off[oj + step] <= e) oj += step;
+    const int sj = o_score[oj];
+    const int j = lev_of[sj];
+    if (j < 0) continue;
+    const uint32_t x = olist[e];
+    const int pos = lower_bound_u32(p_node, np, x);
+    if (pos < np && p_node[pos] == x) continue;
+    const int removed = count_lt(k_old, key(sj, x)) - st_old[j];
+    const int added = count_lt(k_new, key(sj, x)) - st_new[j];
+    out[n_off[j] + (e - o_off[oj]) - removed + added] = x;
+  }
+  // prev rows at a listed level: after the new prev rows and the kept stale entries of a smaller node
+  if (t < np) {
+    const int sn = p_new[t];
+    const int j = sn >= 0 ? lev_of[sn] : -1;
+    if (j >= 0) {
+      const uint32_t z = p_node[t];
+      const int r = count_lt(k_new, key(sn, z)) - st_new[j];
+      int before = 0;
+      for (int i = 0; i < onlev; ++i)
+        if (o_score[i] == sn) {
+          before = lower_bound_u32(olist + o_off[i], o_count[i], z) - (count_lt(k_old, key(sn, z)) - st_old[j]);
+          break;
+        }
+      out[n_off[j] + r + before] = z;
+    }
+  }
+  CT(7);
+  if (t == 0) {
+    LevelHdr h;
+    h.nlev = nlev < MAXLEV ? nlev : MAXLEV;
+    h.feasible = s_ofeas + s_fd;
+    h.next = nlev > MAXLEV ? n_score[MAXLEV] : s_next;
+    int32_t tot = 0;
+    for (int j = 0; j < MAXLEV; ++j) { h.score[j] = n_score[j]; h.count[j] = n_count[j]; tot += n_count[j]; }
+    h.total = tot;
+    hdrs[k] = h;
+    LevelExt x;
+    x.nlev = nlev;
+    x.next = s_next;
+    for (int j = 0; j < LEVX; ++j) { x.score[j] = n_score[MAXLEV + j]; x.count[j] = n_count[MAXLEV + j]; }
     ext[k] = x;
   }
 }
@@ -1491,6 +1769,17 @@ static bool cand_wide(int max_score) {
 
 static uint64_t* g_cand_stamps = nullptr;
 void set_cand_stamps(uint64_t* p) { g_cand_stamps = p; }
+
+hipError_t launch_fix_levels(int16_t* S, uint32_t ld, int npods, int max_score, int lcap, uint32_t* lists,
+                             LevelHdr* hdrs, LevelExt* ext, const CandPatch& cp, hipStream_t st) {
+  if (lcap < 1 || lcap > LCAP || !cp.hist || max_score < 0 || max_score > MAX_SCORE_LIMIT || npods > MAX_BATCH)
+    return hipErrorInvalidValue;
+  const size_t smem = ((size_t)max_score + 1 + (size_t)lcap) * 4 + (size_t)max_score + 1;
+  hipLaunchKernelGGL(fix_levels_kernel, dim3(npods), dim3(FIX_THREADS), smem, st, S, ld, max_score, lcap, lists, hdrs, ext,
+                     cp, g_cand_stamps);
+  return hipGetLastError();
+}
+
 
 hipError_t launch_cand(int16_t* S, uint32_t ld, uint32_t len, uint32_t n0, int npods, int max_score, int lcap,
                        uint32_t* lists, LevelHdr* hdrs, LevelExt* ext, hipStream_t st, const CandPatch* patch) {
