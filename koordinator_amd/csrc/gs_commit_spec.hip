@@ -179,8 +179,9 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
   int16_t* hval = L.hval;
   Job* jobq = L.jobq;               // [Reserve wave][ring]
 
+  const uint64_t rt0 = __builtin_amdgcn_s_memrealtime();   // the kernel's duration -> committed[4] (100 MHz ticks)
   if (a.prev && a.prev[1] != 1) {   // speculative pass behind a batch that left work for the host: no-op
-    if (tid == 0) { a.committed[0] = -1; a.committed[1] = 0; a.committed[3] = 0; }
+    if (tid == 0) { a.committed[0] = -1; a.committed[1] = 0; a.committed[3] = 0; a.committed[4] = 0; }
     return;
   }
   for (int i = tid; i < B; i += SP_THREADS) {
@@ -1286,6 +1287,7 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
     a.committed[1] = (committed == B && !s_hostcut && !s_err) ? 1 : 0;
     a.committed[2] = s_endwhy;   // diagnostics: why a batch ended early (GS_DEBUG_CUTS)
     a.committed[3] = s_err;
+    a.committed[4] = (int32_t)(__builtin_amdgcn_s_memrealtime() - rt0);
   }
 }
 

@@ -1040,9 +1040,8 @@ int launch_batch(gs_ctx* c, int b, const int32_t* prev, const PlacementDev* prev
     HIP_TRY(c, launch_cand(c->d_S, c->ld, len, c->n0, b, c->max_score, c->lstride, d_lists, d_hdrs, d_ext, c->st,
                            fused ? &cp : nullptr));
   }
-  // GS_EV_MIN=1 (experiment): no timing markers between cand and commit (the interval is then booked as commit)
-  static const bool ev_min = getenv("GS_EV_MIN") && getenv("GS_EV_MIN")[0] == '1';
-  if (!ev_min) HIP_TRY(c, hipEventRecord(c->ev[2], c->st));
+  // no timing markers between the levels and the commit kernel (each one held the commit's dispatch ~13 us): the
+  // commit's duration comes from the kernel itself (committed[4]), the levels' interval is the rest up to ev[4]
   if (c->nranks > 1) {
     int rc = exchange(c, c->d_xchg_send, c->d_xchg_recv, c->xchg_bytes);
     if (rc) return rc;
@@ -1052,7 +1051,6 @@ int launch_batch(gs_ctx* c, int b, const int32_t* prev, const PlacementDev* prev
   }
   CommitArgs a = commit_args(c, b);
   a.prev = prev;
-  if (!ev_min) HIP_TRY(c, hipEventRecord(c->ev[3], c->st));
   HIP_TRY(c, launch_commit(a, c->st));
   HIP_TRY(c, hipEventRecord(c->ev[4], c->st));
   // full batches: readback on its own stream, so that the speculative next batch's patch / cand start right after the
@@ -1060,7 +1058,7 @@ int launch_batch(gs_ctx* c, int b, const int32_t* prev, const PlacementDev* prev
   // waits on each one) keep it in order on st: the extra queue hop costs more than it hides there.
   hipStream_t rb = b >= 32 ? c->st_rb : c->st;
   if (rb != c->st) HIP_TRY(c, hipStreamWaitEvent(rb, c->ev[4], 0));
-  HIP_TRY(c, hipMemcpyAsync(c->h_committed, c->d_committed, 16, hipMemcpyDeviceToHost, rb));
+  HIP_TRY(c, hipMemcpyAsync(c->h_committed, c->d_committed, 32, hipMemcpyDeviceToHost, rb));
   HIP_TRY(c, hipMemcpyAsync(c->h_out, c->d_out, sizeof(PlacementDev) * b, hipMemcpyDeviceToHost, rb));
   HIP_TRY(c, hipEventRecord(c->ev[5], rb));
   return GS_OK;
@@ -1073,12 +1071,10 @@ int finish_batch(gs_ctx* c, int b, bool clobbered, int* committed_out) {
   HIP_TRY(c, hipEventSynchronize(c->ev[5]));
   flush_exchange_times(c);
   c->stats.eval_ms += ev_ms(c->ev[0], c->ev[1]);
-  static const bool ev_min = getenv("GS_EV_MIN") && getenv("GS_EV_MIN")[0] == '1';
-  if (ev_min) {
-    c->stats.commit_ms += ev_ms(c->ev[1], c->ev[4]);
-  } else {
-    c->stats.cand_ms += ev_ms(c->ev[1], c->ev[2]);
-    c->stats.commit_ms += ev_ms(c->ev[3], c->ev[4]);
+  {   // commit kernel: its own duration (s_memrealtime, 100 MHz) in committed[4]; levels: the rest from the eval's end
+    const double cm = (double)(uint32_t)c->h_committed[4] * 1e-5;
+    c->stats.commit_ms += cm;
+    c->stats.cand_ms += std::max(0.0, ev_ms(c->ev[1], c->ev[4]) - cm);
   }
   c->stats.eval_launches += 1;
   c->stats.eval_pairs += (uint64_t)b * len;
@@ -1151,7 +1147,7 @@ int finish_batch(gs_ctx* c, int b, bool clobbered, int* committed_out) {
     HIP_TRY(c, hipEventRecord(c->ev[3], c->st));
     HIP_TRY(c, launch_commit(a, c->st));
     HIP_TRY(c, hipEventRecord(c->ev[4], c->st));
-    HIP_TRY(c, hipMemcpyAsync(c->h_committed, c->d_committed, 16, hipMemcpyDeviceToHost, c->st));
+    HIP_TRY(c, hipMemcpyAsync(c->h_committed, c->d_committed, 32, hipMemcpyDeviceToHost, c->st));
     HIP_TRY(c, hipStreamSynchronize(c->st));
     c->stats.commit_ms += ev_ms(c->ev[3], c->ev[4]);
     committed = c->h_committed[0];
@@ -1780,7 +1776,7 @@ int gs_create(const gs_config* cfg, gs_ctx** out) {
   if ((e = hipMalloc(&c->d_xchg_send, xb)) != hipSuccess) return bail("hipMalloc", e);
   c->xchg_bytes = xb;
   if ((e = hipMalloc(&c->d_out, sizeof(PlacementDev) * c->B)) != hipSuccess) return bail("hipMalloc", e);
-  if ((e = hipMalloc(&c->d_committed, 16)) != hipSuccess) return bail("hipMalloc", e);
+  if ((e = hipMalloc(&c->d_committed, 32)) != hipSuccess) return bail("hipMalloc", e);
   if ((e = hipMalloc(&c->d_tb, sizeof(int32_t) * TB_N * c->B)) != hipSuccess) return bail("hipMalloc", e);
   if ((e = hipMalloc(&c->d_rowstat, sizeof(RowStat) * (1 + MAX_RANKS))) != hipSuccess) return bail("hipMalloc", e);
   if ((e = hipMalloc(&c->d_sel, 4 * (1 + MAX_RANKS))) != hipSuccess) return bail("hipMalloc", e);
@@ -1792,7 +1788,7 @@ int gs_create(const gs_config* cfg, gs_ctx** out) {
   if ((e = hipHostMalloc(&c->h_pods, sizeof(PodVec) * c->B, hipHostMallocDefault)) != hipSuccess) return bail("hipHostMalloc", e);
   if ((e = hipHostMalloc(&c->h_seq, 8 * c->B, hipHostMallocDefault)) != hipSuccess) return bail("hipHostMalloc", e);
   if ((e = hipHostMalloc(&c->h_out, sizeof(PlacementDev) * c->B, hipHostMallocDefault)) != hipSuccess) return bail("hipHostMalloc", e);
-  if ((e = hipHostMalloc(&c->h_committed, 16, hipHostMallocDefault)) != hipSuccess) return bail("hipHostMalloc", e);
+  if ((e = hipHostMalloc(&c->h_committed, 32, hipHostMallocDefault)) != hipSuccess) return bail("hipHostMalloc", e);
   if ((e = hipHostMalloc(&c->h_xchg_send, xb, hipHostMallocDefault)) != hipSuccess) return bail("hipHostMalloc", e);
   (void)hipMemset(c->d_S, 0xff, (size_t)c->B * c->ld * 2);
   {
@@ -1812,11 +1808,11 @@ int gs_create(const gs_config* cfg, gs_ctx** out) {
     if ((e = hipMalloc(&s1.d_pods, sizeof(PodVec) * c->B)) != hipSuccess) return bail("hipMalloc", e);
     if ((e = hipMalloc(&s1.d_seq, 8 * c->B)) != hipSuccess) return bail("hipMalloc", e);
     if ((e = hipMalloc(&s1.d_out, sizeof(PlacementDev) * c->B)) != hipSuccess) return bail("hipMalloc", e);
-    if ((e = hipMalloc(&s1.d_committed, 16)) != hipSuccess) return bail("hipMalloc", e);
+    if ((e = hipMalloc(&s1.d_committed, 32)) != hipSuccess) return bail("hipMalloc", e);
     if ((e = hipHostMalloc(&s1.h_pods, sizeof(PodVec) * c->B, hipHostMallocDefault)) != hipSuccess) return bail("hipHostMalloc", e);
     if ((e = hipHostMalloc(&s1.h_seq, 8 * c->B, hipHostMallocDefault)) != hipSuccess) return bail("hipHostMalloc", e);
     if ((e = hipHostMalloc(&s1.h_out, sizeof(PlacementDev) * c->B, hipHostMallocDefault)) != hipSuccess) return bail("hipHostMalloc", e);
-    if ((e = hipHostMalloc(&s1.h_committed, 16, hipHostMallocDefault)) != hipSuccess) return bail("hipHostMalloc", e);
+    if ((e = hipHostMalloc(&s1.h_committed, 32, hipHostMallocDefault)) != hipSuccess) return bail("hipHostMalloc", e);
     for (auto& ev : s1.ev)
       if ((e = hipEventCreate(&ev)) != hipSuccess) return bail("hipEventCreate", e);
     c->cand_overlap = !(getenv("GS_CAND_OVERLAP") && getenv("GS_CAND_OVERLAP")[0] == '0');

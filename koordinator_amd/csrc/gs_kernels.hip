@@ -926,7 +926,7 @@ __global__ void __launch_bounds__(COMMIT_THREADS) commit_kernel(CommitArgs a) {
   // speculative pass queued behind another batch: only if that one committed every pod with nothing left for
   // the host (committed[1] == 1); otherwise a no-op (committed = -1) the host discards
   if (a.prev && a.prev[1] != 1) {
-    if (tid == 0) { a.committed[0] = -1; a.committed[1] = 0; a.committed[3] = 0; }
+    if (tid == 0) { a.committed[0] = -1; a.committed[1] = 0; a.committed[3] = 0; a.committed[4] = 0; }
     return;
   }
 
@@ -1573,6 +1573,7 @@ __global__ void __launch_bounds__(COMMIT_THREADS) commit_kernel(CommitArgs a) {
     a.committed[1] = (committed == B && !host_cut) ? 1 : 0;
     a.committed[2] = (int32_t)s_start;
     a.committed[3] = 0;
+    a.committed[4] = 0;
   }
   if (ST && tid == 0) {
     for (int i = 0; i < 12; ++i) a.stamps[i] += st_acc[i];
