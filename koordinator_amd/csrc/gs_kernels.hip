@@ -486,11 +486,11 @@ __global__ void __launch_bounds__(FIX_THREADS) fix_levels_kernel(int16_t* __rest
   uint32_t* olist = smem + nbins;        // [lcap] the stale listed nodes
   __shared__ uint32_t p_raw[MAX_BATCH], p_node[MAX_BATCH];   // prev rows (raw order; distinct, ascending)
   __shared__ int32_t p_old[MAX_BATCH], p_new[MAX_BATCH];
-  __shared__ uint64_t kr_old[MAX_BATCH], kr_new[MAX_BATCH], k_old[MAX_BATCH], k_new[MAX_BATCH];
+  __shared__ unsigned long long m_old[LEVALL][2], m_new[LEVALL][2];
+  __shared__ int32_t n_ol[LEVALL];
   __shared__ int32_t o_score[LEVALL], o_count[LEVALL], o_off[LEVALL];
   __shared__ int32_t n_score[LEVALL], n_count[LEVALL], n_off[LEVALL];
   __shared__ int32_t s_onlev, s_onext, s_ofeas, s_np, s_fd, s_nlev, s_next, s_top;
-  __shared__ int32_t st_old[LEVALL], st_new[LEVALL];   // new level j: prev rows keyed below (score_j + 1, 0)
   __shared__ int32_t r_old[MAX_BATCH], r_new[MAX_BATCH], p_sidx[MAX_BATCH];   // per raw entry; raw index by rank
   __shared__ int32_t s_wd[2];
   int8_t* lev_of = reinterpret_cast<int8_t*>(olist + lcap);   // [nbins] bin -> new level (-1: not listed)
@@ -629,6 +629,9 @@ __global__ void __launch_bounds__(FIX_THREADS) fix_levels_kernel(int16_t* __rest
       cum += (uint32_t)wave_sum((int)c);
     }
     for (int j = nlev + lane; j < LEVALL; j += 64) { n_score[j] = -1; n_count[j] = 0; }
+    WAVE_FENCE();
+    const int cnt = lane < LEVALL ? n_count[lane] : 0;
+    if (lane < LEVALL) n_off[lane] = wave_incl_scan(cnt) - cnt;
     if (lane == 0) {
       s_nlev = nlev;
       s_next = next;
@@ -637,44 +640,29 @@ __global__ void __launch_bounds__(FIX_THREADS) fix_levels_kernel(int16_t* __rest
   __syncthreads();
   CT(6);
   const int nlev = s_nlev;
-  // the prev rows keyed (score + 1, node), ascending, by their stale and by their new score; the new levels' offsets
-  // and a bin -> new level map
-  auto key = [](int sc, uint32_t node) { return (uint64_t)(uint32_t)(sc + 1) << 32 | node; };
-  if (t < np) {
-    kr_old[t] = key(p_old[t], p_node[t]);
-    kr_new[t] = key(p_new[t], p_node[t]);
-  }
+  // per new level j: the prev rows (bit i = p_node[i], node order) whose stale / new score is its score, and the stale
+  // level of the same score (-1: none); a bin -> new level map
   for (int b = t; b < nbins; b += FIX_THREADS) lev_of[b] = -1;
-  if (t == 0) {
-    int off = 0;
-    for (int j = 0; j < nlev; ++j) { n_off[j] = off; off += n_count[j]; }
-  }
+  if (t < LEVALL * 2) { m_old[t >> 1][t & 1] = 0; m_new[t >> 1][t & 1] = 0; }
   __syncthreads();
-  if (t < nlev) lev_of[n_score[t]] = (int8_t)t;
-  if (t < np) {
-    const uint64_t ko = kr_old[t], kn = kr_new[t];
-    int ro = 0, rn = 0;
-    for (int i = 0; i < np; ++i) {
-      ro += kr_old[i] < ko ? 1 : 0;
-      rn += kr_new[i] < kn ? 1 : 0;
-    }
-    k_old[ro] = ko;
-    k_new[rn] = kn;
-  }
-  __syncthreads();
-  auto count_lt = [&](const uint64_t* arr, uint64_t x) {
-    int lo = 0, n = np;
-    while (n > 0) {
-      const int h = n >> 1;
-      if (arr[lo + h] < x) { lo += h + 1; n -= h + 1; } else { n = h; }
-    }
-    return lo;
-  };
   if (t < nlev) {
-    st_old[t] = count_lt(k_old, key(n_score[t], 0));
-    st_new[t] = count_lt(k_new, key(n_score[t], 0));
+    lev_of[n_score[t]] = (int8_t)t;
+    int o = -1;
+    for (int i = 0; i < s_onlev; ++i) o = o_score[i] == n_score[t] ? i : o;
+    n_ol[t] = o;
   }
   __syncthreads();
+  if (t < np) {
+    const int jo = p_old[t] >= 0 ? lev_of[p_old[t]] : -1, jn = p_new[t] >= 0 ? lev_of[p_new[t]] : -1;
+    if (jo >= 0) atomicOr(&m_old[jo][t >> 6], 1ull << (t & 63));
+    if (jn >= 0) atomicOr(&m_new[jn][t >> 6], 1ull << (t & 63));
+  }
+  __syncthreads();
+  auto below = [](const unsigned long long (&m)[2], int pos) {   // bits < pos
+    const int lo = min(pos, 64), hi = max(pos - 64, 0);
+    return __popcll(lo >= 64 ? m[0] : (m[0] & ((1ull << lo) - 1ull))) +
+           __popcll(hi >= 64 ? m[1] : (m[1] & ((1ull << hi) - 1ull)));
+  };
   uint32_t* out = lists + (size_t)k * lcap;
   const int onlev = s_onlev;
   const int otot = onlev > 0 ? o_off[onlev - 1] + o_count[onlev - 1] : 0;
@@ -684,30 +672,21 @@ __global__ void __launch_bounds__(FIX_THREADS) fix_levels_kernel(int16_t* __rest
     int oj = 0;   // the stale level holding entry e: last o_off <= e
     for (int step = 16; step; step >>= 1)
       if (oj + step < onlev && o_off[oj + step] <= e) oj += step;
-    const int sj = o_score[oj];
-    const int j = lev_of[sj];
+    const int j = lev_of[o_score[oj]];
     if (j < 0) continue;
     const uint32_t x = olist[e];
     const int pos = lower_bound_u32(p_node, np, x);
     if (pos < np && p_node[pos] == x) continue;
-    const int removed = count_lt(k_old, key(sj, x)) - st_old[j];
-    const int added = count_lt(k_new, key(sj, x)) - st_new[j];
-    out[n_off[j] + (e - o_off[oj]) - removed + added] = x;
+    out[n_off[j] + (e - o_off[oj]) - below(m_old[j], pos) + below(m_new[j], pos)] = x;
   }
   // prev rows at a listed level: after the new prev rows and the kept stale entries of a smaller node
   if (t < np) {
     const int sn = p_new[t];
     const int j = sn >= 0 ? lev_of[sn] : -1;
     if (j >= 0) {
-      const uint32_t z = p_node[t];
-      const int r = count_lt(k_new, key(sn, z)) - st_new[j];
-      int before = 0;
-      for (int i = 0; i < onlev; ++i)
-        if (o_score[i] == sn) {
-          before = lower_bound_u32(olist + o_off[i], o_count[i], z) - (count_lt(k_old, key(sn, z)) - st_old[j]);
-          break;
-        }
-      out[n_off[j] + r + before] = z;
+      const int oj = n_ol[j];
+      const int before = oj >= 0 ? lower_bound_u32(olist + o_off[oj], o_count[oj], p_node[t]) - below(m_old[j], t) : 0;
+      out[n_off[j] + below(m_new[j], t) + before] = p_node[t];
     }
   }
   CT(7);
