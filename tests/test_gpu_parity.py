@@ -98,6 +98,24 @@ def test_schedule_in_chunks_and_custom_seq():
         _check_schedule(e, o, c.pods[lo:lo + 150], seq[lo:lo + 150])
 
 
+@pytest.mark.parametrize("numa", [False, True])
+def test_overlapped_levels_match_serial_levels(numa, monkeypatch):
+    """Candidate levels built beside the previous batch's commit and fixed up after it (fix_levels_kernel, the
+    default) against levels built after the commit (GS_CAND_OVERLAP=0): identical placements, both the oracle's."""
+    c = synth.make_cluster(4000, 1200, 5)
+    if numa:
+        synth.make_numa(c)
+    kw = dict(enabled=abi.GS_ENABLE_ALL) if numa else {}
+    got = {}
+    for mode in ("1", "0"):
+        monkeypatch.setenv("GS_CAND_OVERLAP", mode)
+        e, o = pair(c, **kw)
+        got[mode] = _check_schedule(e, o, c.pods)
+        assert e.stats()["batches"] >= 9
+    for f in ("node", "score", "ties", "feasible"):
+        assert (got["1"][f] == got["0"][f]).all()
+
+
 def homogeneous_cluster(nodes, pods, seed):
     c = synth.make_cluster(nodes, pods, seed)
     c.nodes["requested"] = 0
