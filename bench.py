@@ -299,11 +299,14 @@ def main() -> None:
                       "achieved_GBps": eval_achieved, "frac": eval_achieved / HBM_PEAK_GBPS,
                       "pmc_bytes_per_launch": pmc_bytes("gs::eval"),
                       "share_of_step": st["eval_ms"] / args.steps / step_ms},
-        "patch_cand_interval": {"what": "HIP events from the eval pass's end to cand_kernel's end: patch_kernel + "
-                                        "cand_kernel plus the wait for the previous batch's commit (they share its "
-                                        "stream); the kernels' own durations are in the rocprof summary",
+        "patch_cand_interval": {"what": "from the eval pass's end (HIP event) to the commit kernel's start (the "
+                                        "batch's end event minus the commit's own s_memrealtime duration): "
+                                        "cand_kernel beside the previous batch's commit, the wait for that commit, "
+                                        "then fix_levels_kernel (its landed rows re-evaluated and folded into the "
+                                        "levels); the kernels' own durations are in the rocprof summary",
                                 "avg_us": st["cand_ms"] / batches * 1e3,
-                                "pmc_bytes_per_launch": pmc_bytes("gs::cand"),
+                                "pmc_bytes_per_launch": (pmc_bytes("gs::cand") or 0) + (pmc_bytes("gs::fix_levels") or 0)
+                                if (pmc_bytes("gs::cand") or pmc_bytes("gs::fix_levels")) else None,
                                 "share_of_step": st["cand_ms"] / args.steps / step_ms},
         "commit_kernel": {"bound": "latency: one workgroup walks the batch's pods in order (selectHost, Reserve, "
                                    "re-scoring of the rows earlier pods landed on)",
