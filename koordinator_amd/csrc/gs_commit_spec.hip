@@ -218,11 +218,28 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
       for (uint64_t b = m0; b; b &= b - 1) fn((uint32_t)__builtin_amdgcn_readlane((int)dn0, __builtin_ctzll(b)));
       for (uint64_t b = m1; b; b &= b - 1) fn((uint32_t)__builtin_amdgcn_readlane((int)dn1, __builtin_ctzll(b)));
     };
-    auto hash_insert = [&](uint32_t node, int slot) {
-      uint32_t h = (node * 2654435761u) & (SP_HASH - 1);
-      while (hkey[h] >= 0) h = (h + 1) & (SP_HASH - 1);
-      hkey[h] = (int32_t)node;
-      hval[h] = (int16_t)slot;
+    // node -> slot hash, needed only by the full-row resolution: rebuilt there when slots changed since (one lane per
+    // slot; an LDS compare-and-swap claims a probe position, and a key only moves past occupied positions, so
+    // linear-probe lookups find it)
+    bool hash_ok = true;
+    auto rebuild_hash = [&]() {
+      for (int i = lane; i < SP_HASH; i += 64) { hkey[i] = -1; hval[i] = -1; }
+      WAVE_FENCE();
+      for (int half = 0; half < 2; ++half) {
+        bool todo = lane + 64 * half < nd;
+        const uint32_t nn = half ? dn1 : dn0;
+        uint32_t h = (nn * 2654435761u) & (SP_HASH - 1);
+        while (todo) {
+          if (atomicCAS(&hkey[h], -1, (int32_t)nn) == -1) {
+            hval[h] = (int16_t)(lane + 64 * half);
+            todo = false;
+          } else {
+            h = (h + 1) & (SP_HASH - 1);
+          }
+        }
+        WAVE_FENCE();
+      }
+      hash_ok = true;
     };
     auto sp_hash_find = [&](uint32_t node) -> int {
       uint32_t h = (node * 2654435761u) & (SP_HASH - 1);
@@ -318,25 +335,8 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
         if (lane + 64 >= ndv) { dn1 = 0xffffffffu; pv1 = -1; }
         for (int s = ndv + lane; s < nd; s += 64) { has_row[s] = 0; done_ver[s] = -1; }
         nd = ndv;
-        for (int i = lane; i < SP_HASH; i += 64) { hkey[i] = -1; hval[i] = -1; }
-        WAVE_FENCE();
-        // the surviving slots back into the hash, one lane per slot (LDS compare-and-swap claims a probe position; a
-        // key only moves past occupied positions, so linear-probe lookups find it)
-        for (int half = 0; half < 2; ++half) {
-          bool todo = lane + 64 * half < nd;
-          const uint32_t nn = half ? dn1 : dn0;
-          uint32_t h = (nn * 2654435761u) & (SP_HASH - 1);
-          while (todo) {
-            if (atomicCAS(&hkey[h], -1, (int32_t)nn) == -1) {
-              hval[h] = (int16_t)(lane + 64 * half);
-              todo = false;
-            } else {
-              h = (h + 1) & (SP_HASH - 1);
-            }
-          }
-          WAVE_FENCE();
-        }
-        SPM(38);   // rollback: undo log, slot versions, hash rebuild
+        hash_ok = false;   // rebuilt by the next full-row resolution that needs it
+        SPM(38);   // rollback: undo log, slot versions
         if (ST) st_acc[40] += __popcll(redo0) + __popcll(redo1);
         // re-score the restored rows for pods v.. (their dsc entries after the undone landing are stale)
         for (int pass = 0; pass < 2; ++pass) {
@@ -597,6 +597,7 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
       if (ST) st_acc[10] += full_row ? 1 : 0;
       SPM(19);   // decide: tie-break position, winner among listed + dirty ties
       if (full_row) {
+        if (!hash_ok) rebuild_hash();
         // exact resolution of pod p from its whole score row: batch-start S[p][*] for clean nodes, the current
         // score for ready dirty rows, pending rows left out (verified later like any decision)
         const int16_t* row = a.S + (size_t)p * a.ld;
@@ -772,10 +773,8 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
             if (q0 < B) dso[q0 * SB + slot] = SO_UNKNOWN;
             if (q1 < B) dso[q1 * SB + slot] = SO_UNKNOWN;
           }
-          if (lane == 0) {
-            hash_insert(winner, slot);
-            done_ver[slot] = -1;
-          }
+          if (lane == 0) done_ver[slot] = -1;
+          hash_ok = false;
           ++nd;
           SPM(20);   // decide: fresh slot's batch-start scores (S_own loads)
         } else {          // a ready dirty row lands another pod: pending again
