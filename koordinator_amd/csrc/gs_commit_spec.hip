@@ -208,6 +208,8 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
   if (wv == 0) {
     // ==================================================== decide ====================================================
     __builtin_amdgcn_s_setprio(3);
+    // decisions ahead of the verifier: SP_LAG (the undo log's depth), or fewer (GS_SPEC_LAG, experiments)
+    const int lag = ((a.dbg >> 12) & 15u) ? (int)min((a.dbg >> 12) & 15u, (uint32_t)SP_LAG) : SP_LAG;
     uint32_t dn0 = 0xffffffffu, dn1 = 0xffffffffu;   // slot s's node in lane s % 64 of dn0 / dn1
     int32_t pv0 = -1, pv1 = -1;                      // slot s's latest decided version (pod index)
     int nd = 0, q = 0, end_at = B, end_why = 0;
@@ -391,7 +393,7 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
       }
       SPM(27);   // rollback / batch-end checks
       // ------------------------------------------------ decide pod q
-      if (q >= end_at || q - ld_acq(&s_verified) >= SP_LAG || ld_acq(&s_cut_at) >= 0) {
+      if (q >= end_at || q - ld_acq(&s_verified) >= lag || ld_acq(&s_cut_at) >= 0) {
         if (++spins > SP_SPIN_LIMIT) { err = true; err_code = 2; break; }
         if (const int we = ld_acq(&s_werr)) { err = true; err_code = we; break; }
         sp_sleep();

@@ -958,7 +958,9 @@ CommitArgs commit_args(gs_ctx* c, int b) {
   static const bool nospec = getenv("GS_SPEC_WAIT") && getenv("GS_SPEC_WAIT")[0] == '1';
   // GS_SPEC_PRIO (experiments): issue priorities of the roles, bits 4-5 Reserve, 6-7 re-scoring, 8-9 verify
   static const uint32_t prio = getenv("GS_SPEC_PRIO") ? (uint32_t)strtoul(getenv("GS_SPEC_PRIO"), nullptr, 0) & 0x3f0u : 0u;
-  a.dbg = (nospec ? 1u : 0u) | prio;
+  // GS_SPEC_LAG (experiments): decisions ahead of the verifier, 1..12 (bits 12-15; 0: the kernel's SP_LAG)
+  static const uint32_t lag = getenv("GS_SPEC_LAG") ? (uint32_t)std::min(12L, std::max(0L, atol(getenv("GS_SPEC_LAG")))) : 0u;
+  a.dbg = (nospec ? 1u : 0u) | prio | lag << 12;
   a.tb = c->d_tb;
   return a;
 }
@@ -1726,6 +1728,10 @@ int gs_create(const gs_config* cfg, gs_ctx** out) {
   c->npad = (c->N + 1023) & ~1023u;
   c->nodes.resize(c->N);
   c->numa.resize(c->N);
+  // pod uid -> node maps grow by one entry per placement: buckets for a few pods per node up front, so the scheduling
+  // loop does not stop for a rehash of tens of thousands of entries (a multi-ms stall of the batch pipeline)
+  c->uid_node.reserve(std::max<size_t>(size_t(1) << 17, 4 * (size_t)c->N));
+  c->numa_uid_node.reserve(std::max<size_t>(size_t(1) << 16, (size_t)c->N));
   c->row_dirty.assign(c->N, 0);
   c->devs.assign(c->N, gs_node_devices{});
   c->dev_dirty.assign(c->N, 0);
