@@ -47,9 +47,9 @@ def cpu_baseline(cluster, cfg, pods, seq, given, sample_start: int, sample_pods:
     o.schedule(pods[i:i + warm], seq[i:i + warm], nthreads=threads)
     i += warm
     o.phase_times()
-    # the timed pods one scheduleOne at a time (the reference's loop), their times grouped into 5 strided chunks (pod
-    # j -> chunk j % 5): every chunk samples the same mix of pods (cpuset / NUMA / plain) along the queue, so the chunk
-    # rates differ by the machine's noise, not by which pods a contiguous chunk happened to hold
+    # the timed pods one scheduleOne at a time (the reference's loop), their times grouped into 5 chunks by a fixed
+    # random permutation: every chunk is a random sample of the queue's pods (a contiguous or a j % 5 chunk can hold a
+    # skewed share of the expensive cpuset / NUMA pods: the synthetic queue's kinds follow index patterns)
     n_t = max(5, sample_pods - warm)
     per = np.zeros(n_t)
     for j in range(n_t):
@@ -58,7 +58,8 @@ def cpu_baseline(cluster, cfg, pods, seq, given, sample_start: int, sample_pods:
         per[j] = time.perf_counter() - t0
     i += n_t
     chunk = n_t // 5
-    rates = [float(chunk / per[c::5][:chunk].sum()) for c in range(5)]
+    perm = np.random.default_rng(20260).permutation(n_t)
+    rates = [float(chunk / per[perm[c * chunk:(c + 1) * chunk]].sum()) for c in range(5)]
     secs = float(per.sum())
     phases = o.phase_times()
     n1 = max(4, chunk // 8)
@@ -68,12 +69,12 @@ def cpu_baseline(cluster, cfg, pods, seq, given, sample_start: int, sample_pods:
     pods_per_s = float(np.median(rates))
     return {"pods_per_s": pods_per_s, "evals_per_s": pods_per_s * cluster.num_nodes, "seconds": secs,
             "chunks": 5, "chunk_pods": chunk, "chunk_pods_per_s": rates,
-            "chunk_spread": (max(rates) - min(rates)) / (2 * pods_per_s),
+            "chunk_spread": (max(rates) - min(rates)) / (2 * pods_per_s), "all_pods_per_s": float(n_t / secs),
             "phase_share": {k: v / max(secs, 1e-12) for k, v in phases.items()},
             "single_thread_pods_per_s": r1, "single_thread_evals_per_s": r1 * cluster.num_nodes,
             "sample": f"pods {sample_start}..{i + n1} of the timed workload on the GPU's state at the start of the timed "
                       f"region (oracle replay of the {sample_start} warm-up placements); {warm} warm-up pods, {n_t} timed "
-                      f"pods at {threads} threads one scheduleOne at a time, rates of 5 strided chunks of {chunk} pods "
+                      f"pods at {threads} threads one scheduleOne at a time, rates of 5 random chunks of {chunk} pods "
                       f"(median), {n1} pods at 1 thread"}
 
 
@@ -340,7 +341,7 @@ def main() -> None:
                          "(parallelize.Until emulation, parallelism=16 = the reference default and this box's CPU "
                          "share); CPU restatement of the reference Go path (oracle/), not the Go binary",
                "pods_per_s": r["pods_per_s"], "seconds": r["seconds"], "chunk_pods_per_s": r["chunk_pods_per_s"],
-               "chunk_spread": r["chunk_spread"],
+               "chunk_spread": r["chunk_spread"], "all_pods_per_s": r["all_pods_per_s"],
                "phase_share": r["phase_share"], "single_thread_evals_per_s": r["single_thread_evals_per_s"],
                "single_thread_pods_per_s": r["single_thread_pods_per_s"]}
 
