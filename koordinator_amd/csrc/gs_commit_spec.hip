@@ -1227,6 +1227,7 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
       const Row rr = drows[jb.slot];
       if (numa_on && ((rr.nr.nflags >> NF_POLICY_SHIFT) & 3u)) hint_table_fill(tab, rr.nr, zone_avail(rr.nr), lane);
       WAVE_FENCE();
+      SPM(9);   // re-scoring job: row copy + hint table
       const int q2 = jb.q + 1 + jb.range * 64 + lane;
       if (q2 < B) dsc[q2 * SB + jb.slot] = (int16_t)row_score(rr, pods(q2), a.pf, m, &tab);
       WAVE_FENCE();
@@ -1237,6 +1238,7 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
           __atomic_store_n(&rescored[jb.q], 1, __ATOMIC_RELEASE);
       }
       WAVE_FENCE();
+      if (ST) st_acc[10] += 1;
       SPM(7);
     }
   }

@@ -1895,7 +1895,9 @@ int gs_destroy(gs_ctx* c) {
           fprintf(stderr, "  wave %d (Reserve): fetch+undo %.0f numa_eval %.0f lane0 %.0f rest %.0f (fresh fetch %.0f, landed-"
                   "again wait %.0f) waiting %.0f (first decision %.0f)\n", w, W(w, 15), W(w, 16), W(w, 17), W(w, 5), W(w, 21),
                   W(w, 22), W(w, 6), W(w, 26));
-        for (int w : {1, 5, 6, 7}) fprintf(stderr, "  wave %d (re-scoring): busy %.0f waiting %.0f\n", w, W(w, 7), W(w, 8));
+        for (int w : {1, 5, 6, 7})
+          fprintf(stderr, "  wave %d (re-scoring): busy %.0f (row copy + hint table %.0f, scores %.0f) waiting %.0f, jobs %.2f "
+                  "per pod\n", w, W(w, 7) + W(w, 9), W(w, 9), W(w, 7), W(w, 8), W(w, 10));
         const double nb = c->stats.batches ? (double)c->stats.batches * c->B : 1.0;
         fprintf(stderr, "gpuscore cand_kernel, wave-0 cycles per pod row: pass 1 %.0f, level sums %.0f, level pick %.0f, "
                 "offsets %.0f, pass 2 %.0f\n", sa[512] / nb, sa[513] / nb, sa[514] / nb, sa[515] / nb, sa[516] / nb);
