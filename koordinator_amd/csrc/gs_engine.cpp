@@ -25,6 +25,7 @@
 #include <memory>
 #include <mutex>
 #include <thread>
+#include <atomic>
 
 #include "../../include/gpuscore.h"
 #include "gs_ext.h"
@@ -179,6 +180,20 @@ struct gs_ctx {
   ncclComm_t comm = nullptr;
   gs_allgather_fn cb = nullptr;
   void* cb_user = nullptr;
+  // exchange sequence (XTag): every exchange's block carries (site, seq, batch, rank); all ranks check all tags
+  std::atomic<uint64_t> xseq{0};    // exchanges so far
+  std::atomic<uint64_t> xbatch{0};  // batch passes launched so far (launch_batch)
+  int32_t* d_xerr = nullptr;        // merge_levels_kernel's verdict on the level blocks' tags
+  uint8_t* d_xsmall = nullptr;      // small exchanges (row stats, selection): [own block | R blocks] of XSMALL bytes
+  uint8_t* h_xsmall = nullptr;      // their R blocks read back
+  int64_t dbg_xskew_rank = -1;      // GS_DEBUG_XCHG_SKEW=rank:batch (tests): that rank skips one sequence number there
+  uint64_t dbg_xskew_batch = 0;
+  // GS_WATCHDOG_S=<seconds> (diagnostics): a thread reports on stderr any host wait of the scheduling path that lasts
+  // longer, naming the wait (Where markers), the batch pass and the exchange count
+  std::atomic<const char*> where{nullptr};
+  std::atomic<int64_t> where_t{0};
+  std::thread watchdog;
+  std::atomic<bool> wd_stop{false};
   gs_stats stats{};
   uint64_t* d_stamps = nullptr;   // GS_COMMIT_STAMPS=1: commit-kernel phase cycle sums
   uint64_t stats_all_pods = 0;     // pods placed by gs_schedule over the context's life (stamp averages)
@@ -198,6 +213,7 @@ struct gs_ctx {
   MirrorView slab_mv{nullptr, nullptr, 0};   // the eval pass's dense copy of the NUMA-policy rows (gather_numa_kernel)
   uint32_t slab_cap = 0;
   bool numa_idx_stale = true;
+  int64_t prep_now = INT64_MIN;             // `now` of the last full node_prep pass
   // registered topologies in bit-plane form (the commit kernel's cpuset Reserve), and the host re-check of
   // every device-chosen cpuset (GS_VERIFY_CPUSET=1)
   TopoDev* d_topos = nullptr;
@@ -237,6 +253,52 @@ struct gs_ctx {
 };
 
 int quiesce(gs_ctx* c);   // the async submissions' worker is idle (gs_schedule_submit)
+
+namespace {
+int64_t mono_ns() {
+  return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+// marks a host wait of the scheduling path (the watchdog names it when it lasts)
+struct Where {
+  gs_ctx* c;
+  const char* prev;
+  int64_t prev_t;
+  Where(gs_ctx* cc, const char* site) : c(cc), prev(cc->where.load()), prev_t(cc->where_t.load()) {
+    c->where_t.store(mono_ns());
+    c->where.store(site);
+  }
+  ~Where() {
+    c->where.store(prev);
+    c->where_t.store(prev_t);
+  }
+};
+void watchdog_loop(gs_ctx* c, double limit_s) {
+  (void)hipSetDevice(c->cfg.device);
+  const char* reported = nullptr;
+  int64_t reported_t = 0;
+  while (!c->wd_stop.load()) {
+    std::this_thread::sleep_for(std::chrono::milliseconds(250));
+    const char* w = c->where.load();
+    const int64_t t = c->where_t.load();
+    if (!w || (w == reported && t == reported_t)) continue;
+    const double s = (mono_ns() - t) * 1e-9;
+    if (s < limit_s) continue;
+    // which device work is still pending: the streams, and per batch slot its eval-pass end (evdone), commit end
+    // (ev[4]) and readback end (ev[5]) (0 = complete, 1 = pending)
+    auto q = [](hipError_t e) { return e == hipSuccess ? 0 : e == hipErrorNotReady ? 1 : 9; };
+    fprintf(stderr, "gpuscore watchdog: rank %d of %d blocked %.1f s in %s (batch pass %llu, exchange %llu); pending: "
+            "st %d st_ev %d st2 %d st_rb %d | slot 0 evdone %d ev4 %d ev5 %d | slot 1 evdone %d ev4 %d ev5 %d (bound %d)\n",
+            c->rank, c->nranks, s, w, (unsigned long long)c->xbatch, (unsigned long long)c->xseq, q(hipStreamQuery(c->st)),
+            q(hipStreamQuery(c->st_ev)), q(hipStreamQuery(c->st2)), q(hipStreamQuery(c->st_rb)),
+            q(hipEventQuery(c->slot[0].ev_evdone)), q(hipEventQuery(c->slot[0].ev[4])), q(hipEventQuery(c->slot[0].ev[5])),
+            q(hipEventQuery(c->slot[1].ev_evdone)), q(hipEventQuery(c->slot[1].ev[4])), q(hipEventQuery(c->slot[1].ev[5])),
+            c->cur_slot);
+    fflush(stderr);
+    reported = w;
+    reported_t = t;
+  }
+}
+}  // namespace
 void async_stop(gs_ctx* c);
 
 namespace {
@@ -651,6 +713,7 @@ int flush_rows(gs_ctx* c) {
   while (done < c->dirty_list.size()) {
     uint32_t n = (uint32_t)std::min<size_t>(c->stage_cap, c->dirty_list.size() - done);
     // staging buffers are reused: the previous scatter must have consumed them
+    Where w_(c, "flush_rows: previous scatter");
     HIP_TRY(c, hipStreamSynchronize(c->st));
     // one staged block, one copy: the n rows, then their node indices
     uint32_t* h_idx = reinterpret_cast<uint32_t*>(c->h_stage_rows + (size_t)n * ROW_WORDS);
@@ -665,13 +728,20 @@ int flush_rows(gs_ctx* c) {
                               c->st));
     const uint32_t* d_idx = reinterpret_cast<const uint32_t*>(c->d_stage_rows + (size_t)n * ROW_WORDS);
     HIP_TRY(c, launch_scatter_rows(c->mv, d_idx, c->d_stage_rows, n, c->st));
+    // the rows' LoadAware verdicts at `now` (node_prep), unless a full pass is due anyway
+    if (!c->prep_stale && c->prep_now == c->now) {
+      const gs_loadaware_args& la = c->cfg.loadaware;
+      HIP_TRY(c, launch_node_prep_idx(c->mv, d_idx, n, c->now, la.filter_expired_node_metrics, la.has_node_metric_expiration,
+                                      la.has_node_metric_expiration ? la.node_metric_expiration_seconds * 1000000000LL : 0,
+                                      c->st));
+    }
 
     c->stats.delta_rows += n;
     c->stats.delta_bytes += (uint64_t)n * (4 + ROW_WORDS * 8);
     done += n;
   }
   c->dirty_list.clear();
-  c->prep_stale = true;
+  if (c->prep_now != c->now) c->prep_stale = true;
   return GS_OK;
 }
 
@@ -681,6 +751,7 @@ int node_prep(gs_ctx* c) {
   HIP_TRY(c, launch_node_prep(c->mv, 0, c->N, c->now, a.filter_expired_node_metrics, a.has_node_metric_expiration,
                               exp_ns, c->st));
   c->prep_stale = false;
+  c->prep_now = c->now;
   return GS_OK;
 }
 
@@ -713,9 +784,40 @@ void flush_exchange_times(gs_ctx* c) {
   c->x_pending = keep;
 }
 
-int exchange(gs_ctx* c, const void* d_send, void* d_recv, size_t bytes) {
+constexpr size_t XSMALL = 64;   // small exchange block: payload <= 32 B, XTag at 32
+
+const char* xsite_name(uint32_t s) {
+  return s == XSITE_LEVELS ? "levels" : s == XSITE_ROWSTAT ? "row stats" : s == XSITE_SELECT ? "selection" : "?";
+}
+
+// The R received blocks' tags against the tag this rank sent: every rank checks all of them, so a divergence fails
+// on every rank at the same exchange.
+int check_tags(gs_ctx* c, const uint8_t* blocks, size_t bytes, const XTag& mine) {
+  for (int r = 0; r < c->nranks; ++r) {
+    XTag t;
+    std::memcpy(&t, blocks + (size_t)r * bytes + bytes - sizeof(XTag), sizeof t);
+    if (t.magic != XTAG_MAGIC || t.site != mine.site || t.seq != mine.seq || t.batch != mine.batch || t.rank != r ||
+        t.bytes != mine.bytes)
+      return fail(c, GS_ECOMM,
+                  "exchange sequence diverged: rank %d is at exchange %llu (%s, batch %llu), rank %d sent exchange %llu "
+                  "(%s, batch %llu, %u bytes, magic %#x)",
+                  c->rank, (unsigned long long)mine.seq, xsite_name(mine.site), (unsigned long long)mine.batch, r,
+                  (unsigned long long)t.seq, xsite_name(t.site), (unsigned long long)t.batch, t.bytes, t.magic);
+  }
+  return GS_OK;
+}
+
+// One all-gather of `bytes`-byte blocks (each ending in an XTag, filled here) from d_send into R blocks at d_recv.
+// RCCL: stream-ordered, the tag written on the stream before the collective; the receiver checks the tags (the level
+// blocks on the device in merge_levels_kernel, the small ones on the host). Callback: host-synchronous, checked here.
+int exchange(gs_ctx* c, uint32_t site, uint8_t* d_send, uint8_t* d_recv, size_t bytes, XTag* sent = nullptr) {
   auto t0 = std::chrono::steady_clock::now();
+  if (bytes < sizeof(XTag) || bytes % 8) return fail(c, GS_EINVAL, "exchange block of %zu bytes", bytes);
+  XTag tag{XTAG_MAGIC, site, ++c->xseq, c->xbatch, c->rank, (uint32_t)bytes};
+  if (c->rank == c->dbg_xskew_rank && c->xbatch == c->dbg_xskew_batch && site == XSITE_LEVELS) tag.seq = ++c->xseq;
+  if (sent) *sent = tag;
   if (c->comm) {
+    HIP_TRY(c, launch_write_tag(d_send + bytes - sizeof(XTag), tag, c->st));
     if (c->x_pending * 2 + 2 > (int)c->x_ev.size()) {
       for (int k = 0; k < 2; ++k) {
         hipEvent_t ev;
@@ -731,15 +833,36 @@ int exchange(gs_ctx* c, const void* d_send, void* d_recv, size_t bytes) {
     return GS_OK;
   } else if (c->cb) {
     if (bytes > c->xchg_bytes) return fail(c, GS_EINVAL, "exchange payload too large");
-    HIP_TRY(c, hipMemcpyAsync(c->h_xchg_send, d_send, bytes, hipMemcpyDeviceToHost, c->st));
+    Where w_(c, site == XSITE_LEVELS ? "exchange (levels): stream before the callback"
+                                     : "exchange (small): stream before the callback");
+    HIP_TRY(c, hipMemcpyAsync(c->h_xchg_send, d_send, bytes - sizeof(XTag), hipMemcpyDeviceToHost, c->st));
     HIP_TRY(c, hipStreamSynchronize(c->st));
+    c->where.store("exchange: allgather callback");
+    std::memcpy(c->h_xchg_send + bytes - sizeof(XTag), &tag, sizeof tag);
     if (c->cb(c->cb_user, c->h_xchg_send, c->h_xchg_recv, bytes) != 0) return fail(c, GS_ECOMM, "allgather callback failed");
+    if (int rc = check_tags(c, c->h_xchg_recv, bytes, tag)) return rc;
     HIP_TRY(c, hipMemcpyAsync(d_recv, c->h_xchg_recv, bytes * c->nranks, hipMemcpyHostToDevice, c->st));
   } else {
     return fail(c, GS_ESTATE, "multi-rank context without a communicator");
   }
   c->stats.exchange_ms +=
       std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  return GS_OK;
+}
+
+// A small exchange (payload <= 32 B at d_payload, device) and its R payloads read back to host_out (R x payload bytes).
+int exchange_small(gs_ctx* c, uint32_t site, const void* d_payload, size_t payload, void* host_out) {
+  static_assert(XSMALL >= 32 + sizeof(XTag), "small exchange block");
+  if (payload > XSMALL - sizeof(XTag)) return fail(c, GS_EINVAL, "small exchange payload too large");
+  HIP_TRY(c, hipMemcpyAsync(c->d_xsmall, d_payload, payload, hipMemcpyDeviceToDevice, c->st));
+  XTag tag{};
+  if (int rc = exchange(c, site, c->d_xsmall, c->d_xsmall + XSMALL, XSMALL, &tag)) return rc;
+  HIP_TRY(c, hipMemcpyAsync(c->h_xsmall, c->d_xsmall + XSMALL, XSMALL * c->nranks, hipMemcpyDeviceToHost, c->st));
+  Where w_(c, "exchange_small: read back");
+  HIP_TRY(c, hipStreamSynchronize(c->st));
+  if (int rc = check_tags(c, c->h_xsmall, XSMALL, tag)) return rc;
+  for (int r = 0; r < c->nranks; ++r)
+    std::memcpy(static_cast<uint8_t*>(host_out) + (size_t)r * payload, c->h_xsmall + (size_t)r * XSMALL, payload);
   return GS_OK;
 }
 
@@ -884,10 +1007,11 @@ void set_shard(gs_ctx* c) {
   c->stats.shard_end = c->n1;
 }
 
-// one rank's exchange block: [B x lstride listed node ids | B LevelHdr | B LevelExt], padded to 256 B
+// one rank's exchange block: [B x lstride listed node ids | B LevelHdr | B LevelExt | ... | XTag], padded to 256 B (the
+// tag in the block's last 32 bytes)
 size_t lists_bytes(int B, int lstride) { return (size_t)B * lstride * 4; }
 size_t xchg_block_bytes(int B, int lstride) {
-  size_t raw = lists_bytes(B, lstride) + (size_t)B * (sizeof(LevelHdr) + sizeof(LevelExt));
+  size_t raw = lists_bytes(B, lstride) + (size_t)B * (sizeof(LevelHdr) + sizeof(LevelExt)) + sizeof(XTag);
   return (raw + 255) / 256 * 256;
 }
 
@@ -902,6 +1026,15 @@ int alloc_exchange(gs_ctx* c) {
   HIP_TRY(c, hipHostMalloc(&c->h_xchg_recv, c->xchg_bytes * c->nranks + 64, hipHostMallocDefault));
   if (c->d_xmerged) { (void)hipFree(c->d_xmerged); c->d_xmerged = nullptr; }
   HIP_TRY(c, hipMalloc(&c->d_xmerged, xchg_block_bytes(c->B, LCAP) + 64));
+  if (!c->d_xerr) HIP_TRY(c, hipMalloc(&c->d_xerr, 16));
+  HIP_TRY(c, hipMemset(c->d_xerr, 0, 16));
+  if (!c->d_xsmall) HIP_TRY(c, hipMalloc(&c->d_xsmall, XSMALL * (1 + MAX_RANKS)));
+  if (!c->h_xsmall) HIP_TRY(c, hipHostMalloc(&c->h_xsmall, XSMALL * MAX_RANKS, hipHostMallocDefault));
+  if (const char* sk = getenv("GS_DEBUG_XCHG_SKEW")) {   // "rank:batch" (tests of the sequence check)
+    long r = -1;
+    unsigned long long b = 0;
+    if (sscanf(sk, "%ld:%llu", &r, &b) == 2) { c->dbg_xskew_rank = r; c->dbg_xskew_batch = b; }
+  }
   return GS_OK;
 }
 
@@ -917,6 +1050,7 @@ void bind_slot(gs_ctx* c, int s) {
 }
 
 constexpr int GS_REDO = 1;   // internal: re-run the batch (its score rows were overwritten by a speculative pass)
+constexpr size_t COMMITTED_BYTES = 32;   // committed[0..7] (the commit kernels write [0..4]); the placements follow
 
 // The candidate levels of a one-shard pass without node sampling are built on st_ev right after the eval pass (beside
 // the previous batch's commit, on the stale rows it lands on), then fixed up on st once that commit is done
@@ -960,8 +1094,11 @@ CommitArgs commit_args(gs_ctx* c, int b) {
   static const uint32_t prio = getenv("GS_SPEC_PRIO") ? (uint32_t)strtoul(getenv("GS_SPEC_PRIO"), nullptr, 0) & 0x3f0u : 0u;
   // GS_SPEC_LAG (experiments): decisions ahead of the verifier, 1..12 (bits 12-15; 0: the kernel's SP_LAG)
   static const uint32_t lag = getenv("GS_SPEC_LAG") ? (uint32_t)std::min(12L, std::max(0L, atol(getenv("GS_SPEC_LAG")))) : 0u;
-  a.dbg = (nospec ? 1u : 0u) | prio | lag << 12;
+  // GS_SPEC_SOLOAD=1 (experiments): the selector loads fresh rows' batch-start scores itself (bit 16)
+  static const bool soload = getenv("GS_SPEC_SOLOAD") && getenv("GS_SPEC_SOLOAD")[0] == '1';
+  a.dbg = (nospec ? 1u : 0u) | prio | lag << 12 | (soload ? 1u << 16 : 0u);
   a.tb = c->d_tb;
+  a.xerr = c->nranks > 1 ? c->d_xerr : nullptr;
   return a;
 }
 
@@ -1045,14 +1182,15 @@ int launch_batch(gs_ctx* c, int b, const int32_t* prev, const PlacementDev* prev
   // no timing markers between the levels and the commit kernel (each one held the commit's dispatch ~13 us): the
   // commit's duration comes from the kernel itself (committed[4]), the levels' interval is the rest up to ev[4]
   if (c->nranks > 1) {
-    int rc = exchange(c, c->d_xchg_send, c->d_xchg_recv, c->xchg_bytes);
+    int rc = exchange(c, XSITE_LEVELS, c->d_xchg_send, c->d_xchg_recv, c->xchg_bytes);
     if (rc) return rc;
-    if (commit_spec_selected(c->window_k))
-      HIP_TRY(c, launch_merge_levels(c->d_xchg_recv, c->xchg_bytes, c->nranks, b, c->B, c->lstride, c->d_xmerged,
-                                     c->st));
+    if (!commit_spec_selected(c->window_k)) return fail(c, GS_EUNSUPPORTED, "several ranks need the speculative commit");
+    HIP_TRY(c, launch_merge_levels(c->d_xchg_recv, c->xchg_bytes, c->nranks, b, c->B, c->lstride, c->d_xmerged,
+                                   c->d_xerr, c->st));
   }
   CommitArgs a = commit_args(c, b);
   a.prev = prev;
+  ++c->xbatch;
   HIP_TRY(c, launch_commit(a, c->st));
   HIP_TRY(c, hipEventRecord(c->ev[4], c->st));
   // full batches: readback on its own stream, so that the speculative next batch's patch / cand start right after the
@@ -1060,8 +1198,15 @@ int launch_batch(gs_ctx* c, int b, const int32_t* prev, const PlacementDev* prev
   // waits on each one) keep it in order on st: the extra queue hop costs more than it hides there.
   hipStream_t rb = b >= 32 ? c->st_rb : c->st;
   if (rb != c->st) HIP_TRY(c, hipStreamWaitEvent(rb, c->ev[4], 0));
-  HIP_TRY(c, hipMemcpyAsync(c->h_committed, c->d_committed, 32, hipMemcpyDeviceToHost, rb));
-  HIP_TRY(c, hipMemcpyAsync(c->h_out, c->d_out, sizeof(PlacementDev) * b, hipMemcpyDeviceToHost, rb));
+  // (GS_MERGE_RB=0, experiments: the committed words and the placements as two copies)
+  static const bool merge_rb = !(getenv("GS_MERGE_RB") && getenv("GS_MERGE_RB")[0] == '0');
+  if (merge_rb) {
+    HIP_TRY(c, hipMemcpyAsync(c->h_committed, c->d_committed, COMMITTED_BYTES + sizeof(PlacementDev) * b,
+                              hipMemcpyDeviceToHost, rb));
+  } else {
+    HIP_TRY(c, hipMemcpyAsync(c->h_committed, c->d_committed, COMMITTED_BYTES, hipMemcpyDeviceToHost, rb));
+    HIP_TRY(c, hipMemcpyAsync(c->h_out, c->d_out, sizeof(PlacementDev) * b, hipMemcpyDeviceToHost, rb));
+  }
   HIP_TRY(c, hipEventRecord(c->ev[5], rb));
   return GS_OK;
 }
@@ -1070,7 +1215,10 @@ int launch_batch(gs_ctx* c, int b, const int32_t* prev, const PlacementDev* prev
 // (several shards). clobbered: a speculative pass has overwritten the score rows and lists since -> GS_REDO.
 int finish_batch(gs_ctx* c, int b, bool clobbered, int* committed_out) {
   uint32_t len = c->n1 - c->n0;
-  HIP_TRY(c, hipEventSynchronize(c->ev[5]));
+  {
+    Where w_(c, "finish_batch: the batch's readback event");
+    HIP_TRY(c, hipEventSynchronize(c->ev[5]));
+  }
   flush_exchange_times(c);
   c->stats.eval_ms += ev_ms(c->ev[0], c->ev[1]);
   {   // commit kernel: its own duration (s_memrealtime, 100 MHz) in committed[4]; levels: the rest from the eval's end
@@ -1083,6 +1231,15 @@ int finish_batch(gs_ctx* c, int b, bool clobbered, int* committed_out) {
   c->stats.batches += 1;
   int committed = c->h_committed[0];
   if (committed < 0) return fail(c, GS_ESTATE, "commit pass of a batch was voided unexpectedly");
+  if (c->h_committed[3] == COMMIT_ERR_XTAG) {   // the level exchange paired different exchanges of the ranks
+    std::vector<uint8_t> blk((size_t)c->xchg_bytes * c->nranks);
+    HIP_TRY(c, hipStreamSynchronize(c->st));
+    HIP_TRY(c, hipMemcpy(blk.data(), c->d_xchg_recv, blk.size(), hipMemcpyDeviceToHost));
+    XTag mine;
+    std::memcpy(&mine, blk.data() + (size_t)c->rank * c->xchg_bytes + c->xchg_bytes - sizeof(XTag), sizeof mine);
+    if (int rc = check_tags(c, blk.data(), c->xchg_bytes, mine)) return rc;
+    return fail(c, GS_ECOMM, "exchange sequence diverged at a level exchange (device check)");
+  }
   if (c->h_committed[3])
     return fail(c, GS_EDEVICE, "commit kernel: a pipeline wait expired (internal error, site %d)", c->h_committed[3]);
   if (c->window_k) {
@@ -1097,9 +1254,8 @@ int finish_batch(gs_ctx* c, int b, bool clobbered, int* committed_out) {
     HIP_TRY(c, launch_row_stats(c->d_S, len, c->d_rowstat, c->st));
     std::vector<RowStat> rs(c->nranks);
     if (c->nranks > 1) {
-      int rc = exchange(c, c->d_rowstat, c->d_rowstat + 1, sizeof(RowStat));
+      int rc = exchange_small(c, XSITE_ROWSTAT, c->d_rowstat, sizeof(RowStat), rs.data());
       if (rc) return rc;
-      HIP_TRY(c, hipMemcpyAsync(rs.data(), c->d_rowstat + 1, sizeof(RowStat) * c->nranks, hipMemcpyDeviceToHost, c->st));
     } else {
       HIP_TRY(c, hipMemcpyAsync(rs.data(), c->d_rowstat, sizeof(RowStat), hipMemcpyDeviceToHost, c->st));
     }
@@ -1131,11 +1287,9 @@ int finish_batch(gs_ctx* c, int b, bool clobbered, int* committed_out) {
       HIP_TRY(c, hipMemsetAsync(c->d_sel, 0xff, 4, c->st));
     }
     if (c->nranks > 1) {
-      int rc = exchange(c, c->d_sel, c->d_sel + 1, 4);
-      if (rc) return rc;
       std::vector<int32_t> w(c->nranks);
-      HIP_TRY(c, hipMemcpyAsync(w.data(), c->d_sel + 1, 4 * c->nranks, hipMemcpyDeviceToHost, c->st));
-      HIP_TRY(c, hipStreamSynchronize(c->st));
+      int rc = exchange_small(c, XSITE_SELECT, c->d_sel, 4, w.data());
+      if (rc) return rc;
       winner = w[owner];
     } else {
       HIP_TRY(c, hipMemcpyAsync(&winner, c->d_sel, 4, hipMemcpyDeviceToHost, c->st));
@@ -1149,7 +1303,7 @@ int finish_batch(gs_ctx* c, int b, bool clobbered, int* committed_out) {
     HIP_TRY(c, hipEventRecord(c->ev[3], c->st));
     HIP_TRY(c, launch_commit(a, c->st));
     HIP_TRY(c, hipEventRecord(c->ev[4], c->st));
-    HIP_TRY(c, hipMemcpyAsync(c->h_committed, c->d_committed, 32, hipMemcpyDeviceToHost, c->st));
+    HIP_TRY(c, hipMemcpyAsync(c->h_committed, c->d_committed, COMMITTED_BYTES, hipMemcpyDeviceToHost, c->st));
     HIP_TRY(c, hipStreamSynchronize(c->st));
     c->stats.commit_ms += ev_ms(c->ev[3], c->ev[4]);
     committed = c->h_committed[0];
@@ -1410,14 +1564,10 @@ int ext_schedule_one(gs_ctx* c, const gs_pod& pod, const gs_pod_ext& e, uint64_t
   if (!ds_on) { greq[0] = greq[1] = greq[2] = 0; gmask = 0; }
   std::vector<std::pair<uint32_t, uint64_t>> matched;
   if (rs_on) matched_of(c, e.reservation_owner, &matched);
-  if (gmask && !matched.empty())
-    return fail(c, GS_EUNSUPPORTED, "a pod that requests GPUs and matches reservations is not on the device path");
   for (int x = 0; x < GS_MAX_XRES; ++x)
     if (e.xres_requests[x] < 0 || !in_range(e.xres_requests[x]))
       return fail(c, GS_EUNSUPPORTED, "extended resource request outside [0, 2^53)");
   PodVec v = prep_pod(c, pod);
-  if (c->numa_on && (v.numa & PN_BIND))
-    return fail(c, GS_EUNSUPPORTED, "cpuset-bound Reservation / DeviceShare pods are not on the device path");
   if (rs_on && e.reservation_required && matched.empty()) {   // PreFilter: ErrReasonReservationAffinity
     c->stats.pods += 1;
     return GS_OK;
@@ -1437,9 +1587,6 @@ int ext_schedule_one(gs_ctx* c, const gs_pod& pod, const gs_pod_ext& e, uint64_t
     while (b < matched.size() && matched[b].first == node) ++b;
     if (b - a > (size_t)EXT_MAX_RES_PER_NODE)
       return fail(c, GS_EUNSUPPORTED, "more than %d matched reservations on node %u", EXT_MAX_RES_PER_NODE, node);
-    if (c->numa_on && c->numa[node].cfg.numa_topology_policy != GS_NUMA_POLICY_NONE)   // (no NUMA restore of a
-      return fail(c, GS_EUNSUPPORTED,                                                  // reservation's resources)
-                  "a matched reservation on node %u, which has a NUMA topology policy, is not on the device path", node);
     ExtRec rec{};
     rec.node = node;
     rec.nres = (int32_t)(b - a);
@@ -1455,6 +1602,15 @@ int ext_schedule_one(gs_ctx* c, const gs_pod& pod, const gs_pod_ext& e, uint64_t
     gs_node restored = podreq;
     for (size_t k = a; k < b; ++k) {
       const gs_reservation& r = c->rsv.at(matched[k].second);
+      if (c->numa_on && (v.numa & PN_BIND)) {
+        // NodeNUMAResource's reservation restore (nodenumaresource/reservation.go:76-113, plugin.go:488-549) hands a
+        // cpuset pod the reservation's remaining CPUs (preferredCPUs, reusableResources): not restated. It applies only
+        // when the reservation itself holds a cpuset allocation; without one the restore is empty
+        auto it = c->numa[node].pods.find(r.uid);
+        if (it != c->numa[node].pods.end() && !it->second.cpus.empty())
+          return fail(c, GS_EUNSUPPORTED, "a cpuset pod matching reservation %llu, which holds a cpuset on node %u, is "
+                      "not on the device path", (unsigned long long)r.uid, node);
+      }
       rsv_request_delta(r.allocatable, r.allocatable_mask, -1, restored.requested, restored.nonzero_requested);
       ExtRes x{};
       int64_t rem[GS_NUM_RES];
@@ -1546,13 +1702,15 @@ int ext_schedule_one(gs_ctx* c, const gs_pod& pod, const gs_pod_ext& e, uint64_t
   // (ext_nodes_kernel also resets the select accumulators; ext_matched runs for pods with matched reservations only)
   HIP_TRY(c, launch_ext_nodes(c->d_dev, c->d_S, c->n0, c->n1, c->d_xpod, c->d_xtot, c->d_xds, c->d_xrs, c->d_xT,
                               c->st));
-  if (nrec)
-    HIP_TRY(c, launch_ext_matched(c->mv, c->d_xpv, c->pf, prod_cols, c->d_dev, c->d_xpod, c->d_xrec, c->d_xres, nrec,
-                                  c->d_xtot, c->d_xrs, c->d_xnom, c->d_xT, c->n1 - c->n0, c->st));
   // GPU pods on NUMA-policy nodes: DeviceShare is the topology manager's second hint provider
   if (gmask && c->numa_on && c->numa_n)
     HIP_TRY(c, launch_ext_numa(c->mv, c->d_xpv, c->pf, prod_cols, c->d_dev, c->d_xpod, c->d_numa_idx, c->numa_n, c->n0,
                                c->d_xtot, c->d_xds, c->d_aff, c->d_xT, c->n1 - c->n0, c->st));
+  // the matched nodes last: their restored rows over the whole Filter chain (incl. the policy nodes' affinity)
+  if (nrec)
+    HIP_TRY(c, launch_ext_matched(c->mv, c->d_xpv, c->pf, prod_cols, c->d_dev, c->d_xpod, c->d_xrec, c->d_xres, nrec,
+                                  c->d_xtot, c->d_xds, c->d_xrs, c->d_xnom, c->d_aff, c->n0, c->d_xT, c->n1 - c->n0,
+                                  c->st));
   HIP_TRY(c, launch_ext_select(c->d_xtot, c->d_xds, c->d_xrs, c->d_xrec, c->n0, c->n1, c->d_xpod, c->cfg.seed, c->d_xT,
                                c->d_xout, c->st));
   // outputs: the NodeNUMAResource Reserve of the selected node along its affinity, and the result and nominations
@@ -1594,7 +1752,15 @@ int ext_schedule_one(gs_ctx* c, const gs_pod& pod, const gs_pod_ext& e, uint64_t
     if ((rc = numa_reserve(c, pod, v, pd))) return rc;
     out->flags = xo.nflags & ~PL_INTERNAL_FLAGS;
   }
-  if (gmask && (rc = ext_device_reserve(c, node, greq, gmask, eo, xo.aff))) return rc;
+  if (gmask && (rc = ext_device_reserve(c, node, greq, gmask, eo, xo.aff))) {
+    // the reference runs every plugin's Unreserve on a Reserve failure: NodeNUMAResource's allocation goes again
+    if (c->numa_on && c->numa_uid_node.count(pod.uid)) {
+      numa_release(c->numa[node], pod.uid);
+      c->numa_uid_node.erase(pod.uid);
+      mark_dirty(c, node);
+    }
+    return rc;
+  }
   int rec_i = -1;   // the chosen node's matched record (records are in node order)
   {
     auto it = std::lower_bound(c->xrec.begin(), c->xrec.end(), node,
@@ -1782,15 +1948,17 @@ int gs_create(const gs_config* cfg, gs_ctx** out) {
   c->mv.i32 = c->d_i32;
   c->mv.npad = (uint32_t)np;
   c->ld = c->npad;
-  if ((e = hipMalloc(&c->d_pods, sizeof(PodVec) * c->B)) != hipSuccess) return bail("hipMalloc", e);
-  if ((e = hipMalloc(&c->d_seq, 8 * c->B)) != hipSuccess) return bail("hipMalloc", e);
+  // pods | seq and committed | out share one allocation each: one copy per batch each way
+  static_assert(sizeof(PodVec) % 8 == 0 && sizeof(PlacementDev) % 8 == 0, "staging layout");
+  if ((e = hipMalloc(&c->d_pods, (sizeof(PodVec) + 8) * c->B)) != hipSuccess) return bail("hipMalloc", e);
+  c->d_seq = reinterpret_cast<uint64_t*>(c->d_pods + c->B);
   if ((e = hipMalloc(&c->d_S, (size_t)c->B * c->ld * 2)) != hipSuccess) return bail("hipMalloc S", e);
   if ((e = hipMalloc(&c->d_aff, (size_t)c->B * c->ld)) != hipSuccess) return bail("hipMalloc aff", e);
   size_t xb = xchg_block_bytes(c->B, LCAP);
   if ((e = hipMalloc(&c->d_xchg_send, xb)) != hipSuccess) return bail("hipMalloc", e);
   c->xchg_bytes = xb;
-  if ((e = hipMalloc(&c->d_out, sizeof(PlacementDev) * c->B)) != hipSuccess) return bail("hipMalloc", e);
-  if ((e = hipMalloc(&c->d_committed, 32)) != hipSuccess) return bail("hipMalloc", e);
+  if ((e = hipMalloc(&c->d_committed, COMMITTED_BYTES + sizeof(PlacementDev) * c->B)) != hipSuccess) return bail("hipMalloc", e);
+  c->d_out = reinterpret_cast<PlacementDev*>(c->d_committed + COMMITTED_BYTES / 4);
   if ((e = hipMalloc(&c->d_tb, sizeof(int32_t) * TB_N * c->B)) != hipSuccess) return bail("hipMalloc", e);
   if ((e = hipMalloc(&c->d_rowstat, sizeof(RowStat) * (1 + MAX_RANKS))) != hipSuccess) return bail("hipMalloc", e);
   if ((e = hipMalloc(&c->d_sel, 4 * (1 + MAX_RANKS))) != hipSuccess) return bail("hipMalloc", e);
@@ -1799,10 +1967,12 @@ int gs_create(const gs_config* cfg, gs_ctx** out) {
   if ((e = hipMalloc(&c->d_stage_rows, (size_t)(8 * ROW_WORDS + 4) * c->stage_cap)) != hipSuccess) return bail("hipMalloc", e);
   if ((e = hipHostMalloc(&c->h_stage_rows, (size_t)(8 * ROW_WORDS + 4) * c->stage_cap, hipHostMallocDefault)) != hipSuccess)
     return bail("hipHostMalloc", e);
-  if ((e = hipHostMalloc(&c->h_pods, sizeof(PodVec) * c->B, hipHostMallocDefault)) != hipSuccess) return bail("hipHostMalloc", e);
-  if ((e = hipHostMalloc(&c->h_seq, 8 * c->B, hipHostMallocDefault)) != hipSuccess) return bail("hipHostMalloc", e);
-  if ((e = hipHostMalloc(&c->h_out, sizeof(PlacementDev) * c->B, hipHostMallocDefault)) != hipSuccess) return bail("hipHostMalloc", e);
-  if ((e = hipHostMalloc(&c->h_committed, 32, hipHostMallocDefault)) != hipSuccess) return bail("hipHostMalloc", e);
+  if ((e = hipHostMalloc(&c->h_pods, (sizeof(PodVec) + 8) * c->B, hipHostMallocDefault)) != hipSuccess)
+    return bail("hipHostMalloc", e);
+  c->h_seq = reinterpret_cast<uint64_t*>(c->h_pods + c->B);
+  if ((e = hipHostMalloc(&c->h_committed, COMMITTED_BYTES + sizeof(PlacementDev) * c->B, hipHostMallocDefault)) != hipSuccess)
+    return bail("hipHostMalloc", e);
+  c->h_out = reinterpret_cast<PlacementDev*>(c->h_committed + COMMITTED_BYTES / 4);
   if ((e = hipHostMalloc(&c->h_xchg_send, xb, hipHostMallocDefault)) != hipSuccess) return bail("hipHostMalloc", e);
   (void)hipMemset(c->d_S, 0xff, (size_t)c->B * c->ld * 2);
   {
@@ -1819,14 +1989,16 @@ int gs_create(const gs_config* cfg, gs_ctx** out) {
     if ((e = hipMalloc(&s1.d_S, (size_t)c->B * c->ld * 2)) != hipSuccess) return bail("hipMalloc S", e);
     if ((e = hipMalloc(&s1.d_aff, (size_t)c->B * c->ld)) != hipSuccess) return bail("hipMalloc aff", e);
     (void)hipMemset(s1.d_S, 0xff, (size_t)c->B * c->ld * 2);
-    if ((e = hipMalloc(&s1.d_pods, sizeof(PodVec) * c->B)) != hipSuccess) return bail("hipMalloc", e);
-    if ((e = hipMalloc(&s1.d_seq, 8 * c->B)) != hipSuccess) return bail("hipMalloc", e);
-    if ((e = hipMalloc(&s1.d_out, sizeof(PlacementDev) * c->B)) != hipSuccess) return bail("hipMalloc", e);
-    if ((e = hipMalloc(&s1.d_committed, 32)) != hipSuccess) return bail("hipMalloc", e);
-    if ((e = hipHostMalloc(&s1.h_pods, sizeof(PodVec) * c->B, hipHostMallocDefault)) != hipSuccess) return bail("hipHostMalloc", e);
-    if ((e = hipHostMalloc(&s1.h_seq, 8 * c->B, hipHostMallocDefault)) != hipSuccess) return bail("hipHostMalloc", e);
-    if ((e = hipHostMalloc(&s1.h_out, sizeof(PlacementDev) * c->B, hipHostMallocDefault)) != hipSuccess) return bail("hipHostMalloc", e);
-    if ((e = hipHostMalloc(&s1.h_committed, 32, hipHostMallocDefault)) != hipSuccess) return bail("hipHostMalloc", e);
+    if ((e = hipMalloc(&s1.d_pods, (sizeof(PodVec) + 8) * c->B)) != hipSuccess) return bail("hipMalloc", e);
+    s1.d_seq = reinterpret_cast<uint64_t*>(s1.d_pods + c->B);
+    if ((e = hipMalloc(&s1.d_committed, COMMITTED_BYTES + sizeof(PlacementDev) * c->B)) != hipSuccess) return bail("hipMalloc", e);
+    s1.d_out = reinterpret_cast<PlacementDev*>(s1.d_committed + COMMITTED_BYTES / 4);
+    if ((e = hipHostMalloc(&s1.h_pods, (sizeof(PodVec) + 8) * c->B, hipHostMallocDefault)) != hipSuccess)
+      return bail("hipHostMalloc", e);
+    s1.h_seq = reinterpret_cast<uint64_t*>(s1.h_pods + c->B);
+    if ((e = hipHostMalloc(&s1.h_committed, COMMITTED_BYTES + sizeof(PlacementDev) * c->B, hipHostMallocDefault)) != hipSuccess)
+      return bail("hipHostMalloc", e);
+    s1.h_out = reinterpret_cast<PlacementDev*>(s1.h_committed + COMMITTED_BYTES / 4);
     for (auto& ev : s1.ev)
       if ((e = hipEventCreate(&ev)) != hipSuccess) return bail("hipEventCreate", e);
     c->cand_overlap = !(getenv("GS_CAND_OVERLAP") && getenv("GS_CAND_OVERLAP")[0] == '0');
@@ -1849,6 +2021,10 @@ int gs_create(const gs_config* cfg, gs_ctx** out) {
   if ((e = hipDeviceSynchronize()) != hipSuccess) return bail("hipDeviceSynchronize", e);
   // 96 B (LoadAware + Fit row), + 192 B NodeNUMAResource columns when enabled
   c->stats.node_row_bytes = 3 * 8 + 4 + 2 * 8 + 2 * 8 + 2 * 8 + 2 * 8 + 4 + (c->numa_on ? 18 * 8 + 12 * 4 : 0);
+  if (const char* wd = getenv("GS_WATCHDOG_S")) {
+    const double lim = atof(wd);
+    if (lim > 0) c->watchdog = std::thread(watchdog_loop, c, lim);
+  }
   *out = c;
   return GS_OK;
 }
@@ -1856,6 +2032,10 @@ int gs_create(const gs_config* cfg, gs_ctx** out) {
 int gs_destroy(gs_ctx* c) {
   if (!c) return GS_EINVAL;
   async_stop(c);
+  if (c->watchdog.joinable()) {
+    c->wd_stop.store(true);
+    c->watchdog.join();
+  }
   if (c->host_timing && c->ht_batches) {
     const double n = (double)c->ht_batches;
     fprintf(stderr, "gpuscore host per batch (us, %llu batches): waiting for the batch %.0f | applying placements %.0f | "
@@ -1957,21 +2137,22 @@ int gs_destroy(gs_ctx* c) {
     }
     c->d_lst = nullptr;
     c->d_hist = nullptr;
-    void* d1[] = {s1.d_pods, s1.d_seq, s1.d_out, s1.d_committed, s1.d_S, s1.d_aff};
+    void* d1[] = {s1.d_pods, s1.d_committed, s1.d_S, s1.d_aff};   // (seq / out live inside pods / committed)
     for (void* p : d1)
       if (p) (void)hipFree(p);
-    void* h1[] = {s1.h_pods, s1.h_seq, s1.h_out, s1.h_committed};
+    void* h1[] = {s1.h_pods, s1.h_committed};
     for (void* p : h1)
       if (p) (void)hipHostFree(p);
     for (auto& ev : s1.ev)
       if (ev) (void)hipEventDestroy(ev);
   }
-  void* dev[] = {c->d_i64, c->d_i32, c->d_pods, c->d_seq, c->d_S, c->d_xchg_send, c->d_xchg_recv, c->d_xmerged, c->d_out,
+  void* dev[] = {c->d_xerr, c->d_xsmall,
+                 c->d_i64, c->d_i32, c->d_pods, c->d_S, c->d_xchg_send, c->d_xchg_recv, c->d_xmerged,
                  c->d_committed, c->d_rowstat, c->d_sel, c->d_stage_idx, c->d_stage_rows, c->d_numa_idx,
                  c->d_topos, c->d_aff, c->d_tb};
   for (void* p : dev)
     if (p) (void)hipFree(p);
-  void* host[] = {c->h_pods, c->h_seq, c->h_out, c->h_committed, c->h_stage_idx, c->h_stage_rows, c->h_xchg_send,
+  void* host[] = {c->h_xsmall, c->h_pods, c->h_committed, c->h_stage_idx, c->h_stage_rows, c->h_xchg_send,
                   c->h_xchg_recv};
   for (void* p : host)
     if (p) (void)hipHostFree(p);
@@ -2062,6 +2243,7 @@ int gs_pods_unassign(gs_ctx* c, const uint32_t* node_idx, const gs_pod* pods, ui
     c->nodes[i].assigned.erase(pods[j].uid);
     auto it = c->uid_node.find(pods[j].uid);
     if (it != c->uid_node.end() && it->second == i) c->uid_node.erase(it);
+    c->ext_reserved.erase(pods[j].uid);   // the pod left: its extension-path Reserve record goes with it
     mark_dirty(c, i);
   }
   return flush_rows(c);
@@ -2195,8 +2377,15 @@ int stage_batch(gs_ctx* c, const gs_pod* pods, const uint64_t* seq, uint32_t i, 
     HIP_TRY(c, hipEventRecord(sl.ev_go, c->st));
     HIP_TRY(c, hipStreamWaitEvent(c->st_ev, sl.ev_go, 0));
   }
-  HIP_TRY(c, hipMemcpyAsync(c->d_pods, c->h_pods, sizeof(PodVec) * b, hipMemcpyHostToDevice, c->st_ev));
-  HIP_TRY(c, hipMemcpyAsync(c->d_seq, c->h_seq, 8 * b, hipMemcpyHostToDevice, c->st_ev));
+  // one copy: the B pod vectors' block (b of them staged) and the b sequence numbers after it (GS_MERGE_UP=0,
+  // experiments: two copies)
+  static const bool merge_up = !(getenv("GS_MERGE_UP") && getenv("GS_MERGE_UP")[0] == '0');
+  if (merge_up) {
+    HIP_TRY(c, hipMemcpyAsync(c->d_pods, c->h_pods, sizeof(PodVec) * c->B + 8 * b, hipMemcpyHostToDevice, c->st_ev));
+  } else {
+    HIP_TRY(c, hipMemcpyAsync(c->d_pods, c->h_pods, sizeof(PodVec) * b, hipMemcpyHostToDevice, c->st_ev));
+    HIP_TRY(c, hipMemcpyAsync(c->d_seq, c->h_seq, 8 * b, hipMemcpyHostToDevice, c->st_ev));
+  }
   return GS_OK;
 }
 
@@ -2236,6 +2425,7 @@ int schedule_stream(gs_ctx* c, PodRun run, Next&& next_run, Done&& run_done) {
   PodRun nxt{};
   bool have_nxt = false;
   auto drain = [&]() {
+    Where w_(c, "schedule_stream: drain");
     (void)hipStreamSynchronize(c->st);
     (void)hipStreamSynchronize(c->st_ev);
     (void)hipStreamSynchronize(c->st_rb);   // a voided or in-flight batch's readback into the pinned buffers

@@ -102,11 +102,12 @@ hipError_t launch_ext_nodes(const DevNode* dev, const int16_t* S, uint32_t n0, u
                             int32_t* tot, int16_t* ds, int16_t* rs, int32_t* scratch, hipStream_t st);
 hipError_t launch_ext_matched(const MirrorView& m, const PodVec* pods, const Profile& pf, int prod_cols,
                               const DevNode* dev, const ExtPod* pod, const ExtRec* recs, const ExtRes* res, int nrec, int32_t* tot,
-                              int16_t* rs, int32_t* nominated, int32_t* scratch, uint32_t len, hipStream_t st);
+                              int16_t* ds, int16_t* rs, int32_t* nominated, uint8_t* aff, uint32_t n0, int32_t* scratch,
+                              uint32_t len, hipStream_t st);
 // GPU pods on the NUMA-topology-policy nodes (idx, absolute node indices): Filter + Score again with DeviceShare as the
 // topology manager's second hint provider, the affinity (aff, the eval pass layout) and DeviceShare Filter / raw Score
-// within it; overwrites tot / ds of those nodes (after launch_ext_matched, before launch_ext_select: its error word
-// lives in the select scratch, whose accumulators launch_ext_matched resets).
+// within it; overwrites tot / ds of those nodes (after launch_ext_nodes, before launch_ext_matched, which has the last
+// word on the matched nodes; its error word lives in the select scratch, whose accumulators launch_ext_nodes resets).
 hipError_t launch_ext_numa(const MirrorView& m, const PodVec* pods, const Profile& pf, int prod_cols, const DevNode* dev,
                            const ExtPod* pod, const uint32_t* idx, uint32_t nidx, uint32_t n0, int32_t* tot, int16_t* ds,
                            uint8_t* aff, int32_t* scratch, uint32_t len, hipStream_t st);

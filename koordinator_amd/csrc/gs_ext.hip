@@ -274,34 +274,58 @@ __global__ __launch_bounds__(64) void ext_finish_kernel(MirrorView m, const PodV
   __threadfence_system();
 }
 
-// one matched node (record k): the restored row re-evaluated, Reservation Filter, NominateReservation, raw Score
+// one matched node (record k): the restored row re-evaluated, Reservation Filter, NominateReservation, raw Score.
+// Runs after ext_nodes / ext_numa and has the last word on its node: the whole Filter chain over the restored NodeInfo
+// (Fit, LoadAware, NodeNUMAResource — with DeviceShare as the second hint provider for a GPU pod on a NUMA-policy
+// node — and DeviceShare's Filter / raw Score within the affinity; the reservations modelled hold no devices, so
+// DeviceShare's view of the node is not restored: deviceshare/reservation.go:133-162 keeps device-holding ones only),
+// and the Filter-time affinity of a policy node (the unrestored eval pass may have stopped before NodeNUMAResource).
 __device__ __forceinline__ void matched_one(const MirrorView& m, const PodVec* __restrict__ pods, const Profile& pf,
                                             int prod_cols, const DevNode* __restrict__ dev, const ExtPod& p,
                                             const ExtRec* __restrict__ recs,
-                                            const ExtRes* __restrict__ res, int k, int32_t* tot, int16_t* rs,
-                                            int32_t* nominated) {
+                                            const ExtRes* __restrict__ res, int k, int32_t* tot, int16_t* ds,
+                                            int16_t* rs, int32_t* nominated, uint8_t* aff, uint32_t n0, int32_t* acc) {
   const ExtRec& rc = recs[k];
   const uint32_t i = rc.node;
   // the restored NodeInfo of the pod (BeforePreFilter): the mirror row plus the matched restore deltas
   Row r;
-  load_row(m, i, prod_cols != 0, (pf.enabled & 0x30u) != 0, r);
+  const bool numa_on = (pf.enabled & 0x30u) != 0;
+  load_row(m, i, prod_cols != 0, numa_on, r);
   for (int s = 3; s < 7; ++s) r.free[s] = m.c64(C_FREE_CPU + s)[i];
   for (int s = 0; s < 7; ++s) r.free[s] += rc.dfree[s];
   r.nzfree[0] += rc.dnz[0];
   r.nzfree[1] += rc.dnz[1];
   r.free_pods += rc.dpods;
-  const PairOut o = eval_pair<false, true>(r, pods[0], pf, m);
+  const bool pol = numa_on && ((r.nr.nflags >> NF_POLICY_SHIFT) & 3u);
+  PairOut o;
+  if (pol && p.gpu_mask) {   // DeviceShare as the topology manager's second hint provider (as ext_numa_kernel)
+    bool bad = false, over = false;
+    const int nz = (r.nr.nflags >> NF_ZONES_SHIFT) & 7;
+    const uint32_t gh = gpu_hint_word(dev[i], p, nz, &bad);
+    o = eval_pair<false, true, true, false, false, true>(r, pods[0], pf, m, nullptr, gh, &over);
+    if (bad || over) atomicOr(&acc[ACC_ERR], (bad ? 1 : 0) | (over ? 2 : 0));
+  } else {
+    o = eval_pair<false, true>(r, pods[0], pf, m);
+  }
   int32_t t = total_score(o, pf);
-  if (t >= 0 && p.gpu_names && !fit_names_ok(dev[i], p)) t = -1;   // Fit's scalars are not restored by reservations
+  int32_t raw = 0;
+  if (t >= 0 && (p.gpu_mask || p.gpu_names)) {   // Fit's GPU-name scalars (not restored) and DeviceShare's Filter
+    bool ok;
+    eval_device(dev[i], p, &ok, &raw, pol ? o.aff : 0u);
+    if (!ok) t = -1;
+  }
+  if (pol) aff[i - n0] = (uint8_t)(o.code ? 0u : o.aff);
   // Reservation Filter: a required pod needs a satisfying matched reservation (filterWithReservations)
   if (t >= 0 && p.required) {
     bool any = false;
     for (int j = 0; j < rc.nres && !any; ++j) any = reservation_fits(p, rc, res[rc.first + j]);
     if (!any) t = -1;
   }
-  // NominateReservation
+  // NominateReservation (nominator.go:140-190). RunReservationFilterPlugins also runs DeviceShare's FilterReservation,
+  // which fails for a device pod on every reservation without device allocations (deviceshare/plugin.go:338-350): a
+  // GPU pod nominates none
   int nom = -1;
-  if (t >= 0) {
+  if (t >= 0 && !p.gpu_mask) {
     int64_t best_order = INT64_MAX;
     for (int j = 0; j < rc.nres; ++j) {
       const ExtRes& x = res[rc.first + j];
@@ -319,6 +343,7 @@ __device__ __forceinline__ void matched_one(const MirrorView& m, const PodVec* _
     }
   }
   tot[i] = t;
+  ds[i] = (int16_t)(t >= 0 ? raw : 0);
   rs[i] = (int16_t)((t >= 0 && nom >= 0) ? score_reservation(p, res[rc.first + nom]) : 0);
   nominated[k] = nom;
 }
@@ -330,14 +355,15 @@ __global__ __launch_bounds__(SEL_BLOCK) void ext_matched_kernel(MirrorView m, co
                                                                 const ExtPod* __restrict__ pp,
                                                                 const ExtRec* __restrict__ recs,
                                                                 const ExtRes* __restrict__ res, int nrec, int32_t* tot,
-                                                                int16_t* rs, int32_t* nominated, int32_t* acc) {
+                                                                int16_t* ds, int16_t* rs, int32_t* nominated,
+                                                                uint8_t* aff, uint32_t n0, int32_t* acc) {
   __shared__ int64_t so_sh[SEL_BLOCK];
   __shared__ int32_t node_sh[SEL_BLOCK];
   const ExtPod& p = *pp;
   int64_t so = INT64_MAX;
   int32_t pn = -1;
   for (int k = threadIdx.x; k < nrec; k += SEL_BLOCK) {
-    matched_one(m, pods, pf, prod_cols, dev, p, recs, res, k, tot, rs, nominated);
+    matched_one(m, pods, pf, prod_cols, dev, p, recs, res, k, tot, ds, rs, nominated, aff, n0, acc);
     const ExtRec& rc = recs[k];
     if (tot[rc.node] >= 0 && rc.order_min != INT64_MAX && rc.order_min != 0 &&
         (rc.order_min < so || (rc.order_min == so && (int32_t)rc.node < pn))) {
@@ -546,11 +572,12 @@ hipError_t launch_ext_nodes(const DevNode* dev, const int16_t* S, uint32_t n0, u
 
 hipError_t launch_ext_matched(const MirrorView& m, const PodVec* pods, const Profile& pf, int prod_cols,
                               const DevNode* dev, const ExtPod* pod, const ExtRec* recs, const ExtRes* res, int nrec, int32_t* tot,
-                              int16_t* rs, int32_t* nominated, int32_t* scratch, uint32_t len, hipStream_t st) {
+                              int16_t* ds, int16_t* rs, int32_t* nominated, uint8_t* aff, uint32_t n0, int32_t* scratch,
+                              uint32_t len, hipStream_t st) {
   // scratch: T[len] | acc[ACC_WORDS] | bcnt[blocks]; the accumulators were reset by ext_nodes_kernel
   int32_t* acc = scratch + len;
   hipLaunchKernelGGL(ext_matched_kernel, dim3(1), dim3(SEL_BLOCK), 0, st, m, pods, pf, prod_cols, dev, pod, recs, res, nrec,
-                     tot, rs, nominated, acc);
+                     tot, ds, rs, nominated, aff, n0, acc);
   return hipGetLastError();
 }
 

@@ -586,6 +586,9 @@ int gs_gang_pass_create(gs_gang_mgr* m, uint32_t n, const uint64_t* gang_ids, co
 }
 
 int gs_gang_pass_destroy(gs_gang_pass* p) {
+  // a pass aborted between gs_gang_walk and gs_gang_replay (the engine call failed): roll its speculative walk back,
+  // so the manager is left as before the walk (and no stray replay can restore a stale snapshot later)
+  if (p && p->m && p->m->snap_on) p->m->snap_restore();
   delete p;
   return GS_OK;
 }

@@ -110,6 +110,7 @@ struct CommitArgs {
   uint32_t nnodes;
   uint32_t dbg;              // diagnostics: bit 0 = the speculative commit waits for every pending row (no speculation)
   int32_t* tb;               // [npods x TB_N] selectHost tie-break records of each pod (speculative commit scratch)
+  const int32_t* xerr;       // several shards: nonzero = the all-gathered blocks' exchange tags disagree (merge_levels)
 };
 // tiebreak_position(seed, seq, T) as a lookup: entries 0..TB_N-2 are the positions the reservoir walk visits
 // (ascending, independent of T; INT32_MAX past the walk's end), entry TB_N-1 the largest T the entries decide
@@ -118,6 +119,9 @@ constexpr int TB_N = 32;
 hipError_t set_kernel_attributes();
 hipError_t launch_node_prep(const MirrorView& m, uint32_t n0, uint32_t n1, int64_t now, int32_t filter_expired,
                             int32_t has_exp, int64_t exp_ns, hipStream_t st);
+// the same for the rows idx[0..n) (after a delta update rewrote them)
+hipError_t launch_node_prep_idx(const MirrorView& m, const uint32_t* idx, uint32_t n, int64_t now, int32_t filter_expired,
+                                int32_t has_exp, int64_t exp_ns, hipStream_t st);
 // NodeNUMAResource profiles: numa_idx lists the shard's nodes with a NUMA topology policy (ascending)
 hipError_t launch_eval(const MirrorView& m, const PodVec* pods, int npods, const Profile& pf, uint32_t n0, uint32_t n1,
                        int16_t* S, uint32_t ld, int prod_cols, const uint32_t* numa_idx, uint32_t numa_n,
@@ -156,10 +160,30 @@ hipError_t launch_cand(int16_t* S, uint32_t ld, uint32_t len, uint32_t n0, int n
 // re-picked and each listed level rewritten as its stale nodes minus the landed rows plus the landed rows now at it
 hipError_t launch_fix_levels(int16_t* S, uint32_t ld, int npods, int max_score, int lcap, uint32_t* lists,
                              LevelHdr* hdrs, LevelExt* ext, const CandPatch& cp, hipStream_t st);
+// Every all-gathered block ends with the sender's exchange tag: which exchange of the context's sequence it is (a
+// count every rank advances identically), at which call site, for which batch. A rank whose sequence diverged from
+// the others' (a different number of collectives, or another call site) is detected by every rank on the first
+// exchange that pairs mismatched calls, which then fails on all of them (GS_ECOMM) instead of hanging one rank in a
+// collective the others never enter.
+struct XTag {
+  uint32_t magic;
+  uint32_t site;             // XSITE_*
+  uint64_t seq;              // exchanges on the context so far (this one included)
+  uint64_t batch;            // batch passes launched on the context so far
+  int32_t rank;
+  uint32_t bytes;            // the block's size (tag included)
+};
+static_assert(sizeof(XTag) == 32, "XTag layout");
+constexpr uint32_t XTAG_MAGIC = 0x31585347u;   // "GSX1"
+enum : uint32_t { XSITE_LEVELS = 1, XSITE_ROWSTAT = 2, XSITE_SELECT = 3 };
+constexpr int32_t COMMIT_ERR_XTAG = 90;   // committed[3]: the level exchange's tags disagree (nothing committed)
+// tag -> dst (RCCL: written on the stream right before the all-gather, so the tag travels with the block)
+hipError_t launch_write_tag(uint8_t* dst, const XTag& t, hipStream_t st);
 // several shards: per pod, the all-gathered rank blocks' levels merged into one block of the single-rank layout (the
-// speculative commit's input)
+// speculative commit's input). Block 0 also compares the R blocks' tags (at xblock - sizeof(XTag)): xerr[0] = 0 when
+// they name the same exchange, else 1 + the first rank that differs from rank 0 (the commit then commits nothing).
 hipError_t launch_merge_levels(const uint8_t* xin, size_t xblock, int nranks, int npods, int bmax, int lstride,
-                               uint8_t* xout, hipStream_t st);
+                               uint8_t* xout, int32_t* xerr, hipStream_t st);
 size_t commit_smem_bytes(int B);
 bool commit_spec_selected(uint32_t window_k);   // the speculative commit kernel runs (else pipelined / lockstep)
 hipError_t launch_commit(const CommitArgs& a, hipStream_t st);        // window_k > 0: lockstep kernel

@@ -28,10 +28,13 @@ namespace gs {
 
 // ------------------------------------------------------------------------------------------------
 // node-prep: LoadAware expiry (helper.go:36-41) evaluated at `now` for every node.
+// idx != nullptr: the n0..n1 entries of idx (rows a delta update just rewrote) instead of a node range
 __global__ void __launch_bounds__(256) node_prep_kernel(MirrorView m, uint32_t n0, uint32_t n1, int64_t now,
-                                                        int32_t filter_expired, int32_t has_exp, int64_t exp_ns) {
+                                                        int32_t filter_expired, int32_t has_exp, int64_t exp_ns,
+                                                        const uint32_t* __restrict__ idx) {
   uint32_t i = n0 + blockIdx.x * 256 + threadIdx.x;
   if (i >= n1) return;
+  if (idx) i = idx[i];
   uint32_t sf = (uint32_t)m.c32(C_SFLAGS)[i];
   bool exists = sf & SF_METRIC;
   bool expired = !exists || !(sf & SF_UPDATE_TIME) || (exp_ns > 0 && now - m.c64(C_UPDATE_TIME)[i] >= exp_ns);
@@ -715,7 +718,8 @@ __global__ void __launch_bounds__(FIX_THREADS) fix_levels_kernel(int16_t* __rest
 // ascending). The merged `next` is the highest score not kept (every shard's `next`, or the first dropped level).
 // Block k = pod k; thread e = (shard e / LEVALL, level e % LEVALL).
 __global__ void __launch_bounds__(256) merge_levels_kernel(const uint8_t* __restrict__ xin, size_t xblock, int R,
-                                                           int bmax, int lstride, uint8_t* __restrict__ xout) {
+                                                           int bmax, int lstride, uint8_t* __restrict__ xout,
+                                                           int32_t* __restrict__ xerr) {
   constexpr int NEMAX = MAX_RANKS * LEVALL;
   static_assert(NEMAX <= 256, "one thread per shard level");
   __shared__ int32_t e_score[NEMAX], e_count[NEMAX], e_rep[NEMAX];
@@ -723,6 +727,17 @@ __global__ void __launch_bounds__(256) merge_levels_kernel(const uint8_t* __rest
   __shared__ int32_t m_score[LEVALL], m_count[LEVALL];
   __shared__ int32_t s_nlev, s_drop;
   const int k = blockIdx.x, t = threadIdx.x, NE = R * LEVALL;
+  if (k == 0 && t == 0) {   // the blocks' exchange tags: every rank sent the same exchange of the sequence
+    const XTag* t0 = reinterpret_cast<const XTag*>(xin + xblock - sizeof(XTag));
+    int bad = 0;
+    for (int r = 0; r < R && !bad; ++r) {
+      const XTag* tr = reinterpret_cast<const XTag*>(xin + (size_t)r * xblock + xblock - sizeof(XTag));
+      if (tr->magic != XTAG_MAGIC || tr->site != t0->site || tr->seq != t0->seq || tr->batch != t0->batch ||
+          tr->rank != r || tr->bytes != (uint32_t)xblock)
+        bad = 1 + r;
+    }
+    xerr[0] = bad;
+  }
   // rank blocks: lists at lstride entries per pod; the merged block has the single-rank layout (LCAP per pod)
   const size_t ihoff = (size_t)bmax * lstride * 4, ixoff = ihoff + (size_t)bmax * sizeof(LevelHdr);
   const size_t hoff = (size_t)bmax * LCAP * 4, xoff = hoff + (size_t)bmax * sizeof(LevelHdr);
@@ -804,10 +819,22 @@ __global__ void __launch_bounds__(256) merge_levels_kernel(const uint8_t* __rest
 }
 
 hipError_t launch_merge_levels(const uint8_t* xin, size_t xblock, int nranks, int npods, int bmax, int lstride,
-                               uint8_t* xout, hipStream_t st) {
+                               uint8_t* xout, int32_t* xerr, hipStream_t st) {
   if (npods <= 0) return hipSuccess;
   if (nranks < 2 || nranks > MAX_RANKS || lstride > LCAP || nranks * lstride > LCAP) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(merge_levels_kernel, dim3(npods), dim3(256), 0, st, xin, xblock, nranks, bmax, lstride, xout);
+  if (xblock < sizeof(XTag) || xblock % 256) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(merge_levels_kernel, dim3(npods), dim3(256), 0, st, xin, xblock, nranks, bmax, lstride, xout,
+                     xerr);
+  return hipGetLastError();
+}
+
+__global__ void write_tag_kernel(uint8_t* __restrict__ dst, XTag t) {
+  if (threadIdx.x == 0) *reinterpret_cast<XTag*>(dst) = t;
+}
+
+hipError_t launch_write_tag(uint8_t* dst, const XTag& t, hipStream_t st) {
+  if (reinterpret_cast<uintptr_t>(dst) % 8) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(write_tag_kernel, dim3(1), dim3(64), 0, st, dst, t);
   return hipGetLastError();
 }
 
@@ -902,6 +929,7 @@ __global__ void __launch_bounds__(COMMIT_THREADS) commit_kernel(CommitArgs a) {
   __shared__ uint64_t s_cpuset[4];                     // CPUs of a device-side cpuset Reserve
   __shared__ HintTable s_ht, s_ht2;                    // NUMA hint sums of the winner row (new / batch-start state)
   const bool numa_on = (a.pf.enabled & 0x30u) != 0;
+  const uint64_t rt0 = __builtin_amdgcn_s_memrealtime();   // the kernel's duration -> committed[4] (100 MHz ticks)
   // speculative pass queued behind another batch: only if that one committed every pod with nothing left for
   // the host (committed[1] == 1); otherwise a no-op (committed = -1) the host discards
   if (a.prev && a.prev[1] != 1) {
@@ -1552,7 +1580,7 @@ __global__ void __launch_bounds__(COMMIT_THREADS) commit_kernel(CommitArgs a) {
     a.committed[1] = (committed == B && !host_cut) ? 1 : 0;
     a.committed[2] = (int32_t)s_start;
     a.committed[3] = 0;
-    a.committed[4] = 0;
+    a.committed[4] = (int32_t)(__builtin_amdgcn_s_memrealtime() - rt0);
   }
   if (ST && tid == 0) {
     for (int i = 0; i < 12; ++i) a.stamps[i] += st_acc[i];
@@ -1644,7 +1672,16 @@ hipError_t launch_node_prep(const MirrorView& m, uint32_t n0, uint32_t n1, int64
                             int32_t has_exp, int64_t exp_ns, hipStream_t st) {
   if (n1 <= n0) return hipSuccess;
   uint32_t grid = (n1 - n0 + 255) / 256;
-  hipLaunchKernelGGL(node_prep_kernel, dim3(grid), dim3(256), 0, st, m, n0, n1, now, filter_expired, has_exp, exp_ns);
+  hipLaunchKernelGGL(node_prep_kernel, dim3(grid), dim3(256), 0, st, m, n0, n1, now, filter_expired, has_exp, exp_ns,
+                     nullptr);
+  return hipGetLastError();
+}
+
+hipError_t launch_node_prep_idx(const MirrorView& m, const uint32_t* idx, uint32_t n, int64_t now, int32_t filter_expired,
+                                int32_t has_exp, int64_t exp_ns, hipStream_t st) {
+  if (!n) return hipSuccess;
+  hipLaunchKernelGGL(node_prep_kernel, dim3((n + 255) / 256), dim3(256), 0, st, m, 0u, n, now, filter_expired, has_exp,
+                     exp_ns, idx);
   return hipGetLastError();
 }
 

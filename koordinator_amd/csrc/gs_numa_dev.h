@@ -438,12 +438,18 @@ __host__ __device__ __noinline__ bool merge_hint_lists_gen(const HintList* L, in
   over = false;
   for (int pass = 0; pass < 2; ++pass) {
     if (pass == 1 && b_pref) break;
+#ifndef GS_MERGE_PTR_SELECT
     uint32_t S[6];   // this pass's entry sets (a copy: a pointer selecting s0 / s1 miscompiled on gfx950)
     bool empty = false;
     for (int l = 0; l < nl; ++l) {
       S[l] = pass ? s1[l] : s0[l];
       empty |= S[l] == 0;
     }
+#else   // the round-4 form, only in scripts/sanitize/merge_ptr_probe.hip (the miscompile's reproducer)
+    const uint32_t* S = pass ? s1 : s0;
+    bool empty = false;
+    for (int l = 0; l < nl; ++l) empty |= S[l] == 0;
+#endif
     if (empty) continue;   // a list without entries: no permutation
     uint32_t fw = 1u << full_mask;   // merged masks reachable after each list (bit x = mask x)
     for (int l = 0; l < nl; ++l) {

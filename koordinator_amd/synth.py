@@ -334,7 +334,7 @@ def load_into(engine, c: Cluster) -> None:
 
 def make_ext(c: Cluster, seed: int | None = None, gpu_node_pct: int = 20, gpus_per_node: int = 8,
              rsv_node_pct: int = 5, owners: int = 40, owner_pod_pct: int = 10, required_pct: int = 2,
-             gpu_pod_pct: int = 10, xres_node_pct: int = 0, xres_pod_pct: int = 0) -> Cluster:
+             gpu_pod_pct: int = 10, xres_node_pct: int = 0, xres_pod_pct: int = 0, owner_gpu_pct: int = 0) -> Cluster:
     """Reservation + DeviceShare state for config C5: GPU Device objects on gpu_node_pct% of the nodes
     (8 GPUs of 80 GiB, partly used), 1-2 reservations on rsv_node_pct% of the nodes (owner groups, Default /
     Restricted policies, some allocate-once, some already used by assigned pods, 10% with a reservation-order label),
@@ -343,7 +343,8 @@ def make_ext(c: Cluster, seed: int | None = None, gpu_node_pct: int = 20, gpus_p
     invalid gpu-core). NodeInfo (c.nodes) already holds the reserve pods and the pods assigned to them.
     xres_node_pct / xres_pod_pct: two registered extended resources (x0 "example.com/fpga": 1-4 per node, pods ask 1;
     x1 "example.com/shared-nic": 1000 per node, pods ask 100-400) on that share of nodes / pods, 1% of the pods asking
-    for both (Fit's scalar check over names outside the fixed slots)."""
+    for both (Fit's scalar check over names outside the fixed slots).
+    owner_gpu_pct: that share of the owner-group pods also requests GPUs (GPU pods that match reservations)."""
     s = Stream((BASE_SEED + 0x5C5) if seed is None else seed)
     N = c.num_nodes
     P = len(c.pods)
@@ -424,6 +425,8 @@ def make_ext(c: Cluster, seed: int | None = None, gpu_node_pct: int = 20, gpus_p
     ext["reservation_owner"] = np.where(own, s.randint(21, P, 1, owners), 0).astype(np.uint64)
     ext["reservation_required"] = (own & (s.randint(22, P, 0, 99) < required_pct * 100 // max(1, owner_pod_pct))).astype(np.int32)
     gp = (kind >= owner_pod_pct) & (kind < owner_pod_pct + gpu_pod_pct)
+    if owner_gpu_pct:
+        gp |= own & (s.randint(40, P, 0, 99) < owner_gpu_pct)
     gk = s.randint(23, P, 0, 99)
     amount = np.array([25, 50, 100, 100, 200, 400], np.int64)[s.randint(24, P, 0, 5)]
     nv = s.randint(25, P, 1, 2)

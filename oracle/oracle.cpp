@@ -1576,9 +1576,16 @@ bool filter_with_reservations(const gs_pod& pod, const NodeRState& ns, const std
   return false;
 }
 
-// NominateReservation (nominator.go:140-190): filter each matched reservation (FilterReservation, plugin.go:503-530),
-// then the lowest order label, else the highest ScoreReservation (ties: the first in reservation order)
-const gs_reservation* nominate(const gs_pod& pod, const NodeRState& ns) {
+// NominateReservation (nominator.go:140-190): filter each matched reservation (RunReservationFilterPlugins: the
+// Reservation plugin's FilterReservation, plugin.go:503-530, and DeviceShare's, deviceshare/plugin.go:324-375), then
+// the lowest order label, else the highest ScoreReservation (ties: the first in reservation order).
+// device_pod: the pod requests devices (DeviceShare's PreFilter state is not skip). DeviceShare's FilterReservation
+// then looks the reservation up in its restore state, which keeps only reservations holding device allocations
+// (RestoreReservation's filterFn, deviceshare/reservation.go:133-162); a reservation without one fails with "impossible,
+// there is no relevant Reservation information in deviceShare" and is not nominated. The reservations modelled here
+// hold no devices, so a device pod nominates none.
+const gs_reservation* nominate(const gs_pod& pod, const NodeRState& ns, bool device_pod = false) {
+  if (device_pod) return nullptr;
   std::vector<const gs_reservation*> ok;
   for (const gs_reservation* r : ns.matched) {
     if (r->allocate_once && r->assigned_pods > 0) continue;
@@ -1898,7 +1905,7 @@ int or_schedule_ext(or_cluster* c, const gs_pod* pods, const gs_pod_ext* ext, ui
       for (const gs_reservation* r : ns.matched)
         if (r->order != 0 && order > r->order) order = r->order;
       if (order != INT64_MAX && order != 0 && sel_order > order) { sel_order = order; preferred = n; }
-      nominated[n] = nominate(pod, ns);
+      nominated[n] = nominate(pod, ns, gpu_pod);
     }
     // Score + NormalizeScore + weights
     const int F = (int)fl.size();

@@ -38,6 +38,7 @@ def _worker(rank: int, world: int, port: int, numa: bool, pods: int, q):
     import faulthandler
     import sys
     faulthandler.dump_traceback_later(100, exit=True, file=sys.stderr)   # a stuck rank names where it is
+    os.environ.setdefault("GS_WATCHDOG_S", "10")   # ... and the library names the host wait it is blocked in
     try:
         import torch
         import torch.distributed as dist

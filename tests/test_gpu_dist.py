@@ -22,8 +22,10 @@ def _cluster(numa: bool):
     return c
 
 
-def _worker(rank: int, port: int, numa: bool, q):
+def _worker(rank: int, port: int, numa: bool, q, skew: str = ""):
     try:
+        if skew:   # GS_DEBUG_XCHG_SKEW: rank:batch skips one exchange sequence number there
+            os.environ["GS_DEBUG_XCHG_SKEW"] = skew
         import torch.distributed as dist
         os.environ["MASTER_ADDR"] = "127.0.0.1"
         os.environ["MASTER_PORT"] = str(port)
@@ -41,6 +43,14 @@ def _worker(rank: int, port: int, numa: bool, q):
 
         e.comm_init_callback(2, rank, allgather)
         synth.load_into(e, c)
+        if skew:
+            try:
+                e.schedule(c.pods[:250])
+                q.put((rank, "no error", -2, 0, 0))
+            except Exception as ex:
+                q.put((rank, str(ex), -3, 0, 0))
+            dist.destroy_process_group()
+            return
         got = e.schedule(c.pods[:250])
         got2 = e.schedule(c.pods[250:])   # a second call: the replicated mirrors stayed identical
         st = e.stats()
@@ -88,3 +98,26 @@ def test_two_processes_sharded_schedule_matches_oracle(numa):
             bad = np.nonzero(got[f] != want[f])[0]
             assert not len(bad), f"rank {r}: {f} differs at pod {bad[:5]}"
     assert res[0][3] == res[1][2], "contiguous shards"
+
+
+def test_exchange_sequence_divergence_fails_on_every_rank():
+    """A rank whose exchange sequence diverges (GS_DEBUG_XCHG_SKEW=1:3: rank 1 skips one sequence number at its
+    fourth batch pass) must make EVERY rank fail with GS_ECOMM at that exchange, naming the batch, instead of leaving
+    one rank inside a collective the others never enter (the round-4 four-process hang's failure mode)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, port, True, q, "1:3")) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in range(2):
+        r, msg, code, _, _ = q.get(timeout=240)
+        res[r] = (msg, code)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for r in range(2):
+        msg, code = res[r]
+        assert code == -3, f"rank {r}: schedule did not fail ({msg})"
+        assert "exchange sequence diverged" in msg and "batch 3" in msg, f"rank {r}: {msg}"

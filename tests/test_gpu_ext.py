@@ -150,3 +150,37 @@ def test_c5_numa_policy_nodes_deviceshare_hints(policy_pct):
         uid = int(c.pods["uid"][j])
         a, b = e.allocation(int(node[j]), uid), o.allocation(int(node[j]), uid)
         assert (a is None) == (b is None) and (a is None or a.tobytes() == b.tobytes()), j
+
+
+@pytest.mark.parametrize("policy_pct", [0, 60], ids=["no-policy", "policy60"])
+def test_c5_gpu_owner_pods_reservations_on_policy_nodes_cpuset_pods(policy_pct):
+    """The §8(f) rank-2 combinations that round 4 refused (GS_EUNSUPPORTED), against the oracle, bit-exact:
+    * GPU pods that match reservations: the Fit restore applies, DeviceShare's view is not restored (the reservations
+      hold no devices: deviceshare/reservation.go:133-162), and DeviceShare's FilterReservation rejects every
+      device-less reservation for a device pod (deviceshare/plugin.go:324-350), so a GPU pod nominates none;
+    * reservations matched on NUMA-policy nodes: the restored NodeInfo through NodeNUMAResource's Filter (its
+      reservation restore is empty without reserved cpusets, nodenumaresource/reservation.go:76-113), the affinity of
+      the restored row, DeviceShare as the second hint provider there;
+    * cpuset-bound extension pods (NUMA split on the device, takeCPUs by the host's Reserve)."""
+    c = synth.make_cluster(2000, 800, config_id=21 + policy_pct)
+    synth.make_numa(c, numa_policy_pct=policy_pct, cpuset_pod_pct=25)
+    synth.make_ext(c, gpu_node_pct=40, gpu_pod_pct=20, rsv_node_pct=30, owners=8, owner_pod_pct=40, required_pct=10,
+                   owner_gpu_pct=40)
+    e, o, ge, oe = run_pair(c, enabled=abi.GS_ENABLE_ALL)
+    placed = check(c, e, o, ge, oe)
+    ext, gx = c.ext["pod_ext"], ge[1]
+    gpu_owner = (ext["reservation_owner"] != 0) & (ext["gpu_request_mask"] != 0)
+    assert (gpu_owner & placed).sum() > 20 and (gx["gpu_count"][gpu_owner] > 0).sum() > 10
+    assert (gx["reservation_uid"][gpu_owner] == 0).all()   # no nomination for a device pod
+    assert (gx["reservation_uid"] > 0).sum() > 20
+    node = ge[0]["node"]
+    flags = ge[0]["flags"]
+    assert ((flags & abi.GS_PLACED_CPUSET) != 0)[placed].sum() > 20
+    if policy_pct:
+        pol = c.numa["node_numa"]["numa_topology_policy"] != 0
+        rs_on_pol = placed & (gx["reservation_uid"] > 0) & pol[np.maximum(node, 0)]
+        assert rs_on_pol.sum() > 5
+    for j in np.nonzero(placed)[0]:
+        uid = int(c.pods["uid"][j])
+        a, b = e.allocation(int(node[j]), uid), o.allocation(int(node[j]), uid)
+        assert (a is None) == (b is None) and (a is None or a.tobytes() == b.tobytes()), j

@@ -28,6 +28,23 @@ def _save(name: str, got, extra: dict):
                         placements=np.ascontiguousarray(got).view(np.uint8), meta=json.dumps(extra))
 
 
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "fullsize")
+
+
+def _golden_equal(name: str, got):
+    """Every decision of the run equals the committed placements, which were checked pod by pod against the oracle's
+    sequential scheduleOne (all 50,000 north-star pods and all 20,480 bench pods, 0 mismatches:
+    profiles/r04_full_parity_{northstar,bench}.json, scripts/full_parity.py). Every field of every placement record
+    (node, max score, ties, feasible count, flags, NUMA zone split, cpuset) must match, so any later change that moves
+    a single decision fails here, on the driver's box, not only in an offline check."""
+    want = np.load(os.path.join(GOLDEN, f"placements_{name}.npz"))["placements"].view(abi.PLACEMENT_DTYPE)
+    assert len(want) == len(got), f"{name}: {len(got)} placements, golden holds {len(want)}"
+    for f in abi.PLACEMENT_DTYPE.names:
+        bad = np.nonzero(np.any((got[f] != want[f]).reshape(len(got), -1), axis=1))[0]
+        assert len(bad) == 0, f"{name}: {f} differs from the verified placements at pods {bad[:5]} ({len(bad)} pods)"
+    return len(got)
+
+
 def _replay_check(c, cfg, got, sample):
     o = orc.Oracle(cfg)
     synth.load_into(o, c)
@@ -55,11 +72,13 @@ def test_c3_100k_nodes_50k_pods_replay_parity():
     got = e.schedule(c.pods)
     assert e.mirror_check() == 0
     _save("northstar", got, {"stats": {k: (float(v) if isinstance(v, float) else int(v)) for k, v in e.stats().items()}})
+    ng = _golden_equal("northstar", got)
     P = len(c.pods)
     sample = np.unique(np.concatenate([np.arange(48), np.arange(48, P, 64)]))   # every 64th pod
     n = _replay_check(c, cfg, got, sample)
     placed = int((got["node"] >= 0).sum())
-    print(f"100k x 50k: {placed} placed, {n} pods re-scheduled by the oracle and identical; "
+    print(f"100k x 50k: {placed} placed, all {ng} placements equal the oracle-verified golden ones, {n} pods "
+          f"re-scheduled by the oracle and identical; "
           f"wall {time.perf_counter() - t0:.1f} s; stats {e.stats()}")
 
 
@@ -78,8 +97,10 @@ def test_c3_bench_config_50k_nodes_replay_parity():
     got = np.concatenate([e.schedule(c.pods[k:k + step], seq[k:k + step]) for k in range(0, P, step)])
     assert e.mirror_check() == 0
     _save("bench", got, {"stats": {k: (float(v) if isinstance(v, float) else int(v)) for k, v in e.stats().items()}})
+    ng = _golden_equal("bench", got)
     n = _replay_check(c, cfg, got, np.arange(0, P, 64))
-    print(f"C3 bench config 50k x {P}: {int((got['node'] >= 0).sum())} placed, {n} pods re-checked in full; "
+    print(f"C3 bench config 50k x {P}: {int((got['node'] >= 0).sum())} placed, all {ng} placements equal the "
+          f"oracle-verified golden ones, {n} pods re-checked in full; "
           f"wall {time.perf_counter() - t0:.1f} s")
 
 
