@@ -47,19 +47,32 @@ def cpu_baseline(cluster, cfg, pods, seq, given, sample_start: int, sample_pods:
     o.schedule(pods[i:i + warm], seq[i:i + warm], nthreads=threads)
     i += warm
     o.phase_times()
-    # the timed pods one scheduleOne at a time (the reference's loop), their times grouped into 5 chunks by a fixed
-    # random permutation: every chunk is a random sample of the queue's pods (a contiguous or a j % 5 chunk can hold a
-    # skewed share of the expensive cpuset / NUMA pods: the synthetic queue's kinds follow index patterns)
+    # the timed pods one scheduleOne at a time (the reference's loop), their times grouped into 5 chunks by a
+    # stratified random draw: the pods are split by kind (QoS x priority class, required / preferred CPU bind policy,
+    # exclusive policy, whole CPUs requested: a cpuset-bound LSE / LSR pod's Filter runs takeCPUs on every node whose
+    # bind policy is required and costs ~20 plain pods, with a spread set by those attributes), each kind in a fixed
+    # random order dealt round-robin over the chunks, so every chunk holds the same mix and its rate differs from the
+    # others by the cost spread within a kind only (plain random chunks of 198 pods spread ±15-26%)
     n_t = max(5, sample_pods - warm)
     per = np.zeros(n_t)
     for j in range(n_t):
         t0 = time.perf_counter()
         o.schedule(pods[i + j:i + j + 1], seq[i + j:i + j + 1], nthreads=threads)
         per[j] = time.perf_counter() - t0
+    tp = pods[i:i + n_t]
     i += n_t
+    kind = ((tp["qos_class"].astype(np.int64) * 16 + tp["priority_class"]) * 1000 +
+            tp["required_cpu_bind_policy"].astype(np.int64) * 100 + tp["preferred_cpu_bind_policy"] * 10 +
+            tp["preferred_cpu_exclusive_policy"]) * 100 + tp["requests"][:, 0] // 1000
+    rng = np.random.default_rng(20260)
+    chunk_of = np.empty(n_t, np.int64)
+    dealt = 0
+    for k in np.unique(kind):
+        idx = rng.permutation(np.nonzero(kind == k)[0])
+        chunk_of[idx] = (dealt + np.arange(len(idx))) % 5
+        dealt += len(idx)
     chunk = n_t // 5
-    perm = np.random.default_rng(20260).permutation(n_t)
-    rates = [float(chunk / per[perm[c * chunk:(c + 1) * chunk]].sum()) for c in range(5)]
+    rates = [float((chunk_of == c).sum() / per[chunk_of == c].sum()) for c in range(5)]
     secs = float(per.sum())
     phases = o.phase_times()
     n1 = max(4, chunk // 8)
@@ -74,8 +87,10 @@ def cpu_baseline(cluster, cfg, pods, seq, given, sample_start: int, sample_pods:
             "single_thread_pods_per_s": r1, "single_thread_evals_per_s": r1 * cluster.num_nodes,
             "sample": f"pods {sample_start}..{i + n1} of the timed workload on the GPU's state at the start of the timed "
                       f"region (oracle replay of the {sample_start} warm-up placements); {warm} warm-up pods, {n_t} timed "
-                      f"pods at {threads} threads one scheduleOne at a time, rates of 5 random chunks of {chunk} pods "
-                      f"(median), {n1} pods at 1 thread"}
+                      f"pods at {threads} threads one scheduleOne at a time, rates of 5 chunks of ~{chunk} pods drawn "
+                      f"at random within each pod kind (QoS x priority class, CPU bind / exclusive policies, CPUs; equal "
+                      f"kind mix per chunk; median), {n1} "
+                      f"pods at 1 thread"}
 
 
 def cpu_baseline_c5(cluster, cfg, ext_args, pods, seq, sample_pods: int) -> dict:
@@ -146,7 +161,7 @@ def main() -> None:
     ap.add_argument("--scaling", choices=["strong", "weak"], default="strong")
     ap.add_argument("--pods-per-step", type=int, default=2048)
     ap.add_argument("--batch", type=int, default=128)
-    ap.add_argument("--cpu-sample-pods", type=int, default=1100)
+    ap.add_argument("--cpu-sample-pods", type=int, default=2200)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--profile", choices=["c3", "la-fit", "c5"], default="c3",
                     help="c5: 100k nodes, LoadAware + Fit + DeviceShare + Reservation (SURVEY 8(d) C5, see --nodes)")

@@ -155,6 +155,7 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   const MirrorView& m = a.m;
   const bool numa_on = (a.pf.enabled & 0x30u) != 0;
+  const bool multi = a.nranks > 1;   // merged levels of several shards; rows outside [own0, own1) have no S_own
   const uint64_t lt_mask = (1ull << lane) - 1ull;
   // ---- LDS (fixed layout, SpecLds)
   extern __shared__ __align__(16) unsigned char cm[];
@@ -213,9 +214,6 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
     __builtin_amdgcn_s_setprio(3);
     // decisions ahead of the verifier: SP_LAG (the undo log's depth), or fewer (GS_SPEC_LAG, experiments)
     const int lag = ((a.dbg >> 12) & 15u) ? (int)min((a.dbg >> 12) & 15u, (uint32_t)SP_LAG) : SP_LAG;
-    // GS_SPEC_SOLOAD=1 (experiments): the selector loads a fresh own-shard row's batch-start scores itself (the round-4
-    // form) instead of leaving them to the Reserve wave (unknown until filled, resolved from the list head)
-    const bool so_load = (a.dbg >> 16) & 1u;
     uint32_t dn0 = 0xffffffffu, dn1 = 0xffffffffu;   // slot s's node in lane s % 64 of dn0 / dn1
     int32_t pv0 = -1, pv1 = -1;                      // slot s's latest decided version (pod index)
     int nd = 0, q = 0, end_at = B, end_why = 0;
@@ -430,11 +428,9 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
       if (lane + 64 < nd) { so1 = dso[p * SB + 64 + lane]; if (rdy1) sc1 = dsc[p * SB + 64 + lane]; }
       SPM(29);   // next header's loads issued, pending fresh slot stored, dirty scores loaded
       uint64_t unk0 = 0, unk1 = 0;
-      {
-        // fresh rows whose batch-start scores are not in dso yet (the Reserve wave's fill from S_own, or for another
-        // shard's row the batch-start job): a node in the list head has its listed level as batch-start score (exact);
-        // any other is unknown, counted as clean and unlisted (checked at verification, or resolved from S on the
-        // full-row path)
+      if (multi) {
+        // off-shard fresh rows whose batch-start job has not finished: a node in the list head has its listed level
+        // as batch-start score (exact); any other is unknown, counted as clean and unlisted (checked at verification)
         const uint64_t u0 = __ballot(lane < nd && so0 == SO_UNKNOWN), u1 = __ballot(lane + 64 < nd && so1 == SO_UNKNOWN);
         if (u0 | u1) {
           const int incl = wave_incl_scan(lane < nlev ? hc : 0);   // list end of level `lane`
@@ -472,7 +468,7 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
         if (cj > dj) { ctop = cj - dj; Mclean = sj; break; }
       }
       const int Md = wave_max(max(sc0, sc1));
-      int Fd = wave_sum((sc0 >= 0) - (so0 >= 0) + (sc1 >= 0) - (so1 >= 0));
+      const int Fd = wave_sum((sc0 >= 0) - (so0 >= 0) + (sc1 >= 0) - (so1 >= 0));
       M = max(Mclean, Md);
       F = Fd + feas;
       SPM(18);   // decide: dirty-slot state, level scan
@@ -612,12 +608,6 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
         // score for ready dirty rows, pending rows left out (verified later like any decision)
         const int16_t* row = a.S + (size_t)p * a.ld;
         const uint32_t len = a.own1 - a.own0;
-        if (unk0 | unk1) {   // (one shard) the unknown batch-start scores straight from the row; F's dirty term again
-          if ((unk0 >> lane) & 1ull) so0 = row[dn0 - a.own0];
-          if ((unk1 >> lane) & 1ull) so1 = row[dn1 - a.own0];
-          unk0 = unk1 = 0;
-          Fd = wave_sum((sc0 >= 0) - (so0 >= 0) + (sc1 >= 0) - (so1 >= 0));
-        }
         constexpr int VB = 8;
         auto load_blk = [&](uint32_t i0, int16_t (&x)[8]) {
           if (i0 + 8 <= len) {
@@ -776,8 +766,7 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
           d.flags |= SP_FRESH;
           if (lane == (nd & 63)) { if (nd < 64) { dn0 = winner; pv0 = p; } else { dn1 = winner; pv1 = p; } }
           const int q0 = p + 1 + lane, q1 = q0 + 64;
-          const bool own = winner - a.own0 < a.own1 - a.own0;
-          if (own && so_load) {
+          if (winner - a.own0 < a.own1 - a.own0) {
             // both loads issued unconditionally (rows clamped into the batch; flush_fresh stores only q < B): no exec-mask
             // branch between them, so neither waits for the other, nor for the next header's loads in flight
             const int16_t* col = a.S_own + (winner - a.own0);
@@ -785,10 +774,8 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
             ps_v1 = col[(size_t)min(q1, B - 1) * a.ld];
             ps_slot = slot;
             ps_p = p;
-          } else {
-            // unknown until filled: the own shard's S_own column by the Reserve wave of this pod (one load per lane, off
-            // the decisions' chain), another shard's row by the batch-start job
-            if (!own) d.flags |= SP_OFFSHARD;
+          } else {   // another shard's row: unknown until the Reserve wave's batch-start job has evaluated it
+            d.flags |= SP_OFFSHARD;
             if (q0 < B) dso[q0 * SB + slot] = SO_UNKNOWN;
             if (q1 < B) dso[q1 * SB + slot] = SO_UNKNOWN;
           }
@@ -962,16 +949,6 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
     };
     int q = wr, pf_q = -1;   // pf_q: the pod whose fresh winner row is in flight in pf_v
     int64_t pf_v = 0;
-    // a fresh own-shard row's batch-start scores for the later pods (S_own column, lane i: pods q+1+i, q+65+i), loaded
-    // with the row (also one pod ahead) and stored into dso, where the decisions find them (unknown until then)
-    const bool so_fill = !((a.dbg >> 16) & 1u);
-    int16_t pf_s0 = 0, pf_s1 = 0;
-    auto fetch_so = [&](int qq, uint32_t node, int16_t& s0, int16_t& s1) {
-      if (!so_fill || node - a.own0 >= a.own1 - a.own0) return;
-      const int16_t* col = a.S_own + (node - a.own0);
-      s0 = col[(size_t)min(qq + 1 + lane, B - 1) * a.ld];
-      s1 = col[(size_t)min(qq + 65 + lane, B - 1) * a.ld];
-    };
     uint32_t spins = 0;
     // room for n more jobs in this wave's ring (it is the only producer); false: a rollback or the end intervened
     auto room = [&](int n) -> bool {
@@ -1025,25 +1002,12 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
       const uint32_t winner = (uint32_t)d.winner;
       const bool fresh = d.flags & SP_FRESH;
       if (fresh) {   // the row: one load per lane (issued one pod ahead when pod q was already decided), then LDS
-        int16_t so0 = 0, so1 = 0;
-        int64_t vv;
-        if (pf_q == q) {
-          vv = pf_v;
-          so0 = pf_s0;
-          so1 = pf_s1;
-        } else {
-          vv = fetch(q, winner);
-          fetch_so(q, winner, so0, so1);
-        }
+        const int64_t vv = pf_q == q ? pf_v : fetch(q, winner);
         pf_q = -1;
         const int qn = q + SP_NRES;   // this wave's next pod
         if (qn < ld_acq(&s_decided)) {   // prefetch its fresh winner row
           const DecRec& dn = dec[qn];
-          if ((dn.flags & (SP_FRESH | SP_FITERR)) == SP_FRESH) {
-            pf_v = fetch(qn, (uint32_t)dn.winner);
-            fetch_so(qn, (uint32_t)dn.winner, pf_s0, pf_s1);
-            pf_q = qn;
-          }
+          if ((dn.flags & (SP_FRESH | SP_FITERR)) == SP_FRESH) { pf_v = fetch(qn, (uint32_t)dn.winner); pf_q = qn; }
         }
         if (f_kind) {
           unsigned char* dst = f_region == 0 ? reinterpret_cast<unsigned char*>(&drows[slot])
@@ -1051,11 +1015,6 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
                                              : reinterpret_cast<unsigned char*>(&s_aff_w);
           if (f_size == 8) *reinterpret_cast<int64_t*>(dst + f_off) = vv;
           else *reinterpret_cast<int32_t*>(dst + f_off) = (int32_t)vv;
-        }
-        if (so_fill && winner - a.own0 < a.own1 - a.own0) {   // before the row's jobs (and so its rescored flag)
-          const int q0 = q + 1 + lane, q1 = q0 + 64;
-          if (q0 < B) dso[q0 * SB + slot] = so0;
-          if (q1 < B) dso[q1 * SB + slot] = so1;
         }
         if (lane == 0) has_row[slot] = 1;
         SPM(21);   // fresh row fetch
@@ -1172,7 +1131,6 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
         const DecRec& dn = dec[q + SP_NRES];
         if ((dn.flags & (SP_FRESH | SP_FITERR)) == SP_FRESH) {
           pf_v = fetch(q + SP_NRES, (uint32_t)dn.winner);
-          fetch_so(q + SP_NRES, (uint32_t)dn.winner, pf_s0, pf_s1);
           pf_q = q + SP_NRES;
         }
       }

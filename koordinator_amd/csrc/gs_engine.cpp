@@ -272,6 +272,47 @@ struct Where {
     c->where_t.store(prev_t);
   }
 };
+// Host waits of the scheduling path: poll the event / stream (spin, then yield, then short sleeps) instead of HIP's
+// blocking synchronisation. Several processes sharing one GPU (the C4 rehearsal) showed a rank parked for 10-100 s
+// inside hipStreamSynchronize / hipEventSynchronize while every stream and event of that rank had long completed (the
+// watchdog's queries), i.e. a lost wake-up of the blocking wait. A poll sees the completion at once;
+// bounded: past GS_WAIT_LIMIT_S (default 600 s) the call fails with GS_EDEVICE naming the wait. GS_WAIT_BLOCKING=1:
+// HIP's blocking calls (experiments).
+bool wait_blocking() {
+  static const bool b = getenv("GS_WAIT_BLOCKING") && getenv("GS_WAIT_BLOCKING")[0] == '1';
+  return b;
+}
+template <class Query>
+hipError_t poll_until(Query&& query, double limit_s) {
+  const auto t0 = std::chrono::steady_clock::now();
+  for (uint64_t it = 0;; ++it) {
+    const hipError_t e = query();
+    if (e != hipErrorNotReady) return e;
+    if (it < 2000) {
+      __builtin_ia32_pause();
+    } else if (it < 20000) {
+      std::this_thread::yield();
+    } else {
+      std::this_thread::sleep_for(std::chrono::microseconds(20));
+      if ((it & 1023) == 0 &&
+          std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > limit_s)
+        return hipErrorLaunchTimeOut;   // (the wait exceeded its bound: reported as GS_EDEVICE)
+    }
+  }
+}
+double wait_limit_s() {
+  static const double lim = getenv("GS_WAIT_LIMIT_S") ? atof(getenv("GS_WAIT_LIMIT_S")) : 600.0;
+  return lim > 0 ? lim : 600.0;
+}
+hipError_t host_wait_event(hipEvent_t ev) {
+  if (wait_blocking()) return hipEventSynchronize(ev);
+  return poll_until([&] { return hipEventQuery(ev); }, wait_limit_s());
+}
+hipError_t host_wait_stream(hipStream_t st) {
+  if (wait_blocking()) return hipStreamSynchronize(st);
+  return poll_until([&] { return hipStreamQuery(st); }, wait_limit_s());
+}
+
 void watchdog_loop(gs_ctx* c, double limit_s) {
   (void)hipSetDevice(c->cfg.device);
   const char* reported = nullptr;
@@ -714,7 +755,7 @@ int flush_rows(gs_ctx* c) {
     uint32_t n = (uint32_t)std::min<size_t>(c->stage_cap, c->dirty_list.size() - done);
     // staging buffers are reused: the previous scatter must have consumed them
     Where w_(c, "flush_rows: previous scatter");
-    HIP_TRY(c, hipStreamSynchronize(c->st));
+    HIP_TRY(c, host_wait_stream(c->st));
     // one staged block, one copy: the n rows, then their node indices
     uint32_t* h_idx = reinterpret_cast<uint32_t*>(c->h_stage_rows + (size_t)n * ROW_WORDS);
     for (uint32_t j = 0; j < n; ++j) {
@@ -836,7 +877,7 @@ int exchange(gs_ctx* c, uint32_t site, uint8_t* d_send, uint8_t* d_recv, size_t 
     Where w_(c, site == XSITE_LEVELS ? "exchange (levels): stream before the callback"
                                      : "exchange (small): stream before the callback");
     HIP_TRY(c, hipMemcpyAsync(c->h_xchg_send, d_send, bytes - sizeof(XTag), hipMemcpyDeviceToHost, c->st));
-    HIP_TRY(c, hipStreamSynchronize(c->st));
+    HIP_TRY(c, host_wait_stream(c->st));
     c->where.store("exchange: allgather callback");
     std::memcpy(c->h_xchg_send + bytes - sizeof(XTag), &tag, sizeof tag);
     if (c->cb(c->cb_user, c->h_xchg_send, c->h_xchg_recv, bytes) != 0) return fail(c, GS_ECOMM, "allgather callback failed");
@@ -859,7 +900,7 @@ int exchange_small(gs_ctx* c, uint32_t site, const void* d_payload, size_t paylo
   if (int rc = exchange(c, site, c->d_xsmall, c->d_xsmall + XSMALL, XSMALL, &tag)) return rc;
   HIP_TRY(c, hipMemcpyAsync(c->h_xsmall, c->d_xsmall + XSMALL, XSMALL * c->nranks, hipMemcpyDeviceToHost, c->st));
   Where w_(c, "exchange_small: read back");
-  HIP_TRY(c, hipStreamSynchronize(c->st));
+  HIP_TRY(c, host_wait_stream(c->st));
   if (int rc = check_tags(c, c->h_xsmall, XSMALL, tag)) return rc;
   for (int r = 0; r < c->nranks; ++r)
     std::memcpy(static_cast<uint8_t*>(host_out) + (size_t)r * payload, c->h_xsmall + (size_t)r * XSMALL, payload);
@@ -1094,9 +1135,7 @@ CommitArgs commit_args(gs_ctx* c, int b) {
   static const uint32_t prio = getenv("GS_SPEC_PRIO") ? (uint32_t)strtoul(getenv("GS_SPEC_PRIO"), nullptr, 0) & 0x3f0u : 0u;
   // GS_SPEC_LAG (experiments): decisions ahead of the verifier, 1..12 (bits 12-15; 0: the kernel's SP_LAG)
   static const uint32_t lag = getenv("GS_SPEC_LAG") ? (uint32_t)std::min(12L, std::max(0L, atol(getenv("GS_SPEC_LAG")))) : 0u;
-  // GS_SPEC_SOLOAD=1 (experiments): the selector loads fresh rows' batch-start scores itself (bit 16)
-  static const bool soload = getenv("GS_SPEC_SOLOAD") && getenv("GS_SPEC_SOLOAD")[0] == '1';
-  a.dbg = (nospec ? 1u : 0u) | prio | lag << 12 | (soload ? 1u << 16 : 0u);
+  a.dbg = (nospec ? 1u : 0u) | prio | lag << 12;
   a.tb = c->d_tb;
   a.xerr = c->nranks > 1 ? c->d_xerr : nullptr;
   return a;
@@ -1122,8 +1161,8 @@ int launch_batch(gs_ctx* c, int b, const int32_t* prev, const PlacementDev* prev
     for (uint32_t n = c->n0; n < c->n1; ++n)
       if (c->numa[n].cfg.numa_topology_policy != GS_NUMA_POLICY_NONE) idx.push_back(n);
     if (c->d_numa_idx) {
-      HIP_TRY(c, hipStreamSynchronize(c->st));
-      HIP_TRY(c, hipStreamSynchronize(c->st_ev));
+      HIP_TRY(c, host_wait_stream(c->st));
+      HIP_TRY(c, host_wait_stream(c->st_ev));
       (void)hipFree(c->d_numa_idx);
       c->d_numa_idx = nullptr;
     }
@@ -1134,7 +1173,7 @@ int launch_batch(gs_ctx* c, int b, const int32_t* prev, const PlacementDev* prev
     }
     static const bool no_slab = getenv("GS_NUMA_SLAB") && getenv("GS_NUMA_SLAB")[0] == '0';
     if (!no_slab && c->numa_n > c->slab_cap) {   // columns of numa_n entries (rounded), the mirror's numbering
-      HIP_TRY(c, hipStreamSynchronize(c->st_ev));
+      HIP_TRY(c, host_wait_stream(c->st_ev));
       if (c->slab_mv.i64) (void)hipFree(c->slab_mv.i64);
       if (c->slab_mv.i32) (void)hipFree(c->slab_mv.i32);
       c->slab_mv = MirrorView{nullptr, nullptr, 0};
@@ -1217,7 +1256,7 @@ int finish_batch(gs_ctx* c, int b, bool clobbered, int* committed_out) {
   uint32_t len = c->n1 - c->n0;
   {
     Where w_(c, "finish_batch: the batch's readback event");
-    HIP_TRY(c, hipEventSynchronize(c->ev[5]));
+    HIP_TRY(c, host_wait_event(c->ev[5]));
   }
   flush_exchange_times(c);
   c->stats.eval_ms += ev_ms(c->ev[0], c->ev[1]);
@@ -1233,7 +1272,7 @@ int finish_batch(gs_ctx* c, int b, bool clobbered, int* committed_out) {
   if (committed < 0) return fail(c, GS_ESTATE, "commit pass of a batch was voided unexpectedly");
   if (c->h_committed[3] == COMMIT_ERR_XTAG) {   // the level exchange paired different exchanges of the ranks
     std::vector<uint8_t> blk((size_t)c->xchg_bytes * c->nranks);
-    HIP_TRY(c, hipStreamSynchronize(c->st));
+    HIP_TRY(c, host_wait_stream(c->st));
     HIP_TRY(c, hipMemcpy(blk.data(), c->d_xchg_recv, blk.size(), hipMemcpyDeviceToHost));
     XTag mine;
     std::memcpy(&mine, blk.data() + (size_t)c->rank * c->xchg_bytes + c->xchg_bytes - sizeof(XTag), sizeof mine);
@@ -1259,7 +1298,7 @@ int finish_batch(gs_ctx* c, int b, bool clobbered, int* committed_out) {
     } else {
       HIP_TRY(c, hipMemcpyAsync(rs.data(), c->d_rowstat, sizeof(RowStat), hipMemcpyDeviceToHost, c->st));
     }
-    HIP_TRY(c, hipStreamSynchronize(c->st));
+    HIP_TRY(c, host_wait_stream(c->st));
     int M = -1;
     int64_t T = 0, F = 0;
     for (const auto& r : rs) {
@@ -1293,7 +1332,7 @@ int finish_batch(gs_ctx* c, int b, bool clobbered, int* committed_out) {
       winner = w[owner];
     } else {
       HIP_TRY(c, hipMemcpyAsync(&winner, c->d_sel, 4, hipMemcpyDeviceToHost, c->st));
-      HIP_TRY(c, hipStreamSynchronize(c->st));
+      HIP_TRY(c, host_wait_stream(c->st));
     }
     if (winner < 0) return fail(c, GS_ESTATE, "exact path could not locate tie %lld", (long long)jstar);
     a.forced_node = winner;
@@ -1304,12 +1343,12 @@ int finish_batch(gs_ctx* c, int b, bool clobbered, int* committed_out) {
     HIP_TRY(c, launch_commit(a, c->st));
     HIP_TRY(c, hipEventRecord(c->ev[4], c->st));
     HIP_TRY(c, hipMemcpyAsync(c->h_committed, c->d_committed, COMMITTED_BYTES, hipMemcpyDeviceToHost, c->st));
-    HIP_TRY(c, hipStreamSynchronize(c->st));
+    HIP_TRY(c, host_wait_stream(c->st));
     c->stats.commit_ms += ev_ms(c->ev[3], c->ev[4]);
     committed = c->h_committed[0];
     if (committed < 1) return fail(c, GS_ESTATE, "forced commit made no progress");
     HIP_TRY(c, hipMemcpyAsync(c->h_out, c->d_out, sizeof(PlacementDev) * committed, hipMemcpyDeviceToHost, c->st));
-    HIP_TRY(c, hipStreamSynchronize(c->st));
+    HIP_TRY(c, host_wait_stream(c->st));
   }
   flush_exchange_times(c);
   if (committed < b) {
@@ -1409,7 +1448,7 @@ int ext_stage_reserve(gs_ctx* c, uint32_t nrec, uint32_t nres) {
   c->xin_off_rec = off_pv + al(sizeof(PodVec));
   c->xin_off_res = c->xin_off_rec + al(sizeof(ExtRec) * c->xrec_cap);
   c->xin_bytes = c->xin_off_res + sizeof(ExtRes) * c->xres_cap;
-  HIP_TRY(c, hipStreamSynchronize(c->st));
+  HIP_TRY(c, host_wait_stream(c->st));
   if (c->h_xin) (void)hipHostFree(c->h_xin);
   if (c->d_xin) (void)hipFree(c->d_xin);
   if (c->d_xnom) (void)hipFree(c->d_xnom);
@@ -1436,7 +1475,7 @@ int ext_flush_devices(gs_ctx* c) {
   }
   for (size_t done = 0; done < c->dev_dirty_list.size();) {
     const uint32_t n = (uint32_t)std::min<size_t>(EXT_DEV_STAGE, c->dev_dirty_list.size() - done);
-    HIP_TRY(c, hipStreamSynchronize(c->st));   // the previous scatter has consumed the staging buffers
+    HIP_TRY(c, host_wait_stream(c->st));   // the previous scatter has consumed the staging buffers
     uint32_t* h_idx = reinterpret_cast<uint32_t*>(c->h_dev_stage + n);
     for (uint32_t j = 0; j < n; ++j) {
       const uint32_t i = c->dev_dirty_list[done + j];
@@ -1673,8 +1712,8 @@ int ext_schedule_one(gs_ctx* c, const gs_pod& pod, const gs_pod_ext& e, uint64_t
     std::vector<uint32_t> idx;
     for (uint32_t n = c->n0; n < c->n1; ++n)
       if (c->numa[n].cfg.numa_topology_policy != GS_NUMA_POLICY_NONE) idx.push_back(n);
-    HIP_TRY(c, hipStreamSynchronize(c->st));
-    HIP_TRY(c, hipStreamSynchronize(c->st_ev));
+    HIP_TRY(c, host_wait_stream(c->st));
+    HIP_TRY(c, host_wait_stream(c->st_ev));
     if (c->d_numa_idx) { (void)hipFree(c->d_numa_idx); c->d_numa_idx = nullptr; }
     c->numa_n = (uint32_t)idx.size();
     if (c->numa_n) {
@@ -1718,7 +1757,7 @@ int ext_schedule_one(gs_ctx* c, const gs_pod& pod, const gs_pod_ext& e, uint64_t
   HIP_TRY(c, launch_ext_finish(c->mv, c->d_xpv, c->pf, prod_cols, c->d_aff, c->n0, c->numa_on ? 1 : 0, c->d_xout,
                                c->d_xnom, nrec, c->h_xout, c->h_xnom, c->st));
   if (ext_ev) HIP_TRY(c, hipEventRecord(c->ev[4], c->st));
-  HIP_TRY(c, hipStreamSynchronize(c->st));
+  HIP_TRY(c, host_wait_stream(c->st));
   if (ext_ev) {
     c->stats.eval_ms += ev_ms(c->ev[0], c->ev[1]);
     c->stats.commit_ms += ev_ms(c->ev[1], c->ev[4]);
@@ -2119,9 +2158,9 @@ int gs_destroy(gs_ctx* c) {
   }
   if (c->comm) ncclCommDestroy(c->comm);
   for (hipEvent_t ev : c->x_ev) (void)hipEventDestroy(ev);
-  if (c->st) (void)hipStreamSynchronize(c->st);
-  if (c->st_ev) (void)hipStreamSynchronize(c->st_ev);
-  if (c->st_rb) (void)hipStreamSynchronize(c->st_rb);   // readbacks into the pinned buffers freed below
+  if (c->st) (void)host_wait_stream(c->st);
+  if (c->st_ev) (void)host_wait_stream(c->st_ev);
+  if (c->st_rb) (void)host_wait_stream(c->st_rb);   // readbacks into the pinned buffers freed below
   if (c->slot[0].d_pods) bind_slot(c, 0);
   {
     gs_ctx::Slot& s1 = c->slot[1];
@@ -2162,7 +2201,7 @@ int gs_destroy(gs_ctx* c) {
   if (c->st_rb) (void)hipStreamDestroy(c->st_rb);
   if (c->slab_mv.i64) (void)hipFree(c->slab_mv.i64);
   if (c->slab_mv.i32) (void)hipFree(c->slab_mv.i32);
-  if (c->st2) (void)hipStreamSynchronize(c->st2);
+  if (c->st2) (void)host_wait_stream(c->st2);
   if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
   if (c->ev_join) (void)hipEventDestroy(c->ev_join);
   if (c->st2) (void)hipStreamDestroy(c->st2);
@@ -2345,7 +2384,7 @@ int gs_evaluate(gs_ctx* c, const gs_pod* pods, uint32_t npods, int16_t* scores, 
     if (plugin_scores)
       HIP_TRY(c, hipMemcpyAsync(plugin_scores + (size_t)p0 * N * GS_NUM_PLUGINS, d_pl, (size_t)b * N * 2 * GS_NUM_PLUGINS,
                                 hipMemcpyDeviceToHost, c->st));
-    HIP_TRY(c, hipStreamSynchronize(c->st));
+    HIP_TRY(c, host_wait_stream(c->st));
   }
   (void)hipFree(d_sc);
   (void)hipFree(d_cd);
@@ -2426,9 +2465,9 @@ int schedule_stream(gs_ctx* c, PodRun run, Next&& next_run, Done&& run_done) {
   bool have_nxt = false;
   auto drain = [&]() {
     Where w_(c, "schedule_stream: drain");
-    (void)hipStreamSynchronize(c->st);
-    (void)hipStreamSynchronize(c->st_ev);
-    (void)hipStreamSynchronize(c->st_rb);   // a voided or in-flight batch's readback into the pinned buffers
+    (void)host_wait_stream(c->st);
+    (void)host_wait_stream(c->st_ev);
+    (void)host_wait_stream(c->st_rb);   // a voided or in-flight batch's readback into the pinned buffers
   };
   auto apply_batch = [&](const gs_pod* pods, gs_placement* outp, int n, const PlacementDev* hout, const PodVec* hpods,
                          bool special) -> int {
@@ -2735,7 +2774,7 @@ int gs_topology_register(gs_ctx* c, const gs_cpu_topology* t, int32_t* id) {
   // device copy of every registered topology's TopoDev (index = topology id)
   std::vector<TopoDev> all(c->topos.size());
   for (size_t i = 0; i < all.size(); ++i) all[i] = c->topos[i]->dev;
-  HIP_TRY(c, hipStreamSynchronize(c->st));
+  HIP_TRY(c, host_wait_stream(c->st));
   if (c->d_topos) { (void)hipFree(c->d_topos); c->d_topos = nullptr; }
   HIP_TRY(c, hipMalloc(&c->d_topos, sizeof(TopoDev) * all.size()));
   HIP_TRY(c, hipMemcpy(c->d_topos, all.data(), sizeof(TopoDev) * all.size(), hipMemcpyHostToDevice));
@@ -2885,9 +2924,9 @@ int gs_reset_stats(gs_ctx* c) {
 int gs_synchronize(gs_ctx* c) {
   if (!c) return GS_EINVAL;
   quiesce(c);
-  HIP_TRY(c, hipStreamSynchronize(c->st_ev));
-  HIP_TRY(c, hipStreamSynchronize(c->st));
-  HIP_TRY(c, hipStreamSynchronize(c->st_rb));
+  HIP_TRY(c, host_wait_stream(c->st_ev));
+  HIP_TRY(c, host_wait_stream(c->st));
+  HIP_TRY(c, host_wait_stream(c->st_rb));
   return GS_OK;
 }
 
@@ -2896,10 +2935,10 @@ int gs_synchronize(gs_ctx* c) {
 int gs_reset(gs_ctx* c) {
   if (!c) return GS_EINVAL;
   quiesce(c);
-  (void)hipStreamSynchronize(c->st);
-  (void)hipStreamSynchronize(c->st_ev);
-  (void)hipStreamSynchronize(c->st2);
-  (void)hipStreamSynchronize(c->st_rb);
+  (void)host_wait_stream(c->st);
+  (void)host_wait_stream(c->st_ev);
+  (void)host_wait_stream(c->st2);
+  (void)host_wait_stream(c->st_rb);
   (void)hipGetLastError();
   for (uint32_t i = 0; i < c->N; ++i)
     if (c->nodes[i].valid) mark_dirty(c, i);
@@ -2910,7 +2949,7 @@ int gs_reset(gs_ctx* c) {
   if (!rc) rc = ext_flush_devices(c);
   if (rc) return rc;
   if ((rc = node_prep(c))) return rc;
-  hipError_t e = hipStreamSynchronize(c->st);
+  hipError_t e = host_wait_stream(c->st);
   if (e != hipSuccess) return fail(c, GS_EDEVICE, "reset: the device is unusable (%s): destroy and recreate the context",
                                    hipGetErrorString(e));
   c->err.clear();
@@ -2958,9 +2997,9 @@ int gs_debug_pair_probe(gs_ctx* c, const gs_pod* pods, uint32_t npods, const uin
   if (e == hipSuccess) e = hipMemcpy(d_p, pv.data(), sizeof(PodVec) * npods, hipMemcpyHostToDevice);
   if (e == hipSuccess) e = hipMemcpy(d_n, nodes, 4 * n, hipMemcpyHostToDevice);
   if (e == hipSuccess) e = hipMemcpy(d_o, pod_of, 4 * n, hipMemcpyHostToDevice);
-  if (e == hipSuccess) e = hipStreamSynchronize(c->st);
+  if (e == hipSuccess) e = host_wait_stream(c->st);
   if (e == hipSuccess) e = launch_probe(mode, c->mv, c->pf, d_p, (int)npods, d_n, d_o, n, prod_cols, d_s, d_c, c->st);
-  if (e == hipSuccess) e = hipStreamSynchronize(c->st);
+  if (e == hipSuccess) e = host_wait_stream(c->st);
   if (e == hipSuccess) e = hipMemcpy(scores, d_s, 4 * ns, hipMemcpyDeviceToHost);
   if (e == hipSuccess) e = hipMemcpy(cycles, d_c, 80 * n, hipMemcpyDeviceToHost);
   (void)hipFree(d_p); (void)hipFree(d_n); (void)hipFree(d_o); (void)hipFree(d_s); (void)hipFree(d_c);
@@ -2982,9 +3021,9 @@ int gs_debug_numa_merge(gs_ctx* c, const gs_merge_case* cases, uint32_t n, gs_me
   hipError_t e = hipMalloc(&d_c, sizeof(gs_merge_case) * n);
   if (e == hipSuccess) e = hipMalloc(&d_o, sizeof(gs_merge_result) * n);
   if (e == hipSuccess) e = hipMemcpy(d_c, cases, sizeof(gs_merge_case) * n, hipMemcpyHostToDevice);
-  if (e == hipSuccess) e = hipStreamSynchronize(c->st);
+  if (e == hipSuccess) e = host_wait_stream(c->st);
   if (e == hipSuccess) e = launch_merge_probe(d_c, (int)n, d_o, c->st);
-  if (e == hipSuccess) e = hipStreamSynchronize(c->st);
+  if (e == hipSuccess) e = host_wait_stream(c->st);
   if (e == hipSuccess) e = hipMemcpy(out, d_o, sizeof(gs_merge_result) * n, hipMemcpyDeviceToHost);
   (void)hipFree(d_c);
   (void)hipFree(d_o);
@@ -3000,7 +3039,7 @@ int gs_debug_mirror_check(gs_ctx* c) {
   if (rc) return rc;
   std::vector<int64_t> d64((size_t)c->npad * NUM_I64_COLS);
   std::vector<int32_t> d32((size_t)c->npad * NUM_I32_COLS);
-  HIP_TRY(c, hipStreamSynchronize(c->st));
+  HIP_TRY(c, host_wait_stream(c->st));
   HIP_TRY(c, hipMemcpy(d64.data(), c->d_i64, d64.size() * 8, hipMemcpyDeviceToHost));
   HIP_TRY(c, hipMemcpy(d32.data(), c->d_i32, d32.size() * 4, hipMemcpyDeviceToHost));
   int bad = 0;

@@ -101,13 +101,13 @@ def test_two_processes_sharded_schedule_matches_oracle(numa):
 
 
 def test_exchange_sequence_divergence_fails_on_every_rank():
-    """A rank whose exchange sequence diverges (GS_DEBUG_XCHG_SKEW=1:3: rank 1 skips one sequence number at its
-    fourth batch pass) must make EVERY rank fail with GS_ECOMM at that exchange, naming the batch, instead of leaving
+    """A rank whose exchange sequence diverges (GS_DEBUG_XCHG_SKEW=1:1: rank 1 skips one sequence number at its
+    second batch pass) must make EVERY rank fail with GS_ECOMM at that exchange, naming the batch, instead of leaving
     one rank inside a collective the others never enter (the round-4 four-process hang's failure mode)."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, port, True, q, "1:3")) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, port, True, q, "1:1")) for r in range(2)]
     for p in procs:
         p.start()
     res = {}
@@ -120,4 +120,4 @@ def test_exchange_sequence_divergence_fails_on_every_rank():
     for r in range(2):
         msg, code = res[r]
         assert code == -3, f"rank {r}: schedule did not fail ({msg})"
-        assert "exchange sequence diverged" in msg and "batch 3" in msg, f"rank {r}: {msg}"
+        assert "exchange sequence diverged" in msg and "batch 1" in msg, f"rank {r}: {msg}"
