@@ -117,18 +117,24 @@ static_assert(sizeof(SpecLds) + 8 * MAX_BATCH + 160 <= 160 * 1024, "commit_spec_
 // LDS hand-off words between the roles (namespace scope: the role functions below and the kernel share them)
 __shared__ uint64_t s_cpuset[SP_NRES][4];
 __shared__ int32_t s_aff[SP_NRES];
-__shared__ int32_t s_decided, s_stop, s_parked, s_finish, s_cut_at, s_err;
+// the four words the selector checks before every decision, adjacent: one 128-bit LDS read (ld_ctl) instead of four
+// dependent acquire loads
+__shared__ __attribute__((aligned(16))) int32_t s_ctl[4];
+#define s_rb_req s_ctl[0]     // verifier -> wave 0: v + 1 = roll back to pod v (0: none)
+#define s_vend s_ctl[1]       // verifier: the batch's committed count (-1: not yet)
+#define s_verified s_ctl[2]   // verifier: pods verified (wave 0 decides at most SP_LAG ahead of it)
+#define s_cut_at s_ctl[3]     // Reserve: the first pod whose cpuset the host selects (-1: none)
+__shared__ int32_t s_decided, s_stop, s_parked, s_finish, s_err;
 __shared__ int32_t s_werr;        // a verify / Reserve / re-scoring wave's bounded wait expired (its site code)
 __shared__ int32_t s_jq_head[SP_NRES], s_jq_tail[SP_NRES];
-__shared__ int32_t s_verified;    // verifier: pods verified (wave 0 decides at most SP_LAG ahead of it)
-__shared__ int32_t s_rb_req;      // verifier -> wave 0: v + 1 = roll back to pod v (0: none)
 __shared__ int32_t s_rb_at;       // the last rollback's pod (where the parked waves resume)
 __shared__ int32_t s_end_at;      // wave 0: decisions end before this pod (B: every pod)
-__shared__ int32_t s_vend;        // verifier: the batch's committed count (-1: not yet), s_vcut: a host cut ends it
-__shared__ int32_t s_vcut;
+__shared__ int32_t s_vcut;        // verifier: a host cut ends the batch (with s_vend)
 __shared__ int32_t s_committed, s_hostcut, s_nd, s_endwhy;
 __shared__ uint64_t sseq[MAX_BATCH];
 
+// (s_memtime is a scalar-memory instruction: reading its result waits for every LDS operation and scalar load in flight,
+// so a stamp also closes the latency of the prefetches issued before it. HW_REG_SHADER_CYCLES reads 0 on gfx950.)
 #define SPM(i)                                          \
   do {                                                  \
     if (ST) {                                           \
@@ -140,6 +146,13 @@ __shared__ uint64_t sseq[MAX_BATCH];
 
 __device__ __forceinline__ int32_t ld_acq(const int32_t* p) { return __atomic_load_n(p, __ATOMIC_ACQUIRE); }
 __device__ __forceinline__ void st_rel(int32_t* p, int32_t v) { __atomic_store_n(p, v, __ATOMIC_RELEASE); }
+typedef int32_t v4i32 __attribute__((ext_vector_type(4)));
+// s_ctl as one snapshot: a 128-bit LDS read, then acquire (the words are written with release stores)
+__device__ __forceinline__ v4i32 ld_ctl() {
+  const v4i32 v = *reinterpret_cast<const volatile v4i32*>(s_ctl);
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  return v;
+}
 
 
 // ST: diagnostic build — per-role cycle sums (s_memtime) into a.stamps: 0 decide, 1 verify, 2 wave 0 waiting,
@@ -296,8 +309,9 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
     uint32_t spins = 0;
     while (!err) {
       SPM(2);
+      const v4i32 ctl = ld_ctl();   // rb_req, vend, verified, cut_at
       // ------------------------------------------------ a rollback the verifier requested: to pod v
-      if (const int rq = ld_acq(&s_rb_req)) {
+      if (const int rq = ctl.x) {
         const int v = rq - 1;
         if (ST) {
           st_acc[43] += (dec[v].flags & SP_PRED_GE) ? 1 : 0;
@@ -388,7 +402,7 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
         continue;
       }
       {   // the verifier has verified every pod before the batch's end (or a host cut)
-        const int vend = ld_acq(&s_vend);
+        const int vend = ctl.y;
         if (vend >= 0) {
           committed = vend;
           host_cut = ld_acq(&s_vcut) != 0;
@@ -397,7 +411,7 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
       }
       SPM(27);   // rollback / batch-end checks
       // ------------------------------------------------ decide pod q
-      if (q >= end_at || q - ld_acq(&s_verified) >= lag || ld_acq(&s_cut_at) >= 0) {
+      if (q >= end_at || q - ctl.z >= lag || ctl.w >= 0) {
         if (++spins > SP_SPIN_LIMIT) { err = true; err_code = 2; break; }
         if (const int we = ld_acq(&s_werr)) { err = true; err_code = we; break; }
         sp_sleep();
@@ -410,9 +424,20 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
       const int hs = n_hs, hc = n_hc, nlev = n_nlev, feas = n_feas, next = n_next;
       const uint32_t lh = n_lh;
       const int32_t tbv = n_tb;
-      // dirty slots: ready (exact current score) or pending (left out)
-      const int dv0 = lane < nd ? ld_acq(&done_ver[lane]) : -1;
-      const int dv1 = lane + 64 < nd ? ld_acq(&done_ver[lane + 64]) : -1;
+      // dirty slots: ready (exact current score) or pending (left out). The slot versions, then the slots' current and
+      // batch-start scores for pod p, as one group of LDS reads: the wave's LDS reads execute in issue order, so a
+      // current score read after a version that shows its re-scoring complete is that re-scoring's (the re-scoring wave
+      // stores the scores before it releases the version); a pending slot's current score is read and discarded
+      flush_fresh();   // (the fresh slot's batch-start scores of the decision before: stored before they are read)
+      const volatile int32_t* dvv = done_ver;
+      const volatile int16_t* dscv = dsc;
+      const int dv0 = lane < nd ? dvv[lane] : -1;
+      const int dv1 = lane + 64 < nd ? dvv[lane + 64] : -1;
+      const int sc0r = lane < nd ? (int)dscv[p * SB + lane] : -1;
+      const int sc1r = lane + 64 < nd ? (int)dscv[p * SB + 64 + lane] : -1;
+      const int so0r = lane < nd ? (int)dso[p * SB + lane] : -1;
+      const int so1r = lane + 64 < nd ? (int)dso[p * SB + 64 + lane] : -1;
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
       const bool rdy0 = lane < nd && dv0 == pv0, rdy1 = lane + 64 < nd && dv1 == pv1;
       const uint64_t pend0 = __ballot(lane < nd && !rdy0), pend1 = __ballot(lane + 64 < nd && !rdy1);
       if ((a.dbg & 1u) && (pend0 | pend1)) {   // diagnostics: no speculation, wait for the pending rows
@@ -422,10 +447,8 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
       }
       SPM(28);   // dirty-slot state (versions, ballots)
       if (p + 1 < B) load_hdr(p + 1, n_hs, n_hc, n_nlev, n_feas, n_next, n_lh, n_tb);   // consumed by the next decision
-      int sc0 = -1, so0 = -1, sc1 = -1, so1 = -1;
-      flush_fresh();
-      if (lane < nd) { so0 = dso[p * SB + lane]; if (rdy0) sc0 = dsc[p * SB + lane]; }
-      if (lane + 64 < nd) { so1 = dso[p * SB + 64 + lane]; if (rdy1) sc1 = dsc[p * SB + 64 + lane]; }
+      int so0 = so0r, so1 = so1r;
+      const int sc0 = rdy0 ? sc0r : -1, sc1 = rdy1 ? sc1r : -1;
       SPM(29);   // next header's loads issued, pending fresh slot stored, dirty scores loaded
       uint64_t unk0 = 0, unk1 = 0;
       if (multi) {
@@ -491,6 +514,7 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
         // clean listed ties: only at the top clean level (a higher M is a dirty row's: every listed node there is dirty)
         T = (int64_t)(M == Mclean ? ctop : 0) + __popcll(__ballot(nw0)) + __popcll(__ballot(nw1));
         const int64_t jp = tb_pos(p, tbv, T);
+        SPM(30);   // winner: ties, tie-break position
         // level M's segment of the list: offset = listed nodes above it, len = listed nodes at it (0: not listed)
         const uint64_t atm = __ballot(lane < nlev && hs == M);
         const int jm = atm ? __builtin_ctzll(atm) : nlev;
@@ -517,6 +541,7 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
           uint32_t x = 0xffffffffu;
           if (lane < W) x = e < 64 ? fromh : list_ptr(a, 0, p)[e];
           const uint32_t win0 = (uint32_t)__builtin_amdgcn_readlane((int)x, 0);
+          SPM(46);   // winner (old-nodes path): level segment, window of the list
           bool ow = false;
           int base_old = 0;
           each_node(old0, old1, [&](uint32_t n) {

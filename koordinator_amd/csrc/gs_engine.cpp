@@ -1237,8 +1237,10 @@ int launch_batch(gs_ctx* c, int b, const int32_t* prev, const PlacementDev* prev
   // waits on each one) keep it in order on st: the extra queue hop costs more than it hides there.
   hipStream_t rb = b >= 32 ? c->st_rb : c->st;
   if (rb != c->st) HIP_TRY(c, hipStreamWaitEvent(rb, c->ev[4], 0));
-  // (GS_MERGE_RB=0, experiments: the committed words and the placements as two copies)
-  static const bool merge_rb = !(getenv("GS_MERGE_RB") && getenv("GS_MERGE_RB")[0] == '0');
+  // Two copies, not one over the adjacent committed words and placements: with one merged copy, 4 processes sharing the
+  // GPU (the C4 rehearsal) stalled for 10-100 s at a time, every rank's commit and next eval pass pending (DESIGN §8;
+  // GS_MERGE_RB=1 restores the merged copy for that experiment)
+  static const bool merge_rb = getenv("GS_MERGE_RB") && getenv("GS_MERGE_RB")[0] == '1';
   if (merge_rb) {
     HIP_TRY(c, hipMemcpyAsync(c->h_committed, c->d_committed, COMMITTED_BYTES + sizeof(PlacementDev) * b,
                               hipMemcpyDeviceToHost, rb));
@@ -2104,6 +2106,12 @@ int gs_destroy(gs_ctx* c) {
         fprintf(stderr, "  wave 0 total %.0f: checks %.0f | dirty state %.0f | hdr+fresh store+dirty loads %.0f | level scan "
                 "%.0f | winner %.0f | fresh slot %.0f | record %.0f | waiting %.0f (at batch end %.0f) | full-row %.0f\n",
                 W(0, 12), W(0, 27), W(0, 28), W(0, 29), W(0, 18), W(0, 19), W(0, 20), W(0, 0), W(0, 2), W(0, 23), W(0, 11));
+        fprintf(stderr, "  winner split: ties + tie-break position %.0f | old-nodes path: level segment + list window %.0f\n",
+                W(0, 30), W(0, 46));
+        fprintf(stderr, "  wave 0 raw (cycles per pod by stamp index):");
+        for (int i = 0; i < 48; ++i)
+          if (sa[i]) fprintf(stderr, " %d=%.0f", i, W(0, i));
+        fprintf(stderr, "\n");
         const double ng = sa[31] ? (double)sa[31] : 1.0;
         fprintf(stderr, "  winner: old-nodes-only path %llu decisions (%.1f%%), general path %llu (%.1f%%): avg old %.1f new "
                 "%.1f window %.1f; avg dirty slots %.1f; list window beyond 32: %llu, beyond 64: %llu\n",

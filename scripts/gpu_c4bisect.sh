@@ -4,7 +4,8 @@
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-for combo in ${COMBOS:-"0 0" "1 0" "0 1" "1 1"}; do
+IFS=, read -ra combos <<< "${COMBOS:-0 0,1 0,0 1,1 1}"
+for combo in "${combos[@]}"; do
   set -- $combo
   log=gpurun_out/c4bisect_up$1_rb$2.log
   GS_MERGE_UP=$1 GS_MERGE_RB=$2 timeout -k 10 300 python -u -m pytest tests/test_assign_cache.py tests/test_gpu_async.py \

@@ -6,7 +6,7 @@
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-NO_STAMPS=1 AB_ENV="GS_WAIT_BLOCKING=1" bash scripts/gpu_iter5.sh || exit $?
+AB_ENV="GS_WAIT_BLOCKING=1" bash scripts/gpu_iter5.sh || exit $?
 COMBOS="0 1" bash scripts/gpu_c4bisect.sh || exit $?
 timeout -k 10 900 python -u -m pytest tests/test_gpu_c4.py tests/test_gpu_dist.py -m gpu -x -v -s --timeout 300 \
     --timeout-method thread > gpurun_out/c4full.log 2>&1

@@ -24,5 +24,5 @@ done
 if [ -z "$NO_STAMPS" ]; then
   GS_COMMIT_STAMPS=1 timeout -k 10 200 python -u bench.py --steps 5 --warmup 1 --no-cpu-baseline ${BENCH_ARGS} \
       > gpurun_out/stamps.json 2> gpurun_out/stamps.err
-  rc=$?; echo "STAMPS rc=$rc"; grep -A12 "gpuscore spec" gpurun_out/stamps.err
+  rc=$?; echo "STAMPS rc=$rc"; grep -A16 "gpuscore spec" gpurun_out/stamps.err
 fi
