@@ -424,20 +424,9 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
       const int hs = n_hs, hc = n_hc, nlev = n_nlev, feas = n_feas, next = n_next;
       const uint32_t lh = n_lh;
       const int32_t tbv = n_tb;
-      // dirty slots: ready (exact current score) or pending (left out). The slot versions, then the slots' current and
-      // batch-start scores for pod p, as one group of LDS reads: the wave's LDS reads execute in issue order, so a
-      // current score read after a version that shows its re-scoring complete is that re-scoring's (the re-scoring wave
-      // stores the scores before it releases the version); a pending slot's current score is read and discarded
-      flush_fresh();   // (the fresh slot's batch-start scores of the decision before: stored before they are read)
-      const volatile int32_t* dvv = done_ver;
-      const volatile int16_t* dscv = dsc;
-      const int dv0 = lane < nd ? dvv[lane] : -1;
-      const int dv1 = lane + 64 < nd ? dvv[lane + 64] : -1;
-      const int sc0r = lane < nd ? (int)dscv[p * SB + lane] : -1;
-      const int sc1r = lane + 64 < nd ? (int)dscv[p * SB + 64 + lane] : -1;
-      const int so0r = lane < nd ? (int)dso[p * SB + lane] : -1;
-      const int so1r = lane + 64 < nd ? (int)dso[p * SB + 64 + lane] : -1;
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+      // dirty slots: ready (exact current score) or pending (left out)
+      const int dv0 = lane < nd ? ld_acq(&done_ver[lane]) : -1;
+      const int dv1 = lane + 64 < nd ? ld_acq(&done_ver[lane + 64]) : -1;
       const bool rdy0 = lane < nd && dv0 == pv0, rdy1 = lane + 64 < nd && dv1 == pv1;
       const uint64_t pend0 = __ballot(lane < nd && !rdy0), pend1 = __ballot(lane + 64 < nd && !rdy1);
       if ((a.dbg & 1u) && (pend0 | pend1)) {   // diagnostics: no speculation, wait for the pending rows
@@ -447,8 +436,10 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
       }
       SPM(28);   // dirty-slot state (versions, ballots)
       if (p + 1 < B) load_hdr(p + 1, n_hs, n_hc, n_nlev, n_feas, n_next, n_lh, n_tb);   // consumed by the next decision
-      int so0 = so0r, so1 = so1r;
-      const int sc0 = rdy0 ? sc0r : -1, sc1 = rdy1 ? sc1r : -1;
+      int sc0 = -1, so0 = -1, sc1 = -1, so1 = -1;
+      flush_fresh();
+      if (lane < nd) { so0 = dso[p * SB + lane]; if (rdy0) sc0 = dsc[p * SB + lane]; }
+      if (lane + 64 < nd) { so1 = dso[p * SB + 64 + lane]; if (rdy1) sc1 = dsc[p * SB + 64 + lane]; }
       SPM(29);   // next header's loads issued, pending fresh slot stored, dirty scores loaded
       uint64_t unk0 = 0, unk1 = 0;
       if (multi) {
