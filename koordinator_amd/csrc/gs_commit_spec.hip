@@ -60,7 +60,7 @@ constexpr int SP_HASH = 256;     // node -> slot (full-row resolution)
 constexpr int SP_FRESH = 1, SP_FITERR = 2, SP_SLOW = 4, SP_OFFSHARD = 8;   // DecRec.flags
 constexpr int SP_PRED_GE = 16, SP_PRED_GT = 32;   // diagnostics (ST): a pending row's pre-landing score >= / > M
 constexpr uint32_t SP_SPIN_LIMIT = 1u << 24;
-constexpr int SP_NST = 48, SP_STRIDE = 64;   // diagnostics: stamps per wave, the wave's region in a.stamps
+constexpr int SP_NST = 60, SP_STRIDE = 64;   // diagnostics: stamps per wave, the wave's region in a.stamps
 constexpr int16_t SO_UNKNOWN = -2;    // dso: batch-start score of an off-shard fresh row not evaluated yet
 constexpr int16_t SO_UNLISTED = -3;   // a decision's view of such a row not in the pod's list head
 
@@ -81,6 +81,42 @@ struct UndoRec {         // a slot's state before a Reserve
 };
 struct Job {
   int32_t slot, q, range, tbl;
+};
+// the split pipeline (SPLIT): the prep wave's provisional decision of pod p for wave 0
+constexpr int SP_KW = 4;          // ties recorded from the tie-break position on (the window wave 0 re-ranks in)
+constexpr int SP_PREPQ = 2;       // PrepRec ring: the prep wave works at most SP_PREPQ - 1 pods ahead of wave 0
+constexpr int SP_W_PREP = 1;      // its wave (SIMD 1; wave 0 decides on SIMD 0)
+struct PrepRec {                    // (the first 80 bytes read as five 16-byte words)
+  int32_t pod, q_s, nd_s, action;   // q_s: decisions in the snapshot (nd_s slots); action 0, 1 (FitError), 2 (stop),
+                                    // 5: only over the exact state (q_s == pod)
+  int32_t M, Mclean, F, ntw;        // ntw: ties in tw
+  int32_t end_why, slow;            // action 2 (stop; exact snapshots only): why; slow: forced / full-row decision
+  int32_t T_lo, T_hi, jp_lo, jp_hi, pad0, pad1;
+  uint32_t tw[SP_KW];               // the ties ranked jp, jp+1, ... (node ids)
+  uint8_t sf[MAX_BATCH];            // per snapshot slot: SF_* flags
+};
+constexpr int SF_READY = 1, SF_FEAS = 2, SF_TIE = 4, SF_PEND = 8;   // ready (exact score counted), ... feasible, ... at
+                                                                     // M; pending (left out)
+struct Hdr {             // a pod's level header and list head, one value per lane (load_hdr)
+  int hs, hc, nlev, feas, next;
+  uint32_t lh;
+  int32_t tbv;
+};
+struct Dc {              // a decision before it is recorded (decide_core)
+  int action, end_why;   // 0 commit, 1 FitError, 2 stop before the pod, 3 full-row resolution, 4 wait (diagnostics)
+  uint32_t winner;
+  int M, F, Mclean, Md, Fd;
+  int64_t T, jp;
+  bool slowpath;
+  uint64_t pend0, pend1, unk0, unk1;
+  int sc0, sc1, so0, so1;            // per lane: slot lane / lane + 64
+  int sf0, sf1;                      // prep wave, per lane: slot lane / lane + 64's SF_* flags
+  uint32_t twv;                      // prep wave: tie jp + k in lane k
+  int ntw;
+};
+template <bool B_>
+struct Tag {
+  static constexpr bool v = B_;
 };
 
 __device__ __forceinline__ void sp_sleep() { __builtin_amdgcn_s_sleep(2); }
@@ -108,11 +144,14 @@ struct alignas(16) SpecLds {
   alignas(16) int32_t hkey[SP_HASH];
   alignas(16) int16_t hval[SP_HASH];   // slot of the node in hkey
   alignas(16) Job jobq[SP_NRES * SP_JOBQ];
+  alignas(16) PrepRec prq[SP_PREPQ];       // split pipeline: the prep wave's records
+  alignas(16) int32_t slot_node[SB];   // split pipeline: the slot table the prep wave snapshots
+  alignas(16) int16_t slot_pv[SB];
 };
 
 size_t spec_smem_bytes(int) { return sizeof(SpecLds); }
-// the CU's 160 KiB hold SpecLds and the kernel's static __shared__ words (sseq + ~160 B of hand-off words)
-static_assert(sizeof(SpecLds) + 8 * MAX_BATCH + 160 <= 160 * 1024, "commit_spec_kernel LDS over the CU's 160 KiB");
+// the CU's 160 KiB hold SpecLds and the kernel's static __shared__ words (~200 B of hand-off words)
+static_assert(sizeof(SpecLds) + 200 <= 160 * 1024, "commit_spec_kernel LDS over the CU's 160 KiB");
 
 // LDS hand-off words between the roles (namespace scope: the role functions below and the kernel share them)
 __shared__ uint64_t s_cpuset[SP_NRES][4];
@@ -131,7 +170,10 @@ __shared__ int32_t s_rb_at;       // the last rollback's pod (where the parked w
 __shared__ int32_t s_end_at;      // wave 0: decisions end before this pod (B: every pod)
 __shared__ int32_t s_vcut;        // verifier: a host cut ends the batch (with s_vend)
 __shared__ int32_t s_committed, s_hostcut, s_nd, s_endwhy;
-__shared__ uint64_t sseq[MAX_BATCH];
+__shared__ int32_t s_snap;        // split: decisions whose slot table and batch-start scores the prep wave may read
+__shared__ int32_t s_prep_done;   // split: pods the prep wave has recorded
+__shared__ int32_t s_reprep;      // split: wave 0 -> prep wave: p + 1 = record pod p again over the exact state
+__shared__ int32_t s_vlock, s_vwm;   // split, shared verification: the verifier's lock, its re-scored frontier
 
 // (s_memtime is a scalar-memory instruction: reading its result waits for every LDS operation and scalar load in flight,
 // so a stamp also closes the latency of the prefetches issued before it. HW_REG_SHADER_CYCLES reads 0 on gfx950.)
@@ -146,6 +188,10 @@ __shared__ uint64_t sseq[MAX_BATCH];
 
 __device__ __forceinline__ int32_t ld_acq(const int32_t* p) { return __atomic_load_n(p, __ATOMIC_ACQUIRE); }
 __device__ __forceinline__ void st_rel(int32_t* p, int32_t v) { __atomic_store_n(p, v, __ATOMIC_RELEASE); }
+__device__ __forceinline__ uint64_t rfl64(uint64_t x) {   // a uniform 64-bit value into scalar registers
+  return ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(x >> 32)) << 32) |
+         (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)x);
+}
 typedef int32_t v4i32 __attribute__((ext_vector_type(4)));
 // s_ctl as one snapshot: a 128-bit LDS read, then acquire (the words are written with release stores)
 __device__ __forceinline__ v4i32 ld_ctl() {
@@ -158,7 +204,7 @@ __device__ __forceinline__ v4i32 ld_ctl() {
 // ST: diagnostic build — per-role cycle sums (s_memtime) into a.stamps: 0 decide, 1 verify, 2 wave 0 waiting,
 // 3 rollbacks, 4 rollback cycles, 5 Reserve busy, 6 Reserve waiting, 7 re-scoring busy, 8 re-scoring waiting,
 // 9 decisions, 10 full-row decisions, 11 full-row cycles, 12 wave 0 total
-template <bool ST>
+template <bool ST, bool SPLIT>
 __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
   uint64_t st_acc[SP_NST] = {};
   uint64_t st_last = ST ? __builtin_amdgcn_s_memtime() : 0;
@@ -203,7 +249,6 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
   }
   for (int i = tid; i < B; i += SP_THREADS) {
     pods(i) = a.pods[i];
-    sseq[i] = a.seq[i];
     done_ver[i] = -1;
     has_row[i] = 0;
     rescored[i] = 0;
@@ -218,9 +263,523 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
     for (int k = 0; k < SP_NRES; ++k) { s_jq_head[k] = 0; s_jq_tail[k] = 0; }
     s_verified = 0; s_rb_req = 0; s_end_at = B; s_vend = -1; s_vcut = 0;
     s_committed = 0; s_hostcut = 0; s_nd = 0;
+    s_snap = 0; s_prep_done = 0; s_reprep = 0; s_vlock = 0; s_vwm = 0;
   }
   __syncthreads();
 
+
+  // ---- shared by the deciding waves (wave 0; the prep wave of the split pipeline)
+  // header of pod p (lanes 0..7: level j score / count) and the head of its level list (lane i: entry i)
+  // (all LEVALL levels: the LevelHdr's first MAXLEV and the LevelExt's rest)
+  auto load_hdr = [&](int p, Hdr& o) {
+    const LevelHdr* h = hdr_ptr(a, 0, p);
+    const LevelExt* x = reinterpret_cast<const LevelExt*>(a.xbase + (size_t)a.bmax * LCAP * 4 +
+                                                          (size_t)a.bmax * sizeof(LevelHdr)) + p;
+    o.nlev = x->nlev;
+    o.feas = h->feasible;
+    o.next = x->next;
+    o.hs = lane < MAXLEV ? h->score[lane] : lane < LEVALL ? x->score[lane - MAXLEV] : -1;
+    o.hc = lane < MAXLEV ? h->count[lane] : lane < LEVALL ? x->count[lane - MAXLEV] : 0;
+    o.lh = list_ptr(a, 0, p)[lane];
+    o.tbv = a.tb[(size_t)p * TB_N + (lane & (TB_N - 1))];
+  };
+  // tiebreak_position(a.seed, seq[p], T) from pod p's records (tbv, lane k: entry k)
+  auto tb_pos = [&](int p, int32_t tbv, int64_t T) -> int64_t {
+    const int32_t lim = __builtin_amdgcn_readlane(tbv, TB_N - 1);
+    if (T > (int64_t)lim) return tiebreak_position(a.seed, a.seq[p], T);   // (past the records: rare)
+    const int cnt = __popcll(__ballot(lane < TB_N - 1 && tbv != INT32_MAX && (int64_t)tbv <= T));
+    return cnt ? (int64_t)__builtin_amdgcn_readlane(tbv, cnt - 1) : 1;
+  };
+  // selectHost of pod p over its levels and the dirty slots [0, nd) (slot s: node in lane s % 64 of dn0 / dn1, latest
+  // decided version in pv0 / pv1): ready slots with their exact current score, pending ones left out. nh: where the
+  // next pod's header loads go (issued once this pod's dirty-slot state is read); pre_dso: runs before the dso loads.
+  // PREP (the split pipeline's prep wave): also the masks and the tie window the final decision needs (PrepRec).
+  auto decide_core = [&](int p, const Hdr& h, Hdr& nh, bool want_next, auto&& pre_dso, int nd, uint32_t dn0, uint32_t dn1, int32_t pv0,
+                         int32_t pv1, auto prep_tag, Dc& r) {
+    constexpr bool PREP = decltype(prep_tag)::v;
+    const int hs = h.hs, hc = h.hc, nlev = h.nlev, feas = h.feas, next = h.next;
+    const uint32_t lh = h.lh;
+    const int32_t tbv = h.tbv;
+    auto each_node = [&](uint64_t m0, uint64_t m1, auto&& fn) {
+      for (uint64_t b = m0; b; b &= b - 1) fn((uint32_t)__builtin_amdgcn_readlane((int)dn0, __builtin_ctzll(b)));
+      for (uint64_t b = m1; b; b &= b - 1) fn((uint32_t)__builtin_amdgcn_readlane((int)dn1, __builtin_ctzll(b)));
+    };
+    r.action = 0;
+    r.end_why = 0;
+    r.winner = 0xffffffffu;
+    r.ntw = 0;
+    r.twv = 0xffffffffu;
+    // dirty slots: ready (exact current score) or pending (left out)
+    const int dv0 = lane < nd ? ld_acq(&done_ver[lane]) : -1;
+    const int dv1 = lane + 64 < nd ? ld_acq(&done_ver[lane + 64]) : -1;
+    const bool rdy0 = lane < nd && dv0 == pv0, rdy1 = lane + 64 < nd && dv1 == pv1;
+    const uint64_t pend0 = __ballot(lane < nd && !rdy0), pend1 = __ballot(lane + 64 < nd && !rdy1);
+    r.pend0 = pend0;
+    r.pend1 = pend1;
+    if ((a.dbg & 1u) && (pend0 | pend1)) {   // diagnostics: no speculation, wait for the pending rows
+      r.action = 4;
+      return;
+    }
+    SPM(28);   // dirty-slot state (versions, ballots)
+    if (want_next && p + 1 < B) load_hdr(p + 1, nh);   // consumed by the next decision
+    int sc0 = -1, so0 = -1, sc1 = -1, so1 = -1;
+    pre_dso();
+    if (lane < nd) { so0 = dso[p * SB + lane]; if (rdy0) sc0 = dsc[p * SB + lane]; }
+    if (lane + 64 < nd) { so1 = dso[p * SB + 64 + lane]; if (rdy1) sc1 = dsc[p * SB + 64 + lane]; }
+    SPM(29);   // next header's loads issued, pending fresh slot stored, dirty scores loaded
+    uint64_t unk0 = 0, unk1 = 0;
+    if (multi) {
+      // off-shard fresh rows whose batch-start job has not finished: a node in the list head has its listed level
+      // as batch-start score (exact); any other is unknown, counted as clean and unlisted (checked at verification)
+      const uint64_t u0 = __ballot(lane < nd && so0 == SO_UNKNOWN), u1 = __ballot(lane + 64 < nd && so1 == SO_UNKNOWN);
+      if (u0 | u1) {
+        const int incl = wave_incl_scan(lane < nlev ? hc : 0);   // list end of level `lane`
+        const int listed = __builtin_amdgcn_readlane(incl, 63);
+        for (int pass = 0; pass < 2; ++pass)
+          for (uint64_t bb = pass ? u1 : u0; bb; bb &= bb - 1) {
+            const int s = __builtin_ctzll(bb);
+            const uint32_t nn = (uint32_t)__builtin_amdgcn_readlane((int)(pass ? dn1 : dn0), s);
+            const uint64_t f = __ballot(lane < listed && lh == nn);
+            int sv = SO_UNLISTED;
+            if (f) {
+              const int e = __builtin_ctzll(f);
+              sv = __builtin_amdgcn_readlane(hs, __popcll(__ballot(lane < nlev && incl <= e)));
+            } else if (pass) {
+              unk1 |= 1ull << s;
+            } else {
+              unk0 |= 1ull << s;
+            }
+            if (lane == s) { if (pass) so1 = sv; else so0 = sv; }
+          }
+      }
+    }
+    r.unk0 = unk0;
+    r.unk1 = unk1;
+    // action 0 commit, 1 FitError, 2 stop deciding before p, 3 full-row resolution (wave 0)
+    int action = 0;
+    uint32_t winner = 0xffffffffu;
+    int M = -1, F = 0;
+    int64_t T = 0, jp = 0;
+    bool slowpath = p == 0 && a.forced_node >= 0;
+    // the highest listed level that still holds a clean node: listed count minus the dirty rows listed there (their
+    // batch-start score), from the top (usually the first level)
+    int ctop = 0, Mclean = -1;
+    for (int j = 0; j < nlev; ++j) {
+      const int sj = __builtin_amdgcn_readlane(hs, j), cj = __builtin_amdgcn_readlane(hc, j);
+      const int dj = __popcll(__ballot(so0 == sj)) + __popcll(__ballot(so1 == sj));
+      if (cj > dj) { ctop = cj - dj; Mclean = sj; break; }
+    }
+    const int Md = wave_max(max(sc0, sc1));
+    const int Fd = wave_sum((sc0 >= 0) - (so0 >= 0) + (sc1 >= 0) - (so1 >= 0));
+    M = max(Mclean, Md);
+    F = Fd + feas;
+    SPM(18);   // decide: dirty-slot state, level scan
+    if (slowpath) {
+      M = a.forced_score;
+      F = a.forced_feasible;
+      T = a.forced_ties;
+      winner = (uint32_t)a.forced_node;
+    } else if (M < 0 && next < 0) {
+      action = 1;   // every feasible node is listed, none clean, no dirty row feasible: FitError
+    } else if (M <= next) {
+      action = a.S != nullptr ? 3 : 2;
+      if (action == 2) r.end_why = 3;
+      if (ST) st_acc[M < 0 ? 13 : 14] += 1;
+    } else if (M < 0) {
+      action = 1;
+    } else {
+      const bool nw0 = sc0 == M, nw1 = sc1 == M;
+      // clean listed ties: only at the top clean level (a higher M is a dirty row's: every listed node there is dirty)
+      T = (int64_t)(M == Mclean ? ctop : 0) + __popcll(__ballot(nw0)) + __popcll(__ballot(nw1));
+      jp = tb_pos(p, tbv, T);
+      if (ST && !PREP && !SPLIT && p > 0 && !(dec[p - 1].flags & SP_FITERR)) {
+        // diagnostics: a decision made before pod p-1's landing was known (its row as it stood) vs this one
+        const DecRec& pd = dec[p - 1];
+        const int sl = pd.slot;
+        const int ov = (pd.flags & SP_FRESH) ? __builtin_amdgcn_readlane(sl < 64 ? so0 : so1, sl & 63)
+                                              : (int)dsc[p * SB + sl];
+        st_acc[47] += 1;
+        st_acc[48] += ov > M ? 1 : 0;
+        st_acc[49] += ov == M ? 1 : 0;
+        st_acc[50] += (ov == M && tb_pos(p, tbv, T + 1) != jp) ? 1 : 0;
+      }
+      SPM(30);   // winner: ties, tie-break position
+      // level M's segment of the list: offset = listed nodes above it, len = listed nodes at it (0: not listed)
+      const uint64_t atm = __ballot(lane < nlev && hs == M);
+      const int jm = atm ? __builtin_ctzll(atm) : nlev;
+      const int len = atm ? __builtin_amdgcn_readlane(hc, jm) : 0;
+      const int off = wave_sum(lane < jm && lane < nlev ? hc : 0);
+      const uint64_t new0 = __ballot(nw0), new1 = __ballot(nw1);
+      const uint64_t old0 = __ballot(so0 == M && lane < nd), old1 = __ballot(so1 == M && lane + 64 < nd);
+      const int nnew = __popcll(new0) + __popcll(new1), nold = __popcll(old0) + __popcll(old1);
+      if (nnew == 0 && nold == 0) {
+        // no dirty row at M (then level M is listed: M is its clean level): the jp-th listed node of level M
+        const int e = off + (int)jp - 1;
+        winner = e < 64 ? (uint32_t)__builtin_amdgcn_readlane((int)lh, e) : list_ptr(a, 0, p)[e];
+        if (PREP) {   // the ties after it: listed nodes e+1, e+2, ...
+          const int nk = (int)min<int64_t>(SP_KW, T - jp + 1);
+          const int ek = e + lane;
+          const uint32_t fromh = (uint32_t)__shfl((int)lh, ek & 63);
+          if (lane < nk) r.twv = ek < 64 ? fromh : list_ptr(a, 0, p)[ek];
+          r.ntw = nk;
+        }
+        if (ST) { st_acc[24] += e >= 32 ? 1 : 0; st_acc[25] += e >= 64 ? 1 : 0; }
+      } else if (nnew == 0 && nold <= 61 - (PREP ? SP_KW - 1 : 0)) {
+        // only listed nodes at M, some of them dirty rows no longer at M ("old"; the common case): the jp-th of the
+        // others in list order lies in the window [jp-2, jp-1+nold] of level M's segment (<= 64 entries, one per
+        // lane); old nodes before the window are those with a lower node id (the segment is in node order)
+        if (ST) { st_acc[36] += 1; st_acc[32] += nold; }
+        const int lo = (int)max<int64_t>(0, jp - 2);
+        const int hi = (int)min<int64_t>(len - 1, jp - 1 + nold + (PREP ? SP_KW - 1 : 0));
+        const int W = hi - lo + 1;
+        const int e = off + lo + lane;
+        const uint32_t fromh = (uint32_t)__shfl((int)lh, e & 63);
+        uint32_t x = 0xffffffffu;
+        if (lane < W) x = e < 64 ? fromh : list_ptr(a, 0, p)[e];
+        const uint32_t win0 = (uint32_t)__builtin_amdgcn_readlane((int)x, 0);
+        SPM(46);   // winner (old-nodes path): level segment, window of the list
+        bool ow = false;
+        int base_old = 0;
+        each_node(old0, old1, [&](uint32_t n) {
+          base_old += n < win0 ? 1 : 0;
+          ow |= x == n;
+        });
+        const uint64_t bo = __ballot(lane < W && ow);
+        const int older = base_old + __popcll(bo & lt_mask);
+        const int64_t rk = (int64_t)(lo + lane - older + 1);   // the lane's rank among the ties
+        const uint64_t hit = __ballot(lane < W && !ow && rk == jp);
+        if (ST) { st_acc[24] += off + hi >= 32 ? 1 : 0; st_acc[25] += off + hi >= 64 ? 1 : 0; }
+        if (!hit) { action = 2; r.end_why = 1; }
+        else winner = (uint32_t)__builtin_amdgcn_readlane((int)x, __builtin_ctzll(hit));
+        if (PREP && hit) {   // the ties ranked jp .. jp+SP_KW-1
+          r.twv = winner;
+          int k = 1;
+          for (; k < SP_KW; ++k) {
+            const uint64_t hk = __ballot(lane < W && !ow && rk == jp + k);
+            if (!hk) break;
+            const uint32_t xk = (uint32_t)__builtin_amdgcn_readlane((int)x, __builtin_ctzll(hk));
+            if (lane == k) r.twv = xk;
+          }
+          r.ntw = k;
+        }
+      } else {
+        if (ST) { st_acc[31] += 1; st_acc[32] += nold; st_acc[33] += nnew; }
+        const int lo = (int)max<int64_t>(0, jp - 2 - nnew);
+        const int hi = (int)min<int64_t>(len - 1, jp - 1 + nold);
+        const int W = hi - lo + 1;
+        if (ST) st_acc[34] += W > 0 ? W : 0;
+        const uint32_t* L = list_ptr(a, 0, p);
+        constexpr int WCH = (2 * MAX_BATCH + 2 + 63) / 64;
+        uint32_t xw[WCH];
+        bool ow[WCH];
+        uint32_t cand = 0xffffffffu;
+        int base_old = 0;
+        if (len > 0) {
+#pragma unroll
+          for (int c = 0; c < WCH; ++c) {
+            const int i = c * 64 + lane, e = off + lo + i;
+            const uint32_t fromh = (uint32_t)__shfl((int)lh, e & 63);
+            xw[c] = 0xffffffffu;
+            if (c * 64 < W && i < W) xw[c] = e < 64 ? fromh : L[e];
+          }
+          if (ST) { st_acc[24] += off + hi >= 32 ? 1 : 0; st_acc[25] += off + hi >= 64 ? 1 : 0; }
+          const uint32_t win0 = (uint32_t)__builtin_amdgcn_readlane((int)xw[0], 0);
+#pragma unroll
+          for (int c = 0; c < WCH; ++c) ow[c] = false;
+          each_node(old0, old1, [&](uint32_t n) {
+            base_old += n < win0 ? 1 : 0;
+#pragma unroll
+            for (int c = 0; c < WCH; ++c) ow[c] |= xw[c] == n;
+          });
+          int running = base_old;
+#pragma unroll
+          for (int c = 0; c < WCH; ++c) {
+            if (c * 64 >= W) break;
+            const int i = c * 64 + lane;
+            const bool valid = i < W;
+            const uint64_t bo = __ballot(valid && ow[c]);
+            const int older = running + __popcll(bo & lt_mask);
+            int newer = 0;
+            each_node(new0, new1, [&](uint32_t n) { newer += n < xw[c] ? 1 : 0; });
+            if (valid && !ow[c] && (int64_t)(lo + i - older + newer + 1) == jp) cand = xw[c];
+            running += __popcll(bo);
+          }
+        }
+        each_node(new0, new1, [&](uint32_t n) {
+          int u = 0;
+          each_node(new0, new1, [&](uint32_t n2) { u += n2 < n ? 1 : 0; });
+          int64_t ltn = -1;
+          int older = 0;
+          if (len == 0) {
+            ltn = 0;
+          } else {
+            int pp = 0;
+#pragma unroll
+            for (int c = 0; c < WCH; ++c) {
+              if (c * 64 >= W) break;
+              const bool valid = c * 64 + lane < W;
+              pp += __popcll(__ballot(valid && xw[c] < n));
+              older += __popcll(__ballot(valid && ow[c] && xw[c] < n));
+            }
+            older += base_old;
+            if (pp == 0) ltn = (lo == 0) ? 0 : -1;
+            else if (pp == W) ltn = (hi == len - 1) ? len : -1;
+            else ltn = lo + pp;
+          }
+          if (ltn >= 0 && ltn - older + u + 1 == jp) cand = n;
+        });
+        const uint64_t got = __ballot(cand != 0xffffffffu);
+        if (!got) { action = 2; r.end_why = 1; }
+        else winner = (uint32_t)__builtin_amdgcn_readlane((int)cand, __ffsll((long long)got) - 1);
+        if (PREP && got) {   // the window is the winner alone: any tie excluded before it leaves p to wave 0
+          r.twv = winner;
+          r.ntw = 1;
+        }
+      }
+    }
+    SPM(19);   // decide: tie-break position, winner among listed + dirty ties
+    r.action = action;
+    r.winner = winner;
+    r.M = M;
+    r.F = F;
+    r.T = T;
+    r.jp = jp;
+    r.slowpath = slowpath;
+    r.Mclean = Mclean;
+    r.Md = Md;
+    r.Fd = Fd;
+    r.sc0 = sc0;
+    r.sc1 = sc1;
+    r.so0 = so0;
+    r.so1 = so1;
+    if (PREP) {
+      const bool tok = M >= 0 && action == 0;
+      r.sf0 = (rdy0 ? SF_READY : 0) | (sc0 >= 0 ? SF_FEAS : 0) | (tok && sc0 == M ? SF_TIE : 0) |
+              (lane < nd && !rdy0 ? SF_PEND : 0);
+      r.sf1 = (rdy1 ? SF_READY : 0) | (sc1 >= 0 ? SF_FEAS : 0) | (tok && sc1 == M ? SF_TIE : 0) |
+              (lane + 64 < nd && !rdy1 ? SF_PEND : 0);
+    }
+  };
+
+  // node -> slot hash, needed only by the full-row resolution: rebuilt there when slots changed since (one lane per
+  // slot; an LDS compare-and-swap claims a probe position, and a key only moves past occupied positions, so
+  // linear-probe lookups find it)
+  auto rebuild_hash = [&](int nd, uint32_t dn0, uint32_t dn1) {
+    for (int i = lane; i < SP_HASH; i += 64) { hkey[i] = -1; hval[i] = -1; }
+    WAVE_FENCE();
+    for (int half = 0; half < 2; ++half) {
+      bool todo = lane + 64 * half < nd;
+      const uint32_t nn = half ? dn1 : dn0;
+      uint32_t h = (nn * 2654435761u) & (SP_HASH - 1);
+      while (todo) {
+        if (atomicCAS(&hkey[h], -1, (int32_t)nn) == -1) {
+          hval[h] = (int16_t)(lane + 64 * half);
+          todo = false;
+        } else {
+          h = (h + 1) & (SP_HASH - 1);
+        }
+      }
+      WAVE_FENCE();
+    }
+  };
+  auto sp_hash_find = [&](uint32_t node) -> int {
+    uint32_t h = (node * 2654435761u) & (SP_HASH - 1);
+    for (int probe = 0; probe < SP_HASH; ++probe) {
+      const int kk = hkey[h];
+      if (kk == (int)node) return hval[h];
+      if (kk < 0) return -1;
+      h = (h + 1) & (SP_HASH - 1);
+    }
+    return -1;
+  };
+  // ------------------------------------------------ exact resolution of pod p from its whole score row
+  // batch-start S[p][*] for clean nodes, the current score for ready dirty rows, pending rows left out (verified
+  // later like any decision)
+  auto full_row_resolve = [&](int p, int32_t tbv, Dc& r, int nd, uint32_t dn0, uint32_t dn1, bool& hash_ok) {
+    if (!hash_ok) {
+      rebuild_hash(nd, dn0, dn1);
+      hash_ok = true;
+    }
+    auto each_node = [&](uint64_t m0, uint64_t m1, auto&& fn) {
+      for (uint64_t b = m0; b; b &= b - 1) fn((uint32_t)__builtin_amdgcn_readlane((int)dn0, __builtin_ctzll(b)));
+      for (uint64_t b = m1; b; b &= b - 1) fn((uint32_t)__builtin_amdgcn_readlane((int)dn1, __builtin_ctzll(b)));
+    };
+    const int sc0 = r.sc0, sc1 = r.sc1, so0 = r.so0, so1 = r.so1, Md = r.Md, Fd = r.Fd;
+    const int16_t* row = a.S + (size_t)p * a.ld;
+    const uint32_t len = a.own1 - a.own0;
+    constexpr int VB = 8;
+    auto load_blk = [&](uint32_t i0, int16_t (&x)[8]) {
+      if (i0 + 8 <= len) {
+        const uint4 vv = *reinterpret_cast<const uint4*>(row + i0);
+        const uint32_t w[4] = {vv.x, vv.y, vv.z, vv.w};
+#pragma unroll
+        for (int k = 0; k < 8; ++k) x[k] = (int16_t)(w[k >> 1] >> (16 * (k & 1)));
+      } else {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) x[k] = i0 + k < len ? row[i0 + k] : (int16_t)-1;
+      }
+    };
+    int lmax = -1, lcnt = 0, lfeas = 0;
+    for (uint32_t b0 = 0; b0 < len; b0 += 512u * VB) {
+      int16_t x[VB][8];
+#pragma unroll
+      for (int u = 0; u < VB; ++u) load_blk(b0 + 512u * u + 8u * lane, x[u]);
+#pragma unroll
+      for (int u = 0; u < VB; ++u)
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const int xv = x[u][k];
+          lfeas += xv >= 0 ? 1 : 0;
+          lcnt = xv > lmax ? 1 : lcnt + (xv == lmax ? 1 : 0);
+          lmax = xv > lmax ? xv : lmax;
+        }
+    }
+    r.F = wave_sum(lfeas) + Fd;
+    int Mc = wave_max(lmax);
+    int64_t Tc = Mc >= 0 ? (int64_t)wave_sum(lmax == Mc ? lcnt : 0) - __popcll(__ballot(lane < nd && so0 == Mc)) -
+                               __popcll(__ballot(lane + 64 < nd && so1 == Mc))
+                         : 0;
+    if (Mc >= 0 && Tc <= 0) {
+      lmax = -1;
+      lcnt = 0;
+      for (uint32_t b0 = 0; b0 < len; b0 += 512u * VB) {
+        int16_t x[VB][8];
+#pragma unroll
+        for (int u = 0; u < VB; ++u) load_blk(b0 + 512u * u + 8u * lane, x[u]);
+#pragma unroll
+        for (int u = 0; u < VB; ++u)
+#pragma unroll
+          for (int k = 0; k < 8; ++k) {
+            const int xv = x[u][k];
+            if (xv >= 0 && xv >= lmax && sp_hash_find(a.own0 + b0 + 512u * u + 8u * lane + k) < 0) {
+              lcnt = xv > lmax ? 1 : lcnt + 1;
+              lmax = xv;
+            }
+          }
+      }
+      Mc = wave_max(lmax);
+      Tc = Mc >= 0 ? (int64_t)wave_sum(lmax == Mc ? lcnt : 0) : 0;
+    }
+    const int M = max(Mc, Md);
+    r.M = M;
+    if (M < 0) {
+      r.action = 1;
+      return;
+    }
+    const uint64_t new0 = __ballot(sc0 == M), new1 = __ballot(sc1 == M);
+    const uint64_t old0 = __ballot(lane < nd && so0 == M), old1 = __ballot(lane + 64 < nd && so1 == M);
+    const int64_t T = (Mc == M ? Tc : 0) + __popcll(new0) + __popcll(new1);
+    r.T = T;
+    const int64_t jp = tb_pos(p, tbv, T);
+    int64_t run = 0;
+    int64_t found = -1;
+    for (uint32_t b0 = 0; b0 < len && found == -1; b0 += 512u * VB) {
+      int16_t x[VB][8];
+#pragma unroll
+      for (int u = 0; u < VB; ++u) load_blk(b0 + 512u * u + 8u * lane, x[u]);
+#pragma unroll
+      for (int u = 0; u < VB; ++u) {
+        const uint32_t i0 = b0 + 512u * u;
+        uint32_t fl = 0;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) fl |= (x[u][k] == M ? 1u : 0u) << k;
+        const bool in0 = dn0 - a.own0 - i0 < 512u, in1 = dn1 - a.own0 - i0 < 512u;
+        const uint64_t bn0 = new0 & __ballot(in0), bn1 = new1 & __ballot(in1);
+        const uint64_t bo0 = old0 & __ballot(in0), bo1 = old1 & __ballot(in1);
+        const int tot = wave_sum(__popc(fl)) + __popcll(bn0) + __popcll(bn1) - __popcll(bo0) - __popcll(bo1);
+        if (found == -1 && run + tot >= jp) {
+          each_node(bo0, bo1, [&](uint32_t nn) {
+            const uint32_t o = nn - a.own0 - i0;
+            if ((uint32_t)lane == (o >> 3)) fl &= ~(1u << (o & 7u));
+          });
+          each_node(bn0, bn1, [&](uint32_t nn) {
+            const uint32_t o = nn - a.own0 - i0;
+            if ((uint32_t)lane == (o >> 3)) fl |= 1u << (o & 7u);
+          });
+          const int c = __popc(fl);
+          const int incl = wave_incl_scan(c);
+          int64_t need = jp - (run + incl - c);
+          int64_t f = -1;
+          if (need >= 1 && need <= c) {
+            uint32_t bits = fl;
+            while (--need) bits &= bits - 1;
+            f = (int64_t)(a.own0 + i0 + 8u * lane + (uint32_t)__builtin_ctz(bits));
+          }
+          const uint64_t gg = __ballot(f >= 0);
+          found = gg ? (int64_t)__builtin_amdgcn_readlane((int)f, __ffsll((long long)gg) - 1) : -2;
+        }
+        run += tot;
+      }
+    }
+    if (found < 0) {
+      r.action = 2;
+      r.end_why = 2;
+      const int osl = old0 ? __builtin_ctzll(old0) : old1 ? 64 + __builtin_ctzll(old1) : -1;
+      const uint32_t onode = osl < 0 ? 0u : (uint32_t)__builtin_amdgcn_readlane((int)(osl < 64 ? dn0 : dn1), osl & 63);
+      const int ohash = osl < 0 ? -9 : sp_hash_find(onode);
+      const int osv = osl < 0 ? -9 : (int)a.S[(size_t)p * a.ld + (onode - a.own0)];
+      const int odso = osl < 0 ? -9 : (int)dso[p * SB + osl];
+      if (lane == 0)   // diagnostics (GS_DEBUG_CUTS): the inconsistent tie count
+        a.out[p] = PlacementDev{-7, (uint32_t)run, (int64_t)M | ((int64_t)Mc << 20) | ((int64_t)Md << 40), (uint32_t)T,
+                                (uint32_t)Tc, (uint32_t)(__popcll(new0) + __popcll(new1)),
+                                (uint32_t)(__popcll(old0) + __popcll(old1)), {(int64_t)jp, (int64_t)nd, (int64_t)__popcll(r.pend0), 0}, {0, 0, 0, 0},
+                                {(uint64_t)osl, (uint64_t)onode, (uint64_t)(int64_t)ohash,
+                                 (uint64_t)(((int64_t)osv << 32) | (uint32_t)odso)}};
+    } else {
+      r.action = 0;
+      r.winner = (uint32_t)found;
+    }
+    r.slowpath = true;
+  };
+  // split pipeline, shared verification (dbg bit 17): the decided pods verified in order by whichever wave holds the
+  // lock — the re-scoring and Reserve waves when they complete a pod's re-scoring, wave 0 while it waits. Same rule
+  // as the verify wave: pod v stands iff every row pending at its decision now scores below its maximum for it (its
+  // feasible ones join the Feasible count); a miss asks wave 0 to roll back to v (s_rb_req).
+  const bool vshare = SPLIT && ((a.dbg >> 17) & 1u);
+  auto verify_try = [&]() {
+    int got = 0;
+    if (lane == 0) {
+      int expect = 0;
+      got = __atomic_compare_exchange_n(&s_vlock, &expect, 1, false, __ATOMIC_ACQUIRE, __ATOMIC_RELAXED) ? 1 : 0;
+    }
+    if (!__builtin_amdgcn_readfirstlane(got)) return;
+    if (!ld_acq(&s_rb_req) && !ld_acq(&s_stop)) {
+      int v = ld_acq(&s_verified), wm = ld_acq(&s_vwm);
+      const int qd = ld_acq(&s_decided);
+      while (wm < qd && ld_acq(&rescored[wm])) ++wm;
+      const int cut_v = ld_acq(&s_cut_at);   // (after the frontier: a cut is published before its pod is re-scored)
+      while (v < qd && v <= wm) {
+        if (cut_v >= 0 && v > cut_v) break;
+        const DecRec& d = dec[v];
+        const uint64_t dp0 = d.pend0, dp1 = d.pend1;
+        const int dM = d.M;
+        int mis = 0, fadd = 0;
+        if ((dp0 >> lane) & 1ull) {
+          const int sc = dsc[v * SB + lane];
+          mis |= sc >= 0 && sc >= dM;
+          fadd += sc >= 0;
+        }
+        if ((dp1 >> lane) & 1ull) {
+          const int sc = dsc[v * SB + 64 + lane];
+          mis |= sc >= 0 && sc >= dM;
+          fadd += sc >= 0;
+        }
+        if (__ballot(mis)) {
+          if (lane == 0) st_rel(&s_rb_req, v + 1);
+          break;
+        }
+        const int F = d.F + wave_sum(fadd);
+        if (lane == 0) final_F[v] = F;
+        ++v;
+      }
+      if (lane == 0) {
+        s_vwm = wm;
+        st_rel(&s_verified, v);
+      }
+    }
+    WAVE_FENCE();
+    if (lane == 0) st_rel(&s_vlock, 0);
+  };
 
   if (wv == 0) {
     // ==================================================== decide ====================================================
@@ -233,64 +792,7 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
     int committed = 0;
     bool host_cut = false, err = false;
     int err_code = 0;   // which bounded wait expired (reported in committed[3])
-    auto each_node = [&](uint64_t m0, uint64_t m1, auto&& fn) {
-      for (uint64_t b = m0; b; b &= b - 1) fn((uint32_t)__builtin_amdgcn_readlane((int)dn0, __builtin_ctzll(b)));
-      for (uint64_t b = m1; b; b &= b - 1) fn((uint32_t)__builtin_amdgcn_readlane((int)dn1, __builtin_ctzll(b)));
-    };
-    // node -> slot hash, needed only by the full-row resolution: rebuilt there when slots changed since (one lane per
-    // slot; an LDS compare-and-swap claims a probe position, and a key only moves past occupied positions, so
-    // linear-probe lookups find it)
-    bool hash_ok = true;
-    auto rebuild_hash = [&]() {
-      for (int i = lane; i < SP_HASH; i += 64) { hkey[i] = -1; hval[i] = -1; }
-      WAVE_FENCE();
-      for (int half = 0; half < 2; ++half) {
-        bool todo = lane + 64 * half < nd;
-        const uint32_t nn = half ? dn1 : dn0;
-        uint32_t h = (nn * 2654435761u) & (SP_HASH - 1);
-        while (todo) {
-          if (atomicCAS(&hkey[h], -1, (int32_t)nn) == -1) {
-            hval[h] = (int16_t)(lane + 64 * half);
-            todo = false;
-          } else {
-            h = (h + 1) & (SP_HASH - 1);
-          }
-        }
-        WAVE_FENCE();
-      }
-      hash_ok = true;
-    };
-    auto sp_hash_find = [&](uint32_t node) -> int {
-      uint32_t h = (node * 2654435761u) & (SP_HASH - 1);
-      for (int probe = 0; probe < SP_HASH; ++probe) {
-        const int kk = hkey[h];
-        if (kk == (int)node) return hval[h];
-        if (kk < 0) return -1;
-        h = (h + 1) & (SP_HASH - 1);
-      }
-      return -1;
-    };
-    // header of pod p (lanes 0..7: level j score / count) and the head of its level list (lane i: entry i)
-    // (all LEVALL levels: the LevelHdr's first MAXLEV and the LevelExt's rest)
-    auto load_hdr = [&](int p, int& hs, int& hc, int& nlev, int& feas, int& next, uint32_t& lh, int32_t& tbv) {
-      const LevelHdr* h = hdr_ptr(a, 0, p);
-      const LevelExt* x = reinterpret_cast<const LevelExt*>(a.xbase + (size_t)a.bmax * LCAP * 4 +
-                                                            (size_t)a.bmax * sizeof(LevelHdr)) + p;
-      nlev = x->nlev;
-      feas = h->feasible;
-      next = x->next;
-      hs = lane < MAXLEV ? h->score[lane] : lane < LEVALL ? x->score[lane - MAXLEV] : -1;
-      hc = lane < MAXLEV ? h->count[lane] : lane < LEVALL ? x->count[lane - MAXLEV] : 0;
-      lh = list_ptr(a, 0, p)[lane];
-      tbv = a.tb[(size_t)p * TB_N + (lane & (TB_N - 1))];
-    };
-    // tiebreak_position(a.seed, sseq[p], T) from pod p's records (tbv, lane k: entry k)
-    auto tb_pos = [&](int p, int32_t tbv, int64_t T) -> int64_t {
-      const int32_t lim = __builtin_amdgcn_readlane(tbv, TB_N - 1);
-      if (T > (int64_t)lim) return tiebreak_position(a.seed, sseq[p], T);
-      const int cnt = __popcll(__ballot(lane < TB_N - 1 && tbv != INT32_MAX && (int64_t)tbv <= T));
-      return cnt ? (int64_t)__builtin_amdgcn_readlane(tbv, cnt - 1) : 1;
-    };
+    bool hash_ok = true;   // the node -> slot hash matches the slots (full-row resolution)
     // a fresh slot's batch-start scores for the later pods (S_own column loads), issued when the slot is created and
     // stored into dso by the next decision (the loads' latency hides behind the verification in between)
     int ps_slot = -1, ps_p = 0;
@@ -302,475 +804,134 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
       if (q1 < B) dso[q1 * SB + ps_slot] = ps_v1;
       ps_slot = -1;
     };
-    int n_hs = -1, n_hc = 0, n_nlev = 0, n_feas = 0, n_next = -1;
-    uint32_t n_lh = 0xffffffffu;
-    int32_t n_tb = 1;
-    load_hdr(0, n_hs, n_hc, n_nlev, n_feas, n_next, n_lh, n_tb);
+    Hdr nh{-1, 0, 0, 0, -1, 0xffffffffu, 1};
+    if (!SPLIT) load_hdr(0, nh);
     uint32_t spins = 0;
-    while (!err) {
-      SPM(2);
-      const v4i32 ctl = ld_ctl();   // rb_req, vend, verified, cut_at
-      // ------------------------------------------------ a rollback the verifier requested: to pod v
-      if (const int rq = ctl.x) {
-        const int v = rq - 1;
-        if (ST) {
-          st_acc[43] += (dec[v].flags & SP_PRED_GE) ? 1 : 0;
-          st_acc[45] += (dec[v].flags & SP_PRED_GT) ? 1 : 0;
-        }
-        // park the other waves, undo the Reserves of pods >= v (newest first: the two Reserve waves finish pods out of
-        // order, so by their flags), restore the slot versions
-        st_rel(&s_stop, 1);
-        spins = 0;
-        while (ld_acq(&s_parked) < SP_WAVES - 1) {
-          if (++spins > SP_SPIN_LIMIT) { err = true; err_code = 1; break; }
-          sp_sleep();
-        }
-        if (err) break;
-        SPM(37);   // rollback: parking the other waves
-        if (ST) st_acc[41] += q - v;
-        for (int qq = q - 1; qq >= v; --qq) {
-          if (!resv[qq] || (dec[qq].flags & SP_FITERR)) continue;
-          const UndoRec& u = undo[qq % SP_LAG];
-          const int sl = u.slot;
-          const uint64_t* src = reinterpret_cast<const uint64_t*>(&u.row);
-          uint64_t* dst = reinterpret_cast<uint64_t*>(&drows[sl]);
-          for (int i = lane; i < (int)(sizeof(Row) / 8); i += 64) dst[i] = src[i];
-          const uint64_t* s2 = reinterpret_cast<const uint64_t*>(&u.cs);
-          uint64_t* d2 = reinterpret_cast<uint64_t*>(&cst[sl]);
-          for (int i = lane; i < (int)(sizeof(CpuStateDev) / 8); i += 64) d2[i] = s2[i];
+    int ver = 0, wm = 0;   // split pipeline: pods verified here, the re-scored frontier
+    // ------------------------------------------------ roll back to pod v
+    auto rollback = [&](int v) -> bool {
+      if (ST) {
+        st_acc[43] += (dec[v].flags & SP_PRED_GE) ? 1 : 0;
+        st_acc[45] += (dec[v].flags & SP_PRED_GT) ? 1 : 0;
+      }
+      // park the other waves, undo the Reserves of pods >= v (newest first: the two Reserve waves finish pods out of
+      // order, so by their flags), restore the slot versions
+      st_rel(&s_stop, 1);
+      spins = 0;
+      while (ld_acq(&s_parked) < SP_WAVES - 1) {
+        if (++spins > SP_SPIN_LIMIT) { err = true; err_code = 1; return false; }
+        sp_sleep();
+      }
+      SPM(37);   // rollback: parking the other waves
+      if (ST) st_acc[41] += q - v;
+      for (int qq = q - 1; qq >= v; --qq) {
+        if (!resv[qq] || (dec[qq].flags & SP_FITERR)) continue;
+        const UndoRec& u = undo[qq % SP_LAG];
+        const int sl = u.slot;
+        const uint64_t* src = reinterpret_cast<const uint64_t*>(&u.row);
+        uint64_t* dst = reinterpret_cast<uint64_t*>(&drows[sl]);
+        for (int i = lane; i < (int)(sizeof(Row) / 8); i += 64) dst[i] = src[i];
+        const uint64_t* s2 = reinterpret_cast<const uint64_t*>(&u.cs);
+        uint64_t* d2 = reinterpret_cast<uint64_t*>(&cst[sl]);
+        for (int i = lane; i < (int)(sizeof(CpuStateDev) / 8); i += 64) d2[i] = s2[i];
+        WAVE_FENCE();
+      }
+      // versions of the slots that survive, newest undone landing first
+      uint64_t redo0 = 0, redo1 = 0;   // surviving slots whose row was restored: re-score them for pods >= v
+      for (int qq = q - 1; qq >= v; --qq) {
+        const DecRec& e = dec[qq];
+        if ((e.flags & (SP_FITERR | SP_FRESH)) || e.slot >= dec[v].nd_before) continue;
+        const int sl = e.slot;
+        if (lane == (sl & 63)) { if (sl < 64) pv0 = e.prev_pend; else pv1 = e.prev_pend; }
+        if (resv[qq]) { if (sl < 64) redo0 |= 1ull << sl; else redo1 |= 1ull << (sl - 64); }
+      }
+      const int ndv = dec[v].nd_before;
+      ps_slot = -1;   // a pending fresh slot is the last decision's: >= ndv, undone
+      if (lane >= ndv) { dn0 = 0xffffffffu; pv0 = -1; }
+      if (lane + 64 >= ndv) { dn1 = 0xffffffffu; pv1 = -1; }
+      for (int s = ndv + lane; s < nd; s += 64) { has_row[s] = 0; done_ver[s] = -1; }
+      nd = ndv;
+      hash_ok = false;   // rebuilt by the next full-row resolution that needs it
+      SPM(38);   // rollback: undo log, slot versions
+      if (ST) st_acc[40] += __popcll(redo0) + __popcll(redo1);
+      // re-score the restored rows for pods v.. (their dsc entries after the undone landing are stale)
+      for (int pass = 0; pass < 2; ++pass) {
+        for (uint64_t bb = pass ? redo1 : redo0; bb; bb &= bb - 1) {
+          const int sl = (pass ? 64 : 0) + __builtin_ctzll(bb);
+          const Row rr = drows[sl];
+          // (the re-scoring waves are parked: wave 0 borrows the first one's hint table)
+          if (numa_on && ((rr.nr.nflags >> NF_POLICY_SHIFT) & 3u)) hint_table_fill(tables[0], rr.nr, zone_avail(rr.nr), lane);
+          WAVE_FENCE();
+          for (int q2 = v + lane; q2 < B; q2 += 64) dsc[q2 * SB + sl] = (int16_t)row_score(rr, pods(q2), a.pf, m, &tables[0]);
           WAVE_FENCE();
         }
-        // versions of the slots that survive, newest undone landing first
-        uint64_t redo0 = 0, redo1 = 0;   // surviving slots whose row was restored: re-score them for pods >= v
-        for (int qq = q - 1; qq >= v; --qq) {
-          const DecRec& e = dec[qq];
-          if ((e.flags & (SP_FITERR | SP_FRESH)) || e.slot >= dec[v].nd_before) continue;
-          const int sl = e.slot;
-          if (lane == (sl & 63)) { if (sl < 64) pv0 = e.prev_pend; else pv1 = e.prev_pend; }
-          if (resv[qq]) { if (sl < 64) redo0 |= 1ull << sl; else redo1 |= 1ull << (sl - 64); }
-        }
-        const int ndv = dec[v].nd_before;
-        ps_slot = -1;   // a pending fresh slot is the last decision's: >= ndv, undone
-        if (lane >= ndv) { dn0 = 0xffffffffu; pv0 = -1; }
-        if (lane + 64 >= ndv) { dn1 = 0xffffffffu; pv1 = -1; }
-        for (int s = ndv + lane; s < nd; s += 64) { has_row[s] = 0; done_ver[s] = -1; }
-        nd = ndv;
-        hash_ok = false;   // rebuilt by the next full-row resolution that needs it
-        SPM(38);   // rollback: undo log, slot versions
-        if (ST) st_acc[40] += __popcll(redo0) + __popcll(redo1);
-        // re-score the restored rows for pods v.. (their dsc entries after the undone landing are stale)
-        for (int pass = 0; pass < 2; ++pass) {
-          for (uint64_t bb = pass ? redo1 : redo0; bb; bb &= bb - 1) {
-            const int sl = (pass ? 64 : 0) + __builtin_ctzll(bb);
-            const Row rr = drows[sl];
-            // (the re-scoring waves are parked: wave 0 borrows the first one's hint table)
-            if (numa_on && ((rr.nr.nflags >> NF_POLICY_SHIFT) & 3u)) hint_table_fill(tables[0], rr.nr, zone_avail(rr.nr), lane);
-            WAVE_FENCE();
-            for (int q2 = v + lane; q2 < B; q2 += 64) dsc[q2 * SB + sl] = (int16_t)row_score(rr, pods(q2), a.pf, m, &tables[0]);
-            WAVE_FENCE();
-          }
-        }
-        SPM(39);   // rollback: re-scoring the restored rows
-        const int32_t myv0 = pv0, myv1 = pv1;
-        if (lane < nd) done_ver[lane] = myv0;
-        if (lane + 64 < nd) done_ver[lane + 64] = myv1;
-        for (int qq = v + lane; qq < B; qq += 64) {
-          rescored[qq] = 0;
-          jobs_left[qq] = 0;
-          jobs_all[qq] = 0;
-          resv[qq] = 0;
-        }
-        if (lane == 0) {
-          for (int k = 0; k < SP_NRES; ++k) { s_jq_head[k] = 0; s_jq_tail[k] = 0; }
-          if (s_cut_at >= v) s_cut_at = -1;   // a cut before v stands (its pod is not undone)
-          s_decided = v;
-          s_verified = v;
-          s_rb_at = v;
-          s_end_at = B;
-          s_parked = 0;
-          s_rb_req = 0;
-        }
-        WAVE_FENCE();
-        q = v;
-        end_at = B;
-        end_why = 0;
-        if (lane == 0) st_rel(&s_stop, 0);
-        n_hs = -1;   // reload pod v's header
-        load_hdr(v, n_hs, n_hc, n_nlev, n_feas, n_next, n_lh, n_tb);
-        if (ST) st_acc[3] += 1;
-        SPM(4);
-        continue;
       }
-      {   // the verifier has verified every pod before the batch's end (or a host cut)
-        const int vend = ctl.y;
-        if (vend >= 0) {
-          committed = vend;
-          host_cut = ld_acq(&s_vcut) != 0;
-          break;
-        }
+      SPM(39);   // rollback: re-scoring the restored rows
+      const int32_t myv0 = pv0, myv1 = pv1;
+      if (lane < nd) done_ver[lane] = myv0;
+      if (lane + 64 < nd) done_ver[lane + 64] = myv1;
+      if (SPLIT) {   // the slot table the prep wave snapshots
+        if (lane < nd) L.slot_pv[lane] = myv0;
+        if (lane + 64 < nd) L.slot_pv[lane + 64] = myv1;
       }
-      SPM(27);   // rollback / batch-end checks
-      // ------------------------------------------------ decide pod q
-      if (q >= end_at || q - ctl.z >= lag || ctl.w >= 0) {
-        if (++spins > SP_SPIN_LIMIT) { err = true; err_code = 2; break; }
-        if (const int we = ld_acq(&s_werr)) { err = true; err_code = we; break; }
-        sp_sleep();
-        if (q >= end_at) SPM(23);   // waiting at the batch's end
-        continue;
+      for (int qq = v + lane; qq < B; qq += 64) {
+        rescored[qq] = 0;
+        jobs_left[qq] = 0;
+        jobs_all[qq] = 0;
+        resv[qq] = 0;
       }
-      spins = 0;
-      if (ST) st_acc[35] += nd;
-      const int p = q;
-      const int hs = n_hs, hc = n_hc, nlev = n_nlev, feas = n_feas, next = n_next;
-      const uint32_t lh = n_lh;
-      const int32_t tbv = n_tb;
-      // dirty slots: ready (exact current score) or pending (left out)
-      const int dv0 = lane < nd ? ld_acq(&done_ver[lane]) : -1;
-      const int dv1 = lane + 64 < nd ? ld_acq(&done_ver[lane + 64]) : -1;
-      const bool rdy0 = lane < nd && dv0 == pv0, rdy1 = lane + 64 < nd && dv1 == pv1;
-      const uint64_t pend0 = __ballot(lane < nd && !rdy0), pend1 = __ballot(lane + 64 < nd && !rdy1);
-      if ((a.dbg & 1u) && (pend0 | pend1)) {   // diagnostics: no speculation, wait for the pending rows
-        if (++spins > SP_SPIN_LIMIT) { err = true; err_code = 3; break; }
-        sp_sleep();
-        continue;
+      if (lane == 0) {
+        for (int k = 0; k < SP_NRES; ++k) { s_jq_head[k] = 0; s_jq_tail[k] = 0; }
+        if (s_cut_at >= v) s_cut_at = -1;   // a cut before v stands (its pod is not undone)
+        s_decided = v;
+        s_verified = v;
+        s_rb_at = v;
+        s_end_at = B;
+        s_snap = v;
+        s_prep_done = v;
+        s_reprep = 0;
+        s_vwm = v;
+        s_parked = 0;
+        s_rb_req = 0;
       }
-      SPM(28);   // dirty-slot state (versions, ballots)
-      if (p + 1 < B) load_hdr(p + 1, n_hs, n_hc, n_nlev, n_feas, n_next, n_lh, n_tb);   // consumed by the next decision
-      int sc0 = -1, so0 = -1, sc1 = -1, so1 = -1;
-      flush_fresh();
-      if (lane < nd) { so0 = dso[p * SB + lane]; if (rdy0) sc0 = dsc[p * SB + lane]; }
-      if (lane + 64 < nd) { so1 = dso[p * SB + 64 + lane]; if (rdy1) sc1 = dsc[p * SB + 64 + lane]; }
-      SPM(29);   // next header's loads issued, pending fresh slot stored, dirty scores loaded
-      uint64_t unk0 = 0, unk1 = 0;
-      if (multi) {
-        // off-shard fresh rows whose batch-start job has not finished: a node in the list head has its listed level
-        // as batch-start score (exact); any other is unknown, counted as clean and unlisted (checked at verification)
-        const uint64_t u0 = __ballot(lane < nd && so0 == SO_UNKNOWN), u1 = __ballot(lane + 64 < nd && so1 == SO_UNKNOWN);
-        if (u0 | u1) {
-          const int incl = wave_incl_scan(lane < nlev ? hc : 0);   // list end of level `lane`
-          const int listed = __builtin_amdgcn_readlane(incl, 63);
-          for (int pass = 0; pass < 2; ++pass)
-            for (uint64_t bb = pass ? u1 : u0; bb; bb &= bb - 1) {
-              const int s = __builtin_ctzll(bb);
-              const uint32_t nn = (uint32_t)__builtin_amdgcn_readlane((int)(pass ? dn1 : dn0), s);
-              const uint64_t f = __ballot(lane < listed && lh == nn);
-              int sv = SO_UNLISTED;
-              if (f) {
-                const int e = __builtin_ctzll(f);
-                sv = __builtin_amdgcn_readlane(hs, __popcll(__ballot(lane < nlev && incl <= e)));
-              } else if (pass) {
-                unk1 |= 1ull << s;
-              } else {
-                unk0 |= 1ull << s;
-              }
-              if (lane == s) { if (pass) so1 = sv; else so0 = sv; }
-            }
-        }
+      WAVE_FENCE();
+      q = v;
+      ver = v;
+      wm = v;
+      end_at = B;
+      end_why = 0;
+      if (lane == 0) st_rel(&s_stop, 0);
+      if (!SPLIT) {
+        nh.hs = -1;   // reload pod v's header
+        load_hdr(v, nh);
       }
-      // action 0 commit, 1 FitError, 2 stop deciding before p
-      int action = 0;
-      uint32_t winner = 0xffffffffu;
-      int M = -1, F = 0;
-      int64_t T = 0;
-      bool slowpath = p == 0 && a.forced_node >= 0;
-      // the highest listed level that still holds a clean node: listed count minus the dirty rows listed there (their
-      // batch-start score), from the top (usually the first level)
-      int ctop = 0, Mclean = -1;
-      for (int j = 0; j < nlev; ++j) {
-        const int sj = __builtin_amdgcn_readlane(hs, j), cj = __builtin_amdgcn_readlane(hc, j);
-        const int dj = __popcll(__ballot(so0 == sj)) + __popcll(__ballot(so1 == sj));
-        if (cj > dj) { ctop = cj - dj; Mclean = sj; break; }
-      }
-      const int Md = wave_max(max(sc0, sc1));
-      const int Fd = wave_sum((sc0 >= 0) - (so0 >= 0) + (sc1 >= 0) - (so1 >= 0));
-      M = max(Mclean, Md);
-      F = Fd + feas;
-      SPM(18);   // decide: dirty-slot state, level scan
-      bool full_row = false;
-      if (slowpath) {
-        M = a.forced_score;
-        F = a.forced_feasible;
-        T = a.forced_ties;
-        winner = (uint32_t)a.forced_node;
-      } else if (M < 0 && next < 0) {
-        action = 1;   // every feasible node is listed, none clean, no dirty row feasible: FitError
-      } else if (M <= next) {
-        full_row = a.S != nullptr;
-        if (!full_row) { action = 2; end_why = 3; }
-        if (ST) st_acc[M < 0 ? 13 : 14] += 1;
-      } else if (M < 0) {
-        action = 1;
-      } else {
-        const bool nw0 = sc0 == M, nw1 = sc1 == M;
-        // clean listed ties: only at the top clean level (a higher M is a dirty row's: every listed node there is dirty)
-        T = (int64_t)(M == Mclean ? ctop : 0) + __popcll(__ballot(nw0)) + __popcll(__ballot(nw1));
-        const int64_t jp = tb_pos(p, tbv, T);
-        SPM(30);   // winner: ties, tie-break position
-        // level M's segment of the list: offset = listed nodes above it, len = listed nodes at it (0: not listed)
-        const uint64_t atm = __ballot(lane < nlev && hs == M);
-        const int jm = atm ? __builtin_ctzll(atm) : nlev;
-        const int len = atm ? __builtin_amdgcn_readlane(hc, jm) : 0;
-        const int off = wave_sum(lane < jm && lane < nlev ? hc : 0);
-        const uint64_t new0 = __ballot(nw0), new1 = __ballot(nw1);
-        const uint64_t old0 = __ballot(so0 == M && lane < nd), old1 = __ballot(so1 == M && lane + 64 < nd);
-        const int nnew = __popcll(new0) + __popcll(new1), nold = __popcll(old0) + __popcll(old1);
-        if (nnew == 0 && nold == 0) {
-          // no dirty row at M (then level M is listed: M is its clean level): the jp-th listed node of level M
-          const int e = off + (int)jp - 1;
-          winner = e < 64 ? (uint32_t)__builtin_amdgcn_readlane((int)lh, e) : list_ptr(a, 0, p)[e];
-          if (ST) { st_acc[24] += e >= 32 ? 1 : 0; st_acc[25] += e >= 64 ? 1 : 0; }
-        } else if (nnew == 0 && nold <= 61) {
-          // only listed nodes at M, some of them dirty rows no longer at M ("old"; the common case): the jp-th of the
-          // others in list order lies in the window [jp-2, jp-1+nold] of level M's segment (<= 64 entries, one per
-          // lane); old nodes before the window are those with a lower node id (the segment is in node order)
-          if (ST) { st_acc[36] += 1; st_acc[32] += nold; }
-          const int lo = (int)max<int64_t>(0, jp - 2);
-          const int hi = (int)min<int64_t>(len - 1, jp - 1 + nold);
-          const int W = hi - lo + 1;
-          const int e = off + lo + lane;
-          const uint32_t fromh = (uint32_t)__shfl((int)lh, e & 63);
-          uint32_t x = 0xffffffffu;
-          if (lane < W) x = e < 64 ? fromh : list_ptr(a, 0, p)[e];
-          const uint32_t win0 = (uint32_t)__builtin_amdgcn_readlane((int)x, 0);
-          SPM(46);   // winner (old-nodes path): level segment, window of the list
-          bool ow = false;
-          int base_old = 0;
-          each_node(old0, old1, [&](uint32_t n) {
-            base_old += n < win0 ? 1 : 0;
-            ow |= x == n;
-          });
-          const uint64_t bo = __ballot(lane < W && ow);
-          const int older = base_old + __popcll(bo & lt_mask);
-          const uint64_t hit = __ballot(lane < W && !ow && (int64_t)(lo + lane - older + 1) == jp);
-          if (ST) { st_acc[24] += off + hi >= 32 ? 1 : 0; st_acc[25] += off + hi >= 64 ? 1 : 0; }
-          if (!hit) { action = 2; end_why = 1; }
-          else winner = (uint32_t)__builtin_amdgcn_readlane((int)x, __builtin_ctzll(hit));
-        } else {
-          if (ST) { st_acc[31] += 1; st_acc[32] += nold; st_acc[33] += nnew; }
-          const int lo = (int)max<int64_t>(0, jp - 2 - nnew);
-          const int hi = (int)min<int64_t>(len - 1, jp - 1 + nold);
-          const int W = hi - lo + 1;
-          if (ST) st_acc[34] += W > 0 ? W : 0;
-          const uint32_t* L = list_ptr(a, 0, p);
-          constexpr int WCH = (2 * MAX_BATCH + 2 + 63) / 64;
-          uint32_t xw[WCH];
-          bool ow[WCH];
-          uint32_t cand = 0xffffffffu;
-          int base_old = 0;
-          if (len > 0) {
-#pragma unroll
-            for (int c = 0; c < WCH; ++c) {
-              const int i = c * 64 + lane, e = off + lo + i;
-              const uint32_t fromh = (uint32_t)__shfl((int)lh, e & 63);
-              xw[c] = 0xffffffffu;
-              if (c * 64 < W && i < W) xw[c] = e < 64 ? fromh : L[e];
-            }
-            if (ST) { st_acc[24] += off + hi >= 32 ? 1 : 0; st_acc[25] += off + hi >= 64 ? 1 : 0; }
-            const uint32_t win0 = (uint32_t)__builtin_amdgcn_readlane((int)xw[0], 0);
-#pragma unroll
-            for (int c = 0; c < WCH; ++c) ow[c] = false;
-            each_node(old0, old1, [&](uint32_t n) {
-              base_old += n < win0 ? 1 : 0;
-#pragma unroll
-              for (int c = 0; c < WCH; ++c) ow[c] |= xw[c] == n;
-            });
-            int running = base_old;
-#pragma unroll
-            for (int c = 0; c < WCH; ++c) {
-              if (c * 64 >= W) break;
-              const int i = c * 64 + lane;
-              const bool valid = i < W;
-              const uint64_t bo = __ballot(valid && ow[c]);
-              const int older = running + __popcll(bo & lt_mask);
-              int newer = 0;
-              each_node(new0, new1, [&](uint32_t n) { newer += n < xw[c] ? 1 : 0; });
-              if (valid && !ow[c] && (int64_t)(lo + i - older + newer + 1) == jp) cand = xw[c];
-              running += __popcll(bo);
-            }
-          }
-          each_node(new0, new1, [&](uint32_t n) {
-            int u = 0;
-            each_node(new0, new1, [&](uint32_t n2) { u += n2 < n ? 1 : 0; });
-            int64_t ltn = -1;
-            int older = 0;
-            if (len == 0) {
-              ltn = 0;
-            } else {
-              int pp = 0;
-#pragma unroll
-              for (int c = 0; c < WCH; ++c) {
-                if (c * 64 >= W) break;
-                const bool valid = c * 64 + lane < W;
-                pp += __popcll(__ballot(valid && xw[c] < n));
-                older += __popcll(__ballot(valid && ow[c] && xw[c] < n));
-              }
-              older += base_old;
-              if (pp == 0) ltn = (lo == 0) ? 0 : -1;
-              else if (pp == W) ltn = (hi == len - 1) ? len : -1;
-              else ltn = lo + pp;
-            }
-            if (ltn >= 0 && ltn - older + u + 1 == jp) cand = n;
-          });
-          const uint64_t got = __ballot(cand != 0xffffffffu);
-          if (!got) { action = 2; end_why = 1; }
-          else winner = (uint32_t)__builtin_amdgcn_readlane((int)cand, __ffsll((long long)got) - 1);
-        }
-      }
-      if (ST) st_acc[10] += full_row ? 1 : 0;
-      SPM(19);   // decide: tie-break position, winner among listed + dirty ties
-      if (full_row) {
-        if (!hash_ok) rebuild_hash();
-        // exact resolution of pod p from its whole score row: batch-start S[p][*] for clean nodes, the current
-        // score for ready dirty rows, pending rows left out (verified later like any decision)
-        const int16_t* row = a.S + (size_t)p * a.ld;
-        const uint32_t len = a.own1 - a.own0;
-        constexpr int VB = 8;
-        auto load_blk = [&](uint32_t i0, int16_t (&x)[8]) {
-          if (i0 + 8 <= len) {
-            const uint4 vv = *reinterpret_cast<const uint4*>(row + i0);
-            const uint32_t w[4] = {vv.x, vv.y, vv.z, vv.w};
-#pragma unroll
-            for (int k = 0; k < 8; ++k) x[k] = (int16_t)(w[k >> 1] >> (16 * (k & 1)));
-          } else {
-#pragma unroll
-            for (int k = 0; k < 8; ++k) x[k] = i0 + k < len ? row[i0 + k] : (int16_t)-1;
-          }
-        };
-        int lmax = -1, lcnt = 0, lfeas = 0;
-        for (uint32_t b0 = 0; b0 < len; b0 += 512u * VB) {
-          int16_t x[VB][8];
-#pragma unroll
-          for (int u = 0; u < VB; ++u) load_blk(b0 + 512u * u + 8u * lane, x[u]);
-#pragma unroll
-          for (int u = 0; u < VB; ++u)
-#pragma unroll
-            for (int k = 0; k < 8; ++k) {
-              const int xv = x[u][k];
-              lfeas += xv >= 0 ? 1 : 0;
-              lcnt = xv > lmax ? 1 : lcnt + (xv == lmax ? 1 : 0);
-              lmax = xv > lmax ? xv : lmax;
-            }
-        }
-        F = wave_sum(lfeas) + Fd;
-        int Mc = wave_max(lmax);
-        int64_t Tc = Mc >= 0 ? (int64_t)wave_sum(lmax == Mc ? lcnt : 0) - __popcll(__ballot(lane < nd && so0 == Mc)) -
-                                   __popcll(__ballot(lane + 64 < nd && so1 == Mc))
-                             : 0;
-        if (Mc >= 0 && Tc <= 0) {
-          lmax = -1;
-          lcnt = 0;
-          for (uint32_t b0 = 0; b0 < len; b0 += 512u * VB) {
-            int16_t x[VB][8];
-#pragma unroll
-            for (int u = 0; u < VB; ++u) load_blk(b0 + 512u * u + 8u * lane, x[u]);
-#pragma unroll
-            for (int u = 0; u < VB; ++u)
-#pragma unroll
-              for (int k = 0; k < 8; ++k) {
-                const int xv = x[u][k];
-                if (xv >= 0 && xv >= lmax && sp_hash_find(a.own0 + b0 + 512u * u + 8u * lane + k) < 0) {
-                  lcnt = xv > lmax ? 1 : lcnt + 1;
-                  lmax = xv;
-                }
-              }
-          }
-          Mc = wave_max(lmax);
-          Tc = Mc >= 0 ? (int64_t)wave_sum(lmax == Mc ? lcnt : 0) : 0;
-        }
-        M = max(Mc, Md);
-        if (M < 0) {
-          action = 1;
-        } else {
-          const uint64_t new0 = __ballot(sc0 == M), new1 = __ballot(sc1 == M);
-          const uint64_t old0 = __ballot(lane < nd && so0 == M), old1 = __ballot(lane + 64 < nd && so1 == M);
-          T = (Mc == M ? Tc : 0) + __popcll(new0) + __popcll(new1);
-          const int64_t jp = tb_pos(p, tbv, T);
-          int64_t run = 0;
-          int64_t found = -1;
-          for (uint32_t b0 = 0; b0 < len && found == -1; b0 += 512u * VB) {
-            int16_t x[VB][8];
-#pragma unroll
-            for (int u = 0; u < VB; ++u) load_blk(b0 + 512u * u + 8u * lane, x[u]);
-#pragma unroll
-            for (int u = 0; u < VB; ++u) {
-              const uint32_t i0 = b0 + 512u * u;
-              uint32_t fl = 0;
-#pragma unroll
-              for (int k = 0; k < 8; ++k) fl |= (x[u][k] == M ? 1u : 0u) << k;
-              const bool in0 = dn0 - a.own0 - i0 < 512u, in1 = dn1 - a.own0 - i0 < 512u;
-              const uint64_t bn0 = new0 & __ballot(in0), bn1 = new1 & __ballot(in1);
-              const uint64_t bo0 = old0 & __ballot(in0), bo1 = old1 & __ballot(in1);
-              const int tot = wave_sum(__popc(fl)) + __popcll(bn0) + __popcll(bn1) - __popcll(bo0) - __popcll(bo1);
-              if (found == -1 && run + tot >= jp) {
-                each_node(bo0, bo1, [&](uint32_t nn) {
-                  const uint32_t o = nn - a.own0 - i0;
-                  if ((uint32_t)lane == (o >> 3)) fl &= ~(1u << (o & 7u));
-                });
-                each_node(bn0, bn1, [&](uint32_t nn) {
-                  const uint32_t o = nn - a.own0 - i0;
-                  if ((uint32_t)lane == (o >> 3)) fl |= 1u << (o & 7u);
-                });
-                const int c = __popc(fl);
-                const int incl = wave_incl_scan(c);
-                int64_t need = jp - (run + incl - c);
-                int64_t f = -1;
-                if (need >= 1 && need <= c) {
-                  uint32_t bits = fl;
-                  while (--need) bits &= bits - 1;
-                  f = (int64_t)(a.own0 + i0 + 8u * lane + (uint32_t)__builtin_ctz(bits));
-                }
-                const uint64_t gg = __ballot(f >= 0);
-                found = gg ? (int64_t)__builtin_amdgcn_readlane((int)f, __ffsll((long long)gg) - 1) : -2;
-              }
-              run += tot;
-            }
-          }
-          if (found < 0) {
-            action = 2;
-            end_why = 2;
-            const int osl = old0 ? __builtin_ctzll(old0) : old1 ? 64 + __builtin_ctzll(old1) : -1;
-            const uint32_t onode = osl < 0 ? 0u : (uint32_t)__builtin_amdgcn_readlane((int)(osl < 64 ? dn0 : dn1), osl & 63);
-            const int ohash = osl < 0 ? -9 : sp_hash_find(onode);
-            const int osv = osl < 0 ? -9 : (int)a.S[(size_t)p * a.ld + (onode - a.own0)];
-            const int odso = osl < 0 ? -9 : (int)dso[p * SB + osl];
-            if (lane == 0)   // diagnostics (GS_DEBUG_CUTS): the inconsistent tie count
-              a.out[p] = PlacementDev{-7, (uint32_t)run, (int64_t)M | ((int64_t)Mc << 20) | ((int64_t)Md << 40), (uint32_t)T,
-                                      (uint32_t)Tc, (uint32_t)(__popcll(new0) + __popcll(new1)),
-                                      (uint32_t)(__popcll(old0) + __popcll(old1)), {(int64_t)jp, (int64_t)nd, (int64_t)__popcll(pend0), 0}, {0, 0, 0, 0},
-                                      {(uint64_t)osl, (uint64_t)onode, (uint64_t)(int64_t)ohash,
-                                       (uint64_t)(((int64_t)osv << 32) | (uint32_t)odso)}};
-          }
-          else winner = (uint32_t)found;
-          slowpath = true;
-        }
-      }
-      if (full_row) SPM(11);
-      if (action == 0 && (int32_t)winner < 0) { action = 2; end_why = 4; }
-      if (action == 2) {   // stop deciding here: the batch ends at p once everything before it is verified
-        end_at = p;
-        if (lane == 0) st_rel(&s_end_at, p);
-        continue;
-      }
-      // ---- record the decision, claim / version the winner's slot
+      if (ST) st_acc[3] += 1;
+      SPM(4);
+      return true;
+    };
+    // ------------------------------------------------ record decision p, claim / version the winner's slot
+    auto record = [&](int p, const Dc& r) {
+      const int action = r.action;
+      const uint32_t winner = r.winner;
       DecRec d{};
       d.winner = action == 1 ? -1 : (int32_t)winner;
-      d.M = action == 1 ? -1 : M;
-      d.T = (int32_t)T;
-      d.F = F;
+      d.M = action == 1 ? -1 : r.M;
+      d.T = (int32_t)r.T;
+      d.F = r.F;
       d.nd_before = nd;
-      d.pend0 = pend0;
-      d.pend1 = pend1;
-      d.unk0 = unk0;
-      d.unk1 = unk1;
-      d.flags = (action == 1 ? SP_FITERR : 0u) | (slowpath ? SP_SLOW : 0u);
-      if (ST && action == 0 && (pend0 | pend1)) {
+      d.pend0 = r.pend0;
+      d.pend1 = r.pend1;
+      d.unk0 = r.unk0;
+      d.unk1 = r.unk1;
+      d.flags = (action == 1 ? SP_FITERR : 0u) | (r.slowpath ? SP_SLOW : 0u);
+      if (ST && !SPLIT && action == 0 && (r.pend0 | r.pend1)) {
         // would a rule "wait when a pending row scored >= M (> M) for p before its landing" have foreseen the rollbacks?
         int o0 = -1, o1 = -1;
-        if ((pend0 >> lane) & 1ull) o0 = dec[pv0].prev_pend < 0 ? so0 : (int)dsc[p * SB + lane];
-        if ((pend1 >> lane) & 1ull) o1 = dec[pv1].prev_pend < 0 ? so1 : (int)dsc[p * SB + 64 + lane];
+        if ((r.pend0 >> lane) & 1ull) o0 = dec[pv0].prev_pend < 0 ? r.so0 : (int)dsc[p * SB + lane];
+        if ((r.pend1 >> lane) & 1ull) o1 = dec[pv1].prev_pend < 0 ? r.so1 : (int)dsc[p * SB + 64 + lane];
         const int om = wave_max(max(o0, o1));
-        if (om >= M) { d.flags |= SP_PRED_GE; st_acc[42] += 1; }
-        if (om > M) { d.flags |= SP_PRED_GT; st_acc[44] += 1; }
+        if (om >= r.M) { d.flags |= SP_PRED_GE; st_acc[42] += 1; }
+        if (om > r.M) { d.flags |= SP_PRED_GT; st_acc[44] += 1; }
       }
       d.slot = -1;
       d.prev_pend = -1;
@@ -805,13 +966,264 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
           if (lane == (slot & 63)) { if (slot < 64) pv0 = p; else pv1 = p; }
         }
         d.slot = slot;
+        if (SPLIT && lane == 0) {   // the slot table the prep wave snapshots
+          L.slot_node[slot] = (int32_t)winner;
+          L.slot_pv[slot] = p;
+        }
       }
       if (lane == 0) dec[p] = d;
       WAVE_FENCE();
       if (lane == 0) st_rel(&s_decided, p + 1);
-      ++q;
       if (ST) st_acc[9] += 1;
       SPM(0);
+    };
+    // ------------------------------------------------ split pipeline: verification of the decided pods, in order
+    // pod v stands iff every row pending at its decision now scores below its maximum for it; the rows it excluded
+    // that are feasible join its Feasible count (same rule as the verify wave of the unsplit pipeline). 0: nothing
+    // more now, 1: roll back to `ver`, 2: the batch ends at `committed`.
+    auto verify_step = [&](int cut_at) -> int {
+      while (wm < q && ld_acq(&rescored[wm])) ++wm;
+      while (ver < q && ver <= wm) {
+        if (cut_at >= 0 && ver > cut_at) break;
+        const DecRec& d = dec[ver];
+        const uint64_t dp0 = d.pend0, dp1 = d.pend1;
+        const int dM = d.M;
+        int mis = 0, fadd = 0;
+        if ((dp0 >> lane) & 1ull) {
+          const int sc = dsc[ver * SB + lane];
+          mis |= sc >= 0 && sc >= dM;
+          fadd += sc >= 0;
+        }
+        if ((dp1 >> lane) & 1ull) {
+          const int sc = dsc[ver * SB + 64 + lane];
+          mis |= sc >= 0 && sc >= dM;
+          fadd += sc >= 0;
+        }
+        if (__ballot(mis)) return 1;
+        const int F = d.F + wave_sum(fadd);
+        if (lane == 0) final_F[ver] = F;
+        ++ver;
+      }
+      // a Reserve that needs the host's cpuset selection ends the batch right after its pod
+      if (cut_at >= 0 && ver > cut_at) { committed = cut_at + 1; host_cut = true; return 2; }
+      if (ver == end_at) { committed = ver; return 2; }   // every pod before the end of the decisions is verified
+      return 0;
+    };
+    // ------------------------------------------------ split pipeline: the final decision of pod p from its PrepRec
+    // The prep wave decided p over a snapshot of the decisions before rec.q_s; the decisions [q_s, p) landed after it.
+    // Each such landing makes its slot pending: a slot the snapshot held as ready loses its exact score (a tie at M is
+    // excluded, its feasibility leaves F); a slot created after the snapshot was a clean node to the prep wave (a
+    // clean tie at M is excluded, its batch-start feasibility leaves F). M stands (exclusions only lower the field); the
+    // tie-break position stands while T' >= jp (records are a prefix property); the winner is the jp-th of the
+    // remaining ties, found in the window of ties the prep wave recorded. false: p needs a full decision here.
+    auto apply_late = [&](int p, Dc& r) -> bool {
+      const PrepRec& rec = L.prq[p % SP_PREPQ];
+      // the record (five 16-byte words, uniform), the late decisions (lane i: decision q_s + i) and the snapshot's slot
+      // flags (lane: slot lane / lane + 64), read together
+      typedef int32_t i4 __attribute__((ext_vector_type(4)));
+      const i4 h0 = reinterpret_cast<const i4*>(&rec)[0], h1 = reinterpret_cast<const i4*>(&rec)[1];
+      const i4 h2 = reinterpret_cast<const i4*>(&rec)[2], h3 = reinterpret_cast<const i4*>(&rec)[3];
+      const uint32_t twv = lane < SP_KW ? rec.tw[lane] : 0xffffffffu;
+      const int pod = __builtin_amdgcn_readfirstlane(h0.x), qs = __builtin_amdgcn_readfirstlane(h0.y);
+      const int nds = __builtin_amdgcn_readfirstlane(h0.z), action = __builtin_amdgcn_readfirstlane(h0.w);
+      const int sfa = lane < nds ? rec.sf[lane] : 0, sfb = lane + 64 < nds ? rec.sf[lane + 64] : 0;
+      const int nl = p - qs;
+      int s = -1;
+      uint32_t w = 0, fl = SP_FITERR;
+      if (lane < nl) {
+        const DecRec& e = dec[qs + lane];
+        fl = e.flags;
+        s = e.slot;
+        w = (uint32_t)e.winner;
+      }
+      if (pod != p || nl > 64 || action > 2 || (action == 2 && nl != 0)) return false;
+      SPM(52);   // split: the record, the late decisions
+      if (action == 2) {   // stop deciding before p (an exact record)
+        r.action = 2;
+        r.end_why = __builtin_amdgcn_readfirstlane(h2.x);
+        return true;
+      }
+      const int M = __builtin_amdgcn_readfirstlane(h1.x), Mclean = __builtin_amdgcn_readfirstlane(h1.y);
+      const int F0 = __builtin_amdgcn_readfirstlane(h1.z), ntw = __builtin_amdgcn_readfirstlane(h1.w);
+      const bool val = lane < nl && !(fl & SP_FITERR);
+      // a slot landed on twice after the snapshot counts once; lt0 / lt1: slot lane / lane + 64 landed on since
+      bool dup = false, lt0 = false, lt1 = false;
+      for (int j = 0; j < nl; ++j) {
+        const int sj = __builtin_amdgcn_readlane(s, j);
+        dup |= lane > j && s == sj;
+        lt0 |= lane == sj;
+        lt1 |= lane + 64 == sj;
+      }
+      const bool use = val && !dup;
+      const bool in_snap = s < nds;
+      int sfv = 0, so = -1;
+      if (use) {
+        if (in_snap) sfv = rec.sf[s];
+        else so = dso[p * SB + s];
+      }
+      // a slot the snapshot held ready loses its exact score (tie / feasible); one created after it was a clean node
+      const bool fdec = use && (in_snap ? (sfv & SF_FEAS) != 0 : so >= 0);
+      const bool tie = use && action == 0 && (in_snap ? (sfv & SF_TIE) != 0 : so == M && M == Mclean);
+      // (a clean node above M cannot be: the prep wave's M is at least its clean level)
+      if (__ballot(use && !in_snap && so > M && action == 0)) return false;
+      int F = F0 - __popcll(__ballot(fdec));
+      const int ne = __popcll(__ballot(tie));
+      SPM(53);   // split: the late slots' exclusions
+      // rows pending at the snapshot, not landed on since, whose re-scoring is complete now: their exact score for p
+      // settles them here (one at or above M: p is recorded again over the exact state, instead of a rollback later)
+      bool chk0 = (sfa & SF_PEND) && !lt0, chk1 = (sfb & SF_PEND) && !lt1;
+      if (chk0) chk0 = ld_acq(&done_ver[lane]) == pv0;
+      if (chk1) chk1 = ld_acq(&done_ver[lane + 64]) == pv1;
+      int sc0 = -1, sc1 = -1;
+      if (chk0) sc0 = dsc[p * SB + lane];
+      if (chk1) sc1 = dsc[p * SB + 64 + lane];
+      if (__ballot((sc0 >= 0 && sc0 >= M) || (sc1 >= 0 && sc1 >= M))) return false;
+      F += wave_sum((sc0 >= 0 ? 1 : 0) + (sc1 >= 0 ? 1 : 0));
+      SPM(54);   // split: rows settled early
+      r.action = action;
+      r.M = M;
+      r.F = F;
+      r.T = (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane(h2.w) << 32) |
+                      (uint32_t)__builtin_amdgcn_readfirstlane(h2.z));
+      r.pend0 = __ballot((((sfa & SF_PEND) != 0) || lt0) && !chk0);
+      r.pend1 = __ballot((((sfb & SF_PEND) != 0) || lt1) && !chk1);
+      r.unk0 = 0;
+      r.unk1 = 0;
+      r.slowpath = __builtin_amdgcn_readfirstlane(h2.y) != 0;
+      r.end_why = 0;
+      r.winner = 0xffffffffu;
+      if (ST) { st_acc[47] += nl; st_acc[49] += ne; st_acc[50] += __popcll(__ballot(chk0)) + __popcll(__ballot(chk1)); }
+      if (action == 1) return true;
+      if (ntw < 1) return false;
+      if (ne == 0) {
+        r.winner = (uint32_t)__builtin_amdgcn_readfirstlane((int)twv);
+        return true;
+      }
+      // exclusions: the jp-th of the remaining ties, in the window (tie jp + k in lane k of twv)
+      const int64_t jp = (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane(h3.y) << 32) |
+                                   (uint32_t)__builtin_amdgcn_readfirstlane(h3.x));
+      r.T -= ne;
+      if (r.T < jp) return false;
+      for (int k = 0; k < ntw; ++k) {
+        const uint32_t x = (uint32_t)__builtin_amdgcn_readlane((int)twv, k);
+        const bool ex = __ballot(tie && w == x) != 0;
+        const int c = __popcll(__ballot(tie && w < x));
+        if (!ex && c == k) { r.winner = x; return true; }
+      }
+      return false;
+    };
+
+    while (!err) {
+      SPM(2);
+      if (SPLIT) {
+        int cut_at;
+        if (vshare) {
+          const v4i32 ctl = ld_ctl();   // rb_req, vend (unused), verified, cut_at
+          if (const int rq = ctl.x) {
+            if (!rollback(rq - 1)) break;
+            continue;
+          }
+          ver = ctl.z;
+          cut_at = ctl.w;
+          // a Reserve that needs the host's cpuset selection ends the batch right after its pod; else every pod
+          // before the end of the decisions verified
+          if (cut_at >= 0 && ver > cut_at) { committed = cut_at + 1; host_cut = true; break; }
+          if (ver == end_at) { committed = ver; break; }
+        } else {
+          cut_at = ld_acq(&s_cut_at);
+          const int vs = verify_step(cut_at);
+          if (vs == 1) {
+            if (!rollback(ver)) break;
+            continue;
+          }
+          if (vs == 2) break;
+        }
+        SPM(55);   // split: verification
+        if (ps_slot >= 0) {   // the last fresh slot's batch-start scores, then the snapshot the prep wave reads
+          flush_fresh();
+          WAVE_FENCE();
+        }
+        if (lane == 0 && ld_acq(&s_snap) != q) st_rel(&s_snap, q);
+        SPM(27);   // verification, fresh slot's scores
+        if (q >= end_at || q - ver >= lag || cut_at >= 0 || ld_acq(&s_prep_done) <= q || ld_acq(&s_reprep)) {
+          if (++spins > SP_SPIN_LIMIT) { err = true; err_code = 2; break; }
+          if (const int we = ld_acq(&s_werr)) { err = true; err_code = we; break; }
+          if (vshare) verify_try();
+          else __builtin_amdgcn_s_sleep(1);
+          if (q >= end_at) SPM(23);   // waiting at the batch's end
+          continue;
+        }
+        spins = 0;
+        if (ST) st_acc[35] += nd;
+        const int p = q;
+        Dc r;
+        if (!apply_late(p, r)) {   // the prep wave records p again over the exact state (every decision before p)
+          if (ST) st_acc[48] += 1;
+          if (lane == 0) st_rel(&s_reprep, p + 1);
+          SPM(11);
+          continue;
+        }
+        if (ST) st_acc[10] += r.slowpath ? 1 : 0;
+        SPM(19);   // the prep record, the late landings
+        if (r.action == 0 && (int32_t)r.winner < 0) { r.action = 2; r.end_why = 4; }
+        if (r.action == 2) {   // stop deciding here: the batch ends at p once everything before it is verified
+          end_at = p;
+          end_why = r.end_why;
+          continue;
+        }
+        record(p, r);
+        ++q;
+        continue;
+      }
+      const v4i32 ctl = ld_ctl();   // rb_req, vend, verified, cut_at
+      // ------------------------------------------------ a rollback the verifier requested: to pod v
+      if (const int rq = ctl.x) {
+        if (!rollback(rq - 1)) break;
+        continue;
+      }
+      {   // the verifier has verified every pod before the batch's end (or a host cut)
+        const int vend = ctl.y;
+        if (vend >= 0) {
+          committed = vend;
+          host_cut = ld_acq(&s_vcut) != 0;
+          break;
+        }
+      }
+      SPM(27);   // rollback / batch-end checks
+      // ------------------------------------------------ decide pod q
+      if (q >= end_at || q - ctl.z >= lag || ctl.w >= 0) {
+        if (++spins > SP_SPIN_LIMIT) { err = true; err_code = 2; break; }
+        if (const int we = ld_acq(&s_werr)) { err = true; err_code = we; break; }
+        sp_sleep();
+        if (q >= end_at) SPM(23);   // waiting at the batch's end
+        continue;
+      }
+      spins = 0;
+      if (ST) st_acc[35] += nd;
+      const int p = q;
+      const Hdr h = nh;
+      Dc r;
+      decide_core(p, h, nh, true, flush_fresh, nd, dn0, dn1, pv0, pv1, Tag<false>{}, r);
+      if (r.action == 4) {   // diagnostics (no speculation): wait for the pending rows
+        if (++spins > SP_SPIN_LIMIT) { err = true; err_code = 3; break; }
+        sp_sleep();
+        continue;
+      }
+      const bool full_row = r.action == 3;
+      if (ST) st_acc[10] += full_row ? 1 : 0;
+      if (full_row) {
+        full_row_resolve(p, h.tbv, r, nd, dn0, dn1, hash_ok);
+        SPM(11);
+      }
+      if (r.action == 0 && (int32_t)r.winner < 0) { r.action = 2; r.end_why = 4; }
+      if (r.action == 2) {   // stop deciding here: the batch ends at p once everything before it is verified
+        end_at = p;
+        end_why = r.end_why;
+        if (lane == 0) st_rel(&s_end_at, p);
+        continue;
+      }
+      record(p, r);
+      ++q;
     }
     if (!err && committed > 0) {   // every committed pod's Reserve is in place before the waves stop
       uint32_t w = 0;
@@ -839,7 +1251,102 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
       if (err) s_err = err_code ? err_code : 9;
       st_rel(&s_finish, 1);
     }
-  } else if (wv == SP_W_VERIFY) {
+  } else if (SPLIT && wv == SP_W_PREP) {
+    // ===================================================== prep =====================================================
+    // Pod p's selectHost over the snapshot of the decisions published in s_snap (slot table in LDS), up to
+    // SP_PREPQ - 1 pods ahead of wave 0, into the PrepRec ring; wave 0 applies the landings after the snapshot.
+    __builtin_amdgcn_s_setprio(3);
+    int pn = 0;   // the next pod in queue order (its header prefetched in nh)
+    Hdr nh;
+    load_hdr(0, nh);
+    int hash_nd = -1;   // the node -> slot hash holds the snapshot's first hash_nd slots (full-row resolution)
+    uint32_t spins = 0;
+    for (;;) {
+      if (ld_acq(&s_stop)) {   // a rollback: park; resume at its pod
+        if (lane == 0) __atomic_fetch_add(&s_parked, 1, __ATOMIC_ACQ_REL);
+        while (ld_acq(&s_stop) && !ld_acq(&s_finish)) sp_sleep();
+        pn = ld_acq(&s_rb_at);
+        if (pn < B) load_hdr(pn, nh);
+        hash_nd = -1;
+        SPM(2);
+        continue;
+      }
+      if (ld_acq(&s_finish)) break;
+      const int rq = ld_acq(&s_reprep);
+      int p = pn;
+      bool wait = false;
+      if (rq) {   // wave 0 asks for pod rq - 1 over the exact state: once the snapshot holds every decision before it
+        p = rq - 1;
+        wait = ld_acq(&s_snap) != p;
+      } else {
+        wait = pn >= B || pn >= ld_acq(&s_decided) + SP_PREPQ;
+      }
+      if (wait) {
+        if (++spins > SP_SPIN_LIMIT) {
+          if (lane == 0) __atomic_store_n(&s_werr, 10, __ATOMIC_RELEASE);
+          break;
+        }
+        if (pn >= B && !rq) sp_sleep();
+        else __builtin_amdgcn_s_sleep(1);
+        SPM(2);
+        continue;
+      }
+      spins = 0;
+      const int qs = ld_acq(&s_snap);
+      int nds = 0;
+      if (qs > 0) nds = dec[qs - 1].nd_before + ((dec[qs - 1].flags & SP_FRESH) ? 1 : 0);
+      const uint32_t dn0 = lane < nds ? (uint32_t)L.slot_node[lane] : 0xffffffffu;
+      const uint32_t dn1 = lane + 64 < nds ? (uint32_t)L.slot_node[lane + 64] : 0xffffffffu;
+      const int32_t pv0 = lane < nds ? L.slot_pv[lane] : -1;
+      const int32_t pv1 = lane + 64 < nds ? L.slot_pv[lane + 64] : -1;
+      Hdr h = nh;
+      if (rq) load_hdr(p, h);
+      Dc r;
+      decide_core(p, h, nh, !rq, [] {}, nds, dn0, dn1, pv0, pv1, Tag<true>{}, r);
+      const bool exact = qs == p;
+      if (r.action == 3 && exact) {
+        bool ok = hash_nd == nds;
+        full_row_resolve(p, h.tbv, r, nds, dn0, dn1, ok);
+        hash_nd = nds;
+      }
+      int act = r.action;
+      if (act == 0 && (int32_t)r.winner < 0) { act = 2; r.end_why = 4; }
+      if (act >= 3 || (!exact && (act == 2 || r.slowpath))) act = 5;
+      if (act == 0 && r.ntw == 0) {   // (forced / full-row decisions) the window is the winner alone
+        r.ntw = 1;
+        r.twv = lane == 0 ? r.winner : 0xffffffffu;
+      }
+      PrepRec& o = L.prq[p % SP_PREPQ];
+      if (lane == 0) {
+        o.pod = p;
+        o.q_s = qs;
+        o.nd_s = nds;
+        o.action = act;
+        o.M = r.M;
+        o.Mclean = r.Mclean;
+        o.F = r.F;
+        o.ntw = r.ntw;
+        o.end_why = r.end_why;
+        o.slow = r.slowpath ? 1 : 0;
+        o.T_lo = (int32_t)r.T;
+        o.T_hi = (int32_t)(r.T >> 32);
+        o.jp_lo = (int32_t)r.jp;
+        o.jp_hi = (int32_t)(r.jp >> 32);
+      }
+      if (lane < SP_KW) o.tw[lane] = r.twv;
+      if (lane < nds) o.sf[lane] = (uint8_t)r.sf0;
+      if (lane + 64 < nds) o.sf[lane + 64] = (uint8_t)r.sf1;
+      WAVE_FENCE();
+      if (rq) {
+        if (lane == 0) st_rel(&s_reprep, 0);
+      } else {
+        if (lane == 0) st_rel(&s_prep_done, p + 1);
+        ++pn;
+      }
+      if (ST) st_acc[9] += 1;
+      SPM(0);
+    }
+  } else if (!SPLIT && wv == SP_W_VERIFY) {
     // ==================================================== verify ====================================================
     // pod v stands iff every row pending at its decision now scores below its maximum for it (and every row whose
     // batch-start score was unknown scored below it at batch start); the rows it excluded that are feasible join its
@@ -1011,6 +1518,7 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
           __atomic_store_n(&resv[q], 1, __ATOMIC_RELEASE);
         }
         WAVE_FENCE();
+        if (vshare) verify_try();
         q += SP_NRES;
         continue;
       }
@@ -1179,13 +1687,14 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
       WAVE_FENCE();
       if (lane == 0) __atomic_store_n(&resv[q], 1, __ATOMIC_RELEASE);
       WAVE_FENCE();
+      if (vshare && njobs == 0) verify_try();
       q += SP_NRES;
       SPM(5);
     }
   } else {
     // ============================================== re-scoring jobs ==============================================
     uint32_t spins = 0;
-    const int ri = sp_rescore_index(wv);
+    const int ri = SPLIT ? wv - SP_RS0 : sp_rescore_index(wv);   // split: waves 4-7
     sp_prio((a.dbg >> 6) & 3u);
     int ring = ri % SP_NRES;
     for (;;) {
@@ -1251,13 +1760,17 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
       const int q2 = jb.q + 1 + jb.range * 64 + lane;
       if (q2 < B) dsc[q2 * SB + jb.slot] = (int16_t)row_score(rr, pods(q2), a.pf, m, &tab);
       WAVE_FENCE();
+      int fin = 0;
       if (lane == 0) {
         if (__atomic_fetch_sub(&jobs_left[jb.q], 1, __ATOMIC_ACQ_REL) == 1)
           __atomic_store_n(&done_ver[jb.slot], jb.q, __ATOMIC_RELEASE);
-        if (__atomic_fetch_sub(&jobs_all[jb.q], 1, __ATOMIC_ACQ_REL) == 1)
+        if (__atomic_fetch_sub(&jobs_all[jb.q], 1, __ATOMIC_ACQ_REL) == 1) {
           __atomic_store_n(&rescored[jb.q], 1, __ATOMIC_RELEASE);
+          fin = 1;
+        }
       }
       WAVE_FENCE();
+      if (vshare && __builtin_amdgcn_readfirstlane(fin)) verify_try();
       if (ST) st_acc[10] += 1;
       SPM(7);
     }
@@ -1316,33 +1829,50 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
 
 // With an exclusive commit CU the workgroup declares the CU's whole LDS, and the kernels that run beside it (the
 // next batch's eval pass) declare a few bytes (eval_lds_bytes), so none of their waves is placed on the commit's CU.
-template <bool STAMPS>
+template <bool STAMPS, bool SPLIT>
 static size_t spec_launch_bytes(int npods) {
   if (!commit_cu_exclusive()) return spec_smem_bytes(npods);
   static const size_t dyn = [] {
     hipFuncAttributes fa{};
     size_t st = 0;
-    if (hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(commit_spec_kernel<STAMPS>)) == hipSuccess)
+    if (hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(commit_spec_kernel<STAMPS, SPLIT>)) == hipSuccess)
       st = fa.sharedSizeBytes;   // the variant's static LDS
     return std::max(spec_smem_bytes(MAX_BATCH), (size_t)LDS_PER_CU - st);
   }();
   return dyn;
 }
 
+template <bool STAMPS, bool SPLIT>
+static void spec_launch(const CommitArgs& a, hipStream_t st) {
+  const size_t bytes = spec_launch_bytes<STAMPS, SPLIT>(a.npods);
+  hipLaunchKernelGGL((commit_spec_kernel<STAMPS, SPLIT>), dim3(1), dim3(SP_THREADS), bytes, st, a);
+}
+
 hipError_t launch_commit_spec(const CommitArgs& a, hipStream_t st) {
-  if (a.stamps)
-    hipLaunchKernelGGL(commit_spec_kernel<true>, dim3(1), dim3(SP_THREADS), spec_launch_bytes<true>(a.npods), st, a);
-  else
-    hipLaunchKernelGGL(commit_spec_kernel<false>, dim3(1), dim3(SP_THREADS), spec_launch_bytes<false>(a.npods), st, a);
+  // the split pipeline (GS_SPEC_SPLIT, dbg bit 16): one shard, speculation on
+  const bool split = ((a.dbg >> 16) & 1u) && a.nranks <= 1 && !(a.dbg & 1u);
+  if (a.stamps) {
+    if (split) spec_launch<true, true>(a, st);
+    else spec_launch<true, false>(a, st);
+  } else {
+    if (split) spec_launch<false, true>(a, st);
+    else spec_launch<false, false>(a, st);
+  }
   return hipGetLastError();
 }
 
+template <bool STAMPS, bool SPLIT>
+static hipError_t spec_attr() {
+  return hipFuncSetAttribute(reinterpret_cast<const void*>(commit_spec_kernel<STAMPS, SPLIT>),
+                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)spec_launch_bytes<STAMPS, SPLIT>(MAX_BATCH));
+}
+
 hipError_t set_commit_spec_attributes() {
-  hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(commit_spec_kernel<false>),
-                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)spec_launch_bytes<false>(MAX_BATCH));
-  if (e != hipSuccess) return e;
-  return hipFuncSetAttribute(reinterpret_cast<const void*>(commit_spec_kernel<true>),
-                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)spec_launch_bytes<true>(MAX_BATCH));
+  hipError_t e = spec_attr<false, false>();
+  if (e == hipSuccess) e = spec_attr<false, true>();
+  if (e == hipSuccess) e = spec_attr<true, false>();
+  if (e == hipSuccess) e = spec_attr<true, true>();
+  return e;
 }
 
 #undef SPM

@@ -1135,7 +1135,11 @@ CommitArgs commit_args(gs_ctx* c, int b) {
   static const uint32_t prio = getenv("GS_SPEC_PRIO") ? (uint32_t)strtoul(getenv("GS_SPEC_PRIO"), nullptr, 0) & 0x3f0u : 0u;
   // GS_SPEC_LAG (experiments): decisions ahead of the verifier, 1..12 (bits 12-15; 0: the kernel's SP_LAG)
   static const uint32_t lag = getenv("GS_SPEC_LAG") ? (uint32_t)std::min(12L, std::max(0L, atol(getenv("GS_SPEC_LAG")))) : 0u;
-  a.dbg = (nospec ? 1u : 0u) | prio | lag << 12;
+  // GS_SPEC_SPLIT=1 (experiments): the split selector (a prep wave decides ahead over a snapshot, wave 0 applies the
+  // landings after it), bit 16
+  // GS_SPEC_SPLIT=2: and the decided pods verified by the re-scoring / Reserve waves (bit 17)
+  static const int split = getenv("GS_SPEC_SPLIT") ? atoi(getenv("GS_SPEC_SPLIT")) : 0;
+  a.dbg = (nospec ? 1u : 0u) | prio | lag << 12 | (split >= 1 ? 1u << 16 : 0u) | (split >= 2 ? 1u << 17 : 0u);
   a.tb = c->d_tb;
   a.xerr = c->nranks > 1 ? c->d_xerr : nullptr;
   return a;
@@ -2108,10 +2112,17 @@ int gs_destroy(gs_ctx* c) {
                 W(0, 12), W(0, 27), W(0, 28), W(0, 29), W(0, 18), W(0, 19), W(0, 20), W(0, 0), W(0, 2), W(0, 23), W(0, 11));
         fprintf(stderr, "  winner split: ties + tie-break position %.0f | old-nodes path: level segment + list window %.0f\n",
                 W(0, 30), W(0, 46));
+        fprintf(stderr, "  late-landing estimate: %llu decisions, previous pod's row as it stood > M %llu, == M %llu (tie-break "
+                "position moves %llu)\n", (unsigned long long)sa[47], (unsigned long long)sa[48], (unsigned long long)sa[49],
+                (unsigned long long)sa[50]);
         fprintf(stderr, "  wave 0 raw (cycles per pod by stamp index):");
-        for (int i = 0; i < 48; ++i)
-          if (sa[i]) fprintf(stderr, " %d=%.0f", i, W(0, i));
-        fprintf(stderr, "\n");
+        for (int i = 0; i < 60; ++i)
+          if (sa[i] && (i < 47 || i > 50)) fprintf(stderr, " %d=%.0f", i, W(0, i));
+        fprintf(stderr, "\n  wave 1 raw (the split selector's prep wave):");
+        for (int i = 0; i < 52; ++i)
+          if (sa[64 + i]) fprintf(stderr, " %d=%.0f", i, W(1, i));
+        fprintf(stderr, "\n  split: late landings %llu, full decisions %llu, excluded ties %llu, rows settled early %llu\n",
+                (unsigned long long)sa[47], (unsigned long long)sa[48], (unsigned long long)sa[49], (unsigned long long)sa[50]);
         const double ng = sa[31] ? (double)sa[31] : 1.0;
         fprintf(stderr, "  winner: old-nodes-only path %llu decisions (%.1f%%), general path %llu (%.1f%%): avg old %.1f new "
                 "%.1f window %.1f; avg dirty slots %.1f; list window beyond 32: %llu, beyond 64: %llu\n",
