@@ -23,6 +23,7 @@ def main():
     ap.add_argument("--gang-pct", type=int, default=25)
     ap.add_argument("--gang-size", type=int, default=8)
     ap.add_argument("--chunk", type=int, default=2048)
+    ap.add_argument("--run-cap", type=int, default=192, help="schedule_with_gangs run_cap (pods per engine call)")
     args = ap.parse_args()
     from koordinator_amd import abi, config, synth
     from koordinator_amd import gang as gg
@@ -72,7 +73,7 @@ def main():
         if gang_ids[i]:
             mgr.pod_add(int(gang_ids[i]), int(pods["uid"][i]))
     states, carried, waiting = [], {}, gg.WaitingPods()
-    calls = {"schedule": 0, "schedule_s": 0.0, "forget": 0}
+    calls = {"schedule": 0, "schedule_s": 0.0, "forget": 0, "forget_s": 0.0, "run_pods": []}
     sched, forget = e.schedule, e.forget
 
     def timed_schedule(p, q):
@@ -80,17 +81,22 @@ def main():
         r = sched(p, q)
         calls["schedule"] += 1
         calls["schedule_s"] += time.perf_counter() - t
+        calls["run_pods"].append(len(p))
         return r
 
     def counted_forget(nodes, p):
         calls["forget"] += 1
-        return forget(nodes, p)
+        t = time.perf_counter()
+        r = forget(nodes, p)
+        calls["forget_s"] += time.perf_counter() - t
+        return r
 
     e.schedule, e.forget = timed_schedule, counted_forget
     t0 = time.perf_counter()
     for lo in range(warm, total, args.chunk):
         hi = min(total, lo + args.chunk)
-        _, res = gg.schedule_with_gangs(e, mgr, pods[lo:hi], gang_ids[lo:hi], seq[lo:hi], waiting=waiting)
+        _, res = gg.schedule_with_gangs(e, mgr, pods[lo:hi], gang_ids[lo:hi], seq[lo:hi], waiting=waiting,
+                                        run_cap=args.run_cap)
         states.append(res["state"])
         carried.update(res["carried"])
     e.synchronize()
@@ -109,6 +115,8 @@ def main():
         "rejected": int(np.count_nonzero(st == gg.ST_REJECTED)),
         "unschedulable": int(np.count_nonzero(st == gg.ST_UNSCHEDULABLE)),
         "engine_calls": calls["schedule"], "engine_s": calls["schedule_s"], "forget_calls": calls["forget"],
+        "forget_s": calls["forget_s"], "run_pods_mean": float(np.mean(calls["run_pods"])) if calls["run_pods"] else 0.0,
+        "run_pods_single": int(sum(1 for x in calls["run_pods"] if x == 1)),
         "total_s": gang_s,
         "config": "C3 (NUMA profile), 2048-pod calls after one 2048-pod warm-up call, batch 128, gangs Strict with "
                   "minMember = gang size, PodGroups known up front; one GPU"}))
