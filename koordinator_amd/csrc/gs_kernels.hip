@@ -106,6 +106,51 @@ __global__ void __launch_bounds__(256) eval_numa_kernel(MirrorView m, MirrorView
   }
 }
 
+// Tiled form (the default for full batches, PPT 8): a workgroup is a tile of 64 policy rows x NUMA_TWAVES * PPT pods; lane
+// = row, wave w = pods [w * PPT, (w + 1) * PPT) of the workgroup's pod range. The waves of a workgroup read the same
+// rows (one fetch from HBM, three cache hits), and the workgroups of one tile are numbered so they land on one XCD
+// (blocks go round-robin over the 8 XCDs: id % 8 = tile % 8) and are dispatched together (ids of 8 consecutive tiles x
+// every pod range form one run of ids), so each tile leaves HBM about once per pass instead of once per pod group
+// (round 4: ~26 reads of the slab per pass, 140 MB for a 4.6 MB slab at C3). ntiles8: tiles rounded up to 8.
+constexpr int NUMA_TWAVES = 4;
+template <int PPT>
+__global__ void __launch_bounds__(64 * NUMA_TWAVES) eval_numa_tile_kernel(MirrorView m, MirrorView sv,
+                                                                          const PodVec* __restrict__ pods, int npods,
+                                                                          Profile pf, const uint32_t* __restrict__ idx,
+                                                                          uint32_t nidx, uint32_t n0, int16_t* __restrict__ S,
+                                                                          uint32_t ld, int prod_cols,
+                                                                          uint8_t* __restrict__ aff, uint32_t npr,
+                                                                          int xcd_map) {
+  const uint32_t id = blockIdx.x;
+  uint32_t pr, tile;
+  if (xcd_map) {
+    const uint32_t grp = id / (8u * npr), rem = id % (8u * npr);
+    pr = rem / 8u;
+    tile = grp * 8u + rem % 8u;
+  } else {
+    pr = id % npr;
+    tile = id / npr;
+  }
+  const uint32_t t = tile * 64u + (threadIdx.x & 63u);
+  const int w = threadIdx.x >> 6;
+  const int k0 = (int)pr * (NUMA_TWAVES * PPT) + w * PPT;
+  if (t >= nidx || k0 >= npods) return;
+  const int k1 = min(npods, k0 + PPT);
+  const uint32_t node = idx[t];
+  Row row;
+  if (sv.i64) {
+    load_row(sv, t, prod_cols, true, row);
+    row.node = node;
+  } else {
+    load_row(m, node, prod_cols, true, row);
+  }
+  for (int k = k0; k < k1; ++k) {
+    PairOut o = eval_pair<false, false, true>(row, pods[k], pf, m);
+    S[(size_t)k * ld + (node - n0)] = (int16_t)total_score(o, pf);
+    aff[(size_t)k * ld + (node - n0)] = (uint8_t)(o.code ? 0u : o.aff);
+  }
+}
+
 // The NUMA-policy rows of the batch's eval pass gathered into a dense slab (same column numbering, entry t = node
 // idx[t]): eval_numa_kernel then reads each row once per pod group from whole cache lines instead of the ~30% of every
 // line the ascending index list uses in the mirror (the gather reads the sparse lines once per batch).
@@ -1722,7 +1767,28 @@ hipError_t launch_eval(const MirrorView& m, const PodVec* pods, int npods, const
       hipLaunchKernelGGL(gather_numa_kernel, dim3((numa_n + 255) / 256, SLAB64 + SLAB32), dim3(256), xl, st, m, sv,
                          numa_idx, numa_n);
     }
+    // GS_NUMA_TILE=0 (experiments): the untiled grid
+    // (GS_NUMA_TILE=2: tiled without the XCD numbering)
+    static const int tile_mode = getenv("GS_NUMA_TILE") ? atoi(getenv("GS_NUMA_TILE")) : 1;
+    const bool tile = tile_mode != 0;
     if (numa_n == 0) {
+    } else if (tile && ppt == NUMA_PPT) {
+      // pods per thread of the tiled kernel: 8 (GS_NUMA_TILE_PPT: 2, 4, 8). Tiled, 8 pods per thread: 337 us per pass
+      // and 2.4 MB of reads; untiled (4): 241 us and 58.5 MB. The pass runs beside the previous batch's commit, which
+      // it slows less when tiled: 182.8-183.7k vs 180.0-180.5k pods/s in three alternations
+      static const int tppt = getenv("GS_NUMA_TILE_PPT") ? atoi(getenv("GS_NUMA_TILE_PPT")) : 8;
+      const uint32_t ntiles8 = ((numa_n + 63) / 64 + 7) / 8 * 8;
+      const uint32_t npr = (npods + NUMA_TWAVES * tppt - 1) / (NUMA_TWAVES * tppt);
+      const int xm = tile_mode == 1 ? 1 : 0;
+      if (tppt == 2)
+        hipLaunchKernelGGL(eval_numa_tile_kernel<2>, dim3(ntiles8 * npr), dim3(64 * NUMA_TWAVES), xl, st, m, sv, pods,
+                           npods, pf, numa_idx, numa_n, n0, S, ld, prod_cols, aff, npr, xm);
+      else if (tppt == 8)
+        hipLaunchKernelGGL(eval_numa_tile_kernel<8>, dim3(ntiles8 * npr), dim3(64 * NUMA_TWAVES), xl, st, m, sv, pods,
+                           npods, pf, numa_idx, numa_n, n0, S, ld, prod_cols, aff, npr, xm);
+      else
+        hipLaunchKernelGGL(eval_numa_tile_kernel<NUMA_PPT>, dim3(ntiles8 * npr), dim3(64 * NUMA_TWAVES), xl, st, m, sv,
+                           pods, npods, pf, numa_idx, numa_n, n0, S, ld, prod_cols, aff, npr, xm);
     } else if (ppt == 2) {
       hipLaunchKernelGGL(eval_numa_kernel<2>, g, dim3(256), xl, st, m, sv, pods, npods, pf, numa_idx, numa_n, n0, S, ld,
                          prod_cols, aff);
