@@ -1135,10 +1135,10 @@ CommitArgs commit_args(gs_ctx* c, int b) {
   static const uint32_t prio = getenv("GS_SPEC_PRIO") ? (uint32_t)strtoul(getenv("GS_SPEC_PRIO"), nullptr, 0) & 0x3f0u : 0u;
   // GS_SPEC_LAG (experiments): decisions ahead of the verifier, 1..12 (bits 12-15; 0: the kernel's SP_LAG)
   static const uint32_t lag = getenv("GS_SPEC_LAG") ? (uint32_t)std::min(12L, std::max(0L, atol(getenv("GS_SPEC_LAG")))) : 0u;
-  // GS_SPEC_SPLIT=1 (experiments): the split selector (a prep wave decides ahead over a snapshot, wave 0 applies the
-  // landings after it), bit 16
-  // GS_SPEC_SPLIT=2: and the decided pods verified by the re-scoring / Reserve waves (bit 17)
-  static const int split = getenv("GS_SPEC_SPLIT") ? atoi(getenv("GS_SPEC_SPLIT")) : 0;
+  // the split selector (one shard; a prep wave decides ahead over a snapshot, wave 0 applies the landings after it),
+  // bit 16: the default (GS_SPEC_SPLIT=0: the single selector wave); GS_SPEC_SPLIT=2 (experiments): and the decided
+  // pods verified by the re-scoring / Reserve waves (bit 17)
+  static const int split = getenv("GS_SPEC_SPLIT") ? atoi(getenv("GS_SPEC_SPLIT")) : 1;
   a.dbg = (nospec ? 1u : 0u) | prio | lag << 12 | (split >= 1 ? 1u << 16 : 0u) | (split >= 2 ? 1u << 17 : 0u);
   a.tb = c->d_tb;
   a.xerr = c->nranks > 1 ? c->d_xerr : nullptr;
