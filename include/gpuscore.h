@@ -587,6 +587,14 @@ int gs_comm_unique_id(uint8_t out[128]);
 int gs_comm_init_rccl(gs_ctx* ctx, const uint8_t id[128], int nranks, int rank);
 /* Caller-supplied transport (host buffers): */
 int gs_comm_init_callback(gs_ctx* ctx, int nranks, int rank, gs_allgather_fn fn, void* user);
+/* In-process device transport (the ranks are threads of one process, e.g. several contexts on one GPU in tests): the
+ * all-gather is stream-ordered like ncclAllGather — device-to-device copies ordered by events on each rank's stream, no
+ * host wait on the GPU (the threads meet twice per exchange on the host to trade buffers and events). One group per
+ * set of ranks, created before and destroyed after their contexts. */
+typedef struct gs_local_group gs_local_group;
+int gs_local_group_create(int nranks, gs_local_group** out);
+int gs_local_group_destroy(gs_local_group* g);
+int gs_comm_init_local(gs_ctx* ctx, gs_local_group* g, int rank);
 
 /* ---- ingest decoders: the annotation / label text the plugins parse per call in the
  * reference, decoded once on the host into the ABI structs above (pure host functions, no device call) ---- */

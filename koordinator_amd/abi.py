@@ -338,6 +338,9 @@ SIGNATURES = {
     "gs_comm_unique_id": (C.c_int, [P]),
     "gs_comm_init_rccl": (C.c_int, [P, P, C.c_int, C.c_int]),
     "gs_comm_init_callback": (C.c_int, [P, C.c_int, C.c_int, ALLGATHER_FN, P]),
+    "gs_local_group_create": (C.c_int, [C.c_int, C.POINTER(P)]),
+    "gs_local_group_destroy": (C.c_int, [P]),
+    "gs_comm_init_local": (C.c_int, [P, P, C.c_int]),
     "gs_get_stats": (C.c_int, [P, C.POINTER(GsStats)]),
     "gs_reset_stats": (C.c_int, [P]),
     "gs_synchronize": (C.c_int, [P]),

@@ -94,6 +94,43 @@ struct AsyncQueue {
 };
 
 
+// In-process device transport (gs_comm_init_local): the ranks are threads of one process. Per exchange each rank
+// publishes its send block and the event recorded after its tag, the threads meet (host barrier, no GPU wait), every
+// rank enqueues on its stream a wait on each rank's event and the device-to-device copy of its block, publishes the
+// event after its copies, and after a second meeting waits on every rank's copies event on its stream: the collective
+// is complete on a rank's stream only once every rank has read its block, as with ncclAllGather, and the host never
+// waits for the GPU. A rank that does not arrive within GS_LOCAL_WAIT_S (60 s) fails the call with GS_ECOMM.
+struct gs_local_group {
+  int n = 0;
+  std::mutex mu;
+  std::condition_variable cv;
+  int arrived = 0;
+  uint64_t gen = 0;
+  bool broken = false;
+  std::vector<const uint8_t*> send;
+  std::vector<size_t> bytes;
+  std::vector<hipEvent_t> ready, done;
+  // true: every rank arrived; false: the wait expired or the group is broken (a rank failed)
+  bool meet(double limit_s) {
+    std::unique_lock<std::mutex> lk(mu);
+    if (broken) return false;
+    const uint64_t g = gen;
+    if (++arrived == n) {
+      arrived = 0;
+      ++gen;
+      cv.notify_all();
+      return true;
+    }
+    const bool ok = cv.wait_for(lk, std::chrono::duration<double>(limit_s), [&] { return gen != g || broken; });
+    if (!ok || broken) {
+      broken = true;
+      cv.notify_all();
+      return false;
+    }
+    return true;
+  }
+};
+
 struct gs_ctx {
   std::unordered_set<uint64_t> ext_reserved;   // pods placed with an extension-path Reserve (gs_schedule_ext)
   gs_config cfg{};
@@ -180,6 +217,8 @@ struct gs_ctx {
   ncclComm_t comm = nullptr;
   gs_allgather_fn cb = nullptr;
   void* cb_user = nullptr;
+  gs_local_group* lg = nullptr;     // in-process device transport (tests: ranks as threads)
+  hipEvent_t lg_ready = nullptr, lg_done = nullptr;
   // exchange sequence (XTag): every exchange's block carries (site, seq, batch, rank); all ranks check all tags
   std::atomic<uint64_t> xseq{0};    // exchanges so far
   std::atomic<uint64_t> xbatch{0};  // batch passes launched so far (launch_batch)
@@ -872,6 +911,59 @@ int exchange(gs_ctx* c, uint32_t site, uint8_t* d_send, uint8_t* d_recv, size_t 
     HIP_TRY(c, hipEventRecord(c->x_ev[2 * c->x_pending + 1], c->st));
     ++c->x_pending;
     return GS_OK;
+  } else if (c->lg) {
+    gs_local_group& g = *c->lg;
+    static const double limit = getenv("GS_LOCAL_WAIT_S") ? atof(getenv("GS_LOCAL_WAIT_S")) : 60.0;
+    HIP_TRY(c, launch_write_tag(d_send + bytes - sizeof(XTag), tag, c->st));
+    if (c->x_pending * 2 + 2 > (int)c->x_ev.size()) {
+      for (int k = 0; k < 2; ++k) {
+        hipEvent_t ev;
+        HIP_TRY(c, hipEventCreate(&ev));
+        c->x_ev.push_back(ev);
+      }
+    }
+    HIP_TRY(c, hipEventRecord(c->x_ev[2 * c->x_pending], c->st));
+    HIP_TRY(c, hipEventRecord(c->lg_ready, c->st));
+    {
+      std::lock_guard<std::mutex> lk(g.mu);
+      g.send[c->rank] = d_send;
+      g.bytes[c->rank] = bytes;
+      g.ready[c->rank] = c->lg_ready;
+    }
+    bool met;
+    {
+      Where w_(c, "exchange (local transport): the ranks' send blocks");
+      met = g.meet(limit);
+    }
+    if (!met)
+      return fail(c, GS_ECOMM, "local transport: a rank did not reach exchange %llu (%s, batch %llu) within %.0f s",
+                  (unsigned long long)tag.seq, xsite_name(site), (unsigned long long)tag.batch, limit);
+    bool same = true;
+    for (int s = 0; s < c->nranks; ++s) same = same && g.bytes[s] == bytes;
+    if (same)
+      for (int s = 0; s < c->nranks; ++s) {
+        HIP_TRY(c, hipStreamWaitEvent(c->st, g.ready[s], 0));
+        HIP_TRY(c, hipMemcpyAsync(d_recv + (size_t)s * bytes, g.send[s], bytes, hipMemcpyDeviceToDevice, c->st));
+      }
+    HIP_TRY(c, hipEventRecord(c->lg_done, c->st));
+    {
+      std::lock_guard<std::mutex> lk(g.mu);
+      g.done[c->rank] = c->lg_done;
+    }
+    {
+      Where w_(c, "exchange (local transport): the ranks' copies");
+      met = g.meet(limit);
+    }
+    if (!met)
+      return fail(c, GS_ECOMM, "local transport: a rank did not finish exchange %llu (%s, batch %llu) within %.0f s",
+                  (unsigned long long)tag.seq, xsite_name(site), (unsigned long long)tag.batch, limit);
+    if (!same) return fail(c, GS_ECOMM, "local transport: the ranks' blocks of exchange %llu differ in size",
+                           (unsigned long long)tag.seq);
+    for (int s = 0; s < c->nranks; ++s)
+      if (s != c->rank) HIP_TRY(c, hipStreamWaitEvent(c->st, g.done[s], 0));
+    HIP_TRY(c, hipEventRecord(c->x_ev[2 * c->x_pending + 1], c->st));
+    ++c->x_pending;
+    return GS_OK;
   } else if (c->cb) {
     if (bytes > c->xchg_bytes) return fail(c, GS_EINVAL, "exchange payload too large");
     Where w_(c, site == XSITE_LEVELS ? "exchange (levels): stream before the callback"
@@ -1067,8 +1159,8 @@ int alloc_exchange(gs_ctx* c) {
   HIP_TRY(c, hipHostMalloc(&c->h_xchg_recv, c->xchg_bytes * c->nranks + 64, hipHostMallocDefault));
   if (c->d_xmerged) { (void)hipFree(c->d_xmerged); c->d_xmerged = nullptr; }
   HIP_TRY(c, hipMalloc(&c->d_xmerged, xchg_block_bytes(c->B, LCAP) + 64));
-  if (!c->d_xerr) HIP_TRY(c, hipMalloc(&c->d_xerr, 16));
-  HIP_TRY(c, hipMemset(c->d_xerr, 0, 16));
+  if (!c->d_xerr) HIP_TRY(c, hipMalloc(&c->d_xerr, XERR_BYTES));
+  HIP_TRY(c, hipMemset(c->d_xerr, 0, XERR_BYTES));
   if (!c->d_xsmall) HIP_TRY(c, hipMalloc(&c->d_xsmall, XSMALL * (1 + MAX_RANKS)));
   if (!c->h_xsmall) HIP_TRY(c, hipHostMalloc(&c->h_xsmall, XSMALL * MAX_RANKS, hipHostMallocDefault));
   if (const char* sk = getenv("GS_DEBUG_XCHG_SKEW")) {   // "rank:batch" (tests of the sequence check)
@@ -1277,12 +1369,14 @@ int finish_batch(gs_ctx* c, int b, bool clobbered, int* committed_out) {
   int committed = c->h_committed[0];
   if (committed < 0) return fail(c, GS_ESTATE, "commit pass of a batch was voided unexpectedly");
   if (c->h_committed[3] == COMMIT_ERR_XTAG) {   // the level exchange paired different exchanges of the ranks
-    std::vector<uint8_t> blk((size_t)c->xchg_bytes * c->nranks);
+    // the first mismatching exchange's tags, as merge_levels_kernel kept them
+    std::vector<uint8_t> xe(XERR_BYTES);
     HIP_TRY(c, host_wait_stream(c->st));
-    HIP_TRY(c, hipMemcpy(blk.data(), c->d_xchg_recv, blk.size(), hipMemcpyDeviceToHost));
+    HIP_TRY(c, hipMemcpy(xe.data(), c->d_xerr, xe.size(), hipMemcpyDeviceToHost));
+    const uint8_t* tags = xe.data() + 4 * XERR_TAGS;
     XTag mine;
-    std::memcpy(&mine, blk.data() + (size_t)c->rank * c->xchg_bytes + c->xchg_bytes - sizeof(XTag), sizeof mine);
-    if (int rc = check_tags(c, blk.data(), c->xchg_bytes, mine)) return rc;
+    std::memcpy(&mine, tags + (size_t)c->rank * sizeof(XTag), sizeof mine);
+    if (int rc = check_tags(c, tags, sizeof(XTag), mine)) return rc;
     return fail(c, GS_ECOMM, "exchange sequence diverged at a level exchange (device check)");
   }
   if (c->h_committed[3])
@@ -2176,6 +2270,8 @@ int gs_destroy(gs_ctx* c) {
     (void)hipFree(c->d_stamps);
   }
   if (c->comm) ncclCommDestroy(c->comm);
+  if (c->lg_ready) (void)hipEventDestroy(c->lg_ready);
+  if (c->lg_done) (void)hipEventDestroy(c->lg_done);
   for (hipEvent_t ev : c->x_ev) (void)hipEventDestroy(ev);
   if (c->st) (void)host_wait_stream(c->st);
   if (c->st_ev) (void)host_wait_stream(c->st_ev);
@@ -2915,6 +3011,38 @@ int gs_comm_init_callback(gs_ctx* c, int nranks, int rank, gs_allgather_fn fn, v
   c->cb = fn;
   c->cb_user = user;
   c->nranks = nranks;
+  c->rank = rank;
+  set_shard(c);
+  c->numa_idx_stale = true;
+  return alloc_exchange(c);
+}
+
+int gs_local_group_create(int nranks, gs_local_group** out) {
+  if (!out || nranks < 1 || nranks > MAX_RANKS) return GS_EINVAL;
+  gs_local_group* g = new gs_local_group;
+  g->n = nranks;
+  g->send.assign(nranks, nullptr);
+  g->bytes.assign(nranks, 0);
+  g->ready.assign(nranks, nullptr);
+  g->done.assign(nranks, nullptr);
+  *out = g;
+  return GS_OK;
+}
+
+int gs_local_group_destroy(gs_local_group* g) {
+  delete g;
+  return GS_OK;
+}
+
+int gs_comm_init_local(gs_ctx* c, gs_local_group* g, int rank) {
+  if (!c || !g || rank < 0 || rank >= g->n) return GS_EINVAL;
+  quiesce(c);
+  if (c->window_k && g->n > 1) return fail(c, GS_EUNSUPPORTED, "node sampling runs on one GPU");
+  HIP_TRY(c, hipSetDevice(c->cfg.device));
+  if (!c->lg_ready) HIP_TRY(c, hipEventCreateWithFlags(&c->lg_ready, hipEventDisableTiming));
+  if (!c->lg_done) HIP_TRY(c, hipEventCreateWithFlags(&c->lg_done, hipEventDisableTiming));
+  c->lg = g;
+  c->nranks = g->n;
   c->rank = rank;
   set_shard(c);
   c->numa_idx_stale = true;

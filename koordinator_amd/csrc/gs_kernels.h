@@ -177,6 +177,8 @@ static_assert(sizeof(XTag) == 32, "XTag layout");
 constexpr uint32_t XTAG_MAGIC = 0x31585347u;   // "GSX1"
 enum : uint32_t { XSITE_LEVELS = 1, XSITE_ROWSTAT = 2, XSITE_SELECT = 3 };
 constexpr int32_t COMMIT_ERR_XTAG = 90;   // committed[3]: the level exchange's tags disagree (nothing committed)
+constexpr int XERR_TAGS = 8;   // merge_levels_kernel's xerr: [0] verdict, [1] first mismatch kept, [8..] its R tags
+constexpr size_t XERR_BYTES = 4 * XERR_TAGS + sizeof(XTag) * MAX_RANKS;
 // tag -> dst (RCCL: written on the stream right before the all-gather, so the tag travels with the block)
 hipError_t launch_write_tag(uint8_t* dst, const XTag& t, hipStream_t st);
 // several shards: per pod, the all-gathered rank blocks' levels merged into one block of the single-rank layout (the

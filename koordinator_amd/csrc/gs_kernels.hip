@@ -782,6 +782,16 @@ __global__ void __launch_bounds__(256) merge_levels_kernel(const uint8_t* __rest
         bad = 1 + r;
     }
     xerr[0] = bad;
+    // the first mismatch's tags, kept for the host's report (the blocks themselves are overwritten by the next
+    // exchange, which a stream-ordered transport has enqueued before the host reads this batch's verdict)
+    if (bad && !xerr[1]) {
+      xerr[1] = 1;
+      uint32_t* dst = reinterpret_cast<uint32_t*>(xerr + XERR_TAGS);
+      for (int r = 0; r < R; ++r) {
+        const uint32_t* tr = reinterpret_cast<const uint32_t*>(xin + (size_t)r * xblock + xblock - sizeof(XTag));
+        for (int w = 0; w < (int)(sizeof(XTag) / 4); ++w) dst[r * (sizeof(XTag) / 4) + w] = tr[w];
+      }
+    }
   }
   // rank blocks: lists at lstride entries per pod; the merged block has the single-rank layout (LCAP per pod)
   const size_t ihoff = (size_t)bmax * lstride * 4, ixoff = ihoff + (size_t)bmax * sizeof(LevelHdr);

@@ -35,6 +35,22 @@ class GpuScoreError(RuntimeError):
     pass
 
 
+class LocalGroup:
+    """The in-process device transport's group (gs_local_group): the ranks are threads of this process, each with its
+    own Engine; the level all-gathers run stream-ordered on the device as ncclAllGather does."""
+
+    def __init__(self, nranks: int):
+        self._h = C.c_void_p()
+        rc = lib().gs_local_group_create(nranks, C.byref(self._h))
+        if rc != 0:
+            raise GpuScoreError(f"gs_local_group_create: {rc}")
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            lib().gs_local_group_destroy(self._h)
+            self._h = None
+
+
 class Engine:
     def __init__(self, cfg: abi.GsConfig):
         self.cfg = cfg
@@ -240,6 +256,11 @@ class Engine:
                 return -1
         self._cb = abi.ALLGATHER_FN(_cb)
         self._chk(lib().gs_comm_init_callback(self._h, nranks, rank, self._cb, None), "gs_comm_init_callback")
+
+    def comm_init_local(self, group: "LocalGroup", rank: int):
+        """In-process device transport: this context is rank `rank` of `group` (ranks as threads of this process)."""
+        self._group = group   # the group outlives its contexts
+        self._chk(lib().gs_comm_init_local(self._h, group._h, rank), "gs_comm_init_local")
 
     def stats(self) -> dict:
         s = abi.GsStats()

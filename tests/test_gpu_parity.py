@@ -246,6 +246,67 @@ def test_two_ranks_on_one_gpu_callback_transport():
     assert engines[0].stats()["shard_end"] == engines[1].stats()["shard_begin"]
 
 
+def run_ranks_local(c, cfg, n, pods=None, enabled=None):
+    """n ranks as threads of this process on the box's GPU, over the in-process device transport
+    (gs_comm_init_local): the level all-gathers run stream-ordered, as ncclAllGather does, instead of through a host
+    callback; returns every rank's placements (or its exception)."""
+    from koordinator_amd.engine import Engine, LocalGroup
+    g = LocalGroup(n)
+    engines = [Engine(cfg) for _ in range(n)]
+    for r, x in enumerate(engines):
+        synth.load_into(x, c)
+        x.comm_init_local(g, r)
+    pods = c.pods if pods is None else pods
+    res = [None] * n
+
+    def run(r):
+        try:
+            res[r] = engines[r].schedule(pods)
+        except Exception as ex:   # noqa: BLE001 (reported per rank)
+            res[r] = ex
+    th = [threading.Thread(target=run, args=(r,)) for r in range(n)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=300)
+    return res, engines, g
+
+
+@pytest.mark.parametrize("n,numa", [(2, False), (4, True)], ids=["2ranks", "4ranks-numa"])
+def test_ranks_on_one_gpu_device_transport(n, numa):
+    """The sharded path over the stream-ordered device transport (RCCL's ordering: tags written on the stream, the
+    blocks copied device-to-device behind the senders' events, the next batch's kernels behind every rank's copies,
+    batches in flight across exchanges): every rank's placements equal the oracle's."""
+    c = synth.make_cluster(3001, 400, 13)
+    en = abi.GS_ENABLE_ALL if numa else abi.GS_ENABLE_LA_FIT
+    if numa:
+        synth.make_numa(c)
+    cfg = config.make_config(c.num_nodes, enabled=en)
+    res, engines, _ = run_ranks_local(c, cfg, n)
+    o = orc.Oracle(cfg)
+    synth.load_into(o, c)
+    want = o.schedule(c.pods)
+    for r in range(n):
+        assert not isinstance(res[r], Exception) and res[r] is not None, (r, res[r])
+        for f in ("node", "score", "ties", "feasible"):
+            assert np.array_equal(res[r][f], want[f]), (r, f)
+    for r in range(n - 1):
+        assert engines[r].stats()["shard_end"] == engines[r + 1].stats()["shard_begin"]
+
+
+def test_device_transport_divergence_fails_on_every_rank(monkeypatch):
+    """A rank whose exchange sequence diverges over the device transport: every rank fails with GS_ECOMM naming the
+    batch (the tags travel with the blocks and merge_levels_kernel checks them on each rank's stream)."""
+    c = synth.make_cluster(3001, 300, 13)
+    cfg = config.make_config(c.num_nodes)
+    monkeypatch.setenv("GS_DEBUG_XCHG_SKEW", "1:1")
+    res, _, _ = run_ranks_local(c, cfg, 2)
+    for r in range(2):
+        assert isinstance(res[r], Exception), (r, res[r])
+        msg = str(res[r])
+        assert "exchange sequence diverged" in msg and "batch 1" in msg, (r, msg)
+
+
 def test_reset_rebuilds_mirror():
     """gs_reset (device-error recovery) rebuilds the HBM mirror from the host state: scheduling continues
     bit-exact with the oracle."""
