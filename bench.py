@@ -305,21 +305,26 @@ def main() -> None:
     setup = ("gs::scatter_rows_kernel", "gs::node_prep_kernel")
     if kpmc:
         # the profiled run's step count: commit_spec_kernel launches once per batch
-        commit = kpmc.get("gs::commit_spec_kernel<false>", {})
+        commit = next((v for k, v in kpmc.items() if k.startswith("gs::commit_spec_kernel<false")), {})
         steps_in_pmc = max(1.0, commit.get("dispatches", 0) / max(1.0, batches / args.steps))
         traffic_step = sum(v["hbm_bytes_per_launch"] * v["dispatches"] for k, v in kpmc.items()
                            if k.startswith("gs::") and not k.startswith(setup)) / steps_in_pmc
     kernels = {
-        "eval_pass": {"kernels": "eval_kernel + eval_numa_kernel (concurrent streams), one launch each per batch",
+        "eval_pass": {"kernels": "gather_numa_kernel -> eval_numa_tile_kernel (full batches) beside eval_kernel on a second "
+                                 "stream, one launch each per batch",
                       "avg_launch_us": eval_us, "pairs_per_launch": pairs_per_launch,
                       "achieved_GBps": eval_achieved, "frac": eval_achieved / HBM_PEAK_GBPS,
-                      "pmc_bytes_per_launch": pmc_bytes("gs::eval"),
+                      "pmc_bytes_per_launch": (pmc_bytes("gs::eval") or 0) + (pmc_bytes("gs::gather_numa") or 0)
+                      if pmc_bytes("gs::eval") else None,
                       "share_of_step": st["eval_ms"] / args.steps / step_ms},
         "patch_cand_interval": {"what": "from the eval pass's end (HIP event) to the commit kernel's start (the "
                                         "batch's end event minus the commit's own s_memrealtime duration): "
                                         "cand_kernel beside the previous batch's commit, the wait for that commit, "
                                         "then fix_levels_kernel (its landed rows re-evaluated and folded into the "
                                         "levels); the kernels' own durations are in the rocprof summary",
+                                "critical_path": "only fix_levels_kernel (~32 us per batch in the kernel trace) and "
+                                                 "its launch gap are on the commit chain; the rest of the interval "
+                                                 "runs beside, or waits for, the previous batch's commit",
                                 "avg_us": st["cand_ms"] / batches * 1e3,
                                 "pmc_bytes_per_launch": (pmc_bytes("gs::cand") or 0) + (pmc_bytes("gs::fix_levels") or 0)
                                 if (pmc_bytes("gs::cand") or pmc_bytes("gs::fix_levels")) else None,

@@ -34,7 +34,7 @@ def main():
         kernels[k] = {"dispatches": max(f.get(k, (0, 0))[1], w.get(k, (0, 0))[1]),
                       "FETCH_SIZE_KiB": fk, "WRITE_SIZE_KiB": wk,
                       "hbm_bytes_per_launch": 2 * fk * 1024 + wk * 1024}
-    ev = [k for k in kernels if k.startswith("gs::eval_kernel") or k.startswith("gs::eval_numa_kernel")]
+    ev = [k for k in kernels if k.startswith("gs::eval_") or k.startswith("gs::gather_numa")]
     res = {
         "note": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes over bench.py --steps 1 "
                 "--warmup 0 (C3); per-dispatch means; read bytes = 2 x FETCH_SIZE (gfx950 correction)",
