@@ -2204,6 +2204,11 @@ int gs_destroy(gs_ctx* c) {
         fprintf(stderr, "  wave 0 total %.0f: checks %.0f | dirty state %.0f | hdr+fresh store+dirty loads %.0f | level scan "
                 "%.0f | winner %.0f | fresh slot %.0f | record %.0f | waiting %.0f (at batch end %.0f) | full-row %.0f\n",
                 W(0, 12), W(0, 27), W(0, 28), W(0, 29), W(0, 18), W(0, 19), W(0, 20), W(0, 0), W(0, 2), W(0, 23), W(0, 11));
+        if (sa[64 + 9] > 0)   // the split selector: wave 0 finishes the prep wave's decisions and verifies
+          fprintf(stderr, "  wave 0 (split): verification loop %.0f | fresh slot's scores + snapshot %.0f | record read + late "
+                  "decisions %.0f | exclusions %.0f | rows settled early %.0f | window %.0f | record %.0f (fresh slot %.0f) | "
+                  "waiting %.0f (the loop's passes while waiting count in the first two)\n", W(0, 55), W(0, 27), W(0, 52),
+                  W(0, 53), W(0, 54), W(0, 19), W(0, 0), W(0, 20), W(0, 2));
         fprintf(stderr, "  winner split: ties + tie-break position %.0f | old-nodes path: level segment + list window %.0f\n",
                 W(0, 30), W(0, 46));
         fprintf(stderr, "  late-landing estimate: %llu decisions, previous pod's row as it stood > M %llu, == M %llu (tie-break "
@@ -2230,12 +2235,18 @@ int gs_destroy(gs_ctx* c) {
         fprintf(stderr, "  pending row's pre-landing score >= M: %llu decisions, %llu of the rollbacks; > M: %llu decisions, %llu "
                 "of the rollbacks\n", (unsigned long long)sa[42], (unsigned long long)sa[43], (unsigned long long)sa[44],
                 (unsigned long long)sa[45]);
-        fprintf(stderr, "  wave 4 (verify): busy %.0f waiting %.0f\n", W(4, 1), W(4, 2));
+        const bool split = sa[64 + 9] > 0;   // the prep wave counted its records: the split selector ran
+        if (split)
+          fprintf(stderr, "  wave 1 (prep): busy %.0f (dirty state %.0f, loads %.0f, level scan %.0f, winner %.0f, record "
+                  "%.0f) waiting %.0f\n", W(1, 28) + W(1, 29) + W(1, 18) + W(1, 30) + W(1, 46) + W(1, 19) + W(1, 0),
+                  W(1, 28), W(1, 29), W(1, 18), W(1, 30) + W(1, 46) + W(1, 19), W(1, 0), W(1, 2));
+        else
+          fprintf(stderr, "  wave 4 (verify): busy %.0f waiting %.0f\n", W(4, 1), W(4, 2));
         for (int w = 2; w < 4; ++w)
           fprintf(stderr, "  wave %d (Reserve): fetch+undo %.0f numa_eval %.0f lane0 %.0f rest %.0f (fresh fetch %.0f, landed-"
                   "again wait %.0f) waiting %.0f (first decision %.0f)\n", w, W(w, 15), W(w, 16), W(w, 17), W(w, 5), W(w, 21),
                   W(w, 22), W(w, 6), W(w, 26));
-        for (int w : {1, 5, 6, 7})
+        for (int w : {split ? 4 : 1, 5, 6, 7})
           fprintf(stderr, "  wave %d (re-scoring): busy %.0f (row copy + hint table %.0f, scores %.0f) waiting %.0f, jobs %.2f "
                   "per pod\n", w, W(w, 7) + W(w, 9), W(w, 9), W(w, 7), W(w, 8), W(w, 10));
         const double nb = c->stats.batches ? (double)c->stats.batches * c->B : 1.0;
