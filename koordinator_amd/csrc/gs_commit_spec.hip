@@ -56,11 +56,11 @@ constexpr int SP_W_VERIFY = 4;
 __device__ __forceinline__ int sp_reserve_index(int wv) { return wv == 2 ? 0 : wv == 3 ? 1 : -1; }
 __device__ __forceinline__ int sp_rescore_index(int wv) { return wv == 1 ? 0 : wv >= 5 ? wv - 4 : -1; }
 constexpr int SP_JOBQ = 24;      // job ring per Reserve wave (<= 3 jobs per pod, <= SP_LAG / 2 + 2 pods in flight)
-constexpr int SP_HASH = 256;     // node -> slot (full-row resolution)
+constexpr int SP_HASH = 128;     // node -> slot (full-row resolution; <= MAX_BATCH slots, linear probing)
 constexpr int SP_FRESH = 1, SP_FITERR = 2, SP_SLOW = 4, SP_OFFSHARD = 8;   // DecRec.flags
 constexpr int SP_PRED_GE = 16, SP_PRED_GT = 32;   // diagnostics (ST): a pending row's pre-landing score >= / > M
 constexpr uint32_t SP_SPIN_LIMIT = 1u << 24;
-constexpr int SP_NST = 60, SP_STRIDE = 64;   // diagnostics: stamps per wave, the wave's region in a.stamps
+constexpr int SP_NST = 62, SP_STRIDE = 64;   // diagnostics: stamps per wave, the wave's region in a.stamps
 constexpr int16_t SO_UNKNOWN = -2;    // dso: batch-start score of an off-shard fresh row not evaluated yet
 constexpr int16_t SO_UNLISTED = -3;   // a decision's view of such a row not in the pod's list head
 
@@ -84,7 +84,7 @@ struct Job {
 };
 // the split pipeline (SPLIT): the prep wave's provisional decision of pod p for wave 0
 constexpr int SP_KW = 4;          // ties recorded from the tie-break position on (the window wave 0 re-ranks in)
-constexpr int SP_PREPQ = 2;       // PrepRec ring: the prep wave works at most SP_PREPQ - 1 pods ahead of wave 0
+constexpr int SP_PREPQ = 3;       // PrepRec ring: the prep wave works at most SP_PREPQ - 1 pods ahead of wave 0
 constexpr int SP_W_PREP = 1;      // its wave (SIMD 1; wave 0 decides on SIMD 0)
 struct PrepRec {                    // (the first 80 bytes read as five 16-byte words)
   int32_t pod, q_s, nd_s, action;   // q_s: decisions in the snapshot (nd_s slots); action 0, 1 (FitError), 2 (stop),
@@ -736,6 +736,8 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
   // as the verify wave: pod v stands iff every row pending at its decision now scores below its maximum for it (its
   // feasible ones join the Feasible count); a miss asks wave 0 to roll back to v (s_rb_req).
   const bool vshare = SPLIT && ((a.dbg >> 17) & 1u);
+  // pods the prep wave may work ahead of wave 0's decisions: 1 + 1 (GS_SPEC_AHEAD=2, dbg bit 18: + 2)
+  const int prep_ahead = ((a.dbg >> 18) & 1u) ? SP_PREPQ : SP_PREPQ - 1;
   auto verify_try = [&]() {
     int got = 0;
     if (lane == 0) {
@@ -1146,6 +1148,12 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
         if (lane == 0 && ld_acq(&s_snap) != q) st_rel(&s_snap, q);
         SPM(27);   // verification, fresh slot's scores
         if (q >= end_at || q - ver >= lag || cut_at >= 0 || ld_acq(&s_prep_done) <= q || ld_acq(&s_reprep)) {
+          if (ST) {   // diagnostics: why wave 0 waits (first reason that holds)
+            const uint64_t tw = __builtin_amdgcn_s_memtime();
+            const int why = q >= end_at ? 0 : q - ver >= lag ? 1 : cut_at >= 0 ? 2 : ld_acq(&s_reprep) ? 3 : 4;
+            st_acc[56 + why] += 1;
+            (void)tw;
+          }
           if (++spins > SP_SPIN_LIMIT) { err = true; err_code = 2; break; }
           if (const int we = ld_acq(&s_werr)) { err = true; err_code = we; break; }
           if (vshare) verify_try();
@@ -1279,7 +1287,7 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
         p = rq - 1;
         wait = ld_acq(&s_snap) != p;
       } else {
-        wait = pn >= B || pn >= ld_acq(&s_decided) + SP_PREPQ;
+        wait = pn >= B || pn >= ld_acq(&s_decided) + prep_ahead;
       }
       if (wait) {
         if (++spins > SP_SPIN_LIMIT) {

@@ -1231,7 +1231,10 @@ CommitArgs commit_args(gs_ctx* c, int b) {
   // bit 16: the default (GS_SPEC_SPLIT=0: the single selector wave); GS_SPEC_SPLIT=2 (experiments): and the decided
   // pods verified by the re-scoring / Reserve waves (bit 17)
   static const int split = getenv("GS_SPEC_SPLIT") ? atoi(getenv("GS_SPEC_SPLIT")) : 1;
-  a.dbg = (nospec ? 1u : 0u) | prio | lag << 12 | (split >= 1 ? 1u << 16 : 0u) | (split >= 2 ? 1u << 17 : 0u);
+  // GS_SPEC_AHEAD=2 (experiments): the prep wave may run two pods ahead (bit 18)
+  static const bool ahead2 = getenv("GS_SPEC_AHEAD") && getenv("GS_SPEC_AHEAD")[0] == '2';
+  a.dbg = (nospec ? 1u : 0u) | prio | lag << 12 | (split >= 1 ? 1u << 16 : 0u) | (split >= 2 ? 1u << 17 : 0u) |
+          (ahead2 ? 1u << 18 : 0u);
   a.tb = c->d_tb;
   a.xerr = c->nranks > 1 ? c->d_xerr : nullptr;
   return a;
@@ -2209,6 +2212,9 @@ int gs_destroy(gs_ctx* c) {
                   "decisions %.0f | exclusions %.0f | rows settled early %.0f | window %.0f | record %.0f (fresh slot %.0f) | "
                   "waiting %.0f (the loop's passes while waiting count in the first two)\n", W(0, 55), W(0, 27), W(0, 52),
                   W(0, 53), W(0, 54), W(0, 19), W(0, 0), W(0, 20), W(0, 2));
+        if (sa[64 + 9] > 0)
+          fprintf(stderr, "  wave 0 (split) waiting passes per pod: batch end %.2f | speculation depth %.2f | host cut %.2f | "
+                  "exact record asked %.2f | prep record not ready %.2f\n", W(0, 56), W(0, 57), W(0, 58), W(0, 59), W(0, 60));
         fprintf(stderr, "  winner split: ties + tie-break position %.0f | old-nodes path: level segment + list window %.0f\n",
                 W(0, 30), W(0, 46));
         fprintf(stderr, "  late-landing estimate: %llu decisions, previous pod's row as it stood > M %llu, == M %llu (tie-break "
