@@ -82,6 +82,20 @@ def test_no_gpu_fails_loudly():
         engine.Engine(cfg)
 
 
+def test_local_group_host_side(lib):
+    """The device transport's group is host-only state: it is created and destroyed without a GPU, and refuses a bad
+    rank count; binding a context to it needs one (GPU tests: test_gpu_parity.py)."""
+    import ctypes as C
+    from koordinator_amd.engine import LocalGroup
+    g = LocalGroup(4)
+    assert g._h
+    del g
+    h = C.c_void_p()
+    assert lib.gs_local_group_create(0, C.byref(h)) != 0
+    assert lib.gs_local_group_create(abi.MAX_RANKS + 1 if hasattr(abi, "MAX_RANKS") else 9, C.byref(h)) != 0
+    assert lib.gs_comm_init_local(None, None, 0) != 0
+
+
 def test_pod_decoding_quantities():
     p = objects.make_pod({"containers": [{"requests": {"cpu": "1500m", "memory": "1Gi"},
                                           "limits": {"cpu": "2", "memory": "1Gi"}}]})
