@@ -2217,7 +2217,8 @@ int gs_destroy(gs_ctx* c) {
                   "exact record asked %.2f | prep record not ready %.2f\n", W(0, 56), W(0, 57), W(0, 58), W(0, 59), W(0, 60));
         fprintf(stderr, "  winner split: ties + tie-break position %.0f | old-nodes path: level segment + list window %.0f\n",
                 W(0, 30), W(0, 46));
-        fprintf(stderr, "  late-landing estimate: %llu decisions, previous pod's row as it stood > M %llu, == M %llu (tie-break "
+        if (sa[64 + 9] == 0)   // (single selector wave; the split selector reuses these entries, printed below)
+          fprintf(stderr, "  late-landing estimate: %llu decisions, previous pod's row as it stood > M %llu, == M %llu (tie-break "
                 "position moves %llu)\n", (unsigned long long)sa[47], (unsigned long long)sa[48], (unsigned long long)sa[49],
                 (unsigned long long)sa[50]);
         fprintf(stderr, "  wave 0 raw (cycles per pod by stamp index):");
