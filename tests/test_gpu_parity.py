@@ -133,6 +133,28 @@ def homogeneous_cluster(nodes, pods, seed):
     return c
 
 
+@pytest.mark.parametrize("nodes,pods,numa,batch", [(60, 1024, False, 128), (200, 1024, False, 32), (90, 640, True, 128)],
+                         ids=["60n", "200n-b32", "90n-numa"])
+def test_contention_few_nodes_many_pods(nodes, pods, numa, batch):
+    """Many pods on few nodes: most decisions land on rows earlier pods of the batch landed on (re-landings, dirty
+    slots past 64, rollbacks, the split selector's exclusions, exact re-records and full decisions), bit-exact."""
+    c = synth.make_cluster(nodes, pods, 21)
+    if numa:
+        synth.make_numa(c)
+    kw = dict(enabled=abi.GS_ENABLE_ALL) if numa else {}
+    e, o = pair(c, batch_size=batch, **kw)
+    got = _check_schedule(e, o, c.pods)
+    assert (got["node"] >= 0).sum() > pods // 4
+
+
+def test_homogeneous_cluster_massive_ties_many_pods():
+    """Identical empty nodes, 1,024 pods: every decision a large tie whose winner moves as rows fill up."""
+    c = homogeneous_cluster(400, 1024, 5)
+    e, o = pair(c)
+    got = _check_schedule(e, o, c.pods)
+    assert got["ties"].max() > 100
+
+
 def test_homogeneous_cluster_massive_ties():
     """Identical empty nodes: every node ties, candidate lists overflow -> exact full-row path (in the commit
     kernel on a single shard)."""
