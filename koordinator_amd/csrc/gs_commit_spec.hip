@@ -736,6 +736,8 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
   // as the verify wave: pod v stands iff every row pending at its decision now scores below its maximum for it (its
   // feasible ones join the Feasible count); a miss asks wave 0 to roll back to v (s_rb_req).
   const bool vshare = SPLIT && ((a.dbg >> 17) & 1u);
+  // (dbg bit 19, with 17: the prep wave verifies while it waits for the ring, the re-scoring / Reserve waves do not)
+  const bool vprep = vshare && ((a.dbg >> 19) & 1u);
   // pods the prep wave may work ahead of wave 0's decisions: 1 + 1 (GS_SPEC_AHEAD=2, dbg bit 18: + 2)
   const int prep_ahead = ((a.dbg >> 18) & 1u) ? SP_PREPQ : SP_PREPQ - 1;
   auto verify_try = [&]() {
@@ -1294,7 +1296,8 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
           if (lane == 0) __atomic_store_n(&s_werr, 10, __ATOMIC_RELEASE);
           break;
         }
-        if (pn >= B && !rq) sp_sleep();
+        if (vprep) verify_try();   // its idle time: the decided pods' verification
+        else if (pn >= B && !rq) sp_sleep();
         else __builtin_amdgcn_s_sleep(1);
         SPM(2);
         continue;
@@ -1526,7 +1529,7 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
           __atomic_store_n(&resv[q], 1, __ATOMIC_RELEASE);
         }
         WAVE_FENCE();
-        if (vshare) verify_try();
+        if (vshare && !vprep) verify_try();
         q += SP_NRES;
         continue;
       }
@@ -1695,7 +1698,7 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
       WAVE_FENCE();
       if (lane == 0) __atomic_store_n(&resv[q], 1, __ATOMIC_RELEASE);
       WAVE_FENCE();
-      if (vshare && njobs == 0) verify_try();
+      if (vshare && !vprep && njobs == 0) verify_try();
       q += SP_NRES;
       SPM(5);
     }
@@ -1778,7 +1781,7 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
         }
       }
       WAVE_FENCE();
-      if (vshare && __builtin_amdgcn_readfirstlane(fin)) verify_try();
+      if (vshare && !vprep && __builtin_amdgcn_readfirstlane(fin)) verify_try();
       if (ST) st_acc[10] += 1;
       SPM(7);
     }

@@ -1233,8 +1233,9 @@ CommitArgs commit_args(gs_ctx* c, int b) {
   static const int split = getenv("GS_SPEC_SPLIT") ? atoi(getenv("GS_SPEC_SPLIT")) : 1;
   // GS_SPEC_AHEAD=2 (experiments): the prep wave may run two pods ahead (bit 18)
   static const bool ahead2 = getenv("GS_SPEC_AHEAD") && getenv("GS_SPEC_AHEAD")[0] == '2';
+  // GS_SPEC_SPLIT=3 (experiments): shared verification by the prep wave while it waits (bits 17 and 19)
   a.dbg = (nospec ? 1u : 0u) | prio | lag << 12 | (split >= 1 ? 1u << 16 : 0u) | (split >= 2 ? 1u << 17 : 0u) |
-          (ahead2 ? 1u << 18 : 0u);
+          (ahead2 ? 1u << 18 : 0u) | (split >= 3 ? 1u << 19 : 0u);
   a.tb = c->d_tb;
   a.xerr = c->nranks > 1 ? c->d_xerr : nullptr;
   return a;
