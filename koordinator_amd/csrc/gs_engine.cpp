@@ -2619,6 +2619,25 @@ int schedule_stream(gs_ctx* c, PodRun run, Next&& next_run, Done&& run_done) {
     }
     return GS_OK;
   };
+  // Deferred application: a batch that committed every pod with no host work and no special pod changes no row on
+  // the host side (apply_placement / numa_reserve only mirror what the commit wrote to HBM), so its placements are
+  // applied to the host state after the batch two ahead is launched — the eval pass then starts right as the previous
+  // commit ends instead of after the host's ~0.2 ms of bookkeeping, and runs beside the next commit (GS_DEFER_APPLY=0:
+  // apply first).
+  static const bool defer_ok = !(getenv("GS_DEFER_APPLY") && getenv("GS_DEFER_APPLY")[0] == '0');
+  struct Pend {
+    const gs_pod* pods = nullptr;
+    gs_placement* out = nullptr;
+    int n = 0;
+    bool active = false;
+  } pend;
+  std::vector<PlacementDev> pend_out;
+  std::vector<PodVec> pend_pods;
+  auto apply_pending = [&]() -> int {
+    if (!pend.active) return GS_OK;
+    pend.active = false;
+    return apply_batch(pend.pods, pend.out, pend.n, pend_out.data(), pend_pods.data(), false);
+  };
   auto body = [&]() -> int {
     int rc = GS_OK;
     uint32_t i = 0;
@@ -2626,6 +2645,7 @@ int schedule_stream(gs_ctx* c, PodRun run, Next&& next_run, Done&& run_done) {
     int cur_b = 0;
     for (;;) {
       if (i == run.n) {   // the run is complete; the next one (its first batch may be in flight already)
+        if ((rc = apply_pending())) { drain(); return rc; }
         run_done(run, GS_OK);
         if (!have_nxt) have_nxt = next_run(&nxt);
         if (!have_nxt) break;
@@ -2636,6 +2656,7 @@ int schedule_stream(gs_ctx* c, PodRun run, Next&& next_run, Done&& run_done) {
       }
       const gs_pod* pods = run.pods;
       if (!inflight) {
+        if ((rc = apply_pending())) { drain(); return rc; }
         if ((rc = flush_rows(c))) return rc;
         if (c->prep_stale && (rc = node_prep(c))) return rc;
         cur_b = batch_len(c, pods, i, run.n, &cur_special);
@@ -2659,6 +2680,10 @@ int schedule_stream(gs_ctx* c, PodRun run, Next&& next_run, Done&& run_done) {
       using hclk = std::chrono::steady_clock;
       const auto t_a = hclk::now();
       double busy = 0;
+      if (pend.active && np) {   // the next batch shares a pod uid with the deferred one: its host state first
+        const int nb0 = std::min<int>(c->B, (int)(nn - nj));
+        if (uid_overlap(pend.pods, pend.n, np + nj, nb0) && (rc = apply_pending())) { drain(); return rc; }
+      }
       if (can_spec && spec_ok && !cur_special && np && c->dirty_list.empty() && !c->prep_stale) {
         bool sf = false;
         nb = batch_len(c, np, nj, nn, &sf);
@@ -2682,6 +2707,8 @@ int schedule_stream(gs_ctx* c, PodRun run, Next&& next_run, Done&& run_done) {
           spec = true;
         }
       }
+      // the previous batch's deferred placements, while this batch and the one after it run
+      if ((rc = apply_pending())) { drain(); return rc; }
       spec_ok = true;
       int committed = 0;
       const auto t_w = hclk::now();
@@ -2689,6 +2716,7 @@ int schedule_stream(gs_ctx* c, PodRun run, Next&& next_run, Done&& run_done) {
       const auto t_f = hclk::now();
       if (rc == GS_REDO) {   // pod 0 needs the full-row path, the speculative pass (void) overwrote its lists: re-run
         drain();
+        if ((rc = apply_pending())) return rc;
         if ((rc = stage_batch(c, pods, run.seq, i, cur_b, false))) return rc;
         if ((rc = launch_batch(c, cur_b, nullptr))) return rc;
         inflight = true;
@@ -2697,7 +2725,16 @@ int schedule_stream(gs_ctx* c, PodRun run, Next&& next_run, Done&& run_done) {
       }
       if (rc) { if (spec) drain(); return rc; }
       const bool host_work = c->h_committed[1] != 1;   // the device-side continuation flag the speculative pass read
-      if ((rc = apply_batch(pods + i, run.out + i, committed, c->h_out, c->h_pods, cur_special))) {
+      if (defer_ok && spec && !host_work && !cur_special && committed == cur_b) {
+        // no host row changes: keep the results (this slot's buffers are reused by the batch two ahead) and apply them
+        // after that batch is launched
+        pend_out.assign(c->h_out, c->h_out + committed);
+        pend_pods.assign(c->h_pods, c->h_pods + committed);
+        pend.pods = pods + i;
+        pend.out = run.out + i;
+        pend.n = committed;
+        pend.active = true;
+      } else if ((rc = apply_batch(pods + i, run.out + i, committed, c->h_out, c->h_pods, cur_special))) {
         if (spec) drain();
         return rc;
       }
@@ -2730,9 +2767,14 @@ int schedule_stream(gs_ctx* c, PodRun run, Next&& next_run, Done&& run_done) {
         }
       }
     }
+    if ((rc = apply_pending())) return rc;
     return flush_rows(c);
   };
   int rc = body();
+  if (rc && pend.active) {   // a batch the device committed: its placements reach the outputs and the host state
+    drain();
+    (void)apply_pending();
+  }
   if (rc) {
     run_done(run, rc);
     if (have_nxt) run_done(nxt, GS_ESTATE);
