@@ -808,13 +808,14 @@ int flush_rows(gs_ctx* c) {
     HIP_TRY(c, hipMemcpyAsync(c->d_stage_rows, c->h_stage_rows, (size_t)n * (ROW_WORDS * 8 + 4), hipMemcpyHostToDevice,
                               c->st));
     const uint32_t* d_idx = reinterpret_cast<const uint32_t*>(c->d_stage_rows + (size_t)n * ROW_WORDS);
-    HIP_TRY(c, launch_scatter_rows(c->mv, d_idx, c->d_stage_rows, n, c->st));
-    // the rows' LoadAware verdicts at `now` (node_prep), unless a full pass is due anyway
+    // with the rows' LoadAware verdicts at `now` (node_prep, fused into the scatter), unless a full pass is due anyway
     if (!c->prep_stale && c->prep_now == c->now) {
       const gs_loadaware_args& la = c->cfg.loadaware;
-      HIP_TRY(c, launch_node_prep_idx(c->mv, d_idx, n, c->now, la.filter_expired_node_metrics, la.has_node_metric_expiration,
-                                      la.has_node_metric_expiration ? la.node_metric_expiration_seconds * 1000000000LL : 0,
-                                      c->st));
+      const ScatterPrep sp{c->now, la.filter_expired_node_metrics, la.has_node_metric_expiration,
+                           la.has_node_metric_expiration ? la.node_metric_expiration_seconds * 1000000000LL : 0};
+      HIP_TRY(c, launch_scatter_rows(c->mv, d_idx, c->d_stage_rows, n, c->st, &sp));
+    } else {
+      HIP_TRY(c, launch_scatter_rows(c->mv, d_idx, c->d_stage_rows, n, c->st));
     }
 
     c->stats.delta_rows += n;

@@ -200,8 +200,13 @@ hipError_t set_commit_spec_attributes();
 hipError_t launch_row_stats(const int16_t* S, uint32_t len, RowStat* out, hipStream_t st);
 hipError_t launch_row_select(const int16_t* S, uint32_t len, int score, int64_t target, uint32_t n0, int32_t* out,
                              hipStream_t st);
+struct ScatterPrep {   // node_prep_kernel's arguments, fused into the scatter
+  int64_t now;
+  int32_t filter_expired, has_exp;
+  int64_t exp_ns;
+};
 hipError_t launch_scatter_rows(const MirrorView& m, const uint32_t* idx, const int64_t* rows, uint32_t nrows,
-                               hipStream_t st);
+                               hipStream_t st, const ScatterPrep* prep = nullptr);
 int64_t host_tiebreak_position(uint64_t seed, uint64_t seq, int64_t T);
 // diagnostics (gs_probe.hip): cycles of one pair evaluation as the commit kernel runs it
 hipError_t launch_probe(int mode, const MirrorView& m, const Profile& pf, const PodVec* pods, int npods,

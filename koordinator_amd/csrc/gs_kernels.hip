@@ -29,15 +29,10 @@ namespace gs {
 // ------------------------------------------------------------------------------------------------
 // node-prep: LoadAware expiry (helper.go:36-41) evaluated at `now` for every node.
 // idx != nullptr: the n0..n1 entries of idx (rows a delta update just rewrote) instead of a node range
-__global__ void __launch_bounds__(256) node_prep_kernel(MirrorView m, uint32_t n0, uint32_t n1, int64_t now,
-                                                        int32_t filter_expired, int32_t has_exp, int64_t exp_ns,
-                                                        const uint32_t* __restrict__ idx) {
-  uint32_t i = n0 + blockIdx.x * 256 + threadIdx.x;
-  if (i >= n1) return;
-  if (idx) i = idx[i];
-  uint32_t sf = (uint32_t)m.c32(C_SFLAGS)[i];
+__device__ __forceinline__ uint32_t node_prep_flags(uint32_t sf, int64_t update_time, int64_t now, int32_t filter_expired,
+                                                    int32_t has_exp, int64_t exp_ns) {
   bool exists = sf & SF_METRIC;
-  bool expired = !exists || !(sf & SF_UPDATE_TIME) || (exp_ns > 0 && now - m.c64(C_UPDATE_TIME)[i] >= exp_ns);
+  bool expired = !exists || !(sf & SF_UPDATE_TIME) || (exp_ns > 0 && now - update_time >= exp_ns);
   bool skip_filter = !exists || (filter_expired && has_exp && expired);
   uint32_t df = 0;
   if (!skip_filter) {
@@ -50,7 +45,17 @@ __global__ void __launch_bounds__(256) node_prep_kernel(MirrorView m, uint32_t n
     }
   }
   if (!exists || (has_exp && expired)) df |= DF_LA_ZERO;
-  m.c32(C_DFLAGS)[i] = (int32_t)df;
+  return df;
+}
+
+__global__ void __launch_bounds__(256) node_prep_kernel(MirrorView m, uint32_t n0, uint32_t n1, int64_t now,
+                                                        int32_t filter_expired, int32_t has_exp, int64_t exp_ns,
+                                                        const uint32_t* __restrict__ idx) {
+  uint32_t i = n0 + blockIdx.x * 256 + threadIdx.x;
+  if (i >= n1) return;
+  if (idx) i = idx[i];
+  m.c32(C_DFLAGS)[i] = (int32_t)node_prep_flags((uint32_t)m.c32(C_SFLAGS)[i], m.c64(C_UPDATE_TIME)[i], now,
+                                                filter_expired, has_exp, exp_ns);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1711,14 +1716,21 @@ __global__ void __launch_bounds__(1024) row_select_kernel(const int16_t* __restr
 }
 
 // ------------------------------------------------------------------------------------------------
+// prep: the rows' LoadAware verdicts at `now` computed from the staged words (node_prep_kernel's rule, one launch less
+// on the delta path's chain)
 __global__ void __launch_bounds__(256) scatter_rows_kernel(MirrorView m, const uint32_t* __restrict__ idx,
-                                                           const int64_t* __restrict__ rows, uint32_t nrows) {
+                                                           const int64_t* __restrict__ rows, uint32_t nrows, int prep,
+                                                           int64_t now, int32_t filter_expired, int32_t has_exp,
+                                                           int64_t exp_ns) {
   uint32_t r = blockIdx.x * 256 + threadIdx.x;
   if (r >= nrows) return;
   uint32_t i = idx[r];
   const int64_t* src = rows + (size_t)r * ROW_WORDS;
   for (int c = 0; c < NUM_I64_COLS; ++c) m.c64(c)[i] = src[c];
   for (int c = 0; c < NUM_I32_COLS; ++c) m.c32(c)[i] = (int32_t)src[NUM_I64_COLS + c];
+  if (prep)
+    m.c32(C_DFLAGS)[i] = (int32_t)node_prep_flags((uint32_t)src[NUM_I64_COLS + C_SFLAGS], src[C_UPDATE_TIME], now,
+                                                  filter_expired, has_exp, exp_ns);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1922,9 +1934,11 @@ hipError_t launch_row_select(const int16_t* S, uint32_t len, int score, int64_t 
 }
 
 hipError_t launch_scatter_rows(const MirrorView& m, const uint32_t* idx, const int64_t* rows, uint32_t nrows,
-                               hipStream_t st) {
+                               hipStream_t st, const ScatterPrep* prep) {
   if (!nrows) return hipSuccess;
-  hipLaunchKernelGGL(scatter_rows_kernel, dim3((nrows + 255) / 256), dim3(256), 0, st, m, idx, rows, nrows);
+  hipLaunchKernelGGL(scatter_rows_kernel, dim3((nrows + 255) / 256), dim3(256), 0, st, m, idx, rows, nrows,
+                     prep ? 1 : 0, prep ? prep->now : 0, prep ? prep->filter_expired : 0, prep ? prep->has_exp : 0,
+                     prep ? prep->exp_ns : 0);
   return hipGetLastError();
 }
 
