@@ -26,6 +26,16 @@
 //                earlier pod landed on waits until that version is re-scored (so the other wave's Reserve is in).
 //   waves 1, 5, 6, 7  re-scoring jobs from both rings: a reserved row's new score for 64 later pods, one pod per lane
 //                (each wave builds the row's hint table itself).
+// Split selector (SPLIT, the default for one shard): the decision is two waves.
+//   wave 1       prep: selectHost of pod p over a snapshot of the decisions published so far (s_snap, the slot table
+//                in LDS), at most one pod ahead of wave 0, into a PrepRec (M, T, F, tie-break position, the next
+//                SP_KW ties in node order, per-slot ready / feasible / tie / pending flags); on request it records a
+//                pod again over the exact state (full-row and forced decisions, stops, anything wave 0 cannot patch).
+//   wave 0       applies the decisions made after the snapshot (landed slots lose their exact score / were clean
+//                nodes to the prep wave: ties excluded and re-ranked in the window, feasibility out of F), settles
+//                pending rows whose re-scoring has finished, records the decision, verifies the decided pods in order
+//                (no verify wave) and performs the rollbacks.
+//   waves 4-7    re-scoring; waves 2, 3 Reserve as above.
 // All hand-offs are LDS words (release / acquire); every wait is bounded: an expired wait (any wave) ends the kernel
 // with a site code in committed[3], nothing committed and nothing written back (the host fails the call with
 // GS_EDEVICE; HBM and host mirror both keep the batch-start state), so a bug cannot hang the GPU.
@@ -1151,10 +1161,8 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
         SPM(27);   // verification, fresh slot's scores
         if (q >= end_at || q - ver >= lag || cut_at >= 0 || ld_acq(&s_prep_done) <= q || ld_acq(&s_reprep)) {
           if (ST) {   // diagnostics: why wave 0 waits (first reason that holds)
-            const uint64_t tw = __builtin_amdgcn_s_memtime();
             const int why = q >= end_at ? 0 : q - ver >= lag ? 1 : cut_at >= 0 ? 2 : ld_acq(&s_reprep) ? 3 : 4;
             st_acc[56 + why] += 1;
-            (void)tw;
           }
           if (++spins > SP_SPIN_LIMIT) { err = true; err_code = 2; break; }
           if (const int we = ld_acq(&s_werr)) { err = true; err_code = we; break; }
