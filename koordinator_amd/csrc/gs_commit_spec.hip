@@ -1869,7 +1869,10 @@ static void spec_launch(const CommitArgs& a, hipStream_t st) {
 
 hipError_t launch_commit_spec(const CommitArgs& a, hipStream_t st) {
   // the split pipeline (GS_SPEC_SPLIT, dbg bit 16): one shard, speculation on
-  const bool split = ((a.dbg >> 16) & 1u) && a.nranks <= 1 && !(a.dbg & 1u);
+  // and batches of GS_SPEC_SPLIT_MINB pods or more (default 32): a short batch has no selection to hide behind the
+  // prep wave, only its start-up
+  static const int min_b = getenv("GS_SPEC_SPLIT_MINB") ? atoi(getenv("GS_SPEC_SPLIT_MINB")) : 32;
+  const bool split = ((a.dbg >> 16) & 1u) && a.nranks <= 1 && !(a.dbg & 1u) && a.npods >= min_b;
   if (a.stamps) {
     if (split) spec_launch<true, true>(a, st);
     else spec_launch<true, false>(a, st);

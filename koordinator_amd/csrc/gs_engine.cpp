@@ -200,6 +200,7 @@ struct gs_ctx {
   bool cand_overlap = false;        // GS_CAND_OVERLAP (default on): cand beside the previous commit, fix_levels after it
   uint8_t* d_lst = nullptr;         // the bound slot's (cand_overlap)
   uint32_t* d_hist = nullptr;
+  uint32_t* d_cscratch = nullptr;   // launch_cand's short-batch split (slice histograms, slice offsets)
   int cur_slot = 0;
   // host mirror
   std::vector<HostNode> nodes;
@@ -1301,7 +1302,8 @@ int launch_batch(gs_ctx* c, int b, const int32_t* prev, const PlacementDev* prev
     CandPatch cp{};
     cp.extra = fix ? prev_b : 0;
     cp.hist = fix ? c->d_hist : nullptr;
-    HIP_TRY(c, launch_cand(c->d_S, c->ld, len, c->n0, b, c->max_score, c->lstride, d_lists, d_hdrs, d_ext, c->st_ev, &cp));
+    HIP_TRY(c, launch_cand(c->d_S, c->ld, len, c->n0, b, c->max_score, c->lstride, d_lists, d_hdrs, d_ext, c->st_ev, &cp,
+                           c->d_cscratch));
   }
   HIP_TRY(c, hipEventRecord(sl.ev_evdone, c->st_ev));
   HIP_TRY(c, hipStreamWaitEvent(c->st, sl.ev_evdone, 0));
@@ -1321,7 +1323,7 @@ int launch_batch(gs_ctx* c, int b, const int32_t* prev, const PlacementDev* prev
   if (!c->window_k && !ovl) {   // node sampling selects over the rotation window, not the candidate levels
     CandPatch cp{c->mv, c->d_pods, c->pf, c->n0, c->n1, prod_cols, 1, c->d_aff, prev_out, prev};
     HIP_TRY(c, launch_cand(c->d_S, c->ld, len, c->n0, b, c->max_score, c->lstride, d_lists, d_hdrs, d_ext, c->st,
-                           fused ? &cp : nullptr));
+                           fused ? &cp : nullptr, c->d_cscratch));
   }
   // no timing markers between the levels and the commit kernel (each one held the commit's dispatch ~13 us): the
   // commit's duration comes from the kernel itself (committed[4]), the levels' interval is the rest up to ev[4]
@@ -2158,6 +2160,7 @@ int gs_create(const gs_config* cfg, gs_ctx** out) {
     c->d_lst = s0.d_lst;
     c->d_hist = s0.d_hist;
   }
+  if ((e = hipMalloc(&c->d_cscratch, cand_split_scratch_bytes())) != hipSuccess) return bail("hipMalloc", e);
   c->host_timing = getenv("GS_HOST_TIMING") && getenv("GS_HOST_TIMING")[0] == '1';
   if (getenv("GS_COMMIT_STAMPS") && getenv("GS_COMMIT_STAMPS")[0] == '1') {
     // 8 waves x 64 entries (commit_spec_kernel: one region per wave; the other commit kernels: region 0), then the
@@ -2315,6 +2318,8 @@ int gs_destroy(gs_ctx* c) {
     }
     c->d_lst = nullptr;
     c->d_hist = nullptr;
+    if (c->d_cscratch) (void)hipFree(c->d_cscratch);
+    c->d_cscratch = nullptr;
     void* d1[] = {s1.d_pods, s1.d_committed, s1.d_S, s1.d_aff};   // (seq / out live inside pods / committed)
     for (void* p : d1)
       if (p) (void)hipFree(p);

@@ -153,8 +153,13 @@ struct CandPatch {
   int extra;
   uint32_t* hist;
 };
+// split_scratch (cand_split_scratch_bytes()): a short batch (<= CS_MAXB pods, no patch) spreads each row over up to
+// CS_GMAX slices (cs_hist / cs_pick / cs_list kernels, GS_CAND_SPLIT=0 disables); nullptr: cand_kernel always
+constexpr int CS_GMAX = 64, CS_MAXB = 32;
+size_t cand_split_scratch_bytes();
 hipError_t launch_cand(int16_t* S, uint32_t ld, uint32_t len, uint32_t n0, int npods, int max_score, int lcap,
-                       uint32_t* lists, LevelHdr* hdrs, LevelExt* ext, hipStream_t st, const CandPatch* patch = nullptr);
+                       uint32_t* lists, LevelHdr* hdrs, LevelExt* ext, hipStream_t st, const CandPatch* patch = nullptr,
+                       uint32_t* split_scratch = nullptr);
 // The previous batch's landed rows folded into stale levels (cand_kernel with cp.extra / cp.hist, before that batch's
 // commit ended): the rows re-evaluated (S, aff patched as by cand_kernel's patch), the histogram updated, the levels
 // re-picked and each listed level rewritten as its stale nodes minus the landed rows plus the landed rows now at it

@@ -505,7 +505,189 @@ __global__ void __launch_bounds__(64 * W) cand_kernel(int16_t* __restrict__ S, u
 }
 
 // ------------------------------------------------------------------------------------------------
-// Stale levels fixed up once the previous batch has committed: cand_kernel ran beside that batch's commit on rows whose
+// Candidate levels of a short batch (a few pods over a long row, the plain runs between C5's extension pods):
+// cand_kernel streams each row from one CU (33 us at 100k nodes, LDS-atomic bound). Here every row is cut into G
+// slices spread over the chip: cs_hist_kernel histograms each (slice, pod), cs_pick_kernel (one block per pod) sums
+// them, picks the levels as cand_kernel's wave 0 does and gives every slice its output position within each level,
+// and cs_list_kernel compacts each slice in node order. The lists, headers and extensions equal cand_kernel's (the
+// plain case: no patch, no stale-level margin).
+__global__ void __launch_bounds__(256) cs_hist_kernel(const int16_t* __restrict__ S, uint32_t ld, uint32_t lenv,
+                                                      int nbins, uint32_t slice, int G, uint32_t* __restrict__ ghist) {
+  extern __shared__ __align__(16) uint32_t hist[];
+  const int g = blockIdx.x, k = blockIdx.y, t = threadIdx.x;
+  for (int b = t; b < nbins; b += 256) hist[b] = 0;
+  __syncthreads();
+  const uint32_t b0 = (uint32_t)g * slice, b1 = min(lenv, b0 + slice);
+  const int4* row4 = reinterpret_cast<const int4*>(S + (size_t)k * ld);
+  for (uint32_t i = b0 + t * 8; i < b1; i += 2 * 2048) {
+    const int4 q0 = row4[i / 8];
+    const int4 q1 = i + 2048 < b1 ? row4[(i + 2048) / 8] : make_int4(-1, -1, -1, -1);
+    const int16_t* e0 = reinterpret_cast<const int16_t*>(&q0);
+    const int16_t* e1 = reinterpret_cast<const int16_t*>(&q1);
+#pragma unroll
+    for (int x = 0; x < 8; ++x) {
+      if (e0[x] >= 0) atomicAdd(&hist[e0[x]], 1u);
+      if (e1[x] >= 0) atomicAdd(&hist[e1[x]], 1u);
+    }
+  }
+  __syncthreads();
+  uint32_t* out = ghist + ((size_t)k * G + g) * nbins;
+  for (int b = t; b < nbins; b += 256) out[b] = hist[b];
+}
+
+__global__ void __launch_bounds__(256) cs_pick_kernel(const uint32_t* __restrict__ ghist, int nbins, int G, int lcap,
+                                                      uint32_t* __restrict__ offs, LevelHdr* __restrict__ hdrs,
+                                                      LevelExt* __restrict__ ext) {
+  extern __shared__ __align__(16) uint32_t comb[];   // [nbins]
+  __shared__ uint32_t s_total;
+  __shared__ int32_t s_nlev, s_next, s_score[LEVALL], s_count[LEVALL];
+  __shared__ uint32_t s_v[CS_GMAX][LEVALL];
+  const int k = blockIdx.x, t = threadIdx.x, wave = t >> 6, lane = t & 63;
+  const uint32_t* h = ghist + (size_t)k * G * nbins;
+  for (int b = t; b < nbins; b += 256) comb[b] = 0;
+  if (t == 0) s_total = 0;
+  __syncthreads();
+  // the slice histograms are contiguous: entry e is bin e % nbins of slice e / nbins
+  const int tot = G * nbins;
+  for (int e0 = t; e0 < tot; e0 += 4 * 256) {
+    uint32_t v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) v[u] = e0 + u * 256 < tot ? h[e0 + u * 256] : 0u;
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      if (v[u]) atomicAdd(&comb[(e0 + u * 256) % nbins], v[u]);
+  }
+  __syncthreads();
+  {
+    uint32_t s = 0;
+    for (int b = t; b < nbins; b += 256) s += comb[b];
+    s = (uint32_t)wave_sum((int)s);
+    if (lane == 0 && s) atomicAdd(&s_total, s);
+  }
+  if (wave == 0) {   // cand_kernel's level pick (target k + 1)
+    const uint32_t target = (uint32_t)k + 1;
+    const uint64_t lt = (1ull << lane) - 1ull;
+    int nlev = 0, next = -1;
+    uint32_t cum = 0;
+    for (int hi = nbins - 1; hi >= 0; hi -= 64) {
+      const int b = hi - lane;
+      const uint32_t c = b >= 0 ? comb[b] : 0u;
+      const bool nz = c != 0;
+      const uint64_t nzm = __ballot(nz);
+      if (!nzm) continue;
+      const uint32_t cb = cum + (uint32_t)(wave_incl_scan((int)c) - (int)c);
+      const int nb = nlev + __popcll(nzm & lt);
+      const bool stop = nz && (nb == LEVALL || cb + c > (uint32_t)lcap || cb >= target);
+      const uint64_t sm = __ballot(stop);
+      const int ls = sm ? __builtin_ctzll(sm) : 64;
+      if (nz && lane < ls) {
+        s_score[nb] = b;
+        s_count[nb] = (int32_t)c;
+      }
+      if (sm) {
+        next = __builtin_amdgcn_readlane(b, ls);
+        nlev += __popcll(nzm & ((1ull << ls) - 1ull));
+        break;
+      }
+      nlev += __popcll(nzm);
+      cum += (uint32_t)wave_sum((int)c);
+    }
+    for (int j = nlev + lane; j < LEVALL; j += 64) { s_score[j] = -1; s_count[j] = 0; }
+    if (lane == 0) {
+      s_nlev = nlev;
+      s_next = next;
+    }
+  }
+  __syncthreads();
+  const int nlev = s_nlev;
+  // each slice's node count at each listed level, then per level the running start over the slices
+  for (int e = t; e < G * LEVALL; e += 256) {
+    const int g = e / LEVALL, j = e % LEVALL;
+    s_v[g][j] = j < nlev ? h[(size_t)g * nbins + s_score[j]] : 0u;
+  }
+  __syncthreads();
+  if (t < LEVALL) {
+    uint32_t base = 0;
+    for (int jj = 0; jj < t && jj < nlev; ++jj) base += (uint32_t)s_count[jj];
+    uint32_t* o = offs + (size_t)k * G * LEVALL;
+    for (int g = 0; g < G; ++g) {
+      o[g * LEVALL + t] = base;
+      base += s_v[g][t];
+    }
+  }
+  if (t == 0) {
+    LevelHdr hd;
+    hd.nlev = nlev < MAXLEV ? nlev : MAXLEV;
+    hd.feasible = (int32_t)s_total;
+    hd.next = nlev > MAXLEV ? s_score[MAXLEV] : s_next;
+    int32_t sum = 0;
+    for (int j = 0; j < MAXLEV; ++j) { hd.score[j] = s_score[j]; hd.count[j] = s_count[j]; sum += s_count[j]; }
+    hd.total = sum;
+    hdrs[k] = hd;
+    LevelExt x;
+    x.nlev = nlev;
+    x.next = s_next;
+    for (int j = 0; j < LEVX; ++j) { x.score[j] = s_score[MAXLEV + j]; x.count[j] = s_count[MAXLEV + j]; }
+    ext[k] = x;
+  }
+}
+
+__global__ void __launch_bounds__(64) cs_list_kernel(const int16_t* __restrict__ S, uint32_t ld, uint32_t lenv,
+                                                     uint32_t n0, int nbins, uint32_t slice, int G, int lcap,
+                                                     const uint32_t* __restrict__ offs,
+                                                     const LevelHdr* __restrict__ hdrs,
+                                                     const LevelExt* __restrict__ ext, uint32_t* __restrict__ lists) {
+  extern __shared__ __align__(16) int8_t slot_of[];   // [nbins]: bin -> listed level, -1 none
+  const int g = blockIdx.x, k = blockIdx.y, lane = threadIdx.x;
+  const int nlev = ext[k].nlev;
+  if (nlev <= 0) return;
+  for (int b = lane; b < nbins; b += 64) slot_of[b] = -1;
+  __syncthreads();
+  int sc = -1;
+  if (lane < nlev) sc = lane < MAXLEV ? hdrs[k].score[lane] : ext[k].score[lane - MAXLEV];
+  if (lane < nlev) slot_of[sc] = (int8_t)lane;
+  const int thr = __shfl(sc, nlev - 1);
+  __syncthreads();
+  uint32_t run_l = lane < LEVALL ? offs[((size_t)k * G + g) * LEVALL + lane] : 0u;
+  uint32_t* out = lists + (size_t)k * lcap;
+  const uint32_t b0 = (uint32_t)g * slice, b1 = min(lenv, b0 + slice);
+  const int4* row4 = reinterpret_cast<const int4*>(S + (size_t)k * ld);
+  for (uint32_t gb = b0; gb < b1; gb += 4 * 512) {
+    int4 qs[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      qs[u] = gb + u * 512 < b1 ? row4[(gb + u * 512 + lane * 8) / 8] : make_int4(-1, -1, -1, -1);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const uint32_t base = gb + u * 512;
+      const int16_t* e = reinterpret_cast<const int16_t*>(&qs[u]);
+      int slot[8];
+      uint32_t present = 0;
+#pragma unroll
+      for (int x = 0; x < 8; ++x) {
+        slot[x] = e[x] >= thr ? slot_of[e[x]] : -1;   // every non-empty bin >= thr is a listed level
+        if (slot[x] >= 0) present |= 1u << slot[x];
+      }
+      uint32_t pw = (uint32_t)wave_or((int)present);
+      for (; pw; pw &= pw - 1) {
+        const int j = __ffs(pw) - 1;
+        int c = 0;
+#pragma unroll
+        for (int x = 0; x < 8; ++x) c += slot[x] == j;
+        const int incl = wave_incl_scan(c);
+        int pos = __builtin_amdgcn_readlane((int)run_l, j) + incl - c;
+#pragma unroll
+        for (int x = 0; x < 8; ++x)
+          if (slot[x] == j) out[pos++] = n0 + base + lane * 8 + x;
+        const int tot = __builtin_amdgcn_readlane(incl, 63);
+        if (lane == j) run_l += tot;
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// Stale levels fixed up once the previous batch has committed:cand_kernel ran beside that batch's commit on rows whose
 // landed nodes ("prev rows") still held their pre-commit scores, listing cp.extra nodes beyond pod k's k+1 and writing
 // its histogram. Block k (pod k): re-evaluate the prev rows on their committed state (S, aff patched), move them in the
 // histogram, and re-pick the levels from the top down. A score above the stale `next` is fully known: every non-prev
@@ -1886,11 +2068,35 @@ hipError_t launch_fix_levels(int16_t* S, uint32_t ld, int npods, int max_score, 
 }
 
 
+size_t cand_split_scratch_bytes() {
+  return (size_t)4 * CS_MAXB * CS_GMAX * (MAX_SCORE_LIMIT + 1 + LEVALL);
+}
+
 hipError_t launch_cand(int16_t* S, uint32_t ld, uint32_t len, uint32_t n0, int npods, int max_score, int lcap,
-                       uint32_t* lists, LevelHdr* hdrs, LevelExt* ext, hipStream_t st, const CandPatch* patch) {
+                       uint32_t* lists, LevelHdr* hdrs, LevelExt* ext, hipStream_t st, const CandPatch* patch,
+                       uint32_t* split_scratch) {
   if (lcap < 1 || lcap > LCAP) return hipErrorInvalidValue;
   CandPatch cp{};
   if (patch) cp = *patch;
+  static const bool no_split = getenv("GS_CAND_SPLIT") && getenv("GS_CAND_SPLIT")[0] == '0';
+  const uint32_t lenv = (len + 511) & ~511u;
+  if (split_scratch && !no_split && !cp.on && !cp.hist && cp.extra == 0 && !g_cand_stamps && npods >= 1 &&
+      npods <= CS_MAXB && max_score >= 0 && max_score <= MAX_SCORE_LIMIT && lenv >= 2 * 2048) {
+    // slices of whole 2048-entry steps, at most CS_GMAX of them (rows are padded with -1 up to ld >= lenv)
+    const uint32_t g0 = min((uint32_t)CS_GMAX, (lenv + 2047) / 2048);
+    const uint32_t slice = ((lenv + g0 - 1) / g0 + 2047) & ~2047u;
+    const int G = (int)((lenv + slice - 1) / slice);
+    const int nbins = max_score + 1;
+    uint32_t* ghist = split_scratch;
+    uint32_t* offs = split_scratch + (size_t)CS_MAXB * CS_GMAX * (MAX_SCORE_LIMIT + 1);
+    hipLaunchKernelGGL(cs_hist_kernel, dim3(G, npods), dim3(256), (size_t)4 * nbins, st, S, ld, lenv, nbins, slice, G,
+                       ghist);
+    hipLaunchKernelGGL(cs_pick_kernel, dim3(npods), dim3(256), (size_t)4 * nbins, st, ghist, nbins, G, lcap, offs, hdrs,
+                       ext);
+    hipLaunchKernelGGL(cs_list_kernel, dim3(G, npods), dim3(64), ((size_t)nbins + 15) & ~(size_t)15, st, S, ld, lenv,
+                       n0, nbins, slice, G, lcap, offs, hdrs, ext, lists);
+    return hipGetLastError();
+  }
   if (cand_wide(max_score))
     hipLaunchKernelGGL(cand_kernel<16>, dim3(npods), dim3(1024), cand_smem_bytes(max_score, 16), st, S, ld, len, n0,
                        max_score, lcap, lists, hdrs, ext, g_cand_stamps, cp);

@@ -98,6 +98,23 @@ def test_schedule_in_chunks_and_custom_seq():
         _check_schedule(e, o, c.pods[lo:lo + 150], seq[lo:lo + 150])
 
 
+@pytest.mark.parametrize("chunk,numa,homog", [(1, False, False), (5, False, False), (32, True, False),
+                                              (7, False, True)], ids=["1", "5", "32-numa", "7-ties"])
+def test_short_batches_over_long_rows_match_oracle(chunk, numa, homog):
+    """A gs_schedule call's first batch of <= 32 pods over rows of >= 4096 entries builds its levels over row slices
+    spread across the chip (launch_cand's cs_hist / cs_pick / cs_list kernels, the plain runs between C5's extension
+    pods): calls of `chunk` pods on a 20k-node cluster, every placement the oracle's. 7-ties: one level of 20k nodes, too
+    large to list (no listed level: the exact full-row path)."""
+    c = homogeneous_cluster(20_000, 224, 4) if homog else synth.make_cluster(20_000, 224, 3)
+    if numa:
+        synth.make_numa(c)
+    kw = dict(enabled=abi.GS_ENABLE_ALL) if numa else {}
+    e, o = pair(c, **kw)
+    for lo in range(0, 224, chunk):
+        _check_schedule(e, o, c.pods[lo:lo + chunk], np.arange(lo, min(224, lo + chunk), dtype=np.uint64))
+    assert e.stats()["batches"] >= 224 // chunk
+
+
 @pytest.mark.parametrize("numa", [False, True])
 def test_overlapped_levels_match_serial_levels(numa, monkeypatch):
     """Candidate levels built beside the previous batch's commit and fixed up after it (fix_levels_kernel, the
