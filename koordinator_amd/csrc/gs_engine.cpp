@@ -1194,6 +1194,15 @@ constexpr size_t COMMITTED_BYTES = 32;   // committed[0..7] (the commit kernels 
 // The candidate levels of a one-shard pass without node sampling are built on st_ev right after the eval pass (beside
 // the previous batch's commit, on the stale rows it lands on), then fixed up on st once that commit is done
 // (GS_FUSED_PATCH=0, the separate patch kernel: not overlapped)
+// A batch with no speculative pass before it, of at most GS_DIRECT_B pods (default 32; 0: none), on one shard: its
+// upload, eval pass and levels go on st in order instead of through st_ev (st_ev still waits for st at its start, so a
+// speculative pass after it sees the same order). Short runs (the plain pods between C5's extension pods) lose two
+// queue hops per batch.
+bool direct_batch(const gs_ctx* c, int b, bool speculative) {
+  static const int max_b = getenv("GS_DIRECT_B") ? atoi(getenv("GS_DIRECT_B")) : 32;
+  return !speculative && b <= max_b && c->nranks == 1;
+}
+
 bool cand_overlapped(const gs_ctx* c) {
   static const bool separate = getenv("GS_FUSED_PATCH") && getenv("GS_FUSED_PATCH")[0] == '0';
   return c->cand_overlap && c->nranks == 1 && !c->window_k && c->d_lst && !separate;
@@ -1291,10 +1300,13 @@ int launch_batch(gs_ctx* c, int b, const int32_t* prev, const PlacementDev* prev
     c->numa_idx_stale = false;
   }
   const gs_ctx::Slot& sl = c->slot[c->cur_slot];
-  HIP_TRY(c, hipEventRecord(c->ev[0], c->st_ev));
+  // a short batch with no pass beside it: upload, eval and levels in order on st (no queue hops)
+  const bool direct = direct_batch(c, b, prev != nullptr);
+  hipStream_t se = direct ? c->st : c->st_ev;
+  HIP_TRY(c, hipEventRecord(c->ev[0], se));
   HIP_TRY(c, launch_eval(c->mv, c->d_pods, b, c->pf, c->n0, c->n1, c->d_S, c->ld, prod_cols, c->d_numa_idx, c->numa_n,
-                         c->d_aff, c->st_ev, c->st2, c->ev_fork, c->ev_join, c->slab_mv.i64 ? &c->slab_mv : nullptr));
-  HIP_TRY(c, hipEventRecord(c->ev[1], c->st_ev));
+                         c->d_aff, se, c->st2, c->ev_fork, c->ev_join, c->slab_mv.i64 ? &c->slab_mv : nullptr));
+  HIP_TRY(c, hipEventRecord(c->ev[1], se));
   const bool fix = ovl && prev && prev_b > 0;
   if (ovl) {
     // levels on st_ev beside the previous batch's commit: the rows it lands on are stale here (listed with a margin of
@@ -1302,11 +1314,13 @@ int launch_batch(gs_ctx* c, int b, const int32_t* prev, const PlacementDev* prev
     CandPatch cp{};
     cp.extra = fix ? prev_b : 0;
     cp.hist = fix ? c->d_hist : nullptr;
-    HIP_TRY(c, launch_cand(c->d_S, c->ld, len, c->n0, b, c->max_score, c->lstride, d_lists, d_hdrs, d_ext, c->st_ev, &cp,
+    HIP_TRY(c, launch_cand(c->d_S, c->ld, len, c->n0, b, c->max_score, c->lstride, d_lists, d_hdrs, d_ext, se, &cp,
                            c->d_cscratch));
   }
-  HIP_TRY(c, hipEventRecord(sl.ev_evdone, c->st_ev));
-  HIP_TRY(c, hipStreamWaitEvent(c->st, sl.ev_evdone, 0));
+  if (!direct) {
+    HIP_TRY(c, hipEventRecord(sl.ev_evdone, c->st_ev));
+    HIP_TRY(c, hipStreamWaitEvent(c->st, sl.ev_evdone, 0));
+  }
   if (fix) {
     CandPatch cp{c->mv, c->d_pods, c->pf, c->n0, c->n1, prod_cols, 0, c->d_aff, prev_out, prev};
     cp.extra = prev_b;
@@ -2564,11 +2578,12 @@ int stage_batch(gs_ctx* c, const gs_pod* pods, const uint64_t* seq, uint32_t i, 
   // one copy: the B pod vectors' block (b of them staged) and the b sequence numbers after it (GS_MERGE_UP=0,
   // experiments: two copies)
   static const bool merge_up = !(getenv("GS_MERGE_UP") && getenv("GS_MERGE_UP")[0] == '0');
+  hipStream_t up = direct_batch(c, b, speculative) ? c->st : c->st_ev;
   if (merge_up) {
-    HIP_TRY(c, hipMemcpyAsync(c->d_pods, c->h_pods, sizeof(PodVec) * c->B + 8 * b, hipMemcpyHostToDevice, c->st_ev));
+    HIP_TRY(c, hipMemcpyAsync(c->d_pods, c->h_pods, sizeof(PodVec) * c->B + 8 * b, hipMemcpyHostToDevice, up));
   } else {
-    HIP_TRY(c, hipMemcpyAsync(c->d_pods, c->h_pods, sizeof(PodVec) * b, hipMemcpyHostToDevice, c->st_ev));
-    HIP_TRY(c, hipMemcpyAsync(c->d_seq, c->h_seq, 8 * b, hipMemcpyHostToDevice, c->st_ev));
+    HIP_TRY(c, hipMemcpyAsync(c->d_pods, c->h_pods, sizeof(PodVec) * b, hipMemcpyHostToDevice, up));
+    HIP_TRY(c, hipMemcpyAsync(c->d_seq, c->h_seq, 8 * b, hipMemcpyHostToDevice, up));
   }
   return GS_OK;
 }
