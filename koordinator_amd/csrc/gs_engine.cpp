@@ -242,6 +242,10 @@ struct gs_ctx {
   bool host_timing = false;
   double ht_wait = 0, ht_apply = 0, ht_stage = 0, ht_launch = 0, ht_max_busy = 0;
   uint64_t ht_batches = 0, ht_busy_hist[8] = {};
+  // ... and of gs_schedule_ext: per extension pod (records, flushes, the device chain up to the host's wake-up, the
+  // Reserves) and per plain run (the whole gs_schedule call)
+  double hx_prep = 0, hx_flush = 0, hx_gpu = 0, hx_reserve = 0, hx_plain = 0;
+  uint64_t hx_pods = 0, hx_runs = 0;
   // NodeNUMAResource: per-node TopologyOptions + NodeAllocation mirror, registered CPU topologies
   std::vector<NumaNode> numa;
   std::vector<std::shared_ptr<TopoClass>> topos;
@@ -1361,8 +1365,10 @@ int launch_batch(gs_ctx* c, int b, const int32_t* prev, const PlacementDev* prev
   // Two copies, not one over the adjacent committed words and placements: with one merged copy, 4 processes sharing the
   // GPU (the C4 rehearsal) stalled for 10-100 s at a time, every rank's commit and next eval pass pending (DESIGN §8;
   // GS_MERGE_RB=1 restores the merged copy for that experiment)
+  // A direct batch (one shard, on st, the host waiting on it) reads back in one copy (GS_DIRECT_MERGE_RB=0: two)
   static const bool merge_rb = getenv("GS_MERGE_RB") && getenv("GS_MERGE_RB")[0] == '1';
-  if (merge_rb) {
+  static const bool merge_direct = !(getenv("GS_DIRECT_MERGE_RB") && getenv("GS_DIRECT_MERGE_RB")[0] == '0');
+  if (merge_rb || (direct && merge_direct && rb == c->st)) {
     HIP_TRY(c, hipMemcpyAsync(c->h_committed, c->d_committed, COMMITTED_BYTES + sizeof(PlacementDev) * b,
                               hipMemcpyDeviceToHost, rb));
   } else {
@@ -1737,10 +1743,13 @@ int ext_schedule_one(gs_ctx* c, const gs_pod& pod, const gs_pod_ext& e, uint64_t
     return GS_OK;
   }
   int rc;
+  using hx_clk = std::chrono::steady_clock;
+  const auto hx0 = hx_clk::now();
   if ((rc = ext_alloc(c))) return rc;
   if ((rc = ext_flush_devices(c))) return rc;
   if ((rc = flush_rows(c))) return rc;
   if (c->prep_stale && (rc = node_prep(c))) return rc;
+  const auto hx1 = hx_clk::now();
   // ---- BeforePreFilter: per-node restore records (reservation/transformer.go:50-235)
   c->xrec.clear();
   c->xres.clear();
@@ -1883,6 +1892,14 @@ int ext_schedule_one(gs_ctx* c, const gs_pod& pod, const gs_pod_ext& e, uint64_t
                                c->d_xnom, nrec, c->h_xout, c->h_xnom, c->st));
   if (ext_ev) HIP_TRY(c, hipEventRecord(c->ev[4], c->st));
   HIP_TRY(c, host_wait_stream(c->st));
+  const auto hx3 = hx_clk::now();
+  if (c->host_timing) {
+    const auto us = [](hx_clk::duration d) { return std::chrono::duration<double, std::micro>(d).count(); };
+    c->hx_flush += us(hx1 - hx0);
+    c->hx_prep += us(ext_t0 - hx1);
+    c->hx_gpu += us(hx3 - ext_t0);
+    c->hx_pods += 1;
+  }
   if (ext_ev) {
     c->stats.eval_ms += ev_ms(c->ev[0], c->ev[1]);
     c->stats.commit_ms += ev_ms(c->ev[1], c->ev[4]);
@@ -1951,6 +1968,8 @@ int ext_schedule_one(gs_ctx* c, const gs_pod& pod, const gs_pod_ext& e, uint64_t
   if (gmask || (rs_on && rec_i >= 0 && c->h_xnom[rec_i] >= 0) || gpu_names_all || xres_all)
     c->ext_reserved.insert(pod.uid);   // gs_pods_forget cannot undo these Reserves
   apply_placement(c, pod, xo.node, true);
+  if (c->host_timing)
+    c->hx_reserve += std::chrono::duration<double, std::micro>(hx_clk::now() - hx3).count();
   return GS_OK;
 }
 
@@ -2209,6 +2228,13 @@ int gs_destroy(gs_ctx* c) {
             c->ht_max_busy);
     for (int k = 0; k < 8; ++k) fprintf(stderr, " %llu", (unsigned long long)c->ht_busy_hist[k]);
     fprintf(stderr, "\n");
+  }
+  if (c->host_timing && c->hx_pods) {
+    const double n = (double)c->hx_pods;
+    fprintf(stderr, "gpuscore extension path (us): per extension pod (%llu): records %.1f | flushes %.1f | device chain "
+            "to wake-up %.1f | Reserves %.1f; per plain run (%llu): gs_schedule %.1f\n", (unsigned long long)c->hx_pods,
+            c->hx_prep / n, c->hx_flush / n, c->hx_gpu / n, c->hx_reserve / n, (unsigned long long)c->hx_runs,
+            c->hx_runs ? c->hx_plain / (double)c->hx_runs : 0.0);
   }
   if (c->d_dev_stage) (void)hipFree(c->d_dev_stage);
   if (c->h_dev_stage) (void)hipHostFree(c->h_dev_stage);
@@ -3439,7 +3465,12 @@ int gs_schedule_ext(gs_ctx* c, const gs_pod* pods, const gs_pod_ext* ext, uint32
     if (j > i) {
       std::vector<uint64_t> sq;
       if (!seq) { sq.resize(j - i); for (uint32_t k = i; k < j; ++k) sq[k - i] = k; }
+      const auto hp0 = std::chrono::steady_clock::now();
       if ((rc = gs_schedule(c, pods + i, j - i, seq ? seq + i : sq.data(), out + i))) return rc;
+      if (c->host_timing) {
+        c->hx_plain += std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - hp0).count();
+        c->hx_runs += 1;
+      }
       if (ext_out) std::memset(ext_out + i, 0, sizeof(gs_ext_placement) * (j - i));
       i = j;
       continue;
