@@ -103,11 +103,179 @@ def cpu_baseline_c5(cluster, cfg, ext_args, pods, seq, sample_pods: int) -> dict
     synth.load_ext_into(o, cluster, ext_args)
     n = max(8, sample_pods)
     t0 = time.perf_counter()
-    o.schedule_ext(pods[:n], cluster.ext["pod_ext"][:n], seq[:n])
+    out = o.schedule_ext(pods[:n], cluster.ext["pod_ext"][:n], seq[:n])[0]
     dt = time.perf_counter() - t0
-    return {"pods_per_s": n / dt, "evals_per_s": n / dt * cluster.num_nodes, "seconds": dt,
+    return {"pods_per_s": n / dt, "evals_per_s": n / dt * cluster.num_nodes, "seconds": dt, "placements": out,
             "sample": f"pods 0..{n} of the workload on the fresh cluster, one thread (or_schedule_ext: Fit + LoadAware + "
                       "DeviceShare + Reservation restatement)"}
+
+
+class _ThreadedOracle:
+    """The oracle engine with its Filter / Score fan-out over `threads` host threads, for the gang sample's sequential
+    reference order (schedule / forget as Engine has them)."""
+
+    def __init__(self, o, threads: int):
+        self.o, self.threads = o, threads
+
+    def schedule(self, pods, seq=None):
+        return self.o.schedule(pods, seq, nthreads=self.threads)
+
+    def forget(self, nodes, pods):
+        return self.o.forget(nodes, pods)
+
+
+def cpu_gang_sample(cluster, cfg, warm: int, given, pods, seq, gang_ids, specs, sample: int, threads: int) -> dict:
+    """The gang extra's CPU leg: the oracle replays the GPU's warm-up placements, then runs the reference's
+    one-pod-at-a-time Coscheduling order (oracle/coscheduling.py schedule_sequential) over the first `sample` pods of the
+    gang queue; returns its decisions and rate (the caller compares them with the GPU's)."""
+    from oracle import oracle as orc
+    from oracle import coscheduling as oc
+    from koordinator_amd import synth
+    o = orc.Oracle(cfg)
+    synth.load_into(o, cluster)
+    o.schedule_replay(pods[:warm], given[:warm], seq[:warm], nthreads=threads)
+    om = oc.PodGroupManager()
+    for sp in specs:
+        om.podgroup_upsert(sp)
+    for k in range(warm, len(gang_ids)):
+        if gang_ids[k]:
+            om.pod_add(int(gang_ids[k]), int(pods["uid"][k]))
+    hi = warm + sample
+    t0 = time.perf_counter()
+    want, wres = oc.schedule_sequential(_ThreadedOracle(o, threads), om, pods[warm:hi], gang_ids[warm:hi], seq[warm:hi])
+    return {"want": want, "wres": wres, "seconds": time.perf_counter() - t0}
+
+
+def extra_c5(P: int, steps: int, nodes: int, sample: int) -> dict:
+    """C5 beside the headline: 100k nodes, LoadAware + Fit + DeviceShare + Reservation, one warm-up step
+    and `steps` timed steps of P pods through gs_schedule_ext; the first `sample` pods (warm-up step) checked against
+    the oracle's restatement from the same fresh cluster, which is also the CPU line."""
+    import torch
+    from koordinator_amd import abi, config, synth
+    from koordinator_amd.engine import Engine
+    total = (1 + steps) * P
+    c = synth.make_cluster(nodes, total, config_id=5)
+    synth.make_ext(c)
+    cfg = config.make_config(nodes, device=0, batch_size=128, enabled=abi.GS_ENABLE_LA_FIT)
+    eng = Engine(cfg)
+    synth.load_into(eng, c)
+    ea = abi.GsExtArgs()
+    abi.load().gs_ext_args_default(abi.C.byref(ea))
+    synth.load_ext_into(eng, c, ea)
+    pods, ext = c.pods, c.ext["pod_ext"]
+    seq = np.arange(total, dtype=np.uint64)
+    first = eng.schedule_ext(pods[:P], ext[:P], seq[:P])[0]
+    eng.synchronize()
+    eng.reset_stats()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    placed = 0
+    for s in range(1, 1 + steps):
+        out = eng.schedule_ext(pods[s * P:(s + 1) * P], ext[s * P:(s + 1) * P], seq[s * P:(s + 1) * P])[0]
+        placed += int((out["node"] >= 0).sum())
+    eng.synchronize()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    st = eng.stats()
+    del eng
+    r = cpu_baseline_c5(c, cfg, ea, pods, seq, sample)
+    want = r.pop("placements")
+    bad = [f for f in ("node", "score", "ties", "feasible") if not np.array_equal(first[f][:sample], want[f][:sample])]
+    return {"pods_per_s": steps * P / dt, "evals_per_s": steps * P * nodes / dt, "steps": steps, "pods_per_step": P,
+            "nodes": nodes, "ms_per_step": dt / steps * 1e3, "placed": placed,
+            "batches": st["batches"], "workload": "C5: Fit(LeastAllocated) + LoadAware + DeviceShare (GPU) + Reservation "
+                                                  "filter+score with normalize, selectHost, assume+Reserve; 20% GPU "
+                                                  "nodes, 5% nodes with reservations, ~10% owner pods, ~10% GPU pods; "
+                                                  "blocking gs_schedule_ext per step",
+            "parity_sample": {"pods": sample, "fields": ["node", "score", "ties", "feasible"], "mismatched_fields": bad,
+                              "ok": not bad, "what": "the first pods of the untimed warm-up step against the oracle's "
+                                                     "sequential restatement (or_schedule_ext) from the same cluster"},
+            "cpu_baseline": {"value": r["evals_per_s"], "unit": "evals/s", "cores": 1, "kind": "port",
+                             "pods_per_s": r["pods_per_s"], "seconds": r["seconds"], "sample": r["sample"]}}
+
+
+def extra_gang(cluster, cfg, P: int, calls: int, sample: int, threads: int, gang_pct: int = 25, gang_size: int = 8,
+               run_cap: int = 192) -> dict:
+    """Coscheduling beside the headline: the headline's C3 cluster from a fresh engine, one 2048-pod
+    warm-up call, then `calls` calls of P pods of which ~gang_pct% are in Strict gangs of gang_size
+    (koordinator_amd.gang.schedule_with_gangs: speculative engine runs + gang replay); the first `sample` pods of the gang
+    queue checked against the reference's one-pod-at-a-time order on the oracle (gang PreFilter codes; node, score, ties,
+    feasible of the pods that reached the node loop)."""
+    import torch
+    from koordinator_amd import gang as gg, synth
+    from koordinator_amd.engine import Engine
+    warm = P
+    total = warm + calls * P
+    pods = cluster.pods[:total]
+    seq = np.arange(total, dtype=np.uint64)
+    rng = np.random.default_rng(7)
+    gang_ids = np.zeros(total, np.uint64)
+    n_g, k = 0, warm
+    g = gang_pct / 100.0
+    p_start = g / (gang_size * (1 - g) + g)
+    while k + gang_size <= total:
+        if rng.random() < p_start:
+            n_g += 1
+            gang_ids[k:k + gang_size] = n_g
+            k += gang_size
+        else:
+            k += 1
+    specs = [dict(gang_id=j, min_member=gang_size, mode=gg.STRICT, wait_time_ns=60 * 10**9) for j in range(1, n_g + 1)]
+    e = Engine(cfg)
+    synth.load_into(e, cluster)
+    wout = e.schedule(pods[:warm], seq[:warm])
+    given = np.where(wout["node"] >= 0, wout["node"], -2).astype(np.int32)
+    mgr = gg.GangManager()
+    for sp in specs:
+        mgr.podgroup_upsert(gg.spec(**sp))
+    for j in range(warm, total):
+        if gang_ids[j]:
+            mgr.pod_add(int(gang_ids[j]), int(pods["uid"][j]))
+    e.synchronize()
+    torch.cuda.synchronize()
+    waiting = gg.WaitingPods()
+    states, carried, first = [], {}, None
+    t0 = time.perf_counter()
+    for lo in range(warm, total, P):
+        hi = min(total, lo + P)
+        out, res = gg.schedule_with_gangs(e, mgr, pods[lo:hi], gang_ids[lo:hi], seq[lo:hi], waiting=waiting,
+                                          run_cap=run_cap)
+        if first is None:
+            first = (out, res)
+        states.append(res["state"])
+        carried.update(res["carried"])
+    e.synchronize()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    del e
+    st = np.concatenate(states)
+    idx = {int(u): j - warm for j, u in enumerate(pods["uid"]) if j >= warm}
+    for uid, s_new in carried.items():
+        st[idx[uid]] = s_new
+    r = cpu_gang_sample(cluster, cfg, warm, given, pods, seq, gang_ids, specs, sample, threads)
+    want, wres = r["want"], r["wres"]
+    got, gres = first
+    bad = []
+    if not np.array_equal(np.asarray(gres["prefilter"])[:sample], np.asarray(wres["prefilter"])):
+        bad.append("prefilter")
+    ran = want["node"] >= 0
+    for f in ("node", "score", "ties", "feasible"):
+        if not np.array_equal(got[f][:sample][ran], want[f][ran]):
+            bad.append(f)
+    n = total - warm
+    return {"pods_per_s": n / dt, "pods": n, "calls": calls, "pods_per_call": P, "nodes": cluster.num_nodes,
+            "seconds": dt, "gangs": n_g, "gang_size": gang_size, "gang_pods": int(np.count_nonzero(gang_ids[warm:])),
+            "bound": int(np.count_nonzero(st == gg.ST_BOUND)), "waiting": int(np.count_nonzero(st == gg.ST_WAITING)),
+            "rejected": int(np.count_nonzero(st == gg.ST_REJECTED)),
+            "unschedulable": int(np.count_nonzero(st == gg.ST_UNSCHEDULABLE)),
+            "workload": "C3 (NUMA profile) with Coscheduling: Strict gangs (minMember = size, PodGroups known up front), "
+                        f"schedule_with_gangs run cap {run_cap}; decided pods/s",
+            "parity_sample": {"pods": sample, "ran_node_loop": int(ran.sum()), "mismatched_fields": bad, "ok": not bad,
+                              "what": "the first pods of the gang queue against oracle/coscheduling.py's one-pod-at-a-time "
+                                      "order on the oracle engine after replaying the same warm-up placements"},
+            "cpu_baseline": {"pods_per_s": sample / r["seconds"], "cores": threads, "kind": "port",
+                             "seconds": r["seconds"], "sample": f"{sample} pods, one scheduleOne at a time with the gang "
+                                                                 f"gates, Filter/Score over {threads} threads"}}
 
 
 def host_cpus() -> dict:
@@ -171,6 +339,8 @@ def main() -> None:
                     help="several ranks: RCCL all-gather (production) or gloo through the host-callback transport")
     ap.add_argument("--share-gpu", action="store_true", help="every rank on device 0 (gloo rehearsal on one GPU)")
     ap.add_argument("--sync", action="store_true", help="one blocking gs_schedule per step (no submission ahead)")
+    ap.add_argument("--no-extras", action="store_true",
+                    help="skip the C5 and Coscheduling sub-objects of the default (one-GPU, C3) line")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -340,6 +510,7 @@ def main() -> None:
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline and c5:
         r = cpu_baseline_c5(cluster, cfg, ext_args, pods, seq, args.cpu_sample_pods // 4)
+        r.pop("placements")
         cpu = {"value": r["evals_per_s"], "unit": "evals/s", "cores": 1, "kind": "port", "pods_per_s": r["pods_per_s"],
                "seconds": r["seconds"], "sample": r["sample"]}
     elif rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -428,6 +599,11 @@ def main() -> None:
                              "slowpath_pods": st["slowpath_pods"]},
             "cpu_baseline": cpu,
         }
+        if world == 1 and args.profile == "c3" and args.sample_pct is None and not args.no_extras:
+            # the C5 and Coscheduling configurations beside the headline (extra keys; the C3 line above is unchanged)
+            del eng
+            line["c5"] = extra_c5(P, steps=3, nodes=100_000, sample=40)
+            line["gang"] = extra_gang(cluster, cfg, P, calls=5, sample=40, threads=min(16, host_cpus()["usable"]))
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -164,6 +164,8 @@ struct gs_ctx {
   PlacementDev* d_out = nullptr;
   int32_t* d_committed = nullptr;
   int32_t* d_tb = nullptr;          // speculative commit: tie-break records of the batch's pods
+  uint64_t* d_help = nullptr;       // speculative commit: the re-scoring helpers' job / result rings (help_bytes())
+  uint32_t help_epoch = 0;          // commit launches that used them (tags the rings' entries)
   RowStat* d_rowstat = nullptr;
   int32_t* d_sel = nullptr;
   uint32_t* d_stage_idx = nullptr;
@@ -1199,9 +1201,10 @@ constexpr size_t COMMITTED_BYTES = 32;   // committed[0..7] (the commit kernels 
 // the previous batch's commit, on the stale rows it lands on), then fixed up on st once that commit is done
 // (GS_FUSED_PATCH=0, the separate patch kernel: not overlapped)
 // A batch with no speculative pass before it, of at most GS_DIRECT_B pods (default 32; 0: none), on one shard: its
-// upload, eval pass and levels go on st in order instead of through st_ev (st_ev still waits for st at its start, so a
-// speculative pass after it sees the same order). Short runs (the plain pods between C5's extension pods) lose two
-// queue hops per batch.
+// upload, eval pass and levels go on st in order instead of through st_ev. st_ev then waits for that eval pass and its
+// levels (launch_batch): a speculative pass enqueued after it on st_ev shares the NUMA slab, st2 and the fork / join
+// events with it, so it starts only once they are done. Short runs (the plain pods between C5's extension pods) lose
+// two queue hops per batch.
 bool direct_batch(const gs_ctx* c, int b, bool speculative) {
   static const int max_b = getenv("GS_DIRECT_B") ? atoi(getenv("GS_DIRECT_B")) : 32;
   return !speculative && b <= max_b && c->nranks == 1;
@@ -1253,9 +1256,18 @@ CommitArgs commit_args(gs_ctx* c, int b) {
   // GS_SPEC_AHEAD=2 (experiments): the prep wave may run two pods ahead (bit 18)
   static const bool ahead2 = getenv("GS_SPEC_AHEAD") && getenv("GS_SPEC_AHEAD")[0] == '2';
   // GS_SPEC_SPLIT=3 (experiments): shared verification by the prep wave while it waits (bits 17 and 19)
+  static const uint32_t rsx = getenv("GS_RESCORE_X") ? (uint32_t)atoi(getenv("GS_RESCORE_X")) & 3u : 0u;
+  // GS_HELP_CHECK=1 (diagnostics): the receiver re-scores every helper job itself and counts mismatches (gs_destroy
+  // prints them)
+  static const uint32_t hchk = getenv("GS_HELP_CHECK") && getenv("GS_HELP_CHECK")[0] == '1' ? 1u << 22 : 0u;
   a.dbg = (nospec ? 1u : 0u) | prio | lag << 12 | (split >= 1 ? 1u << 16 : 0u) | (split >= 2 ? 1u << 17 : 0u) |
-          (ahead2 ? 1u << 18 : 0u) | (split >= 3 ? 1u << 19 : 0u);
+          (ahead2 ? 1u << 18 : 0u) | (split >= 3 ? 1u << 19 : 0u) | rsx << 20 | hchk;
   a.tb = c->d_tb;
+  // re-scoring on GS_RESCORE_HELPERS helper workgroups beside the split commit (default 2; 0: on the commit's CU)
+  static const int nhelp = getenv("GS_RESCORE_HELPERS") ? std::max(0, std::min(8, atoi(getenv("GS_RESCORE_HELPERS")))) : 0;
+  a.help = nhelp > 0 ? c->d_help : nullptr;
+  a.nhelp = nhelp;
+  a.help_epoch = ++c->help_epoch;
   a.xerr = c->nranks > 1 ? c->d_xerr : nullptr;
   return a;
 }
@@ -1324,6 +1336,9 @@ int launch_batch(gs_ctx* c, int b, const int32_t* prev, const PlacementDev* prev
   if (!direct) {
     HIP_TRY(c, hipEventRecord(sl.ev_evdone, c->st_ev));
     HIP_TRY(c, hipStreamWaitEvent(c->st, sl.ev_evdone, 0));
+  } else {   // the next speculative pass on st_ev (gather into the shared slab, eval) after this one
+    HIP_TRY(c, hipEventRecord(sl.ev_evdone, c->st));
+    HIP_TRY(c, hipStreamWaitEvent(c->st_ev, sl.ev_evdone, 0));
   }
   if (fix) {
     CandPatch cp{c->mv, c->d_pods, c->pf, c->n0, c->n1, prod_cols, 0, c->d_aff, prev_out, prev};
@@ -1365,9 +1380,10 @@ int launch_batch(gs_ctx* c, int b, const int32_t* prev, const PlacementDev* prev
   // Two copies, not one over the adjacent committed words and placements: with one merged copy, 4 processes sharing the
   // GPU (the C4 rehearsal) stalled for 10-100 s at a time, every rank's commit and next eval pass pending (DESIGN §8;
   // GS_MERGE_RB=1 restores the merged copy for that experiment)
-  // A direct batch (one shard, on st, the host waiting on it) reads back in one copy (GS_DIRECT_MERGE_RB=0: two)
+  // A direct batch reads back in two copies as well: the merged form measured within noise there and its
+  // stall with several processes on one GPU is not understood (GS_DIRECT_MERGE_RB=1, experiments: one copy)
   static const bool merge_rb = getenv("GS_MERGE_RB") && getenv("GS_MERGE_RB")[0] == '1';
-  static const bool merge_direct = !(getenv("GS_DIRECT_MERGE_RB") && getenv("GS_DIRECT_MERGE_RB")[0] == '0');
+  static const bool merge_direct = getenv("GS_DIRECT_MERGE_RB") && getenv("GS_DIRECT_MERGE_RB")[0] == '1';
   if (merge_rb || (direct && merge_direct && rb == c->st)) {
     HIP_TRY(c, hipMemcpyAsync(c->h_committed, c->d_committed, COMMITTED_BYTES + sizeof(PlacementDev) * b,
                               hipMemcpyDeviceToHost, rb));
@@ -2143,6 +2159,10 @@ int gs_create(const gs_config* cfg, gs_ctx** out) {
   if ((e = hipMalloc(&c->d_committed, COMMITTED_BYTES + sizeof(PlacementDev) * c->B)) != hipSuccess) return bail("hipMalloc", e);
   c->d_out = reinterpret_cast<PlacementDev*>(c->d_committed + COMMITTED_BYTES / 4);
   if ((e = hipMalloc(&c->d_tb, sizeof(int32_t) * TB_N * c->B)) != hipSuccess) return bail("hipMalloc", e);
+  // uncached: the rings are read and written by workgroups on different XCDs (gs_commit_spec.hip, REMOTE)
+  if ((e = hipExtMallocWithFlags(reinterpret_cast<void**>(&c->d_help), help_bytes(), hipDeviceMallocUncached)) != hipSuccess)
+    return bail("hipExtMallocWithFlags", e);
+  if ((e = hipMemset(c->d_help, 0, help_bytes())) != hipSuccess) return bail("hipMemset", e);
   if ((e = hipMalloc(&c->d_rowstat, sizeof(RowStat) * (1 + MAX_RANKS))) != hipSuccess) return bail("hipMalloc", e);
   if ((e = hipMalloc(&c->d_sel, 4 * (1 + MAX_RANKS))) != hipSuccess) return bail("hipMalloc", e);
   c->stage_cap = std::min<uint32_t>(c->N, 65536);
@@ -2369,10 +2389,24 @@ int gs_destroy(gs_ctx* c) {
     for (auto& ev : s1.ev)
       if (ev) (void)hipEventDestroy(ev);
   }
+  if (c->d_help && getenv("GS_HELP_CHECK") && getenv("GS_HELP_CHECK")[0] == '1') {
+    uint64_t w[16] = {};
+    if (hipMemcpy(w, c->d_help, sizeof w, hipMemcpyDeviceToHost) == hipSuccess) {
+      fprintf(stderr, "gpuscore help check: block 0 end %llu, last helper exit %llu (x10 ns); helper waves ended by the end "
+                      "word %llu, by the bound %llu; jobs taken %llu; published rows differing %llu (first word %llu: %llx vs %llx)\n",
+              (unsigned long long)w[5], (unsigned long long)w[6], (unsigned long long)w[7], (unsigned long long)w[8],
+              (unsigned long long)w[9], (unsigned long long)w[11], (unsigned long long)w[12], (unsigned long long)w[13],
+              (unsigned long long)w[14]);
+      fprintf(stderr, "gpuscore help check: %llu of %llu helper jobs differ; first q %llu slot %llu range %llu lane %llu helper %d local %d\n",
+              (unsigned long long)w[2], (unsigned long long)w[3], (unsigned long long)(w[4] & 0xff),
+              (unsigned long long)((w[4] >> 8) & 0xff), (unsigned long long)((w[4] >> 16) & 0xff),
+              (unsigned long long)((w[4] >> 24) & 0xff), (int)(int16_t)(w[4] >> 32), (int)(int16_t)(w[4] >> 48));
+    }
+  }
   void* dev[] = {c->d_xerr, c->d_xsmall,
                  c->d_i64, c->d_i32, c->d_pods, c->d_S, c->d_xchg_send, c->d_xchg_recv, c->d_xmerged,
                  c->d_committed, c->d_rowstat, c->d_sel, c->d_stage_idx, c->d_stage_rows, c->d_numa_idx,
-                 c->d_topos, c->d_aff, c->d_tb};
+                 c->d_topos, c->d_aff, c->d_tb, c->d_help};
   for (void* p : dev)
     if (p) (void)hipFree(p);
   void* host[] = {c->h_xsmall, c->h_pods, c->h_committed, c->h_stage_idx, c->h_stage_rows, c->h_xchg_send,
@@ -2605,7 +2639,8 @@ int stage_batch(gs_ctx* c, const gs_pod* pods, const uint64_t* seq, uint32_t i, 
   // experiments: two copies)
   static const bool merge_up = !(getenv("GS_MERGE_UP") && getenv("GS_MERGE_UP")[0] == '0');
   hipStream_t up = direct_batch(c, b, speculative) ? c->st : c->st_ev;
-  if (merge_up) {
+  // (the merged copy spans all B pod vectors, d_seq following the block: a short batch copies its b vectors and seq)
+  if (merge_up && 4 * b >= c->B) {
     HIP_TRY(c, hipMemcpyAsync(c->d_pods, c->h_pods, sizeof(PodVec) * c->B + 8 * b, hipMemcpyHostToDevice, up));
   } else {
     HIP_TRY(c, hipMemcpyAsync(c->d_pods, c->h_pods, sizeof(PodVec) * b, hipMemcpyHostToDevice, up));
