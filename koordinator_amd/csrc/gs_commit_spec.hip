@@ -98,7 +98,6 @@ struct Job {
 constexpr int SP_KW = 4;          // ties recorded from the tie-break position on (the window wave 0 re-ranks in)
 constexpr int SP_PREPQ = 3;       // PrepRec ring: the prep wave works at most SP_PREPQ - 1 pods ahead of wave 0
 constexpr int SP_W_PREP = 1;      // its wave (SIMD 1; wave 0 decides on SIMD 0)
-constexpr int SP_W_RECV = 6;      // REMOTE: the receiver of the helpers' results (SIMD 2, beside a Reserve wave)
 struct PrepRec {                    // (the first 80 bytes read as five 16-byte words)
   int32_t pod, q_s, nd_s, action;   // q_s: decisions in the snapshot (nd_s slots); action 0, 1 (FitError), 2 (stop),
                                     // 5: only over the exact state (q_s == pod)
@@ -110,67 +109,6 @@ struct PrepRec {                    // (the first 80 bytes read as five 16-byte 
 };
 constexpr int SF_READY = 1, SF_FEAS = 2, SF_TIE = 4, SF_PEND = 8;   // ready (exact score counted), ... feasible, ... at
                                                                      // M; pending (left out)
-// Re-scoring on helper workgroups (REMOTE: one shard, the split pipeline, a.nhelp > 0). The
-// re-scoring jobs leave the commit's CU: a Reserve wave publishes each job (the row's new state, the pod, the range of
-// 64 later pods) into a ring in HBM, the helper workgroups' waves (blocks 1..nhelp of the same launch, on other CUs)
-// claim jobs in order, score the row for the 64 pods and publish the 64 scores; one receiver wave on the commit's CU
-// consumes the results in job order into dsc and does the bookkeeping the re-scoring waves did. Every hand-off byte is
-// stored and loaded sc1 (agent-scope relaxed atomics: L1 bypassed), each storing wave drains its stores
-// (s_waitcnt vmcnt(0)) before one lane stores the entry's tag (MI355X_MICROARCH.md, inter-workgroup visibility). The
-// rings live in uncached device memory (hipDeviceMallocUncached): with hipMalloc'd memory the helpers (on other XCDs)
-// read job rows and the end word stale from their own L2 (measured: 1,397 of 1,502 jobs scored on an earlier row of
-// their ring entry, and no helper saw the end word until its bounded wait expired).
-// Tags carry the launch's epoch (help_epoch, per context, never repeated) and the job's sequence number, so the rings
-// are never reset.
-constexpr int HR = 64;                              // ring entries (jobs between publication and the receiver)
-constexpr int ROW_W = (int)(sizeof(Row) / 8);       // the row's words
-constexpr int HJ_W = 48;                            // job entry: tag, header (q | range << 16), the row
-constexpr int HR_W = 32;                            // result entry: tag (line 0), 16 words = 64 int16 scores (line 1)
-constexpr int HG_CTL = 32;                          // control: [0] claims (epoch << 32 | next seq), [16] end (epoch << 32),
-                                                    // [2..7] diagnostics (GS_HELP_CHECK)
-constexpr int HG_FIN = 16;
-static_assert(sizeof(Row) % 8 == 0 && ROW_W + 2 <= HJ_W, "job entry holds the row");
-size_t help_bytes() { return 8 * (HG_CTL + (size_t)HR * (HJ_W + HR_W)); }
-struct JobMeta {          // LDS: a published job as the receiver needs it
-  int32_t seq1;           // sequence number + 1 (release-stored last)
-  uint32_t info;          // slot | q << 8 | range << 16 | JM_CANCEL
-};
-constexpr uint32_t JM_CANCEL = 1u << 24;   // a rollback undid its pod: the result is consumed, not applied
-__device__ __forceinline__ uint64_t g_ld(const uint64_t* p) {
-  return __hip_atomic_load(const_cast<uint64_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void g_st(uint64_t* p, uint64_t v) {
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void vm_drain() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
-// a polled word read where the atomics are performed (a compare-and-swap that never changes the value)
-__device__ __forceinline__ uint64_t g_poll(uint64_t* p) {
-  uint64_t e = 0x5A5A5A5A5A5A5A5Aull;
-  __hip_atomic_compare_exchange_strong(p, &e, e, __ATOMIC_RELAXED, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  return e;
-}
-__device__ __forceinline__ uint64_t shfl64(uint64_t v, int src) {
-  return (uint64_t)(uint32_t)__shfl((int)(uint32_t)v, src) | (uint64_t)(uint32_t)__shfl((int)(uint32_t)(v >> 32), src) << 32;
-}
-// Every hand-off carries a hash of its words and its sequence number, checked by the reader before it uses them: a
-// payload read before all of its words arrived (or a stale copy of an earlier job's) is read again, never used.
-__device__ __forceinline__ uint64_t hand_hash(uint64_t w, int lane, bool on, uint64_t seq) {
-  uint64_t x = on ? mix64(w ^ ((uint64_t)(lane + 1) * 0x9E3779B97F4A7C15ull)) : 0;
-#pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) x ^= shfl64(x, lane ^ o);
-  return x ^ mix64(seq + 0x51ED27ull);
-}
-// the next job of this launch (the claim word restarts at 0 when it holds another launch's epoch)
-__device__ __forceinline__ uint32_t help_claim(uint64_t* g, uint32_t epoch) {
-  uint64_t cur = g_ld(g);
-  for (;;) {
-    const uint32_t seq = (uint32_t)(cur >> 32) == epoch ? (uint32_t)cur : 0u;
-    const uint64_t nxt = ((uint64_t)epoch << 32) | (uint64_t)(seq + 1);
-    if (__hip_atomic_compare_exchange_strong(g, &cur, nxt, __ATOMIC_RELAXED, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
-      return seq;
-  }
-}
-
 struct Hdr {             // a pod's level header and list head, one value per lane (load_hdr)
   int hs, hc, nlev, feas, next;
   uint32_t lh;
@@ -217,23 +155,13 @@ struct alignas(16) SpecLds {
   alignas(16) int32_t final_F[SB], done_ver[SB], has_row[SB], rescored[SB], jobs_left[SB], jobs_all[SB], resv[SB];
   alignas(16) int32_t hkey[SP_HASH];
   alignas(16) int16_t hval[SP_HASH];   // slot of the node in hkey
-  union alignas(16) {
-    Job jobq[SP_NRES * SP_JOBQ];   // local re-scoring: the Reserve waves' job rings
-    JobMeta jmeta[HR];             // REMOTE: the published jobs, by sequence number mod HR
-  };
+  alignas(16) Job jobq[SP_NRES * SP_JOBQ];
   alignas(16) PrepRec prq[SP_PREPQ];       // split pipeline: the prep wave's records
   alignas(16) int32_t slot_node[SB];   // split pipeline: the slot table the prep wave snapshots
   alignas(16) int16_t slot_pv[SB];
 };
 
 size_t spec_smem_bytes(int) { return sizeof(SpecLds); }
-// a helper workgroup's view of the same LDS: the pod vectors, a row and a hint table per wave
-struct alignas(16) HelpLds {
-  alignas(16) unsigned char pods_b[SB * POD_STRIDE];
-  alignas(16) Row rows[SP_WAVES];
-  alignas(16) HintTable tables[SP_WAVES];
-};
-static_assert(sizeof(HelpLds) <= sizeof(SpecLds), "helper LDS within the launch's");
 // the CU's 160 KiB hold SpecLds and the kernel's static __shared__ words (~200 B of hand-off words)
 static_assert(sizeof(SpecLds) + 200 <= 160 * 1024, "commit_spec_kernel LDS over the CU's 160 KiB");
 
@@ -258,7 +186,6 @@ __shared__ int32_t s_snap;        // split: decisions whose slot table and batch
 __shared__ int32_t s_prep_done;   // split: pods the prep wave has recorded
 __shared__ int32_t s_reprep;      // split: wave 0 -> prep wave: p + 1 = record pod p again over the exact state
 __shared__ int32_t s_vlock, s_vwm;   // split, shared verification: the verifier's lock, its re-scored frontier
-__shared__ int32_t s_galloc, s_rseq;  // REMOTE: jobs allocated (sequence numbers), results consumed by the receiver
 
 // (s_memtime is a scalar-memory instruction: reading its result waits for every LDS operation and scalar load in flight,
 // so a stamp also closes the latency of the prefetches issued before it. HW_REG_SHADER_CYCLES reads 0 on gfx950.)
@@ -332,76 +259,6 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
     if (tid == 0) { a.committed[0] = 0; a.committed[1] = 0; a.committed[2] = 0; a.committed[3] = COMMIT_ERR_XTAG; a.committed[4] = 0; }
     return;
   }
-  // REMOTE (header): blocks 1.. are helper workgroups, block 0 the commit
-  const bool remote = SPLIT && a.help != nullptr && gridDim.x > 1;
-  const uint64_t hep = (uint64_t)a.help_epoch << 32;
-  if (blockIdx.x > 0) {
-    // ============================================ helper: re-scoring jobs ============================================
-    if (!remote) return;
-    HelpLds& H = *reinterpret_cast<HelpLds*>(cm);
-    for (int i = tid; i < B; i += SP_THREADS) *reinterpret_cast<PodVec*>(H.pods_b + (size_t)i * POD_STRIDE) = a.pods[i];
-    __syncthreads();
-    uint64_t* const G = a.help;
-    Row* hrow = &H.rows[wv];
-    HintTable& tab = H.tables[wv];
-    for (;;) {
-      uint32_t seq = 0;
-      if (lane == 0) seq = help_claim(G, a.help_epoch);
-      seq = (uint32_t)__builtin_amdgcn_readfirstlane((int)seq);
-      const uint64_t want = hep | (uint64_t)(seq + 1);
-      const uint64_t* job = G + HG_CTL + (size_t)(seq % HR) * HJ_W;
-      bool quit = false;
-      uint64_t w = 0;
-      for (uint32_t spins = 0;; ++spins) {   // until the job is published (and its words verified), or the commit ended
-        uint64_t t = 0, f = 0;
-        if (lane == 0) { t = g_poll(const_cast<uint64_t*>(job)); f = g_poll(G + HG_FIN); }
-        t = rfl64(t);
-        f = rfl64(f);
-        if (t == want) {
-          w = lane < 2 + ROW_W ? g_ld(job + 1 + lane) : 0;   // header, the row, the hash
-          const uint64_t h = hand_hash(w, lane, lane < 1 + ROW_W, seq);
-          const uint64_t hw = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(w >> 32), 1 + ROW_W) << 32) |
-                              (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)w, 1 + ROW_W);
-          if (rfl64(h) == hw) break;
-        }
-        if (f == hep || spins > SP_SPIN_LIMIT) { quit = true; break; }
-        __builtin_amdgcn_s_sleep(1);
-      }
-      if (quit) {
-        if ((a.dbg >> 22) & 1u && lane == 0) {   // GS_HELP_CHECK: how the helper waves ended
-          __hip_atomic_fetch_add(G + (__builtin_amdgcn_readfirstlane((int)(g_ld(G + HG_FIN) == hep)) ? 7 : 8), (uint64_t)1,
-                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          __hip_atomic_fetch_max(G + 6, (uint64_t)__builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-        break;
-      }
-      if ((a.dbg >> 22) & 1u && lane == 0) __hip_atomic_fetch_add(G + 9, (uint64_t)1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const uint32_t hdr = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)w);
-      if (lane >= 1 && lane < 1 + ROW_W) reinterpret_cast<uint64_t*>(hrow)[lane - 1] = w;
-      // (the row is stored as words and read as a Row: a compiler memory barrier, so that no field load of another
-      // type is moved above the word stores; WAVE_FENCE orders nothing for alias analysis)
-      asm volatile("" ::: "memory");
-      WAVE_FENCE();
-      const Row rr = *hrow;
-      if (numa_on && ((rr.nr.nflags >> NF_POLICY_SHIFT) & 3u)) hint_table_fill(tab, rr.nr, zone_avail(rr.nr), lane);
-      WAVE_FENCE();
-      const int q = (int)(hdr & 0xffffu), range = (int)(hdr >> 16);
-      const int q2 = q + 1 + range * 64 + lane;
-      int sc = -1;
-      if (q2 < B) sc = row_score(rr, *reinterpret_cast<const PodVec*>(H.pods_b + (size_t)q2 * POD_STRIDE), a.pf, m, &tab);
-      // four scores per word: lane i < 16 stores the scores of lanes 4i .. 4i+3
-      const int u = sc & 0xffff, b4 = 4 * (lane & 15);
-      const uint64_t word = (uint64_t)(uint32_t)__shfl(u, b4) | (uint64_t)(uint32_t)__shfl(u, b4 + 1) << 16 |
-                            (uint64_t)(uint32_t)__shfl(u, b4 + 2) << 32 | (uint64_t)(uint32_t)__shfl(u, b4 + 3) << 48;
-      uint64_t* res = G + HG_CTL + (size_t)HR * HJ_W + (size_t)(seq % HR) * HR_W;
-      const uint64_t rh = hand_hash(word, lane, lane < 16, seq);
-      if (lane < 16) g_st(res + 16 + lane, word);
-      if (lane == 0) g_st(res + 1, rh);
-      vm_drain();
-      if (lane == 0) g_st(res, want);
-    }
-    return;
-  }
   for (int i = tid; i < B; i += SP_THREADS) {
     pods(i) = a.pods[i];
     done_ver[i] = -1;
@@ -419,10 +276,7 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
     s_verified = 0; s_rb_req = 0; s_end_at = B; s_vend = -1; s_vcut = 0;
     s_committed = 0; s_hostcut = 0; s_nd = 0;
     s_snap = 0; s_prep_done = 0; s_reprep = 0; s_vlock = 0; s_vwm = 0;
-    s_galloc = 0; s_rseq = 0;
   }
-  if (remote)
-    for (int i = tid; i < HR; i += SP_THREADS) L.jmeta[i].seq1 = 0;
   __syncthreads();
 
 
@@ -980,7 +834,7 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
       // order, so by their flags), restore the slot versions
       st_rel(&s_stop, 1);
       spins = 0;
-      while (ld_acq(&s_parked) < SP_WAVES - 1 - (remote ? 3 : 0)) {   // (REMOTE: three idle waves do not park)
+      while (ld_acq(&s_parked) < SP_WAVES - 1) {
         if (++spins > SP_SPIN_LIMIT) { err = true; err_code = 1; return false; }
         sp_sleep();
       }
@@ -1041,14 +895,6 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
         jobs_left[qq] = 0;
         jobs_all[qq] = 0;
         resv[qq] = 0;
-      }
-      if (remote) {   // jobs of undone pods still in the helpers' hands: the receiver consumes them unapplied
-        const int r0 = s_rseq, r1 = s_galloc;
-        for (int sq = r0 + lane; sq < r1; sq += 64) {
-          JobMeta& jm = L.jmeta[sq % HR];
-          if ((int)((jm.info >> 8) & 0xffu) >= v) jm.info |= JM_CANCEL;
-        }
-        WAVE_FENCE();
       }
       if (lane == 0) {
         for (int k = 0; k < SP_NRES; ++k) { s_jq_head[k] = 0; s_jq_tail[k] = 0; }
@@ -1661,31 +1507,6 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
       }
       return true;
     };
-    // REMOTE: n sequence numbers for this pod's jobs, once the rings hold them (-1: a rollback or the end intervened)
-    auto galloc = [&](int n) -> int {
-      int base = -1;
-      if (lane == 0) {
-        uint32_t w = 0;
-        int cur = ld_acq(&s_galloc);
-        for (;;) {
-          if (cur + n - ld_acq(&s_rseq) <= HR) {
-            if (__atomic_compare_exchange_n(&s_galloc, &cur, cur + n, false, __ATOMIC_ACQ_REL, __ATOMIC_ACQUIRE)) {
-              base = cur;
-              break;
-            }
-            continue;
-          }
-          if (ld_acq(&s_stop) || ld_acq(&s_finish)) break;
-          if (++w > SP_SPIN_LIMIT) {
-            __atomic_store_n(&s_werr, 7, __ATOMIC_RELEASE);
-            break;
-          }
-          sp_sleep();
-          cur = ld_acq(&s_galloc);
-        }
-      }
-      return __builtin_amdgcn_readfirstlane(base);
-    };
     for (;;) {
       if (ld_acq(&s_stop)) {   // rollback: park until wave 0 has repaired the state, resume at its pod of our parity
         if (lane == 0) __atomic_fetch_add(&s_parked, 1, __ATOMIC_ACQ_REL);
@@ -1756,12 +1577,7 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
       const int njobs = (nlater + 63) / 64;
       const bool xjob = (d.flags & SP_OFFSHARD) && njobs > 0;
       // ring room for this pod's jobs before the Reserve changes anything (a rollback may end the wait; it only grows)
-      int gbase = 0;
-      if (remote) {
-        if (njobs > 0 && (gbase = galloc(njobs)) < 0) continue;
-      } else if (!room(njobs + (xjob ? 1 : 0))) {
-        continue;
-      }
+      if (!room(njobs + (xjob ? 1 : 0))) continue;
       if (xjob) {   // another shard's row: its batch-start job goes first, ahead of the row's re-scoring jobs
         if (lane == 0) {
           jobs_left[q] = njobs;
@@ -1878,33 +1694,6 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
           __atomic_store_n(&done_ver[slot], q, __ATOMIC_RELEASE);
           __atomic_store_n(&rescored[q], 1, __ATOMIC_RELEASE);
         }
-      } else if (remote) {
-        // publish: the receiver's LDS record, the ring entries (header, row: sc1 stores), drained, then the tags
-        // (the row read as words after lane 0's field stores of the Reserve: a compiler memory barrier first)
-        asm volatile("" ::: "memory");
-        const uint64_t rword = lane < ROW_W ? reinterpret_cast<const uint64_t*>(&drows[slot])[lane] : 0;
-        const uint64_t rup = shfl64(rword, lane > 0 ? lane - 1 : 0);   // entry word 1 + lane: lane 0 the header
-        if (lane == 0) {
-          jobs_left[q] = njobs;
-          jobs_all[q] = njobs;
-        }
-        for (int j = 0; j < njobs; ++j) {
-          const int sq = gbase + j;
-          uint64_t* job = a.help + HG_CTL + (size_t)(sq % HR) * HJ_W;
-          const uint64_t v = lane == 0 ? (uint64_t)(uint32_t)(q | j << 16) : rup;
-          const uint64_t h = hand_hash(v, lane, lane < 1 + ROW_W, (uint64_t)sq);
-          if (lane < 1 + ROW_W) g_st(job + 1 + lane, v);
-          if (lane == 0) g_st(job + 2 + ROW_W, h);
-        }
-        vm_drain();
-        if (lane == 0)
-          for (int j = 0; j < njobs; ++j) {
-            const int sq = gbase + j;
-            g_st(a.help + HG_CTL + (size_t)(sq % HR) * HJ_W, hep | (uint64_t)(uint32_t)(sq + 1));
-            JobMeta& jm = L.jmeta[sq % HR];
-            jm.info = (uint32_t)slot | (uint32_t)q << 8 | (uint32_t)j << 16;
-            st_rel(&jm.seq1, sq + 1);
-          }
       } else {
         if (lane == 0) {
           if (!xjob) {
@@ -1922,108 +1711,6 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
       if (vshare && !vprep && njobs == 0) verify_try();
       q += SP_NRES;
       SPM(5);
-    }
-  } else if (remote && wv != SP_W_RECV) {
-    // REMOTE: the other re-scoring waves idle until the batch ends (they do not park: wave 0 counts 4 parked waves)
-    while (!ld_acq(&s_finish)) __builtin_amdgcn_s_sleep(8);
-  } else if (remote) {
-    // ============================================ receiver (REMOTE) ============================================
-    // the helpers' results in job order: dsc entries of the job's 64 later pods, then the bookkeeping of a re-scoring
-    // wave (done_ver when the row's version is complete, rescored when the pod is)
-    uint32_t spins = 0;
-    int rs = 0;   // the next job (s_rseq)
-    for (;;) {
-      if (ld_acq(&s_stop)) {
-        if (lane == 0) __atomic_fetch_add(&s_parked, 1, __ATOMIC_ACQ_REL);
-        while (ld_acq(&s_stop) && !ld_acq(&s_finish)) sp_sleep();
-        continue;
-      }
-      if (ld_acq(&s_finish)) break;
-      const JobMeta& jm = L.jmeta[rs % HR];
-      const uint64_t* res = a.help + HG_CTL + (size_t)HR * HJ_W + (size_t)(rs % HR) * HR_W;
-      bool ready = ld_acq(&jm.seq1) == rs + 1;
-      uint64_t w = 0;
-      if (ready) {
-        uint64_t t = 0;
-        if (lane == 0) t = g_poll(const_cast<uint64_t*>(res));
-        ready = rfl64(t) == (hep | (uint64_t)(uint32_t)(rs + 1));
-        if (ready) {   // the 16 words of scores and their hash
-          w = lane < 16 ? g_ld(res + 16 + lane) : lane == 16 ? g_ld(res + 1) : 0;
-          const uint64_t hw = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(w >> 32), 16) << 32) |
-                              (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)w, 16);
-          ready = rfl64(hand_hash(w, lane, lane < 16, (uint64_t)rs)) == hw;
-        }
-      }
-      if (!ready) {
-        if (++spins > SP_SPIN_LIMIT) {
-          if (lane == 0) __atomic_store_n(&s_werr, 6, __ATOMIC_RELEASE);
-          break;
-        }
-        sp_sleep();
-        SPM(8);
-        continue;
-      }
-      spins = 0;
-      const uint32_t info = (uint32_t)__builtin_amdgcn_readfirstlane((int)jm.info);
-      int fin = 0;
-      if (!(info & JM_CANCEL)) {
-        const int slot = (int)(info & 0xffu), q = (int)((info >> 8) & 0xffu), range = (int)((info >> 16) & 0xffu);
-        const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)w, lane >> 2), hi = (uint32_t)__shfl((int)(uint32_t)(w >> 32), lane >> 2);
-        const int sh = 16 * (lane & 1);
-        const int16_t v = (int16_t)(((lane & 2) ? hi : lo) >> sh);
-        const int q2 = q + 1 + range * 64 + lane;
-        int16_t vv = v;
-        if ((a.dbg >> 22) & 1u) {   // GS_HELP_CHECK (diagnostics): the job scored here too; mismatches counted in the ring
-          const Row rr = drows[slot];
-          HintTable& tab = tables[1];
-          if (numa_on && ((rr.nr.nflags >> NF_POLICY_SHIFT) & 3u)) hint_table_fill(tab, rr.nr, zone_avail(rr.nr), lane);
-          WAVE_FENCE();
-          const int loc = q2 < B ? row_score(rr, pods(q2), a.pf, m, &tab) : -1;
-          const uint64_t bad = __ballot(q2 < B && loc != (int)v);
-          if (lane == 0) {
-            __hip_atomic_fetch_add(a.help + 3, (uint64_t)1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (bad) __hip_atomic_fetch_add(a.help + 2, (uint64_t)1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          }
-          const int fl = bad ? __builtin_ctzll(bad) : -1;
-          if (bad && lane == fl) {
-            uint64_t z = 0;
-            const uint64_t rec = (uint64_t)(uint32_t)q | (uint64_t)(uint32_t)slot << 8 | (uint64_t)(uint32_t)range << 16 |
-                                 (uint64_t)(uint32_t)lane << 24 | (uint64_t)(uint16_t)v << 32 | (uint64_t)(uint16_t)loc << 48;
-            __hip_atomic_compare_exchange_strong(a.help + 4, &z, rec, __ATOMIC_RELAXED, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          }
-          vv = (int16_t)loc;
-          // the published row against the slot's row now
-          const uint64_t* jrow = a.help + HG_CTL + (size_t)(rs % HR) * HJ_W + 2;
-          const uint64_t pw = lane < ROW_W ? g_ld(jrow + lane) : 0;
-          const uint64_t lw = lane < ROW_W ? reinterpret_cast<const uint64_t*>(&drows[slot])[lane] : 0;
-          const uint64_t rb = __ballot(lane < ROW_W && pw != lw);
-          if (rb && lane == 0) __hip_atomic_fetch_add(a.help + 11, (uint64_t)1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          if (rb && lane == __builtin_ctzll(rb)) {
-            uint64_t z = 0;
-            if (__hip_atomic_compare_exchange_strong(a.help + 12, &z, (uint64_t)lane + 1, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
-                                                     __HIP_MEMORY_SCOPE_AGENT)) {
-              g_st(a.help + 13, pw);
-              g_st(a.help + 14, lw);
-            }
-          }
-        }
-        if (q2 < B) dsc[q2 * SB + slot] = vv;
-        WAVE_FENCE();
-        if (lane == 0) {
-          if (__atomic_fetch_sub(&jobs_left[q], 1, __ATOMIC_ACQ_REL) == 1)
-            __atomic_store_n(&done_ver[slot], q, __ATOMIC_RELEASE);
-          if (__atomic_fetch_sub(&jobs_all[q], 1, __ATOMIC_ACQ_REL) == 1) {
-            __atomic_store_n(&rescored[q], 1, __ATOMIC_RELEASE);
-            fin = 1;
-          }
-        }
-        if (ST) st_acc[10] += 1;
-      }
-      ++rs;
-      if (lane == 0) st_rel(&s_rseq, rs);
-      WAVE_FENCE();
-      if (vshare && !vprep && __builtin_amdgcn_readfirstlane(fin)) verify_try();
-      SPM(7);
     }
   } else {
     // ============================================== re-scoring jobs ==============================================
@@ -2092,16 +1779,7 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
       WAVE_FENCE();
       SPM(9);   // re-scoring job: row copy + hint table
       const int q2 = jb.q + 1 + jb.range * 64 + lane;
-      if (q2 < B) {
-        int scv = row_score(rr, pods(q2), a.pf, m, &tab);
-        const int xr = (a.dbg >> 20) & 3u;   // EXPERIMENT: repeat the re-scoring xr more times
-        for (int r = 0; r < xr; ++r) {
-          int qq = q2;
-          asm volatile("" : "+v"(qq));
-          scv = min(scv, (int)row_score(rr, pods(qq), a.pf, m, &tab));
-        }
-        dsc[q2 * SB + jb.slot] = (int16_t)scv;
-      }
+      if (q2 < B) dsc[q2 * SB + jb.slot] = (int16_t)row_score(rr, pods(q2), a.pf, m, &tab);
       WAVE_FENCE();
       int fin = 0;
       if (lane == 0) {
@@ -2119,10 +1797,6 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
     }
   }
   __syncthreads();
-  if (remote && tid == 0) {
-    g_st(a.help + HG_FIN, hep);   // the helpers stop
-    if ((a.dbg >> 22) & 1u) __hip_atomic_fetch_max(a.help + 5, (uint64_t)__builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
   // ---- a host cut ends the batch after its pod, but the other Reserve wave may have reserved a later decided pod
   // meanwhile: those Reserves are undone (newest first) before the write-back
   if (wv == 0 && s_hostcut && !s_err) {
@@ -2192,8 +1866,7 @@ static size_t spec_launch_bytes(int npods) {
 template <bool STAMPS, bool SPLIT>
 static void spec_launch(const CommitArgs& a, hipStream_t st) {
   const size_t bytes = spec_launch_bytes<STAMPS, SPLIT>(a.npods);
-  const int grid = SPLIT && a.help && a.nhelp > 0 ? 1 + a.nhelp : 1;   // + the re-scoring helpers (REMOTE)
-  hipLaunchKernelGGL((commit_spec_kernel<STAMPS, SPLIT>), dim3(grid), dim3(SP_THREADS), bytes, st, a);
+  hipLaunchKernelGGL((commit_spec_kernel<STAMPS, SPLIT>), dim3(1), dim3(SP_THREADS), bytes, st, a);
 }
 
 hipError_t launch_commit_spec(const CommitArgs& a, hipStream_t st) {

@@ -164,8 +164,6 @@ struct gs_ctx {
   PlacementDev* d_out = nullptr;
   int32_t* d_committed = nullptr;
   int32_t* d_tb = nullptr;          // speculative commit: tie-break records of the batch's pods
-  uint64_t* d_help = nullptr;       // speculative commit: the re-scoring helpers' job / result rings (help_bytes())
-  uint32_t help_epoch = 0;          // commit launches that used them (tags the rings' entries)
   RowStat* d_rowstat = nullptr;
   int32_t* d_sel = nullptr;
   uint32_t* d_stage_idx = nullptr;
@@ -855,7 +853,10 @@ int ready(gs_ctx* c) {
 
 double ev_ms(hipEvent_t a, hipEvent_t b) {
   float ms = 0;
-  if (hipEventElapsedTime(&ms, a, b) != hipSuccess) return 0;
+  if (hipEventElapsedTime(&ms, a, b) != hipSuccess) {
+    (void)hipGetLastError();   // (an event without timing: not sticky for the next launch's check)
+    return 0;
+  }
   return ms;
 }
 
@@ -1256,18 +1257,9 @@ CommitArgs commit_args(gs_ctx* c, int b) {
   // GS_SPEC_AHEAD=2 (experiments): the prep wave may run two pods ahead (bit 18)
   static const bool ahead2 = getenv("GS_SPEC_AHEAD") && getenv("GS_SPEC_AHEAD")[0] == '2';
   // GS_SPEC_SPLIT=3 (experiments): shared verification by the prep wave while it waits (bits 17 and 19)
-  static const uint32_t rsx = getenv("GS_RESCORE_X") ? (uint32_t)atoi(getenv("GS_RESCORE_X")) & 3u : 0u;
-  // GS_HELP_CHECK=1 (diagnostics): the receiver re-scores every helper job itself and counts mismatches (gs_destroy
-  // prints them)
-  static const uint32_t hchk = getenv("GS_HELP_CHECK") && getenv("GS_HELP_CHECK")[0] == '1' ? 1u << 22 : 0u;
   a.dbg = (nospec ? 1u : 0u) | prio | lag << 12 | (split >= 1 ? 1u << 16 : 0u) | (split >= 2 ? 1u << 17 : 0u) |
-          (ahead2 ? 1u << 18 : 0u) | (split >= 3 ? 1u << 19 : 0u) | rsx << 20 | hchk;
+          (ahead2 ? 1u << 18 : 0u) | (split >= 3 ? 1u << 19 : 0u);
   a.tb = c->d_tb;
-  // re-scoring on GS_RESCORE_HELPERS helper workgroups beside the split commit (default 2; 0: on the commit's CU)
-  static const int nhelp = getenv("GS_RESCORE_HELPERS") ? std::max(0, std::min(8, atoi(getenv("GS_RESCORE_HELPERS")))) : 0;
-  a.help = nhelp > 0 ? c->d_help : nullptr;
-  a.nhelp = nhelp;
-  a.help_epoch = ++c->help_epoch;
   a.xerr = c->nranks > 1 ? c->d_xerr : nullptr;
   return a;
 }
@@ -2138,6 +2130,12 @@ int gs_create(const gs_config* cfg, gs_ctx** out) {
   if ((e = hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming)) != hipSuccess) return bail("hipEventCreate", e);
   for (auto& ev : c->ev)
     if ((e = hipEventCreate(&ev)) != hipSuccess) return bail("hipEventCreate", e);
+  // GS_EV4_NT=1 (experiments): the commit-end event without timing (the levels interval then reads 0)
+  static const bool ev4_nt = getenv("GS_EV4_NT") && getenv("GS_EV4_NT")[0] == '1';
+  if (ev4_nt) {
+    (void)hipEventDestroy(c->ev[4]);
+    if ((e = hipEventCreateWithFlags(&c->ev[4], hipEventDisableTiming)) != hipSuccess) return bail("hipEventCreate", e);
+  }
   size_t np = c->npad;
   if ((e = hipMalloc(&c->d_i64, np * NUM_I64_COLS * 8)) != hipSuccess) return bail("hipMalloc mirror", e);
   if ((e = hipMalloc(&c->d_i32, np * NUM_I32_COLS * 4)) != hipSuccess) return bail("hipMalloc mirror", e);
@@ -2159,10 +2157,6 @@ int gs_create(const gs_config* cfg, gs_ctx** out) {
   if ((e = hipMalloc(&c->d_committed, COMMITTED_BYTES + sizeof(PlacementDev) * c->B)) != hipSuccess) return bail("hipMalloc", e);
   c->d_out = reinterpret_cast<PlacementDev*>(c->d_committed + COMMITTED_BYTES / 4);
   if ((e = hipMalloc(&c->d_tb, sizeof(int32_t) * TB_N * c->B)) != hipSuccess) return bail("hipMalloc", e);
-  // uncached: the rings are read and written by workgroups on different XCDs (gs_commit_spec.hip, REMOTE)
-  if ((e = hipExtMallocWithFlags(reinterpret_cast<void**>(&c->d_help), help_bytes(), hipDeviceMallocUncached)) != hipSuccess)
-    return bail("hipExtMallocWithFlags", e);
-  if ((e = hipMemset(c->d_help, 0, help_bytes())) != hipSuccess) return bail("hipMemset", e);
   if ((e = hipMalloc(&c->d_rowstat, sizeof(RowStat) * (1 + MAX_RANKS))) != hipSuccess) return bail("hipMalloc", e);
   if ((e = hipMalloc(&c->d_sel, 4 * (1 + MAX_RANKS))) != hipSuccess) return bail("hipMalloc", e);
   c->stage_cap = std::min<uint32_t>(c->N, 65536);
@@ -2202,8 +2196,9 @@ int gs_create(const gs_config* cfg, gs_ctx** out) {
     if ((e = hipHostMalloc(&s1.h_committed, COMMITTED_BYTES + sizeof(PlacementDev) * c->B, hipHostMallocDefault)) != hipSuccess)
       return bail("hipHostMalloc", e);
     s1.h_out = reinterpret_cast<PlacementDev*>(s1.h_committed + COMMITTED_BYTES / 4);
-    for (auto& ev : s1.ev)
-      if ((e = hipEventCreate(&ev)) != hipSuccess) return bail("hipEventCreate", e);
+    for (int i = 0; i < 6; ++i)
+      if ((e = hipEventCreateWithFlags(&s1.ev[i], i == 4 && ev4_nt ? hipEventDisableTiming : 0)) != hipSuccess)
+        return bail("hipEventCreate", e);
     c->cand_overlap = !(getenv("GS_CAND_OVERLAP") && getenv("GS_CAND_OVERLAP")[0] == '0');
     if (c->cand_overlap)
       for (auto& sl : c->slot) {
@@ -2389,24 +2384,10 @@ int gs_destroy(gs_ctx* c) {
     for (auto& ev : s1.ev)
       if (ev) (void)hipEventDestroy(ev);
   }
-  if (c->d_help && getenv("GS_HELP_CHECK") && getenv("GS_HELP_CHECK")[0] == '1') {
-    uint64_t w[16] = {};
-    if (hipMemcpy(w, c->d_help, sizeof w, hipMemcpyDeviceToHost) == hipSuccess) {
-      fprintf(stderr, "gpuscore help check: block 0 end %llu, last helper exit %llu (x10 ns); helper waves ended by the end "
-                      "word %llu, by the bound %llu; jobs taken %llu; published rows differing %llu (first word %llu: %llx vs %llx)\n",
-              (unsigned long long)w[5], (unsigned long long)w[6], (unsigned long long)w[7], (unsigned long long)w[8],
-              (unsigned long long)w[9], (unsigned long long)w[11], (unsigned long long)w[12], (unsigned long long)w[13],
-              (unsigned long long)w[14]);
-      fprintf(stderr, "gpuscore help check: %llu of %llu helper jobs differ; first q %llu slot %llu range %llu lane %llu helper %d local %d\n",
-              (unsigned long long)w[2], (unsigned long long)w[3], (unsigned long long)(w[4] & 0xff),
-              (unsigned long long)((w[4] >> 8) & 0xff), (unsigned long long)((w[4] >> 16) & 0xff),
-              (unsigned long long)((w[4] >> 24) & 0xff), (int)(int16_t)(w[4] >> 32), (int)(int16_t)(w[4] >> 48));
-    }
-  }
   void* dev[] = {c->d_xerr, c->d_xsmall,
                  c->d_i64, c->d_i32, c->d_pods, c->d_S, c->d_xchg_send, c->d_xchg_recv, c->d_xmerged,
                  c->d_committed, c->d_rowstat, c->d_sel, c->d_stage_idx, c->d_stage_rows, c->d_numa_idx,
-                 c->d_topos, c->d_aff, c->d_tb, c->d_help};
+                 c->d_topos, c->d_aff, c->d_tb};
   for (void* p : dev)
     if (p) (void)hipFree(p);
   void* host[] = {c->h_xsmall, c->h_pods, c->h_committed, c->h_stage_idx, c->h_stage_rows, c->h_xchg_send,

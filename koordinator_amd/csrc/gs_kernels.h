@@ -111,13 +111,7 @@ struct CommitArgs {
   uint32_t dbg;              // diagnostics: bit 0 = the speculative commit waits for every pending row (no speculation)
   int32_t* tb;               // [npods x TB_N] selectHost tie-break records of each pod (speculative commit scratch)
   const int32_t* xerr;       // several shards: nonzero = the all-gathered blocks' exchange tags disagree (merge_levels)
-  // Re-scoring on helper workgroups (one shard, split pipeline): nhelp workgroups beside the commit's, on other CUs,
-  // take the re-scoring jobs through the rings at `help` (help_bytes()); help_epoch tags this launch's ring entries
-  uint64_t* help;
-  uint32_t help_epoch;
-  int32_t nhelp;
 };
-size_t help_bytes();
 // tiebreak_position(seed, seq, T) as a lookup: entries 0..TB_N-2 are the positions the reservoir walk visits
 // (ascending, independent of T; INT32_MAX past the walk's end), entry TB_N-1 the largest T the entries decide
 constexpr int TB_N = 32;

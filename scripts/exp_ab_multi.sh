@@ -8,7 +8,7 @@ IFS='|' read -ra VARS <<< "${AB_VARIANTS:--}"
 for k in $(seq 1 ${AB_REPS:-2}); do
   for v in "${VARS[@]}"; do
     [ "$v" = "-" ] && v=""
-    env $v timeout -k 10 300 python -u bench.py --steps ${AB_STEPS:-20} --warmup 3 --no-cpu-baseline ${BENCH_ARGS} > gpurun_out/ab.json 2> gpurun_out/ab.err
+    env $v timeout -k 10 300 python -u bench.py --steps ${AB_STEPS:-20} --warmup 3 --no-cpu-baseline --no-extras ${BENCH_ARGS} > gpurun_out/ab.json 2> gpurun_out/ab.err
     rc=$?; [ $rc -eq 0 ] || { echo "rc=$rc"; tail -5 gpurun_out/ab.err; exit $rc; }
     python -c "
 import json; d=json.loads(open('gpurun_out/ab.json').read().strip().splitlines()[-1])

@@ -9,4 +9,4 @@ timeout -k 10 ${TEST_LIMIT:-600} python -u -m pytest ${PYTEST_ARGS:-tests/test_g
 rc=$?; echo "PYTEST rc=$rc"; tail -3 gpurun_out/r6_iter_tests.log
 grep -E "FAILED|Error" gpurun_out/r6_iter_tests.log | head -10
 [ $rc -eq 0 ] || exit $rc
-[ -n "$AB_VARIANTS" ] && bash scripts/exp_ab_multi.sh
+if [ -n "$AB_VARIANTS" ]; then bash scripts/exp_ab_multi.sh; fi

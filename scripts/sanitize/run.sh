@@ -39,6 +39,23 @@ HSAN="-Xarch_host -fsanitize=address -Xarch_host -fsanitize=undefined -Xarch_hos
 $HIPCC -x hip --offload-host-only -std=c++17 -O1 -g $HSAN -ffp-contract=off -fno-omit-frame-pointer \
     -o $OUT/san_merge san_merge.cpp -x c++ $ROOT/oracle/numa.cpp $ROOT/oracle/oracle.cpp -pthread
 
+echo "== build san_merge_msan (MemorySanitizer: uninitialized reads, which ASan + UBSan do not see; linked without the"
+echo "   HIP runtime, whose uninstrumented initialisers MSan would report; both the library's copy form of the merge and"
+echo "   the round-4 pointer-select form, GS_MERGE_PTR_SELECT)"
+MSAN="-fsanitize=memory -fsanitize-memory-track-origins=2 -fno-sanitize-recover=all"
+XMSAN="-Xarch_host -fsanitize=memory -Xarch_host -fsanitize-memory-track-origins=2 -Xarch_host -fno-sanitize-recover=all"
+for f in numa oracle; do
+  /opt/rocm/llvm/bin/clang++ -std=c++17 -O1 -g $MSAN -ffp-contract=off -fno-omit-frame-pointer -c -o $OUT/${f}_msan.o $ROOT/oracle/$f.cpp
+done
+for v in copy ptr; do
+  D=""; [ $v = ptr ] && D="-DGS_MERGE_PTR_SELECT"
+  $HIPCC -x hip --offload-host-only $D -std=c++17 -O1 -g $XMSAN -ffp-contract=off -fno-omit-frame-pointer \
+      -c -o $OUT/san_merge_msan_$v.o san_merge.cpp
+  /opt/rocm/llvm/bin/clang++ -fsanitize=memory -o $OUT/san_merge_msan_$v $OUT/san_merge_msan_$v.o $OUT/numa_msan.o \
+      $OUT/oracle_msan.o -pthread
+done
+export MSAN_OPTIONS=halt_on_error=1
+
 echo "== run"
 for w in c2 c3 c5; do $OUT/san_host replay $OUT/$w.bin "$(cat $OUT/$w.bin.expect)"; done
 $OUT/san_host ingest $OUT/ingest.corpus
@@ -46,4 +63,6 @@ $OUT/san_host quota 1 3000
 $OUT/san_host gang 1 1500
 for seed in 1 2 3 4; do $OUT/san_host cpuset $seed 40000; done
 for seed in 1 2; do $OUT/san_merge $seed 100000; done
+for seed in 1 2; do $OUT/san_merge_msan_copy $seed 100000; done
+$OUT/san_merge_msan_ptr 3 100000
 echo "SANITIZERS CLEAN"
