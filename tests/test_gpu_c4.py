@@ -39,6 +39,11 @@ def _worker(rank: int, world: int, port: int, numa: bool, pods: int, q):
     import sys
     faulthandler.dump_traceback_later(100, exit=True, file=sys.stderr)   # a stuck rank names where it is
     os.environ.setdefault("GS_WATCHDOG_S", "10")   # ... and the library names the host wait it is blocked in
+    # Several processes on the box's one GPU (a rehearsal; production runs one process per GPU): two hardware queues
+    # per rank process, so that the ranks plus the parent test process do not oversubscribe the GPU's hardware queues.
+    # Oversubscribed, the scheduler time-slices the processes' queues and a rank waited ~10 s at a time for its queue
+    # (reproduced with 4 HIP queues per process, gone with 2). Read by HIP at its initialisation below.
+    os.environ["GPU_MAX_HW_QUEUES"] = "2"
     try:
         import torch
         import torch.distributed as dist

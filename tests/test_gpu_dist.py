@@ -23,6 +23,7 @@ def _cluster(numa: bool):
 
 
 def _worker(rank: int, port: int, numa: bool, q, skew: str = ""):
+    os.environ["GPU_MAX_HW_QUEUES"] = "2"   # ranks sharing the box's one GPU: no hardware-queue oversubscription (test_gpu_c4)
     try:
         if skew:   # GS_DEBUG_XCHG_SKEW: rank:batch skips one exchange sequence number there
             os.environ["GS_DEBUG_XCHG_SKEW"] = skew
