@@ -214,7 +214,18 @@ struct gs_ctx {
   int max_score = 0;
   // sharding
   int nranks = 1, rank = 0;
-  uint32_t n0 = 0, n1 = 0;
+  uint32_t n0 = 0, n1 = 0;          // the node range the levels, fixes and commit see (all nodes: one rank, scores)
+  // Several ranks exchange either their score rows (sgather, the default: every rank evaluates its shard [e0, e1), the
+  // all-gather makes the full rows, and the one-shard pipeline runs on every rank) or their candidate levels
+  // (GS_XCHG=levels: n0/n1 = the shard, merged level lists, the multi-shard commit)
+  bool sgather = false;
+  uint32_t e0 = 0, e1 = 0;          // the node range this rank evaluates
+  uint32_t sx_per = 0, sx_pld = 0;  // nodes per shard, the block's row stride
+  size_t sx_bytes = 0;              // one rank's score block (tag included)
+  uint8_t* d_sx_send = nullptr;     // [B x pld int16 | B x pld u8 | ... | XTag]
+  uint8_t* d_sx_recv = nullptr;     // R blocks
+  uint8_t* h_sx_send = nullptr;     // host-callback transport
+  uint8_t* h_sx_recv = nullptr;
   uint32_t n_valid = 0;   // nodes upserted at least once (ready())
   ncclComm_t comm = nullptr;
   gs_allgather_fn cb = nullptr;
@@ -880,7 +891,8 @@ void flush_exchange_times(gs_ctx* c) {
 constexpr size_t XSMALL = 64;   // small exchange block: payload <= 32 B, XTag at 32
 
 const char* xsite_name(uint32_t s) {
-  return s == XSITE_LEVELS ? "levels" : s == XSITE_ROWSTAT ? "row stats" : s == XSITE_SELECT ? "selection" : "?";
+  return s == XSITE_LEVELS ? "levels" : s == XSITE_ROWSTAT ? "row stats" : s == XSITE_SELECT ? "selection"
+       : s == XSITE_SCORES ? "score rows" : "?";
 }
 
 // The R received blocks' tags against the tag this rank sent: every rank checks all of them, so a divergence fails
@@ -903,14 +915,21 @@ int check_tags(gs_ctx* c, const uint8_t* blocks, size_t bytes, const XTag& mine)
 // One all-gather of `bytes`-byte blocks (each ending in an XTag, filled here) from d_send into R blocks at d_recv.
 // RCCL: stream-ordered, the tag written on the stream before the collective; the receiver checks the tags (the level
 // blocks on the device in merge_levels_kernel, the small ones on the host). Callback: host-synchronous, checked here.
-int exchange(gs_ctx* c, uint32_t site, uint8_t* d_send, uint8_t* d_recv, size_t bytes, XTag* sent = nullptr) {
+int exchange(gs_ctx* c, uint32_t site, uint8_t* d_send, uint8_t* d_recv, size_t bytes, XTag* sent = nullptr,
+             hipStream_t xs = nullptr) {
   auto t0 = std::chrono::steady_clock::now();
+  if (!xs) xs = c->st;
+  // the host-callback transport's staging: the score blocks have their own buffers
+  uint8_t* h_send = site == XSITE_SCORES ? c->h_sx_send : c->h_xchg_send;
+  uint8_t* h_recv = site == XSITE_SCORES ? c->h_sx_recv : c->h_xchg_recv;
+  const size_t h_cap = site == XSITE_SCORES ? c->sx_bytes : c->xchg_bytes;
   if (bytes < sizeof(XTag) || bytes % 8) return fail(c, GS_EINVAL, "exchange block of %zu bytes", bytes);
   XTag tag{XTAG_MAGIC, site, ++c->xseq, c->xbatch, c->rank, (uint32_t)bytes};
-  if (c->rank == c->dbg_xskew_rank && c->xbatch == c->dbg_xskew_batch && site == XSITE_LEVELS) tag.seq = ++c->xseq;
+  if (c->rank == c->dbg_xskew_rank && c->xbatch == c->dbg_xskew_batch && (site == XSITE_LEVELS || site == XSITE_SCORES))
+    tag.seq = ++c->xseq;
   if (sent) *sent = tag;
   if (c->comm) {
-    HIP_TRY(c, launch_write_tag(d_send + bytes - sizeof(XTag), tag, c->st));
+    HIP_TRY(c, launch_write_tag(d_send + bytes - sizeof(XTag), tag, xs));
     if (c->x_pending * 2 + 2 > (int)c->x_ev.size()) {
       for (int k = 0; k < 2; ++k) {
         hipEvent_t ev;
@@ -918,16 +937,16 @@ int exchange(gs_ctx* c, uint32_t site, uint8_t* d_send, uint8_t* d_recv, size_t 
         c->x_ev.push_back(ev);
       }
     }
-    HIP_TRY(c, hipEventRecord(c->x_ev[2 * c->x_pending], c->st));
-    ncclResult_t r = ncclAllGather(d_send, d_recv, bytes, ncclUint8, c->comm, c->st);
+    HIP_TRY(c, hipEventRecord(c->x_ev[2 * c->x_pending], xs));
+    ncclResult_t r = ncclAllGather(d_send, d_recv, bytes, ncclUint8, c->comm, xs);
     if (r != ncclSuccess) return fail(c, GS_ECOMM, "ncclAllGather: %s", ncclGetErrorString(r));
-    HIP_TRY(c, hipEventRecord(c->x_ev[2 * c->x_pending + 1], c->st));
+    HIP_TRY(c, hipEventRecord(c->x_ev[2 * c->x_pending + 1], xs));
     ++c->x_pending;
     return GS_OK;
   } else if (c->lg) {
     gs_local_group& g = *c->lg;
     static const double limit = getenv("GS_LOCAL_WAIT_S") ? atof(getenv("GS_LOCAL_WAIT_S")) : 60.0;
-    HIP_TRY(c, launch_write_tag(d_send + bytes - sizeof(XTag), tag, c->st));
+    HIP_TRY(c, launch_write_tag(d_send + bytes - sizeof(XTag), tag, xs));
     if (c->x_pending * 2 + 2 > (int)c->x_ev.size()) {
       for (int k = 0; k < 2; ++k) {
         hipEvent_t ev;
@@ -935,8 +954,8 @@ int exchange(gs_ctx* c, uint32_t site, uint8_t* d_send, uint8_t* d_recv, size_t 
         c->x_ev.push_back(ev);
       }
     }
-    HIP_TRY(c, hipEventRecord(c->x_ev[2 * c->x_pending], c->st));
-    HIP_TRY(c, hipEventRecord(c->lg_ready, c->st));
+    HIP_TRY(c, hipEventRecord(c->x_ev[2 * c->x_pending], xs));
+    HIP_TRY(c, hipEventRecord(c->lg_ready, xs));
     {
       std::lock_guard<std::mutex> lk(g.mu);
       g.send[c->rank] = d_send;
@@ -955,10 +974,10 @@ int exchange(gs_ctx* c, uint32_t site, uint8_t* d_send, uint8_t* d_recv, size_t 
     for (int s = 0; s < c->nranks; ++s) same = same && g.bytes[s] == bytes;
     if (same)
       for (int s = 0; s < c->nranks; ++s) {
-        HIP_TRY(c, hipStreamWaitEvent(c->st, g.ready[s], 0));
-        HIP_TRY(c, hipMemcpyAsync(d_recv + (size_t)s * bytes, g.send[s], bytes, hipMemcpyDeviceToDevice, c->st));
+        HIP_TRY(c, hipStreamWaitEvent(xs, g.ready[s], 0));
+        HIP_TRY(c, hipMemcpyAsync(d_recv + (size_t)s * bytes, g.send[s], bytes, hipMemcpyDeviceToDevice, xs));
       }
-    HIP_TRY(c, hipEventRecord(c->lg_done, c->st));
+    HIP_TRY(c, hipEventRecord(c->lg_done, xs));
     {
       std::lock_guard<std::mutex> lk(g.mu);
       g.done[c->rank] = c->lg_done;
@@ -973,21 +992,22 @@ int exchange(gs_ctx* c, uint32_t site, uint8_t* d_send, uint8_t* d_recv, size_t 
     if (!same) return fail(c, GS_ECOMM, "local transport: the ranks' blocks of exchange %llu differ in size",
                            (unsigned long long)tag.seq);
     for (int s = 0; s < c->nranks; ++s)
-      if (s != c->rank) HIP_TRY(c, hipStreamWaitEvent(c->st, g.done[s], 0));
-    HIP_TRY(c, hipEventRecord(c->x_ev[2 * c->x_pending + 1], c->st));
+      if (s != c->rank) HIP_TRY(c, hipStreamWaitEvent(xs, g.done[s], 0));
+    HIP_TRY(c, hipEventRecord(c->x_ev[2 * c->x_pending + 1], xs));
     ++c->x_pending;
     return GS_OK;
   } else if (c->cb) {
-    if (bytes > c->xchg_bytes) return fail(c, GS_EINVAL, "exchange payload too large");
-    Where w_(c, site == XSITE_LEVELS ? "exchange (levels): stream before the callback"
-                                     : "exchange (small): stream before the callback");
-    HIP_TRY(c, hipMemcpyAsync(c->h_xchg_send, d_send, bytes - sizeof(XTag), hipMemcpyDeviceToHost, c->st));
-    HIP_TRY(c, host_wait_stream(c->st));
+    if (bytes > h_cap || !h_send) return fail(c, GS_EINVAL, "exchange payload too large");
+    Where w_(c, site == XSITE_LEVELS   ? "exchange (levels): stream before the callback"
+                : site == XSITE_SCORES ? "exchange (score rows): stream before the callback"
+                                       : "exchange (small): stream before the callback");
+    HIP_TRY(c, hipMemcpyAsync(h_send, d_send, bytes - sizeof(XTag), hipMemcpyDeviceToHost, xs));
+    HIP_TRY(c, host_wait_stream(xs));
     c->where.store("exchange: allgather callback");
-    std::memcpy(c->h_xchg_send + bytes - sizeof(XTag), &tag, sizeof tag);
-    if (c->cb(c->cb_user, c->h_xchg_send, c->h_xchg_recv, bytes) != 0) return fail(c, GS_ECOMM, "allgather callback failed");
-    if (int rc = check_tags(c, c->h_xchg_recv, bytes, tag)) return rc;
-    HIP_TRY(c, hipMemcpyAsync(d_recv, c->h_xchg_recv, bytes * c->nranks, hipMemcpyHostToDevice, c->st));
+    std::memcpy(h_send + bytes - sizeof(XTag), &tag, sizeof tag);
+    if (c->cb(c->cb_user, h_send, h_recv, bytes) != 0) return fail(c, GS_ECOMM, "allgather callback failed");
+    if (int rc = check_tags(c, h_recv, bytes, tag)) return rc;
+    HIP_TRY(c, hipMemcpyAsync(d_recv, h_recv, bytes * c->nranks, hipMemcpyHostToDevice, xs));
   } else {
     return fail(c, GS_ESTATE, "multi-rank context without a communicator");
   }
@@ -1147,11 +1167,20 @@ int compute_profile(gs_ctx* c) {
 
 void set_shard(gs_ctx* c) {
   uint32_t per = (c->N + c->nranks - 1) / c->nranks;
-  c->n0 = std::min(c->N, per * (uint32_t)c->rank);
-  c->n1 = std::min(c->N, c->n0 + per);
-  c->stats.shard_begin = c->n0;
-  c->stats.shard_end = c->n1;
+  c->e0 = std::min(c->N, per * (uint32_t)c->rank);
+  c->e1 = std::min(c->N, c->e0 + per);
+  const bool levels = getenv("GS_XCHG") && std::strcmp(getenv("GS_XCHG"), "levels") == 0;   // (read per comm init)
+  c->sgather = c->nranks > 1 && !levels;
+  c->n0 = c->sgather ? 0 : c->e0;
+  c->n1 = c->sgather ? c->N : c->e1;
+  c->sx_per = per;
+  c->sx_pld = (per + 1023) / 1024 * 1024;
+  c->stats.shard_begin = c->e0;
+  c->stats.shard_end = c->e1;
 }
+
+// ranks whose candidate levels the commit merges: 1 unless the ranks exchange level lists (GS_XCHG=levels)
+int lvl_ranks(const gs_ctx* c) { return c->sgather ? 1 : c->nranks; }
 
 // one rank's exchange block: [B x lstride listed node ids | B LevelHdr | B LevelExt | ... | XTag], padded to 256 B (the
 // tag in the block's last 32 bytes)
@@ -1164,7 +1193,8 @@ size_t xchg_block_bytes(int B, int lstride) {
 int alloc_exchange(gs_ctx* c) {
   // the speculative commit merges the shards' lists: XCAP listed nodes per (pod, shard) are enough for a pod at batch
   // position k (k + 1 per shard), and the all-gathered block is 8x smaller; the other kernels read LCAP-wide blocks
-  c->lstride = commit_spec_selected(c->window_k) ? XCAP : LCAP;
+  // (score rows: every rank runs the one-shard pipeline over all nodes, LCAP-wide local lists)
+  c->lstride = !c->sgather && commit_spec_selected(c->window_k) ? XCAP : LCAP;
   c->xchg_bytes = xchg_block_bytes(c->B, c->lstride);
   if (c->d_xchg_recv) { (void)hipFree(c->d_xchg_recv); c->d_xchg_recv = nullptr; }
   if (c->h_xchg_recv) { (void)hipHostFree(c->h_xchg_recv); c->h_xchg_recv = nullptr; }
@@ -1172,8 +1202,22 @@ int alloc_exchange(gs_ctx* c) {
   HIP_TRY(c, hipHostMalloc(&c->h_xchg_recv, c->xchg_bytes * c->nranks + 64, hipHostMallocDefault));
   if (c->d_xmerged) { (void)hipFree(c->d_xmerged); c->d_xmerged = nullptr; }
   HIP_TRY(c, hipMalloc(&c->d_xmerged, xchg_block_bytes(c->B, LCAP) + 64));
-  if (!c->d_xerr) HIP_TRY(c, hipMalloc(&c->d_xerr, XERR_BYTES));
-  HIP_TRY(c, hipMemset(c->d_xerr, 0, XERR_BYTES));
+  if (!c->d_xerr) HIP_TRY(c, hipMalloc(&c->d_xerr, 2 * XERR_BYTES));   // one per batch slot (score rows)
+  HIP_TRY(c, hipMemset(c->d_xerr, 0, 2 * XERR_BYTES));
+  if (c->d_sx_send) { (void)hipFree(c->d_sx_send); c->d_sx_send = nullptr; }
+  if (c->d_sx_recv) { (void)hipFree(c->d_sx_recv); c->d_sx_recv = nullptr; }
+  if (c->h_sx_send) { (void)hipHostFree(c->h_sx_send); c->h_sx_send = nullptr; }
+  if (c->h_sx_recv) { (void)hipHostFree(c->h_sx_recv); c->h_sx_recv = nullptr; }
+  c->sx_bytes = 0;
+  if (c->sgather) {
+    c->sx_bytes = ((size_t)c->B * c->sx_pld * 3 + sizeof(XTag) + 255) / 256 * 256;
+    HIP_TRY(c, hipMalloc(&c->d_sx_send, c->sx_bytes * 2));               // one per batch slot
+    HIP_TRY(c, hipMalloc(&c->d_sx_recv, c->sx_bytes * c->nranks * 2));
+    if (c->cb) {
+      HIP_TRY(c, hipHostMalloc(&c->h_sx_send, c->sx_bytes, hipHostMallocDefault));
+      HIP_TRY(c, hipHostMalloc(&c->h_sx_recv, c->sx_bytes * c->nranks, hipHostMallocDefault));
+    }
+  }
   if (!c->d_xsmall) HIP_TRY(c, hipMalloc(&c->d_xsmall, XSMALL * (1 + MAX_RANKS)));
   if (!c->h_xsmall) HIP_TRY(c, hipHostMalloc(&c->h_xsmall, XSMALL * MAX_RANKS, hipHostMallocDefault));
   if (const char* sk = getenv("GS_DEBUG_XCHG_SKEW")) {   // "rank:batch" (tests of the sequence check)
@@ -1208,12 +1252,12 @@ constexpr size_t COMMITTED_BYTES = 32;   // committed[0..7] (the commit kernels 
 // two queue hops per batch.
 bool direct_batch(const gs_ctx* c, int b, bool speculative) {
   static const int max_b = getenv("GS_DIRECT_B") ? atoi(getenv("GS_DIRECT_B")) : 32;
-  return !speculative && b <= max_b && c->nranks == 1;
+  return !speculative && b <= max_b && lvl_ranks(c) == 1;
 }
 
 bool cand_overlapped(const gs_ctx* c) {
   static const bool separate = getenv("GS_FUSED_PATCH") && getenv("GS_FUSED_PATCH")[0] == '0';
-  return c->cand_overlap && c->nranks == 1 && !c->window_k && c->d_lst && !separate;
+  return c->cand_overlap && lvl_ranks(c) == 1 && !c->window_k && c->d_lst && !separate;
 }
 
 CommitArgs commit_args(gs_ctx* c, int b) {
@@ -1222,10 +1266,10 @@ CommitArgs commit_args(gs_ctx* c, int b) {
   a.pods = c->d_pods;
   a.seq = c->d_seq;
   a.npods = b;
-  a.nranks = c->nranks;
-  a.shard_size = (c->N + c->nranks - 1) / c->nranks;
+  a.nranks = lvl_ranks(c);
+  a.shard_size = (c->N + a.nranks - 1) / a.nranks;
   // several ranks: the speculative commit reads the merged levels, the pipelined / lockstep kernels every rank block
-  a.xbase = c->nranks == 1 ? (cand_overlapped(c) ? c->d_lst : c->d_xchg_send)
+  a.xbase = a.nranks == 1 ? (cand_overlapped(c) ? c->d_lst : c->d_xchg_send)
                             : commit_spec_selected(c->window_k) ? c->d_xmerged : c->d_xchg_recv;
   a.xblock = c->xchg_bytes;
   a.bmax = c->B;
@@ -1240,7 +1284,7 @@ CommitArgs commit_args(gs_ctx* c, int b) {
   a.ld = c->ld;
   a.own0 = c->n0;
   a.own1 = c->n1;
-  a.S = c->nranks == 1 ? c->d_S : nullptr;
+  a.S = a.nranks == 1 ? c->d_S : nullptr;
   a.S_own = c->d_S;
   a.window_k = c->window_k;
   a.start = c->next_start;
@@ -1260,7 +1304,8 @@ CommitArgs commit_args(gs_ctx* c, int b) {
   a.dbg = (nospec ? 1u : 0u) | prio | lag << 12 | (split >= 1 ? 1u << 16 : 0u) | (split >= 2 ? 1u << 17 : 0u) |
           (ahead2 ? 1u << 18 : 0u) | (split >= 3 ? 1u << 19 : 0u);
   a.tb = c->d_tb;
-  a.xerr = c->nranks > 1 ? c->d_xerr : nullptr;
+  // (score rows: the batch slot's verdict of unpack_scores_kernel; levels: merge_levels_kernel's)
+  a.xerr = c->sgather ? c->d_xerr + (XERR_BYTES / 4) * c->cur_slot : c->nranks > 1 ? c->d_xerr : nullptr;
   return a;
 }
 
@@ -1280,8 +1325,8 @@ int launch_batch(gs_ctx* c, int b, const int32_t* prev, const PlacementDev* prev
   for (int i = 0; i < b; ++i) prod_cols |= (c->h_pods[i].flags & PF_PROD_SCORE) ? 1 : 0;
   uint32_t len = c->n1 - c->n0;
   if (c->numa_on && c->numa_idx_stale) {
-    std::vector<uint32_t> idx;
-    for (uint32_t n = c->n0; n < c->n1; ++n)
+    std::vector<uint32_t> idx;   // the policy nodes this rank evaluates
+    for (uint32_t n = c->e0; n < c->e1; ++n)
       if (c->numa[n].cfg.numa_topology_policy != GS_NUMA_POLICY_NONE) idx.push_back(n);
     if (c->d_numa_idx) {
       HIP_TRY(c, host_wait_stream(c->st));
@@ -1312,9 +1357,25 @@ int launch_batch(gs_ctx* c, int b, const int32_t* prev, const PlacementDev* prev
   const bool direct = direct_batch(c, b, prev != nullptr);
   hipStream_t se = direct ? c->st : c->st_ev;
   HIP_TRY(c, hipEventRecord(c->ev[0], se));
-  HIP_TRY(c, launch_eval(c->mv, c->d_pods, b, c->pf, c->n0, c->n1, c->d_S, c->ld, prod_cols, c->d_numa_idx, c->numa_n,
-                         c->d_aff, se, c->st2, c->ev_fork, c->ev_join, c->slab_mv.i64 ? &c->slab_mv : nullptr));
-  HIP_TRY(c, hipEventRecord(c->ev[1], se));
+  if (c->sgather) {
+    // several ranks, score rows: this rank's shard into its block of the all-gather (rows of sx_pld entries), then the
+    // R blocks into the full-width rows S / aff: every rank continues with the one-shard pipeline over all nodes
+    const uint32_t pld = c->sx_pld;
+    uint8_t* blk = c->d_sx_send + c->sx_bytes * c->cur_slot;
+    uint8_t* rcv = c->d_sx_recv + c->sx_bytes * c->nranks * c->cur_slot;
+    HIP_TRY(c, launch_eval(c->mv, c->d_pods, b, c->pf, c->e0, c->e1, reinterpret_cast<int16_t*>(blk), pld, prod_cols,
+                           c->d_numa_idx, c->numa_n, blk + (size_t)b * pld * 2, se, c->st2, c->ev_fork, c->ev_join,
+                           c->slab_mv.i64 ? &c->slab_mv : nullptr));
+    HIP_TRY(c, hipEventRecord(c->ev[1], se));
+    const size_t bytes = ((size_t)b * pld * 3 + sizeof(XTag) + 255) / 256 * 256;
+    if (int rc = exchange(c, XSITE_SCORES, blk, rcv, bytes, nullptr, se)) return rc;
+    HIP_TRY(c, launch_unpack_scores(rcv, bytes, c->nranks, b, c->sx_per, pld, c->N, c->d_S, c->d_aff, c->ld,
+                                    c->d_xerr + (XERR_BYTES / 4) * c->cur_slot, se));
+  } else {
+    HIP_TRY(c, launch_eval(c->mv, c->d_pods, b, c->pf, c->n0, c->n1, c->d_S, c->ld, prod_cols, c->d_numa_idx, c->numa_n,
+                           c->d_aff, se, c->st2, c->ev_fork, c->ev_join, c->slab_mv.i64 ? &c->slab_mv : nullptr));
+    HIP_TRY(c, hipEventRecord(c->ev[1], se));
+  }
   const bool fix = ovl && prev && prev_b > 0;
   if (ovl) {
     // levels on st_ev beside the previous batch's commit: the rows it lands on are stale here (listed with a margin of
@@ -1352,7 +1413,7 @@ int launch_batch(gs_ctx* c, int b, const int32_t* prev, const PlacementDev* prev
   }
   // no timing markers between the levels and the commit kernel (each one held the commit's dispatch ~13 us): the
   // commit's duration comes from the kernel itself (committed[4]), the levels' interval is the rest up to ev[4]
-  if (c->nranks > 1) {
+  if (lvl_ranks(c) > 1) {
     int rc = exchange(c, XSITE_LEVELS, c->d_xchg_send, c->d_xchg_recv, c->xchg_bytes);
     if (rc) return rc;
     if (!commit_spec_selected(c->window_k)) return fail(c, GS_EUNSUPPORTED, "several ranks need the speculative commit");
@@ -1403,7 +1464,7 @@ int finish_batch(gs_ctx* c, int b, bool clobbered, int* committed_out) {
     c->stats.cand_ms += std::max(0.0, ev_ms(c->ev[1], c->ev[4]) - cm);
   }
   c->stats.eval_launches += 1;
-  c->stats.eval_pairs += (uint64_t)b * len;
+  c->stats.eval_pairs += (uint64_t)b * (c->e1 - c->e0);
   c->stats.batches += 1;
   int committed = c->h_committed[0];
   if (committed < 0) return fail(c, GS_ESTATE, "commit pass of a batch was voided unexpectedly");
@@ -1411,12 +1472,14 @@ int finish_batch(gs_ctx* c, int b, bool clobbered, int* committed_out) {
     // the first mismatching exchange's tags, as merge_levels_kernel kept them
     std::vector<uint8_t> xe(XERR_BYTES);
     HIP_TRY(c, host_wait_stream(c->st));
-    HIP_TRY(c, hipMemcpy(xe.data(), c->d_xerr, xe.size(), hipMemcpyDeviceToHost));
+    HIP_TRY(c, hipMemcpy(xe.data(), c->d_xerr + (c->sgather ? (XERR_BYTES / 4) * c->cur_slot : 0), xe.size(),
+                         hipMemcpyDeviceToHost));
     const uint8_t* tags = xe.data() + 4 * XERR_TAGS;
     XTag mine;
     std::memcpy(&mine, tags + (size_t)c->rank * sizeof(XTag), sizeof mine);
     if (int rc = check_tags(c, tags, sizeof(XTag), mine)) return rc;
-    return fail(c, GS_ECOMM, "exchange sequence diverged at a level exchange (device check)");
+    return fail(c, GS_ECOMM, "exchange sequence diverged at a %s exchange (device check)",
+                c->sgather ? "score-row" : "level");
   }
   if (c->h_committed[3])
     return fail(c, GS_EDEVICE, "commit kernel: a pipeline wait expired (internal error, site %d)", c->h_committed[3]);
@@ -1430,8 +1493,9 @@ int finish_batch(gs_ctx* c, int b, bool clobbered, int* committed_out) {
     CommitArgs a = commit_args(c, b);
     // exact full-row path for pod 0: (max, ties, feasible) of every shard's row, global selection
     HIP_TRY(c, launch_row_stats(c->d_S, len, c->d_rowstat, c->st));
-    std::vector<RowStat> rs(c->nranks);
-    if (c->nranks > 1) {
+    const int lr = lvl_ranks(c);
+    std::vector<RowStat> rs(lr);
+    if (lr > 1) {
       int rc = exchange_small(c, XSITE_ROWSTAT, c->d_rowstat, sizeof(RowStat), rs.data());
       if (rc) return rc;
     } else {
@@ -1453,19 +1517,19 @@ int finish_batch(gs_ctx* c, int b, bool clobbered, int* committed_out) {
     int64_t jstar = host_tiebreak_position(c->cfg.seed, c->h_seq[0], T);
     int owner = -1;
     int64_t before = 0;
-    for (int r = 0; r < c->nranks; ++r) {
+    for (int r = 0; r < lr; ++r) {
       if (rs[r].max_score != M) continue;
       if (jstar <= before + rs[r].ties) { owner = r; break; }
       before += rs[r].ties;
     }
     int32_t winner = -1;
-    if (owner == c->rank) {
+    if (owner == (lr > 1 ? c->rank : 0)) {
       HIP_TRY(c, launch_row_select(c->d_S, len, M, jstar - before, c->n0, c->d_sel, c->st));
     } else {
       HIP_TRY(c, hipMemsetAsync(c->d_sel, 0xff, 4, c->st));
     }
-    if (c->nranks > 1) {
-      std::vector<int32_t> w(c->nranks);
+    if (lr > 1) {
+      std::vector<int32_t> w(lr);
       int rc = exchange_small(c, XSITE_SELECT, c->d_sel, 4, w.data());
       if (rc) return rc;
       winner = w[owner];
@@ -2387,10 +2451,10 @@ int gs_destroy(gs_ctx* c) {
   void* dev[] = {c->d_xerr, c->d_xsmall,
                  c->d_i64, c->d_i32, c->d_pods, c->d_S, c->d_xchg_send, c->d_xchg_recv, c->d_xmerged,
                  c->d_committed, c->d_rowstat, c->d_sel, c->d_stage_idx, c->d_stage_rows, c->d_numa_idx,
-                 c->d_topos, c->d_aff, c->d_tb};
+                 c->d_topos, c->d_aff, c->d_tb, c->d_sx_send, c->d_sx_recv};
   for (void* p : dev)
     if (p) (void)hipFree(p);
-  void* host[] = {c->h_xsmall, c->h_pods, c->h_committed, c->h_stage_idx, c->h_stage_rows, c->h_xchg_send,
+  void* host[] = {c->h_sx_send, c->h_sx_recv, c->h_xsmall, c->h_pods, c->h_committed, c->h_stage_idx, c->h_stage_rows, c->h_xchg_send,
                   c->h_xchg_recv};
   for (void* p : host)
     if (p) (void)hipHostFree(p);

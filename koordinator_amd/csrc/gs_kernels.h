@@ -180,7 +180,7 @@ struct XTag {
 };
 static_assert(sizeof(XTag) == 32, "XTag layout");
 constexpr uint32_t XTAG_MAGIC = 0x31585347u;   // "GSX1"
-enum : uint32_t { XSITE_LEVELS = 1, XSITE_ROWSTAT = 2, XSITE_SELECT = 3 };
+enum : uint32_t { XSITE_LEVELS = 1, XSITE_ROWSTAT = 2, XSITE_SELECT = 3, XSITE_SCORES = 4 };
 constexpr int32_t COMMIT_ERR_XTAG = 90;   // committed[3]: the level exchange's tags disagree (nothing committed)
 constexpr int XERR_TAGS = 8;   // merge_levels_kernel's xerr: [0] verdict, [1] first mismatch kept, [8..] its R tags
 constexpr size_t XERR_BYTES = 4 * XERR_TAGS + sizeof(XTag) * MAX_RANKS;
@@ -191,6 +191,12 @@ hipError_t launch_write_tag(uint8_t* dst, const XTag& t, hipStream_t st);
 // they name the same exchange, else 1 + the first rank that differs from rank 0 (the commit then commits nothing).
 hipError_t launch_merge_levels(const uint8_t* xin, size_t xblock, int nranks, int npods, int bmax, int lstride,
                                uint8_t* xout, int32_t* xerr, hipStream_t st);
+// several shards, score-row exchange (the default; GS_XCHG=levels: the level lists above): rank r's all-gathered block
+// is [b x pld int16 scores | b x pld affinity bytes | ... | XTag] over its nodes [r*per, min(N, (r+1)*per)); the R blocks
+// are written into the full-width score rows S[k][node] (stride ld) and affinities of the batch. Block 0 checks the R
+// blocks' tags into xerr like merge_levels_kernel (the commit then commits nothing on a mismatch).
+hipError_t launch_unpack_scores(const uint8_t* xin, size_t xblock, int nranks, int npods, uint32_t per, uint32_t pld,
+                                uint32_t N, int16_t* S, uint8_t* aff, uint32_t ld, int32_t* xerr, hipStream_t st);
 size_t commit_smem_bytes(int B);
 bool commit_spec_selected(uint32_t window_k);   // the speculative commit kernel runs (else pipelined / lockstep)
 hipError_t launch_commit(const CommitArgs& a, hipStream_t st);        // window_k > 0: lockstep kernel

@@ -949,6 +949,50 @@ __global__ void __launch_bounds__(FIX_THREADS) fix_levels_kernel(int16_t* __rest
 // nodes; a level's nodes in shard order, i.e. node order (shards are contiguous ranges, each shard's level segment is
 // ascending). The merged `next` is the highest score not kept (every shard's `next`, or the first dropped level).
 // Block k = pod k; thread e = (shard e / LEVALL, level e % LEVALL).
+// Several ranks, score-row exchange: rank r evaluated its shard [r*per, min(N, (r+1)*per)) into the block layout of
+// launch_unpack_scores (gs_kernels.h); here the R all-gathered blocks become the batch's full-width score rows and
+// Filter-time affinities, so every rank continues with the one-shard pipeline over the whole cluster. Grid: (pld/256,
+// npods, R). Block (0, 0, 0) checks the blocks' exchange tags as merge_levels_kernel does.
+__global__ void __launch_bounds__(256) unpack_scores_kernel(const uint8_t* __restrict__ xin, size_t xblock, int R,
+                                                            int npods, uint32_t per, uint32_t pld, uint32_t N,
+                                                            int16_t* __restrict__ S, uint8_t* __restrict__ aff,
+                                                            uint32_t ld, int32_t* __restrict__ xerr) {
+  const int r = blockIdx.z, k = blockIdx.y;
+  const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+  if (r == 0 && k == 0 && blockIdx.x == 0 && threadIdx.x == 0) {
+    const XTag* t0 = reinterpret_cast<const XTag*>(xin + xblock - sizeof(XTag));
+    int bad = 0;
+    for (int q = 0; q < R && !bad; ++q) {
+      const XTag* tq = reinterpret_cast<const XTag*>(xin + (size_t)q * xblock + xblock - sizeof(XTag));
+      if (tq->magic != XTAG_MAGIC || tq->site != t0->site || tq->seq != t0->seq || tq->batch != t0->batch ||
+          tq->rank != q || tq->bytes != (uint32_t)xblock)
+        bad = 1 + q;
+    }
+    xerr[0] = bad;
+    if (bad && !xerr[1]) {
+      xerr[1] = 1;
+      uint32_t* dst = reinterpret_cast<uint32_t*>(xerr + XERR_TAGS);
+      for (int q = 0; q < R; ++q) {
+        const uint32_t* tq = reinterpret_cast<const uint32_t*>(xin + (size_t)q * xblock + xblock - sizeof(XTag));
+        for (int w = 0; w < (int)(sizeof(XTag) / 4); ++w) dst[q * (sizeof(XTag) / 4) + w] = tq[w];
+      }
+    }
+  }
+  const uint32_t node = (uint32_t)r * per + i;
+  if (i >= per || node >= N) return;
+  const uint8_t* blk = xin + (size_t)r * xblock;
+  S[(size_t)k * ld + node] = reinterpret_cast<const int16_t*>(blk)[(size_t)k * pld + i];
+  aff[(size_t)k * ld + node] = blk[(size_t)npods * pld * 2 + (size_t)k * pld + i];
+}
+
+hipError_t launch_unpack_scores(const uint8_t* xin, size_t xblock, int nranks, int npods, uint32_t per, uint32_t pld,
+                                uint32_t N, int16_t* S, uint8_t* aff, uint32_t ld, int32_t* xerr, hipStream_t st) {
+  if (npods <= 0 || nranks <= 0) return hipSuccess;
+  hipLaunchKernelGGL(unpack_scores_kernel, dim3((per + 255) / 256, npods, nranks), dim3(256), 0, st, xin, xblock,
+                     nranks, npods, per, pld, N, S, aff, ld, xerr);
+  return hipGetLastError();
+}
+
 __global__ void __launch_bounds__(256) merge_levels_kernel(const uint8_t* __restrict__ xin, size_t xblock, int R,
                                                            int bmax, int lstride, uint8_t* __restrict__ xout,
                                                            int32_t* __restrict__ xerr) {

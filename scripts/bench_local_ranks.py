@@ -1,6 +1,7 @@
 """Multi-rank rehearsal on ONE GPU over the in-process device transport (gs_comm_init_local): N ranks as threads of
 this process, each an Engine over its node shard of the C3 bench cluster, the level all-gathers stream-ordered on the
-device (as ncclAllGather runs them), every rank scheduling the same queue in 2048-pod steps. Prints one JSON line:
+device (as ncclAllGather runs them; score rows by default, GS_XCHG=levels the candidate level lists), every rank
+scheduling the same queue in 2048-pod steps. Prints one JSON line:
 the wall-clock pods/s of the slowest rank and, per rank, the batch chain's parts (eval pass, levels + exchange,
 commit). All N ranks share the box's one GPU, so this is not a scaling point: it measures what the sharded flow
 costs per batch — the merged-list commit against one rank's commit. N = 1 runs the single-rank path
@@ -9,6 +10,7 @@ costs per batch — the merged-list commit against one rank's commit (DESIGN.md 
     python scripts/bench_local_ranks.py [--ranks 2] [--nodes 50000] [--steps 10] [--warmup 2]
 """
 import argparse
+import hashlib
 import json
 import os
 import sys
@@ -87,8 +89,10 @@ def main():
                     "commit_ms_per_batch": round(st["commit_ms"] / b, 4),
                     "exchange_ms_per_batch": round(st["exchange_ms"] / b, 4)})
     print(json.dumps({"metric": "pods/s, N ranks as threads on one GPU (device transport)", "ranks": n,
+                      "exchange": (os.environ.get("GS_XCHG") or "scores") if n > 1 else None,
                       "nodes": args.nodes, "pods": args.steps * P, "pods_per_s": args.steps * P / dt,
-                      "placed": res[0][1], "identical_placements_on_every_rank": bool(same), "per_rank": per,
+                      "placed": res[0][1], "identical_placements_on_every_rank": bool(same),
+                      "placements_sha1": hashlib.sha1(res[0][3].tobytes()).hexdigest()[:16], "per_rank": per,
                       "config": "C3 (NUMA profile), 2048-pod blocking gs_schedule steps, batch 128; every rank on the "
                                 "box's one GPU"}))
 

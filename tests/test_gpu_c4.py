@@ -44,6 +44,9 @@ def _worker(rank: int, world: int, port: int, numa: bool, pods: int, q):
     # Oversubscribed, the scheduler time-slices the processes' queues and a rank waited ~10 s at a time for its queue
     # (reproduced with 4 HIP queues per process, gone with 2). Read by HIP at its initialisation below.
     os.environ["GPU_MAX_HW_QUEUES"] = "2"
+    # the level-list exchange (GS_XCHG=levels): these 100k-node clusters' score-row blocks (the default exchange, tested
+    # over 2-4 ranks at 3k nodes in test_gpu_parity / test_gpu_dist) would move gigabytes through gloo per test
+    os.environ["GS_XCHG"] = "levels"
     try:
         import torch
         import torch.distributed as dist

@@ -311,11 +311,15 @@ def run_ranks_local(c, cfg, n, pods=None, enabled=None):
     return res, engines, g
 
 
-@pytest.mark.parametrize("n,numa", [(2, False), (4, True)], ids=["2ranks", "4ranks-numa"])
-def test_ranks_on_one_gpu_device_transport(n, numa):
+@pytest.mark.parametrize("n,numa,xchg", [(2, False, "scores"), (4, True, "scores"), (2, True, "levels"), (4, True, "levels")],
+                         ids=["2ranks", "4ranks-numa", "2ranks-numa-levels", "4ranks-numa-levels"])
+def test_ranks_on_one_gpu_device_transport(n, numa, xchg, monkeypatch):
     """The sharded path over the stream-ordered device transport (RCCL's ordering: tags written on the stream, the
     blocks copied device-to-device behind the senders' events, the next batch's kernels behind every rank's copies,
-    batches in flight across exchanges): every rank's placements equal the oracle's."""
+    batches in flight across exchanges): every rank's placements equal the oracle's. Both exchanges: the score rows of
+    every shard (the default; every rank then runs the one-shard pipeline over all nodes) and the candidate levels
+    (GS_XCHG=levels: merged level lists, the multi-shard commit)."""
+    monkeypatch.setenv("GS_XCHG", xchg)
     c = synth.make_cluster(3001, 400, 13)
     en = abi.GS_ENABLE_ALL if numa else abi.GS_ENABLE_LA_FIT
     if numa:
@@ -333,11 +337,14 @@ def test_ranks_on_one_gpu_device_transport(n, numa):
         assert engines[r].stats()["shard_end"] == engines[r + 1].stats()["shard_begin"]
 
 
-def test_device_transport_divergence_fails_on_every_rank(monkeypatch):
+@pytest.mark.parametrize("xchg", ["scores", "levels"])
+def test_device_transport_divergence_fails_on_every_rank(xchg, monkeypatch):
     """A rank whose exchange sequence diverges over the device transport: every rank fails with GS_ECOMM naming the
-    batch (the tags travel with the blocks and merge_levels_kernel checks them on each rank's stream)."""
+    batch (the tags travel with the blocks and unpack_scores_kernel / merge_levels_kernel checks them on each rank's
+    stream)."""
     c = synth.make_cluster(3001, 300, 13)
     cfg = config.make_config(c.num_nodes)
+    monkeypatch.setenv("GS_XCHG", xchg)
     monkeypatch.setenv("GS_DEBUG_XCHG_SKEW", "1:1")
     res, _, _ = run_ranks_local(c, cfg, 2)
     for r in range(2):
