@@ -892,7 +892,7 @@ constexpr size_t XSMALL = 64;   // small exchange block: payload <= 32 B, XTag a
 
 const char* xsite_name(uint32_t s) {
   return s == XSITE_LEVELS ? "levels" : s == XSITE_ROWSTAT ? "row stats" : s == XSITE_SELECT ? "selection"
-       : s == XSITE_SCORES ? "score rows" : "?";
+       : s == XSITE_SCORES ? "score rows" : s == XSITE_RUNS ? "run boundary" : "?";
 }
 
 // The R received blocks' tags against the tag this rank sent: every rank checks all of them, so a divergence fails
@@ -1017,15 +1017,23 @@ int exchange(gs_ctx* c, uint32_t site, uint8_t* d_send, uint8_t* d_recv, size_t 
 }
 
 // A small exchange (payload <= 32 B at d_payload, device) and its R payloads read back to host_out (R x payload bytes).
-int exchange_small(gs_ctx* c, uint32_t site, const void* d_payload, size_t payload, void* host_out) {
+// xs: the stream (default st); a host payload (d_payload == nullptr) is taken from host_in.
+int exchange_small(gs_ctx* c, uint32_t site, const void* d_payload, size_t payload, void* host_out,
+                   hipStream_t xs = nullptr, const void* host_in = nullptr) {
   static_assert(XSMALL >= 32 + sizeof(XTag), "small exchange block");
   if (payload > XSMALL - sizeof(XTag)) return fail(c, GS_EINVAL, "small exchange payload too large");
-  HIP_TRY(c, hipMemcpyAsync(c->d_xsmall, d_payload, payload, hipMemcpyDeviceToDevice, c->st));
+  if (!xs) xs = c->st;
+  if (d_payload) {
+    HIP_TRY(c, hipMemcpyAsync(c->d_xsmall, d_payload, payload, hipMemcpyDeviceToDevice, xs));
+  } else {   // (h_xsmall is free between small exchanges: staged through it, in stream order)
+    std::memcpy(c->h_xsmall, host_in, payload);
+    HIP_TRY(c, hipMemcpyAsync(c->d_xsmall, c->h_xsmall, payload, hipMemcpyHostToDevice, xs));
+  }
   XTag tag{};
-  if (int rc = exchange(c, site, c->d_xsmall, c->d_xsmall + XSMALL, XSMALL, &tag)) return rc;
-  HIP_TRY(c, hipMemcpyAsync(c->h_xsmall, c->d_xsmall + XSMALL, XSMALL * c->nranks, hipMemcpyDeviceToHost, c->st));
+  if (int rc = exchange(c, site, c->d_xsmall, c->d_xsmall + XSMALL, XSMALL, &tag, xs)) return rc;
+  HIP_TRY(c, hipMemcpyAsync(c->h_xsmall, c->d_xsmall + XSMALL, XSMALL * c->nranks, hipMemcpyDeviceToHost, xs));
   Where w_(c, "exchange_small: read back");
-  HIP_TRY(c, host_wait_stream(c->st));
+  HIP_TRY(c, host_wait_stream(xs));
   if (int rc = check_tags(c, c->h_xsmall, XSMALL, tag)) return rc;
   for (int r = 0; r < c->nranks; ++r)
     std::memcpy(static_cast<uint8_t*>(host_out) + (size_t)r * payload, c->h_xsmall + (size_t)r * XSMALL, payload);
@@ -2715,6 +2723,19 @@ struct PodRun {
   void* tag = nullptr;
 };
 
+// Several ranks: whether the next run is already known (gs_schedule_submit) is a matter of each rank's timing. The
+// ranks agree on it at every batch that ends a run (all of them must hold it), so that they speculate across the run
+// boundary together and their exchanges pair up; a rank that holds the next run when the others do not starts it
+// after the current one without speculation, as they do. On st2 (idle between eval passes): the batch in flight
+// keeps running.
+int agree_next_run(gs_ctx* c, bool* use) {
+  const uint32_t mine = *use ? 1u : 0u;
+  std::vector<uint32_t> all(c->nranks);
+  if (int rc = exchange_small(c, XSITE_RUNS, nullptr, 4, all.data(), c->st2, &mine)) return rc;
+  for (uint32_t v : all) *use = *use && v;
+  return GS_OK;
+}
+
 // The scheduleOne loop over the pod stream, batch by batch. Pipelining: while batch [i, i+b) runs, the next batch is
 // staged and enqueued behind it on the stream (other slot). Its commit kernel checks on the device that the batch
 // before committed all its pods with no host-side Reserve pending, else it is a no-op; the host only keeps it when the
@@ -2805,7 +2826,9 @@ int schedule_stream(gs_ctx* c, PodRun run, Next&& next_run, Done&& run_done) {
         np = pods; ns = run.seq; nj = j; nn = run.n;
       } else {
         if (!have_nxt) have_nxt = next_run(&nxt);
-        if (have_nxt && nxt.n) { np = nxt.pods; ns = nxt.seq; nn = nxt.n; }
+        bool use = have_nxt && nxt.n;
+        if (c->nranks > 1 && (rc = agree_next_run(c, &use))) { drain(); return rc; }
+        if (use) { np = nxt.pods; ns = nxt.seq; nn = nxt.n; }
       }
       bool spec = false;
       int nb = 0;
@@ -3009,7 +3032,6 @@ int gs_schedule(gs_ctx* c, const gs_pod* pods, uint32_t npods, const uint64_t* s
 int gs_schedule_submit(gs_ctx* c, const gs_pod* pods, uint32_t npods, const uint64_t* seq, gs_placement* out,
                        uint64_t* ticket) {
   if (!c || !ticket || (npods && (!pods || !out))) return GS_EINVAL;
-  if (c->nranks > 1) return fail(c, GS_EUNSUPPORTED, "gs_schedule_submit: one rank (use gs_schedule with several)");
   if (c->window_k) return fail(c, GS_EUNSUPPORTED, "gs_schedule_submit: not with node sampling");
   auto r = std::make_shared<AsyncRun>();
   // checks that write nothing (the worker may be running): on an error, wait for it, then report

@@ -180,7 +180,7 @@ struct XTag {
 };
 static_assert(sizeof(XTag) == 32, "XTag layout");
 constexpr uint32_t XTAG_MAGIC = 0x31585347u;   // "GSX1"
-enum : uint32_t { XSITE_LEVELS = 1, XSITE_ROWSTAT = 2, XSITE_SELECT = 3, XSITE_SCORES = 4 };
+enum : uint32_t { XSITE_LEVELS = 1, XSITE_ROWSTAT = 2, XSITE_SELECT = 3, XSITE_SCORES = 4, XSITE_RUNS = 5 };
 constexpr int32_t COMMIT_ERR_XTAG = 90;   // committed[3]: the level exchange's tags disagree (nothing committed)
 constexpr int XERR_TAGS = 8;   // merge_levels_kernel's xerr: [0] verdict, [1] first mismatch kept, [8..] its R tags
 constexpr size_t XERR_BYTES = 4 * XERR_TAGS + sizeof(XTag) * MAX_RANKS;

@@ -337,6 +337,52 @@ def test_ranks_on_one_gpu_device_transport(n, numa, xchg, monkeypatch):
         assert engines[r].stats()["shard_end"] == engines[r + 1].stats()["shard_begin"]
 
 
+@pytest.mark.parametrize("n,xchg", [(2, "scores"), (3, "scores"), (2, "levels")])
+def test_ranks_submit_across_runs(n, xchg, monkeypatch):
+    """gs_schedule_submit on several ranks: each rank submits the same runs at its own pace (rank-dependent sleeps,
+    so at a run boundary one rank may hold the next run while another does not). The ranks agree at every run-ending
+    batch whether to speculate into the next run (XSITE_RUNS), so their exchanges pair up and the placements of every
+    rank equal the oracle's over the whole stream."""
+    import time
+    from koordinator_amd.engine import Engine, LocalGroup
+    monkeypatch.setenv("GS_XCHG", xchg)
+    c = synth.make_cluster(3001, 700, 13)
+    synth.make_numa(c)
+    cfg = config.make_config(c.num_nodes, enabled=abi.GS_ENABLE_ALL)
+    cuts = [0, 150, 240, 300, 470, 600, 700]
+    seq = np.arange(700, dtype=np.uint64)
+    g = LocalGroup(n)
+    engines = [Engine(cfg) for _ in range(n)]
+    for r, x in enumerate(engines):
+        synth.load_into(x, c)
+        x.comm_init_local(g, r)
+    rng = np.random.default_rng(5)
+    delays = rng.uniform(0, 0.004, size=(n, len(cuts) - 1))
+    res = [None] * n
+
+    def run(r):
+        try:
+            hs = []
+            for k in range(len(cuts) - 1):
+                time.sleep(delays[r, k])
+                hs.append(engines[r].schedule_submit(c.pods[cuts[k]:cuts[k + 1]], seq[cuts[k]:cuts[k + 1]]))
+            res[r] = np.concatenate([engines[r].schedule_wait(h) for h in hs])
+        except Exception as ex:   # noqa: BLE001 (reported per rank)
+            res[r] = ex
+    th = [threading.Thread(target=run, args=(r,)) for r in range(n)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=300)
+    o = orc.Oracle(cfg)
+    synth.load_into(o, c)
+    want = o.schedule(c.pods)
+    for r in range(n):
+        assert not isinstance(res[r], Exception) and res[r] is not None, (r, res[r])
+        for f in ("node", "score", "ties", "feasible"):
+            assert np.array_equal(res[r][f], want[f]), (r, f)
+
+
 @pytest.mark.parametrize("xchg", ["scores", "levels"])
 def test_device_transport_divergence_fails_on_every_rank(xchg, monkeypatch):
     """A rank whose exchange sequence diverges over the device transport: every rank fails with GS_ECOMM naming the
