@@ -2285,8 +2285,8 @@ int gs_create(const gs_config* cfg, gs_ctx** out) {
   if (getenv("GS_COMMIT_STAMPS") && getenv("GS_COMMIT_STAMPS")[0] == '1') {
     // 8 waves x 64 entries (commit_spec_kernel: one region per wave; the other commit kernels: region 0), then the
     // cand kernel's 8 at entry 512
-    if ((e = hipMalloc(&c->d_stamps, 8 * 520)) != hipSuccess) return bail("hipMalloc", e);
-    (void)hipMemset(c->d_stamps, 0, 8 * 520);
+    if ((e = hipMalloc(&c->d_stamps, 8 * 524)) != hipSuccess) return bail("hipMalloc", e);
+    (void)hipMemset(c->d_stamps, 0, 8 * 524);
     set_cand_stamps(c->d_stamps + 512);
   }
   if ((e = hipDeviceSynchronize()) != hipSuccess) return bail("hipDeviceSynchronize", e);
@@ -2331,8 +2331,8 @@ int gs_destroy(gs_ctx* c) {
   for (void* p : {(void*)c->h_xin, (void*)c->h_xout, (void*)c->h_xnom})
     if (p) (void)hipHostFree(p);
   if (c->d_stamps) {
-    std::vector<uint64_t> sa(520);
-    if (hipMemcpy(sa.data(), c->d_stamps, 8 * 520, hipMemcpyDeviceToHost) == hipSuccess) {
+    std::vector<uint64_t> sa(524);
+    if (hipMemcpy(sa.data(), c->d_stamps, 8 * 524, hipMemcpyDeviceToHost) == hipSuccess) {
       if (!c->window_k) {   // speculative commit kernel: one stamp region per wave
         const double np = c->stats_all_pods ? (double)c->stats_all_pods : 1.0;
         auto W = [&](int w, int i) { return (double)sa[w * 64 + i] / np; };
@@ -2396,7 +2396,9 @@ int gs_destroy(gs_ctx* c) {
         fprintf(stderr, "gpuscore cand_kernel, wave-0 cycles per pod row: pass 1 %.0f, level sums %.0f, level pick %.0f, "
                 "offsets %.0f, pass 2 %.0f\n", sa[512] / nb, sa[513] / nb, sa[514] / nb, sa[515] / nb, sa[516] / nb);
         fprintf(stderr, "gpuscore fix_levels_kernel, thread-0 cycles per pod row: loads+dedupe %.0f, landed rows + level pick "
-                "%.0f, lists %.0f\n", sa[517] / nb, sa[518] / nb, sa[519] / nb);
+                "%.0f, lists %.0f; the block's slowest landed-row lane: row loads %.0f, loads + evaluation %.0f; thread 0: "
+                "start -> its evaluation %.0f, start -> every lane evaluated %.0f\n",
+                sa[517] / nb, sa[518] / nb, sa[519] / nb, sa[520] / nb, sa[521] / nb, sa[522] / nb, sa[523] / nb);
         (void)hipFree(c->d_stamps);
         c->d_stamps = nullptr;
       }

@@ -732,9 +732,15 @@ __global__ void __launch_bounds__(FIX_THREADS) fix_levels_kernel(int16_t* __rest
   const int k = blockIdx.x, t = threadIdx.x, lane = t & 63;
   const int npr = min(cp.prev_committed[0], MAX_BATCH);   // -1: a voided pass (its lists are never used)
   if (npr <= 0) return;
-  // phase 1 (no barrier): wave 3 reads the stale levels, every thread part of the histogram, and thread j < npr
+  __shared__ unsigned int s_ev_max[2];   // diagnostics: the block's slowest lane (row loads, row loads + evaluation)
+  if (stamps && t < 2) s_ev_max[t] = 0;
+  if (stamps) __syncthreads();
+  // phase 1 (no barrier): the evaluation of the landed rows is the long chain (row loads ~15k cycles, then one pair
+  // evaluation, ~26k for the slowest lane of a wave whose rows differ), so waves 0-1 do only that: thread j < npr
   // evaluates landed entry j (duplicates too: a node several pods landed on gives the same result each time; its stale
-  // score is read here, before any entry's write below)
+  // score is read here, before any entry's write below). Beside it wave 3 reads the stale levels and stages the stale
+  // lists in LDS, and wave 2 the histogram (their HBM round trips overlap the evaluation).
+  static_assert(FIX_THREADS == 256 && MAX_BATCH <= 128, "fix_levels_kernel: waves 0-1 evaluate, 2-3 load");
   if (t >= FIX_THREADS - 64) {   // the stale levels: one lane per level (independent loads), offsets by a wave scan
     const LevelHdr& h = hdrs[k];
     const LevelExt& x = ext[k];
@@ -758,8 +764,25 @@ __global__ void __launch_bounds__(FIX_THREADS) fix_levels_kernel(int16_t* __rest
       s_fd = 0;
       s_top = onl > 0 ? h.score[0] : x.next;   // the highest non-empty bin before the landed rows move
     }
+    // the stale lists into LDS (8 loads in flight per lane)
+    const int otot = onl > 0 ? __shfl(incl, onl - 1) : 0;
+    const uint32_t* src = lists + (size_t)k * lcap;
+    for (int e0 = 0; e0 < otot; e0 += 8 * 64) {
+      uint32_t v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int e = e0 + u * 64 + lane;
+        v[u] = e < otot ? src[e] : 0u;
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int e = e0 + u * 64 + lane;
+        if (e < otot) olist[e] = v[u];
+      }
+    }
+  } else if (t >= FIX_THREADS - 128) {
+    for (int b = lane; b < nbins; b += 64) hist[b] = cp.hist[(size_t)k * nbins + b];
   }
-  for (int b = t; b < nbins; b += FIX_THREADS) hist[b] = cp.hist[(size_t)k * nbins + b];
   const bool numa = (cp.pf.enabled & 0x30u) != 0;
   size_t at = 0;
   int so = -1, sn = -1, aff_v = -1;
@@ -769,37 +792,45 @@ __global__ void __launch_bounds__(FIX_THREADS) fix_levels_kernel(int16_t* __rest
     valid = node >= 0 && (uint32_t)node >= cp.n0 && (uint32_t)node < cp.n1;
     p_raw[t] = valid ? (uint32_t)node : 0xffffffffu;
     if (valid) {
+      const uint64_t e0 = stamps ? __builtin_amdgcn_s_memtime() : 0;
+      if (stamps && t == 0)
+        atomicAdd(reinterpret_cast<unsigned long long*>(&stamps[10]), (unsigned long long)(e0 - ct_last));
       at = (size_t)k * ld + ((uint32_t)node - cp.n0);
       so = S[at];
       Row r;
       load_row(cp.m, (uint32_t)node, cp.prod_cols, numa, r);
+      if (stamps) {
+        __builtin_amdgcn_s_waitcnt(0);
+        atomicMax(&s_ev_max[0], (unsigned int)(__builtin_amdgcn_s_memtime() - e0));
+      }
       const PairOut o = eval_pair<false, false, true>(r, cp.pods[k], cp.pf, cp.m);
       sn = total_score(o, cp.pf);
       if (numa && ((r.nr.nflags >> NF_POLICY_SHIFT) & 3u)) aff_v = o.code ? 0 : (int)o.aff;
+      if (stamps) atomicMax(&s_ev_max[1], (unsigned int)(__builtin_amdgcn_s_memtime() - e0));
     }
     r_old[t] = so;
     r_new[t] = sn;
   }
   __syncthreads();
-  // phase 2: the stale lists into LDS; the patched scores out; landed entries ranked by (node, index)
-  {
-    const int otot = s_onlev > 0 ? o_off[s_onlev - 1] + o_count[s_onlev - 1] : 0;
-    const uint32_t* src = lists + (size_t)k * lcap;
-    for (int e = t; e < otot; e += FIX_THREADS) olist[e] = src[e];
+  if (stamps && t == 0) {
+    atomicAdd(reinterpret_cast<unsigned long long*>(&stamps[8]), (unsigned long long)s_ev_max[0]);
+    atomicAdd(reinterpret_cast<unsigned long long*>(&stamps[9]), (unsigned long long)s_ev_max[1]);
+    atomicAdd(reinterpret_cast<unsigned long long*>(&stamps[11]),
+              (unsigned long long)(__builtin_amdgcn_s_memtime() - ct_last));   // kernel start -> every lane evaluated
   }
-  if (valid) {
-    S[at] = (int16_t)sn;
-    if (aff_v >= 0) cp.aff[at] = (uint8_t)aff_v;
-  }
-  if (t < npr) {
-    const uint32_t x = p_raw[t];
+  // phase 2: landed entries ranked by (node, index). The patched scores go out at the end of the kernel: vmcnt counts
+  // stores too, and the compiler's vmcnt(0) before the ranking made the stores' round trip part of the chain
+  if (t < 128) {   // waves 0-1: the 128 keys in two registers per lane, compared through readlane (no LDS per key)
+    const uint32_t x = t < npr ? p_raw[t] : 0u;
+    const uint32_t k0 = lane < npr ? p_raw[lane] : 0u, k1 = 64 + lane < npr ? p_raw[64 + lane] : 0u;
     int rank = 0;
-#pragma unroll 16
-    for (int i = 0; i < MAX_BATCH; ++i) {
-      const uint32_t y = p_raw[i];
-      rank += (i < npr && (y < x || (y == x && i < t))) ? 1 : 0;
+#pragma unroll
+    for (int i = 0; i < 64; ++i) {
+      const uint32_t y0 = __builtin_amdgcn_readlane(k0, i), y1 = __builtin_amdgcn_readlane(k1, i);
+      rank += (i < npr && (y0 < x || (y0 == x && i < t))) ? 1 : 0;
+      rank += (64 + i < npr && (y1 < x || (y1 == x && 64 + i < t))) ? 1 : 0;
     }
-    p_sidx[rank] = t;
+    if (t < npr) p_sidx[rank] = t;
   }
   __syncthreads();
   // the first entry of each node, in node order: the distinct landed rows, moved in the histogram
@@ -939,6 +970,10 @@ __global__ void __launch_bounds__(FIX_THREADS) fix_levels_kernel(int16_t* __rest
     x.next = s_next;
     for (int j = 0; j < LEVX; ++j) { x.score[j] = n_score[MAXLEV + j]; x.count[j] = n_count[MAXLEV + j]; }
     ext[k] = x;
+  }
+  if (valid) {   // the patched scores and Filter-time affinities of the landed rows
+    S[at] = (int16_t)sn;
+    if (aff_v >= 0) cp.aff[at] = (uint8_t)aff_v;
   }
 }
 

@@ -29,6 +29,7 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--pods-per-step", type=int, default=2048)
+    ap.add_argument("--sync", action="store_true", help="blocking gs_schedule per step (default: submit one ahead)")
     args = ap.parse_args()
     from koordinator_amd import abi, config, synth
     from koordinator_amd.engine import Engine, LocalGroup
@@ -58,12 +59,18 @@ def main():
             e.reset_stats()
             bar.wait()
             t0 = time.perf_counter()
-            placed = 0
             outs = []
-            for s in range(args.warmup, args.warmup + args.steps):
-                out = e.schedule(c.pods[s * P:(s + 1) * P], seq[s * P:(s + 1) * P])
-                placed += int((out["node"] >= 0).sum())
-                outs.append(out["node"].copy())
+            s0, s1 = args.warmup, args.warmup + args.steps
+            if args.sync:
+                for s in range(s0, s1):
+                    outs.append(e.schedule(c.pods[s * P:(s + 1) * P], seq[s * P:(s + 1) * P])["node"].copy())
+            else:   # each step submitted before the previous one is waited for, as bench.py does
+                h = e.schedule_submit(c.pods[s0 * P:(s0 + 1) * P], seq[s0 * P:(s0 + 1) * P])
+                for s in range(s0 + 1, s1 + 1):
+                    h2 = e.schedule_submit(c.pods[s * P:(s + 1) * P], seq[s * P:(s + 1) * P]) if s < s1 else None
+                    outs.append(e.schedule_wait(h)["node"].copy())
+                    h = h2
+            placed = sum(int((o >= 0).sum()) for o in outs)
             e.synchronize()
             res[r] = (time.perf_counter() - t0, placed, e.stats(), np.concatenate(outs))
         except Exception as ex:   # noqa: BLE001
@@ -93,8 +100,9 @@ def main():
                       "nodes": args.nodes, "pods": args.steps * P, "pods_per_s": args.steps * P / dt,
                       "placed": res[0][1], "identical_placements_on_every_rank": bool(same),
                       "placements_sha1": hashlib.sha1(res[0][3].tobytes()).hexdigest()[:16], "per_rank": per,
-                      "config": "C3 (NUMA profile), 2048-pod blocking gs_schedule steps, batch 128; every rank on the "
-                                "box's one GPU"}))
+                      "config": "C3 (NUMA profile), 2048-pod steps (" + ("blocking gs_schedule" if args.sync else
+                                "gs_schedule_submit one ahead") + "), batch 128; every rank on the box's one GPU",
+                      "gpu_max_hw_queues": os.environ.get("GPU_MAX_HW_QUEUES")}))
 
 
 if __name__ == "__main__":

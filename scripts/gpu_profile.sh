@@ -10,13 +10,13 @@ timeout -k 10 400 python -u bench.py ${BENCH_ARGS:-} > gpurun_out/bench.json 2> 
 rc=$?; echo "BENCH rc=$rc"; cat gpurun_out/bench.json; tail -3 gpurun_out/bench.err
 [ $rc -eq 0 ] || exit $rc
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$PWD/gpurun_out/prof" -o bench --output-format csv -- \
-    python -u bench.py --steps 5 --warmup 1 --no-cpu-baseline ${BENCH_ARGS:-} > gpurun_out/prof.log 2>&1
+    python -u bench.py --steps 5 --warmup 1 --no-cpu-baseline --no-extras ${BENCH_ARGS:-} > gpurun_out/prof.log 2>&1
 rc=$?; echo "PROF rc=$rc"; tail -2 gpurun_out/prof.log
 [ $rc -eq 0 ] || exit $rc
 for ctr in FETCH_SIZE WRITE_SIZE; do
   d=gpurun_out/pmc_$(echo $ctr | tr A-Z a-z | cut -d_ -f1)
   timeout -s KILL 240 rocprofv3 --pmc $ctr -d "$PWD/$d" -o pmc --output-format csv -- \
-      python -u bench.py --steps 1 --warmup 0 --no-cpu-baseline ${BENCH_ARGS:-} > $d.log 2>&1
+      python -u bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-extras ${BENCH_ARGS:-} > $d.log 2>&1
   rc=$?; echo "PMC $ctr rc=$rc"; tail -2 $d.log
   [ $rc -eq 0 ] || exit $rc
 done

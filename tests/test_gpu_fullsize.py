@@ -123,3 +123,42 @@ def test_c2_5k_nodes_10k_pods_full_parity():
         assert len(bad) == 0, f"{f} differs at pods {bad[:5]}"
     print(f"C2 5k x 10k: {int((got['node'] >= 0).sum())} placed, all 10,000 decisions identical; "
           f"wall {time.perf_counter() - t0:.1f} s")
+
+
+@pytest.mark.parametrize("n,xchg", [(2, "scores"), (4, "scores"), (2, "levels")])
+def test_c3_bench_config_ranks_equal_golden(n, xchg, monkeypatch):
+    """The bench workload sharded over n ranks (threads of this process on the box's GPU, the stream-ordered device
+    transport that has RCCL's ordering), submitted one 2048-pod call ahead as bench.py does at every N: every rank's
+    20,480 placements — every field, NUMA zone split and cpuset included — equal the oracle-verified golden ones of
+    the one-GPU run, for the score-row exchange (the default) and the level exchange."""
+    import threading
+    from koordinator_amd.engine import Engine, LocalGroup
+    monkeypatch.setenv("GS_XCHG", xchg)
+    P, step = 20_480, 2048
+    c = synth.make_cluster(50_000, P, config_id=2)
+    synth.make_numa(c)
+    cfg = config.make_config(c.num_nodes, batch_size=128, enabled=abi.GS_ENABLE_ALL)
+    g = LocalGroup(n)
+    engines = [Engine(cfg) for _ in range(n)]
+    for r, e in enumerate(engines):
+        synth.load_into(e, c)
+        e.comm_init_local(g, r)
+    seq = np.arange(P, dtype=np.uint64)
+    res = [None] * n
+
+    def run(r):
+        try:
+            e = engines[r]
+            hs = [e.schedule_submit(c.pods[k:k + step], seq[k:k + step]) for k in range(0, P, step)]
+            res[r] = np.concatenate([e.schedule_wait(h) for h in hs])
+        except Exception as ex:   # noqa: BLE001 (reported per rank)
+            res[r] = ex
+    th = [threading.Thread(target=run, args=(r,)) for r in range(n)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=200)
+    for r in range(n):
+        assert not isinstance(res[r], Exception) and res[r] is not None, (r, res[r])
+        _golden_equal("bench", res[r])
+        assert engines[r].mirror_check() == 0
