@@ -1779,6 +1779,38 @@ __global__ void __launch_bounds__(SP_THREADS) commit_spec_kernel(CommitArgs a) {
       WAVE_FENCE();
       SPM(9);   // re-scoring job: row copy + hint table
       const int q2 = jb.q + 1 + jb.range * 64 + lane;
+      if (ST) {
+        // diagnostics: could the job's lanes have been skipped? Per later pod q2, from the row's batch-start score so
+        // (an upper bound of every later version's under LeastAllocated on a row without a NUMA policy): 0 infeasible
+        // at batch start, 1 feasible below q2's lowest listed level (its lists hold >= q2 + 1 nodes), 2 needed exactly,
+        // 3 lists too short for the bound. Regions 30.. (no policy) and 40.. (policy rows) of the re-scoring waves.
+        const bool pol = numa_on && ((rr.nr.nflags >> NF_POLICY_SHIFT) & 3u);
+        int cat = -1;
+        if (q2 < B) {
+          const int so = dso[q2 * SB + jb.slot];
+          const LevelHdr* h = hdr_ptr(a, 0, q2);
+          const LevelExt* x = reinterpret_cast<const LevelExt*>(a.xbase + (size_t)a.bmax * LCAP * 4 +
+                                                                (size_t)a.bmax * sizeof(LevelHdr)) + q2;
+          const int nl = min(x->nlev, LEVALL);
+          int tot = 0, lo = -1;
+          for (int j = 0; j < nl; ++j) {
+            tot += j < MAXLEV ? h->count[j] : x->count[j - MAXLEV];
+            lo = j < MAXLEV ? h->score[j] : x->score[j - MAXLEV];
+          }
+          cat = so < 0 ? 0 : tot < q2 + 1 ? 3 : so < lo ? 1 : 2;
+        }
+        const uint64_t act = __ballot(q2 < B), c0 = __ballot(cat == 0), c1 = __ballot(cat == 1), c2 = __ballot(cat == 2),
+                       c3 = __ballot(cat == 3);
+        const int base = pol ? 40 : 30;
+        st_acc[base] += 1;
+        st_acc[base + 1] += __popcll(act);
+        st_acc[base + 2] += __popcll(c0);
+        st_acc[base + 3] += __popcll(c1);
+        st_acc[base + 4] += __popcll(c2);
+        st_acc[base + 5] += __popcll(c3);
+        st_acc[base + 6] += (c1 | c2 | c3) == 0 ? 1 : 0;   // every lane infeasible at batch start
+        st_acc[base + 7] += (c2 | c3) == 0 ? 1 : 0;        // no lane needs the exact score
+      }
       if (q2 < B) dsc[q2 * SB + jb.slot] = (int16_t)row_score(rr, pods(q2), a.pf, m, &tab);
       WAVE_FENCE();
       int fin = 0;

@@ -2392,6 +2392,16 @@ int gs_destroy(gs_ctx* c) {
         for (int w : {split ? 4 : 1, 5, 6, 7})
           fprintf(stderr, "  wave %d (re-scoring): busy %.0f (row copy + hint table %.0f, scores %.0f) waiting %.0f, jobs %.2f "
                   "per pod\n", w, W(w, 7) + W(w, 9), W(w, 9), W(w, 7), W(w, 8), W(w, 10));
+        for (int base : {30, 40}) {   // re-scoring jobs by what their lanes needed (gs_commit_spec.hip, ST)
+          uint64_t v[8] = {};
+          for (int w : {split ? 4 : 1, 5, 6, 7})
+            for (int i = 0; i < 8; ++i) v[i] += sa[w * 64 + base + i];
+          fprintf(stderr, "  re-scoring jobs on %s rows: %llu jobs, %llu lanes: infeasible at batch start %llu, below the "
+                  "lowest listed level %llu, needed %llu, lists too short %llu; jobs with every lane infeasible %llu, with "
+                  "no lane needed %llu\n", base == 30 ? "no-policy" : "NUMA-policy", (unsigned long long)v[0],
+                  (unsigned long long)v[1], (unsigned long long)v[2], (unsigned long long)v[3], (unsigned long long)v[4],
+                  (unsigned long long)v[5], (unsigned long long)v[6], (unsigned long long)v[7]);
+        }
         const double nb = c->stats.batches ? (double)c->stats.batches * c->B : 1.0;
         fprintf(stderr, "gpuscore cand_kernel, wave-0 cycles per pod row: pass 1 %.0f, level sums %.0f, level pick %.0f, "
                 "offsets %.0f, pass 2 %.0f\n", sa[512] / nb, sa[513] / nb, sa[514] / nb, sa[515] / nb, sa[516] / nb);
