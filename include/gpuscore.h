@@ -429,8 +429,10 @@ int gs_schedule(gs_ctx* ctx, const gs_pod* pods, uint32_t npods, const uint64_t*
  * the batch pipeline keeps running across submissions — while one submission's last batch commits, the next one's
  * first batch is evaluated and the host applies the finished batch's placements. pods / seq are copied; out must stay
  * valid until gs_schedule_wait(ticket) returns. Every other call on ctx first waits until all submissions are complete
- * (a scheduler submits the next queue chunk, then waits for the previous one). One rank, no node sampling. Returns
- * GS_OK and the submission's ticket, or an error (invalid pod, no mirror yet) with nothing submitted. */
+ * (a scheduler submits the next queue chunk, then waits for the previous one). No node sampling. Several ranks: every
+ * rank submits the same runs, at its own pace; the ranks agree at each run boundary whether the pipeline continues
+ * into the next run. Returns GS_OK and the submission's ticket, or an error (invalid pod, no mirror yet) with nothing
+ * submitted. */
 int gs_schedule_submit(gs_ctx* ctx, const gs_pod* pods, uint32_t npods, const uint64_t* seq, gs_placement* out,
                        uint64_t* ticket);
 /* Blocks until submission `ticket` is complete: its gs_schedule result. An error fails every later submission
@@ -582,7 +584,9 @@ int gs_schedule_ext(gs_ctx* ctx, const gs_pod* pods, const gs_pod_ext* ext, uint
                     gs_placement* out, gs_ext_placement* ext_out);
 
 /* Multi-GPU: nodes are sharded in contiguous ranges [r*ceil(N/R), (r+1)*ceil(N/R)); every rank keeps the full
- * mirror (replicated deltas) and evaluates only its shard. Native RCCL over xGMI: */
+ * mirror (replicated deltas) and evaluates only its shard. Per batch the shards' score rows are all-gathered and every
+ * rank runs the one-GPU selection and Reserve over all nodes (GS_XCHG=levels at init: the per-shard candidate levels
+ * instead, merged on the device). Native RCCL over xGMI: */
 int gs_comm_unique_id(uint8_t out[128]);
 int gs_comm_init_rccl(gs_ctx* ctx, const uint8_t id[128], int nranks, int rank);
 /* Caller-supplied transport (host buffers): */
