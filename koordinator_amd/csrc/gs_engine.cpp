@@ -2738,12 +2738,13 @@ struct PodRun {
 // Several ranks: whether the next run is already known (gs_schedule_submit) is a matter of each rank's timing. The
 // ranks agree on it at every batch that ends a run (all of them must hold it), so that they speculate across the run
 // boundary together and their exchanges pair up; a rank that holds the next run when the others do not starts it
-// after the current one without speculation, as they do. On st2 (idle between eval passes): the batch in flight
-// keeps running.
+// after the current one without speculation, as they do. Behind the current batch's all-gather on its stream, so that
+// every collective of the context is ordered by its streams (an RCCL communicator's collectives must run in issue
+// order): score rows on st_ev (the commit in flight on st keeps running while the host waits), levels on st.
 int agree_next_run(gs_ctx* c, bool* use) {
   const uint32_t mine = *use ? 1u : 0u;
   std::vector<uint32_t> all(c->nranks);
-  if (int rc = exchange_small(c, XSITE_RUNS, nullptr, 4, all.data(), c->st2, &mine)) return rc;
+  if (int rc = exchange_small(c, XSITE_RUNS, nullptr, 4, all.data(), c->sgather ? c->st_ev : c->st, &mine)) return rc;
   for (uint32_t v : all) *use = *use && v;
   return GS_OK;
 }

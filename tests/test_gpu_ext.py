@@ -135,8 +135,8 @@ def test_c5_numa_policy_nodes_deviceshare_hints(policy_pct):
     (deviceshare/topology_hint.go:33-214), merged with NodeNUMAResource's hints; the Filter-time affinity restricts
     DeviceShare's Allocate / Score / Reserve to the GPUs on its NUMA nodes, and NodeNUMAResource's Reserve allocates
     the zones along it. Placements, GPU minors, NUMA allocations and the final state bit-exact against the oracle."""
-    # (400 pods: the oracle's permutation merge over every provider list is most of the test's ~1 min)
-    c = synth.make_cluster(1500, 400 if policy_pct == 100 else 600, config_id=13 + policy_pct)
+    # (260 / 400 pods: the oracle's permutation merge over every provider list is most of the test's time)
+    c = synth.make_cluster(1500, 260 if policy_pct == 100 else 400, config_id=13 + policy_pct)
     synth.make_numa(c, numa_policy_pct=policy_pct, cpuset_pod_pct=0)
     synth.make_ext(c, gpu_node_pct=50, gpu_pod_pct=50, owner_pod_pct=0)
     e, o, ge, oe = run_pair(c, enabled=abi.GS_ENABLE_ALL)
@@ -163,7 +163,7 @@ def test_c5_gpu_owner_pods_reservations_on_policy_nodes_cpuset_pods(policy_pct):
       reservation restore is empty without reserved cpusets, nodenumaresource/reservation.go:76-113), the affinity of
       the restored row, DeviceShare as the second hint provider there;
     * cpuset-bound extension pods (NUMA split on the device, takeCPUs by the host's Reserve)."""
-    c = synth.make_cluster(2000, 520, config_id=21 + policy_pct)
+    c = synth.make_cluster(2000, 380, config_id=21 + policy_pct)
     synth.make_numa(c, numa_policy_pct=policy_pct, cpuset_pod_pct=25)
     synth.make_ext(c, gpu_node_pct=40, gpu_pod_pct=20, rsv_node_pct=30, owners=8, owner_pod_pct=40, required_pct=10,
                    owner_gpu_pct=40)
