@@ -2200,8 +2200,16 @@ int gs_create(const gs_config* cfg, gs_ctx** out) {
   if ((e = hipStreamCreateWithFlags(&c->st_rb, hipStreamNonBlocking)) != hipSuccess) return bail("hipStreamCreate", e);
   if ((e = hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming)) != hipSuccess) return bail("hipEventCreate", e);
   if ((e = hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming)) != hipSuccess) return bail("hipEventCreate", e);
-  for (auto& ev : c->ev)
-    if ((e = hipEventCreate(&ev)) != hipSuccess) return bail("hipEventCreate", e);
+  // GS_EV_FENCE (experiments): the device-side timing events 0, 1, 4 (and with "dev2" the eval-done events the commit
+  // stream waits on) recorded with a device-scope release ("dev") or no system-scope fence ("none") instead of the
+  // default system-scope release (an L2 write-back between the commit and the next kernel on its stream)
+  static const char* evf = getenv("GS_EV_FENCE");
+  const unsigned ev_fence = !evf ? 0u : !strncmp(evf, "dev", 3) ? (unsigned)hipEventReleaseToDevice
+                          : !strcmp(evf, "none") ? (unsigned)hipEventDisableSystemFence : 0u;
+  const bool evdone_fence = evf && !strcmp(evf, "dev2");
+  for (int i = 0; i < 6; ++i)
+    if ((e = hipEventCreateWithFlags(&c->ev[i], (i == 0 || i == 1 || i == 4) ? ev_fence : 0u)) != hipSuccess)
+      return bail("hipEventCreate", e);
   // GS_EV4_NT=1 (experiments): the commit-end event without timing (the levels interval then reads 0)
   static const bool ev4_nt = getenv("GS_EV4_NT") && getenv("GS_EV4_NT")[0] == '1';
   if (ev4_nt) {
@@ -2247,7 +2255,9 @@ int gs_create(const gs_config* cfg, gs_ctx** out) {
   {
     for (auto& sl : c->slot) {
       if ((e = hipEventCreateWithFlags(&sl.ev_go, hipEventDisableTiming)) != hipSuccess) return bail("hipEventCreate", e);
-      if ((e = hipEventCreateWithFlags(&sl.ev_evdone, hipEventDisableTiming)) != hipSuccess) return bail("hipEventCreate", e);
+      if ((e = hipEventCreateWithFlags(&sl.ev_evdone, hipEventDisableTiming |
+                                                         (evdone_fence ? (unsigned)hipEventReleaseToDevice : 0u))) != hipSuccess)
+        return bail("hipEventCreate", e);
     }
     gs_ctx::Slot& s0 = c->slot[0];
     s0.d_S = c->d_S; s0.d_aff = c->d_aff;
@@ -2269,7 +2279,8 @@ int gs_create(const gs_config* cfg, gs_ctx** out) {
       return bail("hipHostMalloc", e);
     s1.h_out = reinterpret_cast<PlacementDev*>(s1.h_committed + COMMITTED_BYTES / 4);
     for (int i = 0; i < 6; ++i)
-      if ((e = hipEventCreateWithFlags(&s1.ev[i], i == 4 && ev4_nt ? hipEventDisableTiming : 0)) != hipSuccess)
+      if ((e = hipEventCreateWithFlags(&s1.ev[i], i == 4 && ev4_nt ? hipEventDisableTiming
+                                                   : (i == 0 || i == 1 || i == 4) ? ev_fence : 0u)) != hipSuccess)
         return bail("hipEventCreate", e);
     c->cand_overlap = !(getenv("GS_CAND_OVERLAP") && getenv("GS_CAND_OVERLAP")[0] == '0');
     if (c->cand_overlap)
