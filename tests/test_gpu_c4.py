@@ -47,7 +47,7 @@ def _worker(rank: int, world: int, port: int, numa: bool, pods: int, xchg: str, 
     # (reproduced with 4 HIP queues per process, gone with 2). Read by HIP at its initialisation below.
     os.environ["GPU_MAX_HW_QUEUES"] = "2"
     # mostly the level-list exchange (GS_XCHG=levels): these 100k-node clusters' score-row blocks (the default exchange)
-    # move ~19 MB per rank and batch through gloo, so the score-row case is three 2048-pod calls
+    # move ~19 MB per rank and batch through gloo, so the score-row case schedules 6,144 pods
     os.environ["GS_XCHG"] = xchg
     try:
         import torch
