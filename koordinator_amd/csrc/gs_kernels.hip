@@ -730,6 +730,8 @@ __global__ void __launch_bounds__(FIX_THREADS) fix_levels_kernel(int16_t* __rest
   __shared__ int32_t s_wd[2];
   int8_t* lev_of = reinterpret_cast<int8_t*>(olist + lcap);   // [nbins] bin -> new level (-1: not listed)
   const int k = blockIdx.x, t = threadIdx.x, lane = t & 63;
+  // the landed node of entry t (cp.extra = the previous batch's size bounds its placements) loads beside the count
+  const int32_t node_t = t < cp.extra ? cp.prev_out[t].node : -1;
   const int npr = min(cp.prev_committed[0], MAX_BATCH);   // -1: a voided pass (its lists are never used)
   if (npr <= 0) return;
   __shared__ unsigned int s_ev_max[2];   // diagnostics: the block's slowest lane (row loads, row loads + evaluation)
@@ -788,7 +790,7 @@ __global__ void __launch_bounds__(FIX_THREADS) fix_levels_kernel(int16_t* __rest
   int so = -1, sn = -1, aff_v = -1;
   bool valid = false;
   if (t < npr) {
-    const int32_t node = cp.prev_out[t].node;
+    const int32_t node = node_t;
     valid = node >= 0 && (uint32_t)node >= cp.n0 && (uint32_t)node < cp.n1;
     p_raw[t] = valid ? (uint32_t)node : 0xffffffffu;
     if (valid) {
