@@ -58,7 +58,24 @@ def _replay_check(c, cfg, got, sample):
     for f in ("node", "score", "ties", "feasible"):
         bad = np.nonzero(got[f][chk] != want[f][chk])[0]
         assert len(bad) == 0, f"{f} differs at pod {np.nonzero(chk)[0][bad[:5]]}"
+    _replay_check.oracle = o
     return int(chk.sum())
+
+
+def _allocations_equal(e, o, c, got):
+    """Every placed pod's NodeNUMAResource allocation — NUMA zone split and cpuset, which the GPU chose and the engine
+    recorded — equals the one the oracle's Reserve made on the same node during the replay (resourceManager.Allocate
+    -> takeCPUs, nodenumaresource/plugin.go:375-419): the placement records' zone and cpuset fields pinned pod by pod
+    against the oracle, not only through the golden files."""
+    n = 0
+    for j in np.nonzero(got["node"] >= 0)[0]:
+        node, uid = int(got["node"][j]), int(c.pods["uid"][j])
+        a, b = e.allocation(node, uid), o.allocation(node, uid)
+        assert (a is None) == (b is None), f"pod {j}: allocation on one side only ({a is None}, {b is None})"
+        if a is not None:
+            assert a.tobytes() == b.tobytes(), f"pod {j} on node {node}: GPU allocation {a} oracle {b}"
+            n += 1
+    return n
 
 
 def test_c3_100k_nodes_50k_pods_replay_parity():
@@ -76,9 +93,10 @@ def test_c3_100k_nodes_50k_pods_replay_parity():
     P = len(c.pods)
     sample = np.unique(np.concatenate([np.arange(48), np.arange(48, P, 64)]))   # every 64th pod
     n = _replay_check(c, cfg, got, sample)
+    na = _allocations_equal(e, _replay_check.oracle, c, got)
     placed = int((got["node"] >= 0).sum())
     print(f"100k x 50k: {placed} placed, all {ng} placements equal the oracle-verified golden ones, {n} pods "
-          f"re-scheduled by the oracle and identical; "
+          f"re-scheduled by the oracle and identical, {na} NUMA / cpuset allocations equal the oracle's; "
           f"wall {time.perf_counter() - t0:.1f} s; stats {e.stats()}")
 
 
@@ -99,8 +117,11 @@ def test_c3_bench_config_50k_nodes_replay_parity():
     _save("bench", got, {"stats": {k: (float(v) if isinstance(v, float) else int(v)) for k, v in e.stats().items()}})
     ng = _golden_equal("bench", got)
     n = _replay_check(c, cfg, got, np.arange(0, P, 64))
+    na = _allocations_equal(e, _replay_check.oracle, c, got)
+    assert na > 1000
     print(f"C3 bench config 50k x {P}: {int((got['node'] >= 0).sum())} placed, all {ng} placements equal the "
-          f"oracle-verified golden ones, {n} pods re-checked in full; "
+          f"oracle-verified golden ones, {n} pods re-checked in full, {na} NUMA / cpuset allocations equal the "
+          f"oracle's; "
           f"wall {time.perf_counter() - t0:.1f} s")
 
 
