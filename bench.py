@@ -4,7 +4,8 @@ A step = one pass of the hot path over one batch of synthetic pending pods: the 
 (NodeResourcesFit + LoadAwareScheduling + NodeNUMAResource Filter over every node, their Scores, selectHost,
 assume + Reserve incl. NUMA allocation and cpuset selection) for `--pods-per-step` pods, sequentially, against
 the 50k-node synthetic C3 cluster. Several GPUs: strong scaling by default (the metric's 50k nodes in total,
-node-sharded, RCCL all-gather of per-shard candidate lists per batch, the commit replicated); `--scaling weak`
+node-sharded, RCCL all-gather of each shard's score rows per batch, the one-GPU commit replicated on every rank);
+`--scaling weak`
 gives every GPU 50k nodes. `--profile la-fit` drops NodeNUMAResource (the C2 plugin set).
 
     python bench.py [--gpus N] [--steps K] [--warmup W]

@@ -37,7 +37,8 @@ class GpuScoreError(RuntimeError):
 
 class LocalGroup:
     """The in-process device transport's group (gs_local_group): the ranks are threads of this process, each with its
-    own Engine; the level all-gathers run stream-ordered on the device as ncclAllGather does."""
+    own Engine; the per-batch all-gathers (score rows, or candidate levels under GS_XCHG=levels) run stream-ordered on
+    the device as ncclAllGather does."""
 
     def __init__(self, nranks: int):
         self._h = C.c_void_p()
