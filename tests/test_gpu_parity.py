@@ -337,6 +337,26 @@ def test_ranks_on_one_gpu_device_transport(n, numa, xchg, monkeypatch):
         assert engines[r].stats()["shard_end"] == engines[r + 1].stats()["shard_begin"]
 
 
+@pytest.mark.parametrize("xchg", ["scores", "levels"])
+def test_ranks_with_an_empty_shard(xchg, monkeypatch):
+    """5 nodes over 4 ranks: shards of 2, 2, 1 and 0 nodes (the last rank evaluates nothing and all-gathers an empty
+    block). Every rank's placements equal the oracle's, contention included."""
+    monkeypatch.setenv("GS_XCHG", xchg)
+    c = synth.make_cluster(5, 90, 31)
+    synth.make_numa(c)
+    cfg = config.make_config(c.num_nodes, enabled=abi.GS_ENABLE_ALL)
+    res, engines, _ = run_ranks_local(c, cfg, 4)
+    o = orc.Oracle(cfg)
+    synth.load_into(o, c)
+    want = o.schedule(c.pods)
+    for r in range(4):
+        assert not isinstance(res[r], Exception) and res[r] is not None, (r, res[r])
+        for f in ("node", "score", "ties", "feasible"):
+            assert np.array_equal(res[r][f], want[f]), (r, f)
+    assert engines[3].stats()["shard_begin"] == engines[3].stats()["shard_end"] == 5
+    assert (want["node"] >= 0).sum() > 5
+
+
 @pytest.mark.parametrize("n,xchg", [(2, "scores"), (3, "scores"), (2, "levels")])
 def test_ranks_submit_across_runs(n, xchg, monkeypatch):
     """gs_schedule_submit on several ranks: each rank submits the same runs at its own pace (rank-dependent sleeps,
