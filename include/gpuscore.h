@@ -579,7 +579,8 @@ int gs_reservations_remove(gs_ctx* ctx, const uint64_t* uids, uint32_t n);
 int gs_reservation_get(gs_ctx* ctx, uint64_t uid, gs_reservation* out);   /* 1 = found, 0 = none */
 /* gs_schedule with the Reservation / DeviceShare plugins: ext[i] (ext may be NULL: no pod uses them) holds pod i's
  * plugin inputs; ext_out[i] (may be NULL) receives the reservation and GPU minors the Reserve assumed. Pods on the
- * extension path need one rank and no node sampling (GS_EUNSUPPORTED otherwise). */
+ * extension path need no node sampling, and one rank or several over the score-row exchange (each extension pod then
+ * runs whole on every rank; GS_EUNSUPPORTED under GS_XCHG=levels). */
 int gs_schedule_ext(gs_ctx* ctx, const gs_pod* pods, const gs_pod_ext* ext, uint32_t npods, const uint64_t* seq,
                     gs_placement* out, gs_ext_placement* ext_out);
 

@@ -270,6 +270,8 @@ struct gs_ctx {
   MirrorView slab_mv{nullptr, nullptr, 0};   // the eval pass's dense copy of the NUMA-policy rows (gather_numa_kernel)
   uint32_t slab_cap = 0;
   bool numa_idx_stale = true;
+  uint32_t numa_idx_lo = 0, numa_idx_hi = 0;   // the node range d_numa_idx lists (the batch path: the shard
+                                                // [e0, e1); the extension path: [n0, n1), every node)
   int64_t prep_now = INT64_MIN;             // `now` of the last full node_prep pass
   // registered topologies in bit-plane form (the commit kernel's cpuset Reserve), and the host re-check of
   // every device-chosen cpuset (GS_VERIFY_CPUSET=1)
@@ -1333,7 +1335,7 @@ int launch_batch(gs_ctx* c, int b, const int32_t* prev, const PlacementDev* prev
   int prod_cols = 0;
   for (int i = 0; i < b; ++i) prod_cols |= (c->h_pods[i].flags & PF_PROD_SCORE) ? 1 : 0;
   uint32_t len = c->n1 - c->n0;
-  if (c->numa_on && c->numa_idx_stale) {
+  if (c->numa_on && (c->numa_idx_stale || c->numa_idx_lo != c->e0 || c->numa_idx_hi != c->e1)) {
     std::vector<uint32_t> idx;   // the policy nodes this rank evaluates
     for (uint32_t n = c->e0; n < c->e1; ++n)
       if (c->numa[n].cfg.numa_topology_policy != GS_NUMA_POLICY_NONE) idx.push_back(n);
@@ -1360,6 +1362,8 @@ int launch_batch(gs_ctx* c, int b, const int32_t* prev, const PlacementDev* prev
       c->slab_mv.npad = c->slab_cap;
     }
     c->numa_idx_stale = false;
+    c->numa_idx_lo = c->e0;
+    c->numa_idx_hi = c->e1;
   }
   const gs_ctx::Slot& sl = c->slot[c->cur_slot];
   // a short batch with no pass beside it: upload, eval and levels in order on st (no queue hops)
@@ -1809,8 +1813,12 @@ int ext_schedule_one(gs_ctx* c, const gs_pod& pod, const gs_pod_ext& e, uint64_t
                      gs_ext_placement* eo) {
   *out = gs_placement{-1, 0, 0, 0, 0};
   *eo = gs_ext_placement{};
-  if (c->nranks > 1 || c->window_k)
-    return fail(c, GS_EUNSUPPORTED, "Reservation / DeviceShare pods need one rank and no node sampling");
+  // several ranks: with the score-row exchange every rank holds every node's state and runs the one-GPU pipeline, so an
+  // extension pod runs whole on every rank (no exchange: the same inputs give the same placement everywhere); the
+  // level exchange's ranks hold their shard's rows only
+  if ((c->nranks > 1 && !c->sgather) || c->window_k)
+    return fail(c, GS_EUNSUPPORTED, "Reservation / DeviceShare pods need one rank (or the score-row exchange) and no "
+                "node sampling");
   const bool ds_on = c->ext.enabled & GS_EXT_DEVICESHARE, rs_on = c->ext.enabled & GS_EXT_RESERVATION;
   int64_t greq[3];
   uint32_t gmask = 0;
@@ -1930,7 +1938,7 @@ int ext_schedule_one(gs_ctx* c, const gs_pod& pod, const gs_pod_ext& e, uint64_t
   if (gpu_names_all || xres_all) v.flags &= ~PF_ALL_ZERO;
   *reinterpret_cast<PodVec*>(c->h_xin + ((sizeof(ExtPod) + 15) & ~(size_t)15)) = v;
   // numa_idx (the eval pass's NUMA-policy work list) as launch_batch keeps it
-  if (c->numa_on && c->numa_idx_stale) {
+  if (c->numa_on && (c->numa_idx_stale || c->numa_idx_lo != c->n0 || c->numa_idx_hi != c->n1)) {
     std::vector<uint32_t> idx;
     for (uint32_t n = c->n0; n < c->n1; ++n)
       if (c->numa[n].cfg.numa_topology_policy != GS_NUMA_POLICY_NONE) idx.push_back(n);
@@ -1943,6 +1951,8 @@ int ext_schedule_one(gs_ctx* c, const gs_pod& pod, const gs_pod_ext& e, uint64_t
       HIP_TRY(c, hipMemcpy(c->d_numa_idx, idx.data(), 4 * idx.size(), hipMemcpyHostToDevice));
     }
     c->numa_idx_stale = false;
+    c->numa_idx_lo = c->n0;
+    c->numa_idx_hi = c->n1;
   }
   const int prod_cols = (v.flags & PF_PROD_SCORE) ? 1 : 0;
   // inputs: one copy of the staged block (ExtPod, PodVec, the matched records and reservations)

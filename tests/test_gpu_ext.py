@@ -185,3 +185,80 @@ def test_c5_gpu_owner_pods_reservations_on_policy_nodes_cpuset_pods(policy_pct):
         uid = int(c.pods["uid"][j])
         a, b = e.allocation(int(node[j]), uid), o.allocation(int(node[j]), uid)
         assert (a is None) == (b is None) and (a is None or a.tobytes() == b.tobytes()), j
+
+
+@pytest.mark.parametrize("n,numa", [(2, False), (3, True)], ids=["2ranks", "3ranks-numa"])
+def test_c5_on_several_ranks_score_rows(n, numa):
+    """Reservation + DeviceShare pods on several ranks (threads over the in-process device transport, the default
+    score-row exchange): the plain runs between extension pods go through the sharded batch pipeline with its
+    all-gathers, each extension pod runs whole on every rank. Every rank's placements, reservations, GPU minors and
+    normalized scores equal the oracle's, and the ranks' device and reservation state equal it too."""
+    import threading
+    from koordinator_amd.engine import Engine, LocalGroup
+    c = synth.make_cluster(2500, 600, config_id=33 + n)
+    if numa:
+        synth.make_numa(c, numa_policy_pct=40, cpuset_pod_pct=10)
+    synth.make_ext(c, gpu_node_pct=30, gpu_pod_pct=15)
+    cfg = config.make_config(c.num_nodes, enabled=abi.GS_ENABLE_ALL if numa else abi.GS_ENABLE_LA_FIT)
+    a = orc.ext_args_default()
+    g = LocalGroup(n)
+    engines = [Engine(cfg) for _ in range(n)]
+    for r, x in enumerate(engines):
+        synth.load_into(x, c)
+        synth.load_ext_into(x, c, a)
+        x.comm_init_local(g, r)
+    seq = np.arange(len(c.pods), dtype=np.uint64)
+    res = [None] * n
+
+    def run(r):
+        try:
+            outs = [engines[r].schedule_ext(c.pods[k:k + 200], c.ext["pod_ext"][k:k + 200], seq[k:k + 200])
+                    for k in range(0, len(c.pods), 200)]
+            res[r] = (np.concatenate([x[0] for x in outs]), np.concatenate([x[1] for x in outs]))
+        except Exception as ex:   # noqa: BLE001 (reported per rank)
+            res[r] = ex
+    th = [threading.Thread(target=run, args=(r,)) for r in range(n)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=300)
+    o = orc.Oracle(cfg)
+    synth.load_into(o, c)
+    synth.load_ext_into(o, c, a)
+    oe = o.schedule_ext(c.pods, c.ext["pod_ext"], seq)
+    for r in range(n):
+        assert not isinstance(res[r], Exception) and res[r] is not None, (r, res[r])
+        check(c, engines[r], o, res[r], oe)
+    assert (res[0][1]["gpu_count"] > 0).sum() > 20 and (res[0][1]["reservation_uid"] > 0).sum() > 5
+
+
+def test_c5_on_several_ranks_level_exchange_refused(monkeypatch):
+    """Under the level exchange (GS_XCHG=levels) a rank holds only its shard's rows, so an extension pod is refused
+    loudly (GS_EUNSUPPORTED) on every rank instead of being scored on part of the cluster."""
+    import threading
+    from koordinator_amd.engine import Engine, LocalGroup
+    monkeypatch.setenv("GS_XCHG", "levels")
+    c = synth.make_cluster(1000, 200, config_id=37)
+    synth.make_ext(c, gpu_node_pct=30, gpu_pod_pct=20)
+    cfg = config.make_config(c.num_nodes, enabled=abi.GS_ENABLE_LA_FIT)
+    a = orc.ext_args_default()
+    g = LocalGroup(2)
+    engines = [Engine(cfg) for _ in range(2)]
+    for r, x in enumerate(engines):
+        synth.load_into(x, c)
+        synth.load_ext_into(x, c, a)
+        x.comm_init_local(g, r)
+    res = [None] * 2
+
+    def run(r):
+        try:
+            res[r] = engines[r].schedule_ext(c.pods, c.ext["pod_ext"], np.arange(len(c.pods), dtype=np.uint64))
+        except Exception as ex:   # noqa: BLE001 (reported per rank)
+            res[r] = ex
+    th = [threading.Thread(target=run, args=(r,)) for r in range(2)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=120)
+    for r in range(2):
+        assert isinstance(res[r], Exception) and "score-row exchange" in str(res[r]), (r, res[r])
