@@ -373,7 +373,7 @@ def main() -> None:
     total_pods = (args.warmup + args.steps) * args.pods_per_step
     c5 = args.profile == "c5"
     if c5 and world > 1:
-        raise SystemExit("--profile c5 runs on one GPU (extension pods need one rank)")
+        raise SystemExit("--profile c5 runs on one GPU (the C5 bench is a one-GPU configuration)")
     cluster = synth.make_cluster(n_nodes, total_pods, config_id=5 if c5 else 2)
     numa = args.profile == "c3"
     if numa:

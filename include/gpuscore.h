@@ -273,7 +273,8 @@ typedef struct gs_config {
    * harness's percentageOfNodesToScore = 100; nextStartNodeIndex never moves). sample_nodes = 1: the scheduler
    * keeps nextStartNodeIndex and checks nodes in rotation order from it until numFeasibleNodesToFind(N) feasible
    * nodes are found (parallelism-1 order; percentage_of_nodes_to_score 0 = the adaptive default
-   * 50 - N/125 %, at least 5 % and 100 nodes). Single GPU only (GS_EUNSUPPORTED with several ranks). */
+   * 50 - N/125 %, at least 5 % and 100 nodes). Several ranks: with the score-row exchange (every rank resolves the
+ * window over the all-gathered rows); GS_EUNSUPPORTED at gs_comm_init_* under GS_XCHG=levels. */
   int32_t sample_nodes;
   int32_t percentage_of_nodes_to_score;
 } gs_config;

@@ -1176,12 +1176,14 @@ int compute_profile(gs_ctx* c) {
   return GS_OK;
 }
 
+// GS_XCHG=levels (read at every comm init): the per-shard candidate levels instead of the score rows
+bool xchg_levels() { return getenv("GS_XCHG") && std::strcmp(getenv("GS_XCHG"), "levels") == 0; }
+
 void set_shard(gs_ctx* c) {
   uint32_t per = (c->N + c->nranks - 1) / c->nranks;
   c->e0 = std::min(c->N, per * (uint32_t)c->rank);
   c->e1 = std::min(c->N, c->e0 + per);
-  const bool levels = getenv("GS_XCHG") && std::strcmp(getenv("GS_XCHG"), "levels") == 0;   // (read per comm init)
-  c->sgather = c->nranks > 1 && !levels;
+  c->sgather = c->nranks > 1 && !xchg_levels();
   c->n0 = c->sgather ? 0 : c->e0;
   c->n1 = c->sgather ? c->N : c->e1;
   c->sx_per = per;
@@ -3245,7 +3247,9 @@ int gs_comm_unique_id(uint8_t out[128]) {
 int gs_comm_init_rccl(gs_ctx* c, const uint8_t id[128], int nranks, int rank) {
   if (!c || !id || nranks < 1 || nranks > MAX_RANKS || rank < 0 || rank >= nranks) return GS_EINVAL;
   quiesce(c);
-  if (c->window_k && nranks > 1) return fail(c, GS_EUNSUPPORTED, "node sampling runs on one GPU");
+  // node sampling's rotation window needs every node's Filter verdict on every rank: the score rows carry them
+  if (c->window_k && nranks > 1 && xchg_levels())
+    return fail(c, GS_EUNSUPPORTED, "node sampling on several ranks needs the score-row exchange");
   if (nranks > 1) {
     ncclUniqueId uid;
     std::memcpy(&uid, id, 128);
@@ -3263,7 +3267,9 @@ int gs_comm_init_rccl(gs_ctx* c, const uint8_t id[128], int nranks, int rank) {
 int gs_comm_init_callback(gs_ctx* c, int nranks, int rank, gs_allgather_fn fn, void* user) {
   if (!c || !fn || nranks < 1 || nranks > MAX_RANKS || rank < 0 || rank >= nranks) return GS_EINVAL;
   quiesce(c);
-  if (c->window_k && nranks > 1) return fail(c, GS_EUNSUPPORTED, "node sampling runs on one GPU");
+  // node sampling's rotation window needs every node's Filter verdict on every rank: the score rows carry them
+  if (c->window_k && nranks > 1 && xchg_levels())
+    return fail(c, GS_EUNSUPPORTED, "node sampling on several ranks needs the score-row exchange");
   c->cb = fn;
   c->cb_user = user;
   c->nranks = nranks;
@@ -3293,7 +3299,8 @@ int gs_local_group_destroy(gs_local_group* g) {
 int gs_comm_init_local(gs_ctx* c, gs_local_group* g, int rank) {
   if (!c || !g || rank < 0 || rank >= g->n) return GS_EINVAL;
   quiesce(c);
-  if (c->window_k && g->n > 1) return fail(c, GS_EUNSUPPORTED, "node sampling runs on one GPU");
+  if (c->window_k && g->n > 1 && xchg_levels())
+    return fail(c, GS_EUNSUPPORTED, "node sampling on several ranks needs the score-row exchange");
   HIP_TRY(c, hipSetDevice(c->cfg.device));
   if (!c->lg_ready) HIP_TRY(c, hipEventCreateWithFlags(&c->lg_ready, hipEventDisableTiming));
   if (!c->lg_done) HIP_TRY(c, hipEventCreateWithFlags(&c->lg_done, hipEventDisableTiming));

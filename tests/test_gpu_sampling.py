@@ -78,12 +78,52 @@ def test_sampling_homogeneous_ties():
     assert got["ties"].max() >= 100
 
 
-def test_sampling_refuses_several_ranks():
+def test_sampling_refuses_several_ranks_under_levels(monkeypatch):
+    """The level exchange holds a shard's rows only: node sampling's rotation window needs every node's verdict."""
+    monkeypatch.setenv("GS_XCHG", "levels")
     c = synth.make_cluster(500, 8, 15)
     e, _ = sampling_pair(c, 0)
     from koordinator_amd.engine import GpuScoreError
-    with pytest.raises(GpuScoreError, match="one GPU"):
+    with pytest.raises(GpuScoreError, match="score-row exchange"):
         e.comm_init_callback(2, 0, lambda send: [send, send])
+
+
+@pytest.mark.parametrize("n,pct", [(2, 0), (3, 10)])
+def test_sampling_on_several_ranks_score_rows(n, pct):
+    """Node sampling on several ranks (threads over the in-process device transport, score-row exchange): every rank
+    holds every node's scores after the all-gather and resolves the rotation window itself; placements and
+    nextStartNodeIndex of every rank equal the oracle's."""
+    import threading
+    from koordinator_amd.engine import Engine, LocalGroup
+    c = loaded_cluster(4000, 500, 18 + n)
+    cfg = config.make_config(c.num_nodes, percentage_of_nodes_to_score=pct)
+    g = LocalGroup(n)
+    engines = [Engine(cfg) for _ in range(n)]
+    for r, x in enumerate(engines):
+        synth.load_into(x, c)
+        x.comm_init_local(g, r)
+    seq = np.arange(len(c.pods), dtype=np.uint64)
+    res = [None] * n
+
+    def run(r):
+        try:
+            res[r] = np.concatenate([engines[r].schedule(c.pods[k:k + 250], seq[k:k + 250]) for k in (0, 250)])
+        except Exception as ex:   # noqa: BLE001 (reported per rank)
+            res[r] = ex
+    th = [threading.Thread(target=run, args=(r,)) for r in range(n)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=200)
+    o = orc.Oracle(cfg)
+    synth.load_into(o, c)
+    want = o.schedule(c.pods, seq)
+    for r in range(n):
+        assert not isinstance(res[r], Exception) and res[r] is not None, (r, res[r])
+        for f in ("node", "score", "ties", "feasible"):
+            assert np.array_equal(res[r][f], want[f]), (r, f)
+        assert engines[r].stats()["next_start_node_index"] == o.next_start_node_index
+    assert want["feasible"].max() == orc.num_feasible_nodes_to_find(4000, pct)
 
 
 @pytest.mark.parametrize("kind", ["homogeneous", "loaded"])
