@@ -381,8 +381,8 @@ def main() -> None:
     if c5:
         synth.make_ext(cluster)
     from koordinator_amd import abi
-    if args.sample_pct is not None and world > 1:
-        raise SystemExit("--sample-pct runs on one GPU")
+    if args.sample_pct is not None and world > 1 and os.environ.get("GS_XCHG") == "levels":
+        raise SystemExit("--sample-pct on several GPUs needs the score-row exchange")
     cfg = config.make_config(n_nodes, device=device, batch_size=args.batch,
                              enabled=abi.GS_ENABLE_ALL if numa else abi.GS_ENABLE_LA_FIT,
                              percentage_of_nodes_to_score=args.sample_pct)
