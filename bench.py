@@ -427,7 +427,7 @@ def main() -> None:
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     placed = 0
-    if args.sync or c5 or args.sample_pct is not None:
+    if args.sync or c5:
         for s in range(args.warmup, args.warmup + args.steps):
             out = run(s * P, (s + 1) * P)
             placed += int((out["node"] >= 0).sum())
@@ -566,7 +566,7 @@ def main() -> None:
                              f"{P} pods/step, NodeResourcesFit(LeastAllocated)+LoadAwareScheduling filter+score, "
                              "selectHost, assume+Reserve"),
                 "nodes": n_nodes, "pods_per_step": P, "batch": args.batch,
-                "submission": "blocking gs_schedule per step" if (args.sync or c5 or args.sample_pct is not None)
+                "submission": "blocking gs_schedule per step" if (args.sync or c5)
                               else "gs_schedule_submit one step ahead (the batch pipeline runs across steps)",
                 "parallelism": f"node-shard x{world}" + ("" if world == 1 else
                                ", candidate levels all-gathered, merged-list commit on every rank"

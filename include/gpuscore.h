@@ -430,7 +430,8 @@ int gs_schedule(gs_ctx* ctx, const gs_pod* pods, uint32_t npods, const uint64_t*
  * the batch pipeline keeps running across submissions — while one submission's last batch commits, the next one's
  * first batch is evaluated and the host applies the finished batch's placements. pods / seq are copied; out must stay
  * valid until gs_schedule_wait(ticket) returns. Every other call on ctx first waits until all submissions are complete
- * (a scheduler submits the next queue chunk, then waits for the previous one). No node sampling. Several ranks: every
+ * (a scheduler submits the next queue chunk, then waits for the previous one). Node sampling included
+ * (nextStartNodeIndex carries across submissions). Several ranks: every
  * rank submits the same runs, at its own pace; the ranks agree at each run boundary whether the pipeline continues
  * into the next run. Returns GS_OK and the submission's ticket, or an error (invalid pod, no mirror yet) with nothing
  * submitted. */

@@ -3076,7 +3076,6 @@ int gs_schedule(gs_ctx* c, const gs_pod* pods, uint32_t npods, const uint64_t* s
 int gs_schedule_submit(gs_ctx* c, const gs_pod* pods, uint32_t npods, const uint64_t* seq, gs_placement* out,
                        uint64_t* ticket) {
   if (!c || !ticket || (npods && (!pods || !out))) return GS_EINVAL;
-  if (c->window_k) return fail(c, GS_EUNSUPPORTED, "gs_schedule_submit: not with node sampling");
   auto r = std::make_shared<AsyncRun>();
   // checks that write nothing (the worker may be running): on an error, wait for it, then report
   if (c->n_valid != c->N) {

@@ -69,3 +69,27 @@ def test_invalid_submission_is_refused():
         e.schedule_submit(bad)
     out = e.schedule_wait(e.schedule_submit(c.pods[:100]))
     assert (out["node"] >= 0).sum() > 50
+
+
+@pytest.mark.parametrize("pct", [0, 10])
+def test_submissions_with_node_sampling(pct):
+    """Node sampling under gs_schedule_submit: nextStartNodeIndex carries across submissions as across batches (the
+    speculative pass reads it on the device from the batch before); placements and the final index equal the
+    oracle's sequential scheduleOne."""
+    c = synth.make_cluster(4000, 1100, 9)
+    c.pods["requests"][::3, 0] = 60_000
+    c.pods["request_mask"][:] |= 0x1
+    cfg = config.make_config(c.num_nodes, device=0, percentage_of_nodes_to_score=pct)
+    e = Engine(cfg)
+    synth.load_into(e, c)
+    seq = np.arange(len(c.pods), dtype=np.uint64)
+    cuts = [0, 200, 437, 700, 701, 1100]
+    hs = [e.schedule_submit(c.pods[a:b], seq[a:b]) for a, b in zip(cuts, cuts[1:])]
+    got = np.concatenate([e.schedule_wait(h) for h in hs])
+    o = orc.Oracle(cfg)
+    synth.load_into(o, c)
+    want = o.schedule(c.pods, seq)
+    for f in ("node", "score", "ties", "feasible"):
+        assert np.array_equal(got[f], want[f]), f
+    assert e.stats()["next_start_node_index"] == o.next_start_node_index
+    assert want["feasible"].max() == orc.num_feasible_nodes_to_find(4000, pct)
