@@ -270,8 +270,12 @@ struct gs_ctx {
   MirrorView slab_mv{nullptr, nullptr, 0};   // the eval pass's dense copy of the NUMA-policy rows (gather_numa_kernel)
   uint32_t slab_cap = 0;
   bool numa_idx_stale = true;
-  uint32_t numa_idx_lo = 0, numa_idx_hi = 0;   // the node range d_numa_idx lists (the batch path: the shard
-                                                // [e0, e1); the extension path: [n0, n1), every node)
+  // the extension path's list over [n0, n1) (all nodes under the score-row exchange, where the batch path's list covers
+  // the rank's shard only): its own buffer, so pods alternating between the two paths rebuild neither
+  uint32_t* d_xnuma_idx = nullptr;
+  uint32_t xnuma_n = 0;
+  bool xnuma_stale = true;
+  uint32_t numa_idx_lo = 0, numa_idx_hi = 0;   // the node range d_numa_idx lists (the batch path's shard [e0, e1))
   int64_t prep_now = INT64_MIN;             // `now` of the last full node_prep pass
   // registered topologies in bit-plane form (the commit kernel's cpuset Reserve), and the host re-check of
   // every device-chosen cpuset (GS_VERIFY_CPUSET=1)
@@ -1939,22 +1943,19 @@ int ext_schedule_one(gs_ctx* c, const gs_pod& pod, const gs_pod_ext& e, uint64_t
   // GPU names are scalar requests: the Fit filter's all-zero short cut no longer applies
   if (gpu_names_all || xres_all) v.flags &= ~PF_ALL_ZERO;
   *reinterpret_cast<PodVec*>(c->h_xin + ((sizeof(ExtPod) + 15) & ~(size_t)15)) = v;
-  // numa_idx (the eval pass's NUMA-policy work list) as launch_batch keeps it
-  if (c->numa_on && (c->numa_idx_stale || c->numa_idx_lo != c->n0 || c->numa_idx_hi != c->n1)) {
+  // the NUMA-policy work list over [n0, n1) for the eval pass and ext_numa_kernel (launch_batch's list is the shard's)
+  if (c->numa_on && c->xnuma_stale) {
     std::vector<uint32_t> idx;
     for (uint32_t n = c->n0; n < c->n1; ++n)
       if (c->numa[n].cfg.numa_topology_policy != GS_NUMA_POLICY_NONE) idx.push_back(n);
     HIP_TRY(c, host_wait_stream(c->st));
-    HIP_TRY(c, host_wait_stream(c->st_ev));
-    if (c->d_numa_idx) { (void)hipFree(c->d_numa_idx); c->d_numa_idx = nullptr; }
-    c->numa_n = (uint32_t)idx.size();
-    if (c->numa_n) {
-      HIP_TRY(c, hipMalloc(&c->d_numa_idx, 4 * idx.size()));
-      HIP_TRY(c, hipMemcpy(c->d_numa_idx, idx.data(), 4 * idx.size(), hipMemcpyHostToDevice));
+    if (c->d_xnuma_idx) { (void)hipFree(c->d_xnuma_idx); c->d_xnuma_idx = nullptr; }
+    c->xnuma_n = (uint32_t)idx.size();
+    if (c->xnuma_n) {
+      HIP_TRY(c, hipMalloc(&c->d_xnuma_idx, 4 * idx.size()));
+      HIP_TRY(c, hipMemcpy(c->d_xnuma_idx, idx.data(), 4 * idx.size(), hipMemcpyHostToDevice));
     }
-    c->numa_idx_stale = false;
-    c->numa_idx_lo = c->n0;
-    c->numa_idx_hi = c->n1;
+    c->xnuma_stale = false;
   }
   const int prod_cols = (v.flags & PF_PROD_SCORE) ? 1 : 0;
   // inputs: one copy of the staged block (ExtPod, PodVec, the matched records and reservations)
@@ -1969,15 +1970,15 @@ int ext_schedule_one(gs_ctx* c, const gs_pod& pod, const gs_pod_ext& e, uint64_t
   const auto ext_t0 = std::chrono::steady_clock::now();
   HIP_TRY(c, hipMemcpyAsync(c->d_xin, c->h_xin, in_bytes, hipMemcpyHostToDevice, c->st));
   if (ext_ev) HIP_TRY(c, hipEventRecord(c->ev[0], c->st));
-  HIP_TRY(c, launch_eval(c->mv, c->d_xpv, 1, c->pf, c->n0, c->n1, c->d_S, c->ld, prod_cols, c->d_numa_idx, c->numa_n,
+  HIP_TRY(c, launch_eval(c->mv, c->d_xpv, 1, c->pf, c->n0, c->n1, c->d_S, c->ld, prod_cols, c->d_xnuma_idx, c->xnuma_n,
                          c->d_aff, c->st));
   if (ext_ev) HIP_TRY(c, hipEventRecord(c->ev[1], c->st));
   // (ext_nodes_kernel also resets the select accumulators; ext_matched runs for pods with matched reservations only)
   HIP_TRY(c, launch_ext_nodes(c->d_dev, c->d_S, c->n0, c->n1, c->d_xpod, c->d_xtot, c->d_xds, c->d_xrs, c->d_xT,
                               c->st));
   // GPU pods on NUMA-policy nodes: DeviceShare is the topology manager's second hint provider
-  if (gmask && c->numa_on && c->numa_n)
-    HIP_TRY(c, launch_ext_numa(c->mv, c->d_xpv, c->pf, prod_cols, c->d_dev, c->d_xpod, c->d_numa_idx, c->numa_n, c->n0,
+  if (gmask && c->numa_on && c->xnuma_n)
+    HIP_TRY(c, launch_ext_numa(c->mv, c->d_xpv, c->pf, prod_cols, c->d_dev, c->d_xpod, c->d_xnuma_idx, c->xnuma_n, c->n0,
                                c->d_xtot, c->d_xds, c->d_aff, c->d_xT, c->n1 - c->n0, c->st));
   // the matched nodes last: their restored rows over the whole Filter chain (incl. the policy nodes' affinity)
   if (nrec)
@@ -2501,7 +2502,7 @@ int gs_destroy(gs_ctx* c) {
   }
   void* dev[] = {c->d_xerr, c->d_xsmall,
                  c->d_i64, c->d_i32, c->d_pods, c->d_S, c->d_xchg_send, c->d_xchg_recv, c->d_xmerged,
-                 c->d_committed, c->d_rowstat, c->d_sel, c->d_stage_idx, c->d_stage_rows, c->d_numa_idx,
+                 c->d_committed, c->d_rowstat, c->d_sel, c->d_stage_idx, c->d_stage_rows, c->d_numa_idx, c->d_xnuma_idx,
                  c->d_topos, c->d_aff, c->d_tb, c->d_sx_send, c->d_sx_recv};
   for (void* p : dev)
     if (p) (void)hipFree(p);
@@ -3174,7 +3175,7 @@ int gs_nodes_numa_upsert(gs_ctx* c, const uint32_t* idx, const gs_node_numa* nn,
     if (x.has_options && x.topology >= (int32_t)c->topos.size())
       return fail(c, GS_EINVAL, "node %u: topology id %d not registered", i, x.topology);
     NumaNode& st = c->numa[i];
-    if (st.cfg.numa_topology_policy != x.numa_topology_policy) c->numa_idx_stale = true;
+    if (st.cfg.numa_topology_policy != x.numa_topology_policy) c->numa_idx_stale = c->xnuma_stale = true;
     st.cfg = x;
     if (c->devs[i].has_device) dev_mark(c, i);   // its GPUs' zone slots (dev_image)
     st.topo = !x.has_options ? nullptr : (x.topology >= 0 ? c->topos[x.topology] : c->empty_topo);
@@ -3259,7 +3260,7 @@ int gs_comm_init_rccl(gs_ctx* c, const uint8_t id[128], int nranks, int rank) {
   c->nranks = nranks;
   c->rank = rank;
   set_shard(c);
-  c->numa_idx_stale = true;
+  c->numa_idx_stale = c->xnuma_stale = true;
   return alloc_exchange(c);
 }
 
@@ -3274,7 +3275,7 @@ int gs_comm_init_callback(gs_ctx* c, int nranks, int rank, gs_allgather_fn fn, v
   c->nranks = nranks;
   c->rank = rank;
   set_shard(c);
-  c->numa_idx_stale = true;
+  c->numa_idx_stale = c->xnuma_stale = true;
   return alloc_exchange(c);
 }
 
@@ -3307,7 +3308,7 @@ int gs_comm_init_local(gs_ctx* c, gs_local_group* g, int rank) {
   c->nranks = g->n;
   c->rank = rank;
   set_shard(c);
-  c->numa_idx_stale = true;
+  c->numa_idx_stale = c->xnuma_stale = true;
   return alloc_exchange(c);
 }
 
@@ -3351,7 +3352,7 @@ int gs_reset(gs_ctx* c) {
   (void)hipGetLastError();
   for (uint32_t i = 0; i < c->N; ++i)
     if (c->nodes[i].valid) mark_dirty(c, i);
-  c->numa_idx_stale = true;
+  c->numa_idx_stale = c->xnuma_stale = true;
   if (c->d_dev)
     for (uint32_t i = 0; i < c->N; ++i) dev_mark(c, i);
   int rc = flush_rows(c);
