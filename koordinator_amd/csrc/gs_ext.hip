@@ -211,6 +211,8 @@ __device__ int64_t score_reservation(const ExtPod& p, const ExtRes& r) {
 }
 
 constexpr int SEL_BLOCK = 256;
+constexpr int SEL_PER = 4;                       // nodes per thread in the select passes
+constexpr int SEL_SPAN = SEL_BLOCK * SEL_PER;     // nodes per block (a contiguous range: the ties pass relies on it)
 enum { ACC_DS = 0, ACC_RS = 1, ACC_FEAS = 2, ACC_MAX = 3, ACC_DONE = 4, ACC_TIES = 5, ACC_PREF = 6, ACC_ERR = 7,
        ACC_WORDS = 8 };
 static_assert(ACC_WORDS == ACC_WORDS_N && ACC_PREF == 6, "accumulator layout (ext_nodes_kernel resets it)");
@@ -391,6 +393,9 @@ __global__ __launch_bounds__(SEL_BLOCK) void ext_matched_kernel(MirrorView m, co
 //   ext_total_kernel  weighted totals T[j] with both DefaultNormalizeScore passes, per-block max -> atomicMax
 //   ext_ties_kernel   per-block tie counts at the max (blocks cover contiguous node ranges); the last block to finish
 //                     scans the block counts, finds the block of the j*-th tie (selectHost) and the node in it
+// A block covers SEL_SPAN nodes, SEL_PER per thread in SEL_BLOCK-wide coalesced chunks: a quarter of the blocks and of
+// the same-address atomics of one node per thread (the three passes 27.6 -> 18.8 us per pod at 100k nodes; 2 and 8
+// per thread measured 20.6 and 22.5 us, profiles/r06_c5_select_span.txt)
 
 __device__ __forceinline__ int32_t block_max_i32(int32_t v, int32_t* sh) {
   v = wave_max(v);
@@ -420,12 +425,15 @@ __global__ __launch_bounds__(SEL_BLOCK) void ext_acc_kernel(const int32_t* __res
                                                             const ExtPod* __restrict__ pp, int32_t* acc) {
   __shared__ int32_t sh[SEL_BLOCK / 64];
   const int32_t pref = acc[ACC_PREF];
-  const uint32_t j = blockIdx.x * SEL_BLOCK + threadIdx.x;
   int32_t f = 0, d = 0, r = 0;
-  if (j < len && tot[j] >= 0) {
-    f = 1;
-    d = ds[j];
-    r = (int32_t)(j + n0) == pref ? 1000 : rs[j];
+#pragma unroll
+  for (int q = 0; q < SEL_PER; ++q) {
+    const uint32_t j = blockIdx.x * SEL_SPAN + q * SEL_BLOCK + threadIdx.x;
+    if (j < len && tot[j] >= 0) {
+      f += 1;
+      d = max(d, (int32_t)ds[j]);
+      r = max(r, (int32_t)(j + n0) == pref ? 1000 : (int32_t)rs[j]);
+    }
   }
   d = block_max_i32(d, sh);
   r = block_max_i32(r, sh);
@@ -446,19 +454,24 @@ __global__ __launch_bounds__(SEL_BLOCK) void ext_total_kernel(const int32_t* __r
   const ExtPod& p = *pp;
   const int32_t pref_sh = acc[ACC_PREF];
   const int64_t MDS = acc[ACC_DS], MRS = acc[ACC_RS];
-  const uint32_t j = blockIdx.x * SEL_BLOCK + threadIdx.x;
-  int32_t t = -1;
-  if (j < len && tot[j] >= 0) {
-    int64_t x = tot[j];
-    if (p.ds_on) x += (MDS ? kMaxNodeScore * ds[j] / MDS : (int64_t)ds[j]) * p.w_ds;
-    if (p.rs_on) {
-      const int64_t r = (int32_t)(j + n0) == pref_sh ? 1000 : rs[j];
-      x += (MRS ? kMaxNodeScore * r / MRS : r) * p.w_rs;
+  int32_t tm = -1;
+#pragma unroll
+  for (int q = 0; q < SEL_PER; ++q) {
+    const uint32_t j = blockIdx.x * SEL_SPAN + q * SEL_BLOCK + threadIdx.x;
+    int32_t t = -1;
+    if (j < len && tot[j] >= 0) {
+      int64_t x = tot[j];
+      if (p.ds_on) x += (MDS ? kMaxNodeScore * ds[j] / MDS : (int64_t)ds[j]) * p.w_ds;
+      if (p.rs_on) {
+        const int64_t r = (int32_t)(j + n0) == pref_sh ? 1000 : rs[j];
+        x += (MRS ? kMaxNodeScore * r / MRS : r) * p.w_rs;
+      }
+      t = (int32_t)x;
     }
-    t = (int32_t)x;
+    if (j < len) T[j] = t;
+    tm = max(tm, t);
   }
-  if (j < len) T[j] = t;
-  const int32_t m = block_max_i32(t, sh);
+  const int32_t m = block_max_i32(tm, sh);
   if (threadIdx.x == 0 && m >= 0) atomicMax(&acc[ACC_MAX], m + 1);
 }
 
@@ -473,8 +486,13 @@ __global__ __launch_bounds__(SEL_BLOCK) void ext_ties_kernel(const int32_t* __re
   __shared__ int32_t found_block, found_rank;
   const ExtPod& p = *pp;
   const int32_t M = acc[ACC_MAX] - 1;
-  const uint32_t j = blockIdx.x * SEL_BLOCK + threadIdx.x;
-  const int32_t c = block_sum_i32((M >= 0 && j < len && T[j] == M) ? 1 : 0, sh);
+  int32_t mine_ties = 0;
+#pragma unroll
+  for (int q = 0; q < SEL_PER; ++q) {
+    const uint32_t j = blockIdx.x * SEL_SPAN + q * SEL_BLOCK + threadIdx.x;
+    mine_ties += (M >= 0 && j < len && T[j] == M) ? 1 : 0;
+  }
+  const int32_t c = block_sum_i32(mine_ties, sh);
   if (threadIdx.x == 0) {
     bcnt[blockIdx.x] = c;
     __threadfence();
@@ -523,24 +541,33 @@ __global__ __launch_bounds__(SEL_BLOCK) void ext_ties_kernel(const int32_t* __re
     }
   }
   __syncthreads();
-  const uint32_t jj = (uint32_t)found_block * SEL_BLOCK + threadIdx.x;
-  const int is_tie = (jj < len && __atomic_load_n(&T[jj], __ATOMIC_RELAXED) == M) ? 1 : 0;
-  const int tincl = wave_incl_scan(is_tie);
-  __syncthreads();
-  if ((threadIdx.x & 63) == 63) sh[w] = tincl;
-  __syncthreads();
-  int rank = tincl;
-  for (int i = 0; i < w; ++i) rank += sh[i];
-  if (is_tie && rank == found_rank) {
-    const int32_t node = (int32_t)(jj + n0);
-    const int64_t MDS = acc[ACC_DS], MRS = acc[ACC_RS];
-    const int64_t dsn = MDS ? kMaxNodeScore * ds[jj] / MDS : ds[jj];
-    const int64_t rr = node == pref ? 1000 : rs[jj];
-    const int64_t rsn = MRS ? kMaxNodeScore * rr / MRS : rr;
-    ExtOut o{};
-    o.node = node; o.feasible = (uint32_t)F; o.score = M; o.ties = (uint32_t)ties; o.rec = -1;
-    o.ds_norm = (int32_t)(p.ds_on ? dsn : 0); o.rs_norm = (int32_t)(p.rs_on ? rsn : 0); o.pref_node = pref; o.err = err;
-    *out = o;
+  // the found block's range in node order, one SEL_BLOCK chunk at a time (seen: the ties of its earlier chunks)
+  int32_t seen = 0;
+  for (int q = 0; q < SEL_PER && seen < found_rank; ++q) {
+    const uint32_t jj = (uint32_t)found_block * SEL_SPAN + q * SEL_BLOCK + threadIdx.x;
+    const int is_tie = (jj < len && __atomic_load_n(&T[jj], __ATOMIC_RELAXED) == M) ? 1 : 0;
+    const int tincl = wave_incl_scan(is_tie);
+    if ((threadIdx.x & 63) == 63) sh[w] = tincl;
+    __syncthreads();
+    int rank = seen + tincl, chunk = 0;
+    for (int i = 0; i < SEL_BLOCK / 64; ++i) {
+      if (i < w) rank += sh[i];
+      chunk += sh[i];
+    }
+    seen += chunk;
+    __syncthreads();   // (sh is rewritten by the next chunk)
+    if (is_tie && rank == found_rank) {
+      const int32_t node = (int32_t)(jj + n0);
+      const int64_t MDS = acc[ACC_DS], MRS = acc[ACC_RS];
+      const int64_t dsn = MDS ? kMaxNodeScore * ds[jj] / MDS : ds[jj];
+      const int64_t rr = node == pref ? 1000 : rs[jj];
+      const int64_t rsn = MRS ? kMaxNodeScore * rr / MRS : rr;
+      ExtOut o{};
+      o.node = node; o.feasible = (uint32_t)F; o.score = M; o.ties = (uint32_t)ties; o.rec = -1;
+      o.ds_norm = (int32_t)(p.ds_on ? dsn : 0); o.rs_norm = (int32_t)(p.rs_on ? rsn : 0); o.pref_node = pref;
+      o.err = err;
+      *out = o;
+    }
   }
 }
 
@@ -585,7 +612,7 @@ hipError_t launch_ext_select(const int32_t* tot, const int16_t* ds, const int16_
                              uint32_t n1, const ExtPod* pod, uint64_t seed, int32_t* scratch, ExtOut* out,
                              hipStream_t st) {
   const uint32_t len = n1 - n0;
-  const uint32_t blocks = (len + SEL_BLOCK - 1) / SEL_BLOCK;
+  const uint32_t blocks = len ? (len + SEL_SPAN - 1) / SEL_SPAN : 1;
   int32_t* T = scratch;
   int32_t* acc = scratch + len;
   int32_t* bcnt = acc + ACC_WORDS;
